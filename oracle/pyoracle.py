@@ -1,0 +1,264 @@
+"""ctypes wrapper over oracle/build/libngp_oracle.so.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, as the checker. The product path (instant-ngp_amd) never imports this module.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libngp_oracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+class Pcg32(C.Structure):
+    _fields_ = [("state", C.c_uint64), ("inc", C.c_uint64)]
+
+
+class Grid(C.Structure):
+    _fields_ = [
+        ("n_dims", C.c_uint32), ("n_levels", C.c_uint32), ("n_features", C.c_uint32),
+        ("log2_hashmap", C.c_uint32), ("base_resolution", C.c_uint32), ("per_level_scale", C.c_float),
+        ("offsets", C.c_uint32 * 33), ("scale", C.c_float * 32), ("resolution", C.c_uint32 * 32),
+    ]
+
+
+class Mlp(C.Structure):
+    _fields_ = [("in_pad", C.c_uint32), ("width", C.c_uint32), ("n_hidden", C.c_uint32), ("out_pad", C.c_uint32)]
+
+
+class Nerf(C.Structure):
+    _fields_ = [("grid", Grid), ("density", Mlp), ("rgb", Mlp), ("dir_offset", C.c_uint32), ("in_stride", C.c_uint32)]
+
+
+class AdamCfg(C.Structure):
+    _fields_ = [("lr", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float), ("l2", C.c_float),
+                ("ema_decay", C.c_float), ("decay_start", C.c_uint32), ("decay_interval", C.c_uint32),
+                ("decay_base", C.c_float)]
+
+
+P = C.c_void_p
+
+
+def _declare(L):
+    def d(name, res, *args):
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = list(args)
+    u32, u64, i64, f32, sz = C.c_uint32, C.c_uint64, C.c_int64, C.c_float, C.c_size_t
+    d("orc_f32_to_f16", C.c_uint16, f32)
+    d("orc_f16_to_f32", f32, C.c_uint16)
+    d("orc_f32_to_f16_array", None, P, P, sz)
+    d("orc_f16_to_f32_array", None, P, P, sz)
+    d("orc_pcg32_seed", None, P, u64, u64)
+    d("orc_pcg32_default", None, P)
+    d("orc_pcg32_next_uint", u32, P)
+    d("orc_pcg32_next_float", f32, P)
+    d("orc_pcg32_advance", None, P, i64)
+    d("orc_generate_random_uniform", None, P, sz, P, f32, f32)
+    d("orc_grid_init", u32, P, u32, u32, u32, u32, u32, f32)
+    d("orc_grid_forward", None, P, sz, P, u32, P, f32, P, P)
+    d("orc_grid_backward", None, P, sz, P, u32, P, f32, P, P)
+    d("orc_grid_indices", None, P, sz, P, u32, P)
+    d("orc_sh4", None, f32, f32, f32, P)
+    d("orc_mlp_n_params", u32, P)
+    d("orc_mlp_forward", None, P, P, sz, P, P)
+    d("orc_mlp_backward", None, P, P, sz, P, P, P, P)
+    d("orc_mlp_init", None, P, P, P)
+    d("orc_nerf_n_params", u32, P)
+    d("orc_nerf_forward", None, P, P, sz, P, P)
+    d("orc_nerf_density", None, P, P, sz, P, u32, P)
+    d("orc_nerf_backward", None, P, P, sz, P, P, P, P)
+    d("orc_nerf_init", None, P, u64, P)
+    d("orc_lr_at_step", f32, P, u32)
+    d("orc_adam_step", None, P, u32, sz, sz, f32, P, P, P, P, P, P, P, P)
+    d("orc_morton3D", u32, u32, u32, u32)
+    d("orc_srgb_to_linear", f32, f32)
+    d("orc_linear_to_srgb", f32, f32)
+    d("orc_num_threads", C.c_int)
+
+
+def ptr(a):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "oracle needs contiguous arrays"
+    return a.ctypes.data_as(C.c_void_p)
+
+
+# ---------------------------------------------------------------------------------------------
+# Thin pythonic helpers
+# ---------------------------------------------------------------------------------------------
+def f32_to_f16_bits(a):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    out = np.empty(a.shape, dtype=np.uint16)
+    lib().orc_f32_to_f16_array(ptr(a), ptr(out), a.size)
+    return out
+
+
+def f16_bits_to_f32(a):
+    a = np.ascontiguousarray(a, dtype=np.uint16)
+    out = np.empty(a.shape, dtype=np.float32)
+    lib().orc_f16_to_f32_array(ptr(a), ptr(out), a.size)
+    return out
+
+
+class Rng:
+    """tcnn::pcg32 restated (pcg32(initstate, initseq=1))."""
+
+    def __init__(self, seed=None, seq=1):
+        self.s = Pcg32()
+        if seed is None:
+            lib().orc_pcg32_default(C.byref(self.s))
+        else:
+            lib().orc_pcg32_seed(C.byref(self.s), seed, seq)
+
+    def next_uint(self):
+        return lib().orc_pcg32_next_uint(C.byref(self.s))
+
+    def next_float(self):
+        return lib().orc_pcg32_next_float(C.byref(self.s))
+
+    def advance(self, delta):
+        lib().orc_pcg32_advance(C.byref(self.s), delta)
+
+    def uniform(self, n, lo=0.0, hi=1.0):
+        out = np.empty(n, dtype=np.float32)
+        lib().orc_generate_random_uniform(C.byref(self.s), n, ptr(out), lo, hi)
+        return out
+
+
+def make_grid(D, L, F, log2T, Nmin=16, b=2.0):
+    g = Grid()
+    lib().orc_grid_init(C.byref(g), D, L, F, log2T, Nmin, b)
+    return g
+
+
+def grid_n_entries(g):
+    return g.offsets[g.n_levels]
+
+
+def grid_forward(g, pos, table16, max_level=1.0, max_level_per_sample=None, stride=None):
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    n = pos.shape[0]
+    stride = stride or pos.shape[1]
+    out = np.zeros((n, g.n_levels * g.n_features), dtype=np.float32)
+    mls = None if max_level_per_sample is None else np.ascontiguousarray(max_level_per_sample, np.float32)
+    lib().orc_grid_forward(C.byref(g), n, ptr(pos), stride, ptr(np.ascontiguousarray(table16)), max_level, ptr(mls), ptr(out))
+    return out
+
+
+def grid_backward(g, pos, dL_dy, max_level=1.0, max_level_per_sample=None, stride=None):
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    n = pos.shape[0]
+    stride = stride or pos.shape[1]
+    grad = np.zeros(grid_n_entries(g) * g.n_features, dtype=np.float64)
+    mls = None if max_level_per_sample is None else np.ascontiguousarray(max_level_per_sample, np.float32)
+    lib().orc_grid_backward(C.byref(g), n, ptr(pos), stride, ptr(np.ascontiguousarray(dL_dy, np.float32)), max_level,
+                            ptr(mls), ptr(grad))
+    return grad
+
+
+def grid_indices(g, pos, stride=None):
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    n = pos.shape[0]
+    idx = np.zeros((n, g.n_levels, 1 << g.n_dims), dtype=np.uint32)
+    lib().orc_grid_indices(C.byref(g), n, ptr(pos), stride or pos.shape[1], ptr(idx))
+    return idx
+
+
+def sh4(d):
+    out = np.zeros(16, dtype=np.float32)
+    lib().orc_sh4(float(d[0]), float(d[1]), float(d[2]), ptr(out))
+    return out
+
+
+def make_mlp(in_pad, width, n_hidden, out_pad):
+    return Mlp(in_pad, width, n_hidden, out_pad)
+
+
+def mlp_n_params(m):
+    return lib().orc_mlp_n_params(C.byref(m))
+
+
+def mlp_forward(m, w16, x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.zeros((x.shape[0], m.out_pad), dtype=np.float32)
+    lib().orc_mlp_forward(C.byref(m), ptr(np.ascontiguousarray(w16)), x.shape[0], ptr(x), ptr(y))
+    return y
+
+
+def mlp_backward(m, w16, x, dy, want_dx=True):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    dy = np.ascontiguousarray(dy, dtype=np.float32)
+    dW = np.zeros(mlp_n_params(m), dtype=np.float64)
+    dx = np.zeros_like(x) if want_dx else None
+    lib().orc_mlp_backward(C.byref(m), ptr(np.ascontiguousarray(w16)), x.shape[0], ptr(x), ptr(dy), ptr(dW), ptr(dx))
+    return dW, dx
+
+
+def make_nerf(L=4, F=4, log2T=19, Nmin=16, b=2.0, width=64, density_hidden=1, rgb_hidden=2, dir_offset=4, in_stride=7):
+    n = Nerf()
+    lib().orc_grid_init(C.byref(n.grid), 3, L, F, log2T, Nmin, b)
+    enc_pad = (L * F + 15) // 16 * 16
+    n.density = Mlp(enc_pad, width, density_hidden, 16)
+    n.rgb = Mlp(32, width, rgb_hidden, 16)
+    n.dir_offset = dir_offset
+    n.in_stride = in_stride
+    return n
+
+
+def nerf_n_params(m):
+    return lib().orc_nerf_n_params(C.byref(m))
+
+
+def nerf_init(m, seed=1337):
+    p = np.zeros(nerf_n_params(m), dtype=np.float32)
+    lib().orc_nerf_init(C.byref(m), seed, ptr(p))
+    return p
+
+
+def nerf_forward(m, params16, coords):
+    coords = np.ascontiguousarray(coords, dtype=np.float32)
+    out = np.zeros((coords.shape[0], 16), dtype=np.float32)
+    lib().orc_nerf_forward(C.byref(m), ptr(np.ascontiguousarray(params16)), coords.shape[0], ptr(coords), ptr(out))
+    return out
+
+
+def nerf_density(m, params16, coords, stride=None):
+    coords = np.ascontiguousarray(coords, dtype=np.float32)
+    out = np.zeros((coords.shape[0], 16), dtype=np.float32)
+    lib().orc_nerf_density(C.byref(m), ptr(np.ascontiguousarray(params16)), coords.shape[0], ptr(coords),
+                           stride or coords.shape[1], ptr(out))
+    return out
+
+
+def nerf_backward(m, params16, coords, dL_dout, want_denc=False):
+    coords = np.ascontiguousarray(coords, dtype=np.float32)
+    grads = np.zeros(nerf_n_params(m), dtype=np.float64)
+    denc = np.zeros((coords.shape[0], m.density.in_pad), dtype=np.float32) if want_denc else None
+    lib().orc_nerf_backward(C.byref(m), ptr(np.ascontiguousarray(params16)), coords.shape[0], ptr(coords),
+                            ptr(np.ascontiguousarray(dL_dout, np.float32)), ptr(grads), ptr(denc))
+    return (grads, denc) if want_denc else grads
+
+
+def adam_step(cfg, step, n_matrix, loss_scale, w32, w16, g16, m1, m2, steps, ema32=None, ema16=None):
+    lib().orc_adam_step(C.byref(cfg), step, w32.size, n_matrix, loss_scale, ptr(w32), ptr(w16), ptr(g16), ptr(m1),
+                        ptr(m2), ptr(steps), ptr(ema32), ptr(ema16))

@@ -1,0 +1,296 @@
+"""CPU tests pinning the oracle (oracle/ngp_oracle.c) before it is trusted as the checker.
+
+- pcg32 against the published PCG known-answer vector (tests/golden/pcg32_kat.json);
+- fp16 conversion against numpy's IEEE binary16 (all 65536 patterns + random floats);
+- hash-grid forward/backward, MLP forward/backward and the NerfNetwork composition against an
+  independent PyTorch (CPU, float64 autograd) restatement. That cross-check is independent of the
+  oracle's code, not of tiny-cuda-nn (absent: parity unpinned).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_pcg32_kat(orc):
+    kat = json.load(open(os.path.join(GOLDEN, "pcg32_kat.json")))
+    r = orc.Rng(kat["initstate"], kat["initseq"])
+    assert [r.next_uint() for _ in range(len(kat["outputs"]))] == [int(x, 16) for x in kat["outputs"]]
+
+
+def test_pcg32_advance_matches_stepping(orc):
+    a = orc.Rng(1337)
+    b = orc.Rng(1337)
+    for _ in range(1000):
+        a.next_uint()
+    b.advance(1000)
+    assert a.next_uint() == b.next_uint()
+    # negative advance (two's complement) goes back
+    b.advance(-1)
+    c = orc.Rng(1337)
+    c.advance(1000)
+    assert b.next_uint() == c.next_uint()
+
+
+def test_pcg32_next_float_range(orc):
+    r = orc.Rng(7)
+    v = np.array([r.next_float() for _ in range(10000)])
+    assert v.min() >= 0.0 and v.max() < 1.0
+    assert abs(v.mean() - 0.5) < 0.02
+
+
+def test_f16_roundtrip_all_patterns(orc):
+    bits = np.arange(65536, dtype=np.uint16)
+    ref = bits.view(np.float16).astype(np.float32)
+    got = orc.f16_bits_to_f32(bits)
+    finite = np.isfinite(ref)
+    assert np.array_equal(got[finite].view(np.uint32), ref[finite].view(np.uint32))
+    assert np.all(np.isnan(got[np.isnan(ref)]))
+
+
+def test_f32_to_f16_matches_numpy(orc):
+    rng = np.random.default_rng(0)
+    x = np.concatenate([
+        rng.standard_normal(200000).astype(np.float32) * np.float32(10.0) ** rng.integers(-9, 6, 200000).astype(np.float32),
+        np.array([0.0, -0.0, 65504.0, 65519.0, 65520.0, 1e-8, 2.0 ** -25, 2.0 ** -24, 3 * 2.0 ** -26, 6.1e-5], np.float32),
+    ])
+    got = orc.f32_to_f16_bits(x)
+    with np.errstate(over="ignore"):
+        ref = x.astype(np.float16).view(np.uint16)
+    assert np.array_equal(got, ref)
+
+
+def test_grid_offsets_match_survey(orc):
+    # SURVEY §8 parameter table (tcnn offset-table rules)
+    assert orc.grid_n_entries(orc.make_grid(3, 4, 4, 19)) == 823296
+    assert orc.grid_n_entries(orc.make_grid(3, 16, 2, 19)) == 7114752
+    assert orc.grid_n_entries(orc.make_grid(3, 16, 2, 22)) == 52727808
+    assert orc.grid_n_entries(orc.make_grid(2, 4, 2, 14)) == 21760
+
+
+def test_nerf_param_count_matches_survey(orc):
+    assert orc.nerf_n_params(orc.make_nerf()) == 3302400
+    assert orc.nerf_n_params(orc.make_nerf(L=16, F=2)) == 14239744
+
+
+# ------------------------------------------------------------------------------------------------
+# Independent torch restatement of the hash grid (float64), for forward + autograd backward
+# ------------------------------------------------------------------------------------------------
+PRIMES = [1, 2654435761, 805459861]
+
+
+def torch_grid(g, pos, table):
+    """pos: (n, D) float32; table: (entries, F) float64 tensor requiring grad. Returns (n, L*F)."""
+    n, D = pos.shape
+    outs = []
+    for l in range(g.n_levels):
+        scale = np.float32(g.scale[l])
+        res = int(g.resolution[l])
+        T = int(g.offsets[l + 1] - g.offsets[l])
+        p = np.float32(scale) * pos.astype(np.float32) + np.float32(0.5)  # fmaf may differ by 1ulp: use float64 check below
+        p = (pos.astype(np.float64) * np.float64(scale) + 0.5).astype(np.float32)
+        base = np.floor(p)
+        frac = (p - base).astype(np.float32)
+        base = base.astype(np.int64).astype(np.uint64)
+        acc = 0
+        for c in range(1 << D):
+            w = np.ones(n, np.float32)
+            pc = []
+            for d in range(D):
+                if c & (1 << d):
+                    w = w * frac[:, d]
+                    pc.append(base[:, d] + 1)
+                else:
+                    w = w * (np.float32(1) - frac[:, d])
+                    pc.append(base[:, d])
+            # index
+            stride = 1
+            index = np.zeros(n, np.uint64)
+            dense = True
+            for d in range(D):
+                if stride > T:
+                    break
+                index = (index + pc[d] * np.uint64(stride)) & np.uint64(0xFFFFFFFF)
+                stride *= res
+            if T < stride:
+                index = np.zeros(n, np.uint64)
+                for d in range(D):
+                    index ^= (pc[d] * np.uint64(PRIMES[d])) & np.uint64(0xFFFFFFFF)
+            index = (index % np.uint64(T)).astype(np.int64) + int(g.offsets[l])
+            acc = acc + torch.from_numpy(w.astype(np.float64))[:, None] * table[torch.from_numpy(index)]
+        outs.append(acc)
+    return torch.cat(outs, dim=1)
+
+
+@pytest.mark.parametrize("D,L,F,log2T", [(3, 4, 4, 19), (3, 16, 2, 14), (2, 4, 2, 14), (3, 8, 1, 12), (3, 6, 8, 10)])
+def test_grid_forward_backward_vs_torch(orc, D, L, F, log2T):
+    g = orc.make_grid(D, L, F, log2T)
+    rng = np.random.default_rng(D * 100 + L)
+    n = 512
+    pos = rng.random((n, D), dtype=np.float32)
+    pos[:4] = np.array([0.0, 1.0, 0.5, 0.999999], np.float32)[:, None]  # edges: wraparound in dense levels
+    E = orc.grid_n_entries(g)
+    table32 = (rng.random(E * F, dtype=np.float32) * 2 - 1).astype(np.float16).astype(np.float32)
+    table16 = table32.astype(np.float16).view(np.uint16)
+    out = orc.grid_forward(g, pos, table16)
+    t = torch.from_numpy(table32.astype(np.float64).reshape(E, F)).requires_grad_(True)
+    ref = torch_grid(g, pos, t)
+    np.testing.assert_allclose(out, ref.detach().numpy(), rtol=1e-5, atol=1e-6)
+    # indices are integers: the oracle's hashing must agree bit-exactly with the restatement above
+    dy = rng.standard_normal((n, L * F)).astype(np.float32)
+    ref.backward(torch.from_numpy(dy.astype(np.float64)))
+    grad = orc.grid_backward(g, pos, dy)
+    np.testing.assert_allclose(grad, t.grad.numpy().reshape(-1), rtol=1e-5, atol=1e-6)
+
+
+def test_grid_max_level_zeroes_levels(orc):
+    g = orc.make_grid(3, 8, 2, 14)
+    rng = np.random.default_rng(1)
+    pos = rng.random((64, 3), dtype=np.float32)
+    E = orc.grid_n_entries(g)
+    table16 = (rng.random(E * 2, dtype=np.float32) - 0.5).astype(np.float16).view(np.uint16)
+    full = orc.grid_forward(g, pos, table16, 1.0)
+    half = orc.grid_forward(g, pos, table16, 0.5)  # tcnn: level >= 0.5*8 + 1e-3 zeroed -> levels 5..7
+    np.testing.assert_array_equal(half[:, :10], full[:, :10])
+    assert np.all(half[:, 10:] == 0)
+
+
+def test_sh4_orthonormal(orc):
+    # Monte-Carlo orthonormality of the 16 real SH basis functions over the sphere
+    rng = np.random.default_rng(3)
+    d = rng.standard_normal((20000, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    Y = np.stack([orc.sh4((v + 1) / 2) for v in d])
+    G = Y.T @ Y / len(d) * 4 * np.pi
+    np.testing.assert_allclose(G, np.eye(16), atol=0.06)
+
+
+# ------------------------------------------------------------------------------------------------
+# MLP vs torch float64 (tolerance covers the oracle's per-layer fp16 rounding)
+# ------------------------------------------------------------------------------------------------
+def torch_mlp(m, w, x):
+    h = x
+    off = 0
+    nl = m.n_hidden + 1
+    for l in range(nl):
+        i = m.in_pad if l == 0 else m.width
+        o = m.out_pad if l == nl - 1 else m.width
+        W = w[off:off + i * o].view(o, i)
+        off += i * o
+        h = (h @ W.T).half().double()  # fp16 activations (cast is straight-through for grads)
+        if l < nl - 1:
+            h = torch.relu(h)
+    return h
+
+
+@pytest.mark.parametrize("in_pad,width,n_hidden,out_pad", [(16, 64, 1, 16), (32, 64, 2, 16), (32, 64, 3, 16), (16, 16, 2, 16)])
+def test_mlp_vs_torch(orc, in_pad, width, n_hidden, out_pad):
+    m = orc.make_mlp(in_pad, width, n_hidden, out_pad)
+    npar = orc.mlp_n_params(m)
+    rng = orc.Rng(11)
+    w32 = np.zeros(npar, np.float32)
+    orc.lib().orc_mlp_init(orc.C.byref(m), orc.C.byref(rng.s), orc.ptr(w32))
+    w16 = orc.f32_to_f16_bits(w32)
+    wq = orc.f16_bits_to_f32(w16)
+    r = np.random.default_rng(5)
+    x = orc.f16_bits_to_f32(orc.f32_to_f16_bits(r.standard_normal((256, in_pad)).astype(np.float32)))
+    y = orc.mlp_forward(m, w16, x)
+    wt = torch.from_numpy(wq.astype(np.float64)).requires_grad_(True)
+    xt = torch.from_numpy(x.astype(np.float64)).requires_grad_(True)
+    yt = torch_mlp(m, wt, xt)
+    scale = np.abs(yt.detach().numpy()).max()
+    np.testing.assert_allclose(y, yt.detach().numpy(), atol=2e-3 * scale)
+    dy = orc.f16_bits_to_f32(orc.f32_to_f16_bits(r.standard_normal((256, out_pad)).astype(np.float32)))
+    dW, dx = orc.mlp_backward(m, w16, x, dy)
+    yt.backward(torch.from_numpy(dy.astype(np.float64)))
+    gW = wt.grad.numpy()
+    np.testing.assert_allclose(dW, gW, atol=1e-2 * np.abs(gW).max())
+    gx = xt.grad.numpy()
+    np.testing.assert_allclose(dx, gx, atol=1e-2 * np.abs(gx).max())
+
+
+def test_nerf_composition_vs_torch(orc):
+    """NerfNetwork fwd/bwd (nerf_network.h:116-335) vs torch restatement of the same composition."""
+    m = orc.make_nerf(L=4, F=4, log2T=12)
+    p32 = orc.nerf_init(m, 1337)
+    # make the grid larger so the encoding matters
+    nd, nr = orc.mlp_n_params(m.density), orc.mlp_n_params(m.rgb)
+    r = np.random.default_rng(9)
+    p32[nd + nr:] = r.uniform(-1, 1, p32.size - nd - nr).astype(np.float32)
+    p16 = orc.f32_to_f16_bits(p32)
+    pq = orc.f16_bits_to_f32(p16).astype(np.float64)
+    n = 128
+    coords = np.zeros((n, 7), np.float32)
+    coords[:, :3] = r.random((n, 3))
+    coords[:, 3] = 0.01
+    d = r.standard_normal((n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    coords[:, 4:7] = (d + 1) / 2
+    out = orc.nerf_forward(m, p16, coords)
+
+    pt = torch.from_numpy(pq).requires_grad_(True)
+    E = orc.grid_n_entries(m.grid)
+    table = pt[nd + nr:].view(E, 4)
+    enc = torch_grid(m.grid, coords[:, :3], table)
+    dout = torch_mlp(m.density, pt[:nd], enc)
+    sh = torch.from_numpy(np.stack([orc.sh4(c[4:7]) for c in coords]).astype(np.float64))
+    rout = torch_mlp(m.rgb, pt[nd:nd + nr], torch.cat([dout, sh], 1))
+    ref = torch.cat([rout[:, :3], dout[:, :1], rout[:, 4:]], 1)
+    sc = np.abs(ref.detach().numpy()).max()
+    np.testing.assert_allclose(out, ref.detach().numpy(), atol=5e-3 * sc)
+
+    dL = np.zeros((n, 16), np.float32)
+    dL[:, :4] = orc.f16_bits_to_f32(orc.f32_to_f16_bits(r.standard_normal((n, 4)).astype(np.float32)))
+    grads = orc.nerf_backward(m, p16, coords, dL)
+    ref.backward(torch.from_numpy(dL.astype(np.float64)))
+    g = pt.grad.numpy()
+    for lo, hi in [(0, nd), (nd, nd + nr), (nd + nr, g.size)]:
+        np.testing.assert_allclose(grads[lo:hi], g[lo:hi], atol=2e-2 * np.abs(g[lo:hi]).max())
+
+
+def test_adam_matches_numpy(orc):
+    cfg = orc.AdamCfg(1e-2, 0.9, 0.99, 1e-15, 1e-6, 0.95, 20000, 10000, 0.33)
+    n, nm = 1000, 300
+    r = np.random.default_rng(2)
+    w32 = r.standard_normal(n).astype(np.float32)
+    w16 = orc.f32_to_f16_bits(w32)
+    m1 = np.zeros(n, np.float32); m2 = np.zeros(n, np.float32); steps = np.zeros(n, np.uint32)
+    ema32 = np.zeros(n, np.float32); ema16 = np.zeros(n, np.uint16)
+    g = r.standard_normal(n).astype(np.float32) * 128
+    g[nm::7] = 0  # lazily skipped non-matrix params
+    g16 = orc.f32_to_f16_bits(g)
+    w0 = w32.copy()
+    orc.adam_step(cfg, 0, nm, 128.0, w32, w16, g16, m1, m2, steps, ema32, ema16)
+    gr = orc.f16_bits_to_f32(g16) / 128
+    gr[:nm] += 1e-6 * w0[:nm]
+    mm = 0.1 * gr
+    vv = 0.01 * gr * gr
+    lr = 1e-2 * np.sqrt(1 - 0.99) / (1 - 0.9)
+    exp = w0 - lr / (np.sqrt(vv) + 1e-15) * mm
+    skip = np.zeros(n, bool); skip[nm::7] = True
+    np.testing.assert_allclose(w32[~skip], exp[~skip], rtol=1e-5)
+    np.testing.assert_array_equal(w32[skip], w0[skip])
+    assert np.all(steps[~skip] == 1) and np.all(steps[skip] == 0)
+    # EMA debiased after one step equals the weights
+    np.testing.assert_allclose(orc.f16_bits_to_f32(ema16), w32, rtol=1e-3, atol=1e-4)
+
+
+def test_lr_schedule(orc):
+    cfg = orc.AdamCfg(1e-2, 0.9, 0.99, 1e-15, 1e-6, 0.95, 20000, 10000, 0.33)
+    assert orc.lib().orc_lr_at_step(orc.C.byref(cfg), 0) == pytest.approx(1e-2)
+    assert orc.lib().orc_lr_at_step(orc.C.byref(cfg), 19999) == pytest.approx(1e-2)
+    assert orc.lib().orc_lr_at_step(orc.C.byref(cfg), 20000) == pytest.approx(3.3e-3)
+    assert orc.lib().orc_lr_at_step(orc.C.byref(cfg), 30000) == pytest.approx(3.3e-3 * 0.33)
+
+
+def test_morton_and_srgb(orc):
+    assert orc.lib().orc_morton3D(1, 0, 0) == 4
+    assert orc.lib().orc_morton3D(0, 1, 0) == 2
+    assert orc.lib().orc_morton3D(0, 0, 1) == 1
+    assert orc.lib().orc_morton3D(127, 127, 127) == 128 ** 3 - 1
+    for v in [0.0, 0.01, 0.04045, 0.5, 1.0]:
+        assert orc.lib().orc_linear_to_srgb(orc.lib().orc_srgb_to_linear(v)) == pytest.approx(v, abs=1e-3)
