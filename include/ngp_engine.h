@@ -1,0 +1,142 @@
+/*
+ * ngp_engine.h — C-ABI of the MI355X (gfx950) instant-ngp hot-path engine.
+ *
+ * The engine is a drop-in for the tiny-cuda-nn model/trainer objects the reference's Testbed drives:
+ *   tcnn::NetworkWithInputEncoding  (src/testbed.cu:4110, image/SDF primitives)
+ *   ngp::NerfNetwork                (include/neural-graphics-primitives/nerf_network.h:77-578)
+ *   tcnn::Trainer + Optimizer chain (src/testbed.cu:4129; configs/nerf/base.json:5-22)
+ * plus the NeRF training kernels of src/testbed_nerf.cu (ngp_nerf_* below).
+ *
+ * Conventions
+ *  - Plain C types only; half-precision buffers are `void*` holding IEEE binary16.
+ *  - Device pointers unless a name says _host. `stream` is a hipStream_t (NULL = default stream).
+ *  - Matrices follow tcnn's naming: input  element (i, d) at input[i * input_stride + d] ("CM"/AoS,
+ *    the NerfCoordinate layout, nerf.h:85-128); outputs AoS (layout 0: out[i * stride + f]) or
+ *    SoA (layout 1: out[f * stride + i], tcnn "RM").
+ *  - Errors: every int-returning function returns 0 on success and a negative code on failure;
+ *    ngp_last_error() gives the message (the reference throws std::runtime_error /
+ *    CUDA_CHECK_THROW, e.g. nerf_network.h:338-340). Handles are not internally synchronised:
+ *    one host thread per (device, stream) handle, as the reference's one-stream-per-device Testbed
+ *    (testbed.h:989).
+ */
+#ifndef NGP_ENGINE_H
+#define NGP_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+#pragma GCC visibility push(default)
+
+typedef struct ngp_model ngp_model;     /* a network: NerfNetwork or NetworkWithInputEncoding */
+typedef struct ngp_ctx ngp_ctx;         /* forward context (tcnn::Context, nerf_network.h:566-577) */
+typedef struct ngp_trainer ngp_trainer; /* params + gradients + optimizer state (tcnn::Trainer) */
+
+enum { NGP_OK = 0, NGP_ERROR = -1, NGP_INVALID = -2 };
+enum { NGP_LAYOUT_AOS = 0, NGP_LAYOUT_SOA = 1 };
+enum { NGP_GRAD_OVERWRITE = 0, NGP_GRAD_ACCUMULATE = 1 }; /* tcnn::EGradientMode */
+
+/* ---- library ------------------------------------------------------------------------------ */
+const char* ngp_last_error(void);
+const char* ngp_version(void);
+/* device name and CU count of the current HIP device */
+int ngp_device_info(int* cu_count, char* name, size_t name_len);
+/* device memory helpers for FFI callers without their own allocator */
+int ngp_malloc(void** ptr, size_t bytes);
+int ngp_free(void* ptr);
+int ngp_memcpy(void* dst, const void* src, size_t bytes, int kind /* hipMemcpyKind */);
+int ngp_stream_synchronize(void* stream);
+
+/* ---- models (tcnn::Network<float, __half> surface) ------------------------------------------ */
+/* NerfNetwork ctor (nerf_network.h:81-112); JSON strings are the config sections the Testbed passes
+ * (src/testbed.cu:4029-4042: "encoding", "dir_encoding", "network", "rgb_network"). */
+int ngp_nerf_network_create(uint32_t n_pos_dims, uint32_t n_dir_dims, uint32_t n_extra_dims, uint32_t dir_offset,
+                            const char* pos_encoding_json, const char* dir_encoding_json,
+                            const char* density_network_json, const char* rgb_network_json, ngp_model** out);
+/* tcnn::NetworkWithInputEncoding(n_input_dims, n_output_dims, encoding, network) (src/testbed.cu:4101-4110) */
+int ngp_network_with_input_encoding_create(uint32_t n_input_dims, uint32_t n_output_dims, const char* encoding_json,
+                                           const char* network_json, ngp_model** out);
+void ngp_model_destroy(ngp_model* m);
+
+uint64_t ngp_model_n_params(const ngp_model* m);           /* n_params()            nerf_network.h:459 */
+uint64_t ngp_model_n_matrix_params(const ngp_model* m);    /* sum of layer_sizes()  nerf_network.h:483, testbed.cu:3834-3846 */
+uint32_t ngp_model_input_width(const ngp_model* m);        /* input_width()         nerf_network.h:467 */
+uint32_t ngp_model_padded_output_width(const ngp_model* m);/* padded_output_width() nerf_network.h:463 */
+uint32_t ngp_model_output_width(const ngp_model* m);       /* output_width()        nerf_network.h:471 */
+
+/* Parameter layout: [density MLP | rgb MLP | position grid | dir encoding] (nerf_network.h:430-443);
+ * NetworkWithInputEncoding: [MLP | grid]. Grid level offsets in entries (GridEncoding
+ * level_params_offset / level_n_params, src/testbed.cu:4849-4856). */
+typedef struct {
+	uint64_t density_mlp_offset, density_mlp_params;
+	uint64_t rgb_mlp_offset, rgb_mlp_params;
+	uint64_t grid_offset, grid_params;
+	uint32_t grid_dims, grid_levels, grid_features, grid_log2_hashmap, grid_base_resolution;
+	float grid_per_level_scale;
+	uint32_t grid_level_offsets[33]; /* entries; params = entries * grid_features */
+	uint32_t grid_resolution[32];
+	float grid_scale[32];
+	uint32_t encoding_width;         /* padded encoding output width (density MLP input) */
+} ngp_param_layout;
+int ngp_model_param_layout(const ngp_model* m, ngp_param_layout* out);
+
+/* set_params(params, inference_params, gradients) (nerf_network.h:430): fp16 device buffers of n_params */
+int ngp_model_set_params(ngp_model* m, void* params, void* inference_params, void* gradients);
+/* initialize_params(rnd, params_full_precision, scale) (nerf_network.h:445-457), host fp32 buffer */
+int ngp_model_initialize_params(const ngp_model* m, uint64_t seed, float* params_full_precision_host, float scale);
+/* GridEncoding::set_max_level / set_max_level_gpu (src/testbed.cu:3856-3864; testbed_nerf.cu:3996,4004) */
+int ngp_model_set_max_level(ngp_model* m, float max_level, const float* max_level_per_sample);
+/* pre-size internal workspaces for batches up to n (lets callers capture steps into HIP graphs) */
+int ngp_model_reserve(ngp_model* m, uint32_t n);
+
+/* inference_mixed_precision (nerf_network.h:116-174): output fp16 [n x padded_output_width] */
+int ngp_inference(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                  uint32_t output_stride, uint32_t output_layout, int use_inference_params);
+/* NerfNetwork::density (nerf_network.h:337-353): density MLP output fp16 [n x 16] */
+int ngp_density(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                uint32_t output_stride, uint32_t output_layout, int use_inference_params);
+/* forward_impl (nerf_network.h:179-254) -> context; output may be NULL */
+int ngp_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                uint32_t output_stride, int use_inference_params, ngp_ctx** ctx);
+/* backward_impl (nerf_network.h:256-335): param gradients into the gradient buffer given to set_params */
+int ngp_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* dL_doutput, uint32_t dL_stride, int grad_mode);
+void ngp_ctx_destroy(ngp_ctx* ctx);
+/* fused training pass = forward_impl + backward_impl (src/testbed_nerf.cu:4077-4078) in one call */
+int ngp_forward_backward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                         uint32_t output_stride, const void* dL_doutput, uint32_t dL_stride, int grad_mode);
+
+/* Raw position-encoding access (tcnn GridEncoding forward / backward). out fp16 [n x encoding_width]. */
+int ngp_encoding_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                         uint32_t output_stride, uint32_t output_layout, int use_inference_params);
+int ngp_encoding_backward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                          const void* dL_doutput, uint32_t dL_stride, uint32_t dL_layout, int grad_mode);
+
+/* ---- trainer (tcnn::Trainer<float, __half, __half>, src/testbed.cu:4129) -------------------- */
+/* optimizer_json: the "optimizer" config section (Ema / ExponentialDecay / Adam nesting).
+ * Allocates fp32 master params, fp16 params / inference(EMA) params / gradients and Adam state,
+ * initialises parameters from `seed` (default_rng_t, src/testbed.cu:3906) and calls set_params. */
+int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, ngp_trainer** out);
+void ngp_trainer_destroy(ngp_trainer* t);
+/* Trainer::optimizer_step(stream, loss_scale) (src/testbed_nerf.cu:3678) */
+int ngp_trainer_optimizer_step(ngp_trainer* t, void* stream, float loss_scale);
+void* ngp_trainer_gradients(ngp_trainer* t);               /* fp16 [n_params], the DP all-reduce buffer */
+void* ngp_trainer_params(ngp_trainer* t);                  /* fp16 [n_params] */
+void* ngp_trainer_inference_params(ngp_trainer* t);        /* fp16 [n_params] (EMA when configured) */
+float* ngp_trainer_params_full_precision(ngp_trainer* t);  /* fp32 [n_params] */
+uint32_t ngp_trainer_step(const ngp_trainer* t);
+float ngp_trainer_learning_rate(const ngp_trainer* t);     /* optimizer->learning_rate() (testbed_nerf.cu:3771) */
+int ngp_trainer_set_learning_rate(ngp_trainer* t, float lr);
+/* set_params_full_precision (src/testbed.cu:4146): host fp32 -> master, fp16 params and inference params */
+int ngp_trainer_set_params_full_precision(ngp_trainer* t, const float* params_host, uint64_t n);
+/* serialize / deserialize (src/testbed.cu:4874,5040): flat little-endian blob, size query with buf=NULL */
+int ngp_trainer_serialize(ngp_trainer* t, void* buf_host, uint64_t* size);
+int ngp_trainer_deserialize(ngp_trainer* t, const void* buf_host, uint64_t size);
+
+#pragma GCC visibility pop
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NGP_ENGINE_H */

@@ -1,0 +1,103 @@
+"""Network config loading with the reference's `parent` deep-merge (src/testbed.cu:95-106,228-314:
+configs/<mode>/<name>.json may name a parent whose keys it patches). Comments (//) are allowed, as in
+configs/image/base.json."""
+import json
+import os
+import re
+
+
+def _strip_comments(text):
+    out, i, in_str = [], 0, False
+    while i < len(text):
+        c = text[i]
+        if in_str:
+            out.append(c)
+            if c == "\\":
+                out.append(text[i + 1]); i += 1
+            elif c == '"':
+                in_str = False
+        elif c == '"':
+            in_str = True; out.append(c)
+        elif text.startswith("//", i):
+            while i < len(text) and text[i] != "\n":
+                i += 1
+            continue
+        else:
+            out.append(c)
+        i += 1
+    return re.sub(r",(\s*[}\]])", r"\1", "".join(out))
+
+
+def merge_patch(base, patch):
+    """RFC 7386 JSON merge patch (nlohmann::json::merge_patch, used by the reference)."""
+    if not isinstance(patch, dict):
+        return patch
+    out = dict(base) if isinstance(base, dict) else {}
+    for k, v in patch.items():
+        if v is None:
+            out.pop(k, None)
+        else:
+            out[k] = merge_patch(out.get(k), v)
+    return out
+
+
+def load_config(path):
+    with open(path) as f:
+        cfg = json.loads(_strip_comments(f.read()))
+    if "parent" in cfg:
+        parent = os.path.join(os.path.dirname(path), cfg.pop("parent"))
+        cfg = merge_patch(load_config(parent), cfg)
+    return cfg
+
+
+# configs/nerf/base.json of the reference fork (L=4, F=4, T=2^19), restated as data so
+# nothing under /root/reference is read at run time.
+NERF_BASE = {
+    "loss": {"otype": "Huber"},
+    "optimizer": {"otype": "Ema", "decay": 0.95, "nested": {
+        "otype": "ExponentialDecay", "decay_start": 20000, "decay_interval": 10000, "decay_base": 0.33,
+        "nested": {"otype": "Adam", "learning_rate": 1e-2, "beta1": 0.9, "beta2": 0.99, "epsilon": 1e-15,
+                   "l2_reg": 1e-6}}},
+    "encoding": {"otype": "HashGrid", "n_levels": 4, "n_features_per_level": 4, "log2_hashmap_size": 19,
+                 "base_resolution": 16},
+    "network": {"otype": "FullyFusedMLP", "activation": "ReLU", "output_activation": "None", "n_neurons": 64,
+                "n_hidden_layers": 1},
+    "dir_encoding": {"otype": "Composite", "nested": [
+        {"n_dims_to_encode": 3, "otype": "SphericalHarmonics", "degree": 4}, {"otype": "Identity"}]},
+    "rgb_network": {"otype": "FullyFusedMLP", "activation": "ReLU", "output_activation": "None", "n_neurons": 64,
+                    "n_hidden_layers": 2},
+}
+
+# configs/sdf/base.json (L=16, F=2, T=2^19; BASELINE C5 uses T=2^22) and configs/image/base.json.
+SDF_BASE = {
+    "loss": {"otype": "MAPE"},
+    "optimizer": {"otype": "Ema", "decay": 0.95, "nested": {
+        "otype": "ExponentialDecay", "decay_start": 10000, "decay_interval": 5000, "decay_base": 0.33,
+        "nested": {"otype": "Adam", "learning_rate": 1e-4, "beta1": 0.9, "beta2": 0.99, "epsilon": 1e-15,
+                   "l2_reg": 1e-6}}},
+    "encoding": {"otype": "HashGrid", "n_levels": 16, "n_features_per_level": 2, "log2_hashmap_size": 19,
+                 "base_resolution": 16},
+    "network": {"otype": "FullyFusedMLP", "activation": "ReLU", "output_activation": "None", "n_neurons": 64,
+                "n_hidden_layers": 2},
+}
+
+IMAGE_BASE = {
+    "loss": {"otype": "L2"},
+    "optimizer": {"otype": "ExponentialDecay", "decay_start": 20000, "decay_interval": 10000, "decay_base": 0.33,
+                  "nested": {"otype": "Adam", "learning_rate": 1e-2, "beta1": 0.9, "beta2": 0.99, "epsilon": 1e-15,
+                             "l2_reg": 1e-6}},
+    "encoding": {"otype": "HashGrid", "n_levels": 16, "n_features_per_level": 2, "log2_hashmap_size": 24,
+                 "base_resolution": 16},
+    "network": {"otype": "FullyFusedMLP", "activation": "ReLU", "output_activation": "None", "n_neurons": 64,
+                "n_hidden_layers": 2},
+}
+
+
+def nerf_config(variant="C2"):
+    """BASELINE configs: C2 = fork base.json (L=4 F=4 T=2^19); C2p = the 'L=16' variant (L=16 F=2 T=2^19)."""
+    cfg = json.loads(json.dumps(NERF_BASE))
+    if variant == "C2p":
+        cfg["encoding"].update({"n_levels": 16, "n_features_per_level": 2, "log2_hashmap_size": 19})
+    # the fork forces per_level_scale = 2.0 in reset_network (src/testbed.cu:3991)
+    cfg["encoding"]["per_level_scale"] = 2.0
+    return cfg

@@ -1,0 +1,601 @@
+// engine.hip — model / trainer objects behind the C-ABI (include/ngp_engine.h).
+//
+// Mirrors the tcnn object graph the reference's Testbed builds in reset_network
+// (src/testbed.cu:3903-4151): NerfNetwork = position GridEncoding -> density FullyFusedMLP ->
+// [density out | SH(dir)] -> rgb FullyFusedMLP; NetworkWithInputEncoding = encoding -> MLP;
+// Trainer = fp32 master weights + fp16 params/inference params/gradients + optimizer state.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../../include/ngp_engine.h"
+#include "common.h"
+#include "grid.h"
+#include "json.h"
+#include "mlp.h"
+#include "optimizer.h"
+
+namespace ngp {
+
+int device_cu_count() {
+	static int cached = -1;
+	if (cached < 0) {
+		int dev = 0;
+		NGP_HIP(hipGetDevice(&dev));
+		NGP_HIP(hipDeviceGetAttribute(&cached, hipDeviceAttributeMultiprocessorCount, dev));
+	}
+	return cached;
+}
+
+// Growable device buffer (grows outside the hot loop; ngp_model_reserve pre-sizes it).
+struct DevBuf {
+	void* p = nullptr;
+	size_t bytes = 0;
+	void* get(size_t need) {
+		if (need > bytes) {
+			if (p) NGP_HIP(hipFree(p));
+			NGP_HIP(hipMalloc(&p, need));
+			bytes = need;
+		}
+		return p;
+	}
+	~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+// ---- pcg32 (tcnn::pcg32, random_val.cuh:26-43) used for parameter initialisation -------------
+struct Pcg32 {
+	uint64_t state = 0x853c49e6748fea9bULL, inc = 0xda3e39cb94b95bdbULL;
+	static constexpr uint64_t MULT = 0x5851f42d4c957f2dULL;
+	Pcg32(uint64_t initstate, uint64_t initseq = 1u) {
+		state = 0u; inc = (initseq << 1u) | 1u; next_uint(); state += initstate; next_uint();
+	}
+	uint32_t next_uint() {
+		uint64_t old = state;
+		state = old * MULT + inc;
+		uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u), rot = (uint32_t)(old >> 59u);
+		return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+	}
+	float next_float() { uint32_t u = (next_uint() >> 9) | 0x3f800000u; float f; memcpy(&f, &u, 4); return f - 1.0f; }
+	void advance(uint64_t delta) {
+		uint64_t cm = MULT, cp = inc, am = 1u, ap = 0u;
+		while (delta > 0) {
+			if (delta & 1) { am *= cm; ap = ap * cm + cp; }
+			cp = (cm + 1) * cp; cm *= cm; delta /= 2;
+		}
+		state = am * state + ap;
+	}
+	// tcnn generate_random_uniform: element k takes draw k of the stream; the caller advances by n
+	void uniform(size_t n, float* out, float lo, float hi) {
+		Pcg32 r = *this;
+		for (size_t k = 0; k < n; ++k) out[k] = r.next_float() * (hi - lo) + lo;
+		advance(n);
+	}
+};
+
+static void init_mlp(const MlpDims& d, Pcg32& rng, float* p, float scale) {
+	for (uint32_t l = 0; l <= d.n_hidden; ++l) {
+		const uint32_t in = d.layer_in(l), out = d.layer_out(l);
+		const float s = sqrtf(6.0f / (float)(in + out)) * scale;  // Xavier-uniform
+		rng.uniform((size_t)in * out, p + d.layer_off(l), -s, s);
+	}
+}
+
+static GridDesc parse_grid(uint32_t n_dims, const Json& j) {
+	const std::string ot = j.string_or("otype", "HashGrid");
+	NGP_CHECK(iequals(ot, "HashGrid") || iequals(ot, "Grid"), "encoding: only HashGrid is implemented (got " + ot + ")");
+	NGP_CHECK(iequals(j.string_or("type", "Hash"), "Hash"), "encoding: only hash grids are implemented");
+	NGP_CHECK(iequals(j.string_or("interpolation", "Linear"), "Linear"), "encoding: only linear interpolation is implemented");
+	GridDesc g;
+	grid_desc_init(g, n_dims, (uint32_t)j.number_or("n_levels", 16), (uint32_t)j.number_or("n_features_per_level", 2),
+	               (uint32_t)j.number_or("log2_hashmap_size", 19), (uint32_t)j.number_or("base_resolution", 16),
+	               (float)j.number_or("per_level_scale", 2.0));
+	return g;
+}
+
+static uint32_t parse_mlp_hidden(const Json& j, uint32_t* width) {
+	const std::string ot = j.string_or("otype", "FullyFusedMLP");
+	NGP_CHECK(iequals(ot, "FullyFusedMLP") || iequals(ot, "CutlassMLP") || iequals(ot, "MegakernelMLP"),
+	          "network: only FullyFusedMLP-shaped networks are implemented (got " + ot + ")");
+	NGP_CHECK(iequals(j.string_or("activation", "ReLU"), "ReLU"), "network: only ReLU hidden activation is implemented");
+	NGP_CHECK(iequals(j.string_or("output_activation", "None"), "None"), "network: only output_activation None is implemented");
+	*width = (uint32_t)j.number_or("n_neurons", 64);
+	return (uint32_t)j.number_or("n_hidden_layers", 2);
+}
+
+}  // namespace ngp
+
+using namespace ngp;
+
+struct ngp_ctx {
+	uint32_t n;
+	const float* input;
+	uint32_t input_stride;
+	bool use_inference_params;
+	uint64_t generation;  // the model workspace generation the encoding lives in
+};
+
+struct ngp_model {
+	bool nerf = true;
+	GridDesc grid;
+	uint32_t n_pos_dims = 3, n_dir_dims = 3, n_extra_dims = 0, dir_offset = 4, n_input_dims = 3, n_output_dims = 4;
+	uint32_t enc_width = 16;
+	NerfMlpPlan nplan;
+	MlpPlan mplan;
+	uint64_t mlp0_params = 0, mlp1_params = 0, grid_params = 0, n_params = 0;
+	FragDesc* d_descs = nullptr;
+	uint32_t n_all_frags = 0;
+	DevBuf frags, frags_inf, enc, denc, slabs;
+	f16 *params = nullptr, *inference_params = nullptr, *gradients = nullptr;
+	float max_level = 1.0f;
+	const float* max_level_per_sample = nullptr;
+	uint64_t generation = 0;
+	std::unique_ptr<ngp_ctx> last_ctx;
+
+	~ngp_model() { if (d_descs) (void)hipFree(d_descs); }
+
+	const std::vector<FragDesc>& descs() const { return nerf ? nplan.descs : mplan.descs; }
+	uint64_t grid_offset() const { return mlp0_params + mlp1_params; }
+	uint64_t n_matrix() const { return mlp0_params + mlp1_params; }
+
+	void finalize() {
+		grid_params = grid.n_params();
+		n_params = mlp0_params + mlp1_params + grid_params;
+		const auto& d = descs();
+		n_all_frags = (uint32_t)d.size();
+		NGP_HIP(hipMalloc(&d_descs, d.size() * sizeof(FragDesc)));
+		NGP_HIP(hipMemcpy(d_descs, d.data(), d.size() * sizeof(FragDesc), hipMemcpyHostToDevice));
+	}
+	void require_params(bool inference) const {
+		NGP_CHECK(inference ? inference_params != nullptr : params != nullptr,
+		          "model has no parameters: call ngp_model_set_params or create a trainer first");
+	}
+	const f16* pick(bool inference) const { return inference ? inference_params : params; }
+	f16x8* prep(hipStream_t s, bool inference) {
+		f16x8* f = (f16x8*)(inference ? frags_inf : frags).get((size_t)n_all_frags * 1024);
+		prepare_frags(d_descs, n_all_frags, pick(inference), f, s);
+		return f;
+	}
+	void encode(hipStream_t s, uint32_t n, const float* in, uint32_t stride, f16* out, uint32_t out_stride, uint32_t layout, bool inference) {
+		if (enc_width > grid.n_levels * grid.n_features && layout == AoS) {
+			// zero the padding columns once per call (tcnn pads the encoding output with zeros)
+			NGP_HIP(hipMemsetAsync(out, 0, (size_t)n * out_stride * sizeof(f16), s));
+		}
+		GridFwdArgs a{n, in, stride, pick(inference) + grid_offset(), out, out_stride, layout, max_level, max_level_per_sample};
+		grid_forward(grid, a, s);
+	}
+	void run_mlp(hipStream_t s, MlpMode mode, uint32_t n, const float* in, uint32_t stride, const f16* encbuf, f16* out,
+	             uint32_t out_stride, uint32_t out_layout, const f16* dL, uint32_t dL_stride, f16* dL_denc, float* slab,
+	             bool inference) {
+		f16x8* f = prep(s, inference);
+		if (nerf) {
+			NerfMlpArgs a{};
+			a.n = n; a.enc = encbuf; a.enc_stride = enc_width; a.coords = in; a.coord_stride = stride; a.dir_offset = dir_offset;
+			a.frags = f; a.n_frags = n_all_frags; a.out = out; a.out_stride = out_stride; a.out_layout = out_layout;
+			a.dL_dout = dL; a.dL_stride = dL_stride; a.dL_denc = dL_denc; a.denc_stride = enc_width; a.dw_slab = slab;
+			a.n_matrix = (uint32_t)n_matrix(); a.density_woff = 0; a.rgb_woff = (uint32_t)mlp0_params;
+			nerf_mlp_run(nplan, mode, a, s);
+		} else {
+			MlpArgs a{};
+			a.n = n; a.enc = encbuf; a.enc_stride = enc_width; a.frags = f; a.n_frags = n_all_frags;
+			a.out = out; a.out_stride = out_stride; a.out_layout = out_layout; a.dL_dout = dL; a.dL_stride = dL_stride;
+			a.dL_denc = dL_denc; a.denc_stride = enc_width; a.dw_slab = slab; a.n_matrix = (uint32_t)n_matrix();
+			mlp_run(mplan, mode == MLP_DENSITY ? MLP_INFER : mode, a, s);
+		}
+	}
+	// backward given the encoding already in `encbuf`: MLP fwd+bwd (+output), dW slabs, grid scatter
+	void train_pass(hipStream_t s, uint32_t n, const float* in, uint32_t stride, const f16* encbuf, f16* out, uint32_t out_stride,
+	                const void* dL, uint32_t dL_stride, int grad_mode) {
+		NGP_CHECK(gradients, "model has no gradient buffer: call ngp_model_set_params");
+		f16* dL_denc = (f16*)denc.get((size_t)n * enc_width * sizeof(f16));
+		const uint32_t blocks = nerf ? nerf_mlp_train_blocks(n) : mlp_train_blocks(n);
+		float* slab = (float*)slabs.get((size_t)blocks * n_matrix() * sizeof(float));
+		run_mlp(s, MLP_TRAIN, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride, dL_denc, slab, false);
+		reduce_slabs(slab, blocks, (uint32_t)n_matrix(), gradients, grad_mode == NGP_GRAD_ACCUMULATE, s);
+		if (grad_mode != NGP_GRAD_ACCUMULATE)
+			NGP_HIP(hipMemsetAsync(gradients + grid_offset(), 0, grid_params * sizeof(f16), s));
+		GridBwdArgs b{n, in, stride, dL_denc, enc_width, AoS, gradients + grid_offset(), max_level, max_level_per_sample};
+		grid_backward(grid, b, s);
+	}
+};
+
+struct ngp_trainer {
+	ngp_model* model = nullptr;
+	AdamConfig cfg;
+	uint32_t step = 0;
+	uint64_t n = 0;
+	void* arena = nullptr;
+	float *w32 = nullptr, *m1 = nullptr, *m2 = nullptr, *ema32 = nullptr;
+	f16 *w16 = nullptr, *inf16 = nullptr, *g16 = nullptr;
+	uint32_t* steps = nullptr;
+	~ngp_trainer() { if (arena) (void)hipFree(arena); }
+};
+
+// ------------------------------------------------------------------------------------------------
+// C-ABI
+// ------------------------------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+
+#define NGP_TRY(...)                        \
+	try {                                   \
+		__VA_ARGS__;                        \
+		return NGP_OK;                      \
+	} catch (const std::exception& e) {     \
+		g_last_error = e.what();            \
+		return NGP_ERROR;                   \
+	}
+
+#define NGP_ARG(cond)                                                          \
+	do {                                                                       \
+		if (!(cond)) { g_last_error = "invalid argument: " #cond; return NGP_INVALID; } \
+	} while (0)
+
+static hipStream_t S(void* s) { return (hipStream_t)s; }
+
+extern "C" {
+
+const char* ngp_last_error(void) { return g_last_error.c_str(); }
+const char* ngp_version(void) { return "ngp-mi355x 0.1 (gfx950)"; }
+
+int ngp_device_info(int* cu_count, char* name, size_t name_len) {
+	NGP_TRY({
+		int dev = 0;
+		NGP_HIP(hipGetDevice(&dev));
+		hipDeviceProp_t p;
+		NGP_HIP(hipGetDeviceProperties(&p, dev));
+		if (cu_count) *cu_count = p.multiProcessorCount;
+		if (name && name_len) { strncpy(name, p.gcnArchName, name_len - 1); name[name_len - 1] = 0; }
+	});
+}
+
+int ngp_malloc(void** ptr, size_t bytes) { NGP_ARG(ptr); NGP_TRY(NGP_HIP(hipMalloc(ptr, bytes))); }
+int ngp_free(void* ptr) { NGP_TRY(NGP_HIP(hipFree(ptr))); }
+int ngp_memcpy(void* dst, const void* src, size_t bytes, int kind) { NGP_TRY(NGP_HIP(hipMemcpy(dst, src, bytes, (hipMemcpyKind)kind))); }
+int ngp_stream_synchronize(void* stream) { NGP_TRY(NGP_HIP(hipStreamSynchronize(S(stream)))); }
+
+int ngp_nerf_network_create(uint32_t n_pos_dims, uint32_t n_dir_dims, uint32_t n_extra_dims, uint32_t dir_offset,
+                            const char* pos_encoding_json, const char* dir_encoding_json, const char* density_network_json,
+                            const char* rgb_network_json, ngp_model** out) {
+	NGP_ARG(out && pos_encoding_json && density_network_json && rgb_network_json);
+	NGP_TRY({
+		auto m = std::make_unique<ngp_model>();
+		m->nerf = true;
+		NGP_CHECK(n_pos_dims == 3, "NerfNetwork: n_pos_dims must be 3");
+		NGP_CHECK(n_dir_dims == 3, "NerfNetwork: n_dir_dims must be 3");
+		NGP_CHECK(n_extra_dims == 0, "NerfNetwork: extra dims (latent codes) are not implemented");
+		m->n_pos_dims = n_pos_dims; m->n_dir_dims = n_dir_dims; m->n_extra_dims = n_extra_dims; m->dir_offset = dir_offset;
+		m->grid = parse_grid(3, Json::parse(pos_encoding_json));
+		if (dir_encoding_json) {
+			Json d = Json::parse(dir_encoding_json);
+			const Json* sh = &d;
+			if (iequals(d.string_or("otype", ""), "Composite")) sh = &d["nested"].arr.at(0);
+			NGP_CHECK(iequals(sh->string_or("otype", ""), "SphericalHarmonics") && (int)sh->number_or("degree", 4) == 4,
+			          "NerfNetwork: dir_encoding must be SphericalHarmonics of degree 4");
+		}
+		uint32_t wd, wr;
+		const uint32_t dh = parse_mlp_hidden(Json::parse(density_network_json), &wd);
+		const uint32_t rh = parse_mlp_hidden(Json::parse(rgb_network_json), &wr);
+		NGP_CHECK(wd == wr, "NerfNetwork: density and rgb networks must share n_neurons");
+		m->enc_width = next_multiple(m->grid.n_levels * m->grid.n_features, 16);
+		m->nplan = make_nerf_mlp_plan(m->enc_width, wd, dh, rh);
+		m->mlp0_params = m->nplan.density.n_params();
+		m->mlp1_params = m->nplan.rgb.n_params();
+		m->n_input_dims = dir_offset + n_dir_dims + n_extra_dims;
+		m->n_output_dims = 4;
+		m->finalize();
+		*out = m.release();
+	});
+}
+
+int ngp_network_with_input_encoding_create(uint32_t n_input_dims, uint32_t n_output_dims, const char* encoding_json,
+                                           const char* network_json, ngp_model** out) {
+	NGP_ARG(out && encoding_json && network_json);
+	NGP_TRY({
+		auto m = std::make_unique<ngp_model>();
+		m->nerf = false;
+		NGP_CHECK(n_input_dims == 2 || n_input_dims == 3, "NetworkWithInputEncoding: 2 or 3 input dims");
+		NGP_CHECK(n_output_dims >= 1 && n_output_dims <= 16, "NetworkWithInputEncoding: 1..16 outputs");
+		m->n_pos_dims = n_input_dims; m->n_input_dims = n_input_dims; m->n_output_dims = n_output_dims;
+		m->grid = parse_grid(n_input_dims, Json::parse(encoding_json));
+		uint32_t w;
+		const uint32_t hid = parse_mlp_hidden(Json::parse(network_json), &w);
+		m->enc_width = next_multiple(m->grid.n_levels * m->grid.n_features, 16);
+		m->mplan = make_mlp_plan(m->enc_width, w, hid, 16);
+		m->mlp0_params = m->mplan.mlp.n_params();
+		m->mlp1_params = 0;
+		m->finalize();
+		*out = m.release();
+	});
+}
+
+void ngp_model_destroy(ngp_model* m) { delete m; }
+uint64_t ngp_model_n_params(const ngp_model* m) { return m ? m->n_params : 0; }
+uint64_t ngp_model_n_matrix_params(const ngp_model* m) { return m ? m->n_matrix() : 0; }
+uint32_t ngp_model_input_width(const ngp_model* m) { return m ? m->n_input_dims : 0; }
+uint32_t ngp_model_padded_output_width(const ngp_model* m) { return m ? 16 : 0; }
+uint32_t ngp_model_output_width(const ngp_model* m) { return m ? m->n_output_dims : 0; }
+
+int ngp_model_param_layout(const ngp_model* m, ngp_param_layout* o) {
+	NGP_ARG(m && o);
+	NGP_TRY({
+		memset(o, 0, sizeof(*o));
+		o->density_mlp_offset = 0; o->density_mlp_params = m->mlp0_params;
+		o->rgb_mlp_offset = m->mlp0_params; o->rgb_mlp_params = m->mlp1_params;
+		o->grid_offset = m->grid_offset(); o->grid_params = m->grid_params;
+		o->grid_dims = m->grid.n_dims; o->grid_levels = m->grid.n_levels; o->grid_features = m->grid.n_features;
+		o->grid_log2_hashmap = m->grid.log2_hashmap; o->grid_base_resolution = m->grid.base_resolution;
+		o->grid_per_level_scale = m->grid.per_level_scale;
+		memcpy(o->grid_level_offsets, m->grid.offsets, sizeof(o->grid_level_offsets));
+		memcpy(o->grid_resolution, m->grid.resolution, sizeof(o->grid_resolution));
+		memcpy(o->grid_scale, m->grid.scale, sizeof(o->grid_scale));
+		o->encoding_width = m->enc_width;
+	});
+}
+
+int ngp_model_set_params(ngp_model* m, void* params, void* inference_params, void* gradients) {
+	NGP_ARG(m);
+	NGP_TRY({
+		m->params = (f16*)params;
+		m->inference_params = (f16*)(inference_params ? inference_params : params);
+		m->gradients = (f16*)gradients;
+	});
+}
+
+int ngp_model_initialize_params(const ngp_model* m, uint64_t seed, float* p, float scale) {
+	NGP_ARG(m && p);
+	NGP_TRY({
+		Pcg32 rng(seed);
+		if (m->nerf) {
+			init_mlp(m->nplan.density, rng, p, scale);
+			init_mlp(m->nplan.rgb, rng, p + m->mlp0_params, scale);
+		} else {
+			init_mlp(m->mplan.mlp, rng, p, scale);
+		}
+		rng.uniform(m->grid_params, p + m->grid_offset(), -1e-4f * scale, 1e-4f * scale);
+	});
+}
+
+int ngp_model_set_max_level(ngp_model* m, float max_level, const float* per_sample) {
+	NGP_ARG(m);
+	NGP_TRY({ m->max_level = max_level; m->max_level_per_sample = per_sample; });
+}
+
+int ngp_model_reserve(ngp_model* m, uint32_t n) {
+	NGP_ARG(m);
+	NGP_TRY({
+		m->enc.get((size_t)n * m->enc_width * sizeof(f16));
+		m->denc.get((size_t)n * m->enc_width * sizeof(f16));
+		m->slabs.get((size_t)nerf_mlp_train_blocks(n) * m->n_matrix() * sizeof(float));
+		m->frags.get((size_t)m->n_all_frags * 1024);
+		m->frags_inf.get((size_t)m->n_all_frags * 1024);
+	});
+}
+
+int ngp_encoding_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                         uint32_t output_stride, uint32_t output_layout, int use_inference_params) {
+	NGP_ARG(m && (n == 0 || (input && output)) && output_layout <= 1);
+	NGP_TRY({
+		m->require_params(use_inference_params);
+		m->encode(S(stream), n, input, input_stride, (f16*)output, output_stride, output_layout, use_inference_params);
+	});
+}
+
+int ngp_encoding_backward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                          const void* dL_doutput, uint32_t dL_stride, uint32_t dL_layout, int grad_mode) {
+	NGP_ARG(m && (n == 0 || (input && dL_doutput)) && dL_layout <= 1);
+	NGP_TRY({
+		NGP_CHECK(m->gradients, "model has no gradient buffer");
+		if (grad_mode != NGP_GRAD_ACCUMULATE)
+			NGP_HIP(hipMemsetAsync(m->gradients + m->grid_offset(), 0, m->grid_params * sizeof(f16), S(stream)));
+		GridBwdArgs b{n, input, input_stride, (const f16*)dL_doutput, dL_stride, dL_layout, m->gradients + m->grid_offset(),
+		              m->max_level, m->max_level_per_sample};
+		grid_backward(m->grid, b, S(stream));
+	});
+}
+
+int ngp_inference(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                  uint32_t output_stride, uint32_t output_layout, int use_inference_params) {
+	NGP_ARG(m && (n == 0 || (input && output)) && output_layout <= 1);
+	NGP_TRY({
+		if (n == 0) return NGP_OK;
+		m->require_params(use_inference_params);
+		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
+		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, use_inference_params);
+		m->run_mlp(S(stream), MLP_INFER, n, input, input_stride, e, (f16*)output, output_stride, output_layout, nullptr, 0,
+		           nullptr, nullptr, use_inference_params);
+		m->generation++;
+	});
+}
+
+int ngp_density(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                uint32_t output_stride, uint32_t output_layout, int use_inference_params) {
+	NGP_ARG(m && (n == 0 || (input && output)) && output_layout <= 1);
+	NGP_TRY({
+		NGP_CHECK(m->nerf, "density() is a NerfNetwork method");
+		if (n == 0) return NGP_OK;
+		m->require_params(use_inference_params);
+		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
+		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, use_inference_params);
+		m->run_mlp(S(stream), MLP_DENSITY, n, input, input_stride, e, (f16*)output, output_stride, output_layout, nullptr, 0,
+		           nullptr, nullptr, use_inference_params);
+		m->generation++;
+	});
+}
+
+int ngp_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                uint32_t output_stride, int use_inference_params, ngp_ctx** ctx) {
+	NGP_ARG(m && ctx && (n == 0 || input));
+	NGP_TRY({
+		m->require_params(use_inference_params);
+		f16* e = (f16*)m->enc.get((size_t)(n ? n : 1) * m->enc_width * sizeof(f16));
+		m->generation++;
+		if (n) {
+			m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, use_inference_params);
+			if (output)
+				m->run_mlp(S(stream), MLP_INFER, n, input, input_stride, e, (f16*)output, output_stride, AoS, nullptr, 0, nullptr,
+				           nullptr, use_inference_params);
+		}
+		*ctx = new ngp_ctx{n, input, input_stride, (bool)use_inference_params, m->generation};
+	});
+}
+
+int ngp_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* dL_doutput, uint32_t dL_stride, int grad_mode) {
+	NGP_ARG(m && ctx && (ctx->n == 0 || dL_doutput));
+	NGP_TRY({
+		NGP_CHECK(ctx->generation == m->generation,
+		          "backward: the forward context is stale (another forward/inference ran on this model since)");
+		if (ctx->n == 0) return NGP_OK;
+		m->train_pass(S(stream), ctx->n, ctx->input, ctx->input_stride, (const f16*)m->enc.p, nullptr, 0, dL_doutput, dL_stride,
+		              grad_mode);
+	});
+}
+
+void ngp_ctx_destroy(ngp_ctx* ctx) { delete ctx; }
+
+int ngp_forward_backward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                         uint32_t output_stride, const void* dL_doutput, uint32_t dL_stride, int grad_mode) {
+	NGP_ARG(m && (n == 0 || (input && dL_doutput)));
+	NGP_TRY({
+		if (n == 0) return NGP_OK;
+		m->require_params(false);
+		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
+		m->generation++;
+		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, false);
+		m->train_pass(S(stream), n, input, input_stride, e, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode);
+	});
+}
+
+// ---- trainer ------------------------------------------------------------------------------
+static void parse_optimizer(const Json& j, AdamConfig& c) {
+	const std::string ot = j.string_or("otype", "Adam");
+	if (iequals(ot, "Ema")) {
+		c.ema_decay = (float)j.number_or("decay", 0.99);
+		parse_optimizer(j["nested"], c);
+	} else if (iequals(ot, "ExponentialDecay")) {
+		c.decay_start = (uint32_t)j.number_or("decay_start", 0);
+		c.decay_interval = (uint32_t)j.number_or("decay_interval", 10000);
+		c.decay_base = (float)j.number_or("decay_base", 0.1);
+		parse_optimizer(j["nested"], c);
+	} else if (iequals(ot, "Adam")) {
+		c.lr = (float)j.number_or("learning_rate", 1e-3);
+		c.beta1 = (float)j.number_or("beta1", 0.9);
+		c.beta2 = (float)j.number_or("beta2", 0.999);
+		c.eps = (float)j.number_or("epsilon", 1e-8);
+		c.l2 = (float)j.number_or("l2_reg", 1e-8);
+	} else {
+		throw Error("optimizer: unsupported otype " + ot + " (Ema / ExponentialDecay / Adam implemented)");
+	}
+}
+
+int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, ngp_trainer** out) {
+	NGP_ARG(m && out);
+	NGP_TRY({
+		auto t = std::make_unique<ngp_trainer>();
+		t->model = m;
+		if (optimizer_json) parse_optimizer(Json::parse(optimizer_json), t->cfg);
+		const uint64_t n = m->n_params;
+		t->n = n;
+		auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+		const size_t b32 = al(n * 4), b16 = al(n * 2);
+		const size_t total = 4 * b32 + 3 * b16 + b32 /*steps*/;
+		NGP_HIP(hipMalloc(&t->arena, total));
+		char* p = (char*)t->arena;
+		t->w32 = (float*)p; p += b32;
+		t->m1 = (float*)p; p += b32;
+		t->m2 = (float*)p; p += b32;
+		t->ema32 = (float*)p; p += b32;
+		t->steps = (uint32_t*)p; p += b32;
+		t->w16 = (f16*)p; p += b16;
+		t->inf16 = (f16*)p; p += b16;
+		t->g16 = (f16*)p; p += b16;
+		NGP_HIP(hipMemset(t->arena, 0, total));
+		std::vector<float> host(n);
+		if (ngp_model_initialize_params(m, seed, host.data(), 1.0f) != NGP_OK) throw Error(g_last_error);
+		*out = t.release();
+		if (ngp_trainer_set_params_full_precision(*out, host.data(), n) != NGP_OK) throw Error(g_last_error);
+	});
+}
+
+void ngp_trainer_destroy(ngp_trainer* t) {
+	if (!t) return;
+	if (t->model && t->model->params == t->w16) ngp_model_set_params(t->model, nullptr, nullptr, nullptr);
+	delete t;
+}
+
+int ngp_trainer_optimizer_step(ngp_trainer* t, void* stream, float loss_scale) {
+	NGP_ARG(t && loss_scale > 0.f);
+	NGP_TRY({
+		adam_ema_step(t->cfg, t->step, (uint32_t)t->n, (uint32_t)t->model->n_matrix(), loss_scale, t->w32, t->w16, t->g16, t->m1,
+		              t->m2, t->steps, t->ema32, t->inf16, S(stream));
+		t->step++;
+	});
+}
+
+void* ngp_trainer_gradients(ngp_trainer* t) { return t ? t->g16 : nullptr; }
+void* ngp_trainer_params(ngp_trainer* t) { return t ? t->w16 : nullptr; }
+void* ngp_trainer_inference_params(ngp_trainer* t) { return t ? (t->cfg.ema_decay > 0.f ? t->inf16 : t->w16) : nullptr; }
+float* ngp_trainer_params_full_precision(ngp_trainer* t) { return t ? t->w32 : nullptr; }
+uint32_t ngp_trainer_step(const ngp_trainer* t) { return t ? t->step : 0; }
+float ngp_trainer_learning_rate(const ngp_trainer* t) { return t ? t->cfg.lr_at(t->step) : 0.f; }
+int ngp_trainer_set_learning_rate(ngp_trainer* t, float lr) {
+	NGP_ARG(t && lr >= 0.f);
+	NGP_TRY({ t->cfg.lr = lr; });
+}
+
+__global__ static void k_f32_to_f16(const float* a, f16* b, f16* c, uint64_t n) {
+	const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+	if (i < n) { b[i] = (f16)a[i]; c[i] = (f16)a[i]; }
+}
+
+int ngp_trainer_set_params_full_precision(ngp_trainer* t, const float* params_host, uint64_t n) {
+	NGP_ARG(t && params_host && n == t->n);
+	NGP_TRY({
+		NGP_HIP(hipMemcpy(t->w32, params_host, n * 4, hipMemcpyHostToDevice));
+		k_f32_to_f16<<<div_round_up(n, 256), 256>>>(t->w32, t->w16, t->inf16, n);
+		NGP_HIP(hipGetLastError());
+		NGP_HIP(hipDeviceSynchronize());
+		ngp_model_set_params(t->model, t->w16, t->cfg.ema_decay > 0.f ? t->inf16 : t->w16, t->g16);
+	});
+}
+
+// Blob: magic, version, n, step, then w32, m1, m2, ema32 (f32), steps (u32)
+int ngp_trainer_serialize(ngp_trainer* t, void* buf, uint64_t* size) {
+	NGP_ARG(t && size);
+	NGP_TRY({
+		const uint64_t need = 32 + t->n * 4 * 5;
+		if (!buf) { *size = need; return NGP_OK; }
+		NGP_CHECK(*size >= need, "serialize: buffer too small");
+		char* p = (char*)buf;
+		const uint64_t hdr[4] = {0x4e47504d49333535ULL /* "NGPMI355" */, 1, t->n, t->step};
+		memcpy(p, hdr, 32); p += 32;
+		NGP_HIP(hipDeviceSynchronize());
+		for (void* src : {(void*)t->w32, (void*)t->m1, (void*)t->m2, (void*)t->ema32, (void*)t->steps}) {
+			NGP_HIP(hipMemcpy(p, src, t->n * 4, hipMemcpyDeviceToHost));
+			p += t->n * 4;
+		}
+		*size = need;
+	});
+}
+
+int ngp_trainer_deserialize(ngp_trainer* t, const void* buf, uint64_t size) {
+	NGP_ARG(t && buf);
+	NGP_TRY({
+		const char* p = (const char*)buf;
+		uint64_t hdr[4];
+		NGP_CHECK(size >= 32, "deserialize: truncated");
+		memcpy(hdr, p, 32); p += 32;
+		NGP_CHECK(hdr[0] == 0x4e47504d49333535ULL && hdr[1] == 1, "deserialize: bad magic/version");
+		NGP_CHECK(hdr[2] == t->n && size >= 32 + t->n * 20, "deserialize: parameter count mismatch");
+		t->step = (uint32_t)hdr[3];
+		for (void* dst : {(void*)t->w32, (void*)t->m1, (void*)t->m2, (void*)t->ema32, (void*)t->steps}) {
+			NGP_HIP(hipMemcpy(dst, p, t->n * 4, hipMemcpyHostToDevice));
+			p += t->n * 4;
+		}
+		k_f32_to_f16<<<div_round_up(t->n, 256), 256>>>(t->w32, t->w16, t->inf16, t->n);
+		NGP_HIP(hipGetLastError());
+		NGP_HIP(hipDeviceSynchronize());
+	});
+}
+
+}  // extern "C"

@@ -1,0 +1,222 @@
+// grid.hip — hash-grid encoding kernels (forward gather, backward packed-fp16 scatter).
+//
+// Forward: one thread per sample walks all levels; per level the 2^D corner entries are gathered as
+// one F*2-byte vector each (8 B for F=4) from the L2/Infinity-Cache-resident table and trilinearly
+// blended in fp32 (tcnn blends in the table precision; see DESIGN.md §Grid for the tolerance).
+// Backward: F/2 lanes per sample so that the lanes updating one entry hit one 64-B atomic segment —
+// MI355X executes global float atomics at the memory side at ~21 G requests/s (measured,
+// profiles/r01_atomics.txt), so requests, not bytes, are the cost.
+#include "grid.h"
+
+#include <cmath>
+#include <cstring>
+
+namespace ngp {
+
+void grid_desc_init(GridDesc& g, uint32_t D, uint32_t L, uint32_t F, uint32_t log2T, uint32_t Nmin, float b) {
+	NGP_CHECK(D == 2 || D == 3, "GridEncoding: n_dims must be 2 or 3");
+	NGP_CHECK(L >= 1 && L <= 32, "GridEncoding: n_levels must be in [1, 32]");
+	NGP_CHECK(F == 1 || F == 2 || F == 4 || F == 8, "GridEncoding: n_features_per_level must be 1, 2, 4 or 8");
+	NGP_CHECK(log2T >= 4 && log2T <= 28, "GridEncoding: log2_hashmap_size out of range");
+	g = GridDesc{};
+	g.n_dims = D; g.n_levels = L; g.n_features = F; g.log2_hashmap = log2T; g.base_resolution = Nmin;
+	g.per_level_scale = b;
+	const float log2b = log2f(b);
+	uint32_t off = 0;
+	for (uint32_t l = 0; l < L; ++l) {
+		float s = exp2f((float)l * log2b) * (float)Nmin - 1.0f;
+		uint32_t res = (uint32_t)ceilf(s) + 1u;
+		g.scale[l] = s;
+		g.resolution[l] = res;
+		const uint32_t max_params = 0xffffffffu / 2;
+		uint32_t n;
+		if (powf((float)res, (float)D) > (float)max_params) n = max_params;
+		else { n = 1; for (uint32_t d = 0; d < D; ++d) n *= res; }
+		n = (n + 7u) / 8u * 8u;
+		if (n > (1u << log2T)) n = 1u << log2T;
+		g.offsets[l] = off;
+		off += n;
+	}
+	g.offsets[L] = off;
+}
+
+static GridConst make_const(const GridDesc& g) {
+	GridConst c;
+	c.n_levels = g.n_levels;
+	c.n_features = g.n_features;
+	memcpy(c.offsets, g.offsets, sizeof(c.offsets));
+	memcpy(c.scale, g.scale, sizeof(c.scale));
+	memcpy(c.resolution, g.resolution, sizeof(c.resolution));
+	return c;
+}
+
+template <uint32_t F> struct FeatVec;
+template <> struct FeatVec<1> { typedef f16 T; };
+template <> struct FeatVec<2> { typedef f16x2 T; };
+template <> struct FeatVec<4> { typedef f16x4 T; };
+template <> struct FeatVec<8> { typedef f16x8 T; };
+
+template <uint32_t D>
+__device__ __forceinline__ uint32_t corner_index(const GridConst& c, uint32_t l, const uint32_t* base, uint32_t corner) {
+	const uint32_t T = c.offsets[l + 1] - c.offsets[l];
+	const uint32_t res = c.resolution[l];
+	const uint32_t x = base[0] + (corner & 1u);
+	const uint32_t y = base[1] + ((corner >> 1) & 1u);
+	if constexpr (D == 3) {
+		const uint32_t z = base[2] + ((corner >> 2) & 1u);
+		return c.offsets[l] + grid_index3(T, res, x, y, z);
+	} else {
+		return c.offsets[l] + grid_index2(T, res, x, y);
+	}
+}
+
+template <uint32_t D>
+__device__ __forceinline__ float corner_weight(const float* frac, uint32_t corner) {
+	float w = 1.0f;
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) w *= ((corner >> d) & 1u) ? frac[d] : 1.0f - frac[d];
+	return w;
+}
+
+template <uint32_t D>
+__device__ __forceinline__ void level_setup(const GridConst& c, uint32_t l, const float* x, float* frac, uint32_t* base) {
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) {
+		float p = __builtin_fmaf(c.scale[l], x[d], 0.5f);
+		float t = floorf(p);
+		base[d] = (uint32_t)(int)t;
+		frac[d] = p - t;
+	}
+}
+
+template <uint32_t D, uint32_t F>
+__global__ void __launch_bounds__(256) k_grid_forward(const GridConst c, const GridFwdArgs a) {
+	typedef typename FeatVec<F>::T V;
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= a.n) return;
+	float x[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * a.pos_stride + d];
+	const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
+	for (uint32_t l = 0; l < c.n_levels; ++l) {
+		float acc[F];
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) acc[f] = 0.f;
+		if (!((float)l >= ml + 1e-3f)) {
+			float frac[D]; uint32_t base[D];
+			level_setup<D>(c, l, x, frac, base);
+			V v[1u << D];
+#pragma unroll
+			for (uint32_t k = 0; k < (1u << D); ++k) v[k] = *(const V*)(a.table + (size_t)corner_index<D>(c, l, base, k) * F);
+#pragma unroll
+			for (uint32_t k = 0; k < (1u << D); ++k) {
+				const float w = corner_weight<D>(frac, k);
+				if constexpr (F == 1) acc[0] = __builtin_fmaf(w, (float)v[k], acc[0]);
+				else {
+#pragma unroll
+					for (uint32_t f = 0; f < F; ++f) acc[f] = __builtin_fmaf(w, (float)v[k][f], acc[f]);
+				}
+			}
+		}
+		if (a.out_layout == AoS) {
+			V o;
+			if constexpr (F == 1) o = (f16)acc[0];
+			else {
+#pragma unroll
+				for (uint32_t f = 0; f < F; ++f) o[f] = (f16)acc[f];
+			}
+			*(V*)(a.out + (size_t)i * a.out_stride + l * F) = o;
+		} else {
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) a.out[(size_t)(l * F + f) * a.out_stride + i] = (f16)acc[f];
+		}
+	}
+}
+
+// Backward: thread t handles sample t / P and feature pair t % P (P = max(F/2, 1)).
+template <uint32_t D, uint32_t F>
+__global__ void __launch_bounds__(256) k_grid_backward(const GridConst c, const GridBwdArgs a) {
+	constexpr uint32_t P = F >= 2 ? F / 2 : 1;
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t i = t / P;
+	const uint32_t pair = t % P;
+	if (i >= a.n) return;
+	float x[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * a.pos_stride + d];
+	const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
+	for (uint32_t l = 0; l < c.n_levels; ++l) {
+		if ((float)l > ml + 1e-3f) break;
+		float g0, g1;
+		const uint32_t f0 = l * F + (F >= 2 ? 2 * pair : 0);
+		if (a.dy_layout == AoS) {
+			if constexpr (F >= 2) {
+				f16x2 g = *(const f16x2*)(a.dL_dy + (size_t)i * a.dy_stride + f0);
+				g0 = (float)g[0]; g1 = (float)g[1];
+			} else {
+				g0 = (float)a.dL_dy[(size_t)i * a.dy_stride + f0]; g1 = 0.f;
+			}
+		} else {
+			g0 = (float)a.dL_dy[(size_t)f0 * a.dy_stride + i];
+			g1 = F >= 2 ? (float)a.dL_dy[(size_t)(f0 + 1) * a.dy_stride + i] : 0.f;
+		}
+		float frac[D]; uint32_t base[D];
+		level_setup<D>(c, l, x, frac, base);
+#pragma unroll
+		for (uint32_t k = 0; k < (1u << D); ++k) {
+			const float w = corner_weight<D>(frac, k);
+			const uint32_t e = corner_index<D>(c, l, base, k);
+			if constexpr (F >= 2) {
+				atomic_add_f16x2(a.grad + (size_t)e * F + 2 * pair, f16x2{(f16)(w * g0), (f16)(w * g1)});
+			} else {
+				// F == 1: pack with a +0 partner so the 4-byte aligned packed add touches only entry e
+				const size_t idx = e;
+				f16x2 v = (idx & 1) ? f16x2{(f16)0.f, (f16)(w * g0)} : f16x2{(f16)(w * g0), (f16)0.f};
+				atomic_add_f16x2(a.grad + (idx & ~(size_t)1), v);
+			}
+		}
+	}
+}
+
+template <uint32_t D>
+static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hipStream_t s) {
+	const dim3 grid(div_round_up(a.n, 256)), block(256);
+	switch (F) {
+		case 1: k_grid_forward<D, 1><<<grid, block, 0, s>>>(c, a); break;
+		case 2: k_grid_forward<D, 2><<<grid, block, 0, s>>>(c, a); break;
+		case 4: k_grid_forward<D, 4><<<grid, block, 0, s>>>(c, a); break;
+		case 8: k_grid_forward<D, 8><<<grid, block, 0, s>>>(c, a); break;
+		default: throw Error("GridEncoding: unsupported F");
+	}
+}
+
+template <uint32_t D>
+static void launch_bwd(uint32_t F, const GridConst& c, const GridBwdArgs& a, hipStream_t s) {
+	const uint32_t P = F >= 2 ? F / 2 : 1;
+	const dim3 grid(div_round_up((uint64_t)a.n * P, 256)), block(256);
+	switch (F) {
+		case 1: k_grid_backward<D, 1><<<grid, block, 0, s>>>(c, a); break;
+		case 2: k_grid_backward<D, 2><<<grid, block, 0, s>>>(c, a); break;
+		case 4: k_grid_backward<D, 4><<<grid, block, 0, s>>>(c, a); break;
+		case 8: k_grid_backward<D, 8><<<grid, block, 0, s>>>(c, a); break;
+		default: throw Error("GridEncoding: unsupported F");
+	}
+}
+
+void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream) {
+	if (a.n == 0) return;
+	GridConst c = make_const(g);
+	if (g.n_dims == 3) launch_fwd<3>(g.n_features, c, a, stream);
+	else launch_fwd<2>(g.n_features, c, a, stream);
+	NGP_HIP(hipGetLastError());
+}
+
+void grid_backward(const GridDesc& g, const GridBwdArgs& a, hipStream_t stream) {
+	if (a.n == 0) return;
+	GridConst c = make_const(g);
+	if (g.n_dims == 3) launch_bwd<3>(g.n_features, c, a, stream);
+	else launch_bwd<2>(g.n_features, c, a, stream);
+	NGP_HIP(hipGetLastError());
+}
+
+}  // namespace ngp

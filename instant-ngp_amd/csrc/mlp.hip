@@ -1,0 +1,713 @@
+// mlp.hip — MFMA kernels for the NerfNetwork MLP pair and for a single MLP (see mlp.h for the
+// register/LDS layout contract).
+#include "mlp.h"
+
+namespace ngp {
+
+// ------------------------------------------------------------------------------------------------
+// Fragment plans
+// ------------------------------------------------------------------------------------------------
+static void add_frags(std::vector<FragDesc>& v, uint32_t woff, uint32_t in, uint32_t out, uint32_t tiles, uint32_t steps,
+                      bool transposed, int perm_steps_mask) {
+	for (uint32_t t = 0; t < tiles; ++t)
+		for (uint32_t s = 0; s < steps; ++s) {
+			FragDesc d;
+			d.woff = woff; d.in_dim = (uint16_t)in; d.out_dim = (uint16_t)out;
+			d.tile = (uint8_t)t; d.step = (uint8_t)s; d.transposed = transposed ? 1 : 0;
+			d.perm = (perm_steps_mask >> s) & 1;
+			v.push_back(d);
+		}
+}
+
+NerfMlpPlan make_nerf_mlp_plan(uint32_t enc_width, uint32_t width, uint32_t d_hidden, uint32_t r_hidden) {
+	NGP_CHECK(width == 64, "FullyFusedMLP: this engine implements n_neurons == 64");
+	NGP_CHECK(enc_width == 16 || enc_width == 32, "NerfNetwork: position encoding width must pad to 16 or 32");
+	NGP_CHECK(d_hidden >= 1 && d_hidden <= 3 && r_hidden >= 1 && r_hidden <= 3, "NerfNetwork: 1..3 hidden layers supported");
+	NerfMlpPlan p;
+	p.enc_steps = enc_width / 16; p.d_hidden = d_hidden; p.r_hidden = r_hidden;
+	p.density = MlpDims{enc_width, width, d_hidden, 16};
+	p.rgb = MlpDims{32, width, r_hidden, 16};
+	const uint32_t rw = p.density.n_params();  // rgb MLP follows the density MLP (nerf_network.h:430-443)
+	auto& v = p.descs;
+	// forward fragments
+	add_frags(v, p.density.layer_off(0), enc_width, 64, 2, p.enc_steps, false, 0);
+	for (uint32_t h = 1; h < d_hidden; ++h) add_frags(v, p.density.layer_off(h), 64, 64, 2, 4, false, 0xF);
+	add_frags(v, p.density.layer_off(d_hidden), 64, 16, 1, 4, false, 0xF);
+	add_frags(v, rw + p.rgb.layer_off(0), 32, 64, 2, 2, false, 0x1);  // step 0 = packed density output, step 1 = SH
+	for (uint32_t h = 1; h < r_hidden; ++h) add_frags(v, rw + p.rgb.layer_off(h), 64, 64, 2, 4, false, 0xF);
+	add_frags(v, rw + p.rgb.layer_off(r_hidden), 64, 16, 1, 4, false, 0xF);
+	p.n_fwd_frags = (uint32_t)v.size();
+	// backward (transposed) fragments, in the order the backward chain consumes them
+	add_frags(v, rw + p.rgb.layer_off(r_hidden), 64, 16, 2, 1, true, 0xF);
+	for (uint32_t h = r_hidden - 1; h >= 1; --h) add_frags(v, rw + p.rgb.layer_off(h), 64, 64, 2, 4, true, 0xF);
+	add_frags(v, rw + p.rgb.layer_off(0), 32, 64, 1, 4, true, 0xF);
+	add_frags(v, p.density.layer_off(d_hidden), 64, 16, 2, 1, true, 0xF);
+	for (uint32_t h = d_hidden - 1; h >= 1; --h) add_frags(v, p.density.layer_off(h), 64, 64, 2, 4, true, 0xF);
+	add_frags(v, p.density.layer_off(0), enc_width, 64, (enc_width + 31) / 32, 4, true, 0xF);
+	p.n_bwd_frags = (uint32_t)v.size() - p.n_fwd_frags;
+	return p;
+}
+
+MlpPlan make_mlp_plan(uint32_t enc_width, uint32_t width, uint32_t hidden, uint32_t out_pad) {
+	NGP_CHECK(width == 64, "FullyFusedMLP: this engine implements n_neurons == 64");
+	NGP_CHECK(enc_width == 16 || enc_width == 32, "NetworkWithInputEncoding: encoding width must pad to 16 or 32");
+	NGP_CHECK(out_pad == 16, "FullyFusedMLP: output width must pad to 16");
+	NGP_CHECK(hidden >= 1 && hidden <= 4, "FullyFusedMLP: 1..4 hidden layers supported");
+	MlpPlan p;
+	p.enc_steps = enc_width / 16; p.hidden = hidden;
+	p.mlp = MlpDims{enc_width, width, hidden, out_pad};
+	auto& v = p.descs;
+	add_frags(v, p.mlp.layer_off(0), enc_width, 64, 2, p.enc_steps, false, 0);
+	for (uint32_t h = 1; h < hidden; ++h) add_frags(v, p.mlp.layer_off(h), 64, 64, 2, 4, false, 0xF);
+	add_frags(v, p.mlp.layer_off(hidden), 64, 16, 1, 4, false, 0xF);
+	p.n_fwd_frags = (uint32_t)v.size();
+	add_frags(v, p.mlp.layer_off(hidden), 64, 16, 2, 1, true, 0xF);
+	for (uint32_t h = hidden - 1; h >= 1; --h) add_frags(v, p.mlp.layer_off(h), 64, 64, 2, 4, true, 0xF);
+	add_frags(v, p.mlp.layer_off(0), enc_width, 64, (enc_width + 31) / 32, 4, true, 0xF);
+	p.n_bwd_frags = (uint32_t)v.size() - p.n_fwd_frags;
+	return p;
+}
+
+// k index held by element j of lane half h in k-step s.
+__device__ __forceinline__ uint32_t frag_k(uint32_t s, uint32_t j, uint32_t h, bool perm) {
+	return perm ? 16 * s + 8 * (j >> 2) + 4 * h + (j & 3) : 16 * s + 8 * h + j;
+}
+
+__global__ void k_prepare_frags(const FragDesc* __restrict__ descs, uint32_t n_frags, const f16* __restrict__ params,
+                                f16x8* __restrict__ frags) {
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= n_frags * 64) return;
+	const FragDesc d = descs[t / 64];
+	const uint32_t lane = t % 64, h = lane >> 5, r = 32 * d.tile + (lane & 31);
+	f16x8 v;
+#pragma unroll
+	for (uint32_t j = 0; j < 8; ++j) {
+		const uint32_t k = frag_k(d.step, j, h, d.perm);
+		f16 x = (f16)0.f;
+		if (!d.transposed) {  // A = W: row r = output unit, k = input unit
+			if (r < d.out_dim && k < d.in_dim) x = params[d.woff + r * d.in_dim + k];
+		} else {              // A = W^T: row r = input unit, k = output unit
+			if (r < d.in_dim && k < d.out_dim) x = params[d.woff + k * d.in_dim + r];
+		}
+		v[j] = x;
+	}
+	frags[t] = v;
+}
+
+void prepare_frags(const FragDesc* descs_dev, uint32_t n_frags, const f16* params, f16x8* frags, hipStream_t s) {
+	k_prepare_frags<<<div_round_up(n_frags * 64, 256), 256, 0, s>>>(descs_dev, n_frags, params, frags);
+	NGP_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// Device building blocks
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ f32x16 mfma32(f16x8 a, f16x8 b, f32x16 c) {
+	return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+	return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// acc[t] = sum_s A(frag base + t*STEPS + s) * in[s]
+template <int TILES, int STEPS>
+__device__ __forceinline__ void layer_fwd(f32x16 (&acc)[TILES], const f16x8 (&in)[STEPS], const f16x8* frags, int lane) {
+#pragma unroll
+	for (int t = 0; t < TILES; ++t) {
+		f32x16 c = {};
+#pragma unroll
+		for (int s = 0; s < STEPS; ++s) c = mfma32(frags[(t * STEPS + s) * 64 + lane], in[s], c);
+		acc[t] = c;
+	}
+}
+
+// Round an accumulator tile to fp16 (optionally ReLU) and split into the two k-step fragments.
+__device__ __forceinline__ void pack_tile(const f32x16& a, f16x8& lo, f16x8& hi, bool relu) {
+#pragma unroll
+	for (int j = 0; j < 8; ++j) {
+		f16 x = (f16)a[j], y = (f16)a[8 + j];
+		if (relu) { x = x > (f16)0.f ? x : (f16)0.f; y = y > (f16)0.f ? y : (f16)0.f; }
+		lo[j] = x; hi[j] = y;
+	}
+}
+
+template <int TILES>
+__device__ __forceinline__ void pack_tiles(const f32x16 (&acc)[TILES], f16x8 (&out)[2 * TILES], bool relu) {
+#pragma unroll
+	for (int t = 0; t < TILES; ++t) pack_tile(acc[t], out[2 * t], out[2 * t + 1], relu);
+}
+
+// ReLU backward against the saved (packed) forward activation, then round to fp16.
+template <int TILES>
+__device__ __forceinline__ void mask_pack(const f32x16 (&acc)[TILES], const f16x8 (&act)[2 * TILES], f16x8 (&out)[2 * TILES]) {
+#pragma unroll
+	for (int t = 0; t < TILES; ++t)
+#pragma unroll
+		for (int r = 0; r < 16; ++r) {
+			const f16 a = act[2 * t + (r >> 3)][r & 7];
+			const f16 g = (f16)acc[t][r];
+			out[2 * t + (r >> 3)][r & 7] = a > (f16)0.f ? g : (f16)0.f;
+		}
+}
+
+// Write packed accumulator-layout fragments (frags[2t+s] = tile t regs 8s..8s+7) of one sample
+// column into the wave's [sample][feature] image: features 32t + 16s + 8k + 4h + (0..3).
+template <int NFRAG>
+__device__ __forceinline__ void img_store_acc(f16* img, int stride, const f16x8 (&f)[NFRAG], int lane, int feat0 = 0) {
+	const int smp = lane & 31, h = lane >> 5;
+	f16* row = img + smp * stride + feat0 + 4 * h;
+#pragma unroll
+	for (int q = 0; q < NFRAG; ++q) {
+		// frag q covers tile q>>1, regs 8(q&1)..: features 32(q>>1) + 16(q&1) + 8k + 4h, k = 0,1
+		const int base = 32 * (q >> 1) + 16 * (q & 1);
+		*(f16x4*)(row + base) = f16x4{f[q][0], f[q][1], f[q][2], f[q][3]};
+		*(f16x4*)(row + base + 8) = f16x4{f[q][4], f[q][5], f[q][6], f[q][7]};
+	}
+}
+
+// Standard-order fragment (lane half h holds features 16s + 8h + 0..7) into the image.
+__device__ __forceinline__ void img_store_std(f16* img, int stride, const f16x8& f, int s, int lane) {
+	const int smp = lane & 31, h = lane >> 5;
+	*(f16x8*)(img + smp * stride + 16 * s + 8 * h) = f;
+}
+
+// Operand for v_mfma_f32_16x16x32_f16 with K = the 32 samples: lane gets feature feat0 + (lane&15),
+// samples 8(lane>>4) + 0..7, via two ds_read_b64_tr_b16 (4 samples x 16 features per 16-lane group).
+__device__ __forceinline__ f16x8 img_frag(const f16* img, int stride, int feat0, int lane) {
+	const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+	const f16* a0 = img + (8 * g + q) * stride + feat0 + 4 * p;
+	const f16x4 lo = lds_read_tr16(a0);
+	const f16x4 hi = lds_read_tr16(a0 + 4 * stride);
+	return f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// dW[out x in] += dZ * X^T over the wave's 32 samples, 16x16 tiles (mt over out, nt over in).
+template <int MT, int NT>
+__device__ __forceinline__ void dw_accum(f32x4* dw, const f16* dz_img, int dz_stride, const f16* x_img, int x_stride, int lane) {
+	f16x8 a[MT], b[NT];
+#pragma unroll
+	for (int m = 0; m < MT; ++m) a[m] = img_frag(dz_img, dz_stride, 16 * m, lane);
+#pragma unroll
+	for (int n = 0; n < NT; ++n) b[n] = img_frag(x_img, x_stride, 16 * n, lane);
+#pragma unroll
+	for (int m = 0; m < MT; ++m)
+#pragma unroll
+		for (int n = 0; n < NT; ++n) dw[m * NT + n] = mfma16(a[m], b[n], dw[m * NT + n]);
+}
+
+// Flush one layer's dW tiles (16x16, 4 regs: out = 16m + 4(lane>>4) + r, in = 16n + (lane&15)) into
+// the block's fp32 LDS reduction buffer laid out as the parameter slice [out x in].
+template <int MT, int NT>
+__device__ __forceinline__ void dw_flush(const f32x4* dw, float* red, uint32_t woff, uint32_t in_dim, int lane) {
+#pragma unroll
+	for (int m = 0; m < MT; ++m)
+#pragma unroll
+		for (int n = 0; n < NT; ++n)
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const uint32_t o = 16 * m + 4 * (lane >> 4) + r, i = 16 * n + (lane & 15);
+				atomicAdd(red + woff + o * in_dim + i, dw[m * NT + n][r]);
+			}
+}
+
+// SH degree 4 of the warped direction (tcnn SphericalHarmonics; oracle orc_sh4), features 8h..8h+7.
+__device__ __forceinline__ f16x8 sh4_frag(float dx, float dy, float dz, int h) {
+	const float x = dx * 2.f - 1.f, y = dy * 2.f - 1.f, z = dz * 2.f - 1.f;
+	const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+	float o[8];
+	if (h == 0) {
+		o[0] = 0.28209479177387814f;
+		o[1] = -0.48860251190291987f * y;
+		o[2] = 0.48860251190291987f * z;
+		o[3] = -0.48860251190291987f * x;
+		o[4] = 1.0925484305920792f * xy;
+		o[5] = -1.0925484305920792f * yz;
+		o[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+		o[7] = -1.0925484305920792f * xz;
+	} else {
+		o[0] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+		o[1] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
+		o[2] = 2.8906114426405538f * xy * z;
+		o[3] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
+		o[4] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
+		o[5] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
+		o[6] = 1.4453057213202769f * z * (x2 - y2);
+		o[7] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+	}
+	f16x8 r;
+#pragma unroll
+	for (int j = 0; j < 8; ++j) r[j] = (f16)o[j];
+	return r;
+}
+
+// Store rows 0..15 of an accumulator-layout output (regs 0..7) for one sample: lane half h holds
+// rows 4h..4h+3 (regs 0..3) and 8+4h..8+4h+3 (regs 4..7).
+__device__ __forceinline__ void store_out16(f16* out, uint32_t stride, uint32_t layout, uint32_t n, uint32_t sample, int h,
+                                            const f16x8& v) {
+	if (layout == 0) {
+		f16* row = out + (size_t)sample * stride;
+		*(f16x4*)(row + 4 * h) = f16x4{v[0], v[1], v[2], v[3]};
+		*(f16x4*)(row + 8 + 4 * h) = f16x4{v[4], v[5], v[6], v[7]};
+	} else {
+#pragma unroll
+		for (int j = 0; j < 8; ++j) out[(size_t)(8 * (j >> 2) + 4 * h + (j & 3)) * stride + sample] = v[j];
+	}
+}
+
+// ------------------------------------------------------------------------------------------------
+// NerfNetwork MLP pair: density (enc -> 64 x DH -> 16) and rgb ([density out | SH] -> 64 x RH -> 16)
+// ------------------------------------------------------------------------------------------------
+template <int ES, int DH, int RH>
+struct NerfLayout {
+	// forward fragment offsets
+	static constexpr int F_D0 = 0;
+	static constexpr int F_DH = F_D0 + 2 * ES;
+	static constexpr int F_DO = F_DH + 8 * (DH - 1);
+	static constexpr int F_R0 = F_DO + 4;
+	static constexpr int F_RH = F_R0 + 4;
+	static constexpr int F_RO = F_RH + 8 * (RH - 1);
+	static constexpr int N_FWD = F_RO + 4;
+	// backward fragment offsets
+	static constexpr int B_RO = N_FWD;
+	static constexpr int B_RH = B_RO + 2;                 // layers RH-1 .. 1
+	static constexpr int B_R0 = B_RH + 8 * (RH - 1);
+	static constexpr int B_DO = B_R0 + 4;
+	static constexpr int B_DH = B_DO + 2;                 // layers DH-1 .. 1
+	static constexpr int B_D0 = B_DH + 8 * (DH - 1);
+	static constexpr int ET = (ES + 1) / 2;               // 32-row tiles of the encoding gradient
+	static constexpr int N_ALL = B_D0 + 4 * ET;
+	// per-wave LDS images (halves); strides padded by 4 halves (8 B) against bank conflicts
+	static constexpr int S_XE = 16 * ES + 4;
+	static constexpr int S_64 = 64 + 4;
+	static constexpr int S_RIN = 32 + 4;
+	static constexpr int I_XE = 0;
+	static constexpr int I_HD = I_XE + 32 * S_XE;         // DH images
+	static constexpr int I_RIN = I_HD + DH * 32 * S_64;
+	static constexpr int I_HR = I_RIN + 32 * S_RIN;       // RH images
+	static constexpr int I_DZ = I_HR + RH * 32 * S_64;
+	static constexpr int IMG_HALVES = I_DZ + 32 * S_64;
+	// dW accumulator tiles (16x16)
+	static constexpr int W_RO = 0;                        // 1 x 4
+	static constexpr int W_RH = W_RO + 4;                 // (RH-1) x 16
+	static constexpr int W_R0 = W_RH + 16 * (RH - 1);     // 4 x 2
+	static constexpr int W_DO = W_R0 + 8;                 // 1 x 4
+	static constexpr int W_DH = W_DO + 4;                 // (DH-1) x 16
+	static constexpr int W_D0 = W_DH + 16 * (DH - 1);     // 4 x ES
+	static constexpr int N_DW = W_D0 + 4 * ES;
+};
+
+template <int ES, int DH, int RH, int MODE>
+__global__ void __launch_bounds__(256, 1) k_nerf_mlp(const NerfMlpArgs a) {
+	using Lay = NerfLayout<ES, DH, RH>;
+	constexpr bool TRAIN = MODE == MLP_TRAIN;
+	constexpr bool DENSITY = MODE == MLP_DENSITY;
+	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (DENSITY ? Lay::F_R0 : Lay::N_FWD);
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	f16x8* lfrag = (f16x8*)smem;
+	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+
+	for (int i = threadIdx.x; i < NFRAG * 64; i += blockDim.x) lfrag[i] = a.frags[i];
+	__syncthreads();
+
+	f16* img = (f16*)(smem + NFRAG * 1024) + wave * Lay::IMG_HALVES;
+	f32x4 dw[TRAIN ? Lay::N_DW : 1];
+	if constexpr (TRAIN) {
+#pragma unroll
+		for (int q = 0; q < Lay::N_DW; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+	}
+
+	const uint32_t n_tiles = (a.n + 31) / 32;
+	for (uint32_t tile = blockIdx.x * 4 + wave; tile < n_tiles; tile += gridDim.x * 4) {
+		const uint32_t sample = tile * 32 + (lane & 31);
+		const bool valid = sample < a.n;
+		const uint32_t ls = valid ? sample : 0;
+
+		// ---- density forward -------------------------------------------------------------------
+		f16x8 xe[ES];
+#pragma unroll
+		for (int s = 0; s < ES; ++s) {
+			xe[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
+			if (!valid) xe[s] = f16x8{};
+			if constexpr (TRAIN) img_store_std(img + Lay::I_XE, Lay::S_XE, xe[s], s, lane);
+		}
+		f32x16 acc[2];
+		f16x8 hd[DH][4];
+		layer_fwd<2, ES>(acc, xe, lfrag + Lay::F_D0 * 64, lane);
+		pack_tiles<2>(acc, hd[0], true);
+#pragma unroll
+		for (int l = 1; l < DH; ++l) {
+			layer_fwd<2, 4>(acc, hd[l - 1], lfrag + (Lay::F_DH + 8 * (l - 1)) * 64, lane);
+			pack_tiles<2>(acc, hd[l], true);
+		}
+		f32x16 dacc[1];
+		layer_fwd<1, 4>(dacc, hd[DH - 1], lfrag + Lay::F_DO * 64, lane);
+		f16x8 dout[2];
+		pack_tile(dacc[0], dout[0], dout[1], false);  // dout[0] = rows 0..15 (density network output)
+		if constexpr (DENSITY) {
+			if (valid) store_out16(a.out, a.out_stride, a.out_layout, a.n, sample, h, dout[0]);
+			continue;
+		}
+
+		// ---- rgb forward -----------------------------------------------------------------------
+		const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
+		f16x8 rin[2] = {dout[0], sh4_frag(cd[0], cd[1], cd[2], h)};
+		if (!valid) rin[1] = f16x8{};
+		f16x8 hr[RH][4];
+		layer_fwd<2, 2>(acc, rin, lfrag + Lay::F_R0 * 64, lane);
+		pack_tiles<2>(acc, hr[0], true);
+#pragma unroll
+		for (int l = 1; l < RH; ++l) {
+			layer_fwd<2, 4>(acc, hr[l - 1], lfrag + (Lay::F_RH + 8 * (l - 1)) * 64, lane);
+			pack_tiles<2>(acc, hr[l], true);
+		}
+		f32x16 racc[1];
+		layer_fwd<1, 4>(racc, hr[RH - 1], lfrag + Lay::F_RO * 64, lane);
+		if (a.out && valid) {
+			f16x8 ro, ro_hi;
+			pack_tile(racc[0], ro, ro_hi, false);
+			if (h == 0) ro[3] = dout[0][0];  // extract_density: row 3 <- density row 0 (nerf_network.h:32-43)
+			store_out16(a.out, a.out_stride, a.out_layout, a.n, sample, h, ro);
+		}
+		if constexpr (!TRAIN) continue;
+		else {
+			// ---- images of the forward activations (dW operands) ------------------------------
+#pragma unroll
+			for (int l = 0; l < DH; ++l) img_store_acc<4>(img + Lay::I_HD + l * 32 * Lay::S_64, Lay::S_64, hd[l], lane);
+			{
+				f16x8 d1[1] = {dout[0]};
+				img_store_acc<1>(img + Lay::I_RIN, Lay::S_RIN, d1, lane);
+				img_store_std(img + Lay::I_RIN, Lay::S_RIN, rin[1], 1, lane);
+			}
+#pragma unroll
+			for (int l = 0; l < RH; ++l) img_store_acc<4>(img + Lay::I_HR + l * 32 * Lay::S_64, Lay::S_64, hr[l], lane);
+
+			// ---- rgb backward ---------------------------------------------------------------
+			f16* dz_img = img + Lay::I_DZ;
+			float dsig = 0.f;
+			f16x8 dz1[1];
+			{
+				f16x4 d = valid ? *(const f16x4*)(a.dL_dout + (size_t)sample * a.dL_stride) : f16x4{};
+				dsig = (float)d[3];
+				// extract_rgb (nerf_network.h:46-60): rows 0..2 of dL/drgb, the rest zero
+				dz1[0] = h == 0 ? f16x8{d[0], d[1], d[2], (f16)0.f, 0, 0, 0, 0} : f16x8{};
+			}
+			img_store_acc<1>(dz_img, Lay::S_64, dz1, lane);
+			dw_accum<1, 4>(dw + Lay::W_RO, dz_img, Lay::S_64, img + Lay::I_HR + (RH - 1) * 32 * Lay::S_64, Lay::S_64, lane);
+			f16x8 dz[4];
+			layer_fwd<2, 1>(acc, dz1, lfrag + Lay::B_RO * 64, lane);
+			mask_pack<2>(acc, hr[RH - 1], dz);
+#pragma unroll
+			for (int l = RH - 1; l >= 1; --l) {
+				img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
+				dw_accum<4, 4>(dw + Lay::W_RH + 16 * (RH - 1 - l), dz_img, Lay::S_64, img + Lay::I_HR + (l - 1) * 32 * Lay::S_64,
+				               Lay::S_64, lane);
+				layer_fwd<2, 4>(acc, dz, lfrag + (Lay::B_RH + 8 * (RH - 1 - l)) * 64, lane);
+				mask_pack<2>(acc, hr[l - 1], dz);
+			}
+			img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
+			dw_accum<4, 2>(dw + Lay::W_R0, dz_img, Lay::S_64, img + Lay::I_RIN, Lay::S_RIN, lane);
+			f32x16 a1[1];
+			layer_fwd<1, 4>(a1, dz, lfrag + Lay::B_R0 * 64, lane);
+			// dL/d(density output) = rows 0..15; add_density_gradient (nerf_network.h:63-74) in fp16
+			f16x8 dd[1], unused;
+			pack_tile(a1[0], dd[0], unused, false);
+			if (h == 0) dd[0][0] = (f16)((float)dd[0][0] + dsig);
+
+			// ---- density backward ------------------------------------------------------------
+			img_store_acc<1>(dz_img, Lay::S_64, dd, lane);
+			dw_accum<1, 4>(dw + Lay::W_DO, dz_img, Lay::S_64, img + Lay::I_HD + (DH - 1) * 32 * Lay::S_64, Lay::S_64, lane);
+			layer_fwd<2, 1>(acc, dd, lfrag + Lay::B_DO * 64, lane);
+			mask_pack<2>(acc, hd[DH - 1], dz);
+#pragma unroll
+			for (int l = DH - 1; l >= 1; --l) {
+				img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
+				dw_accum<4, 4>(dw + Lay::W_DH + 16 * (DH - 1 - l), dz_img, Lay::S_64, img + Lay::I_HD + (l - 1) * 32 * Lay::S_64,
+				               Lay::S_64, lane);
+				layer_fwd<2, 4>(acc, dz, lfrag + (Lay::B_DH + 8 * (DH - 1 - l)) * 64, lane);
+				mask_pack<2>(acc, hd[l - 1], dz);
+			}
+			img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
+			dw_accum<4, ES>(dw + Lay::W_D0, dz_img, Lay::S_64, img + Lay::I_XE, Lay::S_XE, lane);
+			if (a.dL_denc && valid) {
+				f32x16 ae[Lay::ET];
+				layer_fwd<Lay::ET, 4>(ae, dz, lfrag + Lay::B_D0 * 64, lane);
+#pragma unroll
+				for (int t = 0; t < Lay::ET; ++t) {
+					f16x8 lo, hi;
+					pack_tile(ae[t], lo, hi, false);
+					// rows 32t + 8k + 4h + (0..3): lo holds k = 0,1; hi holds k = 2,3
+					f16* row = a.dL_denc + (size_t)sample * a.denc_stride + 32 * t + 4 * h;
+					*(f16x4*)(row + 0) = f16x4{lo[0], lo[1], lo[2], lo[3]};
+					*(f16x4*)(row + 8) = f16x4{lo[4], lo[5], lo[6], lo[7]};
+					if (32 * t + 16 < 16 * ES) {
+						*(f16x4*)(row + 16) = f16x4{hi[0], hi[1], hi[2], hi[3]};
+						*(f16x4*)(row + 24) = f16x4{hi[4], hi[5], hi[6], hi[7]};
+					}
+				}
+			}
+		}
+	}
+
+	if constexpr (TRAIN) {
+		// block reduction of dW into LDS (parameter-slice layout), then one slab per block
+		__syncthreads();
+		float* red = (float*)smem;
+		for (uint32_t i = threadIdx.x; i < a.n_matrix; i += blockDim.x) red[i] = 0.f;
+		__syncthreads();
+		const uint32_t dw0 = a.density_woff, rw0 = a.rgb_woff;
+		const uint32_t d_out_off = dw0 + 64 * 16 * ES + 64 * 64 * (DH - 1);
+		const uint32_t r_out_off = rw0 + 64 * 32 + 64 * 64 * (RH - 1);
+		dw_flush<1, 4>(dw + Lay::W_RO, red, r_out_off, 64, lane);
+#pragma unroll
+		for (int l = RH - 1; l >= 1; --l) dw_flush<4, 4>(dw + Lay::W_RH + 16 * (RH - 1 - l), red, rw0 + 64 * 32 + 64 * 64 * (l - 1), 64, lane);
+		dw_flush<4, 2>(dw + Lay::W_R0, red, rw0, 32, lane);
+		dw_flush<1, 4>(dw + Lay::W_DO, red, d_out_off, 64, lane);
+#pragma unroll
+		for (int l = DH - 1; l >= 1; --l) dw_flush<4, 4>(dw + Lay::W_DH + 16 * (DH - 1 - l), red, dw0 + 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane);
+		dw_flush<4, ES>(dw + Lay::W_D0, red, dw0, 16 * ES, lane);
+		__syncthreads();
+		float* slab = a.dw_slab + (size_t)blockIdx.x * a.n_matrix;
+		for (uint32_t i = threadIdx.x; i < a.n_matrix; i += blockDim.x) slab[i] = red[i];
+	}
+}
+
+template <int ES, int DH, int RH, int MODE>
+static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
+	using Lay = NerfLayout<ES, DH, RH>;
+	constexpr bool TRAIN = MODE == MLP_TRAIN;
+	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (MODE == MLP_DENSITY ? Lay::F_R0 : Lay::N_FWD);
+	size_t lds = (size_t)NFRAG * 1024 + (TRAIN ? 4 * Lay::IMG_HALVES * sizeof(f16) : 0);
+	if (TRAIN) lds = std::max(lds, (size_t)a.n_matrix * sizeof(float));
+	NGP_CHECK(lds <= 160 * 1024, "NerfNetwork MLP: LDS budget exceeded");
+	const uint32_t tiles = (a.n + 31) / 32;
+	uint32_t blocks = TRAIN ? nerf_mlp_train_blocks(a.n) : std::min<uint32_t>(div_round_up(tiles, 4), 8 * device_cu_count());
+	if (blocks == 0) return;
+	auto kern = k_nerf_mlp<ES, DH, RH, MODE>;
+	static bool attr_set = false;
+	if (!attr_set) {
+		NGP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		attr_set = true;
+	}
+	kern<<<blocks, 256, lds, s>>>(a);
+	NGP_HIP(hipGetLastError());
+}
+
+uint32_t nerf_mlp_train_blocks(uint32_t n) {
+	const uint32_t tiles = (n + 31) / 32;
+	return std::max<uint32_t>(1, std::min<uint32_t>(div_round_up(tiles, 4), device_cu_count()));
+}
+
+template <int MODE>
+static void dispatch_nerf(const NerfMlpPlan& p, const NerfMlpArgs& a, hipStream_t s) {
+	const uint32_t key = p.enc_steps * 100 + p.d_hidden * 10 + p.r_hidden;
+	switch (key) {
+		case 112: launch_nerf<1, 1, 2, MODE>(a, s); break;
+		case 212: launch_nerf<2, 1, 2, MODE>(a, s); break;
+		case 111: launch_nerf<1, 1, 1, MODE>(a, s); break;
+		case 122: launch_nerf<1, 2, 2, MODE>(a, s); break;
+		case 113: launch_nerf<1, 1, 3, MODE>(a, s); break;
+		case 213: launch_nerf<2, 1, 3, MODE>(a, s); break;
+		case 222: launch_nerf<2, 2, 2, MODE>(a, s); break;
+		default: throw Error("NerfNetwork: unsupported (encoding width, density/rgb hidden layers) combination");
+	}
+}
+
+void nerf_mlp_run(const NerfMlpPlan& p, MlpMode mode, const NerfMlpArgs& a, hipStream_t s) {
+	if (a.n == 0) return;
+	switch (mode) {
+		case MLP_INFER: dispatch_nerf<MLP_INFER>(p, a, s); break;
+		case MLP_TRAIN: dispatch_nerf<MLP_TRAIN>(p, a, s); break;
+		case MLP_DENSITY: dispatch_nerf<MLP_DENSITY>(p, a, s); break;
+	}
+}
+
+// ------------------------------------------------------------------------------------------------
+// Single MLP (NetworkWithInputEncoding): enc -> 64 x NH -> 16
+// ------------------------------------------------------------------------------------------------
+template <int ES, int NH>
+struct MlpLayout {
+	static constexpr int F_0 = 0;
+	static constexpr int F_H = F_0 + 2 * ES;
+	static constexpr int F_O = F_H + 8 * (NH - 1);
+	static constexpr int N_FWD = F_O + 4;
+	static constexpr int B_O = N_FWD;
+	static constexpr int B_H = B_O + 2;
+	static constexpr int B_0 = B_H + 8 * (NH - 1);
+	static constexpr int ET = (ES + 1) / 2;
+	static constexpr int N_ALL = B_0 + 4 * ET;
+	static constexpr int S_XE = 16 * ES + 4;
+	static constexpr int S_64 = 64 + 4;
+	static constexpr int I_XE = 0;
+	static constexpr int I_H = I_XE + 32 * S_XE;
+	static constexpr int I_DZ = I_H + NH * 32 * S_64;
+	static constexpr int IMG_HALVES = I_DZ + 32 * S_64;
+	static constexpr int W_O = 0;
+	static constexpr int W_H = 4;
+	static constexpr int W_0 = W_H + 16 * (NH - 1);
+	static constexpr int N_DW = W_0 + 4 * ES;
+};
+
+template <int ES, int NH, int MODE>
+__global__ void __launch_bounds__(256, 1) k_mlp(const MlpArgs a) {
+	using Lay = MlpLayout<ES, NH>;
+	constexpr bool TRAIN = MODE == MLP_TRAIN;
+	constexpr int NFRAG = TRAIN ? Lay::N_ALL : Lay::N_FWD;
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	f16x8* lfrag = (f16x8*)smem;
+	const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+	for (int i = threadIdx.x; i < NFRAG * 64; i += blockDim.x) lfrag[i] = a.frags[i];
+	__syncthreads();
+	f16* img = (f16*)(smem + NFRAG * 1024) + wave * Lay::IMG_HALVES;
+	f32x4 dw[TRAIN ? Lay::N_DW : 1];
+	if constexpr (TRAIN) {
+#pragma unroll
+		for (int q = 0; q < Lay::N_DW; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+	}
+	const uint32_t n_tiles = (a.n + 31) / 32;
+	for (uint32_t tile = blockIdx.x * 4 + wave; tile < n_tiles; tile += gridDim.x * 4) {
+		const uint32_t sample = tile * 32 + (lane & 31);
+		const bool valid = sample < a.n;
+		const uint32_t ls = valid ? sample : 0;
+		f16x8 xe[ES];
+#pragma unroll
+		for (int s = 0; s < ES; ++s) {
+			xe[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
+			if (!valid) xe[s] = f16x8{};
+			if constexpr (TRAIN) img_store_std(img + Lay::I_XE, Lay::S_XE, xe[s], s, lane);
+		}
+		f32x16 acc[2];
+		f16x8 hh[NH][4];
+		layer_fwd<2, ES>(acc, xe, lfrag + Lay::F_0 * 64, lane);
+		pack_tiles<2>(acc, hh[0], true);
+#pragma unroll
+		for (int l = 1; l < NH; ++l) {
+			layer_fwd<2, 4>(acc, hh[l - 1], lfrag + (Lay::F_H + 8 * (l - 1)) * 64, lane);
+			pack_tiles<2>(acc, hh[l], true);
+		}
+		f32x16 oacc[1];
+		layer_fwd<1, 4>(oacc, hh[NH - 1], lfrag + Lay::F_O * 64, lane);
+		if (a.out && valid) {
+			f16x8 lo, hi;
+			pack_tile(oacc[0], lo, hi, false);
+			store_out16(a.out, a.out_stride, a.out_layout, a.n, sample, h, lo);
+		}
+		if constexpr (TRAIN) {
+#pragma unroll
+			for (int l = 0; l < NH; ++l) img_store_acc<4>(img + Lay::I_H + l * 32 * Lay::S_64, Lay::S_64, hh[l], lane);
+			f16* dz_img = img + Lay::I_DZ;
+			f16x8 dzo[1];
+			{
+				// all 16 padded output rows carry gradient (tcnn loss writes the padded rows as zero)
+				f16x8 d = f16x8{};
+				if (valid) {
+					const f16* r = a.dL_dout + (size_t)sample * a.dL_stride;
+					const f16x4 p0 = *(const f16x4*)(r + 4 * h), p1 = *(const f16x4*)(r + 8 + 4 * h);
+					d = f16x8{p0[0], p0[1], p0[2], p0[3], p1[0], p1[1], p1[2], p1[3]};
+				}
+				dzo[0] = d;
+			}
+			img_store_acc<1>(dz_img, Lay::S_64, dzo, lane);
+			dw_accum<1, 4>(dw + Lay::W_O, dz_img, Lay::S_64, img + Lay::I_H + (NH - 1) * 32 * Lay::S_64, Lay::S_64, lane);
+			f16x8 dz[4];
+			layer_fwd<2, 1>(acc, dzo, lfrag + Lay::B_O * 64, lane);
+			mask_pack<2>(acc, hh[NH - 1], dz);
+#pragma unroll
+			for (int l = NH - 1; l >= 1; --l) {
+				img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
+				dw_accum<4, 4>(dw + Lay::W_H + 16 * (NH - 1 - l), dz_img, Lay::S_64, img + Lay::I_H + (l - 1) * 32 * Lay::S_64, Lay::S_64, lane);
+				layer_fwd<2, 4>(acc, dz, lfrag + (Lay::B_H + 8 * (NH - 1 - l)) * 64, lane);
+				mask_pack<2>(acc, hh[l - 1], dz);
+			}
+			img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
+			dw_accum<4, ES>(dw + Lay::W_0, dz_img, Lay::S_64, img + Lay::I_XE, Lay::S_XE, lane);
+			if (a.dL_denc && valid) {
+				f32x16 ae[Lay::ET];
+				layer_fwd<Lay::ET, 4>(ae, dz, lfrag + Lay::B_0 * 64, lane);
+#pragma unroll
+				for (int t = 0; t < Lay::ET; ++t) {
+					f16x8 lo, hi;
+					pack_tile(ae[t], lo, hi, false);
+					f16* row = a.dL_denc + (size_t)sample * a.denc_stride + 32 * t + 4 * h;
+					*(f16x4*)(row + 0) = f16x4{lo[0], lo[1], lo[2], lo[3]};
+					*(f16x4*)(row + 8) = f16x4{lo[4], lo[5], lo[6], lo[7]};
+					if (32 * t + 16 < 16 * ES) {
+						*(f16x4*)(row + 16) = f16x4{hi[0], hi[1], hi[2], hi[3]};
+						*(f16x4*)(row + 24) = f16x4{hi[4], hi[5], hi[6], hi[7]};
+					}
+				}
+			}
+		}
+	}
+	if constexpr (TRAIN) {
+		__syncthreads();
+		float* red = (float*)smem;
+		for (uint32_t i = threadIdx.x; i < a.n_matrix; i += blockDim.x) red[i] = 0.f;
+		__syncthreads();
+		const uint32_t o_off = 64 * 16 * ES + 64 * 64 * (NH - 1);
+		dw_flush<1, 4>(dw + Lay::W_O, red, o_off, 64, lane);
+#pragma unroll
+		for (int l = NH - 1; l >= 1; --l) dw_flush<4, 4>(dw + Lay::W_H + 16 * (NH - 1 - l), red, 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane);
+		dw_flush<4, ES>(dw + Lay::W_0, red, 0, 16 * ES, lane);
+		__syncthreads();
+		float* slab = a.dw_slab + (size_t)blockIdx.x * a.n_matrix;
+		for (uint32_t i = threadIdx.x; i < a.n_matrix; i += blockDim.x) slab[i] = red[i];
+	}
+}
+
+uint32_t mlp_train_blocks(uint32_t n) { return nerf_mlp_train_blocks(n); }
+
+template <int ES, int NH, int MODE>
+static void launch_mlp(const MlpArgs& a, hipStream_t s) {
+	using Lay = MlpLayout<ES, NH>;
+	constexpr bool TRAIN = MODE == MLP_TRAIN;
+	constexpr int NFRAG = TRAIN ? Lay::N_ALL : Lay::N_FWD;
+	size_t lds = (size_t)NFRAG * 1024 + (TRAIN ? 4 * Lay::IMG_HALVES * sizeof(f16) : 0);
+	if (TRAIN) lds = std::max(lds, (size_t)a.n_matrix * sizeof(float));
+	NGP_CHECK(lds <= 160 * 1024, "MLP: LDS budget exceeded");
+	const uint32_t tiles = (a.n + 31) / 32;
+	uint32_t blocks = TRAIN ? mlp_train_blocks(a.n) : std::min<uint32_t>(div_round_up(tiles, 4), 8 * device_cu_count());
+	auto kern = k_mlp<ES, NH, MODE>;
+	static bool attr_set = false;
+	if (!attr_set) {
+		NGP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		attr_set = true;
+	}
+	kern<<<blocks, 256, lds, s>>>(a);
+	NGP_HIP(hipGetLastError());
+}
+
+template <int MODE>
+static void dispatch_mlp(const MlpPlan& p, const MlpArgs& a, hipStream_t s) {
+	switch (p.enc_steps * 10 + p.hidden) {
+		case 11: launch_mlp<1, 1, MODE>(a, s); break;
+		case 12: launch_mlp<1, 2, MODE>(a, s); break;
+		case 13: launch_mlp<1, 3, MODE>(a, s); break;
+		case 21: launch_mlp<2, 1, MODE>(a, s); break;
+		case 22: launch_mlp<2, 2, MODE>(a, s); break;
+		case 23: launch_mlp<2, 3, MODE>(a, s); break;
+		case 24: launch_mlp<2, 4, MODE>(a, s); break;
+		default: throw Error("FullyFusedMLP: unsupported (encoding width, hidden layers) combination");
+	}
+}
+
+void mlp_run(const MlpPlan& p, MlpMode mode, const MlpArgs& a, hipStream_t s) {
+	if (a.n == 0) return;
+	if (mode == MLP_TRAIN) dispatch_mlp<MLP_TRAIN>(p, a, s);
+	else dispatch_mlp<MLP_INFER>(p, a, s);
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ void k_reduce_slabs(const float* __restrict__ slabs, uint32_t n_slabs, uint32_t n, f16* __restrict__ grad, bool accumulate) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	float s = accumulate ? (float)grad[i] : 0.f;
+	for (uint32_t b = 0; b < n_slabs; ++b) s += slabs[(size_t)b * n + i];
+	grad[i] = (f16)s;
+}
+
+void reduce_slabs(const float* slabs, uint32_t n_slabs, uint32_t n, f16* grad, bool accumulate, hipStream_t s) {
+	k_reduce_slabs<<<div_round_up(n, 256), 256, 0, s>>>(slabs, n_slabs, n, grad, accumulate);
+	NGP_HIP(hipGetLastError());
+}
+
+}  // namespace ngp

@@ -1,0 +1,241 @@
+"""Host-side mirror of the reference's model/trainer interface over the C-ABI.
+
+Names and argument meaning follow the objects the reference's Testbed drives
+(tcnn::NetworkWithInputEncoding, ngp::NerfNetwork — include/neural-graphics-primitives/nerf_network.h,
+tcnn::Trainer — src/testbed.cu:4129). Device buffers are torch tensors (PyTorch is plumbing for
+device memory, streams and torch.distributed here); every compute call goes to the HIP engine.
+"""
+import ctypes as C
+import json
+
+import torch
+
+from ._capi import ParamLayout, check, lib
+
+LAYOUT_AOS, LAYOUT_SOA = 0, 1
+GRAD_OVERWRITE, GRAD_ACCUMULATE = 0, 1
+
+
+def _js(cfg):
+    if cfg is None:
+        return None
+    return (cfg if isinstance(cfg, str) else json.dumps(cfg)).encode()
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _check_input(x, width):
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1):
+        raise ValueError("input must be a CUDA float32 [n, stride] row-major tensor")
+    if x.shape[1] < width:
+        raise ValueError(f"input has {x.shape[1]} columns, the model reads {width}")
+
+
+class _CudaArray:
+    """Exposes an engine-owned device buffer to torch via __cuda_array_interface__."""
+
+    def __init__(self, ptr, n, typestr):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False), "version": 3, "strides": None}
+
+
+def wrap_device(ptr, n, dtype):
+    typestr = {torch.float16: "<f2", torch.float32: "<f4"}[dtype]
+    return torch.as_tensor(_CudaArray(ptr, n, typestr), device="cuda")
+
+
+class Context:
+    def __init__(self, model, handle, n):
+        self.model, self.handle, self.n = model, handle, n
+
+    def __del__(self):
+        if self.handle:
+            lib().ngp_ctx_destroy(self.handle)
+            self.handle = None
+
+
+class Model:
+    """Common surface of tcnn::Network<float, __half> as the Testbed uses it."""
+
+    def __init__(self, handle):
+        self.handle = handle
+        self._keep = []
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            lib().ngp_model_destroy(self.handle)
+            self.handle = None
+
+    # -- shape queries ------------------------------------------------------------------------
+    @property
+    def n_params(self):
+        return lib().ngp_model_n_params(self.handle)
+
+    @property
+    def n_matrix_params(self):
+        return lib().ngp_model_n_matrix_params(self.handle)
+
+    def input_width(self):
+        return lib().ngp_model_input_width(self.handle)
+
+    def padded_output_width(self):
+        return lib().ngp_model_padded_output_width(self.handle)
+
+    def output_width(self):
+        return lib().ngp_model_output_width(self.handle)
+
+    def layout(self):
+        lo = ParamLayout()
+        check(lib().ngp_model_param_layout(self.handle, C.byref(lo)))
+        return lo
+
+    # -- parameters ---------------------------------------------------------------------------
+    def set_params(self, params, inference_params=None, gradients=None):
+        for t in (params, inference_params, gradients):
+            if t is not None and (t.dtype != torch.float16 or t.numel() != self.n_params or not t.is_cuda):
+                raise ValueError("parameter buffers must be CUDA fp16 tensors of n_params elements")
+        self._keep = [params, inference_params, gradients]
+        check(lib().ngp_model_set_params(self.handle, _ptr(params), _ptr(inference_params), _ptr(gradients)))
+
+    def initialize_params(self, seed=1337, scale=1.0):
+        import numpy as np
+        out = np.zeros(self.n_params, dtype=np.float32)
+        check(lib().ngp_model_initialize_params(self.handle, seed, out.ctypes.data_as(C.c_void_p), scale))
+        return out
+
+    def set_max_level(self, max_level=1.0, per_sample=None):
+        self._max_level_keep = per_sample
+        check(lib().ngp_model_set_max_level(self.handle, float(max_level), _ptr(per_sample)))
+
+    def reserve(self, n):
+        check(lib().ngp_model_reserve(self.handle, n))
+
+    # -- compute ------------------------------------------------------------------------------
+    def inference(self, x, output=None, layout=LAYOUT_AOS, use_inference_params=True, stream=None):
+        _check_input(x, self.input_width())
+        n = x.shape[0]
+        if output is None:
+            output = torch.empty((n, 16) if layout == LAYOUT_AOS else (16, n), dtype=torch.float16, device=x.device)
+        stride = output.stride(0)
+        check(lib().ngp_inference(self.handle, _stream(stream), n, _ptr(x), x.stride(0), _ptr(output), stride, layout,
+                                  int(use_inference_params)))
+        return output
+
+    def forward(self, x, output=None, use_inference_params=False, stream=None):
+        _check_input(x, self.input_width())
+        h = C.c_void_p()
+        check(lib().ngp_forward(self.handle, _stream(stream), x.shape[0], _ptr(x), x.stride(0), _ptr(output),
+                                output.stride(0) if output is not None else 0, int(use_inference_params), C.byref(h)))
+        return Context(self, h, x.shape[0]), output
+
+    def backward(self, ctx, dL_doutput, grad_mode=GRAD_OVERWRITE, stream=None):
+        assert dL_doutput.dtype == torch.float16 and dL_doutput.shape[1] >= 16
+        check(lib().ngp_backward(self.handle, _stream(stream), ctx.handle, _ptr(dL_doutput), dL_doutput.stride(0), grad_mode))
+
+    def forward_backward(self, x, dL_doutput, output=None, grad_mode=GRAD_OVERWRITE, stream=None):
+        _check_input(x, self.input_width())
+        assert dL_doutput.dtype == torch.float16 and dL_doutput.shape[1] >= 16
+        check(lib().ngp_forward_backward(self.handle, _stream(stream), x.shape[0], _ptr(x), x.stride(0), _ptr(output),
+                                         output.stride(0) if output is not None else 0, _ptr(dL_doutput),
+                                         dL_doutput.stride(0), grad_mode))
+        return output
+
+    def encode(self, x, layout=LAYOUT_AOS, use_inference_params=False, stream=None):
+        n = x.shape[0]
+        w = self.layout().encoding_width
+        out = torch.zeros((n, w) if layout == LAYOUT_AOS else (w, n), dtype=torch.float16, device=x.device)
+        check(lib().ngp_encoding_forward(self.handle, _stream(stream), n, _ptr(x), x.stride(0), _ptr(out), out.stride(0),
+                                         layout, int(use_inference_params)))
+        return out
+
+    def encoding_backward(self, x, dL_dy, layout=LAYOUT_AOS, grad_mode=GRAD_OVERWRITE, stream=None):
+        check(lib().ngp_encoding_backward(self.handle, _stream(stream), x.shape[0], _ptr(x), x.stride(0), _ptr(dL_dy),
+                                          dL_dy.stride(0), layout, grad_mode))
+
+
+class NerfNetwork(Model):
+    """ngp::NerfNetwork<__half>(n_pos_dims, n_dir_dims, n_extra_dims, dir_offset, pos_encoding,
+    dir_encoding, density_network, rgb_network) — nerf_network.h:81-112."""
+
+    def __init__(self, n_pos_dims, n_dir_dims, n_extra_dims, dir_offset, pos_encoding, dir_encoding, density_network,
+                 rgb_network):
+        h = C.c_void_p()
+        check(lib().ngp_nerf_network_create(n_pos_dims, n_dir_dims, n_extra_dims, dir_offset, _js(pos_encoding),
+                                            _js(dir_encoding), _js(density_network), _js(rgb_network), C.byref(h)))
+        super().__init__(h)
+
+    def density(self, x, output=None, layout=LAYOUT_AOS, use_inference_params=True, stream=None):
+        n = x.shape[0]
+        if output is None:
+            output = torch.empty((n, 16) if layout == LAYOUT_AOS else (16, n), dtype=torch.float16, device=x.device)
+        check(lib().ngp_density(self.handle, _stream(stream), n, _ptr(x), x.stride(0), _ptr(output), output.stride(0), layout,
+                                int(use_inference_params)))
+        return output
+
+
+class NetworkWithInputEncoding(Model):
+    """tcnn::NetworkWithInputEncoding(n_input_dims, n_output_dims, encoding, network) — src/testbed.cu:4110."""
+
+    def __init__(self, n_input_dims, n_output_dims, encoding, network):
+        h = C.c_void_p()
+        check(lib().ngp_network_with_input_encoding_create(n_input_dims, n_output_dims, _js(encoding), _js(network),
+                                                           C.byref(h)))
+        super().__init__(h)
+
+
+class Trainer:
+    """tcnn::Trainer<float, __half, __half>(network, optimizer, loss, seed) — src/testbed.cu:4129.
+    The loss is applied by the caller (NeRF computes dL/doutput itself, testbed_nerf.cu:1660-2012)."""
+
+    def __init__(self, model, optimizer, seed=1337):
+        self.model = model
+        h = C.c_void_p()
+        check(lib().ngp_trainer_create(model.handle, _js(optimizer), seed, C.byref(h)))
+        self.handle = h
+        n = model.n_params
+        L = lib()
+        self.gradients = wrap_device(L.ngp_trainer_gradients(h), n, torch.float16)
+        self.params = wrap_device(L.ngp_trainer_params(h), n, torch.float16)
+        self.inference_params = wrap_device(L.ngp_trainer_inference_params(h), n, torch.float16)
+        self.params_full_precision = wrap_device(L.ngp_trainer_params_full_precision(h), n, torch.float32)
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            lib().ngp_trainer_destroy(self.handle)
+            self.handle = None
+
+    def optimizer_step(self, loss_scale=128.0, stream=None):
+        check(lib().ngp_trainer_optimizer_step(self.handle, _stream(stream), float(loss_scale)))
+
+    @property
+    def step(self):
+        return lib().ngp_trainer_step(self.handle)
+
+    @property
+    def learning_rate(self):
+        return lib().ngp_trainer_learning_rate(self.handle)
+
+    @learning_rate.setter
+    def learning_rate(self, lr):
+        check(lib().ngp_trainer_set_learning_rate(self.handle, float(lr)))
+
+    def set_params_full_precision(self, params_host):
+        import numpy as np
+        a = np.ascontiguousarray(params_host, dtype=np.float32)
+        check(lib().ngp_trainer_set_params_full_precision(self.handle, a.ctypes.data_as(C.c_void_p), a.size))
+
+    def serialize(self):
+        size = C.c_uint64(0)
+        check(lib().ngp_trainer_serialize(self.handle, None, C.byref(size)))
+        buf = C.create_string_buffer(size.value)
+        check(lib().ngp_trainer_serialize(self.handle, buf, C.byref(size)))
+        return buf.raw
+
+    def deserialize(self, blob):
+        check(lib().ngp_trainer_deserialize(self.handle, blob, len(blob)))
