@@ -48,6 +48,11 @@ int ngp_malloc(void** ptr, size_t bytes);
 int ngp_free(void* ptr);
 int ngp_memcpy(void* dst, const void* src, size_t bytes, int kind /* hipMemcpyKind */);
 int ngp_stream_synchronize(void* stream);
+/* per-kernel HIP-event timing on each kernel's launch stream (off by default). read() fills a JSON
+ * object {"phase": {"calls": n, "ms": total}} and returns the length needed (incl. NUL). */
+int ngp_profiler_enable(int enable);
+int ngp_profiler_reset(void);
+int ngp_profiler_read(char* json_buf, size_t len);
 
 /* ---- models (tcnn::Network<float, __half> surface) ------------------------------------------ */
 /* NerfNetwork ctor (nerf_network.h:81-112); JSON strings are the config sections the Testbed passes

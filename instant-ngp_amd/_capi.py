@@ -42,6 +42,9 @@ SIGNATURES = {
     "ngp_free": (i32, [P]),
     "ngp_memcpy": (i32, [P, P, sz, i32]),
     "ngp_stream_synchronize": (i32, [P]),
+    "ngp_profiler_enable": (i32, [i32]),
+    "ngp_profiler_reset": (i32, []),
+    "ngp_profiler_read": (i32, [C.c_char_p, sz]),
     "ngp_nerf_network_create": (i32, [u32, u32, u32, u32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(P)]),
     "ngp_network_with_input_encoding_create": (i32, [u32, u32, C.c_char_p, C.c_char_p, C.POINTER(P)]),
     "ngp_model_destroy": (None, [P]),

@@ -16,6 +16,7 @@
 #include "json.h"
 #include "mlp.h"
 #include "optimizer.h"
+#include "profiler.h"
 
 namespace ngp {
 
@@ -154,6 +155,7 @@ struct ngp_model {
 	const f16* pick(bool inference) const { return inference ? inference_params : params; }
 	f16x8* prep(hipStream_t s, bool inference) {
 		f16x8* f = (f16x8*)(inference ? frags_inf : frags).get((size_t)n_all_frags * 1024);
+		ProfScope ps("prepare_frags", s);
 		prepare_frags(d_descs, n_all_frags, pick(inference), f, s);
 		return f;
 	}
@@ -163,6 +165,7 @@ struct ngp_model {
 			NGP_HIP(hipMemsetAsync(out, 0, (size_t)n * out_stride * sizeof(f16), s));
 		}
 		GridFwdArgs a{n, in, stride, pick(inference) + grid_offset(), out, out_stride, layout, max_level, max_level_per_sample};
+		ProfScope ps("grid_forward", s);
 		grid_forward(grid, a, s);
 	}
 	void run_mlp(hipStream_t s, MlpMode mode, uint32_t n, const float* in, uint32_t stride, const f16* encbuf, f16* out,
@@ -175,12 +178,14 @@ struct ngp_model {
 			a.frags = f; a.n_frags = n_all_frags; a.out = out; a.out_stride = out_stride; a.out_layout = out_layout;
 			a.dL_dout = dL; a.dL_stride = dL_stride; a.dL_denc = dL_denc; a.denc_stride = enc_width; a.dw_slab = slab;
 			a.n_matrix = (uint32_t)n_matrix(); a.density_woff = 0; a.rgb_woff = (uint32_t)mlp0_params;
+			ProfScope ps(mode == MLP_TRAIN ? "mlp_train" : mode == MLP_DENSITY ? "mlp_density" : "mlp_infer", s);
 			nerf_mlp_run(nplan, mode, a, s);
 		} else {
 			MlpArgs a{};
 			a.n = n; a.enc = encbuf; a.enc_stride = enc_width; a.frags = f; a.n_frags = n_all_frags;
 			a.out = out; a.out_stride = out_stride; a.out_layout = out_layout; a.dL_dout = dL; a.dL_stride = dL_stride;
 			a.dL_denc = dL_denc; a.denc_stride = enc_width; a.dw_slab = slab; a.n_matrix = (uint32_t)n_matrix();
+			ProfScope ps(mode == MLP_TRAIN ? "mlp_train" : "mlp_infer", s);
 			mlp_run(mplan, mode == MLP_DENSITY ? MLP_INFER : mode, a, s);
 		}
 	}
@@ -192,10 +197,16 @@ struct ngp_model {
 		const uint32_t blocks = nerf ? nerf_mlp_train_blocks(n) : mlp_train_blocks(n);
 		float* slab = (float*)slabs.get((size_t)blocks * n_matrix() * sizeof(float));
 		run_mlp(s, MLP_TRAIN, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride, dL_denc, slab, false);
-		reduce_slabs(slab, blocks, (uint32_t)n_matrix(), gradients, grad_mode == NGP_GRAD_ACCUMULATE, s);
-		if (grad_mode != NGP_GRAD_ACCUMULATE)
+		{
+			ProfScope ps("reduce_slabs", s);
+			reduce_slabs(slab, blocks, (uint32_t)n_matrix(), gradients, grad_mode == NGP_GRAD_ACCUMULATE, s);
+		}
+		if (grad_mode != NGP_GRAD_ACCUMULATE) {
+			ProfScope ps("grid_grad_zero", s);
 			NGP_HIP(hipMemsetAsync(gradients + grid_offset(), 0, grid_params * sizeof(f16), s));
+		}
 		GridBwdArgs b{n, in, stride, dL_denc, enc_width, AoS, gradients + grid_offset(), max_level, max_level_per_sample};
+		ProfScope ps("grid_backward", s);
 		grid_backward(grid, b, s);
 	}
 };
@@ -526,6 +537,7 @@ void ngp_trainer_destroy(ngp_trainer* t) {
 int ngp_trainer_optimizer_step(ngp_trainer* t, void* stream, float loss_scale) {
 	NGP_ARG(t && loss_scale > 0.f);
 	NGP_TRY({
+		ProfScope ps("optimizer", S(stream));
 		adam_ema_step(t->cfg, t->step, (uint32_t)t->n, (uint32_t)t->model->n_matrix(), loss_scale, t->w32, t->w16, t->g16, t->m1,
 		              t->m2, t->steps, t->ema32, t->inf16, S(stream));
 		t->step++;

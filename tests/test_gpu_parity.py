@@ -63,7 +63,9 @@ def test_encoding_forward_bitexact(pkg, orc, D, L, F, T):
     g = orc.make_grid(D, L, F, T)
     ref = orc.f32_to_f16_bits(orc.grid_forward(g, x, p16[net.n_matrix_params:]))
     LF = L * F
-    assert np.array_equal(got[:, :LF], ref), f"{(got[:, :LF] != ref).sum()} mismatching fp16 features"
+    bad = np.argwhere(got[:, :LF] != ref)
+    detail = [(int(i), int(f), hex(got[i, f]), hex(ref[i, f]), x[i].tolist()) for i, f in bad[:5]]
+    assert len(bad) == 0, f"{len(bad)} mismatching fp16 features: {detail}"
     assert np.all(got[:, LF:] == 0)
     # SoA (tcnn RM) layout gives the same values
     soa = net.encode(xt, layout=pkg.LAYOUT_SOA).cpu().numpy().view(np.uint16)
