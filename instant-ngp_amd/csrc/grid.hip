@@ -118,6 +118,10 @@ __global__ void __launch_bounds__(256) k_grid_forward(const GridConst c, const G
 				}
 			}
 		}
+		// keep the fp32 sum opaque so the last FMA is not fused with the f16 conversion (v_fma_mix*):
+		// the contract is round-to-fp32 then RNE to fp16, as the oracle does
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) asm volatile("" : "+v"(acc[f]));
 		if (a.out_layout == AoS) {
 			V o;
 			if constexpr (F == 1) o = (f16)acc[0];

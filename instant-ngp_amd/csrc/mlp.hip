@@ -428,13 +428,15 @@ __global__ void __launch_bounds__(256, 1) k_nerf_mlp(const NerfMlpArgs a) {
 			}
 			img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
 			dw_accum<4, ES>(dw + Lay::W_D0, dz_img, Lay::S_64, img + Lay::I_XE, Lay::S_XE, lane);
-			if (a.dL_denc && valid) {
+			if (a.dL_denc) {
+				// the MFMAs run with the full wave (every lane supplies A rows); only the stores are masked
 				f32x16 ae[Lay::ET];
 				layer_fwd<Lay::ET, 4>(ae, dz, lfrag + Lay::B_D0 * 64, lane);
 #pragma unroll
 				for (int t = 0; t < Lay::ET; ++t) {
 					f16x8 lo, hi;
 					pack_tile(ae[t], lo, hi, false);
+					if (!valid) continue;
 					// rows 32t + 8k + 4h + (0..3): lo holds k = 0,1; hi holds k = 2,3
 					f16* row = a.dL_denc + (size_t)sample * a.denc_stride + 32 * t + 4 * h;
 					*(f16x4*)(row + 0) = f16x4{lo[0], lo[1], lo[2], lo[3]};
@@ -620,13 +622,14 @@ __global__ void __launch_bounds__(256, 1) k_mlp(const MlpArgs a) {
 			}
 			img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
 			dw_accum<4, ES>(dw + Lay::W_0, dz_img, Lay::S_64, img + Lay::I_XE, Lay::S_XE, lane);
-			if (a.dL_denc && valid) {
+			if (a.dL_denc) {
 				f32x16 ae[Lay::ET];
 				layer_fwd<Lay::ET, 4>(ae, dz, lfrag + Lay::B_0 * 64, lane);
 #pragma unroll
 				for (int t = 0; t < Lay::ET; ++t) {
 					f16x8 lo, hi;
 					pack_tile(ae[t], lo, hi, false);
+					if (!valid) continue;
 					f16* row = a.dL_denc + (size_t)sample * a.denc_stride + 32 * t + 4 * h;
 					*(f16x4*)(row + 0) = f16x4{lo[0], lo[1], lo[2], lo[3]};
 					*(f16x4*)(row + 8) = f16x4{lo[4], lo[5], lo[6], lo[7]};

@@ -50,14 +50,22 @@ def wrap_device(ptr, n, dtype):
     return torch.as_tensor(_CudaArray(ptr, n, typestr), device="cuda")
 
 
+def _destroy(obj, fn):
+    h = getattr(obj, "handle", None)
+    if h:
+        try:
+            getattr(lib(), fn)(h)
+        except Exception:  # interpreter teardown: module globals may already be gone
+            pass
+        obj.handle = None
+
+
 class Context:
     def __init__(self, model, handle, n):
         self.model, self.handle, self.n = model, handle, n
 
     def __del__(self):
-        if self.handle:
-            lib().ngp_ctx_destroy(self.handle)
-            self.handle = None
+        _destroy(self, "ngp_ctx_destroy")
 
 
 class Model:
@@ -68,9 +76,7 @@ class Model:
         self._keep = []
 
     def __del__(self):
-        if getattr(self, "handle", None):
-            lib().ngp_model_destroy(self.handle)
-            self.handle = None
+        _destroy(self, "ngp_model_destroy")
 
     # -- shape queries ------------------------------------------------------------------------
     @property
@@ -206,9 +212,7 @@ class Trainer:
         self.params_full_precision = wrap_device(L.ngp_trainer_params_full_precision(h), n, torch.float32)
 
     def __del__(self):
-        if getattr(self, "handle", None):
-            lib().ngp_trainer_destroy(self.handle)
-            self.handle = None
+        _destroy(self, "ngp_trainer_destroy")
 
     def optimizer_step(self, loss_scale=128.0, stream=None):
         check(lib().ngp_trainer_optimizer_step(self.handle, _stream(stream), float(loss_scale)))
