@@ -81,16 +81,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
     from __graft_entry__ import load_package
     pkg = load_package()
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    rank, world, local_rank = pkg.dp.init_from_env()
 
     cfg = pkg.nerf_config(args.variant)
     net = pkg.create_nerf_network(cfg)
@@ -103,9 +98,8 @@ def main():
 
     def step():
         net.forward_backward(x, dL)
-        if world > 1:
-            dist.all_reduce(grads)  # RCCL over xGMI; the 1/N average is folded into the loss scale
-        trainer.optimizer_step(loss_scale * world)
+        div = pkg.dp.allreduce_gradients(grads, world)  # RCCL over xGMI; 1/N folded into the loss scale
+        trainer.optimizer_step(loss_scale * div)
 
     for _ in range(args.warmup):
         step()

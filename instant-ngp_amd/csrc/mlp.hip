@@ -196,9 +196,10 @@ __device__ __forceinline__ void dw_accum(f32x4* dw, const f16* dz_img, int dz_st
 }
 
 // Flush one layer's dW tiles (16x16, 4 regs: out = 16m + 4(lane>>4) + r, in = 16n + (lane&15)) into
-// the block's fp32 LDS reduction buffer laid out as the parameter slice [out x in].
+// the block's fp32 LDS reduction buffer laid out as the parameter slice [out x in]. Waves flush one
+// after another (FIRST: store, else add) so the sum order is fixed: bitwise-reproducible gradients.
 template <int MT, int NT>
-__device__ __forceinline__ void dw_flush(const f32x4* dw, float* red, uint32_t woff, uint32_t in_dim, int lane) {
+__device__ __forceinline__ void dw_flush(const f32x4* dw, float* red, uint32_t woff, uint32_t in_dim, int lane, bool first) {
 #pragma unroll
 	for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -206,7 +207,8 @@ __device__ __forceinline__ void dw_flush(const f32x4* dw, float* red, uint32_t w
 #pragma unroll
 			for (int r = 0; r < 4; ++r) {
 				const uint32_t o = 16 * m + 4 * (lane >> 4) + r, i = 16 * n + (lane & 15);
-				atomicAdd(red + woff + o * in_dim + i, dw[m * NT + n][r]);
+				float* p = red + woff + o * in_dim + i;
+				*p = first ? dw[m * NT + n][r] : *p + dw[m * NT + n][r];
 			}
 }
 
@@ -452,21 +454,26 @@ __global__ void __launch_bounds__(256, 1) k_nerf_mlp(const NerfMlpArgs a) {
 
 	if constexpr (TRAIN) {
 		// block reduction of dW into LDS (parameter-slice layout), then one slab per block
-		__syncthreads();
 		float* red = (float*)smem;
-		for (uint32_t i = threadIdx.x; i < a.n_matrix; i += blockDim.x) red[i] = 0.f;
-		__syncthreads();
 		const uint32_t dw0 = a.density_woff, rw0 = a.rgb_woff;
 		const uint32_t d_out_off = dw0 + 64 * 16 * ES + 64 * 64 * (DH - 1);
 		const uint32_t r_out_off = rw0 + 64 * 32 + 64 * 64 * (RH - 1);
-		dw_flush<1, 4>(dw + Lay::W_RO, red, r_out_off, 64, lane);
+		for (int w = 0; w < 4; ++w) {
+			__syncthreads();
+			if (wave == w) {
+				const bool first = w == 0;
+				dw_flush<1, 4>(dw + Lay::W_RO, red, r_out_off, 64, lane, first);
 #pragma unroll
-		for (int l = RH - 1; l >= 1; --l) dw_flush<4, 4>(dw + Lay::W_RH + 16 * (RH - 1 - l), red, rw0 + 64 * 32 + 64 * 64 * (l - 1), 64, lane);
-		dw_flush<4, 2>(dw + Lay::W_R0, red, rw0, 32, lane);
-		dw_flush<1, 4>(dw + Lay::W_DO, red, d_out_off, 64, lane);
+				for (int l = RH - 1; l >= 1; --l)
+					dw_flush<4, 4>(dw + Lay::W_RH + 16 * (RH - 1 - l), red, rw0 + 64 * 32 + 64 * 64 * (l - 1), 64, lane, first);
+				dw_flush<4, 2>(dw + Lay::W_R0, red, rw0, 32, lane, first);
+				dw_flush<1, 4>(dw + Lay::W_DO, red, d_out_off, 64, lane, first);
 #pragma unroll
-		for (int l = DH - 1; l >= 1; --l) dw_flush<4, 4>(dw + Lay::W_DH + 16 * (DH - 1 - l), red, dw0 + 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane);
-		dw_flush<4, ES>(dw + Lay::W_D0, red, dw0, 16 * ES, lane);
+				for (int l = DH - 1; l >= 1; --l)
+					dw_flush<4, 4>(dw + Lay::W_DH + 16 * (DH - 1 - l), red, dw0 + 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane, first);
+				dw_flush<4, ES>(dw + Lay::W_D0, red, dw0, 16 * ES, lane, first);
+			}
+		}
 		__syncthreads();
 		float* slab = a.dw_slab + (size_t)blockIdx.x * a.n_matrix;
 		for (uint32_t i = threadIdx.x; i < a.n_matrix; i += blockDim.x) slab[i] = red[i];
@@ -642,15 +649,19 @@ __global__ void __launch_bounds__(256, 1) k_mlp(const MlpArgs a) {
 		}
 	}
 	if constexpr (TRAIN) {
-		__syncthreads();
 		float* red = (float*)smem;
-		for (uint32_t i = threadIdx.x; i < a.n_matrix; i += blockDim.x) red[i] = 0.f;
-		__syncthreads();
 		const uint32_t o_off = 64 * 16 * ES + 64 * 64 * (NH - 1);
-		dw_flush<1, 4>(dw + Lay::W_O, red, o_off, 64, lane);
+		for (int w = 0; w < 4; ++w) {
+			__syncthreads();
+			if (wave == w) {
+				const bool first = w == 0;
+				dw_flush<1, 4>(dw + Lay::W_O, red, o_off, 64, lane, first);
 #pragma unroll
-		for (int l = NH - 1; l >= 1; --l) dw_flush<4, 4>(dw + Lay::W_H + 16 * (NH - 1 - l), red, 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane);
-		dw_flush<4, ES>(dw + Lay::W_0, red, 0, 16 * ES, lane);
+				for (int l = NH - 1; l >= 1; --l)
+					dw_flush<4, 4>(dw + Lay::W_H + 16 * (NH - 1 - l), red, 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane, first);
+				dw_flush<4, ES>(dw + Lay::W_0, red, 0, 16 * ES, lane, first);
+			}
+		}
 		__syncthreads();
 		float* slab = a.dw_slab + (size_t)blockIdx.x * a.n_matrix;
 		for (uint32_t i = threadIdx.x; i < a.n_matrix; i += blockDim.x) slab[i] = red[i];

@@ -1,0 +1,51 @@
+"""Data-parallel training over the GPUs of one node: one process per GPU,
+torch.distributed with the "nccl" backend (= RCCL over xGMI on ROCm), one all-reduce of the
+contiguous fp16 gradient buffer per step, the 1/N average folded into the optimizer's loss scale.
+
+The reference trains on one GPU only (multi-GPU is render replication); this module is
+the new exchange step. Sharding keeps the *global* ray index i so every rank draws exactly the rays
+the 1-GPU run would draw (rng.advance(i * N_MAX_RANDOM_SAMPLES_PER_RAY), src/testbed_nerf.cu:1417-1421).
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend=None):
+    """Initialise the process group from RANK/WORLD_SIZE/MASTER_* (torch.distributed.run)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {"device_id": torch.device("cuda", local_rank)} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
+    return rank, world, local_rank
+
+
+def shard_range(n_global, rank, world):
+    """Contiguous shard [lo, hi) of n_global items for `rank`; shards partition [0, n_global)."""
+    lo = n_global * rank // world
+    hi = n_global * (rank + 1) // world
+    return lo, hi
+
+
+def allreduce_gradients(grads, world, group=None):
+    """Sum the gradient buffer over ranks in place (RCCL all-reduce). Returns the loss-scale factor
+    the optimizer must divide by (world) so that the update uses the mean gradient."""
+    if world > 1:
+        dist.all_reduce(grads, op=dist.ReduceOp.SUM, group=group)
+    return float(world)
+
+
+def allreduce_counters(values, world):
+    """All-reduce the per-step scalars (measured sample counts, loss sum) used by the rays-per-batch
+    adaptation (NerfCounters::update_after_training, src/testbed_nerf.cu:3583-3609)."""
+    on_gpu = dist.is_initialized() and dist.get_backend() == "nccl"
+    t = torch.as_tensor(values, dtype=torch.float64, device="cuda" if on_gpu else "cpu")
+    if world > 1:
+        dist.all_reduce(t)
+    return t.cpu().tolist()
