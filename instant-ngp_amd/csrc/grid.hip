@@ -137,13 +137,17 @@ __global__ void __launch_bounds__(256) k_grid_forward(const GridConst c, const G
 	}
 }
 
-// Backward: thread t handles sample t / P and feature pair t % P (P = max(F/2, 1)).
+// Backward: 2P lanes per sample (P = feature pairs per entry), ordered [x0: pair 0..P-1 | x1: pair
+// 0..P-1]. One wave-instruction then updates a corner and its +x neighbour, which are adjacent
+// entries (dense levels) or in one aligned 8-entry group 7/8 of the time (the hash keeps x coherent:
+// prime 1), so both land in one 64-B atomic segment = one memory-side request instead of two.
 template <uint32_t D, uint32_t F>
 __global__ void __launch_bounds__(256) k_grid_backward(const GridConst c, const GridBwdArgs a) {
 	constexpr uint32_t P = F >= 2 ? F / 2 : 1;
 	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-	const uint32_t i = t / P;
-	const uint32_t pair = t % P;
+	const uint32_t i = t / (2 * P);
+	const uint32_t sub = t % (2 * P);
+	const uint32_t xbit = sub / P, pair = sub % P;
 	if (i >= a.n) return;
 	float x[D];
 #pragma unroll
@@ -167,7 +171,8 @@ __global__ void __launch_bounds__(256) k_grid_backward(const GridConst c, const 
 		float frac[D]; uint32_t base[D];
 		level_setup<D>(c, l, x, frac, base);
 #pragma unroll
-		for (uint32_t k = 0; k < (1u << D); ++k) {
+		for (uint32_t q = 0; q < (1u << (D - 1)); ++q) {
+			const uint32_t k = xbit | (q << 1);
 			const float w = corner_weight<D>(frac, k);
 			const uint32_t e = corner_index<D>(c, l, base, k);
 			if constexpr (F >= 2) {
@@ -197,7 +202,7 @@ static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hip
 template <uint32_t D>
 static void launch_bwd(uint32_t F, const GridConst& c, const GridBwdArgs& a, hipStream_t s) {
 	const uint32_t P = F >= 2 ? F / 2 : 1;
-	const dim3 grid(div_round_up((uint64_t)a.n * P, 256)), block(256);
+	const dim3 grid(div_round_up((uint64_t)a.n * 2 * P, 256)), block(256);
 	switch (F) {
 		case 1: k_grid_backward<D, 1><<<grid, block, 0, s>>>(c, a); break;
 		case 2: k_grid_backward<D, 2><<<grid, block, 0, s>>>(c, a); break;

@@ -711,16 +711,27 @@ void mlp_run(const MlpPlan& p, MlpMode mode, const MlpArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------------
-__global__ void k_reduce_slabs(const float* __restrict__ slabs, uint32_t n_slabs, uint32_t n, f16* __restrict__ grad, bool accumulate) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= n) return;
-	float s = accumulate ? (float)grad[i] : 0.f;
-	for (uint32_t b = 0; b < n_slabs; ++b) s += slabs[(size_t)b * n + i];
-	grad[i] = (f16)s;
+// Block = 32 parameters x 8 slab groups; each thread sums every 8th slab of one parameter, then the 8
+// partial sums are added in a fixed order (deterministic).
+__global__ void __launch_bounds__(256) k_reduce_slabs(const float* __restrict__ slabs, uint32_t n_slabs, uint32_t n,
+                                                      f16* __restrict__ grad, bool accumulate) {
+	__shared__ float part[8][33];
+	const uint32_t p = blockIdx.x * 32 + (threadIdx.x & 31), g = threadIdx.x >> 5;
+	float s = 0.f;
+	if (p < n)
+		for (uint32_t b = g; b < n_slabs; b += 8) s += slabs[(size_t)b * n + p];
+	part[g][threadIdx.x & 31] = s;
+	__syncthreads();
+	if (g == 0 && p < n) {
+		float t = accumulate ? (float)grad[p] : 0.f;
+#pragma unroll
+		for (int k = 0; k < 8; ++k) t += part[k][threadIdx.x];
+		grad[p] = (f16)t;
+	}
 }
 
 void reduce_slabs(const float* slabs, uint32_t n_slabs, uint32_t n, f16* grad, bool accumulate, hipStream_t s) {
-	k_reduce_slabs<<<div_round_up(n, 256), 256, 0, s>>>(slabs, n_slabs, n, grad, accumulate);
+	k_reduce_slabs<<<div_round_up(n, 32), 256, 0, s>>>(slabs, n_slabs, n, grad, accumulate);
 	NGP_HIP(hipGetLastError());
 }
 
