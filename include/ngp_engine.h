@@ -93,6 +93,9 @@ int ngp_model_set_params(ngp_model* m, void* params, void* inference_params, voi
 int ngp_model_initialize_params(const ngp_model* m, uint64_t seed, float* params_full_precision_host, float scale);
 /* GridEncoding::set_max_level / set_max_level_gpu (src/testbed.cu:3856-3864; testbed_nerf.cu:3996,4004) */
 int ngp_model_set_max_level(ngp_model* m, float max_level, const float* max_level_per_sample);
+/* engine knobs: "grid_backward_mode" = 0 auto, 1 direct packed-f16 atomics (tcnn-style),
+ * 2 spatially binned LDS windows for the coarse levels (+ direct for the rest) */
+int ngp_model_set_option(ngp_model* m, const char* key, double value);
 /* pre-size internal workspaces for batches up to n (lets callers capture steps into HIP graphs) */
 int ngp_model_reserve(ngp_model* m, uint32_t n);
 

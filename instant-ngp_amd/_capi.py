@@ -57,6 +57,7 @@ SIGNATURES = {
     "ngp_model_set_params": (i32, [P, P, P, P]),
     "ngp_model_initialize_params": (i32, [P, u64, P, f32]),
     "ngp_model_set_max_level": (i32, [P, f32, P]),
+    "ngp_model_set_option": (i32, [P, C.c_char_p, C.c_double]),
     "ngp_model_reserve": (i32, [P, u32]),
     "ngp_inference": (i32, [P, P, u32, P, u32, P, u32, u32, i32]),
     "ngp_density": (i32, [P, P, u32, P, u32, P, u32, u32, i32]),

@@ -1,0 +1,41 @@
+// binning.h — spatial binning of samples + LDS-windowed hash-grid backward (see binning.hip).
+#pragma once
+#include <algorithm>
+
+#include "grid.h"
+
+namespace ngp {
+
+constexpr uint32_t BIN_BLOCK = 1024;  // samples per histogram block
+
+struct WinPlan {
+	uint32_t R = 0;        // bins per axis
+	uint32_t n_bins = 0;   // R^D
+	uint32_t n_win = 0;    // levels 0..n_win-1 are accumulated in LDS windows
+	uint32_t W[16] = {};   // window width (vertices per axis) per level
+	uint32_t voff[17] = {};// window vertex offsets in LDS
+};
+
+struct WinArgs {
+	uint32_t n;
+	const float* pos; uint32_t pos_stride;
+	const f16* dL_dy; uint32_t dy_stride;  // AoS
+	f16* grad;
+	const uint32_t* sorted;                // sample ids grouped by bin
+	const uint32_t* offs;                  // exclusive-scanned bin-major histogram [bin][hist block]
+	uint32_t n_hist_blocks;
+	uint32_t R, n_bins, n_win;
+	uint32_t W[16];
+	uint32_t voff[17];
+};
+
+// Choose R and the windowed level prefix by a request-count cost model (0 windowed levels => none).
+WinPlan make_win_plan(const GridDesc& g, uint32_t n, size_t lds_budget_bytes);
+inline uint32_t bin_hist_len(const WinPlan& p, uint32_t n) { return p.n_bins * ((n + BIN_BLOCK - 1) / BIN_BLOCK); }
+// hist: [n_bins x ceil(n/BIN_BLOCK)] u32 (becomes the scanned offsets), sorted: [n] u32
+void bin_samples(uint32_t D, uint32_t n, const float* pos, uint32_t stride, const WinPlan& p, uint32_t* hist,
+                 uint32_t* sorted, hipStream_t s);
+void grid_backward_windowed(const GridDesc& g, const WinPlan& p, const GridBwdArgs& b, const uint32_t* hist,
+                            const uint32_t* sorted, hipStream_t s);
+
+}  // namespace ngp

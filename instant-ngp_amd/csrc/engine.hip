@@ -12,6 +12,7 @@
 
 #include "../../include/ngp_engine.h"
 #include "common.h"
+#include "binning.h"
 #include "grid.h"
 #include "json.h"
 #include "mlp.h"
@@ -127,7 +128,10 @@ struct ngp_model {
 	uint64_t mlp0_params = 0, mlp1_params = 0, grid_params = 0, n_params = 0;
 	FragDesc* d_descs = nullptr;
 	uint32_t n_all_frags = 0;
-	DevBuf frags, frags_inf, enc, denc, slabs;
+	DevBuf frags, frags_inf, enc, denc, slabs, bin_hist, bin_sorted;
+	int grid_backward_mode = 0;  // 0 auto, 1 direct (tcnn-style), 2 windowed (binned LDS)
+	WinPlan win_plan;
+	uint32_t win_plan_n = 0;
 	f16 *params = nullptr, *inference_params = nullptr, *gradients = nullptr;
 	float max_level = 1.0f;
 	const float* max_level_per_sample = nullptr;
@@ -206,6 +210,30 @@ struct ngp_model {
 			NGP_HIP(hipMemsetAsync(gradients + grid_offset(), 0, grid_params * sizeof(f16), s));
 		}
 		GridBwdArgs b{n, in, stride, dL_denc, enc_width, AoS, gradients + grid_offset(), max_level, max_level_per_sample};
+		scatter_grid_grad(s, b);
+	}
+	// Hash-grid backward: windowed (spatial bins + LDS) for the coarse levels when it pays, direct
+	// packed-f16 atomics for the rest. The windowed path needs all levels active (max_level >= 1).
+	void scatter_grid_grad(hipStream_t s, GridBwdArgs b) {
+		const bool can_win = grid_backward_mode != 1 && b.dy_layout == AoS && !b.max_level_per_sample &&
+		                     b.max_level >= 1.0f && grid.n_features >= 2 && b.n >= 4096;
+		if (can_win) {
+			if (win_plan_n != b.n) { win_plan = make_win_plan(grid, b.n, 120 * 1024); win_plan_n = b.n; }
+			if (win_plan.n_win > 0) {
+				uint32_t* hist = (uint32_t*)bin_hist.get((size_t)bin_hist_len(win_plan, b.n) * 4);
+				uint32_t* sorted = (uint32_t*)bin_sorted.get((size_t)b.n * 4);
+				{
+					ProfScope ps("bin_samples", s);
+					bin_samples(grid.n_dims, b.n, b.pos, b.pos_stride, win_plan, hist, sorted, s);
+				}
+				{
+					ProfScope ps("grid_backward_win", s);
+					grid_backward_windowed(grid, win_plan, b, hist, sorted, s);
+				}
+				b.level_begin = win_plan.n_win;
+				if (b.level_begin >= grid.n_levels) return;
+			}
+		}
 		ProfScope ps("grid_backward", s);
 		grid_backward(grid, b, s);
 	}
@@ -372,6 +400,19 @@ int ngp_model_set_max_level(ngp_model* m, float max_level, const float* per_samp
 	NGP_TRY({ m->max_level = max_level; m->max_level_per_sample = per_sample; });
 }
 
+int ngp_model_set_option(ngp_model* m, const char* key, double value) {
+	NGP_ARG(m && key);
+	NGP_TRY({
+		const std::string k = key;
+		if (k == "grid_backward_mode") {
+			NGP_CHECK(value == 0 || value == 1 || value == 2, "grid_backward_mode must be 0 (auto), 1 (direct), 2 (windowed)");
+			m->grid_backward_mode = (int)value;
+		} else {
+			throw Error("unknown model option: " + k);
+		}
+	});
+}
+
 int ngp_model_reserve(ngp_model* m, uint32_t n) {
 	NGP_ARG(m);
 	NGP_TRY({
@@ -401,7 +442,7 @@ int ngp_encoding_backward(ngp_model* m, void* stream, uint32_t n, const float* i
 			NGP_HIP(hipMemsetAsync(m->gradients + m->grid_offset(), 0, m->grid_params * sizeof(f16), S(stream)));
 		GridBwdArgs b{n, input, input_stride, (const f16*)dL_doutput, dL_stride, dL_layout, m->gradients + m->grid_offset(),
 		              m->max_level, m->max_level_per_sample};
-		grid_backward(m->grid, b, S(stream));
+		m->scatter_grid_grad(S(stream), b);
 	});
 }
 

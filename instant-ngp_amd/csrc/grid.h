@@ -46,6 +46,7 @@ struct GridBwdArgs {
 	f16* grad;                 // [entries x F], accumulated with packed fp16 atomics
 	float max_level;
 	const float* max_level_per_sample;
+	uint32_t level_begin = 0;  // levels below were handled elsewhere (windowed backward)
 };
 
 void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream);
@@ -76,5 +77,8 @@ __device__ __forceinline__ uint32_t grid_index2(uint32_t T, uint32_t res, uint32
 	if (T < stride) index = x ^ (y * 2654435761u);
 	return index % T;
 }
+
+GridConst make_grid_const(const GridDesc& g);
+int device_cu_count();
 
 }  // namespace ngp

@@ -40,7 +40,7 @@ void grid_desc_init(GridDesc& g, uint32_t D, uint32_t L, uint32_t F, uint32_t lo
 	g.offsets[L] = off;
 }
 
-static GridConst make_const(const GridDesc& g) {
+GridConst make_grid_const(const GridDesc& g) {
 	GridConst c;
 	c.n_levels = g.n_levels;
 	c.n_features = g.n_features;
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(256) k_grid_backward(const GridConst c, const 
 #pragma unroll
 	for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * a.pos_stride + d];
 	const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
-	for (uint32_t l = 0; l < c.n_levels; ++l) {
+	for (uint32_t l = a.level_begin; l < c.n_levels; ++l) {
 		if ((float)l > ml + 1e-3f) break;
 		float g0, g1;
 		const uint32_t f0 = l * F + (F >= 2 ? 2 * pair : 0);
@@ -214,7 +214,7 @@ static void launch_bwd(uint32_t F, const GridConst& c, const GridBwdArgs& a, hip
 
 void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream) {
 	if (a.n == 0) return;
-	GridConst c = make_const(g);
+	GridConst c = make_grid_const(g);
 	if (g.n_dims == 3) launch_fwd<3>(g.n_features, c, a, stream);
 	else launch_fwd<2>(g.n_features, c, a, stream);
 	NGP_HIP(hipGetLastError());
@@ -222,7 +222,7 @@ void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream) {
 
 void grid_backward(const GridDesc& g, const GridBwdArgs& a, hipStream_t stream) {
 	if (a.n == 0) return;
-	GridConst c = make_const(g);
+	GridConst c = make_grid_const(g);
 	if (g.n_dims == 3) launch_bwd<3>(g.n_features, c, a, stream);
 	else launch_bwd<2>(g.n_features, c, a, stream);
 	NGP_HIP(hipGetLastError());

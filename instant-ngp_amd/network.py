@@ -119,6 +119,9 @@ class Model:
         self._max_level_keep = per_sample
         check(lib().ngp_model_set_max_level(self.handle, float(max_level), _ptr(per_sample)))
 
+    def set_option(self, key, value):
+        check(lib().ngp_model_set_option(self.handle, key.encode(), float(value)))
+
     def reserve(self, n):
         check(lib().ngp_model_reserve(self.handle, n))
 
