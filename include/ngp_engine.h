@@ -142,6 +142,82 @@ int ngp_trainer_set_params_full_precision(ngp_trainer* t, const float* params_ho
 int ngp_trainer_serialize(ngp_trainer* t, void* buf_host, uint64_t* size);
 int ngp_trainer_deserialize(ngp_trainer* t, const void* buf_host, uint64_t size);
 
+/* ---- NeRF training kernels (src/testbed_nerf.cu), without OptiX --------------------------- */
+typedef struct ngp_nerf_dataset ngp_nerf_dataset;  /* training images on device + cameras */
+typedef struct ngp_nerf_trainer ngp_nerf_trainer;  /* Testbed NeRF training state (grid, counters, rng) */
+
+/* One training image (TrainingImageMetadata, nerf_loader.h; xform after nerf_matrix_to_ngp):
+ * camera-to-world mat4x3, column-major {x axis, y axis, z axis, origin}. */
+typedef struct {
+	uint32_t width, height;
+	float focal_length[2];
+	float principal_point[2];
+	float xform[12];
+} ngp_nerf_image;
+
+/* Training knobs with the reference defaults (testbed.h:716-785; load_nerf_post testbed_nerf.cu:3093-3109). */
+typedef struct {
+	float aabb_min[3], aabb_max[3];   /* m_aabb */
+	float cone_angle_constant;        /* 0 when aabb_scale <= 1, else 1/256 */
+	uint32_t max_cascade;             /* ceil(log2(aabb_scale)) */
+	uint32_t snap_to_pixel_centers;   /* 1 */
+	uint32_t random_bg_color;         /* 1 */
+	uint32_t linear_colors;           /* 0 */
+	uint32_t color_space_linear;      /* 1 (m_color_space = Linear) */
+	float background_color[3];        /* 0 */
+	uint32_t rgb_activation;          /* 0 None, 1 ReLU, 2 Logistic, 3 Exponential; default 3 */
+	uint32_t density_activation;      /* default 3 */
+	uint32_t loss_type;               /* 0 L2, 1 L1, 2 MAPE, 3 SMAPE, 4 Huber, 5 LogL1, 6 RelativeL2; base.json: Huber */
+	float near_distance;              /* 0.1 */
+	uint32_t target_batch_size;       /* 2^18 */
+} ngp_nerf_config;
+
+typedef struct { uint64_t state, inc; } ngp_rng; /* tcnn::pcg32 state (default_rng_t) */
+
+typedef struct {
+	uint32_t step, rays_per_batch, measured_batch_size, measured_batch_size_before_compaction;
+	float loss;
+} ngp_nerf_stats;
+
+int ngp_nerf_default_config(float aabb_scale, ngp_nerf_config* out);
+/* images: RGBA8 sRGB (EImageDataType::Byte; 0x00FF00FF marks masked pixels, common_device.cuh:893) */
+int ngp_nerf_dataset_create(uint32_t n_images, const ngp_nerf_image* images, const void* const* rgba8_host,
+                            ngp_nerf_dataset** out);
+void ngp_nerf_dataset_destroy(ngp_nerf_dataset* ds);
+
+/* generate_training_samples_nerf (testbed_nerf.cu:1382-1658); deterministic slots (prefix scans).
+ * rays: [n_rays x 6] {o, d}; numsteps: [n_rays x 2] {n, base}; coords: [max_samples x 7];
+ * counters: [2] = {rays kept, total steps incl. dropped rays}. */
+int ngp_nerf_generate_training_samples(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream,
+                                       uint32_t n_rays, uint32_t ray_offset, uint32_t n_rays_total, ngp_rng rng,
+                                       uint32_t max_samples, const uint8_t* bitfield, uint32_t* ray_indices, float* rays,
+                                       uint32_t* numsteps, float* coords, uint32_t* counters);
+/* compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012): composite, loss, compaction, dL/doutput */
+int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
+                          uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
+                          const void* network_output, const uint32_t* ray_indices, const float* rays, uint32_t* numsteps,
+                          const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
+                          uint32_t* compacted_counter, const float* mean_density, float loss_scale);
+/* tcnn fill_rollover / fill_rollover_and_rescale (testbed_nerf.cu:4061-4069); dtype 0 f32, 1 f16 */
+int ngp_nerf_fill_rollover(void* stream, uint32_t n_elements, uint32_t stride, const uint32_t* n_input, void* data,
+                           int dtype, int rescale);
+/* occupancy grid (testbed_nerf.cu:635-809, 3412-3567) */
+int ngp_nerf_grid_generate_samples(void* stream, const ngp_nerf_config* cfg, uint32_t n, ngp_rng rng, uint32_t step,
+                                   const float* grid, uint32_t n_cascades, float thresh, float* positions,
+                                   uint32_t* indices);
+int ngp_nerf_grid_splat_max(void* stream, uint32_t n, const uint32_t* indices, const void* density_rm,
+                            uint32_t density_activation, float* grid_tmp);
+int ngp_nerf_grid_ema(void* stream, uint32_t n, float decay, float* grid, const float* grid_tmp);
+int ngp_nerf_grid_mean_and_bitfield(void* stream, const float* grid, uint32_t max_cascade, float* mean, uint8_t* bitfield);
+
+/* Testbed-level NeRF training (Testbed::train -> training_prep_nerf + train_nerf, src/testbed.cu:4285-4370,
+ * testbed_nerf.cu:3611-3862, 4137-4152). The model/trainer must be a NerfNetwork and its Trainer. */
+int ngp_nerf_trainer_create(ngp_model* model, ngp_trainer* trainer, const ngp_nerf_dataset* ds,
+                            const ngp_nerf_config* cfg, uint64_t seed, ngp_nerf_trainer** out);
+void ngp_nerf_trainer_destroy(ngp_nerf_trainer* t);
+int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_nerf_stats* out);
+int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** density_grid, uint8_t** bitfield, float** mean_density);
+
 #pragma GCC visibility pop
 #ifdef __cplusplus
 }

@@ -14,6 +14,7 @@ struct WinPlan {
 	uint32_t n_win = 0;    // levels 0..n_win-1 are accumulated in LDS windows
 	uint32_t W[16] = {};   // window width (vertices per axis) per level
 	uint32_t voff[17] = {};// window vertex offsets in LDS
+	uint32_t debug = 0;    // timing experiments only: 1 skip accumulate, 2 skip flush
 };
 
 struct WinArgs {
@@ -27,12 +28,15 @@ struct WinArgs {
 	uint32_t R, n_bins, n_win;
 	uint32_t W[16];
 	uint32_t voff[17];
+	uint32_t debug;
 };
 
 // Choose R and the windowed level prefix by a request-count cost model (0 windowed levels => none).
 WinPlan make_win_plan(const GridDesc& g, uint32_t n, size_t lds_budget_bytes);
 inline uint32_t bin_hist_len(const WinPlan& p, uint32_t n) { return p.n_bins * ((n + BIN_BLOCK - 1) / BIN_BLOCK); }
-// hist: [n_bins x ceil(n/BIN_BLOCK)] u32 (becomes the scanned offsets), sorted: [n] u32
+// workspace (u32 count) for bin_samples' histogram + scanned offsets + scan temp; sorted: [n] u32
+size_t bin_workspace_u32(const WinPlan& p, uint32_t n);
+const uint32_t* bin_offsets(const WinPlan& p, uint32_t n, const uint32_t* ws);
 void bin_samples(uint32_t D, uint32_t n, const float* pos, uint32_t stride, const WinPlan& p, uint32_t* hist,
                  uint32_t* sorted, hipStream_t s);
 void grid_backward_windowed(const GridDesc& g, const WinPlan& p, const GridBwdArgs& b, const uint32_t* hist,

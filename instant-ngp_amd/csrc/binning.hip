@@ -9,6 +9,8 @@
 // aligned x-group inside one aligned 8-entry group since the x prime is 1). Requests drop to about
 // bins x window surface instead of samples x corners. Levels whose window does not fit LDS fall back
 // to the direct kernel (grid.hip). Semantics are unchanged (same weights, same entries, fp16 sums).
+#include <hipcub/hipcub.hpp>
+
 #include "binning.h"
 
 #include <cmath>
@@ -122,7 +124,7 @@ __global__ void __launch_bounds__(512) k_grid_backward_win(const GridConst c, co
 		__syncthreads();
 
 		// accumulate: one work item per (sample, windowed level)
-		const uint32_t items = (end - start) * nwin;
+		const uint32_t items = (a.debug & 1) ? 0 : (end - start) * nwin;
 		for (uint32_t w = threadIdx.x; w < items; w += blockDim.x) {
 			const uint32_t l = w % nwin;
 			const uint32_t i = a.sorted[start + w / nwin];
@@ -191,7 +193,7 @@ __global__ void __launch_bounds__(512) k_grid_backward_win(const GridConst c, co
 			const int gx0 = org[0] & ~7;
 			const uint32_t groups = (uint32_t)(((org[0] + (int)W - 1) >> 3) - (org[0] >> 3) + 1);
 			const uint32_t rows = D == 3 ? W * W : W;
-			const uint32_t items = rows * groups * 8 * P;
+			const uint32_t items = (a.debug & 2) ? 0 : rows * groups * 8 * P;
 			for (uint32_t w = threadIdx.x; w < items; w += blockDim.x) {
 				const uint32_t pair = w % P;
 				const uint32_t vtx = (w / P) % 8;
@@ -259,6 +261,15 @@ WinPlan make_win_plan(const GridDesc& g, uint32_t n, size_t lds_budget_bytes) {
 	return best;
 }
 
+size_t bin_workspace_u32(const WinPlan& p, uint32_t n) {
+	const uint32_t len = bin_hist_len(p, n);
+	size_t bytes = 0;
+	NGP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)len));
+	return 2 * (size_t)len + (bytes + 3) / 4 + 64;
+}
+
+const uint32_t* bin_offsets(const WinPlan& p, uint32_t n, const uint32_t* ws) { return ws + bin_hist_len(p, n); }
+
 void bin_samples(uint32_t D, uint32_t n, const float* pos, uint32_t stride, const WinPlan& p, uint32_t* hist,
                  uint32_t* sorted, hipStream_t s) {
 	const uint32_t nb = div_round_up(n, BIN_BLOCK);
@@ -266,8 +277,13 @@ void bin_samples(uint32_t D, uint32_t n, const float* pos, uint32_t stride, cons
 	if (D == 3) k_bin_hist<3><<<nb, 256, lds, s>>>(n, pos, stride, p.R, p.n_bins, hist);
 	else k_bin_hist<2><<<nb, 256, lds, s>>>(n, pos, stride, p.R, p.n_bins, hist);
 	NGP_HIP(hipGetLastError());
-	k_scan_exclusive<<<1, 1024, 0, s>>>(hist, p.n_bins * nb);
-	NGP_HIP(hipGetLastError());
+	// exclusive scan of the bin-major histogram (hipCUB device scan, in place via the tail buffer)
+	const uint32_t len = p.n_bins * nb;
+	uint32_t* scanned = hist + len;
+	size_t bytes = 0;
+	NGP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, hist, scanned, (int)len, s));
+	NGP_HIP(hipcub::DeviceScan::ExclusiveSum((void*)(scanned + len), bytes, hist, scanned, (int)len, s));
+	hist = scanned;
 	if (D == 3) k_bin_scatter<3><<<nb, 256, lds, s>>>(n, pos, stride, p.R, p.n_bins, hist, sorted);
 	else k_bin_scatter<2><<<nb, 256, lds, s>>>(n, pos, stride, p.R, p.n_bins, hist, sorted);
 	NGP_HIP(hipGetLastError());
@@ -277,7 +293,8 @@ void grid_backward_windowed(const GridDesc& g, const WinPlan& p, const GridBwdAr
                             const uint32_t* sorted, hipStream_t s) {
 	WinArgs a{};
 	a.n = b.n; a.pos = b.pos; a.pos_stride = b.pos_stride; a.dL_dy = b.dL_dy; a.dy_stride = b.dy_stride; a.grad = b.grad;
-	a.sorted = sorted; a.offs = hist; a.n_hist_blocks = div_round_up(b.n, BIN_BLOCK);
+	a.sorted = sorted; a.offs = bin_offsets(p, b.n, hist); a.n_hist_blocks = div_round_up(b.n, BIN_BLOCK);
+	a.debug = p.debug;
 	a.R = p.R; a.n_bins = p.n_bins; a.n_win = p.n_win;
 	for (uint32_t l = 0; l < 16; ++l) a.W[l] = p.W[l];
 	for (uint32_t l = 0; l <= 16; ++l) a.voff[l] = p.voff[l];

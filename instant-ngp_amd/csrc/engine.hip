@@ -130,6 +130,7 @@ struct ngp_model {
 	uint32_t n_all_frags = 0;
 	DevBuf frags, frags_inf, enc, denc, slabs, bin_hist, bin_sorted;
 	int grid_backward_mode = 0;  // 0 auto, 1 direct (tcnn-style), 2 windowed (binned LDS)
+	uint32_t win_debug = 0;      // timing experiments only (see binning.h)
 	WinPlan win_plan;
 	uint32_t win_plan_n = 0;
 	f16 *params = nullptr, *inference_params = nullptr, *gradients = nullptr;
@@ -220,7 +221,8 @@ struct ngp_model {
 		if (can_win) {
 			if (win_plan_n != b.n) { win_plan = make_win_plan(grid, b.n, 120 * 1024); win_plan_n = b.n; }
 			if (win_plan.n_win > 0) {
-				uint32_t* hist = (uint32_t*)bin_hist.get((size_t)bin_hist_len(win_plan, b.n) * 4);
+				win_plan.debug = win_debug;
+				uint32_t* hist = (uint32_t*)bin_hist.get(bin_workspace_u32(win_plan, b.n) * 4);
 				uint32_t* sorted = (uint32_t*)bin_sorted.get((size_t)b.n * 4);
 				{
 					ProfScope ps("bin_samples", s);
@@ -407,6 +409,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 		if (k == "grid_backward_mode") {
 			NGP_CHECK(value == 0 || value == 1 || value == 2, "grid_backward_mode must be 0 (auto), 1 (direct), 2 (windowed)");
 			m->grid_backward_mode = (int)value;
+		} else if (k == "win_debug") {
+			m->win_debug = (uint32_t)value;
 		} else {
 			throw Error("unknown model option: " + k);
 		}

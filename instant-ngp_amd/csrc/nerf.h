@@ -1,0 +1,99 @@
+// nerf.h — NeRF training kernels (sampling, loss + compaction, rollover, occupancy grid) for gfx950.
+//
+// Re-implements src/testbed_nerf.cu's training kernels without OptiX.
+// Difference by design: the reference assigns sample / ray / compacted slots with
+// atomicAdd counters, so its sample order is nondeterministic; here slots come from exclusive
+// prefix scans in ray order, so the output is deterministic and equal to the reference's as a
+// multiset keyed by (ray, step). Counters keep the reference's meaning (totals include rays that
+// were dropped for exceeding the sample budget).
+#pragma once
+#include "../../include/ngp_engine.h"
+#include "common.h"
+
+namespace ngp {
+namespace nerf {
+
+constexpr uint32_t GRIDSIZE = 128;                         // NERF_GRIDSIZE (nerf.h:24-30)
+constexpr uint32_t GRID_N_CELLS = GRIDSIZE * GRIDSIZE * GRIDSIZE;
+constexpr uint32_t CASCADES = 8;                           // NERF_CASCADES (testbed_nerf.cu:59)
+constexpr uint32_t STEPS = 1024;                           // NERF_STEPS (:58)
+constexpr float SQRT3 = 1.73205080757f;
+constexpr float MIN_CONE_STEPSIZE = SQRT3 / STEPS;         // STEPSIZE() (:65-71)
+constexpr float MAX_CONE_STEPSIZE = MIN_CONE_STEPSIZE * (1 << (CASCADES - 1)) * STEPS / GRIDSIZE;  // (:76-79)
+constexpr uint32_t N_MAX_RANDOM_SAMPLES_PER_RAY = 16;      // (:85-87)
+constexpr float MIN_OPTICAL_THICKNESS = 0.01f;             // (:92-94)
+constexpr uint32_t BITFIELD_BYTES = GRID_N_CELLS * CASCADES / 8;  // grid_mip_offset(NERF_CASCADES)/8
+
+enum Activation : uint32_t { ACT_NONE = 0, ACT_RELU = 1, ACT_LOGISTIC = 2, ACT_EXP = 3 };
+enum LossType : uint32_t { LOSS_L2 = 0, LOSS_L1 = 1, LOSS_MAPE = 2, LOSS_SMAPE = 3, LOSS_HUBER = 4, LOSS_LOGL1 = 5, LOSS_RELL2 = 6 };
+
+struct Camera {          // per image, device side
+	uint32_t width, height;
+	float focal[2], principal[2];
+	float m[12];         // effective camera matrix (rolling-shutter slerp at t=0 applied on the host)
+	uint64_t pixel_offset;  // first RGBA8 pixel of this image in the packed image buffer
+};
+
+struct Rng { uint64_t state, inc; };  // tcnn::pcg32 state
+
+// Host: effective camera matrix = get_xform_given_rolling_shutter(start == end, t = 0)
+// (common_device.cuh:401-408): rotation goes through glm quat_cast / slerp / normalize / mat3_cast.
+void effective_camera_matrix(const float xform[12], float out[12]);
+
+struct Dataset {
+	uint32_t n_images = 0;
+	Camera* d_cams = nullptr;
+	uint32_t* d_pixels = nullptr;  // RGBA8 packed, sRGB
+	std::vector<Camera> cams;
+	~Dataset();
+};
+
+struct SampleArgs {
+	uint32_t n_rays, ray_offset, n_rays_total_for_image_idx;  // image_idx uses the global ray id
+	uint32_t max_samples;
+	Rng rng;
+	const uint8_t* bitfield;
+	uint32_t* ray_indices;     // [n_rays] compacted
+	float* rays;               // [n_rays x 6] {o, d} (unnormalized d)
+	uint32_t* numsteps;        // [n_rays x 2] {numsteps, base}
+	float* coords;             // [max_samples x 7] NerfCoordinate
+	uint32_t* counters;        // [2]: rays kept, numsteps total (incl. dropped)
+};
+
+struct LossArgs {
+	uint32_t n_rays;           // rays_per_batch (kernel grid); rays kept are counters[0]
+	uint32_t n_rays_total_for_image_idx;
+	Rng rng;
+	uint32_t max_samples_compacted;
+	const uint32_t* ray_counter;
+	const f16* network_output;  // [n x 16]
+	const uint32_t* ray_indices;
+	const float* rays;
+	uint32_t* numsteps;        // in: {numsteps, base}; out: {compacted numsteps, compacted base}
+	const float* coords_in;
+	float* coords_out;         // [max_samples_compacted x 7]
+	f16* dloss_doutput;        // [max_samples_compacted x 16]
+	float* loss;               // [n_rays]
+	uint32_t* compacted_counter;  // [1]
+	const float* mean_density;    // [1]
+	float loss_scale;
+	float bg[3];
+};
+
+// The kernels (each cites its reference kernel in nerf.hip).
+void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs& a, void* scan_tmp, size_t scan_bytes,
+                 uint32_t* tmp_u32, float* tmp_f32, hipStream_t s);
+void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs& a, void* scan_tmp, size_t scan_bytes,
+                  uint32_t* tmp_u32, float* tmp_f32, hipStream_t s);
+void fill_rollover_f16(uint32_t n_elements, uint32_t stride, const uint32_t* n_input, f16* data, bool rescale, hipStream_t s);
+void fill_rollover_f32(uint32_t n_elements, uint32_t stride, const uint32_t* n_input, float* data, hipStream_t s);
+void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_config& cfg, const float* grid_in,
+                           uint32_t n_cascades, float thresh, float* positions, uint32_t* indices, hipStream_t s);
+void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t density_activation, float* grid_tmp,
+                    hipStream_t s);
+void grid_ema(uint32_t n, float decay, float* grid, const float* grid_tmp, hipStream_t s);
+void grid_mean_bitfield(const float* grid, uint32_t max_cascade, float* mean_out, uint8_t* bitfield, hipStream_t s);
+size_t scan_temp_bytes(uint32_t n);
+
+}  // namespace nerf
+}  // namespace ngp

@@ -1,0 +1,746 @@
+// nerf.hip — NeRF training kernels for gfx950 (see nerf.h). Each kernel cites the reference kernel
+// it re-implements; float formulas follow the reference line by line (glm vector ops written out
+// per component, -ffp-contract=off), so with cone_angle = 0 sample coordinates match the oracle
+// bit for bit. With cone_angle > 0 the log/exp stepping uses ocml logf/expf (the reference uses
+// --use_fast_math intrinsics), so positions match within float rounding.
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstring>
+
+#include "nerf.h"
+
+namespace ngp {
+namespace nerf {
+
+// ------------------------------------------------------------------------------------------------
+// device math
+// ------------------------------------------------------------------------------------------------
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+
+__device__ __forceinline__ uint32_t pcg_next(Rng& r) {
+	const uint64_t old = r.state;
+	r.state = old * 0x5851f42d4c957f2dULL + r.inc;
+	const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u), rot = (uint32_t)(old >> 59u);
+	return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+}
+__device__ __forceinline__ float pcg_float(Rng& r) { return __uint_as_float((pcg_next(r) >> 9) | 0x3f800000u) - 1.0f; }
+__device__ __forceinline__ void pcg_advance(Rng& r, uint64_t delta) {
+	uint64_t cm = 0x5851f42d4c957f2dULL, cp = r.inc, am = 1u, ap = 0u;
+	while (delta > 0) {
+		if (delta & 1) { am *= cm; ap = ap * cm + cp; }
+		cp = (cm + 1) * cp; cm *= cm; delta /= 2;
+	}
+	r.state = am * r.state + ap;
+}
+
+// testbed_nerf.cu:114-184
+__device__ float to_stepping_space(float t, float cone) {
+	if (cone <= 1e-5f) return t / MIN_CONE_STEPSIZE;
+	const float log1p_c = logf(1.0f + cone);
+	const float a = (logf(MIN_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
+	const float b = (logf(MAX_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
+	const float at = expf(a * log1p_c), bt = expf(b * log1p_c);
+	if (t <= at) return (t - at) / MIN_CONE_STEPSIZE + a;
+	if (t <= bt) return logf(t) / log1p_c;
+	return (t - bt) / MAX_CONE_STEPSIZE + b;
+}
+__device__ float from_stepping_space(float n, float cone) {
+	if (cone <= 1e-5f) return n * MIN_CONE_STEPSIZE;
+	const float log1p_c = logf(1.0f + cone);
+	const float a = (logf(MIN_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
+	const float b = (logf(MAX_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
+	const float at = expf(a * log1p_c), bt = expf(b * log1p_c);
+	if (n <= a) return (n - a) * MIN_CONE_STEPSIZE + at;
+	if (n <= b) return expf(n * log1p_c);
+	return (n - b) * MAX_CONE_STEPSIZE + bt;
+}
+__device__ __forceinline__ float advance_n_steps(float t, float cone, float n) { return from_stepping_space(to_stepping_space(t, cone) + n, cone); }
+__device__ __forceinline__ float calc_dt(float t, float cone) { return advance_n_steps(t, cone, 1.0f) - t; }
+
+__device__ __forceinline__ float signf_(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }  // glm::sign
+
+// testbed_nerf.cu:272-315
+__device__ float distance_to_next_voxel(V3 pos, V3 dir, V3 idir, float res) {
+	const V3 p = v3(res * (pos.x - 0.5f), res * (pos.y - 0.5f), res * (pos.z - 0.5f));
+	const float tx = (floorf(p.x + 0.5f + 0.5f * signf_(dir.x)) - p.x) * idir.x;
+	const float ty = (floorf(p.y + 0.5f + 0.5f * signf_(dir.y)) - p.y) * idir.y;
+	const float tz = (floorf(p.z + 0.5f + 0.5f * signf_(dir.z)) - p.z) * idir.z;
+	const float t = fminf(fminf(tx, ty), tz);
+	return fmaxf(t / res, 0.0f);
+}
+__device__ float advance_to_next_voxel(float t, float cone, V3 pos, V3 dir, V3 idir, uint32_t mip) {
+	const float res = scalbnf((float)GRIDSIZE, -(int)mip);
+	float t_target = t + distance_to_next_voxel(pos, dir, idir, res);
+	t = to_stepping_space(t, cone);
+	t_target = to_stepping_space(t_target, cone);
+	return from_stepping_space(t + ceilf(fmaxf(t_target - t, 0.5f)), cone);
+}
+
+// testbed_nerf.cu:614-633
+__device__ uint32_t mip_from_pos(V3 pos, uint32_t max_cascade) {
+	int exponent;
+	const float maxval = fmaxf(fmaxf(fabsf(pos.x - 0.5f), fabsf(pos.y - 0.5f)), fabsf(pos.z - 0.5f));
+	frexpf(maxval, &exponent);
+	const int e = exponent + 1;
+	return (uint32_t)(e < 0 ? 0 : (e > (int)max_cascade ? (int)max_cascade : e));
+}
+__device__ uint32_t mip_from_dt(float dt, V3 pos, uint32_t max_cascade) {
+	const uint32_t mip = mip_from_pos(pos, max_cascade);
+	dt *= 2 * GRIDSIZE;
+	if (dt < 1.0f) return mip;
+	int exponent;
+	frexpf(dt, &exponent);
+	int v = (int)mip > exponent ? (int)mip : exponent;  // tcnn::clamp(mip, exponent, max_cascade)
+	return (uint32_t)(v < (int)max_cascade ? v : (int)max_cascade);
+}
+
+__device__ __forceinline__ uint32_t expand_bits(uint32_t v) {
+	v = (v * 0x00010001u) & 0xFF0000FFu;
+	v = (v * 0x00000101u) & 0x0F00F00Fu;
+	v = (v * 0x00000011u) & 0xC30C30C3u;
+	v = (v * 0x00000005u) & 0x49249249u;
+	return v;
+}
+// tcnn morton3D: x in bit 0 (consistent with morton3D_invert(idx >> 0) = x, testbed_nerf.cu:518-520)
+__device__ __forceinline__ uint32_t morton3D(uint32_t x, uint32_t y, uint32_t z) {
+	return expand_bits(x) | (expand_bits(y) << 1) | (expand_bits(z) << 2);
+}
+__device__ __forceinline__ uint32_t morton3D_invert(uint32_t x) {
+	x = x & 0x49249249u;
+	x = (x | (x >> 2)) & 0xc30c30c3u;
+	x = (x | (x >> 4)) & 0x0f00f00fu;
+	x = (x | (x >> 8)) & 0xff0000ffu;
+	x = (x | (x >> 16)) & 0x0000ffffu;
+	return x;
+}
+
+// testbed_nerf.cu:433-457
+__device__ uint32_t cascaded_grid_idx_at(V3 pos, uint32_t mip) {
+	const float mip_scale = scalbnf(1.0f, -(int)mip);
+	pos = v3((pos.x - 0.5f) * mip_scale + 0.5f, (pos.y - 0.5f) * mip_scale + 0.5f, (pos.z - 0.5f) * mip_scale + 0.5f);
+	const int ix = (int)(pos.x * (float)GRIDSIZE), iy = (int)(pos.y * (float)GRIDSIZE), iz = (int)(pos.z * (float)GRIDSIZE);
+	if (ix < 0 || ix >= (int)GRIDSIZE || iy < 0 || iy >= (int)GRIDSIZE || iz < 0 || iz >= (int)GRIDSIZE) return 0xFFFFFFFFu;
+	return morton3D((uint32_t)ix, (uint32_t)iy, (uint32_t)iz);
+}
+__device__ bool density_grid_occupied_at(V3 pos, const uint8_t* bitfield, uint32_t mip) {
+	const uint32_t idx = cascaded_grid_idx_at(pos, mip);
+	if (idx == 0xFFFFFFFFu) return false;
+	return bitfield[idx / 8 + GRID_N_CELLS * mip / 8] & (1 << (idx % 8));
+}
+
+struct Aabb { V3 mn, mx; };
+__device__ __forceinline__ bool aabb_contains(const Aabb& b, V3 p) {
+	return p.x >= b.mn.x && p.x <= b.mx.x && p.y >= b.mn.y && p.y <= b.mx.y && p.z >= b.mn.z && p.z <= b.mx.z;
+}
+// bounding_box.cuh:163-216
+__device__ void aabb_ray_intersect(const Aabb& b, V3 pos, V3 dir, float* out_min, float* out_max) {
+	const float FMAX = 3.402823466e+38f;
+	float tmin = (b.mn.x - pos.x) / dir.x, tmax = (b.mx.x - pos.x) / dir.x;
+	if (tmin > tmax) { float t = tmin; tmin = tmax; tmax = t; }
+	float tymin = (b.mn.y - pos.y) / dir.y, tymax = (b.mx.y - pos.y) / dir.y;
+	if (tymin > tymax) { float t = tymin; tymin = tymax; tymax = t; }
+	if (tmin > tymax || tymin > tmax) { *out_min = FMAX; *out_max = FMAX; return; }
+	if (tymin > tmin) tmin = tymin;
+	if (tymax < tmax) tmax = tymax;
+	float tzmin = (b.mn.z - pos.z) / dir.z, tzmax = (b.mx.z - pos.z) / dir.z;
+	if (tzmin > tzmax) { float t = tzmin; tzmin = tzmax; tzmax = t; }
+	if (tmin > tzmax || tzmin > tmax) { *out_min = FMAX; *out_max = FMAX; return; }
+	if (tzmin > tmin) tmin = tzmin;
+	if (tzmax < tmax) tmax = tzmax;
+	*out_min = tmin; *out_max = tmax;
+}
+
+__device__ __forceinline__ float warp_dt(float dt) {  // :413-416
+	const float max_stepsize = MIN_CONE_STEPSIZE * (1 << (CASCADES - 1));
+	return (dt - MIN_CONE_STEPSIZE) / (max_stepsize - MIN_CONE_STEPSIZE);
+}
+__device__ __forceinline__ float unwarp_dt(float dt) {  // :418-421
+	const float max_stepsize = MIN_CONE_STEPSIZE * (1 << (CASCADES - 1));
+	return dt * (max_stepsize - MIN_CONE_STEPSIZE) + MIN_CONE_STEPSIZE;
+}
+
+// common_device.cuh:75-121
+__device__ __forceinline__ float srgb_to_linear(float s) { return s <= 0.04045f ? s / 12.92f : powf((s + 0.055f) / 1.055f, 2.4f); }
+__device__ __forceinline__ float linear_to_srgb(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * powf(l, 0.41666f) - 0.055f; }
+
+__device__ __forceinline__ float logistic(float x) { return 1.0f / (1.0f + expf(-x)); }  // tcnn::logistic
+// testbed_nerf.cu:317-378 (the reference's __expf is the fast intrinsic; ocml __expf here)
+__device__ float network_to_rgb(float v, uint32_t act) {
+	switch (act) {
+		case ACT_NONE: return v;
+		case ACT_RELU: return v > 0.0f ? v : 0.0f;
+		case ACT_LOGISTIC: return logistic(v);
+		case ACT_EXP: return __expf(fminf(fmaxf(v, -10.0f), 10.0f));
+	}
+	return 0.0f;
+}
+__device__ float network_to_rgb_derivative(float v, uint32_t act) {
+	switch (act) {
+		case ACT_NONE: return 1.0f;
+		case ACT_RELU: return v > 0.0f ? 1.0f : 0.0f;
+		case ACT_LOGISTIC: { const float d = logistic(v); return d * (1 - d); }
+		case ACT_EXP: return __expf(fminf(fmaxf(v, -10.0f), 10.0f));
+	}
+	return 0.0f;
+}
+__device__ float network_to_density(float v, uint32_t act) {
+	switch (act) {
+		case ACT_NONE: return v;
+		case ACT_RELU: return v > 0.0f ? v : 0.0f;
+		case ACT_LOGISTIC: return logistic(v);
+		case ACT_EXP: return __expf(v);
+	}
+	return 0.0f;
+}
+__device__ float network_to_density_derivative(float v, uint32_t act) {
+	switch (act) {
+		case ACT_NONE: return 1.0f;
+		case ACT_RELU: return v > 0.0f ? 1.0f : 0.0f;
+		case ACT_LOGISTIC: { const float d = logistic(v); return d * (1 - d); }
+		case ACT_EXP: return __expf(fminf(fmaxf(v, -15.0f), 15.0f));
+	}
+	return 0.0f;
+}
+
+// loss_and_gradient (testbed_nerf.cu:1340-1355) per channel
+__device__ void loss_channel(float target, float pred, uint32_t type, float* loss, float* grad) {
+	const float d = pred - target;
+	switch (type) {
+		case LOSS_RELL2: { const float den = pred * pred + 1e-2f; *loss = d * d / den; *grad = 2.0f * d / den; return; }
+		case LOSS_L1: *loss = fabsf(d); *grad = copysignf(1.0f, d); return;
+		case LOSS_MAPE: { const float den = fabsf(pred) + 1e-2f; *loss = fabsf(d) / den; *grad = copysignf(1.0f / den, d); return; }
+		case LOSS_SMAPE: { const float den = 0.5f * (fabsf(pred) + fabsf(target)) + 1e-2f; *loss = fabsf(d) / den; *grad = copysignf(1.0f / den, d); return; }
+		case LOSS_HUBER: {
+			const float alpha = 0.1f, ad = fabsf(d), sq = 0.5f / alpha * d * d;
+			*loss = (ad > alpha ? (ad - 0.5f * alpha) : sq) / 5.0f;
+			*grad = (ad > alpha ? (d > 0 ? 1.0f : -1.0f) : (d / alpha)) / 5.0f;
+			return;
+		}
+		case LOSS_LOGL1: { const float div = fabsf(d) + 1.0f; *loss = logf(div); *grad = copysignf(1.0f / div, d); return; }
+		default: *loss = d * d; *grad = 2.0f * d; return;
+	}
+}
+
+__device__ __forceinline__ Aabb cfg_aabb(const ngp_nerf_config& c) {
+	return Aabb{v3(c.aabb_min[0], c.aabb_min[1], c.aabb_min[2]), v3(c.aabb_max[0], c.aabb_max[1], c.aabb_max[2])};
+}
+
+// image_idx (testbed_nerf.cu:1317-1338), uniform branch
+__device__ __forceinline__ uint32_t image_idx(uint32_t base_idx, uint32_t n_rays, uint32_t n_images) {
+	return ((base_idx * n_images) / n_rays) % n_images;
+}
+
+// nerf_random_image_pos_training (:1292-1315) without error-map CDFs
+__device__ void random_image_pos(Rng& rng, uint32_t w, uint32_t h, bool snap, float* u, float* v) {
+	*u = pcg_float(rng);
+	*v = pcg_float(rng);
+	if (snap) {
+		int px = (int)(*u * (float)w), py = (int)(*v * (float)h);
+		px = px < 0 ? 0 : (px > (int)w - 1 ? (int)w - 1 : px);
+		py = py < 0 ? 0 : (py > (int)h - 1 ? (int)h - 1 : py);
+		*u = ((float)px + 0.5f) / (float)w;
+		*v = ((float)py + 0.5f) / (float)h;
+	}
+}
+
+__device__ __forceinline__ uint64_t pixel_index(float u, float v, uint32_t w, uint32_t h) {  // image_pos + pixel_idx
+	int px = (int)(u * (float)w), py = (int)(v * (float)h);
+	px = px < 0 ? 0 : (px > (int)w - 1 ? (int)w - 1 : px);
+	py = py < 0 ? 0 : (py > (int)h - 1 ? (int)h - 1 : py);
+	return (uint64_t)px + (uint64_t)py * w;
+}
+
+// Ray setup shared by the sampler's two passes (testbed_nerf.cu:1415-1493).
+struct RaySetup {
+	bool valid;
+	V3 o, d, dn, idir;
+	float startt, cone;
+};
+
+__device__ RaySetup setup_ray(const Camera* cams, const uint32_t* pixels, uint32_t n_images, const ngp_nerf_config& cfg,
+                              uint32_t ig, uint32_t n_rays_div, Rng rng) {
+	RaySetup r;
+	r.valid = false;
+	const uint32_t img = image_idx(ig, n_rays_div, n_images);
+	const Camera& cam = cams[img];
+	pcg_advance(rng, (uint64_t)ig * N_MAX_RANDOM_SAMPLES_PER_RAY);
+	float u, v;
+	random_image_pos(rng, cam.width, cam.height, cfg.snap_to_pixel_centers != 0, &u, &v);
+	const uint32_t raw = pixels[cam.pixel_offset + pixel_index(u, v, cam.width, cam.height)];
+	if (raw == 0x00FF00FFu) return r;  // masked (read_rgba returns -1)
+	(void)pcg_float(rng);              // motionblur_time
+	// uv_to_ray, pinhole (common_device.cuh:443-510)
+	const float dx = (u - cam.principal[0]) * (float)cam.width / cam.focal[0];
+	const float dy = (v - cam.principal[1]) * (float)cam.height / cam.focal[1];
+	const float dz = 1.0f;
+	const float* m = cam.m;
+	r.d = v3(m[0] * dx + m[3] * dy + m[6] * dz, m[1] * dx + m[4] * dy + m[7] * dz, m[2] * dx + m[5] * dy + m[8] * dz);
+	r.o = v3(m[9], m[10], m[11]);
+	const float inv = 1.0f / sqrtf(r.d.x * r.d.x + r.d.y * r.d.y + r.d.z * r.d.z);
+	r.dn = v3(r.d.x * inv, r.d.y * inv, r.d.z * inv);
+	float tmin, tmax;
+	aabb_ray_intersect(cfg_aabb(cfg), r.o, r.dn, &tmin, &tmax);
+	r.cone = cfg.cone_angle_constant;
+	tmin = fmaxf(tmin, 0.0f);
+	r.startt = advance_n_steps(tmin, r.cone, pcg_float(rng));
+	r.idir = v3(1.0f / r.dn.x, 1.0f / r.dn.y, 1.0f / r.dn.z);
+	r.valid = true;
+	return r;
+}
+
+// generate_training_samples_nerf pass 1: count the occupied steps of each ray.
+__global__ void __launch_bounds__(128) k_sample_count(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
+                                                      uint32_t n_images, const ngp_nerf_config cfg, SampleArgs a,
+                                                      uint32_t* __restrict__ nsteps) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= a.n_rays) return;
+	const RaySetup r = setup_ray(cams, pixels, n_images, cfg, i + a.ray_offset, a.n_rays_total_for_image_idx, a.rng);
+	uint32_t j = 0;
+	if (r.valid) {
+		const Aabb box = cfg_aabb(cfg);
+		float t = r.startt;
+		V3 pos;
+		while (aabb_contains(box, pos = v3(r.o.x + t * r.dn.x, r.o.y + t * r.dn.y, r.o.z + t * r.dn.z)) && j < STEPS) {
+			const float dt = calc_dt(t, r.cone);
+			const uint32_t mip = mip_from_dt(dt, pos, cfg.max_cascade);
+			if (density_grid_occupied_at(pos, a.bitfield, mip)) { ++j; t += dt; }
+			else t = advance_to_next_voxel(t, r.cone, pos, r.dn, r.idir, mip);
+		}
+	}
+	nsteps[i] = j;
+}
+
+__global__ void k_sample_keep(uint32_t n, const uint32_t* __restrict__ nsteps, const uint32_t* __restrict__ base,
+                              uint32_t max_samples, uint32_t* __restrict__ keep) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	keep[i] = (nsteps[i] > 0 && base[i] + nsteps[i] <= max_samples) ? 1u : 0u;
+}
+
+// pass 2: write the ray records and the NerfCoordinates of kept rays.
+__global__ void __launch_bounds__(128) k_sample_write(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
+                                                      uint32_t n_images, const ngp_nerf_config cfg, SampleArgs a,
+                                                      const uint32_t* __restrict__ nsteps, const uint32_t* __restrict__ base,
+                                                      const uint32_t* __restrict__ keep, const uint32_t* __restrict__ slot) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i == 0) {  // counters: rays kept, total steps of every ray that found samples
+		a.counters[0] = slot[a.n_rays - 1] + keep[a.n_rays - 1];
+		a.counters[1] = base[a.n_rays - 1] + nsteps[a.n_rays - 1];
+	}
+	if (i >= a.n_rays || !keep[i]) return;
+	const uint32_t ig = i + a.ray_offset;
+	const RaySetup r = setup_ray(cams, pixels, n_images, cfg, ig, a.n_rays_total_for_image_idx, a.rng);
+	const uint32_t s = slot[i], numsteps = nsteps[i], b = base[i];
+	a.ray_indices[s] = ig;
+	float* ro = a.rays + (size_t)s * 6;
+	ro[0] = r.o.x; ro[1] = r.o.y; ro[2] = r.o.z; ro[3] = r.d.x; ro[4] = r.d.y; ro[5] = r.d.z;
+	a.numsteps[2 * s] = numsteps;
+	a.numsteps[2 * s + 1] = b;
+	const Aabb box = cfg_aabb(cfg);
+	const V3 diag = v3(box.mx.x - box.mn.x, box.mx.y - box.mn.y, box.mx.z - box.mn.z);
+	const V3 wdir = v3((r.dn.x + 1.0f) * 0.5f, (r.dn.y + 1.0f) * 0.5f, (r.dn.z + 1.0f) * 0.5f);
+	float t = r.startt;
+	uint32_t j = 0;
+	V3 pos;
+	while (aabb_contains(box, pos = v3(r.o.x + t * r.dn.x, r.o.y + t * r.dn.y, r.o.z + t * r.dn.z)) && j < numsteps) {
+		const float dt = calc_dt(t, r.cone);
+		const uint32_t mip = mip_from_dt(dt, pos, cfg.max_cascade);
+		if (density_grid_occupied_at(pos, a.bitfield, mip)) {
+			float* c = a.coords + (size_t)(b + j) * 7;
+			c[0] = (pos.x - box.mn.x) / diag.x; c[1] = (pos.y - box.mn.y) / diag.y; c[2] = (pos.z - box.mn.z) / diag.z;
+			c[3] = warp_dt(dt);
+			c[4] = wdir.x; c[5] = wdir.y; c[6] = wdir.z;
+			++j;
+			t += dt;
+		} else {
+			t = advance_to_next_voxel(t, r.cone, pos, r.dn, r.idir, mip);
+		}
+	}
+}
+
+size_t scan_temp_bytes(uint32_t n) {
+	size_t bytes = 0;
+	NGP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n));
+	return bytes;
+}
+
+static void exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* tmp, size_t bytes, hipStream_t s) {
+	size_t need = bytes;
+	NGP_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, need, in, out, (int)n, s));
+}
+
+void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs& a, void* scan_tmp, size_t scan_bytes,
+                 uint32_t* tmp, float*, hipStream_t s) {
+	if (a.n_rays == 0) return;
+	uint32_t* nsteps = tmp;
+	uint32_t* base = tmp + a.n_rays;
+	uint32_t* keep = tmp + 2 * (size_t)a.n_rays;
+	uint32_t* slot = tmp + 3 * (size_t)a.n_rays;
+	const uint32_t blocks = div_round_up(a.n_rays, 128);
+	k_sample_count<<<blocks, 128, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps);
+	NGP_HIP(hipGetLastError());
+	exclusive_scan(nsteps, base, a.n_rays, scan_tmp, scan_bytes, s);
+	k_sample_keep<<<div_round_up(a.n_rays, 256), 256, 0, s>>>(a.n_rays, nsteps, base, a.max_samples, keep);
+	exclusive_scan(keep, slot, a.n_rays, scan_tmp, scan_bytes, s);
+	k_sample_write<<<blocks, 128, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, base, keep, slot);
+	NGP_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012), split at its atomicAdd into two passes
+// around a prefix scan. Error map / sharpness / envmap / exposure / depth supervision are off in the
+// reference's default training and not implemented.
+// ------------------------------------------------------------------------------------------------
+struct LossRay {  // pass-1 results kept for pass 2
+	float grad[3];
+	float rgb_ray[3];
+};
+
+__device__ __forceinline__ V3 unwarp_pos(const float* c, const Aabb& b) {
+	return v3(b.mn.x + c[0] * (b.mx.x - b.mn.x), b.mn.y + c[1] * (b.mx.y - b.mn.y), b.mn.z + c[2] * (b.mx.z - b.mn.z));
+}
+
+__global__ void __launch_bounds__(128) k_loss_pass1(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
+                                                    uint32_t n_images, const ngp_nerf_config cfg, LossArgs a,
+                                                    uint32_t* __restrict__ craw, LossRay* __restrict__ lr) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= a.n_rays) return;
+	if (i >= *a.ray_counter) { craw[i] = 0; return; }
+	const uint32_t numsteps = a.numsteps[2 * i], base = a.numsteps[2 * i + 1];
+	const f16* out = a.network_output + (size_t)base * 16;
+	const float* ci = a.coords_in + (size_t)base * 7;
+	const Aabb box = cfg_aabb(cfg);
+	float t = 1.f;
+	const float eps = 1e-4f;
+	float rr = 0.f, rg = 0.f, rb = 0.f;
+	uint32_t cn = 0;
+	for (; cn < numsteps; ++cn) {
+		if (t < eps) break;
+		const f16x4 o = *(const f16x4*)(out + (size_t)cn * 16);
+		const float dt = unwarp_dt(ci[(size_t)cn * 7 + 3]);
+		const float density = network_to_density((float)o[3], cfg.density_activation);
+		const float alpha = 1.f - __expf(-density * dt);
+		const float weight = alpha * t;
+		rr += weight * network_to_rgb((float)o[0], cfg.rgb_activation);
+		rg += weight * network_to_rgb((float)o[1], cfg.rgb_activation);
+		rb += weight * network_to_rgb((float)o[2], cfg.rgb_activation);
+		t *= (1.f - alpha);
+	}
+	// same random stream as the sampler for the same ray
+	const uint32_t ray_idx = a.ray_indices[i];
+	Rng rng = a.rng;
+	pcg_advance(rng, (uint64_t)ray_idx * N_MAX_RANDOM_SAMPLES_PER_RAY);
+	const uint32_t img = image_idx(ray_idx, a.n_rays_total_for_image_idx, n_images);
+	const Camera& cam = cams[img];
+	float u, v;
+	random_image_pos(rng, cam.width, cam.height, cfg.snap_to_pixel_centers != 0, &u, &v);
+	pcg_advance(rng, 1);  // motionblur_time
+	float bg[3] = {cfg.background_color[0], cfg.background_color[1], cfg.background_color[2]};
+	if (cfg.random_bg_color) { bg[0] = pcg_float(rng); bg[1] = pcg_float(rng); bg[2] = pcg_float(rng); }
+	for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear(bg[k]);
+	// read_rgba, Byte images (common_device.cuh:885-904)
+	const uint32_t raw = pixels[cam.pixel_offset + pixel_index(u, v, cam.width, cam.height)];
+	float tex[4];
+	if (raw == 0x00FF00FFu) { tex[0] = tex[1] = tex[2] = tex[3] = -1.0f; }
+	else {
+		const float alpha = (float)(raw >> 24) * (1.0f / 255.0f);
+		tex[0] = srgb_to_linear((float)(raw & 0xff) * (1.0f / 255.0f)) * alpha;
+		tex[1] = srgb_to_linear((float)((raw >> 8) & 0xff) * (1.0f / 255.0f)) * alpha;
+		tex[2] = srgb_to_linear((float)((raw >> 16) & 0xff) * (1.0f / 255.0f)) * alpha;
+		tex[3] = alpha;
+	}
+	const float exposure_scale = expf(0.6931471805599453f * 0.0f);
+	float target[3];
+	if (cfg.linear_colors || cfg.color_space_linear) {
+		for (int k = 0; k < 3; ++k) target[k] = exposure_scale * tex[k] + (1.0f - tex[3]) * bg[k];
+		if (!cfg.linear_colors)
+			for (int k = 0; k < 3; ++k) { target[k] = linear_to_srgb(target[k]); bg[k] = linear_to_srgb(bg[k]); }
+	} else {
+		for (int k = 0; k < 3; ++k) bg[k] = linear_to_srgb(bg[k]);
+		if (tex[3] > 0)
+			for (int k = 0; k < 3; ++k) target[k] = linear_to_srgb(exposure_scale * tex[k] / tex[3]) * tex[3] + (1.0f - tex[3]) * bg[k];
+		else
+			for (int k = 0; k < 3; ++k) target[k] = bg[k];
+	}
+	if (cn == numsteps) { rr += t * bg[0]; rg += t * bg[1]; rb += t * bg[2]; }
+	float l[3], g[3];
+	loss_channel(target[0], rr, cfg.loss_type, &l[0], &g[0]);
+	loss_channel(target[1], rg, cfg.loss_type, &l[1], &g[1]);
+	loss_channel(target[2], rb, cfg.loss_type, &l[2], &g[2]);
+	const float mean_loss = (l[0] + l[1] + l[2]) / 3.0f;
+	if (a.loss) a.loss[i] = mean_loss / (float)a.n_rays;
+	craw[i] = cn;
+	LossRay q;
+	q.grad[0] = g[0]; q.grad[1] = g[1]; q.grad[2] = g[2];
+	q.rgb_ray[0] = rr; q.rgb_ray[1] = rg; q.rgb_ray[2] = rb;
+	lr[i] = q;
+}
+
+__global__ void __launch_bounds__(128) k_loss_pass2(const ngp_nerf_config cfg, LossArgs a, const uint32_t* __restrict__ craw,
+                                                    const uint32_t* __restrict__ cbase, const LossRay* __restrict__ lr) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i == 0) *a.compacted_counter = cbase[a.n_rays - 1] + craw[a.n_rays - 1];
+	if (i >= a.n_rays || i >= *a.ray_counter) return;
+	const uint32_t base = a.numsteps[2 * i + 1];
+	const uint32_t compacted_base = cbase[i];
+	const uint32_t mx = a.max_samples_compacted;
+	const uint32_t cn = min(mx - min(mx, compacted_base), craw[i]);
+	a.numsteps[2 * i] = cn;
+	a.numsteps[2 * i + 1] = compacted_base;
+	if (cn == 0) return;
+	const LossRay q = lr[i];
+	const float loss_scale = a.loss_scale / (float)a.n_rays;
+	const float output_l2_reg = cfg.rgb_activation == ACT_EXP ? 1e-4f : 0.0f;
+	const float output_l1_reg_density = *a.mean_density < MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
+	const Aabb box = cfg_aabb(cfg);
+	const float* ray = a.rays + (size_t)i * 6;
+	const f16* out = a.network_output + (size_t)base * 16;
+	const float* ci = a.coords_in + (size_t)base * 7;
+	float* co = a.coords_out + (size_t)compacted_base * 7;
+	f16* dl = a.dloss_doutput + (size_t)compacted_base * 16;
+	float r2[3] = {0.f, 0.f, 0.f};
+	float t = 1.0f;
+	for (uint32_t j = 0; j < cn; ++j) {
+		const float* c = ci + (size_t)j * 7;
+#pragma unroll
+		for (int k = 0; k < 7; ++k) co[(size_t)j * 7 + k] = c[k];
+		const V3 pos = unwarp_pos(c, box);
+		const float ddx = pos.x - ray[0], ddy = pos.y - ray[1], ddz = pos.z - ray[2];
+		const float depth = sqrtf(ddx * ddx + ddy * ddy + ddz * ddz);
+		const float dt = unwarp_dt(c[3]);
+		const f16x4 o = *(const f16x4*)(out + (size_t)j * 16);
+		float rgb[3];
+		for (int k = 0; k < 3; ++k) rgb[k] = network_to_rgb((float)o[k], cfg.rgb_activation);
+		const float density = network_to_density((float)o[3], cfg.density_activation);
+		const float alpha = 1.f - __expf(-density * dt);
+		const float weight = alpha * t;
+		for (int k = 0; k < 3; ++k) r2[k] += weight * rgb[k];
+		t *= (1.0f - alpha);
+		float suffix[3];
+		for (int k = 0; k < 3; ++k) suffix[k] = q.rgb_ray[k] - r2[k];
+		f16x4 g;
+		for (int k = 0; k < 3; ++k) {
+			const float dloss_by_drgb = weight * q.grad[k];
+			g[k] = (f16)(loss_scale * (dloss_by_drgb * network_to_rgb_derivative((float)o[k], cfg.rgb_activation) +
+			                           fmaxf(0.0f, output_l2_reg * (float)o[k])));
+		}
+		const float density_derivative = network_to_density_derivative((float)o[3], cfg.density_activation);
+		const float dotv = q.grad[0] * (t * rgb[0] - suffix[0]) + q.grad[1] * (t * rgb[1] - suffix[1]) +
+		                   q.grad[2] * (t * rgb[2] - suffix[2]);
+		const float dloss_by_dmlp = density_derivative * (dt * (dotv + 0.0f));
+		const float o3 = (float)o[3];
+		g[3] = (f16)(loss_scale * dloss_by_dmlp + (o3 < 0.0f ? -output_l1_reg_density : 0.0f) +
+		             (o3 > -10.0f && depth < cfg.near_distance ? 1e-4f : 0.0f));
+		*(f16x4*)(dl + (size_t)j * 16) = g;
+	}
+}
+
+void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs& a, void* scan_tmp, size_t scan_bytes,
+                  uint32_t* tmp, float* tmpf, hipStream_t s) {
+	if (a.n_rays == 0) return;
+	uint32_t* craw = tmp;
+	uint32_t* cbase = tmp + a.n_rays;
+	LossRay* lr = (LossRay*)tmpf;
+	const uint32_t blocks = div_round_up(a.n_rays, 128);
+	k_loss_pass1<<<blocks, 128, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, craw, lr);
+	NGP_HIP(hipGetLastError());
+	exclusive_scan(craw, cbase, a.n_rays, scan_tmp, scan_bytes, s);
+	k_loss_pass2<<<blocks, 128, 0, s>>>(cfg, a, craw, cbase, lr);
+	NGP_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// tcnn fill_rollover / fill_rollover_and_rescale
+// ------------------------------------------------------------------------------------------------
+__global__ void k_rollover_f16(uint32_t n_elements, uint32_t stride, const uint32_t* n_input_ptr, f16* data, bool rescale) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t n_in = *n_input_ptr;
+	if (i < n_in * stride || i >= n_elements * stride || n_in == 0) return;
+	f16 r = data[i % (n_in * stride)];
+	if (rescale) r = (f16)((float)r * n_in / n_elements);
+	data[i] = r;
+}
+__global__ void k_rollover_f32(uint32_t n_elements, uint32_t stride, const uint32_t* n_input_ptr, float* data) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t n_in = *n_input_ptr;
+	if (i < n_in * stride || i >= n_elements * stride || n_in == 0) return;
+	data[i] = data[i % (n_in * stride)];
+}
+void fill_rollover_f16(uint32_t n_elements, uint32_t stride, const uint32_t* n_input, f16* data, bool rescale, hipStream_t s) {
+	k_rollover_f16<<<div_round_up((uint64_t)n_elements * stride, 256), 256, 0, s>>>(n_elements, stride, n_input, data, rescale);
+	NGP_HIP(hipGetLastError());
+}
+void fill_rollover_f32(uint32_t n_elements, uint32_t stride, const uint32_t* n_input, float* data, hipStream_t s) {
+	k_rollover_f32<<<div_round_up((uint64_t)n_elements * stride, 256), 256, 0, s>>>(n_elements, stride, n_input, data);
+	NGP_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// occupancy grid
+// ------------------------------------------------------------------------------------------------
+// generate_grid_samples_nerf_nonuniform (testbed_nerf.cu:635-676)
+__global__ void k_grid_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_config cfg, const float* __restrict__ grid_in,
+                               uint32_t n_cascades, float thresh, float* __restrict__ out, uint32_t* __restrict__ indices) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	pcg_advance(rng, (uint64_t)i * 4);
+	const uint32_t level = (uint32_t)(pcg_float(rng) * n_cascades) % n_cascades;
+	uint32_t idx = 0;
+	for (uint32_t j = 0; j < 10; ++j) {
+		idx = ((i + step * n) * 56924617u + j * 19349663u + 96925573u) % GRID_N_CELLS;
+		idx += level * GRID_N_CELLS;
+		if (grid_in[idx] > thresh) break;
+	}
+	const uint32_t pos_idx = idx % GRID_N_CELLS;
+	const uint32_t x = morton3D_invert(pos_idx >> 0), y = morton3D_invert(pos_idx >> 1), z = morton3D_invert(pos_idx >> 2);
+	const float r0 = pcg_float(rng), r1 = pcg_float(rng), r2 = pcg_float(rng);
+	const float sc = scalbnf(1.0f, (int)level);
+	const float px = (((float)x + r0) / (float)GRIDSIZE - 0.5f) * sc + 0.5f;
+	const float py = (((float)y + r1) / (float)GRIDSIZE - 0.5f) * sc + 0.5f;
+	const float pz = (((float)z + r2) / (float)GRIDSIZE - 0.5f) * sc + 0.5f;
+	out[(size_t)i * 3 + 0] = (px - cfg.aabb_min[0]) / (cfg.aabb_max[0] - cfg.aabb_min[0]);
+	out[(size_t)i * 3 + 1] = (py - cfg.aabb_min[1]) / (cfg.aabb_max[1] - cfg.aabb_min[1]);
+	out[(size_t)i * 3 + 2] = (pz - cfg.aabb_min[2]) / (cfg.aabb_max[2] - cfg.aabb_min[2]);
+	indices[i] = idx;
+}
+
+// splat_grid_samples_nerf_max_nearest_neighbor (:678-702); density_rm = density MLP output row 0 (RM)
+__global__ void k_grid_splat(uint32_t n, const uint32_t* __restrict__ indices, const f16* __restrict__ density, uint32_t act,
+                             float* __restrict__ grid_out) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const float mlp = network_to_density((float)density[i], act);
+	const float thickness = mlp * scalbnf(MIN_CONE_STEPSIZE, 0);
+	atomicMax((uint32_t*)&grid_out[indices[i]], __float_as_uint(thickness));
+}
+
+// ema_grid_samples_nerf (:731-754): max-filter
+__global__ void k_grid_ema(uint32_t n, float decay, float* __restrict__ grid, const float* __restrict__ tmp) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const float prev = grid[i];
+	grid[i] = prev < 0.f ? prev : fmaxf(prev * decay, tmp[i]);
+}
+
+// reduce_sum(max(v,0)/N) over cascade 0 (:3544-3551), fixed order: 512 blocks x 256 threads, then one block.
+__global__ void __launch_bounds__(256) k_grid_mean_partial(const float* __restrict__ grid, float* __restrict__ partial) {
+	__shared__ float s[256];
+	const uint32_t per_block = GRID_N_CELLS / 512;
+	const uint32_t base = blockIdx.x * per_block;
+	float acc = 0.f;
+	for (uint32_t k = threadIdx.x; k < per_block; k += 256) acc += fmaxf(grid[base + k], 0.f) / (float)GRID_N_CELLS;
+	s[threadIdx.x] = acc;
+	__syncthreads();
+	for (uint32_t off = 128; off > 0; off >>= 1) {
+		if (threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off];
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) partial[blockIdx.x] = s[0];
+}
+__global__ void __launch_bounds__(512) k_grid_mean_final(const float* __restrict__ partial, float* __restrict__ mean) {
+	__shared__ float s[512];
+	s[threadIdx.x] = partial[threadIdx.x];
+	__syncthreads();
+	for (uint32_t off = 256; off > 0; off >>= 1) {
+		if (threadIdx.x < off) s[threadIdx.x] += s[threadIdx.x + off];
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) *mean = s[0];
+}
+
+// grid_to_bitfield (:762-786)
+__global__ void k_grid_to_bitfield(uint32_t n_elements, uint32_t n_nonzero, const float* __restrict__ grid,
+                                   uint8_t* __restrict__ bitfield, const float* __restrict__ mean) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n_elements) return;
+	if (i >= n_nonzero) { bitfield[i] = 0; return; }
+	const float thresh = fminf(MIN_OPTICAL_THICKNESS, *mean);
+	uint8_t bits = 0;
+#pragma unroll
+	for (uint8_t j = 0; j < 8; ++j) bits |= grid[i * 8 + j] > thresh ? ((uint8_t)1 << j) : 0;
+	bitfield[i] = bits;
+}
+
+// bitfield_max_pool (:788-809)
+__global__ void k_bitfield_max_pool(uint32_t n, const uint8_t* __restrict__ prev, uint8_t* __restrict__ next) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	uint8_t bits = 0;
+#pragma unroll
+	for (uint8_t j = 0; j < 8; ++j) bits |= prev[i * 8 + j] > 0 ? ((uint8_t)1 << j) : 0;
+	const uint32_t x = morton3D_invert(i >> 0) + GRIDSIZE / 8;
+	const uint32_t y = morton3D_invert(i >> 1) + GRIDSIZE / 8;
+	const uint32_t z = morton3D_invert(i >> 2) + GRIDSIZE / 8;
+	next[morton3D(x, y, z)] |= bits;
+}
+
+void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_config& cfg, const float* grid_in,
+                           uint32_t n_cascades, float thresh, float* positions, uint32_t* indices, hipStream_t s) {
+	if (n == 0) return;
+	k_grid_samples<<<div_round_up(n, 128), 128, 0, s>>>(n, rng, step, cfg, grid_in, n_cascades, thresh, positions, indices);
+	NGP_HIP(hipGetLastError());
+}
+void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t act, float* grid_tmp, hipStream_t s) {
+	if (n == 0) return;
+	k_grid_splat<<<div_round_up(n, 128), 128, 0, s>>>(n, indices, density_rm, act, grid_tmp);
+	NGP_HIP(hipGetLastError());
+}
+void grid_ema(uint32_t n, float decay, float* grid, const float* tmp, hipStream_t s) {
+	k_grid_ema<<<div_round_up(n, 256), 256, 0, s>>>(n, decay, grid, tmp);
+	NGP_HIP(hipGetLastError());
+}
+void grid_mean_bitfield(const float* grid, uint32_t max_cascade, float* mean_out, uint8_t* bitfield, hipStream_t s) {
+	float* partial = mean_out + 1;  // caller provides [1 + 512] floats
+	k_grid_mean_partial<<<512, 256, 0, s>>>(grid, partial);
+	k_grid_mean_final<<<1, 512, 0, s>>>(partial, mean_out);
+	const uint32_t n_bytes = GRID_N_CELLS / 8 * CASCADES;
+	k_grid_to_bitfield<<<div_round_up(n_bytes, 256), 256, 0, s>>>(n_bytes, GRID_N_CELLS / 8 * (max_cascade + 1), grid, bitfield, mean_out);
+	for (uint32_t level = 1; level < CASCADES; ++level) {
+		const uint32_t n = GRID_N_CELLS / 64;
+		k_bitfield_max_pool<<<div_round_up(n, 256), 256, 0, s>>>(n, bitfield + (size_t)(level - 1) * GRID_N_CELLS / 8,
+		                                                          bitfield + (size_t)level * GRID_N_CELLS / 8);
+	}
+	NGP_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------------
+// host: effective camera matrix (glm quat_cast -> slerp(t=0, start == end) -> normalize -> mat3_cast)
+// ------------------------------------------------------------------------------------------------
+void effective_camera_matrix(const float xf[12], float out[12]) {
+	// glm column-major m[c][r] = xf[3c + r]
+	auto M = [&](int c, int r) { return xf[3 * c + r]; };
+	const float fx = M(0, 0) - M(1, 1) - M(2, 2), fy = M(1, 1) - M(0, 0) - M(2, 2), fz = M(2, 2) - M(0, 0) - M(1, 1);
+	const float fw = M(0, 0) + M(1, 1) + M(2, 2);
+	int bi = 0;
+	float big = fw;
+	if (fx > big) { big = fx; bi = 1; }
+	if (fy > big) { big = fy; bi = 2; }
+	if (fz > big) { big = fz; bi = 3; }
+	const float bv = sqrtf(big + 1.0f) * 0.5f, mult = 0.25f / bv;
+	float w, x, y, z;
+	switch (bi) {
+		case 0: w = bv; x = (M(1, 2) - M(2, 1)) * mult; y = (M(2, 0) - M(0, 2)) * mult; z = (M(0, 1) - M(1, 0)) * mult; break;
+		case 1: w = (M(1, 2) - M(2, 1)) * mult; x = bv; y = (M(0, 1) + M(1, 0)) * mult; z = (M(2, 0) + M(0, 2)) * mult; break;
+		case 2: w = (M(2, 0) - M(0, 2)) * mult; x = (M(0, 1) + M(1, 0)) * mult; y = bv; z = (M(1, 2) + M(2, 1)) * mult; break;
+		default: w = (M(0, 1) - M(1, 0)) * mult; x = (M(2, 0) + M(0, 2)) * mult; y = (M(1, 2) + M(2, 1)) * mult; z = bv; break;
+	}
+	// slerp(q, q, 0) takes the linear branch: q * 1 + q * 0 = q; then normalize
+	const float len = sqrtf(w * w + x * x + y * y + z * z);
+	if (len <= 0.f) { w = 1.f; x = y = z = 0.f; }
+	else { const float inv = 1.0f / len; w *= inv; x *= inv; y *= inv; z *= inv; }
+	const float qxx = x * x, qyy = y * y, qzz = z * z, qxz = x * z, qxy = x * y, qyz = y * z, qwx = w * x, qwy = w * y, qwz = w * z;
+	out[0] = 1.f - 2.f * (qyy + qzz); out[1] = 2.f * (qxy + qwz); out[2] = 2.f * (qxz - qwy);
+	out[3] = 2.f * (qxy - qwz); out[4] = 1.f - 2.f * (qxx + qzz); out[5] = 2.f * (qyz + qwx);
+	out[6] = 2.f * (qxz + qwy); out[7] = 2.f * (qyz - qwx); out[8] = 1.f - 2.f * (qxx + qyy);
+	out[9] = xf[9]; out[10] = xf[10]; out[11] = xf[11];
+}
+
+Dataset::~Dataset() {
+	if (d_cams) (void)hipFree(d_cams);
+	if (d_pixels) (void)hipFree(d_pixels);
+}
+
+}  // namespace nerf
+}  // namespace ngp
