@@ -30,6 +30,33 @@ class ParamLayout(C.Structure):
     ]
 
 
+class NerfImage(C.Structure):
+    """ngp_nerf_image: TrainingImageMetadata + camera-to-world mat4x3 (column-major)."""
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("focal_length", C.c_float * 2),
+                ("principal_point", C.c_float * 2), ("xform", C.c_float * 12)]
+
+
+class NerfConfig(C.Structure):
+    """ngp_nerf_config: Testbed NeRF training knobs (testbed.h:716-785)."""
+    _fields_ = [
+        ("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3), ("cone_angle_constant", C.c_float),
+        ("max_cascade", C.c_uint32), ("snap_to_pixel_centers", C.c_uint32), ("random_bg_color", C.c_uint32),
+        ("linear_colors", C.c_uint32), ("color_space_linear", C.c_uint32), ("background_color", C.c_float * 3),
+        ("rgb_activation", C.c_uint32), ("density_activation", C.c_uint32), ("loss_type", C.c_uint32),
+        ("near_distance", C.c_float), ("target_batch_size", C.c_uint32),
+    ]
+
+
+class Rng(C.Structure):
+    """ngp_rng: tcnn::pcg32 state, passed by value."""
+    _fields_ = [("state", C.c_uint64), ("inc", C.c_uint64)]
+
+
+class NerfStats(C.Structure):
+    _fields_ = [("step", C.c_uint32), ("rays_per_batch", C.c_uint32), ("measured_batch_size", C.c_uint32),
+                ("measured_batch_size_before_compaction", C.c_uint32), ("loss", C.c_float)]
+
+
 P = C.c_void_p
 u32, u64, f32, i32, sz = C.c_uint32, C.c_uint64, C.c_float, C.c_int, C.c_size_t
 
@@ -80,6 +107,22 @@ SIGNATURES = {
     "ngp_trainer_set_params_full_precision": (i32, [P, P, u64]),
     "ngp_trainer_serialize": (i32, [P, P, C.POINTER(u64)]),
     "ngp_trainer_deserialize": (i32, [P, P, u64]),
+    "ngp_nerf_default_config": (i32, [f32, C.POINTER(NerfConfig)]),
+    "ngp_nerf_dataset_create": (i32, [u32, C.POINTER(NerfImage), C.POINTER(P), C.POINTER(P)]),
+    "ngp_nerf_dataset_destroy": (None, [P]),
+    "ngp_nerf_generate_training_samples": (i32, [P, C.POINTER(NerfConfig), P, u32, u32, u32, Rng, u32, P, P, P, P, P,
+                                                 P]),
+    "ngp_nerf_compute_loss": (i32, [P, C.POINTER(NerfConfig), P, u32, u32, Rng, u32, P, P, P, P, P, P, P, P, P, P, P,
+                                    f32]),
+    "ngp_nerf_fill_rollover": (i32, [P, u32, u32, P, P, i32, i32]),
+    "ngp_nerf_grid_generate_samples": (i32, [P, C.POINTER(NerfConfig), u32, Rng, u32, P, u32, f32, P, P]),
+    "ngp_nerf_grid_splat_max": (i32, [P, u32, P, P, u32, P]),
+    "ngp_nerf_grid_ema": (i32, [P, u32, f32, P, P]),
+    "ngp_nerf_grid_mean_and_bitfield": (i32, [P, P, u32, P, P]),
+    "ngp_nerf_trainer_create": (i32, [P, P, P, C.POINTER(NerfConfig), u64, C.POINTER(P)]),
+    "ngp_nerf_trainer_destroy": (None, [P]),
+    "ngp_nerf_train_step": (i32, [P, P, i32, C.POINTER(NerfStats)]),
+    "ngp_nerf_trainer_buffers": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
 }
 
 

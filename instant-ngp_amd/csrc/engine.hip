@@ -216,8 +216,10 @@ struct ngp_model {
 	// Hash-grid backward: windowed (spatial bins + LDS) for the coarse levels when it pays, direct
 	// packed-f16 atomics for the rest. The windowed path needs all levels active (max_level >= 1).
 	void scatter_grid_grad(hipStream_t s, GridBwdArgs b) {
-		const bool can_win = grid_backward_mode != 1 && b.dy_layout == AoS && !b.max_level_per_sample &&
-		                     b.max_level >= 1.0f && grid.n_features >= 2 && b.n >= 4096;
+		// auto: windowed only where it measured faster (F=2: C2' 774 vs 911 us; F=4: C2 257 vs 240 us)
+		const bool want_win = grid_backward_mode == 2 || (grid_backward_mode == 0 && grid.n_features == 2);
+		const bool can_win = want_win && b.dy_layout == AoS && !b.max_level_per_sample && b.max_level >= 1.0f &&
+		                     grid.n_features >= 2 && b.n >= 4096;
 		if (can_win) {
 			if (win_plan_n != b.n) { win_plan = make_win_plan(grid, b.n, 120 * 1024); win_plan_n = b.n; }
 			if (win_plan.n_win > 0) {
@@ -273,6 +275,10 @@ static thread_local std::string g_last_error;
 	} while (0)
 
 static hipStream_t S(void* s) { return (hipStream_t)s; }
+
+namespace ngp {
+void set_last_error(const char* msg) { g_last_error = msg; }
+}  // namespace ngp
 
 extern "C" {
 

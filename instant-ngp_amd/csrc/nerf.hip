@@ -396,6 +396,7 @@ void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs
 struct LossRay {  // pass-1 results kept for pass 2
 	float grad[3];
 	float rgb_ray[3];
+	float mean_loss;
 };
 
 __device__ __forceinline__ V3 unwarp_pos(const float* c, const Aabb& b) {
@@ -411,7 +412,6 @@ __global__ void __launch_bounds__(128) k_loss_pass1(const Camera* __restrict__ c
 	const uint32_t numsteps = a.numsteps[2 * i], base = a.numsteps[2 * i + 1];
 	const f16* out = a.network_output + (size_t)base * 16;
 	const float* ci = a.coords_in + (size_t)base * 7;
-	const Aabb box = cfg_aabb(cfg);
 	float t = 1.f;
 	const float eps = 1e-4f;
 	float rr = 0.f, rg = 0.f, rb = 0.f;
@@ -469,10 +469,9 @@ __global__ void __launch_bounds__(128) k_loss_pass1(const Camera* __restrict__ c
 	loss_channel(target[0], rr, cfg.loss_type, &l[0], &g[0]);
 	loss_channel(target[1], rg, cfg.loss_type, &l[1], &g[1]);
 	loss_channel(target[2], rb, cfg.loss_type, &l[2], &g[2]);
-	const float mean_loss = (l[0] + l[1] + l[2]) / 3.0f;
-	if (a.loss) a.loss[i] = mean_loss / (float)a.n_rays;
 	craw[i] = cn;
 	LossRay q;
+	q.mean_loss = (l[0] + l[1] + l[2]) / 3.0f;
 	q.grad[0] = g[0]; q.grad[1] = g[1]; q.grad[2] = g[2];
 	q.rgb_ray[0] = rr; q.rgb_ray[1] = rg; q.rgb_ray[2] = rb;
 	lr[i] = q;
@@ -491,6 +490,7 @@ __global__ void __launch_bounds__(128) k_loss_pass2(const ngp_nerf_config cfg, L
 	a.numsteps[2 * i + 1] = compacted_base;
 	if (cn == 0) return;
 	const LossRay q = lr[i];
+	if (a.loss) a.loss[i] = q.mean_loss / (float)a.n_rays;  // written after the compaction early-out (:1836-1866)
 	const float loss_scale = a.loss_scale / (float)a.n_rays;
 	const float output_l2_reg = cfg.rgb_activation == ACT_EXP ? 1e-4f : 0.0f;
 	const float output_l1_reg_density = *a.mean_density < MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;

@@ -1,0 +1,418 @@
+// nerf_trainer.hip — C-ABI for the NeRF kernels and the Testbed-level NeRF training step.
+//
+// ngp_nerf_train_step mirrors Testbed::train for NeRF (src/testbed.cu:4285-4370): training_prep_nerf
+// (occupancy-grid update every clamp(step/16, 1, 16) steps, testbed_nerf.cu:4137-4152) then
+// train_nerf (testbed_nerf.cu:3611-3862): sample -> inference over every sample -> loss/compaction
+// -> rollover -> forward/backward on the compacted batch -> optimizer step -> counters (host sync) ->
+// rays_per_batch adaptation.
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "nerf.h"
+
+using namespace ngp;
+using namespace ngp::nerf;
+
+struct ngp_nerf_dataset {
+	Dataset ds;
+};
+
+namespace {
+
+struct HostPcg {  // tcnn::pcg32 (host) for the Testbed's m_rng / density_grid_rng
+	uint64_t state, inc;
+	explicit HostPcg(uint64_t initstate, uint64_t initseq = 1u) {
+		state = 0u; inc = (initseq << 1u) | 1u; next_uint(); state += initstate; next_uint();
+	}
+	uint32_t next_uint() {
+		const uint64_t old = state;
+		state = old * 0x5851f42d4c957f2dULL + inc;
+		const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u), rot = (uint32_t)(old >> 59u);
+		return (xs >> rot) | (xs << ((~rot + 1u) & 31));
+	}
+	void advance(uint64_t delta = (1ull << 32)) {
+		uint64_t cm = 0x5851f42d4c957f2dULL, cp = inc, am = 1u, ap = 0u;
+		while (delta > 0) {
+			if (delta & 1) { am *= cm; ap = ap * cm + cp; }
+			cp = (cm + 1) * cp; cm *= cm; delta /= 2;
+		}
+		state = am * state + ap;
+	}
+	Rng dev() const { return Rng{state, inc}; }
+};
+
+struct Buf {
+	void* p = nullptr;
+	size_t n = 0;
+	template <typename T> T* get(size_t count) {
+		const size_t need = count * sizeof(T);
+		if (need > n) {
+			if (p) NGP_HIP(hipFree(p));
+			NGP_HIP(hipMalloc(&p, need));
+			n = need;
+		}
+		return (T*)p;
+	}
+	~Buf() { if (p) (void)hipFree(p); }
+};
+
+}  // namespace
+
+// external engine entry points used by the orchestrator
+extern "C" int ngp_inference(ngp_model*, void*, uint32_t, const float*, uint32_t, void*, uint32_t, uint32_t, int);
+extern "C" int ngp_density(ngp_model*, void*, uint32_t, const float*, uint32_t, void*, uint32_t, uint32_t, int);
+extern "C" int ngp_forward_backward(ngp_model*, void*, uint32_t, const float*, uint32_t, void*, uint32_t, const void*, uint32_t, int);
+extern "C" int ngp_trainer_optimizer_step(ngp_trainer*, void*, float);
+extern "C" const char* ngp_last_error(void);
+
+struct ngp_nerf_trainer {
+	ngp_model* model;
+	ngp_trainer* trainer;
+	const ngp_nerf_dataset* data;
+	ngp_nerf_config cfg;
+	HostPcg rng{1337}, grid_rng{1};
+	uint32_t training_step = 0, ema_step = 0;
+	uint32_t rays_per_batch = 1u << 12;  // testbed.h:440
+	uint32_t n_rays_total = 0;
+	uint32_t measured_batch_size = 0, measured_before_compaction = 0;
+	// occupancy grid
+	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens;
+	// training workspaces
+	Buf ray_indices, rays, numsteps, coords, mlp_out, dloss, coords_c, loss, counters, scan_tmp, tmp_u32, tmp_f32;
+};
+
+static hipStream_t S(void* s) { return (hipStream_t)s; }
+
+#define NERF_TRY(...)                                  \
+	try {                                              \
+		__VA_ARGS__;                                   \
+		return NGP_OK;                                 \
+	} catch (const std::exception& e) {                \
+		nerf_set_error(e.what());                      \
+		return NGP_ERROR;                              \
+	}
+
+// share the engine's thread-local error string through a tiny hook in engine.hip
+namespace ngp { void set_last_error(const char* msg); }
+static void nerf_set_error(const char* m) { ngp::set_last_error(m); }
+
+// mark_untrained_density_grid (testbed_nerf.cu:503-592) for perspective cameras
+__global__ void k_mark_untrained(uint32_t n_elements, float* __restrict__ grid, uint32_t n_images, const Camera* __restrict__ cams,
+                                 const float* __restrict__ raw_xforms, bool clear_visible) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n_elements) return;
+	if (grid[i] == -1.0f) return;
+	const uint32_t level = i / GRID_N_CELLS, pos_idx = i % GRID_N_CELLS;
+	auto inv = [](uint32_t x) {
+		x = x & 0x49249249u; x = (x | (x >> 2)) & 0xc30c30c3u; x = (x | (x >> 4)) & 0x0f00f00fu;
+		x = (x | (x >> 8)) & 0xff0000ffu; x = (x | (x >> 16)) & 0x0000ffffu; return x;
+	};
+	const uint32_t x = inv(pos_idx >> 0), y = inv(pos_idx >> 1), z = inv(pos_idx >> 2);
+	const float vs = scalbnf(1.0f / GRIDSIZE, (int)level), sc = scalbnf(1.0f, (int)level);
+	const float px = ((float)x / (float)GRIDSIZE - 0.5f) * sc + 0.5f;
+	const float py = ((float)y / (float)GRIDSIZE - 0.5f) * sc + 0.5f;
+	const float pz = ((float)z / (float)GRIDSIZE - 0.5f) * sc + 0.5f;
+	uint32_t count = 0;
+	for (uint32_t j = 0; j < n_images && count < 1; ++j) {
+		const float* m = raw_xforms + 12 * j;  // training_xforms[j].start
+		const Camera& cam = cams[j];
+		// inverse(mat3(m)) via the adjugate (glm::inverse)
+		const float a00 = m[0], a01 = m[1], a02 = m[2], a10 = m[3], a11 = m[4], a12 = m[5], a20 = m[6], a21 = m[7], a22 = m[8];
+		const float det = a00 * (a11 * a22 - a21 * a12) - a10 * (a01 * a22 - a21 * a02) + a20 * (a01 * a12 - a11 * a02);
+		const float id = 1.0f / det;
+		float I[9];
+		I[0] = (a11 * a22 - a21 * a12) * id; I[3] = -(a10 * a22 - a20 * a12) * id; I[6] = (a10 * a21 - a20 * a11) * id;
+		I[1] = -(a01 * a22 - a21 * a02) * id; I[4] = (a00 * a22 - a20 * a02) * id; I[7] = -(a00 * a21 - a20 * a01) * id;
+		I[2] = (a01 * a12 - a11 * a02) * id; I[5] = -(a00 * a12 - a10 * a02) * id; I[8] = (a00 * a11 - a10 * a01) * id;
+		for (uint32_t k = 0; k < 8; ++k) {
+			const float cx = px + ((k & 1) ? vs : 0.f), cy = py + ((k & 2) ? vs : 0.f), cz = pz + ((k & 4) ? vs : 0.f);
+			float dx = cx - m[9], dy = cy - m[10], dz = cz - m[11];
+			const float il = 1.0f / sqrtf(dx * dx + dy * dy + dz * dz);
+			const float nx = dx * il, ny = dy * il, nz = dz * il;
+			if (nx * m[6] + ny * m[7] + nz * m[8] < 1e-4f) continue;
+			// pos_to_uv (common_device.cuh:547-585), perspective
+			float ex = I[0] * dx + I[3] * dy + I[6] * dz, ey = I[1] * dx + I[4] * dy + I[7] * dz, ez = I[2] * dx + I[5] * dy + I[8] * dz;
+			ex /= ez; ey /= ez;
+			const float u = ex * cam.focal[0] / (float)cam.width + cam.principal[0];
+			const float v = ey * cam.focal[1] / (float)cam.height + cam.principal[1];
+			// uv_to_ray with the raw xform, compare directions
+			const float rx = (u - cam.principal[0]) * (float)cam.width / cam.focal[0];
+			const float ry = (v - cam.principal[1]) * (float)cam.height / cam.focal[1];
+			const float ddx = m[0] * rx + m[3] * ry + m[6], ddy = m[1] * rx + m[4] * ry + m[7], ddz = m[2] * rx + m[5] * ry + m[8];
+			const float rl = 1.0f / sqrtf(ddx * ddx + ddy * ddy + ddz * ddz);
+			const float qx = ddx * rl - nx, qy = ddy * rl - ny, qz = ddz * rl - nz;
+			if (u > 0.0f && v > 0.0f && u < 1.0f && v < 1.0f && sqrtf(qx * qx + qy * qy + qz * qz) < 1e-3f) { ++count; break; }
+		}
+	}
+	if (clear_visible || (grid[i] < 0) != (count < 1)) grid[i] = count >= 1 ? 1.f : -1.f;
+	else grid[i] = 1.0f;
+}
+
+extern "C" {
+
+int ngp_nerf_default_config(float aabb_scale, ngp_nerf_config* o) {
+	if (!o || !(aabb_scale >= 1.0f)) return NGP_INVALID;
+	memset(o, 0, sizeof(*o));
+	const float inflate = 0.5f * std::min((float)(1 << (CASCADES - 1)), aabb_scale);  // testbed_nerf.cu:3093-3094
+	for (int k = 0; k < 3; ++k) { o->aabb_min[k] = 0.5f - inflate; o->aabb_max[k] = 0.5f + inflate; }
+	uint32_t mc = 0;
+	while ((float)(1u << mc) < aabb_scale) ++mc;  // :3102-3105
+	o->max_cascade = mc;
+	o->cone_angle_constant = aabb_scale <= 1.0f ? 0.0f : 1.0f / 256.0f;  // :3109
+	o->snap_to_pixel_centers = 1;
+	o->random_bg_color = 1;
+	o->linear_colors = 0;
+	o->color_space_linear = 1;
+	o->rgb_activation = ACT_EXP;
+	o->density_activation = ACT_EXP;
+	o->loss_type = LOSS_HUBER;  // configs/nerf/base.json "loss": Huber
+	o->near_distance = 0.1f;
+	o->target_batch_size = 1u << 18;
+	return NGP_OK;
+}
+
+int ngp_nerf_dataset_create(uint32_t n_images, const ngp_nerf_image* images, const void* const* rgba8, ngp_nerf_dataset** out) {
+	if (!out || !images || !rgba8 || n_images == 0) return NGP_INVALID;
+	NERF_TRY({
+		auto d = std::make_unique<ngp_nerf_dataset>();
+		d->ds.n_images = n_images;
+		uint64_t total = 0;
+		std::vector<Camera> cams(n_images);
+		for (uint32_t i = 0; i < n_images; ++i) {
+			const ngp_nerf_image& im = images[i];
+			Camera& c = cams[i];
+			c.width = im.width; c.height = im.height;
+			c.focal[0] = im.focal_length[0]; c.focal[1] = im.focal_length[1];
+			c.principal[0] = im.principal_point[0]; c.principal[1] = im.principal_point[1];
+			effective_camera_matrix(im.xform, c.m);
+			c.pixel_offset = total;
+			total += (uint64_t)im.width * im.height;
+		}
+		NGP_HIP(hipMalloc(&d->ds.d_pixels, total * 4 + 12 * 4 * n_images));
+		for (uint32_t i = 0; i < n_images; ++i)
+			NGP_HIP(hipMemcpy(d->ds.d_pixels + cams[i].pixel_offset, rgba8[i], (size_t)images[i].width * images[i].height * 4,
+			                  hipMemcpyHostToDevice));
+		// raw (start) transforms after the pixels, for mark_untrained_density_grid
+		std::vector<float> raw(12 * n_images);
+		for (uint32_t i = 0; i < n_images; ++i) memcpy(&raw[12 * i], images[i].xform, 48);
+		NGP_HIP(hipMemcpy(d->ds.d_pixels + total, raw.data(), raw.size() * 4, hipMemcpyHostToDevice));
+		NGP_HIP(hipMalloc(&d->ds.d_cams, n_images * sizeof(Camera)));
+		NGP_HIP(hipMemcpy(d->ds.d_cams, cams.data(), n_images * sizeof(Camera), hipMemcpyHostToDevice));
+		d->ds.cams = cams;
+		*out = d.release();
+	});
+}
+
+void ngp_nerf_dataset_destroy(ngp_nerf_dataset* d) { delete d; }
+
+static const float* raw_xforms(const Dataset& ds) {
+	const Camera& last = ds.cams.back();
+	return (const float*)(ds.d_pixels + last.pixel_offset + (uint64_t)last.width * last.height);
+}
+
+int ngp_nerf_generate_training_samples(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
+                                       uint32_t ray_offset, uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples,
+                                       const uint8_t* bitfield, uint32_t* ray_indices, float* rays, uint32_t* numsteps,
+                                       float* coords, uint32_t* counters) {
+	if (!ds || !cfg || !bitfield || !ray_indices || !rays || !numsteps || !coords || !counters) return NGP_INVALID;
+	NERF_TRY({
+		SampleArgs a{};
+		a.n_rays = n_rays; a.ray_offset = ray_offset; a.n_rays_total_for_image_idx = n_rays_total ? n_rays_total : n_rays;
+		a.max_samples = max_samples; a.rng = Rng{rng.state, rng.inc}; a.bitfield = bitfield;
+		a.ray_indices = ray_indices; a.rays = rays; a.numsteps = numsteps; a.coords = coords; a.counters = counters;
+		static thread_local Buf scan, tmp;
+		const size_t sb = scan_temp_bytes(n_rays);
+		if (n_rays == 0) { NGP_HIP(hipMemsetAsync(counters, 0, 8, S(stream))); return NGP_OK; }
+		sample_rays(ds->ds, *cfg, a, scan.get<char>(sb), sb, tmp.get<uint32_t>(4 * (size_t)n_rays), nullptr, S(stream));
+	});
+}
+
+int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
+                          uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
+                          const void* network_output, const uint32_t* ray_indices, const float* rays, uint32_t* numsteps,
+                          const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
+                          uint32_t* compacted_counter, const float* mean_density, float loss_scale) {
+	if (!ds || !cfg || !ray_counter || !network_output || !numsteps || !coords_in || !coords_out || !dloss_doutput ||
+	    !compacted_counter || !mean_density)
+		return NGP_INVALID;
+	NERF_TRY({
+		LossArgs a{};
+		a.n_rays = n_rays; a.n_rays_total_for_image_idx = n_rays_total ? n_rays_total : n_rays; a.rng = Rng{rng.state, rng.inc};
+		a.max_samples_compacted = max_samples_compacted; a.ray_counter = ray_counter; a.network_output = (const f16*)network_output;
+		a.ray_indices = ray_indices; a.rays = rays; a.numsteps = numsteps; a.coords_in = coords_in; a.coords_out = coords_out;
+		a.dloss_doutput = (f16*)dloss_doutput; a.loss = loss; a.compacted_counter = compacted_counter;
+		a.mean_density = mean_density; a.loss_scale = loss_scale;
+		if (n_rays == 0) { NGP_HIP(hipMemsetAsync(compacted_counter, 0, 4, S(stream))); return NGP_OK; }
+		static thread_local Buf scan, tmp, tmpf;
+		const size_t sb = scan_temp_bytes(n_rays);
+		compute_loss(ds->ds, *cfg, a, scan.get<char>(sb), sb, tmp.get<uint32_t>(2 * (size_t)n_rays), tmpf.get<float>(6 * (size_t)n_rays),
+		             S(stream));
+	});
+}
+
+int ngp_nerf_fill_rollover(void* stream, uint32_t n_elements, uint32_t stride, const uint32_t* n_input, void* data, int dtype,
+                           int rescale) {
+	if (!n_input || !data) return NGP_INVALID;
+	NERF_TRY({
+		if (dtype == 1) fill_rollover_f16(n_elements, stride, n_input, (f16*)data, rescale != 0, S(stream));
+		else fill_rollover_f32(n_elements, stride, n_input, (float*)data, S(stream));
+	});
+}
+
+int ngp_nerf_grid_generate_samples(void* stream, const ngp_nerf_config* cfg, uint32_t n, ngp_rng rng, uint32_t step,
+                                   const float* grid, uint32_t n_cascades, float thresh, float* positions, uint32_t* indices) {
+	if (!cfg || !grid || !positions || !indices) return NGP_INVALID;
+	NERF_TRY(grid_generate_samples(n, Rng{rng.state, rng.inc}, step, *cfg, grid, n_cascades, thresh, positions, indices, S(stream)));
+}
+int ngp_nerf_grid_splat_max(void* stream, uint32_t n, const uint32_t* indices, const void* density_rm, uint32_t act, float* tmp) {
+	if (!indices || !density_rm || !tmp) return NGP_INVALID;
+	NERF_TRY(grid_splat_max(n, indices, (const f16*)density_rm, act, tmp, S(stream)));
+}
+int ngp_nerf_grid_ema(void* stream, uint32_t n, float decay, float* grid, const float* tmp) {
+	if (!grid || !tmp) return NGP_INVALID;
+	NERF_TRY(grid_ema(n, decay, grid, tmp, S(stream)));
+}
+int ngp_nerf_grid_mean_and_bitfield(void* stream, const float* grid, uint32_t max_cascade, float* mean, uint8_t* bitfield) {
+	if (!grid || !mean || !bitfield || max_cascade >= CASCADES) return NGP_INVALID;
+	NERF_TRY(grid_mean_bitfield(grid, max_cascade, mean, bitfield, S(stream)));
+}
+
+// ---- Testbed-level ---------------------------------------------------------------------------
+int ngp_nerf_trainer_create(ngp_model* model, ngp_trainer* trainer, const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg,
+                            uint64_t seed, ngp_nerf_trainer** out) {
+	if (!model || !trainer || !ds || !cfg || !out) return NGP_INVALID;
+	NERF_TRY({
+		auto t = std::make_unique<ngp_nerf_trainer>();
+		t->model = model; t->trainer = trainer; t->data = ds; t->cfg = *cfg;
+		t->rng = HostPcg(seed);                          // m_rng = default_rng_t{m_seed} (testbed.cu:3906)
+		t->grid_rng = HostPcg(t->rng.next_uint());       // density_grid_rng (testbed.cu:3919)
+		const uint32_t n_el = GRID_N_CELLS * (cfg->max_cascade + 1);
+		NGP_HIP(hipMemset(t->grid.get<float>(n_el), 0, (size_t)n_el * 4));
+		NGP_HIP(hipMemset(t->bitfield.get<uint8_t>(BITFIELD_BYTES), 0, BITFIELD_BYTES));
+		NGP_HIP(hipMemset(t->mean.get<float>(1 + 512), 0, (1 + 512) * 4));
+		*out = t.release();
+	});
+}
+
+void ngp_nerf_trainer_destroy(ngp_nerf_trainer* t) { delete t; }
+
+int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** grid, uint8_t** bitfield, float** mean) {
+	if (!t) return NGP_INVALID;
+	if (grid) *grid = (float*)t->grid.p;
+	if (bitfield) *bitfield = (uint8_t*)t->bitfield.p;
+	if (mean) *mean = (float*)t->mean.p;
+	return NGP_OK;
+}
+
+static void check_rc(int rc) { if (rc != NGP_OK) throw Error(ngp_last_error()); }
+
+// update_density_grid_nerf (testbed_nerf.cu:3412-3536)
+static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay, uint32_t n_uniform, uint32_t n_nonuniform) {
+	const ngp_nerf_config& cfg = t->cfg;
+	const uint32_t n_cascades = cfg.max_cascade + 1;
+	const uint32_t n_el = GRID_N_CELLS * n_cascades;
+	float* grid = (float*)t->grid.p;
+	if (t->training_step == 0) {
+		t->ema_step = 0;
+		const Dataset& ds = t->data->ds;
+		k_mark_untrained<<<div_round_up(n_el, 128), 128, 0, s>>>(n_el, grid, ds.n_images, ds.d_cams, raw_xforms(ds), true);
+		NGP_HIP(hipGetLastError());
+	}
+	const uint32_t n = n_uniform + n_nonuniform;
+	float* tmp = t->grid_tmp.get<float>(n_el);
+	NGP_HIP(hipMemsetAsync(tmp, 0, (size_t)n_el * 4, s));
+	float* pos = t->gpos.get<float>((size_t)n * 3);
+	uint32_t* idx = t->gidx.get<uint32_t>(n);
+	grid_generate_samples(n_uniform, t->grid_rng.dev(), t->ema_step, cfg, grid, n_cascades, -0.01f, pos, idx, s);
+	t->grid_rng.advance();
+	grid_generate_samples(n_nonuniform, t->grid_rng.dev(), t->ema_step, cfg, grid, n_cascades, MIN_OPTICAL_THICKNESS,
+	                      pos + (size_t)n_uniform * 3, idx + n_uniform, s);
+	t->grid_rng.advance();
+	f16* dens = t->gdens.get<f16>((size_t)n * 16);
+	check_rc(ngp_density(t->model, s, n, pos, 3, dens, n, NGP_LAYOUT_SOA, 0));  // row 0 = raw density
+	grid_splat_max(n, idx, dens, cfg.density_activation, tmp, s);
+	grid_ema(n_el, decay, grid, tmp, s);
+	++t->ema_step;
+	grid_mean_bitfield(grid, cfg.max_cascade, (float*)t->mean.p, (uint8_t*)t->bitfield.p, s);
+}
+
+int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_nerf_stats* st) {
+	if (!t) return NGP_INVALID;
+	NERF_TRY({
+		hipStream_t s = S(stream);
+		const ngp_nerf_config& cfg = t->cfg;
+		const uint32_t B = cfg.target_batch_size;
+		// training_prep_nerf
+		const uint32_t skip = std::min(std::max(t->training_step / 16u, 1u), 16u);
+		if (t->training_step % skip == 0) {
+			const uint32_t nc = cfg.max_cascade + 1;
+			if (t->training_step < 256) update_density_grid(t, s, 0.95f, GRID_N_CELLS * nc, 0);
+			else update_density_grid(t, s, 0.95f, GRID_N_CELLS / 4 * nc, GRID_N_CELLS / 4 * nc);
+		}
+		// train_nerf_step (testbed_nerf.cu:3867-4132)
+		const uint32_t R = t->rays_per_batch;
+		const uint32_t max_samples = B * 16;
+		uint32_t max_inference;
+		if (t->measured_before_compaction == 0) t->measured_before_compaction = max_inference = max_samples;
+		else max_inference = next_multiple(std::min(t->measured_before_compaction, max_samples), 256);
+		if (t->training_step == 0) t->n_rays_total = 0;
+		const uint32_t n_rays_total = t->n_rays_total;
+		t->n_rays_total += R;
+		uint32_t* ray_indices = t->ray_indices.get<uint32_t>(R);
+		float* rays = t->rays.get<float>((size_t)R * 6);
+		uint32_t* numsteps = t->numsteps.get<uint32_t>((size_t)R * 2);
+		float* coords = t->coords.get<float>((size_t)max_samples * 7);
+		f16* mlp_out = t->mlp_out.get<f16>((size_t)std::max(B, max_samples) * 16);
+		f16* dloss = t->dloss.get<f16>((size_t)B * 16);
+		float* coords_c = t->coords_c.get<float>((size_t)B * 7);
+		float* loss = t->loss.get<float>(R);
+		uint32_t* ctr = t->counters.get<uint32_t>(4);  // rays kept, steps, compacted steps
+		NGP_HIP(hipMemsetAsync(loss, 0, (size_t)R * 4, s));
+		(void)n_rays_total;
+		ngp_rng rng{t->rng.state, t->rng.inc};
+		check_rc(ngp_nerf_generate_training_samples(t->data, &cfg, s, R, 0, 0, rng, max_inference, (const uint8_t*)t->bitfield.p,
+		                                            ray_indices, rays, numsteps, coords, ctr));
+		check_rc(ngp_inference(t->model, s, max_inference, coords, 7, mlp_out, 16, NGP_LAYOUT_AOS, 0));
+		check_rc(ngp_nerf_compute_loss(t->data, &cfg, s, R, 0, rng, B, ctr, mlp_out, ray_indices, rays, numsteps, coords, coords_c,
+		                               dloss, loss, ctr + 2, (const float*)t->mean.p, 128.0f));
+		fill_rollover_f16(B, 16, ctr + 2, dloss, true, s);
+		fill_rollover_f32(B, 7, ctr + 2, coords_c, s);
+		check_rc(ngp_forward_backward(t->model, s, B, coords_c, 7, nullptr, 0, dloss, 16, NGP_GRAD_OVERWRITE));
+		t->rng.advance();  // m_rng.advance() (testbed_nerf.cu:4127)
+		check_rc(ngp_trainer_optimizer_step(t->trainer, s, 128.0f));
+		++t->training_step;
+		// NerfCounters::update_after_training (testbed_nerf.cu:3583-3609): host sync
+		uint32_t h[4];
+		NGP_HIP(hipMemcpyAsync(h, ctr, 16, hipMemcpyDeviceToHost, s));
+		std::vector<float> hl;
+		if (get_loss) { hl.resize(R); NGP_HIP(hipMemcpyAsync(hl.data(), loss, (size_t)R * 4, hipMemcpyDeviceToHost, s)); }
+		NGP_HIP(hipStreamSynchronize(s));
+		float loss_scalar = 0.f;
+		t->measured_batch_size = 0;
+		t->measured_before_compaction = 0;
+		if (h[1] != 0 && h[2] != 0) {
+			t->measured_before_compaction = h[1];
+			t->measured_batch_size = h[2];
+			if (get_loss) {
+				double sum = 0;
+				for (float v : hl) sum += v;
+				loss_scalar = (float)(sum * (double)t->measured_batch_size / (double)B);
+			}
+			uint32_t r = (uint32_t)((float)t->rays_per_batch * (float)B / (float)t->measured_batch_size);
+			t->rays_per_batch = std::min(next_multiple(r, 256), 1u << 18);
+		}
+		if (st) {
+			st->step = t->training_step;
+			st->rays_per_batch = t->rays_per_batch;
+			st->measured_batch_size = t->measured_batch_size;
+			st->measured_batch_size_before_compaction = t->measured_before_compaction;
+			st->loss = loss_scalar;
+		}
+		NGP_CHECK(t->measured_batch_size > 0, "Nerf training generated 0 samples (testbed_nerf.cu:3693-3697)");
+	});
+}
+
+}  // extern "C"

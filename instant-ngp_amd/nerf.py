@@ -1,0 +1,219 @@
+"""Host mirror of the Testbed's NeRF training path (src/testbed_nerf.cu) over the C-ABI.
+
+`NerfTraining` is Testbed::train for a NeRF testbed (training_prep_nerf + train_nerf,
+testbed_nerf.cu:3611-3862, 4137-4152); the free functions expose the individual kernels
+(generate_training_samples_nerf, compute_loss_kernel_train_nerf, the density-grid update) with
+the reference's argument meaning so they can be tested one by one. Every call runs HIP.
+"""
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from ._capi import NerfConfig, NerfImage, NerfStats, Rng, check, lib
+from .network import _ptr, _stream, wrap_device
+
+NERF_GRIDSIZE = 128
+NERF_CASCADES = 8
+N_CELLS = NERF_GRIDSIZE ** 3
+BITFIELD_BYTES = N_CELLS // 8 * NERF_CASCADES
+ACT = {"None": 0, "ReLU": 1, "Logistic": 2, "Exponential": 3}
+LOSS = {"L2": 0, "L1": 1, "MAPE": 2, "SMAPE": 3, "Huber": 4, "LogL1": 5, "RelativeL2": 6}
+
+
+def default_config(aabb_scale=1.0, **overrides):
+    """Testbed NeRF defaults after load_nerf_post (testbed_nerf.cu:3093-3109, testbed.h:716-785)."""
+    cfg = NerfConfig()
+    check(lib().ngp_nerf_default_config(float(aabb_scale), C.byref(cfg)))
+    for k, v in overrides.items():
+        if isinstance(getattr(cfg, k), C.Array):
+            getattr(cfg, k)[:] = list(v)
+        else:
+            setattr(cfg, k, v)
+    return cfg
+
+
+def rng_state(state, inc):
+    return Rng(state, inc)
+
+
+def pcg32(seed, seq=1):
+    """tcnn::pcg32(initstate, initseq) seeding (pcg32.h), host side."""
+    mask = (1 << 64) - 1
+    mult = 0x5851F42D4C957F2D
+    inc = ((seq << 1) | 1) & mask
+    state = 0
+    state = (state * mult + inc) & mask
+    state = (state + seed) & mask
+    state = (state * mult + inc) & mask
+    return Rng(state, inc)
+
+
+def nerf_matrix_to_ngp(m, scale=0.33, offset=(0.5, 0.5, 0.5)):
+    """NerfDataset::nerf_matrix_to_ngp (nerf_loader.h:120-140), non-mitsuba branch.
+    m: 3x4 (or 4x4) camera-to-world in the NeRF/Blender convention. Returns the 12 floats of the
+    column-major mat4x3 the engine takes."""
+    m = np.asarray(m, dtype=np.float32)[:3, :4].copy()
+    m[:, 1] *= -1.0
+    m[:, 2] *= -1.0
+    m[:, 3] = m[:, 3] * np.float32(scale) + np.asarray(offset, np.float32)
+    m = m[[1, 2, 0], :]  # cycle axes xyz <- yzx
+    return np.ascontiguousarray(m.T).reshape(12)
+
+
+def make_image(width, height, xform12, focal=None, camera_angle_x=None, principal=(0.5, 0.5)):
+    im = NerfImage()
+    im.width, im.height = width, height
+    if focal is None:
+        f = 0.5 * width / math.tan(0.5 * camera_angle_x)  # nerf_loader.cu: fl from camera_angle_x
+        focal = (f, f)
+    im.focal_length[:] = list(focal)
+    im.principal_point[:] = list(principal)
+    im.xform[:] = [float(v) for v in xform12]
+    return im
+
+
+class NerfDataset:
+    """Training images (RGBA8 sRGB, EImageDataType::Byte) + cameras on the device."""
+
+    def __init__(self, images, rgba8):
+        if len(images) != len(rgba8) or not images:
+            raise ValueError("need one RGBA8 array per image")
+        arr = (NerfImage * len(images))(*images)
+        self.images = list(images)
+        bufs = []
+        for im, px in zip(images, rgba8):
+            px = np.ascontiguousarray(px, dtype=np.uint8)
+            if px.shape != (im.height, im.width, 4):
+                raise ValueError(f"image buffer shape {px.shape} != {(im.height, im.width, 4)}")
+            bufs.append(px)
+        self._host = bufs
+        ptrs = (C.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
+        h = C.c_void_p()
+        check(lib().ngp_nerf_dataset_create(len(images), arr, ptrs, C.byref(h)))
+        self.handle = h
+
+    def __len__(self):
+        return len(self.images)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                lib().ngp_nerf_dataset_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+# ---- kernel-level entry points ------------------------------------------------------------------
+def generate_training_samples(ds, cfg, n_rays, rng, max_samples, bitfield, ray_offset=0, n_rays_total=None,
+                              stream=None):
+    """generate_training_samples_nerf (testbed_nerf.cu:1382-1658)."""
+    dev = bitfield.device
+    out = {
+        "ray_indices": torch.zeros(n_rays, dtype=torch.int32, device=dev),
+        "rays": torch.zeros((n_rays, 6), dtype=torch.float32, device=dev),
+        "numsteps": torch.zeros((n_rays, 2), dtype=torch.int32, device=dev),
+        "coords": torch.zeros((max_samples, 7), dtype=torch.float32, device=dev),
+        "counters": torch.zeros(2, dtype=torch.int32, device=dev),
+    }
+    check(lib().ngp_nerf_generate_training_samples(
+        ds.handle, C.byref(cfg), _stream(stream), n_rays, ray_offset, n_rays_total or n_rays, rng, max_samples,
+        _ptr(bitfield), _ptr(out["ray_indices"]), _ptr(out["rays"]), _ptr(out["numsteps"]), _ptr(out["coords"]),
+        _ptr(out["counters"])))
+    return out
+
+
+def compute_loss(ds, cfg, n_rays, rng, max_compacted, samples, network_output, mean_density, loss_scale=128.0,
+                 n_rays_total=None, stream=None):
+    """compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012). `samples` is the dict returned by
+    generate_training_samples (its numsteps is rewritten to the compacted {n, base})."""
+    dev = network_output.device
+    out = {
+        "coords_compacted": torch.zeros((max_compacted, 7), dtype=torch.float32, device=dev),
+        "dloss_doutput": torch.zeros((max_compacted, 16), dtype=torch.float16, device=dev),
+        "loss": torch.zeros(n_rays, dtype=torch.float32, device=dev),
+        "compacted_counter": torch.zeros(1, dtype=torch.int32, device=dev),
+    }
+    check(lib().ngp_nerf_compute_loss(
+        ds.handle, C.byref(cfg), _stream(stream), n_rays, n_rays_total or n_rays, rng, max_compacted,
+        _ptr(samples["counters"]), _ptr(network_output), _ptr(samples["ray_indices"]), _ptr(samples["rays"]),
+        _ptr(samples["numsteps"]), _ptr(samples["coords"]), _ptr(out["coords_compacted"]), _ptr(out["dloss_doutput"]),
+        _ptr(out["loss"]), _ptr(out["compacted_counter"]), _ptr(mean_density), float(loss_scale)))
+    return out
+
+
+def fill_rollover(data, n_input, rescale=False, stream=None):
+    """tcnn fill_rollover / fill_rollover_and_rescale over the rows of a 2D tensor (testbed_nerf.cu:4061-4069)."""
+    dtype = {torch.float32: 0, torch.float16: 1}[data.dtype]
+    check(lib().ngp_nerf_fill_rollover(_stream(stream), data.shape[0], data.shape[1], _ptr(n_input), _ptr(data), dtype,
+                                       int(rescale)))
+
+
+def grid_generate_samples(cfg, n, rng, step, grid, n_cascades, thresh, stream=None):
+    """generate_grid_samples_nerf_nonuniform (testbed_nerf.cu:635-676)."""
+    pos = torch.zeros((n, 3), dtype=torch.float32, device=grid.device)
+    idx = torch.zeros(n, dtype=torch.int32, device=grid.device)
+    check(lib().ngp_nerf_grid_generate_samples(_stream(stream), C.byref(cfg), n, rng, step, _ptr(grid), n_cascades,
+                                               float(thresh), _ptr(pos), _ptr(idx)))
+    return pos, idx
+
+
+def grid_splat_max(indices, density_out, density_activation, grid_tmp, stream=None):
+    """splat_grid_samples_nerf_max_nearest_neighbor (testbed_nerf.cu:678-702). density_out: the density
+    network's fp16 output, row-major [16 x n] (feature-major), density in row 0."""
+    check(lib().ngp_nerf_grid_splat_max(_stream(stream), indices.shape[0], _ptr(indices), _ptr(density_out),
+                                        density_activation, _ptr(grid_tmp)))
+
+
+def grid_ema(decay, grid, grid_tmp, stream=None):
+    """ema_grid_samples_nerf (testbed_nerf.cu:731-754)."""
+    check(lib().ngp_nerf_grid_ema(_stream(stream), grid.numel(), float(decay), _ptr(grid), _ptr(grid_tmp)))
+
+
+def grid_mean_and_bitfield(grid, max_cascade, stream=None):
+    """update_density_grid_mean_and_bitfield (testbed_nerf.cu:3538-3567)."""
+    mean = torch.zeros(1 + 512, dtype=torch.float32, device=grid.device)
+    bf = torch.zeros(BITFIELD_BYTES, dtype=torch.uint8, device=grid.device)
+    check(lib().ngp_nerf_grid_mean_and_bitfield(_stream(stream), _ptr(grid), max_cascade, _ptr(mean), _ptr(bf)))
+    return mean, bf
+
+
+# ---- Testbed-level training -------------------------------------------------------------------
+class NerfTraining:
+    """Testbed::train for NeRF: density-grid update + one training step per call (testbed.cu:4285-4370)."""
+
+    def __init__(self, network, trainer, dataset, cfg=None, seed=1337):
+        self.network, self.trainer, self.dataset = network, trainer, dataset
+        self.cfg = cfg if cfg is not None else default_config()
+        h = C.c_void_p()
+        check(lib().ngp_nerf_trainer_create(network.handle, trainer.handle, dataset.handle, C.byref(self.cfg), seed,
+                                            C.byref(h)))
+        self.handle = h
+        g, b, m = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        check(lib().ngp_nerf_trainer_buffers(h, C.byref(g), C.byref(b), C.byref(m)))
+        # density grid holds max_cascade + 1 cascades (testbed_nerf.cu:3412-3420); the bitfield all 8
+        self.density_grid = wrap_device(g.value, N_CELLS * (self.cfg.max_cascade + 1), torch.float32)
+        self._bitfield_ptr = b.value
+        self.mean_density = wrap_device(m.value, 1, torch.float32)
+
+    @property
+    def bitfield(self):
+        words = wrap_device(self._bitfield_ptr, BITFIELD_BYTES // 4, torch.float32)
+        return words.view(torch.uint8)
+
+    def train_step(self, get_loss=True, stream=None):
+        st = NerfStats()
+        check(lib().ngp_nerf_train_step(self.handle, _stream(stream), int(get_loss), C.byref(st)))
+        return {k: getattr(st, k) for k, _ in NerfStats._fields_}
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                lib().ngp_nerf_trainer_destroy(h)
+            except Exception:
+                pass
+            self.handle = None

@@ -64,8 +64,8 @@ class Context:
     def __init__(self, model, handle, n):
         self.model, self.handle, self.n = model, handle, n
 
-    def __del__(self):
-        _destroy(self, "ngp_ctx_destroy")
+    def __del__(self, _d=_destroy):
+        _d(self, "ngp_ctx_destroy")
 
 
 class Model:
@@ -75,8 +75,8 @@ class Model:
         self.handle = handle
         self._keep = []
 
-    def __del__(self):
-        _destroy(self, "ngp_model_destroy")
+    def __del__(self, _d=_destroy):
+        _d(self, "ngp_model_destroy")
 
     # -- shape queries ------------------------------------------------------------------------
     @property
@@ -214,8 +214,8 @@ class Trainer:
         self.inference_params = wrap_device(L.ngp_trainer_inference_params(h), n, torch.float16)
         self.params_full_precision = wrap_device(L.ngp_trainer_params_full_precision(h), n, torch.float32)
 
-    def __del__(self):
-        _destroy(self, "ngp_trainer_destroy")
+    def __del__(self, _d=_destroy):
+        _d(self, "ngp_trainer_destroy")
 
     def optimizer_step(self, loss_scale=128.0, stream=None):
         check(lib().ngp_trainer_optimizer_step(self.handle, _stream(stream), float(loss_scale)))

@@ -1,0 +1,521 @@
+/*
+ * ngp_nerf_oracle.c — CPU restatement of the NeRF training kernels of src/testbed_nerf.cu.
+ * TEST INFRASTRUCTURE ONLY (see ngp_oracle.c header). Sequential, deterministic: slots are assigned in
+ * ray order, which is the multiset-equivalent of the reference's atomicAdd ordering.
+ * Parity status: restated from code present in the reference (file:line per function); no golden
+ * vectors exist in the reference for these kernels, and the reference cannot run here.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EXPORT __attribute__((visibility("default")))
+
+typedef struct { uint64_t state, inc; } orc_pcg32;
+uint32_t orc_pcg32_next_uint(orc_pcg32* r);
+float orc_pcg32_next_float(orc_pcg32* r);
+void orc_pcg32_advance(orc_pcg32* r, int64_t delta);
+float orc_f16_to_f32(uint16_t h);
+uint16_t orc_f32_to_f16(float f);
+
+#define GRIDSIZE 128u
+#define N_CELLS (GRIDSIZE * GRIDSIZE * GRIDSIZE)
+#define CASCADES 8u
+#define NSTEPS 1024u
+#define SQRT3 1.73205080757f
+#define MIN_STEP (SQRT3 / NSTEPS)
+#define MAX_STEP (MIN_STEP * (1 << (CASCADES - 1)) * NSTEPS / GRIDSIZE)
+#define MIN_OPT 0.01f
+
+/* mirrors ngp_nerf_config / ngp_nerf_image of include/ngp_engine.h (same field order) */
+typedef struct {
+	float aabb_min[3], aabb_max[3];
+	float cone_angle_constant;
+	uint32_t max_cascade, snap_to_pixel_centers, random_bg_color, linear_colors, color_space_linear;
+	float background_color[3];
+	uint32_t rgb_activation, density_activation, loss_type;
+	float near_distance;
+	uint32_t target_batch_size;
+} ocfg;
+
+typedef struct {
+	uint32_t width, height;
+	float focal_length[2], principal_point[2];
+	float xform[12];
+} oimg;
+
+/* ---- stepping (testbed_nerf.cu:114-184) ---- */
+static float to_step(float t, float c) {
+	if (c <= 1e-5f) return t / MIN_STEP;
+	float l = logf(1.0f + c);
+	float a = (logf(MIN_STEP) - logf(l)) / l, b = (logf(MAX_STEP) - logf(l)) / l;
+	float at = expf(a * l), bt = expf(b * l);
+	if (t <= at) return (t - at) / MIN_STEP + a;
+	else if (t <= bt) return logf(t) / l;
+	else return (t - bt) / MAX_STEP + b;
+}
+static float from_step(float n, float c) {
+	if (c <= 1e-5f) return n * MIN_STEP;
+	float l = logf(1.0f + c);
+	float a = (logf(MIN_STEP) - logf(l)) / l, b = (logf(MAX_STEP) - logf(l)) / l;
+	float at = expf(a * l), bt = expf(b * l);
+	if (n <= a) return (n - a) * MIN_STEP + at;
+	else if (n <= b) return expf(n * l);
+	else return (n - b) * MAX_STEP + bt;
+}
+static float calc_dt(float t, float c) { return from_step(to_step(t, c) + 1.0f, c) - t; }
+static float sgn(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }
+
+static float dist_next_voxel(const float* pos, const float* dir, const float* idir, float res) {
+	float p[3], t[3];
+	for (int k = 0; k < 3; ++k) p[k] = res * (pos[k] - 0.5f);
+	for (int k = 0; k < 3; ++k) t[k] = (floorf(p[k] + 0.5f + 0.5f * sgn(dir[k])) - p[k]) * idir[k];
+	float m = fminf(fminf(t[0], t[1]), t[2]);
+	return fmaxf(m / res, 0.0f);
+}
+static float advance_voxel(float t, float c, const float* pos, const float* dir, const float* idir, uint32_t mip) {
+	float res = scalbnf((float)GRIDSIZE, -(int)mip);
+	float tt = t + dist_next_voxel(pos, dir, idir, res);
+	t = to_step(t, c);
+	tt = to_step(tt, c);
+	return from_step(t + ceilf(fmaxf(tt - t, 0.5f)), c);
+}
+
+/* testbed_nerf.cu:614-633 */
+static uint32_t mip_pos(const float* p, uint32_t mc) {
+	int e;
+	float m = fmaxf(fmaxf(fabsf(p[0] - 0.5f), fabsf(p[1] - 0.5f)), fabsf(p[2] - 0.5f));
+	frexpf(m, &e);
+	int v = e + 1;
+	if (v < 0) v = 0;
+	if (v > (int)mc) v = (int)mc;
+	return (uint32_t)v;
+}
+static uint32_t mip_dt(float dt, const float* p, uint32_t mc) {
+	uint32_t m = mip_pos(p, mc);
+	dt *= 2 * GRIDSIZE;
+	if (dt < 1.0f) return m;
+	int e;
+	frexpf(dt, &e);
+	int v = (int)m < e ? e : (int)m;
+	if (v > (int)mc) v = (int)mc;
+	return (uint32_t)v;
+}
+
+static uint32_t ebits(uint32_t v) {
+	v = (v * 0x00010001u) & 0xFF0000FFu;
+	v = (v * 0x00000101u) & 0x0F00F00Fu;
+	v = (v * 0x00000011u) & 0xC30C30C3u;
+	v = (v * 0x00000005u) & 0x49249249u;
+	return v;
+}
+/* tcnn morton3D with x in bit 0 (round trip of morton3D_invert(idx>>0) = x, testbed_nerf.cu:518-520) */
+EXPORT uint32_t orc_morton3D(uint32_t x, uint32_t y, uint32_t z) { return ebits(x) | (ebits(y) << 1) | (ebits(z) << 2); }
+EXPORT uint32_t orc_morton3D_invert(uint32_t x) {
+	x = x & 0x49249249u;
+	x = (x | (x >> 2)) & 0xc30c30c3u;
+	x = (x | (x >> 4)) & 0x0f00f00fu;
+	x = (x | (x >> 8)) & 0xff0000ffu;
+	x = (x | (x >> 16)) & 0x0000ffffu;
+	return x;
+}
+
+/* testbed_nerf.cu:433-457 */
+static uint32_t grid_idx_at(const float* p, uint32_t mip) {
+	float s = scalbnf(1.0f, -(int)mip), q[3];
+	for (int k = 0; k < 3; ++k) q[k] = (p[k] - 0.5f) * s + 0.5f;
+	int i[3];
+	for (int k = 0; k < 3; ++k) i[k] = (int)(q[k] * (float)GRIDSIZE);
+	for (int k = 0; k < 3; ++k)
+		if (i[k] < 0 || i[k] >= (int)GRIDSIZE) return 0xFFFFFFFFu;
+	return orc_morton3D((uint32_t)i[0], (uint32_t)i[1], (uint32_t)i[2]);
+}
+static int occupied(const float* p, const uint8_t* bf, uint32_t mip) {
+	uint32_t idx = grid_idx_at(p, mip);
+	if (idx == 0xFFFFFFFFu) return 0;
+	return (bf[idx / 8 + N_CELLS * mip / 8] >> (idx % 8)) & 1;
+}
+
+static int contains(const ocfg* c, const float* p) {
+	for (int k = 0; k < 3; ++k)
+		if (!(p[k] >= c->aabb_min[k] && p[k] <= c->aabb_max[k])) return 0;
+	return 1;
+}
+/* bounding_box.cuh:163-216 */
+static void ray_box(const ocfg* c, const float* o, const float* d, float* tmin_o, float* tmax_o) {
+	float tmin = (c->aabb_min[0] - o[0]) / d[0], tmax = (c->aabb_max[0] - o[0]) / d[0], tt;
+	if (tmin > tmax) { tt = tmin; tmin = tmax; tmax = tt; }
+	float tymin = (c->aabb_min[1] - o[1]) / d[1], tymax = (c->aabb_max[1] - o[1]) / d[1];
+	if (tymin > tymax) { tt = tymin; tymin = tymax; tymax = tt; }
+	if (tmin > tymax || tymin > tmax) { *tmin_o = *tmax_o = 3.402823466e+38f; return; }
+	if (tymin > tmin) tmin = tymin;
+	if (tymax < tmax) tmax = tymax;
+	float tzmin = (c->aabb_min[2] - o[2]) / d[2], tzmax = (c->aabb_max[2] - o[2]) / d[2];
+	if (tzmin > tzmax) { tt = tzmin; tzmin = tzmax; tzmax = tt; }
+	if (tmin > tzmax || tzmin > tmax) { *tmin_o = *tmax_o = 3.402823466e+38f; return; }
+	if (tzmin > tmin) tmin = tzmin;
+	if (tzmax < tmax) tmax = tzmax;
+	*tmin_o = tmin; *tmax_o = tmax;
+}
+
+/* get_xform_given_rolling_shutter with start == end, t = 0 (common_device.cuh:401-408): glm quat_cast,
+ * slerp (linear branch returns the input), normalize, mat3_cast. xf column-major m[c][r] = xf[3c+r]. */
+EXPORT void orc_camera_matrix(const float* xf, float* out) {
+#define MM(c, r) xf[3 * (c) + (r)]
+	float fx = MM(0, 0) - MM(1, 1) - MM(2, 2), fy = MM(1, 1) - MM(0, 0) - MM(2, 2), fz = MM(2, 2) - MM(0, 0) - MM(1, 1);
+	float fw = MM(0, 0) + MM(1, 1) + MM(2, 2);
+	int bi = 0;
+	float big = fw;
+	if (fx > big) { big = fx; bi = 1; }
+	if (fy > big) { big = fy; bi = 2; }
+	if (fz > big) { big = fz; bi = 3; }
+	float bv = sqrtf(big + 1.0f) * 0.5f, mu = 0.25f / bv, q[4]; /* w x y z */
+	if (bi == 0) { q[0] = bv; q[1] = (MM(1, 2) - MM(2, 1)) * mu; q[2] = (MM(2, 0) - MM(0, 2)) * mu; q[3] = (MM(0, 1) - MM(1, 0)) * mu; }
+	else if (bi == 1) { q[0] = (MM(1, 2) - MM(2, 1)) * mu; q[1] = bv; q[2] = (MM(0, 1) + MM(1, 0)) * mu; q[3] = (MM(2, 0) + MM(0, 2)) * mu; }
+	else if (bi == 2) { q[0] = (MM(2, 0) - MM(0, 2)) * mu; q[1] = (MM(0, 1) + MM(1, 0)) * mu; q[2] = bv; q[3] = (MM(1, 2) + MM(2, 1)) * mu; }
+	else { q[0] = (MM(0, 1) - MM(1, 0)) * mu; q[1] = (MM(2, 0) + MM(0, 2)) * mu; q[2] = (MM(1, 2) + MM(2, 1)) * mu; q[3] = bv; }
+#undef MM
+	float len = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+	if (len <= 0.f) { q[0] = 1.f; q[1] = q[2] = q[3] = 0.f; }
+	else { float inv = 1.0f / len; for (int k = 0; k < 4; ++k) q[k] *= inv; }
+	float w = q[0], x = q[1], y = q[2], z = q[3];
+	float xx = x * x, yy = y * y, zz = z * z, xz = x * z, xy = x * y, yz = y * z, wx = w * x, wy = w * y, wz = w * z;
+	out[0] = 1.f - 2.f * (yy + zz); out[1] = 2.f * (xy + wz); out[2] = 2.f * (xz - wy);
+	out[3] = 2.f * (xy - wz); out[4] = 1.f - 2.f * (xx + zz); out[5] = 2.f * (yz + wx);
+	out[6] = 2.f * (xz + wy); out[7] = 2.f * (yz - wx); out[8] = 1.f - 2.f * (xx + yy);
+	out[9] = xf[9]; out[10] = xf[10]; out[11] = xf[11];
+}
+
+static void rand_uv(orc_pcg32* r, const oimg* im, int snap, float* u, float* v) {
+	*u = orc_pcg32_next_float(r);
+	*v = orc_pcg32_next_float(r);
+	if (snap) {
+		int px = (int)(*u * (float)im->width), py = (int)(*v * (float)im->height);
+		if (px < 0) px = 0;
+		if (px > (int)im->width - 1) px = (int)im->width - 1;
+		if (py < 0) py = 0;
+		if (py > (int)im->height - 1) py = (int)im->height - 1;
+		*u = ((float)px + 0.5f) / (float)im->width;
+		*v = ((float)py + 0.5f) / (float)im->height;
+	}
+}
+static uint64_t pix(float u, float v, const oimg* im) {
+	int px = (int)(u * (float)im->width), py = (int)(v * (float)im->height);
+	if (px < 0) px = 0;
+	if (px > (int)im->width - 1) px = (int)im->width - 1;
+	if (py < 0) py = 0;
+	if (py > (int)im->height - 1) py = (int)im->height - 1;
+	return (uint64_t)px + (uint64_t)py * im->width;
+}
+
+typedef struct { int valid; float o[3], d[3], dn[3], idir[3], startt, cone; } oray;
+
+static oray setup(const ocfg* c, const oimg* ims, const float* cams, const uint32_t* const* px, uint32_t n_img, uint32_t ig,
+                  uint32_t n_div, orc_pcg32 rng) {
+	oray r;
+	memset(&r, 0, sizeof(r));
+	uint32_t img = ((ig * n_img) / n_div) % n_img; /* image_idx, testbed_nerf.cu:1317-1338 */
+	const oimg* im = &ims[img];
+	orc_pcg32_advance(&rng, (int64_t)ig * 16);
+	float u, v;
+	rand_uv(&rng, im, c->snap_to_pixel_centers != 0, &u, &v);
+	if (px[img][pix(u, v, im)] == 0x00FF00FFu) return r;
+	(void)orc_pcg32_next_float(&rng); /* motionblur_time */
+	const float* m = cams + 12 * img;
+	float dx = (u - im->principal_point[0]) * (float)im->width / im->focal_length[0];
+	float dy = (v - im->principal_point[1]) * (float)im->height / im->focal_length[1];
+	float dz = 1.0f;
+	r.d[0] = m[0] * dx + m[3] * dy + m[6] * dz;
+	r.d[1] = m[1] * dx + m[4] * dy + m[7] * dz;
+	r.d[2] = m[2] * dx + m[5] * dy + m[8] * dz;
+	r.o[0] = m[9]; r.o[1] = m[10]; r.o[2] = m[11];
+	float inv = 1.0f / sqrtf(r.d[0] * r.d[0] + r.d[1] * r.d[1] + r.d[2] * r.d[2]);
+	for (int k = 0; k < 3; ++k) r.dn[k] = r.d[k] * inv;
+	float tmin, tmax;
+	ray_box(c, r.o, r.dn, &tmin, &tmax);
+	r.cone = c->cone_angle_constant;
+	tmin = fmaxf(tmin, 0.0f);
+	r.startt = from_step(to_step(tmin, r.cone) + orc_pcg32_next_float(&rng), r.cone);
+	for (int k = 0; k < 3; ++k) r.idir[k] = 1.0f / r.dn[k];
+	r.valid = 1;
+	return r;
+}
+
+/* generate_training_samples_nerf (testbed_nerf.cu:1382-1658) */
+EXPORT void orc_nerf_generate_samples(const ocfg* c, const oimg* ims, const uint32_t* const* px, uint32_t n_img, uint32_t n_rays,
+                                      uint32_t ray_offset, uint32_t n_div, orc_pcg32 rng, uint32_t max_samples, const uint8_t* bf,
+                                      uint32_t* ray_indices, float* rays, uint32_t* numsteps, float* coords, uint32_t* counters) {
+	float* cams = (float*)malloc(sizeof(float) * 12 * n_img);
+	for (uint32_t i = 0; i < n_img; ++i) orc_camera_matrix(ims[i].xform, cams + 12 * i);
+	uint32_t total = 0, kept = 0;
+	float diag[3];
+	for (int k = 0; k < 3; ++k) diag[k] = c->aabb_max[k] - c->aabb_min[k];
+	for (uint32_t i = 0; i < n_rays; ++i) {
+		uint32_t ig = i + ray_offset;
+		oray r = setup(c, ims, cams, px, n_img, ig, n_div ? n_div : n_rays, rng);
+		if (!r.valid) continue;
+		uint32_t j = 0;
+		float t = r.startt, pos[3];
+		for (;;) {
+			for (int k = 0; k < 3; ++k) pos[k] = r.o[k] + t * r.dn[k];
+			if (!(contains(c, pos) && j < NSTEPS)) break;
+			float dt = calc_dt(t, r.cone);
+			uint32_t mip = mip_dt(dt, pos, c->max_cascade);
+			if (occupied(pos, bf, mip)) { ++j; t += dt; }
+			else t = advance_voxel(t, r.cone, pos, r.dn, r.idir, mip);
+		}
+		if (j == 0) continue;
+		uint32_t base = total;
+		total += j;
+		if (base + j > max_samples) continue;
+		uint32_t s = kept++;
+		ray_indices[s] = ig;
+		for (int k = 0; k < 3; ++k) { rays[6 * s + k] = r.o[k]; rays[6 * s + 3 + k] = r.d[k]; }
+		numsteps[2 * s] = j;
+		numsteps[2 * s + 1] = base;
+		uint32_t jj = 0;
+		t = r.startt;
+		for (;;) {
+			for (int k = 0; k < 3; ++k) pos[k] = r.o[k] + t * r.dn[k];
+			if (!(contains(c, pos) && jj < j)) break;
+			float dt = calc_dt(t, r.cone);
+			uint32_t mip = mip_dt(dt, pos, c->max_cascade);
+			if (occupied(pos, bf, mip)) {
+				float* co = coords + (size_t)(base + jj) * 7;
+				for (int k = 0; k < 3; ++k) co[k] = (pos[k] - c->aabb_min[k]) / diag[k];
+				float maxs = MIN_STEP * (1 << (CASCADES - 1));
+				co[3] = (dt - MIN_STEP) / (maxs - MIN_STEP);
+				for (int k = 0; k < 3; ++k) co[4 + k] = (r.dn[k] + 1.0f) * 0.5f;
+				++jj;
+				t += dt;
+			} else {
+				t = advance_voxel(t, r.cone, pos, r.dn, r.idir, mip);
+			}
+		}
+	}
+	counters[0] = kept;
+	counters[1] = total;
+	free(cams);
+}
+
+static float s2l(float s) { return s <= 0.04045f ? s / 12.92f : powf((s + 0.055f) / 1.055f, 2.4f); }
+static float l2s(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * powf(l, 0.41666f) - 0.055f; }
+static float logistic(float x) { return 1.0f / (1.0f + expf(-x)); }
+static float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
+/* testbed_nerf.cu:317-378 (expf for the reference's __expf) */
+static float to_rgb(float v, uint32_t a) {
+	switch (a) { case 0: return v; case 1: return v > 0 ? v : 0; case 2: return logistic(v); default: return expf(clampf(v, -10.f, 10.f)); }
+}
+static float to_rgb_d(float v, uint32_t a) {
+	switch (a) { case 0: return 1; case 1: return v > 0 ? 1.f : 0.f; case 2: { float d = logistic(v); return d * (1 - d); } default: return expf(clampf(v, -10.f, 10.f)); }
+}
+static float to_dens(float v, uint32_t a) {
+	switch (a) { case 0: return v; case 1: return v > 0 ? v : 0; case 2: return logistic(v); default: return expf(v); }
+}
+static float to_dens_d(float v, uint32_t a) {
+	switch (a) { case 0: return 1; case 1: return v > 0 ? 1.f : 0.f; case 2: { float d = logistic(v); return d * (1 - d); } default: return expf(clampf(v, -15.f, 15.f)); }
+}
+/* testbed_nerf.cu:186-276, 1340-1355 */
+static void lossg(float tgt, float p, uint32_t type, float* l, float* g) {
+	float d = p - tgt;
+	switch (type) {
+		case 6: { float den = p * p + 1e-2f; *l = d * d / den; *g = 2.0f * d / den; return; }
+		case 1: *l = fabsf(d); *g = copysignf(1.0f, d); return;
+		case 2: { float den = fabsf(p) + 1e-2f; *l = fabsf(d) / den; *g = copysignf(1.0f / den, d); return; }
+		case 3: { float den = 0.5f * (fabsf(p) + fabsf(tgt)) + 1e-2f; *l = fabsf(d) / den; *g = copysignf(1.0f / den, d); return; }
+		case 4: {
+			float al = 0.1f, ad = fabsf(d), sq = 0.5f / al * d * d;
+			*l = (ad > al ? (ad - 0.5f * al) : sq) / 5.0f;
+			*g = (ad > al ? (d > 0 ? 1.0f : -1.0f) : (d / al)) / 5.0f;
+			return;
+		}
+		case 5: { float dv = fabsf(d) + 1.0f; *l = logf(dv); *g = copysignf(1.0f / dv, d); return; }
+		default: *l = d * d; *g = 2.0f * d; return;
+	}
+}
+
+/* compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012); network_output fp16 bits [n x 16];
+ * dloss fp16 bits [max_c x 16] (rows 0..3 written). */
+EXPORT void orc_nerf_compute_loss(const ocfg* c, const oimg* ims, const uint32_t* const* px, uint32_t n_img, uint32_t n_rays,
+                                  uint32_t n_div, orc_pcg32 rng0, uint32_t max_c, uint32_t ray_counter, const uint16_t* out16,
+                                  const uint32_t* ray_indices, const float* rays, uint32_t* numsteps, const float* coords_in,
+                                  float* coords_out, uint16_t* dloss, float* loss, uint32_t* compacted_counter, float mean_density,
+                                  float loss_scale) {
+	uint32_t ctotal = 0;
+	float diag[3];
+	for (int k = 0; k < 3; ++k) diag[k] = c->aabb_max[k] - c->aabb_min[k];
+	const float maxs = MIN_STEP * (1 << (CASCADES - 1));
+	for (uint32_t i = 0; i < ray_counter && i < n_rays; ++i) {
+		uint32_t ns = numsteps[2 * i], base = numsteps[2 * i + 1];
+		const uint16_t* o = out16 + (size_t)base * 16;
+		const float* ci = coords_in + (size_t)base * 7;
+		float t = 1.f, rgb_ray[3] = {0, 0, 0};
+		uint32_t cn = 0;
+		for (; cn < ns; ++cn) {
+			if (t < 1e-4f) break;
+			float dt = ci[(size_t)cn * 7 + 3] * (maxs - MIN_STEP) + MIN_STEP;
+			float dens = to_dens(orc_f16_to_f32(o[cn * 16 + 3]), c->density_activation);
+			float alpha = 1.f - expf(-dens * dt), w = alpha * t;
+			for (int k = 0; k < 3; ++k) rgb_ray[k] += w * to_rgb(orc_f16_to_f32(o[cn * 16 + k]), c->rgb_activation);
+			t *= (1.f - alpha);
+		}
+		uint32_t ray_idx = ray_indices[i];
+		orc_pcg32 rng = rng0;
+		orc_pcg32_advance(&rng, (int64_t)ray_idx * 16);
+		uint32_t img = ((ray_idx * n_img) / (n_div ? n_div : n_rays)) % n_img;
+		const oimg* im = &ims[img];
+		float u, v;
+		rand_uv(&rng, im, c->snap_to_pixel_centers != 0, &u, &v);
+		orc_pcg32_advance(&rng, 1);
+		float bg[3] = {c->background_color[0], c->background_color[1], c->background_color[2]};
+		if (c->random_bg_color) for (int k = 0; k < 3; ++k) bg[k] = orc_pcg32_next_float(&rng);
+		for (int k = 0; k < 3; ++k) bg[k] = s2l(bg[k]);
+		uint32_t raw = px[img][pix(u, v, im)];
+		float tex[4];
+		if (raw == 0x00FF00FFu) tex[0] = tex[1] = tex[2] = tex[3] = -1.0f;
+		else {
+			float a = (float)(raw >> 24) * (1.0f / 255.0f);
+			for (int k = 0; k < 3; ++k) tex[k] = s2l((float)((raw >> (8 * k)) & 0xff) * (1.0f / 255.0f)) * a;
+			tex[3] = a;
+		}
+		float es = expf(0.6931471805599453f * 0.0f), tgt[3];
+		if (c->linear_colors || c->color_space_linear) {
+			for (int k = 0; k < 3; ++k) tgt[k] = es * tex[k] + (1.0f - tex[3]) * bg[k];
+			if (!c->linear_colors) for (int k = 0; k < 3; ++k) { tgt[k] = l2s(tgt[k]); bg[k] = l2s(bg[k]); }
+		} else {
+			for (int k = 0; k < 3; ++k) bg[k] = l2s(bg[k]);
+			if (tex[3] > 0) for (int k = 0; k < 3; ++k) tgt[k] = l2s(es * tex[k] / tex[3]) * tex[3] + (1.0f - tex[3]) * bg[k];
+			else for (int k = 0; k < 3; ++k) tgt[k] = bg[k];
+		}
+		if (cn == ns) for (int k = 0; k < 3; ++k) rgb_ray[k] += t * bg[k];
+		uint32_t cbase = ctotal;
+		ctotal += cn;
+		uint32_t mn = max_c < cbase ? max_c : cbase;
+		uint32_t cnum = (max_c - mn) < cn ? (max_c - mn) : cn;
+		numsteps[2 * i] = cnum;
+		numsteps[2 * i + 1] = cbase;
+		if (cnum == 0) continue;
+		float l[3], g[3];
+		for (int k = 0; k < 3; ++k) lossg(tgt[k], rgb_ray[k], c->loss_type, &l[k], &g[k]);
+		if (loss) loss[i] = ((l[0] + l[1] + l[2]) / 3.0f) / (float)n_rays;
+		float ls = loss_scale / (float)n_rays;
+		float l2reg = c->rgb_activation == 3 ? 1e-4f : 0.0f, l1d = mean_density < MIN_OPT ? 1e-4f : 0.0f;
+		const float* ray = rays + (size_t)i * 6;
+		float r2[3] = {0, 0, 0};
+		t = 1.0f;
+		for (uint32_t j = 0; j < cnum; ++j) {
+			const float* cc = ci + (size_t)j * 7;
+			memcpy(coords_out + (size_t)(cbase + j) * 7, cc, 7 * sizeof(float));
+			float pos[3], dd[3];
+			for (int k = 0; k < 3; ++k) { pos[k] = c->aabb_min[k] + cc[k] * diag[k]; dd[k] = pos[k] - ray[k]; }
+			float depth = sqrtf(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
+			float dt = cc[3] * (maxs - MIN_STEP) + MIN_STEP;
+			float ov[4], rgb[3];
+			for (int k = 0; k < 4; ++k) ov[k] = orc_f16_to_f32(o[j * 16 + k]);
+			for (int k = 0; k < 3; ++k) rgb[k] = to_rgb(ov[k], c->rgb_activation);
+			float dens = to_dens(ov[3], c->density_activation);
+			float alpha = 1.f - expf(-dens * dt), w = alpha * t;
+			for (int k = 0; k < 3; ++k) r2[k] += w * rgb[k];
+			t *= (1.0f - alpha);
+			float suf[3];
+			for (int k = 0; k < 3; ++k) suf[k] = rgb_ray[k] - r2[k];
+			uint16_t* dl = dloss + (size_t)(cbase + j) * 16;
+			for (int k = 0; k < 3; ++k)
+				dl[k] = orc_f32_to_f16(ls * (w * g[k] * to_rgb_d(ov[k], c->rgb_activation) + fmaxf(0.0f, l2reg * ov[k])));
+			float dotv = g[0] * (t * rgb[0] - suf[0]) + g[1] * (t * rgb[1] - suf[1]) + g[2] * (t * rgb[2] - suf[2]);
+			float dmlp = to_dens_d(ov[3], c->density_activation) * (dt * (dotv + 0.0f));
+			dl[3] = orc_f32_to_f16(ls * dmlp + (ov[3] < 0.0f ? -l1d : 0.0f) + (ov[3] > -10.0f && depth < c->near_distance ? 1e-4f : 0.0f));
+		}
+	}
+	*compacted_counter = ctotal;
+}
+
+/* generate_grid_samples_nerf_nonuniform (testbed_nerf.cu:635-676) */
+EXPORT void orc_nerf_grid_samples(const ocfg* c, uint32_t n, orc_pcg32 rng0, uint32_t step, const float* grid, uint32_t n_casc,
+                                  float thresh, float* out, uint32_t* indices) {
+	for (uint32_t i = 0; i < n; ++i) {
+		orc_pcg32 rng = rng0;
+		orc_pcg32_advance(&rng, (int64_t)i * 4);
+		uint32_t level = (uint32_t)(orc_pcg32_next_float(&rng) * n_casc) % n_casc, idx = 0;
+		for (uint32_t j = 0; j < 10; ++j) {
+			idx = ((i + step * n) * 56924617u + j * 19349663u + 96925573u) % N_CELLS;
+			idx += level * N_CELLS;
+			if (grid[idx] > thresh) break;
+		}
+		uint32_t p = idx % N_CELLS;
+		uint32_t x = orc_morton3D_invert(p), y = orc_morton3D_invert(p >> 1), z = orc_morton3D_invert(p >> 2);
+		float r[3];
+		for (int k = 0; k < 3; ++k) r[k] = orc_pcg32_next_float(&rng);
+		float s = scalbnf(1.0f, (int)level), xyz[3] = {(float)x, (float)y, (float)z};
+		for (int k = 0; k < 3; ++k) {
+			float pp = ((xyz[k] + r[k]) / (float)GRIDSIZE - 0.5f) * s + 0.5f;
+			out[(size_t)i * 3 + k] = (pp - c->aabb_min[k]) / (c->aabb_max[k] - c->aabb_min[k]);
+		}
+		indices[i] = idx;
+	}
+}
+
+/* splat (:678-702), ema (:731-754) */
+EXPORT void orc_nerf_grid_splat_ema(uint32_t n, const uint32_t* indices, const uint16_t* density16, uint32_t act, uint32_t n_el,
+                                    float decay, float* grid) {
+	float* tmp = (float*)calloc(n_el, sizeof(float));
+	for (uint32_t i = 0; i < n; ++i) {
+		float th = to_dens(orc_f16_to_f32(density16[i]), act) * scalbnf(MIN_STEP, 0);
+		if (th > tmp[indices[i]] || (tmp[indices[i]] == 0.f)) {
+			/* atomicMax on the uint bits: the same as a float max for non-negative values */
+			uint32_t a, b;
+			memcpy(&a, &th, 4);
+			memcpy(&b, &tmp[indices[i]], 4);
+			if (a > b) tmp[indices[i]] = th;
+		}
+	}
+	for (uint32_t i = 0; i < n_el; ++i) {
+		float prev = grid[i];
+		grid[i] = prev < 0.f ? prev : fmaxf(prev * decay, tmp[i]);
+	}
+	free(tmp);
+}
+
+/* update_density_grid_mean_and_bitfield (:3538-3567), grid_to_bitfield (:762-786), bitfield_max_pool
+ * (:788-809). The mean is order-dependent in the reference (reduce_sum); here it is an input. */
+EXPORT double orc_nerf_grid_mean(const float* grid) {
+	double s = 0.0;
+	for (uint32_t i = 0; i < N_CELLS; ++i) s += (double)(fmaxf(grid[i], 0.f) / (float)N_CELLS);
+	return s;
+}
+EXPORT void orc_nerf_grid_bitfield(const float* grid, uint32_t max_cascade, float mean, uint8_t* bf) {
+	uint32_t n_bytes = N_CELLS / 8 * CASCADES, n_nz = N_CELLS / 8 * (max_cascade + 1);
+	float th = fminf(MIN_OPT, mean);
+	for (uint32_t i = 0; i < n_bytes; ++i) {
+		if (i >= n_nz) { bf[i] = 0; continue; }
+		uint8_t b = 0;
+		for (uint32_t j = 0; j < 8; ++j) b |= grid[i * 8 + j] > th ? (uint8_t)(1u << j) : 0;
+		bf[i] = b;
+	}
+	for (uint32_t level = 1; level < CASCADES; ++level) {
+		const uint8_t* prev = bf + (size_t)(level - 1) * N_CELLS / 8;
+		uint8_t* next = bf + (size_t)level * N_CELLS / 8;
+		for (uint32_t i = 0; i < N_CELLS / 64; ++i) {
+			uint8_t b = 0;
+			for (uint32_t j = 0; j < 8; ++j) b |= prev[i * 8 + j] > 0 ? (uint8_t)(1u << j) : 0;
+			uint32_t x = orc_morton3D_invert(i) + GRIDSIZE / 8, y = orc_morton3D_invert(i >> 1) + GRIDSIZE / 8,
+			         z = orc_morton3D_invert(i >> 2) + GRIDSIZE / 8;
+			next[orc_morton3D(x, y, z)] |= b;
+		}
+	}
+}
+
+/* tcnn fill_rollover(_and_rescale) */
+EXPORT void orc_fill_rollover_f32(uint32_t n_el, uint32_t stride, uint32_t n_in, float* d) {
+	if (n_in == 0) return;
+	for (uint32_t i = n_in * stride; i < n_el * stride; ++i) d[i] = d[i % (n_in * stride)];
+}
+EXPORT void orc_fill_rollover_f16(uint32_t n_el, uint32_t stride, uint32_t n_in, uint16_t* d, int rescale) {
+	if (n_in == 0) return;
+	for (uint32_t i = n_in * stride; i < n_el * stride; ++i) {
+		uint16_t r = d[i % (n_in * stride)];
+		if (rescale) r = orc_f32_to_f16(orc_f16_to_f32(r) * n_in / n_el);
+		d[i] = r;
+	}
+}

@@ -567,17 +567,7 @@ EXPORT void orc_adam_step(const orc_adam_cfg* c, uint32_t step, size_t n, size_t
 /* ------------------------------------------------------------------------------------------------
  * NeRF helpers restated from the reference (src/testbed_nerf.cu, common_device.cuh).
  * ---------------------------------------------------------------------------------------------- */
-/* tcnn morton3D (used via cascaded_grid_idx_at, src/testbed_nerf.cu:433-447) */
-static inline uint32_t expand_bits(uint32_t v) {
-	v = (v * 0x00010001u) & 0xFF0000FFu;
-	v = (v * 0x00000101u) & 0x0F00F00Fu;
-	v = (v * 0x00000011u) & 0xC30C30C3u;
-	v = (v * 0x00000005u) & 0x49249249u;
-	return v;
-}
-EXPORT uint32_t orc_morton3D(uint32_t x, uint32_t y, uint32_t z) {
-	return (expand_bits(x) << 2) | (expand_bits(y) << 1) | expand_bits(z);
-}
+/* morton3D lives in ngp_nerf_oracle.c with the occupancy-grid restatement. */
 
 /* common_device.cuh:75-121 */
 EXPORT float orc_srgb_to_linear(float srgb) {

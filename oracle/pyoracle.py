@@ -94,6 +94,7 @@ def _declare(L):
     d("orc_srgb_to_linear", f32, f32)
     d("orc_linear_to_srgb", f32, f32)
     d("orc_num_threads", C.c_int)
+    _declare_nerf(L)
 
 
 def ptr(a):
@@ -262,3 +263,114 @@ def nerf_backward(m, params16, coords, dL_dout, want_denc=False):
 def adam_step(cfg, step, n_matrix, loss_scale, w32, w16, g16, m1, m2, steps, ema32=None, ema16=None):
     lib().orc_adam_step(C.byref(cfg), step, w32.size, n_matrix, loss_scale, ptr(w32), ptr(w16), ptr(g16), ptr(m1),
                         ptr(m2), ptr(steps), ptr(ema32), ptr(ema16))
+
+
+# ---------------------------------------------------------------------------------------------
+# NeRF training kernels (oracle/ngp_nerf_oracle.c). cfg / images are ctypes structures with the
+# layout of ngp_nerf_config / ngp_nerf_image (include/ngp_engine.h); they are passed by address.
+# ---------------------------------------------------------------------------------------------
+def _declare_nerf(L):
+    def d(name, res, *args):
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = list(args)
+    u32, f32 = C.c_uint32, C.c_float
+    d("orc_morton3D_invert", u32, u32)
+    d("orc_camera_matrix", None, P, P)
+    d("orc_nerf_generate_samples", None, P, P, P, u32, u32, u32, u32, Pcg32, u32, P, P, P, P, P, P)
+    d("orc_nerf_compute_loss", None, P, P, P, u32, u32, u32, Pcg32, u32, u32, P, P, P, P, P, P, P, P, P, f32, f32)
+    d("orc_nerf_grid_samples", None, P, u32, Pcg32, u32, P, u32, f32, P, P)
+    d("orc_nerf_grid_splat_ema", None, u32, P, P, u32, u32, f32, P)
+    d("orc_nerf_grid_mean", C.c_double, P)
+    d("orc_nerf_grid_bitfield", None, P, u32, f32, P)
+    d("orc_fill_rollover_f32", None, u32, u32, u32, P)
+    d("orc_fill_rollover_f16", None, u32, u32, u32, P, C.c_int)
+
+
+N_CELLS = 128 ** 3
+
+
+def _images_arg(images):
+    arr_t = type(images[0]) * len(images)
+    return arr_t(*images)
+
+
+def _pixels_arg(pixels):
+    pix = [np.ascontiguousarray(p, dtype=np.uint8) for p in pixels]
+    return pix, (C.c_void_p * len(pix))(*[p.ctypes.data for p in pix])
+
+
+def pcg(state, inc):
+    return Pcg32(state, inc)
+
+
+def camera_matrix(xform12):
+    out = np.zeros(12, np.float32)
+    lib().orc_camera_matrix(ptr(np.ascontiguousarray(xform12, np.float32)), ptr(out))
+    return out
+
+
+def nerf_generate_samples(cfg, images, pixels, n_rays, rng, max_samples, bitfield, ray_offset=0, n_div=None):
+    ims = _images_arg(images)
+    keep, pix = _pixels_arg(pixels)
+    out = {
+        "ray_indices": np.zeros(n_rays, np.uint32), "rays": np.zeros((n_rays, 6), np.float32),
+        "numsteps": np.zeros((n_rays, 2), np.uint32), "coords": np.zeros((max_samples, 7), np.float32),
+        "counters": np.zeros(2, np.uint32),
+    }
+    lib().orc_nerf_generate_samples(C.byref(cfg), ims, pix, len(images), n_rays, ray_offset, n_div or n_rays, rng,
+                                    max_samples, ptr(np.ascontiguousarray(bitfield, np.uint8)), ptr(out["ray_indices"]),
+                                    ptr(out["rays"]), ptr(out["numsteps"]), ptr(out["coords"]), ptr(out["counters"]))
+    del keep
+    return out
+
+
+def nerf_compute_loss(cfg, images, pixels, n_rays, rng, max_compacted, samples, out16, mean_density, loss_scale=128.0,
+                      n_div=None):
+    """samples: dict from nerf_generate_samples (numpy; its numsteps is rewritten in place)."""
+    ims = _images_arg(images)
+    keep, pix = _pixels_arg(pixels)
+    res = {
+        "coords_compacted": np.zeros((max_compacted, 7), np.float32),
+        "dloss_doutput": np.zeros((max_compacted, 16), np.uint16),
+        "loss": np.zeros(n_rays, np.float32), "compacted_counter": np.zeros(1, np.uint32),
+    }
+    lib().orc_nerf_compute_loss(C.byref(cfg), ims, pix, len(images), n_rays, n_div or n_rays, rng, max_compacted,
+                                int(samples["counters"][0]), ptr(np.ascontiguousarray(out16, np.uint16)),
+                                ptr(samples["ray_indices"]), ptr(samples["rays"]), ptr(samples["numsteps"]),
+                                ptr(samples["coords"]), ptr(res["coords_compacted"]), ptr(res["dloss_doutput"]),
+                                ptr(res["loss"]), ptr(res["compacted_counter"]), float(mean_density), float(loss_scale))
+    del keep
+    return res
+
+
+def nerf_grid_samples(cfg, n, rng, step, grid, n_cascades, thresh):
+    pos = np.zeros((n, 3), np.float32)
+    idx = np.zeros(n, np.uint32)
+    lib().orc_nerf_grid_samples(C.byref(cfg), n, rng, step, ptr(np.ascontiguousarray(grid, np.float32)), n_cascades,
+                                thresh, ptr(pos), ptr(idx))
+    return pos, idx
+
+
+def nerf_grid_splat_ema(indices, density16, act, grid, decay=0.95):
+    """density16: fp16 bits of the density output (one per sample). Updates grid (float32) in place."""
+    lib().orc_nerf_grid_splat_ema(indices.size, ptr(np.ascontiguousarray(indices, np.uint32)),
+                                  ptr(np.ascontiguousarray(density16, np.uint16)), act, grid.size, decay, ptr(grid))
+
+
+def nerf_grid_mean(grid):
+    return lib().orc_nerf_grid_mean(ptr(np.ascontiguousarray(grid, np.float32)))
+
+
+def nerf_grid_bitfield(grid, max_cascade, mean):
+    bf = np.zeros(N_CELLS // 8 * 8, np.uint8)
+    lib().orc_nerf_grid_bitfield(ptr(np.ascontiguousarray(grid, np.float32)), max_cascade, mean, ptr(bf))
+    return bf
+
+
+def fill_rollover(data, n_in, rescale=False):
+    n, stride = data.shape
+    if data.dtype == np.float32:
+        lib().orc_fill_rollover_f32(n, stride, n_in, ptr(data))
+    else:
+        lib().orc_fill_rollover_f16(n, stride, n_in, ptr(data), int(rescale))

@@ -1,0 +1,204 @@
+"""GPU parity of the NeRF training kernels (src/testbed_nerf.cu) against oracle/ngp_nerf_oracle.c.
+
+Bars: sample generation (ray indices, per-ray step counts and bases, ray origins/directions, sample
+coordinates) bit-exact with cone_angle 0 (no transcendental on that path; slots from prefix scans
+equal the oracle's ray-order slots); density-grid sample positions/indices and bitfields bit-exact;
+rollover bit-exact. Compositing uses __expf like the reference (testbed_nerf.cu:1744), so the loss
+pass is compared within 1e-4 relative (loss), fp16 gradients within 2e-3 of their scale, and the
+early-termination count may differ on at most 0.5 % of rays.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    from __graft_entry__ import load_package
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return load_package()
+
+
+@pytest.fixture(scope="module")
+def scene(pkg):
+    S = pkg.synthetic
+    ims, pix = [], []
+    for i, c2w in enumerate(S.camera_poses(6, seed=1)):
+        w, h = 96 + 8 * i, 80 + 4 * i  # ragged image sizes
+        ims.append(pkg.nerf.make_image(w, h, pkg.nerf.nerf_matrix_to_ngp(c2w), camera_angle_x=S.LEGO_CAMERA_ANGLE_X))
+        px = S.render(c2w, w, h)
+        px[3:5, 7:40] = np.array([255, 0, 255, 0], np.uint8)  # masked pixels (0x00FF00FF)
+        pix.append(px)
+    ds = pkg.nerf.NerfDataset(ims, pix)
+    return ds, ims, pix
+
+
+def occupancy(orc, seed=0, frac=0.3, max_cascade=0):
+    g = np.random.default_rng(seed)
+    grid = np.where(g.random(128 ** 3 * 8) < frac, 1.0, 0.0).astype(np.float32)
+    return grid, orc.nerf_grid_bitfield(grid, max_cascade, 0.005)
+
+
+def rng(pkg, seed):
+    r = pkg.nerf.pcg32(seed)
+    return r
+
+
+def orc_rng(orc, r):
+    return orc.pcg(r.state, r.inc)
+
+
+@pytest.mark.parametrize("n_rays,max_samples,frac", [(1, 4096, 1.0), (777, 1 << 16, 0.3), (4096, 1 << 15, 0.5),
+                                                     (4096, 1 << 18, 0.02)])
+def test_generate_training_samples_bitexact(pkg, orc, scene, n_rays, max_samples, frac):
+    ds, ims, pix = scene
+    cfg = pkg.nerf.default_config(1.0)
+    _, bf = occupancy(orc, seed=n_rays, frac=frac)
+    r = rng(pkg, 1337 + n_rays)
+    got = pkg.nerf.generate_training_samples(ds, cfg, n_rays, r, max_samples, torch.from_numpy(bf).cuda(),
+                                             n_rays_total=n_rays)
+    ref = orc.nerf_generate_samples(cfg, ims, pix, n_rays, orc_rng(orc, r), max_samples, bf)
+    got = {k: v.cpu().numpy() for k, v in got.items()}
+    np.testing.assert_array_equal(got["counters"].view(np.uint32), ref["counters"])
+    kept = int(ref["counters"][0])
+    assert kept > 0
+    np.testing.assert_array_equal(got["ray_indices"][:kept].view(np.uint32), ref["ray_indices"][:kept])
+    np.testing.assert_array_equal(got["numsteps"][:kept].view(np.uint32), ref["numsteps"][:kept])
+    np.testing.assert_array_equal(got["rays"][:kept], ref["rays"][:kept])
+    used = min(int(ref["counters"][1]), max_samples)
+    np.testing.assert_array_equal(got["coords"][:used], ref["coords"][:used])
+
+
+def test_generate_training_samples_cone(pkg, orc, scene):
+    """aabb_scale 4: cone-angle stepping (logf/expf) and cascades 0..2. An ulp of logf/expf moves t and
+    can flip a voxel-boundary decision further along the ray, so per-ray counts agree on >= 90 % of rays
+    (measured 94 %) and the batch total within 1 %."""
+    ds, ims, pix = scene
+    cfg = pkg.nerf.default_config(4.0)
+    _, bf = occupancy(orc, seed=5, frac=0.4, max_cascade=cfg.max_cascade)
+    r = rng(pkg, 99)
+    n = 2048
+    got = pkg.nerf.generate_training_samples(ds, cfg, n, r, 1 << 20, torch.from_numpy(bf).cuda())
+    ref = orc.nerf_generate_samples(cfg, ims, pix, n, orc_rng(orc, r), 1 << 20, bf)
+    c_got = got["counters"].cpu().numpy().view(np.uint32)
+    assert c_got[0] == ref["counters"][0]
+    assert abs(int(c_got[1]) - int(ref["counters"][1])) <= 0.01 * ref["counters"][1]
+    kept = int(ref["counters"][0])
+    np.testing.assert_array_equal(got["ray_indices"].cpu().numpy()[:kept].view(np.uint32), ref["ray_indices"][:kept])
+    steps_got = got["numsteps"].cpu().numpy()[:kept, 0].view(np.uint32)
+    assert np.mean(steps_got == ref["numsteps"][:kept, 0]) > 0.90
+
+
+@pytest.mark.parametrize("loss_type,act", [(4, 3), (0, 2), (1, 3)])
+def test_compute_loss(pkg, orc, scene, loss_type, act):
+    ds, ims, pix = scene
+    cfg = pkg.nerf.default_config(1.0, loss_type=loss_type, rgb_activation=act, density_activation=3)
+    _, bf = occupancy(orc, seed=2, frac=0.5)
+    n_rays, max_samples = 2000, 1 << 16
+    r = rng(pkg, 7)
+    samples = pkg.nerf.generate_training_samples(ds, cfg, n_rays, r, max_samples, torch.from_numpy(bf).cuda())
+    ref_s = orc.nerf_generate_samples(cfg, ims, pix, n_rays, orc_rng(orc, r), max_samples, bf)
+    g = np.random.default_rng(loss_type)
+    out = g.uniform(-3.0, 2.0, (max_samples, 16)).astype(np.float16)
+    out_t = torch.from_numpy(out).cuda()
+    mean = torch.tensor([0.003], device="cuda")
+    max_c = 1 << 15
+    got = pkg.nerf.compute_loss(ds, cfg, n_rays, r, max_c, samples, out_t, mean)
+    ref = orc.nerf_compute_loss(cfg, ims, pix, n_rays, orc_rng(orc, r), max_c, ref_s, out.view(np.uint16), 0.003)
+    kept = int(ref_s["counters"][0])
+    ns_got = samples["numsteps"].cpu().numpy()[:kept].view(np.uint32)
+    ns_ref = ref_s["numsteps"][:kept]
+    same = ns_got[:, 0] == ns_ref[:, 0]
+    assert same.mean() >= 0.995
+    cc = int(got["compacted_counter"].cpu().numpy().view(np.uint32)[0])
+    assert abs(cc - int(ref["compacted_counter"][0])) <= 0.005 * int(ref["compacted_counter"][0]) + 4
+    loss_got = got["loss"].cpu().numpy()[:kept]
+    np.testing.assert_allclose(loss_got[same], ref["loss"][:kept][same], rtol=1e-4, atol=1e-9)
+    # per-sample gradients of rays whose compacted range matches exactly
+    dl_got = got["dloss_doutput"].cpu().numpy().astype(np.float32)
+    dl_ref = orc.f16_bits_to_f32(ref["dloss_doutput"])
+    co_got = got["coords_compacted"].cpu().numpy()
+    scale = np.abs(dl_ref[:, :4]).max()
+    n_checked = 0
+    for i in np.nonzero(same & (ns_got[:, 1] == ns_ref[:, 1]))[0][:400]:
+        n, b = int(ns_ref[i, 0]), int(ns_ref[i, 1])
+        if n == 0:
+            continue
+        np.testing.assert_allclose(dl_got[b:b + n, :4], dl_ref[b:b + n, :4], atol=2e-3 * scale, rtol=2e-3)
+        np.testing.assert_array_equal(co_got[b:b + n], ref["coords_compacted"][b:b + n])
+        n_checked += 1
+    assert n_checked > 50
+
+
+@pytest.mark.parametrize("dtype,rescale", [(torch.float32, False), (torch.float16, False), (torch.float16, True)])
+def test_fill_rollover(pkg, orc, dtype, rescale):
+    g = np.random.default_rng(1)
+    n, stride, n_in = 1000, 7 if dtype == torch.float32 else 16, 333
+    a = g.standard_normal((n, stride)).astype(np.float32 if dtype == torch.float32 else np.float16)
+    t = torch.from_numpy(a.copy()).cuda()
+    pkg.nerf.fill_rollover(t, torch.tensor([n_in], dtype=torch.int32, device="cuda"), rescale=rescale)
+    ref = a.copy() if dtype == torch.float32 else a.view(np.uint16).copy()
+    orc.fill_rollover(ref, n_in, rescale)
+    got = t.cpu().numpy()
+    np.testing.assert_array_equal(got if dtype == torch.float32 else got.view(np.uint16), ref)
+
+
+def test_density_grid_update(pkg, orc):
+    cfg = pkg.nerf.default_config(4.0)
+    g = np.random.default_rng(3)
+    grid = np.where(g.random(128 ** 3 * 8) < 0.5, g.random(128 ** 3 * 8) * 0.02, 0.0).astype(np.float32)
+    grid[:1000] = -1.0  # untrained cells stay negative through the EMA
+    n_casc = cfg.max_cascade + 1
+    n = 128 ** 3 * n_casc // 4
+    r = rng(pkg, 11)
+    grid_t = torch.from_numpy(grid).cuda()
+    pos, idx = pkg.nerf.grid_generate_samples(cfg, n, r, 3, grid_t, n_casc, 0.01)
+    pos_ref, idx_ref = orc.nerf_grid_samples(cfg, n, orc_rng(orc, r), 3, grid, n_casc, 0.01)
+    np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), idx_ref)
+    np.testing.assert_array_equal(pos.cpu().numpy(), pos_ref)
+    dens = g.uniform(-8, 3, (n, 16)).astype(np.float16)
+    tmp = torch.zeros_like(grid_t)
+    # the density network output is row-major [16 x n] (feature-major), density in row 0 (testbed_nerf.cu:3488-3496)
+    pkg.nerf.grid_splat_max(idx, torch.from_numpy(np.ascontiguousarray(dens.T)).cuda(), 3, tmp)
+    pkg.nerf.grid_ema(0.95, grid_t, tmp)
+    ref_grid = grid.copy()
+    orc.nerf_grid_splat_ema(idx_ref, dens[:, 0].copy().view(np.uint16), 3, ref_grid, 0.95)
+    got = grid_t.cpu().numpy()
+    np.testing.assert_allclose(got, ref_grid, rtol=1e-5, atol=0)
+    mean, bf = pkg.nerf.grid_mean_and_bitfield(grid_t, cfg.max_cascade)
+    m = float(mean[0].item())
+    assert m == pytest.approx(orc.nerf_grid_mean(got), rel=1e-5)
+    np.testing.assert_array_equal(bf.cpu().numpy(), orc.nerf_grid_bitfield(got, cfg.max_cascade, m))
+
+
+def test_nerf_training_end_to_end(pkg, orc):
+    """Testbed-style training on the procedural scene: loss falls, occupancy grid prunes, the
+    bitfield agrees with the oracle's restatement of the trainer's own density grid."""
+    ds = pkg.synthetic.lego_like_dataset(n_images=12, width=128, height=128, seed=2)
+    cfg = pkg.nerf.default_config(1.0)
+    net = pkg.create_nerf_network(pkg.nerf_config("C2"))
+    tr = pkg.Trainer(net, pkg.nerf_config("C2")["optimizer"])
+    run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
+    losses, stats = [], []
+    for _ in range(700):
+        s = run.train_step(get_loss=True)
+        stats.append(s)
+        losses.append(s["loss"])
+    assert stats[-1]["step"] == 700
+    assert all(np.isfinite(losses))
+    assert np.mean(losses[-20:]) < 0.5 * np.mean(losses[:20])
+    # compacted count before clamping to the batch (testbed_nerf.cu:3598); rays_per_batch adapts toward it
+    assert 0 < stats[-1]["measured_batch_size"] <= stats[-1]["measured_batch_size_before_compaction"]
+    assert stats[-1]["rays_per_batch"] % 256 == 0
+    grid = run.density_grid.cpu().numpy()
+    m = float(run.mean_density.cpu().numpy()[0])
+    bf = run.bitfield.cpu().numpy()
+    assert grid.size == 128 ** 3 * (cfg.max_cascade + 1)
+    full = np.zeros(128 ** 3 * 8, np.float32)
+    full[:grid.size] = grid
+    np.testing.assert_array_equal(bf, orc.nerf_grid_bitfield(full, cfg.max_cascade, m))
+    occupied = np.unpackbits(bf[:128 ** 3 // 8]).mean()
+    assert 0.0 < occupied < 0.5  # the grid prunes once step >= 256 switches to the 0.01 threshold (:3518)

@@ -1,0 +1,109 @@
+"""CPU tests of the NeRF host side and of the NeRF oracle's own invariants (no GPU calls)."""
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    from __graft_entry__ import load_package
+    return load_package()
+
+
+def test_default_config_matches_reference_defaults(pkg):
+    c = pkg.nerf.default_config(1.0)
+    assert list(c.aabb_min) == [0, 0, 0] and list(c.aabb_max) == [1, 1, 1]
+    assert c.cone_angle_constant == 0.0 and c.max_cascade == 0
+    assert (c.snap_to_pixel_centers, c.random_bg_color, c.linear_colors, c.color_space_linear) == (1, 1, 0, 1)
+    assert (c.rgb_activation, c.density_activation, c.loss_type) == (3, 3, 4)
+    assert c.near_distance == pytest.approx(0.1) and c.target_batch_size == 1 << 18
+    c = pkg.nerf.default_config(16.0)
+    assert list(c.aabb_min) == [-7.5] * 3 and list(c.aabb_max) == [8.5] * 3
+    assert c.max_cascade == 4 and c.cone_angle_constant == pytest.approx(1 / 256)
+    c = pkg.nerf.default_config(256.0)  # inflation capped at 2^(cascades-1) = 128 (testbed_nerf.cu:3093)
+    assert list(c.aabb_max) == [64.5] * 3 and c.max_cascade == 8
+    c = pkg.nerf.default_config(2.0, loss_type=0, background_color=(1, 0.5, 0))
+    assert c.loss_type == 0 and list(c.background_color) == [1, 0.5, 0]
+
+
+def test_pcg32_seeding_matches_oracle(pkg, orc):
+    r = pkg.nerf.pcg32(1337)
+    o = orc.Rng(1337)
+    assert (r.state, r.inc) == (o.s.state, o.s.inc)
+
+
+def test_nerf_matrix_to_ngp(pkg):
+    m = np.eye(4)
+    m[:3, 3] = [1.0, 2.0, 3.0]
+    x = pkg.nerf.nerf_matrix_to_ngp(m).reshape(4, 3)  # columns
+    # column 1/2 negated, translation scaled + offset, rows cycled xyz <- yzx
+    np.testing.assert_allclose(x[0], [0, 0, 1])
+    np.testing.assert_allclose(x[1], [-1, 0, 0])
+    np.testing.assert_allclose(x[2], [0, -1, 0])
+    np.testing.assert_allclose(x[3], [2 * 0.33 + 0.5, 3 * 0.33 + 0.5, 1 * 0.33 + 0.5], rtol=1e-6)
+
+
+def test_camera_matrix_of_rotation_is_identity_map(pkg, orc):
+    S = pkg.synthetic
+    for c2w in S.camera_poses(5, seed=4):
+        x = pkg.nerf.nerf_matrix_to_ngp(c2w)
+        np.testing.assert_allclose(orc.camera_matrix(x), x, atol=2e-6)
+
+
+def test_synthetic_render(pkg):
+    S = pkg.synthetic
+    px = S.render(S.camera_poses(1)[0], 64, 48)
+    assert px.shape == (48, 64, 4) and px.dtype == np.uint8
+    a = px[..., 3]
+    assert 0.05 < (a == 255).mean() < 0.9 and set(np.unique(a)) <= {0, 255}
+    assert (px[a == 0][:, :3] == 0).all()
+
+
+def _scene(pkg, n=3, w=40, h=30):
+    S = pkg.synthetic
+    ims, pix = [], []
+    for c2w in S.camera_poses(n, seed=9):
+        ims.append(pkg.nerf.make_image(w, h, pkg.nerf.nerf_matrix_to_ngp(c2w), camera_angle_x=S.LEGO_CAMERA_ANGLE_X))
+        pix.append(S.render(c2w, w, h))
+    return ims, pix
+
+
+def test_oracle_sampler_invariants(pkg, orc):
+    ims, pix = _scene(pkg)
+    cfg = pkg.nerf.default_config(1.0)
+    full = np.full(128 ** 3, 1.0, np.float32)
+    bf = orc.nerf_grid_bitfield(np.concatenate([full] + [np.zeros_like(full)] * 7), 0, 0.005)
+    out = orc.nerf_generate_samples(cfg, ims, pix, 64, orc.pcg(*_st(pkg.nerf.pcg32(5))), 1 << 16, bf)
+    kept, total = out["counters"]
+    assert 0 < kept <= 64
+    ns = out["numsteps"][:kept]
+    assert ns[:, 0].sum() == total and (ns[:, 1] == np.concatenate([[0], np.cumsum(ns[:-1, 0])])).all()
+    c = out["coords"][:total]
+    assert (c[:, :3] >= 0).all() and (c[:, :3] <= 1).all()
+    np.testing.assert_allclose(c[:, 3], 0.0, atol=1e-6)  # dt = MIN_CONE_STEPSIZE at cone 0 -> warped 0
+    assert (np.diff(out["ray_indices"][:kept].astype(np.int64)) > 0).all()
+    empty = orc.nerf_generate_samples(cfg, ims, pix, 64, orc.pcg(*_st(pkg.nerf.pcg32(5))), 1 << 16, np.zeros_like(bf))
+    assert list(empty["counters"]) == [0, 0]
+
+
+def _st(r):
+    return r.state, r.inc
+
+
+def test_oracle_bitfield_max_pool(orc):
+    g = np.zeros(128 ** 3 * 8, np.float32)
+    x, y, z = 70, 3, 127
+    g[orc.lib().orc_morton3D(x, y, z)] = 1.0
+    bf = orc.nerf_grid_bitfield(g, 0, 0.005)
+    bits = np.unpackbits(bf, bitorder="little").reshape(8, -1)
+    assert bits[0].sum() == 1
+    for level in range(1, 8):
+        assert bits[level].sum() == 1
+        x, y, z = x // 2 + 32, y // 2 + 32, z // 2 + 32
+        assert bits[level][orc.lib().orc_morton3D(x, y, z)] == 1
+
+
+def test_oracle_rollover(orc):
+    a = np.arange(40, dtype=np.float32).reshape(10, 4)
+    orc.fill_rollover(a, 3)
+    np.testing.assert_array_equal(a[3:6], a[0:3])
+    np.testing.assert_array_equal(a[9], a[0])

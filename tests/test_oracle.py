@@ -288,9 +288,14 @@ def test_lr_schedule(orc):
 
 
 def test_morton_and_srgb(orc):
-    assert orc.lib().orc_morton3D(1, 0, 0) == 4
+    # x in bit 0: morton3D_invert(i) / (i >> 1) / (i >> 2) recovers x / y / z (testbed_nerf.cu:518-520)
+    assert orc.lib().orc_morton3D(1, 0, 0) == 1
     assert orc.lib().orc_morton3D(0, 1, 0) == 2
-    assert orc.lib().orc_morton3D(0, 0, 1) == 1
+    assert orc.lib().orc_morton3D(0, 0, 1) == 4
     assert orc.lib().orc_morton3D(127, 127, 127) == 128 ** 3 - 1
+    inv = orc.lib().orc_morton3D_invert
+    for x, y, z in [(3, 77, 120), (127, 0, 64), (5, 5, 5)]:
+        i = orc.lib().orc_morton3D(x, y, z)
+        assert (inv(i), inv(i >> 1), inv(i >> 2)) == (x, y, z)
     for v in [0.0, 0.01, 0.04045, 0.5, 1.0]:
         assert orc.lib().orc_linear_to_srgb(orc.lib().orc_srgb_to_linear(v)) == pytest.approx(v, abs=1e-3)
