@@ -2,7 +2,7 @@
 
 A step = one NerfNetwork training pass over one synthetic batch of B = 2^18 samples per GPU:
 hash-grid encoding forward -> fused density+rgb MLP forward/backward (MFMA) -> hash-grid backward
-(packed fp16 atomics) -> [RCCL all-reduce of the fp16 gradient buffer when N > 1] -> fused
+(destination-bucketed exact reduction; its histogram overlaps the forward on a side stream) -> [RCCL all-reduce of the fp16 gradient buffer when N > 1] -> fused
 Adam/EMA optimizer step. Config C2 = the fork's configs/nerf/base.json (L=4, F=4, T=2^19,
 64-wide MLPs, fp16) — BASELINE.json configs[1]. Inputs are resident in HBM before timing starts.
 
@@ -135,6 +135,7 @@ def main():
         roof = {
             "grid_forward": ("hbm", a["enc_fwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
             "grid_backward": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
+            "grid_backward_sorted": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
             "mlp_train": ("mfma", a["mlp_train_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
         }
         dom = max((k for k in roof if k in per_kernel), key=lambda k: per_kernel[k])

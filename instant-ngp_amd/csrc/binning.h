@@ -13,7 +13,7 @@ struct WinPlan {
 	uint32_t n_bins = 0;   // R^D
 	uint32_t n_win = 0;    // levels 0..n_win-1 are accumulated in LDS windows
 	uint32_t W[16] = {};   // window width (vertices per axis) per level
-	uint32_t voff[17] = {};// window vertex offsets in LDS
+	uint32_t max_verts = 0;// largest window (vertices); LDS holds one level's window at a time
 	uint32_t debug = 0;    // timing experiments only: 1 skip accumulate, 2 skip flush
 };
 
@@ -27,11 +27,11 @@ struct WinArgs {
 	uint32_t n_hist_blocks;
 	uint32_t R, n_bins, n_win;
 	uint32_t W[16];
-	uint32_t voff[17];
 	uint32_t debug;
 };
 
 // Choose R and the windowed level prefix by a request-count cost model (0 windowed levels => none).
+// lds_budget_bytes bounds one level's window (int32 fixed point, F per vertex).
 WinPlan make_win_plan(const GridDesc& g, uint32_t n, size_t lds_budget_bytes);
 inline uint32_t bin_hist_len(const WinPlan& p, uint32_t n) { return p.n_bins * ((n + BIN_BLOCK - 1) / BIN_BLOCK); }
 // workspace (u32 count) for bin_samples' histogram + scanned offsets + scan temp; sorted: [n] u32

@@ -13,6 +13,7 @@
 #include "../../include/ngp_engine.h"
 #include "common.h"
 #include "binning.h"
+#include "grid_scatter.h"
 #include "grid.h"
 #include "json.h"
 #include "mlp.h"
@@ -128,18 +129,53 @@ struct ngp_model {
 	uint64_t mlp0_params = 0, mlp1_params = 0, grid_params = 0, n_params = 0;
 	FragDesc* d_descs = nullptr;
 	uint32_t n_all_frags = 0;
-	DevBuf frags, frags_inf, enc, denc, slabs, bin_hist, bin_sorted;
-	int grid_backward_mode = 0;  // 0 auto, 1 direct (tcnn-style), 2 windowed (binned LDS)
-	uint32_t win_debug = 0;      // timing experiments only (see binning.h)
+	DevBuf frags, frags_inf, enc, denc, slabs, bin_hist, bin_sorted, scatter_ws;
+	int grid_backward_mode = 0;  // 0 auto, 1 direct (tcnn-style), 2 windowed (binned LDS), 3 bucketed (grid_scatter.h)
+	uint32_t win_debug = 0;      // timing experiments only (see binning.h, grid_scatter.h)
 	WinPlan win_plan;
 	uint32_t win_plan_n = 0;
+	ScatterPlan sc_plan;
+	uint32_t sc_plan_n = 0;
+	bool sc_prepared = false;               // phase 1 of the bucketed backward already enqueued (side stream)
+	hipStream_t side = nullptr;             // overlaps the bucket histogram with forward + MLP
+	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 	f16 *params = nullptr, *inference_params = nullptr, *gradients = nullptr;
 	float max_level = 1.0f;
 	const float* max_level_per_sample = nullptr;
 	uint64_t generation = 0;
 	std::unique_ptr<ngp_ctx> last_ctx;
 
-	~ngp_model() { if (d_descs) (void)hipFree(d_descs); }
+	~ngp_model() {
+		if (d_descs) (void)hipFree(d_descs);
+		if (ev_fork) (void)hipEventDestroy(ev_fork);
+		if (ev_join) (void)hipEventDestroy(ev_join);
+		if (side) (void)hipStreamDestroy(side);
+	}
+	bool use_sorted(uint32_t n) const { return grid_backward_mode == 3 || (grid_backward_mode == 0 && n >= 4096); }
+	void* sorted_workspace(uint32_t n) {
+		if (sc_plan_n != n) { sc_plan = make_scatter_plan(grid, n); sc_plan_n = n; }
+		return scatter_ws.get(sc_plan.total);
+	}
+	// Phase 1 of the bucketed grid backward on a side stream: it only needs the positions, so it runs
+	// concurrently with the forward encoding and the MLP; train_pass joins before the scatter.
+	void prepare_grid_backward_async(hipStream_t s, uint32_t n, const float* in, uint32_t stride) {
+		if (!use_sorted(n)) return;
+		if (!side) {
+			NGP_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+			NGP_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+			NGP_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+		}
+		void* ws = sorted_workspace(n);
+		GridBwdArgs b{n, in, stride, nullptr, 0, AoS, nullptr, max_level, max_level_per_sample};
+		NGP_HIP(hipEventRecord(ev_fork, s));
+		NGP_HIP(hipStreamWaitEvent(side, ev_fork, 0));
+		{
+			ProfScope ps("grid_bwd_prepare", side);
+			grid_scatter_prepare(grid, b, sc_plan, ws, side);
+		}
+		NGP_HIP(hipEventRecord(ev_join, side));
+		sc_prepared = true;
+	}
 
 	const std::vector<FragDesc>& descs() const { return nerf ? nplan.descs : mplan.descs; }
 	uint64_t grid_offset() const { return mlp0_params + mlp1_params; }
@@ -206,22 +242,34 @@ struct ngp_model {
 			ProfScope ps("reduce_slabs", s);
 			reduce_slabs(slab, blocks, (uint32_t)n_matrix(), gradients, grad_mode == NGP_GRAD_ACCUMULATE, s);
 		}
-		if (grad_mode != NGP_GRAD_ACCUMULATE) {
-			ProfScope ps("grid_grad_zero", s);
-			NGP_HIP(hipMemsetAsync(gradients + grid_offset(), 0, grid_params * sizeof(f16), s));
-		}
 		GridBwdArgs b{n, in, stride, dL_denc, enc_width, AoS, gradients + grid_offset(), max_level, max_level_per_sample};
-		scatter_grid_grad(s, b);
+		scatter_grid_grad(s, b, grad_mode != NGP_GRAD_ACCUMULATE);
 	}
 	// Hash-grid backward: windowed (spatial bins + LDS) for the coarse levels when it pays, direct
 	// packed-f16 atomics for the rest. The windowed path needs all levels active (max_level >= 1).
-	void scatter_grid_grad(hipStream_t s, GridBwdArgs b) {
-		// auto: windowed only where it measured faster (F=2: C2' 774 vs 911 us; F=4: C2 257 vs 240 us)
-		const bool want_win = grid_backward_mode == 2 || (grid_backward_mode == 0 && grid.n_features == 2);
+	void scatter_grid_grad(hipStream_t s, GridBwdArgs b, bool overwrite) {
+		if (use_sorted(b.n)) {
+			void* ws = sorted_workspace(b.n);
+			if (sc_prepared) {
+				NGP_HIP(hipStreamWaitEvent(s, ev_join, 0));
+				sc_prepared = false;
+			} else {
+				ProfScope ps("grid_bwd_prepare", s);
+				grid_scatter_prepare(grid, b, sc_plan, ws, s);
+			}
+			ProfScope ps("grid_backward_sorted", s);
+			grid_backward_sorted(grid, b, sc_plan, ws, s, overwrite, win_debug);
+			return;
+		}
+		if (overwrite) {
+			ProfScope ps("grid_grad_zero", s);
+			NGP_HIP(hipMemsetAsync(b.grad, 0, grid_params * sizeof(f16), s));
+		}
+		const bool want_win = grid_backward_mode == 2;
 		const bool can_win = want_win && b.dy_layout == AoS && !b.max_level_per_sample && b.max_level >= 1.0f &&
 		                     grid.n_features >= 2 && b.n >= 4096;
 		if (can_win) {
-			if (win_plan_n != b.n) { win_plan = make_win_plan(grid, b.n, 120 * 1024); win_plan_n = b.n; }
+			if (win_plan_n != b.n) { win_plan = make_win_plan(grid, b.n, 64 * 1024); win_plan_n = b.n; }
 			if (win_plan.n_win > 0) {
 				win_plan.debug = win_debug;
 				uint32_t* hist = (uint32_t*)bin_hist.get(bin_workspace_u32(win_plan, b.n) * 4);
@@ -413,7 +461,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 	NGP_TRY({
 		const std::string k = key;
 		if (k == "grid_backward_mode") {
-			NGP_CHECK(value == 0 || value == 1 || value == 2, "grid_backward_mode must be 0 (auto), 1 (direct), 2 (windowed)");
+			NGP_CHECK(value == 0 || value == 1 || value == 2 || value == 3,
+			          "grid_backward_mode must be 0 (auto), 1 (direct), 2 (windowed), 3 (bucketed)");
 			m->grid_backward_mode = (int)value;
 		} else if (k == "win_debug") {
 			m->win_debug = (uint32_t)value;
@@ -448,11 +497,9 @@ int ngp_encoding_backward(ngp_model* m, void* stream, uint32_t n, const float* i
 	NGP_ARG(m && (n == 0 || (input && dL_doutput)) && dL_layout <= 1);
 	NGP_TRY({
 		NGP_CHECK(m->gradients, "model has no gradient buffer");
-		if (grad_mode != NGP_GRAD_ACCUMULATE)
-			NGP_HIP(hipMemsetAsync(m->gradients + m->grid_offset(), 0, m->grid_params * sizeof(f16), S(stream)));
 		GridBwdArgs b{n, input, input_stride, (const f16*)dL_doutput, dL_stride, dL_layout, m->gradients + m->grid_offset(),
 		              m->max_level, m->max_level_per_sample};
-		m->scatter_grid_grad(S(stream), b);
+		m->scatter_grid_grad(S(stream), b, grad_mode != NGP_GRAD_ACCUMULATE);
 	});
 }
 
@@ -523,6 +570,7 @@ int ngp_forward_backward(ngp_model* m, void* stream, uint32_t n, const float* in
 		m->require_params(false);
 		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
 		m->generation++;
+		m->prepare_grid_backward_async(S(stream), n, input, input_stride);
 		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, false);
 		m->train_pass(S(stream), n, input, input_stride, e, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode);
 	});

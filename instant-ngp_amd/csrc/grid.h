@@ -78,6 +78,39 @@ __device__ __forceinline__ uint32_t grid_index2(uint32_t T, uint32_t res, uint32
 	return index % T;
 }
 
+template <uint32_t D>
+__device__ __forceinline__ uint32_t corner_index(const GridConst& c, uint32_t l, const uint32_t* base, uint32_t corner) {
+	const uint32_t T = c.offsets[l + 1] - c.offsets[l];
+	const uint32_t res = c.resolution[l];
+	const uint32_t x = base[0] + (corner & 1u);
+	const uint32_t y = base[1] + ((corner >> 1) & 1u);
+	if constexpr (D == 3) {
+		const uint32_t z = base[2] + ((corner >> 2) & 1u);
+		return c.offsets[l] + grid_index3(T, res, x, y, z);
+	} else {
+		return c.offsets[l] + grid_index2(T, res, x, y);
+	}
+}
+
+template <uint32_t D>
+__device__ __forceinline__ float corner_weight(const float* frac, uint32_t corner) {
+	float w = 1.0f;
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) w *= ((corner >> d) & 1u) ? frac[d] : 1.0f - frac[d];
+	return w;
+}
+
+template <uint32_t D>
+__device__ __forceinline__ void level_setup(const GridConst& c, uint32_t l, const float* x, float* frac, uint32_t* base) {
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) {
+		float p = __builtin_fmaf(c.scale[l], x[d], 0.5f);
+		float t = floorf(p);
+		base[d] = (uint32_t)(int)t;
+		frac[d] = p - t;
+	}
+}
+
 GridConst make_grid_const(const GridDesc& g);
 int device_cu_count();
 

@@ -292,11 +292,12 @@ def test_large_batch_properties(pkg, nerf_setup):
     assert torch.equal(ref_out, out)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("D,L,F,T,n", [(3, 4, 4, 19, 20000), (3, 16, 2, 19, 12000), (2, 16, 2, 14, 9000), (3, 4, 8, 14, 8192)])
+@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("D,L,F,T,n", [(3, 4, 4, 19, 20000), (3, 16, 2, 19, 12000), (2, 16, 2, 14, 9000), (3, 4, 8, 14, 8192),
+                                       (3, 8, 1, 12, 6000)])
 def test_encoding_backward_modes(pkg, orc, mode, D, L, F, T, n):
-    """Direct (tcnn-style) and spatially binned LDS-window backward both match the oracle, including
-    positions on the cube faces/edges and a few outside [0,1] (window fallback path)."""
+    """Direct (tcnn-style), spatially binned LDS-window and destination-bucketed backward all match the
+    oracle, including positions on the cube faces/edges and a few outside [0,1] (window fallback path)."""
     net = pkg.NetworkWithInputEncoding(D, 1, enc_cfg(L, F, T), MLP2)
     tr = pkg.Trainer(net, ADAM)
     net.set_option("grid_backward_mode", mode)
@@ -313,6 +314,33 @@ def test_encoding_backward_modes(pkg, orc, mode, D, L, F, T, n):
     got = tr.gradients.float().cpu().numpy()[net.n_matrix_params:]
     ref = orc.grid_backward(orc.make_grid(D, L, F, T), x, dy[:, :L * F].astype(np.float32))
     err = np.abs(got - ref)
-    # mode 2 accumulates a bin's contributions in fp32 before one fp16 atomic: tighter than mode 1
+    # modes 2/3 sum contributions exactly (fixed point) before one fp16 atomic: tighter than mode 1
     tol = (3e-2 if mode == 1 else 1e-2) * np.abs(ref).max() + 1e-3
     assert err.max() <= tol, (err.max(), np.abs(ref).max())
+
+
+@pytest.mark.parametrize("mode", [1, 3])
+def test_encoding_backward_accumulate(pkg, orc, mode):
+    """GRAD_ACCUMULATE adds to the existing grid gradient (tcnn accumulate semantics); overwrite replaces it."""
+    D, L, F, T, n = 3, 8, 2, 16, 30000
+    net = pkg.NetworkWithInputEncoding(D, 1, enc_cfg(L, F, T), MLP2)
+    tr = pkg.Trainer(net, ADAM)
+    net.set_option("grid_backward_mode", mode)
+    g = np.random.default_rng(5)
+    x = torch.from_numpy(g.random((n, D), dtype=np.float32)).cuda()
+    W = net.layout().encoding_width
+    dy = np.zeros((n, W), np.float16)
+    dy[:, :L * F] = g.uniform(-1, 1, (n, L * F))
+    dy = torch.from_numpy(dy).cuda()
+    nm = net.n_matrix_params
+    tr.gradients[nm:] = 5.0  # stale values must be overwritten
+    net.encoding_backward(x, dy)
+    g1 = tr.gradients[nm:].float().clone()
+    net.encoding_backward(x, dy, grad_mode=pkg.GRAD_ACCUMULATE)
+    g2 = tr.gradients[nm:].float().clone()
+    torch.cuda.synchronize()
+    ref = orc.grid_backward(orc.make_grid(D, L, F, T), x.cpu().numpy(), dy.cpu().numpy()[:, :L * F].astype(np.float32))
+    scale = np.abs(ref).max()
+    tol = (3e-2 if mode == 1 else 1e-2) * scale + 1e-3
+    assert np.abs(g1.cpu().numpy() - ref).max() <= tol
+    assert np.abs(g2.cpu().numpy() - 2 * ref).max() <= 2 * tol

@@ -1,6 +1,6 @@
-"""Timing-only experiment: where does the windowed hash-grid backward spend its time (C2, 2^18)."""
+"""Timing-only experiment: hash-grid backward variants and their phases (C2 / C2p, 2^18 samples)."""
 import ctypes, json, os, sys
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np, torch
 from __graft_entry__ import load_package
 pkg = load_package()
@@ -13,7 +13,7 @@ for variant in ["C2", "C2p"]:
     x = torch.rand((n, 7), device="cuda")
     W = net.layout().encoding_width
     dy = ((torch.rand((n, W), device="cuda") - 0.5) * 0.01).half()
-    for mode, dbg in [(1, 0), (2, 0), (2, 1), (2, 2), (2, 3)]:
+    for mode, dbg in [(1, 0), (3, 0), (3, 1), (3, 56), (3, 56 | 64), (3, 56 | 64 | 128), (3, 1 | 4)]:
         net.set_option("grid_backward_mode", mode)
         net.set_option("win_debug", dbg)
         for _ in range(3):
