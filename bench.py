@@ -79,6 +79,7 @@ def main():
     ap.add_argument("--variant", default="C2", choices=["C2", "C2p"])
     ap.add_argument("--batch", type=int, default=B)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", type=int, default=1, help="1: time the K steps as one captured HIP graph (N=1)")
     args = ap.parse_args()
 
     from __graft_entry__ import load_package
@@ -101,23 +102,46 @@ def main():
         div = pkg.dp.allreduce_gradients(grads, world)  # RCCL over xGMI; 1/N folded into the loss scale
         trainer.optimizer_step(loss_scale * div)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
     lib = pkg.lib()
-    lib.ngp_profiler_reset()
-    lib.ngp_profiler_enable(1)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    lib.ngp_profiler_enable(0)
+    stream = torch.cuda.Stream()
+    use_graph = bool(args.graph) and world == 1
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        graph = None
+        if use_graph:
+            # the K timed steps as one HIP graph launch (forward_backward + optimizer per step)
+            graph = trainer.capture_training_step(x, dL, loss_scale, n_steps=args.steps)
+            graph.launch()  # untimed replay: graph upload / first-launch costs
+            torch.cuda.synchronize()
+        else:
+            lib.ngp_profiler_reset()
+            lib.ngp_profiler_enable(1)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if graph is not None:
+            graph.launch()
+        else:
+            for _ in range(args.steps):
+                step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        if graph is not None:
+            # per-kernel HIP-event timing: the same K steps replayed eagerly, queued behind one more
+            # graph launch so the host is ahead of the GPU and the events bracket kernels only
+            lib.ngp_profiler_reset()
+            for _ in range(3):  # ~3x the host's enqueue time of K eager steps
+                graph.launch()
+            lib.ngp_profiler_enable(1)
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+        lib.ngp_profiler_enable(0)
     dt = t1 - t0
     if world > 1:
         t = torch.tensor([dt], device="cuda")
@@ -164,7 +188,10 @@ def main():
             "config": {"workload": f"NerfNetwork training pass, {args.variant} (configs/nerf/base.json fork: "
                                    + ("L=4 F=4 T=2^19" if args.variant == "C2" else "L=16 F=2 T=2^19")
                                    + ", density 1x64 + rgb 2x64 fp16 MLPs), fwd+bwd+Adam/EMA",
-                       "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}"},
+                       "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
+                       "launch": "hip_graph" if graph is not None else "eager"},
+            "kernel_timing": ("HIP events per kernel on the launch stream, eager replay of the same K steps queued "
+                              "behind a graph launch" if graph is not None else "HIP events per kernel over the timed region"),
             "roofline": {"kernel": dom, "bound": bound, "achieved": round(achieved, 1), "peak": peak, "unit": unit,
                          "frac": round(achieved / peak, 4), "traffic": None},
             "kernels": kern_summary,

@@ -142,6 +142,18 @@ int ngp_trainer_set_params_full_precision(ngp_trainer* t, const float* params_ho
 int ngp_trainer_serialize(ngp_trainer* t, void* buf_host, uint64_t* size);
 int ngp_trainer_deserialize(ngp_trainer* t, const void* buf_host, uint64_t size);
 
+/* Engine extension (no reference counterpart): capture n_steps of {forward_backward(input, dL/doutput)
+ * [+ optimizer_step(loss_scale) if with_optimizer]} on `stream` (not the null stream) into one HIP
+ * graph, replayed by ngp_graph_launch. Inputs are read from the captured device pointers at every
+ * launch. The optimizer step counter lives on the device, so replays follow the same learning-rate/EMA
+ * schedule as eager steps. For launch-bound training loops (one launch instead of ~15 per step). */
+typedef struct ngp_graph ngp_graph;
+int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                                      const void* dL_doutput, uint32_t dL_stride, float loss_scale, uint32_t n_steps,
+                                      int with_optimizer, ngp_graph** out);
+int ngp_graph_launch(ngp_graph* g, void* stream);
+void ngp_graph_destroy(ngp_graph* g);
+
 /* ---- NeRF training kernels (src/testbed_nerf.cu), without OptiX --------------------------- */
 typedef struct ngp_nerf_dataset ngp_nerf_dataset;  /* training images on device + cameras */
 typedef struct ngp_nerf_trainer ngp_nerf_trainer;  /* Testbed NeRF training state (grid, counters, rng) */

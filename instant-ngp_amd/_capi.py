@@ -107,6 +107,9 @@ SIGNATURES = {
     "ngp_trainer_set_params_full_precision": (i32, [P, P, u64]),
     "ngp_trainer_serialize": (i32, [P, P, C.POINTER(u64)]),
     "ngp_trainer_deserialize": (i32, [P, P, u64]),
+    "ngp_trainer_capture_training_step": (i32, [P, P, u32, P, u32, P, u32, f32, u32, i32, C.POINTER(P)]),
+    "ngp_graph_launch": (i32, [P, P]),
+    "ngp_graph_destroy": (None, [P]),
     "ngp_nerf_default_config": (i32, [f32, C.POINTER(NerfConfig)]),
     "ngp_nerf_dataset_create": (i32, [u32, C.POINTER(NerfImage), C.POINTER(P), C.POINTER(P)]),
     "ngp_nerf_dataset_destroy": (None, [P]),

@@ -397,7 +397,7 @@ void grid_backward_windowed(const GridDesc& g, const WinPlan& p, const GridBwdAr
 	const size_t lds = (size_t)p.max_verts * g.n_features * sizeof(int32_t);
 	const uint32_t blocks = std::min<uint32_t>(p.n_bins, 8 * device_cu_count());
 	auto launch = [&](auto kern) {
-		NGP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		ensure_dynamic_lds((const void*)kern, lds);
 		kern<<<blocks, 256, lds, s>>>(c, a);
 	};
 	const uint32_t key = g.n_dims * 10 + g.n_features;

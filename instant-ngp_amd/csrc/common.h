@@ -2,6 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include <cstdint>
 #include <stdexcept>
 #include <string>
@@ -54,6 +57,17 @@ __device__ __forceinline__ void atomic_add_f16x2(f16* addr, f16x2 v) {
 __device__ __forceinline__ f16x4 lds_read_tr16(const f16* p) {
 	s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
 	return __builtin_bit_cast(f16x4, v);
+}
+
+// hipFuncSetAttribute is a host-side driver call (microseconds); set each kernel's dynamic-LDS limit once.
+inline void ensure_dynamic_lds(const void* kern, size_t bytes) {
+	static std::mutex mu;
+	static std::unordered_map<const void*, size_t> done;
+	std::lock_guard<std::mutex> lock(mu);
+	auto it = done.find(kern);
+	if (it != done.end() && it->second >= bytes) return;
+	NGP_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+	done[kern] = bytes;
 }
 
 }  // namespace ngp

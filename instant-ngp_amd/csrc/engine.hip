@@ -151,6 +151,25 @@ struct ngp_model {
 		if (ev_join) (void)hipEventDestroy(ev_join);
 		if (side) (void)hipStreamDestroy(side);
 	}
+	// allocate every buffer a training pass over n samples touches (nothing may allocate during graph capture)
+	void reserve(uint32_t n) {
+		enc.get((size_t)n * enc_width * sizeof(f16));
+		denc.get((size_t)n * enc_width * sizeof(f16));
+		const uint32_t blocks = nerf ? nerf_mlp_train_blocks(n) : mlp_train_blocks(n);
+		slabs.get((size_t)blocks * n_matrix() * sizeof(float));
+		frags.get((size_t)n_all_frags * 1024);
+		frags_inf.get((size_t)n_all_frags * 1024);
+		if (use_sorted(n)) {
+			sorted_workspace(n);
+			ensure_side_stream();
+		}
+	}
+	void ensure_side_stream() {
+		if (side) return;
+		NGP_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+		NGP_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+		NGP_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+	}
 	bool use_sorted(uint32_t n) const { return grid_backward_mode == 3 || (grid_backward_mode == 0 && n >= 4096); }
 	void* sorted_workspace(uint32_t n) {
 		if (sc_plan_n != n) { sc_plan = make_scatter_plan(grid, n); sc_plan_n = n; }
@@ -160,11 +179,7 @@ struct ngp_model {
 	// concurrently with the forward encoding and the MLP; train_pass joins before the scatter.
 	void prepare_grid_backward_async(hipStream_t s, uint32_t n, const float* in, uint32_t stride) {
 		if (!use_sorted(n)) return;
-		if (!side) {
-			NGP_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-			NGP_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-			NGP_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-		}
+		ensure_side_stream();
 		void* ws = sorted_workspace(n);
 		GridBwdArgs b{n, in, stride, nullptr, 0, AoS, nullptr, max_level, max_level_per_sample};
 		NGP_HIP(hipEventRecord(ev_fork, s));
@@ -300,7 +315,21 @@ struct ngp_trainer {
 	float *w32 = nullptr, *m1 = nullptr, *m2 = nullptr, *ema32 = nullptr;
 	f16 *w16 = nullptr, *inf16 = nullptr, *g16 = nullptr;
 	uint32_t* steps = nullptr;
+	uint32_t* ctl = nullptr;  // device {optimizer step, block counter}; `step` mirrors ctl[0] on the host
 	~ngp_trainer() { if (arena) (void)hipFree(arena); }
+	void sync_device_step() { NGP_HIP(hipMemcpy(ctl, &step, sizeof(uint32_t), hipMemcpyHostToDevice)); }
+};
+
+// A captured training step (forward_backward + optimizer) replayed as one HIP graph launch.
+struct ngp_graph {
+	hipGraph_t graph = nullptr;
+	hipGraphExec_t exec = nullptr;
+	ngp_trainer* trainer = nullptr;
+	uint32_t steps_per_launch = 1;
+	~ngp_graph() {
+		if (exec) (void)hipGraphExecDestroy(exec);
+		if (graph) (void)hipGraphDestroy(graph);
+	}
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -474,13 +503,7 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 
 int ngp_model_reserve(ngp_model* m, uint32_t n) {
 	NGP_ARG(m);
-	NGP_TRY({
-		m->enc.get((size_t)n * m->enc_width * sizeof(f16));
-		m->denc.get((size_t)n * m->enc_width * sizeof(f16));
-		m->slabs.get((size_t)nerf_mlp_train_blocks(n) * m->n_matrix() * sizeof(float));
-		m->frags.get((size_t)m->n_all_frags * 1024);
-		m->frags_inf.get((size_t)m->n_all_frags * 1024);
-	});
+	NGP_TRY({ m->reserve(n); });
 }
 
 int ngp_encoding_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
@@ -608,7 +631,7 @@ int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, 
 		t->n = n;
 		auto al = [](size_t b) { return (b + 255) / 256 * 256; };
 		const size_t b32 = al(n * 4), b16 = al(n * 2);
-		const size_t total = 4 * b32 + 3 * b16 + b32 /*steps*/;
+		const size_t total = 4 * b32 + 3 * b16 + b32 /*steps*/ + 256 /*ctl*/;
 		NGP_HIP(hipMalloc(&t->arena, total));
 		char* p = (char*)t->arena;
 		t->w32 = (float*)p; p += b32;
@@ -619,6 +642,7 @@ int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, 
 		t->w16 = (f16*)p; p += b16;
 		t->inf16 = (f16*)p; p += b16;
 		t->g16 = (f16*)p; p += b16;
+		t->ctl = (uint32_t*)p; p += 256;
 		NGP_HIP(hipMemset(t->arena, 0, total));
 		std::vector<float> host(n);
 		if (ngp_model_initialize_params(m, seed, host.data(), 1.0f) != NGP_OK) throw Error(g_last_error);
@@ -637,11 +661,62 @@ int ngp_trainer_optimizer_step(ngp_trainer* t, void* stream, float loss_scale) {
 	NGP_ARG(t && loss_scale > 0.f);
 	NGP_TRY({
 		ProfScope ps("optimizer", S(stream));
-		adam_ema_step(t->cfg, t->step, (uint32_t)t->n, (uint32_t)t->model->n_matrix(), loss_scale, t->w32, t->w16, t->g16, t->m1,
-		              t->m2, t->steps, t->ema32, t->inf16, S(stream));
+		adam_ema_step(t->cfg, (uint32_t)t->n, (uint32_t)t->model->n_matrix(), loss_scale, t->w32, t->w16, t->g16, t->m1, t->m2,
+		              t->steps, t->ema32, t->inf16, t->ctl, S(stream));
 		t->step++;
 	});
 }
+
+int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                                      const void* dL_doutput, uint32_t dL_stride, float loss_scale, uint32_t n_steps,
+                                      int with_optimizer, ngp_graph** out) {
+	NGP_ARG(t && out && stream && n > 0 && input && dL_doutput && loss_scale > 0.f && n_steps >= 1);
+	NGP_TRY({
+		ngp_model* m = t->model;
+		m->require_params(false);
+		NGP_CHECK(m->gradients == t->g16, "capture: the model's gradient buffer must be this trainer's");
+		m->reserve(n);
+		hipStream_t s = S(stream);
+		auto g = std::make_unique<ngp_graph>();
+		g->trainer = t;
+		g->steps_per_launch = with_optimizer ? n_steps : 0;
+		NGP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+		int rc = NGP_OK;
+		for (uint32_t k = 0; k < n_steps && rc == NGP_OK; ++k) {
+			rc = ngp_forward_backward(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE);
+			if (rc == NGP_OK && with_optimizer) {
+				try {
+					ProfScope ps("optimizer", s);
+					adam_ema_step(t->cfg, (uint32_t)t->n, (uint32_t)m->n_matrix(), loss_scale, t->w32, t->w16, t->g16, t->m1, t->m2,
+					              t->steps, t->ema32, t->inf16, t->ctl, s);
+				} catch (const std::exception& e) {
+					g_last_error = e.what();
+					rc = NGP_ERROR;
+				}
+			}
+		}
+		hipGraph_t graph = nullptr;
+		const hipError_t end = hipStreamEndCapture(s, &graph);
+		if (rc != NGP_OK) {
+			if (graph) (void)hipGraphDestroy(graph);
+			throw Error(g_last_error);
+		}
+		NGP_HIP(end);
+		g->graph = graph;
+		NGP_HIP(hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0));
+		*out = g.release();
+	});
+}
+
+int ngp_graph_launch(ngp_graph* g, void* stream) {
+	NGP_ARG(g && g->exec);
+	NGP_TRY({
+		NGP_HIP(hipGraphLaunch(g->exec, S(stream)));
+		g->trainer->step += g->steps_per_launch;
+	});
+}
+
+void ngp_graph_destroy(ngp_graph* g) { delete g; }
 
 void* ngp_trainer_gradients(ngp_trainer* t) { return t ? t->g16 : nullptr; }
 void* ngp_trainer_params(ngp_trainer* t) { return t ? t->w16 : nullptr; }
@@ -699,6 +774,7 @@ int ngp_trainer_deserialize(ngp_trainer* t, const void* buf, uint64_t size) {
 		NGP_CHECK(hdr[0] == 0x4e47504d49333535ULL && hdr[1] == 1, "deserialize: bad magic/version");
 		NGP_CHECK(hdr[2] == t->n && size >= 32 + t->n * 20, "deserialize: parameter count mismatch");
 		t->step = (uint32_t)hdr[3];
+		t->sync_device_step();
 		for (void* dst : {(void*)t->w32, (void*)t->m1, (void*)t->m2, (void*)t->ema32, (void*)t->steps}) {
 			NGP_HIP(hipMemcpy(dst, p, t->n * 4, hipMemcpyHostToDevice));
 			p += t->n * 4;

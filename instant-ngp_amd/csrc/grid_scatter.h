@@ -6,9 +6,9 @@ namespace ngp {
 
 struct ScatterPlan {
 	uint32_t B = 0;          // log2 entries per bucket (a bucket's accumulators fill one LDS tile)
-	uint32_t n_buckets = 0;
-	uint32_t spb = 0;        // samples per histogram/scatter block
-	uint32_t n_blocks = 0;
+	uint32_t n_buckets = 0;  // buckets are level-aligned: a bucket never spans two levels
+	uint32_t spb = 0;        // samples per chunk (hist/scatter blocks are (chunk, level))
+	uint32_t n_chunks = 0;
 	uint32_t max_lb = 0;     // most buckets any one level spans
 	uint64_t n_items = 0;    // n * L * 2^D contributions
 	uint32_t split_limit = 0;// buckets with more items are summed in parts (k_sc_split)
@@ -16,7 +16,7 @@ struct ScatterPlan {
 	uint32_t max_split_blocks = 0;
 	size_t cub_bytes = 0;
 	// workspace layout (bytes)
-	size_t off_hist = 0, off_scan = 0, off_cub = 0, off_split = 0, off_idx = 0, off_val = 0, total = 0;
+	size_t off_hist = 0, off_scan = 0, off_cur = 0, off_cub = 0, off_split = 0, off_idx = 0, off_val = 0, total = 0;
 };
 
 ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n);

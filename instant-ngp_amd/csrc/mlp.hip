@@ -494,7 +494,7 @@ static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	auto kern = k_nerf_mlp<ES, DH, RH, MODE>;
 	static bool attr_set = false;
 	if (!attr_set) {
-		NGP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		ensure_dynamic_lds((const void*)kern, lds);
 		attr_set = true;
 	}
 	kern<<<blocks, 256, lds, s>>>(a);
@@ -683,7 +683,7 @@ static void launch_mlp(const MlpArgs& a, hipStream_t s) {
 	auto kern = k_mlp<ES, NH, MODE>;
 	static bool attr_set = false;
 	if (!attr_set) {
-		NGP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+		ensure_dynamic_lds((const void*)kern, lds);
 		attr_set = true;
 	}
 	kern<<<blocks, 256, lds, s>>>(a);

@@ -12,7 +12,8 @@ struct AdamConfig {
 	float lr_at(uint32_t step) const;  // learning rate used by optimizer step `step` (0-based)
 };
 
-void adam_ema_step(const AdamConfig& c, uint32_t step, uint32_t n, uint32_t n_matrix, float loss_scale, float* w32, f16* w16,
-                   const f16* g16, float* m1, float* m2, uint32_t* steps, float* ema32, f16* ema16, hipStream_t s);
+// ctl: device optimizer step; the update reads it and then advances it (stream-ordered).
+void adam_ema_step(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float loss_scale, float* w32, f16* w16, const f16* g16,
+                   float* m1, float* m2, uint32_t* steps, float* ema32, f16* ema16, uint32_t* ctl, hipStream_t s);
 
 }  // namespace ngp

@@ -41,7 +41,7 @@ hipEvent_t profiler_event() {
 	std::lock_guard<std::mutex> l(mu);
 	if (pool.empty()) {
 		hipEvent_t e;
-		NGP_HIP(hipEventCreate(&e));
+		NGP_HIP(hipEventCreateWithFlags(&e, hipEventDefault));
 		return e;
 	}
 	hipEvent_t e = pool.back();
@@ -62,6 +62,12 @@ extern "C" {
 int ngp_profiler_enable(int enable) {
 	std::lock_guard<std::mutex> l(ngp::mu);
 	ngp::enabled = enable != 0;
+	// events are created up front: creating them while a stream is being captured into a graph fails
+	while (ngp::enabled && ngp::pool.size() < 8192) {
+		hipEvent_t e;
+		if (hipEventCreateWithFlags(&e, hipEventDefault) != hipSuccess) return NGP_ERROR;
+		ngp::pool.push_back(e);
+	}
 	return NGP_OK;
 }
 

@@ -246,3 +246,27 @@ class Trainer:
 
     def deserialize(self, blob):
         check(lib().ngp_trainer_deserialize(self.handle, blob, len(blob)))
+
+    def capture_training_step(self, x, dL_doutput, loss_scale=128.0, n_steps=1, with_optimizer=True, stream=None):
+        """Engine extension: n_steps of forward_backward(x, dL_doutput) [+ optimizer_step] captured into
+        one HIP graph (TrainingGraph.launch replays it). `stream` must not be the null stream."""
+        s = _stream(stream)
+        if not s.value:
+            raise ValueError("graph capture needs a non-default stream (use torch.cuda.Stream())")
+        _check_input(x, self.model.input_width())
+        h = C.c_void_p()
+        check(lib().ngp_trainer_capture_training_step(self.handle, s, x.shape[0], _ptr(x), x.stride(0), _ptr(dL_doutput),
+                                                      dL_doutput.stride(0), float(loss_scale), n_steps, int(with_optimizer),
+                                                      C.byref(h)))
+        return TrainingGraph(h, (x, dL_doutput))
+
+
+class TrainingGraph:
+    def __init__(self, handle, keep):
+        self.handle, self._keep = handle, keep
+
+    def launch(self, stream=None):
+        check(lib().ngp_graph_launch(self.handle, _stream(stream)))
+
+    def __del__(self, _d=_destroy):
+        _d(self, "ngp_graph_destroy")
