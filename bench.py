@@ -80,6 +80,7 @@ def main():
     ap.add_argument("--batch", type=int, default=B)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="1: time the K steps as one captured HIP graph (N=1)")
+    ap.add_argument("--overlap", type=int, default=None, help="engine side-stream overlap bitmask (engine.hip)")
     args = ap.parse_args()
 
     from __graft_entry__ import load_package
@@ -90,6 +91,8 @@ def main():
 
     cfg = pkg.nerf_config(args.variant)
     net = pkg.create_nerf_network(cfg)
+    if args.overlap is not None:
+        net.set_option("overlap", args.overlap)
     trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
     n = args.batch
     net.reserve(n)

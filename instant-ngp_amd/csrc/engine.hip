@@ -128,6 +128,8 @@ struct ngp_model {
 	MlpPlan mplan;
 	uint64_t mlp0_params = 0, mlp1_params = 0, grid_params = 0, n_params = 0;
 	FragDesc* d_descs = nullptr;
+	uint32_t* d_fragmap = nullptr;  // [n_matrix x 2] fragment slot (f16 index) of each matrix param: fwd, bwd
+	bool frags_current = false;     // `frags` holds the fragments of the current `params` (kept by the optimizer)
 	uint32_t n_all_frags = 0;
 	DevBuf frags, frags_inf, enc, denc, slabs, bin_hist, bin_sorted, scatter_ws;
 	int grid_backward_mode = 0;  // 0 auto, 1 direct (tcnn-style), 2 windowed (binned LDS), 3 bucketed (grid_scatter.h)
@@ -137,8 +139,14 @@ struct ngp_model {
 	ScatterPlan sc_plan;
 	uint32_t sc_plan_n = 0;
 	bool sc_prepared = false;               // phase 1 of the bucketed backward already enqueued (side stream)
-	hipStream_t side = nullptr;             // overlaps the bucket histogram with forward + MLP
-	hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+	bool frags_async = false;               // training fragments already enqueued on the side stream
+	// side-stream overlap (bitmask): 1 bucket histogram under forward + MLP, 2 weight fragments,
+	// 4 dW slab reduction under the grid backward, 8 optimizer step advance. Each costs a cross-queue
+	// dependency edge, which in a HIP graph is not free.
+	uint32_t overlap = 0;
+	hipStream_t side = nullptr;             // overlaps fragments + bucket histogram with forward + MLP,
+	                                        // and the dW slab reduction with the grid backward
+	hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_frags = nullptr, ev_mlp = nullptr, ev_red = nullptr;
 	f16 *params = nullptr, *inference_params = nullptr, *gradients = nullptr;
 	float max_level = 1.0f;
 	const float* max_level_per_sample = nullptr;
@@ -147,8 +155,9 @@ struct ngp_model {
 
 	~ngp_model() {
 		if (d_descs) (void)hipFree(d_descs);
-		if (ev_fork) (void)hipEventDestroy(ev_fork);
-		if (ev_join) (void)hipEventDestroy(ev_join);
+		if (d_fragmap) (void)hipFree(d_fragmap);
+		for (hipEvent_t e : {ev_fork, ev_join, ev_frags, ev_mlp, ev_red})
+			if (e) (void)hipEventDestroy(e);
 		if (side) (void)hipStreamDestroy(side);
 	}
 	// allocate every buffer a training pass over n samples touches (nothing may allocate during graph capture)
@@ -169,8 +178,12 @@ struct ngp_model {
 		NGP_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
 		NGP_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
 		NGP_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+		NGP_HIP(hipEventCreateWithFlags(&ev_frags, hipEventDisableTiming));
+		NGP_HIP(hipEventCreateWithFlags(&ev_mlp, hipEventDisableTiming));
+		NGP_HIP(hipEventCreateWithFlags(&ev_red, hipEventDisableTiming));
 	}
 	bool use_sorted(uint32_t n) const { return grid_backward_mode == 3 || (grid_backward_mode == 0 && n >= 4096); }
+	bool side_prepare(uint32_t n) const { return use_sorted(n) && (overlap & 1); }
 	void* sorted_workspace(uint32_t n) {
 		if (sc_plan_n != n) { sc_plan = make_scatter_plan(grid, n); sc_plan_n = n; }
 		return scatter_ws.get(sc_plan.total);
@@ -178,12 +191,19 @@ struct ngp_model {
 	// Phase 1 of the bucketed grid backward on a side stream: it only needs the positions, so it runs
 	// concurrently with the forward encoding and the MLP; train_pass joins before the scatter.
 	void prepare_grid_backward_async(hipStream_t s, uint32_t n, const float* in, uint32_t stride) {
-		if (!use_sorted(n)) return;
+		if (!side_prepare(n)) return;
 		ensure_side_stream();
 		void* ws = sorted_workspace(n);
 		GridBwdArgs b{n, in, stride, nullptr, 0, AoS, nullptr, max_level, max_level_per_sample};
 		NGP_HIP(hipEventRecord(ev_fork, s));
 		NGP_HIP(hipStreamWaitEvent(side, ev_fork, 0));
+		// the training MLP's weight fragments depend only on the parameters: build them here, off the
+		// critical path (run_mlp waits on ev_frags instead of launching k_prepare_frags itself)
+		if ((overlap & 2) && !frags_current) {
+			prep(side, false);
+			NGP_HIP(hipEventRecord(ev_frags, side));
+			frags_async = true;
+		}
 		{
 			ProfScope ps("grid_bwd_prepare", side);
 			grid_scatter_prepare(grid, b, sc_plan, ws, side);
@@ -203,6 +223,27 @@ struct ngp_model {
 		n_all_frags = (uint32_t)d.size();
 		NGP_HIP(hipMalloc(&d_descs, d.size() * sizeof(FragDesc)));
 		NGP_HIP(hipMemcpy(d_descs, d.data(), d.size() * sizeof(FragDesc), hipMemcpyHostToDevice));
+		// inverse of k_prepare_frags: where each matrix parameter lives in the fragment buffer
+		std::vector<uint32_t> map(2 * n_matrix(), ~0u);
+		for (uint32_t f = 0; f < n_all_frags; ++f)
+			for (uint32_t lane = 0; lane < 64; ++lane)
+				for (uint32_t j = 0; j < 8; ++j) {
+					const FragDesc& q = d[f];
+					const uint32_t h = lane >> 5, r = 32 * q.tile + (lane & 31);
+					const uint32_t k = q.perm ? 16 * q.step + 8 * (j >> 2) + 4 * h + (j & 3) : 16 * q.step + 8 * h + j;
+					uint64_t pi;
+					if (!q.transposed) {
+						if (!(r < q.out_dim && k < q.in_dim)) continue;
+						pi = q.woff + (uint64_t)r * q.in_dim + k;
+					} else {
+						if (!(r < q.in_dim && k < q.out_dim)) continue;
+						pi = q.woff + (uint64_t)k * q.in_dim + r;
+					}
+					NGP_CHECK(pi < n_matrix() && map[2 * pi + q.transposed] == ~0u, "fragment map: parameter mapped twice");
+					map[2 * pi + q.transposed] = (f * 64 + lane) * 8 + j;
+				}
+		NGP_HIP(hipMalloc(&d_fragmap, map.size() * sizeof(uint32_t)));
+		NGP_HIP(hipMemcpy(d_fragmap, map.data(), map.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
 	}
 	void require_params(bool inference) const {
 		NGP_CHECK(inference ? inference_params != nullptr : params != nullptr,
@@ -213,21 +254,31 @@ struct ngp_model {
 		f16x8* f = (f16x8*)(inference ? frags_inf : frags).get((size_t)n_all_frags * 1024);
 		ProfScope ps("prepare_frags", s);
 		prepare_frags(d_descs, n_all_frags, pick(inference), f, s);
+		if (!inference) frags_current = true;
 		return f;
 	}
 	void encode(hipStream_t s, uint32_t n, const float* in, uint32_t stride, f16* out, uint32_t out_stride, uint32_t layout, bool inference) {
-		if (enc_width > grid.n_levels * grid.n_features && layout == AoS) {
-			// zero the padding columns once per call (tcnn pads the encoding output with zeros)
+		GridFwdArgs a{n, in, stride, pick(inference) + grid_offset(), out, out_stride, layout, max_level, max_level_per_sample};
+		if (enc_width > grid.n_levels * grid.n_features && layout == AoS && !grid_forward_rows_ok(grid, a)) {
+			// zero the padding columns (tcnn pads the encoding output with zeros); the row kernel writes them
 			NGP_HIP(hipMemsetAsync(out, 0, (size_t)n * out_stride * sizeof(f16), s));
 		}
-		GridFwdArgs a{n, in, stride, pick(inference) + grid_offset(), out, out_stride, layout, max_level, max_level_per_sample};
 		ProfScope ps("grid_forward", s);
 		grid_forward(grid, a, s);
 	}
 	void run_mlp(hipStream_t s, MlpMode mode, uint32_t n, const float* in, uint32_t stride, const f16* encbuf, f16* out,
 	             uint32_t out_stride, uint32_t out_layout, const f16* dL, uint32_t dL_stride, f16* dL_denc, float* slab,
 	             bool inference) {
-		f16x8* f = prep(s, inference);
+		f16x8* f;
+		if (frags_async && !inference) {
+			f = (f16x8*)frags.p;
+			NGP_HIP(hipStreamWaitEvent(s, ev_frags, 0));
+			frags_async = false;
+		} else if (!inference && frags_current && frags.p) {
+			f = (f16x8*)frags.p;  // kept current by the optimizer (k_adam_ema writes the fragment slots)
+		} else {
+			f = prep(s, inference);
+		}
 		if (nerf) {
 			NerfMlpArgs a{};
 			a.n = n; a.enc = encbuf; a.enc_stride = enc_width; a.coords = in; a.coord_stride = stride; a.dir_offset = dir_offset;
@@ -253,12 +304,24 @@ struct ngp_model {
 		const uint32_t blocks = nerf ? nerf_mlp_train_blocks(n) : mlp_train_blocks(n);
 		float* slab = (float*)slabs.get((size_t)blocks * n_matrix() * sizeof(float));
 		run_mlp(s, MLP_TRAIN, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride, dL_denc, slab, false);
-		{
-			ProfScope ps("reduce_slabs", s);
-			reduce_slabs(slab, blocks, (uint32_t)n_matrix(), gradients, grad_mode == NGP_GRAD_ACCUMULATE, s);
+		// the dW slab reduction (MLP section of the gradient) and the grid backward (grid section) are
+		// independent: for large batches the reduction runs on the side stream under the grid backward
+		const bool ovl = use_sorted(n) && (overlap & 4);
+		hipStream_t rs = s;
+		if (ovl) {
+			ensure_side_stream();
+			NGP_HIP(hipEventRecord(ev_mlp, s));
+			NGP_HIP(hipStreamWaitEvent(side, ev_mlp, 0));
+			rs = side;
 		}
+		{
+			ProfScope ps("reduce_slabs", rs);
+			reduce_slabs(slab, blocks, (uint32_t)n_matrix(), gradients, grad_mode == NGP_GRAD_ACCUMULATE, rs);
+		}
+		if (ovl) NGP_HIP(hipEventRecord(ev_red, side));
 		GridBwdArgs b{n, in, stride, dL_denc, enc_width, AoS, gradients + grid_offset(), max_level, max_level_per_sample};
 		scatter_grid_grad(s, b, grad_mode != NGP_GRAD_ACCUMULATE);
+		if (ovl) NGP_HIP(hipStreamWaitEvent(s, ev_red, 0));
 	}
 	// Hash-grid backward: windowed (spatial bins + LDS) for the coarse levels when it pays, direct
 	// packed-f16 atomics for the rest. The windowed path needs all levels active (max_level >= 1).
@@ -318,6 +381,15 @@ struct ngp_trainer {
 	uint32_t* ctl = nullptr;  // device {optimizer step, block counter}; `step` mirrors ctl[0] on the host
 	~ngp_trainer() { if (arena) (void)hipFree(arena); }
 	void sync_device_step() { NGP_HIP(hipMemcpy(ctl, &step, sizeof(uint32_t), hipMemcpyHostToDevice)); }
+	// One optimizer step on stream s. step_base/step_add: see AdamState (optimizer.h).
+	void run_step(hipStream_t s, float loss_scale, const uint32_t* step_base, uint32_t step_add) {
+		ngp_model* m = model;
+		const bool own = m->params == w16;
+		AdamState st{w32, w16, g16, m1, m2, steps, ema32, inf16,
+		             own && m->frags_current ? (f16*)m->frags.p : nullptr, m->d_fragmap, step_base, step_add};
+		ProfScope ps("optimizer", s);
+		adam_ema_update(cfg, (uint32_t)n, (uint32_t)m->n_matrix(), loss_scale, st, s);
+	}
 };
 
 // A captured training step (forward_backward + optimizer) replayed as one HIP graph launch.
@@ -461,6 +533,7 @@ int ngp_model_set_params(ngp_model* m, void* params, void* inference_params, voi
 	NGP_ARG(m);
 	NGP_TRY({
 		m->params = (f16*)params;
+		m->frags_current = false;
 		m->inference_params = (f16*)(inference_params ? inference_params : params);
 		m->gradients = (f16*)gradients;
 	});
@@ -493,6 +566,9 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			NGP_CHECK(value == 0 || value == 1 || value == 2 || value == 3,
 			          "grid_backward_mode must be 0 (auto), 1 (direct), 2 (windowed), 3 (bucketed)");
 			m->grid_backward_mode = (int)value;
+		} else if (k == "overlap") {
+			NGP_CHECK(value >= 0 && value <= 15, "overlap is a bitmask in [0, 15]");
+			m->overlap = (uint32_t)value;
 		} else if (k == "win_debug") {
 			m->win_debug = (uint32_t)value;
 		} else {
@@ -660,9 +736,7 @@ void ngp_trainer_destroy(ngp_trainer* t) {
 int ngp_trainer_optimizer_step(ngp_trainer* t, void* stream, float loss_scale) {
 	NGP_ARG(t && loss_scale > 0.f);
 	NGP_TRY({
-		ProfScope ps("optimizer", S(stream));
-		adam_ema_step(t->cfg, (uint32_t)t->n, (uint32_t)t->model->n_matrix(), loss_scale, t->w32, t->w16, t->g16, t->m1, t->m2,
-		              t->steps, t->ema32, t->inf16, t->ctl, S(stream));
+		t->run_step(S(stream), loss_scale, nullptr, t->step);
 		t->step++;
 	});
 }
@@ -686,9 +760,7 @@ int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, 
 			rc = ngp_forward_backward(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE);
 			if (rc == NGP_OK && with_optimizer) {
 				try {
-					ProfScope ps("optimizer", s);
-					adam_ema_step(t->cfg, (uint32_t)t->n, (uint32_t)m->n_matrix(), loss_scale, t->w32, t->w16, t->g16, t->m1, t->m2,
-					              t->steps, t->ema32, t->inf16, t->ctl, s);
+					t->run_step(s, loss_scale, t->ctl, k);  // step = device base (set per launch) + k
 				} catch (const std::exception& e) {
 					g_last_error = e.what();
 					rc = NGP_ERROR;
@@ -711,6 +783,7 @@ int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, 
 int ngp_graph_launch(ngp_graph* g, void* stream) {
 	NGP_ARG(g && g->exec);
 	NGP_TRY({
+		if (g->steps_per_launch) set_device_step(g->trainer->ctl, g->trainer->step, S(stream));
 		NGP_HIP(hipGraphLaunch(g->exec, S(stream)));
 		g->trainer->step += g->steps_per_launch;
 	});
@@ -782,6 +855,7 @@ int ngp_trainer_deserialize(ngp_trainer* t, const void* buf, uint64_t size) {
 		k_f32_to_f16<<<div_round_up(t->n, 256), 256>>>(t->w32, t->w16, t->inf16, t->n);
 		NGP_HIP(hipGetLastError());
 		NGP_HIP(hipDeviceSynchronize());
+		t->model->frags_current = false;
 	});
 }
 

@@ -50,6 +50,8 @@ struct GridBwdArgs {
 };
 
 void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream);
+// true when grid_forward writes whole AoS rows (padding columns included: no memset needed)
+bool grid_forward_rows_ok(const GridDesc& g, const GridFwdArgs& a);
 void grid_backward(const GridDesc& g, const GridBwdArgs& a, hipStream_t stream);
 
 // ---- device-side building blocks (shared with fused kernels) ---------------------------------

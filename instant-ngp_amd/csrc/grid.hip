@@ -104,6 +104,57 @@ __global__ void __launch_bounds__(256) k_grid_forward(const GridConst c, const G
 	}
 }
 
+// AoS fast path: every level's result stays in registers and the whole row (out_stride halves,
+// zero-padded past L*F) is written with back-to-back 16-B stores, so each 64-B segment is filled by
+// one wave within a few cycles. Per-level 8-B stores spaced a level's gathers apart reach HBM as
+// partial segments (rocprof WRITE_SIZE 3.6x the 8.4 MB of a C2 batch, profiles/r01b_pmc_c2.json).
+template <uint32_t D, uint32_t F>
+__global__ void __launch_bounds__(256) k_grid_forward_rows(const GridConst c, const GridFwdArgs a) {
+	typedef typename FeatVec<F>::T V;
+	constexpr uint32_t MAXL = 32 / F;
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= a.n) return;
+	float x[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * a.pos_stride + d];
+	const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
+	f16 row[32];
+#pragma unroll
+	for (uint32_t l = 0; l < MAXL; ++l) {
+		float acc[F];
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) acc[f] = 0.f;
+		if (l < c.n_levels && !((float)l >= ml + 1e-3f)) {
+			float frac[D]; uint32_t base[D];
+			level_setup<D>(c, l, x, frac, base);
+			V v[1u << D];
+#pragma unroll
+			for (uint32_t k = 0; k < (1u << D); ++k) v[k] = *(const V*)(a.table + (size_t)corner_index<D>(c, l, base, k) * F);
+#pragma unroll
+			for (uint32_t k = 0; k < (1u << D); ++k) {
+				const float w = corner_weight<D>(frac, k);
+				if constexpr (F == 1) acc[0] = __builtin_fmaf(w, (float)v[k], acc[0]);
+				else {
+#pragma unroll
+					for (uint32_t f = 0; f < F; ++f) acc[f] = __builtin_fmaf(w, (float)v[k][f], acc[f]);
+				}
+			}
+		}
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) {
+			asm volatile("" : "+v"(acc[f]));  // round to fp32, then RNE to fp16 (no v_fma_mix fusion)
+			row[l * F + f] = (f16)acc[f];
+		}
+	}
+	f16x8* dst = (f16x8*)(a.out + (size_t)i * a.out_stride);
+#pragma unroll
+	for (uint32_t q = 0; q < 4; ++q) {
+		if (8 * q >= a.out_stride) break;
+		dst[q] = f16x8{row[8 * q], row[8 * q + 1], row[8 * q + 2], row[8 * q + 3],
+		               row[8 * q + 4], row[8 * q + 5], row[8 * q + 6], row[8 * q + 7]};
+	}
+}
+
 // Backward: 2P lanes per sample (P = feature pairs per entry), ordered [x0: pair 0..P-1 | x1: pair
 // 0..P-1]. One wave-instruction then updates a corner and its +x neighbour, which are adjacent
 // entries (dense levels) or in one aligned 8-entry group 7/8 of the time (the hash keeps x coherent:
@@ -154,9 +205,23 @@ __global__ void __launch_bounds__(256) k_grid_backward(const GridConst c, const 
 	}
 }
 
+bool grid_forward_rows_ok(const GridDesc& g, const GridFwdArgs& a) {
+	return a.out_layout == AoS && a.out_stride % 8 == 0 && a.out_stride <= 32 && g.n_levels * g.n_features <= a.out_stride &&
+	       ((uintptr_t)a.out & 15) == 0;
+}
+
 template <uint32_t D>
-static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hipStream_t s) {
+static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hipStream_t s, bool rows) {
 	const dim3 grid(div_round_up(a.n, 256)), block(256);
+	if (rows) {
+		switch (F) {
+			case 1: k_grid_forward_rows<D, 1><<<grid, block, 0, s>>>(c, a); return;
+			case 2: k_grid_forward_rows<D, 2><<<grid, block, 0, s>>>(c, a); return;
+			case 4: k_grid_forward_rows<D, 4><<<grid, block, 0, s>>>(c, a); return;
+			case 8: k_grid_forward_rows<D, 8><<<grid, block, 0, s>>>(c, a); return;
+			default: throw Error("GridEncoding: unsupported F");
+		}
+	}
 	switch (F) {
 		case 1: k_grid_forward<D, 1><<<grid, block, 0, s>>>(c, a); break;
 		case 2: k_grid_forward<D, 2><<<grid, block, 0, s>>>(c, a); break;
@@ -182,8 +247,9 @@ static void launch_bwd(uint32_t F, const GridConst& c, const GridBwdArgs& a, hip
 void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream) {
 	if (a.n == 0) return;
 	GridConst c = make_grid_const(g);
-	if (g.n_dims == 3) launch_fwd<3>(g.n_features, c, a, stream);
-	else launch_fwd<2>(g.n_features, c, a, stream);
+	const bool rows = grid_forward_rows_ok(g, a);
+	if (g.n_dims == 3) launch_fwd<3>(g.n_features, c, a, stream, rows);
+	else launch_fwd<2>(g.n_features, c, a, stream, rows);
 	NGP_HIP(hipGetLastError());
 }
 

@@ -718,8 +718,18 @@ __global__ void __launch_bounds__(256) k_reduce_slabs(const float* __restrict__ 
 	__shared__ float part[8][33];
 	const uint32_t p = blockIdx.x * 32 + (threadIdx.x & 31), g = threadIdx.x >> 5;
 	float s = 0.f;
-	if (p < n)
-		for (uint32_t b = g; b < n_slabs; b += 8) s += slabs[(size_t)b * n + p];
+	if (p < n) {
+		// 8 independent loads in flight per step (the adds stay in slab order: deterministic)
+		uint32_t b = g;
+		for (; b + 56 < n_slabs; b += 64) {
+			float v[8];
+#pragma unroll
+			for (int k = 0; k < 8; ++k) v[k] = slabs[(size_t)(b + 8 * k) * n + p];
+#pragma unroll
+			for (int k = 0; k < 8; ++k) s += v[k];
+		}
+		for (; b < n_slabs; b += 8) s += slabs[(size_t)b * n + p];
+	}
 	part[g][threadIdx.x & 31] = s;
 	__syncthreads();
 	if (g == 0 && p < n) {

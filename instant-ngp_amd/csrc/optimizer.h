@@ -12,8 +12,19 @@ struct AdamConfig {
 	float lr_at(uint32_t step) const;  // learning rate used by optimizer step `step` (0-based)
 };
 
-// ctl: device optimizer step; the update reads it and then advances it (stream-ordered).
-void adam_ema_step(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float loss_scale, float* w32, f16* w16, const f16* g16,
-                   float* m1, float* m2, uint32_t* steps, float* ema32, f16* ema16, uint32_t* ctl, hipStream_t s);
+// One fused update. The optimizer step used for the schedule / bias correction / EMA debias is
+// (step_base ? *step_base : 0) + step_add: eager steps pass the host step in step_add; a captured HIP
+// graph of K steps reads the base from device memory (set once per launch) plus the step's index.
+// frags/fragmap (optional): the MLP weight fragments (mlp.h) are rewritten in place from the new fp16
+// matrix params, so the next MLP launch needs no k_prepare_frags (fragmap: 2 slots per matrix param).
+struct AdamState {
+	float* w32; f16* w16; const f16* g16;
+	float* m1; float* m2; uint32_t* steps;
+	float* ema32; f16* ema16;
+	f16* frags; const uint32_t* fragmap;
+	const uint32_t* step_base; uint32_t step_add;
+};
+void adam_ema_update(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float loss_scale, const AdamState& st, hipStream_t s);
+void set_device_step(uint32_t* ctl, uint32_t step, hipStream_t s);
 
 }  // namespace ngp

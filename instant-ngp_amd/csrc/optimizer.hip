@@ -11,9 +11,9 @@
 
 namespace ngp {
 
-// The optimizer step count lives on the device (ctl[0]) so the step can be replayed from a HIP graph:
-// the update kernel reads it and a one-thread kernel after it advances it (a last-block counter would
-// put ~13k same-address atomics on one L2 line: measured 330 us).
+// The optimizer step: eager launches pass it by value; a HIP graph of K captured steps reads a base
+// from device memory (written once per graph launch by k_set_step) plus the step's index in the graph,
+// so no per-step counter kernel is needed.
 __device__ __forceinline__ float lr_schedule(const AdamConfig& c, uint32_t step) {
 	float r = c.lr;
 	if (c.decay_interval == 0 || step < c.decay_start) return r;
@@ -23,38 +23,42 @@ __device__ __forceinline__ float lr_schedule(const AdamConfig& c, uint32_t step)
 }
 
 __global__ void k_adam_ema(const uint32_t n, const uint32_t n_matrix, const float loss_scale, const AdamConfig c,
-                           float* __restrict__ w32, f16* __restrict__ w16, const f16* __restrict__ g16,
-                           float* __restrict__ m1, float* __restrict__ m2, uint32_t* __restrict__ steps,
-                           float* __restrict__ ema32, f16* __restrict__ ema16, uint32_t* __restrict__ ctl) {
+                           const AdamState st) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	const uint32_t step = ctl[0];
+	const uint32_t step = (st.step_base ? *st.step_base : 0u) + st.step_add;
 	if (i < n) {
 		const float lr = lr_schedule(c, step);
-		float g = (float)g16[i] / loss_scale;
-		float w = w32[i];
+		float g = (float)st.g16[i] / loss_scale;
+		float w = st.w32[i];
 		if (!(i >= n_matrix && g == 0.f)) {
 			if (i < n_matrix) g += c.l2 * w;
-			const float mm = c.beta1 * m1[i] + (1.f - c.beta1) * g;
-			const float vv = c.beta2 * m2[i] + (1.f - c.beta2) * (g * g);
-			m1[i] = mm;
-			m2[i] = vv;
-			const uint32_t s = steps[i] + 1;
-			steps[i] = s;
+			const float mm = c.beta1 * st.m1[i] + (1.f - c.beta1) * g;
+			const float vv = c.beta2 * st.m2[i] + (1.f - c.beta2) * (g * g);
+			st.m1[i] = mm;
+			st.m2[i] = vv;
+			const uint32_t s = st.steps[i] + 1;
+			st.steps[i] = s;
 			const float lr_s = lr * sqrtf(1.f - powf(c.beta2, (float)s)) / (1.f - powf(c.beta1, (float)s));
 			w = w - lr_s / (sqrtf(vv) + c.eps) * mm;
-			w32[i] = w;
-			w16[i] = (f16)w;
+			st.w32[i] = w;
+			const f16 h = (f16)w;
+			st.w16[i] = h;
+			if (st.frags && i < n_matrix) {
+				const uint32_t q0 = st.fragmap[2 * i], q1 = st.fragmap[2 * i + 1];
+				if (q0 != ~0u) st.frags[q0] = h;
+				if (q1 != ~0u) st.frags[q1] = h;
+			}
 		}
-		if (ema32) {
+		if (st.ema32) {
 			const float debias = 1.f - powf(c.ema_decay, (float)(step + 1));
-			const float v = c.ema_decay * ema32[i] + (1.f - c.ema_decay) * w;
-			ema32[i] = v;
-			ema16[i] = (f16)(v / debias);
+			const float v = c.ema_decay * st.ema32[i] + (1.f - c.ema_decay) * w;
+			st.ema32[i] = v;
+			st.ema16[i] = (f16)(v / debias);
 		}
 	}
 }
 
-__global__ void k_step_advance(uint32_t* ctl) { ctl[0] += 1; }
+__global__ void k_set_step(uint32_t* ctl, uint32_t step) { ctl[0] = step; }
 
 float AdamConfig::lr_at(uint32_t step) const {
 	float r = lr;
@@ -64,12 +68,15 @@ float AdamConfig::lr_at(uint32_t step) const {
 	return r;
 }
 
-void adam_ema_step(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float loss_scale, float* w32, f16* w16, const f16* g16,
-                   float* m1, float* m2, uint32_t* steps, float* ema32, f16* ema16, uint32_t* ctl, hipStream_t s) {
-	k_adam_ema<<<div_round_up(n, 256), 256, 0, s>>>(n, n_matrix, loss_scale, c, w32, w16, g16, m1, m2, steps,
-	                                                 c.ema_decay > 0.f ? ema32 : nullptr, ema16, ctl);
+void adam_ema_update(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float loss_scale, const AdamState& st, hipStream_t s) {
+	AdamState a = st;
+	if (c.ema_decay <= 0.f) a.ema32 = nullptr;
+	k_adam_ema<<<div_round_up(n, 256), 256, 0, s>>>(n, n_matrix, loss_scale, c, a);
 	NGP_HIP(hipGetLastError());
-	k_step_advance<<<1, 1, 0, s>>>(ctl);
+}
+
+void set_device_step(uint32_t* ctl, uint32_t step, hipStream_t s) {
+	k_set_step<<<1, 1, 0, s>>>(ctl, step);
 	NGP_HIP(hipGetLastError());
 }
 
