@@ -14,14 +14,13 @@ struct ScatterPlan {
 	uint32_t split_limit = 0;// buckets with more items are summed in parts (k_sc_split)
 	uint32_t part = 0;
 	uint32_t max_split_blocks = 0;
-	size_t cub_bytes = 0;
 	// workspace layout (bytes)
-	size_t off_hist = 0, off_scan = 0, off_cur = 0, off_cub = 0, off_split = 0, off_idx = 0, off_val = 0, total = 0;
+	size_t off_hist = 0, off_cur = 0, off_tot = 0, off_split = 0, off_idx = 0, off_val = 0, total = 0;
 };
 
 ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n);
 // Phase 1 (positions only, so it can run on a side stream while the forward pass and the MLP run):
-// bucket histogram per block of samples + exclusive scan.
+// bucket histogram per block of samples + per-bucket scans.
 void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace, hipStream_t s);
 // Phase 2: dL/dy -> gradient. overwrite: b.grad's grid section is fully written (no memset needed);
 // otherwise the sums are added to it. Same level masking as grid_backward.

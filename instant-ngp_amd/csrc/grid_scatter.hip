@@ -12,17 +12,17 @@
 // exact partial sums with one packed fp16 atomic per entry pair.
 //
 // Work is cut into (chunk of samples, level) blocks so no block walks the levels serially:
-//   prepare (positions only; runs on a side stream while the forward pass and the MLP run)
+//   prepare (positions only)
 //     k_sc_hist       per (chunk, level): LDS histogram over the level's buckets -> hist[bucket][chunk]
-//     (hipCUB)        exclusive scan of hist (bucket-major: each bucket's items are contiguous)
-//     k_sc_transpose  cursors[chunk][bucket] for coalesced loads in the scatter
+//     k_sc_scan       per bucket: exclusive scan over its chunks -> cursor within the bucket
+//                     cur[chunk][bucket] and the bucket total tot[bucket]. Every sample emits 2^D
+//                     items per level, so level l starts at item n * 2^D * l and a bucket's start is
+//                     that plus the scan of its level's totals (done where needed, <= 256 values).
 //   backward
 //     k_sc_scatter    per (chunk, level): items ranked per bucket in LDS, staged in bucket order, written
 //                     out as runs: (entry & (2^B-1)) u16 + F fp16 values
 //     k_sc_bucket     per bucket: zero LDS, accumulate, store every entry once (no memset, no atomics)
 //     k_sc_split      parts of oversized buckets: accumulate, packed fp16 atomics
-#include <hipcub/hipcub.hpp>
-
 #include "grid_scatter.h"
 
 #include <algorithm>
@@ -107,25 +107,50 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) hist[(size_t)(lv.vb_base[l] + j) * n_chunks + chunk] = h[j];
 }
 
-// offs[bucket][chunk] -> cur[chunk][bucket]
-__global__ void __launch_bounds__(256) k_sc_transpose(const uint32_t* __restrict__ in, uint32_t rows, uint32_t cols,
-                                                      uint32_t* __restrict__ out) {
-	__shared__ uint32_t tile[32][33];
-	const uint32_t r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
-	for (uint32_t k = threadIdx.x; k < 32 * 32; k += blockDim.x) {
-		const uint32_t r = r0 + k / 32, cI = c0 + k % 32;
-		if (r < rows && cI < cols) tile[k / 32][k % 32] = in[(size_t)r * cols + cI];
+// per bucket: exclusive scan of hist[bucket][0..n_chunks) -> cur[chunk][bucket]; tot[bucket] = total.
+// Also resets the split-part counter for this backward (split[0]).
+__global__ void __launch_bounds__(SC_THREADS) k_sc_scan(const uint32_t* __restrict__ hist, uint32_t n_chunks, uint32_t n_vb,
+                                                        uint32_t* __restrict__ cur, uint32_t* __restrict__ tot,
+                                                        uint32_t* __restrict__ split) {
+	__shared__ uint32_t wsum[SC_THREADS / 64];
+	const uint32_t vb = blockIdx.x;
+	const uint32_t* h = hist + (size_t)vb * n_chunks;
+	uint32_t carry = 0;
+	for (uint32_t b0 = 0; b0 < n_chunks; b0 += SC_THREADS) {
+		const uint32_t b = b0 + threadIdx.x;
+		const uint32_t v = b < n_chunks ? h[b] : 0u;
+		const uint32_t incl = wave_inclusive_scan(v);
+		if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+		__syncthreads();
+		uint32_t pre = carry;
+		for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) pre += wsum[w];
+		if (b < n_chunks) cur[(size_t)b * n_vb + vb] = pre + incl - v;
+		carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+		__syncthreads();
 	}
+	if (threadIdx.x == 0) {
+		tot[vb] = carry;
+		if (vb == 0) split[0] = 0u;
+	}
+}
+
+// sum of v[0..n) by one block (every thread gets the result)
+__device__ __forceinline__ uint32_t block_sum(const uint32_t* v, uint32_t n, uint32_t* wsum) {
+	uint32_t x = 0;
+	for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) x += v[k];
+	x = wave_inclusive_scan(x);
+	x = __shfl(x, 63);
 	__syncthreads();
-	for (uint32_t k = threadIdx.x; k < 32 * 32; k += blockDim.x) {
-		const uint32_t cI = c0 + k / 32, r = r0 + k % 32;
-		if (r < rows && cI < cols) out[(size_t)cI * rows + r] = tile[k % 32][k / 32];
-	}
+	if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = x;
+	__syncthreads();
+	uint32_t t = 0;
+	for (uint32_t w = 0; w < blockDim.x / 64; ++w) t += wsum[w];
+	return t;
 }
 
 template <uint32_t D, uint32_t F>
 __global__ void __launch_bounds__(SC_THREADS) k_sc_scatter(const GridConst c, const Levels lv, const GridBwdArgs a, uint32_t B,
-                                                           uint32_t n_vb, const uint32_t* __restrict__ cur_t,
+                                                           uint32_t n_vb, const uint32_t* __restrict__ cur_t, const uint32_t* __restrict__ tot,
                                                            uint16_t* __restrict__ item_idx, f16* __restrict__ item_val, uint32_t debug) {
 	typedef typename ValVec<F>::T V;
 	constexpr uint32_t NC = 1u << D;
@@ -140,8 +165,14 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_scatter(const GridConst c, co
 	uint32_t* st_pos = loff + nvb + 1;                     // [NIT] global position of the item in slot order
 	uint16_t* st_idx = (uint16_t*)(st_pos + NIT);          // [NIT]
 	V* st_val = (V*)(((uintptr_t)(st_idx + NIT) + 15) & ~(uintptr_t)15);  // [NIT]
+	// bucket starts of this level: n * 2^D * l + exclusive scan of the level's bucket totals
+	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) lh[j] = tot[lv.vb_base[l] + j];
+	__syncthreads();
+	block_exclusive_scan(lh, loff, nvb, wsum);
+	__syncthreads();
+	const uint32_t level_base = a.n * NC * l;
 	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) {
-		cur[j] = cur_t[(size_t)chunk * n_vb + lv.vb_base[l] + j];
+		cur[j] = level_base + loff[j] + cur_t[(size_t)chunk * n_vb + lv.vb_base[l] + j];
 		lh[j] = 0;
 	}
 	__syncthreads();
@@ -261,23 +292,30 @@ __device__ __forceinline__ void bucket_entries(const GridConst& c, const Levels&
 	n_e = min(1u << B, c.offsets[l + 1] - e0);
 }
 
-__device__ __forceinline__ uint32_t bucket_start(const uint32_t* offs, uint32_t n_chunks, uint32_t n_vb, uint32_t n_items, uint32_t vb) {
-	return vb >= n_vb ? n_items : offs[(size_t)vb * n_chunks];
+// bucket vb -> [lo, hi) in the item arrays (see k_sc_scan)
+template <uint32_t D>
+__device__ __forceinline__ void bucket_range(const Levels& lv, const uint32_t* tot, uint32_t n, uint32_t vb, uint32_t* wsum,
+                                             uint32_t& lo, uint32_t& hi) {
+	uint32_t l = 0;
+	while (lv.vb_base[l + 1] <= vb) ++l;
+	lo = n * (1u << D) * l + block_sum(tot + lv.vb_base[l], vb - lv.vb_base[l], wsum);
+	hi = lo + tot[vb];
 }
 
 // One workgroup per bucket: exact sum of the bucket's items, written once per entry with plain
 // stores (overwrite: every entry, untouched ones get 0 — no separate memset; accumulate: old + sum).
 // Buckets above `split_limit` items are zeroed here (overwrite) and queued for k_sc_split.
-template <uint32_t F>
-__global__ void __launch_bounds__(SC_THREADS) k_sc_bucket(const GridConst c, const Levels lv, const uint32_t* __restrict__ offs,
-                                                          uint32_t n_chunks, uint32_t n_vb, uint32_t n_items, uint32_t B,
+template <uint32_t D, uint32_t F>
+__global__ void __launch_bounds__(SC_THREADS) k_sc_bucket(const GridConst c, const Levels lv, const uint32_t* __restrict__ tot,
+                                                          uint32_t n, uint32_t B,
                                                           uint32_t split_limit, uint32_t part, const uint16_t* __restrict__ item_idx,
                                                           const f16* __restrict__ item_val, f16* __restrict__ grad, bool overwrite,
                                                           uint32_t* __restrict__ split, uint32_t debug) {
 	extern __shared__ unsigned long long acc[];
+	__shared__ uint32_t wsum[SC_THREADS / 64];
 	const uint32_t vb = blockIdx.x;
-	const uint32_t lo = bucket_start(offs, n_chunks, n_vb, n_items, vb);
-	const uint32_t hi = bucket_start(offs, n_chunks, n_vb, n_items, vb + 1);
+	uint32_t lo, hi;
+	bucket_range<D>(lv, tot, n, vb, wsum, lo, hi);
 	uint32_t e0, n_e;
 	bucket_entries(c, lv, B, vb, e0, n_e);
 	f16* g = grad + (size_t)e0 * F;
@@ -349,32 +387,31 @@ Levels make_levels(const GridDesc& g, uint32_t B) {
 template <uint32_t D>
 void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const GridBwdArgs& a, const ScatterPlan& p, char* ws,
                      hipStream_t s, bool overwrite, uint32_t debug) {
-	const uint32_t* scan = (const uint32_t*)(ws + p.off_scan);
+	const uint32_t* tot = (const uint32_t*)(ws + p.off_tot);
 	const uint32_t* cur_t = (const uint32_t*)(ws + p.off_cur);
 	uint32_t* split = (uint32_t*)(ws + p.off_split);
 	uint16_t* idx = (uint16_t*)(ws + p.off_idx);
 	f16* val = (f16*)(ws + p.off_val);
 	const uint32_t NIT = SC_THREADS * SC_SPT * (1u << D);
 	const size_t lds_s = (size_t)(3 * p.max_lb + 1) * 4 + (size_t)NIT * 6 + 16 + (size_t)NIT * F * 2;
-	const uint32_t n_items = (uint32_t)p.n_items;
 	const dim3 grid_s(p.n_chunks, c.n_levels);
 	auto go = [&](auto scatter, auto bucket, auto splitk) {
 		ensure_dynamic_lds((const void*)scatter, lds_s);
-		if (!(debug & 4)) scatter<<<grid_s, SC_THREADS, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, cur_t, idx, val, debug);
+		if (!(debug & 4)) scatter<<<grid_s, SC_THREADS, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, cur_t, tot, idx, val, debug);
 		NGP_HIP(hipGetLastError());
 		ensure_dynamic_lds((const void*)bucket, SC_LDS_BYTES);
 		ensure_dynamic_lds((const void*)splitk, SC_LDS_BYTES);
-		bucket<<<p.n_buckets, SC_THREADS, SC_LDS_BYTES, s>>>(c, lv, scan, p.n_chunks, p.n_buckets, n_items, p.B, p.split_limit, p.part,
-		                                                     idx, val, a.grad, overwrite, split, debug);
+		bucket<<<p.n_buckets, SC_THREADS, SC_LDS_BYTES, s>>>(c, lv, tot, a.n, p.B, p.split_limit, p.part, idx, val, a.grad, overwrite,
+		                                                     split, debug);
 		NGP_HIP(hipGetLastError());
 		splitk<<<p.max_split_blocks, SC_THREADS, SC_LDS_BYTES, s>>>(c, lv, idx, val, a.grad, p.B, split, debug);
 		NGP_HIP(hipGetLastError());
 	};
 	switch (F) {
-		case 1: go(k_sc_scatter<D, 1>, k_sc_bucket<1>, k_sc_split<1>); break;
-		case 2: go(k_sc_scatter<D, 2>, k_sc_bucket<2>, k_sc_split<2>); break;
-		case 4: go(k_sc_scatter<D, 4>, k_sc_bucket<4>, k_sc_split<4>); break;
-		case 8: go(k_sc_scatter<D, 8>, k_sc_bucket<8>, k_sc_split<8>); break;
+		case 1: go(k_sc_scatter<D, 1>, k_sc_bucket<D, 1>, k_sc_split<1>); break;
+		case 2: go(k_sc_scatter<D, 2>, k_sc_bucket<D, 2>, k_sc_split<2>); break;
+		case 4: go(k_sc_scatter<D, 4>, k_sc_bucket<D, 4>, k_sc_split<4>); break;
+		case 8: go(k_sc_scatter<D, 8>, k_sc_bucket<D, 8>, k_sc_split<8>); break;
 		default: throw Error("grid backward: unsupported F");
 	}
 }
@@ -401,13 +438,11 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	p.max_split_blocks = (uint32_t)(div_round_up(p.n_items, (uint64_t)p.part) + div_round_up(p.n_items, (uint64_t)p.split_limit) + 1);
 	const uint64_t len = (uint64_t)p.n_buckets * p.n_chunks;
 	NGP_CHECK(len < (1ull << 31), "grid backward: bucket histogram too large");
-	NGP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, p.cub_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)len));
 	auto align = [](size_t v) { return (v + 255) / 256 * 256; };
 	p.off_hist = 0;
-	p.off_scan = align(p.off_hist + len * 4);
-	p.off_cur = align(p.off_scan + len * 4);
-	p.off_cub = align(p.off_cur + len * 4);
-	p.off_split = align(p.off_cub + p.cub_bytes);
+	p.off_cur = align(p.off_hist + len * 4);
+	p.off_tot = align(p.off_cur + len * 4);
+	p.off_split = align(p.off_tot + (size_t)p.n_buckets * 4);
 	p.off_idx = align(p.off_split + (1 + 3 * (size_t)p.max_split_blocks) * 4);
 	p.off_val = align(p.off_idx + p.n_items * 2);
 	p.total = align(p.off_val + p.n_items * F * 2);
@@ -420,18 +455,14 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const Scatter
 	const GridConst c = make_grid_const(g);
 	const Levels lv = make_levels(g, p.B);
 	uint32_t* hist = (uint32_t*)(ws + p.off_hist);
-	uint32_t* scan = (uint32_t*)(ws + p.off_scan);
 	const dim3 grid_h(p.n_chunks, g.n_levels);
 	const size_t lds_h = (size_t)p.max_lb * 4;
 	if (g.n_dims == 3) k_sc_hist<3><<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
 	else k_sc_hist<2><<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
 	NGP_HIP(hipGetLastError());
-	size_t bytes = p.cub_bytes;
-	NGP_HIP(hipcub::DeviceScan::ExclusiveSum((void*)(ws + p.off_cub), bytes, hist, scan, (int)(p.n_buckets * p.n_chunks), s));
-	const dim3 grid_t(div_round_up(p.n_chunks, 32), div_round_up(p.n_buckets, 32));
-	k_sc_transpose<<<grid_t, 256, 0, s>>>(scan, p.n_buckets, p.n_chunks, (uint32_t*)(ws + p.off_cur));
+	k_sc_scan<<<p.n_buckets, SC_THREADS, 0, s>>>(hist, p.n_chunks, p.n_buckets, (uint32_t*)(ws + p.off_cur),
+	                                              (uint32_t*)(ws + p.off_tot), (uint32_t*)(ws + p.off_split));
 	NGP_HIP(hipGetLastError());
-	NGP_HIP(hipMemsetAsync(ws + p.off_split, 0, 4, s));
 }
 
 void grid_backward_sorted(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace, hipStream_t s,
