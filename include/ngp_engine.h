@@ -154,6 +154,66 @@ int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, 
 int ngp_graph_launch(ngp_graph* g, void* stream);
 void ngp_graph_destroy(ngp_graph* g);
 
+typedef struct { uint64_t state, inc; } ngp_rng; /* tcnn::pcg32 state (default_rng_t) */
+
+/* ---- losses and the generic training step (tcnn::Trainer::training_step) ------------------- */
+/* tcnn Loss otypes as named in the configs (configs/image/base.json:2-4 "L2", configs/sdf/base.json
+ * "MAPE"): value = l(pred, target) / (n * dims), gradient = loss_scale * dl/dpred / (n * dims) rounded
+ * to fp16; output columns >= dims get a zero gradient. */
+enum { NGP_LOSS_L2 = 0, NGP_LOSS_L1 = 1, NGP_LOSS_MAPE = 2, NGP_LOSS_SMAPE = 3, NGP_LOSS_RELATIVE_L2 = 4 };
+/* output fp16 AoS [n x output_stride], target fp32 AoS [n x target_stride], dL_doutput fp16 AoS;
+ * values (optional, device [n]): per-sample loss; loss_sum (optional, device scalar): += total */
+int ngp_loss_evaluate(int loss_type, void* stream, uint32_t n, uint32_t dims, const void* output, uint32_t output_stride,
+                      const float* target, uint32_t target_stride, float loss_scale, void* dL_doutput, uint32_t dL_stride,
+                      float* values, float* loss_sum);
+/* tcnn::Trainer::training_step(stream, input, target, data_pdf = nullptr, run_optimizer)
+ * (src/testbed_image.cu:276, src/testbed_sdf.cu:1304): forward, loss over the model's output_width
+ * columns, backward into the gradient buffer (overwrite) and, if run_optimizer, optimizer_step. */
+int ngp_trainer_training_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                              const float* target, uint32_t target_stride, int loss_type, float loss_scale, int run_optimizer,
+                              float* loss_sum);
+
+/* ---- image primitive (BASELINE C1; src/testbed_image.cu) -------------------------------------- */
+typedef struct ngp_image ngp_image;
+enum { NGP_IMAGE_RANDOM = 0, NGP_IMAGE_STRATIFIED = 3 };  /* ERandomMode (common.h:124-130) */
+typedef struct {
+	uint32_t random_mode;            /* Stratified (testbed.h:875) */
+	uint32_t snap_to_pixel_centers;  /* 1 (testbed.h:871) */
+	uint32_t linear_colors;          /* 0 (testbed.h:872): targets are sRGB-encoded */
+} ngp_image_config;
+int ngp_image_default_config(ngp_image_config* out);
+/* texture: RGBA fp32 [height x width x 4] in linear colours (EDataType::Float, e.g. albert.exr) */
+int ngp_image_create(uint32_t width, uint32_t height, const float* rgba_host, ngp_image** out);
+void ngp_image_destroy(ngp_image* img);
+/* generate_training_data of Testbed::train_image (testbed_image.cu:223-265): generate_random_uniform
+ * (advances *rng by 2n), stratify2_kernel (:62-76), eval_image_kernel_and_snap<float, 3> (:167-212).
+ * positions [n x 2], targets [n x 3] (device). */
+int ngp_image_generate_training_samples(const ngp_image* img, void* stream, uint32_t n, ngp_rng* rng, const ngp_image_config* cfg,
+                                        float* positions, float* targets);
+/* Testbed::train_image (testbed_image.cu:214-285): samples, training_step (L2, no optimizer), optimizer_step(128) */
+int ngp_image_train_step(ngp_image* img, ngp_trainer* t, void* stream, uint32_t batch, ngp_rng* rng, const ngp_image_config* cfg,
+                         float* loss_sum);
+
+/* ---- SDF primitive (BASELINE C5; src/testbed_sdf.cu) ------------------------------------------ */
+typedef struct ngp_sdf_mesh ngp_sdf_mesh;
+/* triangles [n x 9] already normalised to the unit cube (Testbed::load_mesh, testbed_sdf.cu:1120-1150);
+ * builds the surface-area CDF (triangle_distribution, :1167-1175) */
+int ngp_sdf_mesh_create(uint32_t n_triangles, const float* tris_host, ngp_sdf_mesh** out);
+void ngp_sdf_mesh_destroy(ngp_sdf_mesh* m);
+/* generate_training_samples_sdf (testbed_sdf.cu:1187-1275), non-octree branch: n/8 * {4 on the surface,
+ * 3 surface + logistic offset, 1 uniform in aabb}; n must be a multiple of 8; advances *rng by
+ * 3n + 3 * (3n/8). Signed distances by brute force over the triangles (the BVH is SURVEY §8f). */
+int ngp_sdf_generate_training_samples(ngp_sdf_mesh* m, void* stream, uint32_t n, ngp_rng* rng, const float* aabb_min,
+                                      const float* aabb_max, float stddev, float* positions, float* distances);
+/* signed_distance_raystab semantics (triangle_bvh.cu:415-433) over every triangle */
+int ngp_sdf_signed_distance(ngp_sdf_mesh* m, void* stream, uint32_t n, const float* positions, float* distances);
+/* shuffle<vec3> / shuffle<float> (testbed_sdf.cu:1295-1296): a bijection seeded by the training step */
+int ngp_sdf_shuffle(void* stream, uint32_t n, uint32_t seed, const float* positions, const float* distances,
+                    float* positions_shuffled, float* distances_shuffled);
+/* Testbed::train_sdf (testbed_sdf.cu:1289-1312): shuffle, training_step (MAPE, loss scale 128, optimizer) */
+int ngp_sdf_train_step(ngp_trainer* t, void* stream, uint32_t n, const float* positions, const float* distances, uint32_t step,
+                       float* positions_shuffled, float* distances_shuffled, float* loss_sum);
+
 /* ---- NeRF training kernels (src/testbed_nerf.cu), without OptiX --------------------------- */
 typedef struct ngp_nerf_dataset ngp_nerf_dataset;  /* training images on device + cameras */
 typedef struct ngp_nerf_trainer ngp_nerf_trainer;  /* Testbed NeRF training state (grid, counters, rng) */
@@ -184,7 +244,6 @@ typedef struct {
 	uint32_t target_batch_size;       /* 2^18 */
 } ngp_nerf_config;
 
-typedef struct { uint64_t state, inc; } ngp_rng; /* tcnn::pcg32 state (default_rng_t) */
 
 typedef struct {
 	uint32_t step, rays_per_batch, measured_batch_size, measured_batch_size_before_compaction;

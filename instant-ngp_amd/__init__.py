@@ -4,11 +4,11 @@ NeRF training kernels, behind the C-ABI in include/ngp_engine.h.
 The directory name is not a Python identifier; load it as `instant_ngp_amd` via
 __graft_entry__.load_package() (tests/conftest.py does the same).
 """
-from . import dp, nerf, synthetic  # noqa: F401
+from . import dp, image, nerf, sdf, synthetic  # noqa: F401
 from ._capi import NgpError, lib  # noqa: F401
 from .config import IMAGE_BASE, NERF_BASE, SDF_BASE, load_config, merge_patch, nerf_config  # noqa: F401
 from .network import (GRAD_ACCUMULATE, GRAD_OVERWRITE, LAYOUT_AOS, LAYOUT_SOA, Model, NerfNetwork,  # noqa: F401
-                      NetworkWithInputEncoding, Trainer, TrainingGraph, wrap_device)
+                      NetworkWithInputEncoding, Trainer, TrainingGraph, loss_evaluate, wrap_device)
 
 
 def create_nerf_network(cfg, n_pos_dims=3, n_dir_dims=3, n_extra_dims=0, dir_offset=4):

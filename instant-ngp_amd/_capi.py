@@ -52,6 +52,11 @@ class Rng(C.Structure):
     _fields_ = [("state", C.c_uint64), ("inc", C.c_uint64)]
 
 
+class ImageConfig(C.Structure):
+    """ngp_image_config: Testbed image training knobs (testbed.h:871-875)."""
+    _fields_ = [("random_mode", C.c_uint32), ("snap_to_pixel_centers", C.c_uint32), ("linear_colors", C.c_uint32)]
+
+
 class NerfStats(C.Structure):
     _fields_ = [("step", C.c_uint32), ("rays_per_batch", C.c_uint32), ("measured_batch_size", C.c_uint32),
                 ("measured_batch_size_before_compaction", C.c_uint32), ("loss", C.c_float)]
@@ -110,6 +115,19 @@ SIGNATURES = {
     "ngp_trainer_capture_training_step": (i32, [P, P, u32, P, u32, P, u32, f32, u32, i32, C.POINTER(P)]),
     "ngp_graph_launch": (i32, [P, P]),
     "ngp_graph_destroy": (None, [P]),
+    "ngp_loss_evaluate": (i32, [i32, P, u32, u32, P, u32, P, u32, f32, P, u32, P, P]),
+    "ngp_trainer_training_step": (i32, [P, P, u32, P, u32, P, u32, i32, f32, i32, P]),
+    "ngp_image_default_config": (i32, [C.POINTER(ImageConfig)]),
+    "ngp_image_create": (i32, [u32, u32, P, C.POINTER(P)]),
+    "ngp_image_destroy": (None, [P]),
+    "ngp_image_generate_training_samples": (i32, [P, P, u32, C.POINTER(Rng), C.POINTER(ImageConfig), P, P]),
+    "ngp_image_train_step": (i32, [P, P, P, u32, C.POINTER(Rng), C.POINTER(ImageConfig), P]),
+    "ngp_sdf_mesh_create": (i32, [u32, P, C.POINTER(P)]),
+    "ngp_sdf_mesh_destroy": (None, [P]),
+    "ngp_sdf_generate_training_samples": (i32, [P, P, u32, C.POINTER(Rng), P, P, f32, P, P]),
+    "ngp_sdf_signed_distance": (i32, [P, P, u32, P, P]),
+    "ngp_sdf_shuffle": (i32, [P, u32, u32, P, P, P, P]),
+    "ngp_sdf_train_step": (i32, [P, P, u32, P, P, u32, P, P, P]),
     "ngp_nerf_default_config": (i32, [f32, C.POINTER(NerfConfig)]),
     "ngp_nerf_dataset_create": (i32, [u32, C.POINTER(NerfImage), C.POINTER(P), C.POINTER(P)]),
     "ngp_nerf_dataset_destroy": (None, [P]),

@@ -19,6 +19,7 @@
 #include "mlp.h"
 #include "optimizer.h"
 #include "profiler.h"
+#include "training.h"
 
 namespace ngp {
 
@@ -131,7 +132,7 @@ struct ngp_model {
 	uint32_t* d_fragmap = nullptr;  // [n_matrix x 2] fragment slot (f16 index) of each matrix param: fwd, bwd
 	bool frags_current = false;     // `frags` holds the fragments of the current `params` (kept by the optimizer)
 	uint32_t n_all_frags = 0;
-	DevBuf frags, frags_inf, enc, denc, slabs, bin_hist, bin_sorted, scatter_ws;
+	DevBuf frags, frags_inf, enc, denc, slabs, bin_hist, bin_sorted, scatter_ws, out_ws, dl_ws;
 	int grid_backward_mode = 0;  // 0 auto, 1 direct (tcnn-style), 2 windowed (binned LDS), 3 bucketed (grid_scatter.h)
 	uint32_t win_debug = 0;      // timing experiments only (see binning.h, grid_scatter.h)
 	WinPlan win_plan;
@@ -738,6 +739,51 @@ int ngp_trainer_optimizer_step(ngp_trainer* t, void* stream, float loss_scale) {
 	NGP_TRY({
 		t->run_step(S(stream), loss_scale, nullptr, t->step);
 		t->step++;
+	});
+}
+
+int ngp_loss_evaluate(int loss_type, void* stream, uint32_t n, uint32_t dims, const void* output, uint32_t output_stride,
+                      const float* target, uint32_t target_stride, float loss_scale, void* dL_doutput, uint32_t dL_stride,
+                      float* values, float* loss_sum) {
+	NGP_ARG(loss_type >= 0 && (n == 0 || (output && target && dL_doutput)));
+	NGP_TRY({
+		LossEvalArgs a{n, dims, (const f16*)output, output_stride, target, target_stride, loss_scale, (f16*)dL_doutput, dL_stride,
+		               values, loss_sum};
+		loss_evaluate((uint32_t)loss_type, a, S(stream));
+	});
+}
+
+// tcnn::Trainer::training_step(stream, input, target, data_pdf = nullptr, run_optimizer)
+// (src/testbed_image.cu:276, src/testbed_sdf.cu:1304): forward -> loss -> backward [-> optimizer].
+// The fused MLP kernel needs dL/doutput up front, so the forward runs once as inference (output for
+// the loss) and once more inside the backward (recompute instead of stored activations).
+int ngp_trainer_training_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                              const float* target, uint32_t target_stride, int loss_type, float loss_scale, int run_optimizer,
+                              float* loss_sum) {
+	NGP_ARG(t && (n == 0 || (input && target)) && loss_scale > 0.f && loss_type >= 0);
+	NGP_TRY({
+		if (n == 0) return NGP_OK;
+		ngp_model* m = t->model;
+		m->require_params(false);
+		NGP_CHECK(m->gradients == t->g16, "training_step: the model's gradient buffer must be this trainer's");
+		hipStream_t s = S(stream);
+		const uint32_t W = 16;  // padded_output_width (nerf_network.h:463-465; FullyFusedMLP pads to 16)
+		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
+		f16* out = (f16*)m->out_ws.get((size_t)n * W * sizeof(f16));
+		f16* dl = (f16*)m->dl_ws.get((size_t)n * W * sizeof(f16));
+		m->generation++;
+		m->encode(s, n, input, input_stride, e, m->enc_width, AoS, false);
+		m->run_mlp(s, MLP_INFER, n, input, input_stride, e, out, W, AoS, nullptr, 0, nullptr, nullptr, false);
+		LossEvalArgs la{n, m->n_output_dims, out, W, target, target_stride, loss_scale, dl, W, nullptr, loss_sum};
+		{
+			ProfScope ps("loss", s);
+			loss_evaluate((uint32_t)loss_type, la, s);
+		}
+		m->train_pass(s, n, input, input_stride, e, nullptr, 0, dl, W, NGP_GRAD_OVERWRITE);
+		if (run_optimizer) {
+			t->run_step(s, loss_scale, nullptr, t->step);
+			t->step++;
+		}
 	});
 }
 

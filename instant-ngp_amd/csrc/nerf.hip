@@ -9,6 +9,7 @@
 #include <cstring>
 
 #include "nerf.h"
+#include "rng.h"
 
 namespace ngp {
 namespace nerf {
@@ -18,22 +19,6 @@ namespace nerf {
 // ------------------------------------------------------------------------------------------------
 struct V3 { float x, y, z; };
 __device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
-
-__device__ __forceinline__ uint32_t pcg_next(Rng& r) {
-	const uint64_t old = r.state;
-	r.state = old * 0x5851f42d4c957f2dULL + r.inc;
-	const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u), rot = (uint32_t)(old >> 59u);
-	return (xs >> rot) | (xs << ((~rot + 1u) & 31));
-}
-__device__ __forceinline__ float pcg_float(Rng& r) { return __uint_as_float((pcg_next(r) >> 9) | 0x3f800000u) - 1.0f; }
-__device__ __forceinline__ void pcg_advance(Rng& r, uint64_t delta) {
-	uint64_t cm = 0x5851f42d4c957f2dULL, cp = r.inc, am = 1u, ap = 0u;
-	while (delta > 0) {
-		if (delta & 1) { am *= cm; ap = ap * cm + cp; }
-		cp = (cm + 1) * cp; cm *= cm; delta /= 2;
-	}
-	r.state = am * r.state + ap;
-}
 
 // testbed_nerf.cu:114-184
 __device__ float to_stepping_space(float t, float cone) {

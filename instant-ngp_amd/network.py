@@ -198,6 +198,22 @@ class NetworkWithInputEncoding(Model):
         super().__init__(h)
 
 
+LOSSES = {"L2": 0, "L1": 1, "MAPE": 2, "SMAPE": 3, "RelativeL2": 4}  # NGP_LOSS_* (tcnn loss otypes)
+
+
+def loss_evaluate(loss, output, target, dims, loss_scale=128.0, stream=None):
+    """tcnn Loss::evaluate restated: output fp16 [n, 16], target float32 [n, >= dims] ->
+    (dL/doutput fp16 [n, 16], per-sample values float32 [n], total float)."""
+    n = output.shape[0]
+    dl = torch.empty((n, output.shape[1]), dtype=torch.float16, device=output.device)
+    vals = torch.empty(n, dtype=torch.float32, device=output.device)
+    tot = torch.zeros(1, dtype=torch.float32, device=output.device)
+    check(lib().ngp_loss_evaluate(LOSSES[loss] if isinstance(loss, str) else int(loss), _stream(stream), n, dims,
+                                  _ptr(output), output.stride(0), _ptr(target), target.stride(0), float(loss_scale),
+                                  _ptr(dl), dl.stride(0), _ptr(vals), _ptr(tot)))
+    return dl, vals, float(tot.item())
+
+
 class Trainer:
     """tcnn::Trainer<float, __half, __half>(network, optimizer, loss, seed) — src/testbed.cu:4129.
     The loss is applied by the caller (NeRF computes dL/doutput itself, testbed_nerf.cu:1660-2012)."""
@@ -236,6 +252,18 @@ class Trainer:
         import numpy as np
         a = np.ascontiguousarray(params_host, dtype=np.float32)
         check(lib().ngp_trainer_set_params_full_precision(self.handle, a.ctypes.data_as(C.c_void_p), a.size))
+
+    def training_step(self, x, target, loss="L2", loss_scale=128.0, run_optimizer=True, get_loss=True, stream=None):
+        """tcnn Trainer::training_step(stream, input, target, nullptr, run_optimizer) (src/testbed_image.cu:276,
+        src/testbed_sdf.cu:1304). target: CUDA float32 [n, >= output_width]. Returns the loss scalar."""
+        _check_input(x, self.model.input_width())
+        if not (target.is_cuda and target.dtype == torch.float32 and target.dim() == 2 and target.stride(1) == 1):
+            raise ValueError("target must be a CUDA float32 [n, dims] row-major tensor")
+        acc = torch.zeros(1, dtype=torch.float32, device=x.device) if get_loss else None
+        check(lib().ngp_trainer_training_step(self.handle, _stream(stream), x.shape[0], _ptr(x), x.stride(0), _ptr(target),
+                                              target.stride(0), LOSSES[loss] if isinstance(loss, str) else int(loss),
+                                              float(loss_scale), int(run_optimizer), _ptr(acc)))
+        return float(acc.item()) if get_loss else None
 
     def serialize(self):
         size = C.c_uint64(0)

@@ -109,3 +109,54 @@ def lego_like_dataset(n_images=100, width=800, height=800, seed=0, device="cpu",
         pixels.append(render(c2w, width, height, device=device))
     ds = NerfDataset(images, pixels)
     return (ds, images, pixels) if return_host else ds
+
+
+# ---- image / SDF stand-ins (albert.exr and armadillo.obj are not on the GPU box) --------------
+def synthetic_image(width=1024, height=1024, seed=0):
+    """An RGBA float32 [H, W, 4] linear-colour test image with edges, gradients and fine texture
+    (stand-in for data/image/albert.exr, 1024^2 RGBA float)."""
+    rs = np.random.RandomState(seed)
+    y, x = np.mgrid[0:height, 0:width].astype(np.float32)
+    x /= width
+    y /= height
+    img = np.zeros((height, width, 4), np.float32)
+    img[..., 0] = 0.5 + 0.5 * np.sin(12 * np.pi * x * (1 + y))
+    img[..., 1] = ((x - 0.5) ** 2 + (y - 0.5) ** 2 < 0.1).astype(np.float32) * 0.8 + 0.1 * y
+    img[..., 2] = np.clip(np.abs(np.sin(40 * x) * np.cos(33 * y)) + 0.05 * rs.standard_normal((height, width)), 0, 1)
+    img[..., 3] = 1.0
+    return np.ascontiguousarray(img ** 2.2)  # stored linear, like an EXR
+
+
+def icosphere(subdivisions=2, radius=1.0, center=(0.0, 0.0, 0.0), bumps=0.0, seed=0):
+    """Closed triangle mesh [T*3, 3] (outward winding). bumps > 0 displaces vertices radially by a
+    smooth random field (an armadillo stand-in with concavities)."""
+    t = (1.0 + 5 ** 0.5) / 2
+    verts = [(-1, t, 0), (1, t, 0), (-1, -t, 0), (1, -t, 0), (0, -1, t), (0, 1, t), (0, -1, -t), (0, 1, -t),
+             (t, 0, -1), (t, 0, 1), (-t, 0, -1), (-t, 0, 1)]
+    faces = [(0, 11, 5), (0, 5, 1), (0, 1, 7), (0, 7, 10), (0, 10, 11), (1, 5, 9), (5, 11, 4), (11, 10, 2), (10, 7, 6),
+             (7, 1, 8), (3, 9, 4), (3, 4, 2), (3, 2, 6), (3, 6, 8), (3, 8, 9), (4, 9, 5), (2, 4, 11), (6, 2, 10),
+             (8, 6, 7), (9, 8, 1)]
+    v = [np.array(p, np.float64) / np.linalg.norm(p) for p in verts]
+    for _ in range(subdivisions):
+        cache, nf = {}, []
+
+        def mid(a, b):
+            k = (min(a, b), max(a, b))
+            if k not in cache:
+                m = v[a] + v[b]
+                v.append(m / np.linalg.norm(m))
+                cache[k] = len(v) - 1
+            return cache[k]
+        for a, b, c in faces:
+            ab, bc, ca = mid(a, b), mid(b, c), mid(c, a)
+            nf += [(a, ab, ca), (b, bc, ab), (c, ca, bc), (ab, bc, ca)]
+        faces = nf
+    V = np.array(v)
+    if bumps > 0:
+        rs = np.random.RandomState(seed)
+        dirs = rs.standard_normal((6, 3))
+        dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+        field = sum(np.exp(4.0 * (V @ d - 1.0)) * rs.uniform(-1, 1) for d in dirs)
+        V = V * (1.0 + bumps * field)[:, None]
+    V = V * radius + np.asarray(center, np.float64)
+    return V[np.array(faces).reshape(-1)].astype(np.float32)

@@ -94,6 +94,11 @@ def _declare(L):
     d("orc_srgb_to_linear", f32, f32)
     d("orc_linear_to_srgb", f32, f32)
     d("orc_num_threads", C.c_int)
+    d("orc_loss", C.c_double, C.c_int, u32, u32, P, u32, P, u32, f32, P, u32, P)
+    d("orc_image_samples", None, u32, P, C.c_int, C.c_int, C.c_int, u32, u32, P, P, P)
+    d("orc_triangle_cdf", None, u32, P, P)
+    d("orc_sdf_samples", None, u32, P, u32, P, P, P, P, f32, P, P)
+    d("orc_sdf_signed_distance", None, u32, P, u32, P, P)
     _declare_nerf(L)
 
 
@@ -374,3 +379,58 @@ def fill_rollover(data, n_in, rescale=False):
         lib().orc_fill_rollover_f32(n, stride, n_in, ptr(data))
     else:
         lib().orc_fill_rollover_f16(n, stride, n_in, ptr(data), int(rescale))
+
+
+# ---- image / SDF / losses (ngp_train_oracle.c) ------------------------------------------------
+LOSSES = {"L2": 0, "L1": 1, "MAPE": 2, "SMAPE": 3, "RelativeL2": 4}
+
+
+def loss(loss_type, out16_bits, target, dims, loss_scale=128.0, dL_stride=16):
+    """tcnn loss restated: returns (total, dL/dout fp16 bits [n x dL_stride], per-sample values)."""
+    out16_bits = np.ascontiguousarray(out16_bits, dtype=np.uint16)
+    target = np.ascontiguousarray(target, dtype=np.float32)
+    n = out16_bits.shape[0]
+    dl = np.zeros((n, dL_stride), np.uint16)
+    vals = np.zeros(n, np.float32)
+    t = lib().orc_loss(LOSSES.get(loss_type, loss_type), n, dims, ptr(out16_bits), out16_bits.shape[1], ptr(target),
+                       target.shape[1], loss_scale, ptr(dl), dL_stride, ptr(vals))
+    return t, dl, vals
+
+
+def image_samples(n, rng, texture, random_mode=3, snap=True, linear_colors=False):
+    """Testbed::train_image's generate_training_data (testbed_image.cu:223-265). rng: Rng (advanced)."""
+    texture = np.ascontiguousarray(texture, dtype=np.float32)
+    H, W = texture.shape[:2]
+    pos = np.zeros((n, 2), np.float32)
+    tgt = np.zeros((n, 3), np.float32)
+    lib().orc_image_samples(n, C.byref(rng.s), random_mode, int(snap), int(linear_colors), W, H, ptr(texture), ptr(pos),
+                            ptr(tgt))
+    return pos, tgt
+
+
+def triangle_cdf(tris):
+    tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+    cdf = np.zeros(tris.shape[0], np.float32)
+    lib().orc_triangle_cdf(tris.shape[0], ptr(tris), ptr(cdf))
+    return cdf
+
+
+def sdf_samples(n, rng, tris, aabb_min, aabb_max, stddev):
+    """generate_training_samples_sdf positions + upper-bound distances (before the signed distance)."""
+    tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+    cdf = triangle_cdf(tris)
+    pos = np.zeros((n, 3), np.float32)
+    dist = np.zeros(n, np.float32)
+    lo = np.asarray(aabb_min, np.float32)
+    hi = np.asarray(aabb_max, np.float32)
+    lib().orc_sdf_samples(n, C.byref(rng.s), tris.shape[0], ptr(tris), ptr(cdf), ptr(lo), ptr(hi), stddev, ptr(pos),
+                          ptr(dist))
+    return pos, dist
+
+
+def sdf_signed_distance(pos, tris):
+    pos = np.ascontiguousarray(pos, dtype=np.float32).reshape(-1, 3)
+    tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+    out = np.zeros(pos.shape[0], np.float32)
+    lib().orc_sdf_signed_distance(pos.shape[0], ptr(pos), tris.shape[0], ptr(tris), ptr(out))
+    return out
