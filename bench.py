@@ -30,6 +30,19 @@ MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA spec
 ALGO = {
     "C2": {"enc_fwd_B": 300, "enc_bwd_B": 556, "mlp_train_flop": 55296, "mlp_fwd_flop": 18432},
     "C2p": {"enc_fwd_B": 588, "enc_bwd_B": 1100, "mlp_train_flop": 61440, "mlp_fwd_flop": 20480},
+    # SDF C5 (3D, L=16 F=2 T=2^22, 32 -> 64 -> 64 -> 16): training_step = inference + train pass
+    "C5": {"enc_fwd_B": 588, "enc_bwd_B": 1100, "mlp_train_flop": 43008, "mlp_fwd_flop": 14336},
+    # image (configs/image/base.json: 2D, L=16 F=2 T=2^24): 8 + 4*L*F*2 + L*F*2 fwd, 8 + 64 + 2*4*64 bwd
+    "IMG": {"enc_fwd_B": 328, "enc_bwd_B": 584, "mlp_train_flop": 43008, "mlp_fwd_flop": 14336},
+}
+WORKLOADS = {
+    "C2": "NerfNetwork training pass, C2 (configs/nerf/base.json fork: L=4 F=4 T=2^19, density 1x64 + rgb 2x64 fp16 MLPs), "
+          "fwd+bwd+Adam/EMA",
+    "C2p": "NerfNetwork training pass, C2' (L=16 F=2 T=2^19, density 1x64 + rgb 2x64 fp16 MLPs), fwd+bwd+Adam/EMA",
+    "C5": "Testbed::train_sdf step, C5 (configs/sdf/base.json with T=2^22: L=16 F=2, 2x64 MLP): shuffle + "
+          "training_step (inference, MAPE loss, fwd+bwd, Ema/Adam) on a resident synthetic batch",
+    "IMG": "Testbed::train_image step (configs/image/base.json: 2D L=16 F=2 T=2^24, 2x64 MLP): stratified samples, "
+           "sRGB targets, training_step (L2), optimizer_step",
 }
 
 
@@ -76,7 +89,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--variant", default="C2", choices=["C2", "C2p"])
+    ap.add_argument("--variant", default="C2", choices=["C2", "C2p", "C5", "IMG"])
     ap.add_argument("--batch", type=int, default=B)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="1: time the K steps as one captured HIP graph (N=1)")
@@ -89,25 +102,57 @@ def main():
     torch.cuda.set_device(local_rank)
     rank, world, local_rank = pkg.dp.init_from_env()
 
-    cfg = pkg.nerf_config(args.variant)
-    net = pkg.create_nerf_network(cfg)
-    if args.overlap is not None:
-        net.set_option("overlap", args.overlap)
-    trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
     n = args.batch
-    net.reserve(n)
-    x, dL = synthetic_batch(n, 1337 + rank, "cuda")
-    grads = trainer.gradients
     loss_scale = 128.0
+    if args.variant in ("C2", "C2p"):
+        cfg = pkg.nerf_config(args.variant)
+        net = pkg.create_nerf_network(cfg)
+        if args.overlap is not None:
+            net.set_option("overlap", args.overlap)
+        trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+        net.reserve(n)
+        x, dL = synthetic_batch(n, 1337 + rank, "cuda")
+        grads = trainer.gradients
 
-    def step():
-        net.forward_backward(x, dL)
-        div = pkg.dp.allreduce_gradients(grads, world)  # RCCL over xGMI; 1/N folded into the loss scale
-        trainer.optimizer_step(loss_scale * div)
+        def step():
+            net.forward_backward(x, dL)
+            div = pkg.dp.allreduce_gradients(grads, world)  # RCCL over xGMI; 1/N folded into the loss scale
+            trainer.optimizer_step(loss_scale * div)
+        graphable = True
+    elif args.variant == "C5":
+        cfg = json.loads(json.dumps(pkg.SDF_BASE))
+        cfg["encoding"].update({"log2_hashmap_size": 22, "per_level_scale": 2.0})
+        net = pkg.NetworkWithInputEncoding(3, 1, cfg["encoding"], cfg["network"])
+        trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+        verts = pkg.synthetic.icosphere(4, radius=0.35, bumps=0.3, seed=rank)
+        tris, amin, amax, brad = pkg.sdf.load_mesh(verts)
+        mesh = pkg.sdf.SdfMesh(tris)
+        sdf = pkg.sdf.SdfTraining(net, trainer, mesh, amin, amax, brad, seed=1337 + rank, batch_size=n)
+        sdf.generate_training_samples(n, sdf.positions, sdf.distances)  # resident batch (online regeneration untimed)
+        torch.cuda.synchronize()
+        if world > 1:
+            raise SystemExit("C5 bench is single-GPU")
+
+        def step():
+            sdf.train_step(get_loss=False, regenerate=False)
+        graphable = False
+    else:  # IMG
+        cfg = json.loads(json.dumps(pkg.IMAGE_BASE))
+        cfg["encoding"]["per_level_scale"] = 2.0
+        net = pkg.NetworkWithInputEncoding(2, 3, cfg["encoding"], cfg["network"])
+        trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+        img = pkg.image.Image(pkg.synthetic.synthetic_image(1024, 1024, seed=rank))
+        it = pkg.image.ImageTraining(net, trainer, img, seed=1337 + rank, batch_size=n)
+        if world > 1:
+            raise SystemExit("IMG bench is single-GPU")
+
+        def step():
+            it.train_step(get_loss=False)
+        graphable = False
 
     lib = pkg.lib()
     stream = torch.cuda.Stream()
-    use_graph = bool(args.graph) and world == 1
+    use_graph = bool(args.graph) and world == 1 and graphable
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
             step()
@@ -164,6 +209,7 @@ def main():
             "grid_backward": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
             "grid_backward_sorted": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
             "mlp_train": ("mfma", a["mlp_train_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
+            "mlp_infer": ("mfma", a["mlp_fwd_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
         }
         dom = max((k for k in roof if k in per_kernel), key=lambda k: per_kernel[k])
         bound, work, peak, unit = roof[dom]
@@ -188,9 +234,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f16",
             "data": "synthetic (U[0,1)^3 positions, uniform S^2 directions, U(+-1e-2) dL/dout; random-init weights)",
-            "config": {"workload": f"NerfNetwork training pass, {args.variant} (configs/nerf/base.json fork: "
-                                   + ("L=4 F=4 T=2^19" if args.variant == "C2" else "L=16 F=2 T=2^19")
-                                   + ", density 1x64 + rgb 2x64 fp16 MLPs), fwd+bwd+Adam/EMA",
+            "config": {"workload": WORKLOADS[args.variant],
                        "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
                        "launch": "hip_graph" if graph is not None else "eager"},
             "kernel_timing": ("HIP events per kernel on the launch stream, eager replay of the same K steps queued "
@@ -199,7 +243,7 @@ def main():
                          "frac": round(achieved / peak, 4), "traffic": None},
             "kernels": kern_summary,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.variant in ("C2", "C2p"):
             res["cpu_baseline"] = cpu_baseline(args.variant)
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -22,9 +22,9 @@ __device__ __forceinline__ float lr_schedule(const AdamConfig& c, uint32_t step)
 	return r;
 }
 
-__global__ void k_adam_ema(const uint32_t n, const uint32_t n_matrix, const float loss_scale, const AdamConfig c,
+__global__ void k_adam_ema(const uint32_t i0, const uint32_t n, const uint32_t n_matrix, const float loss_scale, const AdamConfig c,
                            const AdamState st) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t step = (st.step_base ? *st.step_base : 0u) + st.step_add;
 	if (i < n) {
 		const float lr = lr_schedule(c, step);
@@ -58,6 +58,78 @@ __global__ void k_adam_ema(const uint32_t n, const uint32_t n_matrix, const floa
 	}
 }
 
+// Four consecutive parameters per thread with 16-B loads/stores (8-B for the fp16 arrays): the update
+// is HBM-bound once the state outgrows the Infinity Cache (C5: 105 M params, 4.8 GB per step). A
+// group whose four parameters are all lazily skipped (grid entries without gradient) reads only the
+// gradient and the EMA inputs. Same per-parameter arithmetic as k_adam_ema.
+__global__ void __launch_bounds__(256) k_adam_ema4(const uint32_t n4, const uint32_t n_matrix, const float loss_scale,
+                                                   const AdamConfig c, const AdamState st) {
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= n4) return;
+	const uint32_t i0 = 4 * t;
+	const uint32_t step = (st.step_base ? *st.step_base : 0u) + st.step_add;
+	const f16x4 gh = *(const f16x4*)(st.g16 + i0);
+	float g[4];
+	bool act[4], any = false;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		g[k] = (float)gh[k] / loss_scale;
+		act[k] = !(i0 + k >= n_matrix && g[k] == 0.f);
+		any |= act[k];
+	}
+	if (!any && !st.ema32) return;
+	f32x4 w = *(const f32x4*)(st.w32 + i0);
+	if (any) {
+		const float lr = lr_schedule(c, step);
+		f32x4 m1 = *(const f32x4*)(st.m1 + i0), m2 = *(const f32x4*)(st.m2 + i0);
+		uint4 sp = *(const uint4*)(st.steps + i0);
+		uint32_t sv[4] = {sp.x, sp.y, sp.z, sp.w};
+		f16x4 wh = {};
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			if (act[k]) {
+				float gk = g[k];
+				if (i0 + k < n_matrix) gk += c.l2 * w[k];
+				const float mm = c.beta1 * m1[k] + (1.f - c.beta1) * gk;
+				const float vv = c.beta2 * m2[k] + (1.f - c.beta2) * (gk * gk);
+				m1[k] = mm;
+				m2[k] = vv;
+				const uint32_t sk = sv[k] + 1;
+				sv[k] = sk;
+				const float lr_s = lr * sqrtf(1.f - powf(c.beta2, (float)sk)) / (1.f - powf(c.beta1, (float)sk));
+				w[k] = w[k] - lr_s / (sqrtf(vv) + c.eps) * mm;
+			}
+			wh[k] = (f16)w[k];
+		}
+		*(f32x4*)(st.m1 + i0) = m1;
+		*(f32x4*)(st.m2 + i0) = m2;
+		*(uint4*)(st.steps + i0) = uint4{sv[0], sv[1], sv[2], sv[3]};
+		*(f32x4*)(st.w32 + i0) = w;
+		*(f16x4*)(st.w16 + i0) = wh;
+		if (st.frags && i0 < n_matrix) {
+#pragma unroll
+			for (int k = 0; k < 4; ++k) {
+				if (i0 + k >= n_matrix || !act[k]) continue;
+				const uint32_t q0 = st.fragmap[2 * (i0 + k)], q1 = st.fragmap[2 * (i0 + k) + 1];
+				if (q0 != ~0u) st.frags[q0] = wh[k];
+				if (q1 != ~0u) st.frags[q1] = wh[k];
+			}
+		}
+	}
+	if (st.ema32) {
+		const float debias = 1.f - powf(c.ema_decay, (float)(step + 1));
+		f32x4 e = *(const f32x4*)(st.ema32 + i0);
+		f16x4 eh;
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			e[k] = c.ema_decay * e[k] + (1.f - c.ema_decay) * w[k];
+			eh[k] = (f16)(e[k] / debias);
+		}
+		*(f32x4*)(st.ema32 + i0) = e;
+		*(f16x4*)(st.ema16 + i0) = eh;
+	}
+}
+
 __global__ void k_set_step(uint32_t* ctl, uint32_t step) { ctl[0] = step; }
 
 float AdamConfig::lr_at(uint32_t step) const {
@@ -71,7 +143,11 @@ float AdamConfig::lr_at(uint32_t step) const {
 void adam_ema_update(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float loss_scale, const AdamState& st, hipStream_t s) {
 	AdamState a = st;
 	if (c.ema_decay <= 0.f) a.ema32 = nullptr;
-	k_adam_ema<<<div_round_up(n, 256), 256, 0, s>>>(n, n_matrix, loss_scale, c, a);
+	const bool aligned = ((uintptr_t)a.w32 | (uintptr_t)a.m1 | (uintptr_t)a.m2 | (uintptr_t)a.steps | (uintptr_t)a.ema32 |
+	                      (uintptr_t)a.w16 | (uintptr_t)a.g16 | (uintptr_t)a.ema16) % 16 == 0;
+	const uint32_t n4 = aligned ? n / 4 : 0;
+	if (n4) k_adam_ema4<<<div_round_up(n4, 256), 256, 0, s>>>(n4, n_matrix, loss_scale, c, a);
+	if (4 * n4 < n) k_adam_ema<<<div_round_up(n - 4 * n4, 256), 256, 0, s>>>(4 * n4, n, n_matrix, loss_scale, c, a);
 	NGP_HIP(hipGetLastError());
 }
 
