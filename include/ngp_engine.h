@@ -289,6 +289,16 @@ void ngp_nerf_trainer_destroy(ngp_nerf_trainer* t);
 int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_nerf_stats* out);
 int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** density_grid, uint8_t** bitfield, float** mean_density);
 
+/* Data-parallel NeRF training (no counterpart in the reference, which trains on one GPU: SURVEY F7,
+ * §8e). `allreduce` reduces a device buffer in place across the ranks, ordered on `stream` (the
+ * caller's RCCL/torch.distributed binding); it is called for the fp16 gradient buffer (sum, before
+ * the optimizer), the density-grid splat (max) and three f32 counters (sum). Rank r traces the global
+ * rays [R r / N, R (r+1) / N) with their global ids and compacts to B / N samples. */
+enum { NGP_DTYPE_F32 = 0, NGP_DTYPE_F16 = 1 };
+enum { NGP_REDUCE_SUM = 0, NGP_REDUCE_MAX = 1 };
+typedef int (*ngp_allreduce_fn)(void* user, void* device_buf, uint64_t count, int dtype, int op, void* stream);
+int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn allreduce, void* user);
+
 #pragma GCC visibility pop
 #ifdef __cplusplus
 }

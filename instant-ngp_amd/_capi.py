@@ -144,6 +144,7 @@ SIGNATURES = {
     "ngp_nerf_trainer_destroy": (None, [P]),
     "ngp_nerf_train_step": (i32, [P, P, i32, C.POINTER(NerfStats)]),
     "ngp_nerf_trainer_buffers": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
+    "ngp_nerf_trainer_set_data_parallel": (i32, [P, u32, u32, P, P]),
 }
 
 

@@ -66,6 +66,8 @@ extern "C" int ngp_inference(ngp_model*, void*, uint32_t, const float*, uint32_t
 extern "C" int ngp_density(ngp_model*, void*, uint32_t, const float*, uint32_t, void*, uint32_t, uint32_t, int);
 extern "C" int ngp_forward_backward(ngp_model*, void*, uint32_t, const float*, uint32_t, void*, uint32_t, const void*, uint32_t, int);
 extern "C" int ngp_trainer_optimizer_step(ngp_trainer*, void*, float);
+extern "C" void* ngp_trainer_gradients(ngp_trainer*);
+extern "C" uint64_t ngp_model_n_params(const ngp_model*);
 extern "C" const char* ngp_last_error(void);
 
 struct ngp_nerf_trainer {
@@ -78,6 +80,13 @@ struct ngp_nerf_trainer {
 	uint32_t rays_per_batch = 1u << 12;  // testbed.h:440
 	uint32_t n_rays_total = 0;
 	uint32_t measured_batch_size = 0, measured_before_compaction = 0;
+	uint32_t measured_before_compaction_local = 0;  // this rank's pre-compaction count (inference sizing)
+	// data parallelism: rank r traces global rays [R r / N, R (r+1) / N), compacts to B / N,
+	// evaluates 1/N of the density-grid samples; the exchange steps go through `allreduce`
+	uint32_t rank = 0, world = 1;
+	ngp_allreduce_fn allreduce = nullptr;
+	void* allreduce_user = nullptr;
+	Buf dp_scalars;
 	// occupancy grid
 	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens;
 	// training workspaces
@@ -299,6 +308,15 @@ int ngp_nerf_trainer_create(ngp_model* model, ngp_trainer* trainer, const ngp_ne
 
 void ngp_nerf_trainer_destroy(ngp_nerf_trainer* t) { delete t; }
 
+int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn allreduce, void* user) {
+	if (!t || world == 0 || rank >= world || (world > 1 && !allreduce)) return NGP_INVALID;
+	t->rank = rank;
+	t->world = world;
+	t->allreduce = allreduce;
+	t->allreduce_user = user;
+	return NGP_OK;
+}
+
 int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** grid, uint8_t** bitfield, float** mean) {
 	if (!t) return NGP_INVALID;
 	if (grid) *grid = (float*)t->grid.p;
@@ -324,6 +342,7 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	const uint32_t n = n_uniform + n_nonuniform;
 	float* tmp = t->grid_tmp.get<float>(n_el);
 	NGP_HIP(hipMemsetAsync(tmp, 0, (size_t)n_el * 4, s));
+	// every rank generates the same sample set (same density rng); each evaluates its 1/N shard
 	float* pos = t->gpos.get<float>((size_t)n * 3);
 	uint32_t* idx = t->gidx.get<uint32_t>(n);
 	grid_generate_samples(n_uniform, t->grid_rng.dev(), t->ema_step, cfg, grid, n_cascades, -0.01f, pos, idx, s);
@@ -331,9 +350,18 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	grid_generate_samples(n_nonuniform, t->grid_rng.dev(), t->ema_step, cfg, grid, n_cascades, MIN_OPTICAL_THICKNESS,
 	                      pos + (size_t)n_uniform * 3, idx + n_uniform, s);
 	t->grid_rng.advance();
-	f16* dens = t->gdens.get<f16>((size_t)n * 16);
-	check_rc(ngp_density(t->model, s, n, pos, 3, dens, n, NGP_LAYOUT_SOA, 0));  // row 0 = raw density
-	grid_splat_max(n, idx, dens, cfg.density_activation, tmp, s);
+	const uint32_t lo = (uint32_t)((uint64_t)n * t->rank / t->world), hi = (uint32_t)((uint64_t)n * (t->rank + 1) / t->world);
+	const uint32_t ns = hi - lo;
+	f16* dens = t->gdens.get<f16>((size_t)std::max(ns, 1u) * 16);
+	if (ns) {
+		check_rc(ngp_density(t->model, s, ns, pos + (size_t)lo * 3, 3, dens, ns, NGP_LAYOUT_SOA, 0));  // row 0 = raw density
+		grid_splat_max(ns, idx + lo, dens, cfg.density_activation, tmp, s);
+	}
+	if (t->world > 1) {
+		// splatted maxima of all shards (values are >= 0: float max == max of the shards' atomicMax)
+		NGP_CHECK(t->allreduce(t->allreduce_user, tmp, n_el, NGP_DTYPE_F32, NGP_REDUCE_MAX, s) == 0,
+		          "data parallel: density-grid all-reduce failed");
+	}
 	grid_ema(n_el, decay, grid, tmp, s);
 	++t->ema_step;
 	grid_mean_bitfield(grid, cfg.max_cascade, (float*)t->mean.p, (uint8_t*)t->bitfield.p, s);
@@ -354,53 +382,79 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		}
 		// train_nerf_step (testbed_nerf.cu:3867-4132)
 		const uint32_t R = t->rays_per_batch;
-		const uint32_t max_samples = B * 16;
+		const uint32_t W = t->world, rk = t->rank;
+		const uint32_t r_lo = (uint32_t)((uint64_t)R * rk / W), Rl = (uint32_t)((uint64_t)R * (rk + 1) / W) - r_lo;
+		const uint32_t Bg = B;
+		const uint32_t Bl = (uint32_t)((uint64_t)Bg * (rk + 1) / W - (uint64_t)Bg * rk / W);
+		const uint32_t max_samples = Bl * 16;
 		uint32_t max_inference;
-		if (t->measured_before_compaction == 0) t->measured_before_compaction = max_inference = max_samples;
-		else max_inference = next_multiple(std::min(t->measured_before_compaction, max_samples), 256);
+		if (t->measured_before_compaction_local == 0) max_inference = max_samples;
+		else max_inference = next_multiple(std::min(t->measured_before_compaction_local, max_samples), 256);
 		if (t->training_step == 0) t->n_rays_total = 0;
 		const uint32_t n_rays_total = t->n_rays_total;
 		t->n_rays_total += R;
-		uint32_t* ray_indices = t->ray_indices.get<uint32_t>(R);
-		float* rays = t->rays.get<float>((size_t)R * 6);
-		uint32_t* numsteps = t->numsteps.get<uint32_t>((size_t)R * 2);
+		const uint32_t Ra = std::max(Rl, 1u);
+		uint32_t* ray_indices = t->ray_indices.get<uint32_t>(Ra);
+		float* rays = t->rays.get<float>((size_t)Ra * 6);
+		uint32_t* numsteps = t->numsteps.get<uint32_t>((size_t)Ra * 2);
 		float* coords = t->coords.get<float>((size_t)max_samples * 7);
-		f16* mlp_out = t->mlp_out.get<f16>((size_t)std::max(B, max_samples) * 16);
-		f16* dloss = t->dloss.get<f16>((size_t)B * 16);
-		float* coords_c = t->coords_c.get<float>((size_t)B * 7);
-		float* loss = t->loss.get<float>(R);
+		f16* mlp_out = t->mlp_out.get<f16>((size_t)std::max(Bl, max_samples) * 16);
+		f16* dloss = t->dloss.get<f16>((size_t)Bl * 16);
+		float* coords_c = t->coords_c.get<float>((size_t)Bl * 7);
+		float* loss = t->loss.get<float>(Ra);
 		uint32_t* ctr = t->counters.get<uint32_t>(4);  // rays kept, steps, compacted steps
-		NGP_HIP(hipMemsetAsync(loss, 0, (size_t)R * 4, s));
+		NGP_HIP(hipMemsetAsync(loss, 0, (size_t)Ra * 4, s));
 		(void)n_rays_total;
 		ngp_rng rng{t->rng.state, t->rng.inc};
-		check_rc(ngp_nerf_generate_training_samples(t->data, &cfg, s, R, 0, 0, rng, max_inference, (const uint8_t*)t->bitfield.p,
+		// global ray ids (rng.advance(i * 16), image_idx(i, R)) so the shards draw the 1-GPU rays;
+		// dL/doutput is scaled by 128 / R (global), so the summed gradient is the 1-GPU gradient
+		check_rc(ngp_nerf_generate_training_samples(t->data, &cfg, s, Rl, r_lo, R, rng, max_inference, (const uint8_t*)t->bitfield.p,
 		                                            ray_indices, rays, numsteps, coords, ctr));
 		check_rc(ngp_inference(t->model, s, max_inference, coords, 7, mlp_out, 16, NGP_LAYOUT_AOS, 0));
-		check_rc(ngp_nerf_compute_loss(t->data, &cfg, s, R, 0, rng, B, ctr, mlp_out, ray_indices, rays, numsteps, coords, coords_c,
-		                               dloss, loss, ctr + 2, (const float*)t->mean.p, 128.0f));
-		fill_rollover_f16(B, 16, ctr + 2, dloss, true, s);
-		fill_rollover_f32(B, 7, ctr + 2, coords_c, s);
-		check_rc(ngp_forward_backward(t->model, s, B, coords_c, 7, nullptr, 0, dloss, 16, NGP_GRAD_OVERWRITE));
+		const float loss_scale_local = 128.0f * (float)Rl / (float)R;
+		check_rc(ngp_nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, ray_indices, rays, numsteps, coords, coords_c,
+		                               dloss, loss, ctr + 2, (const float*)t->mean.p, W > 1 ? loss_scale_local : 128.0f));
+		fill_rollover_f16(Bl, 16, ctr + 2, dloss, true, s);
+		fill_rollover_f32(Bl, 7, ctr + 2, coords_c, s);
+		check_rc(ngp_forward_backward(t->model, s, Bl, coords_c, 7, nullptr, 0, dloss, 16, NGP_GRAD_OVERWRITE));
 		t->rng.advance();  // m_rng.advance() (testbed_nerf.cu:4127)
+		if (W > 1) {
+			NGP_CHECK(t->allreduce(t->allreduce_user, ngp_trainer_gradients(t->trainer), ngp_model_n_params(t->model), NGP_DTYPE_F16,
+			                       NGP_REDUCE_SUM, s) == 0,
+			          "data parallel: gradient all-reduce failed");
+		}
 		check_rc(ngp_trainer_optimizer_step(t->trainer, s, 128.0f));
 		++t->training_step;
 		// NerfCounters::update_after_training (testbed_nerf.cu:3583-3609): host sync
 		uint32_t h[4];
 		NGP_HIP(hipMemcpyAsync(h, ctr, 16, hipMemcpyDeviceToHost, s));
 		std::vector<float> hl;
-		if (get_loss) { hl.resize(R); NGP_HIP(hipMemcpyAsync(hl.data(), loss, (size_t)R * 4, hipMemcpyDeviceToHost, s)); }
+		if (get_loss && Rl) { hl.resize(Rl); NGP_HIP(hipMemcpyAsync(hl.data(), loss, (size_t)Rl * 4, hipMemcpyDeviceToHost, s)); }
 		NGP_HIP(hipStreamSynchronize(s));
+		double loss_sum = 0;
+		for (float v : hl) loss_sum += v;
+		t->measured_before_compaction_local = h[1];
+		if (W > 1) {
+			// counters and loss of all shards (NerfCounters::update_after_training on the global batch)
+			float* d = t->dp_scalars.get<float>(4);
+			const float hv[4] = {(float)h[1], (float)h[2], (float)loss_sum, 0.f};
+			NGP_HIP(hipMemcpyAsync(d, hv, 16, hipMemcpyHostToDevice, s));
+			NGP_CHECK(t->allreduce(t->allreduce_user, d, 3, NGP_DTYPE_F32, NGP_REDUCE_SUM, s) == 0,
+			          "data parallel: counter all-reduce failed");
+			float gv[4];
+			NGP_HIP(hipMemcpyAsync(gv, d, 16, hipMemcpyDeviceToHost, s));
+			NGP_HIP(hipStreamSynchronize(s));
+			h[1] = (uint32_t)gv[0];
+			h[2] = (uint32_t)gv[1];
+			loss_sum = gv[2];
+		}
 		float loss_scalar = 0.f;
 		t->measured_batch_size = 0;
 		t->measured_before_compaction = 0;
 		if (h[1] != 0 && h[2] != 0) {
 			t->measured_before_compaction = h[1];
 			t->measured_batch_size = h[2];
-			if (get_loss) {
-				double sum = 0;
-				for (float v : hl) sum += v;
-				loss_scalar = (float)(sum * (double)t->measured_batch_size / (double)B);
-			}
+			if (get_loss) loss_scalar = (float)(loss_sum * (double)t->measured_batch_size / (double)B);
 			uint32_t r = (uint32_t)((float)t->rays_per_batch * (float)B / (float)t->measured_batch_size);
 			t->rays_per_batch = std::min(next_multiple(r, 256), 1u << 18);
 		}

@@ -6,10 +6,16 @@ The reference trains on one GPU only (multi-GPU is render replication
 the new exchange step. Sharding keeps the *global* ray index i so every rank draws exactly the rays
 the 1-GPU run would draw (rng.advance(i * N_MAX_RANDOM_SAMPLES_PER_RAY), src/testbed_nerf.cu:1417-1421).
 """
+import ctypes as C
 import os
+import sys
+import traceback
 
 import torch
 import torch.distributed as dist
+
+# ngp_allreduce_fn (include/ngp_engine.h): int (*)(void* user, void* buf, uint64_t count, int dtype, int op, void* stream)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_void_p)
 
 
 def init_from_env(backend=None):
@@ -49,3 +55,33 @@ def allreduce_counters(values, world):
     if world > 1:
         dist.all_reduce(t)
     return t.cpu().tolist()
+
+
+def make_allreduce_callback(group=None):
+    """The engine's exchange hook (ngp_nerf_trainer_set_data_parallel) over torch.distributed.
+
+    nccl (= RCCL over xGMI): the all-reduce is enqueued on the engine's stream. gloo (CPU tests, or
+    several ranks sharing one GPU): host round trip, summed in fp32. Keep the returned object alive
+    while the engine may call it."""
+    from .network import wrap_device
+
+    def cb(user, ptr, count, dtype, op, stream):
+        try:
+            t = wrap_device(ptr, int(count), torch.float32 if dtype == 0 else torch.float16)
+            rop = dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX
+            if dist.get_backend(group) == "nccl":
+                s = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()
+                with torch.cuda.stream(s):
+                    dist.all_reduce(t, op=rop, group=group)
+            else:
+                (torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()).synchronize()
+                h = t.float().cpu()
+                dist.all_reduce(h, op=rop, group=group)
+                t.copy_(h.to(t.dtype))
+                torch.cuda.synchronize()
+            return 0
+        except Exception:
+            traceback.print_exc(file=sys.stderr)
+            return -1
+
+    return ALLREDUCE_FN(cb)

@@ -204,6 +204,16 @@ class NerfTraining:
         words = wrap_device(self._bitfield_ptr, BITFIELD_BYTES // 4, torch.float32)
         return words.view(torch.uint8)
 
+    def set_data_parallel(self, rank, world, group=None):
+        """Shard the rays (global ids kept), the compacted batch and the density-grid evaluation over
+        `world` ranks; gradients, density-grid maxima and counters are all-reduced through
+        torch.distributed (dp.make_allreduce_callback)."""
+        from .dp import make_allreduce_callback
+        self._allreduce = make_allreduce_callback(group) if world > 1 else None
+        check(lib().ngp_nerf_trainer_set_data_parallel(self.handle, rank, world,
+                                                       C.cast(self._allreduce, C.c_void_p) if self._allreduce else None,
+                                                       None))
+
     def train_step(self, get_loss=True, stream=None):
         st = NerfStats()
         check(lib().ngp_nerf_train_step(self.handle, _stream(stream), int(get_loss), C.byref(st)))
