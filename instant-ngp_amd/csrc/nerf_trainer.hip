@@ -437,7 +437,8 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		if (W > 1) {
 			// counters and loss of all shards (NerfCounters::update_after_training on the global batch)
 			float* d = t->dp_scalars.get<float>(4);
-			const float hv[4] = {(float)h[1], (float)h[2], (float)loss_sum, 0.f};
+			// per-ray losses are normalised by this shard's ray count (compute_loss): rescale to 1 / R
+			const float hv[4] = {(float)h[1], (float)h[2], (float)(loss_sum * (double)Rl / (double)R), 0.f};
 			NGP_HIP(hipMemcpyAsync(d, hv, 16, hipMemcpyHostToDevice, s));
 			NGP_CHECK(t->allreduce(t->allreduce_user, d, 3, NGP_DTYPE_F32, NGP_REDUCE_SUM, s) == 0,
 			          "data parallel: counter all-reduce failed");
