@@ -289,6 +289,19 @@ void ngp_nerf_trainer_destroy(ngp_nerf_trainer* t);
 int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_nerf_stats* out);
 int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** density_grid, uint8_t** bitfield, float** mean_density);
 
+/* Rendering (NerfTracer::init_rays_from_camera + trace + shade, testbed_nerf.cu:2229-2659,
+ * 948-1196, 2164-2226; ERenderMode::Shade, pinhole). camera: the view (xform after
+ * nerf_matrix_to_ngp, focal length in pixels, principal point); screen centre = 1 - principal point
+ * (set_camera_to_training_view, testbed.cu:852). spp samples starting at sample_index are averaged;
+ * out_rgba: device float [height x width x 4], linear colours composited over background_rgba
+ * (host, linear; NULL = transparent black). bitfield: the occupancy bitfield (NULL = march everywhere). */
+typedef struct ngp_nerf_renderer ngp_nerf_renderer;
+int ngp_nerf_renderer_create(ngp_nerf_renderer** out);
+void ngp_nerf_renderer_destroy(ngp_nerf_renderer* r);
+int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_config* cfg, void* stream, const ngp_nerf_image* camera,
+                    const uint8_t* bitfield, uint32_t spp, uint32_t sample_index, float min_transmittance,
+                    const float* background_rgba, int use_inference_params, float* out_rgba);
+
 /* Data-parallel NeRF training (no counterpart in the reference, which trains on one GPU: SURVEY F7,
  * §8e). `allreduce` reduces a device buffer in place across the ranks, ordered on `stream` (the
  * caller's RCCL/torch.distributed binding); it is called for the fp16 gradient buffer (sum, before

@@ -10,6 +10,8 @@
 #include "../../include/ngp_engine.h"
 #include "common.h"
 
+#include <functional>
+
 namespace ngp {
 namespace nerf {
 
@@ -94,6 +96,36 @@ void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, 
 void grid_ema(uint32_t n, float decay, float* grid, const float* grid_tmp, hipStream_t s);
 void grid_mean_bitfield(const float* grid, uint32_t max_cascade, float* mean_out, uint8_t* bitfield, hipStream_t s);
 size_t scan_temp_bytes(uint32_t n);
+
+// ---- rendering (NerfTracer) ------------------------------------------------------------------
+struct RenderArgs {
+	uint32_t width, height;
+	float focal[2], screen_center[2];
+	float cam[12];                 // camera-to-world mat4x3 (column-major)
+	float near_distance;
+	float aabb_min[3], aabb_max[3];
+	float cone_angle_constant;
+	uint32_t max_mip;              // max_cascade
+	const uint8_t* bitfield;
+	uint32_t sample_index, snap_to_pixel_centers, linear_colors;
+	uint32_t rgb_activation, density_activation;
+	float min_transmittance;
+	float background[4];           // linear rgba
+};
+struct RenderWorkspace {
+	void* payload[2]; void* payload_hit;
+	float* rgba[2]; float* rgba_hit;
+	float* coords;                 // [2^21 + 256 x 7]
+	f16* out;                      // [16 x (2^21 + 256)] RM
+	float* frame;                  // [W*H x 4]
+	uint32_t* counters;            // device [2]
+	uint32_t* host_counters;       // pinned [2]
+};
+size_t render_payload_bytes();
+// spp samples of one view, averaged into out (linear RGBA [H x W x 4]); infer(n, coords, out_rm)
+// evaluates the network on n NerfCoordinates (output RM, row stride n).
+void render_frame(const RenderArgs& a, uint32_t spp, RenderWorkspace& ws,
+                  const std::function<void(uint32_t, const float*, f16*)>& infer, float* out, hipStream_t s);
 
 }  // namespace nerf
 }  // namespace ngp

@@ -6,6 +6,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <functional>
 #include <cstring>
 
 #include "nerf.h"
@@ -693,6 +694,274 @@ void grid_mean_bitfield(const float* grid, uint32_t max_cascade, float* mean_out
 // ------------------------------------------------------------------------------------------------
 // host: effective camera matrix (glm quat_cast -> slerp(t=0, start == end) -> normalize -> mat3_cast)
 // ------------------------------------------------------------------------------------------------
+
+// ------------------------------------------------------------------------------------------------
+// Rendering: NerfTracer (testbed_nerf.cu:2229-2503 init/advance, 2504-2659 trace, 948-1196
+// generate_next_nerf_network_inputs / composite_kernel_nerf, 2164-2226 shade / compact), pinhole
+// cameras, ERenderMode::Shade. Compaction uses atomic slots like the reference: rays are independent,
+// so the image does not depend on their order.
+// ------------------------------------------------------------------------------------------------
+// random_val.cuh:162-291 (Burley 2019 scrambled Sobol)
+__device__ uint32_t sobol_dim(uint32_t index, uint32_t dim) {
+	// direction numbers of dims 0 and 1 (random_val.cuh:163-181)
+	uint32_t X = 0;
+	if (dim == 0) {
+		X = 0;
+#pragma unroll
+		for (uint32_t bit = 0; bit < 32; ++bit) X ^= ((index >> bit) & 1u) * (0x80000000u >> bit);
+	} else {
+		uint32_t v = 0x80000000u;  // dim 1: v_k = v_{k-1} ^ (v_{k-1} >> 1)
+#pragma unroll
+		for (uint32_t bit = 0; bit < 32; ++bit) {
+			X ^= ((index >> bit) & 1u) * v;
+			v ^= v >> 1;
+		}
+	}
+	return X;
+}
+__device__ __forceinline__ uint32_t hash_combine(uint32_t seed, uint32_t v) { return seed ^ (v + (seed << 6) + (seed >> 2)); }
+__device__ __forceinline__ uint32_t reverse_bits32(uint32_t x) { return __builtin_bitreverse32(x); }
+__device__ __forceinline__ uint32_t laine_karras(uint32_t x, uint32_t seed) {
+	x += seed;
+	x ^= x * 0x6c50b47cu;
+	x ^= x * 0xb82f1e52u;
+	x ^= x * 0xc7afe638u;
+	x ^= x * 0x8d22f6e6u;
+	return x;
+}
+__device__ __forceinline__ uint32_t nus_base2(uint32_t x, uint32_t seed) { return reverse_bits32(laine_karras(reverse_bits32(x), seed)); }
+__device__ float ld_random_val(uint32_t index, uint32_t seed, uint32_t dim = 0) {
+	const float S = (float)(1.0 / 4294967296.0);
+	index = nus_base2(index, seed);
+	return (float)nus_base2(sobol_dim(index, dim), hash_combine(seed, dim)) * S;
+}
+__device__ void ld_random_val_2d(uint32_t index, uint32_t seed, float* x, float* y) {
+	const float S = (float)(1.0 / 4294967296.0);
+	index = nus_base2(index, seed);
+	*x = (float)nus_base2(sobol_dim(index, 0), hash_combine(seed, 0)) * S;
+	*y = (float)nus_base2(sobol_dim(index, 1), hash_combine(seed, 1)) * S;
+}
+__device__ __forceinline__ float fractf_(float x) { return x - floorf(x); }
+__device__ void ld_random_pixel_offset(uint32_t spp, float* ox, float* oy) {  // random_val.cuh:320-326
+	float ax, ay, bx, by;
+	ld_random_val_2d(0, 0xdeadbeefu, &ax, &ay);
+	ld_random_val_2d(spp, 0xdeadbeefu, &bx, &by);
+	*ox = fractf_(0.5f - ax + bx);
+	*oy = fractf_(0.5f - ay + by);
+}
+
+// if_unoccupied_advance_to_next_occupied_voxel<MIP_FROM_DT = false> (testbed_nerf.cu:811-842)
+__device__ float advance_to_occupied(float t, float cone, V3 o, V3 d, V3 idir, const uint8_t* bitfield, uint32_t min_mip,
+                                     uint32_t max_mip, const Aabb& box) {
+	while (true) {
+		const V3 pos = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
+		if (t >= 16384.0f || !aabb_contains(box, pos)) return 16384.0f;
+		uint32_t mip = min(max(mip_from_pos(pos, CASCADES - 1), min_mip), max_mip);
+		if (!bitfield || density_grid_occupied_at(pos, bitfield, mip)) return t;
+		while (mip < max_mip && !density_grid_occupied_at(pos, bitfield, mip + 1)) ++mip;
+		t = advance_to_next_voxel(t, cone, pos, d, idir, mip);
+	}
+}
+
+struct Payload {  // NerfPayload (nerf.h:32-40)
+	float o[3], d[3];
+	float t, max_weight;
+	uint32_t idx, n_steps, alive;
+};
+
+__global__ void k_render_init(RenderArgs a, Payload* __restrict__ pay, float* __restrict__ rgba) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t W = a.width, H = a.height;
+	if (i >= W * H) return;
+	const uint32_t x = i % W, y = i / W;
+	float ox, oy;
+	ld_random_pixel_offset(a.snap_to_pixel_centers ? 0u : a.sample_index, &ox, &oy);
+	const float u = ((float)x + ox) / (float)W, v = ((float)y + oy) / (float)H;
+	// uv_to_ray (common_device.cuh:443-510), pinhole, screen_center = 1 - principal point (testbed.cu:852)
+	const float dx = (u - a.screen_center[0]) * (float)W / a.focal[0];
+	const float dy = (v - a.screen_center[1]) * (float)H / a.focal[1];
+	const float* m = a.cam;
+	V3 d = v3(m[0] * dx + m[3] * dy + m[6], m[1] * dx + m[4] * dy + m[7], m[2] * dx + m[5] * dy + m[8]);
+	V3 o = v3(m[9] + d.x * a.near_distance, m[10] + d.y * a.near_distance, m[11] + d.z * a.near_distance);
+	Payload p;
+	p.max_weight = 0.f;
+	p.idx = i;
+	p.n_steps = 0;
+	p.alive = 0;
+	rgba[4 * (size_t)i] = rgba[4 * (size_t)i + 1] = rgba[4 * (size_t)i + 2] = rgba[4 * (size_t)i + 3] = 0.f;
+	const float inv = 1.0f / sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+	d = v3(d.x * inv, d.y * inv, d.z * inv);
+	p.o[0] = o.x; p.o[1] = o.y; p.o[2] = o.z;
+	p.d[0] = d.x; p.d[1] = d.y; p.d[2] = d.z;
+	const Aabb box{v3(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v3(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
+	float tmin, tmax;
+	aabb_ray_intersect(box, o, d, &tmin, &tmax);
+	float t = fmaxf(tmin, 0.0f) + 1e-6f;
+	if (aabb_contains(box, v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z))) {
+		// advance_pos_nerf (:844-900): jitter the start by a scrambled-Sobol fraction of a step
+		const V3 idir = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+		t = advance_n_steps(t, a.cone_angle_constant, ld_random_val(a.sample_index, i * 786433u));
+		t = advance_to_occupied(t, a.cone_angle_constant, o, d, idir, a.bitfield, 0, a.max_mip, box);
+		if (t < 16384.0f) p.alive = 1;
+	}
+	p.t = t;
+	pay[i] = p;
+}
+
+// compact_kernel_nerf (:2198-2226)
+__global__ void k_render_compact(uint32_t n, const Payload* __restrict__ src, const float* __restrict__ src_rgba,
+                                 Payload* __restrict__ dst, float* __restrict__ dst_rgba, Payload* __restrict__ hit,
+                                 float* __restrict__ hit_rgba, uint32_t* __restrict__ counters) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const Payload p = src[i];
+	const f32x4 c = *(const f32x4*)(src_rgba + 4 * (size_t)i);
+	if (p.alive) {
+		const uint32_t k = atomicAdd(&counters[0], 1u);
+		dst[k] = p;
+		*(f32x4*)(dst_rgba + 4 * (size_t)k) = c;
+	} else if (c[3] > 0.001f) {
+		const uint32_t k = atomicAdd(&counters[1], 1u);
+		hit[k] = p;
+		*(f32x4*)(hit_rgba + 4 * (size_t)k) = c;
+	}
+}
+
+// generate_next_nerf_network_inputs (:948-1014): coordinate (i, j) at row i + j * n
+__global__ void k_render_inputs(RenderArgs a, uint32_t n, uint32_t n_steps, Payload* __restrict__ pay, float* __restrict__ coords) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	Payload& p = pay[i];
+	if (!p.alive) return;
+	const V3 o = v3(p.o[0], p.o[1], p.o[2]), d = v3(p.d[0], p.d[1], p.d[2]);
+	const V3 idir = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+	const Aabb box{v3(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v3(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
+	const V3 diag = v3(box.mx.x - box.mn.x, box.mx.y - box.mn.y, box.mx.z - box.mn.z);
+	const float cone = a.cone_angle_constant;
+	float t = p.t;
+	for (uint32_t j = 0; j < n_steps; ++j) {
+		t = advance_to_occupied(t, cone, o, d, idir, a.bitfield, 0, a.max_mip, box);
+		if (t >= 16384.0f) {
+			p.n_steps = j;
+			return;
+		}
+		const float dt = calc_dt(t, cone);
+		const V3 pos = v3(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
+		float* c = coords + (size_t)(i + j * n) * 7;
+		c[0] = (pos.x - box.mn.x) / diag.x; c[1] = (pos.y - box.mn.y) / diag.y; c[2] = (pos.z - box.mn.z) / diag.z;
+		c[3] = warp_dt(dt);
+		c[4] = (d.x + 1.0f) * 0.5f; c[5] = (d.y + 1.0f) * 0.5f; c[6] = (d.z + 1.0f) * 0.5f;
+		t += dt;
+	}
+	p.t = t;
+	p.n_steps = n_steps;
+}
+
+// composite_kernel_nerf (:1016-1196), ERenderMode::Shade; network output RM [16 x stride]
+__global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, uint32_t current_step, uint32_t n_steps,
+                                   Payload* __restrict__ pay, float* __restrict__ rgba, const float* __restrict__ coords,
+                                   const f16* __restrict__ out) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	Payload& p = pay[i];
+	if (!p.alive) return;
+	f32x4 c = *(const f32x4*)(rgba + 4 * (size_t)i);
+	const uint32_t actual = p.n_steps;
+	uint32_t j = 0;
+	for (; j < actual; ++j) {
+		const size_t r = i + (size_t)j * n;
+		const float o0 = (float)out[r], o1 = (float)out[r + stride], o2 = (float)out[r + 2 * (size_t)stride];
+		const float o3 = (float)out[r + 3 * (size_t)stride];
+		const float T = 1.f - c[3];
+		const float dt = unwarp_dt(coords[r * 7 + 3]);
+		const float alpha = 1.f - __expf(-network_to_density(o3, a.density_activation) * dt);
+		const float weight = alpha * T;
+		c[0] += network_to_rgb(o0, a.rgb_activation) * weight;
+		c[1] += network_to_rgb(o1, a.rgb_activation) * weight;
+		c[2] += network_to_rgb(o2, a.rgb_activation) * weight;
+		c[3] += weight;
+		if (weight > p.max_weight) p.max_weight = weight;
+		if (c[3] > (1.0f - a.min_transmittance)) {
+			const float inv = 1.0f / c[3];
+			c[0] *= inv; c[1] *= inv; c[2] *= inv; c[3] *= inv;
+			break;
+		}
+	}
+	if (j < n_steps) {
+		p.alive = 0;
+		p.n_steps = j + current_step;
+	}
+	*(f32x4*)(rgba + 4 * (size_t)i) = c;
+}
+
+// shade_kernel_nerf (:2164-2196) into the frame (pre-filled with the linear background), then the
+// spp average (the render buffer's accumulation)
+__global__ void k_render_shade(uint32_t n_hit, uint32_t linear_colors, const Payload* __restrict__ hit, const float* __restrict__ hit_rgba,
+                               float* __restrict__ frame) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n_hit) return;
+	f32x4 c = *(const f32x4*)(hit_rgba + 4 * (size_t)i);
+	if (!linear_colors) { c[0] = srgb_to_linear(c[0]); c[1] = srgb_to_linear(c[1]); c[2] = srgb_to_linear(c[2]); }
+	float* f = frame + 4 * (size_t)hit[i].idx;
+	for (int k = 0; k < 4; ++k) f[k] = c[k] + f[k] * (1.0f - c[3]);
+}
+__global__ void k_render_fill(uint32_t n, f32x4 bg, float* __restrict__ frame) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n) *(f32x4*)(frame + 4 * (size_t)i) = bg;
+}
+__global__ void k_render_accumulate(uint32_t n4, float w, const float* __restrict__ frame, float* __restrict__ acc, bool first) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n4) acc[i] = (first ? 0.f : acc[i]) + frame[i] * w;
+}
+
+void render_frame(const RenderArgs& a, uint32_t spp, RenderWorkspace& ws, const std::function<void(uint32_t, const float*, f16*)>& infer,
+                  float* out, hipStream_t s) {
+	const uint32_t n_px = a.width * a.height;
+	if (n_px == 0) return;
+	const uint32_t MARCH_ITER = 10000, MIN_STEPS = 1, MAX_STEPS = 8, TARGET_QUERIES = 2 * 1024 * 1024;
+	Payload* pay[2] = {(Payload*)ws.payload[0], (Payload*)ws.payload[1]};
+	float* rgba[2] = {ws.rgba[0], ws.rgba[1]};
+	Payload* hit = (Payload*)ws.payload_hit;
+	for (uint32_t sidx = 0; sidx < spp; ++sidx) {
+		RenderArgs r = a;
+		r.sample_index = a.sample_index + sidx;
+		k_render_fill<<<div_round_up(n_px, 256), 256, 0, s>>>(n_px, f32x4{a.background[0], a.background[1], a.background[2],
+		                                                                    a.background[3]}, ws.frame);
+		k_render_init<<<div_round_up(n_px, 128), 128, 0, s>>>(r, pay[0], rgba[0]);
+		NGP_HIP(hipGetLastError());
+		NGP_HIP(hipMemsetAsync(ws.counters, 0, 8, s));  // counters[1]: hits (whole trace)
+		uint32_t n_alive = n_px, it = 1, db = 0;
+		while (it < MARCH_ITER) {
+			Payload* src = pay[db % 2];
+			float* src_c = rgba[db % 2];
+			Payload* dst = pay[(db + 1) % 2];
+			float* dst_c = rgba[(db + 1) % 2];
+			++db;
+			NGP_HIP(hipMemsetAsync(ws.counters, 0, 4, s));
+			k_render_compact<<<div_round_up(n_alive, 256), 256, 0, s>>>(n_alive, src, src_c, dst, dst_c, hit, ws.rgba_hit, ws.counters);
+			NGP_HIP(hipGetLastError());
+			NGP_HIP(hipMemcpyAsync(ws.host_counters, ws.counters, 8, hipMemcpyDeviceToHost, s));
+			NGP_HIP(hipStreamSynchronize(s));
+			n_alive = ws.host_counters[0];
+			if (n_alive == 0) break;
+			const uint32_t n_steps = std::min(std::max(TARGET_QUERIES / n_alive, MIN_STEPS), MAX_STEPS);
+			k_render_inputs<<<div_round_up(n_alive, 128), 128, 0, s>>>(r, n_alive, n_steps, dst, ws.coords);
+			NGP_HIP(hipGetLastError());
+			const uint32_t n_el = next_multiple(n_alive * n_steps, 256);
+			infer(n_el, ws.coords, ws.out);
+			k_render_composite<<<div_round_up(n_alive, 128), 128, 0, s>>>(r, n_alive, n_el, it, n_steps, dst, dst_c, ws.coords, ws.out);
+			NGP_HIP(hipGetLastError());
+			it += n_steps;
+		}
+		const uint32_t n_hit = ws.host_counters[1];
+		if (n_hit) k_render_shade<<<div_round_up(n_hit, 256), 256, 0, s>>>(n_hit, a.linear_colors, hit, ws.rgba_hit, ws.frame);
+		k_render_accumulate<<<div_round_up(4 * n_px, 256), 256, 0, s>>>(4 * n_px, 1.0f / (float)spp, ws.frame, out, sidx == 0);
+		NGP_HIP(hipGetLastError());
+	}
+}
+
+size_t render_payload_bytes() { return sizeof(Payload); }
+
 void effective_camera_matrix(const float xf[12], float out[12]) {
 	// glm column-major m[c][r] = xf[3c + r]
 	auto M = [&](int c, int r) { return xf[3 * c + r]; };

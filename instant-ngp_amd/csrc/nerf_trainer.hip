@@ -70,6 +70,12 @@ extern "C" void* ngp_trainer_gradients(ngp_trainer*);
 extern "C" uint64_t ngp_model_n_params(const ngp_model*);
 extern "C" const char* ngp_last_error(void);
 
+struct ngp_nerf_renderer {
+	Buf pay0, pay1, payh, rgba0, rgba1, rgbah, coords, out, frame, counters;
+	uint32_t* host_counters = nullptr;
+	~ngp_nerf_renderer() { if (host_counters) (void)hipHostFree(host_counters); }
+};
+
 struct ngp_nerf_trainer {
 	ngp_model* model;
 	ngp_trainer* trainer;
@@ -308,6 +314,62 @@ int ngp_nerf_trainer_create(ngp_model* model, ngp_trainer* trainer, const ngp_ne
 
 void ngp_nerf_trainer_destroy(ngp_nerf_trainer* t) { delete t; }
 
+static void check_rc(int rc) { if (rc != NGP_OK) throw Error(ngp_last_error()); }
+
+// ---- rendering ---------------------------------------------------------------------------------
+int ngp_nerf_renderer_create(ngp_nerf_renderer** out) {
+	if (!out) return NGP_INVALID;
+	NERF_TRY({ *out = new ngp_nerf_renderer(); });
+}
+void ngp_nerf_renderer_destroy(ngp_nerf_renderer* r) { delete r; }
+
+int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_config* cfg, void* stream, const ngp_nerf_image* camera,
+                    const uint8_t* bitfield, uint32_t spp, uint32_t sample_index, float min_transmittance, const float* background_rgba,
+                    int use_inference_params, float* out_rgba) {
+	if (!r || !model || !cfg || !camera || !out_rgba || spp == 0) return NGP_INVALID;
+	NERF_TRY({
+		hipStream_t s = S(stream);
+		RenderArgs a{};
+		a.width = camera->width; a.height = camera->height;
+		a.focal[0] = camera->focal_length[0]; a.focal[1] = camera->focal_length[1];
+		a.screen_center[0] = 1.0f - camera->principal_point[0];  // set_camera_to_training_view (testbed.cu:852)
+		a.screen_center[1] = 1.0f - camera->principal_point[1];
+		effective_camera_matrix(camera->xform, a.cam);
+		a.near_distance = 0.0f;  // m_render_near_distance (testbed.h:914)
+		for (int k = 0; k < 3; ++k) { a.aabb_min[k] = cfg->aabb_min[k]; a.aabb_max[k] = cfg->aabb_max[k]; }
+		a.cone_angle_constant = cfg->cone_angle_constant;
+		a.max_mip = cfg->max_cascade;
+		a.bitfield = bitfield;
+		a.sample_index = sample_index;
+		a.snap_to_pixel_centers = cfg->snap_to_pixel_centers;
+		a.linear_colors = cfg->linear_colors;
+		a.rgb_activation = cfg->rgb_activation;
+		a.density_activation = cfg->density_activation;
+		a.min_transmittance = min_transmittance;
+		for (int k = 0; k < 4; ++k) a.background[k] = background_rgba ? background_rgba[k] : 0.f;
+		const uint32_t n_px = a.width * a.height;
+		const size_t max_q = (size_t)std::max(n_px, 2u * 1024 * 1024) + 256;
+		RenderWorkspace ws{};
+		const size_t pb = render_payload_bytes();
+		ws.payload[0] = r->pay0.get<char>(pb * n_px);
+		ws.payload[1] = r->pay1.get<char>(pb * n_px);
+		ws.payload_hit = r->payh.get<char>(pb * n_px);
+		ws.rgba[0] = r->rgba0.get<float>(4 * (size_t)n_px);
+		ws.rgba[1] = r->rgba1.get<float>(4 * (size_t)n_px);
+		ws.rgba_hit = r->rgbah.get<float>(4 * (size_t)n_px);
+		ws.coords = r->coords.get<float>(7 * max_q);
+		ws.out = r->out.get<f16>(16 * max_q);
+		ws.frame = r->frame.get<float>(4 * (size_t)n_px);
+		ws.counters = r->counters.get<uint32_t>(2);
+		if (!r->host_counters) NGP_HIP(hipHostMalloc(&r->host_counters, 16));
+		ws.host_counters = r->host_counters;
+		auto infer = [&](uint32_t n, const float* coords, f16* out) {
+			check_rc(ngp_inference(model, s, n, coords, 7, out, n, NGP_LAYOUT_SOA, use_inference_params));
+		};
+		render_frame(a, spp, ws, infer, out_rgba, s);
+	});
+}
+
 int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn allreduce, void* user) {
 	if (!t || world == 0 || rank >= world || (world > 1 && !allreduce)) return NGP_INVALID;
 	t->rank = rank;
@@ -325,7 +387,6 @@ int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** grid, uint8_t** bitfie
 	return NGP_OK;
 }
 
-static void check_rc(int rc) { if (rc != NGP_OK) throw Error(ngp_last_error()); }
 
 // update_density_grid_nerf (testbed_nerf.cu:3412-3536)
 static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay, uint32_t n_uniform, uint32_t n_nonuniform) {

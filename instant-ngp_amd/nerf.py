@@ -227,3 +227,57 @@ class NerfTraining:
             except Exception:
                 pass
             self.handle = None
+
+
+# ---- rendering / evaluation -------------------------------------------------------------------
+class NerfRenderer:
+    """NerfTracer (testbed_nerf.cu:2229-2659): renders a camera view with the network, marching the
+    occupancy bitfield. Output: linear RGBA [H, W, 4] float32 composited over `background` (linear)."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        check(lib().ngp_nerf_renderer_create(C.byref(h)))
+        self.handle = h
+
+    def render(self, network, cfg, camera, bitfield=None, spp=1, sample_index=0, min_transmittance=0.01,
+               background=(0.0, 0.0, 0.0, 0.0), use_inference_params=True, stream=None):
+        out = torch.empty((camera.height, camera.width, 4), dtype=torch.float32, device="cuda")
+        bg = (C.c_float * 4)(*[float(v) for v in background])
+        check(lib().ngp_nerf_render(self.handle, network.handle, C.byref(cfg), _stream(stream), C.byref(camera),
+                                    _ptr(bitfield), spp, sample_index, float(min_transmittance), bg,
+                                    int(use_inference_params), _ptr(out)))
+        return out
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                lib().ngp_nerf_renderer_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
+def linear_to_srgb(x):
+    return torch.where(x < 0.0031308, 12.92 * x, 1.055 * torch.pow(torch.clamp(x, min=0), 0.41666) - 0.055)
+
+
+def srgb_to_linear(x):
+    return torch.where(x <= 0.04045, x / 12.92, torch.pow((x + 0.055) / 1.055, 2.4))
+
+
+def ground_truth_linear(rgba8, background=(0.0, 0.0, 0.0)):
+    """The reference's render_ground_truth of a training/test image (sRGB RGBA8, premultiplied by
+    alpha in linear space, composited over the linear background), as a float [H, W, 4] tensor."""
+    px = torch.as_tensor(rgba8).float() / 255.0
+    a = px[..., 3:4]
+    rgb = srgb_to_linear(px[..., :3]) * a + torch.tensor(background, dtype=torch.float32) * (1 - a)
+    return torch.cat([rgb, torch.ones_like(a)], dim=-1)
+
+
+def psnr(image, ref):
+    """scripts/run.py:245-252: MSE of clip(linear_to_srgb(rgb), 0, 1), PSNR = -10 log10(MSE)."""
+    A = torch.clamp(linear_to_srgb(image[..., :3].float()), 0.0, 1.0)
+    R = torch.clamp(linear_to_srgb(ref[..., :3].float().to(A.device)), 0.0, 1.0)
+    mse = float(torch.mean((A - R) ** 2))
+    return -10.0 * math.log10(max(mse, 1e-12)), mse

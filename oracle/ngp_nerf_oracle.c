@@ -519,3 +519,127 @@ EXPORT void orc_fill_rollover_f16(uint32_t n_el, uint32_t stride, uint32_t n_in,
 		d[i] = r;
 	}
 }
+
+/* ------------------------------------------------------------------------------------------------
+ * Rendering (NerfTracer, testbed_nerf.cu:2229-2503, 2504-2659, 948-1196, 2164-2226), restated per
+ * ray: every ray is marched on its own (the GPU marches in compaction rounds of up to 8 steps; the
+ * per-ray sample sequence is the same). Two passes so the network can be evaluated in between:
+ * orc_nerf_render_march writes each pixel's sample coordinates (at most max_per_ray), then
+ * orc_nerf_render_composite composites the network outputs and shades over the background.
+ * random_val.cuh:162-326: scrambled Sobol (Burley 2019) for the pixel offset and the start jitter.
+ * ---------------------------------------------------------------------------------------------- */
+static uint32_t sobol_d(uint32_t index, uint32_t dim) {
+	uint32_t X = 0, v = 0x80000000u;
+	for (uint32_t bit = 0; bit < 32; ++bit) {
+		if ((index >> bit) & 1u) X ^= dim == 0 ? (0x80000000u >> bit) : v;
+		v ^= v >> 1;
+	}
+	return X;
+}
+static uint32_t hcomb(uint32_t seed, uint32_t v) { return seed ^ (v + (seed << 6) + (seed >> 2)); }
+static uint32_t rbits(uint32_t x) {
+	x = (((x & 0xaaaaaaaau) >> 1) | ((x & 0x55555555u) << 1));
+	x = (((x & 0xccccccccu) >> 2) | ((x & 0x33333333u) << 2));
+	x = (((x & 0xf0f0f0f0u) >> 4) | ((x & 0x0f0f0f0fu) << 4));
+	x = (((x & 0xff00ff00u) >> 8) | ((x & 0x00ff00ffu) << 8));
+	return (x >> 16) | (x << 16);
+}
+static uint32_t lkp(uint32_t x, uint32_t seed) {
+	x += seed; x ^= x * 0x6c50b47cu; x ^= x * 0xb82f1e52u; x ^= x * 0xc7afe638u; x ^= x * 0x8d22f6e6u;
+	return x;
+}
+static uint32_t nus(uint32_t x, uint32_t seed) { return rbits(lkp(rbits(x), seed)); }
+EXPORT float orc_ld_random_val(uint32_t index, uint32_t seed, uint32_t dim) {
+	const float S = (float)(1.0 / 4294967296.0);
+	index = nus(index, seed);
+	return (float)nus(sobol_d(index, dim), hcomb(seed, dim)) * S;
+}
+static float fractf_(float x) { return x - floorf(x); }
+static void pixel_offset(uint32_t spp, float* ox, float* oy) {
+	const float ax = orc_ld_random_val(0, 0xdeadbeefu, 0), ay = orc_ld_random_val(0, 0xdeadbeefu, 1);
+	const float bx = orc_ld_random_val(spp, 0xdeadbeefu, 0), by = orc_ld_random_val(spp, 0xdeadbeefu, 1);
+	*ox = fractf_(0.5f - ax + bx);
+	*oy = fractf_(0.5f - ay + by);
+}
+
+static float adv_occupied(float t, float cone, const float* o, const float* d, const float* idir, const uint8_t* bf,
+                          uint32_t max_mip, const ocfg* c) {
+	for (;;) {
+		float pos[3] = {o[0] + t * d[0], o[1] + t * d[1], o[2] + t * d[2]};
+		if (t >= 16384.0f || !contains(c, pos)) return 16384.0f;
+		uint32_t mip = mip_pos(pos, CASCADES - 1);
+		if (mip > max_mip) mip = max_mip;
+		if (!bf || occupied(pos, bf, mip)) return t;
+		while (mip < max_mip && !occupied(pos, bf, mip + 1)) ++mip;
+		t = advance_voxel(t, cone, pos, d, idir, mip);
+	}
+}
+
+/* coords: [W*H x max_per_ray x 7]; counts: [W*H] (-1 when the ray misses the aabb) */
+EXPORT void orc_nerf_render_march(const ocfg* c, const oimg* cam, const uint8_t* bf, uint32_t sample_index, uint32_t max_per_ray,
+                                  float* coords, int32_t* counts) {
+	float m[12];
+	orc_camera_matrix(cam->xform, m);
+	const uint32_t W = cam->width, H = cam->height;
+	float ox, oy;
+	pixel_offset(c->snap_to_pixel_centers ? 0u : sample_index, &ox, &oy);
+	const float diag[3] = {c->aabb_max[0] - c->aabb_min[0], c->aabb_max[1] - c->aabb_min[1], c->aabb_max[2] - c->aabb_min[2]};
+	for (uint32_t i = 0; i < W * H; ++i) {
+		const uint32_t x = i % W, y = i / W;
+		const float u = ((float)x + ox) / (float)W, v = ((float)y + oy) / (float)H;
+		const float dx = (u - (1.0f - cam->principal_point[0])) * (float)W / cam->focal_length[0];
+		const float dy = (v - (1.0f - cam->principal_point[1])) * (float)H / cam->focal_length[1];
+		float d[3] = {m[0] * dx + m[3] * dy + m[6], m[1] * dx + m[4] * dy + m[7], m[2] * dx + m[5] * dy + m[8]};
+		const float o[3] = {m[9], m[10], m[11]};
+		const float inv = 1.0f / sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+		d[0] *= inv; d[1] *= inv; d[2] *= inv;
+		float tmin, tmax;
+		ray_box(c, o, d, &tmin, &tmax);
+		float t = fmaxf(tmin, 0.0f) + 1e-6f;
+		const float p0[3] = {o[0] + t * d[0], o[1] + t * d[1], o[2] + t * d[2]};
+		counts[i] = -1;
+		if (!contains(c, p0)) continue;
+		const float idir[3] = {1.0f / d[0], 1.0f / d[1], 1.0f / d[2]};
+		const float cone = c->cone_angle_constant;
+		t = from_step(to_step(t, cone) + orc_ld_random_val(sample_index, i * 786433u, 0), cone);
+		uint32_t k = 0;
+		for (; k < max_per_ray; ++k) {
+			t = adv_occupied(t, cone, o, d, idir, bf, c->max_cascade, c);
+			if (t >= 16384.0f) break;
+			const float dt = calc_dt(t, cone);
+			const float pos[3] = {o[0] + d[0] * t, o[1] + d[1] * t, o[2] + d[2] * t};
+			float* q = coords + ((size_t)i * max_per_ray + k) * 7;
+			q[0] = (pos[0] - c->aabb_min[0]) / diag[0]; q[1] = (pos[1] - c->aabb_min[1]) / diag[1]; q[2] = (pos[2] - c->aabb_min[2]) / diag[2];
+			q[3] = (dt - MIN_STEP) / (MIN_STEP * (1 << (CASCADES - 1)) - MIN_STEP);
+			q[4] = (d[0] + 1.0f) * 0.5f; q[5] = (d[1] + 1.0f) * 0.5f; q[6] = (d[2] + 1.0f) * 0.5f;
+			t += dt;
+		}
+		counts[i] = (int32_t)k;
+	}
+}
+
+/* out16: network outputs [W*H x max_per_ray x 16] (AoS, half bits); frame: [W*H x 4] linear rgba */
+EXPORT void orc_nerf_render_composite(const ocfg* c, uint32_t n_px, uint32_t max_per_ray, const float* coords, const int32_t* counts,
+                                      const uint16_t* out16, float min_transmittance, const float* bg, float* frame) {
+	for (uint32_t i = 0; i < n_px; ++i) {
+		float r = 0, g = 0, b = 0, a = 0;
+		for (int32_t k = 0; k < counts[i]; ++k) {
+			const uint16_t* o = out16 + ((size_t)i * max_per_ray + k) * 16;
+			const float T = 1.f - a;
+			const float dt = coords[((size_t)i * max_per_ray + k) * 7 + 3] * (MIN_STEP * (1 << (CASCADES - 1)) - MIN_STEP) + MIN_STEP;
+			const float alpha = 1.f - expf(-to_dens(orc_f16_to_f32(o[3]), c->density_activation) * dt);
+			const float w = alpha * T;
+			r += to_rgb(orc_f16_to_f32(o[0]), c->rgb_activation) * w;
+			g += to_rgb(orc_f16_to_f32(o[1]), c->rgb_activation) * w;
+			b += to_rgb(orc_f16_to_f32(o[2]), c->rgb_activation) * w;
+			a += w;
+			if (a > 1.0f - min_transmittance) { const float inv = 1.0f / a; r *= inv; g *= inv; b *= inv; a *= inv; break; }
+		}
+		float* f = frame + 4 * (size_t)i;
+		f[0] = bg[0]; f[1] = bg[1]; f[2] = bg[2]; f[3] = bg[3];
+		if (counts[i] < 0 || !(a > 0.001f)) continue;
+		if (!c->linear_colors) { r = s2l(r); g = s2l(g); b = s2l(b); }
+		const float cc[4] = {r, g, b, a};
+		for (int k = 0; k < 4; ++k) f[k] = cc[k] + f[k] * (1.0f - a);
+	}
+}

@@ -290,6 +290,9 @@ def _declare_nerf(L):
     d("orc_nerf_grid_bitfield", None, P, u32, f32, P)
     d("orc_fill_rollover_f32", None, u32, u32, u32, P)
     d("orc_fill_rollover_f16", None, u32, u32, u32, P, C.c_int)
+    d("orc_ld_random_val", f32, u32, u32, u32)
+    d("orc_nerf_render_march", None, P, P, P, u32, u32, P, P)
+    d("orc_nerf_render_composite", None, P, u32, u32, P, P, P, f32, P, P)
 
 
 N_CELLS = 128 ** 3
@@ -434,3 +437,24 @@ def sdf_signed_distance(pos, tris):
     out = np.zeros(pos.shape[0], np.float32)
     lib().orc_sdf_signed_distance(pos.shape[0], ptr(pos), tris.shape[0], ptr(tris), ptr(out))
     return out
+
+
+def nerf_render(cfg, cam, model, params16, bitfield, sample_index=0, min_transmittance=0.01, bg=(0, 0, 0, 0),
+                max_per_ray=1024):
+    """NerfTracer restated per ray: march, oracle NerfNetwork on every sample, composite, shade.
+    Returns linear rgba [H, W, 4] and the per-pixel sample counts."""
+    W, H = cam.width, cam.height
+    coords = np.zeros((W * H, max_per_ray, 7), np.float32)
+    counts = np.zeros(W * H, np.int32)
+    bfp = ptr(bitfield) if bitfield is not None else None
+    lib().orc_nerf_render_march(C.byref(cfg), C.byref(cam), bfp, sample_index, max_per_ray, ptr(coords), ptr(counts))
+    mask = np.arange(max_per_ray)[None, :] < counts[:, None]
+    out16 = np.zeros((W * H, max_per_ray, 16), np.uint16)
+    if mask.any():
+        o = nerf_forward(model, params16, np.ascontiguousarray(coords[mask]))
+        out16[mask] = f32_to_f16_bits(o)
+    frame = np.zeros((W * H, 4), np.float32)
+    bgv = np.asarray(bg, np.float32)
+    lib().orc_nerf_render_composite(C.byref(cfg), W * H, max_per_ray, ptr(coords), ptr(counts), ptr(out16),
+                                    min_transmittance, ptr(bgv), ptr(frame))
+    return frame.reshape(H, W, 4), counts
