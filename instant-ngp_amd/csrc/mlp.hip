@@ -121,14 +121,36 @@ __device__ __forceinline__ void layer_fwd(f32x16 (&acc)[TILES], const f16x8 (&in
 	}
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// two fp32 -> packed fp16, round to nearest even (v_cvt_pk_f16_f32 on gfx950)
+__device__ __forceinline__ f16x2 cvt2(float a, float b) { return __builtin_convertvector(f32x2{a, b}, f16x2); }
+// ReLU on a packed pair (v_pk_max_f16)
+__device__ __forceinline__ f16x2 relu2(f16x2 x) { return __builtin_elementwise_max(x, f16x2{(f16)0.f, (f16)0.f}); }
+// backward ReLU: g where the (already ReLU'd, so >= 0) activation is nonzero, else 0, on packed bits:
+// (a & 0x7fff) min 1 is 1 or 0 per half, times g's bits (v_pk_min_u16 + v_pk_mul_lo_u16). Keeps no
+// per-element lane masks alive between the forward and the backward pass.
+__device__ __forceinline__ f16x2 relu_mask2(f16x2 a, f16x2 g) {
+	const u16x2 ab = __builtin_bit_cast(u16x2, a) & (unsigned short)0x7fff;
+	const u16x2 m = __builtin_elementwise_min(ab, u16x2{1, 1});
+	return __builtin_bit_cast(f16x2, (u16x2)(__builtin_bit_cast(u16x2, g) * m));
+}
+__device__ __forceinline__ f16x8 cat4(f16x2 a, f16x2 b, f16x2 c, f16x2 d) {
+	return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
 // Round an accumulator tile to fp16 (optionally ReLU) and split into the two k-step fragments.
 __device__ __forceinline__ void pack_tile(const f32x16& a, f16x8& lo, f16x8& hi, bool relu) {
+	f16x2 l[4], h[4];
 #pragma unroll
-	for (int j = 0; j < 8; ++j) {
-		f16 x = (f16)a[j], y = (f16)a[8 + j];
-		if (relu) { x = x > (f16)0.f ? x : (f16)0.f; y = y > (f16)0.f ? y : (f16)0.f; }
-		lo[j] = x; hi[j] = y;
+	for (int q = 0; q < 4; ++q) {
+		l[q] = cvt2(a[2 * q], a[2 * q + 1]);
+		h[q] = cvt2(a[8 + 2 * q], a[8 + 2 * q + 1]);
+		if (relu) { l[q] = relu2(l[q]); h[q] = relu2(h[q]); }
 	}
+	lo = cat4(l[0], l[1], l[2], l[3]);
+	hi = cat4(h[0], h[1], h[2], h[3]);
 }
 
 template <int TILES>
@@ -143,10 +165,13 @@ __device__ __forceinline__ void mask_pack(const f32x16 (&acc)[TILES], const f16x
 #pragma unroll
 	for (int t = 0; t < TILES; ++t)
 #pragma unroll
-		for (int r = 0; r < 16; ++r) {
-			const f16 a = act[2 * t + (r >> 3)][r & 7];
-			const f16 g = (f16)acc[t][r];
-			out[2 * t + (r >> 3)][r & 7] = a > (f16)0.f ? g : (f16)0.f;
+		for (int h = 0; h < 2; ++h) {
+			const f16x8 a = act[2 * t + h];
+			f16x2 r[4];
+#pragma unroll
+			for (int q = 0; q < 4; ++q)
+				r[q] = relu_mask2(f16x2{a[2 * q], a[2 * q + 1]}, cvt2(acc[t][8 * h + 2 * q], acc[t][8 * h + 2 * q + 1]));
+			out[2 * t + h] = cat4(r[0], r[1], r[2], r[3]);
 		}
 }
 
@@ -299,7 +324,7 @@ struct NerfLayout {
 };
 
 template <int ES, int DH, int RH, int MODE>
-__global__ void __launch_bounds__(256, 1) k_nerf_mlp(const NerfMlpArgs a) {
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_nerf_mlp(const NerfMlpArgs a) {
 	using Lay = NerfLayout<ES, DH, RH>;
 	constexpr bool TRAIN = MODE == MLP_TRAIN;
 	constexpr bool DENSITY = MODE == MLP_DENSITY;
