@@ -48,6 +48,7 @@ struct NerfMlpArgs {
 	f16* dL_denc; uint32_t denc_stride;           // training: [n x enc] (nullptr: skip)
 	float* dw_slab;                               // training: [gridDim.x x n_matrix] partial sums
 	uint32_t n_matrix;                            // matrix params = density MLP + rgb MLP
+	uint32_t n_reg;                               // LDS regions of the dW block reduction (set at launch)
 	uint32_t density_woff, rgb_woff;              // parameter offsets of the two MLPs
 };
 
@@ -59,6 +60,7 @@ struct MlpArgs {  // single MLP behind an encoding (tcnn::NetworkWithInputEncodi
 	const f16* dL_dout; uint32_t dL_stride;
 	f16* dL_denc; uint32_t denc_stride;
 	float* dw_slab; uint32_t n_matrix;
+	uint32_t n_reg;
 };
 
 // Host API ---------------------------------------------------------------------------------------

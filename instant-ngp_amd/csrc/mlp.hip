@@ -2,6 +2,8 @@
 // register/LDS layout contract).
 #include "mlp.h"
 
+#include <type_traits>
+
 namespace ngp {
 
 // ------------------------------------------------------------------------------------------------
@@ -131,10 +133,15 @@ __device__ __forceinline__ f16x2 relu2(f16x2 x) { return __builtin_elementwise_m
 // backward ReLU: g where the (already ReLU'd, so >= 0) activation is nonzero, else 0, on packed bits:
 // (a & 0x7fff) min 1 is 1 or 0 per half, times g's bits (v_pk_min_u16 + v_pk_mul_lo_u16). Keeps no
 // per-element lane masks alive between the forward and the backward pass.
-__device__ __forceinline__ f16x2 relu_mask2(f16x2 a, f16x2 g) {
-	const u16x2 ab = __builtin_bit_cast(u16x2, a) & (unsigned short)0x7fff;
-	const u16x2 m = __builtin_elementwise_min(ab, u16x2{1, 1});
-	return __builtin_bit_cast(f16x2, (u16x2)(__builtin_bit_cast(u16x2, g) * m));
+__device__ __forceinline__ uint32_t relu_mask_bits(uint32_t a, uint32_t g) {
+	// written out: the compiler otherwise turns the idiom back into per-half compares and selects
+	uint32_t t, r;
+	asm("v_and_b32 %0, 0x7fff7fff, %2\n\t"
+	    "v_pk_min_u16 %0, %0, %3\n\t"
+	    "v_pk_mul_lo_u16 %1, %4, %0"
+	    : "=&v"(t), "=v"(r)
+	    : "v"(a), "v"(0x00010001u), "v"(g));
+	return r;
 }
 __device__ __forceinline__ f16x8 cat4(f16x2 a, f16x2 b, f16x2 c, f16x2 d) {
 	return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
@@ -166,12 +173,13 @@ __device__ __forceinline__ void mask_pack(const f32x16 (&acc)[TILES], const f16x
 	for (int t = 0; t < TILES; ++t)
 #pragma unroll
 		for (int h = 0; h < 2; ++h) {
-			const f16x8 a = act[2 * t + h];
-			f16x2 r[4];
+			typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+			const u32x4 a = __builtin_bit_cast(u32x4, act[2 * t + h]);
+			u32x4 r;
 #pragma unroll
 			for (int q = 0; q < 4; ++q)
-				r[q] = relu_mask2(f16x2{a[2 * q], a[2 * q + 1]}, cvt2(acc[t][8 * h + 2 * q], acc[t][8 * h + 2 * q + 1]));
-			out[2 * t + h] = cat4(r[0], r[1], r[2], r[3]);
+				r[q] = relu_mask_bits(a[q], __builtin_bit_cast(uint32_t, cvt2(acc[t][8 * h + 2 * q], acc[t][8 * h + 2 * q + 1])));
+			out[2 * t + h] = __builtin_bit_cast(f16x8, r);
 		}
 }
 
@@ -223,8 +231,10 @@ __device__ __forceinline__ void dw_accum(f32x4* dw, const f16* dz_img, int dz_st
 // Flush one layer's dW tiles (16x16, 4 regs: out = 16m + 4(lane>>4) + r, in = 16n + (lane&15)) into
 // the block's fp32 LDS reduction buffer laid out as the parameter slice [out x in]. Waves flush one
 // after another (FIRST: store, else add) so the sum order is fixed: bitwise-reproducible gradients.
-template <int MT, int NT>
-__device__ __forceinline__ void dw_flush(const f32x4* dw, float* red, uint32_t woff, uint32_t in_dim, int lane, bool first) {
+template <int MT, int NT, bool FIRST>
+__device__ __forceinline__ void dw_flush(const f32x4* dw, float* red, uint32_t woff, uint32_t in_dim, int lane,
+                                         std::integral_constant<bool, FIRST>) {
+	constexpr bool first = FIRST;
 #pragma unroll
 	for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -235,6 +245,28 @@ __device__ __forceinline__ void dw_flush(const f32x4* dw, float* red, uint32_t w
 				float* p = red + woff + o * in_dim + i;
 				*p = first ? dw[m * NT + n][r] : *p + dw[m * NT + n][r];
 			}
+}
+
+// Block reduction of the per-wave dW registers into one fp32 slab, in a fixed order. n_reg LDS regions
+// of n_matrix floats (4 when they fit): waves w < n_reg store into region w, later waves add into
+// region w % n_reg in turn, then all threads sum the regions (0 + 1 + ...) and write the slab with
+// 16-B stores. FLUSH(red, first) stores/adds one wave's tiles at their parameter-slice offsets.
+template <typename Flush>
+__device__ __forceinline__ void dw_block_reduce(float* lds, uint32_t n_matrix, uint32_t n_reg, int wave, float* slab, Flush flush) {
+	for (int round = 0; round * (int)n_reg < 4; ++round) {
+		__syncthreads();
+		if (wave / (int)n_reg == round) {
+			float* red = lds + (size_t)(wave % n_reg) * n_matrix;
+			if (round == 0) flush(red, std::true_type{});
+			else flush(red, std::false_type{});
+		}
+	}
+	__syncthreads();
+	for (uint32_t i = 4 * threadIdx.x; i < n_matrix; i += 4 * blockDim.x) {
+		f32x4 v = *(const f32x4*)(lds + i);
+		for (uint32_t r = 1; r < n_reg; ++r) v += *(const f32x4*)(lds + (size_t)r * n_matrix + i);
+		*(f32x4*)(slab + i) = v;
+	}
 }
 
 // SH degree 4 of the warped direction (tcnn SphericalHarmonics; oracle orc_sh4), features 8h..8h+7.
@@ -478,30 +510,23 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	}
 
 	if constexpr (TRAIN) {
-		// block reduction of dW into LDS (parameter-slice layout), then one slab per block
-		float* red = (float*)smem;
+		// block reduction of dW (parameter-slice layout) into one slab per block
 		const uint32_t dw0 = a.density_woff, rw0 = a.rgb_woff;
 		const uint32_t d_out_off = dw0 + 64 * 16 * ES + 64 * 64 * (DH - 1);
 		const uint32_t r_out_off = rw0 + 64 * 32 + 64 * 64 * (RH - 1);
-		for (int w = 0; w < 4; ++w) {
-			__syncthreads();
-			if (wave == w) {
-				const bool first = w == 0;
-				dw_flush<1, 4>(dw + Lay::W_RO, red, r_out_off, 64, lane, first);
+		dw_block_reduce((float*)smem, a.n_matrix, a.n_reg, wave, a.dw_slab + (size_t)blockIdx.x * a.n_matrix,
+		                [&](float* red, auto first) {
+			dw_flush<1, 4>(dw + Lay::W_RO, red, r_out_off, 64, lane, first);
 #pragma unroll
-				for (int l = RH - 1; l >= 1; --l)
-					dw_flush<4, 4>(dw + Lay::W_RH + 16 * (RH - 1 - l), red, rw0 + 64 * 32 + 64 * 64 * (l - 1), 64, lane, first);
-				dw_flush<4, 2>(dw + Lay::W_R0, red, rw0, 32, lane, first);
-				dw_flush<1, 4>(dw + Lay::W_DO, red, d_out_off, 64, lane, first);
+			for (int l = RH - 1; l >= 1; --l)
+				dw_flush<4, 4>(dw + Lay::W_RH + 16 * (RH - 1 - l), red, rw0 + 64 * 32 + 64 * 64 * (l - 1), 64, lane, first);
+			dw_flush<4, 2>(dw + Lay::W_R0, red, rw0, 32, lane, first);
+			dw_flush<1, 4>(dw + Lay::W_DO, red, d_out_off, 64, lane, first);
 #pragma unroll
-				for (int l = DH - 1; l >= 1; --l)
-					dw_flush<4, 4>(dw + Lay::W_DH + 16 * (DH - 1 - l), red, dw0 + 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane, first);
-				dw_flush<4, ES>(dw + Lay::W_D0, red, dw0, 16 * ES, lane, first);
-			}
-		}
-		__syncthreads();
-		float* slab = a.dw_slab + (size_t)blockIdx.x * a.n_matrix;
-		for (uint32_t i = threadIdx.x; i < a.n_matrix; i += blockDim.x) slab[i] = red[i];
+			for (int l = DH - 1; l >= 1; --l)
+				dw_flush<4, 4>(dw + Lay::W_DH + 16 * (DH - 1 - l), red, dw0 + 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane, first);
+			dw_flush<4, ES>(dw + Lay::W_D0, red, dw0, 16 * ES, lane, first);
+		});
 	}
 }
 
@@ -511,18 +536,18 @@ static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	constexpr bool TRAIN = MODE == MLP_TRAIN;
 	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (MODE == MLP_DENSITY ? Lay::F_R0 : Lay::N_FWD);
 	size_t lds = (size_t)NFRAG * 1024 + (TRAIN ? 4 * Lay::IMG_HALVES * sizeof(f16) : 0);
-	if (TRAIN) lds = std::max(lds, (size_t)a.n_matrix * sizeof(float));
+	uint32_t n_reg = 4;
+	while (n_reg > 1 && (size_t)n_reg * a.n_matrix * sizeof(float) > 160 * 1024) n_reg /= 2;
+	if (TRAIN) lds = std::max(lds, (size_t)n_reg * a.n_matrix * sizeof(float));
 	NGP_CHECK(lds <= 160 * 1024, "NerfNetwork MLP: LDS budget exceeded");
 	const uint32_t tiles = (a.n + 31) / 32;
 	uint32_t blocks = TRAIN ? nerf_mlp_train_blocks(a.n) : std::min<uint32_t>(div_round_up(tiles, 4), 8 * device_cu_count());
 	if (blocks == 0) return;
 	auto kern = k_nerf_mlp<ES, DH, RH, MODE>;
-	static bool attr_set = false;
-	if (!attr_set) {
-		ensure_dynamic_lds((const void*)kern, lds);
-		attr_set = true;
-	}
-	kern<<<blocks, 256, lds, s>>>(a);
+	ensure_dynamic_lds((const void*)kern, lds);
+	auto ak = a;
+	ak.n_reg = n_reg;
+	kern<<<blocks, 256, lds, s>>>(ak);
 	NGP_HIP(hipGetLastError());
 }
 
@@ -674,22 +699,15 @@ __global__ void __launch_bounds__(256, 1) k_mlp(const MlpArgs a) {
 		}
 	}
 	if constexpr (TRAIN) {
-		float* red = (float*)smem;
 		const uint32_t o_off = 64 * 16 * ES + 64 * 64 * (NH - 1);
-		for (int w = 0; w < 4; ++w) {
-			__syncthreads();
-			if (wave == w) {
-				const bool first = w == 0;
-				dw_flush<1, 4>(dw + Lay::W_O, red, o_off, 64, lane, first);
+		dw_block_reduce((float*)smem, a.n_matrix, a.n_reg, wave, a.dw_slab + (size_t)blockIdx.x * a.n_matrix,
+		                [&](float* red, auto first) {
+			dw_flush<1, 4>(dw + Lay::W_O, red, o_off, 64, lane, first);
 #pragma unroll
-				for (int l = NH - 1; l >= 1; --l)
-					dw_flush<4, 4>(dw + Lay::W_H + 16 * (NH - 1 - l), red, 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane, first);
-				dw_flush<4, ES>(dw + Lay::W_0, red, 0, 16 * ES, lane, first);
-			}
-		}
-		__syncthreads();
-		float* slab = a.dw_slab + (size_t)blockIdx.x * a.n_matrix;
-		for (uint32_t i = threadIdx.x; i < a.n_matrix; i += blockDim.x) slab[i] = red[i];
+			for (int l = NH - 1; l >= 1; --l)
+				dw_flush<4, 4>(dw + Lay::W_H + 16 * (NH - 1 - l), red, 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane, first);
+			dw_flush<4, ES>(dw + Lay::W_0, red, 0, 16 * ES, lane, first);
+		});
 	}
 }
 
@@ -701,17 +719,17 @@ static void launch_mlp(const MlpArgs& a, hipStream_t s) {
 	constexpr bool TRAIN = MODE == MLP_TRAIN;
 	constexpr int NFRAG = TRAIN ? Lay::N_ALL : Lay::N_FWD;
 	size_t lds = (size_t)NFRAG * 1024 + (TRAIN ? 4 * Lay::IMG_HALVES * sizeof(f16) : 0);
-	if (TRAIN) lds = std::max(lds, (size_t)a.n_matrix * sizeof(float));
+	uint32_t n_reg = 4;
+	while (n_reg > 1 && (size_t)n_reg * a.n_matrix * sizeof(float) > 160 * 1024) n_reg /= 2;
+	if (TRAIN) lds = std::max(lds, (size_t)n_reg * a.n_matrix * sizeof(float));
 	NGP_CHECK(lds <= 160 * 1024, "MLP: LDS budget exceeded");
 	const uint32_t tiles = (a.n + 31) / 32;
 	uint32_t blocks = TRAIN ? mlp_train_blocks(a.n) : std::min<uint32_t>(div_round_up(tiles, 4), 8 * device_cu_count());
 	auto kern = k_mlp<ES, NH, MODE>;
-	static bool attr_set = false;
-	if (!attr_set) {
-		ensure_dynamic_lds((const void*)kern, lds);
-		attr_set = true;
-	}
-	kern<<<blocks, 256, lds, s>>>(a);
+	ensure_dynamic_lds((const void*)kern, lds);
+	auto ak = a;
+	ak.n_reg = n_reg;
+	kern<<<blocks, 256, lds, s>>>(ak);
 	NGP_HIP(hipGetLastError());
 }
 
