@@ -7,7 +7,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libngp_engine.so")
+# NGP_ENGINE_LIB selects another build of the same library (A/B experiments); default is in-tree.
+LIB_PATH = os.environ.get("NGP_ENGINE_LIB") or os.path.join(HERE, "lib", "libngp_engine.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "ngp_engine.h")
 
 _lib = None

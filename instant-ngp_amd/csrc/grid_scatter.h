@@ -14,8 +14,10 @@ struct ScatterPlan {
 	uint32_t split_limit = 0;// buckets with more items are summed in parts (k_sc_split)
 	uint32_t part = 0;
 	uint32_t max_split_blocks = 0;
+	uint32_t max_split_buckets = 0;
 	// workspace layout (bytes)
-	size_t off_hist = 0, off_cur = 0, off_tot = 0, off_split = 0, off_idx = 0, off_val = 0, total = 0;
+	size_t off_hist = 0, off_cur = 0, off_tot = 0, off_split = 0, off_splitb = 0, off_scratch = 0, off_idx = 0, off_val = 0,
+	       total = 0;
 };
 
 ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n);

@@ -8,8 +8,8 @@
 // bucket sums them in LDS with 64-bit integer atomics in units of 2^-24 (the fp16 quantum, so every
 // fp16 contribution is exact and the sum is order-independent; LDS integer atomics run ~12x faster
 // than LDS float atomics on gfx950, profiles/r01_lds_atomics.txt). The sum is rounded once to fp16
-// and stored; buckets too large for one workgroup (coarse levels) are summed in parts that add their
-// exact partial sums with one packed fp16 atomic per entry pair.
+// and stored; buckets too large for one workgroup (coarse levels) are summed in parts whose exact
+// int64 partial sums are added by a reduce kernel (no fp16 atomics: bitwise reproducible).
 //
 // Work is cut into (chunk of samples, level) blocks so no block walks the levels serially:
 //   prepare (positions only)
@@ -22,17 +22,28 @@
 //     k_sc_scatter    per (chunk, level): items ranked per bucket in LDS, staged in bucket order, written
 //                     out as runs: (entry & (2^B-1)) u16 + F fp16 values
 //     k_sc_bucket     per bucket: zero LDS, accumulate, store every entry once (no memset, no atomics)
-//     k_sc_split      parts of oversized buckets: accumulate, packed fp16 atomics
+//     k_sc_split      parts of oversized buckets: accumulate, store int64 partial sums
+//     k_sc_split_reduce  per oversized bucket: sum its parts (exact), write every entry once
 #include "grid_scatter.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace ngp {
 
 namespace {
 
 constexpr uint32_t SC_THREADS = 256;
-constexpr uint32_t SC_SPT = 2;               // samples per thread in hist/scatter blocks
+constexpr uint32_t SC_BT = 1024;             // bucket/split blocks: 2 per CU by LDS, 32 waves to hide latency
+#ifndef SC_CHUNK_SAMPLES
+#define SC_CHUNK_SAMPLES 512
+#endif
+#ifndef SC_SCATTER_THREADS
+#define SC_SCATTER_THREADS 512
+#endif
+constexpr uint32_t SC_CHUNK = SC_CHUNK_SAMPLES;     // samples per (chunk, level) block
+constexpr uint32_t SC_ST = SC_SCATTER_THREADS;      // scatter block: 16 waves per CU at 2 blocks
+constexpr uint32_t SC_SSPT = SC_CHUNK / SC_ST;      // samples per scatter thread
 constexpr size_t SC_LDS_BYTES = 64 * 1024;   // one bucket's int64 accumulators
 constexpr float FIX_SCALE = 16777216.0f;     // 2^24: fp16 values are integer multiples of 2^-24
 
@@ -55,10 +66,11 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x) {
 	return s;
 }
 
-// Exclusive scan of cnt[0..n) into off[0..n] (off[n] = total) by one 256-thread block.
+// Exclusive scan of cnt[0..n) into off[0..n] (off[n] = total) by one NT-thread block.
+template <uint32_t NT>
 __device__ __forceinline__ void block_exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, uint32_t* wsum) {
 	uint32_t carry = 0;
-	for (uint32_t b0 = 0; b0 < n; b0 += SC_THREADS) {
+	for (uint32_t b0 = 0; b0 < n; b0 += NT) {
 		const uint32_t b = b0 + threadIdx.x;
 		const uint32_t v = b < n ? cnt[b] : 0u;
 		const uint32_t incl = wave_inclusive_scan(v);
@@ -67,7 +79,8 @@ __device__ __forceinline__ void block_exclusive_scan(const uint32_t* cnt, uint32
 		uint32_t pre = carry;
 		for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) pre += wsum[w];
 		if (b < n) off[b] = pre + incl - v;
-		carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+#pragma unroll
+		for (uint32_t w = 0; w < NT / 64; ++w) carry += wsum[w];
 		__syncthreads();
 	}
 	if (threadIdx.x == 0) off[n] = carry;
@@ -93,8 +106,8 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 	__syncthreads();
 	const uint32_t off_l = c.offsets[l];
 #pragma unroll
-	for (uint32_t q = 0; q < SC_SPT; ++q) {
-		const uint32_t i = chunk * SC_THREADS * SC_SPT + q * SC_THREADS + threadIdx.x;
+	for (uint32_t q = 0; q < SC_CHUNK / SC_THREADS; ++q) {
+		const uint32_t i = chunk * SC_CHUNK + q * SC_THREADS + threadIdx.x;
 		if (i >= a.n) continue;
 		float x[D];
 		load_pos<D>(a, i, x);
@@ -108,7 +121,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 }
 
 // per bucket: exclusive scan of hist[bucket][0..n_chunks) -> cur[chunk][bucket]; tot[bucket] = total.
-// Also resets the split-part counter for this backward (split[0]).
+// Also resets the split-part and split-bucket counters for this backward (split[0], split[1]).
 __global__ void __launch_bounds__(SC_THREADS) k_sc_scan(const uint32_t* __restrict__ hist, uint32_t n_chunks, uint32_t n_vb,
                                                         uint32_t* __restrict__ cur, uint32_t* __restrict__ tot,
                                                         uint32_t* __restrict__ split) {
@@ -130,7 +143,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_scan(const uint32_t* __restri
 	}
 	if (threadIdx.x == 0) {
 		tot[vb] = carry;
-		if (vb == 0) split[0] = 0u;
+		if (vb == 0) { split[0] = 0u; split[1] = 0u; }
 	}
 }
 
@@ -149,14 +162,14 @@ __device__ __forceinline__ uint32_t block_sum(const uint32_t* v, uint32_t n, uin
 }
 
 template <uint32_t D, uint32_t F>
-__global__ void __launch_bounds__(SC_THREADS) k_sc_scatter(const GridConst c, const Levels lv, const GridBwdArgs a, uint32_t B,
+__global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const Levels lv, const GridBwdArgs a, uint32_t B,
                                                            uint32_t n_vb, const uint32_t* __restrict__ cur_t, const uint32_t* __restrict__ tot,
                                                            uint16_t* __restrict__ item_idx, f16* __restrict__ item_val, uint32_t debug) {
 	typedef typename ValVec<F>::T V;
 	constexpr uint32_t NC = 1u << D;
-	constexpr uint32_t NIT = SC_THREADS * SC_SPT * NC;  // items per block
+	constexpr uint32_t NIT = SC_CHUNK * NC;  // items per block
 	extern __shared__ uint32_t lds[];
-	__shared__ uint32_t wsum[SC_THREADS / 64];
+	__shared__ uint32_t wsum[SC_ST / 64];
 	const uint32_t chunk = blockIdx.x, l = blockIdx.y;
 	const uint32_t nvb = lv.vb_base[l + 1] - lv.vb_base[l];
 	uint32_t* cur = lds;                                   // [nvb] this block's global cursor per bucket
@@ -168,7 +181,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_scatter(const GridConst c, co
 	// bucket starts of this level: n * 2^D * l + exclusive scan of the level's bucket totals
 	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) lh[j] = tot[lv.vb_base[l] + j];
 	__syncthreads();
-	block_exclusive_scan(lh, loff, nvb, wsum);
+	block_exclusive_scan<SC_ST>(lh, loff, nvb, wsum);
 	__syncthreads();
 	const uint32_t level_base = a.n * NC * l;
 	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) {
@@ -178,12 +191,12 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_scatter(const GridConst c, co
 	__syncthreads();
 	const uint32_t off_l = c.offsets[l];
 	const uint32_t mask = (1u << B) - 1u;
-	uint32_t e[SC_SPT][NC], r[SC_SPT][NC];
-	V val[SC_SPT][NC];
+	uint32_t e[SC_SSPT][NC], r[SC_SSPT][NC];
+	V val[SC_SSPT][NC];
 	uint32_t n_have = 0;
 #pragma unroll
-	for (uint32_t q = 0; q < SC_SPT; ++q) {
-		const uint32_t i = chunk * SC_THREADS * SC_SPT + q * SC_THREADS + threadIdx.x;
+	for (uint32_t q = 0; q < SC_SSPT; ++q) {
+		const uint32_t i = chunk * SC_CHUNK + q * SC_ST + threadIdx.x;
 		if (i >= a.n) continue;
 		n_have = q + 1;
 		float x[D];
@@ -218,10 +231,10 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_scatter(const GridConst c, co
 		}
 	}
 	__syncthreads();
-	block_exclusive_scan(lh, loff, nvb, wsum);
+	block_exclusive_scan<SC_ST>(lh, loff, nvb, wsum);
 	__syncthreads();
 #pragma unroll
-	for (uint32_t q = 0; q < SC_SPT; ++q) {
+	for (uint32_t q = 0; q < SC_SSPT; ++q) {
 		if (q >= n_have) break;
 #pragma unroll
 		for (uint32_t k = 0; k < NC; ++k) {
@@ -242,9 +255,11 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_scatter(const GridConst c, co
 		}
 }
 
+// LDS accumulators are feature-major, acc[f * NE + entry]: a wave's lanes hit 2 * (random entry)
+// banks instead of 8 * entry (entry-major int64 x F=4), ~4x fewer bank conflicts.
 template <uint32_t F>
-__device__ __forceinline__ void accumulate_items(unsigned long long* acc, uint32_t lo, uint32_t hi, const uint16_t* __restrict__ item_idx,
-                                                 const f16* __restrict__ item_val) {
+__device__ __forceinline__ void accumulate_items(unsigned long long* acc, uint32_t NE, uint32_t lo, uint32_t hi,
+                                                 const uint16_t* __restrict__ item_idx, const f16* __restrict__ item_val) {
 	typedef typename ValVec<F>::T V;
 	// U items per thread in flight: the loop is bound by memory-level parallelism, not LDS
 	constexpr uint32_t U = 8;
@@ -265,7 +280,7 @@ __device__ __forceinline__ void accumulate_items(unsigned long long* acc, uint32
 			for (uint32_t f = 0; f < F; ++f) {
 				float x;
 				if constexpr (F == 1) x = (float)v[u]; else x = (float)v[u][f];
-				if (x != 0.f) atomicAdd(&acc[j[u] * F + f], (unsigned long long)(long long)(x * FIX_SCALE));
+				if (x != 0.f) atomicAdd(&acc[f * NE + j[u]], (unsigned long long)(long long)(x * FIX_SCALE));
 			}
 		}
 	}
@@ -276,7 +291,7 @@ __device__ __forceinline__ void accumulate_items(unsigned long long* acc, uint32
 		for (uint32_t f = 0; f < F; ++f) {
 			float x;
 			if constexpr (F == 1) x = (float)vv; else x = (float)vv[f];
-			if (x != 0.f) atomicAdd(&acc[jj * F + f], (unsigned long long)(long long)(x * FIX_SCALE));
+			if (x != 0.f) atomicAdd(&acc[f * NE + jj], (unsigned long long)(long long)(x * FIX_SCALE));
 		}
 	}
 }
@@ -302,45 +317,64 @@ __device__ __forceinline__ void bucket_range(const Levels& lv, const uint32_t* t
 	hi = lo + tot[vb];
 }
 
+// (entry pair k of a bucket) -> the two accumulator slots (feature-major layout)
+template <uint32_t F>
+__device__ __forceinline__ void pair_slots(uint32_t k, uint32_t NE, uint32_t& a, uint32_t& b) {
+	if constexpr (F == 1) { a = 2 * k; b = 2 * k + 1; }
+	else {
+		const uint32_t j = k / (F / 2), fp = k % (F / 2);
+		a = (2 * fp) * NE + j; b = (2 * fp + 1) * NE + j;
+	}
+}
+
 // One workgroup per bucket: exact sum of the bucket's items, written once per entry with plain
 // stores (overwrite: every entry, untouched ones get 0 — no separate memset; accumulate: old + sum).
-// Buckets above `split_limit` items are zeroed here (overwrite) and queued for k_sc_split.
+// Buckets above `split_limit` items are queued for k_sc_split in parts of `part` items.
 template <uint32_t D, uint32_t F>
-__global__ void __launch_bounds__(SC_THREADS) k_sc_bucket(const GridConst c, const Levels lv, const uint32_t* __restrict__ tot,
+__global__ void __launch_bounds__(SC_BT) k_sc_bucket(const GridConst c, const Levels lv, const uint32_t* __restrict__ tot,
                                                           uint32_t n, uint32_t B,
                                                           uint32_t split_limit, uint32_t part, const uint16_t* __restrict__ item_idx,
                                                           const f16* __restrict__ item_val, f16* __restrict__ grad, bool overwrite,
-                                                          uint32_t* __restrict__ split, uint32_t debug) {
+                                                          uint32_t* __restrict__ split, uint32_t* __restrict__ splitb, uint32_t debug) {
 	extern __shared__ unsigned long long acc[];
-	__shared__ uint32_t wsum[SC_THREADS / 64];
-	const uint32_t vb = blockIdx.x;
+	__shared__ uint32_t wsum[SC_BT / 64];
+	const uint32_t vb = blockIdx.x, NE = 1u << B;
 	uint32_t lo, hi;
 	bucket_range<D>(lv, tot, n, vb, wsum, lo, hi);
 	uint32_t e0, n_e;
 	bucket_entries(c, lv, B, vb, e0, n_e);
 	f16* g = grad + (size_t)e0 * F;
-	if (hi - lo > split_limit || lo == hi) {
+	if (lo == hi) {
 		if (overwrite)
 			for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) ((uint32_t*)g)[k] = 0u;
-		if (lo != hi) {  // queue the parts: split[0] counts parts, split[1 + 3p ..] = {bucket, lo, hi}
-			__shared__ uint32_t first;
-			const uint32_t parts = (hi - lo + part - 1) / part;
-			if (threadIdx.x == 0) first = atomicAdd(&split[0], parts);
-			__syncthreads();
-			for (uint32_t q = threadIdx.x; q < parts; q += blockDim.x) {
-				uint32_t* d = split + 1 + 3 * (size_t)(first + q);
-				d[0] = vb; d[1] = lo + q * part; d[2] = min(lo + (q + 1) * part, hi);
-			}
+		return;
+	}
+	if (hi - lo > split_limit) {
+		// queue the parts: split[0] counts parts, split[2 + 3p ..] = {bucket, lo, hi}; the bucket's
+		// parts occupy consecutive slots, recorded in splitb (split[1] counts split buckets)
+		__shared__ uint32_t first;
+		const uint32_t parts = (hi - lo + part - 1) / part;
+		if (threadIdx.x == 0) {
+			first = atomicAdd(&split[0], parts);
+			const uint32_t b = atomicAdd(&split[1], 1u);
+			splitb[3 * b] = vb; splitb[3 * b + 1] = first; splitb[3 * b + 2] = parts;
+		}
+		__syncthreads();
+		for (uint32_t q = threadIdx.x; q < parts; q += blockDim.x) {
+			uint32_t* d = split + 2 + 3 * (size_t)(first + q);
+			d[0] = vb; d[1] = lo + q * part; d[2] = min(lo + (q + 1) * part, hi);
 		}
 		return;
 	}
-	for (uint32_t k = threadIdx.x; k < n_e * F; k += blockDim.x) acc[k] = 0ull;
+	for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) acc[k] = 0ull;
 	__syncthreads();
-	if (!(debug & 1)) accumulate_items<F>(acc, lo, hi, item_idx, item_val);
+	if (!(debug & 1)) accumulate_items<F>(acc, NE, lo, hi, item_idx, item_val);
 	__syncthreads();
 	// two fp16 per thread-step (n_e * F is even: levels hold multiples of 8 entries)
 	for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) {
-		float s0 = fix_to_f32(acc[2 * k]), s1 = fix_to_f32(acc[2 * k + 1]);
+		uint32_t ia, ib;
+		pair_slots<F>(k, NE, ia, ib);
+		float s0 = fix_to_f32(acc[ia]), s1 = fix_to_f32(acc[ib]);
 		if (!overwrite) {
 			const f16x2 o = ((const f16x2*)g)[k];
 			s0 += (float)o[0];
@@ -351,25 +385,60 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_bucket(const GridConst c, con
 }
 
 // Oversized buckets (coarse levels, where thousands of samples share a handful of entries): parts of
-// `part` items, each summed exactly in LDS and added with one packed fp16 atomic per touched pair.
+// `part` items, each summed exactly in LDS and stored as int64 partial sums in its scratch slot.
 template <uint32_t F>
-__global__ void __launch_bounds__(SC_THREADS) k_sc_split(const GridConst c, const Levels lv, const uint16_t* __restrict__ item_idx,
-                                                         const f16* __restrict__ item_val, f16* __restrict__ grad, uint32_t B,
-                                                         const uint32_t* __restrict__ split, uint32_t debug) {
+__global__ void __launch_bounds__(SC_BT) k_sc_split(const GridConst c, const Levels lv, const uint16_t* __restrict__ item_idx,
+                                                         const f16* __restrict__ item_val, uint32_t B, const uint32_t* __restrict__ split,
+                                                         unsigned long long* __restrict__ scratch, uint32_t debug) {
 	extern __shared__ unsigned long long acc[];
 	if (blockIdx.x >= split[0]) return;
-	const uint32_t* d = split + 1 + 3 * (size_t)blockIdx.x;
-	const uint32_t vb = d[0], lo = d[1], hi = d[2];
+	const uint32_t* d = split + 2 + 3 * (size_t)blockIdx.x;
+	const uint32_t lo = d[1], hi = d[2], NE = 1u << B;
+	for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) acc[k] = 0ull;
+	__syncthreads();
+	if (!(debug & 1)) accumulate_items<F>(acc, NE, lo, hi, item_idx, item_val);
+	__syncthreads();
+	unsigned long long* dst = scratch + (size_t)blockIdx.x * NE * F;
+	for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) dst[k] = acc[k];
+}
+
+// One workgroup per split bucket: sum its parts' int64 partials (exact, so the order is immaterial)
+// and write every entry once — no fp16 atomics, bitwise reproducible.
+template <uint32_t F>
+__global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst c, const Levels lv, uint32_t B,
+                                                                const uint32_t* __restrict__ split, const uint32_t* __restrict__ splitb,
+                                                                const unsigned long long* __restrict__ scratch, f16* __restrict__ grad,
+                                                                bool overwrite) {
+	// grid (split bucket, 256-pair chunk): one pair per thread, the parts' loads 8 at a time
+	if (blockIdx.x >= split[1]) return;
+	const uint32_t vb = splitb[3 * blockIdx.x], first = splitb[3 * blockIdx.x + 1], parts = splitb[3 * blockIdx.x + 2];
+	const uint32_t NE = 1u << B;
 	uint32_t e0, n_e;
 	bucket_entries(c, lv, B, vb, e0, n_e);
-	for (uint32_t k = threadIdx.x; k < n_e * F; k += blockDim.x) acc[k] = 0ull;
-	__syncthreads();
-	if (!(debug & 1)) accumulate_items<F>(acc, lo, hi, item_idx, item_val);
-	__syncthreads();
-	for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) {
-		const unsigned long long q0 = acc[2 * k], q1 = acc[2 * k + 1];
-		if (q0 == 0ull && q1 == 0ull) continue;
-		atomic_add_f16x2(grad + (size_t)e0 * F + 2 * k, f16x2{(f16)fix_to_f32(q0), (f16)fix_to_f32(q1)});
+	f16* g = grad + (size_t)e0 * F;
+	const uint32_t k = blockIdx.y * blockDim.x + threadIdx.x;
+	if (k < n_e * F / 2) {
+		uint32_t ia, ib;
+		pair_slots<F>(k, NE, ia, ib);
+		const size_t pstride = (size_t)NE * F;
+		const unsigned long long* src = scratch + (size_t)first * pstride;
+		unsigned long long q0 = 0, q1 = 0;
+		uint32_t p = 0;
+		for (; p + 8 <= parts; p += 8) {
+			unsigned long long x0[8], x1[8];
+#pragma unroll
+			for (int u = 0; u < 8; ++u) { x0[u] = src[(p + u) * pstride + ia]; x1[u] = src[(p + u) * pstride + ib]; }
+#pragma unroll
+			for (int u = 0; u < 8; ++u) { q0 += x0[u]; q1 += x1[u]; }
+		}
+		for (; p < parts; ++p) { q0 += src[p * pstride + ia]; q1 += src[p * pstride + ib]; }
+		float s0 = fix_to_f32(q0), s1 = fix_to_f32(q1);
+		if (!overwrite) {
+			const f16x2 o = ((const f16x2*)g)[k];
+			s0 += (float)o[0];
+			s1 += (float)o[1];
+		}
+		((f16x2*)g)[k] = f16x2{(f16)s0, (f16)s1};
 	}
 }
 
@@ -390,28 +459,33 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 	const uint32_t* tot = (const uint32_t*)(ws + p.off_tot);
 	const uint32_t* cur_t = (const uint32_t*)(ws + p.off_cur);
 	uint32_t* split = (uint32_t*)(ws + p.off_split);
+	uint32_t* splitb = (uint32_t*)(ws + p.off_splitb);
+	unsigned long long* scratch = (unsigned long long*)(ws + p.off_scratch);
 	uint16_t* idx = (uint16_t*)(ws + p.off_idx);
 	f16* val = (f16*)(ws + p.off_val);
-	const uint32_t NIT = SC_THREADS * SC_SPT * (1u << D);
+	const uint32_t NIT = SC_CHUNK * (1u << D);
 	const size_t lds_s = (size_t)(3 * p.max_lb + 1) * 4 + (size_t)NIT * 6 + 16 + (size_t)NIT * F * 2;
 	const dim3 grid_s(p.n_chunks, c.n_levels);
-	auto go = [&](auto scatter, auto bucket, auto splitk) {
+	auto go = [&](auto scatter, auto bucket, auto splitk, auto splitr) {
 		ensure_dynamic_lds((const void*)scatter, lds_s);
-		if (!(debug & 4)) scatter<<<grid_s, SC_THREADS, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, cur_t, tot, idx, val, debug);
+		if (!(debug & 4)) scatter<<<grid_s, SC_ST, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, cur_t, tot, idx, val, debug);
 		NGP_HIP(hipGetLastError());
 		ensure_dynamic_lds((const void*)bucket, SC_LDS_BYTES);
 		ensure_dynamic_lds((const void*)splitk, SC_LDS_BYTES);
-		bucket<<<p.n_buckets, SC_THREADS, SC_LDS_BYTES, s>>>(c, lv, tot, a.n, p.B, p.split_limit, p.part, idx, val, a.grad, overwrite,
-		                                                     split, debug);
+		bucket<<<p.n_buckets, SC_BT, SC_LDS_BYTES, s>>>(c, lv, tot, a.n, p.B, p.split_limit, p.part, idx, val, a.grad, overwrite,
+		                                                     split, splitb, debug);
 		NGP_HIP(hipGetLastError());
-		splitk<<<p.max_split_blocks, SC_THREADS, SC_LDS_BYTES, s>>>(c, lv, idx, val, a.grad, p.B, split, debug);
+		splitk<<<p.max_split_blocks, SC_BT, SC_LDS_BYTES, s>>>(c, lv, idx, val, p.B, split, scratch, debug);
+		NGP_HIP(hipGetLastError());
+		const dim3 grid_r(p.max_split_buckets, div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS));
+		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite);
 		NGP_HIP(hipGetLastError());
 	};
 	switch (F) {
-		case 1: go(k_sc_scatter<D, 1>, k_sc_bucket<D, 1>, k_sc_split<1>); break;
-		case 2: go(k_sc_scatter<D, 2>, k_sc_bucket<D, 2>, k_sc_split<2>); break;
-		case 4: go(k_sc_scatter<D, 4>, k_sc_bucket<D, 4>, k_sc_split<4>); break;
-		case 8: go(k_sc_scatter<D, 8>, k_sc_bucket<D, 8>, k_sc_split<8>); break;
+		case 1: go(k_sc_scatter<D, 1>, k_sc_bucket<D, 1>, k_sc_split<1>, k_sc_split_reduce<1>); break;
+		case 2: go(k_sc_scatter<D, 2>, k_sc_bucket<D, 2>, k_sc_split<2>, k_sc_split_reduce<2>); break;
+		case 4: go(k_sc_scatter<D, 4>, k_sc_bucket<D, 4>, k_sc_split<4>, k_sc_split_reduce<4>); break;
+		case 8: go(k_sc_scatter<D, 8>, k_sc_bucket<D, 8>, k_sc_split<8>, k_sc_split_reduce<8>); break;
 		default: throw Error("grid backward: unsupported F");
 	}
 }
@@ -429,13 +503,16 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	p.max_lb = 0;
 	for (uint32_t l = 0; l < g.n_levels; ++l) p.max_lb = std::max(p.max_lb, lv.vb_base[l + 1] - lv.vb_base[l]);
 	NGP_CHECK((size_t)p.max_lb * 4 <= 32 * 1024, "grid backward: level too large for the bucket histogram");
-	p.spb = SC_THREADS * SC_SPT;
+	p.spb = SC_CHUNK;
 	p.n_chunks = (uint32_t)div_round_up(n, p.spb);
 	p.n_items = (uint64_t)n * g.n_levels * (1u << g.n_dims);
 	NGP_CHECK(p.n_items < (1ull << 32), "grid backward: too many contributions for 32-bit offsets");
 	p.split_limit = 65536;
-	p.part = 16384;
+	p.part = 32768;
+	if (const char* e = getenv("NGP_SC_PART")) p.part = (uint32_t)atoi(e);
+	if (const char* e = getenv("NGP_SC_LIMIT")) p.split_limit = (uint32_t)atoi(e);
 	p.max_split_blocks = (uint32_t)(div_round_up(p.n_items, (uint64_t)p.part) + div_round_up(p.n_items, (uint64_t)p.split_limit) + 1);
+	p.max_split_buckets = (uint32_t)(div_round_up(p.n_items, (uint64_t)p.split_limit) + 1);
 	const uint64_t len = (uint64_t)p.n_buckets * p.n_chunks;
 	NGP_CHECK(len < (1ull << 31), "grid backward: bucket histogram too large");
 	auto align = [](size_t v) { return (v + 255) / 256 * 256; };
@@ -443,7 +520,9 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	p.off_cur = align(p.off_hist + len * 4);
 	p.off_tot = align(p.off_cur + len * 4);
 	p.off_split = align(p.off_tot + (size_t)p.n_buckets * 4);
-	p.off_idx = align(p.off_split + (1 + 3 * (size_t)p.max_split_blocks) * 4);
+	p.off_splitb = align(p.off_split + (2 + 3 * (size_t)p.max_split_blocks) * 4);
+	p.off_scratch = align(p.off_splitb + 3 * (size_t)p.max_split_buckets * 4);
+	p.off_idx = align(p.off_scratch + (size_t)p.max_split_blocks * ((size_t)1 << p.B) * g.n_features * 8);
 	p.off_val = align(p.off_idx + p.n_items * 2);
 	p.total = align(p.off_val + p.n_items * F * 2);
 	return p;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Run bench.py once per argument set (separated by ';' in $SWEEP), print value + per-kernel times.
-# Usage: SWEEP="--overlap 0;--overlap 1" bash tools/bench_sweep.sh TAG
+# Usage: SWEEP="--overlap 0;--overlap 1;VAR=1 --overlap 0" bash tools/bench_sweep.sh TAG  (VAR=val tokens go to the environment)
 set -e -o pipefail
 TAG=${1:-sweep}
 OUT=gpurun_out/$TAG
@@ -8,7 +8,11 @@ mkdir -p "$OUT"
 IFS=';' read -ra CASES <<< "$SWEEP"
 i=0
 for c in "${CASES[@]}"; do
-  timeout -k 10 300 python bench.py --no-cpu-baseline $c > "$OUT/case$i.json" 2> "$OUT/case$i.err"
+  envs=(); args=()
+  for tok in $c; do
+    if [[ "$tok" != --* && "$tok" == *=* ]]; then envs+=("$tok"); else args+=("$tok"); fi
+  done
+  timeout -k 10 300 env "${envs[@]}" python bench.py --no-cpu-baseline "${args[@]}" > "$OUT/case$i.json" 2> "$OUT/case$i.err"
   python3 -c "
 import json,sys
 d=json.load(open('$OUT/case$i.json'))
