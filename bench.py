@@ -94,6 +94,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=1, help="1: time the K steps as one captured HIP graph (N=1)")
     ap.add_argument("--overlap", type=int, default=None, help="engine side-stream overlap bitmask (engine.hip)")
+    ap.add_argument("--opt", action="append", default=[], help="model option key=value (ngp_model_set_option)")
     args = ap.parse_args()
 
     from __graft_entry__ import load_package
@@ -109,6 +110,9 @@ def main():
         net = pkg.create_nerf_network(cfg)
         if args.overlap is not None:
             net.set_option("overlap", args.overlap)
+        for kv in args.opt:
+            k, v = kv.split("=")
+            net.set_option(k, float(v))
         trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
         net.reserve(n)
         x, dL = synthetic_batch(n, 1337 + rank, "cuda")

@@ -140,11 +140,13 @@ struct ngp_model {
 	ScatterPlan sc_plan;
 	uint32_t sc_plan_n = 0;
 	bool sc_prepared = false;               // phase 1 of the bucketed backward already enqueued (side stream)
+	bool sc_hist_done = false;              // the training forward produced the bucket histogram
 	bool frags_async = false;               // training fragments already enqueued on the side stream
 	// side-stream overlap (bitmask): 1 bucket histogram under forward + MLP, 2 weight fragments,
 	// 4 dW slab reduction under the grid backward, 8 optimizer step advance. Each costs a cross-queue
 	// dependency edge, which in a HIP graph is not free.
 	uint32_t overlap = 0;
+	bool fused_hist = true;                 // option "fused_hist": bucket histogram inside the training forward
 	hipStream_t side = nullptr;             // overlaps fragments + bucket histogram with forward + MLP,
 	                                        // and the dW slab reduction with the grid backward
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_frags = nullptr, ev_mlp = nullptr, ev_red = nullptr;
@@ -185,10 +187,11 @@ struct ngp_model {
 	}
 	bool use_sorted(uint32_t n) const { return grid_backward_mode == 3 || (grid_backward_mode == 0 && n >= 4096); }
 	bool side_prepare(uint32_t n) const { return use_sorted(n) && (overlap & 1); }
-	void* sorted_workspace(uint32_t n) {
+	const ScatterPlan& sc_plan_for(uint32_t n) {
 		if (sc_plan_n != n) { sc_plan = make_scatter_plan(grid, n); sc_plan_n = n; }
-		return scatter_ws.get(sc_plan.total);
+		return sc_plan;
 	}
+	void* sorted_workspace(uint32_t n) { return scatter_ws.get(sc_plan_for(n).total); }
 	// Phase 1 of the bucketed grid backward on a side stream: it only needs the positions, so it runs
 	// concurrently with the forward encoding and the MLP; train_pass joins before the scatter.
 	void prepare_grid_backward_async(hipStream_t s, uint32_t n, const float* in, uint32_t stride) {
@@ -258,14 +261,22 @@ struct ngp_model {
 		if (!inference) frags_current = true;
 		return f;
 	}
-	void encode(hipStream_t s, uint32_t n, const float* in, uint32_t stride, f16* out, uint32_t out_stride, uint32_t layout, bool inference) {
+	// want_hist: a training forward whose backward follows on the same positions — count the sorted
+	// backward's bucket histogram in the forward kernel (its corner indices are computed anyway).
+	void encode(hipStream_t s, uint32_t n, const float* in, uint32_t stride, f16* out, uint32_t out_stride, uint32_t layout, bool inference,
+	            bool want_hist = false) {
 		GridFwdArgs a{n, in, stride, pick(inference) + grid_offset(), out, out_stride, layout, max_level, max_level_per_sample};
 		if (enc_width > grid.n_levels * grid.n_features && layout == AoS && !grid_forward_rows_ok(grid, a)) {
 			// zero the padding columns (tcnn pads the encoding output with zeros); the row kernel writes them
 			NGP_HIP(hipMemsetAsync(out, 0, (size_t)n * out_stride * sizeof(f16), s));
 		}
+		sc_hist_done = false;
+		GridHist h;
+		const bool fuse = want_hist && fused_hist && use_sorted(n) && !sc_prepared && grid_forward_rows_ok(grid, a) &&
+		                  scatter_hist(grid, sc_plan_for(n), sorted_workspace(n), h);
 		ProfScope ps("grid_forward", s);
-		grid_forward(grid, a, s);
+		grid_forward(grid, a, s, fuse ? &h : nullptr);
+		sc_hist_done = fuse;
 	}
 	void run_mlp(hipStream_t s, MlpMode mode, uint32_t n, const float* in, uint32_t stride, const f16* encbuf, f16* out,
 	             uint32_t out_stride, uint32_t out_layout, const f16* dL, uint32_t dL_stride, f16* dL_denc, float* slab,
@@ -334,8 +345,9 @@ struct ngp_model {
 				sc_prepared = false;
 			} else {
 				ProfScope ps("grid_bwd_prepare", s);
-				grid_scatter_prepare(grid, b, sc_plan, ws, s);
+				grid_scatter_prepare(grid, b, sc_plan, ws, s, sc_hist_done);
 			}
+			sc_hist_done = false;
 			ProfScope ps("grid_backward_sorted", s);
 			grid_backward_sorted(grid, b, sc_plan, ws, s, overwrite, win_debug);
 			return;
@@ -570,6 +582,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 		} else if (k == "overlap") {
 			NGP_CHECK(value >= 0 && value <= 15, "overlap is a bitmask in [0, 15]");
 			m->overlap = (uint32_t)value;
+		} else if (k == "fused_hist") {
+			m->fused_hist = value != 0;
 		} else if (k == "win_debug") {
 			m->win_debug = (uint32_t)value;
 		} else {
@@ -671,7 +685,7 @@ int ngp_forward_backward(ngp_model* m, void* stream, uint32_t n, const float* in
 		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
 		m->generation++;
 		m->prepare_grid_backward_async(S(stream), n, input, input_stride);
-		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, false);
+		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, false, true);
 		m->train_pass(S(stream), n, input, input_stride, e, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode);
 	});
 }
@@ -772,7 +786,7 @@ int ngp_trainer_training_step(ngp_trainer* t, void* stream, uint32_t n, const fl
 		f16* out = (f16*)m->out_ws.get((size_t)n * W * sizeof(f16));
 		f16* dl = (f16*)m->dl_ws.get((size_t)n * W * sizeof(f16));
 		m->generation++;
-		m->encode(s, n, input, input_stride, e, m->enc_width, AoS, false);
+		m->encode(s, n, input, input_stride, e, m->enc_width, AoS, false, true);
 		m->run_mlp(s, MLP_INFER, n, input, input_stride, e, out, W, AoS, nullptr, 0, nullptr, nullptr, false);
 		LossEvalArgs la{n, m->n_output_dims, out, W, target, target_stride, loss_scale, dl, W, nullptr, loss_sum};
 		{

@@ -49,7 +49,16 @@ struct GridBwdArgs {
 	uint32_t level_begin = 0;  // levels below were handled elsewhere (windowed backward)
 };
 
-void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream);
+// Optional by-product of the training forward: the bucket histogram of the sorted backward
+// (grid_scatter.hip k_sc_hist), counted from the corner indices the forward computes anyway.
+// hist[(vb_base[l] + bucket) * n_chunks + chunk]; one forward block = one chunk of `chunk` samples.
+struct GridHist {
+	uint32_t* hist;
+	uint32_t B, n_chunks, chunk;
+	uint32_t vb_base[33];
+};
+
+void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist = nullptr);
 // true when grid_forward writes whole AoS rows (padding columns included: no memset needed)
 bool grid_forward_rows_ok(const GridDesc& g, const GridFwdArgs& a);
 void grid_backward(const GridDesc& g, const GridBwdArgs& a, hipStream_t stream);

@@ -108,12 +108,17 @@ __global__ void __launch_bounds__(256) k_grid_forward(const GridConst c, const G
 // zero-padded past L*F) is written with back-to-back 16-B stores, so each 64-B segment is filled by
 // one wave within a few cycles. Per-level 8-B stores spaced a level's gathers apart reach HBM as
 // partial segments (rocprof WRITE_SIZE 3.6x the 8.4 MB of a C2 batch, profiles/r01b_pmc_c2.json).
-template <uint32_t D, uint32_t F>
-__global__ void __launch_bounds__(256) k_grid_forward_rows(const GridConst c, const GridFwdArgs a) {
+template <uint32_t D, uint32_t F, bool HIST>
+__global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const GridConst c, const GridFwdArgs a, const GridHist h) {
 	typedef typename FeatVec<F>::T V;
 	constexpr uint32_t MAXL = 32 / F;
+	extern __shared__ uint32_t hl[];  // HIST: [vb_base[L]] bucket counts of this chunk
+	if constexpr (HIST) {
+		for (uint32_t j = threadIdx.x; j < h.vb_base[c.n_levels]; j += blockDim.x) hl[j] = 0;
+		__syncthreads();
+	}
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= a.n) return;
+	if (i < a.n) {
 	float x[D];
 #pragma unroll
 	for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * a.pos_stride + d];
@@ -124,9 +129,23 @@ __global__ void __launch_bounds__(256) k_grid_forward_rows(const GridConst c, co
 		float acc[F];
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) acc[f] = 0.f;
-		if (l < c.n_levels && !((float)l >= ml + 1e-3f)) {
+		const bool active = l < c.n_levels && !((float)l >= ml + 1e-3f);
+		if (HIST && l < c.n_levels && !active) {
+			// the backward stages items for masked levels too (with zero values): count them
 			float frac[D]; uint32_t base[D];
 			level_setup<D>(c, l, x, frac, base);
+#pragma unroll
+			for (uint32_t k = 0; k < (1u << D); ++k)
+				atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
+		}
+		if (active) {
+			float frac[D]; uint32_t base[D];
+			level_setup<D>(c, l, x, frac, base);
+			if constexpr (HIST) {
+#pragma unroll
+				for (uint32_t k = 0; k < (1u << D); ++k)
+					atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
+			}
 			V v[1u << D];
 #pragma unroll
 			for (uint32_t k = 0; k < (1u << D); ++k) v[k] = *(const V*)(a.table + (size_t)corner_index<D>(c, l, base, k) * F);
@@ -152,6 +171,11 @@ __global__ void __launch_bounds__(256) k_grid_forward_rows(const GridConst c, co
 		if (8 * q >= a.out_stride) break;
 		dst[q] = f16x8{row[8 * q], row[8 * q + 1], row[8 * q + 2], row[8 * q + 3],
 		               row[8 * q + 4], row[8 * q + 5], row[8 * q + 6], row[8 * q + 7]};
+	}
+	}
+	if constexpr (HIST) {
+		__syncthreads();
+		for (uint32_t j = threadIdx.x; j < h.vb_base[c.n_levels]; j += blockDim.x) h.hist[(size_t)j * h.n_chunks + blockIdx.x] = hl[j];
 	}
 }
 
@@ -211,14 +235,32 @@ bool grid_forward_rows_ok(const GridDesc& g, const GridFwdArgs& a) {
 }
 
 template <uint32_t D>
-static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hipStream_t s, bool rows) {
+static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hipStream_t s, bool rows, const GridHist* h) {
 	const dim3 grid(div_round_up(a.n, 256)), block(256);
+	if (h) {
+		NGP_CHECK(rows && h->chunk == 512, "grid forward histogram: needs the row kernel and 512-sample chunks");
+		const dim3 grid_h(div_round_up(a.n, 512));
+		NGP_CHECK(grid_h.x == h->n_chunks, "grid forward histogram: chunk count mismatch");
+		const size_t lds = (size_t)h->vb_base[c.n_levels] * 4;
+		auto go = [&](auto kern) {
+			ensure_dynamic_lds((const void*)kern, lds);
+			kern<<<grid_h, 512, lds, s>>>(c, a, *h);
+		};
+		switch (F) {
+			case 1: go(k_grid_forward_rows<D, 1, true>); return;
+			case 2: go(k_grid_forward_rows<D, 2, true>); return;
+			case 4: go(k_grid_forward_rows<D, 4, true>); return;
+			case 8: go(k_grid_forward_rows<D, 8, true>); return;
+			default: throw Error("GridEncoding: unsupported F");
+		}
+	}
+	const GridHist none{};
 	if (rows) {
 		switch (F) {
-			case 1: k_grid_forward_rows<D, 1><<<grid, block, 0, s>>>(c, a); return;
-			case 2: k_grid_forward_rows<D, 2><<<grid, block, 0, s>>>(c, a); return;
-			case 4: k_grid_forward_rows<D, 4><<<grid, block, 0, s>>>(c, a); return;
-			case 8: k_grid_forward_rows<D, 8><<<grid, block, 0, s>>>(c, a); return;
+			case 1: k_grid_forward_rows<D, 1, false><<<grid, block, 0, s>>>(c, a, none); return;
+			case 2: k_grid_forward_rows<D, 2, false><<<grid, block, 0, s>>>(c, a, none); return;
+			case 4: k_grid_forward_rows<D, 4, false><<<grid, block, 0, s>>>(c, a, none); return;
+			case 8: k_grid_forward_rows<D, 8, false><<<grid, block, 0, s>>>(c, a, none); return;
 			default: throw Error("GridEncoding: unsupported F");
 		}
 	}
@@ -244,12 +286,12 @@ static void launch_bwd(uint32_t F, const GridConst& c, const GridBwdArgs& a, hip
 	}
 }
 
-void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream) {
+void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist) {
 	if (a.n == 0) return;
 	GridConst c = make_grid_const(g);
 	const bool rows = grid_forward_rows_ok(g, a);
-	if (g.n_dims == 3) launch_fwd<3>(g.n_features, c, a, stream, rows);
-	else launch_fwd<2>(g.n_features, c, a, stream, rows);
+	if (g.n_dims == 3) launch_fwd<3>(g.n_features, c, a, stream, rows, hist);
+	else launch_fwd<2>(g.n_features, c, a, stream, rows, hist);
 	NGP_HIP(hipGetLastError());
 }
 

@@ -11,19 +11,24 @@ struct ScatterPlan {
 	uint32_t n_chunks = 0;
 	uint32_t max_lb = 0;     // most buckets any one level spans
 	uint64_t n_items = 0;    // n * L * 2^D contributions
-	uint32_t split_limit = 0;// buckets with more items are summed in parts (k_sc_split)
+	uint32_t split_limit = 0;// buckets with more items are summed in parts (k_sc_plan)
 	uint32_t part = 0;
 	uint32_t max_split_blocks = 0;
 	uint32_t max_split_buckets = 0;
 	// workspace layout (bytes)
-	size_t off_hist = 0, off_cur = 0, off_tot = 0, off_split = 0, off_splitb = 0, off_scratch = 0, off_idx = 0, off_val = 0,
+	size_t off_hist = 0, off_cur = 0, off_tot = 0, off_split = 0, off_lo = 0, off_splitb = 0, off_scratch = 0, off_idx = 0, off_val = 0,
 	       total = 0;
 };
 
 ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n);
 // Phase 1 (positions only, so it can run on a side stream while the forward pass and the MLP run):
 // bucket histogram per block of samples + per-bucket scans.
-void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace, hipStream_t s);
+// hist_done: the histogram was produced by the training forward (scatter_hist, grid_forward).
+void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace, hipStream_t s,
+                          bool hist_done = false);
+// The forward-fused histogram for this plan, or false when it does not apply (row kernel needed,
+// the bucket counts of all levels must fit the forward block's LDS).
+bool scatter_hist(const GridDesc& g, const ScatterPlan& p, void* workspace, GridHist& h);
 // Phase 2: dL/dy -> gradient. overwrite: b.grad's grid section is fully written (no memset needed);
 // otherwise the sums are added to it. Same level masking as grid_backward.
 void grid_backward_sorted(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace,

@@ -16,13 +16,13 @@
 //     k_sc_hist       per (chunk, level): LDS histogram over the level's buckets -> hist[bucket][chunk]
 //     k_sc_scan       per bucket: exclusive scan over its chunks -> cursor within the bucket
 //                     cur[chunk][bucket] and the bucket total tot[bucket]. Every sample emits 2^D
-//                     items per level, so level l starts at item n * 2^D * l and a bucket's start is
-//                     that plus the scan of its level's totals (done where needed, <= 256 values).
+//                     items per level, so level l starts at item n * 2^D * l.
+//     k_sc_plan       bucket starts, and the parts list of oversized buckets
 //   backward
 //     k_sc_scatter    per (chunk, level): items ranked per bucket in LDS, staged in bucket order, written
 //                     out as runs: (entry & (2^B-1)) u16 + F fp16 values
-//     k_sc_bucket     per bucket: zero LDS, accumulate, store every entry once (no memset, no atomics)
-//     k_sc_split      parts of oversized buckets: accumulate, store int64 partial sums
+//     k_sc_accumulate per part of an oversized bucket (int64 partial sums to scratch), then per bucket:
+//                     zero LDS, accumulate, store every entry once (no memset, no atomics)
 //     k_sc_split_reduce  per oversized bucket: sum its parts (exact), write every entry once
 #include "grid_scatter.h"
 
@@ -121,10 +121,8 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 }
 
 // per bucket: exclusive scan of hist[bucket][0..n_chunks) -> cur[chunk][bucket]; tot[bucket] = total.
-// Also resets the split-part and split-bucket counters for this backward (split[0], split[1]).
 __global__ void __launch_bounds__(SC_THREADS) k_sc_scan(const uint32_t* __restrict__ hist, uint32_t n_chunks, uint32_t n_vb,
-                                                        uint32_t* __restrict__ cur, uint32_t* __restrict__ tot,
-                                                        uint32_t* __restrict__ split) {
+                                                        uint32_t* __restrict__ cur, uint32_t* __restrict__ tot) {
 	__shared__ uint32_t wsum[SC_THREADS / 64];
 	const uint32_t vb = blockIdx.x;
 	const uint32_t* h = hist + (size_t)vb * n_chunks;
@@ -141,30 +139,54 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_scan(const uint32_t* __restri
 		carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
 		__syncthreads();
 	}
-	if (threadIdx.x == 0) {
-		tot[vb] = carry;
-		if (vb == 0) { split[0] = 0u; split[1] = 0u; }
-	}
+	if (threadIdx.x == 0) tot[vb] = carry;
 }
 
-// sum of v[0..n) by one block (every thread gets the result)
-__device__ __forceinline__ uint32_t block_sum(const uint32_t* v, uint32_t n, uint32_t* wsum) {
-	uint32_t x = 0;
-	for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) x += v[k];
-	x = wave_inclusive_scan(x);
-	x = __shfl(x, 63);
-	__syncthreads();
-	if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = x;
-	__syncthreads();
-	uint32_t t = 0;
-	for (uint32_t w = 0; w < blockDim.x / 64; ++w) t += wsum[w];
-	return t;
+// One block: bucket starts lo[vb] (exclusive scan of tot over all buckets — levels are consecutive
+// and each holds n * 2^D items), and the split list for buckets above split_limit: parts of `part`
+// items at split[2 + 3p ..] = {bucket, lo, hi} (split[0] = parts), split buckets at splitb[3b ..] =
+// {bucket, first part, parts} (split[1] = buckets). Everything downstream is then a static grid.
+constexpr uint32_t SC_PLAN_THREADS = 1024;
+__global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __restrict__ tot, uint32_t n_vb, uint32_t split_limit,
+                                                             uint32_t part, uint32_t* __restrict__ lo_out,
+                                                             uint32_t* __restrict__ split, uint32_t* __restrict__ splitb) {
+	__shared__ uint32_t wsum[3][SC_PLAN_THREADS / 64];
+	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	uint32_t c_lo = 0, c_parts = 0, c_sb = 0;
+	for (uint32_t b0 = 0; b0 < n_vb; b0 += SC_PLAN_THREADS) {
+		const uint32_t vb = b0 + threadIdx.x;
+		const uint32_t t = vb < n_vb ? tot[vb] : 0u;
+		const uint32_t is_split = t > split_limit ? 1u : 0u;
+		const uint32_t parts = is_split ? (t + part - 1) / part : 0u;
+		const uint32_t i0 = wave_inclusive_scan(t), i1 = wave_inclusive_scan(parts), i2 = wave_inclusive_scan(is_split);
+		if (lane == 63) { wsum[0][wave] = i0; wsum[1][wave] = i1; wsum[2][wave] = i2; }
+		__syncthreads();
+		uint32_t p0 = c_lo, p1 = c_parts, p2 = c_sb;
+		for (uint32_t w = 0; w < SC_PLAN_THREADS / 64; ++w) {
+			if (w < wave) { p0 += wsum[0][w]; p1 += wsum[1][w]; p2 += wsum[2][w]; }
+			c_lo += wsum[0][w]; c_parts += wsum[1][w]; c_sb += wsum[2][w];
+		}
+		__syncthreads();
+		if (vb < n_vb) {
+			const uint32_t lo = p0 + i0 - t;
+			lo_out[vb] = lo;
+			if (is_split) {
+				const uint32_t first = p1 + i1 - parts, b = p2 + i2 - 1u;
+				splitb[3 * b] = vb; splitb[3 * b + 1] = first; splitb[3 * b + 2] = parts;
+				for (uint32_t q = 0; q < parts; ++q) {
+					uint32_t* d = split + 2 + 3 * (size_t)(first + q);
+					d[0] = vb; d[1] = lo + q * part; d[2] = min(lo + (q + 1) * part, lo + t);
+				}
+			}
+		}
+	}
+	if (threadIdx.x == 0) { split[0] = c_parts; split[1] = c_sb; }
 }
 
 template <uint32_t D, uint32_t F>
 __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const Levels lv, const GridBwdArgs a, uint32_t B,
-                                                           uint32_t n_vb, const uint32_t* __restrict__ cur_t, const uint32_t* __restrict__ tot,
-                                                           uint16_t* __restrict__ item_idx, f16* __restrict__ item_val, uint32_t debug) {
+                                                      uint32_t n_vb, const uint32_t* __restrict__ cur_t, const uint32_t* __restrict__ lo_vb,
+                                                      uint16_t* __restrict__ item_idx, f16* __restrict__ item_val, uint32_t debug) {
 	typedef typename ValVec<F>::T V;
 	constexpr uint32_t NC = 1u << D;
 	constexpr uint32_t NIT = SC_CHUNK * NC;  // items per block
@@ -175,17 +197,13 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 	uint32_t* cur = lds;                                   // [nvb] this block's global cursor per bucket
 	uint32_t* lh = cur + nvb;                              // [nvb] counts
 	uint32_t* loff = lh + nvb;                             // [nvb + 1] block-local exclusive offsets
-	uint32_t* st_pos = loff + nvb + 1;                     // [NIT] global position of the item in slot order
-	uint16_t* st_idx = (uint16_t*)(st_pos + NIT);          // [NIT]
+	uint16_t* st_b = (uint16_t*)(loff + nvb + 1);          // [NIT] bucket of the item in slot order
+	uint16_t* st_idx = st_b + NIT;                         // [NIT]
 	V* st_val = (V*)(((uintptr_t)(st_idx + NIT) + 15) & ~(uintptr_t)15);  // [NIT]
-	// bucket starts of this level: n * 2^D * l + exclusive scan of the level's bucket totals
-	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) lh[j] = tot[lv.vb_base[l] + j];
-	__syncthreads();
-	block_exclusive_scan<SC_ST>(lh, loff, nvb, wsum);
-	__syncthreads();
-	const uint32_t level_base = a.n * NC * l;
+	// global start of (bucket, this chunk): bucket start (k_sc_plan) + the chunk's cursor (k_sc_scan)
 	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) {
-		cur[j] = level_base + loff[j] + cur_t[(size_t)chunk * n_vb + lv.vb_base[l] + j];
+		const uint32_t vb = lv.vb_base[l] + j;
+		cur[j] = lo_vb[vb] + cur_t[(size_t)chunk * n_vb + vb];
 		lh[j] = 0;
 	}
 	__syncthreads();
@@ -240,7 +258,7 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 		for (uint32_t k = 0; k < NC; ++k) {
 			const uint32_t j = e[q][k] >> B;
 			const uint32_t slot = loff[j] + r[q][k];
-			st_pos[slot] = cur[j] + r[q][k];
+			st_b[slot] = (uint16_t)j;
 			st_idx[slot] = (uint16_t)(e[q][k] & mask);
 			st_val[slot] = val[q][k];
 		}
@@ -249,7 +267,8 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 	const uint32_t n_it = loff[nvb];
 	if (!(debug & 8))
 		for (uint32_t t = threadIdx.x; t < n_it; t += blockDim.x) {
-			const uint32_t gpos = st_pos[t];
+			const uint32_t j = st_b[t];
+			const uint32_t gpos = cur[j] + (t - loff[j]);
 			item_idx[gpos] = st_idx[t];
 			*(V*)(item_val + (size_t)gpos * F) = st_val[t];
 		}
@@ -259,8 +278,19 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 // banks instead of 8 * entry (entry-major int64 x F=4), ~4x fewer bank conflicts.
 template <uint32_t F>
 __device__ __forceinline__ void accumulate_items(unsigned long long* acc, uint32_t NE, uint32_t lo, uint32_t hi,
-                                                 const uint16_t* __restrict__ item_idx, const f16* __restrict__ item_val) {
+                                                 const uint16_t* __restrict__ item_idx, const f16* __restrict__ item_val,
+                                                 uint32_t debug = 0) {
 	typedef typename ValVec<F>::T V;
+	if (debug & 32) {  // timing experiment: the loads without the LDS atomics
+		float sum = 0.f;
+		for (uint32_t t = lo + threadIdx.x; t < hi; t += blockDim.x) {
+			const V vv = *(const V*)(item_val + (size_t)t * F);
+			if constexpr (F == 1) sum += (float)vv; else sum += (float)vv[0];
+			sum += (float)item_idx[t];
+		}
+		acc[threadIdx.x] = (unsigned long long)sum;
+		return;
+	}
 	// U items per thread in flight: the loop is bound by memory-level parallelism, not LDS
 	constexpr uint32_t U = 8;
 	const uint32_t step = blockDim.x * U;
@@ -307,16 +337,6 @@ __device__ __forceinline__ void bucket_entries(const GridConst& c, const Levels&
 	n_e = min(1u << B, c.offsets[l + 1] - e0);
 }
 
-// bucket vb -> [lo, hi) in the item arrays (see k_sc_scan)
-template <uint32_t D>
-__device__ __forceinline__ void bucket_range(const Levels& lv, const uint32_t* tot, uint32_t n, uint32_t vb, uint32_t* wsum,
-                                             uint32_t& lo, uint32_t& hi) {
-	uint32_t l = 0;
-	while (lv.vb_base[l + 1] <= vb) ++l;
-	lo = n * (1u << D) * l + block_sum(tot + lv.vb_base[l], vb - lv.vb_base[l], wsum);
-	hi = lo + tot[vb];
-}
-
 // (entry pair k of a bucket) -> the two accumulator slots (feature-major layout)
 template <uint32_t F>
 __device__ __forceinline__ void pair_slots(uint32_t k, uint32_t NE, uint32_t& a, uint32_t& b) {
@@ -327,48 +347,47 @@ __device__ __forceinline__ void pair_slots(uint32_t k, uint32_t NE, uint32_t& a,
 	}
 }
 
-// One workgroup per bucket: exact sum of the bucket's items, written once per entry with plain
-// stores (overwrite: every entry, untouched ones get 0 — no separate memset; accumulate: old + sum).
-// Buckets above `split_limit` items are queued for k_sc_split in parts of `part` items.
-template <uint32_t D, uint32_t F>
-__global__ void __launch_bounds__(SC_BT) k_sc_bucket(const GridConst c, const Levels lv, const uint32_t* __restrict__ tot,
-                                                          uint32_t n, uint32_t B,
-                                                          uint32_t split_limit, uint32_t part, const uint16_t* __restrict__ item_idx,
-                                                          const f16* __restrict__ item_val, f16* __restrict__ grad, bool overwrite,
-                                                          uint32_t* __restrict__ split, uint32_t* __restrict__ splitb, uint32_t debug) {
+// One workgroup per work unit, heaviest first: blocks [0, max_parts) are the parts of oversized
+// buckets (coarse levels, where thousands of samples share a handful of entries; exact int64 partial
+// sums to their scratch slot, added by k_sc_split_reduce), blocks max_parts + vb the other buckets:
+// exact sum, written once per entry with plain stores (overwrite: every entry, untouched ones get 0
+// — no separate memset; accumulate: old + sum).
+template <uint32_t F>
+__global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, const Levels lv, const uint32_t* __restrict__ tot,
+                                                         const uint32_t* __restrict__ lo_arr, uint32_t B, uint32_t split_limit,
+                                                         uint32_t max_parts, const uint16_t* __restrict__ item_idx,
+                                                         const f16* __restrict__ item_val, f16* __restrict__ grad, bool overwrite,
+                                                         const uint32_t* __restrict__ split, unsigned long long* __restrict__ scratch,
+                                                         uint32_t debug) {
 	extern __shared__ unsigned long long acc[];
-	__shared__ uint32_t wsum[SC_BT / 64];
-	const uint32_t vb = blockIdx.x, NE = 1u << B;
-	uint32_t lo, hi;
-	bucket_range<D>(lv, tot, n, vb, wsum, lo, hi);
+	const uint32_t NE = 1u << B;
+	if (blockIdx.x < max_parts) {
+		if (blockIdx.x >= split[0]) return;
+		const uint32_t* d = split + 2 + 3 * (size_t)blockIdx.x;
+		const uint32_t lo = d[1], hi = d[2];
+		for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) acc[k] = 0ull;
+		__syncthreads();
+		if (!(debug & 1)) accumulate_items<F>(acc, NE, lo, hi, item_idx, item_val, debug);
+		__syncthreads();
+		unsigned long long* dst = scratch + (size_t)blockIdx.x * NE * F;
+		for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) dst[k] = acc[k];
+		return;
+	}
+	const uint32_t vb = blockIdx.x - max_parts;
+	const uint32_t t = tot[vb];
+	if (t > split_limit) return;
 	uint32_t e0, n_e;
 	bucket_entries(c, lv, B, vb, e0, n_e);
 	f16* g = grad + (size_t)e0 * F;
-	if (lo == hi) {
+	if (t == 0) {
 		if (overwrite)
 			for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) ((uint32_t*)g)[k] = 0u;
 		return;
 	}
-	if (hi - lo > split_limit) {
-		// queue the parts: split[0] counts parts, split[2 + 3p ..] = {bucket, lo, hi}; the bucket's
-		// parts occupy consecutive slots, recorded in splitb (split[1] counts split buckets)
-		__shared__ uint32_t first;
-		const uint32_t parts = (hi - lo + part - 1) / part;
-		if (threadIdx.x == 0) {
-			first = atomicAdd(&split[0], parts);
-			const uint32_t b = atomicAdd(&split[1], 1u);
-			splitb[3 * b] = vb; splitb[3 * b + 1] = first; splitb[3 * b + 2] = parts;
-		}
-		__syncthreads();
-		for (uint32_t q = threadIdx.x; q < parts; q += blockDim.x) {
-			uint32_t* d = split + 2 + 3 * (size_t)(first + q);
-			d[0] = vb; d[1] = lo + q * part; d[2] = min(lo + (q + 1) * part, hi);
-		}
-		return;
-	}
+	const uint32_t lo = lo_arr[vb];
 	for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) acc[k] = 0ull;
 	__syncthreads();
-	if (!(debug & 1)) accumulate_items<F>(acc, NE, lo, hi, item_idx, item_val);
+	if (!(debug & 1)) accumulate_items<F>(acc, NE, lo, lo + t, item_idx, item_val, debug);
 	__syncthreads();
 	// two fp16 per thread-step (n_e * F is even: levels hold multiples of 8 entries)
 	for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) {
@@ -382,24 +401,6 @@ __global__ void __launch_bounds__(SC_BT) k_sc_bucket(const GridConst c, const Le
 		}
 		((f16x2*)g)[k] = f16x2{(f16)s0, (f16)s1};
 	}
-}
-
-// Oversized buckets (coarse levels, where thousands of samples share a handful of entries): parts of
-// `part` items, each summed exactly in LDS and stored as int64 partial sums in its scratch slot.
-template <uint32_t F>
-__global__ void __launch_bounds__(SC_BT) k_sc_split(const GridConst c, const Levels lv, const uint16_t* __restrict__ item_idx,
-                                                         const f16* __restrict__ item_val, uint32_t B, const uint32_t* __restrict__ split,
-                                                         unsigned long long* __restrict__ scratch, uint32_t debug) {
-	extern __shared__ unsigned long long acc[];
-	if (blockIdx.x >= split[0]) return;
-	const uint32_t* d = split + 2 + 3 * (size_t)blockIdx.x;
-	const uint32_t lo = d[1], hi = d[2], NE = 1u << B;
-	for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) acc[k] = 0ull;
-	__syncthreads();
-	if (!(debug & 1)) accumulate_items<F>(acc, NE, lo, hi, item_idx, item_val);
-	__syncthreads();
-	unsigned long long* dst = scratch + (size_t)blockIdx.x * NE * F;
-	for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) dst[k] = acc[k];
 }
 
 // One workgroup per split bucket: sum its parts' int64 partials (exact, so the order is immaterial)
@@ -458,34 +459,32 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
                      hipStream_t s, bool overwrite, uint32_t debug) {
 	const uint32_t* tot = (const uint32_t*)(ws + p.off_tot);
 	const uint32_t* cur_t = (const uint32_t*)(ws + p.off_cur);
-	uint32_t* split = (uint32_t*)(ws + p.off_split);
-	uint32_t* splitb = (uint32_t*)(ws + p.off_splitb);
+	const uint32_t* split = (const uint32_t*)(ws + p.off_split);
+	const uint32_t* lo = (const uint32_t*)(ws + p.off_lo);
+	const uint32_t* splitb = (const uint32_t*)(ws + p.off_splitb);
 	unsigned long long* scratch = (unsigned long long*)(ws + p.off_scratch);
 	uint16_t* idx = (uint16_t*)(ws + p.off_idx);
 	f16* val = (f16*)(ws + p.off_val);
 	const uint32_t NIT = SC_CHUNK * (1u << D);
-	const size_t lds_s = (size_t)(3 * p.max_lb + 1) * 4 + (size_t)NIT * 6 + 16 + (size_t)NIT * F * 2;
+	const size_t lds_s = (size_t)(3 * p.max_lb + 1) * 4 + (size_t)NIT * 4 + 16 + (size_t)NIT * F * 2;
 	const dim3 grid_s(p.n_chunks, c.n_levels);
-	auto go = [&](auto scatter, auto bucket, auto splitk, auto splitr) {
+	auto go = [&](auto scatter, auto accum, auto splitr) {
 		ensure_dynamic_lds((const void*)scatter, lds_s);
-		if (!(debug & 4)) scatter<<<grid_s, SC_ST, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, cur_t, tot, idx, val, debug);
+		if (!(debug & 4)) scatter<<<grid_s, SC_ST, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, cur_t, lo, idx, val, debug);
 		NGP_HIP(hipGetLastError());
-		ensure_dynamic_lds((const void*)bucket, SC_LDS_BYTES);
-		ensure_dynamic_lds((const void*)splitk, SC_LDS_BYTES);
-		bucket<<<p.n_buckets, SC_BT, SC_LDS_BYTES, s>>>(c, lv, tot, a.n, p.B, p.split_limit, p.part, idx, val, a.grad, overwrite,
-		                                                     split, splitb, debug);
-		NGP_HIP(hipGetLastError());
-		splitk<<<p.max_split_blocks, SC_BT, SC_LDS_BYTES, s>>>(c, lv, idx, val, p.B, split, scratch, debug);
+		ensure_dynamic_lds((const void*)accum, SC_LDS_BYTES);
+		accum<<<p.max_split_blocks + p.n_buckets, SC_BT, SC_LDS_BYTES, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
+		                                                                     val, a.grad, overwrite, split, scratch, debug);
 		NGP_HIP(hipGetLastError());
 		const dim3 grid_r(p.max_split_buckets, div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS));
 		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite);
 		NGP_HIP(hipGetLastError());
 	};
 	switch (F) {
-		case 1: go(k_sc_scatter<D, 1>, k_sc_bucket<D, 1>, k_sc_split<1>, k_sc_split_reduce<1>); break;
-		case 2: go(k_sc_scatter<D, 2>, k_sc_bucket<D, 2>, k_sc_split<2>, k_sc_split_reduce<2>); break;
-		case 4: go(k_sc_scatter<D, 4>, k_sc_bucket<D, 4>, k_sc_split<4>, k_sc_split_reduce<4>); break;
-		case 8: go(k_sc_scatter<D, 8>, k_sc_bucket<D, 8>, k_sc_split<8>, k_sc_split_reduce<8>); break;
+		case 1: go(k_sc_scatter<D, 1>, k_sc_accumulate<1>, k_sc_split_reduce<1>); break;
+		case 2: go(k_sc_scatter<D, 2>, k_sc_accumulate<2>, k_sc_split_reduce<2>); break;
+		case 4: go(k_sc_scatter<D, 4>, k_sc_accumulate<4>, k_sc_split_reduce<4>); break;
+		case 8: go(k_sc_scatter<D, 8>, k_sc_accumulate<8>, k_sc_split_reduce<8>); break;
 		default: throw Error("grid backward: unsupported F");
 	}
 }
@@ -507,8 +506,8 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	p.n_chunks = (uint32_t)div_round_up(n, p.spb);
 	p.n_items = (uint64_t)n * g.n_levels * (1u << g.n_dims);
 	NGP_CHECK(p.n_items < (1ull << 32), "grid backward: too many contributions for 32-bit offsets");
-	p.split_limit = 65536;
-	p.part = 32768;
+	p.split_limit = 49152;
+	p.part = 49152;
 	if (const char* e = getenv("NGP_SC_PART")) p.part = (uint32_t)atoi(e);
 	if (const char* e = getenv("NGP_SC_LIMIT")) p.split_limit = (uint32_t)atoi(e);
 	p.max_split_blocks = (uint32_t)(div_round_up(p.n_items, (uint64_t)p.part) + div_round_up(p.n_items, (uint64_t)p.split_limit) + 1);
@@ -520,7 +519,8 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	p.off_cur = align(p.off_hist + len * 4);
 	p.off_tot = align(p.off_cur + len * 4);
 	p.off_split = align(p.off_tot + (size_t)p.n_buckets * 4);
-	p.off_splitb = align(p.off_split + (2 + 3 * (size_t)p.max_split_blocks) * 4);
+	p.off_lo = align(p.off_split + (2 + 3 * (size_t)p.max_split_blocks) * 4);
+	p.off_splitb = align(p.off_lo + (size_t)p.n_buckets * 4);
 	p.off_scratch = align(p.off_splitb + 3 * (size_t)p.max_split_buckets * 4);
 	p.off_idx = align(p.off_scratch + (size_t)p.max_split_blocks * ((size_t)1 << p.B) * g.n_features * 8);
 	p.off_val = align(p.off_idx + p.n_items * 2);
@@ -528,19 +528,32 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	return p;
 }
 
-void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const ScatterPlan& p, void* workspace, hipStream_t s) {
+bool scatter_hist(const GridDesc& g, const ScatterPlan& p, void* workspace, GridHist& h) {
+	if ((size_t)p.n_buckets * 4 > 48 * 1024 || p.spb != 512) return false;
+	const Levels lv = make_levels(g, p.B);
+	h.hist = (uint32_t*)((char*)workspace + p.off_hist);
+	h.B = p.B; h.n_chunks = p.n_chunks; h.chunk = p.spb;
+	for (int l = 0; l <= 32; ++l) h.vb_base[l] = lv.vb_base[l];
+	return true;
+}
+
+void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const ScatterPlan& p, void* workspace, hipStream_t s, bool hist_done) {
 	if (a.n == 0) return;
 	char* ws = (char*)workspace;
-	const GridConst c = make_grid_const(g);
-	const Levels lv = make_levels(g, p.B);
 	uint32_t* hist = (uint32_t*)(ws + p.off_hist);
-	const dim3 grid_h(p.n_chunks, g.n_levels);
-	const size_t lds_h = (size_t)p.max_lb * 4;
-	if (g.n_dims == 3) k_sc_hist<3><<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
-	else k_sc_hist<2><<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
+	if (!hist_done) {
+		const GridConst c = make_grid_const(g);
+		const Levels lv = make_levels(g, p.B);
+		const dim3 grid_h(p.n_chunks, g.n_levels);
+		const size_t lds_h = (size_t)p.max_lb * 4;
+		if (g.n_dims == 3) k_sc_hist<3><<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
+		else k_sc_hist<2><<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
+		NGP_HIP(hipGetLastError());
+	}
+	k_sc_scan<<<p.n_buckets, SC_THREADS, 0, s>>>(hist, p.n_chunks, p.n_buckets, (uint32_t*)(ws + p.off_cur), (uint32_t*)(ws + p.off_tot));
 	NGP_HIP(hipGetLastError());
-	k_sc_scan<<<p.n_buckets, SC_THREADS, 0, s>>>(hist, p.n_chunks, p.n_buckets, (uint32_t*)(ws + p.off_cur),
-	                                              (uint32_t*)(ws + p.off_tot), (uint32_t*)(ws + p.off_split));
+	k_sc_plan<<<1, SC_PLAN_THREADS, 0, s>>>((const uint32_t*)(ws + p.off_tot), p.n_buckets, p.split_limit, p.part,
+	                                        (uint32_t*)(ws + p.off_lo), (uint32_t*)(ws + p.off_split), (uint32_t*)(ws + p.off_splitb));
 	NGP_HIP(hipGetLastError());
 }
 
