@@ -147,6 +147,7 @@ struct ngp_model {
 	// dependency edge, which in a HIP graph is not free.
 	uint32_t overlap = 0;
 	bool fused_hist = true;                 // option "fused_hist": bucket histogram inside the training forward
+	int grid_forward_mode = 0;              // option "grid_forward_mode": 0 auto, 1 per-sample rows, 2 XCD-partitioned
 	hipStream_t side = nullptr;             // overlaps fragments + bucket histogram with forward + MLP,
 	                                        // and the dW slab reduction with the grid backward
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_frags = nullptr, ev_mlp = nullptr, ev_red = nullptr;
@@ -272,10 +273,11 @@ struct ngp_model {
 		}
 		sc_hist_done = false;
 		GridHist h;
-		const bool fuse = want_hist && fused_hist && use_sorted(n) && !sc_prepared && grid_forward_rows_ok(grid, a) &&
+		const bool xcd = grid_forward_mode == 2;  // auto = per-sample rows: measured faster (DESIGN.md §Grid forward)
+		const bool fuse = want_hist && fused_hist && use_sorted(n) && !sc_prepared && (xcd || grid_forward_rows_ok(grid, a)) &&
 		                  scatter_hist(grid, sc_plan_for(n), sorted_workspace(n), h);
 		ProfScope ps("grid_forward", s);
-		grid_forward(grid, a, s, fuse ? &h : nullptr);
+		grid_forward(grid, a, s, fuse ? &h : nullptr, xcd ? 2 : 1);
 		sc_hist_done = fuse;
 	}
 	void run_mlp(hipStream_t s, MlpMode mode, uint32_t n, const float* in, uint32_t stride, const f16* encbuf, f16* out,
@@ -582,6 +584,9 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 		} else if (k == "overlap") {
 			NGP_CHECK(value >= 0 && value <= 15, "overlap is a bitmask in [0, 15]");
 			m->overlap = (uint32_t)value;
+		} else if (k == "grid_forward_mode") {
+			NGP_CHECK(value == 0 || value == 1 || value == 2, "grid_forward_mode must be 0 (auto), 1 (rows), 2 (XCD-partitioned)");
+			m->grid_forward_mode = (int)value;
 		} else if (k == "fused_hist") {
 			m->fused_hist = value != 0;
 		} else if (k == "win_debug") {

@@ -58,7 +58,10 @@ struct GridHist {
 	uint32_t vb_base[33];
 };
 
-void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist = nullptr);
+// mode: 0/1 per-sample kernels, 2 XCD-partitioned (level, chunk) kernel (L2-local tables; measured
+// slower than the per-sample row kernel on C2 and C2p, kept as an option)
+void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist = nullptr, int mode = 0);
+bool grid_forward_xcd_ok(const GridDesc& g, const GridFwdArgs& a);
 // true when grid_forward writes whole AoS rows (padding columns included: no memset needed)
 bool grid_forward_rows_ok(const GridDesc& g, const GridFwdArgs& a);
 void grid_backward(const GridDesc& g, const GridBwdArgs& a, hipStream_t stream);
@@ -69,6 +72,7 @@ struct GridConst {
 	uint32_t offsets[33];
 	float scale[32];
 	uint32_t resolution[32];
+	uint32_t hashed;  // bit l: level l is hashed (grid_index3's 32-bit stride > T; T is then a power of two)
 };
 
 __device__ __forceinline__ uint32_t grid_index3(uint32_t T, uint32_t res, uint32_t x, uint32_t y, uint32_t z) {
@@ -89,17 +93,72 @@ __device__ __forceinline__ uint32_t grid_index2(uint32_t T, uint32_t res, uint32
 	return index % T;
 }
 
+// Entry index of a corner. Same function as grid_index3/2 (tcnn grid_index) given the level kind
+// from GridConst::hashed: dense levels need the modulo only for out-of-range coordinates, hashed
+// levels have power-of-two T. Corner bit d offsets dimension d by one.
 template <uint32_t D>
 __device__ __forceinline__ uint32_t corner_index(const GridConst& c, uint32_t l, const uint32_t* base, uint32_t corner) {
-	const uint32_t T = c.offsets[l + 1] - c.offsets[l];
-	const uint32_t res = c.resolution[l];
 	const uint32_t x = base[0] + (corner & 1u);
 	const uint32_t y = base[1] + ((corner >> 1) & 1u);
+	if ((c.hashed >> l) & 1u) {
+		const uint32_t mask = c.offsets[l + 1] - c.offsets[l] - 1u;
+		if constexpr (D == 3) {
+			const uint32_t z = base[2] + ((corner >> 2) & 1u);
+			return c.offsets[l] + ((x ^ (y * 2654435761u) ^ (z * 805459861u)) & mask);
+		} else {
+			return c.offsets[l] + ((x ^ (y * 2654435761u)) & mask);
+		}
+	}
+	const uint32_t res = c.resolution[l];
+	uint32_t idx;
 	if constexpr (D == 3) {
 		const uint32_t z = base[2] + ((corner >> 2) & 1u);
-		return c.offsets[l] + grid_index3(T, res, x, y, z);
+		idx = x + res * (y + res * z);
 	} else {
-		return c.offsets[l] + grid_index2(T, res, x, y);
+		idx = x + res * y;
+	}
+	// in-range coordinates give idx < res^D <= T; out-of-range ones wrap like tcnn's index % T
+	const uint32_t T = c.offsets[l + 1] - c.offsets[l];
+	if (__builtin_expect(idx >= T, 0)) idx %= T;
+	return c.offsets[l] + idx;
+}
+
+// Gather the 2^D corner entries of one level. The two corners of an x-edge are adjacent entries on
+// dense levels, and on hashed levels when base x is even (the hash's x prime is 1, so x+1 flips bit
+// 0 only): then both come from one 2F-wide load — half the gather requests of a dense level.
+template <uint32_t F> struct GridVec;
+template <> struct GridVec<1> { typedef f16 T; typedef f16 __attribute__((ext_vector_type(2), aligned(2))) P; };
+template <> struct GridVec<2> { typedef f16x2 T; typedef f16 __attribute__((ext_vector_type(4), aligned(4))) P; };
+template <> struct GridVec<4> { typedef f16x4 T; typedef f16 __attribute__((ext_vector_type(8), aligned(8))) P; };
+template <> struct GridVec<8> { typedef f16x8 T; typedef f16x8 P; };
+
+template <uint32_t D, uint32_t F>
+__device__ __forceinline__ void gather_corners(const GridConst& c, uint32_t l, const uint32_t* base, const f16* __restrict__ table,
+                                               typename GridVec<F>::T* v) {
+	typedef typename GridVec<F>::T V;
+	typedef typename GridVec<F>::P P;
+	if constexpr (F == 2 || F == 4) {
+#pragma unroll
+		for (uint32_t k = 0; k < (1u << D); k += 2) {
+			const uint32_t i0 = corner_index<D>(c, l, base, k), i1 = corner_index<D>(c, l, base, k + 1);
+			// dense: i1 == i0 + 1 (unless wrapped); hashed with even base x: i1 == i0 ^ 1
+			const uint32_t lo_i = min(i0, i1);
+			if (max(i0, i1) == lo_i + 1u) {
+				const P p = *(const P*)(table + (size_t)lo_i * F);
+				V lo, hi;
+#pragma unroll
+				for (uint32_t f = 0; f < F; ++f) { lo[f] = p[f]; hi[f] = p[F + f]; }
+				const bool swap = i1 < i0;
+				v[k] = swap ? hi : lo;
+				v[k + 1] = swap ? lo : hi;
+			} else {
+				v[k] = *(const V*)(table + (size_t)i0 * F);
+				v[k + 1] = *(const V*)(table + (size_t)i1 * F);
+			}
+		}
+	} else {
+#pragma unroll
+		for (uint32_t k = 0; k < (1u << D); ++k) v[k] = *(const V*)(table + (size_t)corner_index<D>(c, l, base, k) * F);
 	}
 }
 

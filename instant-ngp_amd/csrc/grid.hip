@@ -8,6 +8,8 @@
 // profiles/r01_atomics.txt), so requests, not bytes, are the cost.
 #include "grid.h"
 
+#include <algorithm>
+
 #include <cmath>
 #include <cstring>
 
@@ -47,6 +49,19 @@ GridConst make_grid_const(const GridDesc& g) {
 	memcpy(c.offsets, g.offsets, sizeof(c.offsets));
 	memcpy(c.scale, g.scale, sizeof(c.scale));
 	memcpy(c.resolution, g.resolution, sizeof(c.resolution));
+	c.hashed = 0;
+	for (uint32_t l = 0; l < g.n_levels; ++l) {
+		// the kind exactly as grid_index3/2 decide it: 32-bit stride, multiplied while it fits in T
+		// (fine levels of large-scale grids wrap the stride and stay "dense", with index % T)
+		const uint32_t T = g.offsets[l + 1] - g.offsets[l];
+		uint32_t stride = g.resolution[l];
+		for (uint32_t d = 1; d < g.n_dims; ++d)
+			if (stride <= T) stride *= g.resolution[l];
+		if (T < stride) {
+			NGP_CHECK((T & (T - 1)) == 0, "GridEncoding: hashed level size must be a power of two");
+			c.hashed |= 1u << l;
+		}
+	}
 	return c;
 }
 
@@ -73,8 +88,7 @@ __global__ void __launch_bounds__(256) k_grid_forward(const GridConst c, const G
 			float frac[D]; uint32_t base[D];
 			level_setup<D>(c, l, x, frac, base);
 			V v[1u << D];
-#pragma unroll
-			for (uint32_t k = 0; k < (1u << D); ++k) v[k] = *(const V*)(a.table + (size_t)corner_index<D>(c, l, base, k) * F);
+			gather_corners<D, F>(c, l, base, a.table, v);
 #pragma unroll
 			for (uint32_t k = 0; k < (1u << D); ++k) {
 				const float w = corner_weight<D>(frac, k);
@@ -147,8 +161,7 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 					atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
 			}
 			V v[1u << D];
-#pragma unroll
-			for (uint32_t k = 0; k < (1u << D); ++k) v[k] = *(const V*)(a.table + (size_t)corner_index<D>(c, l, base, k) * F);
+			gather_corners<D, F>(c, l, base, a.table, v);
 #pragma unroll
 			for (uint32_t k = 0; k < (1u << D); ++k) {
 				const float w = corner_weight<D>(frac, k);
@@ -234,6 +247,130 @@ bool grid_forward_rows_ok(const GridDesc& g, const GridFwdArgs& a) {
 	       ((uintptr_t)a.out & 15) == 0;
 }
 
+// XCD-partitioned forward: work = (level, chunk of 512 samples) blocks, ordered so that every block
+// of a level runs on the same XCD slot (blocks are dealt round-robin over the 8 XCDs: b % 8 names a
+// slot, MI355X_MICROARCH §Workgroup dispatch — for speed only, never correctness). Each XCD's 4 MiB L2
+// then holds the tables of its own levels instead of all of them: the gathers hit in L2 instead of
+// the Infinity Cache. L >= 8: slot x owns levels x, x + 8, ... (level-major, all chunks); L < 8
+// (8 % L == 0): slot x owns level x % L and every (8 / L)-th chunk.
+constexpr uint32_t XCD_SLOTS = 8;
+constexpr uint32_t XCD_CHUNK = 512;
+
+struct XcdMap {
+	uint32_t n_chunks, rounds, lpx, reps;  // lpx: levels per slot (L >= 8); reps: slots per level (L < 8)
+};
+
+__host__ __device__ inline XcdMap make_xcd_map(uint32_t n, uint32_t L) {
+	XcdMap m;
+	m.n_chunks = (n + XCD_CHUNK - 1) / XCD_CHUNK;
+	if (L >= XCD_SLOTS) {
+		m.lpx = (L + XCD_SLOTS - 1) / XCD_SLOTS; m.reps = 1;
+		m.rounds = m.lpx * m.n_chunks;
+	} else {
+		m.lpx = 1; m.reps = XCD_SLOTS / L;
+		m.rounds = (m.n_chunks + m.reps - 1) / m.reps;
+	}
+	return m;
+}
+
+template <uint32_t D, uint32_t F, bool HIST>
+__global__ void __launch_bounds__(256) k_grid_forward_xcd(const GridConst c, const GridFwdArgs a, const XcdMap m, const GridHist h) {
+	typedef typename FeatVec<F>::T V;
+	extern __shared__ uint32_t hl[];  // HIST: this (level, chunk)'s bucket counts
+	const uint32_t slot = blockIdx.x % XCD_SLOTS, r = blockIdx.x / XCD_SLOTS;
+	uint32_t l, chunk;
+	if (m.reps == 1) { l = slot + XCD_SLOTS * (r / m.n_chunks); chunk = r % m.n_chunks; }
+	else { l = slot % c.n_levels; chunk = r * m.reps + slot / c.n_levels; }
+	if (l >= c.n_levels || chunk >= m.n_chunks) return;
+	uint32_t nvb = 0;
+	if constexpr (HIST) {
+		nvb = h.vb_base[l + 1] - h.vb_base[l];
+		for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) hl[j] = 0;
+		__syncthreads();
+	}
+#pragma unroll
+	for (uint32_t q = 0; q < XCD_CHUNK / 256; ++q) {
+		const uint32_t i = chunk * XCD_CHUNK + q * 256 + threadIdx.x;
+		if (i >= a.n) break;
+		float x[D];
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * a.pos_stride + d];
+		const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
+		const bool active = !((float)l >= ml + 1e-3f);
+		float acc[F];
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) acc[f] = 0.f;
+		float frac[D]; uint32_t base[D];
+		level_setup<D>(c, l, x, frac, base);
+		if constexpr (HIST) {
+#pragma unroll
+			for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&hl[(corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B], 1u);
+		}
+		if (active) {
+			V v[1u << D];
+			gather_corners<D, F>(c, l, base, a.table, v);
+#pragma unroll
+			for (uint32_t k = 0; k < (1u << D); ++k) {
+				const float w = corner_weight<D>(frac, k);
+				if constexpr (F == 1) acc[0] = __builtin_fmaf(w, (float)v[k], acc[0]);
+				else {
+#pragma unroll
+					for (uint32_t f = 0; f < F; ++f) acc[f] = __builtin_fmaf(w, (float)v[k][f], acc[f]);
+				}
+			}
+		}
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) asm volatile("" : "+v"(acc[f]));
+		if (a.out_layout == AoS) {
+			V o;
+			if constexpr (F == 1) o = (f16)acc[0];
+			else {
+#pragma unroll
+				for (uint32_t f = 0; f < F; ++f) o[f] = (f16)acc[f];
+			}
+			*(V*)(a.out + (size_t)i * a.out_stride + l * F) = o;
+		} else {
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) a.out[(size_t)(l * F + f) * a.out_stride + i] = (f16)acc[f];
+		}
+	}
+	if constexpr (HIST) {
+		__syncthreads();
+		for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) h.hist[(size_t)(h.vb_base[l] + j) * h.n_chunks + chunk] = hl[j];
+	}
+}
+
+bool grid_forward_xcd_ok(const GridDesc& g, const GridFwdArgs& a) {
+	return a.n >= 16384 && (g.n_levels >= XCD_SLOTS || XCD_SLOTS % g.n_levels == 0) &&
+	       (a.out_layout != AoS || a.out_stride == g.n_levels * g.n_features);
+}
+
+template <uint32_t D>
+static void launch_fwd_xcd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hipStream_t s, const GridHist* h) {
+	const XcdMap m = make_xcd_map(a.n, c.n_levels);
+	const dim3 grid(XCD_SLOTS * m.rounds);
+	if (h) NGP_CHECK(h->chunk == XCD_CHUNK && h->n_chunks == m.n_chunks, "grid forward histogram: chunk mismatch");
+	uint32_t max_lb = 0;
+	if (h) for (uint32_t l = 0; l < c.n_levels; ++l) max_lb = std::max(max_lb, h->vb_base[l + 1] - h->vb_base[l]);
+	const size_t lds = (size_t)max_lb * 4;
+	const GridHist none{};
+	auto go = [&](auto kern_nohist, auto kern_hist) {
+		if (h) {
+			ensure_dynamic_lds((const void*)kern_hist, lds);
+			kern_hist<<<grid, 256, lds, s>>>(c, a, m, *h);
+		} else {
+			kern_nohist<<<grid, 256, 0, s>>>(c, a, m, none);
+		}
+	};
+	switch (F) {
+		case 1: go(k_grid_forward_xcd<D, 1, false>, k_grid_forward_xcd<D, 1, true>); return;
+		case 2: go(k_grid_forward_xcd<D, 2, false>, k_grid_forward_xcd<D, 2, true>); return;
+		case 4: go(k_grid_forward_xcd<D, 4, false>, k_grid_forward_xcd<D, 4, true>); return;
+		case 8: go(k_grid_forward_xcd<D, 8, false>, k_grid_forward_xcd<D, 8, true>); return;
+		default: throw Error("GridEncoding: unsupported F");
+	}
+}
+
 template <uint32_t D>
 static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hipStream_t s, bool rows, const GridHist* h) {
 	const dim3 grid(div_round_up(a.n, 256)), block(256);
@@ -286,9 +423,16 @@ static void launch_bwd(uint32_t F, const GridConst& c, const GridBwdArgs& a, hip
 	}
 }
 
-void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist) {
+void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist, int mode) {
 	if (a.n == 0) return;
 	GridConst c = make_grid_const(g);
+	if (mode == 2) {
+		NGP_CHECK(grid_forward_xcd_ok(g, a), "grid forward: the XCD-partitioned kernel does not apply");
+		if (g.n_dims == 3) launch_fwd_xcd<3>(g.n_features, c, a, stream, hist);
+		else launch_fwd_xcd<2>(g.n_features, c, a, stream, hist);
+		NGP_HIP(hipGetLastError());
+		return;
+	}
 	const bool rows = grid_forward_rows_ok(g, a);
 	if (g.n_dims == 3) launch_fwd<3>(g.n_features, c, a, stream, rows, hist);
 	else launch_fwd<2>(g.n_features, c, a, stream, rows, hist);

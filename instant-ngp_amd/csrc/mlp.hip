@@ -376,18 +376,37 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	}
 
 	const uint32_t n_tiles = (a.n + 31) / 32;
+	// One wave per SIMD: the next tile's global inputs (encoding, direction, dL/dout) are loaded while
+	// this tile computes, so their latency is not exposed once per tile.
+	f16x8 xe_n[ES];
+	float cd_n[3] = {0.f, 0.f, 0.f};
+	f16x4 dl_n{};
+	auto load_inputs = [&](uint32_t tile) {
+		const uint32_t smp = tile * 32 + (lane & 31);
+		const uint32_t ls = smp < a.n ? smp : 0;
+#pragma unroll
+		for (int s = 0; s < ES; ++s) xe_n[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
+		if constexpr (!DENSITY) {
+			const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
+			cd_n[0] = cd[0]; cd_n[1] = cd[1]; cd_n[2] = cd[2];
+		}
+		if constexpr (TRAIN) dl_n = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
+	};
+	if (blockIdx.x * 4 + wave < n_tiles) load_inputs(blockIdx.x * 4 + wave);
 	for (uint32_t tile = blockIdx.x * 4 + wave; tile < n_tiles; tile += gridDim.x * 4) {
 		const uint32_t sample = tile * 32 + (lane & 31);
 		const bool valid = sample < a.n;
-		const uint32_t ls = valid ? sample : 0;
-
-		// ---- density forward -------------------------------------------------------------------
 		f16x8 xe[ES];
 #pragma unroll
-		for (int s = 0; s < ES; ++s) {
-			xe[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
-			if (!valid) xe[s] = f16x8{};
-			if constexpr (TRAIN) img_store_std(img + Lay::I_XE, Lay::S_XE, xe[s], s, lane);
+		for (int s = 0; s < ES; ++s) xe[s] = valid ? xe_n[s] : f16x8{};
+		const float cdx = cd_n[0], cdy = cd_n[1], cdz = cd_n[2];
+		const f16x4 dl_cur = dl_n;
+		if (tile + gridDim.x * 4 < n_tiles) load_inputs(tile + gridDim.x * 4);
+
+		// ---- density forward -------------------------------------------------------------------
+		if constexpr (TRAIN) {
+#pragma unroll
+			for (int s = 0; s < ES; ++s) img_store_std(img + Lay::I_XE, Lay::S_XE, xe[s], s, lane);
 		}
 		f32x16 acc[2];
 		f16x8 hd[DH][4];
@@ -408,8 +427,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		}
 
 		// ---- rgb forward -----------------------------------------------------------------------
-		const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
-		f16x8 rin[2] = {dout[0], sh4_frag(cd[0], cd[1], cd[2], h)};
+		f16x8 rin[2] = {dout[0], sh4_frag(cdx, cdy, cdz, h)};
 		if (!valid) rin[1] = f16x8{};
 		f16x8 hr[RH][4];
 		layer_fwd<2, 2>(acc, rin, lfrag + Lay::F_R0 * 64, lane);
@@ -445,7 +463,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 			float dsig = 0.f;
 			f16x8 dz1[1];
 			{
-				f16x4 d = valid ? *(const f16x4*)(a.dL_dout + (size_t)sample * a.dL_stride) : f16x4{};
+				f16x4 d = valid ? dl_cur : f16x4{};
 				dsig = (float)d[3];
 				// extract_rgb (nerf_network.h:46-60): rows 0..2 of dL/drgb, the rest zero
 				dz1[0] = h == 0 ? f16x8{d[0], d[1], d[2], (f16)0.f, 0, 0, 0, 0} : f16x8{};
