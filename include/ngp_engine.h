@@ -225,6 +225,9 @@ typedef struct {
 	float focal_length[2];
 	float principal_point[2];
 	float xform[12];
+	uint32_t lens_mode;      /* Lens (common_device.cuh:288-378, nerf_loader.cu:160-224): 0 perspective,
+	                            1 OpenCV {k1, k2, p1, p2}, 2 OpenCV fisheye {k1, k2, k3, k4} */
+	float lens_params[4];
 } ngp_nerf_image;
 
 /* Training knobs with the reference defaults (testbed.h:716-785; load_nerf_post testbed_nerf.cu:3093-3109). */

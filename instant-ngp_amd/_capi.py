@@ -34,7 +34,8 @@ class ParamLayout(C.Structure):
 class NerfImage(C.Structure):
     """ngp_nerf_image: TrainingImageMetadata + camera-to-world mat4x3 (column-major)."""
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("focal_length", C.c_float * 2),
-                ("principal_point", C.c_float * 2), ("xform", C.c_float * 12)]
+                ("principal_point", C.c_float * 2), ("xform", C.c_float * 12), ("lens_mode", C.c_uint32),
+                ("lens_params", C.c_float * 4)]
 
 
 class NerfConfig(C.Structure):

@@ -9,6 +9,7 @@
 #pragma once
 #include "../../include/ngp_engine.h"
 #include "common.h"
+#include "lens.h"
 
 #include <functional>
 
@@ -34,6 +35,8 @@ struct Camera {          // per image, device side
 	float focal[2], principal[2];
 	float m[12];         // effective camera matrix (rolling-shutter slerp at t=0 applied on the host)
 	uint64_t pixel_offset;  // first RGBA8 pixel of this image in the packed image buffer
+	uint32_t lens_mode;  // LensMode (lens.h)
+	float lens[4];
 };
 
 struct Rng { uint64_t state, inc; };  // tcnn::pcg32 state
@@ -102,6 +105,8 @@ struct RenderArgs {
 	uint32_t width, height;
 	float focal[2], screen_center[2];
 	float cam[12];                 // camera-to-world mat4x3 (column-major)
+	uint32_t lens_mode;            // render_lens of the training view (testbed.cu:846)
+	float lens[4];
 	float near_distance;
 	float aabb_min[3], aabb_max[3];
 	float cone_angle_constant;

@@ -257,9 +257,10 @@ __device__ RaySetup setup_ray(const Camera* cams, const uint32_t* pixels, uint32
 	const uint32_t raw = pixels[cam.pixel_offset + pixel_index(u, v, cam.width, cam.height)];
 	if (raw == 0x00FF00FFu) return r;  // masked (read_rgba returns -1)
 	(void)pcg_float(rng);              // motionblur_time
-	// uv_to_ray, pinhole (common_device.cuh:443-510)
-	const float dx = (u - cam.principal[0]) * (float)cam.width / cam.focal[0];
-	const float dy = (v - cam.principal[1]) * (float)cam.height / cam.focal[1];
+	// uv_to_ray (common_device.cuh:443-510): pinhole, then the lens undistortion
+	float dx = (u - cam.principal[0]) * (float)cam.width / cam.focal[0];
+	float dy = (v - cam.principal[1]) * (float)cam.height / cam.focal[1];
+	lens_undistort(cam.lens_mode, cam.lens, &dx, &dy);
 	const float dz = 1.0f;
 	const float* m = cam.m;
 	r.d = v3(m[0] * dx + m[3] * dy + m[6] * dz, m[1] * dx + m[4] * dy + m[7] * dz, m[2] * dx + m[5] * dy + m[8] * dz);
@@ -827,9 +828,11 @@ __global__ void k_render_init(RenderArgs a, Payload* __restrict__ pay, float* __
 	float ox, oy;
 	ld_random_pixel_offset(a.snap_to_pixel_centers ? 0u : a.sample_index, &ox, &oy);
 	const float u = ((float)x + ox) / (float)W, v = ((float)y + oy) / (float)H;
-	// uv_to_ray (common_device.cuh:443-510), pinhole, screen_center = 1 - principal point (testbed.cu:852)
-	const float dx = (u - a.screen_center[0]) * (float)W / a.focal[0];
-	const float dy = (v - a.screen_center[1]) * (float)H / a.focal[1];
+	// uv_to_ray (common_device.cuh:443-510), screen_center = 1 - principal point (testbed.cu:852), with
+	// the training view's lens (render_with_lens_distortion, testbed.cu:845-846)
+	float dx = (u - a.screen_center[0]) * (float)W / a.focal[0];
+	float dy = (v - a.screen_center[1]) * (float)H / a.focal[1];
+	lens_undistort(a.lens_mode, a.lens, &dx, &dy);
 	const float* m = a.cam;
 	V3 d = v3(m[0] * dx + m[3] * dy + m[6], m[1] * dx + m[4] * dy + m[7], m[2] * dx + m[5] * dy + m[8]);
 	V3 o = v3(m[9] + d.x * a.near_distance, m[10] + d.y * a.near_distance, m[11] + d.z * a.near_distance);

@@ -114,7 +114,7 @@ static hipStream_t S(void* s) { return (hipStream_t)s; }
 namespace ngp { void set_last_error(const char* msg); }
 static void nerf_set_error(const char* m) { ngp::set_last_error(m); }
 
-// mark_untrained_density_grid (testbed_nerf.cu:503-592) for perspective cameras
+// mark_untrained_density_grid (testbed_nerf.cu:503-592) for perspective and OpenCV(-fisheye) cameras
 __global__ void k_mark_untrained(uint32_t n_elements, float* __restrict__ grid, uint32_t n_images, const Camera* __restrict__ cams,
                                  const float* __restrict__ raw_xforms, bool clear_visible) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -148,14 +148,18 @@ __global__ void k_mark_untrained(uint32_t n_elements, float* __restrict__ grid, 
 			const float il = 1.0f / sqrtf(dx * dx + dy * dy + dz * dz);
 			const float nx = dx * il, ny = dy * il, nz = dz * il;
 			if (nx * m[6] + ny * m[7] + nz * m[8] < 1e-4f) continue;
-			// pos_to_uv (common_device.cuh:547-585), perspective
+			// pos_to_uv (common_device.cuh:547-585): perspective projection + forward lens distortion
 			float ex = I[0] * dx + I[3] * dy + I[6] * dz, ey = I[1] * dx + I[4] * dy + I[7] * dz, ez = I[2] * dx + I[5] * dy + I[8] * dz;
 			ex /= ez; ey /= ez;
+			float du, dv;
+			lens_delta(cam.lens_mode, cam.lens, ex, ey, &du, &dv);
+			ex += du; ey += dv;
 			const float u = ex * cam.focal[0] / (float)cam.width + cam.principal[0];
 			const float v = ey * cam.focal[1] / (float)cam.height + cam.principal[1];
-			// uv_to_ray with the raw xform, compare directions
-			const float rx = (u - cam.principal[0]) * (float)cam.width / cam.focal[0];
-			const float ry = (v - cam.principal[1]) * (float)cam.height / cam.focal[1];
+			// uv_to_ray with the raw xform (pos_to_uv is not injective under distortion), compare directions
+			float rx = (u - cam.principal[0]) * (float)cam.width / cam.focal[0];
+			float ry = (v - cam.principal[1]) * (float)cam.height / cam.focal[1];
+			lens_undistort(cam.lens_mode, cam.lens, &rx, &ry);
 			const float ddx = m[0] * rx + m[3] * ry + m[6], ddy = m[1] * rx + m[4] * ry + m[7], ddz = m[2] * rx + m[5] * ry + m[8];
 			const float rl = 1.0f / sqrtf(ddx * ddx + ddy * ddy + ddz * ddz);
 			const float qx = ddx * rl - nx, qy = ddy * rl - ny, qz = ddz * rl - nz;
@@ -202,6 +206,9 @@ int ngp_nerf_dataset_create(uint32_t n_images, const ngp_nerf_image* images, con
 			c.width = im.width; c.height = im.height;
 			c.focal[0] = im.focal_length[0]; c.focal[1] = im.focal_length[1];
 			c.principal[0] = im.principal_point[0]; c.principal[1] = im.principal_point[1];
+			NGP_CHECK(im.lens_mode <= LENS_OPENCV_FISHEYE, "nerf dataset: unsupported lens mode");
+			c.lens_mode = im.lens_mode;
+			for (int k = 0; k < 4; ++k) c.lens[k] = im.lens_params[k];
 			effective_camera_matrix(im.xform, c.m);
 			c.pixel_offset = total;
 			total += (uint64_t)im.width * im.height;
@@ -335,6 +342,9 @@ int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_confi
 		a.screen_center[0] = 1.0f - camera->principal_point[0];  // set_camera_to_training_view (testbed.cu:852)
 		a.screen_center[1] = 1.0f - camera->principal_point[1];
 		effective_camera_matrix(camera->xform, a.cam);
+		NGP_CHECK(camera->lens_mode <= LENS_OPENCV_FISHEYE, "render: unsupported lens mode");
+		a.lens_mode = camera->lens_mode;
+		for (int k = 0; k < 4; ++k) a.lens[k] = camera->lens_params[k];
 		a.near_distance = 0.0f;  // m_render_near_distance (testbed.h:914)
 		for (int k = 0; k < 3; ++k) { a.aabb_min[k] = cfg->aabb_min[k]; a.aabb_max[k] = cfg->aabb_max[k]; }
 		a.cone_angle_constant = cfg->cone_angle_constant;

@@ -62,7 +62,11 @@ def nerf_matrix_to_ngp(m, scale=0.33, offset=(0.5, 0.5, 0.5)):
     return np.ascontiguousarray(m.T).reshape(12)
 
 
-def make_image(width, height, xform12, focal=None, camera_angle_x=None, principal=(0.5, 0.5)):
+LENS_PERSPECTIVE, LENS_OPENCV, LENS_OPENCV_FISHEYE = 0, 1, 2
+
+
+def make_image(width, height, xform12, focal=None, camera_angle_x=None, principal=(0.5, 0.5), lens_mode=LENS_PERSPECTIVE,
+               lens_params=(0.0, 0.0, 0.0, 0.0)):
     im = NerfImage()
     im.width, im.height = width, height
     if focal is None:
@@ -71,6 +75,8 @@ def make_image(width, height, xform12, focal=None, camera_angle_x=None, principa
     im.focal_length[:] = list(focal)
     im.principal_point[:] = list(principal)
     im.xform[:] = [float(v) for v in xform12]
+    im.lens_mode = int(lens_mode)
+    im.lens_params[:] = [float(v) for v in lens_params]
     return im
 
 

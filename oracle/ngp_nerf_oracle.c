@@ -43,7 +43,60 @@ typedef struct {
 	uint32_t width, height;
 	float focal_length[2], principal_point[2];
 	float xform[12];
+	uint32_t lens_mode;
+	float lens_params[4];
 } oimg;
+
+/* ---- lens models (common_device.cuh:288-378): 1 OpenCV {k1,k2,p1,p2}, 2 OpenCV fisheye {k1..k4} ---- */
+static void lens_delta(uint32_t mode, const float* k, float u, float v, float* du, float* dv) {
+	if (mode == 1) { /* opencv_lens_distortion_delta :289-303 */
+		const float u2 = u * u, uv = u * v, v2 = v * v;
+		const float r2 = u2 + v2;
+		const float radial = k[0] * r2 + k[1] * r2 * r2;
+		*du = u * radial + 2.0f * k[2] * uv + k[3] * (r2 + 2.0f * u2);
+		*dv = v * radial + 2.0f * k[3] * uv + k[2] * (r2 + 2.0f * v2);
+	} else if (mode == 2) { /* opencv_fisheye_lens_distortion_delta :305-327 */
+		const float r = sqrtf(u * u + v * v);
+		if (r > 2.220446049250313e-16f) {
+			const float th = atanf(r), th2 = th * th, th4 = th2 * th2, th6 = th4 * th2, th8 = th4 * th4;
+			const float thd = th * (1.0f + k[0] * th2 + k[1] * th4 + k[2] * th6 + k[3] * th8);
+			*du = u * thd / r - u;
+			*dv = v * thd / r - v;
+		} else {
+			*du = 0.0f; *dv = 0.0f;
+		}
+	} else {
+		*du = 0.0f; *dv = 0.0f;
+	}
+}
+
+/* iterative_lens_undistortion :330-369 (Newton, central differences, glm mat2 inverse) */
+static void lens_undistort(uint32_t mode, const float* k, float* u, float* v) {
+	if (mode != 1 && mode != 2) return;
+	const float x0u = *u, x0v = *v;
+	float xu = *u, xv = *v;
+	for (uint32_t i = 0; i < 100; ++i) {
+		const float s0 = fmaxf(1.1920928955078125e-07f, fabsf(1e-6f * xu));
+		const float s1 = fmaxf(1.1920928955078125e-07f, fabsf(1e-6f * xv));
+		float d0, d1, b00, b01, f00, f01, b10, b11, f10, f11;
+		lens_delta(mode, k, xu, xv, &d0, &d1);
+		lens_delta(mode, k, xu - s0, xv, &b00, &b01);
+		lens_delta(mode, k, xu + s0, xv, &f00, &f01);
+		lens_delta(mode, k, xu, xv - s1, &b10, &b11);
+		lens_delta(mode, k, xu, xv + s1, &f10, &f11);
+		const float j00 = 1.0f + (f00 - b00) / (2.0f * s0), j10 = (f10 - b10) / (2.0f * s1);
+		const float j01 = (f01 - b01) / (2.0f * s0), j11 = 1.0f + (f11 - b11) / (2.0f * s1);
+		const float od = 1.0f / (j00 * j11 - j10 * j01);
+		const float i00 = j11 * od, i01 = -j01 * od, i10 = -j10 * od, i11 = j00 * od;
+		const float ru = xu + d0 - x0u, rv = xv + d1 - x0v;
+		const float su = i00 * ru + i10 * rv, sv = i01 * ru + i11 * rv;
+		xu -= su; xv -= sv;
+		if (su * su + sv * sv < 1e-10f) break;
+	}
+	*u = xu; *v = xv;
+}
+
+EXPORT void orc_lens_undistort(uint32_t mode, const float* k, float* u, float* v) { lens_undistort(mode, k, u, v); }
 
 /* ---- stepping (testbed_nerf.cu:114-184) ---- */
 static float to_step(float t, float c) {
@@ -225,6 +278,7 @@ static oray setup(const ocfg* c, const oimg* ims, const float* cams, const uint3
 	const float* m = cams + 12 * img;
 	float dx = (u - im->principal_point[0]) * (float)im->width / im->focal_length[0];
 	float dy = (v - im->principal_point[1]) * (float)im->height / im->focal_length[1];
+	lens_undistort(im->lens_mode, im->lens_params, &dx, &dy);
 	float dz = 1.0f;
 	r.d[0] = m[0] * dx + m[3] * dy + m[6] * dz;
 	r.d[1] = m[1] * dx + m[4] * dy + m[7] * dz;
@@ -587,8 +641,9 @@ EXPORT void orc_nerf_render_march(const ocfg* c, const oimg* cam, const uint8_t*
 	for (uint32_t i = 0; i < W * H; ++i) {
 		const uint32_t x = i % W, y = i / W;
 		const float u = ((float)x + ox) / (float)W, v = ((float)y + oy) / (float)H;
-		const float dx = (u - (1.0f - cam->principal_point[0])) * (float)W / cam->focal_length[0];
-		const float dy = (v - (1.0f - cam->principal_point[1])) * (float)H / cam->focal_length[1];
+		float dx = (u - (1.0f - cam->principal_point[0])) * (float)W / cam->focal_length[0];
+		float dy = (v - (1.0f - cam->principal_point[1])) * (float)H / cam->focal_length[1];
+		lens_undistort(cam->lens_mode, cam->lens_params, &dx, &dy);
 		float d[3] = {m[0] * dx + m[3] * dy + m[6], m[1] * dx + m[4] * dy + m[7], m[2] * dx + m[5] * dy + m[8]};
 		const float o[3] = {m[9], m[10], m[11]};
 		const float inv = 1.0f / sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);

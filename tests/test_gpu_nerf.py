@@ -36,6 +36,24 @@ def scene(pkg):
     return ds, ims, pix
 
 
+FOX_LENS = (0.0578421, -0.0805099, -0.000980296, 0.00015575)  # data/nerf/fox/transforms.json k1 k2 p1 p2
+
+
+@pytest.fixture(scope="module")
+def scene_lens(pkg):
+    """OpenCV-distorted cameras (fox coefficients, and a stronger one) with off-centre principal points."""
+    S = pkg.synthetic
+    ims, pix = [], []
+    for i, c2w in enumerate(S.camera_poses(4, seed=3)):
+        w, h = 90 + 6 * i, 120 - 4 * i
+        k = FOX_LENS if i % 2 == 0 else (-0.21, 0.05, 0.002, -0.001)
+        ims.append(pkg.nerf.make_image(w, h, pkg.nerf.nerf_matrix_to_ngp(c2w), camera_angle_x=S.LEGO_CAMERA_ANGLE_X,
+                                       principal=(0.48 + 0.01 * i, 0.52 - 0.01 * i), lens_mode=pkg.nerf.LENS_OPENCV,
+                                       lens_params=k))
+        pix.append(S.render(c2w, w, h))
+    return pkg.nerf.NerfDataset(ims, pix), ims, pix
+
+
 def occupancy(orc, seed=0, frac=0.3, max_cascade=0):
     g = np.random.default_rng(seed)
     grid = np.where(g.random(128 ** 3 * 8) < frac, 1.0, 0.0).astype(np.float32)
@@ -69,6 +87,25 @@ def test_generate_training_samples_bitexact(pkg, orc, scene, n_rays, max_samples
     np.testing.assert_array_equal(got["numsteps"][:kept].view(np.uint32), ref["numsteps"][:kept])
     np.testing.assert_array_equal(got["rays"][:kept], ref["rays"][:kept])
     used = min(int(ref["counters"][1]), max_samples)
+    np.testing.assert_array_equal(got["coords"][:used], ref["coords"][:used])
+
+
+@pytest.mark.parametrize("n_rays,frac", [(2048, 0.4), (4096, 1.0)])
+def test_generate_training_samples_opencv_lens(pkg, orc, scene_lens, n_rays, frac):
+    """uv_to_ray with OpenCV undistortion (iterative Newton, common_device.cuh:330-369): no
+    transcendental, so rays and samples stay bit-exact with the oracle."""
+    ds, ims, pix = scene_lens
+    cfg = pkg.nerf.default_config(1.0)
+    _, bf = occupancy(orc, seed=n_rays + 7, frac=frac)
+    r = rng(pkg, 4242 + n_rays)
+    got = pkg.nerf.generate_training_samples(ds, cfg, n_rays, r, 1 << 18, torch.from_numpy(bf).cuda(), n_rays_total=n_rays)
+    ref = orc.nerf_generate_samples(cfg, ims, pix, n_rays, orc_rng(orc, r), 1 << 18, bf)
+    got = {k: v.cpu().numpy() for k, v in got.items()}
+    np.testing.assert_array_equal(got["counters"].view(np.uint32), ref["counters"])
+    kept = int(ref["counters"][0])
+    np.testing.assert_array_equal(got["rays"][:kept], ref["rays"][:kept])
+    np.testing.assert_array_equal(got["numsteps"][:kept].view(np.uint32), ref["numsteps"][:kept])
+    used = min(int(ref["counters"][1]), 1 << 18)
     np.testing.assert_array_equal(got["coords"][:used], ref["coords"][:used])
 
 

@@ -55,6 +55,24 @@ def test_render_matches_oracle(pkg, orc, seed, frac, sample_index):
     assert d.mean() < 2e-3, d.mean()
 
 
+@pytest.mark.parametrize("mode,k", [(1, (0.0578421, -0.0805099, -0.000980296, 0.00015575)), (2, (0.05, -0.01, 0.002, 0.0))])
+def test_render_with_lens_matches_oracle(pkg, orc, mode, k):
+    """render_with_lens_distortion with the training view's lens (testbed.cu:845-846): OpenCV and
+    OpenCV fisheye (atanf: an ulp apart from the oracle's, inside the colour tolerance)."""
+    cam, cfg, net, p16, bf, m = _setup(pkg, orc, 4, 0.5)
+    cam.lens_mode = mode
+    cam.lens_params[:] = list(k)
+    cam.principal_point[:] = [0.47, 0.53]
+    r = pkg.nerf.NerfRenderer()
+    img = r.render(net, cfg, cam, torch.from_numpy(bf).cuda(), spp=1, min_transmittance=1e-4, background=(0, 0, 0, 1),
+                   use_inference_params=False).cpu().numpy()
+    ref, counts = orc.nerf_render(cfg, cam, m, p16, bf, sample_index=0, min_transmittance=1e-4, bg=(0, 0, 0, 1))
+    assert (counts > 0).mean() > 0.2
+    d = np.abs(img - ref)
+    assert d.max() < 2e-2, d.max()
+    assert d.mean() < 2e-3, d.mean()
+
+
 def test_render_spp_average_and_background(pkg, orc):
     cam, cfg, net, p16, bf, m = _setup(pkg, orc, 2, 0.0)  # empty grid: every ray misses -> background
     r = pkg.nerf.NerfRenderer()
