@@ -60,6 +60,34 @@ def synthetic_batch(n, seed, device):
     return torch.from_numpy(c).to(device), torch.from_numpy(dL).to(device)
 
 
+# profiler region -> the HIP kernels it launches (substrings of the rocprofv3 kernel names)
+REGION_KERNELS = {
+    "grid_forward": ["k_grid_forward"],
+    "grid_backward": ["k_grid_backward"],
+    "grid_backward_sorted": ["k_sc_scatter", "k_sc_accumulate", "k_sc_split_reduce"],
+    "mlp_train": ["k_nerf_mlp<1,", "k_mlp<1,"],
+    "mlp_infer": ["k_nerf_mlp<0,", "k_mlp<0,"],
+}
+
+
+def pmc_traffic(variant, region):
+    """HBM bytes per launch of `region` from the newest committed rocprofv3 PMC summary
+    (profiles/<round>_pmc_<variant>.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
+    WRITE_SIZE passes of this bench, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM). None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{variant.lower()}.json")))
+    if not files or region not in REGION_KERNELS:
+        return None, None
+    summ = json.load(open(files[-1]))
+    tot, hit = 0.0, False
+    for name, v in summ.items():
+        compact = name.replace(" ", "")
+        if any(k.replace(" ", "") in compact for k in REGION_KERNELS[region]):
+            tot += v["hbm_bytes"]
+            hit = True
+    return (tot if hit else None), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(variant, budget_s=12.0):
     """The oracle (a naive C port of the same encoding + MLP fwd/bwd) timed on the host: 1 thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -218,6 +246,7 @@ def main():
         dom = max((k for k in roof if k in per_kernel), key=lambda k: per_kernel[k])
         bound, work, peak, unit = roof[dom]
         achieved = work / (per_kernel[dom] / 1e3)
+        traffic, traffic_src = pmc_traffic(args.variant, dom)
         kern_summary = {}
         for k, ms in per_kernel.items():
             e = {"avg_ms": round(ms, 4)}
@@ -244,7 +273,12 @@ def main():
             "kernel_timing": ("HIP events per kernel on the launch stream, eager replay of the same K steps queued "
                               "behind a graph launch" if graph is not None else "HIP events per kernel over the timed region"),
             "roofline": {"kernel": dom, "bound": bound, "achieved": round(achieved, 1), "peak": peak, "unit": unit,
-                         "frac": round(achieved / peak, 4), "traffic": None},
+                         "frac": round(achieved / peak, 4),
+                         "traffic": None if traffic is None else round(traffic / 1e6, 2),
+                         "traffic_unit": "MB/launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "algorithmic": round(work * (1e3 if unit == "GB/s" else 1e6), 2),
+                         "algorithmic_unit": "MB/launch" if unit == "GB/s" else "MFLOP/launch"},
             "kernels": kern_summary,
         }
         if world == 1 and not args.no_cpu_baseline and args.variant in ("C2", "C2p"):

@@ -99,6 +99,8 @@ void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, 
 void grid_ema(uint32_t n, float decay, float* grid, const float* grid_tmp, hipStream_t s);
 void grid_mean_bitfield(const float* grid, uint32_t max_cascade, float* mean_out, uint8_t* bitfield, hipStream_t s);
 size_t scan_temp_bytes(uint32_t n);
+size_t sample_tmp_f32(uint32_t n_rays);  // floats of sample_rays' tmp_f32 (stored t per step + ray geometry)
+size_t loss_tmp_f32(uint32_t n_rays);    // floats of compute_loss' tmp_f32 (per-ray pass-1 results)
 
 // ---- rendering (NerfTracer) ------------------------------------------------------------------
 struct RenderArgs {

@@ -10,6 +10,7 @@
 #include <cstring>
 
 #include "nerf.h"
+#include "profiler.h"
 #include "rng.h"
 
 namespace ngp {
@@ -21,9 +22,22 @@ namespace nerf {
 struct V3 { float x, y, z; };
 __device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
 
+// t / MIN_CONE_STEPSIZE, correctly rounded, in three instructions: q = t * RN(1/c) and one residual
+// correction. Checked exhaustively against the IEEE quotient for every float t >= 0
+// (tools/microbench/div_check.c): equal for 1.5e-31 <= t <= 5.7e35; outside that the IEEE divide runs.
+__device__ __forceinline__ float div_min_stepsize(float t) {
+	constexpr float c = MIN_CONE_STEPSIZE;
+	const float r = 1.0f / c;  // folded to RN(1/c) at compile time
+	if (__builtin_expect(t >= 1e-30f && t <= 1e35f, 1)) {
+		const float q = t * r;
+		return __builtin_fmaf(__builtin_fmaf(-q, c, t), r, q);
+	}
+	return t / c;
+}
+
 // testbed_nerf.cu:114-184
 __device__ float to_stepping_space(float t, float cone) {
-	if (cone <= 1e-5f) return t / MIN_CONE_STEPSIZE;
+	if (cone <= 1e-5f) return div_min_stepsize(t);
 	const float log1p_c = logf(1.0f + cone);
 	const float a = (logf(MIN_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
 	const float b = (logf(MAX_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
@@ -54,7 +68,7 @@ __device__ float distance_to_next_voxel(V3 pos, V3 dir, V3 idir, float res) {
 	const float ty = (floorf(p.y + 0.5f + 0.5f * signf_(dir.y)) - p.y) * idir.y;
 	const float tz = (floorf(p.z + 0.5f + 0.5f * signf_(dir.z)) - p.z) * idir.z;
 	const float t = fminf(fminf(tx, ty), tz);
-	return fmaxf(t / res, 0.0f);
+	return fmaxf(t * (1.0f / res), 0.0f);  // res is a power of two: same rounding as t / res, no IEEE divide
 }
 __device__ float advance_to_next_voxel(float t, float cone, V3 pos, V3 dir, V3 idir, uint32_t mip) {
 	const float res = scalbnf((float)GRIDSIZE, -(int)mip);
@@ -288,65 +302,202 @@ __device__ RaySetup setup_ray(const Camera* cams, const uint32_t* pixels, uint32
 // an integer, the frame advance_to_next_voxel / the backward jump use), OR-ed with the sampler's own
 // classification of p (cascaded_grid_idx_at rounds (p - 0.5) * 2^-m + 0.5, which can land in the
 // neighbouring cell within a few ulps of a face): the scan only jumps over cells empty in both.
-__device__ bool scan_occupied(V3 p, const uint8_t* bitfield, uint32_t m) {
-	if (density_grid_occupied_at(p, bitfield, m)) return true;
+// Row-cooperative: lane L probes mip mu + L, so the climb to the coarsest empty mip is one parallel
+// load round trip instead of up to 7 dependent ones; both classifications are loaded unconditionally.
+__device__ __forceinline__ bool scan_occupied_2load(V3 p, const uint8_t* bitfield, uint32_t m) {
+	const uint32_t i0 = cascaded_grid_idx_at(p, m);
 	const float res = scalbnf((float)GRIDSIZE, -(int)m);
 	const int ix = (int)floorf(res * (p.x - 0.5f)) + (int)GRIDSIZE / 2;
 	const int iy = (int)floorf(res * (p.y - 0.5f)) + (int)GRIDSIZE / 2;
 	const int iz = (int)floorf(res * (p.z - 0.5f)) + (int)GRIDSIZE / 2;
-	if (ix < 0 || ix >= (int)GRIDSIZE || iy < 0 || iy >= (int)GRIDSIZE || iz < 0 || iz >= (int)GRIDSIZE) return false;
-	const uint32_t idx = morton3D((uint32_t)ix, (uint32_t)iy, (uint32_t)iz);
-	return bitfield[idx / 8 + GRID_N_CELLS * m / 8] & (1 << (idx % 8));
+	const bool in1 = !(ix < 0 || ix >= (int)GRIDSIZE || iy < 0 || iy >= (int)GRIDSIZE || iz < 0 || iz >= (int)GRIDSIZE);
+	const uint32_t i1 = in1 ? morton3D((uint32_t)ix, (uint32_t)iy, (uint32_t)iz) : 0u;
+	const uint32_t j0 = i0 == 0xFFFFFFFFu ? 0u : i0;
+	const uint8_t b0 = bitfield[j0 / 8 + GRID_N_CELLS * m / 8], b1 = bitfield[i1 / 8 + GRID_N_CELLS * m / 8];
+	return (i0 != 0xFFFFFFFFu && (b0 & (1 << (j0 % 8)))) || (in1 && (b1 & (1 << (i1 % 8))));
 }
 
-__device__ float sampling_end(V3 o, V3 d, V3 idir, float t_start, float cone, const Aabb& box, const uint8_t* bitfield,
-                              uint32_t max_cascade) {
+template <uint32_t G>
+__device__ float sampling_end_row(V3 o, V3 d, V3 idir, float t_start, float cone, const Aabb& box, const uint8_t* bitfield,
+                                  uint32_t max_cascade, uint32_t L) {
+	static_assert(G >= CASCADES, "one lane per mip");
 	float tmin, tmax;
 	aabb_ray_intersect(box, o, d, &tmin, &tmax);
 	if (!(tmax < 3.0e38f)) return t_start;
 	const V3 nd = v3(-d.x, -d.y, -d.z), nidir = v3(-idir.x, -idir.y, -idir.z);
+	const uint32_t shift = __lane_id() & (64u - G);
 	float t = tmax;
 	for (int it = 0; it < 8192; ++it) {
 		if (t <= t_start) return t_start;
 		const V3 p = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
 		const uint32_t mu = mip_from_dt(calc_dt(t, cone), p, max_cascade);
-		if (scan_occupied(p, bitfield, mu)) {
-			// margin: two cells of that mip along the ray past the point found
-			return t + 2.0f * SQRT3 / scalbnf((float)GRIDSIZE, -(int)mu);
-		}
-		uint32_t m = mu;
-		while (m < CASCADES - 1 && !scan_occupied(p, bitfield, m + 1)) ++m;
+		const uint32_t mL = mu + L;
+		const bool probe = mL < CASCADES;
+		const bool occ = probe && scan_occupied_2load(p, bitfield, probe ? mL : 0u);
+		const uint32_t bits = (uint32_t)(__ballot(occ) >> shift) & ((1u << G) - 1u);
+		if (bits & 1u) return t + 2.0f * SQRT3 / scalbnf((float)GRIDSIZE, -(int)mu);
+		const uint32_t m = bits ? mu + __builtin_ctz(bits) - 1u : CASCADES - 1u;
 		const float res = scalbnf((float)GRIDSIZE, -(int)m);
-		// just past the cell's entry face: a couple of ulps, so a ray that only clips the corner of
-		// the next cell still visits it
 		t -= distance_to_next_voxel(p, nd, nidir, res);
 		t -= fmaxf(fabsf(t), 1.0f) * 2.5e-7f;
 	}
-	return 3.402823466e38f;  // give up: march to the exit
+	return 3.402823466e38f;
 }
 
-// generate_training_samples_nerf pass 1: count the occupied steps of each ray.
-__global__ void __launch_bounds__(128) k_sample_count(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
+// ------------------------------------------------------------------------------------------------
+// Ray-parallel marching. The reference marches one ray per thread (testbed_nerf.cu:1432-1480); at
+// ~23 K rays per step that is ~1.4 waves per CU and every step of a long ray waits on one dependent
+// bitfield load. Here a ray owns a lane group (RG = 8 lanes, half a DPP row): the group speculates the next RG states
+// of the reference's sequential march (all occupied: t += calc_dt(t); or all empty:
+// advance_to_next_voxel), tests their occupancy in parallel (one load latency per RG states) and
+// keeps the prefix that the sequential march would take, switching speculation mode at the first
+// lane that disagrees. The t chain itself is evaluated with the reference's float ops in order (every
+// lane of the row evaluates it redundantly), so sample positions stay bit-exact with the sequential
+// algorithm. The count pass stores the t of every occupied step (tbuf, STEPS floats per ray) and the
+// ray geometry, so the write pass is a flat copy instead of a second march.
+// ------------------------------------------------------------------------------------------------
+#ifndef NGP_SAMPLER_RG
+#define NGP_SAMPLER_RG 8
+#endif
+constexpr uint32_t RG = NGP_SAMPLER_RG;  // lanes per ray (16 = one DPP row)
+
+constexpr uint32_t LG = 16;  // lanes per ray in the loss passes: one DPP row
+static_assert(RG >= 8 && RG <= 16 && (RG & (RG - 1)) == 0, "sampler group: 8 or 16 lanes");
+
+__device__ __forceinline__ uint32_t row_ballot(bool p) {  // this ray's RG lanes of a wave ballot
+	const unsigned long long b = __ballot(p);
+	return (uint32_t)(b >> (__lane_id() & (64u - RG))) & ((1u << RG) - 1u);
+}
+__device__ __forceinline__ float dpp_shr1(float v) {  // lane l - 1 of the same DPP row (lane 0 of a row: 0)
+	return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));
+}
+template <int K> __device__ __forceinline__ float row_bcast(float v) {  // v of lane K of this row (row_newbcast)
+	return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + K, 0xF, 0xF, false));
+}
+
+struct RayGeo {  // per ray, count pass -> write pass
+	float o[3], d[3], dn[3];
+	float pad[3];
+};
+
+// The march's state transitions. CONE0: cone_angle <= 1e-5 (every aabb_scale 1 scene), where
+// to/from_stepping_space are t / MIN_CONE_STEPSIZE and back, calc_dt(t) stays within a few ulps of
+// MIN_CONE_STEPSIZE (dt * 2 * GRIDSIZE ~ 0.43 < 1), so mip_from_dt(dt, pos) == mip_from_pos(pos);
+// with max_cascade 0 that is mip 0. Same values as the generic path, fewer instructions per state.
+template <bool CONE0>
+struct Marcher {
+	V3 o, dn, idir;
+	float cone;
+	uint32_t max_cascade;
+	__device__ __forceinline__ V3 pos(float t) const { return v3(o.x + t * dn.x, o.y + t * dn.y, o.z + t * dn.z); }
+	__device__ __forceinline__ float dt_at(float t) const { return calc_dt(t, CONE0 ? 0.0f : cone); }
+	__device__ __forceinline__ uint32_t mip_at(float dt, V3 p) const {
+		if (CONE0) return max_cascade == 0 ? 0u : mip_from_pos(p, max_cascade);
+		return mip_from_dt(dt, p, max_cascade);
+	}
+	__device__ __forceinline__ float step_occupied(float t) const { return t + dt_at(t); }
+	__device__ __forceinline__ float step_empty(float t) const {
+		const V3 p = pos(t);
+		const uint32_t mip = mip_at(CONE0 ? 0.0f : dt_at(t), p);
+		return advance_to_next_voxel(t, CONE0 ? 0.0f : cone, p, dn, idir, mip);
+	}
+};
+
+// generate_training_samples_nerf pass 1: count the occupied steps of each ray, keep their t.
+template <bool CONE0>
+__global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
                                                       uint32_t n_images, const ngp_nerf_config cfg, SampleArgs a,
-                                                      uint32_t* __restrict__ nsteps) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= a.n_rays) return;
+                                                      uint32_t* __restrict__ nsteps, float* __restrict__ tbuf,
+                                                      RayGeo* __restrict__ geo) {
+	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t i = gid / RG, L = gid % RG;
+	if (i >= a.n_rays) return;  // whole rows
 	const RaySetup r = setup_ray(cams, pixels, n_images, cfg, i + a.ray_offset, a.n_rays_total_for_image_idx, a.rng);
 	uint32_t j = 0;
 	if (r.valid) {
 		const Aabb box = cfg_aabb(cfg);
+		const Marcher<CONE0> m{r.o, r.dn, r.idir, r.cone, cfg.max_cascade};
 		float t = r.startt;
-		const float t_end = sampling_end(r.o, r.dn, r.idir, t, r.cone, box, a.bitfield, cfg.max_cascade);
-		V3 pos;
-		while (t <= t_end && aabb_contains(box, pos = v3(r.o.x + t * r.dn.x, r.o.y + t * r.dn.y, r.o.z + t * r.dn.z)) &&
-		       j < STEPS) {
-			const float dt = calc_dt(t, r.cone);
-			const uint32_t mip = mip_from_dt(dt, pos, cfg.max_cascade);
-			if (density_grid_occupied_at(pos, a.bitfield, mip)) { ++j; t += dt; }
-			else t = advance_to_next_voxel(t, r.cone, pos, r.dn, r.idir, mip);
+#if NGP_SAMPLER_DIAG == 2
+		const float t_end = 3.0e38f;
+#else
+		const float t_end = sampling_end_row<RG>(r.o, r.dn, r.idir, t, r.cone, box, a.bitfield, cfg.max_cascade, L);
+#endif
+#if NGP_SAMPLER_DIAG == 1  // timing aid: sampling_end twice (cost of one = difference to the default build)
+		const float t_end2 = sampling_end_row<RG>(r.o, r.dn, r.idir, t + 0.0f * t_end, r.cone, box, a.bitfield, cfg.max_cascade, L);
+		if (t_end2 != t_end) t = t_end2;
+#endif
+		float* tout = tbuf + (size_t)i * STEPS;
+		bool occ_mode = false;  // rays enter the aabb in empty space far more often than not
+		for (;;) {
+			// lanes [0, nvalid) take the next nvalid states of the sequential march, assuming it stays in
+			// the current mode (all occupied / all empty)
+			float tl, last;
+			uint32_t nvalid = RG;
+			if (CONE0 && occ_mode) {
+				// occupied run, cone 0: t_k ~ (t/MIN + k) * MIN. Guess every state from that lattice and
+				// verify all of them at once (lane L redoes the exact step from lane L-1's guess): the
+				// verified prefix is exact; the first lane that fails holds the exact state from its
+				// verified predecessor. A second round re-guesses the remaining lanes from there.
+				const float n0 = div_min_stepsize(t);
+				float cand = L == 0 ? t : (n0 + (float)L) * MIN_CONE_STEPSIZE;
+				float expct = m.step_occupied(dpp_shr1(cand));
+				uint32_t v = __builtin_ctz(row_ballot(L != 0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
+				if (v < RG) {
+					const float tv = __shfl(expct, (int)v, (int)RG);
+					const float nv = div_min_stepsize(tv);
+					cand = L < v ? cand : (L == v ? tv : (nv + (float)(L - v)) * MIN_CONE_STEPSIZE);
+					expct = m.step_occupied(dpp_shr1(cand));
+					v = __builtin_ctz(row_ballot(L > v && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
+					if (v < RG) {
+						if (L == v) cand = expct;
+						nvalid = v + 1;
+					}
+				}
+				tl = cand;
+				last = 0.f;  // taken by shuffle below
+			} else {
+				// chain evaluated in order by every lane of the group; lane L keeps state L
+				float tk = t;
+				tl = t;
+#pragma unroll
+				for (uint32_t k = 1; k < RG; ++k) {
+					tk = occ_mode ? m.step_occupied(tk) : m.step_empty(tk);
+					if (L == k) tl = tk;
+				}
+				last = tk;
+			}
+			const V3 pos = m.pos(tl);
+			const uint32_t mip = m.mip_at(CONE0 ? 0.0f : m.dt_at(tl), pos);
+			const bool inside = L < nvalid && tl <= t_end && aabb_contains(box, pos) && (occ_mode ? j + L : j) < STEPS;
+			const bool occ = inside && density_grid_occupied_at(pos, a.bitfield, mip);
+			const uint32_t cont = row_ballot(inside && occ == occ_mode);
+			const uint32_t f = __builtin_ctz(~cont | (1u << RG));  // first lane the sequential march leaves the mode at
+			if (occ_mode) {
+				if (L < f) tout[j + L] = tl;
+				j += f;
+			}
+			if (f >= nvalid) {  // every state taken stayed in the mode: continue from the last one
+				if (CONE0 && occ_mode) last = __shfl(tl, (int)(nvalid - 1), (int)RG);
+				t = occ_mode ? m.step_occupied(last) : m.step_empty(last);
+				continue;
+			}
+			if (!((row_ballot(inside) >> f) & 1u)) break;  // left the aabb / sampling range / step budget
+			const float tf = __shfl(tl, (int)f, (int)RG);
+			if (occ_mode) t = m.step_empty(tf);  // empty cell at lane f: advance_to_next_voxel
+			else t = tf;                          // occupied cell at lane f: sample it next
+			occ_mode = !occ_mode;
 		}
 	}
-	nsteps[i] = j;
+	if (L == 0) {
+		nsteps[i] = j;
+		RayGeo g;
+		g.o[0] = r.o.x; g.o[1] = r.o.y; g.o[2] = r.o.z;
+		g.d[0] = r.d.x; g.d[1] = r.d.y; g.d[2] = r.d.z;
+		g.dn[0] = r.dn.x; g.dn[1] = r.dn.y; g.dn[2] = r.dn.z;
+		g.pad[0] = r.cone; g.pad[1] = g.pad[2] = 0.f;
+		geo[i] = g;
+	}
 }
 
 __global__ void k_sample_keep(uint32_t n, const uint32_t* __restrict__ nsteps, const uint32_t* __restrict__ base,
@@ -356,44 +507,39 @@ __global__ void k_sample_keep(uint32_t n, const uint32_t* __restrict__ nsteps, c
 	keep[i] = (nsteps[i] > 0 && base[i] + nsteps[i] <= max_samples) ? 1u : 0u;
 }
 
-// pass 2: write the ray records and the NerfCoordinates of kept rays.
-__global__ void __launch_bounds__(128) k_sample_write(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
-                                                      uint32_t n_images, const ngp_nerf_config cfg, SampleArgs a,
-                                                      const uint32_t* __restrict__ nsteps, const uint32_t* __restrict__ base,
-                                                      const uint32_t* __restrict__ keep, const uint32_t* __restrict__ slot) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i == 0) {  // counters: rays kept, total steps of every ray that found samples
+// pass 2: write the ray records and the NerfCoordinates of kept rays from the stored t values.
+__global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg, SampleArgs a, const uint32_t* __restrict__ nsteps,
+                                                      const uint32_t* __restrict__ base, const uint32_t* __restrict__ keep,
+                                                      const uint32_t* __restrict__ slot, const float* __restrict__ tbuf,
+                                                      const RayGeo* __restrict__ geo) {
+	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t i = gid / RG, L = gid % RG;
+	if (gid == 0) {  // counters: rays kept, total steps of every ray that found samples
 		a.counters[0] = slot[a.n_rays - 1] + keep[a.n_rays - 1];
 		a.counters[1] = base[a.n_rays - 1] + nsteps[a.n_rays - 1];
 	}
 	if (i >= a.n_rays || !keep[i]) return;
-	const uint32_t ig = i + a.ray_offset;
-	const RaySetup r = setup_ray(cams, pixels, n_images, cfg, ig, a.n_rays_total_for_image_idx, a.rng);
 	const uint32_t s = slot[i], numsteps = nsteps[i], b = base[i];
-	a.ray_indices[s] = ig;
-	float* ro = a.rays + (size_t)s * 6;
-	ro[0] = r.o.x; ro[1] = r.o.y; ro[2] = r.o.z; ro[3] = r.d.x; ro[4] = r.d.y; ro[5] = r.d.z;
-	a.numsteps[2 * s] = numsteps;
-	a.numsteps[2 * s + 1] = b;
+	const RayGeo g = geo[i];
+	if (L == 0) {
+		a.ray_indices[s] = i + a.ray_offset;
+		float* ro = a.rays + (size_t)s * 6;
+		ro[0] = g.o[0]; ro[1] = g.o[1]; ro[2] = g.o[2]; ro[3] = g.d[0]; ro[4] = g.d[1]; ro[5] = g.d[2];
+		a.numsteps[2 * s] = numsteps;
+		a.numsteps[2 * s + 1] = b;
+	}
 	const Aabb box = cfg_aabb(cfg);
 	const V3 diag = v3(box.mx.x - box.mn.x, box.mx.y - box.mn.y, box.mx.z - box.mn.z);
-	const V3 wdir = v3((r.dn.x + 1.0f) * 0.5f, (r.dn.y + 1.0f) * 0.5f, (r.dn.z + 1.0f) * 0.5f);
-	float t = r.startt;
-	uint32_t j = 0;
-	V3 pos;
-	while (aabb_contains(box, pos = v3(r.o.x + t * r.dn.x, r.o.y + t * r.dn.y, r.o.z + t * r.dn.z)) && j < numsteps) {
-		const float dt = calc_dt(t, r.cone);
-		const uint32_t mip = mip_from_dt(dt, pos, cfg.max_cascade);
-		if (density_grid_occupied_at(pos, a.bitfield, mip)) {
-			float* c = a.coords + (size_t)(b + j) * 7;
-			c[0] = (pos.x - box.mn.x) / diag.x; c[1] = (pos.y - box.mn.y) / diag.y; c[2] = (pos.z - box.mn.z) / diag.z;
-			c[3] = warp_dt(dt);
-			c[4] = wdir.x; c[5] = wdir.y; c[6] = wdir.z;
-			++j;
-			t += dt;
-		} else {
-			t = advance_to_next_voxel(t, r.cone, pos, r.dn, r.idir, mip);
-		}
+	const V3 wdir = v3((g.dn[0] + 1.0f) * 0.5f, (g.dn[1] + 1.0f) * 0.5f, (g.dn[2] + 1.0f) * 0.5f);
+	const float* tin = tbuf + (size_t)i * STEPS;
+	for (uint32_t jj = L; jj < numsteps; jj += RG) {
+		const float t = tin[jj];
+		const V3 pos = v3(g.o[0] + t * g.dn[0], g.o[1] + t * g.dn[1], g.o[2] + t * g.dn[2]);
+		const float dt = calc_dt(t, g.pad[0]);
+		float* c = a.coords + (size_t)(b + jj) * 7;
+		c[0] = (pos.x - box.mn.x) / diag.x; c[1] = (pos.y - box.mn.y) / diag.y; c[2] = (pos.z - box.mn.z) / diag.z;
+		c[3] = warp_dt(dt);
+		c[4] = wdir.x; c[5] = wdir.y; c[6] = wdir.z;
 	}
 }
 
@@ -408,44 +554,67 @@ static void exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* 
 	NGP_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, need, in, out, (int)n, s));
 }
 
+size_t sample_tmp_f32(uint32_t n_rays) { return (size_t)n_rays * (STEPS + sizeof(RayGeo) / 4); }
+
 void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs& a, void* scan_tmp, size_t scan_bytes,
-                 uint32_t* tmp, float*, hipStream_t s) {
+                 uint32_t* tmp, float* tmpf, hipStream_t s) {
 	if (a.n_rays == 0) return;
+	NGP_CHECK(tmpf != nullptr, "sample_rays: float scratch of sample_tmp_f32(n_rays) floats required");
 	uint32_t* nsteps = tmp;
 	uint32_t* base = tmp + a.n_rays;
 	uint32_t* keep = tmp + 2 * (size_t)a.n_rays;
 	uint32_t* slot = tmp + 3 * (size_t)a.n_rays;
-	const uint32_t blocks = div_round_up(a.n_rays, 128);
-	k_sample_count<<<blocks, 128, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps);
-	NGP_HIP(hipGetLastError());
-	exclusive_scan(nsteps, base, a.n_rays, scan_tmp, scan_bytes, s);
-	k_sample_keep<<<div_round_up(a.n_rays, 256), 256, 0, s>>>(a.n_rays, nsteps, base, a.max_samples, keep);
-	exclusive_scan(keep, slot, a.n_rays, scan_tmp, scan_bytes, s);
-	k_sample_write<<<blocks, 128, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, base, keep, slot);
+	float* tbuf = tmpf;
+	RayGeo* geo = (RayGeo*)(tmpf + (size_t)a.n_rays * STEPS);
+	const uint32_t blocks = div_round_up((size_t)a.n_rays * RG, 256);
+	{
+		ProfScope ps("sample_count", s);
+		if (cfg.cone_angle_constant <= 1e-5f)
+			k_sample_count<true><<<blocks, 256, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo);
+		else
+			k_sample_count<false><<<blocks, 256, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo);
+		NGP_HIP(hipGetLastError());
+	}
+	{
+		ProfScope ps("sample_scans", s);
+		exclusive_scan(nsteps, base, a.n_rays, scan_tmp, scan_bytes, s);
+		k_sample_keep<<<div_round_up(a.n_rays, 256), 256, 0, s>>>(a.n_rays, nsteps, base, a.max_samples, keep);
+		exclusive_scan(keep, slot, a.n_rays, scan_tmp, scan_bytes, s);
+	}
+	ProfScope ps("sample_write", s);
+	k_sample_write<<<blocks, 256, 0, s>>>(cfg, a, nsteps, base, keep, slot, tbuf, geo);
 	NGP_HIP(hipGetLastError());
 }
+
 
 // ------------------------------------------------------------------------------------------------
 // compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012), split at its atomicAdd into two passes
 // around a prefix scan. Error map / sharpness / envmap / exposure / depth supervision are off in the
 // reference's default training and not implemented.
+// A ray owns one DPP row: lanes load and activate 16 samples at once (network output, dt, exp), and
+// the compositing recurrence (T *= 1 - alpha, rgb += alpha T c) runs over the row in sample order
+// with row_newbcast broadcasts, i.e. with the reference's float ops in the reference's order.
 // ------------------------------------------------------------------------------------------------
 struct LossRay {  // pass-1 results kept for pass 2
 	float grad[3];
 	float rgb_ray[3];
 	float mean_loss;
+	float pad;
 };
 
 __device__ __forceinline__ V3 unwarp_pos(const float* c, const Aabb& b) {
 	return v3(b.mn.x + c[0] * (b.mx.x - b.mn.x), b.mn.y + c[1] * (b.mx.y - b.mn.y), b.mn.z + c[2] * (b.mx.z - b.mn.z));
 }
 
-__global__ void __launch_bounds__(128) k_loss_pass1(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
+#define NGP_ROW_UNROLL16(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
+
+__global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
                                                     uint32_t n_images, const ngp_nerf_config cfg, LossArgs a,
                                                     uint32_t* __restrict__ craw, LossRay* __restrict__ lr) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t i = gid / LG, L = gid % LG;
 	if (i >= a.n_rays) return;
-	if (i >= *a.ray_counter) { craw[i] = 0; return; }
+	if (i >= *a.ray_counter) { if (L == 0) craw[i] = 0; return; }
 	const uint32_t numsteps = a.numsteps[2 * i], base = a.numsteps[2 * i + 1];
 	const f16* out = a.network_output + (size_t)base * 16;
 	const float* ci = a.coords_in + (size_t)base * 7;
@@ -453,18 +622,36 @@ __global__ void __launch_bounds__(128) k_loss_pass1(const Camera* __restrict__ c
 	const float eps = 1e-4f;
 	float rr = 0.f, rg = 0.f, rb = 0.f;
 	uint32_t cn = 0;
-	for (; cn < numsteps; ++cn) {
-		if (t < eps) break;
-		const f16x4 o = *(const f16x4*)(out + (size_t)cn * 16);
-		const float dt = unwarp_dt(ci[(size_t)cn * 7 + 3]);
-		const float density = network_to_density((float)o[3], cfg.density_activation);
-		const float alpha = 1.f - __expf(-density * dt);
-		const float weight = alpha * t;
-		rr += weight * network_to_rgb((float)o[0], cfg.rgb_activation);
-		rg += weight * network_to_rgb((float)o[1], cfg.rgb_activation);
-		rb += weight * network_to_rgb((float)o[2], cfg.rgb_activation);
-		t *= (1.f - alpha);
+	bool stop = false;
+	for (uint32_t c = 0; c < numsteps && !stop; c += LG) {
+		const uint32_t jj = c + L;
+		float alpha = 0.f, cr = 0.f, cg = 0.f, cb = 0.f;
+		if (jj < numsteps) {
+			const f16x4 o = *(const f16x4*)(out + (size_t)jj * 16);
+			const float dt = unwarp_dt(ci[(size_t)jj * 7 + 3]);
+			const float density = network_to_density((float)o[3], cfg.density_activation);
+			alpha = 1.f - __expf(-density * dt);
+			cr = network_to_rgb((float)o[0], cfg.rgb_activation);
+			cg = network_to_rgb((float)o[1], cfg.rgb_activation);
+			cb = network_to_rgb((float)o[2], cfg.rgb_activation);
+		}
+#define NGP_LOSS1_STEP(K)                                                                              \
+		{                                                                                              \
+			const float ak = row_bcast<K>(alpha), rk = row_bcast<K>(cr), gk = row_bcast<K>(cg), bk = row_bcast<K>(cb); \
+			if (!stop && c + K < numsteps) {                                                           \
+				if (t < eps) stop = true;                                                              \
+				else {                                                                                 \
+					const float weight = ak * t;                                                       \
+					rr += weight * rk; rg += weight * gk; rb += weight * bk;                           \
+					t *= (1.f - ak);                                                                   \
+					++cn;                                                                              \
+				}                                                                                      \
+			}                                                                                          \
+		}
+		NGP_ROW_UNROLL16(NGP_LOSS1_STEP)
+#undef NGP_LOSS1_STEP
 	}
+	if (L != 0) return;
 	// same random stream as the sampler for the same ray
 	const uint32_t ray_idx = a.ray_indices[i];
 	Rng rng = a.rng;
@@ -511,68 +698,94 @@ __global__ void __launch_bounds__(128) k_loss_pass1(const Camera* __restrict__ c
 	q.mean_loss = (l[0] + l[1] + l[2]) / 3.0f;
 	q.grad[0] = g[0]; q.grad[1] = g[1]; q.grad[2] = g[2];
 	q.rgb_ray[0] = rr; q.rgb_ray[1] = rg; q.rgb_ray[2] = rb;
+	q.pad = 0.f;
 	lr[i] = q;
 }
 
-__global__ void __launch_bounds__(128) k_loss_pass2(const ngp_nerf_config cfg, LossArgs a, const uint32_t* __restrict__ craw,
+__global__ void __launch_bounds__(256) k_loss_pass2(const ngp_nerf_config cfg, LossArgs a, const uint32_t* __restrict__ craw,
                                                     const uint32_t* __restrict__ cbase, const LossRay* __restrict__ lr) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i == 0) *a.compacted_counter = cbase[a.n_rays - 1] + craw[a.n_rays - 1];
+	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t i = gid / LG, L = gid % LG;
+	if (gid == 0) *a.compacted_counter = cbase[a.n_rays - 1] + craw[a.n_rays - 1];
 	if (i >= a.n_rays || i >= *a.ray_counter) return;
 	const uint32_t base = a.numsteps[2 * i + 1];
 	const uint32_t compacted_base = cbase[i];
 	const uint32_t mx = a.max_samples_compacted;
 	const uint32_t cn = min(mx - min(mx, compacted_base), craw[i]);
-	a.numsteps[2 * i] = cn;
-	a.numsteps[2 * i + 1] = compacted_base;
+	if (L == 0) {  // every lane of the row has read numsteps[2i + 1] above (one wave instruction)
+		a.numsteps[2 * i] = cn;
+		a.numsteps[2 * i + 1] = compacted_base;
+	}
 	if (cn == 0) return;
 	const LossRay q = lr[i];
-	if (a.loss) a.loss[i] = q.mean_loss / (float)a.n_rays;  // written after the compaction early-out (:1836-1866)
+	if (L == 0 && a.loss) a.loss[i] = q.mean_loss / (float)a.n_rays;  // written after the compaction early-out (:1836-1866)
 	const float loss_scale = a.loss_scale / (float)a.n_rays;
 	const float output_l2_reg = cfg.rgb_activation == ACT_EXP ? 1e-4f : 0.0f;
 	const float output_l1_reg_density = *a.mean_density < MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
 	const Aabb box = cfg_aabb(cfg);
 	const float* ray = a.rays + (size_t)i * 6;
+	const float ro0 = ray[0], ro1 = ray[1], ro2 = ray[2];
 	const f16* out = a.network_output + (size_t)base * 16;
 	const float* ci = a.coords_in + (size_t)base * 7;
 	float* co = a.coords_out + (size_t)compacted_base * 7;
 	f16* dl = a.dloss_doutput + (size_t)compacted_base * 16;
 	float r2[3] = {0.f, 0.f, 0.f};
 	float t = 1.0f;
-	for (uint32_t j = 0; j < cn; ++j) {
-		const float* c = ci + (size_t)j * 7;
+	for (uint32_t c0 = 0; c0 < cn; c0 += LG) {
+		const uint32_t jj = c0 + L;
+		const bool valid = jj < cn;
+		float cc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+		f16x4 o = {(f16)0.f, (f16)0.f, (f16)0.f, (f16)0.f};
+		float rgb[3] = {0.f, 0.f, 0.f}, alpha = 0.f, dt = 0.f;
+		if (valid) {
 #pragma unroll
-		for (int k = 0; k < 7; ++k) co[(size_t)j * 7 + k] = c[k];
-		const V3 pos = unwarp_pos(c, box);
-		const float ddx = pos.x - ray[0], ddy = pos.y - ray[1], ddz = pos.z - ray[2];
+			for (int k = 0; k < 7; ++k) cc[k] = ci[(size_t)jj * 7 + k];
+			o = *(const f16x4*)(out + (size_t)jj * 16);
+			for (int k = 0; k < 3; ++k) rgb[k] = network_to_rgb((float)o[k], cfg.rgb_activation);
+			dt = unwarp_dt(cc[3]);
+			const float density = network_to_density((float)o[3], cfg.density_activation);
+			alpha = 1.f - __expf(-density * dt);
+		}
+		// compositing in sample order; lane K keeps its weight, transmittance after it and rgb prefix
+		float my_w = 0.f, my_t = 0.f, my_r2[3] = {0.f, 0.f, 0.f};
+#define NGP_LOSS2_STEP(K)                                                                              \
+		{                                                                                              \
+			const float ak = row_bcast<K>(alpha), rk = row_bcast<K>(rgb[0]), gk = row_bcast<K>(rgb[1]), bk = row_bcast<K>(rgb[2]); \
+			if (c0 + K < cn) {                                                                         \
+				const float weight = ak * t;                                                           \
+				r2[0] += weight * rk; r2[1] += weight * gk; r2[2] += weight * bk;                      \
+				t *= (1.0f - ak);                                                                      \
+				if (L == K) { my_w = weight; my_t = t; my_r2[0] = r2[0]; my_r2[1] = r2[1]; my_r2[2] = r2[2]; } \
+			}                                                                                          \
+		}
+		NGP_ROW_UNROLL16(NGP_LOSS2_STEP)
+#undef NGP_LOSS2_STEP
+		if (!valid) continue;
+#pragma unroll
+		for (int k = 0; k < 7; ++k) co[(size_t)jj * 7 + k] = cc[k];
+		const V3 pos = unwarp_pos(cc, box);
+		const float ddx = pos.x - ro0, ddy = pos.y - ro1, ddz = pos.z - ro2;
 		const float depth = sqrtf(ddx * ddx + ddy * ddy + ddz * ddz);
-		const float dt = unwarp_dt(c[3]);
-		const f16x4 o = *(const f16x4*)(out + (size_t)j * 16);
-		float rgb[3];
-		for (int k = 0; k < 3; ++k) rgb[k] = network_to_rgb((float)o[k], cfg.rgb_activation);
-		const float density = network_to_density((float)o[3], cfg.density_activation);
-		const float alpha = 1.f - __expf(-density * dt);
-		const float weight = alpha * t;
-		for (int k = 0; k < 3; ++k) r2[k] += weight * rgb[k];
-		t *= (1.0f - alpha);
 		float suffix[3];
-		for (int k = 0; k < 3; ++k) suffix[k] = q.rgb_ray[k] - r2[k];
+		for (int k = 0; k < 3; ++k) suffix[k] = q.rgb_ray[k] - my_r2[k];
 		f16x4 g;
 		for (int k = 0; k < 3; ++k) {
-			const float dloss_by_drgb = weight * q.grad[k];
+			const float dloss_by_drgb = my_w * q.grad[k];
 			g[k] = (f16)(loss_scale * (dloss_by_drgb * network_to_rgb_derivative((float)o[k], cfg.rgb_activation) +
 			                           fmaxf(0.0f, output_l2_reg * (float)o[k])));
 		}
 		const float density_derivative = network_to_density_derivative((float)o[3], cfg.density_activation);
-		const float dotv = q.grad[0] * (t * rgb[0] - suffix[0]) + q.grad[1] * (t * rgb[1] - suffix[1]) +
-		                   q.grad[2] * (t * rgb[2] - suffix[2]);
+		const float dotv = q.grad[0] * (my_t * rgb[0] - suffix[0]) + q.grad[1] * (my_t * rgb[1] - suffix[1]) +
+		                   q.grad[2] * (my_t * rgb[2] - suffix[2]);
 		const float dloss_by_dmlp = density_derivative * (dt * (dotv + 0.0f));
 		const float o3 = (float)o[3];
 		g[3] = (f16)(loss_scale * dloss_by_dmlp + (o3 < 0.0f ? -output_l1_reg_density : 0.0f) +
 		             (o3 > -10.0f && depth < cfg.near_distance ? 1e-4f : 0.0f));
-		*(f16x4*)(dl + (size_t)j * 16) = g;
+		*(f16x4*)(dl + (size_t)jj * 16) = g;
 	}
 }
+
+size_t loss_tmp_f32(uint32_t n_rays) { return (size_t)n_rays * (sizeof(LossRay) / 4); }
 
 void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs& a, void* scan_tmp, size_t scan_bytes,
                   uint32_t* tmp, float* tmpf, hipStream_t s) {
@@ -580,13 +793,21 @@ void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs&
 	uint32_t* craw = tmp;
 	uint32_t* cbase = tmp + a.n_rays;
 	LossRay* lr = (LossRay*)tmpf;
-	const uint32_t blocks = div_round_up(a.n_rays, 128);
-	k_loss_pass1<<<blocks, 128, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, craw, lr);
-	NGP_HIP(hipGetLastError());
-	exclusive_scan(craw, cbase, a.n_rays, scan_tmp, scan_bytes, s);
-	k_loss_pass2<<<blocks, 128, 0, s>>>(cfg, a, craw, cbase, lr);
+	const uint32_t blocks = div_round_up((size_t)a.n_rays * LG, 256);
+	{
+		ProfScope ps("loss_pass1", s);
+		k_loss_pass1<<<blocks, 256, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, craw, lr);
+		NGP_HIP(hipGetLastError());
+	}
+	{
+		ProfScope ps("loss_scan", s);
+		exclusive_scan(craw, cbase, a.n_rays, scan_tmp, scan_bytes, s);
+	}
+	ProfScope ps("loss_pass2", s);
+	k_loss_pass2<<<blocks, 256, 0, s>>>(cfg, a, craw, cbase, lr);
 	NGP_HIP(hipGetLastError());
 }
+
 
 // ------------------------------------------------------------------------------------------------
 // tcnn fill_rollover / fill_rollover_and_rescale

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "nerf.h"
+#include "profiler.h"
 
 using namespace ngp;
 using namespace ngp::nerf;
@@ -245,10 +246,11 @@ int ngp_nerf_generate_training_samples(const ngp_nerf_dataset* ds, const ngp_ner
 		a.n_rays = n_rays; a.ray_offset = ray_offset; a.n_rays_total_for_image_idx = n_rays_total ? n_rays_total : n_rays;
 		a.max_samples = max_samples; a.rng = Rng{rng.state, rng.inc}; a.bitfield = bitfield;
 		a.ray_indices = ray_indices; a.rays = rays; a.numsteps = numsteps; a.coords = coords; a.counters = counters;
-		static thread_local Buf scan, tmp;
+		static thread_local Buf scan, tmp, tmpf;
 		const size_t sb = scan_temp_bytes(n_rays);
 		if (n_rays == 0) { NGP_HIP(hipMemsetAsync(counters, 0, 8, S(stream))); return NGP_OK; }
-		sample_rays(ds->ds, *cfg, a, scan.get<char>(sb), sb, tmp.get<uint32_t>(4 * (size_t)n_rays), nullptr, S(stream));
+		sample_rays(ds->ds, *cfg, a, scan.get<char>(sb), sb, tmp.get<uint32_t>(4 * (size_t)n_rays),
+		            tmpf.get<float>(sample_tmp_f32(n_rays)), S(stream));
 	});
 }
 
@@ -270,7 +272,7 @@ int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg
 		if (n_rays == 0) { NGP_HIP(hipMemsetAsync(compacted_counter, 0, 4, S(stream))); return NGP_OK; }
 		static thread_local Buf scan, tmp, tmpf;
 		const size_t sb = scan_temp_bytes(n_rays);
-		compute_loss(ds->ds, *cfg, a, scan.get<char>(sb), sb, tmp.get<uint32_t>(2 * (size_t)n_rays), tmpf.get<float>(6 * (size_t)n_rays),
+		compute_loss(ds->ds, *cfg, a, scan.get<char>(sb), sb, tmp.get<uint32_t>(2 * (size_t)n_rays), tmpf.get<float>(loss_tmp_f32(n_rays)),
 		             S(stream));
 	});
 }
@@ -447,6 +449,7 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		// training_prep_nerf
 		const uint32_t skip = std::min(std::max(t->training_step / 16u, 1u), 16u);
 		if (t->training_step % skip == 0) {
+			ProfScope ps("nerf_density_grid", s);
 			const uint32_t nc = cfg.max_cascade + 1;
 			if (t->training_step < 256) update_density_grid(t, s, 0.95f, GRID_N_CELLS * nc, 0);
 			else update_density_grid(t, s, 0.95f, GRID_N_CELLS / 4 * nc, GRID_N_CELLS / 4 * nc);
@@ -479,14 +482,25 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		ngp_rng rng{t->rng.state, t->rng.inc};
 		// global ray ids (rng.advance(i * 16), image_idx(i, R)) so the shards draw the 1-GPU rays;
 		// dL/doutput is scaled by 128 / R (global), so the summed gradient is the 1-GPU gradient
+		{
+		ProfScope ps("nerf_sample", s);
 		check_rc(ngp_nerf_generate_training_samples(t->data, &cfg, s, Rl, r_lo, R, rng, max_inference, (const uint8_t*)t->bitfield.p,
 		                                            ray_indices, rays, numsteps, coords, ctr));
+		}
+		{
+		ProfScope ps("nerf_inference", s);
 		check_rc(ngp_inference(t->model, s, max_inference, coords, 7, mlp_out, 16, NGP_LAYOUT_AOS, 0));
+		}
 		const float loss_scale_local = 128.0f * (float)Rl / (float)R;
+		{
+		ProfScope ps("nerf_loss", s);
 		check_rc(ngp_nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, ray_indices, rays, numsteps, coords, coords_c,
 		                               dloss, loss, ctr + 2, (const float*)t->mean.p, W > 1 ? loss_scale_local : 128.0f));
 		fill_rollover_f16(Bl, 16, ctr + 2, dloss, true, s);
 		fill_rollover_f32(Bl, 7, ctr + 2, coords_c, s);
+		}
+		{
+		ProfScope ps("nerf_train_pass", s);
 		check_rc(ngp_forward_backward(t->model, s, Bl, coords_c, 7, nullptr, 0, dloss, 16, NGP_GRAD_OVERWRITE));
 		t->rng.advance();  // m_rng.advance() (testbed_nerf.cu:4127)
 		if (W > 1) {
@@ -495,6 +509,7 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			          "data parallel: gradient all-reduce failed");
 		}
 		check_rc(ngp_trainer_optimizer_step(t->trainer, s, 128.0f));
+		}
 		++t->training_step;
 		// NerfCounters::update_after_training (testbed_nerf.cu:3583-3609): host sync
 		uint32_t h[4];

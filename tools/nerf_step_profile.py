@@ -1,0 +1,72 @@
+"""Per-phase timing of the full Testbed NeRF training step (training_prep_nerf + train_nerf_step).
+
+Trains --steps steps on the procedural Lego stand-in, then records --measure more steps with the
+engine's HIP-event profiler (events on the launch stream) and prints one JSON object: wall ms per
+step, mean rays / pre-compaction samples / compacted samples per step, and each phase's mean ms per
+call and per step (nerf_density_grid runs every clamp(step/16, 1, 16) steps)."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--measure", type=int, default=200)
+    ap.add_argument("--images", type=int, default=100)
+    ap.add_argument("--res", type=int, default=800)
+    args = ap.parse_args()
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    S = pkg.synthetic
+    ds = S.lego_like_dataset(n_images=args.images, width=args.res, height=args.res, seed=0, device="cuda")
+    cfg = pkg.nerf.default_config(1.0)
+    ncfg = pkg.nerf_config("C2")
+    net = pkg.create_nerf_network(ncfg)
+    tr = pkg.Trainer(net, ncfg["optimizer"])
+    run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
+    lib = pkg.lib()
+    t0 = time.time()
+    for i in range(args.steps):
+        run.train_step(get_loss=False)
+        if i % 500 == 0:
+            print(f"step {i} {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    torch.cuda.synchronize()
+    t_warm = time.time() - t0
+    lib.ngp_profiler_reset()
+    lib.ngp_profiler_enable(1)
+    rays, pre, comp = [], [], []
+    t0 = time.time()
+    for _ in range(args.measure):
+        st = run.train_step(get_loss=False)
+        rays.append(st["rays_per_batch"])
+        pre.append(st["measured_batch_size_before_compaction"])
+        comp.append(st["measured_batch_size"])
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    lib.ngp_profiler_enable(0)
+    need = lib.ngp_profiler_read(None, 0)
+    buf = ctypes.create_string_buffer(need)
+    lib.ngp_profiler_read(buf, need)
+    k = json.loads(buf.value.decode())
+    phases = {n: {"calls": v["calls"], "ms_per_call": round(v["ms"] / max(v["calls"], 1), 4),
+                  "ms_per_step": round(v["ms"] / args.measure, 4)} for n, v in sorted(k.items())}
+    print(json.dumps({
+        "warm_steps": args.steps, "warm_seconds": round(t_warm, 2), "measured_steps": args.measure,
+        "ms_per_step_wall": round(1e3 * dt / args.measure, 4),
+        "rays_per_batch": float(np.mean(rays)), "samples_before_compaction": float(np.mean(pre)),
+        "compacted_samples": float(np.mean(comp)),
+        "samples_per_s": float(np.sum(comp) / dt), "phases": phases}, indent=1), flush=True)
+
+
+if __name__ == "__main__":
+    main()
