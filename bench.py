@@ -145,11 +145,18 @@ def main():
         net.reserve(n)
         x, dL = synthetic_batch(n, 1337 + rank, "cuda")
         grads = trainer.gradients
+        comm = None
+        if world > 1:
+            # the engine's own RCCL communicator: the gradient all-reduce is enqueued by the engine on
+            # its stream, between the backward and the optimizer, and captured into the step's graph
+            comm = pkg.dp.EngineComm(rank, world)
+            trainer.set_allreduce(comm)
 
         def step():
             net.forward_backward(x, dL)
-            div = pkg.dp.allreduce_gradients(grads, world)  # RCCL over xGMI; 1/N folded into the loss scale
-            trainer.optimizer_step(loss_scale * div)
+            if comm is not None:
+                comm.allreduce(grads)  # RCCL over xGMI; 1/N folded into the loss scale
+            trainer.optimizer_step(loss_scale * world)
         graphable = True
     elif args.variant == "C5":
         cfg = json.loads(json.dumps(pkg.SDF_BASE))
@@ -184,7 +191,8 @@ def main():
 
     lib = pkg.lib()
     stream = torch.cuda.Stream()
-    use_graph = bool(args.graph) and world == 1 and graphable
+    use_graph = bool(args.graph) and graphable
+    graph_note = None
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
             step()
@@ -192,10 +200,14 @@ def main():
         graph = None
         if use_graph:
             # the K timed steps as one HIP graph launch (forward_backward + optimizer per step)
-            graph = trainer.capture_training_step(x, dL, loss_scale, n_steps=args.steps)
-            graph.launch()  # untimed replay: graph upload / first-launch costs
-            torch.cuda.synchronize()
-        else:
+            try:
+                graph = trainer.capture_training_step(x, dL, loss_scale, n_steps=args.steps)
+                graph.launch()  # untimed replay: graph upload / first-launch costs
+                torch.cuda.synchronize()
+            except Exception as e:  # same HIP kernels, launched one by one
+                graph, graph_note = None, f"graph capture failed ({e}); eager launches"
+                print(f"[bench] {graph_note}", file=sys.stderr, flush=True)
+        if graph is None:
             lib.ngp_profiler_reset()
             lib.ngp_profiler_enable(1)
         if world > 1:
@@ -269,7 +281,8 @@ def main():
             "data": "synthetic (U[0,1)^3 positions, uniform S^2 directions, U(+-1e-2) dL/dout; random-init weights)",
             "config": {"workload": WORKLOADS[args.variant],
                        "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
-                       "launch": "hip_graph" if graph is not None else "eager"},
+                       "launch": "hip_graph" if graph is not None else (graph_note or "eager"),
+                       "exchange": "engine RCCL all-reduce of the fp16 gradient buffer per step" if world > 1 else None},
             "kernel_timing": ("HIP events per kernel on the launch stream, eager replay of the same K steps queued "
                               "behind a graph launch" if graph is not None else "HIP events per kernel over the timed region"),
             "roofline": {"kernel": dom, "bound": bound, "achieved": round(achieved, 1), "peak": peak, "unit": unit,

@@ -315,6 +315,22 @@ enum { NGP_REDUCE_SUM = 0, NGP_REDUCE_MAX = 1 };
 typedef int (*ngp_allreduce_fn)(void* user, void* device_buf, uint64_t count, int dtype, int op, void* stream);
 int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn allreduce, void* user);
 
+/* The engine's own RCCL communicator (engine extension; SURVEY §8e exchange step). Rank 0 makes the
+ * id, every rank passes the same bytes (any host channel) to ngp_dp_comm_create, which blocks until
+ * all `world` ranks have joined; call it with the rank's HIP device current. ngp_dp_comm_allreduce
+ * is an ngp_allreduce_fn (user = the communicator): ncclAllReduce in place on `stream`, graph-capturable. */
+#define NGP_DP_UNIQUE_ID_BYTES 128
+typedef struct ngp_dp_comm ngp_dp_comm;
+int ngp_dp_comm_unique_id(uint8_t* id_out);
+int ngp_dp_comm_create(uint32_t rank, uint32_t world, const uint8_t* id_in, ngp_dp_comm** out);
+void ngp_dp_comm_destroy(ngp_dp_comm* c);
+int ngp_dp_comm_allreduce(void* user, void* device_buf, uint64_t count, int dtype, int op, void* stream);
+/* Gradient exchange inside the trainer's step (network-level data parallelism, bench.py --gpus N):
+ * after every forward_backward captured by ngp_trainer_capture_training_step, and before the
+ * optimizer, the fp16 gradient buffer is all-reduced (sum) with `allreduce`; the optimizer divides
+ * by `world` (mean gradient) on top of its loss scale. allreduce = NULL turns it off. */
+int ngp_trainer_set_allreduce(ngp_trainer* t, uint32_t world, ngp_allreduce_fn allreduce, void* user);
+
 #pragma GCC visibility pop
 #ifdef __cplusplus
 }

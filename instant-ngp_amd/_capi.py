@@ -147,6 +147,11 @@ SIGNATURES = {
     "ngp_nerf_train_step": (i32, [P, P, i32, C.POINTER(NerfStats)]),
     "ngp_nerf_trainer_buffers": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
     "ngp_nerf_trainer_set_data_parallel": (i32, [P, u32, u32, P, P]),
+    "ngp_dp_comm_unique_id": (i32, [P]),
+    "ngp_dp_comm_create": (i32, [u32, u32, P, C.POINTER(P)]),
+    "ngp_dp_comm_destroy": (None, [P]),
+    "ngp_dp_comm_allreduce": (i32, [P, P, u64, i32, i32, P]),
+    "ngp_trainer_set_allreduce": (i32, [P, u32, P, P]),
     "ngp_nerf_renderer_create": (i32, [C.POINTER(P)]),
     "ngp_nerf_renderer_destroy": (None, [P]),
     "ngp_nerf_render": (i32, [P, P, C.POINTER(NerfConfig), P, C.POINTER(NerfImage), P, u32, u32, f32, P, i32, P]),

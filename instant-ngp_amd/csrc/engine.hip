@@ -394,6 +394,9 @@ struct ngp_trainer {
 	f16 *w16 = nullptr, *inf16 = nullptr, *g16 = nullptr;
 	uint32_t* steps = nullptr;
 	uint32_t* ctl = nullptr;  // device {optimizer step, block counter}; `step` mirrors ctl[0] on the host
+	ngp_allreduce_fn allreduce = nullptr;  // gradient exchange inside captured steps (ngp_trainer_set_allreduce)
+	void* allreduce_user = nullptr;
+	uint32_t world = 1;
 	~ngp_trainer() { if (arena) (void)hipFree(arena); }
 	void sync_device_step() { NGP_HIP(hipMemcpy(ctl, &step, sizeof(uint32_t), hipMemcpyHostToDevice)); }
 	// One optimizer step on stream s. step_base/step_add: see AdamState (optimizer.h).
@@ -823,9 +826,14 @@ int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, 
 		int rc = NGP_OK;
 		for (uint32_t k = 0; k < n_steps && rc == NGP_OK; ++k) {
 			rc = ngp_forward_backward(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE);
+			if (rc == NGP_OK && t->allreduce) {
+				rc = t->allreduce(t->allreduce_user, t->g16, t->n, NGP_DTYPE_F16, NGP_REDUCE_SUM, stream);
+				if (rc != NGP_OK && g_last_error.empty()) g_last_error = "gradient all-reduce failed";
+			}
 			if (rc == NGP_OK && with_optimizer) {
 				try {
-					t->run_step(s, loss_scale, t->ctl, k);  // step = device base (set per launch) + k
+					// the summed gradient of `world` ranks: mean via the loss scale
+					t->run_step(s, loss_scale * (float)t->world, t->ctl, k);  // step = device base (set per launch) + k
 				} catch (const std::exception& e) {
 					g_last_error = e.what();
 					rc = NGP_ERROR;
@@ -842,6 +850,15 @@ int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, 
 		g->graph = graph;
 		NGP_HIP(hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0));
 		*out = g.release();
+	});
+}
+
+int ngp_trainer_set_allreduce(ngp_trainer* t, uint32_t world, ngp_allreduce_fn allreduce, void* user) {
+	NGP_ARG(t && world >= 1);
+	NGP_TRY({
+		t->allreduce = allreduce;
+		t->allreduce_user = user;
+		t->world = allreduce ? world : 1;
 	});
 }
 

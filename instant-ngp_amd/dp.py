@@ -57,6 +57,45 @@ def allreduce_counters(values, world):
     return t.cpu().tolist()
 
 
+class EngineComm:
+    """The engine's own RCCL communicator (ngp_dp_comm_*): rank 0 makes the unique id, torch.distributed
+    broadcasts it, every rank joins. `fn`/`user` plug into the engine's exchange hooks
+    (ngp_trainer_set_allreduce, ngp_nerf_trainer_set_data_parallel), so the all-reduce is issued by the
+    engine on its own stream — inside a captured HIP graph if the step is captured."""
+
+    def __init__(self, rank, world, group=None):
+        from ._capi import check, lib
+        idb = (C.c_uint8 * 128)()
+        if rank == 0:
+            check(lib().ngp_dp_comm_unique_id(idb))
+        t = torch.tensor(list(idb), dtype=torch.uint8)
+        if dist.get_backend(group) == "nccl":
+            t = t.cuda()
+        dist.broadcast(t, src=0, group=group)
+        idb = (C.c_uint8 * 128)(*t.cpu().tolist())
+        h = C.c_void_p()
+        check(lib().ngp_dp_comm_create(rank, world, idb, C.byref(h)))
+        self.handle, self.rank, self.world = h, rank, world
+        self.fn = C.cast(lib().ngp_dp_comm_allreduce, C.c_void_p)
+
+    def allreduce(self, tensor, op="sum", stream=None):
+        from ._capi import check, lib
+        dt = {torch.float32: 0, torch.float16: 1}[tensor.dtype]
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        check(lib().ngp_dp_comm_allreduce(self.handle, C.c_void_p(tensor.data_ptr()), tensor.numel(), dt,
+                                          0 if op == "sum" else 1, C.c_void_p(s)))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            try:
+                from ._capi import lib
+                lib().ngp_dp_comm_destroy(h)
+            except Exception:
+                pass
+            self.handle = None
+
+
 def make_allreduce_callback(group=None):
     """The engine's exchange hook (ngp_nerf_trainer_set_data_parallel) over torch.distributed.
 

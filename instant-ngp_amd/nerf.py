@@ -212,13 +212,22 @@ class NerfTraining:
 
     def set_data_parallel(self, rank, world, group=None):
         """Shard the rays (global ids kept), the compacted batch and the density-grid evaluation over
-        `world` ranks; gradients, density-grid maxima and counters are all-reduced through
-        torch.distributed (dp.make_allreduce_callback)."""
-        from .dp import make_allreduce_callback
-        self._allreduce = make_allreduce_callback(group) if world > 1 else None
-        check(lib().ngp_nerf_trainer_set_data_parallel(self.handle, rank, world,
-                                                       C.cast(self._allreduce, C.c_void_p) if self._allreduce else None,
-                                                       None))
+        `world` ranks; gradients, density-grid maxima and counters are all-reduced by the engine's RCCL
+        communicator (nccl backend) or through torch.distributed (gloo: dp.make_allreduce_callback)."""
+        import torch.distributed as dist
+        from .dp import EngineComm, make_allreduce_callback
+        self._allreduce = None
+        if world > 1 and dist.get_backend(group) == "nccl":
+            # one GPU per rank: the engine's RCCL communicator, enqueued on the training stream
+            self._allreduce = EngineComm(rank, world, group)
+            fn, user = self._allreduce.fn, self._allreduce.handle
+        elif world > 1:
+            # gloo (CPU tests, ranks sharing a GPU): host round trip through torch.distributed
+            self._allreduce = make_allreduce_callback(group)
+            fn, user = C.cast(self._allreduce, C.c_void_p), None
+        else:
+            fn, user = None, None
+        check(lib().ngp_nerf_trainer_set_data_parallel(self.handle, rank, world, fn, user))
 
     def train_step(self, get_loss=True, stream=None):
         st = NerfStats()

@@ -275,6 +275,15 @@ class Trainer:
     def deserialize(self, blob):
         check(lib().ngp_trainer_deserialize(self.handle, blob, len(blob)))
 
+    def set_allreduce(self, comm):
+        """Engine extension: all-reduce (sum) the gradient buffer with `comm` (dp.EngineComm) inside every
+        captured training step, before the optimizer, which then uses the mean gradient. None: off."""
+        if comm is None:
+            check(lib().ngp_trainer_set_allreduce(self.handle, 1, None, None))
+        else:
+            check(lib().ngp_trainer_set_allreduce(self.handle, comm.world, comm.fn, comm.handle))
+        self._comm = comm
+
     def capture_training_step(self, x, dL_doutput, loss_scale=128.0, n_steps=1, with_optimizer=True, stream=None):
         """Engine extension: n_steps of forward_backward(x, dL_doutput) [+ optimizer_step] captured into
         one HIP graph (TrainingGraph.launch replays it). `stream` must not be the null stream."""

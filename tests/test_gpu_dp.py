@@ -65,3 +65,57 @@ def test_nerf_data_parallel_two_ranks(tmp_path):
     l_0 = np.mean([e["loss"] for e in r0[:5]])
     assert l_dp < 0.7 * l_0
     assert l_dp < 1.5 * l_1, (l_dp, l_1)
+
+
+def _engine_comm_run(_rank, port, out_dir):
+    """One rank over the nccl backend (RCCL): the engine's communicator all-reduces the gradient buffer
+    inside a captured 3-step training graph; a world of one must leave training bitwise unchanged."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": "0", "WORLD_SIZE": "1"})
+    import torch.distributed as dist
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    cfg = pkg.nerf_config("C2")
+    cfg["encoding"]["log2_hashmap_size"] = 15
+    g = np.random.default_rng(5)
+    n = 4096
+    x = np.zeros((n, 7), np.float32)
+    x[:, :3] = g.random((n, 3))
+    x[:, 4:] = g.random((n, 3))
+    dL = np.zeros((n, 16), np.float16)
+    dL[:, :4] = g.uniform(-1e-2, 1e-2, (n, 4))
+    x, dL = torch.from_numpy(x).cuda(), torch.from_numpy(dL).cuda()
+    comm = pkg.dp.EngineComm(0, 1)
+    s = torch.cuda.Stream()
+    hashes = []
+    for use_comm in (False, True):
+        net = pkg.create_nerf_network(cfg)
+        tr = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+        net.reserve(n)
+        if use_comm:
+            tr.set_allreduce(comm)
+        with torch.cuda.stream(s):
+            graph = tr.capture_training_step(x, dL, 128.0, n_steps=3)
+            graph.launch()
+            graph.launch()
+            # eager exchange on the same stream through the same communicator
+            net.forward_backward(x, dL)
+            if use_comm:
+                comm.allreduce(tr.gradients)
+            tr.optimizer_step(128.0)
+        torch.cuda.synchronize()
+        hashes.append(hashlib.sha1(tr.params.cpu().numpy().tobytes()).hexdigest())
+    del comm
+    dist.destroy_process_group()
+    with open(os.path.join(out_dir, "comm.json"), "w") as f:
+        json.dump(hashes, f)
+
+
+def test_engine_rccl_allreduce_in_captured_step(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+    mp.spawn(_engine_comm_run, args=(29400 + os.getpid() % 1000, str(tmp_path)), nprocs=1, join=True)
+    a, b = json.load(open(tmp_path / "comm.json"))
+    assert a == b
