@@ -315,6 +315,21 @@ enum { NGP_REDUCE_SUM = 0, NGP_REDUCE_MAX = 1 };
 typedef int (*ngp_allreduce_fn)(void* user, void* device_buf, uint64_t count, int dtype, int op, void* stream);
 int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn allreduce, void* user);
 
+/* Snapshots (Testbed::save_snapshot / load_snapshot, src/testbed.cu:4873-5057; python_api.cu:446-447):
+ * msgpack of the network config (network_config_json, the Testbed's m_network_config; NULL = {}) with
+ * a "snapshot" member holding tcnn Trainer::serialize (n_params, params_type "__half", params_binary),
+ * [optimizer state], version 1, mode "nerf", density_grid_size, density_grid_binary (fp16), nerf.aabb_scale,
+ * nerf.rgb counters, training_step, loss, aabb. Paths ending in .ingp are gzip streams (zstr; level 0
+ * unless compress), others raw msgpack; loading accepts gzip, zlib or raw. Loading restores the params
+ * (and the optimizer state if present), the density grid (mean and bitfield recomputed), the
+ * rays-per-batch counters and the training step; the network must have the snapshot's n_params. */
+int ngp_nerf_save_snapshot(ngp_nerf_trainer* t, void* stream, const char* path, const char* network_config_json,
+                           int include_optimizer_state, int compress);
+int ngp_nerf_load_snapshot(ngp_nerf_trainer* t, void* stream, const char* path);
+/* Testbed::load_network_config (testbed.cu:246) of a snapshot: the config as JSON text without the
+ * "snapshot" member (binaries as {"binary_bytes": n}); size query with json_buf = NULL. */
+int ngp_snapshot_network_config(const char* path, char* json_buf, uint64_t* size);
+
 /* The engine's own RCCL communicator (engine extension; SURVEY §8e exchange step). Rank 0 makes the
  * id, every rank passes the same bytes (any host channel) to ngp_dp_comm_create, which blocks until
  * all `world` ranks have joined; call it with the rank's HIP device current. ngp_dp_comm_allreduce

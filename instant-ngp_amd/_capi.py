@@ -147,6 +147,9 @@ SIGNATURES = {
     "ngp_nerf_train_step": (i32, [P, P, i32, C.POINTER(NerfStats)]),
     "ngp_nerf_trainer_buffers": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
     "ngp_nerf_trainer_set_data_parallel": (i32, [P, u32, u32, P, P]),
+    "ngp_nerf_save_snapshot": (i32, [P, P, C.c_char_p, C.c_char_p, i32, i32]),
+    "ngp_nerf_load_snapshot": (i32, [P, P, C.c_char_p]),
+    "ngp_snapshot_network_config": (i32, [C.c_char_p, C.c_char_p, C.POINTER(u64)]),
     "ngp_dp_comm_unique_id": (i32, [P]),
     "ngp_dp_comm_create": (i32, [u32, u32, P, C.POINTER(P)]),
     "ngp_dp_comm_destroy": (None, [P]),

@@ -11,6 +11,13 @@
 #include <string>
 #include <vector>
 
+#include <zlib.h>
+
+#include <fstream>
+#include <sstream>
+
+#include "json.h"
+#include "msgpack.h"
 #include "nerf.h"
 #include "profiler.h"
 
@@ -88,6 +95,7 @@ struct ngp_nerf_trainer {
 	uint32_t n_rays_total = 0;
 	uint32_t measured_batch_size = 0, measured_before_compaction = 0;
 	uint32_t measured_before_compaction_local = 0;  // this rank's pre-compaction count (inference sizing)
+	float loss_scalar = 0.f;  // m_loss_scalar (last step that computed the loss)
 	// data parallelism: rank r traces global rays [R r / N, R (r+1) / N), compacts to B / N,
 	// evaluates 1/N of the density-grid samples; the exchange steps go through `allreduce`
 	uint32_t rank = 0, world = 1;
@@ -541,7 +549,7 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		if (h[1] != 0 && h[2] != 0) {
 			t->measured_before_compaction = h[1];
 			t->measured_batch_size = h[2];
-			if (get_loss) loss_scalar = (float)(loss_sum * (double)t->measured_batch_size / (double)B);
+			if (get_loss) t->loss_scalar = loss_scalar = (float)(loss_sum * (double)t->measured_batch_size / (double)B);
 			uint32_t r = (uint32_t)((float)t->rays_per_batch * (float)B / (float)t->measured_batch_size);
 			t->rays_per_batch = std::min(next_multiple(r, 256), 1u << 18);
 		}
@@ -553,6 +561,231 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			st->loss = loss_scalar;
 		}
 		NGP_CHECK(t->measured_batch_size > 0, "Nerf training generated 0 samples (testbed_nerf.cu:3693-3697)");
+	});
+}
+
+
+// ---- snapshots (.ingp) ---------------------------------------------------------------------------
+// Testbed::save_snapshot / load_snapshot (src/testbed.cu:4873-5057) for a NeRF testbed: msgpack of the
+// network config with a "snapshot" member; .ingp files are gzip streams (zstr), others raw msgpack.
+// tcnn Trainer::serialize writes n_params / params_type / params_binary (fp16 params); the optimizer
+// member (include_optimizer_state) is this engine's own layout (tcnn absent: parity unpinned).
+}  // extern "C"
+
+namespace {
+using ngp::mp::Value;
+
+constexpr uint32_t SNAPSHOT_FORMAT_VERSION = 1;  // testbed.cu:80
+
+bool ends_with_ci(const std::string& s, const std::string& suf) {
+	return s.size() >= suf.size() && ngp::iequals(s.substr(s.size() - suf.size()), suf);
+}
+
+std::string gzip_bytes(const std::string& in, int level) {
+	z_stream z{};
+	NGP_CHECK(deflateInit2(&z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) == Z_OK, "snapshot: deflateInit2 failed");
+	std::string out(deflateBound(&z, in.size()) + 64, '\0');
+	z.next_in = (Bytef*)in.data();
+	z.avail_in = (uInt)in.size();
+	z.next_out = (Bytef*)out.data();
+	z.avail_out = (uInt)out.size();
+	const int rc = deflate(&z, Z_FINISH);
+	const size_t n = out.size() - z.avail_out;
+	deflateEnd(&z);
+	NGP_CHECK(rc == Z_STREAM_END, "snapshot: deflate failed");
+	out.resize(n);
+	return out;
+}
+
+std::string maybe_inflate(const std::string& in) {
+	const bool gz = in.size() >= 2 && (uint8_t)in[0] == 0x1f && (uint8_t)in[1] == 0x8b;
+	const bool zl = in.size() >= 2 && ((uint8_t)in[0] & 0x0f) == 8 && (((uint8_t)in[0] << 8) | (uint8_t)in[1]) % 31 == 0;
+	if (!gz && !zl) return in;  // raw msgpack
+	z_stream z{};
+	NGP_CHECK(inflateInit2(&z, 15 + 32) == Z_OK, "snapshot: inflateInit2 failed");
+	z.next_in = (Bytef*)in.data();
+	z.avail_in = (uInt)in.size();
+	std::string out;
+	char buf[1 << 16];
+	int rc;
+	do {
+		z.next_out = (Bytef*)buf;
+		z.avail_out = sizeof buf;
+		rc = inflate(&z, Z_NO_FLUSH);
+		NGP_CHECK(rc == Z_OK || rc == Z_STREAM_END, "snapshot: corrupt compressed stream");
+		out.append(buf, sizeof buf - z.avail_out);
+	} while (rc != Z_STREAM_END);
+	inflateEnd(&z);
+	return out;
+}
+
+std::string read_file(const char* path) {
+	std::ifstream f(path, std::ios::binary);
+	NGP_CHECK(f.good(), std::string("snapshot: cannot open '") + path + "'");
+	std::stringstream ss;
+	ss << f.rdbuf();
+	return ss.str();
+}
+
+Value load_network_config(const char* path) {  // Testbed::load_network_config (testbed.cu:246): msgpack branch
+	return ngp::mp::decode(maybe_inflate(read_file(path)));
+}
+
+Value vec3(const float* v) {
+	Value a = Value::array();
+	for (int k = 0; k < 3; ++k) a.arr.push_back(Value::real(v[k]));
+	return a;
+}
+
+template <typename T> std::vector<T> device_to_host(const void* d, size_t n) {
+	std::vector<T> h(n);
+	if (n) NGP_HIP(hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost));
+	return h;
+}
+}  // namespace
+
+extern "C" {
+
+int ngp_nerf_save_snapshot(ngp_nerf_trainer* t, void* stream, const char* path, const char* network_config_json,
+                           int include_optimizer_state, int compress) {
+	if (!t || !path) return NGP_INVALID;
+	NERF_TRY({
+		NGP_HIP(hipStreamSynchronize(S(stream)));
+		Value root = network_config_json && *network_config_json ? ngp::mp::from_json(ngp::Json::parse(network_config_json))
+		                                                          : Value::object();
+		root.erase("snapshot");
+		Value snap = Value::object();
+		// tcnn Trainer::serialize
+		const uint64_t n = ngp_model_n_params(t->model);
+		snap["n_params"] = Value::uint(n);
+		snap["params_type"] = Value::str("__half");
+		{
+			auto p = device_to_host<uint16_t>(ngp_trainer_params(t->trainer), n);
+			snap["params_binary"] = Value::bin(p.data(), p.size() * 2);
+		}
+		if (include_optimizer_state) {
+			uint64_t bytes = 0;
+			check_rc(ngp_trainer_serialize(t->trainer, nullptr, &bytes));
+			std::string blob(bytes, '\0');
+			check_rc(ngp_trainer_serialize(t->trainer, blob.data(), &bytes));
+			uint64_t hdr[4];
+			memcpy(hdr, blob.data(), 32);
+			Value opt = Value::object();
+			opt["otype"] = Value::str("Ema(ExponentialDecay(Adam))");
+			opt["current_step"] = Value::uint(hdr[3]);
+			const char* names[5] = {"full_precision_params_binary", "first_moments_binary", "second_moments_binary",
+			                        "ema_params_binary", "param_steps_binary"};
+			for (int k = 0; k < 5; ++k) opt[names[k]] = Value::bin(blob.data() + 32 + (size_t)k * n * 4, (size_t)n * 4);
+			snap["optimizer"] = opt;
+		}
+		snap["version"] = Value::uint(SNAPSHOT_FORMAT_VERSION);
+		snap["mode"] = Value::str("nerf");
+		snap["density_grid_size"] = Value::uint(GRIDSIZE);
+		{
+			const uint32_t n_el = GRID_N_CELLS * (t->cfg.max_cascade + 1);
+			auto g = device_to_host<float>(t->grid.p, n_el);
+			std::vector<f16> h(n_el);
+			for (uint32_t k = 0; k < n_el; ++k) h[k] = (f16)g[k];  // (__half)density_grid[i]
+			snap["density_grid_binary"] = Value::bin(h.data(), h.size() * 2);
+		}
+		Value& nerf = snap["nerf"];
+		nerf["aabb_scale"] = Value::real(t->cfg.aabb_max[0] - t->cfg.aabb_min[0]);
+		nerf["rgb"]["rays_per_batch"] = Value::uint(t->rays_per_batch);
+		nerf["rgb"]["measured_batch_size"] = Value::uint(t->measured_batch_size);
+		nerf["rgb"]["measured_batch_size_before_compaction"] = Value::uint(t->measured_before_compaction);
+		snap["training_step"] = Value::uint(t->training_step);
+		snap["loss"] = Value::real(t->loss_scalar);
+		snap["aabb"]["min"] = vec3(t->cfg.aabb_min);
+		snap["aabb"]["max"] = vec3(t->cfg.aabb_max);
+		snap["density_grid_ema_step"] = Value::uint(t->ema_step);
+		root["snapshot"] = snap;
+		std::string bytes;
+		ngp::mp::encode(root, bytes);
+		if (ends_with_ci(path, ".ingp")) bytes = gzip_bytes(bytes, compress ? Z_DEFAULT_COMPRESSION : Z_NO_COMPRESSION);
+		std::ofstream f(path, std::ios::binary);
+		NGP_CHECK(f.good(), std::string("snapshot: cannot write '") + path + "'");
+		f.write(bytes.data(), (std::streamsize)bytes.size());
+		NGP_CHECK(f.good(), "snapshot: write failed");
+	});
+}
+
+int ngp_nerf_load_snapshot(ngp_nerf_trainer* t, void* stream, const char* path) {
+	if (!t || !path) return NGP_INVALID;
+	NERF_TRY({
+		hipStream_t s = S(stream);
+		NGP_HIP(hipStreamSynchronize(s));
+		const Value root = load_network_config(path);
+		NGP_CHECK(root.find("snapshot"), std::string("File '") + path + "' does not contain a snapshot.");
+		const Value& snap = root.at("snapshot");
+		NGP_CHECK(snap.number_or("version", 0) >= SNAPSHOT_FORMAT_VERSION, "Snapshot uses an old format and can not be loaded.");
+		if (const Value* m = snap.find("mode")) NGP_CHECK(m->type == Value::Str && m->s == "nerf", "snapshot: not a NeRF snapshot");
+		NGP_CHECK((uint32_t)snap.at("density_grid_size").number() == GRIDSIZE, "Incompatible grid size.");
+		// tcnn Trainer::deserialize
+		const uint64_t n = ngp_model_n_params(t->model);
+		NGP_CHECK((uint64_t)snap.at("n_params").number() == n, "snapshot: parameter count differs from this network");
+		const Value& pb = snap.at("params_binary");
+		const std::string type = snap.find("params_type") ? snap.at("params_type").s : std::string("__half");
+		std::vector<float> w(n);
+		if (type == "float") {
+			NGP_CHECK(pb.s.size() == n * 4, "snapshot: params_binary size");
+			memcpy(w.data(), pb.s.data(), n * 4);
+		} else {
+			NGP_CHECK(type == "__half" && pb.s.size() == n * 2, "snapshot: params_binary size/type");
+			const f16* h = (const f16*)pb.s.data();
+			for (uint64_t k = 0; k < n; ++k) w[k] = (float)h[k];
+		}
+		check_rc(ngp_trainer_set_params_full_precision(t->trainer, w.data(), n));
+		if (const Value* opt = snap.find("optimizer")) {
+			const char* names[5] = {"full_precision_params_binary", "first_moments_binary", "second_moments_binary",
+			                        "ema_params_binary", "param_steps_binary"};
+			std::string blob(32 + (size_t)n * 20, '\0');
+			const uint64_t hdr[4] = {0x4e47504d49333535ULL, 1, n, (uint64_t)opt->at("current_step").number()};
+			memcpy(blob.data(), hdr, 32);
+			for (int k = 0; k < 5; ++k) {
+				const Value& b = opt->at(names[k]);
+				NGP_CHECK(b.s.size() == n * 4, "snapshot: optimizer state size");
+				memcpy(blob.data() + 32 + (size_t)k * n * 4, b.s.data(), n * 4);
+			}
+			check_rc(ngp_trainer_deserialize(t->trainer, blob.data(), blob.size()));
+		}
+		// density grid (fp16 in the file)
+		const Value& gb = snap.at("density_grid_binary");
+		const uint32_t n_el = GRID_N_CELLS * (t->cfg.max_cascade + 1);
+		const size_t n_file = gb.s.size() / 2;
+		if (n_file == n_el) {
+			std::vector<float> g(n_el);
+			const f16* h = (const f16*)gb.s.data();
+			for (uint32_t k = 0; k < n_el; ++k) g[k] = (float)h[k];
+			NGP_HIP(hipMemcpy(t->grid.p, g.data(), (size_t)n_el * 4, hipMemcpyHostToDevice));
+			grid_mean_bitfield((const float*)t->grid.p, t->cfg.max_cascade, (float*)t->mean.p, (uint8_t*)t->bitfield.p, s);
+		} else {
+			// a size of 0 is a never-populated grid (testbed.cu:5000-5005)
+			NGP_CHECK(n_file == 0, "Incompatible number of grid cascades.");
+		}
+		const Value& rgb = snap.at("nerf").at("rgb");
+		t->rays_per_batch = (uint32_t)rgb.at("rays_per_batch").number();
+		t->measured_batch_size = (uint32_t)rgb.at("measured_batch_size").number();
+		t->measured_before_compaction = (uint32_t)rgb.at("measured_batch_size_before_compaction").number();
+		t->measured_before_compaction_local = t->measured_before_compaction / t->world;
+		t->training_step = (uint32_t)snap.at("training_step").number();
+		t->loss_scalar = (float)snap.number_or("loss", 0.0);
+		t->ema_step = (uint32_t)snap.number_or("density_grid_ema_step", (double)t->training_step);
+		NGP_HIP(hipStreamSynchronize(s));
+	});
+}
+
+int ngp_snapshot_network_config(const char* path, char* json_buf, uint64_t* size) {
+	if (!path || !size) return NGP_INVALID;
+	NERF_TRY({
+		Value root = load_network_config(path);
+		NGP_CHECK(root.is_map(), "snapshot: top level is not a map");
+		root.erase("snapshot");
+		std::string text;
+		ngp::mp::to_json_text(root, text);
+		if (!json_buf) { *size = text.size() + 1; return NGP_OK; }
+		NGP_CHECK(*size >= text.size() + 1, "snapshot: buffer too small");
+		memcpy(json_buf, text.c_str(), text.size() + 1);
+		*size = text.size() + 1;
 	});
 }
 

@@ -6,7 +6,9 @@ testbed_nerf.cu:3611-3862, 4137-4152); the free functions expose the individual 
 the reference's argument meaning so they can be tested one by one. Every call runs HIP.
 """
 import ctypes as C
+import json
 import math
+import os
 
 import numpy as np
 import torch
@@ -229,6 +231,17 @@ class NerfTraining:
             fn, user = None, None
         check(lib().ngp_nerf_trainer_set_data_parallel(self.handle, rank, world, fn, user))
 
+    def save_snapshot(self, path, network_config=None, include_optimizer_state=False, compress=True, stream=None):
+        """Testbed::save_snapshot (testbed.cu:4873-4937): .ingp = gzip'd msgpack of the network config
+        (dict, the Testbed's m_network_config) with the "snapshot" member."""
+        cfg = json.dumps(network_config) if network_config is not None else None
+        check(lib().ngp_nerf_save_snapshot(self.handle, _stream(stream), os.fsencode(path),
+                                           cfg.encode() if cfg else None, int(include_optimizer_state), int(compress)))
+
+    def load_snapshot(self, path, stream=None):
+        """Testbed::load_snapshot (testbed.cu:4939-5057) into this trainer's network/optimizer/grid."""
+        check(lib().ngp_nerf_load_snapshot(self.handle, _stream(stream), os.fsencode(path)))
+
     def train_step(self, get_loss=True, stream=None):
         st = NerfStats()
         check(lib().ngp_nerf_train_step(self.handle, _stream(stream), int(get_loss), C.byref(st)))
@@ -242,6 +255,16 @@ class NerfTraining:
             except Exception:
                 pass
             self.handle = None
+
+
+def snapshot_network_config(path):
+    """Testbed::load_network_config (testbed.cu:246) of a snapshot: the network config dict without its
+    "snapshot" member, e.g. to build the network before NerfTraining.load_snapshot."""
+    size = C.c_uint64(0)
+    check(lib().ngp_snapshot_network_config(os.fsencode(path), None, C.byref(size)))
+    buf = C.create_string_buffer(size.value)
+    check(lib().ngp_snapshot_network_config(os.fsencode(path), buf, C.byref(size)))
+    return json.loads(buf.value.decode())
 
 
 # ---- rendering / evaluation -------------------------------------------------------------------
