@@ -507,13 +507,16 @@ __global__ void k_sample_keep(uint32_t n, const uint32_t* __restrict__ nsteps, c
 	keep[i] = (nsteps[i] > 0 && base[i] + nsteps[i] <= max_samples) ? 1u : 0u;
 }
 
+// pass 2: write the ray records and the NerfCoordinates of kept rays from the stored t values; one
+// wave per ray (most rays take one or two iterations, consecutive lanes write consecutive samples).
+constexpr uint32_t WG = 64;
 // pass 2: write the ray records and the NerfCoordinates of kept rays from the stored t values.
 __global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg, SampleArgs a, const uint32_t* __restrict__ nsteps,
                                                       const uint32_t* __restrict__ base, const uint32_t* __restrict__ keep,
                                                       const uint32_t* __restrict__ slot, const float* __restrict__ tbuf,
                                                       const RayGeo* __restrict__ geo) {
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-	const uint32_t i = gid / RG, L = gid % RG;
+	const uint32_t i = gid / WG, L = gid % WG;
 	if (gid == 0) {  // counters: rays kept, total steps of every ray that found samples
 		a.counters[0] = slot[a.n_rays - 1] + keep[a.n_rays - 1];
 		a.counters[1] = base[a.n_rays - 1] + nsteps[a.n_rays - 1];
@@ -532,7 +535,7 @@ __global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg,
 	const V3 diag = v3(box.mx.x - box.mn.x, box.mx.y - box.mn.y, box.mx.z - box.mn.z);
 	const V3 wdir = v3((g.dn[0] + 1.0f) * 0.5f, (g.dn[1] + 1.0f) * 0.5f, (g.dn[2] + 1.0f) * 0.5f);
 	const float* tin = tbuf + (size_t)i * STEPS;
-	for (uint32_t jj = L; jj < numsteps; jj += RG) {
+	for (uint32_t jj = L; jj < numsteps; jj += WG) {
 		const float t = tin[jj];
 		const V3 pos = v3(g.o[0] + t * g.dn[0], g.o[1] + t * g.dn[1], g.o[2] + t * g.dn[2]);
 		const float dt = calc_dt(t, g.pad[0]);
@@ -582,7 +585,7 @@ void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs
 		exclusive_scan(keep, slot, a.n_rays, scan_tmp, scan_bytes, s);
 	}
 	ProfScope ps("sample_write", s);
-	k_sample_write<<<blocks, 256, 0, s>>>(cfg, a, nsteps, base, keep, slot, tbuf, geo);
+	k_sample_write<<<div_round_up((size_t)a.n_rays * WG, 256), 256, 0, s>>>(cfg, a, nsteps, base, keep, slot, tbuf, geo);
 	NGP_HIP(hipGetLastError());
 }
 

@@ -96,6 +96,17 @@ struct ngp_nerf_trainer {
 	uint32_t measured_batch_size = 0, measured_before_compaction = 0;
 	uint32_t measured_before_compaction_local = 0;  // this rank's pre-compaction count (inference sizing)
 	float loss_scalar = 0.f;  // m_loss_scalar (last step that computed the loss)
+	// the training pass (forward_backward + optimizer over the fixed compacted batch) replayed as one
+	// HIP graph per step; re-captured if its buffers move
+	ngp_graph* train_graph = nullptr;
+	const void* graph_in = nullptr;
+	const void* graph_dl = nullptr;
+	uint32_t graph_n = 0;
+	hipStream_t own_stream = nullptr;  // used when the caller passes the null stream (graphs need a stream)
+	~ngp_nerf_trainer() {
+		if (train_graph) ngp_graph_destroy(train_graph);
+		if (own_stream) (void)hipStreamDestroy(own_stream);
+	}
 	// data parallelism: rank r traces global rays [R r / N, R (r+1) / N), compacts to B / N,
 	// evaluates 1/N of the density-grid samples; the exchange steps go through `allreduce`
 	uint32_t rank = 0, world = 1;
@@ -452,6 +463,10 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 	if (!t) return NGP_INVALID;
 	NERF_TRY({
 		hipStream_t s = S(stream);
+		if (!s) {  // a private blocking stream (ordered after the null stream's earlier work)
+			if (!t->own_stream) NGP_HIP(hipStreamCreate(&t->own_stream));
+			s = t->own_stream;
+		}
 		const ngp_nerf_config& cfg = t->cfg;
 		const uint32_t B = cfg.target_batch_size;
 		// training_prep_nerf
@@ -509,14 +524,24 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		}
 		{
 		ProfScope ps("nerf_train_pass", s);
-		check_rc(ngp_forward_backward(t->model, s, Bl, coords_c, 7, nullptr, 0, dloss, 16, NGP_GRAD_OVERWRITE));
-		t->rng.advance();  // m_rng.advance() (testbed_nerf.cu:4127)
-		if (W > 1) {
+		if (W == 1) {
+			if (!t->train_graph || t->graph_in != coords_c || t->graph_dl != dloss || t->graph_n != Bl) {
+				if (t->train_graph) ngp_graph_destroy(t->train_graph);
+				t->train_graph = nullptr;
+				check_rc(ngp_trainer_capture_training_step(t->trainer, s, Bl, coords_c, 7, dloss, 16, 128.0f, 1, 1, &t->train_graph));
+				t->graph_in = coords_c;
+				t->graph_dl = dloss;
+				t->graph_n = Bl;
+			}
+			check_rc(ngp_graph_launch(t->train_graph, s));
+		} else {
+			check_rc(ngp_forward_backward(t->model, s, Bl, coords_c, 7, nullptr, 0, dloss, 16, NGP_GRAD_OVERWRITE));
 			NGP_CHECK(t->allreduce(t->allreduce_user, ngp_trainer_gradients(t->trainer), ngp_model_n_params(t->model), NGP_DTYPE_F16,
 			                       NGP_REDUCE_SUM, s) == 0,
 			          "data parallel: gradient all-reduce failed");
+			check_rc(ngp_trainer_optimizer_step(t->trainer, s, 128.0f));
 		}
-		check_rc(ngp_trainer_optimizer_step(t->trainer, s, 128.0f));
+		t->rng.advance();  // m_rng.advance() (testbed_nerf.cu:4127)
 		}
 		++t->training_step;
 		// NerfCounters::update_after_training (testbed_nerf.cu:3583-3609): host sync
