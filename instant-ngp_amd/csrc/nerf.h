@@ -92,6 +92,8 @@ void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs&
                   uint32_t* tmp_u32, float* tmp_f32, hipStream_t s);
 void fill_rollover_f16(uint32_t n_elements, uint32_t stride, const uint32_t* n_input, f16* data, bool rescale, hipStream_t s);
 void fill_rollover_f32(uint32_t n_elements, uint32_t stride, const uint32_t* n_input, float* data, hipStream_t s);
+void fill_rollover_pair(uint32_t n_elements, const uint32_t* n_input, f16* dloss, uint32_t stride16, float* coords,
+                        uint32_t stride32, hipStream_t s);
 void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_config& cfg, const float* grid_in,
                            uint32_t n_cascades, float thresh, float* positions, uint32_t* indices, hipStream_t s);
 void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t density_activation, float* grid_tmp,

@@ -13,6 +13,7 @@
 
 #include <zlib.h>
 
+#include <chrono>
 #include <fstream>
 #include <sstream>
 
@@ -103,9 +104,14 @@ struct ngp_nerf_trainer {
 	const void* graph_dl = nullptr;
 	uint32_t graph_n = 0;
 	hipStream_t own_stream = nullptr;  // used when the caller passes the null stream (graphs need a stream)
+	// per-step counters published by the step's last kernel into host-coherent pinned memory, read by
+	// spinning on a sequence number (no copy-engine transfer, no blocking stream synchronize)
+	volatile uint32_t* host_ctr = nullptr;
+	uint32_t publish_seq = 0;
 	~ngp_nerf_trainer() {
 		if (train_graph) ngp_graph_destroy(train_graph);
 		if (own_stream) (void)hipStreamDestroy(own_stream);
+		if (host_ctr) (void)hipHostFree((void*)host_ctr);
 	}
 	// data parallelism: rank r traces global rays [R r / N, R (r+1) / N), compacts to B / N,
 	// evaluates 1/N of the density-grid samples; the exchange steps go through `allreduce`
@@ -459,6 +465,29 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	grid_mean_bitfield(grid, cfg.max_cascade, (float*)t->mean.p, (uint8_t*)t->bitfield.p, s);
 }
 
+__global__ void k_publish_counters(const uint32_t* __restrict__ ctr, volatile uint32_t* host, uint32_t seq) {
+	if (threadIdx.x == 0) {
+		host[0] = ctr[0]; host[1] = ctr[1]; host[2] = ctr[2]; host[3] = ctr[3];
+		__threadfence_system();
+		host[4] = seq;
+	}
+}
+
+// Wait until the step's k_publish_counters has run (or the stream failed / stalled for a minute).
+static void wait_published(volatile uint32_t* host, uint32_t seq, hipStream_t s) {
+	const auto t0 = std::chrono::steady_clock::now();
+	for (uint64_t spin = 0;; ++spin) {
+		if (__atomic_load_n(&host[4], __ATOMIC_ACQUIRE) == seq) return;
+		if ((spin & 1023) == 1023) {
+			const hipError_t q = hipStreamQuery(s);
+			if (q != hipSuccess && q != hipErrorNotReady) NGP_HIP(q);
+			if (q == hipSuccess && __atomic_load_n(&host[4], __ATOMIC_ACQUIRE) == seq) return;
+			NGP_CHECK(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60), "nerf train step: counters not published");
+		}
+		__builtin_ia32_pause();
+	}
+}
+
 int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_nerf_stats* st) {
 	if (!t) return NGP_INVALID;
 	NERF_TRY({
@@ -519,8 +548,7 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		ProfScope ps("nerf_loss", s);
 		check_rc(ngp_nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, ray_indices, rays, numsteps, coords, coords_c,
 		                               dloss, loss, ctr + 2, (const float*)t->mean.p, W > 1 ? loss_scale_local : 128.0f));
-		fill_rollover_f16(Bl, 16, ctr + 2, dloss, true, s);
-		fill_rollover_f32(Bl, 7, ctr + 2, coords_c, s);
+		fill_rollover_pair(Bl, ctr + 2, dloss, 16, coords_c, 7, s);  // fill_rollover_and_rescale + fill_rollover
 		}
 		{
 		ProfScope ps("nerf_train_pass", s);
@@ -546,10 +574,23 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		++t->training_step;
 		// NerfCounters::update_after_training (testbed_nerf.cu:3583-3609): host sync
 		uint32_t h[4];
-		NGP_HIP(hipMemcpyAsync(h, ctr, 16, hipMemcpyDeviceToHost, s));
 		std::vector<float> hl;
-		if (get_loss && Rl) { hl.resize(Rl); NGP_HIP(hipMemcpyAsync(hl.data(), loss, (size_t)Rl * 4, hipMemcpyDeviceToHost, s)); }
-		NGP_HIP(hipStreamSynchronize(s));
+		if (!t->host_ctr) {
+			void* p = nullptr;
+			NGP_HIP(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+			t->host_ctr = (volatile uint32_t*)p;
+			memset(p, 0, 64);
+		}
+		k_publish_counters<<<1, 64, 0, s>>>(ctr, t->host_ctr, ++t->publish_seq);
+		NGP_HIP(hipGetLastError());
+		if (get_loss && Rl) {
+			hl.resize(Rl);
+			NGP_HIP(hipMemcpyAsync(hl.data(), loss, (size_t)Rl * 4, hipMemcpyDeviceToHost, s));
+			NGP_HIP(hipStreamSynchronize(s));
+		} else {
+			wait_published(t->host_ctr, t->publish_seq, s);
+		}
+		for (int k = 0; k < 4; ++k) h[k] = t->host_ctr[k];
 		double loss_sum = 0;
 		for (float v : hl) loss_sum += v;
 		t->measured_before_compaction_local = h[1];
