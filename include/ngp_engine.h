@@ -36,6 +36,9 @@ typedef struct ngp_trainer ngp_trainer; /* params + gradients + optimizer state 
 
 enum { NGP_OK = 0, NGP_ERROR = -1, NGP_INVALID = -2 };
 enum { NGP_LAYOUT_AOS = 0, NGP_LAYOUT_SOA = 1 };
+/* Engine extension for NerfNetwork inference outputs: only the 4 live rows (raw rgb, raw density) as
+ * AoS [n x stride >= 4], skipping the 12 padded outputs of padded_output_width 16 (nerf_network.h:463). */
+enum { NGP_LAYOUT_AOS_RGBD = 2 };
 enum { NGP_GRAD_OVERWRITE = 0, NGP_GRAD_ACCUMULATE = 1 }; /* tcnn::EGradientMode */
 
 /* ---- library ------------------------------------------------------------------------------ */

@@ -627,7 +627,8 @@ int ngp_encoding_backward(ngp_model* m, void* stream, uint32_t n, const float* i
 
 int ngp_inference(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
                   uint32_t output_stride, uint32_t output_layout, int use_inference_params) {
-	NGP_ARG(m && (n == 0 || (input && output)) && output_layout <= 1);
+	NGP_ARG(m && (n == 0 || (input && output)) && (output_layout <= 1 || (output_layout == NGP_LAYOUT_AOS_RGBD && m->nerf &&
+	                                                                        output_stride >= 4)));
 	NGP_TRY({
 		if (n == 0) return NGP_OK;
 		m->require_params(use_inference_params);

@@ -303,7 +303,9 @@ __device__ __forceinline__ f16x8 sh4_frag(float dx, float dy, float dz, int h) {
 // rows 4h..4h+3 (regs 0..3) and 8+4h..8+4h+3 (regs 4..7).
 __device__ __forceinline__ void store_out16(f16* out, uint32_t stride, uint32_t layout, uint32_t n, uint32_t sample, int h,
                                             const f16x8& v) {
-	if (layout == 0) {
+	if (layout == 2) {  // NGP_LAYOUT_AOS_RGBD: rows 0..3 only (lane half 0 holds them)
+		if (h == 0) *(f16x4*)(out + (size_t)sample * stride) = f16x4{v[0], v[1], v[2], v[3]};
+	} else if (layout == 0) {
 		f16* row = out + (size_t)sample * stride;
 		*(f16x4*)(row + 4 * h) = f16x4{v[0], v[1], v[2], v[3]};
 		*(f16x4*)(row + 8 + 4 * h) = f16x4{v[4], v[5], v[6], v[7]};

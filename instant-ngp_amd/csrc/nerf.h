@@ -71,7 +71,8 @@ struct LossArgs {
 	Rng rng;
 	uint32_t max_samples_compacted;
 	const uint32_t* ray_counter;
-	const f16* network_output;  // [n x 16]
+	const f16* network_output;  // [n x out_stride] rows 0..2 raw rgb, 3 raw density
+	uint32_t out_stride;       // 16 (padded_output_width) or 4 (NGP_LAYOUT_AOS_RGBD)
 	const uint32_t* ray_indices;
 	const float* rays;
 	uint32_t* numsteps;        // in: {numsteps, base}; out: {compacted numsteps, compacted base}

@@ -619,7 +619,7 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 	if (i >= a.n_rays) return;
 	if (i >= *a.ray_counter) { if (L == 0) craw[i] = 0; return; }
 	const uint32_t numsteps = a.numsteps[2 * i], base = a.numsteps[2 * i + 1];
-	const f16* out = a.network_output + (size_t)base * 16;
+	const f16* out = a.network_output + (size_t)base * a.out_stride;
 	const float* ci = a.coords_in + (size_t)base * 7;
 	float t = 1.f;
 	const float eps = 1e-4f;
@@ -630,7 +630,7 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 		const uint32_t jj = c + L;
 		float alpha = 0.f, cr = 0.f, cg = 0.f, cb = 0.f;
 		if (jj < numsteps) {
-			const f16x4 o = *(const f16x4*)(out + (size_t)jj * 16);
+			const f16x4 o = *(const f16x4*)(out + (size_t)jj * a.out_stride);
 			const float dt = unwarp_dt(ci[(size_t)jj * 7 + 3]);
 			const float density = network_to_density((float)o[3], cfg.density_activation);
 			alpha = 1.f - __expf(-density * dt);
@@ -728,7 +728,7 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const ngp_nerf_config cfg, L
 	const Aabb box = cfg_aabb(cfg);
 	const float* ray = a.rays + (size_t)i * 6;
 	const float ro0 = ray[0], ro1 = ray[1], ro2 = ray[2];
-	const f16* out = a.network_output + (size_t)base * 16;
+	const f16* out = a.network_output + (size_t)base * a.out_stride;
 	const float* ci = a.coords_in + (size_t)base * 7;
 	float* co = a.coords_out + (size_t)compacted_base * 7;
 	f16* dl = a.dloss_doutput + (size_t)compacted_base * 16;
@@ -743,7 +743,7 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const ngp_nerf_config cfg, L
 		if (valid) {
 #pragma unroll
 			for (int k = 0; k < 7; ++k) cc[k] = ci[(size_t)jj * 7 + k];
-			o = *(const f16x4*)(out + (size_t)jj * 16);
+			o = *(const f16x4*)(out + (size_t)jj * a.out_stride);
 			for (int k = 0; k < 3; ++k) rgb[k] = network_to_rgb((float)o[k], cfg.rgb_activation);
 			dt = unwarp_dt(cc[3]);
 			const float density = network_to_density((float)o[3], cfg.density_activation);

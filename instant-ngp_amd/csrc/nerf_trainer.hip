@@ -279,11 +279,27 @@ int ngp_nerf_generate_training_samples(const ngp_nerf_dataset* ds, const ngp_ner
 	});
 }
 
+static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
+                             uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
+                             const void* network_output, uint32_t out_stride, const uint32_t* ray_indices, const float* rays,
+                             uint32_t* numsteps, const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
+                             uint32_t* compacted_counter, const float* mean_density, float loss_scale);
+
 int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
                           uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
                           const void* network_output, const uint32_t* ray_indices, const float* rays, uint32_t* numsteps,
                           const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
                           uint32_t* compacted_counter, const float* mean_density, float loss_scale) {
+	return nerf_compute_loss(ds, cfg, stream, n_rays, n_rays_total, rng, max_samples_compacted, ray_counter, network_output, 16,
+	                         ray_indices, rays, numsteps, coords_in, coords_out, dloss_doutput, loss, compacted_counter, mean_density,
+	                         loss_scale);
+}
+
+static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
+                             uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
+                             const void* network_output, uint32_t out_stride, const uint32_t* ray_indices, const float* rays,
+                             uint32_t* numsteps, const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
+                             uint32_t* compacted_counter, const float* mean_density, float loss_scale) {
 	if (!ds || !cfg || !ray_counter || !network_output || !numsteps || !coords_in || !coords_out || !dloss_doutput ||
 	    !compacted_counter || !mean_density)
 		return NGP_INVALID;
@@ -291,6 +307,7 @@ int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg
 		LossArgs a{};
 		a.n_rays = n_rays; a.n_rays_total_for_image_idx = n_rays_total ? n_rays_total : n_rays; a.rng = Rng{rng.state, rng.inc};
 		a.max_samples_compacted = max_samples_compacted; a.ray_counter = ray_counter; a.network_output = (const f16*)network_output;
+		a.out_stride = out_stride;
 		a.ray_indices = ray_indices; a.rays = rays; a.numsteps = numsteps; a.coords_in = coords_in; a.coords_out = coords_out;
 		a.dloss_doutput = (f16*)dloss_doutput; a.loss = loss; a.compacted_counter = compacted_counter;
 		a.mean_density = mean_density; a.loss_scale = loss_scale;
@@ -541,12 +558,13 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		}
 		{
 		ProfScope ps("nerf_inference", s);
-		check_rc(ngp_inference(t->model, s, max_inference, coords, 7, mlp_out, 16, NGP_LAYOUT_AOS, 0));
+		// only the 4 live outputs (raw rgb, raw density): compute_loss reads nothing else
+		check_rc(ngp_inference(t->model, s, max_inference, coords, 7, mlp_out, 4, NGP_LAYOUT_AOS_RGBD, 0));
 		}
 		const float loss_scale_local = 128.0f * (float)Rl / (float)R;
 		{
 		ProfScope ps("nerf_loss", s);
-		check_rc(ngp_nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, ray_indices, rays, numsteps, coords, coords_c,
+		check_rc(nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, 4, ray_indices, rays, numsteps, coords, coords_c,
 		                               dloss, loss, ctr + 2, (const float*)t->mean.p, W > 1 ? loss_scale_local : 128.0f));
 		fill_rollover_pair(Bl, ctr + 2, dloss, 16, coords_c, 7, s);  // fill_rollover_and_rescale + fill_rollover
 		}

@@ -13,6 +13,7 @@ import torch
 from ._capi import ParamLayout, check, lib
 
 LAYOUT_AOS, LAYOUT_SOA = 0, 1
+LAYOUT_AOS_RGBD = 2  # engine extension: NerfNetwork rows 0..3 only (raw rgb, raw density), [n x 4]
 GRAD_OVERWRITE, GRAD_ACCUMULATE = 0, 1
 
 
@@ -130,7 +131,8 @@ class Model:
         _check_input(x, self.input_width())
         n = x.shape[0]
         if output is None:
-            output = torch.empty((n, 16) if layout == LAYOUT_AOS else (16, n), dtype=torch.float16, device=x.device)
+            shape = {LAYOUT_AOS: (n, 16), LAYOUT_SOA: (16, n), LAYOUT_AOS_RGBD: (n, 4)}[layout]
+            output = torch.empty(shape, dtype=torch.float16, device=x.device)
         stride = output.stride(0)
         check(lib().ngp_inference(self.handle, _stream(stream), n, _ptr(x), x.stride(0), _ptr(output), stride, layout,
                                   int(use_inference_params)))
@@ -182,7 +184,8 @@ class NerfNetwork(Model):
     def density(self, x, output=None, layout=LAYOUT_AOS, use_inference_params=True, stream=None):
         n = x.shape[0]
         if output is None:
-            output = torch.empty((n, 16) if layout == LAYOUT_AOS else (16, n), dtype=torch.float16, device=x.device)
+            shape = {LAYOUT_AOS: (n, 16), LAYOUT_SOA: (16, n), LAYOUT_AOS_RGBD: (n, 4)}[layout]
+            output = torch.empty(shape, dtype=torch.float16, device=x.device)
         check(lib().ngp_density(self.handle, _stream(stream), n, _ptr(x), x.stride(0), _ptr(output), output.stride(0), layout,
                                 int(use_inference_params)))
         return output

@@ -239,3 +239,22 @@ def test_nerf_training_end_to_end(pkg, orc):
     np.testing.assert_array_equal(bf, orc.nerf_grid_bitfield(full, cfg.max_cascade, m))
     occupied = np.unpackbits(bf[:128 ** 3 // 8]).mean()
     assert 0.0 < occupied < 0.5  # the grid prunes once step >= 256 switches to the 0.01 threshold (:3518)
+
+
+def test_inference_rgbd_layout(pkg):
+    """NGP_LAYOUT_AOS_RGBD (the NeRF trainer's inference output) = rows 0..3 of the padded AoS output."""
+    cfg = pkg.nerf_config("C2")
+    cfg["encoding"]["log2_hashmap_size"] = 15
+    net = pkg.create_nerf_network(cfg)
+    tr = pkg.Trainer(net, cfg["optimizer"], seed=3)  # noqa: F841 (owns the parameters)
+    g = np.random.default_rng(4)
+    n = 3000  # ragged tail
+    x = np.zeros((n, 7), np.float32)
+    x[:, :3] = g.random((n, 3))
+    x[:, 4:] = g.random((n, 3))
+    xt = torch.from_numpy(x).cuda()
+    full = net.inference(xt, layout=pkg.LAYOUT_AOS, use_inference_params=False)
+    rgbd = net.inference(xt, layout=pkg.LAYOUT_AOS_RGBD, use_inference_params=False)
+    torch.cuda.synchronize()
+    assert rgbd.shape == (n, 4)
+    np.testing.assert_array_equal(rgbd.cpu().numpy().view(np.uint16), full[:, :4].cpu().numpy().view(np.uint16))
