@@ -203,6 +203,13 @@ typedef struct ngp_sdf_mesh ngp_sdf_mesh;
  * builds the surface-area CDF (triangle_distribution, :1167-1175) */
 int ngp_sdf_mesh_create(uint32_t n_triangles, const float* tris_host, ngp_sdf_mesh** out);
 void ngp_sdf_mesh_destroy(ngp_sdf_mesh* m);
+/* the mesh's triangles in the order the BVH build left them (TriangleBvh4::build reorders
+ * m_sdf.triangles_cpu, testbed_sdf.cu:1157; the surface CDF follows that order): [n x 9] host floats */
+int ngp_sdf_mesh_triangles(const ngp_sdf_mesh* m, float* tris_out);
+/* host-only TriangleBvh4::build (triangle_bvh.cu:540-617) for inspection: reorders tris [n x 9] in place
+ * and writes the nodes, 32 bytes each {float lo[3], hi[3]; int32 left, right} (negative = leaf
+ * triangle range [-left-1, -right-1)). nodes_out = NULL: *n_nodes = the node count, tris untouched. */
+int ngp_sdf_bvh_build(float* tris, uint32_t n_triangles, uint32_t n_primitives_per_leaf, void* nodes_out, uint32_t* n_nodes);
 /* generate_training_samples_sdf (testbed_sdf.cu:1187-1275), non-octree branch: n/8 * {4 on the surface,
  * 3 surface + logistic offset, 1 uniform in aabb}; n must be a multiple of 8; advances *rng by
  * 3n + 3 * (3n/8). Signed distances by brute force over the triangles (the BVH is SURVEY §8f). */

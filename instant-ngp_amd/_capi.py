@@ -126,6 +126,8 @@ SIGNATURES = {
     "ngp_image_train_step": (i32, [P, P, P, u32, C.POINTER(Rng), C.POINTER(ImageConfig), P]),
     "ngp_sdf_mesh_create": (i32, [u32, P, C.POINTER(P)]),
     "ngp_sdf_mesh_destroy": (None, [P]),
+    "ngp_sdf_mesh_triangles": (i32, [P, P]),
+    "ngp_sdf_bvh_build": (i32, [P, u32, u32, P, C.POINTER(u32)]),
     "ngp_sdf_generate_training_samples": (i32, [P, P, u32, C.POINTER(Rng), P, P, f32, P, P]),
     "ngp_sdf_signed_distance": (i32, [P, P, u32, P, P]),
     "ngp_sdf_shuffle": (i32, [P, u32, u32, P, P, P, P]),

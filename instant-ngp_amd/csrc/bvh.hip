@@ -1,0 +1,289 @@
+// bvh.hip — triangle BVH for the SDF ground truth (TriangleBvh4, src/triangle_bvh.cu).
+//
+// Host build restated from TriangleBvhWithBranchingFactor<4>::build (triangle_bvh.cu:540-617): each
+// node splits its triangle range in two at the median centroid (std::nth_element) along the axis of
+// largest centroid variance, twice, into 4 children; ranges of <= n_primitives_per_leaf (8,
+// testbed_sdf.cu:1157) triangles become leaves. The triangle array is reordered in place exactly as
+// the reference reorders m_sdf.triangles_cpu (same algorithm, same libstdc++ nth_element), and the
+// surface-sampling CDF is built over that order afterwards (testbed_sdf.cu:1157-1172).
+//
+// Device queries restated from triangle_bvh.cu:240-433 with a per-thread 32-entry stack
+// (FixedIntStack): closest_triangle with the caller's upper bound (children pushed farthest first,
+// pruned at push time; no triangle within the bound -> distance 0), and signed_distance_raystab:
+// 32 Fibonacci stab rays with the offset random_val_2d of a default pcg32 advanced by 2 i
+// (signed_distance_raystab_kernel, :688-703), positive if any ray escapes MAX_DIST = 10. A stab ray
+// only needs to know whether any triangle is hit before MAX_DIST, so its traversal stops at the first
+// such hit (same sign as the reference's nearest-hit ray_intersect).
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <stack>
+#include <vector>
+
+#include "training.h"
+
+namespace ngp {
+
+namespace {
+constexpr float MAX_DIST = 10.0f;  // triangle_bvh.cu:40
+constexpr int STACK = 32;          // FixedStack<int, 32> (triangle_bvh.cuh:34-55)
+
+struct HostTri {
+	float v[9];
+	float centroid(int axis) const { return (v[axis] + v[3 + axis] + v[6 + axis]) / 3.0f; }
+};
+
+void bbox_of(const HostTri* b, const HostTri* e, BvhNode& n) {
+	for (int d = 0; d < 3; ++d) n.lo[d] = n.hi[d] = b->v[d];
+	for (const HostTri* t = b; t != e; ++t)
+		for (int k = 0; k < 3; ++k)
+			for (int d = 0; d < 3; ++d) {
+				n.lo[d] = std::min(n.lo[d], t->v[3 * k + d]);
+				n.hi[d] = std::max(n.hi[d], t->v[3 * k + d]);
+			}
+}
+}  // namespace
+
+void build_bvh4(float* tris, uint32_t n_triangles, uint32_t n_primitives_per_leaf, std::vector<BvhNode>& nodes) {
+	NGP_CHECK(n_triangles >= 4, "bvh: need at least 4 triangles");
+	HostTri* T = (HostTri*)tris;
+	nodes.clear();
+	nodes.emplace_back();
+	bbox_of(T, T + n_triangles, nodes[0]);
+	struct Build { int node; HostTri* b; HostTri* e; };
+	std::stack<Build> st;
+	st.push({0, T, T + n_triangles});
+	while (!st.empty()) {
+		const Build cur = st.top();
+		st.pop();
+		std::array<Build, 4> ch{};
+		ch[0] = cur;
+		for (int nc = 1; nc < 4; nc *= 2) {
+			for (int i = nc - 1; i >= 0; --i) {
+				const Build c = ch[i];
+				const float cnt = (float)(c.e - c.b);
+				float mean[3] = {0.f, 0.f, 0.f};
+				for (HostTri* t = c.b; t != c.e; ++t)
+					for (int d = 0; d < 3; ++d) mean[d] += (t->v[d] + t->v[3 + d] + t->v[6 + d]) / 3.0f;
+				for (int d = 0; d < 3; ++d) mean[d] /= cnt;
+				float var[3] = {0.f, 0.f, 0.f};
+				for (HostTri* t = c.b; t != c.e; ++t)
+					for (int d = 0; d < 3; ++d) {
+						const float df = (t->v[d] + t->v[3 + d] + t->v[6 + d]) / 3.0f - mean[d];
+						var[d] += df * df;
+					}
+				for (int d = 0; d < 3; ++d) var[d] /= cnt;
+				const float mx = std::max(std::max(var[0], var[1]), var[2]);
+				const int axis = var[0] == mx ? 0 : (var[1] == mx ? 1 : 2);
+				HostTri* m = c.b + (c.e - c.b) / 2;
+				std::nth_element(c.b, m, c.e, [axis](const HostTri& a, const HostTri& b) { return a.centroid(axis) < b.centroid(axis); });
+				ch[2 * i].b = c.b;
+				ch[2 * i + 1].e = c.e;
+				ch[2 * i].e = ch[2 * i + 1].b = m;
+			}
+		}
+		nodes[cur.node].left = (int32_t)nodes.size();
+		for (int i = 0; i < 4; ++i) {
+			NGP_CHECK(ch[i].b != ch[i].e, "bvh: empty child");
+			ch[i].node = (int)nodes.size();
+			nodes.emplace_back();
+			BvhNode& n = nodes.back();
+			bbox_of(ch[i].b, ch[i].e, n);
+			if ((uint32_t)(ch[i].e - ch[i].b) <= n_primitives_per_leaf) {
+				n.left = -(int32_t)(ch[i].b - T) - 1;
+				n.right = -(int32_t)(ch[i].e - T) - 1;
+			} else {
+				st.push(ch[i]);
+			}
+		}
+		nodes[cur.node].right = (int32_t)nodes.size();
+	}
+}
+
+// ---- device -----------------------------------------------------------------------------------
+namespace {
+struct V { float x, y, z; };
+__device__ __forceinline__ V vld(const float* p) { return V{p[0], p[1], p[2]}; }
+__device__ __forceinline__ V vsub(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V vmul(V a, float s) { return V{a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ float vdot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V vcross(V a, V b) { return V{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+__device__ __forceinline__ float clamp01(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
+__device__ __forceinline__ float sgn(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+// Triangle::distance_sq (triangle.cuh:66-85)
+__device__ float tri_dist_sq(const float* t, V pos) {
+	const V A = vld(t), B = vld(t + 3), C = vld(t + 6);
+	const V v21 = vsub(B, A), p1 = vsub(pos, A), v32 = vsub(C, B), p2 = vsub(pos, B), v13 = vsub(A, C), p3 = vsub(pos, C);
+	const V nor = vcross(v21, v13);
+	if (sgn(vdot(vcross(v21, nor), p1)) + sgn(vdot(vcross(v32, nor), p2)) + sgn(vdot(vcross(v13, nor), p3)) < 2.0f) {
+		auto edge = [](V v, V p) {
+			const V q = vsub(vmul(v, clamp01(vdot(v, p) / vdot(v, v))), p);
+			return vdot(q, q);
+		};
+		return fminf(fminf(edge(v21, p1), edge(v32, p2)), edge(v13, p3));
+	}
+	const float d = vdot(nor, p1);
+	return d * d / vdot(nor, nor);
+}
+
+// Triangle::ray_intersect (triangle.cuh:44-58)
+__device__ float tri_ray_t(const float* t, V ro, V rd) {
+	const V A = vld(t);
+	const V v1v0 = vsub(vld(t + 3), A), v2v0 = vsub(vld(t + 6), A), rov0 = vsub(ro, A);
+	const V n = vcross(v1v0, v2v0);
+	const V q = vcross(rov0, rd);
+	const float d = 1.0f / vdot(rd, n);
+	const float u = d * -vdot(q, v2v0);
+	const float v = d * vdot(q, v1v0);
+	float tt = d * -vdot(n, rov0);
+	if (u < 0.0f || u > 1.0f || v < 0.0f || (u + v) > 1.0f || tt < 0.0f) tt = 3.402823466e38f;
+	return tt;
+}
+
+// BoundingBox::distance_sq (bounding_box.cuh:230-232)
+__device__ __forceinline__ float box_dist_sq(const BvhNode& n, V p) {
+	const float dx = fmaxf(fmaxf(n.lo[0] - p.x, p.x - n.hi[0]), 0.0f);
+	const float dy = fmaxf(fmaxf(n.lo[1] - p.y, p.y - n.hi[1]), 0.0f);
+	const float dz = fmaxf(fmaxf(n.lo[2] - p.z, p.z - n.hi[2]), 0.0f);
+	return dx * dx + dy * dy + dz * dz;
+}
+
+// BoundingBox::ray_intersect (bounding_box.cuh:163-216), entry distance
+__device__ float box_ray_t(const BvhNode& n, V o, V d) {
+	const float FMAX = 3.402823466e+38f;
+	float tmin = (n.lo[0] - o.x) / d.x, tmax = (n.hi[0] - o.x) / d.x;
+	if (tmin > tmax) { const float t = tmin; tmin = tmax; tmax = t; }
+	float tymin = (n.lo[1] - o.y) / d.y, tymax = (n.hi[1] - o.y) / d.y;
+	if (tymin > tymax) { const float t = tymin; tymin = tymax; tymax = t; }
+	if (tmin > tymax || tymin > tmax) return FMAX;
+	if (tymin > tmin) tmin = tymin;
+	if (tymax < tmax) tmax = tymax;
+	float tzmin = (n.lo[2] - o.z) / d.z, tzmax = (n.hi[2] - o.z) / d.z;
+	if (tzmin > tzmax) { const float t = tzmin; tzmin = tzmax; tzmax = t; }
+	if (tmin > tzmax || tzmin > tmax) return FMAX;
+	if (tzmin > tmin) tmin = tzmin;
+	return tmin;
+}
+
+template <typename K> __device__ __forceinline__ void sort4_desc(K* k, int* id) {  // sorting_network<4>, largest first
+	auto cs = [&](int a, int b) {
+		if (k[a] < k[b]) { const K tk = k[a]; k[a] = k[b]; k[b] = tk; const int ti = id[a]; id[a] = id[b]; id[b] = ti; }
+	};
+	cs(0, 2); cs(1, 3); cs(0, 1); cs(2, 3); cs(1, 2);
+}
+
+// closest_triangle (triangle_bvh.cu:286-335): squared distance, or -1 if none within max_sq
+__device__ float closest_dist_sq(V p, const BvhNode* __restrict__ nodes, const float* __restrict__ tris, float max_sq) {
+	int stack[STACK];
+	int sp = 0;
+	stack[sp++] = 0;
+	float best = max_sq;
+	bool found = false;
+	while (sp > 0) {
+		const BvhNode node = nodes[stack[--sp]];
+		if (node.left < 0) {
+			const int end = -node.right - 1;
+			for (int i = -node.left - 1; i < end; ++i) {
+				const float d = tri_dist_sq(tris + 9 * (size_t)i, p);
+				if (d <= best) { best = d; found = true; }
+			}
+		} else {
+			float k[4];
+			int id[4];
+#pragma unroll
+			for (int c = 0; c < 4; ++c) { id[c] = node.left + c; k[c] = box_dist_sq(nodes[node.left + c], p); }
+			sort4_desc(k, id);
+#pragma unroll
+			for (int c = 0; c < 4; ++c)
+				if (k[c] <= best && sp < STACK) stack[sp++] = id[c];
+		}
+	}
+	return found ? best : -1.0f;
+}
+
+// any triangle hit closer than MAX_DIST along (o, d)? (ray_intersect(...).first >= 0, :240-284)
+__device__ bool ray_hits(V o, V d, const BvhNode* __restrict__ nodes, const float* __restrict__ tris) {
+	int stack[STACK];
+	int sp = 0;
+	stack[sp++] = 0;
+	while (sp > 0) {
+		const BvhNode node = nodes[stack[--sp]];
+		if (node.left < 0) {
+			const int end = -node.right - 1;
+			for (int i = -node.left - 1; i < end; ++i)
+				if (tri_ray_t(tris + 9 * (size_t)i, o, d) < MAX_DIST) return true;
+		} else {
+			float k[4];
+			int id[4];
+#pragma unroll
+			for (int c = 0; c < 4; ++c) { id[c] = node.left + c; k[c] = box_ray_t(nodes[node.left + c], o, d); }
+			sort4_desc(k, id);
+#pragma unroll
+			for (int c = 0; c < 4; ++c)
+				if (k[c] < MAX_DIST && sp < STACK) stack[sp++] = id[c];
+		}
+	}
+	return false;
+}
+
+// fibonacci_dir<32> (random_val.cuh:84-99) + cylindrical_to_dir (:45-54)
+__device__ V fib_dir32(uint32_t i, float ox, float oy) {
+	const float eps = 1.33f;
+	const float golden = 1.6180339887498948482045868343656f;
+	float a = (i + eps) / (32 - 1 + 2 * eps) + ox;
+	float b = i / golden + oy;
+	a = a - floorf(a);
+	b = b - floorf(b);
+	const float cos_theta = -2.0f * a + 1.0f;
+	const float phi = 2.0f * 3.14159265358979323846f * (b - 0.5f);
+	const float sin_theta = sqrtf(fmaxf(1.0f - cos_theta * cos_theta, 0.0f));
+	float sp, cp;
+	sincosf(phi, &sp, &cp);
+	return V{sin_theta * cp, sin_theta * sp, cos_theta};
+}
+
+__device__ __forceinline__ float pcg_next_float(uint64_t& state, uint64_t inc) {  // tcnn::pcg32::next_float
+	const uint64_t old = state;
+	state = old * 0x5851f42d4c957f2dULL + inc;
+	const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u), rot = (uint32_t)(old >> 59u);
+	const uint32_t u = (xs >> rot) | (xs << ((~rot + 1u) & 31));
+	return __uint_as_float((u >> 9) | 0x3f800000u) - 1.0f;
+}
+__device__ __forceinline__ uint64_t pcg_advanced(uint64_t state, uint64_t inc, uint64_t delta) {  // pcg32::advance
+	uint64_t cm = 0x5851f42d4c957f2dULL, cp = inc, am = 1u, ap = 0u;
+	while (delta > 0) {
+		if (delta & 1) { am *= cm; ap = ap * cm + cp; }
+		cp = (cm + 1) * cp;
+		cm *= cm;
+		delta /= 2;
+	}
+	return am * state + ap;
+}
+
+// signed_distance_raystab_kernel (triangle_bvh.cu:688-703)
+__global__ void __launch_bounds__(128) k_sdf_raystab(uint32_t n, const float* __restrict__ pos, const BvhNode* __restrict__ nodes,
+                                                     const float* __restrict__ tris, float* __restrict__ dist, bool upper_bounds) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const V p = vld(pos + 3 * (size_t)i);
+	const float max_d = upper_bounds ? dist[i] : MAX_DIST;
+	const float dsq = closest_dist_sq(p, nodes, tris, max_d * max_d);
+	const float d = dsq < 0.f ? 0.0f : sqrtf(dsq);
+	const uint64_t inc = 0xda3e39cb94b95bdbULL;  // default_rng_t
+	uint64_t st = pcg_advanced(0x853c49e6748fea9bULL, inc, 2ull * i);
+	const float ox = pcg_next_float(st, inc), oy = pcg_next_float(st, inc);
+	bool escaped = false;
+	for (uint32_t k = 0; k < 32 && !escaped; ++k) escaped = !ray_hits(p, fib_dir32(k, ox, oy), nodes, tris);
+	dist[i] = escaped ? d : -d;
+}
+}  // namespace
+
+void sdf_signed_distance(const SdfMeshDev& m, uint32_t n, const float* positions, float* distances, bool upper_bounds, hipStream_t s) {
+	if (n == 0) return;
+	NGP_CHECK(m.nodes, "sdf: mesh has no BVH");
+	k_sdf_raystab<<<div_round_up(n, 128), 128, 0, s>>>(n, positions, m.nodes, m.tris, distances, upper_bounds);
+	NGP_HIP(hipGetLastError());
+}
+
+}  // namespace ngp

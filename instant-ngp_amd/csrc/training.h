@@ -6,6 +6,7 @@
 // follows Testbed::train_image (src/testbed_image.cu:214-285); SDF sampling follows
 // Testbed::generate_training_samples_sdf (src/testbed_sdf.cu:1187-1275).
 #pragma once
+#include <vector>
 #include "common.h"
 #include "rng.h"
 
@@ -39,11 +40,22 @@ struct ImageSampleArgs {
 void image_generate_samples(const ImageSampleArgs& a, hipStream_t s);
 
 // ---- SDF (BASELINE config C5) -----------------------------------------------------------------
+struct BvhNode {                  // TriangleBvhNode (triangle_bvh.cuh:28-32)
+	float lo[3], hi[3];               // bounding box
+	int32_t left, right;              // children [left, right) or, negative, leaf triangles [-left-1, -right-1)
+};
 struct SdfMeshDev {
 	uint32_t n_triangles;
-	const float* tris;                // [n x 9] vertices a, b, c
+	const float* tris;                // [n x 9] vertices a, b, c, in BVH order
 	const float* cdf;                 // [n] inclusive area CDF normalised to 1 (triangle_cdf)
+	const BvhNode* nodes;             // 4-ary BVH (bvh.hip)
 };
+// TriangleBvh4::build (triangle_bvh.cu:540-617): reorders tris [n x 9] in place, fills nodes
+void build_bvh4(float* tris, uint32_t n_triangles, uint32_t n_primitives_per_leaf, std::vector<BvhNode>& nodes);
+// signed_distance_gpu, EMeshSdfMode::Raystab (triangle_bvh.cu:436-476): upper_bounds = the distances
+// already hold upper bounds of the true distances (use_existing_distances_as_upper_bounds)
+void sdf_signed_distance(const SdfMeshDev& m, uint32_t n, const float* positions, float* distances, bool upper_bounds,
+                         hipStream_t s);
 struct SdfSampleArgs {
 	uint32_t n;                       // multiple of 8 (n/8 * {4 exact, 3 offset, 1 uniform})
 	HostPcg32 rng;
@@ -55,10 +67,6 @@ struct SdfSampleArgs {
 };
 // uniform draws, surface samples, offsets, uniform-in-AABB samples; unsigned upper bounds in distances
 void sdf_generate_samples(const SdfMeshDev& m, const SdfSampleArgs& a, hipStream_t s);
-// Brute-force signed distance (every triangle; the reference's TriangleBvh is SURVEY §8f "next"):
-// closest-triangle distance, sign by 32 Fibonacci stab rays with a default-seeded offset
-// (signed_distance_raystab, src/triangle_bvh.cu:415-433).
-void sdf_signed_distance_bruteforce(const SdfMeshDev& m, uint32_t n, const float* positions, float* distances, hipStream_t s);
 // tcnn shuffle (src/testbed_sdf.cu:1295-1296): out[perm(i)] = in[i], perm a bijection seeded by step.
 void sdf_shuffle(uint32_t n, uint32_t seed, const float* pos_in, const float* dist_in, float* pos_out, float* dist_out,
                  hipStream_t s);

@@ -216,94 +216,9 @@ void sdf_generate_samples(const SdfMeshDev& m, const SdfSampleArgs& a, hipStream
 	const uint32_t base = a.n / 8;
 	k_sdf_samples<<<div_round_up(a.n, 256), 256, 0, s>>>(m, a, 4 * base, 3 * base, base);
 	NGP_HIP(hipGetLastError());
-	sdf_signed_distance_bruteforce(m, 4 * base, a.positions + 3 * (size_t)(4 * base), a.distances + 4 * base, s);
-}
-
-// Triangle::distance_sq (triangle.cuh:66-85)
-__device__ float tri_distance_sq(const float* t, F3 pos) {
-	const F3 A = ld3(t), B = ld3(t + 3), Cc = ld3(t + 6);
-	const F3 v21 = sub(B, A), p1 = sub(pos, A);
-	const F3 v32 = sub(Cc, B), p2 = sub(pos, B);
-	const F3 v13 = sub(A, Cc), p3 = sub(pos, Cc);
-	const F3 nor = cross(v21, v13);
-	if (sgn(dot(cross(v21, nor), p1)) + sgn(dot(cross(v32, nor), p2)) + sgn(dot(cross(v13, nor), p3)) < 2.0f) {
-		const float e1 = len2(sub(mul(v21, clamp01(dot(v21, p1) / len2(v21))), p1));
-		const float e2 = len2(sub(mul(v32, clamp01(dot(v32, p2) / len2(v32))), p2));
-		const float e3 = len2(sub(mul(v13, clamp01(dot(v13, p3) / len2(v13))), p3));
-		return fminf(fminf(e1, e2), e3);
-	}
-	const float d = dot(nor, p1);
-	return d * d / len2(nor);
-}
-
-// Triangle::ray_intersect (triangle.cuh:44-58)
-__device__ float tri_ray(const float* t, F3 ro, F3 rd) {
-	const F3 A = ld3(t);
-	const F3 v1v0 = sub(ld3(t + 3), A), v2v0 = sub(ld3(t + 6), A), rov0 = sub(ro, A);
-	const F3 n = cross(v1v0, v2v0);
-	const F3 q = cross(rov0, rd);
-	const float d = 1.0f / dot(rd, n);
-	const float u = d * -dot(q, v2v0);
-	const float v = d * dot(q, v1v0);
-	float tt = d * -dot(n, rov0);
-	if (u < 0.0f || u > 1.0f || v < 0.0f || (u + v) > 1.0f || tt < 0.0f) tt = 3.402823466e38f;
-	return tt;
-}
-
-// fibonacci_dir<32> (random_val.cuh:84-99) + cylindrical_to_dir (:45-54)
-__device__ F3 fib_dir32(uint32_t i, float ox, float oy) {
-	const float eps = 1.33f;
-	const float golden = 1.6180339887498948482045868343656f;
-	float a = (i + eps) / (32 - 1 + 2 * eps) + ox;
-	float b = i / golden + oy;
-	a = a - floorf(a);
-	b = b - floorf(b);
-	const float cos_theta = -2.0f * a + 1.0f;
-	const float phi = 2.0f * 3.14159265358979323846f * (b - 0.5f);
-	const float sin_theta = sqrtf(fmaxf(1.0f - cos_theta * cos_theta, 0.0f));
-	float sp, cp;
-	sincosf(phi, &sp, &cp);
-	return F3{sin_theta * cp, sin_theta * sp, cos_theta};
-}
-
-__global__ void __launch_bounds__(128) k_sdf_bruteforce(const SdfMeshDev m, uint32_t n, const float* __restrict__ pos,
-                                                        float* __restrict__ dist, float ox, float oy) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= n) return;
-	const F3 p = ld3(pos + 3 * (size_t)i);
-	float best = 3.402823466e38f;
-	for (uint32_t t = 0; t < m.n_triangles; ++t) best = fminf(best, tri_distance_sq(m.tris + 9 * (size_t)t, p));
-	const float d = sqrtf(best);
-	// signed_distance_raystab (triangle_bvh.cu:415-433): positive if any of 32 stab rays escapes
-	// (no triangle hit closer than MAX_DIST = 10)
-	bool escaped = false;
-	for (uint32_t k = 0; k < 32 && !escaped; ++k) {
-		const F3 dir = fib_dir32(k, ox, oy);
-		float mint = 10.0f;
-		for (uint32_t t = 0; t < m.n_triangles; ++t) mint = fminf(mint, tri_ray(m.tris + 9 * (size_t)t, p, dir));
-		escaped = !(mint < 10.0f);
-	}
-	dist[i] = escaped ? d : -d;
-}
-
-void sdf_signed_distance_bruteforce(const SdfMeshDev& m, uint32_t n, const float* positions, float* distances, hipStream_t s) {
-	if (n == 0) return;
-	// random_val_2d of a default-constructed pcg32 (state 0x853c49e6748fea9b, stream 0xda3e39cb94b95bdb)
-	uint64_t st = 0x853c49e6748fea9bULL;
-	const uint64_t inc = 0xda3e39cb94b95bdbULL;
-	float o[2];
-	for (int k = 0; k < 2; ++k) {
-		const uint64_t old = st;
-		st = old * 0x5851f42d4c957f2dULL + inc;
-		const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u), rot = (uint32_t)(old >> 59u);
-		const uint32_t u = (xs >> rot) | (xs << ((~rot + 1u) & 31));
-		uint32_t bits = (u >> 9) | 0x3f800000u;
-		float f;
-		memcpy(&f, &bits, 4);
-		o[k] = f - 1.0f;
-	}
-	k_sdf_bruteforce<<<div_round_up(n, 128), 128, 0, s>>>(m, n, positions, distances, o[0], o[1]);
-	NGP_HIP(hipGetLastError());
+	// the distances written above are upper bounds of the true ones (perturbation length / aabb
+	// diagonal x 1.001): signed_distance_gpu(..., use_existing_distances_as_upper_bounds = true)
+	sdf_signed_distance(m, 4 * base, a.positions + 3 * (size_t)(4 * base), a.distances + 4 * base, true, s);
 }
 
 // ---- shuffle --------------------------------------------------------------------------------

@@ -46,14 +46,18 @@ struct ngp_image {
 
 struct ngp_sdf_mesh {
 	uint32_t n_triangles = 0;
-	float* tris = nullptr;  // [n x 9]
+	float* tris = nullptr;  // [n x 9], BVH order
 	float* cdf = nullptr;   // [n]
+	BvhNode* nodes = nullptr;
+	uint32_t n_nodes = 0;
+	std::vector<float> tris_host;
 	Buf perturbations;
 	~ngp_sdf_mesh() {
 		if (tris) (void)hipFree(tris);
 		if (cdf) (void)hipFree(cdf);
+		if (nodes) (void)hipFree(nodes);
 	}
-	SdfMeshDev dev() const { return SdfMeshDev{n_triangles, tris, cdf}; }
+	SdfMeshDev dev() const { return SdfMeshDev{n_triangles, tris, cdf, nodes}; }
 };
 
 #define TRY(...)                                   \
@@ -146,6 +150,15 @@ int ngp_sdf_mesh_create(uint32_t n_triangles, const float* tris_host, ngp_sdf_me
 	TRY({
 		auto m = std::make_unique<ngp_sdf_mesh>();
 		m->n_triangles = n_triangles;
+		// Testbed::load_mesh (testbed_sdf.cu:1155-1172): the BVH build reorders the triangles, then the
+		// surface-area distribution is built over that order
+		m->tris_host.assign(tris_host, tris_host + (size_t)n_triangles * 9);
+		std::vector<BvhNode> nodes;
+		build_bvh4(m->tris_host.data(), n_triangles, 8, nodes);
+		tris_host = m->tris_host.data();
+		m->n_nodes = (uint32_t)nodes.size();
+		NGP_HIP(hipMalloc(&m->nodes, nodes.size() * sizeof(BvhNode)));
+		NGP_HIP(hipMemcpy(m->nodes, nodes.data(), nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
 		// triangle_distribution.build(surface areas) (testbed_sdf.cu:1167-1172, discrete_distribution.h:20-36)
 		std::vector<float> w(n_triangles), cdf(n_triangles);
 		float total = 0.f;
@@ -173,6 +186,25 @@ int ngp_sdf_mesh_create(uint32_t n_triangles, const float* tris_host, ngp_sdf_me
 
 void ngp_sdf_mesh_destroy(ngp_sdf_mesh* m) { delete m; }
 
+int ngp_sdf_bvh_build(float* tris, uint32_t n_triangles, uint32_t n_primitives_per_leaf, void* nodes_out, uint32_t* n_nodes) {
+	ARG(tris && n_nodes && n_primitives_per_leaf >= 1);
+	TRY({
+		std::vector<float> work(tris, tris + (size_t)n_triangles * 9);
+		std::vector<BvhNode> nodes;
+		build_bvh4(work.data(), n_triangles, n_primitives_per_leaf, nodes);
+		if (!nodes_out) { *n_nodes = (uint32_t)nodes.size(); return NGP_OK; }
+		NGP_CHECK(*n_nodes >= nodes.size(), "bvh: node buffer too small");
+		std::copy(work.begin(), work.end(), tris);
+		std::copy(nodes.begin(), nodes.end(), (BvhNode*)nodes_out);
+		*n_nodes = (uint32_t)nodes.size();
+	});
+}
+
+int ngp_sdf_mesh_triangles(const ngp_sdf_mesh* m, float* tris_out) {
+	ARG(m && tris_out);
+	TRY({ std::copy(m->tris_host.begin(), m->tris_host.end(), tris_out); });
+}
+
 int ngp_sdf_generate_training_samples(ngp_sdf_mesh* m, void* stream, uint32_t n, ngp_rng* rng, const float* aabb_min,
                                       const float* aabb_max, float stddev, float* positions, float* distances) {
 	ARG(m && rng && aabb_min && aabb_max && n % 8 == 0 && (n == 0 || (positions && distances)));
@@ -195,7 +227,7 @@ int ngp_sdf_generate_training_samples(ngp_sdf_mesh* m, void* stream, uint32_t n,
 
 int ngp_sdf_signed_distance(ngp_sdf_mesh* m, void* stream, uint32_t n, const float* positions, float* distances) {
 	ARG(m && (n == 0 || (positions && distances)));
-	TRY({ sdf_signed_distance_bruteforce(m->dev(), n, positions, distances, S(stream)); });
+	TRY({ sdf_signed_distance(m->dev(), n, positions, distances, false, S(stream)); });
 }
 
 int ngp_sdf_shuffle(void* stream, uint32_t n, uint32_t seed, const float* positions, const float* distances,

@@ -3,8 +3,8 @@
 `load_mesh` restates Testbed::load_mesh's normalisation (testbed_sdf.cu:1120-1165); `SdfTraining` is
 training_prep_sdf + train_sdf (:1289-1330): every step regenerates the batch online
 (generate_training_samples_sdf, :1187-1275, non-octree branch), shuffles it and runs tcnn
-training_step with the MAPE loss (configs/sdf/base.json) and the optimizer. Signed distances are
-computed on the GPU by brute force over the triangles (the reference's BVH is SURVEY §8f "next").
+training_step with the MAPE loss (configs/sdf/base.json) and the optimizer. Signed distances come
+from a 4-ary triangle BVH (TriangleBvh4, src/triangle_bvh.cu; csrc/bvh.hip) traversed on the GPU.
 """
 import ctypes as C
 
@@ -37,12 +37,30 @@ def load_mesh(vertices):
             bounding_radius)
 
 
+BVH_NODE = np.dtype([("lo", np.float32, 3), ("hi", np.float32, 3), ("left", np.int32), ("right", np.int32)])
+
+
+def build_bvh(triangles, n_primitives_per_leaf=8):
+    """TriangleBvh4::build on the host (no GPU): (triangles in BVH order, nodes structured array)."""
+    tris = np.array(triangles, dtype=np.float32).reshape(-1, 9)
+    n = C.c_uint32(0)
+    check(lib().ngp_sdf_bvh_build(tris.ctypes.data, tris.shape[0], n_primitives_per_leaf, None, C.byref(n)))
+    nodes = np.zeros(n.value, dtype=BVH_NODE)
+    check(lib().ngp_sdf_bvh_build(tris.ctypes.data, tris.shape[0], n_primitives_per_leaf, nodes.ctypes.data, C.byref(n)))
+    return tris, nodes
+
+
 class SdfMesh:
+    """The mesh on the device with its BVH. `triangles` is the BVH order (the build reorders them, as
+    TriangleBvh4::build reorders m_sdf.triangles_cpu; surface sampling draws from that order)."""
+
     def __init__(self, triangles):
-        self.triangles = np.ascontiguousarray(triangles, dtype=np.float32).reshape(-1, 9)
+        tris = np.ascontiguousarray(triangles, dtype=np.float32).reshape(-1, 9)
         h = C.c_void_p()
-        check(lib().ngp_sdf_mesh_create(self.triangles.shape[0], self.triangles.ctypes.data, C.byref(h)))
+        check(lib().ngp_sdf_mesh_create(tris.shape[0], tris.ctypes.data, C.byref(h)))
         self.handle = h
+        self.triangles = np.empty_like(tris)
+        check(lib().ngp_sdf_mesh_triangles(h, self.triangles.ctypes.data))
 
     def signed_distance(self, positions, stream=None):
         out = torch.empty(positions.shape[0], dtype=torch.float32, device=positions.device)

@@ -246,11 +246,13 @@ static F3 fib_dir32(uint32_t i, float ox, float oy) {
 	return r;
 }
 
+/* signed_distance_raystab_kernel (src/triangle_bvh.cu:688-703) over every triangle (the BVH only
+ * prunes): per element i a default pcg32 advanced by 2 i gives the stab-ray offset random_val_2d. */
 EXPORT void orc_sdf_signed_distance(uint32_t n, const float* positions, uint32_t n_tris, const float* tris, float* distances) {
-	/* random_val_2d of a default-constructed pcg32 */
-	orc_pcg32 r0 = {0x853c49e6748fea9bULL, 0xda3e39cb94b95bdbULL};
-	const float ox = orc_pcg32_next_float(&r0), oy = orc_pcg32_next_float(&r0);
 	for (uint32_t i = 0; i < n; ++i) {
+		orc_pcg32 r0 = {0x853c49e6748fea9bULL, 0xda3e39cb94b95bdbULL};
+		orc_pcg32_advance(&r0, 2 * (int64_t)i);
+		const float ox = orc_pcg32_next_float(&r0), oy = orc_pcg32_next_float(&r0);
 		const F3 p = ld3(positions + 3 * (size_t)i);
 		float best = 3.402823466e38f;
 		for (uint32_t t = 0; t < n_tris; ++t) best = fminf(best, tri_distance_sq(tris + 9 * (size_t)t, p));

@@ -100,6 +100,7 @@ def test_sdf_samples_match_oracle(pkg, orc):
     st = pkg.sdf.SdfTraining(net, tr, mesh, amin, amax, brad, seed=11, batch_size=2048)
     pos, dist = st.generate_training_samples(2048)
     r = orc.Rng(11)
+    tris = mesh.triangles  # BVH order: the surface CDF follows it (testbed_sdf.cu:1157-1172)
     rpos, rdist = orc.sdf_samples(2048, r, tris, amin, amax, st.stddev)
     base = 2048 // 8
     gp, gd = pos.cpu().numpy(), dist.cpu().numpy()
@@ -138,3 +139,19 @@ def test_sdf_training_converges(pkg):
     # MAPE is dominated by the on-surface samples (target 0, scale 1/0.01); it drops after an early spike
     assert np.mean(losses[-10:]) < 0.7 * max(losses[:10]), losses[::12]
     assert np.mean(losses[-10:]) < np.mean(losses[10:20]), losses[::12]
+
+
+def test_sdf_bvh_signed_distance_matches_bruteforce(pkg, orc):
+    """BVH raystab signed distance (csrc/bvh.hip) == the oracle's brute force over every triangle
+    (closest distance and the 32-stab-ray sign with per-sample offsets), on a 20k-triangle mesh."""
+    verts = pkg.synthetic.icosphere(5, radius=0.3, bumps=0.3)
+    tris, amin, amax, brad = pkg.sdf.load_mesh(verts)
+    mesh = pkg.sdf.SdfMesh(tris)
+    assert mesh.triangles.shape[0] >= 20000
+    g = np.random.default_rng(3)
+    pts = np.concatenate([g.uniform(0.0, 1.0, (256, 3)),  # uniform in the cube (mostly outside)
+                          (0.5 + g.normal(0.0, 0.12, (256, 3)))]).astype(np.float32)  # near the surface / inside
+    got = mesh.signed_distance(torch.from_numpy(pts).cuda()).cpu().numpy()
+    ref = orc.sdf_signed_distance(pts, mesh.triangles)
+    assert np.mean(ref < 0) > 0.1 and np.mean(ref > 0) > 0.1
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-5)

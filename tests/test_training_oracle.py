@@ -103,3 +103,26 @@ def test_load_mesh_normalisation(pkg):
     np.testing.assert_allclose((v.max(0) + v.min(0)) / 2, 0.5, atol=1e-5)
     assert np.all(amin >= 0) and np.all(amax <= 1) and np.all(amin < v.min(0)) and np.all(amax > v.max(0))
     assert abs(brad - np.sqrt(0.75)) < 1e-6
+
+
+def test_bvh_build_structure():
+    """TriangleBvh4::build (host, csrc/bvh.hip): 4-ary nodes, every triangle in exactly one leaf of at
+    most 8, child boxes contain their triangles, and the reordering is a permutation."""
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    verts = pkg.synthetic.icosphere(3, radius=0.3, bumps=0.3)
+    tris, _, _, _ = pkg.sdf.load_mesh(verts)
+    out, nodes = pkg.sdf.build_bvh(tris, 8)
+    assert sorted(map(bytes, out)) == sorted(map(bytes, tris))
+    seen = np.zeros(len(out), bool)
+    for n in nodes:
+        if n["left"] < 0:
+            lo, hi = -n["left"] - 1, -n["right"] - 1
+            assert 0 < hi - lo <= 8
+            assert not seen[lo:hi].any()
+            seen[lo:hi] = True
+            v = out[lo:hi].reshape(-1, 3)
+            assert np.all(v >= n["lo"]) and np.all(v <= n["hi"])
+        else:
+            assert n["right"] - n["left"] == 4
+    assert seen.all()
