@@ -304,8 +304,9 @@ int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** density_grid, uint8_t*
 
 /* Rendering (NerfTracer::init_rays_from_camera + trace + shade, testbed_nerf.cu:2229-2659,
  * 948-1196, 2164-2226; ERenderMode::Shade, pinhole). camera: the view (xform after
- * nerf_matrix_to_ngp, focal length in pixels, principal point); screen centre = 1 - principal point
- * (set_camera_to_training_view, testbed.cu:852). spp samples starting at sample_index are averaged;
+ * nerf_matrix_to_ngp, focal length in pixels, principal point); the screen centre is
+ * render_screen_center(1 - principal point) = the principal point (set_camera_to_training_view,
+ * testbed.cu:852, 4376-4379). spp samples starting at sample_index are averaged;
  * out_rgba: device float [height x width x 4], linear colours composited over background_rgba
  * (host, linear; NULL = transparent black). bitfield: the occupancy bitfield (NULL = march everywhere). */
 typedef struct ngp_nerf_renderer ngp_nerf_renderer;

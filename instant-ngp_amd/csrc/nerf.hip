@@ -1071,7 +1071,8 @@ __global__ void k_render_init(RenderArgs a, Payload* __restrict__ pay, float* __
 	float ox, oy;
 	ld_random_pixel_offset(a.snap_to_pixel_centers ? 0u : a.sample_index, &ox, &oy);
 	const float u = ((float)x + ox) / (float)W, v = ((float)y + oy) / (float)H;
-	// uv_to_ray (common_device.cuh:443-510), screen_center = 1 - principal point (testbed.cu:852), with
+	// uv_to_ray (common_device.cuh:443-510), screen_center = render_screen_center(1 - principal point)
+	// (testbed.cu:852, 4376-4379, 4541) = the principal point, with
 	// the training view's lens (render_with_lens_distortion, testbed.cu:845-846)
 	float dx = (u - a.screen_center[0]) * (float)W / a.focal[0];
 	float dy = (v - a.screen_center[1]) * (float)H / a.focal[1];

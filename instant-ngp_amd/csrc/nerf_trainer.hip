@@ -383,8 +383,9 @@ int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_confi
 		RenderArgs a{};
 		a.width = camera->width; a.height = camera->height;
 		a.focal[0] = camera->focal_length[0]; a.focal[1] = camera->focal_length[1];
-		a.screen_center[0] = 1.0f - camera->principal_point[0];  // set_camera_to_training_view (testbed.cu:852)
-		a.screen_center[1] = 1.0f - camera->principal_point[1];
+		// m_screen_center = 1 - principal point (set_camera_to_training_view, testbed.cu:852), then
+		// render_screen_center (testbed.cu:4376-4379, zoom 1): (0.5 - m_screen_center) + 0.5 = principal point
+		for (int k = 0; k < 2; ++k) a.screen_center[k] = (0.5f - (1.0f - camera->principal_point[k])) * 1.0f + 0.5f;
 		effective_camera_matrix(camera->xform, a.cam);
 		NGP_CHECK(camera->lens_mode <= LENS_OPENCV_FISHEYE, "render: unsupported lens mode");
 		a.lens_mode = camera->lens_mode;

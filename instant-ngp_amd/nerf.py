@@ -309,7 +309,7 @@ def ground_truth_linear(rgba8, background=(0.0, 0.0, 0.0)):
     alpha in linear space, composited over the linear background), as a float [H, W, 4] tensor."""
     px = torch.as_tensor(rgba8).float() / 255.0
     a = px[..., 3:4]
-    rgb = srgb_to_linear(px[..., :3]) * a + torch.tensor(background, dtype=torch.float32) * (1 - a)
+    rgb = srgb_to_linear(px[..., :3]) * a + torch.tensor(background, dtype=torch.float32, device=px.device) * (1 - a)
     return torch.cat([rgb, torch.ones_like(a)], dim=-1)
 
 

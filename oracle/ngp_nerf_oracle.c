@@ -641,8 +641,11 @@ EXPORT void orc_nerf_render_march(const ocfg* c, const oimg* cam, const uint8_t*
 	for (uint32_t i = 0; i < W * H; ++i) {
 		const uint32_t x = i % W, y = i / W;
 		const float u = ((float)x + ox) / (float)W, v = ((float)y + oy) / (float)H;
-		float dx = (u - (1.0f - cam->principal_point[0])) * (float)W / cam->focal_length[0];
-		float dy = (v - (1.0f - cam->principal_point[1])) * (float)H / cam->focal_length[1];
+		/* screen centre = render_screen_center(m_screen_center = 1 - principal point), testbed.cu:852,
+		 * 4376-4379 (zoom 1) = (0.5 - (1 - pp)) + 0.5 */
+		const float scx = (0.5f - (1.0f - cam->principal_point[0])) + 0.5f, scy = (0.5f - (1.0f - cam->principal_point[1])) + 0.5f;
+		float dx = (u - scx) * (float)W / cam->focal_length[0];
+		float dy = (v - scy) * (float)H / cam->focal_length[1];
 		lens_undistort(cam->lens_mode, cam->lens_params, &dx, &dy);
 		float d[3] = {m[0] * dx + m[3] * dy + m[6], m[1] * dx + m[4] * dy + m[7], m[2] * dx + m[5] * dy + m[8]};
 		const float o[3] = {m[9], m[10], m[11]};

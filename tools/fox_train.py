@@ -60,6 +60,12 @@ def main():
         img = r.render(net, cfg, d.images[i], run.bitfield, spp=args.spp, min_transmittance=1e-4, background=(0, 0, 0, 1))
         ref = pkg.nerf.ground_truth_linear(torch.from_numpy(d.rgba8[i]).cuda())
         ps.append(pkg.nerf.psnr(img, ref)[0])
+    # training views through the same renderer (fit quality, as opposed to held-out generalisation)
+    ps_train = []
+    for i in train[::max(1, len(train) // 3)][:3]:
+        img = r.render(net, cfg, d.images[i], run.bitfield, spp=args.spp, min_transmittance=1e-4, background=(0, 0, 0, 1))
+        ref = pkg.nerf.ground_truth_linear(torch.from_numpy(d.rgba8[i]).cuda())
+        ps_train.append(pkg.nerf.psnr(img, ref)[0])
     torch.cuda.synchronize()
     t_render = time.time() - t_render
     h, w = d.rgba8[0].shape[:2]
@@ -67,6 +73,7 @@ def main():
         "metric": "training samples/sec + PSNR, NeRF fox (C3) on 1 MI355X",
         "value": samples / t_train, "unit": "samples/s",
         "psnr_heldout": float(np.mean(ps)) if ps else None, "psnr_views": [round(p, 2) for p in ps],
+        "psnr_train_views": [round(p, 2) for p in ps_train],
         "train_seconds": round(t_train, 2), "steps": steps, "ms_per_step": 1e3 * t_train / steps,
         "n_gpus": 1, "dtype": "f16",
         "data": f"data/nerf/fox: {len(d)} frames present ({w}x{h} JPEG, OpenCV lens), {len(train)} trained, "
