@@ -202,31 +202,6 @@ __device__ float closest_dist_sq(V p, const BvhNode* __restrict__ nodes, const f
 	return found ? best : -1.0f;
 }
 
-// any triangle hit closer than MAX_DIST along (o, d)? (ray_intersect(...).first >= 0, :240-284)
-__device__ bool ray_hits(V o, V d, const BvhNode* __restrict__ nodes, const float* __restrict__ tris) {
-	int stack[STACK];
-	int sp = 0;
-	stack[sp++] = 0;
-	while (sp > 0) {
-		const BvhNode node = nodes[stack[--sp]];
-		if (node.left < 0) {
-			const int end = -node.right - 1;
-			for (int i = -node.left - 1; i < end; ++i)
-				if (tri_ray_t(tris + 9 * (size_t)i, o, d) < MAX_DIST) return true;
-		} else {
-			float k[4];
-			int id[4];
-#pragma unroll
-			for (int c = 0; c < 4; ++c) { id[c] = node.left + c; k[c] = box_ray_t(nodes[node.left + c], o, d); }
-			sort4_desc(k, id);
-#pragma unroll
-			for (int c = 0; c < 4; ++c)
-				if (k[c] < MAX_DIST && sp < STACK) stack[sp++] = id[c];
-		}
-	}
-	return false;
-}
-
 // fibonacci_dir<32> (random_val.cuh:84-99) + cylindrical_to_dir (:45-54)
 __device__ V fib_dir32(uint32_t i, float ox, float oy) {
 	const float eps = 1.33f;
@@ -261,28 +236,69 @@ __device__ __forceinline__ uint64_t pcg_advanced(uint64_t state, uint64_t inc, u
 	return am * state + ap;
 }
 
-// signed_distance_raystab_kernel (triangle_bvh.cu:688-703)
-__global__ void __launch_bounds__(128) k_sdf_raystab(uint32_t n, const float* __restrict__ pos, const BvhNode* __restrict__ nodes,
-                                                     const float* __restrict__ tris, float* __restrict__ dist, bool upper_bounds) {
+// signed_distance_raystab_kernel (triangle_bvh.cu:688-703) in two launches. Distance: one thread per
+// point (closest_triangle under the upper bound). Sign: 32 lanes per point, lane k traces stab ray k —
+// the rays of one point traverse similar nodes, so the half-wave stays coherent where one thread would
+// run the 32 traversals back to back; the first lane whose ray escapes raises an LDS flag that stops the
+// others (the sign only asks whether any ray escapes).
+__global__ void __launch_bounds__(128) k_sdf_distance(uint32_t n, const float* __restrict__ pos, const BvhNode* __restrict__ nodes,
+                                                      const float* __restrict__ tris, float* __restrict__ dist, bool upper_bounds) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
-	const V p = vld(pos + 3 * (size_t)i);
 	const float max_d = upper_bounds ? dist[i] : MAX_DIST;
-	const float dsq = closest_dist_sq(p, nodes, tris, max_d * max_d);
-	const float d = dsq < 0.f ? 0.0f : sqrtf(dsq);
-	const uint64_t inc = 0xda3e39cb94b95bdbULL;  // default_rng_t
-	uint64_t st = pcg_advanced(0x853c49e6748fea9bULL, inc, 2ull * i);
-	const float ox = pcg_next_float(st, inc), oy = pcg_next_float(st, inc);
-	bool escaped = false;
-	for (uint32_t k = 0; k < 32 && !escaped; ++k) escaped = !ray_hits(p, fib_dir32(k, ox, oy), nodes, tris);
-	dist[i] = escaped ? d : -d;
+	const float dsq = closest_dist_sq(vld(pos + 3 * (size_t)i), nodes, tris, max_d * max_d);
+	dist[i] = dsq < 0.f ? 0.0f : sqrtf(dsq);
+}
+
+constexpr uint32_t SIGN_T = 256;  // 8 points per block
+__global__ void __launch_bounds__(SIGN_T) k_sdf_sign(uint32_t n, const float* __restrict__ pos, const BvhNode* __restrict__ nodes,
+                                                     const float* __restrict__ tris, float* __restrict__ dist) {
+	__shared__ uint32_t escaped[SIGN_T / 32];
+	const uint32_t g = threadIdx.x / 32, k = threadIdx.x % 32;
+	const uint32_t i = blockIdx.x * (SIGN_T / 32) + g;
+	if (k == 0) escaped[g] = 0u;
+	__syncthreads();
+	if (i < n) {
+		const V p = vld(pos + 3 * (size_t)i);
+		const uint64_t inc = 0xda3e39cb94b95bdbULL;  // default_rng_t advanced by 2 i
+		uint64_t st = pcg_advanced(0x853c49e6748fea9bULL, inc, 2ull * i);
+		const float ox = pcg_next_float(st, inc), oy = pcg_next_float(st, inc);
+		const V d = fib_dir32(k, ox, oy);
+		// any triangle closer than MAX_DIST along ray k? (stops early once another ray escaped)
+		int stack[STACK];
+		int sp = 0;
+		stack[sp++] = 0;
+		bool hit = false;
+		while (sp > 0 && !hit) {
+			if (__hip_atomic_load(&escaped[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+			const BvhNode node = nodes[stack[--sp]];
+			if (node.left < 0) {
+				const int end = -node.right - 1;
+				for (int t = -node.left - 1; t < end && !hit; ++t) hit = tri_ray_t(tris + 9 * (size_t)t, p, d) < MAX_DIST;
+			} else {
+				float kk[4];
+				int id[4];
+#pragma unroll
+				for (int c = 0; c < 4; ++c) { id[c] = node.left + c; kk[c] = box_ray_t(nodes[node.left + c], p, d); }
+				sort4_desc(kk, id);
+#pragma unroll
+				for (int c = 0; c < 4; ++c)
+					if (kk[c] < MAX_DIST && sp < STACK) stack[sp++] = id[c];
+			}
+		}
+		if (!hit && sp == 0) __hip_atomic_store(&escaped[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+	}
+	__syncthreads();
+	if (i < n && k == 0 && !escaped[g]) dist[i] = -dist[i];
 }
 }  // namespace
 
 void sdf_signed_distance(const SdfMeshDev& m, uint32_t n, const float* positions, float* distances, bool upper_bounds, hipStream_t s) {
 	if (n == 0) return;
 	NGP_CHECK(m.nodes, "sdf: mesh has no BVH");
-	k_sdf_raystab<<<div_round_up(n, 128), 128, 0, s>>>(n, positions, m.nodes, m.tris, distances, upper_bounds);
+	k_sdf_distance<<<div_round_up(n, 128), 128, 0, s>>>(n, positions, m.nodes, m.tris, distances, upper_bounds);
+	NGP_HIP(hipGetLastError());
+	k_sdf_sign<<<div_round_up(n, SIGN_T / 32), SIGN_T, 0, s>>>(n, positions, m.nodes, m.tris, distances);
 	NGP_HIP(hipGetLastError());
 }
 
