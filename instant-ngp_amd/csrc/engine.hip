@@ -147,6 +147,7 @@ struct ngp_model {
 	// dependency edge, which in a HIP graph is not free.
 	uint32_t overlap = 0;
 	bool fused_hist = true;                 // option "fused_hist": bucket histogram inside the training forward
+	bool fuse_infer = true;                 // option "fuse_infer": NerfNetwork inference encodes inside the MLP kernel
 	int grid_forward_mode = 0;              // option "grid_forward_mode": 0 auto, 1 per-sample rows, 2 XCD-partitioned
 	hipStream_t side = nullptr;             // overlaps fragments + bucket histogram with forward + MLP,
 	                                        // and the dW slab reduction with the grid backward
@@ -255,6 +256,10 @@ struct ngp_model {
 		          "model has no parameters: call ngp_model_set_params or create a trainer first");
 	}
 	const f16* pick(bool inference) const { return inference ? inference_params : params; }
+	bool fused_inference_ok() const {
+		return nerf && fuse_infer && !max_level_per_sample && nerf_mlp_fused_encoding_ok(grid, enc_width) && nplan.enc_steps == 1 &&
+		       nplan.d_hidden == 1 && nplan.r_hidden >= 1 && nplan.r_hidden <= 3;
+	}
 	f16x8* prep(hipStream_t s, bool inference) {
 		f16x8* f = (f16x8*)(inference ? frags_inf : frags).get((size_t)n_all_frags * 1024);
 		ProfScope ps("prepare_frags", s);
@@ -299,7 +304,11 @@ struct ngp_model {
 			a.frags = f; a.n_frags = n_all_frags; a.out = out; a.out_stride = out_stride; a.out_layout = out_layout;
 			a.dL_dout = dL; a.dL_stride = dL_stride; a.dL_denc = dL_denc; a.denc_stride = enc_width; a.dw_slab = slab;
 			a.n_matrix = (uint32_t)n_matrix(); a.density_woff = 0; a.rgb_woff = (uint32_t)mlp0_params;
-			ProfScope ps(mode == MLP_TRAIN ? "mlp_train" : mode == MLP_DENSITY ? "mlp_density" : "mlp_infer", s);
+			if (mode == MLP_INFER_ENC) {
+				a.table = pick(inference) + grid_offset(); a.max_level = max_level; a.gc = make_grid_const(grid);
+			}
+			ProfScope ps(mode == MLP_TRAIN ? "mlp_train" : mode == MLP_DENSITY ? "mlp_density"
+			             : mode == MLP_INFER_ENC ? "mlp_infer_enc" : "mlp_infer", s);
 			nerf_mlp_run(nplan, mode, a, s);
 		} else {
 			MlpArgs a{};
@@ -592,6 +601,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			m->grid_forward_mode = (int)value;
 		} else if (k == "fused_hist") {
 			m->fused_hist = value != 0;
+		} else if (k == "fuse_infer") {
+			m->fuse_infer = value != 0;
 		} else if (k == "win_debug") {
 			m->win_debug = (uint32_t)value;
 		} else {
@@ -632,10 +643,16 @@ int ngp_inference(ngp_model* m, void* stream, uint32_t n, const float* input, ui
 	NGP_TRY({
 		if (n == 0) return NGP_OK;
 		m->require_params(use_inference_params);
-		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
-		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, use_inference_params);
-		m->run_mlp(S(stream), MLP_INFER, n, input, input_stride, e, (f16*)output, output_stride, output_layout, nullptr, 0,
-		           nullptr, nullptr, use_inference_params);
+		if (m->fused_inference_ok()) {
+			// the encoding never reaches HBM: the MLP kernel gathers and blends the grid levels itself
+			m->run_mlp(S(stream), MLP_INFER_ENC, n, input, input_stride, nullptr, (f16*)output, output_stride, output_layout,
+			           nullptr, 0, nullptr, nullptr, use_inference_params);
+		} else {
+			f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
+			m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, use_inference_params);
+			m->run_mlp(S(stream), MLP_INFER, n, input, input_stride, e, (f16*)output, output_stride, output_layout, nullptr, 0,
+			           nullptr, nullptr, use_inference_params);
+		}
 		m->generation++;
 	});
 }

@@ -362,6 +362,8 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	using Lay = NerfLayout<ES, DH, RH>;
 	constexpr bool TRAIN = MODE == MLP_TRAIN;
 	constexpr bool DENSITY = MODE == MLP_DENSITY;
+	constexpr bool FUSE = MODE == MLP_INFER_ENC;
+	static_assert(!FUSE || ES == 1, "fused encoding: one 16-wide encoding step");
 	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (DENSITY ? Lay::F_R0 : Lay::N_FWD);
 	extern __shared__ __attribute__((aligned(16))) char smem[];
 	f16x8* lfrag = (f16x8*)smem;
@@ -383,27 +385,109 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	f16x8 xe_n[ES];
 	float cd_n[3] = {0.f, 0.f, 0.f};
 	f16x4 dl_n{};
+	// FUSE (MLP_INFER_ENC, ES == 1, F == 4): lane half h encodes levels 2h and 2h+1 of its sample (the 8
+	// features of its B operand). The next tile's corner gathers are issued with the other prefetches
+	// and blended at the top of the next iteration, so the gather latency hides under this tile's MFMAs.
+	// The positions are loaded one tile further ahead still, so the gather addresses never wait on a load.
+	f16x4 graw[FUSE ? 2 : 1][8];
+	float gfrac[FUSE ? 2 : 1][3];
+	float px_n[3];
+	// this lane's two levels, held in registers: GridConst indexed by a per-lane level would become
+	// kernarg loads with a full vmcnt wait inside the gather sequence
+	uint32_t lv_off[2], lv_T[2], lv_res[2];
+	float lv_scale[2];
+	bool lv_hashed[2], lv_active[2];
+	if constexpr (FUSE) {
+		const float ml = a.max_level * (float)a.gc.n_levels;
+#pragma unroll
+		for (int j = 0; j < 2; ++j) {
+			const uint32_t l0 = j, l1 = 2 + j;  // levels of lane half 0 and 1 (compile-time kernarg reads)
+			lv_off[j] = h ? a.gc.offsets[l1] : a.gc.offsets[l0];
+			lv_T[j] = h ? a.gc.offsets[l1 + 1] - a.gc.offsets[l1] : a.gc.offsets[l0 + 1] - a.gc.offsets[l0];
+			lv_res[j] = h ? a.gc.resolution[l1] : a.gc.resolution[l0];
+			lv_scale[j] = h ? a.gc.scale[l1] : a.gc.scale[l0];
+			lv_hashed[j] = (a.gc.hashed >> (h ? l1 : l0)) & 1u;
+			lv_active[j] = !((float)(h ? l1 : l0) >= ml + 1e-3f);
+		}
+	}
+	auto load_pos = [&](uint32_t tile) {
+		const uint32_t smp = tile * 32 + (lane & 31);
+		const float* cp = a.coords + (size_t)(smp < a.n ? smp : 0) * a.coord_stride;
+		px_n[0] = cp[0]; px_n[1] = cp[1]; px_n[2] = cp[2];
+	};
 	auto load_inputs = [&](uint32_t tile) {
 		const uint32_t smp = tile * 32 + (lane & 31);
 		const uint32_t ls = smp < a.n ? smp : 0;
+		if constexpr (FUSE) {
+			const float x[3] = {px_n[0], px_n[1], px_n[2]};
+			load_pos(tile + gridDim.x * 4);
 #pragma unroll
-		for (int s = 0; s < ES; ++s) xe_n[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
+			for (int j = 0; j < 2; ++j) {
+				// level_setup + corner_index (grid.h) with the level's constants in registers; dense and
+				// hashed indices are both formed and selected, so the two lane halves do not diverge
+				uint32_t base[3];
+#pragma unroll
+				for (int d = 0; d < 3; ++d) {
+					const float p = __builtin_fmaf(lv_scale[j], x[d], 0.5f);
+					const float t = floorf(p);
+					base[d] = (uint32_t)(int)t;
+					gfrac[j][d] = p - t;
+				}
+				const f16* tab = a.table + (size_t)lv_off[j] * 4;
+#pragma unroll
+				for (uint32_t k = 0; k < 8; ++k) {
+					const uint32_t cx = base[0] + (k & 1u), cy = base[1] + ((k >> 1) & 1u), cz = base[2] + ((k >> 2) & 1u);
+					const uint32_t ih = (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (lv_T[j] - 1u);
+					uint32_t id = cx + lv_res[j] * (cy + lv_res[j] * cz);
+					if (__builtin_expect(!lv_hashed[j] && id >= lv_T[j], 0)) id %= lv_T[j];
+					const uint32_t idx = lv_hashed[j] ? ih : id;
+					graw[j][k] = lv_active[j] ? *(const f16x4*)(tab + (size_t)idx * 4) : f16x4{};
+				}
+			}
+		} else {
+#pragma unroll
+			for (int s = 0; s < ES; ++s) xe_n[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
+		}
 		if constexpr (!DENSITY) {
 			const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
 			cd_n[0] = cd[0]; cd_n[1] = cd[1]; cd_n[2] = cd[2];
 		}
 		if constexpr (TRAIN) dl_n = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
 	};
-	if (blockIdx.x * 4 + wave < n_tiles) load_inputs(blockIdx.x * 4 + wave);
+	if (blockIdx.x * 4 + wave < n_tiles) {
+		if constexpr (FUSE) load_pos(blockIdx.x * 4 + wave);
+		load_inputs(blockIdx.x * 4 + wave);
+	}
 	for (uint32_t tile = blockIdx.x * 4 + wave; tile < n_tiles; tile += gridDim.x * 4) {
 		const uint32_t sample = tile * 32 + (lane & 31);
 		const bool valid = sample < a.n;
 		f16x8 xe[ES];
+		if constexpr (FUSE) {
+			// trilinear blend in k_grid_forward_rows' order (fp32 FMAs, one RNE rounding per feature)
+			f16x8 r;
 #pragma unroll
-		for (int s = 0; s < ES; ++s) xe[s] = valid ? xe_n[s] : f16x8{};
+			for (int j = 0; j < 2; ++j) {
+				float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+				for (uint32_t k = 0; k < 8; ++k) {
+					const float w = corner_weight<3>(gfrac[j], k);
+#pragma unroll
+					for (int f = 0; f < 4; ++f) acc[f] = __builtin_fmaf(w, (float)graw[j][k][f], acc[f]);
+				}
+#pragma unroll
+				for (int f = 0; f < 4; ++f) {
+					asm volatile("" : "+v"(acc[f]));
+					r[4 * j + f] = (f16)acc[f];
+				}
+			}
+			xe[0] = valid ? r : f16x8{};
+		} else {
+#pragma unroll
+			for (int s = 0; s < ES; ++s) xe[s] = valid ? xe_n[s] : f16x8{};
+		}
 		const float cdx = cd_n[0], cdy = cd_n[1], cdz = cd_n[2];
 		const f16x4 dl_cur = dl_n;
-		if (tile + gridDim.x * 4 < n_tiles) load_inputs(tile + gridDim.x * 4);
+		load_inputs(tile + gridDim.x * 4);  // unconditional (past-the-end tiles read sample 0): no phi copies
 
 		// ---- density forward -------------------------------------------------------------------
 		if constexpr (TRAIN) {
@@ -597,7 +681,19 @@ void nerf_mlp_run(const NerfMlpPlan& p, MlpMode mode, const NerfMlpArgs& a, hipS
 		case MLP_INFER: dispatch_nerf<MLP_INFER>(p, a, s); break;
 		case MLP_TRAIN: dispatch_nerf<MLP_TRAIN>(p, a, s); break;
 		case MLP_DENSITY: dispatch_nerf<MLP_DENSITY>(p, a, s); break;
+		case MLP_INFER_ENC: {
+			const uint32_t key = p.enc_steps * 100 + p.d_hidden * 10 + p.r_hidden;
+			if (key == 112) launch_nerf<1, 1, 2, MLP_INFER_ENC>(a, s);
+			else if (key == 111) launch_nerf<1, 1, 1, MLP_INFER_ENC>(a, s);
+			else if (key == 113) launch_nerf<1, 1, 3, MLP_INFER_ENC>(a, s);
+			else throw Error("NerfNetwork: fused-encoding inference needs one encoding step and one density hidden layer");
+			break;
+		}
 	}
+}
+
+bool nerf_mlp_fused_encoding_ok(const GridDesc& g, uint32_t enc_width) {
+	return g.n_dims == 3 && g.n_levels == 4 && g.n_features == 4 && enc_width == 16;
 }
 
 // ------------------------------------------------------------------------------------------------

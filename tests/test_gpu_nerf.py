@@ -258,3 +258,32 @@ def test_inference_rgbd_layout(pkg):
     torch.cuda.synchronize()
     assert rgbd.shape == (n, 4)
     np.testing.assert_array_equal(rgbd.cpu().numpy().view(np.uint16), full[:, :4].cpu().numpy().view(np.uint16))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log2_T,max_level", [(15, 1.0), (19, 1.0), (19, 0.6)])
+def test_fused_encoding_inference_bitwise(pkg, log2_T, max_level):
+    """NerfNetwork inference with the grid encoding inside the MLP kernel (option fuse_infer, default) is
+    bit-identical to encode-then-MLP (fuse_infer=0) for every output layout, dense and hashed levels,
+    positions outside the unit cube and a lowered max level."""
+    cfg = pkg.nerf_config("C2")
+    cfg["encoding"]["log2_hashmap_size"] = log2_T
+    net = pkg.create_nerf_network(cfg)
+    g = np.random.default_rng(log2_T)
+    params = torch.from_numpy((g.standard_normal(net.n_params) * 0.3).astype(np.float16)).cuda()
+    net.set_params(params, params)
+    net.set_max_level(max_level)
+    n = 5000  # ragged tail
+    x = np.zeros((n, 7), np.float32)
+    x[:, :3] = g.uniform(-0.1, 1.1, (n, 3))
+    x[:, 4:] = g.standard_normal((n, 3))
+    x[:, 4:] /= np.linalg.norm(x[:, 4:], axis=1, keepdims=True)
+    xt = torch.from_numpy(x).cuda()
+    outs = {}
+    for fuse in (1, 0):
+        net.set_option("fuse_infer", fuse)
+        for layout in (pkg.LAYOUT_AOS, pkg.LAYOUT_SOA, pkg.LAYOUT_AOS_RGBD):
+            outs[fuse, layout] = net.inference(xt, layout=layout).cpu().numpy().view(np.uint16)
+    for layout in (pkg.LAYOUT_AOS, pkg.LAYOUT_SOA, pkg.LAYOUT_AOS_RGBD):
+        np.testing.assert_array_equal(outs[1, layout], outs[0, layout])
+    assert np.isfinite(outs[1, pkg.LAYOUT_AOS].view(np.float16)[:, :4].astype(np.float32)).all()

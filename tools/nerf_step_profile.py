@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--measure", type=int, default=200)
     ap.add_argument("--images", type=int, default=100)
     ap.add_argument("--res", type=int, default=800)
+    ap.add_argument("--option", action="append", default=[], help="model option key=value (ngp_model_set_option)")
     args = ap.parse_args()
     from __graft_entry__ import load_package
     pkg = load_package()
@@ -33,6 +34,9 @@ def main():
     ncfg = pkg.nerf_config("C2")
     net = pkg.create_nerf_network(ncfg)
     tr = pkg.Trainer(net, ncfg["optimizer"])
+    for kv in args.option:
+        key, value = kv.split("=")
+        net.set_option(key, float(value))
     run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
     lib = pkg.lib()
     t0 = time.time()
