@@ -148,6 +148,8 @@ struct ngp_model {
 	uint32_t overlap = 0;
 	bool fused_hist = true;                 // option "fused_hist": bucket histogram inside the training forward
 	bool fuse_infer = true;                 // option "fuse_infer": NerfNetwork inference encodes inside the MLP kernel
+	bool fuse_train = false;                // option "fuse_train": ... and the training forward_backward too (off: the
+	                                        // training kernel runs 1 wave/SIMD, the gathers are not hidden; C2 0.157 -> 0.161 ms)
 	int grid_forward_mode = 0;              // option "grid_forward_mode": 0 auto, 1 per-sample rows, 2 XCD-partitioned
 	hipStream_t side = nullptr;             // overlaps fragments + bucket histogram with forward + MLP,
 	                                        // and the dW slab reduction with the grid backward
@@ -256,10 +258,12 @@ struct ngp_model {
 		          "model has no parameters: call ngp_model_set_params or create a trainer first");
 	}
 	const f16* pick(bool inference) const { return inference ? inference_params : params; }
-	bool fused_inference_ok() const {
-		return nerf && fuse_infer && !max_level_per_sample && nerf_mlp_fused_encoding_ok(grid, enc_width) && nplan.enc_steps == 1 &&
+	bool fused_encoding_ok() const {
+		return nerf && !max_level_per_sample && nerf_mlp_fused_encoding_ok(grid, enc_width) && nplan.enc_steps == 1 &&
 		       nplan.d_hidden == 1 && nplan.r_hidden >= 1 && nplan.r_hidden <= 3;
 	}
+	bool fused_inference_ok() const { return fuse_infer && fused_encoding_ok(); }
+	bool fused_training_ok() const { return fuse_train && fused_encoding_ok(); }
 	f16x8* prep(hipStream_t s, bool inference) {
 		f16x8* f = (f16x8*)(inference ? frags_inf : frags).get((size_t)n_all_frags * 1024);
 		ProfScope ps("prepare_frags", s);
@@ -304,11 +308,11 @@ struct ngp_model {
 			a.frags = f; a.n_frags = n_all_frags; a.out = out; a.out_stride = out_stride; a.out_layout = out_layout;
 			a.dL_dout = dL; a.dL_stride = dL_stride; a.dL_denc = dL_denc; a.denc_stride = enc_width; a.dw_slab = slab;
 			a.n_matrix = (uint32_t)n_matrix(); a.density_woff = 0; a.rgb_woff = (uint32_t)mlp0_params;
-			if (mode == MLP_INFER_ENC) {
+			if (mode == MLP_INFER_ENC || mode == MLP_TRAIN_ENC) {
 				a.table = pick(inference) + grid_offset(); a.max_level = max_level; a.gc = make_grid_const(grid);
 			}
 			ProfScope ps(mode == MLP_TRAIN ? "mlp_train" : mode == MLP_DENSITY ? "mlp_density"
-			             : mode == MLP_INFER_ENC ? "mlp_infer_enc" : "mlp_infer", s);
+			             : mode == MLP_INFER_ENC ? "mlp_infer_enc" : mode == MLP_TRAIN_ENC ? "mlp_train_enc" : "mlp_infer", s);
 			nerf_mlp_run(nplan, mode, a, s);
 		} else {
 			MlpArgs a{};
@@ -326,7 +330,9 @@ struct ngp_model {
 		f16* dL_denc = (f16*)denc.get((size_t)n * enc_width * sizeof(f16));
 		const uint32_t blocks = nerf ? nerf_mlp_train_blocks(n) : mlp_train_blocks(n);
 		float* slab = (float*)slabs.get((size_t)blocks * n_matrix() * sizeof(float));
-		run_mlp(s, MLP_TRAIN, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride, dL_denc, slab, false);
+		// encbuf == nullptr: the MLP kernel encodes the positions itself (fused_training_ok)
+		run_mlp(s, encbuf ? MLP_TRAIN : MLP_TRAIN_ENC, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride,
+		        dL_denc, slab, false);
 		// the dW slab reduction (MLP section of the gradient) and the grid backward (grid section) are
 		// independent: for large batches the reduction runs on the side stream under the grid backward
 		const bool ovl = use_sorted(n) && (overlap & 4);
@@ -603,6 +609,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			m->fused_hist = value != 0;
 		} else if (k == "fuse_infer") {
 			m->fuse_infer = value != 0;
+		} else if (k == "fuse_train") {
+			m->fuse_train = value != 0;
 		} else if (k == "win_debug") {
 			m->win_debug = (uint32_t)value;
 		} else {
@@ -711,8 +719,14 @@ int ngp_forward_backward(ngp_model* m, void* stream, uint32_t n, const float* in
 		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
 		m->generation++;
 		m->prepare_grid_backward_async(S(stream), n, input, input_stride);
-		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, false, true);
-		m->train_pass(S(stream), n, input, input_stride, e, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode);
+		if (m->fused_training_ok()) {
+			// no encoding pass: the MLP kernel encodes, the sorted backward counts its own histogram
+			m->sc_hist_done = false;
+			m->train_pass(S(stream), n, input, input_stride, nullptr, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode);
+		} else {
+			m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, false, true);
+			m->train_pass(S(stream), n, input, input_stride, e, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode);
+		}
 	});
 }
 

@@ -51,7 +51,7 @@ struct NerfMlpArgs {
 	uint32_t n_matrix;                            // matrix params = density MLP + rgb MLP
 	uint32_t n_reg;                               // LDS regions of the dW block reduction (set at launch)
 	uint32_t density_woff, rgb_woff;              // parameter offsets of the two MLPs
-	// MLP_INFER_ENC only: the density network's input is encoded in the kernel (hash-grid gather and
+	// MLP_INFER_ENC / MLP_TRAIN_ENC: the density network's input is encoded in the kernel (hash-grid gather and
 	// trilinear blend of the sample's levels, same arithmetic as k_grid_forward_rows) instead of read
 	const f16* table;                             // grid parameters [entries x F]
 	float max_level;                              // tcnn set_max_level (global; per-sample masks not fused)
@@ -88,8 +88,8 @@ MlpPlan make_mlp_plan(uint32_t enc_width, uint32_t width, uint32_t hidden, uint3
 
 void prepare_frags(const FragDesc* descs_dev, uint32_t n_frags, const f16* params, f16x8* frags, hipStream_t s);
 
-enum MlpMode : uint32_t { MLP_INFER = 0, MLP_TRAIN = 1, MLP_DENSITY = 2, MLP_INFER_ENC = 3 };
-// MLP_INFER_ENC is fused for 3D grids with 4 levels of 4 features (one 16-wide encoding step: C2)
+enum MlpMode : uint32_t { MLP_INFER = 0, MLP_TRAIN = 1, MLP_DENSITY = 2, MLP_INFER_ENC = 3, MLP_TRAIN_ENC = 4 };
+// MLP_INFER_ENC / MLP_TRAIN_ENC are fused for 3D grids with 4 levels of 4 features (one 16-wide encoding step: C2)
 bool nerf_mlp_fused_encoding_ok(const GridDesc& g, uint32_t enc_width);
 
 // Launch sizes for the training kernel: one persistent block per CU (slab count = blocks).

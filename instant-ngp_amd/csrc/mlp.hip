@@ -360,9 +360,9 @@ struct NerfLayout {
 template <int ES, int DH, int RH, int MODE>
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_nerf_mlp(const NerfMlpArgs a) {
 	using Lay = NerfLayout<ES, DH, RH>;
-	constexpr bool TRAIN = MODE == MLP_TRAIN;
+	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_TRAIN_ENC;
 	constexpr bool DENSITY = MODE == MLP_DENSITY;
-	constexpr bool FUSE = MODE == MLP_INFER_ENC;
+	constexpr bool FUSE = MODE == MLP_INFER_ENC || MODE == MLP_TRAIN_ENC;
 	static_assert(!FUSE || ES == 1, "fused encoding: one 16-wide encoding step");
 	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (DENSITY ? Lay::F_R0 : Lay::N_FWD);
 	extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -637,7 +637,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 template <int ES, int DH, int RH, int MODE>
 static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	using Lay = NerfLayout<ES, DH, RH>;
-	constexpr bool TRAIN = MODE == MLP_TRAIN;
+	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_TRAIN_ENC;
 	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (MODE == MLP_DENSITY ? Lay::F_R0 : Lay::N_FWD);
 	size_t lds = (size_t)NFRAG * 1024 + (TRAIN ? 4 * Lay::IMG_HALVES * sizeof(f16) : 0);
 	uint32_t n_reg = 4;
@@ -675,20 +675,23 @@ static void dispatch_nerf(const NerfMlpPlan& p, const NerfMlpArgs& a, hipStream_
 	}
 }
 
+template <int MODE>
+static void dispatch_nerf_fused(const NerfMlpPlan& p, const NerfMlpArgs& a, hipStream_t s) {
+	const uint32_t key = p.enc_steps * 100 + p.d_hidden * 10 + p.r_hidden;
+	if (key == 112) launch_nerf<1, 1, 2, MODE>(a, s);
+	else if (key == 111) launch_nerf<1, 1, 1, MODE>(a, s);
+	else if (key == 113) launch_nerf<1, 1, 3, MODE>(a, s);
+	else throw Error("NerfNetwork: the fused encoding needs one encoding step and one density hidden layer");
+}
+
 void nerf_mlp_run(const NerfMlpPlan& p, MlpMode mode, const NerfMlpArgs& a, hipStream_t s) {
 	if (a.n == 0) return;
 	switch (mode) {
 		case MLP_INFER: dispatch_nerf<MLP_INFER>(p, a, s); break;
 		case MLP_TRAIN: dispatch_nerf<MLP_TRAIN>(p, a, s); break;
 		case MLP_DENSITY: dispatch_nerf<MLP_DENSITY>(p, a, s); break;
-		case MLP_INFER_ENC: {
-			const uint32_t key = p.enc_steps * 100 + p.d_hidden * 10 + p.r_hidden;
-			if (key == 112) launch_nerf<1, 1, 2, MLP_INFER_ENC>(a, s);
-			else if (key == 111) launch_nerf<1, 1, 1, MLP_INFER_ENC>(a, s);
-			else if (key == 113) launch_nerf<1, 1, 3, MLP_INFER_ENC>(a, s);
-			else throw Error("NerfNetwork: fused-encoding inference needs one encoding step and one density hidden layer");
-			break;
-		}
+		case MLP_INFER_ENC: dispatch_nerf_fused<MLP_INFER_ENC>(p, a, s); break;
+		case MLP_TRAIN_ENC: dispatch_nerf_fused<MLP_TRAIN_ENC>(p, a, s); break;
 	}
 }
 

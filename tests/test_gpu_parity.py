@@ -377,3 +377,29 @@ def test_training_graph_matches_eager(pkg):
         runs.append((tr.params_full_precision.cpu().numpy().copy(), tr.inference_params.float().cpu().numpy().copy()))
     np.testing.assert_array_equal(runs[1][0], runs[0][0])
     np.testing.assert_array_equal(runs[1][1], runs[0][1])
+
+
+@pytest.mark.parametrize("n", [777, 4096, 50000])
+def test_fused_encoding_training_matches_unfused(pkg, nerf_setup, n):
+    """forward_backward with the encoding inside the MLP training kernel (option fuse_train, off by default)
+    gives the same output and MLP gradients bit for bit as encode-then-MLP, and the same grid gradients
+    (bitwise on the sorted backward, n >= 4096; within fp16 atomic-order noise on the direct one)."""
+    net, tr, p16, m = nerf_setup
+    c = torch.from_numpy(coords_batch(n, seed=11 + n)).cuda()
+    dL = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
+    dL[:, :4] = torch.rand((n, 4), device="cuda").half() - 0.5
+    res = {}
+    for fuse in (1, 0):
+        net.set_option("fuse_train", fuse)
+        out = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
+        net.forward_backward(c, dL, output=out)
+        torch.cuda.synchronize()
+        res[fuse] = (out.clone(), tr.gradients.clone())
+    net.set_option("fuse_train", 0)
+    nm = net.n_matrix_params
+    assert torch.equal(res[1][0], res[0][0])
+    assert torch.equal(res[1][1][:nm], res[0][1][:nm])
+    if n >= 4096:
+        assert torch.equal(res[1][1][nm:], res[0][1][nm:])
+    else:
+        assert torch.allclose(res[1][1][nm:].float(), res[0][1][nm:].float(), atol=3e-3)
