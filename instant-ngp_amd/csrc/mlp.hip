@@ -123,6 +123,19 @@ __device__ __forceinline__ void layer_fwd(f32x16 (&acc)[TILES], const f16x8 (&in
 	}
 }
 
+// Same layer with the weight fragments held in registers (w[off + t * STEPS + s]); off is a
+// compile-time constant after unrolling, so the array never leaves registers.
+template <int TILES, int STEPS, int NR>
+__device__ __forceinline__ void layer_fwd_reg(f32x16 (&acc)[TILES], const f16x8 (&in)[STEPS], const f16x8 (&w)[NR], int off) {
+#pragma unroll
+	for (int t = 0; t < TILES; ++t) {
+		f32x16 c = {};
+#pragma unroll
+		for (int s = 0; s < STEPS; ++s) c = mfma32(w[off + t * STEPS + s], in[s], c);
+		acc[t] = c;
+	}
+}
+
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -371,6 +384,19 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 
 	for (int i = threadIdx.x; i < NFRAG * 64; i += blockDim.x) lfrag[i] = a.frags[i];
 	__syncthreads();
+	// training: the forward weight fragments stay in registers for every tile the wave processes (the
+	// kernel runs one wave per SIMD, so LDS latency is otherwise exposed at each layer)
+	constexpr bool WREG = TRAIN && Lay::N_FWD <= 24;  // larger networks would spill
+	f16x8 wreg[WREG ? Lay::N_FWD : 1];
+	if constexpr (WREG) {
+#pragma unroll
+		for (int q = 0; q < Lay::N_FWD; ++q) wreg[q] = lfrag[q * 64 + lane];
+	}
+#define NGP_FWD(T, S, ACC, IN, OFF)                                             \
+	do {                                                                        \
+		if constexpr (WREG) layer_fwd_reg<T, S>(ACC, IN, wreg, OFF);           \
+		else layer_fwd<T, S>(ACC, IN, lfrag + (OFF) * 64, lane);                \
+	} while (0)
 
 	f16* img = (f16*)(smem + NFRAG * 1024) + wave * Lay::IMG_HALVES;
 	f32x4 dw[TRAIN ? Lay::N_DW : 1];
@@ -496,15 +522,15 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		}
 		f32x16 acc[2];
 		f16x8 hd[DH][4];
-		layer_fwd<2, ES>(acc, xe, lfrag + Lay::F_D0 * 64, lane);
+		NGP_FWD(2, ES, acc, xe, Lay::F_D0);
 		pack_tiles<2>(acc, hd[0], true);
 #pragma unroll
 		for (int l = 1; l < DH; ++l) {
-			layer_fwd<2, 4>(acc, hd[l - 1], lfrag + (Lay::F_DH + 8 * (l - 1)) * 64, lane);
+			NGP_FWD(2, 4, acc, hd[l - 1], Lay::F_DH + 8 * (l - 1));
 			pack_tiles<2>(acc, hd[l], true);
 		}
 		f32x16 dacc[1];
-		layer_fwd<1, 4>(dacc, hd[DH - 1], lfrag + Lay::F_DO * 64, lane);
+		NGP_FWD(1, 4, dacc, hd[DH - 1], Lay::F_DO);
 		f16x8 dout[2];
 		pack_tile(dacc[0], dout[0], dout[1], false);  // dout[0] = rows 0..15 (density network output)
 		if constexpr (DENSITY) {
@@ -516,15 +542,15 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		f16x8 rin[2] = {dout[0], sh4_frag(cdx, cdy, cdz, h)};
 		if (!valid) rin[1] = f16x8{};
 		f16x8 hr[RH][4];
-		layer_fwd<2, 2>(acc, rin, lfrag + Lay::F_R0 * 64, lane);
+		NGP_FWD(2, 2, acc, rin, Lay::F_R0);
 		pack_tiles<2>(acc, hr[0], true);
 #pragma unroll
 		for (int l = 1; l < RH; ++l) {
-			layer_fwd<2, 4>(acc, hr[l - 1], lfrag + (Lay::F_RH + 8 * (l - 1)) * 64, lane);
+			NGP_FWD(2, 4, acc, hr[l - 1], Lay::F_RH + 8 * (l - 1));
 			pack_tiles<2>(acc, hr[l], true);
 		}
 		f32x16 racc[1];
-		layer_fwd<1, 4>(racc, hr[RH - 1], lfrag + Lay::F_RO * 64, lane);
+		NGP_FWD(1, 4, racc, hr[RH - 1], Lay::F_RO);
 		if (a.out && valid) {
 			f16x8 ro, ro_hi;
 			pack_tile(racc[0], ro, ro_hi, false);
