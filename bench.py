@@ -105,10 +105,15 @@ def cpu_baseline(variant, budget_s=12.0):
     x, dL = x.numpy(), dL.float().numpy()
 
     def run(seconds):
+        # one OpenMP thread per caller (the oracle's forward is an omp loop): thread-per-chunk scaling,
+        # output and gradient buffers allocated once per thread
+        orc.set_num_threads(1)
+        out = np.zeros((chunk, 16), np.float32)
+        grads = np.zeros(orc.nerf_n_params(m), np.float64)
         done, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < seconds:
-            orc.nerf_forward(m, p16, x)
-            orc.nerf_backward(m, p16, x, dL)
+            orc.nerf_forward(m, p16, x, out=out)
+            orc.nerf_backward(m, p16, x, dL, grads=grads)
             done += chunk
         return done, time.perf_counter() - t0
 

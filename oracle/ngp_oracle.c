@@ -340,6 +340,8 @@ static void mlp_forward_one(const orc_mlp* m, const uint16_t* w, const float* x,
 	}
 }
 
+EXPORT void orc_set_num_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
+
 EXPORT void orc_mlp_forward(const orc_mlp* m, const uint16_t* w, size_t n, const float* x, float* y) {
 	uint32_t nact = m->n_hidden * m->width + m->out_pad;
 	#pragma omp parallel

@@ -84,6 +84,7 @@ def _declare(L):
     d("orc_mlp_backward", None, P, P, sz, P, P, P, P)
     d("orc_mlp_init", None, P, P, P)
     d("orc_nerf_n_params", u32, P)
+    d("orc_set_num_threads", None, C.c_int)
     d("orc_nerf_forward", None, P, P, sz, P, P)
     d("orc_nerf_density", None, P, P, sz, P, u32, P)
     d("orc_nerf_backward", None, P, P, sz, P, P, P, P)
@@ -241,9 +242,15 @@ def nerf_init(m, seed=1337):
     return p
 
 
-def nerf_forward(m, params16, coords):
+def set_num_threads(n):
+    """OpenMP threads of the calling thread's oracle parallel regions (omp_set_num_threads)."""
+    lib().orc_set_num_threads(int(n))
+
+
+def nerf_forward(m, params16, coords, out=None):
     coords = np.ascontiguousarray(coords, dtype=np.float32)
-    out = np.zeros((coords.shape[0], 16), dtype=np.float32)
+    if out is None:
+        out = np.zeros((coords.shape[0], 16), dtype=np.float32)
     lib().orc_nerf_forward(C.byref(m), ptr(np.ascontiguousarray(params16)), coords.shape[0], ptr(coords), ptr(out))
     return out
 
@@ -256,9 +263,12 @@ def nerf_density(m, params16, coords, stride=None):
     return out
 
 
-def nerf_backward(m, params16, coords, dL_dout, want_denc=False):
+def nerf_backward(m, params16, coords, dL_dout, want_denc=False, grads=None):
     coords = np.ascontiguousarray(coords, dtype=np.float32)
-    grads = np.zeros(nerf_n_params(m), dtype=np.float64)
+    if grads is None:
+        grads = np.zeros(nerf_n_params(m), dtype=np.float64)
+    else:
+        grads.fill(0.0)
     denc = np.zeros((coords.shape[0], m.density.in_pad), dtype=np.float32) if want_denc else None
     lib().orc_nerf_backward(C.byref(m), ptr(np.ascontiguousarray(params16)), coords.shape[0], ptr(coords),
                             ptr(np.ascontiguousarray(dL_dout, np.float32)), ptr(grads), ptr(denc))
