@@ -325,6 +325,13 @@ enum { NGP_DTYPE_F32 = 0, NGP_DTYPE_F16 = 1 };
 enum { NGP_REDUCE_SUM = 0, NGP_REDUCE_MAX = 1 };
 typedef int (*ngp_allreduce_fn)(void* user, void* device_buf, uint64_t count, int dtype, int op, void* stream);
 int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn allreduce, void* user);
+// Sampler pipelining (default on, single GPU): when no density-grid update is due before the next
+// step, ngp_nerf_train_step launches the next step's ray sampling on an internal stream right after
+// this step's loss pass, so it runs under this step's training pass (identical samples: the sampler
+// reads only the occupancy bitfield, the rng and the ray count). Disable before modifying the density
+// grid or bitfield through ngp_nerf_trainer_buffers between steps. No reference counterpart (the
+// Testbed runs the step serially, testbed_nerf.cu:3867-4132).
+int ngp_nerf_trainer_set_pipeline(ngp_nerf_trainer* t, int enable);
 
 /* Snapshots (Testbed::save_snapshot / load_snapshot, src/testbed.cu:4873-5057; python_api.cu:446-447):
  * msgpack of the network config (network_config_json, the Testbed's m_network_config; NULL = {}) with

@@ -148,6 +148,7 @@ SIGNATURES = {
     "ngp_nerf_trainer_destroy": (None, [P]),
     "ngp_nerf_train_step": (i32, [P, P, i32, C.POINTER(NerfStats)]),
     "ngp_nerf_trainer_buffers": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
+    "ngp_nerf_trainer_set_pipeline": (i32, [P, i32]),
     "ngp_nerf_trainer_set_data_parallel": (i32, [P, u32, u32, P, P]),
     "ngp_nerf_save_snapshot": (i32, [P, P, C.c_char_p, C.c_char_p, i32, i32]),
     "ngp_nerf_load_snapshot": (i32, [P, P, C.c_char_p]),

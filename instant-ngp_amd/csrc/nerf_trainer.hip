@@ -108,9 +108,26 @@ struct ngp_nerf_trainer {
 	// spinning on a sequence number (no copy-engine transfer, no blocking stream synchronize)
 	volatile uint32_t* host_ctr = nullptr;
 	uint32_t publish_seq = 0;
+	// Sampler pipelining: the next step's ray sampling depends on the occupancy bitfield, the rng and the
+	// rays-per-batch count, not on the network, so (when no density-grid update is due before it) it is
+	// launched on `sample_stream` as soon as this step's loss pass has released the sample buffers and
+	// runs concurrently with this step's training pass. Same kernels, same inputs: same samples.
+	bool pipeline = true;                // ngp_nerf_trainer_set_pipeline
+	bool prelaunched = false;
+	uint32_t pre_R = 0, pre_max_inference = 0;
+	hipStream_t sample_stream = nullptr;
+	hipEvent_t ev_free = nullptr, ev_samp = nullptr;
+	void drain() {  // the prelaunched sampler finished and discarded (state is about to change)
+		if (sample_stream) (void)hipStreamSynchronize(sample_stream);
+		prelaunched = false;
+	}
 	~ngp_nerf_trainer() {
+		drain();
 		if (train_graph) ngp_graph_destroy(train_graph);
 		if (own_stream) (void)hipStreamDestroy(own_stream);
+		if (sample_stream) (void)hipStreamDestroy(sample_stream);
+		for (hipEvent_t e : {ev_free, ev_samp})
+			if (e) (void)hipEventDestroy(e);
 		if (host_ctr) (void)hipHostFree((void*)host_ctr);
 	}
 	// data parallelism: rank r traces global rays [R r / N, R (r+1) / N), compacts to B / N,
@@ -427,6 +444,7 @@ int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_confi
 
 int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn allreduce, void* user) {
 	if (!t || world == 0 || rank >= world || (world > 1 && !allreduce)) return NGP_INVALID;
+	t->drain();
 	t->rank = rank;
 	t->world = world;
 	t->allreduce = allreduce;
@@ -506,6 +524,53 @@ static void wait_published(volatile uint32_t* host, uint32_t seq, hipStream_t s)
 	}
 }
 
+// Sizes and buffers of one step's sampling (train_nerf_step, testbed_nerf.cu:3867-3953), from the
+// trainer's current rays-per-batch and measured counts.
+struct SamplePlan {
+	uint32_t R, Rl, r_lo, Bl, max_samples, max_inference, Ra;
+	uint32_t* ray_indices;
+	float* rays;
+	uint32_t* numsteps;
+	float* coords;
+	uint32_t* ctr;
+};
+static SamplePlan sample_plan(ngp_nerf_trainer* t) {
+	SamplePlan p;
+	const uint32_t B = t->cfg.target_batch_size, W = t->world, rk = t->rank;
+	p.R = t->rays_per_batch;
+	p.r_lo = (uint32_t)((uint64_t)p.R * rk / W);
+	p.Rl = (uint32_t)((uint64_t)p.R * (rk + 1) / W) - p.r_lo;
+	p.Bl = (uint32_t)((uint64_t)B * (rk + 1) / W - (uint64_t)B * rk / W);
+	p.max_samples = p.Bl * 16;
+	if (t->measured_before_compaction_local == 0) p.max_inference = p.max_samples;
+	else p.max_inference = next_multiple(std::min(t->measured_before_compaction_local, p.max_samples), 256);
+	p.Ra = std::max(p.Rl, 1u);
+	p.ray_indices = t->ray_indices.get<uint32_t>(p.Ra);
+	p.rays = t->rays.get<float>((size_t)p.Ra * 6);
+	p.numsteps = t->numsteps.get<uint32_t>((size_t)p.Ra * 2);
+	p.coords = t->coords.get<float>((size_t)p.max_samples * 7);
+	p.ctr = t->counters.get<uint32_t>(4);  // rays kept, steps, compacted steps
+	return p;
+}
+static void launch_sampler(ngp_nerf_trainer* t, const SamplePlan& p, hipStream_t s) {
+	ProfScope ps("nerf_sample", s);
+	const ngp_rng rng{t->rng.state, t->rng.inc};
+	check_rc(ngp_nerf_generate_training_samples(t->data, &t->cfg, s, p.Rl, p.r_lo, p.R, rng, p.max_inference,
+	                                            (const uint8_t*)t->bitfield.p, p.ray_indices, p.rays, p.numsteps, p.coords, p.ctr));
+}
+static bool density_grid_update_due(uint32_t step) {
+	const uint32_t skip = std::min(std::max(step / 16u, 1u), 16u);
+	return step % skip == 0;
+}
+
+int ngp_nerf_trainer_set_pipeline(ngp_nerf_trainer* t, int enable) {
+	if (!t) return NGP_INVALID;
+	NERF_TRY({
+		t->drain();
+		t->pipeline = enable != 0;
+	});
+}
+
 int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_nerf_stats* st) {
 	if (!t) return NGP_INVALID;
 	NERF_TRY({
@@ -516,46 +581,39 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		}
 		const ngp_nerf_config& cfg = t->cfg;
 		const uint32_t B = cfg.target_batch_size;
-		// training_prep_nerf
-		const uint32_t skip = std::min(std::max(t->training_step / 16u, 1u), 16u);
-		if (t->training_step % skip == 0) {
+		const bool pre = t->prelaunched;
+		t->prelaunched = false;
+		// training_prep_nerf (a prelaunched sampler implies no update was due at this step)
+		if (!pre && density_grid_update_due(t->training_step)) {
 			ProfScope ps("nerf_density_grid", s);
 			const uint32_t nc = cfg.max_cascade + 1;
 			if (t->training_step < 256) update_density_grid(t, s, 0.95f, GRID_N_CELLS * nc, 0);
 			else update_density_grid(t, s, 0.95f, GRID_N_CELLS / 4 * nc, GRID_N_CELLS / 4 * nc);
 		}
 		// train_nerf_step (testbed_nerf.cu:3867-4132)
-		const uint32_t R = t->rays_per_batch;
-		const uint32_t W = t->world, rk = t->rank;
-		const uint32_t r_lo = (uint32_t)((uint64_t)R * rk / W), Rl = (uint32_t)((uint64_t)R * (rk + 1) / W) - r_lo;
-		const uint32_t Bg = B;
-		const uint32_t Bl = (uint32_t)((uint64_t)Bg * (rk + 1) / W - (uint64_t)Bg * rk / W);
-		const uint32_t max_samples = Bl * 16;
-		uint32_t max_inference;
-		if (t->measured_before_compaction_local == 0) max_inference = max_samples;
-		else max_inference = next_multiple(std::min(t->measured_before_compaction_local, max_samples), 256);
+		const SamplePlan sp = sample_plan(t);
+		const uint32_t R = sp.R, Rl = sp.Rl, Bl = sp.Bl, max_inference = sp.max_inference, Ra = sp.Ra;
+		const uint32_t W = t->world;
 		if (t->training_step == 0) t->n_rays_total = 0;
-		const uint32_t n_rays_total = t->n_rays_total;
 		t->n_rays_total += R;
-		const uint32_t Ra = std::max(Rl, 1u);
-		uint32_t* ray_indices = t->ray_indices.get<uint32_t>(Ra);
-		float* rays = t->rays.get<float>((size_t)Ra * 6);
-		uint32_t* numsteps = t->numsteps.get<uint32_t>((size_t)Ra * 2);
-		float* coords = t->coords.get<float>((size_t)max_samples * 7);
-		f16* mlp_out = t->mlp_out.get<f16>((size_t)std::max(Bl, max_samples) * 16);
+		uint32_t* ray_indices = sp.ray_indices;
+		float* rays = sp.rays;
+		uint32_t* numsteps = sp.numsteps;
+		float* coords = sp.coords;
+		uint32_t* ctr = sp.ctr;
+		f16* mlp_out = t->mlp_out.get<f16>((size_t)std::max(Bl, sp.max_samples) * 16);
 		f16* dloss = t->dloss.get<f16>((size_t)Bl * 16);
 		float* coords_c = t->coords_c.get<float>((size_t)Bl * 7);
 		float* loss = t->loss.get<float>(Ra);
-		uint32_t* ctr = t->counters.get<uint32_t>(4);  // rays kept, steps, compacted steps
 		NGP_HIP(hipMemsetAsync(loss, 0, (size_t)Ra * 4, s));
-		(void)n_rays_total;
 		ngp_rng rng{t->rng.state, t->rng.inc};
 		// global ray ids (rng.advance(i * 16), image_idx(i, R)) so the shards draw the 1-GPU rays;
 		// dL/doutput is scaled by 128 / R (global), so the summed gradient is the 1-GPU gradient
-		{
-		ProfScope ps("nerf_sample", s);
-		check_rc(ngp_nerf_generate_training_samples(t->data, &cfg, s, Rl, r_lo, R, rng, max_inference, (const uint8_t*)t->bitfield.p,
-		                                            ray_indices, rays, numsteps, coords, ctr));
+		if (pre) {
+			NGP_CHECK(sp.R == t->pre_R && sp.max_inference == t->pre_max_inference, "nerf: prelaunched sampler is stale");
+			NGP_HIP(hipStreamWaitEvent(s, t->ev_samp, 0));
+		} else {
+			launch_sampler(t, sp, s);
 		}
 		{
 		ProfScope ps("nerf_inference", s);
@@ -568,6 +626,25 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		check_rc(nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, 4, ray_indices, rays, numsteps, coords, coords_c,
 		                               dloss, loss, ctr + 2, (const float*)t->mean.p, W > 1 ? loss_scale_local : 128.0f));
 		fill_rollover_pair(Bl, ctr + 2, dloss, 16, coords_c, 7, s);  // fill_rollover_and_rescale + fill_rollover
+		}
+		// the step's counters are final here (the training pass does not touch them): publish them before
+		// the training pass so the host can size the next step while it runs
+		if (!t->host_ctr) {
+			void* p = nullptr;
+			NGP_HIP(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+			t->host_ctr = (volatile uint32_t*)p;
+			memset(p, 0, 64);
+		}
+		k_publish_counters<<<1, 64, 0, s>>>(ctr, t->host_ctr, ++t->publish_seq);
+		NGP_HIP(hipGetLastError());
+		const bool can_pipeline = t->pipeline && W == 1;
+		if (can_pipeline) {
+			if (!t->sample_stream) {
+				NGP_HIP(hipStreamCreateWithFlags(&t->sample_stream, hipStreamNonBlocking));
+				NGP_HIP(hipEventCreateWithFlags(&t->ev_free, hipEventDisableTiming));
+				NGP_HIP(hipEventCreateWithFlags(&t->ev_samp, hipEventDisableTiming));
+			}
+			NGP_HIP(hipEventRecord(t->ev_free, s));  // sample buffers and counters released
 		}
 		{
 		ProfScope ps("nerf_train_pass", s);
@@ -594,14 +671,6 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		// NerfCounters::update_after_training (testbed_nerf.cu:3583-3609): host sync
 		uint32_t h[4];
 		std::vector<float> hl;
-		if (!t->host_ctr) {
-			void* p = nullptr;
-			NGP_HIP(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
-			t->host_ctr = (volatile uint32_t*)p;
-			memset(p, 0, 64);
-		}
-		k_publish_counters<<<1, 64, 0, s>>>(ctr, t->host_ctr, ++t->publish_seq);
-		NGP_HIP(hipGetLastError());
 		if (get_loss && Rl) {
 			hl.resize(Rl);
 			NGP_HIP(hipMemcpyAsync(hl.data(), loss, (size_t)Rl * 4, hipMemcpyDeviceToHost, s));
@@ -637,6 +706,16 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			if (get_loss) t->loss_scalar = loss_scalar = (float)(loss_sum * (double)t->measured_batch_size / (double)B);
 			uint32_t r = (uint32_t)((float)t->rays_per_batch * (float)B / (float)t->measured_batch_size);
 			t->rays_per_batch = std::min(next_multiple(r, 256), 1u << 18);
+		}
+		// next step's sampler, concurrent with this step's training pass (no density-grid update due first)
+		if (can_pipeline && t->measured_batch_size > 0 && !density_grid_update_due(t->training_step)) {
+			const SamplePlan np = sample_plan(t);
+			NGP_HIP(hipStreamWaitEvent(t->sample_stream, t->ev_free, 0));
+			launch_sampler(t, np, t->sample_stream);
+			NGP_HIP(hipEventRecord(t->ev_samp, t->sample_stream));
+			t->pre_R = np.R;
+			t->pre_max_inference = np.max_inference;
+			t->prelaunched = true;
 		}
 		if (st) {
 			st->step = t->training_step;
@@ -797,6 +876,7 @@ int ngp_nerf_save_snapshot(ngp_nerf_trainer* t, void* stream, const char* path, 
 int ngp_nerf_load_snapshot(ngp_nerf_trainer* t, void* stream, const char* path) {
 	if (!t || !path) return NGP_INVALID;
 	NERF_TRY({
+		t->drain();
 		hipStream_t s = S(stream);
 		NGP_HIP(hipStreamSynchronize(s));
 		const Value root = load_network_config(path);

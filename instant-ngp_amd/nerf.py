@@ -231,6 +231,11 @@ class NerfTraining:
             fn, user = None, None
         check(lib().ngp_nerf_trainer_set_data_parallel(self.handle, rank, world, fn, user))
 
+    def set_pipeline(self, enable):
+        """Launch the next step's ray sampling under this step's training pass (default on; identical
+        samples). Turn off before writing density_grid / bitfield between steps."""
+        check(lib().ngp_nerf_trainer_set_pipeline(self.handle, int(enable)))
+
     def save_snapshot(self, path, network_config=None, include_optimizer_state=False, compress=True, stream=None):
         """Testbed::save_snapshot (testbed.cu:4873-4937): .ingp = gzip'd msgpack of the network config
         (dict, the Testbed's m_network_config) with the "snapshot" member."""

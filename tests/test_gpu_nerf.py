@@ -287,3 +287,26 @@ def test_fused_encoding_inference_bitwise(pkg, log2_T, max_level):
     for layout in (pkg.LAYOUT_AOS, pkg.LAYOUT_SOA, pkg.LAYOUT_AOS_RGBD):
         np.testing.assert_array_equal(outs[1, layout], outs[0, layout])
     assert np.isfinite(outs[1, pkg.LAYOUT_AOS].view(np.float16)[:, :4].astype(np.float32)).all()
+
+
+@pytest.mark.gpu
+def test_sampler_pipelining_is_exact(pkg):
+    """Launching the next step's sampler under the training pass (default) trains exactly like the
+    serial step: same per-step counts, same parameters, density grid and bitfield, bit for bit, across
+    density-grid updates, growing ray counts and steps that read the loss back."""
+    ds = pkg.synthetic.lego_like_dataset(n_images=12, width=128, height=128, seed=5)
+    cfg = pkg.nerf.default_config(1.0)
+    runs = []
+    for pipeline in (True, False):
+        net = pkg.create_nerf_network(pkg.nerf_config("C2"))
+        tr = pkg.Trainer(net, pkg.nerf_config("C2")["optimizer"], seed=7)
+        run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
+        run.set_pipeline(pipeline)
+        stats = [run.train_step(get_loss=(i % 37 == 0)) for i in range(300)]
+        torch.cuda.synchronize()
+        runs.append((stats, tr.serialize(), run.density_grid.cpu().numpy(), run.bitfield.cpu().numpy(), (net, tr, run)))
+    (s1, p1, g1, b1, _), (s0, p0, g0, b0, _) = runs
+    assert s1 == s0
+    assert p1 == p0
+    np.testing.assert_array_equal(g1, g0)
+    np.testing.assert_array_equal(b1, b0)
