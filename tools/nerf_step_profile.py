@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--measure", type=int, default=200)
     ap.add_argument("--images", type=int, default=100)
     ap.add_argument("--res", type=int, default=800)
+    ap.add_argument("--pipeline", type=int, default=1, help="1: next step's sampler under the training pass (default), 0: serial step")
     ap.add_argument("--option", action="append", default=[], help="model option key=value (ngp_model_set_option)")
     args = ap.parse_args()
     from __graft_entry__ import load_package
@@ -38,6 +39,7 @@ def main():
         key, value = kv.split("=")
         net.set_option(key, float(value))
     run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
+    run.set_pipeline(args.pipeline)
     lib = pkg.lib()
     t0 = time.time()
     for i in range(args.steps):
