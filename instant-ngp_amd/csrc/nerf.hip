@@ -621,6 +621,21 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 	const uint32_t numsteps = a.numsteps[2 * i], base = a.numsteps[2 * i + 1];
 	const f16* out = a.network_output + (size_t)base * a.out_stride;
 	const float* ci = a.coords_in + (size_t)base * 7;
+	// target texel first (same random stream as the sampler for the same ray): its dependent chain of
+	// loads (ray index -> camera -> pixel) overlaps the compositing loop instead of following it
+	const uint32_t ray_idx = a.ray_indices[i];
+	Rng rng = a.rng;
+	pcg_advance(rng, (uint64_t)ray_idx * N_MAX_RANDOM_SAMPLES_PER_RAY);
+	const uint32_t img = image_idx(ray_idx, a.n_rays_total_for_image_idx, n_images);
+	const Camera& cam = cams[img];
+	float u, v;
+	random_image_pos(rng, cam.width, cam.height, cfg.snap_to_pixel_centers != 0, &u, &v);
+	pcg_advance(rng, 1);  // motionblur_time
+	float bg[3] = {cfg.background_color[0], cfg.background_color[1], cfg.background_color[2]};
+	if (cfg.random_bg_color) { bg[0] = pcg_float(rng); bg[1] = pcg_float(rng); bg[2] = pcg_float(rng); }
+	for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear(bg[k]);
+	// read_rgba, Byte images (common_device.cuh:885-904)
+	const uint32_t raw = pixels[cam.pixel_offset + pixel_index(u, v, cam.width, cam.height)];
 	float t = 1.f;
 	const float eps = 1e-4f;
 	float rr = 0.f, rg = 0.f, rb = 0.f;
@@ -655,20 +670,6 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 #undef NGP_LOSS1_STEP
 	}
 	if (L != 0) return;
-	// same random stream as the sampler for the same ray
-	const uint32_t ray_idx = a.ray_indices[i];
-	Rng rng = a.rng;
-	pcg_advance(rng, (uint64_t)ray_idx * N_MAX_RANDOM_SAMPLES_PER_RAY);
-	const uint32_t img = image_idx(ray_idx, a.n_rays_total_for_image_idx, n_images);
-	const Camera& cam = cams[img];
-	float u, v;
-	random_image_pos(rng, cam.width, cam.height, cfg.snap_to_pixel_centers != 0, &u, &v);
-	pcg_advance(rng, 1);  // motionblur_time
-	float bg[3] = {cfg.background_color[0], cfg.background_color[1], cfg.background_color[2]};
-	if (cfg.random_bg_color) { bg[0] = pcg_float(rng); bg[1] = pcg_float(rng); bg[2] = pcg_float(rng); }
-	for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear(bg[k]);
-	// read_rgba, Byte images (common_device.cuh:885-904)
-	const uint32_t raw = pixels[cam.pixel_offset + pixel_index(u, v, cam.width, cam.height)];
 	float tex[4];
 	if (raw == 0x00FF00FFu) { tex[0] = tex[1] = tex[2] = tex[3] = -1.0f; }
 	else {
