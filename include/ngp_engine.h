@@ -97,10 +97,20 @@ int ngp_model_initialize_params(const ngp_model* m, uint64_t seed, float* params
 /* GridEncoding::set_max_level / set_max_level_gpu (src/testbed.cu:3856-3864; testbed_nerf.cu:3996,4004) */
 int ngp_model_set_max_level(ngp_model* m, float max_level, const float* max_level_per_sample);
 /* engine knobs: "grid_backward_mode" = 0 auto, 1 direct packed-f16 atomics (tcnn-style),
- * 2 spatially binned LDS windows for the coarse levels (+ direct for the rest) */
+ * 3 destination-bucketed exact sums (auto picks 3 for n >= 4096); "fuse_infer", "fuse_train",
+ * "fused_hist", "overlap", "grid_forward_mode"  */
 int ngp_model_set_option(ngp_model* m, const char* key, double value);
 /* pre-size internal workspaces for batches up to n (lets callers capture steps into HIP graphs) */
 int ngp_model_reserve(ngp_model* m, uint32_t n);
+/* Inspection of the last training pass's intermediates (the role of tcnn's forward_activations(ctx),
+ * nerf_network.h:502-507): "encoding" = fp16 AoS [n x encoding_width] grid output of the last unfused
+ * forward, "dL_dencoding" = fp16 AoS [n x encoding_width] input of the grid backward. Device pointer
+ * valid until the next call that grows the workspace. */
+int ngp_model_workspace(ngp_model* m, const char* name, void** ptr, uint64_t* bytes);
+/* Counts workspace reallocations. A graph from ngp_trainer_capture_training_step holds workspace
+ * pointers: ngp_graph_launch fails (instead of touching freed memory) once the epoch moved past the
+ * capture's; callers re-capture when it changes. */
+uint64_t ngp_model_workspace_epoch(const ngp_model* m);
 
 /* inference_mixed_precision (nerf_network.h:116-174): output fp16 [n x padded_output_width] */
 int ngp_inference(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
@@ -329,7 +339,7 @@ int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint3
 // step, ngp_nerf_train_step launches the next step's ray sampling on an internal stream right after
 // this step's loss pass, so it runs under this step's training pass (identical samples: the sampler
 // reads only the occupancy bitfield, the rng and the ray count). Disable before modifying the density
-// grid or bitfield through ngp_nerf_trainer_buffers between steps. No reference counterpart (the
+// grid or bitfield between steps (ngp_nerf_trainer_buffers discards a prelaunched sampler). No reference counterpart (the
 // Testbed runs the step serially, testbed_nerf.cu:3867-4132).
 int ngp_nerf_trainer_set_pipeline(ngp_nerf_trainer* t, int enable);
 

@@ -93,6 +93,8 @@ SIGNATURES = {
     "ngp_model_set_max_level": (i32, [P, f32, P]),
     "ngp_model_set_option": (i32, [P, C.c_char_p, C.c_double]),
     "ngp_model_reserve": (i32, [P, u32]),
+    "ngp_model_workspace": (i32, [P, C.c_char_p, C.POINTER(P), C.POINTER(u64)]),
+    "ngp_model_workspace_epoch": (u64, [P]),
     "ngp_inference": (i32, [P, P, u32, P, u32, P, u32, u32, i32]),
     "ngp_density": (i32, [P, P, u32, P, u32, P, u32, u32, i32]),
     "ngp_forward": (i32, [P, P, u32, P, u32, P, u32, i32, C.POINTER(P)]),

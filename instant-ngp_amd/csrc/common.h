@@ -48,6 +48,14 @@ int device_cu_count();
 // ---- device helpers ------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
+// fp32 -> fp16 of a value that has been rounded to fp32 first. LLVM folds fptrunc(fmul(a, b)) into
+// v_fma_mixlo_f16, which rounds the exact product once to fp16 instead of rounding it to fp32 first as
+// tcnn's `(__half)(a * b)` (and the oracle) do; the empty asm makes the fp32 value opaque to that fold.
+__device__ __forceinline__ f16 to_f16(float x) {
+	asm("" : "+v"(x));
+	return (f16)x;
+}
+
 // Packed fp16 atomic add (global_atomic_pk_add_f16, no return). Address must be 4-byte aligned.
 __device__ __forceinline__ void atomic_add_f16x2(f16* addr, f16x2 v) {
 	__builtin_amdgcn_global_atomic_fadd_v2f16((__attribute__((address_space(1))) f16x2*)addr, v);

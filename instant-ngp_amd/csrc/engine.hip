@@ -12,7 +12,6 @@
 
 #include "../../include/ngp_engine.h"
 #include "common.h"
-#include "binning.h"
 #include "grid_scatter.h"
 #include "grid.h"
 #include "json.h"
@@ -34,14 +33,19 @@ int device_cu_count() {
 }
 
 // Growable device buffer (grows outside the hot loop; ngp_model_reserve pre-sizes it).
+// Every reallocation bumps *epoch (the owning model's workspace epoch): a captured HIP graph holds raw
+// workspace pointers, so graph launches check the epoch they were captured at.
 struct DevBuf {
 	void* p = nullptr;
 	size_t bytes = 0;
+	uint64_t* epoch = nullptr;
 	void* get(size_t need) {
 		if (need > bytes) {
 			if (p) NGP_HIP(hipFree(p));
+			p = nullptr;
 			NGP_HIP(hipMalloc(&p, need));
 			bytes = need;
+			if (epoch) ++*epoch;
 		}
 		return p;
 	}
@@ -132,11 +136,9 @@ struct ngp_model {
 	uint32_t* d_fragmap = nullptr;  // [n_matrix x 2] fragment slot (f16 index) of each matrix param: fwd, bwd
 	bool frags_current = false;     // `frags` holds the fragments of the current `params` (kept by the optimizer)
 	uint32_t n_all_frags = 0;
-	DevBuf frags, frags_inf, enc, denc, slabs, bin_hist, bin_sorted, scatter_ws, out_ws, dl_ws;
-	int grid_backward_mode = 0;  // 0 auto, 1 direct (tcnn-style), 2 windowed (binned LDS), 3 bucketed (grid_scatter.h)
-	uint32_t win_debug = 0;      // timing experiments only (see binning.h, grid_scatter.h)
-	WinPlan win_plan;
-	uint32_t win_plan_n = 0;
+	DevBuf frags, frags_inf, enc, denc, slabs, scatter_ws, out_ws, dl_ws;
+	int grid_backward_mode = 0;  // 0 auto, 1 direct (tcnn-style), 3 bucketed (grid_scatter.h)
+	uint32_t win_debug = 0;      // timing experiments only (see grid_scatter.h)
 	ScatterPlan sc_plan;
 	uint32_t sc_plan_n = 0;
 	bool sc_prepared = false;               // phase 1 of the bucketed backward already enqueued (side stream)
@@ -158,7 +160,12 @@ struct ngp_model {
 	float max_level = 1.0f;
 	const float* max_level_per_sample = nullptr;
 	uint64_t generation = 0;
+	uint64_t ws_epoch = 0;  // bumped by every workspace reallocation (DevBuf::epoch)
 	std::unique_ptr<ngp_ctx> last_ctx;
+
+	ngp_model() {
+		for (DevBuf* b : {&frags, &frags_inf, &enc, &denc, &slabs, &scatter_ws, &out_ws, &dl_ws}) b->epoch = &ws_epoch;
+	}
 
 	~ngp_model() {
 		if (d_descs) (void)hipFree(d_descs);
@@ -352,8 +359,8 @@ struct ngp_model {
 		scatter_grid_grad(s, b, grad_mode != NGP_GRAD_ACCUMULATE);
 		if (ovl) NGP_HIP(hipStreamWaitEvent(s, ev_red, 0));
 	}
-	// Hash-grid backward: windowed (spatial bins + LDS) for the coarse levels when it pays, direct
-	// packed-f16 atomics for the rest. The windowed path needs all levels active (max_level >= 1).
+	// Hash-grid backward: destination-bucketed exact sums (n >= 4096, or mode 3), else tcnn-style direct
+	// packed-f16 atomics (small batches, where the bucket plan costs more than the atomics).
 	void scatter_grid_grad(hipStream_t s, GridBwdArgs b, bool overwrite) {
 		if (use_sorted(b.n)) {
 			void* ws = sorted_workspace(b.n);
@@ -373,27 +380,6 @@ struct ngp_model {
 			ProfScope ps("grid_grad_zero", s);
 			NGP_HIP(hipMemsetAsync(b.grad, 0, grid_params * sizeof(f16), s));
 		}
-		const bool want_win = grid_backward_mode == 2;
-		const bool can_win = want_win && b.dy_layout == AoS && !b.max_level_per_sample && b.max_level >= 1.0f &&
-		                     grid.n_features >= 2 && b.n >= 4096;
-		if (can_win) {
-			if (win_plan_n != b.n) { win_plan = make_win_plan(grid, b.n, 64 * 1024); win_plan_n = b.n; }
-			if (win_plan.n_win > 0) {
-				win_plan.debug = win_debug;
-				uint32_t* hist = (uint32_t*)bin_hist.get(bin_workspace_u32(win_plan, b.n) * 4);
-				uint32_t* sorted = (uint32_t*)bin_sorted.get((size_t)b.n * 4);
-				{
-					ProfScope ps("bin_samples", s);
-					bin_samples(grid.n_dims, b.n, b.pos, b.pos_stride, win_plan, hist, sorted, s);
-				}
-				{
-					ProfScope ps("grid_backward_win", s);
-					grid_backward_windowed(grid, win_plan, b, hist, sorted, s);
-				}
-				b.level_begin = win_plan.n_win;
-				if (b.level_begin >= grid.n_levels) return;
-			}
-		}
 		ProfScope ps("grid_backward", s);
 		grid_backward(grid, b, s);
 	}
@@ -408,7 +394,7 @@ struct ngp_trainer {
 	float *w32 = nullptr, *m1 = nullptr, *m2 = nullptr, *ema32 = nullptr;
 	f16 *w16 = nullptr, *inf16 = nullptr, *g16 = nullptr;
 	uint32_t* steps = nullptr;
-	uint32_t* ctl = nullptr;  // device {optimizer step, block counter}; `step` mirrors ctl[0] on the host
+	uint32_t* ctl = nullptr;  // device {optimizer step, block counter, .., AdamConfig at ctl + CTL_CFG}; `step` mirrors ctl[0]
 	ngp_allreduce_fn allreduce = nullptr;  // gradient exchange inside captured steps (ngp_trainer_set_allreduce)
 	void* allreduce_user = nullptr;
 	uint32_t world = 1;
@@ -418,8 +404,11 @@ struct ngp_trainer {
 	void run_step(hipStream_t s, float loss_scale, const uint32_t* step_base, uint32_t step_add) {
 		ngp_model* m = model;
 		const bool own = m->params == w16;
+		// captured steps (step_base = ctl) read the hyperparameters from the ctl block, which every graph
+		// launch refreshes with the step: set_learning_rate / set_option reach replayed steps too
 		AdamState st{w32, w16, g16, m1, m2, steps, ema32, inf16,
-		             own && m->frags_current ? (f16*)m->frags.p : nullptr, m->d_fragmap, step_base, step_add};
+		             own && m->frags_current ? (f16*)m->frags.p : nullptr, m->d_fragmap, step_base, step_add,
+		             step_base ? (const AdamConfig*)(ctl + CTL_CFG) : nullptr};
 		ProfScope ps("optimizer", s);
 		adam_ema_update(cfg, (uint32_t)n, (uint32_t)m->n_matrix(), loss_scale, st, s);
 	}
@@ -431,6 +420,7 @@ struct ngp_graph {
 	hipGraphExec_t exec = nullptr;
 	ngp_trainer* trainer = nullptr;
 	uint32_t steps_per_launch = 1;
+	uint64_t ws_epoch = 0;  // the model's workspace epoch at capture
 	~ngp_graph() {
 		if (exec) (void)hipGraphExecDestroy(exec);
 		if (graph) (void)hipGraphDestroy(graph);
@@ -596,8 +586,7 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 	NGP_TRY({
 		const std::string k = key;
 		if (k == "grid_backward_mode") {
-			NGP_CHECK(value == 0 || value == 1 || value == 2 || value == 3,
-			          "grid_backward_mode must be 0 (auto), 1 (direct), 2 (windowed), 3 (bucketed)");
+			NGP_CHECK(value == 0 || value == 1 || value == 3, "grid_backward_mode must be 0 (auto), 1 (direct), 3 (bucketed)");
 			m->grid_backward_mode = (int)value;
 		} else if (k == "overlap") {
 			NGP_CHECK(value >= 0 && value <= 15, "overlap is a bitmask in [0, 15]");
@@ -622,6 +611,19 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 int ngp_model_reserve(ngp_model* m, uint32_t n) {
 	NGP_ARG(m);
 	NGP_TRY({ m->reserve(n); });
+}
+
+uint64_t ngp_model_workspace_epoch(const ngp_model* m) { return m ? m->ws_epoch : 0; }
+
+int ngp_model_workspace(ngp_model* m, const char* name, void** ptr, uint64_t* bytes) {
+	NGP_ARG(m && name && ptr);
+	NGP_TRY({
+		const std::string k(name);
+		DevBuf* b = k == "encoding" ? &m->enc : k == "dL_dencoding" ? &m->denc : nullptr;
+		NGP_CHECK(b, "ngp_model_workspace: unknown workspace '" + k + "' (encoding, dL_dencoding)");
+		*ptr = b->p;
+		if (bytes) *bytes = b->bytes;
+	});
 }
 
 int ngp_encoding_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
@@ -874,6 +876,7 @@ int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, 
 		}
 		hipGraph_t graph = nullptr;
 		const hipError_t end = hipStreamEndCapture(s, &graph);
+		g->ws_epoch = m->ws_epoch;
 		if (rc != NGP_OK) {
 			if (graph) (void)hipGraphDestroy(graph);
 			throw Error(g_last_error);
@@ -897,7 +900,10 @@ int ngp_trainer_set_allreduce(ngp_trainer* t, uint32_t world, ngp_allreduce_fn a
 int ngp_graph_launch(ngp_graph* g, void* stream) {
 	NGP_ARG(g && g->exec);
 	NGP_TRY({
-		if (g->steps_per_launch) set_device_step(g->trainer->ctl, g->trainer->step, S(stream));
+		NGP_CHECK(g->ws_epoch == g->trainer->model->ws_epoch,
+		          "graph launch: the model's workspaces were reallocated since capture (a larger batch or a density "
+		          "pass grew them); capture again (ngp_model_workspace_epoch tells when)");
+		if (g->steps_per_launch) set_device_ctl(g->trainer->ctl, g->trainer->step, g->trainer->cfg, S(stream));
 		NGP_HIP(hipGraphLaunch(g->exec, S(stream)));
 		g->trainer->step += g->steps_per_launch;
 	});

@@ -231,11 +231,11 @@ __global__ void __launch_bounds__(256) k_grid_backward(const GridConst c, const 
 			const float w = corner_weight<D>(frac, k);
 			const uint32_t e = corner_index<D>(c, l, base, k);
 			if constexpr (F >= 2) {
-				atomic_add_f16x2(a.grad + (size_t)e * F + 2 * pair, f16x2{(f16)(w * g0), (f16)(w * g1)});
+				atomic_add_f16x2(a.grad + (size_t)e * F + 2 * pair, f16x2{to_f16(w * g0), to_f16(w * g1)});
 			} else {
 				// F == 1: pack with a +0 partner so the 4-byte aligned packed add touches only entry e
 				const size_t idx = e;
-				f16x2 v = (idx & 1) ? f16x2{(f16)0.f, (f16)(w * g0)} : f16x2{(f16)(w * g0), (f16)0.f};
+				f16x2 v = (idx & 1) ? f16x2{(f16)0.f, to_f16(w * g0)} : f16x2{to_f16(w * g0), (f16)0.f};
 				atomic_add_f16x2(a.grad + (idx & ~(size_t)1), v);
 			}
 		}

@@ -241,10 +241,10 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 			e[q][k] = corner_index<D>(c, l, base, k) - off_l;
 			r[q][k] = atomicAdd(&lh[e[q][k] >> B], 1u);
 			const float w = corner_weight<D>(frac, k);
-			if constexpr (F == 1) val[q][k] = (f16)(w * g[0]);
+			if constexpr (F == 1) val[q][k] = to_f16(w * g[0]);
 			else {
 #pragma unroll
-				for (uint32_t f = 0; f < F; ++f) val[q][k][f] = (f16)(w * g[f]);
+				for (uint32_t f = 0; f < F; ++f) val[q][k][f] = to_f16(w * g[f]);
 			}
 		}
 	}

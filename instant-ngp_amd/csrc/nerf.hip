@@ -1,8 +1,10 @@
 // nerf.hip — NeRF training kernels for gfx950 (see nerf.h). Each kernel cites the reference kernel
 // it re-implements; float formulas follow the reference line by line (glm vector ops written out
-// per component, -ffp-contract=off), so with cone_angle = 0 sample coordinates match the oracle
-// bit for bit. With cone_angle > 0 the log/exp stepping uses ocml logf/expf (the reference uses
-// --use_fast_math intrinsics), so positions match within float rounding.
+// per component, -ffp-contract=off). Every exp/log whose result decides an integer (cone-angle
+// stepping, compositing termination and compaction) is ngp_expf/ngp_logf from ngp_math.h, the same
+// instruction sequence the oracle runs, so sample indices, coordinates and compacted counts match the
+// oracle bit for bit at every cone angle (the reference's libdevice logf/expf/__expf are <= 2-ulp
+// approximations of the same functions).
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
@@ -10,6 +12,7 @@
 #include <cstring>
 
 #include "nerf.h"
+#include "ngp_math.h"
 #include "profiler.h"
 #include "rng.h"
 
@@ -38,22 +41,22 @@ __device__ __forceinline__ float div_min_stepsize(float t) {
 // testbed_nerf.cu:114-184
 __device__ float to_stepping_space(float t, float cone) {
 	if (cone <= 1e-5f) return div_min_stepsize(t);
-	const float log1p_c = logf(1.0f + cone);
-	const float a = (logf(MIN_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
-	const float b = (logf(MAX_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
-	const float at = expf(a * log1p_c), bt = expf(b * log1p_c);
+	const float log1p_c = ngp_logf(1.0f + cone);
+	const float a = (ngp_logf(MIN_CONE_STEPSIZE) - ngp_logf(log1p_c)) / log1p_c;
+	const float b = (ngp_logf(MAX_CONE_STEPSIZE) - ngp_logf(log1p_c)) / log1p_c;
+	const float at = ngp_expf(a * log1p_c), bt = ngp_expf(b * log1p_c);
 	if (t <= at) return (t - at) / MIN_CONE_STEPSIZE + a;
-	if (t <= bt) return logf(t) / log1p_c;
+	if (t <= bt) return ngp_logf(t) / log1p_c;
 	return (t - bt) / MAX_CONE_STEPSIZE + b;
 }
 __device__ float from_stepping_space(float n, float cone) {
 	if (cone <= 1e-5f) return n * MIN_CONE_STEPSIZE;
-	const float log1p_c = logf(1.0f + cone);
-	const float a = (logf(MIN_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
-	const float b = (logf(MAX_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
-	const float at = expf(a * log1p_c), bt = expf(b * log1p_c);
+	const float log1p_c = ngp_logf(1.0f + cone);
+	const float a = (ngp_logf(MIN_CONE_STEPSIZE) - ngp_logf(log1p_c)) / log1p_c;
+	const float b = (ngp_logf(MAX_CONE_STEPSIZE) - ngp_logf(log1p_c)) / log1p_c;
+	const float at = ngp_expf(a * log1p_c), bt = ngp_expf(b * log1p_c);
 	if (n <= a) return (n - a) * MIN_CONE_STEPSIZE + at;
-	if (n <= b) return expf(n * log1p_c);
+	if (n <= b) return ngp_expf(n * log1p_c);
 	return (n - b) * MAX_CONE_STEPSIZE + bt;
 }
 __device__ __forceinline__ float advance_n_steps(float t, float cone, float n) { return from_stepping_space(to_stepping_space(t, cone) + n, cone); }
@@ -165,14 +168,14 @@ __device__ __forceinline__ float unwarp_dt(float dt) {  // :418-421
 __device__ __forceinline__ float srgb_to_linear(float s) { return s <= 0.04045f ? s / 12.92f : powf((s + 0.055f) / 1.055f, 2.4f); }
 __device__ __forceinline__ float linear_to_srgb(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * powf(l, 0.41666f) - 0.055f; }
 
-__device__ __forceinline__ float logistic(float x) { return 1.0f / (1.0f + expf(-x)); }  // tcnn::logistic
-// testbed_nerf.cu:317-378 (the reference's __expf is the fast intrinsic; ocml __expf here)
+__device__ __forceinline__ float logistic(float x) { return 1.0f / (1.0f + ngp_expf(-x)); }  // tcnn::logistic
+// testbed_nerf.cu:317-378 (the reference's __expf; ngp_expf here and in the oracle)
 __device__ float network_to_rgb(float v, uint32_t act) {
 	switch (act) {
 		case ACT_NONE: return v;
 		case ACT_RELU: return v > 0.0f ? v : 0.0f;
 		case ACT_LOGISTIC: return logistic(v);
-		case ACT_EXP: return __expf(fminf(fmaxf(v, -10.0f), 10.0f));
+		case ACT_EXP: return ngp_expf(fminf(fmaxf(v, -10.0f), 10.0f));
 	}
 	return 0.0f;
 }
@@ -181,7 +184,7 @@ __device__ float network_to_rgb_derivative(float v, uint32_t act) {
 		case ACT_NONE: return 1.0f;
 		case ACT_RELU: return v > 0.0f ? 1.0f : 0.0f;
 		case ACT_LOGISTIC: { const float d = logistic(v); return d * (1 - d); }
-		case ACT_EXP: return __expf(fminf(fmaxf(v, -10.0f), 10.0f));
+		case ACT_EXP: return ngp_expf(fminf(fmaxf(v, -10.0f), 10.0f));
 	}
 	return 0.0f;
 }
@@ -190,7 +193,7 @@ __device__ float network_to_density(float v, uint32_t act) {
 		case ACT_NONE: return v;
 		case ACT_RELU: return v > 0.0f ? v : 0.0f;
 		case ACT_LOGISTIC: return logistic(v);
-		case ACT_EXP: return __expf(v);
+		case ACT_EXP: return ngp_expf(v);
 	}
 	return 0.0f;
 }
@@ -199,7 +202,7 @@ __device__ float network_to_density_derivative(float v, uint32_t act) {
 		case ACT_NONE: return 1.0f;
 		case ACT_RELU: return v > 0.0f ? 1.0f : 0.0f;
 		case ACT_LOGISTIC: { const float d = logistic(v); return d * (1 - d); }
-		case ACT_EXP: return __expf(fminf(fmaxf(v, -15.0f), 15.0f));
+		case ACT_EXP: return ngp_expf(fminf(fmaxf(v, -15.0f), 15.0f));
 	}
 	return 0.0f;
 }
@@ -218,7 +221,7 @@ __device__ void loss_channel(float target, float pred, uint32_t type, float* los
 			*grad = (ad > alpha ? (d > 0 ? 1.0f : -1.0f) : (d / alpha)) / 5.0f;
 			return;
 		}
-		case LOSS_LOGL1: { const float div = fabsf(d) + 1.0f; *loss = logf(div); *grad = copysignf(1.0f / div, d); return; }
+		case LOSS_LOGL1: { const float div = fabsf(d) + 1.0f; *loss = ngp_logf(div); *grad = copysignf(1.0f / div, d); return; }
 		default: *loss = d * d; *grad = 2.0f * d; return;
 	}
 }
@@ -648,7 +651,7 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 			const f16x4 o = *(const f16x4*)(out + (size_t)jj * a.out_stride);
 			const float dt = unwarp_dt(ci[(size_t)jj * 7 + 3]);
 			const float density = network_to_density((float)o[3], cfg.density_activation);
-			alpha = 1.f - __expf(-density * dt);
+			alpha = 1.f - ngp_expf(-density * dt);
 			cr = network_to_rgb((float)o[0], cfg.rgb_activation);
 			cg = network_to_rgb((float)o[1], cfg.rgb_activation);
 			cb = network_to_rgb((float)o[2], cfg.rgb_activation);
@@ -748,7 +751,7 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const ngp_nerf_config cfg, L
 			for (int k = 0; k < 3; ++k) rgb[k] = network_to_rgb((float)o[k], cfg.rgb_activation);
 			dt = unwarp_dt(cc[3]);
 			const float density = network_to_density((float)o[3], cfg.density_activation);
-			alpha = 1.f - __expf(-density * dt);
+			alpha = 1.f - ngp_expf(-density * dt);
 		}
 		// compositing in sample order; lane K keeps its weight, transmittance after it and rgb prefix
 		float my_w = 0.f, my_t = 0.f, my_r2[3] = {0.f, 0.f, 0.f};
@@ -1172,7 +1175,7 @@ __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, ui
 		const float o3 = (float)out[r + 3 * (size_t)stride];
 		const float T = 1.f - c[3];
 		const float dt = unwarp_dt(coords[r * 7 + 3]);
-		const float alpha = 1.f - __expf(-network_to_density(o3, a.density_activation) * dt);
+		const float alpha = 1.f - ngp_expf(-network_to_density(o3, a.density_activation) * dt);
 		const float weight = alpha * T;
 		c[0] += network_to_rgb(o0, a.rgb_activation) * weight;
 		c[1] += network_to_rgb(o1, a.rgb_activation) * weight;

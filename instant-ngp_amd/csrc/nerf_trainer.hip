@@ -103,6 +103,7 @@ struct ngp_nerf_trainer {
 	const void* graph_in = nullptr;
 	const void* graph_dl = nullptr;
 	uint32_t graph_n = 0;
+	uint64_t graph_epoch = 0;  // model workspace epoch at capture (ngp_model_workspace_epoch)
 	hipStream_t own_stream = nullptr;  // used when the caller passes the null stream (graphs need a stream)
 	// per-step counters published by the step's last kernel into host-coherent pinned memory, read by
 	// spinning on a sequence number (no copy-engine transfer, no blocking stream synchronize)
@@ -454,6 +455,9 @@ int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint3
 
 int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** grid, uint8_t** bitfield, float** mean) {
 	if (!t) return NGP_INVALID;
+	// the caller may write these: a prelaunched sampler (pipelining) read the bitfield before any such
+	// write, so discard it and let the next step sample serially after the caller's writes
+	t->drain();
 	if (grid) *grid = (float*)t->grid.p;
 	if (bitfield) *bitfield = (uint8_t*)t->bitfield.p;
 	if (mean) *mean = (float*)t->mean.p;
@@ -517,7 +521,11 @@ static void wait_published(volatile uint32_t* host, uint32_t seq, hipStream_t s)
 		if ((spin & 1023) == 1023) {
 			const hipError_t q = hipStreamQuery(s);
 			if (q != hipSuccess && q != hipErrorNotReady) NGP_HIP(q);
-			if (q == hipSuccess && __atomic_load_n(&host[4], __ATOMIC_ACQUIRE) == seq) return;
+			if (q == hipSuccess) {  // the stream drained: the publishing kernel ran, so its write is visible
+				if (__atomic_load_n(&host[4], __ATOMIC_ACQUIRE) == seq) return;
+				const hipError_t e = hipGetLastError();
+				throw Error(std::string("nerf train step: stream idle but counters not published (") + hipGetErrorString(e) + ")");
+			}
 			NGP_CHECK(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60), "nerf train step: counters not published");
 		}
 		__builtin_ia32_pause();
@@ -649,13 +657,17 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		{
 		ProfScope ps("nerf_train_pass", s);
 		if (W == 1) {
-			if (!t->train_graph || t->graph_in != coords_c || t->graph_dl != dloss || t->graph_n != Bl) {
+			// re-record when the graph's buffers moved: the sample buffers, or any model workspace (a
+			// density-grid update through ngp_density can grow the encoding workspace after a snapshot load)
+			if (!t->train_graph || t->graph_in != coords_c || t->graph_dl != dloss || t->graph_n != Bl ||
+			    t->graph_epoch != ngp_model_workspace_epoch(t->model)) {
 				if (t->train_graph) ngp_graph_destroy(t->train_graph);
 				t->train_graph = nullptr;
 				check_rc(ngp_trainer_capture_training_step(t->trainer, s, Bl, coords_c, 7, dloss, 16, 128.0f, 1, 1, &t->train_graph));
 				t->graph_in = coords_c;
 				t->graph_dl = dloss;
 				t->graph_n = Bl;
+				t->graph_epoch = ngp_model_workspace_epoch(t->model);
 			}
 			check_rc(ngp_graph_launch(t->train_graph, s));
 		} else {

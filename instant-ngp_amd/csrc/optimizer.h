@@ -23,8 +23,13 @@ struct AdamState {
 	float* ema32; f16* ema16;
 	f16* frags; const uint32_t* fragmap;
 	const uint32_t* step_base; uint32_t step_add;
+	const AdamConfig* cfg_dev;  // non-null (captured steps): hyperparameters read from device memory
 };
+// The trainer's device control block: ctl[0] optimizer step, ctl[1] block counter, AdamConfig at
+// ctl + CTL_CFG. A graph launch rewrites step and config (set_device_ctl), so replayed steps follow
+// set_learning_rate / set_option like eager ones.
+constexpr uint32_t CTL_CFG = 16;
 void adam_ema_update(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float loss_scale, const AdamState& st, hipStream_t s);
-void set_device_step(uint32_t* ctl, uint32_t step, hipStream_t s);
+void set_device_ctl(uint32_t* ctl, uint32_t step, const AdamConfig& c, hipStream_t s);
 
 }  // namespace ngp

@@ -22,8 +22,9 @@ __device__ __forceinline__ float lr_schedule(const AdamConfig& c, uint32_t step)
 	return r;
 }
 
-__global__ void k_adam_ema(const uint32_t i0, const uint32_t n, const uint32_t n_matrix, const float loss_scale, const AdamConfig c,
+__global__ void k_adam_ema(const uint32_t i0, const uint32_t n, const uint32_t n_matrix, const float loss_scale, const AdamConfig c_arg,
                            const AdamState st) {
+	const AdamConfig c = st.cfg_dev ? *st.cfg_dev : c_arg;
 	const uint32_t i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t step = (st.step_base ? *st.step_base : 0u) + st.step_add;
 	if (i < n) {
@@ -63,9 +64,10 @@ __global__ void k_adam_ema(const uint32_t i0, const uint32_t n, const uint32_t n
 // group whose four parameters are all lazily skipped (grid entries without gradient) reads only the
 // gradient and the EMA inputs. Same per-parameter arithmetic as k_adam_ema.
 __global__ void __launch_bounds__(256) k_adam_ema4(const uint32_t n4, const uint32_t n_matrix, const float loss_scale,
-                                                   const AdamConfig c, const AdamState st) {
+                                                   const AdamConfig c_arg, const AdamState st) {
 	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
 	if (t >= n4) return;
+	const AdamConfig c = st.cfg_dev ? *st.cfg_dev : c_arg;
 	const uint32_t i0 = 4 * t;
 	const uint32_t step = (st.step_base ? *st.step_base : 0u) + st.step_add;
 	const f16x4 gh = *(const f16x4*)(st.g16 + i0);
@@ -130,7 +132,10 @@ __global__ void __launch_bounds__(256) k_adam_ema4(const uint32_t n4, const uint
 	}
 }
 
-__global__ void k_set_step(uint32_t* ctl, uint32_t step) { ctl[0] = step; }
+__global__ void k_set_ctl(uint32_t* ctl, uint32_t step, const AdamConfig c) {
+	ctl[0] = step;
+	*(AdamConfig*)(ctl + CTL_CFG) = c;
+}
 
 float AdamConfig::lr_at(uint32_t step) const {
 	float r = lr;
@@ -151,8 +156,8 @@ void adam_ema_update(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float l
 	NGP_HIP(hipGetLastError());
 }
 
-void set_device_step(uint32_t* ctl, uint32_t step, hipStream_t s) {
-	k_set_step<<<1, 1, 0, s>>>(ctl, step);
+void set_device_ctl(uint32_t* ctl, uint32_t step, const AdamConfig& c, hipStream_t s) {
+	k_set_ctl<<<1, 1, 0, s>>>(ctl, step, c);
 	NGP_HIP(hipGetLastError());
 }
 

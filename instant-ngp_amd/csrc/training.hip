@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(256) k_loss(uint32_t type, const LossEvalArgs 
 				float v, gr;
 				loss_one(type, (float)a.out[(size_t)i * a.out_stride + j], a.target[(size_t)i * a.target_stride + j], inv_n, v, gr);
 				sum += v;
-				g[j] = (f16)(a.loss_scale * gr);
+				g[j] = to_f16(a.loss_scale * gr);
 			} else {
 				g[j] = (f16)0.f;
 			}

@@ -200,16 +200,26 @@ class NerfTraining:
         check(lib().ngp_nerf_trainer_create(network.handle, trainer.handle, dataset.handle, C.byref(self.cfg), seed,
                                             C.byref(h)))
         self.handle = h
+
+    def _buffers(self):
+        # ngp_nerf_trainer_buffers discards a prelaunched (pipelined) sampler, so writes through the
+        # returned views are seen by the next step's sampling
         g, b, m = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        check(lib().ngp_nerf_trainer_buffers(h, C.byref(g), C.byref(b), C.byref(m)))
-        # density grid holds max_cascade + 1 cascades (testbed_nerf.cu:3412-3420); the bitfield all 8
-        self.density_grid = wrap_device(g.value, N_CELLS * (self.cfg.max_cascade + 1), torch.float32)
-        self._bitfield_ptr = b.value
-        self.mean_density = wrap_device(m.value, 1, torch.float32)
+        check(lib().ngp_nerf_trainer_buffers(self.handle, C.byref(g), C.byref(b), C.byref(m)))
+        return g.value, b.value, m.value
+
+    @property
+    def density_grid(self):
+        """fp32 [128^3 x (max_cascade + 1)] (testbed_nerf.cu:3412-3420), Morton order per cascade."""
+        return wrap_device(self._buffers()[0], N_CELLS * (self.cfg.max_cascade + 1), torch.float32)
+
+    @property
+    def mean_density(self):
+        return wrap_device(self._buffers()[2], 1, torch.float32)
 
     @property
     def bitfield(self):
-        words = wrap_device(self._bitfield_ptr, BITFIELD_BYTES // 4, torch.float32)
+        words = wrap_device(self._buffers()[1], BITFIELD_BYTES // 4, torch.float32)
         return words.view(torch.uint8)
 
     def set_data_parallel(self, rank, world, group=None):
@@ -233,7 +243,8 @@ class NerfTraining:
 
     def set_pipeline(self, enable):
         """Launch the next step's ray sampling under this step's training pass (default on; identical
-        samples). Turn off before writing density_grid / bitfield between steps."""
+        samples). Reading density_grid / bitfield / mean_density discards a prelaunched sampler, so
+        writes through them reach the next step."""
         check(lib().ngp_nerf_trainer_set_pipeline(self.handle, int(enable)))
 
     def save_snapshot(self, path, network_config=None, include_optimizer_state=False, compress=True, stream=None):

@@ -126,6 +126,16 @@ class Model:
     def reserve(self, n):
         check(lib().ngp_model_reserve(self.handle, n))
 
+    def workspace(self, name, n):
+        """The last training pass's fp16 intermediates as a [n x encoding_width] view: "encoding" (grid
+        output) or "dL_dencoding" (grid backward input) — tcnn's forward_activations(ctx) role."""
+        p, nb = C.c_void_p(), C.c_uint64()
+        check(lib().ngp_model_workspace(self.handle, name.encode(), C.byref(p), C.byref(nb)))
+        w = self.layout().encoding_width
+        if n * w * 2 > nb.value:
+            raise ValueError(f"workspace {name} holds {nb.value} bytes, fewer than {n} rows")
+        return wrap_device(p.value, n * w, torch.float16).view(n, w)
+
     # -- compute ------------------------------------------------------------------------------
     def inference(self, x, output=None, layout=LAYOUT_AOS, use_inference_params=True, stream=None):
         _check_input(x, self.input_width())

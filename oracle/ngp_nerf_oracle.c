@@ -10,6 +10,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "ngp_math.h" /* the engine's expf/logf: see the header */
+
 #define EXPORT __attribute__((visibility("default")))
 
 typedef struct { uint64_t state, inc; } orc_pcg32;
@@ -101,20 +103,20 @@ EXPORT void orc_lens_undistort(uint32_t mode, const float* k, float* u, float* v
 /* ---- stepping (testbed_nerf.cu:114-184) ---- */
 static float to_step(float t, float c) {
 	if (c <= 1e-5f) return t / MIN_STEP;
-	float l = logf(1.0f + c);
-	float a = (logf(MIN_STEP) - logf(l)) / l, b = (logf(MAX_STEP) - logf(l)) / l;
-	float at = expf(a * l), bt = expf(b * l);
+	float l = ngp_logf(1.0f + c);
+	float a = (ngp_logf(MIN_STEP) - ngp_logf(l)) / l, b = (ngp_logf(MAX_STEP) - ngp_logf(l)) / l;
+	float at = ngp_expf(a * l), bt = ngp_expf(b * l);
 	if (t <= at) return (t - at) / MIN_STEP + a;
-	else if (t <= bt) return logf(t) / l;
+	else if (t <= bt) return ngp_logf(t) / l;
 	else return (t - bt) / MAX_STEP + b;
 }
 static float from_step(float n, float c) {
 	if (c <= 1e-5f) return n * MIN_STEP;
-	float l = logf(1.0f + c);
-	float a = (logf(MIN_STEP) - logf(l)) / l, b = (logf(MAX_STEP) - logf(l)) / l;
-	float at = expf(a * l), bt = expf(b * l);
+	float l = ngp_logf(1.0f + c);
+	float a = (ngp_logf(MIN_STEP) - ngp_logf(l)) / l, b = (ngp_logf(MAX_STEP) - ngp_logf(l)) / l;
+	float at = ngp_expf(a * l), bt = ngp_expf(b * l);
 	if (n <= a) return (n - a) * MIN_STEP + at;
-	else if (n <= b) return expf(n * l);
+	else if (n <= b) return ngp_expf(n * l);
 	else return (n - b) * MAX_STEP + bt;
 }
 static float calc_dt(float t, float c) { return from_step(to_step(t, c) + 1.0f, c) - t; }
@@ -355,20 +357,20 @@ EXPORT void orc_nerf_generate_samples(const ocfg* c, const oimg* ims, const uint
 
 static float s2l(float s) { return s <= 0.04045f ? s / 12.92f : powf((s + 0.055f) / 1.055f, 2.4f); }
 static float l2s(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * powf(l, 0.41666f) - 0.055f; }
-static float logistic(float x) { return 1.0f / (1.0f + expf(-x)); }
+static float logistic(float x) { return 1.0f / (1.0f + ngp_expf(-x)); }
 static float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
-/* testbed_nerf.cu:317-378 (expf for the reference's __expf) */
+/* testbed_nerf.cu:317-378 (ngp_expf for the reference's __expf) */
 static float to_rgb(float v, uint32_t a) {
-	switch (a) { case 0: return v; case 1: return v > 0 ? v : 0; case 2: return logistic(v); default: return expf(clampf(v, -10.f, 10.f)); }
+	switch (a) { case 0: return v; case 1: return v > 0 ? v : 0; case 2: return logistic(v); default: return ngp_expf(clampf(v, -10.f, 10.f)); }
 }
 static float to_rgb_d(float v, uint32_t a) {
-	switch (a) { case 0: return 1; case 1: return v > 0 ? 1.f : 0.f; case 2: { float d = logistic(v); return d * (1 - d); } default: return expf(clampf(v, -10.f, 10.f)); }
+	switch (a) { case 0: return 1; case 1: return v > 0 ? 1.f : 0.f; case 2: { float d = logistic(v); return d * (1 - d); } default: return ngp_expf(clampf(v, -10.f, 10.f)); }
 }
 static float to_dens(float v, uint32_t a) {
-	switch (a) { case 0: return v; case 1: return v > 0 ? v : 0; case 2: return logistic(v); default: return expf(v); }
+	switch (a) { case 0: return v; case 1: return v > 0 ? v : 0; case 2: return logistic(v); default: return ngp_expf(v); }
 }
 static float to_dens_d(float v, uint32_t a) {
-	switch (a) { case 0: return 1; case 1: return v > 0 ? 1.f : 0.f; case 2: { float d = logistic(v); return d * (1 - d); } default: return expf(clampf(v, -15.f, 15.f)); }
+	switch (a) { case 0: return 1; case 1: return v > 0 ? 1.f : 0.f; case 2: { float d = logistic(v); return d * (1 - d); } default: return ngp_expf(clampf(v, -15.f, 15.f)); }
 }
 /* testbed_nerf.cu:186-276, 1340-1355 */
 static void lossg(float tgt, float p, uint32_t type, float* l, float* g) {
@@ -384,7 +386,7 @@ static void lossg(float tgt, float p, uint32_t type, float* l, float* g) {
 			*g = (ad > al ? (d > 0 ? 1.0f : -1.0f) : (d / al)) / 5.0f;
 			return;
 		}
-		case 5: { float dv = fabsf(d) + 1.0f; *l = logf(dv); *g = copysignf(1.0f / dv, d); return; }
+		case 5: { float dv = fabsf(d) + 1.0f; *l = ngp_logf(dv); *g = copysignf(1.0f / dv, d); return; }
 		default: *l = d * d; *g = 2.0f * d; return;
 	}
 }
@@ -410,7 +412,7 @@ EXPORT void orc_nerf_compute_loss(const ocfg* c, const oimg* ims, const uint32_t
 			if (t < 1e-4f) break;
 			float dt = ci[(size_t)cn * 7 + 3] * (maxs - MIN_STEP) + MIN_STEP;
 			float dens = to_dens(orc_f16_to_f32(o[cn * 16 + 3]), c->density_activation);
-			float alpha = 1.f - expf(-dens * dt), w = alpha * t;
+			float alpha = 1.f - ngp_expf(-dens * dt), w = alpha * t;
 			for (int k = 0; k < 3; ++k) rgb_ray[k] += w * to_rgb(orc_f16_to_f32(o[cn * 16 + k]), c->rgb_activation);
 			t *= (1.f - alpha);
 		}
@@ -469,7 +471,7 @@ EXPORT void orc_nerf_compute_loss(const ocfg* c, const oimg* ims, const uint32_t
 			for (int k = 0; k < 4; ++k) ov[k] = orc_f16_to_f32(o[j * 16 + k]);
 			for (int k = 0; k < 3; ++k) rgb[k] = to_rgb(ov[k], c->rgb_activation);
 			float dens = to_dens(ov[3], c->density_activation);
-			float alpha = 1.f - expf(-dens * dt), w = alpha * t;
+			float alpha = 1.f - ngp_expf(-dens * dt), w = alpha * t;
 			for (int k = 0; k < 3; ++k) r2[k] += w * rgb[k];
 			t *= (1.0f - alpha);
 			float suf[3];
@@ -685,7 +687,7 @@ EXPORT void orc_nerf_render_composite(const ocfg* c, uint32_t n_px, uint32_t max
 			const uint16_t* o = out16 + ((size_t)i * max_per_ray + k) * 16;
 			const float T = 1.f - a;
 			const float dt = coords[((size_t)i * max_per_ray + k) * 7 + 3] * (MIN_STEP * (1 << (CASCADES - 1)) - MIN_STEP) + MIN_STEP;
-			const float alpha = 1.f - expf(-to_dens(orc_f16_to_f32(o[3]), c->density_activation) * dt);
+			const float alpha = 1.f - ngp_expf(-to_dens(orc_f16_to_f32(o[3]), c->density_activation) * dt);
 			const float w = alpha * T;
 			r += to_rgb(orc_f16_to_f32(o[0]), c->rgb_activation) * w;
 			g += to_rgb(orc_f16_to_f32(o[1]), c->rgb_activation) * w;
@@ -700,4 +702,9 @@ EXPORT void orc_nerf_render_composite(const ocfg* c, uint32_t n_px, uint32_t max
 		const float cc[4] = {r, g, b, a};
 		for (int k = 0; k < 4; ++k) f[k] = cc[k] + f[k] * (1.0f - a);
 	}
+}
+
+/* The shared transcendental (instant-ngp_amd/csrc/ngp_math.h), exported for its accuracy test. */
+EXPORT void orc_math_eval(int fn, size_t n, const float* x, float* y) {
+	for (size_t i = 0; i < n; ++i) y[i] = fn == 0 ? ngp_expf(x[i]) : ngp_logf(x[i]);
 }

@@ -254,6 +254,60 @@ EXPORT void orc_grid_backward(const orc_grid* g, size_t n, const float* pos, uin
 	}
 }
 
+/* Backward, contribution-exact: tcnn's kernel_grid_backward rounds every contribution w * dL/dy to the
+ * table precision before its half2 atomicAdd (a2: "(__half)((float)g * w)"); this restatement keeps that
+ * rounding, sums the fp16 contributions exactly (every fp16 value is an integer multiple of 2^-24, so
+ * an int64 in those units is exact and the sum order-independent) and rounds once:
+ *   grad16[e] = f16( f32( (double)sum * 2^-24 ) )          (overwrite)
+ *   grad16[e] = f16( f32(sum * 2^-24) + f32(grad16[e]) )    (accumulate)
+ * which is the engine's destination-bucketed backward contract (csrc/grid_scatter.hip), so the two are
+ * compared with array_equal. dL_dy: fp16 bits, element (i, l*F+f) at dL_dy[i * dy_stride + l*F + f].
+ * abs_sum (optional, double [entries*F]) receives sum |w * dL/dy| per parameter: the conditioning of
+ * each sum, used by end-to-end tests whose dL/dy differ from the engine's by fp16 rounding. */
+EXPORT void orc_grid_backward_exact(const orc_grid* g, size_t n, const float* pos, uint32_t pos_stride,
+                                    const uint16_t* dL_dy, uint32_t dy_stride, float max_level,
+                                    const float* max_level_per_sample, int accumulate, uint16_t* grad16, double* abs_sum) {
+	const uint32_t L = g->n_levels, F = g->n_features;
+	const size_t np = (size_t)g->offsets[L] * F;
+	int64_t* acc = (int64_t*)calloc(np, sizeof(int64_t));
+	if (abs_sum) memset(abs_sum, 0, np * sizeof(double));
+	#pragma omp parallel for schedule(static)
+	for (size_t i = 0; i < n; ++i) {
+		const float* x = pos + i * pos_stride;
+		float ml = (max_level_per_sample ? max_level_per_sample[i] : max_level) * (float)L;
+		for (uint32_t l = 0; l < L; ++l) {
+			if ((float)l > ml + 1e-3f) continue; /* tcnn backward: '>' (the forward zeroes at '>=') */
+			float frac[4]; uint32_t base[4], p[4];
+			grid_corner_setup(g, l, x, frac, base);
+			for (uint32_t c = 0; c < (1u << g->n_dims); ++c) {
+				float w = corner_weight(g, c, frac, base, p);
+				size_t e = (size_t)g->offsets[l] + grid_index(g, l, p);
+				for (uint32_t f = 0; f < F; ++f) {
+					float gy = hf(dL_dy[i * dy_stride + l * F + f]);
+					float contrib = hf(fh(w * gy));
+					int64_t q = (int64_t)(contrib * 16777216.0f);
+					if (q) {
+						#pragma omp atomic
+						acc[e * F + f] += q;
+					}
+					if (abs_sum) {
+						double a = fabs((double)w * (double)gy);
+						#pragma omp atomic
+						abs_sum[e * F + f] += a;
+					}
+				}
+			}
+		}
+	}
+	#pragma omp parallel for schedule(static)
+	for (size_t k = 0; k < np; ++k) {
+		float s = (float)((double)acc[k] * (1.0 / 16777216.0));
+		if (accumulate) s += hf(grad16[k]);
+		grad16[k] = fh(s);
+	}
+	free(acc);
+}
+
 /* Entry index per (sample, level, corner): for bit-exact integer parity of the hashing. */
 EXPORT void orc_grid_indices(const orc_grid* g, size_t n, const float* pos, uint32_t pos_stride, uint32_t* idx) {
 	const uint32_t L = g->n_levels, C = 1u << g->n_dims;
@@ -320,7 +374,7 @@ static void layer_dims(const orc_mlp* m, uint32_t l, uint32_t* in, uint32_t* out
 
 /* One sample's forward; acts receives every layer's fp16-rounded output (post-activation for hidden
  * layers), acts must hold (n_hidden)*width + out_pad floats. */
-static void mlp_forward_one(const orc_mlp* m, const uint16_t* w, const float* x, float* acts) {
+static void mlp_forward_one_abs(const orc_mlp* m, const uint16_t* w, const float* x, float* acts, float* out_abs) {
 	uint32_t nl = m->n_hidden + 1;
 	float buf_in[256];
 	memcpy(buf_in, x, m->in_pad * sizeof(float));
@@ -328,9 +382,13 @@ static void mlp_forward_one(const orc_mlp* m, const uint16_t* w, const float* x,
 	for (uint32_t l = 0; l < nl; ++l) {
 		uint32_t in, out; size_t off; layer_dims(m, l, &in, &out, &off);
 		for (uint32_t o = 0; o < out; ++o) {
-			double s = 0.0;
+			double s = 0.0, sa = 0.0;
 			const uint16_t* wr = w + off + (size_t)o * in;
 			for (uint32_t k = 0; k < in; ++k) s += (double)hf(wr[k]) * (double)buf_in[k];
+			if (out_abs && l == nl - 1) {
+				for (uint32_t k = 0; k < in; ++k) sa += fabs((double)hf(wr[k]) * (double)buf_in[k]);
+				out_abs[o] = (float)sa;
+			}
 			float v = rh((float)s);
 			if (l < nl - 1 && v < 0.f) v = 0.f;
 			dst[o] = v;
@@ -338,6 +396,10 @@ static void mlp_forward_one(const orc_mlp* m, const uint16_t* w, const float* x,
 		memcpy(buf_in, dst, out * sizeof(float));
 		dst += out;
 	}
+}
+
+static void mlp_forward_one(const orc_mlp* m, const uint16_t* w, const float* x, float* acts) {
+	mlp_forward_one_abs(m, w, x, acts, NULL);
 }
 
 EXPORT void orc_set_num_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
@@ -359,8 +421,8 @@ EXPORT void orc_mlp_forward(const orc_mlp* m, const uint16_t* w, size_t n, const
 /* Backward of one sample given dL/dy (float, representable in fp16). Accumulates dW (double) and
  * writes dL/dx (fp16-rounded) if dx != NULL. Hidden-layer gradients are rounded to fp16 after the
  * ReLU mask, as the kernel feeds them to the next MFMA in fp16. */
-static void mlp_backward_one(const orc_mlp* m, const uint16_t* w, const float* x, const float* acts,
-                             const float* dy, double* dW, float* dx) {
+static void mlp_backward_one_abs(const orc_mlp* m, const uint16_t* w, const float* x, const float* acts,
+                                 const float* dy, double* dW, double* dWabs, float* dx, float* dxabs) {
 	uint32_t nl = m->n_hidden + 1;
 	float g[256], gn[256];
 	memcpy(g, dy, m->out_pad * sizeof(float));
@@ -370,6 +432,9 @@ static void mlp_backward_one(const orc_mlp* m, const uint16_t* w, const float* x
 		/* dW[o][k] += g[o] * a_in[k] */
 		for (uint32_t o = 0; o < out; ++o)
 			for (uint32_t k = 0; k < in; ++k) dW[off + (size_t)o * in + k] += (double)g[o] * (double)a_in[k];
+		if (dWabs)
+			for (uint32_t o = 0; o < out; ++o)
+				for (uint32_t k = 0; k < in; ++k) dWabs[off + (size_t)o * in + k] += fabs((double)g[o] * (double)a_in[k]);
 		if (l == 0 && !dx) break;
 		for (uint32_t k = 0; k < in; ++k) {
 			double s = 0.0;
@@ -377,10 +442,20 @@ static void mlp_backward_one(const orc_mlp* m, const uint16_t* w, const float* x
 			float v = rh((float)s);
 			if (l > 0 && a_in[k] <= 0.f) v = 0.f; /* ReLU' from the forward activation */
 			gn[k] = v;
+			if (l == 0 && dxabs) {
+				double sa = 0.0;
+				for (uint32_t o = 0; o < out; ++o) sa += fabs((double)hf(w[off + (size_t)o * in + k]) * (double)g[o]);
+				dxabs[k] = (float)sa;
+			}
 		}
 		if (l == 0) { memcpy(dx, gn, in * sizeof(float)); break; }
 		memcpy(g, gn, in * sizeof(float));
 	}
+}
+
+static void mlp_backward_one(const orc_mlp* m, const uint16_t* w, const float* x, const float* acts,
+                             const float* dy, double* dW, float* dx) {
+	mlp_backward_one_abs(m, w, x, acts, dy, dW, NULL, dx, NULL);
 }
 
 EXPORT void orc_mlp_backward(const orc_mlp* m, const uint16_t* w, size_t n, const float* x, const float* dy,
@@ -489,6 +564,113 @@ EXPORT void orc_nerf_backward(const orc_nerf* m, const uint16_t* params, size_t 
 		float gy[256];
 		for (uint32_t k = 0; k < LF; ++k) gy[k] = denc[k];
 		orc_grid_backward(g, 1, x, m->in_stride, gy, 1.0f, NULL, grads + nd + nr);
+	}
+}
+
+/* Full-batch training pass (forward_impl + backward_impl, nerf_network.h:179-335), parallel over samples:
+ *   out      float [n x 16]  network output (fp16-rounded values), out_abs (optional) the sum |w a| of
+ *                            the contraction that produced each output (its conditioning);
+ *   grads    double [nd+nr]  MLP weight gradients, abs (optional) sum |g a| per weight;
+ *   denc16   fp16 bits [n x density.in_pad]  dL/d(encoding), the input of the grid backward
+ *            (orc_grid_backward_exact finishes the gradient with the engine's exact-sum contract),
+ *            denc_abs (optional) the sum |W g| of each dL/d(encoding) contraction.
+ * Per-thread accumulators are added in thread order after the loop (double: order effects ~1e-16). */
+EXPORT void orc_nerf_train_ex(const orc_nerf* m, const uint16_t* params, size_t n, const float* in, const float* dL_dout,
+                              float* out, float* out_abs, double* grads, double* grads_abs, uint16_t* denc16,
+                              float* denc_abs) {
+	size_t nd = orc_mlp_n_params(&m->density), nr = orc_mlp_n_params(&m->rgb);
+	const uint16_t* wd = params;
+	const uint16_t* wr = params + nd;
+	const orc_grid* g = &m->grid;
+	uint32_t LF = g->n_levels * g->n_features;
+	const uint16_t* table = wr + nr;
+	memset(grads, 0, (nd + nr) * sizeof(double));
+	if (grads_abs) memset(grads_abs, 0, (nd + nr) * sizeof(double));
+	#pragma omp parallel
+	{
+		double* lg = (double*)calloc(nd + nr, sizeof(double));
+		double* la = grads_abs ? (double*)calloc(nd + nr, sizeof(double)) : NULL;
+		float enc[256], dacts[1024], racts[1024], rin[32], drgb[16], drin[32], denc[256], dd[16], oa_r[16], oa_d[16];
+		#pragma omp for schedule(static)
+		for (size_t i = 0; i < n; ++i) {
+			const float* x = in + i * m->in_stride;
+			orc_grid_forward(g, 1, x, m->in_stride, table, 1.0f, NULL, enc);
+			for (uint32_t k = 0; k < m->density.in_pad; ++k) enc[k] = k < LF ? rh(enc[k]) : 0.f;
+			mlp_forward_one_abs(&m->density, wd, enc, dacts, oa_d);
+			const float* dout = dacts + m->density.n_hidden * m->density.width;
+			for (uint32_t k = 0; k < 16; ++k) rin[k] = dout[k];
+			float sh[16];
+			orc_sh4(x[m->dir_offset], x[m->dir_offset + 1], x[m->dir_offset + 2], sh);
+			for (uint32_t k = 0; k < 16; ++k) rin[16 + k] = rh(sh[k]);
+			mlp_forward_one_abs(&m->rgb, wr, rin, racts, oa_r);
+			const float* rout = racts + m->rgb.n_hidden * m->rgb.width;
+			for (uint32_t k = 0; k < 16; ++k) {
+				out[i * 16 + k] = k == 3 ? dout[0] : rout[k];
+				if (out_abs) out_abs[i * 16 + k] = k == 3 ? oa_d[0] : oa_r[k];
+			}
+			for (uint32_t k = 0; k < 16; ++k) drgb[k] = k < 3 ? dL_dout[i * 16 + k] : 0.f;
+			mlp_backward_one_abs(&m->rgb, wr, rin, racts, drgb, lg + nd, la ? la + nd : NULL, drin, NULL);
+			for (uint32_t k = 0; k < 16; ++k) dd[k] = drin[k];
+			dd[0] = rh(dd[0] + dL_dout[i * 16 + 3]); /* add_density_gradient, nerf_network.h:63-74 */
+			mlp_backward_one_abs(&m->density, wd, enc, dacts, dd, lg, la, denc,
+			                     denc_abs ? denc_abs + i * m->density.in_pad : NULL);
+			for (uint32_t k = 0; k < m->density.in_pad; ++k) denc16[i * m->density.in_pad + k] = fh(denc[k]);
+		}
+		#pragma omp for ordered schedule(static, 1)
+		for (int t = 0; t < omp_get_num_threads(); ++t) {
+			#pragma omp ordered
+			{
+				for (size_t k = 0; k < nd + nr; ++k) grads[k] += lg[k];
+				if (la) for (size_t k = 0; k < nd + nr; ++k) grads_abs[k] += la[k];
+			}
+		}
+		free(lg);
+		free(la);
+	}
+}
+
+/* The same full-batch pass for tcnn::NetworkWithInputEncoding (grid -> FullyFusedMLP; the image and
+ * SDF primitives, src/testbed.cu:4101-4110): param layout [MLP | grid], pos element (i, d) at
+ * pos[i * pos_stride + d], dL_dout float [n x mlp.out_pad]. Outputs as orc_nerf_train_ex. */
+EXPORT void orc_net_train_ex(const orc_grid* g, const orc_mlp* mlp, const uint16_t* params, size_t n, const float* pos,
+                             uint32_t pos_stride, const float* dL_dout, float* out, float* out_abs, double* grads,
+                             double* grads_abs, uint16_t* denc16, float* denc_abs) {
+	const size_t nm = orc_mlp_n_params(mlp);
+	const uint16_t* table = params + nm;
+	const uint32_t LF = g->n_levels * g->n_features, OP = mlp->out_pad, IP = mlp->in_pad;
+	const uint32_t nact = mlp->n_hidden * mlp->width + OP;
+	memset(grads, 0, nm * sizeof(double));
+	if (grads_abs) memset(grads_abs, 0, nm * sizeof(double));
+	#pragma omp parallel
+	{
+		double* lg = (double*)calloc(nm, sizeof(double));
+		double* la = grads_abs ? (double*)calloc(nm, sizeof(double)) : NULL;
+		float* acts = (float*)malloc(nact * sizeof(float));
+		float enc[512], denc[512], oa[256];
+		#pragma omp for schedule(static)
+		for (size_t i = 0; i < n; ++i) {
+			orc_grid_forward(g, 1, pos + i * pos_stride, pos_stride, table, 1.0f, NULL, enc);
+			for (uint32_t k = 0; k < IP; ++k) enc[k] = k < LF ? rh(enc[k]) : 0.f;
+			mlp_forward_one_abs(mlp, params, enc, acts, oa);
+			const float* o = acts + mlp->n_hidden * mlp->width;
+			for (uint32_t k = 0; k < OP; ++k) {
+				out[i * OP + k] = o[k];
+				if (out_abs) out_abs[i * OP + k] = oa[k];
+			}
+			mlp_backward_one_abs(mlp, params, enc, acts, dL_dout + i * OP, lg, la, denc, denc_abs ? denc_abs + i * IP : NULL);
+			for (uint32_t k = 0; k < IP; ++k) denc16[i * IP + k] = fh(denc[k]);
+		}
+		#pragma omp for ordered schedule(static, 1)
+		for (int t = 0; t < omp_get_num_threads(); ++t) {
+			#pragma omp ordered
+			{
+				for (size_t k = 0; k < nm; ++k) grads[k] += lg[k];
+				if (la) for (size_t k = 0; k < nm; ++k) grads_abs[k] += la[k];
+			}
+		}
+		free(lg);
+		free(la);
+		free(acts);
 	}
 }
 

@@ -78,6 +78,7 @@ def _declare(L):
     d("orc_grid_forward", None, P, sz, P, u32, P, f32, P, P)
     d("orc_grid_backward", None, P, sz, P, u32, P, f32, P, P)
     d("orc_grid_indices", None, P, sz, P, u32, P)
+    d("orc_grid_backward_exact", None, P, sz, P, u32, P, u32, f32, P, C.c_int, P, P)
     d("orc_sh4", None, f32, f32, f32, P)
     d("orc_mlp_n_params", u32, P)
     d("orc_mlp_forward", None, P, P, sz, P, P)
@@ -88,6 +89,8 @@ def _declare(L):
     d("orc_nerf_forward", None, P, P, sz, P, P)
     d("orc_nerf_density", None, P, P, sz, P, u32, P)
     d("orc_nerf_backward", None, P, P, sz, P, P, P, P)
+    d("orc_nerf_train_ex", None, P, P, sz, P, P, P, P, P, P, P, P)
+    d("orc_net_train_ex", None, P, P, P, sz, P, u32, P, P, P, P, P, P, P)
     d("orc_nerf_init", None, P, u64, P)
     d("orc_lr_at_step", f32, P, u32)
     d("orc_adam_step", None, P, u32, sz, sz, f32, P, P, P, P, P, P, P, P)
@@ -95,6 +98,7 @@ def _declare(L):
     d("orc_srgb_to_linear", f32, f32)
     d("orc_linear_to_srgb", f32, f32)
     d("orc_num_threads", C.c_int)
+    d("orc_math_eval", None, C.c_int, sz, P, P)
     d("orc_loss", C.c_double, C.c_int, u32, u32, P, u32, P, u32, f32, P, u32, P)
     d("orc_image_samples", None, u32, P, C.c_int, C.c_int, C.c_int, u32, u32, P, P, P)
     d("orc_triangle_cdf", None, u32, P, P)
@@ -181,6 +185,32 @@ def grid_backward(g, pos, dL_dy, max_level=1.0, max_level_per_sample=None, strid
     lib().orc_grid_backward(C.byref(g), n, ptr(pos), stride, ptr(np.ascontiguousarray(dL_dy, np.float32)), max_level,
                             ptr(mls), ptr(grad))
     return grad
+
+
+def math_eval(fn, x):
+    """ngp_math.h's expf (fn 0) / logf (fn 1) evaluated on the host."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.empty_like(x)
+    lib().orc_math_eval(fn, x.size, ptr(x), ptr(y))
+    return y
+
+
+def grid_backward_exact(g, pos, dL_dy16, max_level=1.0, max_level_per_sample=None, stride=None, grad16=None,
+                        with_abs_sum=False):
+    """Contribution-exact backward (the engine's bucketed contract): fp16 bits of the gradient.
+    dL_dy16: uint16 [n x W] (W >= L*F; only the first L*F columns are read). grad16: accumulate into
+    these fp16 bits (tcnn GradientMode accumulate) instead of overwriting."""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    dy = np.ascontiguousarray(dL_dy16).view(np.uint16)
+    n = pos.shape[0]
+    np_ = grid_n_entries(g) * g.n_features
+    acc = grad16 is not None
+    out = np.ascontiguousarray(grad16, dtype=np.uint16).copy() if acc else np.zeros(np_, np.uint16)
+    absum = np.zeros(np_, np.float64) if with_abs_sum else None
+    mls = None if max_level_per_sample is None else np.ascontiguousarray(max_level_per_sample, np.float32)
+    lib().orc_grid_backward_exact(C.byref(g), n, ptr(pos), stride or pos.shape[1], ptr(dy), dy.shape[1], max_level, ptr(mls),
+                                  int(acc), ptr(out), ptr(absum))
+    return (out, absum) if with_abs_sum else out
 
 
 def grid_indices(g, pos, stride=None):
@@ -273,6 +303,36 @@ def nerf_backward(m, params16, coords, dL_dout, want_denc=False, grads=None):
     lib().orc_nerf_backward(C.byref(m), ptr(np.ascontiguousarray(params16)), coords.shape[0], ptr(coords),
                             ptr(np.ascontiguousarray(dL_dout, np.float32)), ptr(grads), ptr(denc))
     return (grads, denc) if want_denc else grads
+
+
+def nerf_train_ex(m, params16, coords, dL_dout):
+    """Full-batch forward + backward with conditioning companions (orc_nerf_train_ex): dict of out,
+    out_abs [n x 16], grads, grads_abs (MLP section, float64), denc16 (fp16 bits) and denc_abs
+    [n x encoding width]."""
+    coords = np.ascontiguousarray(coords, dtype=np.float32)
+    n = coords.shape[0]
+    nm = mlp_n_params(m.density) + mlp_n_params(m.rgb)
+    r = {"out": np.zeros((n, 16), np.float32), "out_abs": np.zeros((n, 16), np.float32),
+         "grads": np.zeros(nm, np.float64), "grads_abs": np.zeros(nm, np.float64),
+         "denc16": np.zeros((n, m.density.in_pad), np.uint16), "denc_abs": np.zeros((n, m.density.in_pad), np.float32)}
+    lib().orc_nerf_train_ex(C.byref(m), ptr(np.ascontiguousarray(params16)), n, ptr(coords),
+                            ptr(np.ascontiguousarray(dL_dout, np.float32)), ptr(r["out"]), ptr(r["out_abs"]), ptr(r["grads"]),
+                            ptr(r["grads_abs"]), ptr(r["denc16"]), ptr(r["denc_abs"]))
+    return r
+
+
+def net_train_ex(grid, mlp, params16, pos, dL_dout, stride=None):
+    """orc_net_train_ex: NetworkWithInputEncoding full-batch pass with conditioning companions."""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    n = pos.shape[0]
+    nm = mlp_n_params(mlp)
+    r = {"out": np.zeros((n, mlp.out_pad), np.float32), "out_abs": np.zeros((n, mlp.out_pad), np.float32),
+         "grads": np.zeros(nm, np.float64), "grads_abs": np.zeros(nm, np.float64),
+         "denc16": np.zeros((n, mlp.in_pad), np.uint16), "denc_abs": np.zeros((n, mlp.in_pad), np.float32)}
+    lib().orc_net_train_ex(C.byref(grid), C.byref(mlp), ptr(np.ascontiguousarray(params16)), n, ptr(pos),
+                           stride or pos.shape[1], ptr(np.ascontiguousarray(dL_dout, np.float32)), ptr(r["out"]),
+                           ptr(r["out_abs"]), ptr(r["grads"]), ptr(r["grads_abs"]), ptr(r["denc16"]), ptr(r["denc_abs"]))
+    return r
 
 
 def adam_step(cfg, step, n_matrix, loss_scale, w32, w16, g16, m1, m2, steps, ema32=None, ema16=None):

@@ -3,9 +3,9 @@
 Bars: sample generation (ray indices, per-ray step counts and bases, ray origins/directions, sample
 coordinates) bit-exact with cone_angle 0 (no transcendental on that path; slots from prefix scans
 equal the oracle's ray-order slots); density-grid sample positions/indices and bitfields bit-exact;
-rollover bit-exact. Compositing uses __expf like the reference (testbed_nerf.cu:1744), so the loss
-pass is compared within 1e-4 relative (loss), fp16 gradients within 2e-3 of their scale, and the
-early-termination count may differ on at most 0.5 % of rays.
+rollover bit-exact. Cone-angle stepping and compositing evaluate ngp_math.h's expf/logf on both sides,
+so sample indices, compacted counts, bases and coordinates are bit-exact at every aabb_scale; losses
+agree to 1e-4 relative and fp16 loss gradients to 2 fp16 ulp (sRGB targets use powf).
 """
 import numpy as np
 import pytest
@@ -109,32 +109,42 @@ def test_generate_training_samples_opencv_lens(pkg, orc, scene_lens, n_rays, fra
     np.testing.assert_array_equal(got["coords"][:used], ref["coords"][:used])
 
 
-def test_generate_training_samples_cone(pkg, orc, scene):
-    """aabb_scale 4: cone-angle stepping (logf/expf) and cascades 0..2. An ulp of logf/expf moves t and
-    can flip a voxel-boundary decision further along the ray, so per-ray counts agree on >= 90 % of rays
-    (measured 94 %) and the batch total within 1 %."""
+@pytest.mark.parametrize("aabb_scale,n_rays,frac", [(4.0, 2048, 0.4), (8.0, 4096, 0.3), (8.0, 3000, 1.0), (16.0, 2048, 0.2)])
+def test_generate_training_samples_cone(pkg, orc, scene, aabb_scale, n_rays, frac):
+    """aabb_scale > 1 (the fox config is 8: 4 cascades): cone-angle stepping through logf/expf
+    (testbed_nerf.cu:114-184) and mips 0..max_cascade. Engine and oracle evaluate the same
+    ngp_math.h expf/logf, so counts, bases, rays and every sample coordinate are bit-exact."""
     ds, ims, pix = scene
-    cfg = pkg.nerf.default_config(4.0)
-    _, bf = occupancy(orc, seed=5, frac=0.4, max_cascade=cfg.max_cascade)
-    r = rng(pkg, 99)
-    n = 2048
-    got = pkg.nerf.generate_training_samples(ds, cfg, n, r, 1 << 20, torch.from_numpy(bf).cuda())
-    ref = orc.nerf_generate_samples(cfg, ims, pix, n, orc_rng(orc, r), 1 << 20, bf)
-    c_got = got["counters"].cpu().numpy().view(np.uint32)
-    assert c_got[0] == ref["counters"][0]
-    assert abs(int(c_got[1]) - int(ref["counters"][1])) <= 0.01 * ref["counters"][1]
+    cfg = pkg.nerf.default_config(aabb_scale)
+    assert cfg.cone_angle_constant > 1e-5
+    _, bf = occupancy(orc, seed=5 + n_rays, frac=frac, max_cascade=cfg.max_cascade)
+    r = rng(pkg, 99 + n_rays)
+    max_samples = 1 << 20
+    got = pkg.nerf.generate_training_samples(ds, cfg, n_rays, r, max_samples, torch.from_numpy(bf).cuda(), n_rays_total=n_rays)
+    ref = orc.nerf_generate_samples(cfg, ims, pix, n_rays, orc_rng(orc, r), max_samples, bf)
+    got = {k: v.cpu().numpy() for k, v in got.items()}
+    np.testing.assert_array_equal(got["counters"].view(np.uint32), ref["counters"])
     kept = int(ref["counters"][0])
-    np.testing.assert_array_equal(got["ray_indices"].cpu().numpy()[:kept].view(np.uint32), ref["ray_indices"][:kept])
-    steps_got = got["numsteps"].cpu().numpy()[:kept, 0].view(np.uint32)
-    assert np.mean(steps_got == ref["numsteps"][:kept, 0]) > 0.90
+    assert kept > 0
+    np.testing.assert_array_equal(got["ray_indices"][:kept].view(np.uint32), ref["ray_indices"][:kept])
+    np.testing.assert_array_equal(got["numsteps"][:kept].view(np.uint32), ref["numsteps"][:kept])
+    np.testing.assert_array_equal(got["rays"][:kept], ref["rays"][:kept])
+    used = min(int(ref["counters"][1]), max_samples)
+    assert used > 0
+    np.testing.assert_array_equal(got["coords"][:used], ref["coords"][:used])
 
 
-@pytest.mark.parametrize("loss_type,act", [(4, 3), (0, 2), (1, 3)])
-def test_compute_loss(pkg, orc, scene, loss_type, act):
+@pytest.mark.parametrize("loss_type,act,aabb_scale", [(4, 3, 1.0), (0, 2, 1.0), (1, 3, 1.0), (4, 3, 8.0), (0, 2, 4.0)])
+def test_compute_loss(pkg, orc, scene, loss_type, act, aabb_scale):
+    """compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012). Compositing weights use the shared
+    ngp_expf (the reference's __expf site :1744), so where each ray terminates, the compacted count,
+    every compacted {n, base} and every compacted coordinate are bit-exact, cone stepping included.
+    Losses and dL/doutput are floating point: the sRGB targets go through powf (ocml vs glibc), so
+    losses agree to rtol 1e-4 and each fp16 gradient to 2 fp16 ulp (+1e-7 absolute)."""
     ds, ims, pix = scene
-    cfg = pkg.nerf.default_config(1.0, loss_type=loss_type, rgb_activation=act, density_activation=3)
-    _, bf = occupancy(orc, seed=2, frac=0.5)
-    n_rays, max_samples = 2000, 1 << 16
+    cfg = pkg.nerf.default_config(aabb_scale, loss_type=loss_type, rgb_activation=act, density_activation=3)
+    _, bf = occupancy(orc, seed=2, frac=0.5, max_cascade=cfg.max_cascade)
+    n_rays, max_samples = 2000, 1 << 17
     r = rng(pkg, 7)
     samples = pkg.nerf.generate_training_samples(ds, cfg, n_rays, r, max_samples, torch.from_numpy(bf).cuda())
     ref_s = orc.nerf_generate_samples(cfg, ims, pix, n_rays, orc_rng(orc, r), max_samples, bf)
@@ -146,28 +156,20 @@ def test_compute_loss(pkg, orc, scene, loss_type, act):
     got = pkg.nerf.compute_loss(ds, cfg, n_rays, r, max_c, samples, out_t, mean)
     ref = orc.nerf_compute_loss(cfg, ims, pix, n_rays, orc_rng(orc, r), max_c, ref_s, out.view(np.uint16), 0.003)
     kept = int(ref_s["counters"][0])
-    ns_got = samples["numsteps"].cpu().numpy()[:kept].view(np.uint32)
-    ns_ref = ref_s["numsteps"][:kept]
-    same = ns_got[:, 0] == ns_ref[:, 0]
-    assert same.mean() >= 0.995
     cc = int(got["compacted_counter"].cpu().numpy().view(np.uint32)[0])
-    assert abs(cc - int(ref["compacted_counter"][0])) <= 0.005 * int(ref["compacted_counter"][0]) + 4
-    loss_got = got["loss"].cpu().numpy()[:kept]
-    np.testing.assert_allclose(loss_got[same], ref["loss"][:kept][same], rtol=1e-4, atol=1e-9)
-    # per-sample gradients of rays whose compacted range matches exactly
-    dl_got = got["dloss_doutput"].cpu().numpy().astype(np.float32)
-    dl_ref = orc.f16_bits_to_f32(ref["dloss_doutput"])
+    assert cc == int(ref["compacted_counter"][0])
+    assert cc > 0
+    ns_got = samples["numsteps"].cpu().numpy()[:kept].view(np.uint32)
+    np.testing.assert_array_equal(ns_got, ref_s["numsteps"][:kept])
+    n_used = min(cc, max_c)
     co_got = got["coords_compacted"].cpu().numpy()
-    scale = np.abs(dl_ref[:, :4]).max()
-    n_checked = 0
-    for i in np.nonzero(same & (ns_got[:, 1] == ns_ref[:, 1]))[0][:400]:
-        n, b = int(ns_ref[i, 0]), int(ns_ref[i, 1])
-        if n == 0:
-            continue
-        np.testing.assert_allclose(dl_got[b:b + n, :4], dl_ref[b:b + n, :4], atol=2e-3 * scale, rtol=2e-3)
-        np.testing.assert_array_equal(co_got[b:b + n], ref["coords_compacted"][b:b + n])
-        n_checked += 1
-    assert n_checked > 50
+    np.testing.assert_array_equal(co_got[:n_used], ref["coords_compacted"][:n_used])
+    np.testing.assert_allclose(got["loss"].cpu().numpy()[:kept], ref["loss"][:kept], rtol=1e-4, atol=1e-9)
+    dl_got = got["dloss_doutput"].cpu().numpy().astype(np.float32)[:n_used, :4]
+    dl_ref = orc.f16_bits_to_f32(ref["dloss_doutput"])[:n_used, :4]
+    tol = 2 * np.spacing(np.abs(dl_ref).astype(np.float16)).astype(np.float32) + 1e-7
+    bad = np.abs(dl_got - dl_ref) > tol
+    assert not bad.any(), (int(bad.sum()), dl_got[bad][:5], dl_ref[bad][:5])
 
 
 @pytest.mark.parametrize("dtype,rescale", [(torch.float32, False), (torch.float16, False), (torch.float16, True)])
@@ -310,3 +312,53 @@ def test_sampler_pipelining_is_exact(pkg):
     assert p1 == p0
     np.testing.assert_array_equal(g1, g0)
     np.testing.assert_array_equal(b1, b0)
+
+
+@pytest.mark.parametrize("world,aabb_scale", [(2, 1.0), (4, 8.0), (3, 1.0)])
+def test_sharded_samples_equal_single_gpu(pkg, orc, scene, world, aabb_scale):
+    """rank r samples global rays [R r/N, R (r+1)/N) with their global ids (rng.advance(i*16),
+    image_idx(i, R), testbed_nerf.cu:1417-1421), so the shards concatenated in rank order ARE the 1-GPU
+    batch bit for bit: ray ids, rays, per-ray step counts and every sample coordinate; after compaction
+    (dL/doutput scaled by 128/R globally) the compacted coordinates are bit-identical too and dL/doutput
+    agrees to one fp16 ulp (128*Rl/R/Rl vs 128/R rounding)."""
+    ds, ims, pix = scene
+    cfg = pkg.nerf.default_config(aabb_scale)
+    _, bf = occupancy(orc, seed=17, frac=0.35, max_cascade=cfg.max_cascade)
+    bf_t = torch.from_numpy(bf).cuda()
+    R, max_samples = 3000, 1 << 19
+    r = rng(pkg, 4321)
+    full = pkg.nerf.generate_training_samples(ds, cfg, R, r, max_samples, bf_t, n_rays_total=R)
+    g = np.random.default_rng(1)
+    out = torch.from_numpy(g.uniform(-3.0, 2.0, (max_samples, 16)).astype(np.float16)).cuda()
+    mean = torch.tensor([0.003], device="cuda")
+    used_full = int(full["counters"].cpu().numpy()[1])
+    full_loss = pkg.nerf.compute_loss(ds, cfg, R, r, 1 << 19, {k: v.clone() for k, v in full.items()}, out, mean, n_rays_total=R)
+    shards, losses = [], []
+    base = 0
+    for rank in range(world):
+        lo, hi = pkg.dp.shard_range(R, rank, world)
+        s = pkg.nerf.generate_training_samples(ds, cfg, hi - lo, r, max_samples, bf_t, ray_offset=lo, n_rays_total=R)
+        used = int(s["counters"].cpu().numpy()[1])
+        # the shard's network outputs are the full batch's rows of its samples
+        out_s = out[base:base + max(used, 1)].contiguous()
+        shards.append({k: v.cpu().numpy() for k, v in s.items()})
+        losses.append(pkg.nerf.compute_loss(ds, cfg, hi - lo, r, 1 << 19, s, out_s if used else out, mean,
+                                            loss_scale=128.0 * (hi - lo) / R, n_rays_total=R))
+        base += used
+    assert base == used_full
+    f = {k: v.cpu().numpy() for k, v in full.items()}
+    cat = lambda k: np.concatenate([s[k][:len(s["ray_indices"])] for s in shards])
+    np.testing.assert_array_equal(cat("ray_indices"), f["ray_indices"])
+    np.testing.assert_array_equal(cat("rays"), f["rays"])
+    np.testing.assert_array_equal(np.concatenate([s["numsteps"][:, 0] for s in shards]), f["numsteps"][:, 0])
+    coords = np.concatenate([s["coords"][:int(s["counters"][1])] for s in shards])
+    np.testing.assert_array_equal(coords, f["coords"][:used_full])
+    cc = [int(l["compacted_counter"].cpu().numpy()[0]) for l in losses]
+    cc_full = int(full_loss["compacted_counter"].cpu().numpy()[0])
+    assert sum(cc) == cc_full
+    co = np.concatenate([l["coords_compacted"].cpu().numpy()[:c] for l, c in zip(losses, cc)])
+    np.testing.assert_array_equal(co, full_loss["coords_compacted"].cpu().numpy()[:cc_full])
+    dl = np.concatenate([l["dloss_doutput"].cpu().numpy()[:c, :4].astype(np.float32) for l, c in zip(losses, cc)])
+    dl_full = full_loss["dloss_doutput"].cpu().numpy()[:cc_full, :4]
+    tol = np.spacing(np.abs(dl_full)).astype(np.float32) + 1e-7
+    assert np.all(np.abs(dl - dl_full.astype(np.float32)) <= tol)

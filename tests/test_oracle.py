@@ -299,3 +299,75 @@ def test_morton_and_srgb(orc):
         assert (inv(i), inv(i >> 1), inv(i >> 2)) == (x, y, z)
     for v in [0.0, 0.01, 0.04045, 0.5, 1.0]:
         assert orc.lib().orc_linear_to_srgb(orc.lib().orc_srgb_to_linear(v)) == pytest.approx(v, abs=1e-3)
+
+
+def test_shared_math_accuracy(orc):
+    """ngp_math.h (the one expf/logf both the engine kernels and the oracle evaluate, so cone stepping
+    and compaction are bit-exact) is within 1 ulp of float64 over the ranges the NeRF path uses and
+    over random positive bit patterns; special values follow IEEE."""
+    g = np.random.default_rng(0)
+
+    def ulps(y, ref):
+        sp = np.abs(np.spacing(ref.astype(np.float32))).astype(np.float64)
+        return np.abs(y.astype(np.float64) - ref) / sp
+
+    x = np.concatenate([g.uniform(-87.0, 88.7, 1 << 20), g.uniform(-15, 15, 1 << 20)]).astype(np.float32)
+    assert ulps(orc.math_eval(0, x), np.exp(x.astype(np.float64))).max() <= 1.0
+    bits = g.integers(0x00800000, 0x7f800000, 1 << 21, dtype=np.uint32)
+    x = np.concatenate([bits.view(np.float32), np.float32(1) + g.uniform(-0.3, 0.4, 1 << 20).astype(np.float32)])
+    assert ulps(orc.math_eval(1, x), np.log(x.astype(np.float64))).max() <= 1.0
+    sub = orc.math_eval(0, np.array([-100.0, -103.0], np.float32))
+    assert np.all(np.abs(sub.astype(np.float64) - np.exp([-100.0, -103.0])) <= 1.5e-45)
+    sp = orc.math_eval(0, np.array([0, -200, 200, np.nan], np.float32))
+    assert sp[0] == 1 and sp[1] == 0 and np.isinf(sp[2]) and np.isnan(sp[3])
+    sp = orc.math_eval(1, np.array([0, -1, np.inf, np.nan, 1, 1e-40], np.float32))
+    assert np.isneginf(sp[0]) and np.isnan(sp[1]) and np.isinf(sp[2]) and np.isnan(sp[3]) and sp[4] == 0
+    assert abs(sp[5] - np.log(1e-40)) < 1e-5 * abs(np.log(1e-40))
+
+
+def test_grid_backward_exact_vs_double(orc):
+    """The contribution-exact backward (per-contribution fp16 rounding, exact sum, one rounding) agrees
+    with the float64 backward within the per-contribution rounding it adds: <= sum of half an fp16 ulp
+    per contribution + half an ulp of the result."""
+    D, L, F, T, n = 3, 4, 2, 12, 4000
+    g = orc.make_grid(D, L, F, T)
+    rng = np.random.default_rng(2)
+    x = rng.random((n, D), dtype=np.float32)
+    dy = rng.uniform(-1, 1, (n, L * F)).astype(np.float16)
+    exact, absum = orc.grid_backward_exact(g, x, dy, with_abs_sum=True)
+    ref = orc.grid_backward(g, x, dy.astype(np.float32))
+    got = exact.view(np.float16).astype(np.float64)
+    tol = absum * 2.0 ** -11 + np.abs(ref) * 2.0 ** -11 + 2.0 ** -24
+    assert np.all(np.abs(got - ref) <= tol)
+    # accumulate: old + sum
+    init = rng.uniform(-1, 1, exact.size).astype(np.float16).view(np.uint16)
+    acc = orc.grid_backward_exact(g, x, dy, grad16=init)
+    want = (init.view(np.float16).astype(np.float64) + ref)
+    assert np.all(np.abs(acc.view(np.float16).astype(np.float64) - want) <= tol + np.abs(want) * 2.0 ** -10)
+
+
+def test_nerf_train_ex_matches_serial(orc):
+    """The parallel full-batch oracle pass equals the serial restatement: outputs, MLP gradients (up
+    to float64 summation order), dL/d(encoding); its grid gradient (exact contract) stays within the
+    per-contribution fp16 rounding of the float64 grid gradient."""
+    m = orc.make_nerf(L=4, F=4, log2T=12)
+    p = orc.nerf_init(m, 7)
+    p16 = orc.f32_to_f16_bits(p)
+    n = 600
+    g = np.random.default_rng(0)
+    c = np.zeros((n, 7), np.float32)
+    c[:, :3] = g.random((n, 3))
+    c[:, 4:] = g.random((n, 3))
+    dL = np.zeros((n, 16), np.float32)
+    dL[:, :4] = g.uniform(-1, 1, (n, 4)).astype(np.float16)
+    r = orc.nerf_train_ex(m, p16, c, dL)
+    np.testing.assert_array_equal(r["out"], orc.nerf_forward(m, p16, c))
+    ref, denc = orc.nerf_backward(m, p16, c, dL, want_denc=True)
+    nm = r["grads"].size
+    np.testing.assert_allclose(r["grads"], ref[:nm], rtol=1e-12, atol=1e-15)
+    np.testing.assert_array_equal(orc.f16_bits_to_f32(r["denc16"]), denc)
+    assert np.all(r["grads_abs"] >= np.abs(r["grads"]) * (1 - 1e-12))
+    assert np.all(r["out_abs"][:, :4] >= np.abs(r["out"][:, :4]) * (1 - 1e-6))
+    gx, absum = orc.grid_backward_exact(m.grid, c[:, :3].copy(), r["denc16"], stride=3, with_abs_sum=True)
+    tol = absum * 2.0 ** -11 + np.abs(ref[nm:]) * 2.0 ** -11 + 2.0 ** -24
+    assert np.all(np.abs(orc.f16_bits_to_f32(gx) - ref[nm:]) <= tol)

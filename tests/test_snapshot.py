@@ -107,3 +107,58 @@ def test_nerf_snapshot_roundtrip(pkg, orc, tmp_path, with_opt):
         assert tr2.step == tr.step
     st2 = run2.train_step(get_loss=True)
     assert st2["step"] == st["step"] + 1 and np.isfinite(st2["loss"])
+
+
+@pytest.mark.gpu
+def test_resume_past_density_update_rerecords_graph(pkg, tmp_path):
+    """Loading a snapshot at step >= 256 and training past the next density-grid update: that update
+    grows the encoding workspace the captured training graph points into, so the trainer must re-record
+    (ngp_model_workspace_epoch). Control: the same resume on a model whose workspaces were reserved for
+    the density pass up front (nothing reallocates) — both runs must match bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ds = _scene(pkg)
+    run, net, tr, ncfg = _training(pkg, ds)
+    for _ in range(300):
+        run.train_step(get_loss=False)
+    path = tmp_path / "resume.ingp"
+    run.save_snapshot(str(path), ncfg, include_optimizer_state=True)
+    results = []
+    for reserve_first in (False, True):
+        run2, net2, tr2, _ = _training(pkg, ds)
+        if reserve_first:
+            net2.reserve(128 ** 3 * (run2.cfg.max_cascade + 1))
+        run2.load_snapshot(str(path))
+        e0 = pkg.lib().ngp_model_workspace_epoch(net2.handle)
+        for _ in range(40):  # density updates every 16 steps after step 256
+            st = run2.train_step(get_loss=True)
+            assert np.isfinite(st["loss"])
+        torch.cuda.synchronize()
+        if not reserve_first:
+            assert pkg.lib().ngp_model_workspace_epoch(net2.handle) > e0  # the density pass did grow a workspace
+        results.append((tr2.params_full_precision.cpu().numpy().copy(), run2.density_grid.cpu().numpy().copy()))
+    np.testing.assert_array_equal(results[0][0], results[1][0])
+    np.testing.assert_array_equal(results[0][1], results[1][1])
+
+
+@pytest.mark.gpu
+def test_learning_rate_change_reaches_captured_steps(pkg):
+    """set_learning_rate after the NeRF training graph was captured changes the replayed optimizer
+    steps (the captured Adam reads its hyperparameters from the device control block)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ds = _scene(pkg)
+    out = []
+    for lr in (None, 0.0):
+        run, net, tr, ncfg = _training(pkg, ds)
+        for _ in range(5):
+            run.train_step(get_loss=False)
+        if lr is not None:
+            tr.set_learning_rate(lr)
+        w0 = tr.params_full_precision.cpu().numpy().copy()
+        for _ in range(3):
+            run.train_step(get_loss=False)
+        torch.cuda.synchronize()
+        out.append(np.abs(tr.params_full_precision.cpu().numpy() - w0).max())
+    assert out[0] > 0
+    assert out[1] == 0  # lr 0: the replayed steps leave the weights unchanged
