@@ -139,6 +139,10 @@ def compute_loss(ds, cfg, n_rays, rng, max_compacted, samples, network_output, m
     """compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012). `samples` is the dict returned by
     generate_training_samples (its numsteps is rewritten to the compacted {n, base})."""
     dev = network_output.device
+    # the kernel reads one output row per sample; samples never exceed the sampler's coords buffer
+    if network_output.shape[0] < samples["coords"].shape[0]:
+        raise ValueError(f"network_output has {network_output.shape[0]} rows, fewer than the {samples['coords'].shape[0]} "
+                         "sample slots of generate_training_samples")
     out = {
         "coords_compacted": torch.zeros((max_compacted, 7), dtype=torch.float32, device=dev),
         "dloss_doutput": torch.zeros((max_compacted, 16), dtype=torch.float16, device=dev),

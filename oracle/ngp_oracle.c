@@ -374,7 +374,10 @@ static void layer_dims(const orc_mlp* m, uint32_t l, uint32_t* in, uint32_t* out
 
 /* One sample's forward; acts receives every layer's fp16-rounded output (post-activation for hidden
  * layers), acts must hold (n_hidden)*width + out_pad floats. */
-static void mlp_forward_one_abs(const orc_mlp* m, const uint16_t* w, const float* x, float* acts, float* out_abs) {
+/* margin (optional): min over the hidden neurons of |pre-activation| / sum_k |W_ok a_k| — how close a
+ * ReLU is to switching under accumulation-order noise (tests use it to explain outliers). */
+static void mlp_forward_one_abs(const orc_mlp* m, const uint16_t* w, const float* x, float* acts, float* out_abs,
+                                float* margin) {
 	uint32_t nl = m->n_hidden + 1;
 	float buf_in[256];
 	memcpy(buf_in, x, m->in_pad * sizeof(float));
@@ -385,9 +388,12 @@ static void mlp_forward_one_abs(const orc_mlp* m, const uint16_t* w, const float
 			double s = 0.0, sa = 0.0;
 			const uint16_t* wr = w + off + (size_t)o * in;
 			for (uint32_t k = 0; k < in; ++k) s += (double)hf(wr[k]) * (double)buf_in[k];
-			if (out_abs && l == nl - 1) {
+			if ((out_abs && l == nl - 1) || (margin && l < nl - 1))
 				for (uint32_t k = 0; k < in; ++k) sa += fabs((double)hf(wr[k]) * (double)buf_in[k]);
-				out_abs[o] = (float)sa;
+			if (out_abs && l == nl - 1) out_abs[o] = (float)sa;
+			if (margin && l < nl - 1 && sa > 0.0) {
+				float r = (float)(fabs(s) / sa);
+				if (r < *margin) *margin = r;
 			}
 			float v = rh((float)s);
 			if (l < nl - 1 && v < 0.f) v = 0.f;
@@ -399,7 +405,7 @@ static void mlp_forward_one_abs(const orc_mlp* m, const uint16_t* w, const float
 }
 
 static void mlp_forward_one(const orc_mlp* m, const uint16_t* w, const float* x, float* acts) {
-	mlp_forward_one_abs(m, w, x, acts, NULL);
+	mlp_forward_one_abs(m, w, x, acts, NULL, NULL);
 }
 
 EXPORT void orc_set_num_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
@@ -573,11 +579,12 @@ EXPORT void orc_nerf_backward(const orc_nerf* m, const uint16_t* params, size_t 
  *   grads    double [nd+nr]  MLP weight gradients, abs (optional) sum |g a| per weight;
  *   denc16   fp16 bits [n x density.in_pad]  dL/d(encoding), the input of the grid backward
  *            (orc_grid_backward_exact finishes the gradient with the engine's exact-sum contract),
- *            denc_abs (optional) the sum |W g| of each dL/d(encoding) contraction.
+ *            denc_abs (optional) the sum |W g| of each dL/d(encoding) contraction;
+ *   margin   (optional) float [n]: min over the sample's hidden neurons of |pre-activation| / sum |W a|.
  * Per-thread accumulators are added in thread order after the loop (double: order effects ~1e-16). */
 EXPORT void orc_nerf_train_ex(const orc_nerf* m, const uint16_t* params, size_t n, const float* in, const float* dL_dout,
                               float* out, float* out_abs, double* grads, double* grads_abs, uint16_t* denc16,
-                              float* denc_abs) {
+                              float* denc_abs, float* margin) {
 	size_t nd = orc_mlp_n_params(&m->density), nr = orc_mlp_n_params(&m->rgb);
 	const uint16_t* wd = params;
 	const uint16_t* wr = params + nd;
@@ -596,13 +603,15 @@ EXPORT void orc_nerf_train_ex(const orc_nerf* m, const uint16_t* params, size_t 
 			const float* x = in + i * m->in_stride;
 			orc_grid_forward(g, 1, x, m->in_stride, table, 1.0f, NULL, enc);
 			for (uint32_t k = 0; k < m->density.in_pad; ++k) enc[k] = k < LF ? rh(enc[k]) : 0.f;
-			mlp_forward_one_abs(&m->density, wd, enc, dacts, oa_d);
+			float mg = 1.0f;
+			mlp_forward_one_abs(&m->density, wd, enc, dacts, oa_d, &mg);
 			const float* dout = dacts + m->density.n_hidden * m->density.width;
 			for (uint32_t k = 0; k < 16; ++k) rin[k] = dout[k];
 			float sh[16];
 			orc_sh4(x[m->dir_offset], x[m->dir_offset + 1], x[m->dir_offset + 2], sh);
 			for (uint32_t k = 0; k < 16; ++k) rin[16 + k] = rh(sh[k]);
-			mlp_forward_one_abs(&m->rgb, wr, rin, racts, oa_r);
+			mlp_forward_one_abs(&m->rgb, wr, rin, racts, oa_r, &mg);
+			if (margin) margin[i] = mg;
 			const float* rout = racts + m->rgb.n_hidden * m->rgb.width;
 			for (uint32_t k = 0; k < 16; ++k) {
 				out[i * 16 + k] = k == 3 ? dout[0] : rout[k];
@@ -634,7 +643,7 @@ EXPORT void orc_nerf_train_ex(const orc_nerf* m, const uint16_t* params, size_t 
  * pos[i * pos_stride + d], dL_dout float [n x mlp.out_pad]. Outputs as orc_nerf_train_ex. */
 EXPORT void orc_net_train_ex(const orc_grid* g, const orc_mlp* mlp, const uint16_t* params, size_t n, const float* pos,
                              uint32_t pos_stride, const float* dL_dout, float* out, float* out_abs, double* grads,
-                             double* grads_abs, uint16_t* denc16, float* denc_abs) {
+                             double* grads_abs, uint16_t* denc16, float* denc_abs, float* margin) {
 	const size_t nm = orc_mlp_n_params(mlp);
 	const uint16_t* table = params + nm;
 	const uint32_t LF = g->n_levels * g->n_features, OP = mlp->out_pad, IP = mlp->in_pad;
@@ -651,7 +660,9 @@ EXPORT void orc_net_train_ex(const orc_grid* g, const orc_mlp* mlp, const uint16
 		for (size_t i = 0; i < n; ++i) {
 			orc_grid_forward(g, 1, pos + i * pos_stride, pos_stride, table, 1.0f, NULL, enc);
 			for (uint32_t k = 0; k < IP; ++k) enc[k] = k < LF ? rh(enc[k]) : 0.f;
-			mlp_forward_one_abs(mlp, params, enc, acts, oa);
+			float mg = 1.0f;
+			mlp_forward_one_abs(mlp, params, enc, acts, oa, &mg);
+			if (margin) margin[i] = mg;
 			const float* o = acts + mlp->n_hidden * mlp->width;
 			for (uint32_t k = 0; k < OP; ++k) {
 				out[i * OP + k] = o[k];

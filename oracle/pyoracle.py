@@ -89,8 +89,8 @@ def _declare(L):
     d("orc_nerf_forward", None, P, P, sz, P, P)
     d("orc_nerf_density", None, P, P, sz, P, u32, P)
     d("orc_nerf_backward", None, P, P, sz, P, P, P, P)
-    d("orc_nerf_train_ex", None, P, P, sz, P, P, P, P, P, P, P, P)
-    d("orc_net_train_ex", None, P, P, P, sz, P, u32, P, P, P, P, P, P, P)
+    d("orc_nerf_train_ex", None, P, P, sz, P, P, P, P, P, P, P, P, P)
+    d("orc_net_train_ex", None, P, P, P, sz, P, u32, P, P, P, P, P, P, P, P)
     d("orc_nerf_init", None, P, u64, P)
     d("orc_lr_at_step", f32, P, u32)
     d("orc_adam_step", None, P, u32, sz, sz, f32, P, P, P, P, P, P, P, P)
@@ -314,10 +314,11 @@ def nerf_train_ex(m, params16, coords, dL_dout):
     nm = mlp_n_params(m.density) + mlp_n_params(m.rgb)
     r = {"out": np.zeros((n, 16), np.float32), "out_abs": np.zeros((n, 16), np.float32),
          "grads": np.zeros(nm, np.float64), "grads_abs": np.zeros(nm, np.float64),
-         "denc16": np.zeros((n, m.density.in_pad), np.uint16), "denc_abs": np.zeros((n, m.density.in_pad), np.float32)}
+         "denc16": np.zeros((n, m.density.in_pad), np.uint16), "denc_abs": np.zeros((n, m.density.in_pad), np.float32),
+         "margin": np.zeros(n, np.float32)}
     lib().orc_nerf_train_ex(C.byref(m), ptr(np.ascontiguousarray(params16)), n, ptr(coords),
                             ptr(np.ascontiguousarray(dL_dout, np.float32)), ptr(r["out"]), ptr(r["out_abs"]), ptr(r["grads"]),
-                            ptr(r["grads_abs"]), ptr(r["denc16"]), ptr(r["denc_abs"]))
+                            ptr(r["grads_abs"]), ptr(r["denc16"]), ptr(r["denc_abs"]), ptr(r["margin"]))
     return r
 
 
@@ -328,10 +329,12 @@ def net_train_ex(grid, mlp, params16, pos, dL_dout, stride=None):
     nm = mlp_n_params(mlp)
     r = {"out": np.zeros((n, mlp.out_pad), np.float32), "out_abs": np.zeros((n, mlp.out_pad), np.float32),
          "grads": np.zeros(nm, np.float64), "grads_abs": np.zeros(nm, np.float64),
-         "denc16": np.zeros((n, mlp.in_pad), np.uint16), "denc_abs": np.zeros((n, mlp.in_pad), np.float32)}
+         "denc16": np.zeros((n, mlp.in_pad), np.uint16), "denc_abs": np.zeros((n, mlp.in_pad), np.float32),
+         "margin": np.zeros(n, np.float32)}
     lib().orc_net_train_ex(C.byref(grid), C.byref(mlp), ptr(np.ascontiguousarray(params16)), n, ptr(pos),
                            stride or pos.shape[1], ptr(np.ascontiguousarray(dL_dout, np.float32)), ptr(r["out"]),
-                           ptr(r["out_abs"]), ptr(r["grads"]), ptr(r["grads_abs"]), ptr(r["denc16"]), ptr(r["denc_abs"]))
+                           ptr(r["out_abs"]), ptr(r["grads"]), ptr(r["grads_abs"]), ptr(r["denc16"]), ptr(r["denc_abs"]),
+                           ptr(r["margin"]))
     return r
 
 

@@ -318,40 +318,44 @@ def test_sampler_pipelining_is_exact(pkg):
 def test_sharded_samples_equal_single_gpu(pkg, orc, scene, world, aabb_scale):
     """rank r samples global rays [R r/N, R (r+1)/N) with their global ids (rng.advance(i*16),
     image_idx(i, R), testbed_nerf.cu:1417-1421), so the shards concatenated in rank order ARE the 1-GPU
-    batch bit for bit: ray ids, rays, per-ray step counts and every sample coordinate; after compaction
-    (dL/doutput scaled by 128/R globally) the compacted coordinates are bit-identical too and dL/doutput
-    agrees to one fp16 ulp (128*Rl/R/Rl vs 128/R rounding)."""
+    batch bit for bit: kept ray ids, rays, per-ray step counts and every sample coordinate; after
+    compaction (dL/doutput scaled by 128/R globally) the compacted coordinates are bit-identical too and
+    dL/doutput agrees to one fp16 ulp (128*Rl/R/Rl vs 128/R rounding)."""
     ds, ims, pix = scene
     cfg = pkg.nerf.default_config(aabb_scale)
     _, bf = occupancy(orc, seed=17, frac=0.35, max_cascade=cfg.max_cascade)
     bf_t = torch.from_numpy(bf).cuda()
-    R, max_samples = 3000, 1 << 19
+    R, max_samples = 3000, 1 << 22
     r = rng(pkg, 4321)
     full = pkg.nerf.generate_training_samples(ds, cfg, R, r, max_samples, bf_t, n_rays_total=R)
+    f = {k: v.cpu().numpy() for k, v in full.items()}
+    kept_full, used_full = int(f["counters"][0]), int(f["counters"][1])
+    assert 0 < used_full <= max_samples  # no ray dropped: the shards see the same budget
     g = np.random.default_rng(1)
     out = torch.from_numpy(g.uniform(-3.0, 2.0, (max_samples, 16)).astype(np.float16)).cuda()
     mean = torch.tensor([0.003], device="cuda")
-    used_full = int(full["counters"].cpu().numpy()[1])
-    full_loss = pkg.nerf.compute_loss(ds, cfg, R, r, 1 << 19, {k: v.clone() for k, v in full.items()}, out, mean, n_rays_total=R)
+    full_loss = pkg.nerf.compute_loss(ds, cfg, R, r, max_samples, {k: v.clone() for k, v in full.items()}, out, mean,
+                                      n_rays_total=R)
     shards, losses = [], []
     base = 0
     for rank in range(world):
         lo, hi = pkg.dp.shard_range(R, rank, world)
         s = pkg.nerf.generate_training_samples(ds, cfg, hi - lo, r, max_samples, bf_t, ray_offset=lo, n_rays_total=R)
-        used = int(s["counters"].cpu().numpy()[1])
+        sn = {k: v.cpu().numpy() for k, v in s.items()}
+        used = int(sn["counters"][1])
         # the shard's network outputs are the full batch's rows of its samples
-        out_s = out[base:base + max(used, 1)].contiguous()
-        shards.append({k: v.cpu().numpy() for k, v in s.items()})
-        losses.append(pkg.nerf.compute_loss(ds, cfg, hi - lo, r, 1 << 19, s, out_s if used else out, mean,
+        out_s = out[base:base + max_samples].contiguous() if base + max_samples <= out.shape[0] else \
+            torch.cat([out[base:], out[:base + max_samples - out.shape[0]]]).contiguous()
+        shards.append(sn)
+        losses.append(pkg.nerf.compute_loss(ds, cfg, hi - lo, r, max_samples, s, out_s, mean,
                                             loss_scale=128.0 * (hi - lo) / R, n_rays_total=R))
         base += used
     assert base == used_full
-    f = {k: v.cpu().numpy() for k, v in full.items()}
-    cat = lambda k: np.concatenate([s[k][:len(s["ray_indices"])] for s in shards])
-    np.testing.assert_array_equal(cat("ray_indices"), f["ray_indices"])
-    np.testing.assert_array_equal(cat("rays"), f["rays"])
-    np.testing.assert_array_equal(np.concatenate([s["numsteps"][:, 0] for s in shards]), f["numsteps"][:, 0])
-    coords = np.concatenate([s["coords"][:int(s["counters"][1])] for s in shards])
+    cat = lambda k: np.concatenate([sh[k][:int(sh["counters"][0])] for sh in shards])
+    np.testing.assert_array_equal(cat("ray_indices"), f["ray_indices"][:kept_full])
+    np.testing.assert_array_equal(cat("rays"), f["rays"][:kept_full])
+    np.testing.assert_array_equal(cat("numsteps")[:, 0], f["numsteps"][:kept_full, 0])
+    coords = np.concatenate([sh["coords"][:int(sh["counters"][1])] for sh in shards])
     np.testing.assert_array_equal(coords, f["coords"][:used_full])
     cc = [int(l["compacted_counter"].cpu().numpy()[0]) for l in losses]
     cc_full = int(full_loss["compacted_counter"].cpu().numpy()[0])

@@ -16,8 +16,10 @@ Bars (per element, written out below):
 * MLP weight gradients w (fp16 in the gradient buffer): |g_gpu - g_ref| <= 2^-9 * cond(w) +
   ulp16(g_ref), cond(w) = sum_i |g_i a_i| over the batch (grads_abs).
 A ReLU whose pre-activation lies within the accumulation noise of zero can switch between the two
-implementations; such elements are counted and must stay below 1e-4 of the elements checked (their
-error is then bounded by the conditioning of the next contraction, 16x the bar above).
+implementations. Elements beyond the bar are accepted only in samples whose oracle forward shows a
+hidden pre-activation within 2^-12 of zero relative to its conditioning (orc_*_train_ex margin), only
+within their element's whole conditioning, and at most 1e-4 of the elements; MLP weight gradients
+(sums over the batch) get no such allowance.
 """
 import numpy as np
 import pytest
@@ -26,7 +28,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 C = 2.0 ** -9
-FLIP_FRACTION = 1e-4
+MARGIN = 2.0 ** -12
 
 
 @pytest.fixture(scope="module")
@@ -51,17 +53,30 @@ def ulp16(x):
     return np.spacing(np.abs(x).astype(np.float16)).astype(np.float64)
 
 
-def check_close(name, got, ref, cond, extra=0.0):
+def check_close(name, got, ref, cond, margin=None):
+    """Per-element bar |got - ref| <= C * cond + ulp16(ref). With `margin` (per sample, rows of got):
+    elements beyond it must lie in samples whose oracle forward has a hidden pre-activation within
+    MARGIN of zero relative to its conditioning (a ReLU that accumulation noise can switch), and stay
+    within that element's whole conditioning (cond + ulp16)."""
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
+    cond = np.asarray(cond, np.float64)
     err = np.abs(got - ref)
-    tol = C * np.asarray(cond, np.float64) + ulp16(ref) + extra
+    tol = C * cond + ulp16(ref)
     bad = err > tol
-    loose = err > 16 * tol
     ratio = float((err / tol).max()) if err.size else 0.0
-    msg = f"{name}: {int(bad.sum())} of {err.size} beyond the bar (max err/bar {ratio:.3g}), {int(loose.sum())} beyond 16x"
-    assert bad.mean() <= FLIP_FRACTION and not loose.any(), msg
-    return msg
+    n_bad = int(bad.sum())
+    msg = f"{name}: {n_bad} of {err.size} beyond the bar (max err/bar {ratio:.3g})"
+    if margin is None:
+        assert n_bad == 0, msg
+        return msg
+    rows = np.nonzero(bad.reshape(bad.shape[0], -1).any(axis=1))[0]
+    unexplained = rows[margin[rows] >= MARGIN]
+    assert unexplained.size == 0, f"{msg}; samples {unexplained[:5].tolist()} have margin {margin[unexplained[:5]].tolist()}"
+    assert np.all(err[bad] <= cond[bad] + ulp16(ref[bad])), msg + " (beyond the conditioning)"
+    assert n_bad <= 1e-4 * err.size, msg
+    return msg + (f", all in {rows.size} samples with a ReLU within {MARGIN:g} of switching (margins "
+                  f"{np.sort(margin[rows])[-3:].tolist()}; {int((margin < MARGIN).sum())} samples that close)")
 
 
 @pytest.mark.parametrize("cfg_name,log2T,L,F", [("C2", 19, 4, 4), ("C2p", 19, 16, 2)])
@@ -90,9 +105,9 @@ def test_nerf_network_full_batch(pkg, orc, cfg_name, log2T, L, F, record_propert
 
     m = orc.make_nerf(L=L, F=F, log2T=log2T)
     r = orc.nerf_train_ex(m, p16, c, dL.astype(np.float32))
-    msgs = [check_close("output", got_out, r["out"], r["out_abs"]),
+    msgs = [check_close("output", got_out, r["out"], r["out_abs"], r["margin"]),
             check_close("dL/dencoding", got_denc[:, :L * F].astype(np.float64),
-                        orc.f16_bits_to_f32(r["denc16"])[:, :L * F], r["denc_abs"][:, :L * F]),
+                        orc.f16_bits_to_f32(r["denc16"])[:, :L * F], r["denc_abs"][:, :L * F], r["margin"]),
             check_close("MLP dW", got_g[:nm].astype(np.float64), r["grads"], r["grads_abs"])]
     # grid backward at full size, bit for bit on the engine's own dL/d(encoding)
     ref_grid = orc.grid_backward_exact(m.grid, c, got_denc.view(np.uint16), stride=7)
@@ -141,8 +156,9 @@ def test_sdf_training_step_c5_full_batch(pkg, orc, log2T):
     grid = orc.make_grid(3, 16, 2, log2T)
     mlp = orc.make_mlp(32, 64, 2, 16)
     r = orc.net_train_ex(grid, mlp, p16, x, orc.f16_bits_to_f32(dl16))
-    msgs = [check_close("output", orc.f16_bits_to_f32(out16)[:, :1], r["out"][:, :1], r["out_abs"][:, :1]),
-            check_close("dL/dencoding", got_denc.astype(np.float64), orc.f16_bits_to_f32(r["denc16"]), r["denc_abs"]),
+    msgs = [check_close("output", orc.f16_bits_to_f32(out16)[:, :1], r["out"][:, :1], r["out_abs"][:, :1], r["margin"]),
+            check_close("dL/dencoding", got_denc.astype(np.float64), orc.f16_bits_to_f32(r["denc16"]), r["denc_abs"],
+                        r["margin"]),
             check_close("MLP dW", got_g[:nm].astype(np.float64), r["grads"], r["grads_abs"])]
     ref_grid = orc.grid_backward_exact(grid, x, got_denc.view(np.uint16))
     np.testing.assert_array_equal(got_g[nm:].view(np.uint16), ref_grid)

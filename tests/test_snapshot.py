@@ -154,7 +154,7 @@ def test_learning_rate_change_reaches_captured_steps(pkg):
         for _ in range(5):
             run.train_step(get_loss=False)
         if lr is not None:
-            tr.set_learning_rate(lr)
+            tr.learning_rate = lr
         w0 = tr.params_full_precision.cpu().numpy().copy()
         for _ in range(3):
             run.train_step(get_loss=False)
