@@ -6,11 +6,23 @@ hash-grid encoding forward -> fused density+rgb MLP forward/backward (MFMA) -> h
 Adam/EMA optimizer step. Config C2 = the fork's configs/nerf/base.json (L=4, F=4, T=2^19,
 64-wide MLPs, fp16) — BASELINE.json configs[1]. Inputs are resident in HBM before timing starts.
 
-Multi-GPU: one process per GPU (torch.distributed.run), weak scaling (each rank trains its own
-2^18-sample shard per step), gradients summed with one RCCL all-reduce per step.
+Multi-GPU: one process per GPU (torch.distributed.run); --scaling weak (default: each rank trains its
+own 2^18-sample batch per step) or strong (one global 2^18 batch sharded over the ranks); gradients
+summed with one RCCL all-reduce per step, inside the step's HIP graph.
+
+At N=1 the JSON line also carries (rank 0, after the timed region):
+  roofline      the dominant region's algorithmic bytes (or FLOPs) per launch / its HIP-event time;
+                regions: grid forward, grid backward (bucket scan + plan + scatter + accumulate + split
+                reduce), fused MLP training kernel, optimizer (46 B per updated parameter, 16 B per
+                lazily skipped one); `traffic` = bytes that left L2 for the fabric (Infinity Cache + HBM)
+                per launch, from the committed rocprofv3 summary of sized read requests + WRITE_SIZE
+  cpu_baseline  the C oracle's encoding + MLP fwd/bwd on every host core this process may use
+  e2e           the full Testbed NeRF step for 30 s on the procedural Lego stand-in: samples/s and PSNR
+  c2p           the same training pass at C2' (L=16 F=2 T=2^19), BASELINE's literal "L=16"
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -64,16 +76,24 @@ def synthetic_batch(n, seed, device):
 REGION_KERNELS = {
     "grid_forward": ["k_grid_forward"],
     "grid_backward": ["k_grid_backward"],
-    "grid_backward_sorted": ["k_sc_scatter", "k_sc_accumulate", "k_sc_split_reduce"],
+    "grid_backward_total": ["k_sc_scan", "k_sc_plan", "k_sc_scatter", "k_sc_accumulate", "k_sc_split_reduce"],
     "mlp_train": ["k_nerf_mlp<1,", "k_mlp<1,"],
     "mlp_infer": ["k_nerf_mlp<0,", "k_mlp<0,"],
+    "optimizer": ["k_adam_ema"],
 }
+# engine profiler phases that make up a roofline region (each runs once per training step)
+REGION_PHASES = {"grid_backward_total": ["grid_bwd_prepare", "grid_backward_sorted"]}
+# optimizer bytes per parameter (optimizer.hip k_adam_ema4): updated = read g16 w32 m1 m2 steps ema32
+# (22 B) + write w32 m1 m2 steps w16 ema32 ema16 (24 B) = 46 B; lazily skipped grid entry (zero
+# gradient) = read g16 w32 ema32 (10 B) + write ema32 ema16 (6 B) = 16 B
+OPT_B_UPDATED, OPT_B_SKIPPED = 46, 16
 
 
 def pmc_traffic(variant, region):
-    """HBM bytes per launch of `region` from the newest committed rocprofv3 PMC summary
-    (profiles/<round>_pmc_<variant>.json, written by tools/pmc_summary.py from separate FETCH_SIZE and
-    WRITE_SIZE passes of this bench, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM). None if absent."""
+    """Bytes per launch of `region` that left L2 for the fabric (Infinity Cache + HBM), from the newest
+    committed rocprofv3 summary profiles/<round>_pmc_<variant>.json (tools/pmc_summary.py: reads =
+    32/64/128 x TCC_EA0_RDREQ_{32B,64B,128B}, writes = WRITE_SIZE; calibrated against known-byte kernels
+    in profiles/r02_hbm_calib.json — FETCH_SIZE alone counts every 128-B request as 64 B). None if absent."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{variant.lower()}.json")))
     if not files or region not in REGION_KERNELS:
@@ -82,15 +102,28 @@ def pmc_traffic(variant, region):
     tot, hit = 0.0, False
     for name, v in summ.items():
         compact = name.replace(" ", "")
-        if any(k.replace(" ", "") in compact for k in REGION_KERNELS[region]):
-            tot += v["hbm_bytes"]
+        if any(k.replace(" ", "") in compact for k in REGION_KERNELS[region]) and "fabric_bytes" in v:
+            tot += v["fabric_bytes"]
             hit = True
     return (tot if hit else None), os.path.relpath(files[-1], ROOT)
 
 
+def host_cores():
+    """CPU threads this process may use: the affinity mask, capped by a cgroup CPU quota if one is set."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
 def cpu_baseline(variant, budget_s=12.0):
     """The oracle (a naive C port of the same encoding + MLP fwd/bwd, fp32/fp64, no SIMD intrinsics) timed
-    on the host: one thread for a third of the budget, then one thread per host core for the rest
+    on the host: one thread for a third of the budget, then one thread per usable host core for the rest
     (ctypes releases the GIL, each thread owns its chunk and gradient buffer: the OpenMP-over-samples
     baseline of SURVEY §8d). `value` is the all-cores rate."""
     import concurrent.futures as cf
@@ -118,7 +151,7 @@ def cpu_baseline(variant, budget_s=12.0):
         return done, time.perf_counter() - t0
 
     n1, t1 = run(budget_s / 3)
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
+    threads, affinity, quota = host_cores()
     with cf.ThreadPoolExecutor(threads) as ex:
         t0 = time.perf_counter()
         res = list(ex.map(run, [2 * budget_s / 3] * threads))
@@ -126,100 +159,36 @@ def cpu_baseline(variant, budget_s=12.0):
     nt = sum(r[0] for r in res)
     return {"value": nt / dt, "unit": "samples/s", "cores": threads, "kind": "port",
             "single_thread_value": n1 / t1,
+            "hardware_concurrency": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
             "sample": f"NerfNetwork fwd+bwd ({variant}) of an {chunk}-sample synthetic batch in the C oracle: "
-                      f"{n1} samples on 1 thread in {t1:.1f} s, then {nt} samples on {threads} threads in {dt:.1f} s"}
+                      f"{n1} samples on 1 thread in {t1:.1f} s, then {nt} samples on {threads} threads "
+                      f"(every usable core) in {dt:.1f} s"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--variant", default="C2", choices=["C2", "C2p", "C5", "IMG"])
-    ap.add_argument("--batch", type=int, default=B)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--graph", type=int, default=1, help="1: time the K steps as one captured HIP graph (N=1)")
-    ap.add_argument("--overlap", type=int, default=None, help="engine side-stream overlap bitmask (engine.hip)")
-    ap.add_argument("--opt", action="append", default=[], help="model option key=value (ngp_model_set_option)")
-    args = ap.parse_args()
+def read_profiler(lib):
+    import ctypes
+    need = lib.ngp_profiler_read(None, 0)
+    cbuf = ctypes.create_string_buffer(need)
+    lib.ngp_profiler_read(cbuf, need)
+    return json.loads(cbuf.value.decode())
 
-    from __graft_entry__ import load_package
-    pkg = load_package()
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    rank, world, local_rank = pkg.dp.init_from_env()
 
-    n = args.batch
-    loss_scale = 128.0
-    if args.variant in ("C2", "C2p"):
-        cfg = pkg.nerf_config(args.variant)
-        net = pkg.create_nerf_network(cfg)
-        if args.overlap is not None:
-            net.set_option("overlap", args.overlap)
-        for kv in args.opt:
-            k, v = kv.split("=")
-            net.set_option(k, float(v))
-        trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
-        net.reserve(n)
-        x, dL = synthetic_batch(n, 1337 + rank, "cuda")
-        grads = trainer.gradients
-        comm = None
-        if world > 1:
-            # the engine's own RCCL communicator: the gradient all-reduce is enqueued by the engine on
-            # its stream, between the backward and the optimizer, and captured into the step's graph
-            comm = pkg.dp.EngineComm(rank, world)
-            trainer.set_allreduce(comm)
-
-        def step():
-            net.forward_backward(x, dL)
-            if comm is not None:
-                comm.allreduce(grads)  # RCCL over xGMI; 1/N folded into the loss scale
-            trainer.optimizer_step(loss_scale * world)
-        graphable = True
-    elif args.variant == "C5":
-        cfg = json.loads(json.dumps(pkg.SDF_BASE))
-        cfg["encoding"].update({"log2_hashmap_size": 22, "per_level_scale": 2.0})
-        net = pkg.NetworkWithInputEncoding(3, 1, cfg["encoding"], cfg["network"])
-        trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
-        verts = pkg.synthetic.icosphere(4, radius=0.35, bumps=0.3, seed=rank)
-        tris, amin, amax, brad = pkg.sdf.load_mesh(verts)
-        mesh = pkg.sdf.SdfMesh(tris)
-        sdf = pkg.sdf.SdfTraining(net, trainer, mesh, amin, amax, brad, seed=1337 + rank, batch_size=n)
-        sdf.generate_training_samples(n, sdf.positions, sdf.distances)  # resident batch (online regeneration untimed)
-        torch.cuda.synchronize()
-        if world > 1:
-            raise SystemExit("C5 bench is single-GPU")
-
-        def step():
-            sdf.train_step(get_loss=False, regenerate=False)
-        graphable = False
-    else:  # IMG
-        cfg = json.loads(json.dumps(pkg.IMAGE_BASE))
-        cfg["encoding"]["per_level_scale"] = 2.0
-        net = pkg.NetworkWithInputEncoding(2, 3, cfg["encoding"], cfg["network"])
-        trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
-        img = pkg.image.Image(pkg.synthetic.synthetic_image(1024, 1024, seed=rank))
-        it = pkg.image.ImageTraining(net, trainer, img, seed=1337 + rank, batch_size=n)
-        if world > 1:
-            raise SystemExit("IMG bench is single-GPU")
-
-        def step():
-            it.train_step(get_loss=False)
-        graphable = False
-
-    lib = pkg.lib()
+def timed_steps(lib, step, steps, warmup, world, capture=None):
+    """W untimed warmup steps, then K steps between barrier + synchronize on both sides (one captured
+    HIP graph of K steps when `capture` gives one), then the same K steps replayed eagerly with the
+    engine's per-kernel HIP events (queued behind graph launches so the events bracket kernels only).
+    Returns (seconds for the K timed steps, launch mode, per-phase profiler dict)."""
     stream = torch.cuda.Stream()
-    use_graph = bool(args.graph) and graphable
     graph_note = None
     with torch.cuda.stream(stream):
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             step()
         torch.cuda.synchronize()
         graph = None
-        if use_graph:
-            # the K timed steps as one HIP graph launch (forward_backward + optimizer per step)
+        if capture is not None:
             try:
-                graph = trainer.capture_training_step(x, dL, loss_scale, n_steps=args.steps)
+                graph = capture(steps)
                 graph.launch()  # untimed replay: graph upload / first-launch costs
                 torch.cuda.synchronize()
             except Exception as e:  # same HIP kernels, launched one by one
@@ -235,55 +204,174 @@ def main():
         if graph is not None:
             graph.launch()
         else:
-            for _ in range(args.steps):
+            for _ in range(steps):
                 step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
         if graph is not None:
-            # per-kernel HIP-event timing: the same K steps replayed eagerly, queued behind one more
-            # graph launch so the host is ahead of the GPU and the events bracket kernels only
             lib.ngp_profiler_reset()
             for _ in range(3):  # ~3x the host's enqueue time of K eager steps
                 graph.launch()
             lib.ngp_profiler_enable(1)
-            for _ in range(args.steps):
+            for _ in range(steps):
                 step()
             torch.cuda.synchronize()
         lib.ngp_profiler_enable(0)
-    dt = t1 - t0
+    return t1 - t0, ("hip_graph" if graph is not None else (graph_note or "eager")), read_profiler(lib)
+
+
+def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None):
+    """NerfNetwork + Trainer for C2/C2' with a resident synthetic batch; returns (step, capture, net, trainer)."""
+    cfg = pkg.nerf_config(variant)
+    net = pkg.create_nerf_network(cfg)
+    if overlap is not None:
+        net.set_option("overlap", overlap)
+    for kv in opts:
+        k, v = kv.split("=")
+        net.set_option(k, float(v))
+    trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+    net.reserve(n)
+    x, dL = synthetic_batch(n, 1337 + rank, "cuda")
+    grads = trainer.gradients
+    comm = None
+    if world > 1:
+        # the engine's own RCCL communicator: the gradient all-reduce is enqueued by the engine on its
+        # stream, between the backward and the optimizer, and captured into the step's graph
+        comm = pkg.dp.EngineComm(rank, world)
+        trainer.set_allreduce(comm)
+    loss_scale = 128.0
+
+    def step():
+        net.forward_backward(x, dL)
+        if comm is not None:
+            comm.allreduce(grads)  # RCCL over xGMI; 1/N folded into the loss scale
+        trainer.optimizer_step(loss_scale * world)
+
+    def capture(k):
+        return trainer.capture_training_step(x, dL, loss_scale, n_steps=k)
+    return step, capture, net, trainer, comm
+
+
+def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped):
+    """Per-region achieved rate and fraction of peak; returns (summary dict, dominant region)."""
+    a = ALGO[variant]
+    per = {k: v["ms"] / max(v["calls"], 1) for k, v in kernels.items()}
+    for region, phases in REGION_PHASES.items():
+        if all(p in per for p in phases):
+            per[region] = sum(per[p] for p in phases)
+    roof = {
+        "grid_forward": ("hbm", a["enc_fwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
+        "grid_backward": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
+        "grid_backward_total": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
+        "mlp_train": ("mfma", a["mlp_train_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
+        "mlp_infer": ("mfma", a["mlp_fwd_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
+    }
+    if n_opt_updated is not None:
+        roof["optimizer"] = ("hbm", (OPT_B_UPDATED * n_opt_updated + OPT_B_SKIPPED * n_opt_skipped) / 1e9, HBM_PEAK_GBS, "GB/s")
+    summary = {}
+    for k, ms in per.items():
+        e = {"avg_ms": round(ms, 4)}
+        if k in roof:
+            _, w, pk, u = roof[k]
+            e.update({"achieved": round(w / (ms / 1e3), 1), "unit": u, "frac": round(w / (ms / 1e3) / pk, 4)})
+        summary[k] = e
+    cands = [k for k in roof if k in per and not (k == "grid_backward" and "grid_backward_total" in per)]
+    dom = max(cands, key=lambda k: per[k])
+    bound, work, peak, unit = roof[dom]
+    achieved = work / (per[dom] / 1e3)
+    traffic, src = pmc_traffic(variant, dom)
+    rl = {"kernel": dom, "bound": bound, "achieved": round(achieved, 1), "peak": peak, "unit": unit,
+          "frac": round(achieved / peak, 4), "traffic": None if traffic is None else round(traffic / 1e6, 2),
+          "traffic_unit": "MB/launch leaving L2 for the fabric (Infinity Cache + HBM; rocprofv3 sized read requests "
+                          "+ WRITE_SIZE)",
+          "traffic_source": src,
+          "algorithmic": round(work * (1e3 if unit == "GB/s" else 1e6), 2),
+          "algorithmic_unit": "MB/launch" if unit == "GB/s" else "MFLOP/launch"}
+    return summary, rl
+
+
+def optimizer_counts(net, trainer, step):
+    """Parameters the optimizer updates vs lazily skips (grid entries with a zero gradient) in one step."""
+    step()
+    torch.cuda.synchronize()
+    nm = net.n_matrix_params
+    nz = int(torch.count_nonzero(trainer.gradients[nm:]).item())
+    return nm + nz, net.n_params - nm - nz
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--variant", default="C2", choices=["C2", "C2p", "C5", "IMG"])
+    ap.add_argument("--batch", type=int, default=B)
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --batch samples per GPU; strong: --batch samples per step over all GPUs")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-seconds", type=float, default=30.0, help="full NeRF step + PSNR sub-record (0: off)")
+    ap.add_argument("--no-c2p", action="store_true", help="skip the C2' (L=16) sub-record")
+    ap.add_argument("--graph", type=int, default=1, help="1: time the K steps as one captured HIP graph (N=1)")
+    ap.add_argument("--overlap", type=int, default=None, help="engine side-stream overlap bitmask (engine.hip)")
+    ap.add_argument("--opt", action="append", default=[], help="model option key=value (ngp_model_set_option)")
+    args = ap.parse_args()
+
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    rank, world, local_rank = pkg.dp.init_from_env()
+    lib = pkg.lib()
+
+    n = args.batch if args.scaling == "weak" else args.batch // world
+    n_opt = (None, None)
+    if args.variant in ("C2", "C2p"):
+        step, capture, net, trainer, comm = nerf_pass(pkg, args.variant, n, rank, world, args.opt, args.overlap)
+        n_opt = optimizer_counts(net, trainer, step)
+        if not args.graph:
+            capture = None
+    elif args.variant == "C5":
+        if world > 1:
+            raise SystemExit("C5 bench is single-GPU")
+        cfg = json.loads(json.dumps(pkg.SDF_BASE))
+        cfg["encoding"].update({"log2_hashmap_size": 22, "per_level_scale": 2.0})
+        net = pkg.NetworkWithInputEncoding(3, 1, cfg["encoding"], cfg["network"])
+        trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+        verts = pkg.synthetic.icosphere(4, radius=0.35, bumps=0.3, seed=rank)
+        tris, amin, amax, brad = pkg.sdf.load_mesh(verts)
+        mesh = pkg.sdf.SdfMesh(tris)
+        sdf = pkg.sdf.SdfTraining(net, trainer, mesh, amin, amax, brad, seed=1337 + rank, batch_size=n)
+        sdf.generate_training_samples(n, sdf.positions, sdf.distances)  # resident batch (online regeneration untimed)
+        torch.cuda.synchronize()
+
+        def step():
+            sdf.train_step(get_loss=False, regenerate=False)
+        n_opt = optimizer_counts(net, trainer, step)
+        capture = None
+    else:  # IMG
+        if world > 1:
+            raise SystemExit("IMG bench is single-GPU")
+        cfg = json.loads(json.dumps(pkg.IMAGE_BASE))
+        cfg["encoding"]["per_level_scale"] = 2.0
+        net = pkg.NetworkWithInputEncoding(2, 3, cfg["encoding"], cfg["network"])
+        trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+        img = pkg.image.Image(pkg.synthetic.synthetic_image(1024, 1024, seed=rank))
+        it = pkg.image.ImageTraining(net, trainer, img, seed=1337 + rank, batch_size=n)
+
+        def step():
+            it.train_step(get_loss=False)
+        capture = None
+
+    dt, launch, kernels = timed_steps(lib, step, args.steps, args.warmup, world, capture)
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    import ctypes
-    need = lib.ngp_profiler_read(None, 0)
-    cbuf = ctypes.create_string_buffer(need)
-    lib.ngp_profiler_read(cbuf, need)
-    kernels = json.loads(cbuf.value.decode())
 
     if rank == 0:
-        a = ALGO[args.variant]
-        per_kernel = {k: v["ms"] / max(v["calls"], 1) for k, v in kernels.items()}
-        roof = {
-            "grid_forward": ("hbm", a["enc_fwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
-            "grid_backward": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
-            "grid_backward_sorted": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
-            "mlp_train": ("mfma", a["mlp_train_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
-            "mlp_infer": ("mfma", a["mlp_fwd_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
-        }
-        dom = max((k for k in roof if k in per_kernel), key=lambda k: per_kernel[k])
-        bound, work, peak, unit = roof[dom]
-        achieved = work / (per_kernel[dom] / 1e3)
-        traffic, traffic_src = pmc_traffic(args.variant, dom)
-        kern_summary = {}
-        for k, ms in per_kernel.items():
-            e = {"avg_ms": round(ms, 4)}
-            if k in roof:
-                b2, w2, p2, u2 = roof[k]
-                e.update({"achieved": round(w2 / (ms / 1e3), 1), "unit": u2, "frac": round(w2 / (ms / 1e3) / p2, 4)})
-            kern_summary[k] = e
+        kern_summary, rl = roofline(args.variant, n, kernels, *n_opt)
         res = {
             "metric": "training samples/sec + PSNR@30s, NeRF Lego at 1/2/4/8 MI355X",
             "value": n * world * args.steps / dt,
@@ -293,25 +381,38 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f16",
             "data": "synthetic (U[0,1)^3 positions, uniform S^2 directions, U(+-1e-2) dL/dout; random-init weights)",
             "config": {"workload": WORKLOADS[args.variant],
                        "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
-                       "launch": "hip_graph" if graph is not None else (graph_note or "eager"),
+                       "launch": launch,
                        "exchange": "engine RCCL all-reduce of the fp16 gradient buffer per step" if world > 1 else None},
             "kernel_timing": ("HIP events per kernel on the launch stream, eager replay of the same K steps queued "
-                              "behind a graph launch" if graph is not None else "HIP events per kernel over the timed region"),
-            "roofline": {"kernel": dom, "bound": bound, "achieved": round(achieved, 1), "peak": peak, "unit": unit,
-                         "frac": round(achieved / peak, 4),
-                         "traffic": None if traffic is None else round(traffic / 1e6, 2),
-                         "traffic_unit": "MB/launch (HBM, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
-                         "traffic_source": traffic_src,
-                         "algorithmic": round(work * (1e3 if unit == "GB/s" else 1e6), 2),
-                         "algorithmic_unit": "MB/launch" if unit == "GB/s" else "MFLOP/launch"},
+                              "behind a graph launch" if launch == "hip_graph" else "HIP events per kernel over the timed region"),
+            "roofline": rl,
+            "optimizer_params": {"updated": n_opt[0], "skipped": n_opt[1]},
             "kernels": kern_summary,
         }
+        if world == 1 and args.variant == "C2":
+            if not args.no_c2p:
+                # BASELINE's literal "L=16": the same training pass at C2' (L=16 F=2 T=2^19)
+                s2, c2, net2, tr2, _ = nerf_pass(pkg, "C2p", n, 0, 1)
+                o2 = optimizer_counts(net2, tr2, s2)
+                dt2, launch2, k2 = timed_steps(lib, s2, args.steps, args.warmup, 1, c2)
+                ks2, rl2 = roofline("C2p", n, k2, *o2)
+                res["c2p"] = {"workload": WORKLOADS["C2p"], "value": n * args.steps / dt2, "unit": "samples/s",
+                              "ms_per_step": dt2 / args.steps * 1e3, "launch": launch2, "roofline": rl2, "kernels": ks2}
+                del s2, c2, net2, tr2
+            if args.e2e_seconds > 0:
+                # the metric's full form: the Testbed NeRF step (occupancy grid, sampling, inference,
+                # loss/compaction, training pass, optimizer) for 30 s, then PSNR on held-out views
+                sys.path.insert(0, os.path.join(ROOT, "tools"))
+                import psnr30
+                e = psnr30.run(pkg, seconds=args.e2e_seconds)
+                res["e2e"] = {k: e[k] for k in ("value", "unit", "psnr", "psnr_views", "train_seconds", "steps", "ms_per_step",
+                                                "data", "config")}
         if world == 1 and not args.no_cpu_baseline and args.variant in ("C2", "C2p"):
             res["cpu_baseline"] = cpu_baseline(args.variant)
         print(json.dumps(res), flush=True)

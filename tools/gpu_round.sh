@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 has() { [[ " $STAGES " == *" $1 "* ]]; }
 
 if has tests; then
-  timeout -k 10 600 python -m pytest tests -m gpu -x -q > "$OUT/gpu_tests.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
   tail -3 "$OUT/gpu_tests.log"
 fi
 if has smoke; then
@@ -20,24 +20,27 @@ if has smoke; then
   tail -2 "$OUT/smoke.log"
 fi
 if has bench; then
-  timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+  timeout -k 10 400 python bench.py ${BENCH_ARGS} > "$OUT/bench.json" 2> "$OUT/bench.err"
   cat "$OUT/bench.json"
 fi
 if has prof; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- \
-      python3 bench.py --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+      python3 bench.py --no-cpu-baseline --e2e-seconds 0 ${PMC_ARGS} > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
   find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
   head -12 "$OUT/kernel_stats.csv"
 fi
 if has pmc; then
-  # HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots), eager launches
-  for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 300 rocprofv3 --pmc $c -f csv -d "$OUT/pmc_$c" -o run -- \
-        python3 bench.py --no-cpu-baseline --graph 0 --steps 5 --warmup 2 > "$OUT/pmc_$c.json" 2> "$OUT/pmc_$c.err"
-    find "$OUT/pmc_$c" -name '*counter_collection.csv' -exec cp {} "$OUT/counters_$c.csv" \;
+  # separate passes (TCC slots): sized read requests, WRITE_SIZE, MFMA utilisation; eager launches
+  BENCH_PMC="python3 bench.py --no-cpu-baseline --e2e-seconds 0 --no-c2p --graph 0 --steps 5 --warmup 2 ${PMC_ARGS}"
+  i=0
+  for c in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" "WRITE_SIZE" \
+           "MfmaUtil SQ_INSTS_VALU_MFMA_MOPS_F16"; do
+    i=$((i+1))
+    timeout -k 10 300 rocprofv3 --pmc $c -f csv -d "$OUT/pmc_$i" -o run -- $BENCH_PMC > "$OUT/pmc_$i.json" 2> "$OUT/pmc_$i.err"
+    find "$OUT/pmc_$i" -name '*counter_collection.csv' -exec cp {} "$OUT/counters_$i.csv" \;
   done
-  python3 tools/pmc_summary.py "$OUT/counters_FETCH_SIZE.csv" "$OUT/counters_WRITE_SIZE.csv" > "$OUT/pmc_summary.json"
-  cat "$OUT/pmc_summary.json"
+  python3 tools/pmc_summary.py "$OUT"/counters_[0-9].csv > "$OUT/pmc_summary.json"
+  python3 -c "import json; d=json.load(open('$OUT/pmc_summary.json')); [print(k[:60], {a: round(b, 4) if isinstance(b, float) else b for a, b in v.items()}) for k, v in d.items()]"
 fi
 if has pmcx; then
   # extra counters for one pass, e.g. PMCX="TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"

@@ -19,19 +19,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--seconds", type=float, default=30.0)
-    ap.add_argument("--images", type=int, default=100)
-    ap.add_argument("--res", type=int, default=800)
-    ap.add_argument("--test-views", type=int, default=8)
-    ap.add_argument("--spp", type=int, default=8)
-    args = ap.parse_args()
-    from __graft_entry__ import load_package
-    pkg = load_package()
+def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8):
+    """Train the full NeRF step for `seconds` of wall clock on the procedural stand-in, then render the
+    held-out views. Returns the result dict (samples/s over the training wall time, mean PSNR)."""
     S = pkg.synthetic
     t0 = time.time()
-    ds = S.lego_like_dataset(n_images=args.images, width=args.res, height=args.res, seed=0, device="cuda")
+    ds = S.lego_like_dataset(n_images=images, width=res, height=res, seed=0, device="cuda")
     t_data = time.time() - t0
     cfg = pkg.nerf.default_config(1.0)
     ncfg = pkg.nerf_config("C2")
@@ -48,31 +41,44 @@ def main():
         steps += 1
         if steps % 100 == 1:
             curve.append((round(time.time() - t_start, 2), steps, round(st["loss"], 6)))
-        if time.time() - t_start >= args.seconds:
+        if time.time() - t_start >= seconds:
             break
     torch.cuda.synchronize()
     t_train = time.time() - t_start
     r = pkg.nerf.NerfRenderer()
-    poses = S.camera_poses(args.images + args.test_views, seed=12345)[-args.test_views:]
+    poses = S.camera_poses(images + test_views, seed=12345)[-test_views:]
     ps, t_render = [], time.time()
     for c2w in poses:
-        cam = pkg.nerf.make_image(args.res, args.res, pkg.nerf.nerf_matrix_to_ngp(c2w), camera_angle_x=S.LEGO_CAMERA_ANGLE_X)
-        img = r.render(net, cfg, cam, run.bitfield, spp=args.spp, min_transmittance=1e-4, background=(0, 0, 0, 1))
-        ref = pkg.nerf.ground_truth_linear(S.render(c2w, args.res, args.res, device="cuda"))
+        cam = pkg.nerf.make_image(res, res, pkg.nerf.nerf_matrix_to_ngp(c2w), camera_angle_x=S.LEGO_CAMERA_ANGLE_X)
+        img = r.render(net, cfg, cam, run.bitfield, spp=spp, min_transmittance=1e-4, background=(0, 0, 0, 1))
+        ref = pkg.nerf.ground_truth_linear(S.render(c2w, res, res, device="cuda"))
         ps.append(pkg.nerf.psnr(img, ref)[0])
     torch.cuda.synchronize()
     t_render = time.time() - t_render
-    print(json.dumps({
+    return {
         "metric": "training samples/sec + PSNR@30s, NeRF Lego at 1/2/4/8 MI355X",
         "value": samples / t_train, "unit": "samples/s", "psnr": float(np.mean(ps)), "psnr_views": [round(p, 2) for p in ps],
         "train_seconds": round(t_train, 2), "steps": steps, "ms_per_step": 1e3 * t_train / steps,
         "n_gpus": 1, "dtype": "f16",
-        "data": f"procedural Lego stand-in: {args.images} views {args.res}x{args.res} RGBA8, camera_angle_x of lego "
+        "data": f"procedural Lego stand-in: {images} views {res}x{res} RGBA8, camera_angle_x of lego "
                 "(nerf_synthetic is not in the image)",
         "config": {"workload": "Testbed NeRF training (configs/nerf/base.json fork, C2) + NerfTracer eval "
-                               f"(black bg, snapped, spp {args.spp})", "batch": 1 << 18},
+                               f"(black bg, snapped, spp {spp})", "batch": 1 << 18},
         "dataset_seconds": round(t_data, 2), "render_seconds": round(t_render, 2), "loss_curve": curve[:40],
-    }), flush=True)
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=30.0)
+    ap.add_argument("--images", type=int, default=100)
+    ap.add_argument("--res", type=int, default=800)
+    ap.add_argument("--test-views", type=int, default=8)
+    ap.add_argument("--spp", type=int, default=8)
+    args = ap.parse_args()
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    print(json.dumps(run(pkg, args.seconds, args.images, args.res, args.test_views, args.spp)), flush=True)
 
 
 if __name__ == "__main__":
