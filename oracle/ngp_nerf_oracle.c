@@ -708,3 +708,34 @@ EXPORT void orc_nerf_render_composite(const ocfg* c, uint32_t n_px, uint32_t max
 EXPORT void orc_math_eval(int fn, size_t n, const float* x, float* y) {
 	for (size_t i = 0; i < n; ++i) y[i] = fn == 0 ? ngp_expf(x[i]) : ngp_logf(x[i]);
 }
+
+/* ---- NerfCounters (testbed_nerf.cu:3568-3609) and the step's inference size (:3923-3930) ---------
+ * tcnn::batch_size_granularity = 256 (tcnn absent: SURVEY §8a row a11 "granularity†"). */
+static uint32_t next_mult(uint32_t v, uint32_t m) { return (v + m - 1) / m * m; }
+
+/* NerfCounters::update_after_training: from the sampler's step counter (all steps, dropped rays
+ * included) and the compacted counter, the measured sizes, the loss scalar (reduce_sum(loss[R]) *
+ * measured / target) and the next rays_per_batch = min(next_multiple((u32)(R * target / measured), 256),
+ * 2^18), in the reference's float arithmetic. Returns the new rays_per_batch; both counters 0 -> the
+ * reference returns early with R unchanged and the measured sizes zeroed. */
+EXPORT uint32_t orc_nerf_counters_update(uint32_t rays_per_batch, uint32_t target_batch_size, uint32_t numsteps_counter,
+                                         uint32_t compacted_counter, float loss_sum, float* loss_scalar,
+                                         uint32_t* measured_batch_size, uint32_t* measured_before_compaction) {
+	*measured_batch_size = 0;
+	*measured_before_compaction = 0;
+	*loss_scalar = 0.f;
+	if (numsteps_counter == 0 || compacted_counter == 0) return rays_per_batch;
+	*measured_before_compaction = numsteps_counter;
+	*measured_batch_size = compacted_counter;
+	*loss_scalar = loss_sum * (float)compacted_counter / (float)target_batch_size;
+	uint32_t r = (uint32_t)((float)rays_per_batch * (float)target_batch_size / (float)compacted_counter);
+	r = next_mult(r, 256);
+	return r < (1u << 18) ? r : (1u << 18);
+}
+
+/* train_nerf_step's inference size: max_samples while nothing has been measured, else
+ * next_multiple(min(measured_before_compaction, max_samples), 256) (testbed_nerf.cu:3923-3930). */
+EXPORT uint32_t orc_nerf_max_inference(uint32_t measured_before_compaction, uint32_t max_samples) {
+	if (measured_before_compaction == 0) return max_samples;
+	return next_mult(measured_before_compaction < max_samples ? measured_before_compaction : max_samples, 256);
+}

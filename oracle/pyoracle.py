@@ -360,6 +360,8 @@ def _declare_nerf(L):
     d("orc_nerf_grid_samples", None, P, u32, Pcg32, u32, P, u32, f32, P, P)
     d("orc_nerf_grid_splat_ema", None, u32, P, P, u32, u32, f32, P)
     d("orc_nerf_grid_mean", C.c_double, P)
+    d("orc_nerf_counters_update", u32, u32, u32, u32, u32, f32, P, P, P)
+    d("orc_nerf_max_inference", u32, u32, u32)
     d("orc_nerf_grid_bitfield", None, P, u32, f32, P)
     d("orc_fill_rollover_f32", None, u32, u32, u32, P)
     d("orc_fill_rollover_f16", None, u32, u32, u32, P, C.c_int)
@@ -437,6 +439,21 @@ def nerf_grid_splat_ema(indices, density16, act, grid, decay=0.95):
     """density16: fp16 bits of the density output (one per sample). Updates grid (float32) in place."""
     lib().orc_nerf_grid_splat_ema(indices.size, ptr(np.ascontiguousarray(indices, np.uint32)),
                                   ptr(np.ascontiguousarray(density16, np.uint16)), act, grid.size, decay, ptr(grid))
+
+
+def nerf_counters_update(rays_per_batch, target_batch_size, numsteps_counter, compacted_counter, loss_sum=0.0):
+    """NerfCounters::update_after_training (testbed_nerf.cu:3583-3609): returns (rays_per_batch,
+    measured_batch_size, measured_before_compaction, loss_scalar)."""
+    ls = C.c_float(0)
+    mb = C.c_uint32(0)
+    mbc = C.c_uint32(0)
+    r = lib().orc_nerf_counters_update(rays_per_batch, target_batch_size, numsteps_counter, compacted_counter, loss_sum,
+                                       C.byref(ls), C.byref(mb), C.byref(mbc))
+    return r, mb.value, mbc.value, ls.value
+
+
+def nerf_max_inference(measured_before_compaction, max_samples):
+    return lib().orc_nerf_max_inference(measured_before_compaction, max_samples)
 
 
 def nerf_grid_mean(grid):

@@ -60,3 +60,14 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
     monkeypatch.setattr(capi, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(capi.NgpError, match="HIP engine library missing"):
         capi.lib()
+
+
+def test_cpp_drop_in_links_against_the_c_abi():
+    """tests/cabi/drop_in (g++ over include/ngp_tcnn_adapter.hpp, no HIP headers) is built by build(),
+    resolves libngp_engine.so and runs up to its argument check without touching a GPU."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cabi", "drop_in")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "cabi")])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr

@@ -243,6 +243,27 @@ def test_nerf_training_end_to_end(pkg, orc):
     assert 0.0 < occupied < 0.5  # the grid prunes once step >= 256 switches to the 0.01 threshold (:3518)
 
 
+def test_counters_follow_oracle_recurrence(pkg, orc):
+    """Row a11: every step's rays_per_batch is NerfCounters::update_after_training
+    (testbed_nerf.cu:3583-3609, oracle orc_nerf_counters_update) of the rays it traced and its measured
+    counts, from the initial 4096 (testbed.h:440); the counts themselves are bit-exact with the oracle's
+    sampler and compaction (test_generate_training_samples_*, test_compute_loss)."""
+    ds = pkg.synthetic.lego_like_dataset(n_images=8, width=96, height=96, seed=5)
+    cfg = pkg.nerf.default_config(1.0)
+    net = pkg.create_nerf_network(pkg.nerf_config("C2"))
+    tr = pkg.Trainer(net, pkg.nerf_config("C2")["optimizer"])
+    run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
+    B = cfg.target_batch_size
+    R = 4096
+    for k in range(60):
+        s = run.train_step(get_loss=(k % 7 == 0))
+        r, mb, mbc, _ = orc.nerf_counters_update(R, B, s["measured_batch_size_before_compaction"], s["measured_batch_size"])
+        assert (s["rays_per_batch"], s["measured_batch_size"], s["measured_batch_size_before_compaction"]) == (r, mb, mbc), k
+        assert s["measured_batch_size"] <= B
+        R = r
+    assert R > 4096  # the batch grew toward the 2^18 target
+
+
 def test_inference_rgbd_layout(pkg):
     """NGP_LAYOUT_AOS_RGBD (the NeRF trainer's inference output) = rows 0..3 of the padded AoS output."""
     cfg = pkg.nerf_config("C2")

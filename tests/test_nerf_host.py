@@ -107,3 +107,21 @@ def test_oracle_rollover(orc):
     orc.fill_rollover(a, 3)
     np.testing.assert_array_equal(a[3:6], a[0:3])
     np.testing.assert_array_equal(a[9], a[0])
+
+
+def test_counters_update_oracle_hand_cases(orc):
+    """NerfCounters::update_after_training (testbed_nerf.cu:3583-3609), cases worked by hand."""
+    B = 1 << 18
+    # 4096 * 262144 / 100000 = 10737.4 -> 10737 -> next multiple of 256 = 10752
+    assert orc.nerf_counters_update(4096, B, 500000, 100000, 2.0) == (10752, 100000, 500000, pytest.approx(2.0 * 100000 / B))
+    # either counter zero: early return, rays_per_batch unchanged, measured sizes zeroed
+    assert orc.nerf_counters_update(4096, B, 0, 0)[:3] == (4096, 0, 0)
+    assert orc.nerf_counters_update(7936, B, 123, 0)[:3] == (7936, 0, 0)
+    # clamp to 2^18 rays
+    assert orc.nerf_counters_update(1 << 18, B, 4 << 18, 1000)[0] == 1 << 18
+    # exact fit keeps R (already a multiple of 256)
+    assert orc.nerf_counters_update(8192, B, 9 << 18, B)[0] == 8192
+    # the step's inference size (testbed_nerf.cu:3923-3930)
+    assert orc.nerf_max_inference(0, 1 << 22) == 1 << 22
+    assert orc.nerf_max_inference(300001, 1 << 22) == 300032
+    assert orc.nerf_max_inference(5 << 22, 1 << 22) == 1 << 22
