@@ -660,6 +660,332 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	}
 }
 
+// ------------------------------------------------------------------------------------------------
+// NerfNetwork training pass, weight gradients split across the block's four waves
+// ------------------------------------------------------------------------------------------------
+// k_nerf_mlp<TRAIN> keeps every layer's dW in each wave's registers (36 16x16 fp32 tiles at C2 =
+// 144 registers), which leaves no room for the weight fragments: the backward reads them from LDS
+// with a wait per layer, one wave per SIMD. Here a block of 4 waves processes 4 tiles of 32 samples
+// per iteration in two phases:
+//   A  each wave runs its tile's forward and backward dX chains with ALL weight fragments in
+//      registers (no LDS reads), and writes the activations and every layer's output gradient dZ
+//      to its LDS image [sample][feature];
+//   B  after a barrier, wave w accumulates its quarter of dW over the 4 images (K = 128 samples):
+//      row block m = w of the 64-row layers, column block n = w of the 16-row output layers
+//      (9 tiles = 36 registers at C2), then a second barrier frees the images.
+// Each wave ends up with disjoint dW tiles and stores them straight into the block's slab (no
+// cross-wave reduction). Sum order is fixed (block iterations, then waves 0..3): bitwise
+// reproducible like the one-wave-per-tile kernel.
+template <int ES, int DH, int RH>
+struct NerfTrainLayout {
+	using L = NerfLayout<ES, DH, RH>;
+	static constexpr int N_BWD = L::N_ALL - L::N_FWD;
+	static constexpr int S_16 = 16 + 4;
+	// per-wave images (halves)
+	static constexpr int I_XE = 0;                                  // [32][16 ES]
+	static constexpr int I_HD = I_XE + 32 * L::S_XE;                // DH x [32][64]
+	static constexpr int I_RIN = I_HD + DH * 32 * L::S_64;          // [32][32] density out | SH
+	static constexpr int I_HR = I_RIN + 32 * L::S_RIN;              // RH x [32][64]
+	static constexpr int I_ZRO = I_HR + RH * 32 * L::S_64;          // dZ rgb output [32][16]
+	static constexpr int I_ZRH = I_ZRO + 32 * S_16;                 // (RH-1) x [32][64], j-th = layer RH-1-j
+	static constexpr int I_ZR0 = I_ZRH + (RH - 1) * 32 * L::S_64;   // dZ rgb layer 0
+	static constexpr int I_ZDO = I_ZR0 + 32 * L::S_64;              // dZ density output [32][16]
+	static constexpr int I_ZDH = I_ZDO + 32 * S_16;                 // (DH-1) x [32][64]
+	static constexpr int I_ZD0 = I_ZDH + (DH - 1) * 32 * L::S_64;   // dZ density layer 0
+	static constexpr int IMG_HALVES = I_ZD0 + 32 * L::S_64;
+	static constexpr size_t LDS_BYTES = 4 * (size_t)IMG_HALVES * sizeof(f16);
+	// this wave's dW tiles
+	static constexpr int W_RO = 0;                    // rgb output:  m 0,    n = wave
+	static constexpr int W_RH = 1;                    // rgb hidden:  m = wave, n 0..3 (RH-1 layers)
+	static constexpr int W_R0 = W_RH + 4 * (RH - 1);  // rgb layer 0: m = wave, n 0..1
+	static constexpr int W_DO = W_R0 + 2;             // density out: m 0,    n = wave
+	static constexpr int W_DH = W_DO + 1;             // density hidden: m = wave, n 0..3
+	static constexpr int W_D0 = W_DH + 4 * (DH - 1);  // density layer 0: m = wave, n 0..ES-1
+	static constexpr int N_DW = W_D0 + ES;
+};
+
+// dW[m0+m][n0+n] += dZ^T X over one image's 32 samples (16x16x32 MFMAs, K = samples)
+template <int MC, int NC>
+__device__ __forceinline__ void dw_part(f32x4* dw, const f16* dz_img, int dz_stride, int m0, const f16* x_img, int x_stride, int n0,
+                                        int lane) {
+	f16x8 a[MC], b[NC];
+#pragma unroll
+	for (int m = 0; m < MC; ++m) a[m] = img_frag(dz_img, dz_stride, 16 * (m0 + m), lane);
+#pragma unroll
+	for (int n = 0; n < NC; ++n) b[n] = img_frag(x_img, x_stride, 16 * (n0 + n), lane);
+#pragma unroll
+	for (int m = 0; m < MC; ++m)
+#pragma unroll
+		for (int n = 0; n < NC; ++n) dw[m * NC + n] = mfma16(a[m], b[n], dw[m * NC + n]);
+}
+
+// Store dW tiles (16x16, 4 regs: out = 16m + 4(lane>>4) + r, in = 16n + (lane&15)) into the slab at
+// their parameter-slice positions [out x in].
+template <int MC, int NC>
+__device__ __forceinline__ void dw_store(const f32x4* dw, float* slab, uint32_t woff, uint32_t in_dim, int m0, int n0, int lane) {
+#pragma unroll
+	for (int m = 0; m < MC; ++m)
+#pragma unroll
+		for (int n = 0; n < NC; ++n)
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const uint32_t o = 16 * (m0 + m) + 4 * (lane >> 4) + r, i = 16 * (n0 + n) + (lane & 15);
+				slab[woff + o * in_dim + i] = dw[m * NC + n][r];
+			}
+}
+
+template <int ES, int DH, int RH, bool FUSE>
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_nerf_mlp_train(const NerfMlpArgs a) {
+	static_assert(!FUSE || ES == 1, "fused encoding: one 16-wide encoding step");
+	using Lay = NerfLayout<ES, DH, RH>;
+	using T = NerfTrainLayout<ES, DH, RH>;
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	const int lane = threadIdx.x & 63, h = lane >> 5;
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	f16* img_all = (f16*)smem;
+	f16* img = img_all + wave * T::IMG_HALVES;
+
+	// every weight fragment in registers for the whole kernel (loaded once from global)
+	f16x8 wreg[Lay::N_FWD], breg[T::N_BWD];
+#pragma unroll
+	for (int q = 0; q < Lay::N_FWD; ++q) wreg[q] = a.frags[q * 64 + lane];
+#pragma unroll
+	for (int q = 0; q < T::N_BWD; ++q) breg[q] = a.frags[(Lay::N_FWD + q) * 64 + lane];
+	f32x4 dw[T::N_DW];
+#pragma unroll
+	for (int q = 0; q < T::N_DW; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+	const uint32_t n_tiles = (a.n + 31) / 32;
+	f16x8 xe_n[ES];
+	float cd_n[3];
+	f16x4 dl_n;
+	// FUSE (MLP_TRAIN_ENC): the encoding is gathered here, as in k_nerf_mlp's MLP_INFER_ENC path (lane
+	// half h blends levels 2h, 2h+1 with k_grid_forward_rows' arithmetic, one tile ahead)
+	f16x4 graw[FUSE ? 2 : 1][8];
+	float gfrac[FUSE ? 2 : 1][3];
+	float px_n[3];
+	uint32_t lv_off[2], lv_T[2], lv_res[2];
+	float lv_scale[2];
+	bool lv_hashed[2], lv_active[2];
+	if constexpr (FUSE) {
+		const float ml = a.max_level * (float)a.gc.n_levels;
+#pragma unroll
+		for (int j = 0; j < 2; ++j) {
+			const uint32_t l0 = j, l1 = 2 + j;
+			lv_off[j] = h ? a.gc.offsets[l1] : a.gc.offsets[l0];
+			lv_T[j] = h ? a.gc.offsets[l1 + 1] - a.gc.offsets[l1] : a.gc.offsets[l0 + 1] - a.gc.offsets[l0];
+			lv_res[j] = h ? a.gc.resolution[l1] : a.gc.resolution[l0];
+			lv_scale[j] = h ? a.gc.scale[l1] : a.gc.scale[l0];
+			lv_hashed[j] = (a.gc.hashed >> (h ? l1 : l0)) & 1u;
+			lv_active[j] = !((float)(h ? l1 : l0) >= ml + 1e-3f);
+		}
+	}
+	auto load_pos = [&](uint32_t tile) {
+		const uint32_t smp = tile * 32 + (lane & 31);
+		const float* cp = a.coords + (size_t)(smp < a.n ? smp : 0) * a.coord_stride;
+		px_n[0] = cp[0]; px_n[1] = cp[1]; px_n[2] = cp[2];
+	};
+	auto load_inputs = [&](uint32_t tile) {
+		const uint32_t smp = tile * 32 + (lane & 31);
+		const uint32_t ls = smp < a.n ? smp : 0;
+		if constexpr (FUSE) {
+			const float x[3] = {px_n[0], px_n[1], px_n[2]};
+			load_pos(tile + gridDim.x * 4);
+#pragma unroll
+			for (int j = 0; j < 2; ++j) {
+				uint32_t gb[3];
+#pragma unroll
+				for (int d = 0; d < 3; ++d) {
+					const float p = __builtin_fmaf(lv_scale[j], x[d], 0.5f);
+					const float t = floorf(p);
+					gb[d] = (uint32_t)(int)t;
+					gfrac[j][d] = p - t;
+				}
+				const f16* tab = a.table + (size_t)lv_off[j] * 4;
+#pragma unroll
+				for (uint32_t k = 0; k < 8; ++k) {
+					const uint32_t cx = gb[0] + (k & 1u), cy = gb[1] + ((k >> 1) & 1u), cz = gb[2] + ((k >> 2) & 1u);
+					const uint32_t ih = (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (lv_T[j] - 1u);
+					uint32_t id = cx + lv_res[j] * (cy + lv_res[j] * cz);
+					if (__builtin_expect(!lv_hashed[j] && id >= lv_T[j], 0)) id %= lv_T[j];
+					const uint32_t idx = lv_hashed[j] ? ih : id;
+					graw[j][k] = lv_active[j] ? *(const f16x4*)(tab + (size_t)idx * 4) : f16x4{};
+				}
+			}
+		} else {
+#pragma unroll
+			for (int s = 0; s < ES; ++s) xe_n[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
+		}
+		const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
+		cd_n[0] = cd[0]; cd_n[1] = cd[1]; cd_n[2] = cd[2];
+		dl_n = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
+	};
+	if constexpr (FUSE) load_pos(blockIdx.x * 4 + wave);
+	load_inputs(blockIdx.x * 4 + wave);
+	// every wave runs the same number of iterations (the barriers need all four); tiles past the end
+	// run on zero inputs and zero output gradients, so their dW contribution is exactly zero
+	for (uint32_t base = blockIdx.x * 4; base < n_tiles; base += gridDim.x * 4) {
+		const uint32_t tile = base + wave;
+		const uint32_t sample = tile * 32 + (lane & 31);
+		const bool valid = sample < a.n;
+		f16x8 xe[ES];
+		if constexpr (FUSE) {
+			// trilinear blend in k_grid_forward_rows' order (fp32 FMAs, one RNE rounding per feature)
+			f16x8 r;
+#pragma unroll
+			for (int j = 0; j < 2; ++j) {
+				float acc4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+				for (uint32_t k = 0; k < 8; ++k) {
+					const float w = corner_weight<3>(gfrac[j], k);
+#pragma unroll
+					for (int f = 0; f < 4; ++f) acc4[f] = __builtin_fmaf(w, (float)graw[j][k][f], acc4[f]);
+				}
+#pragma unroll
+				for (int f = 0; f < 4; ++f) {
+					asm volatile("" : "+v"(acc4[f]));
+					r[4 * j + f] = (f16)acc4[f];
+				}
+			}
+			xe[0] = valid ? r : f16x8{};
+		} else {
+#pragma unroll
+			for (int s = 0; s < ES; ++s) xe[s] = valid ? xe_n[s] : f16x8{};
+		}
+		const float cdx = cd_n[0], cdy = cd_n[1], cdz = cd_n[2];
+		const f16x4 dl_cur = dl_n;
+		load_inputs(tile + gridDim.x * 4);  // unconditional (past-the-end tiles read sample 0)
+
+		// ---- phase A: forward ----------------------------------------------------------------
+#pragma unroll
+		for (int s = 0; s < ES; ++s) img_store_std(img + T::I_XE, Lay::S_XE, xe[s], s, lane);
+		f32x16 acc[2];
+		f16x8 hd[DH][4];
+		layer_fwd_reg<2, ES>(acc, xe, wreg, Lay::F_D0);
+		pack_tiles<2>(acc, hd[0], true);
+#pragma unroll
+		for (int l = 1; l < DH; ++l) {
+			layer_fwd_reg<2, 4>(acc, hd[l - 1], wreg, Lay::F_DH + 8 * (l - 1));
+			pack_tiles<2>(acc, hd[l], true);
+		}
+		f32x16 dacc[1];
+		layer_fwd_reg<1, 4>(dacc, hd[DH - 1], wreg, Lay::F_DO);
+		f16x8 dout[2];
+		pack_tile(dacc[0], dout[0], dout[1], false);
+		f16x8 rin[2] = {dout[0], sh4_frag(cdx, cdy, cdz, h)};
+		if (!valid) rin[1] = f16x8{};
+		f16x8 hr[RH][4];
+		layer_fwd_reg<2, 2>(acc, rin, wreg, Lay::F_R0);
+		pack_tiles<2>(acc, hr[0], true);
+#pragma unroll
+		for (int l = 1; l < RH; ++l) {
+			layer_fwd_reg<2, 4>(acc, hr[l - 1], wreg, Lay::F_RH + 8 * (l - 1));
+			pack_tiles<2>(acc, hr[l], true);
+		}
+		f32x16 racc[1];
+		layer_fwd_reg<1, 4>(racc, hr[RH - 1], wreg, Lay::F_RO);
+		if (a.out && valid) {
+			f16x8 ro, ro_hi;
+			pack_tile(racc[0], ro, ro_hi, false);
+			if (h == 0) ro[3] = dout[0][0];  // extract_density (nerf_network.h:32-43)
+			store_out16(a.out, a.out_stride, a.out_layout, a.n, sample, h, ro);
+		}
+#pragma unroll
+		for (int l = 0; l < DH; ++l) img_store_acc<4>(img + T::I_HD + l * 32 * Lay::S_64, Lay::S_64, hd[l], lane);
+		{
+			f16x8 d1[1] = {dout[0]};
+			img_store_acc<1>(img + T::I_RIN, Lay::S_RIN, d1, lane);
+			img_store_std(img + T::I_RIN, Lay::S_RIN, rin[1], 1, lane);
+		}
+#pragma unroll
+		for (int l = 0; l < RH; ++l) img_store_acc<4>(img + T::I_HR + l * 32 * Lay::S_64, Lay::S_64, hr[l], lane);
+
+		// ---- phase A: backward dX chain, every dZ kept in LDS ---------------------------------
+		float dsig;
+		f16x8 dz1[1];
+		{
+			const f16x4 d = valid ? dl_cur : f16x4{};
+			dsig = (float)d[3];
+			dz1[0] = h == 0 ? f16x8{d[0], d[1], d[2], (f16)0.f, 0, 0, 0, 0} : f16x8{};  // extract_rgb (:46-60)
+		}
+		img_store_acc<1>(img + T::I_ZRO, T::S_16, dz1, lane);
+		f16x8 dz[4];
+		layer_fwd_reg<2, 1>(acc, dz1, breg, Lay::B_RO - Lay::N_FWD);
+		mask_pack<2>(acc, hr[RH - 1], dz);
+#pragma unroll
+		for (int l = RH - 1; l >= 1; --l) {
+			img_store_acc<4>(img + T::I_ZRH + (RH - 1 - l) * 32 * Lay::S_64, Lay::S_64, dz, lane);
+			layer_fwd_reg<2, 4>(acc, dz, breg, Lay::B_RH - Lay::N_FWD + 8 * (RH - 1 - l));
+			mask_pack<2>(acc, hr[l - 1], dz);
+		}
+		img_store_acc<4>(img + T::I_ZR0, Lay::S_64, dz, lane);
+		f32x16 a1[1];
+		layer_fwd_reg<1, 4>(a1, dz, breg, Lay::B_R0 - Lay::N_FWD);
+		f16x8 dd[1], unused;
+		pack_tile(a1[0], dd[0], unused, false);
+		if (h == 0) dd[0][0] = (f16)((float)dd[0][0] + dsig);  // add_density_gradient (:63-74)
+		img_store_acc<1>(img + T::I_ZDO, T::S_16, dd, lane);
+		layer_fwd_reg<2, 1>(acc, dd, breg, Lay::B_DO - Lay::N_FWD);
+		mask_pack<2>(acc, hd[DH - 1], dz);
+#pragma unroll
+		for (int l = DH - 1; l >= 1; --l) {
+			img_store_acc<4>(img + T::I_ZDH + (DH - 1 - l) * 32 * Lay::S_64, Lay::S_64, dz, lane);
+			layer_fwd_reg<2, 4>(acc, dz, breg, Lay::B_DH - Lay::N_FWD + 8 * (DH - 1 - l));
+			mask_pack<2>(acc, hd[l - 1], dz);
+		}
+		img_store_acc<4>(img + T::I_ZD0, Lay::S_64, dz, lane);
+		if (a.dL_denc) {
+			f32x16 ae[Lay::ET];
+			layer_fwd_reg<Lay::ET, 4>(ae, dz, breg, Lay::B_D0 - Lay::N_FWD);
+#pragma unroll
+			for (int t = 0; t < Lay::ET; ++t) {
+				f16x8 lo, hi;
+				pack_tile(ae[t], lo, hi, false);
+				if (!valid) continue;
+				f16* row = a.dL_denc + (size_t)sample * a.denc_stride + 32 * t + 4 * h;
+				*(f16x4*)(row + 0) = f16x4{lo[0], lo[1], lo[2], lo[3]};
+				*(f16x4*)(row + 8) = f16x4{lo[4], lo[5], lo[6], lo[7]};
+				if (32 * t + 16 < 16 * ES) {
+					*(f16x4*)(row + 16) = f16x4{hi[0], hi[1], hi[2], hi[3]};
+					*(f16x4*)(row + 24) = f16x4{hi[4], hi[5], hi[6], hi[7]};
+				}
+			}
+		}
+		__syncthreads();
+
+		// ---- phase B: this wave's quarter of dW over the four images ---------------------------
+#pragma unroll
+		for (int w = 0; w < 4; ++w) {
+			const f16* im = img_all + w * T::IMG_HALVES;
+			dw_part<1, 1>(dw + T::W_RO, im + T::I_ZRO, T::S_16, 0, im + T::I_HR + (RH - 1) * 32 * Lay::S_64, Lay::S_64, wave, lane);
+#pragma unroll
+			for (int j = 0; j < RH - 1; ++j)
+				dw_part<1, 4>(dw + T::W_RH + 4 * j, im + T::I_ZRH + j * 32 * Lay::S_64, Lay::S_64, wave,
+				              im + T::I_HR + (RH - 2 - j) * 32 * Lay::S_64, Lay::S_64, 0, lane);
+			dw_part<1, 2>(dw + T::W_R0, im + T::I_ZR0, Lay::S_64, wave, im + T::I_RIN, Lay::S_RIN, 0, lane);
+			dw_part<1, 1>(dw + T::W_DO, im + T::I_ZDO, T::S_16, 0, im + T::I_HD + (DH - 1) * 32 * Lay::S_64, Lay::S_64, wave, lane);
+#pragma unroll
+			for (int j = 0; j < DH - 1; ++j)
+				dw_part<1, 4>(dw + T::W_DH + 4 * j, im + T::I_ZDH + j * 32 * Lay::S_64, Lay::S_64, wave,
+				              im + T::I_HD + (DH - 2 - j) * 32 * Lay::S_64, Lay::S_64, 0, lane);
+			dw_part<1, ES>(dw + T::W_D0, im + T::I_ZD0, Lay::S_64, wave, im + T::I_XE, Lay::S_XE, 0, lane);
+		}
+		__syncthreads();
+	}
+
+	// this wave's dW tiles -> the block's slab (parameter-slice layout; the waves' tiles are disjoint)
+	float* slab = a.dw_slab + (size_t)blockIdx.x * a.n_matrix;
+	const uint32_t dw0 = a.density_woff, rw0 = a.rgb_woff;
+	dw_store<1, 1>(dw + T::W_RO, slab, rw0 + 64 * 32 + 64 * 64 * (RH - 1), 64, 0, wave, lane);
+#pragma unroll
+	for (int j = 0; j < RH - 1; ++j) dw_store<1, 4>(dw + T::W_RH + 4 * j, slab, rw0 + 64 * 32 + 64 * 64 * (RH - 2 - j), 64, wave, 0, lane);
+	dw_store<1, 2>(dw + T::W_R0, slab, rw0, 32, wave, 0, lane);
+	dw_store<1, 1>(dw + T::W_DO, slab, dw0 + 64 * 16 * ES + 64 * 64 * (DH - 1), 64, 0, wave, lane);
+#pragma unroll
+	for (int j = 0; j < DH - 1; ++j) dw_store<1, 4>(dw + T::W_DH + 4 * j, slab, dw0 + 64 * 16 * ES + 64 * 64 * (DH - 2 - j), 64, wave, 0, lane);
+	dw_store<1, ES>(dw + T::W_D0, slab, dw0, 16 * ES, wave, 0, lane);
+}
+
 template <int ES, int DH, int RH, int MODE>
 static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	using Lay = NerfLayout<ES, DH, RH>;
@@ -673,6 +999,15 @@ static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	const uint32_t tiles = (a.n + 31) / 32;
 	uint32_t blocks = TRAIN ? nerf_mlp_train_blocks(a.n) : std::min<uint32_t>(div_round_up(tiles, 4), 8 * device_cu_count());
 	if (blocks == 0) return;
+	if constexpr (TRAIN && NerfTrainLayout<ES, DH, RH>::LDS_BYTES <= 160 * 1024 && Lay::N_ALL <= 44) {
+		// weight gradients split across the waves, all fragments in registers (k_nerf_mlp_train)
+		auto kt = k_nerf_mlp_train<ES, DH, RH, MODE == MLP_TRAIN_ENC>;
+		const size_t lt = NerfTrainLayout<ES, DH, RH>::LDS_BYTES;
+		ensure_dynamic_lds((const void*)kt, lt);
+		kt<<<blocks, 256, lt, s>>>(a);
+		NGP_HIP(hipGetLastError());
+		return;
+	}
 	auto kern = k_nerf_mlp<ES, DH, RH, MODE>;
 	ensure_dynamic_lds((const void*)kern, lds);
 	auto ak = a;

@@ -255,13 +255,14 @@ def test_counters_follow_oracle_recurrence(pkg, orc):
     run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
     B = cfg.target_batch_size
     R = 4096
+    seen = set()
     for k in range(60):
         s = run.train_step(get_loss=(k % 7 == 0))
         r, mb, mbc, _ = orc.nerf_counters_update(R, B, s["measured_batch_size_before_compaction"], s["measured_batch_size"])
         assert (s["rays_per_batch"], s["measured_batch_size"], s["measured_batch_size_before_compaction"]) == (r, mb, mbc), k
-        assert s["measured_batch_size"] <= B
-        R = r
-    assert R > 4096  # the batch grew toward the 2^18 target
+        R = r  # (the compacted counter may exceed B: it counts every ray's request, :1825-1835)
+        seen.add(R)
+    assert seen != {4096}  # the ray count adapted (down: the untrained density keeps every ray long)
 
 
 def test_inference_rgbd_layout(pkg):
