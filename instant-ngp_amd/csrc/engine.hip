@@ -12,6 +12,7 @@
 
 #include "../../include/ngp_engine.h"
 #include "common.h"
+#include "engine_internal.h"
 #include "grid_scatter.h"
 #include "grid.h"
 #include "json.h"
@@ -846,7 +847,21 @@ int ngp_trainer_training_step(ngp_trainer* t, void* stream, uint32_t n, const fl
 int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
                                       const void* dL_doutput, uint32_t dL_stride, float loss_scale, uint32_t n_steps,
                                       int with_optimizer, ngp_graph** out) {
-	NGP_ARG(t && out && stream && n > 0 && input && dL_doutput && loss_scale > 0.f && n_steps >= 1);
+	NGP_ARG(t);
+	return ngp::capture_training_step_with(t, stream, n, input, input_stride, dL_doutput, dL_stride, loss_scale, n_steps,
+	                                       with_optimizer, t->allreduce, t->allreduce_user, t->world, out);
+}
+}  // extern "C"
+
+// The capture with an explicit gradient exchange hook and world factor (ngp_trainer_capture_training_step
+// passes the trainer's own; the data-parallel NeRF trainer passes its communicator with world factor 1,
+// because its shards' dL/doutput is already scaled by 128 / R_global, so the summed gradient is the
+// 1-GPU gradient).
+int ngp::capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                                    const void* dL_doutput, uint32_t dL_stride, float loss_scale, uint32_t n_steps,
+                                    int with_optimizer, ngp_allreduce_fn allreduce, void* allreduce_user, uint32_t world,
+                                    ngp_graph** out) {
+	NGP_ARG(t && out && stream && n > 0 && input && dL_doutput && loss_scale > 0.f && n_steps >= 1 && world >= 1);
 	NGP_TRY({
 		ngp_model* m = t->model;
 		m->require_params(false);
@@ -860,14 +875,14 @@ int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, 
 		int rc = NGP_OK;
 		for (uint32_t k = 0; k < n_steps && rc == NGP_OK; ++k) {
 			rc = ngp_forward_backward(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE);
-			if (rc == NGP_OK && t->allreduce) {
-				rc = t->allreduce(t->allreduce_user, t->g16, t->n, NGP_DTYPE_F16, NGP_REDUCE_SUM, stream);
+			if (rc == NGP_OK && allreduce) {
+				rc = allreduce(allreduce_user, t->g16, t->n, NGP_DTYPE_F16, NGP_REDUCE_SUM, stream);
 				if (rc != NGP_OK && g_last_error.empty()) g_last_error = "gradient all-reduce failed";
 			}
 			if (rc == NGP_OK && with_optimizer) {
 				try {
 					// the summed gradient of `world` ranks: mean via the loss scale
-					t->run_step(s, loss_scale * (float)t->world, t->ctl, k);  // step = device base (set per launch) + k
+					t->run_step(s, loss_scale * (float)world, t->ctl, k);  // step = device base (set per launch) + k
 				} catch (const std::exception& e) {
 					g_last_error = e.what();
 					rc = NGP_ERROR;
@@ -887,6 +902,7 @@ int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, 
 		*out = g.release();
 	});
 }
+extern "C" {
 
 int ngp_trainer_set_allreduce(ngp_trainer* t, uint32_t world, ngp_allreduce_fn allreduce, void* user) {
 	NGP_ARG(t && world >= 1);

@@ -17,6 +17,7 @@
 #include <fstream>
 #include <sstream>
 
+#include "engine_internal.h"
 #include "json.h"
 #include "msgpack.h"
 #include "nerf.h"
@@ -136,7 +137,9 @@ struct ngp_nerf_trainer {
 	uint32_t rank = 0, world = 1;
 	ngp_allreduce_fn allreduce = nullptr;
 	void* allreduce_user = nullptr;
+	bool dp_capturable = false;  // the hook is the engine's RCCL communicator: the DP training pass is a graph
 	Buf dp_scalars;
+	bool dp() const { return allreduce != nullptr; }
 	// occupancy grid
 	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens;
 	// training workspaces
@@ -450,6 +453,10 @@ int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint3
 	t->world = world;
 	t->allreduce = allreduce;
 	t->allreduce_user = user;
+	// an RCCL hook is stream-ordered and graph-capturable; a host callback (gloo) is not
+	t->dp_capturable = allreduce == ngp_dp_comm_allreduce;
+	if (t->train_graph) ngp_graph_destroy(t->train_graph);  // re-captured with (or without) the exchange
+	t->train_graph = nullptr;
 	return NGP_OK;
 }
 
@@ -508,6 +515,38 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 __global__ void k_publish_counters(const uint32_t* __restrict__ ctr, volatile uint32_t* host, uint32_t seq) {
 	if (threadIdx.x == 0) {
 		host[0] = ctr[0]; host[1] = ctr[1]; host[2] = ctr[2]; host[3] = ctr[3];
+		__threadfence_system();
+		host[4] = seq;
+	}
+}
+
+// Data parallel: this shard's counters and loss as five floats for one all-reduce (sum). The u32
+// counters travel as 16-bit halves so their sums stay exact in fp32 for up to 256 ranks; the per-ray
+// losses are normalised by the shard's ray count (compute_loss), rescaled here to 1 / R_global.
+__global__ void k_dp_pack(const uint32_t* __restrict__ ctr, const float* __restrict__ loss, uint32_t n_loss, float loss_rescale,
+                          float* __restrict__ out) {
+	__shared__ float part[16];
+	float sum = 0.f;
+	for (uint32_t i = threadIdx.x; i < n_loss; i += blockDim.x) sum += loss[i];
+	for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+	if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		float t = 0.f;
+		for (uint32_t w = 0; w < blockDim.x / 64; ++w) t += part[w];
+		out[0] = (float)(ctr[1] >> 16); out[1] = (float)(ctr[1] & 0xffffu);
+		out[2] = (float)(ctr[2] >> 16); out[3] = (float)(ctr[2] & 0xffffu);
+		out[4] = t * loss_rescale;
+	}
+}
+// the all-reduced counters -> host-coherent memory (host[1] steps, host[2] compacted, host[5] loss bits;
+// host[6] this shard's own step count, which sizes its next inference)
+__global__ void k_dp_publish(const float* __restrict__ red, const uint32_t* __restrict__ ctr, volatile uint32_t* host, uint32_t seq) {
+	if (threadIdx.x == 0) {
+		host[6] = ctr[1];
+		host[1] = ((uint32_t)red[0] << 16) + (uint32_t)red[1];
+		host[2] = ((uint32_t)red[2] << 16) + (uint32_t)red[3];
+		host[5] = __float_as_uint(red[4]);
 		__threadfence_system();
 		host[4] = seq;
 	}
@@ -601,7 +640,6 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		// train_nerf_step (testbed_nerf.cu:3867-4132)
 		const SamplePlan sp = sample_plan(t);
 		const uint32_t R = sp.R, Rl = sp.Rl, Bl = sp.Bl, max_inference = sp.max_inference, Ra = sp.Ra;
-		const uint32_t W = t->world;
 		if (t->training_step == 0) t->n_rays_total = 0;
 		t->n_rays_total += R;
 		uint32_t* ray_indices = sp.ray_indices;
@@ -628,11 +666,12 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		// only the 4 live outputs (raw rgb, raw density): compute_loss reads nothing else
 		check_rc(ngp_inference(t->model, s, max_inference, coords, 7, mlp_out, 4, NGP_LAYOUT_AOS_RGBD, 0));
 		}
+		const bool dp = t->dp();
 		const float loss_scale_local = 128.0f * (float)Rl / (float)R;
 		{
 		ProfScope ps("nerf_loss", s);
 		check_rc(nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, 4, ray_indices, rays, numsteps, coords, coords_c,
-		                               dloss, loss, ctr + 2, (const float*)t->mean.p, W > 1 ? loss_scale_local : 128.0f));
+		                               dloss, loss, ctr + 2, (const float*)t->mean.p, dp ? loss_scale_local : 128.0f));
 		fill_rollover_pair(Bl, ctr + 2, dloss, 16, coords_c, 7, s);  // fill_rollover_and_rescale + fill_rollover
 		}
 		// the step's counters are final here (the training pass does not touch them): publish them before
@@ -643,9 +682,23 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			t->host_ctr = (volatile uint32_t*)p;
 			memset(p, 0, 64);
 		}
-		k_publish_counters<<<1, 64, 0, s>>>(ctr, t->host_ctr, ++t->publish_seq);
+		if (dp) {
+			// NerfCounters::update_after_training on the global batch: this shard's counters and loss
+			// all-reduced on the stream, then published like the single-GPU counters (no copies, no sync)
+			ProfScope ps("nerf_dp_counters", s);
+			float* d = t->dp_scalars.get<float>(8);
+			k_dp_pack<<<1, 1024, 0, s>>>(ctr, loss, get_loss ? Rl : 0u, (float)Rl / (float)R, d);
+			NGP_HIP(hipGetLastError());
+			NGP_CHECK(t->allreduce(t->allreduce_user, d, 5, NGP_DTYPE_F32, NGP_REDUCE_SUM, s) == 0,
+			          "data parallel: counter all-reduce failed");
+			k_dp_publish<<<1, 64, 0, s>>>(d, ctr, t->host_ctr, ++t->publish_seq);
+		} else {
+			k_publish_counters<<<1, 64, 0, s>>>(ctr, t->host_ctr, ++t->publish_seq);
+		}
 		NGP_HIP(hipGetLastError());
-		const bool can_pipeline = t->pipeline && W == 1;
+		// the next step's sampler may run under this step's training pass when the exchange is
+		// stream-ordered (single GPU, or the engine's RCCL communicator)
+		const bool can_pipeline = t->pipeline && (!dp || t->dp_capturable);
 		if (can_pipeline) {
 			if (!t->sample_stream) {
 				NGP_HIP(hipStreamCreateWithFlags(&t->sample_stream, hipStreamNonBlocking));
@@ -656,14 +709,18 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		}
 		{
 		ProfScope ps("nerf_train_pass", s);
-		if (W == 1) {
-			// re-record when the graph's buffers moved: the sample buffers, or any model workspace (a
-			// density-grid update through ngp_density can grow the encoding workspace after a snapshot load)
+		if (!dp || t->dp_capturable) {
+			// one HIP graph per step: forward_backward [+ the gradient all-reduce, RCCL] + optimizer. Re-record
+			// when the graph's buffers moved: the sample buffers, or any model workspace (a density-grid
+			// update through ngp_density can grow the encoding workspace after a snapshot load)
 			if (!t->train_graph || t->graph_in != coords_c || t->graph_dl != dloss || t->graph_n != Bl ||
 			    t->graph_epoch != ngp_model_workspace_epoch(t->model)) {
 				if (t->train_graph) ngp_graph_destroy(t->train_graph);
 				t->train_graph = nullptr;
-				check_rc(ngp_trainer_capture_training_step(t->trainer, s, Bl, coords_c, 7, dloss, 16, 128.0f, 1, 1, &t->train_graph));
+				// data parallel: the shards' dL/doutput is scaled by 128 / R_global, so the summed gradient is
+				// the 1-GPU gradient: world factor 1 in the optimizer
+				check_rc(capture_training_step_with(t->trainer, s, Bl, coords_c, 7, dloss, 16, 128.0f, 1, 1,
+				                                    dp ? t->allreduce : nullptr, t->allreduce_user, 1, &t->train_graph));
 				t->graph_in = coords_c;
 				t->graph_dl = dloss;
 				t->graph_n = Bl;
@@ -671,6 +728,7 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			}
 			check_rc(ngp_graph_launch(t->train_graph, s));
 		} else {
+			// host-callback exchange (gloo): not capturable
 			check_rc(ngp_forward_backward(t->model, s, Bl, coords_c, 7, nullptr, 0, dloss, 16, NGP_GRAD_OVERWRITE));
 			NGP_CHECK(t->allreduce(t->allreduce_user, ngp_trainer_gradients(t->trainer), ngp_model_n_params(t->model), NGP_DTYPE_F16,
 			                       NGP_REDUCE_SUM, s) == 0,
@@ -682,32 +740,24 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		++t->training_step;
 		// NerfCounters::update_after_training (testbed_nerf.cu:3583-3609): host sync
 		uint32_t h[4];
-		std::vector<float> hl;
-		if (get_loss && Rl) {
-			hl.resize(Rl);
+		double loss_sum = 0;
+		if (get_loss && Rl && !dp) {
+			std::vector<float> hl(Rl);
 			NGP_HIP(hipMemcpyAsync(hl.data(), loss, (size_t)Rl * 4, hipMemcpyDeviceToHost, s));
 			NGP_HIP(hipStreamSynchronize(s));
+			for (float v : hl) loss_sum += v;
 		} else {
 			wait_published(t->host_ctr, t->publish_seq, s);
 		}
 		for (int k = 0; k < 4; ++k) h[k] = t->host_ctr[k];
-		double loss_sum = 0;
-		for (float v : hl) loss_sum += v;
-		t->measured_before_compaction_local = h[1];
-		if (W > 1) {
-			// counters and loss of all shards (NerfCounters::update_after_training on the global batch)
-			float* d = t->dp_scalars.get<float>(4);
-			// per-ray losses are normalised by this shard's ray count (compute_loss): rescale to 1 / R
-			const float hv[4] = {(float)h[1], (float)h[2], (float)(loss_sum * (double)Rl / (double)R), 0.f};
-			NGP_HIP(hipMemcpyAsync(d, hv, 16, hipMemcpyHostToDevice, s));
-			NGP_CHECK(t->allreduce(t->allreduce_user, d, 3, NGP_DTYPE_F32, NGP_REDUCE_SUM, s) == 0,
-			          "data parallel: counter all-reduce failed");
-			float gv[4];
-			NGP_HIP(hipMemcpyAsync(gv, d, 16, hipMemcpyDeviceToHost, s));
-			NGP_HIP(hipStreamSynchronize(s));
-			h[1] = (uint32_t)gv[0];
-			h[2] = (uint32_t)gv[1];
-			loss_sum = gv[2];
+		if (dp) {
+			const uint32_t lb = t->host_ctr[5];
+			float lv;
+			memcpy(&lv, &lb, 4);
+			loss_sum = lv;
+			t->measured_before_compaction_local = t->host_ctr[6];
+		} else {
+			t->measured_before_compaction_local = h[1];
 		}
 		float loss_scalar = 0.f;
 		t->measured_batch_size = 0;

@@ -226,14 +226,16 @@ class NerfTraining:
         words = wrap_device(self._buffers()[1], BITFIELD_BYTES // 4, torch.float32)
         return words.view(torch.uint8)
 
-    def set_data_parallel(self, rank, world, group=None):
+    def set_data_parallel(self, rank, world, group=None, exchange_at_world_1=False):
         """Shard the rays (global ids kept), the compacted batch and the density-grid evaluation over
         `world` ranks; gradients, density-grid maxima and counters are all-reduced by the engine's RCCL
-        communicator (nccl backend) or through torch.distributed (gloo: dp.make_allreduce_callback)."""
+        communicator (nccl backend) or through torch.distributed (gloo: dp.make_allreduce_callback).
+        exchange_at_world_1: run the data-parallel step (exchanges included) with one rank too — on a
+        one-GPU box, the way to exercise the RCCL path (it must then train bitwise like the plain step)."""
         import torch.distributed as dist
         from .dp import EngineComm, make_allreduce_callback
         self._allreduce = None
-        if world > 1 and dist.get_backend(group) == "nccl":
+        if (world > 1 or exchange_at_world_1) and dist.get_backend(group) == "nccl":
             # one GPU per rank: the engine's RCCL communicator, enqueued on the training stream
             self._allreduce = EngineComm(rank, world, group)
             fn, user = self._allreduce.fn, self._allreduce.handle

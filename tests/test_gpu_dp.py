@@ -34,9 +34,11 @@ def _run(rank, world, port, out_dir):
     if world > 1:
         run.set_data_parallel(rank, world)
     log = []
-    for _ in range(STEPS):
+    for k in range(STEPS):
         s = run.train_step(get_loss=True)
         torch.cuda.synchronize()
+        if k == 0:  # the step's gradient (all-reduced across the ranks when sharded)
+            np.save(os.path.join(out_dir, f"grad0_w{world}_r{rank}.npy"), tr.gradients.float().cpu().numpy())
         log.append({"loss": s["loss"], "rays": s["rays_per_batch"], "measured": s["measured_batch_size"],
                     "params": hashlib.sha1(tr.params.cpu().numpy().tobytes()).hexdigest(),
                     "grid": hashlib.sha1(run.density_grid.cpu().numpy().tobytes()).hexdigest()})
@@ -56,6 +58,12 @@ def test_nerf_data_parallel_two_ranks(tmp_path):
     r0 = json.load(open(tmp_path / "w2_r0.json"))
     r1 = json.load(open(tmp_path / "w2_r1.json"))
     single = json.load(open(tmp_path / "w1_r0.json"))
+    # step 0: the shards' summed gradient is the 1-GPU gradient up to fp16 rounding of the two partial sums
+    g2 = np.load(tmp_path / "grad0_w2_r0.npy")
+    g1 = np.load(tmp_path / "grad0_w1_r0.npy")
+    assert np.array_equal(g2, np.load(tmp_path / "grad0_w2_r1.npy"))
+    tol = 2 * np.abs(g1) * 2.0 ** -10 + 1e-3 * np.abs(g1).max()
+    assert np.all(np.abs(g2 - g1) <= tol), np.abs(g2 - g1).max()
     for a, b in zip(r0, r1):
         assert a["params"] == b["params"] and a["grid"] == b["grid"]
         assert a["rays"] == b["rays"] and a["measured"] == b["measured"]
@@ -119,3 +127,51 @@ def test_engine_rccl_allreduce_in_captured_step(tmp_path):
     mp.spawn(_engine_comm_run, args=(29400 + os.getpid() % 1000, str(tmp_path)), nprocs=1, join=True)
     a, b = json.load(open(tmp_path / "comm.json"))
     assert a == b
+
+
+def _nerf_rccl_world1(_rank, port, out_dir):
+    """The data-parallel NeRF step with the engine's RCCL communicator at world 1: counters and loss
+    all-reduced on the stream and published (no copies), the training pass one captured graph with the
+    gradient all-reduce inside, the next step's sampler pipelined under it. World 1 must train bitwise
+    like the plain step (N > 1 over xGMI is the driver's scaling run)."""
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": "0", "WORLD_SIZE": "1"})
+    import torch.distributed as dist
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    logs = []
+    for dp_mode in (False, True):
+        ds = pkg.synthetic.lego_like_dataset(n_images=10, width=96, height=96, seed=3)
+        cfg = pkg.nerf.default_config(1.0)
+        ncfg = pkg.nerf_config("C2")
+        net = pkg.create_nerf_network(ncfg)
+        tr = pkg.Trainer(net, ncfg["optimizer"])
+        run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
+        if dp_mode:
+            run.set_data_parallel(0, 1, exchange_at_world_1=True)
+        log = []
+        for k in range(70):
+            s = run.train_step(get_loss=(k % 5 == 0))
+            log.append([s["rays_per_batch"], s["measured_batch_size"], s["measured_batch_size_before_compaction"],
+                        round(float(s["loss"]), 5)])
+        torch.cuda.synchronize()
+        log.append([hashlib.sha1(tr.params.cpu().numpy().tobytes()).hexdigest(),
+                    hashlib.sha1(run.density_grid.cpu().numpy().tobytes()).hexdigest()])
+        logs.append(log)
+        del run
+    dist.destroy_process_group()
+    with open(os.path.join(out_dir, "nerf_world1.json"), "w") as f:
+        json.dump(logs, f)
+
+
+def test_nerf_data_parallel_rccl_world1_is_exact(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+    mp.spawn(_nerf_rccl_world1, args=(29700 + os.getpid() % 1000, str(tmp_path)), nprocs=1, join=True)
+    plain, dp = json.load(open(tmp_path / "nerf_world1.json"))
+    assert plain[-1] == dp[-1]  # parameters and density grid, bitwise
+    for a, b in zip(plain[:-1], dp[:-1]):
+        assert a[:3] == b[:3]  # counters
+        assert b[3] == pytest.approx(a[3], rel=1e-4, abs=1e-7)  # loss (device float sum vs host double sum)

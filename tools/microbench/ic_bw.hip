@@ -49,6 +49,30 @@ __global__ void k_copy8(const uint4* __restrict__ a, uint4* __restrict__ b, size
 		for (int u = 0; u < 4; ++u) if (i + u * stride < n) { v[u].x += 1u; b[i + u * stride] = v[u]; }
 	}
 }
+// one 16-B element per thread, no loop (the optimizer's shape: n/256 blocks, every block resident once)
+__global__ void k_read_flat(const uint4* __restrict__ a, size_t n, float* __restrict__ sink) {
+	const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const uint4 v = a[i];
+	if ((v.x ^ v.y ^ v.z ^ v.w) == 0x12345678u) sink[0] = 1.f;
+}
+__global__ void k_copy_flat(const uint4* __restrict__ a, uint4* __restrict__ b, size_t n) {
+	const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	uint4 v = a[i];
+	v.x += 1u;
+	b[i] = v;
+}
+// read-modify-write of 4 arrays of 16 B per thread (the optimizer's state streams)
+__global__ void k_rmw4_flat(uint4* __restrict__ a, size_t n) {
+	const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	uint4 v[4];
+#pragma unroll
+	for (int k = 0; k < 4; ++k) v[k] = a[k * n + i];
+#pragma unroll
+	for (int k = 0; k < 4; ++k) { v[k].x += 1u; a[k * n + i] = v[k]; }
+}
 __global__ void k_copy(const uint4* __restrict__ a, uint4* __restrict__ b, size_t n) {
 	for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
 		uint4 v = a[i];
@@ -91,6 +115,9 @@ int main() {
 		timed("read16", (double)bytes, [&] { k_read<<<grid, block>>>(buf, n, sink); });
 		timed("write16", (double)bytes, [&] { k_write<<<grid, block>>>(buf, n); });
 		timed("copy16", (double)bytes, [&] { k_copy<<<grid, block>>>(buf, buf + n / 2, n / 2); });
+		timed("read16_flat", (double)bytes, [&] { k_read_flat<<<(unsigned)((n + 255) / 256), block>>>(buf, n, sink); });
+		timed("copy16_flat", (double)bytes, [&] { k_copy_flat<<<(unsigned)((n / 2 + 255) / 256), block>>>(buf, buf + n / 2, n / 2); });
+		timed("rmw4_flat", 2.0 * bytes, [&] { k_rmw4_flat<<<(unsigned)((n / 4 + 255) / 256), block>>>(buf, n / 4); });
 		timed("read16x8", (double)bytes, [&] { k_read8<<<grid, block>>>(buf, n, sink); });
 		timed("copy16x4", (double)bytes, [&] { k_copy8<<<grid, block>>>(buf, buf + n / 2, n / 2); });
 	}
