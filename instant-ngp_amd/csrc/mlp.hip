@@ -51,7 +51,7 @@ NerfMlpPlan make_nerf_mlp_plan(uint32_t enc_width, uint32_t width, uint32_t d_hi
 }
 
 MlpPlan make_mlp_plan(uint32_t enc_width, uint32_t width, uint32_t hidden, uint32_t out_pad) {
-	NGP_CHECK(width == 64, "FullyFusedMLP: this engine implements n_neurons == 64");
+	NGP_CHECK(width == 16 || width == 32 || width == 64, "FullyFusedMLP: this engine implements n_neurons 16, 32 and 64");
 	NGP_CHECK(enc_width == 16 || enc_width == 32, "NetworkWithInputEncoding: encoding width must pad to 16 or 32");
 	NGP_CHECK(out_pad == 16, "FullyFusedMLP: output width must pad to 16");
 	NGP_CHECK(hidden >= 1 && hidden <= 4, "FullyFusedMLP: 1..4 hidden layers supported");
@@ -59,13 +59,15 @@ MlpPlan make_mlp_plan(uint32_t enc_width, uint32_t width, uint32_t hidden, uint3
 	p.enc_steps = enc_width / 16; p.hidden = hidden;
 	p.mlp = MlpDims{enc_width, width, hidden, out_pad};
 	auto& v = p.descs;
-	add_frags(v, p.mlp.layer_off(0), enc_width, 64, 2, p.enc_steps, false, 0);
-	for (uint32_t h = 1; h < hidden; ++h) add_frags(v, p.mlp.layer_off(h), 64, 64, 2, 4, false, 0xF);
-	add_frags(v, p.mlp.layer_off(hidden), 64, 16, 1, 4, false, 0xF);
+	// hidden outputs: HT tiles of 32 rows; hidden inputs: HS k-steps of 16 (MlpLayout)
+	const uint32_t W = width, HT = (W + 31) / 32, HS = W / 16, pm = (1u << HS) - 1u;
+	add_frags(v, p.mlp.layer_off(0), enc_width, W, HT, p.enc_steps, false, 0);
+	for (uint32_t h = 1; h < hidden; ++h) add_frags(v, p.mlp.layer_off(h), W, W, HT, HS, false, pm);
+	add_frags(v, p.mlp.layer_off(hidden), W, 16, 1, HS, false, pm);
 	p.n_fwd_frags = (uint32_t)v.size();
-	add_frags(v, p.mlp.layer_off(hidden), 64, 16, 2, 1, true, 0xF);
-	for (uint32_t h = hidden - 1; h >= 1; --h) add_frags(v, p.mlp.layer_off(h), 64, 64, 2, 4, true, 0xF);
-	add_frags(v, p.mlp.layer_off(0), enc_width, 64, (enc_width + 31) / 32, 4, true, 0xF);
+	add_frags(v, p.mlp.layer_off(hidden), W, 16, HT, 1, true, 0xF);
+	for (uint32_t h = hidden - 1; h >= 1; --h) add_frags(v, p.mlp.layer_off(h), W, W, HT, HS, true, pm);
+	add_frags(v, p.mlp.layer_off(0), enc_width, W, (enc_width + 31) / 32, HS, true, pm);
 	p.n_bwd_frags = (uint32_t)v.size() - p.n_fwd_frags;
 	return p;
 }
@@ -113,7 +115,7 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
 
 // acc[t] = sum_s A(frag base + t*STEPS + s) * in[s]
 template <int TILES, int STEPS>
-__device__ __forceinline__ void layer_fwd(f32x16 (&acc)[TILES], const f16x8 (&in)[STEPS], const f16x8* frags, int lane) {
+__device__ __forceinline__ void layer_fwd(f32x16 (&acc)[TILES], const f16x8* in, const f16x8* frags, int lane) {
 #pragma unroll
 	for (int t = 0; t < TILES; ++t) {
 		f32x16 c = {};
@@ -199,7 +201,7 @@ __device__ __forceinline__ void mask_pack(const f32x16 (&acc)[TILES], const f16x
 // Write packed accumulator-layout fragments (frags[2t+s] = tile t regs 8s..8s+7) of one sample
 // column into the wave's [sample][feature] image: features 32t + 16s + 8k + 4h + (0..3).
 template <int NFRAG>
-__device__ __forceinline__ void img_store_acc(f16* img, int stride, const f16x8 (&f)[NFRAG], int lane, int feat0 = 0) {
+__device__ __forceinline__ void img_store_acc(f16* img, int stride, const f16x8* f, int lane, int feat0 = 0) {
 	const int smp = lane & 31, h = lane >> 5;
 	f16* row = img + smp * stride + feat0 + 4 * h;
 #pragma unroll
@@ -1063,32 +1065,38 @@ bool nerf_mlp_fused_encoding_ok(const GridDesc& g, uint32_t enc_width) {
 // ------------------------------------------------------------------------------------------------
 // Single MLP (NetworkWithInputEncoding): enc -> 64 x NH -> 16
 // ------------------------------------------------------------------------------------------------
-template <int ES, int NH>
+// WD = n_neurons (16, 32 or 64): hidden layers are HT = ceil(WD / 32) accumulator tiles of 32 rows (a
+// 16-wide layer uses rows 0..15 of one tile; the padded rows have zero weights, so they hold zero and
+// never reach the next layer, which reads HS = WD / 16 k-steps).
+template <int ES, int NH, int WD>
 struct MlpLayout {
+	static constexpr int HT = (WD + 31) / 32;
+	static constexpr int HS = WD / 16;
 	static constexpr int F_0 = 0;
-	static constexpr int F_H = F_0 + 2 * ES;
-	static constexpr int F_O = F_H + 8 * (NH - 1);
-	static constexpr int N_FWD = F_O + 4;
+	static constexpr int F_H = F_0 + HT * ES;
+	static constexpr int F_O = F_H + HT * HS * (NH - 1);
+	static constexpr int N_FWD = F_O + HS;
 	static constexpr int B_O = N_FWD;
-	static constexpr int B_H = B_O + 2;
-	static constexpr int B_0 = B_H + 8 * (NH - 1);
+	static constexpr int B_H = B_O + HT;
+	static constexpr int B_0 = B_H + HT * HS * (NH - 1);
 	static constexpr int ET = (ES + 1) / 2;
-	static constexpr int N_ALL = B_0 + 4 * ET;
+	static constexpr int N_ALL = B_0 + ET * HS;
 	static constexpr int S_XE = 16 * ES + 4;
-	static constexpr int S_64 = 64 + 4;
+	static constexpr int S_W = WD + 4;
 	static constexpr int I_XE = 0;
 	static constexpr int I_H = I_XE + 32 * S_XE;
-	static constexpr int I_DZ = I_H + NH * 32 * S_64;
-	static constexpr int IMG_HALVES = I_DZ + 32 * S_64;
+	static constexpr int I_DZ = I_H + NH * 32 * S_W;
+	static constexpr int IMG_HALVES = I_DZ + 32 * S_W;
 	static constexpr int W_O = 0;
-	static constexpr int W_H = 4;
-	static constexpr int W_0 = W_H + 16 * (NH - 1);
-	static constexpr int N_DW = W_0 + 4 * ES;
+	static constexpr int W_H = HS;
+	static constexpr int W_0 = W_H + HS * HS * (NH - 1);
+	static constexpr int N_DW = W_0 + HS * ES;
 };
 
-template <int ES, int NH, int MODE>
+template <int ES, int NH, int WD, int MODE>
 __global__ void __launch_bounds__(256, 1) k_mlp(const MlpArgs a) {
-	using Lay = MlpLayout<ES, NH>;
+	using Lay = MlpLayout<ES, NH, WD>;
+	constexpr int HT = Lay::HT, HS = Lay::HS;
 	constexpr bool TRAIN = MODE == MLP_TRAIN;
 	constexpr int NFRAG = TRAIN ? Lay::N_ALL : Lay::N_FWD;
 	extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1114,17 +1122,17 @@ __global__ void __launch_bounds__(256, 1) k_mlp(const MlpArgs a) {
 			if (!valid) xe[s] = f16x8{};
 			if constexpr (TRAIN) img_store_std(img + Lay::I_XE, Lay::S_XE, xe[s], s, lane);
 		}
-		f32x16 acc[2];
-		f16x8 hh[NH][4];
-		layer_fwd<2, ES>(acc, xe, lfrag + Lay::F_0 * 64, lane);
-		pack_tiles<2>(acc, hh[0], true);
+		f32x16 acc[HT];
+		f16x8 hh[NH][2 * HT];
+		layer_fwd<HT, ES>(acc, xe, lfrag + Lay::F_0 * 64, lane);
+		pack_tiles<HT>(acc, hh[0], true);
 #pragma unroll
 		for (int l = 1; l < NH; ++l) {
-			layer_fwd<2, 4>(acc, hh[l - 1], lfrag + (Lay::F_H + 8 * (l - 1)) * 64, lane);
-			pack_tiles<2>(acc, hh[l], true);
+			layer_fwd<HT, HS>(acc, hh[l - 1], lfrag + (Lay::F_H + HT * HS * (l - 1)) * 64, lane);
+			pack_tiles<HT>(acc, hh[l], true);
 		}
 		f32x16 oacc[1];
-		layer_fwd<1, 4>(oacc, hh[NH - 1], lfrag + Lay::F_O * 64, lane);
+		layer_fwd<1, HS>(oacc, hh[NH - 1], lfrag + Lay::F_O * 64, lane);
 		if (a.out && valid) {
 			f16x8 lo, hi;
 			pack_tile(oacc[0], lo, hi, false);
@@ -1132,7 +1140,7 @@ __global__ void __launch_bounds__(256, 1) k_mlp(const MlpArgs a) {
 		}
 		if constexpr (TRAIN) {
 #pragma unroll
-			for (int l = 0; l < NH; ++l) img_store_acc<4>(img + Lay::I_H + l * 32 * Lay::S_64, Lay::S_64, hh[l], lane);
+			for (int l = 0; l < NH; ++l) img_store_acc<HS>(img + Lay::I_H + l * 32 * Lay::S_W, Lay::S_W, hh[l], lane);
 			f16* dz_img = img + Lay::I_DZ;
 			f16x8 dzo[1];
 			{
@@ -1145,23 +1153,23 @@ __global__ void __launch_bounds__(256, 1) k_mlp(const MlpArgs a) {
 				}
 				dzo[0] = d;
 			}
-			img_store_acc<1>(dz_img, Lay::S_64, dzo, lane);
-			dw_accum<1, 4>(dw + Lay::W_O, dz_img, Lay::S_64, img + Lay::I_H + (NH - 1) * 32 * Lay::S_64, Lay::S_64, lane);
-			f16x8 dz[4];
-			layer_fwd<2, 1>(acc, dzo, lfrag + Lay::B_O * 64, lane);
-			mask_pack<2>(acc, hh[NH - 1], dz);
+			img_store_acc<1>(dz_img, Lay::S_W, dzo, lane);
+			dw_accum<1, HS>(dw + Lay::W_O, dz_img, Lay::S_W, img + Lay::I_H + (NH - 1) * 32 * Lay::S_W, Lay::S_W, lane);
+			f16x8 dz[2 * HT];
+			layer_fwd<HT, 1>(acc, dzo, lfrag + Lay::B_O * 64, lane);
+			mask_pack<HT>(acc, hh[NH - 1], dz);
 #pragma unroll
 			for (int l = NH - 1; l >= 1; --l) {
-				img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
-				dw_accum<4, 4>(dw + Lay::W_H + 16 * (NH - 1 - l), dz_img, Lay::S_64, img + Lay::I_H + (l - 1) * 32 * Lay::S_64, Lay::S_64, lane);
-				layer_fwd<2, 4>(acc, dz, lfrag + (Lay::B_H + 8 * (NH - 1 - l)) * 64, lane);
-				mask_pack<2>(acc, hh[l - 1], dz);
+				img_store_acc<HS>(dz_img, Lay::S_W, dz, lane);
+				dw_accum<HS, HS>(dw + Lay::W_H + HS * HS * (NH - 1 - l), dz_img, Lay::S_W, img + Lay::I_H + (l - 1) * 32 * Lay::S_W, Lay::S_W, lane);
+				layer_fwd<HT, HS>(acc, dz, lfrag + (Lay::B_H + HT * HS * (NH - 1 - l)) * 64, lane);
+				mask_pack<HT>(acc, hh[l - 1], dz);
 			}
-			img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
-			dw_accum<4, ES>(dw + Lay::W_0, dz_img, Lay::S_64, img + Lay::I_XE, Lay::S_XE, lane);
+			img_store_acc<HS>(dz_img, Lay::S_W, dz, lane);
+			dw_accum<HS, ES>(dw + Lay::W_0, dz_img, Lay::S_W, img + Lay::I_XE, Lay::S_XE, lane);
 			if (a.dL_denc) {
 				f32x16 ae[Lay::ET];
-				layer_fwd<Lay::ET, 4>(ae, dz, lfrag + Lay::B_0 * 64, lane);
+				layer_fwd<Lay::ET, HS>(ae, dz, lfrag + Lay::B_0 * 64, lane);
 #pragma unroll
 				for (int t = 0; t < Lay::ET; ++t) {
 					f16x8 lo, hi;
@@ -1179,23 +1187,23 @@ __global__ void __launch_bounds__(256, 1) k_mlp(const MlpArgs a) {
 		}
 	}
 	if constexpr (TRAIN) {
-		const uint32_t o_off = 64 * 16 * ES + 64 * 64 * (NH - 1);
+		const uint32_t o_off = WD * 16 * ES + WD * WD * (NH - 1);
 		dw_block_reduce((float*)smem, a.n_matrix, a.n_reg, wave, a.dw_slab + (size_t)blockIdx.x * a.n_matrix,
 		                [&](float* red, auto first) {
-			dw_flush<1, 4>(dw + Lay::W_O, red, o_off, 64, lane, first);
+			dw_flush<1, HS>(dw + Lay::W_O, red, o_off, WD, lane, first);
 #pragma unroll
 			for (int l = NH - 1; l >= 1; --l)
-				dw_flush<4, 4>(dw + Lay::W_H + 16 * (NH - 1 - l), red, 64 * 16 * ES + 64 * 64 * (l - 1), 64, lane, first);
-			dw_flush<4, ES>(dw + Lay::W_0, red, 0, 16 * ES, lane, first);
+				dw_flush<HS, HS>(dw + Lay::W_H + HS * HS * (NH - 1 - l), red, WD * 16 * ES + WD * WD * (l - 1), WD, lane, first);
+			dw_flush<HS, ES>(dw + Lay::W_0, red, 0, 16 * ES, lane, first);
 		});
 	}
 }
 
 uint32_t mlp_train_blocks(uint32_t n) { return nerf_mlp_train_blocks(n); }
 
-template <int ES, int NH, int MODE>
+template <int ES, int NH, int WD, int MODE>
 static void launch_mlp(const MlpArgs& a, hipStream_t s) {
-	using Lay = MlpLayout<ES, NH>;
+	using Lay = MlpLayout<ES, NH, WD>;
 	constexpr bool TRAIN = MODE == MLP_TRAIN;
 	constexpr int NFRAG = TRAIN ? Lay::N_ALL : Lay::N_FWD;
 	size_t lds = (size_t)NFRAG * 1024 + (TRAIN ? 4 * Lay::IMG_HALVES * sizeof(f16) : 0);
@@ -1205,7 +1213,7 @@ static void launch_mlp(const MlpArgs& a, hipStream_t s) {
 	NGP_CHECK(lds <= 160 * 1024, "MLP: LDS budget exceeded");
 	const uint32_t tiles = (a.n + 31) / 32;
 	uint32_t blocks = TRAIN ? mlp_train_blocks(a.n) : std::min<uint32_t>(div_round_up(tiles, 4), 8 * device_cu_count());
-	auto kern = k_mlp<ES, NH, MODE>;
+	auto kern = k_mlp<ES, NH, WD, MODE>;
 	ensure_dynamic_lds((const void*)kern, lds);
 	auto ak = a;
 	ak.n_reg = n_reg;
@@ -1213,17 +1221,26 @@ static void launch_mlp(const MlpArgs& a, hipStream_t s) {
 	NGP_HIP(hipGetLastError());
 }
 
+template <int WD, int MODE>
+static void dispatch_mlp_w(const MlpPlan& p, const MlpArgs& a, hipStream_t s) {
+	switch (p.enc_steps * 10 + p.hidden) {
+		case 11: launch_mlp<1, 1, WD, MODE>(a, s); break;
+		case 12: launch_mlp<1, 2, WD, MODE>(a, s); break;
+		case 13: launch_mlp<1, 3, WD, MODE>(a, s); break;
+		case 21: launch_mlp<2, 1, WD, MODE>(a, s); break;
+		case 22: launch_mlp<2, 2, WD, MODE>(a, s); break;
+		case 23: launch_mlp<2, 3, WD, MODE>(a, s); break;
+		case 24: launch_mlp<2, 4, WD, MODE>(a, s); break;
+		default: throw Error("FullyFusedMLP: unsupported (encoding width, hidden layers) combination");
+	}
+}
 template <int MODE>
 static void dispatch_mlp(const MlpPlan& p, const MlpArgs& a, hipStream_t s) {
-	switch (p.enc_steps * 10 + p.hidden) {
-		case 11: launch_mlp<1, 1, MODE>(a, s); break;
-		case 12: launch_mlp<1, 2, MODE>(a, s); break;
-		case 13: launch_mlp<1, 3, MODE>(a, s); break;
-		case 21: launch_mlp<2, 1, MODE>(a, s); break;
-		case 22: launch_mlp<2, 2, MODE>(a, s); break;
-		case 23: launch_mlp<2, 3, MODE>(a, s); break;
-		case 24: launch_mlp<2, 4, MODE>(a, s); break;
-		default: throw Error("FullyFusedMLP: unsupported (encoding width, hidden layers) combination");
+	switch (p.mlp.width) {
+		case 16: dispatch_mlp_w<16, MODE>(p, a, s); break;
+		case 32: dispatch_mlp_w<32, MODE>(p, a, s); break;
+		case 64: dispatch_mlp_w<64, MODE>(p, a, s); break;
+		default: throw Error("FullyFusedMLP: n_neurons must be 16, 32 or 64");
 	}
 }
 

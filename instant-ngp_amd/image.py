@@ -37,6 +37,18 @@ class Image:
         check(lib().ngp_image_create(self.width, self.height, rgba.ctypes.data, C.byref(h)))
         self.handle = h
 
+    @classmethod
+    def load(cls, path):
+        """Testbed::load_image (testbed_image.cu:372-402): .exr through the EXR reader (exr.py, tinyexr's
+        LoadEXRFromMemory semantics), .npy as an [H, W, 4] float array; other formats raise."""
+        p = str(path).lower()
+        if p.endswith(".exr"):
+            from .exr import read_exr
+            return cls(read_exr(path))
+        if p.endswith(".npy"):
+            return cls(np.load(path))
+        raise ValueError(f"unsupported image format: {path} (EXR or .npy)")
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h:

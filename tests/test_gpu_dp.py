@@ -58,12 +58,9 @@ def test_nerf_data_parallel_two_ranks(tmp_path):
     r0 = json.load(open(tmp_path / "w2_r0.json"))
     r1 = json.load(open(tmp_path / "w2_r1.json"))
     single = json.load(open(tmp_path / "w1_r0.json"))
-    # step 0: the shards' summed gradient is the 1-GPU gradient up to fp16 rounding of the two partial sums
-    g2 = np.load(tmp_path / "grad0_w2_r0.npy")
-    g1 = np.load(tmp_path / "grad0_w1_r0.npy")
-    assert np.array_equal(g2, np.load(tmp_path / "grad0_w2_r1.npy"))
-    tol = 2 * np.abs(g1) * 2.0 ** -10 + 1e-3 * np.abs(g1).max()
-    assert np.all(np.abs(g2 - g1) <= tol), np.abs(g2 - g1).max()
+    # every rank holds the same all-reduced gradient (the batches differ from the 1-GPU step's wherever
+    # compaction truncates or rolls over per shard, so the sum is compared on a fixed batch below)
+    assert np.array_equal(np.load(tmp_path / "grad0_w2_r0.npy"), np.load(tmp_path / "grad0_w2_r1.npy"))
     for a, b in zip(r0, r1):
         assert a["params"] == b["params"] and a["grid"] == b["grid"]
         assert a["rays"] == b["rays"] and a["measured"] == b["measured"]
@@ -175,3 +172,36 @@ def test_nerf_data_parallel_rccl_world1_is_exact(tmp_path):
     for a, b in zip(plain[:-1], dp[:-1]):
         assert a[:3] == b[:3]  # counters
         assert b[3] == pytest.approx(a[3], rel=1e-4, abs=1e-7)  # loss (device float sum vs host double sum)
+
+
+def test_sharded_gradient_sum_equals_full_batch():
+    """SURVEY §8e collective 1: the shards' gradients (each rank's half of one fixed 2^15-sample batch,
+    dL/doutput scaled by 1/2 as the NeRF step scales by 128 / R_global) sum to the gradient of the whole
+    batch within the fp16 rounding of each partial and of the total (grid: exact sums rounded once per
+    shard; MLP: fp32 slab sums rounded once) — the all-reduce then adds exactly those partials."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    cfg = pkg.nerf_config("C2")
+    cfg["encoding"]["log2_hashmap_size"] = 16
+    n = 1 << 15
+    g = np.random.default_rng(9)
+    x = np.zeros((n, 7), np.float32)
+    x[:, :3] = g.random((n, 3))
+    x[:, 4:] = g.random((n, 3))
+    dL = np.zeros((n, 16), np.float32)
+    dL[:, :4] = g.uniform(-1, 1, (n, 4))
+    net = pkg.create_nerf_network(cfg)
+    tr = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+
+    def grad(lo, hi, scale):
+        net.forward_backward(torch.from_numpy(x[lo:hi]).cuda(), torch.from_numpy((dL[lo:hi] * scale).astype(np.float16)).cuda())
+        torch.cuda.synchronize()
+        return tr.gradients.float().cpu().numpy().copy()
+
+    full = grad(0, n, 0.5)  # the same 1/2 scale, so the halves' rounding of dL/doutput is the full batch's
+    p0, p1 = grad(0, n // 2, 0.5), grad(n // 2, n, 0.5)
+    tol = 2.0 ** -11 * (np.abs(p0) + np.abs(p1) + np.abs(full)) * 1.01 + 2.0 ** -24
+    bad = np.abs((p0 + p1) - full) > tol
+    assert not bad.any(), (int(bad.sum()), float(np.abs(p0 + p1 - full).max()))

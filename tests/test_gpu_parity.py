@@ -230,6 +230,39 @@ def test_network_with_input_encoding(pkg, orc, D, hidden):
     assert np.abs(gg[nm:] - gref).max() <= 2e-2 * np.abs(gref).max() + 1e-4
 
 
+@pytest.mark.parametrize("D,L,F,width,hidden", [(2, 4, 2, 16, 2), (3, 16, 2, 32, 2), (2, 16, 2, 16, 1), (3, 4, 4, 32, 3),
+                                                 (3, 8, 2, 16, 3)])
+def test_fully_fused_mlp_widths(pkg, orc, D, L, F, width, hidden):
+    """tcnn FullyFusedMLP widths 16 and 32 (BASELINE C1: 2D L=4 F=2 T=2^14 with a 2x16 MLP): forward and
+    the parameter / encoding gradients against the oracle, same bars as the 64-wide network."""
+    enc = enc_cfg(L, F, 14)
+    mlp = dict(MLP2, n_neurons=width, n_hidden_layers=hidden)
+    net = pkg.NetworkWithInputEncoding(D, 3, enc, mlp)
+    tr = pkg.Trainer(net, ADAM)
+    p16 = random_params(tr, net, net.n_matrix_params, grid_scale=0.5)
+    n = 2345
+    x = np.random.default_rng(D + width).random((n, D), dtype=np.float32)
+    g = orc.make_grid(D, L, F, 14)
+    ew = -(-L * F // 16) * 16
+    mm = orc.make_mlp(ew, width, hidden, 16)
+    nm = orc.mlp_n_params(mm)
+    assert nm == net.n_matrix_params == width * ew + (hidden - 1) * width * width + 16 * width
+    e = np.zeros((n, ew), np.float32)
+    e[:, :L * F] = orc.f16_bits_to_f32(orc.f32_to_f16_bits(orc.grid_forward(g, x, p16[nm:])))
+    ref = orc.mlp_forward(mm, p16[:nm], e)
+    got = net.inference(torch.from_numpy(x).cuda(), use_inference_params=False).float().cpu().numpy()
+    assert np.abs(got - ref).max() <= 1e-2 * np.abs(ref).max()
+    dy = np.zeros((n, 16), np.float16)
+    dy[:, :3] = np.random.default_rng(7).uniform(-1, 1, (n, 3))
+    net.forward_backward(torch.from_numpy(x).cuda(), torch.from_numpy(dy).cuda())
+    torch.cuda.synchronize()
+    dW, dx = orc.mlp_backward(mm, p16[:nm], e, dy.astype(np.float32))
+    gg = tr.gradients.float().cpu().numpy()
+    assert np.abs(gg[:nm] - dW).max() <= 2e-2 * np.abs(dW).max()
+    gref = orc.grid_backward(g, x, dx[:, :L * F])
+    assert np.abs(gg[nm:] - gref).max() <= 2e-2 * np.abs(gref).max() + 1e-4
+
+
 def test_optimizer_matches_oracle(pkg, orc, nerf_setup):
     net, tr, p16, m = nerf_setup
     cfg = orc.AdamCfg(1e-2, 0.9, 0.99, 1e-15, 1e-6, 0.95, 20000, 10000, 0.33)

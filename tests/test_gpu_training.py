@@ -91,6 +91,31 @@ def test_image_training_converges(pkg):
     assert tr.step == 60
 
 
+def test_image_c1_albert(pkg, orc):
+    """BASELINE configs[0] on the GPU: albert.exr (staged by tools/stage_image.sh) through the EXR reader,
+    the 2D L=4 F=2 T=2^14 grid and a 2x16 FullyFusedMLP; the first batch's positions and targets match the
+    oracle, and training converges."""
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "image", "albert.exr")
+    if not os.path.exists(path):
+        pytest.skip("albert.exr not staged")
+    img = pkg.image.Image.load(path)
+    tex = pkg.exr.read_exr(path)
+    assert (img.width, img.height) == (1024, 1024)
+    net = pkg.NetworkWithInputEncoding(2, 3, enc(2, 4, 2, 14), dict(MLP, n_neurons=16, n_hidden_layers=2))
+    assert net.n_matrix_params == 16 * 16 * 3  # SURVEY §8 C1: 768 MLP params
+    tr = pkg.Trainer(net, ADAM)
+    it = pkg.image.ImageTraining(net, tr, img, batch_size=1 << 16)
+    pos, tgt = it.generate_training_samples(4096)
+    r = orc.Rng(1337)
+    rpos, rtgt = orc.image_samples(4096, r, tex)
+    assert np.array_equal(pos.cpu().numpy(), rpos)
+    np.testing.assert_allclose(tgt.cpu().numpy(), rtgt, rtol=2e-6, atol=2e-7)
+    losses = [it.train_step() for _ in range(150)]
+    assert all(np.isfinite(losses))
+    assert np.mean(losses[-10:]) < 0.5 * np.mean(losses[:3]), losses[::15]
+
+
 def test_sdf_samples_match_oracle(pkg, orc):
     verts = pkg.synthetic.icosphere(2, radius=0.3, bumps=0.3)
     tris, amin, amax, brad = pkg.sdf.load_mesh(verts)
