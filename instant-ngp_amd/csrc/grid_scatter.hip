@@ -86,6 +86,24 @@ __device__ __forceinline__ void block_exclusive_scan(const uint32_t* cnt, uint32
 	if (threadIdx.x == 0) off[n] = carry;
 }
 
+// Rank of this lane's item within bucket j of the block histogram lh. Levels with few buckets (the
+// coarse dense ones: 2 and 16 buckets at C2) would send most of a wave's LDS atomics to one address, so
+// there the lanes with the same bucket are found with ballots and their leader adds their count once.
+__device__ __forceinline__ uint32_t bucket_rank(uint32_t* lh, uint32_t j, uint32_t few_bits) {
+	if (few_bits > 4) return atomicAdd(&lh[j], 1u);
+	uint64_t peers = __ballot(1);
+	for (uint32_t b = 0; b < few_bits; ++b) {
+		const uint64_t m = __ballot((j >> b) & 1u);
+		peers &= ((j >> b) & 1u) ? m : ~m;
+	}
+	const uint32_t lane = __lane_id();
+	const uint32_t leader = __ffsll((unsigned long long)peers) - 1;
+	uint32_t base = 0;
+	if (lane == leader) base = atomicAdd(&lh[j], (uint32_t)__popcll(peers));
+	base = __shfl(base, leader);
+	return base + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+}
+
 template <uint32_t D>
 __device__ __forceinline__ void load_pos(const GridBwdArgs& a, uint32_t i, float* x) {
 #pragma unroll
@@ -185,14 +203,32 @@ __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __r
 
 template <uint32_t D, uint32_t F>
 __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const Levels lv, const GridBwdArgs a, uint32_t B,
-                                                      uint32_t n_vb, const uint32_t* __restrict__ cur_t, const uint32_t* __restrict__ lo_vb,
-                                                      uint16_t* __restrict__ item_idx, f16* __restrict__ item_val, uint32_t debug) {
+                                                      uint32_t n_vb, uint32_t n_chunks, uint32_t xcd_map, const uint32_t* __restrict__ cur_t,
+                                                      const uint32_t* __restrict__ lo_vb, uint16_t* __restrict__ item_idx,
+                                                      f16* __restrict__ item_val, uint32_t debug) {
 	typedef typename ValVec<F>::T V;
 	constexpr uint32_t NC = 1u << D;
 	constexpr uint32_t NIT = SC_CHUNK * NC;  // items per block
 	extern __shared__ uint32_t lds[];
 	__shared__ uint32_t wsum[SC_ST / 64];
-	const uint32_t chunk = blockIdx.x, l = blockIdx.y;
+	// XCD-aware order: blocks b and b + 8 share an XCD (round-robin dispatch), so the L level blocks of a
+	// chunk run back to back on one XCD and its positions and dL/dy rows leave HBM once, not L times
+	uint32_t chunk, l;
+	if (xcd_map == 1) {
+		const uint32_t slot = blockIdx.x >> 3;
+		l = slot % c.n_levels;
+		chunk = (slot / c.n_levels) * 8 + (blockIdx.x & 7);
+	} else if (xcd_map == 2) {
+		// and each XCD owns a contiguous range of chunks: neighbouring runs of a bucket meet in one L2
+		const uint32_t slot = blockIdx.x >> 3, cpx = (n_chunks + 7) >> 3;
+		l = slot % c.n_levels;
+		chunk = (blockIdx.x & 7) * cpx + slot / c.n_levels;
+		if (slot / c.n_levels >= cpx) return;
+	} else {
+		chunk = blockIdx.x % n_chunks;
+		l = blockIdx.x / n_chunks;
+	}
+	if (chunk >= n_chunks) return;
 	const uint32_t nvb = lv.vb_base[l + 1] - lv.vb_base[l];
 	uint32_t* cur = lds;                                   // [nvb] this block's global cursor per bucket
 	uint32_t* lh = cur + nvb;                              // [nvb] counts
@@ -209,6 +245,7 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 	__syncthreads();
 	const uint32_t off_l = c.offsets[l];
 	const uint32_t mask = (1u << B) - 1u;
+	const uint32_t few_bits = nvb <= 1 ? 0u : nvb <= 2 ? 1u : nvb <= 4 ? 2u : nvb <= 8 ? 3u : nvb <= 16 ? 4u : 32u;
 	uint32_t e[SC_SSPT][NC], r[SC_SSPT][NC];
 	V val[SC_SSPT][NC];
 	uint32_t n_have = 0;
@@ -239,7 +276,7 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 #pragma unroll
 		for (uint32_t k = 0; k < NC; ++k) {
 			e[q][k] = corner_index<D>(c, l, base, k) - off_l;
-			r[q][k] = atomicAdd(&lh[e[q][k] >> B], 1u);
+			r[q][k] = bucket_rank(lh, e[q][k] >> B, few_bits);
 			const float w = corner_weight<D>(frac, k);
 			if constexpr (F == 1) val[q][k] = to_f16(w * g[0]);
 			else {
@@ -467,10 +504,11 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 	f16* val = (f16*)(ws + p.off_val);
 	const uint32_t NIT = SC_CHUNK * (1u << D);
 	const size_t lds_s = (size_t)(3 * p.max_lb + 1) * 4 + (size_t)NIT * 4 + 16 + (size_t)NIT * F * 2;
-	const dim3 grid_s(p.n_chunks, c.n_levels);
+	const uint32_t xcd_map = p.xcd_map;
+	const dim3 grid_s(xcd_map ? (uint32_t)div_round_up(p.n_chunks, 8) * 8 * c.n_levels : p.n_chunks * c.n_levels);
 	auto go = [&](auto scatter, auto accum, auto splitr) {
 		ensure_dynamic_lds((const void*)scatter, lds_s);
-		if (!(debug & 4)) scatter<<<grid_s, SC_ST, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, cur_t, lo, idx, val, debug);
+		if (!(debug & 4)) scatter<<<grid_s, SC_ST, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, p.n_chunks, xcd_map, cur_t, lo, idx, val, debug);
 		NGP_HIP(hipGetLastError());
 		ensure_dynamic_lds((const void*)accum, SC_LDS_BYTES);
 		accum<<<p.max_split_blocks + p.n_buckets, SC_BT, SC_LDS_BYTES, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
@@ -512,6 +550,8 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	if (const char* e = getenv("NGP_SC_LIMIT")) p.split_limit = (uint32_t)atoi(e);
 	p.max_split_blocks = (uint32_t)(div_round_up(p.n_items, (uint64_t)p.part) + div_round_up(p.n_items, (uint64_t)p.split_limit) + 1);
 	p.max_split_buckets = (uint32_t)(div_round_up(p.n_items, (uint64_t)p.split_limit) + 1);
+	p.xcd_map = 2;
+	if (const char* e = getenv("NGP_SC_XCD")) p.xcd_map = (uint32_t)atoi(e);
 	const uint64_t len = (uint64_t)p.n_buckets * p.n_chunks;
 	NGP_CHECK(len < (1ull << 31), "grid backward: bucket histogram too large");
 	auto align = [](size_t v) { return (v + 255) / 256 * 256; };

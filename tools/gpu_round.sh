@@ -27,6 +27,7 @@ if has prof; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- \
       python3 bench.py --no-cpu-baseline --e2e-seconds 0 ${PMC_ARGS} > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
   find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
+  rm -rf "$OUT/prof"
   head -12 "$OUT/kernel_stats.csv"
 fi
 if has pmc; then
@@ -38,6 +39,7 @@ if has pmc; then
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $c -f csv -d "$OUT/pmc_$i" -o run -- $BENCH_PMC > "$OUT/pmc_$i.json" 2> "$OUT/pmc_$i.err"
     find "$OUT/pmc_$i" -name '*counter_collection.csv' -exec cp {} "$OUT/counters_$i.csv" \;
+    rm -rf "$OUT/pmc_$i"
   done
   python3 tools/pmc_summary.py "$OUT"/counters_[0-9].csv > "$OUT/pmc_summary.json"
   python3 -c "import json; d=json.load(open('$OUT/pmc_summary.json')); [print(k[:60], {a: round(b, 4) if isinstance(b, float) else b for a, b in v.items()}) for k, v in d.items()]"
@@ -45,7 +47,8 @@ fi
 if has pmcx; then
   # extra counters for one pass, e.g. PMCX="TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"
   timeout -k 10 300 rocprofv3 --pmc ${PMCX} -f csv -d "$OUT/pmcx" -o run -- \
-      python3 bench.py --no-cpu-baseline --graph 0 --steps 5 --warmup 2 > "$OUT/pmcx.json" 2> "$OUT/pmcx.err"
+      python3 bench.py --no-cpu-baseline --e2e-seconds 0 --no-c2p --graph 0 --steps 5 --warmup 2 ${PMC_ARGS} > "$OUT/pmcx.json" 2> "$OUT/pmcx.err"
   find "$OUT/pmcx" -name '*counter_collection.csv' -exec cp {} "$OUT/counters_x.csv" \;
+  rm -rf "$OUT/pmcx"
   python3 tools/pmc_table.py "$OUT/counters_x.csv" | tee "$OUT/pmcx_table.txt"
 fi
