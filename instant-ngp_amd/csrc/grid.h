@@ -51,7 +51,7 @@ struct GridBwdArgs {
 
 // Optional by-product of the training forward: the bucket histogram of the sorted backward
 // (grid_scatter.hip k_sc_hist), counted from the corner indices the forward computes anyway.
-// hist[(vb_base[l] + bucket) * n_chunks + chunk]; one forward block = one chunk of `chunk` samples.
+// hist[chunk * vb_base[L] + vb_base[l] + bucket]; one forward block = one chunk of `chunk` samples.
 struct GridHist {
 	uint32_t* hist;
 	uint32_t B, n_chunks, chunk;

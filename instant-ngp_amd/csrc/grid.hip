@@ -188,7 +188,7 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 	}
 	if constexpr (HIST) {
 		__syncthreads();
-		for (uint32_t j = threadIdx.x; j < h.vb_base[c.n_levels]; j += blockDim.x) h.hist[(size_t)j * h.n_chunks + blockIdx.x] = hl[j];
+		for (uint32_t j = threadIdx.x; j < h.vb_base[c.n_levels]; j += blockDim.x) h.hist[(size_t)blockIdx.x * h.vb_base[c.n_levels] + j] = hl[j];
 	}
 }
 
@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(256) k_grid_forward_xcd(const GridConst c, con
 	}
 	if constexpr (HIST) {
 		__syncthreads();
-		for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) h.hist[(size_t)(h.vb_base[l] + j) * h.n_chunks + chunk] = hl[j];
+		for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) h.hist[(size_t)chunk * h.vb_base[c.n_levels] + h.vb_base[l] + j] = hl[j];
 	}
 }
 

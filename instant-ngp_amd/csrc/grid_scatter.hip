@@ -13,9 +13,11 @@
 //
 // Work is cut into (chunk of samples, level) blocks so no block walks the levels serially:
 //   prepare (positions only)
-//     k_sc_hist       per (chunk, level): LDS histogram over the level's buckets -> hist[bucket][chunk]
+//     k_sc_hist       per (chunk, level): LDS histogram over the level's buckets -> hist[chunk][bucket]
+//                     (one contiguous row segment per block)
 //     k_sc_scan       per bucket: exclusive scan over its chunks -> cursor within the bucket
-//                     cur[chunk][bucket] and the bucket total tot[bucket]. Every sample emits 2^D
+//                     cur[chunk][bucket] and the bucket total tot[bucket] (lanes = consecutive buckets,
+//                     so every hist read and cur write is a coalesced row segment). Every sample emits 2^D
 //                     items per level, so level l starts at item n * 2^D * l.
 //     k_sc_plan       bucket starts, and the parts list of oversized buckets
 //   backward
@@ -135,29 +137,60 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 		for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&h[(corner_index<D>(c, l, base, k) - off_l) >> B], 1u);
 	}
 	__syncthreads();
-	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) hist[(size_t)(lv.vb_base[l] + j) * n_chunks + chunk] = h[j];
+	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) hist[(size_t)chunk * lv.vb_base[c.n_levels] + lv.vb_base[l] + j] = h[j];
 }
 
-// per bucket: exclusive scan of hist[bucket][0..n_chunks) -> cur[chunk][bucket]; tot[bucket] = total.
-__global__ void __launch_bounds__(SC_THREADS) k_sc_scan(const uint32_t* __restrict__ hist, uint32_t n_chunks, uint32_t n_vb,
-                                                        uint32_t* __restrict__ cur, uint32_t* __restrict__ tot) {
-	__shared__ uint32_t wsum[SC_THREADS / 64];
-	const uint32_t vb = blockIdx.x;
-	const uint32_t* h = hist + (size_t)vb * n_chunks;
-	uint32_t carry = 0;
-	for (uint32_t b0 = 0; b0 < n_chunks; b0 += SC_THREADS) {
-		const uint32_t b = b0 + threadIdx.x;
-		const uint32_t v = b < n_chunks ? h[b] : 0u;
-		const uint32_t incl = wave_inclusive_scan(v);
-		if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
-		__syncthreads();
-		uint32_t pre = carry;
-		for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) pre += wsum[w];
-		if (b < n_chunks) cur[(size_t)b * n_vb + vb] = pre + incl - v;
-		carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
-		__syncthreads();
+// per bucket: exclusive scan of hist[0..n_chunks)[bucket] -> cur[chunk][bucket]; tot[bucket] = total.
+// Block = 64 consecutive buckets (lanes) x SCAN_SEG chunk segments (waves): each wave sums its segment's
+// counts, the segment offsets come through LDS, then the wave re-reads its segment (L2) and writes the
+// cursors. Reads and writes are 256-B row segments.
+constexpr uint32_t SCAN_SEG = 16;
+__global__ void __launch_bounds__(64 * SCAN_SEG) k_sc_scan(const uint32_t* __restrict__ hist, uint32_t n_chunks, uint32_t n_vb,
+                                                         uint32_t* __restrict__ cur, uint32_t* __restrict__ tot) {
+	__shared__ uint32_t seg_sum[SCAN_SEG][64];
+	const uint32_t lane = threadIdx.x & 63, seg = threadIdx.x >> 6;
+	const uint32_t vb = blockIdx.x * 64 + lane;
+	const uint32_t per = (n_chunks + SCAN_SEG - 1) / SCAN_SEG;
+	const uint32_t c0 = min(seg * per, n_chunks), c1 = min(c0 + per, n_chunks);
+	constexpr uint32_t U = 8;
+	uint32_t sum = 0;
+	if (vb < n_vb) {
+		uint32_t c = c0;
+		for (; c + U <= c1; c += U) {
+			uint32_t v[U];
+#pragma unroll
+			for (uint32_t u = 0; u < U; ++u) v[u] = hist[(size_t)(c + u) * n_vb + vb];
+#pragma unroll
+			for (uint32_t u = 0; u < U; ++u) sum += v[u];
+		}
+		for (; c < c1; ++c) sum += hist[(size_t)c * n_vb + vb];
 	}
-	if (threadIdx.x == 0) tot[vb] = carry;
+	seg_sum[seg][lane] = sum;
+	__syncthreads();
+	uint32_t run = 0, total = 0;
+	for (uint32_t q = 0; q < SCAN_SEG; ++q) {
+		const uint32_t v = seg_sum[q][lane];
+		if (q < seg) run += v;
+		total += v;
+	}
+	if (vb >= n_vb) return;
+	uint32_t c = c0;
+	for (; c + U <= c1; c += U) {
+		uint32_t v[U];
+#pragma unroll
+		for (uint32_t u = 0; u < U; ++u) v[u] = hist[(size_t)(c + u) * n_vb + vb];
+#pragma unroll
+		for (uint32_t u = 0; u < U; ++u) {
+			cur[(size_t)(c + u) * n_vb + vb] = run;
+			run += v[u];
+		}
+	}
+	for (; c < c1; ++c) {
+		const uint32_t v = hist[(size_t)c * n_vb + vb];
+		cur[(size_t)c * n_vb + vb] = run;
+		run += v;
+	}
+	if (seg == 0) tot[vb] = total;
 }
 
 // One block: bucket starts lo[vb] (exclusive scan of tot over all buckets — levels are consecutive
@@ -590,7 +623,7 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const Scatter
 		else k_sc_hist<2><<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
 		NGP_HIP(hipGetLastError());
 	}
-	k_sc_scan<<<p.n_buckets, SC_THREADS, 0, s>>>(hist, p.n_chunks, p.n_buckets, (uint32_t*)(ws + p.off_cur), (uint32_t*)(ws + p.off_tot));
+	k_sc_scan<<<div_round_up(p.n_buckets, 64), 64 * SCAN_SEG, 0, s>>>(hist, p.n_chunks, p.n_buckets, (uint32_t*)(ws + p.off_cur), (uint32_t*)(ws + p.off_tot));
 	NGP_HIP(hipGetLastError());
 	k_sc_plan<<<1, SC_PLAN_THREADS, 0, s>>>((const uint32_t*)(ws + p.off_tot), p.n_buckets, p.split_limit, p.part,
 	                                        (uint32_t*)(ws + p.off_lo), (uint32_t*)(ws + p.off_split), (uint32_t*)(ws + p.off_splitb));

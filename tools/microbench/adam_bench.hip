@@ -6,6 +6,7 @@
 //   v2  v1 with 8 params / thread (two 4-groups interleaved: twice the loads in flight)
 //   v3  v1 with nontemporal loads and stores on the streamed state
 //   v4  v2 with nontemporal loads and stores
+//   v5  v0 with m1, m2, steps, ema32 interleaved per 4-group (one 64-B record: 5 streams instead of 9)
 // Prints one JSON line per (config, variant): avg/best ms and algorithmic GB/s (46 B per updated
 // parameter, 16 B per skipped one). Also checks every variant leaves bit-identical state.
 // Build: hipcc --offload-arch=gfx950 -O3 -o adam_bench adam_bench.hip
@@ -26,7 +27,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct Cfg { float lr, beta1, beta2, eps, l2, ema_decay; };
-struct St { float* w32; f16* w16; const f16* g16; float* m1; float* m2; uint32_t* steps; float* ema32; f16* ema16; };
+struct St { float* w32; f16* w16; const f16* g16; float* m1; float* m2; uint32_t* steps; float* ema32; f16* ema16; f32x4* rec; };
 
 template <bool NT, typename T> __device__ __forceinline__ T ld(const T* p) {
 	if constexpr (NT) return __builtin_nontemporal_load(p); else return *p;
@@ -124,6 +125,57 @@ __global__ void __launch_bounds__(256) v2(uint32_t n4, uint32_t n_matrix, float 
 	if (vb) group<NT>(s, c, ib, n_matrix, ls, step, gb, wb, eb);
 }
 
+// interleaved state: rec[4t + 0..3] = m1, m2, steps (as bits), ema32 of group t
+__global__ void __launch_bounds__(256) v5(uint32_t n4, uint32_t n_matrix, float ls, Cfg c, St s, uint32_t step) {
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= n4) return;
+	const uint32_t i0 = 4 * t;
+	const f16x4 gh = *(const f16x4*)(s.g16 + i0);
+	float g[4];
+	bool act[4], any = false;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		g[k] = (float)gh[k] / ls;
+		act[k] = !(i0 + k >= n_matrix && g[k] == 0.f);
+		any |= act[k];
+	}
+	f32x4 w = *(const f32x4*)(s.w32 + i0);
+	f32x4* r = s.rec + 4 * (size_t)t;
+	f32x4 e = r[3];
+	if (any) {
+		f32x4 m1 = r[0], m2 = r[1];
+		u32x4 sp = __builtin_bit_cast(u32x4, r[2]);
+		f16x4 wh;
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			if (act[k]) {
+				float gk = g[k];
+				if (i0 + k < n_matrix) gk += c.l2 * w[k];
+				const float mm = c.beta1 * m1[k] + (1.f - c.beta1) * gk;
+				const float vv = c.beta2 * m2[k] + (1.f - c.beta2) * (gk * gk);
+				m1[k] = mm; m2[k] = vv;
+				const uint32_t sk = sp[k] + 1;
+				sp[k] = sk;
+				const float lr_s = c.lr * sqrtf(1.f - powf(c.beta2, (float)sk)) / (1.f - powf(c.beta1, (float)sk));
+				w[k] = w[k] - lr_s / (sqrtf(vv) + c.eps) * mm;
+			}
+			wh[k] = (f16)w[k];
+		}
+		r[0] = m1; r[1] = m2; r[2] = __builtin_bit_cast(f32x4, sp);
+		*(f32x4*)(s.w32 + i0) = w;
+		*(f16x4*)(s.w16 + i0) = wh;
+	}
+	const float debias = 1.f - powf(c.ema_decay, (float)(step + 1));
+	f16x4 eh;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		e[k] = c.ema_decay * e[k] + (1.f - c.ema_decay) * w[k];
+		eh[k] = (f16)(e[k] / debias);
+	}
+	r[3] = e;
+	*(f16x4*)(s.ema16 + i0) = eh;
+}
+
 int main() {
 	struct Conf { const char* name; uint32_t n, n_matrix; double p_active; } confs[] = {
 		{"C5", 105462784u, 7168u, 0.28}, {"C2", 3302400u, 9216u, 0.96}};
@@ -146,6 +198,7 @@ int main() {
 		CHECK(hipMalloc(&s.w32, (size_t)n * 4)); CHECK(hipMalloc(&s.w16, (size_t)n * 2)); CHECK(hipMalloc((void**)&s.g16, (size_t)n * 2));
 		CHECK(hipMalloc(&s.m1, (size_t)n * 4)); CHECK(hipMalloc(&s.m2, (size_t)n * 4)); CHECK(hipMalloc(&s.steps, (size_t)n * 4));
 		CHECK(hipMalloc(&s.ema32, (size_t)n * 4)); CHECK(hipMalloc(&s.ema16, (size_t)n * 2));
+		CHECK(hipMalloc(&s.rec, (size_t)n * 16));
 		CHECK(hipMemcpy((void*)s.g16, g.data(), (size_t)n * 2, hipMemcpyHostToDevice));
 		void* flush;
 		const size_t flush_bytes = (size_t)512 << 20;
@@ -154,6 +207,8 @@ int main() {
 			CHECK(hipMemcpy(s.w32, w0.data(), (size_t)n * 4, hipMemcpyHostToDevice));
 			CHECK(hipMemcpy(s.ema32, w0.data(), (size_t)n * 4, hipMemcpyHostToDevice));
 			CHECK(hipMemset(s.m1, 0, (size_t)n * 4)); CHECK(hipMemset(s.m2, 0, (size_t)n * 4)); CHECK(hipMemset(s.steps, 0, (size_t)n * 4));
+			CHECK(hipMemset(s.rec, 0, (size_t)n * 16));
+			CHECK(hipMemcpy2D((char*)s.rec + 48, 64, w0.data(), 16, 16, n / 4, hipMemcpyHostToDevice));
 		};
 		const Cfg c{1e-2f, 0.9f, 0.99f, 1e-15f, 1e-6f, 0.95f};
 		const uint32_t n4 = n / 4;
@@ -161,6 +216,7 @@ int main() {
 		hipEvent_t e0, e1;
 		CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
 		std::vector<float> ref;
+		bool interleaved = false;
 		auto run = [&](const char* name, auto launch) {
 			reset();
 			CHECK(hipDeviceSynchronize());
@@ -177,7 +233,8 @@ int main() {
 				if (r >= 2) { tot += ms; best = ms < best ? ms : best; }
 			}
 			std::vector<float> out(n);
-			CHECK(hipMemcpy(out.data(), s.ema32, (size_t)n * 4, hipMemcpyDeviceToHost));
+			if (interleaved) CHECK(hipMemcpy2D(out.data(), 16, (char*)s.rec + 48, 64, 16, n / 4, hipMemcpyDeviceToHost));
+			else CHECK(hipMemcpy(out.data(), s.ema32, (size_t)n * 4, hipMemcpyDeviceToHost));
 			bool same = true;
 			if (ref.empty()) ref = out; else same = memcmp(ref.data(), out.data(), (size_t)n * 4) == 0;
 			printf("{\"config\": \"%s\", \"variant\": \"%s\", \"n\": %u, \"updated\": %llu, \"avg_ms\": %.4f, \"best_ms\": %.4f, "
@@ -191,8 +248,12 @@ int main() {
 		run("v2", [&](int r) { v2<false><<<(n4 + 511) / 512, 256>>>(n4, cf.n_matrix, ls, c, s, r); });
 		run("v3", [&](int r) { v1<true><<<(n4 + 255) / 256, 256>>>(n4, cf.n_matrix, ls, c, s, r); });
 		run("v4", [&](int r) { v2<true><<<(n4 + 511) / 512, 256>>>(n4, cf.n_matrix, ls, c, s, r); });
+		interleaved = true;
+		run("v5", [&](int r) { v5<<<(n4 + 255) / 256, 256>>>(n4, cf.n_matrix, ls, c, s, r); });
+		interleaved = false;
+		run("v0", [&](int r) { v0<<<(n4 + 255) / 256, 256>>>(n4, cf.n_matrix, ls, c, s, r); });
 		CHECK(hipFree(s.w32)); CHECK(hipFree(s.w16)); CHECK(hipFree((void*)s.g16)); CHECK(hipFree(s.m1)); CHECK(hipFree(s.m2));
-		CHECK(hipFree(s.steps)); CHECK(hipFree(s.ema32)); CHECK(hipFree(s.ema16)); CHECK(hipFree(flush));
+		CHECK(hipFree(s.steps)); CHECK(hipFree(s.ema32)); CHECK(hipFree(s.ema16)); CHECK(hipFree(s.rec)); CHECK(hipFree(flush));
 	}
 	return 0;
 }
