@@ -78,7 +78,7 @@ REGION_KERNELS = {
     "grid_forward": ["k_grid_forward"],
     "grid_backward": ["k_grid_backward"],
     "grid_backward_total": ["k_sc_scan", "k_sc_plan", "k_sc_scatter", "k_sc_accumulate", "k_sc_split_reduce"],
-    "mlp_train": ["k_nerf_mlp<1,", "k_mlp<1,"],
+    "mlp_train": ["k_nerf_mlp_train<", "k_nerf_mlp<1,", "k_mlp<1,"],
     "mlp_infer": ["k_nerf_mlp<0,", "k_mlp<0,"],
     "optimizer": ["k_adam_ema"],
 }
@@ -107,6 +107,19 @@ def pmc_traffic(variant, region):
             tot += v["fabric_bytes"]
             hit = True
     return (tot if hit else None), os.path.relpath(files[-1], ROOT)
+
+
+def pmc_mfma_util(variant, region):
+    """MFMA utilisation of `region`'s kernels (rocprofv3 MfmaUtil = SQ_VALU_MFMA_BUSY_CYCLES over the
+    SIMD-cycles of the dispatch) from the newest committed PMC summary; None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{variant.lower()}.json")))
+    if not files or region not in REGION_KERNELS:
+        return None
+    summ = json.load(open(files[-1]))
+    vals = [v["mfma_util"] for name, v in summ.items()
+            if any(k.replace(" ", "") in name.replace(" ", "") for k in REGION_KERNELS[region]) and v.get("mfma_util")]
+    return round(max(vals), 4) if vals else None
 
 
 def host_cores():
@@ -282,6 +295,10 @@ def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped):
                 # its bytes do not all come from HBM, so an HBM fraction would overstate it (C2: >1)
                 e.update({"bound": "infinity_cache", "frac": None,
                           "note": "working set < 256 MiB, served on-die; no HBM fraction (HBM spec is not its ceiling)"})
+        if k in ("mlp_train", "mlp_infer"):
+            u = pmc_mfma_util(variant, k)
+            if u is not None:
+                e["mfma_util_pmc"] = u
         summary[k] = e
     cands = [k for k in roof if k in per and not (k == "grid_backward" and "grid_backward_total" in per)
              and summary[k].get("bound") != "infinity_cache"]

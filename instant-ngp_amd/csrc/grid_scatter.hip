@@ -37,15 +37,11 @@ namespace {
 
 constexpr uint32_t SC_THREADS = 256;
 constexpr uint32_t SC_BT = 1024;             // bucket/split blocks: 2 per CU by LDS, 32 waves to hide latency
-#ifndef SC_CHUNK_SAMPLES
-#define SC_CHUNK_SAMPLES 512
-#endif
-#ifndef SC_SCATTER_THREADS
-#define SC_SCATTER_THREADS 512
-#endif
-constexpr uint32_t SC_CHUNK = SC_CHUNK_SAMPLES;     // samples per (chunk, level) block
-constexpr uint32_t SC_ST = SC_SCATTER_THREADS;      // scatter block: 16 waves per CU at 2 blocks
-constexpr uint32_t SC_SSPT = SC_CHUNK / SC_ST;      // samples per scatter thread
+// (chunk, level) blocks: 512 samples with 512 threads where a chunk fills each bucket with long runs
+// (C2: ~40 items per bucket and chunk); sparse tables (C5: T=2^22, ~3.6 items per bucket in a
+// 512-sample chunk) take 1024-sample chunks with 1024 threads, whose runs are twice as long and whose
+// per-(chunk, bucket) histogram and cursor arrays are half the size (C5 backward 385 -> 355 us;
+// 2048-sample chunks measured slower, 372 us).
 constexpr size_t SC_LDS_BYTES = 64 * 1024;   // one bucket's int64 accumulators
 constexpr float FIX_SCALE = 16777216.0f;     // 2^24: fp16 values are integer multiples of 2^-24
 
@@ -116,7 +112,7 @@ struct Levels {
 	uint32_t vb_base[33];  // first bucket of each level; vb_base[L] = number of buckets
 };
 
-template <uint32_t D>
+template <uint32_t D, uint32_t CHUNK>
 __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const Levels lv, const GridBwdArgs a, uint32_t B,
                                                         uint32_t n_chunks, uint32_t* __restrict__ hist) {
 	extern __shared__ uint32_t h[];
@@ -126,8 +122,8 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 	__syncthreads();
 	const uint32_t off_l = c.offsets[l];
 #pragma unroll
-	for (uint32_t q = 0; q < SC_CHUNK / SC_THREADS; ++q) {
-		const uint32_t i = chunk * SC_CHUNK + q * SC_THREADS + threadIdx.x;
+	for (uint32_t q = 0; q < CHUNK / SC_THREADS; ++q) {
+		const uint32_t i = chunk * CHUNK + q * SC_THREADS + threadIdx.x;
 		if (i >= a.n) continue;
 		float x[D];
 		load_pos<D>(a, i, x);
@@ -234,7 +230,7 @@ __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __r
 	if (threadIdx.x == 0) { split[0] = c_parts; split[1] = c_sb; }
 }
 
-template <uint32_t D, uint32_t F>
+template <uint32_t D, uint32_t F, uint32_t SC_CHUNK, uint32_t SC_ST>
 __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const Levels lv, const GridBwdArgs a, uint32_t B,
                                                       uint32_t n_vb, uint32_t n_chunks, uint32_t xcd_map, const uint32_t* __restrict__ cur_t,
                                                       const uint32_t* __restrict__ lo_vb, uint16_t* __restrict__ item_idx,
@@ -242,6 +238,7 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 	typedef typename ValVec<F>::T V;
 	constexpr uint32_t NC = 1u << D;
 	constexpr uint32_t NIT = SC_CHUNK * NC;  // items per block
+	constexpr uint32_t SC_SSPT = SC_CHUNK / SC_ST;  // samples per thread
 	extern __shared__ uint32_t lds[];
 	__shared__ uint32_t wsum[SC_ST / 64];
 	// XCD-aware order: blocks b and b + 8 share an XCD (round-robin dispatch), so the L level blocks of a
@@ -513,6 +510,13 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
 	}
 }
 
+// scatter block LDS: cursors, counts and offsets per bucket, then the staged items (bucket u16,
+// entry u16, F fp16 values)
+size_t scatter_lds_bytes(uint32_t max_lb, uint32_t chunk, uint32_t D, uint32_t F) {
+	const size_t nit = (size_t)chunk << D;
+	return (size_t)(3 * max_lb + 1) * 4 + nit * 4 + 16 + nit * F * 2;
+}
+
 Levels make_levels(const GridDesc& g, uint32_t B) {
 	Levels lv{};
 	uint32_t vb = 0;
@@ -535,13 +539,12 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 	unsigned long long* scratch = (unsigned long long*)(ws + p.off_scratch);
 	uint16_t* idx = (uint16_t*)(ws + p.off_idx);
 	f16* val = (f16*)(ws + p.off_val);
-	const uint32_t NIT = SC_CHUNK * (1u << D);
-	const size_t lds_s = (size_t)(3 * p.max_lb + 1) * 4 + (size_t)NIT * 4 + 16 + (size_t)NIT * F * 2;
+	const size_t lds_s = scatter_lds_bytes(p.max_lb, p.spb, D, F);
 	const uint32_t xcd_map = p.xcd_map;
 	const dim3 grid_s(xcd_map ? (uint32_t)div_round_up(p.n_chunks, 8) * 8 * c.n_levels : p.n_chunks * c.n_levels);
 	auto go = [&](auto scatter, auto accum, auto splitr) {
 		ensure_dynamic_lds((const void*)scatter, lds_s);
-		if (!(debug & 4)) scatter<<<grid_s, SC_ST, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, p.n_chunks, xcd_map, cur_t, lo, idx, val, debug);
+		if (!(debug & 4)) scatter<<<grid_s, p.spb == 512 ? 512 : 1024, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, p.n_chunks, xcd_map, cur_t, lo, idx, val, debug);
 		NGP_HIP(hipGetLastError());
 		ensure_dynamic_lds((const void*)accum, SC_LDS_BYTES);
 		accum<<<p.max_split_blocks + p.n_buckets, SC_BT, SC_LDS_BYTES, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
@@ -551,13 +554,19 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite);
 		NGP_HIP(hipGetLastError());
 	};
+	auto by_chunk = [&](auto sc512, auto sc1024, auto accum, auto splitr) {
+		if (p.spb == 512) go(sc512, accum, splitr);
+		else go(sc1024, accum, splitr);
+	};
+#define NGP_SC_F(FF) by_chunk(k_sc_scatter<D, FF, 512, 512>, k_sc_scatter<D, FF, 1024, 1024>, k_sc_accumulate<FF>, k_sc_split_reduce<FF>)
 	switch (F) {
-		case 1: go(k_sc_scatter<D, 1>, k_sc_accumulate<1>, k_sc_split_reduce<1>); break;
-		case 2: go(k_sc_scatter<D, 2>, k_sc_accumulate<2>, k_sc_split_reduce<2>); break;
-		case 4: go(k_sc_scatter<D, 4>, k_sc_accumulate<4>, k_sc_split_reduce<4>); break;
-		case 8: go(k_sc_scatter<D, 8>, k_sc_accumulate<8>, k_sc_split_reduce<8>); break;
+		case 1: NGP_SC_F(1); break;
+		case 2: NGP_SC_F(2); break;
+		case 4: NGP_SC_F(4); break;
+		case 8: NGP_SC_F(8); break;
 		default: throw Error("grid backward: unsupported F");
 	}
+#undef NGP_SC_F
 }
 
 }  // namespace
@@ -573,7 +582,14 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	p.max_lb = 0;
 	for (uint32_t l = 0; l < g.n_levels; ++l) p.max_lb = std::max(p.max_lb, lv.vb_base[l + 1] - lv.vb_base[l]);
 	NGP_CHECK((size_t)p.max_lb * 4 <= 32 * 1024, "grid backward: level too large for the bucket histogram");
-	p.spb = SC_CHUNK;
+	// samples per chunk: 1024 when 512-sample chunks would average fewer than 16 items per (chunk,
+	// bucket) and the scatter block's LDS allows it
+	const uint64_t items_per_sample = (uint64_t)g.n_levels << g.n_dims;
+	p.spb = 512;
+	if (512ull * items_per_sample < 16ull * p.n_buckets && scatter_lds_bytes(p.max_lb, 1024, g.n_dims, F) <= 160 * 1024) p.spb = 1024;
+	if (const char* e = getenv("NGP_SC_CHUNK")) p.spb = (uint32_t)atoi(e);
+	NGP_CHECK(p.spb == 512 || p.spb == 1024, "grid backward: chunk must be 512 or 1024 samples");
+	NGP_CHECK(scatter_lds_bytes(p.max_lb, p.spb, g.n_dims, F) <= 160 * 1024, "grid backward: scatter chunk exceeds LDS");
 	p.n_chunks = (uint32_t)div_round_up(n, p.spb);
 	p.n_items = (uint64_t)n * g.n_levels * (1u << g.n_dims);
 	NGP_CHECK(p.n_items < (1ull << 32), "grid backward: too many contributions for 32-bit offsets");
@@ -619,8 +635,12 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const Scatter
 		const Levels lv = make_levels(g, p.B);
 		const dim3 grid_h(p.n_chunks, g.n_levels);
 		const size_t lds_h = (size_t)p.max_lb * 4;
-		if (g.n_dims == 3) k_sc_hist<3><<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
-		else k_sc_hist<2><<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
+		auto go = [&](auto k3, auto k2) {
+			if (g.n_dims == 3) k3<<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
+			else k2<<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
+		};
+		if (p.spb == 512) go(k_sc_hist<3, 512>, k_sc_hist<2, 512>);
+		else go(k_sc_hist<3, 1024>, k_sc_hist<2, 1024>);
 		NGP_HIP(hipGetLastError());
 	}
 	k_sc_scan<<<div_round_up(p.n_buckets, 64), 64 * SCAN_SEG, 0, s>>>(hist, p.n_chunks, p.n_buckets, (uint32_t*)(ws + p.off_cur), (uint32_t*)(ws + p.off_tot));

@@ -139,13 +139,15 @@ def test_grid_backward_bitexact_accumulate(pkg, orc):
     np.testing.assert_array_equal(got, ref)
 
 
-def test_grid_backward_ragged_sizes(pkg, orc):
-    """Batch sizes that are not multiples of the 512-sample chunk, at the bucketed threshold."""
-    D, L, F, T = 3, 4, 4, 19
+@pytest.mark.parametrize("D,L,F,T", [(3, 4, 4, 19), (3, 16, 2, 22)])
+def test_grid_backward_ragged_sizes(pkg, orc, D, L, F, T):
+    """Batch sizes that are not multiples of the scatter chunk (512 samples at C2; 1024 at C5, whose
+    sparse 2^22 tables take the larger chunk), at the bucketed threshold."""
     grid = orc.make_grid(D, L, F, T)
     for n in (4096, 4097, 5000, 65535):
         x = positions("nerf", n, D, seed=n)
         dy = dy_batch(None, n, L, F, seed=n)
+        dy = np.concatenate([dy, np.zeros((n, encoding_width(L, F) - L * F), np.float16)], axis=1)
         _, _, got = run_backward(pkg, D, L, F, T, x, dy)
         ref = orc.grid_backward_exact(grid, x, dy)
         np.testing.assert_array_equal(got, ref, err_msg=f"n={n}")
