@@ -193,19 +193,29 @@ __global__ void __launch_bounds__(64 * SCAN_SEG) k_sc_scan(const uint32_t* __res
 // and each holds n * 2^D items), and the split list for buckets above split_limit: parts of `part`
 // items at split[2 + 3p ..] = {bucket, lo, hi} (split[0] = parts), split buckets at splitb[3b ..] =
 // {bucket, first part, parts} (split[1] = buckets). Everything downstream is then a static grid.
+// Thread t owns SC_PLAN_K consecutive buckets per round, all loaded up front (1 for C2's 402 buckets;
+// 32 for C5's ~18k, one round: one load latency instead of one per 1024 buckets).
 constexpr uint32_t SC_PLAN_THREADS = 1024;
+template <uint32_t SC_PLAN_K>
 __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __restrict__ tot, uint32_t n_vb, uint32_t split_limit,
                                                              uint32_t part, uint32_t* __restrict__ lo_out,
                                                              uint32_t* __restrict__ split, uint32_t* __restrict__ splitb) {
 	__shared__ uint32_t wsum[3][SC_PLAN_THREADS / 64];
 	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+	const uint32_t K = min(SC_PLAN_K, (n_vb + SC_PLAN_THREADS - 1) / SC_PLAN_THREADS);
 	uint32_t c_lo = 0, c_parts = 0, c_sb = 0;
-	for (uint32_t b0 = 0; b0 < n_vb; b0 += SC_PLAN_THREADS) {
-		const uint32_t vb = b0 + threadIdx.x;
-		const uint32_t t = vb < n_vb ? tot[vb] : 0u;
-		const uint32_t is_split = t > split_limit ? 1u : 0u;
-		const uint32_t parts = is_split ? (t + part - 1) / part : 0u;
-		const uint32_t i0 = wave_inclusive_scan(t), i1 = wave_inclusive_scan(parts), i2 = wave_inclusive_scan(is_split);
+	for (uint32_t b0 = 0; b0 < n_vb; b0 += SC_PLAN_THREADS * K) {
+		const uint32_t v0 = b0 + threadIdx.x * K;
+		uint32_t t[SC_PLAN_K];
+#pragma unroll
+		for (uint32_t k = 0; k < SC_PLAN_K; ++k) t[k] = (k < K && v0 + k < n_vb) ? tot[v0 + k] : 0u;
+		uint32_t s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+		for (uint32_t k = 0; k < SC_PLAN_K; ++k) {
+			const uint32_t sp = t[k] > split_limit ? 1u : 0u;
+			s0 += t[k]; s1 += sp ? (t[k] + part - 1) / part : 0u; s2 += sp;
+		}
+		const uint32_t i0 = wave_inclusive_scan(s0), i1 = wave_inclusive_scan(s1), i2 = wave_inclusive_scan(s2);
 		if (lane == 63) { wsum[0][wave] = i0; wsum[1][wave] = i1; wsum[2][wave] = i2; }
 		__syncthreads();
 		uint32_t p0 = c_lo, p1 = c_parts, p2 = c_sb;
@@ -214,17 +224,23 @@ __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __r
 			c_lo += wsum[0][w]; c_parts += wsum[1][w]; c_sb += wsum[2][w];
 		}
 		__syncthreads();
-		if (vb < n_vb) {
-			const uint32_t lo = p0 + i0 - t;
+		uint32_t lo = p0 + i0 - s0, first = p1 + i1 - s1, b = p2 + i2 - s2;
+#pragma unroll
+		for (uint32_t k = 0; k < SC_PLAN_K; ++k) {
+			if (k >= K || v0 + k >= n_vb) break;
+			const uint32_t vb = v0 + k, tk = t[k];
 			lo_out[vb] = lo;
-			if (is_split) {
-				const uint32_t first = p1 + i1 - parts, b = p2 + i2 - 1u;
+			if (tk > split_limit) {
+				const uint32_t parts = (tk + part - 1) / part;
 				splitb[3 * b] = vb; splitb[3 * b + 1] = first; splitb[3 * b + 2] = parts;
 				for (uint32_t q = 0; q < parts; ++q) {
 					uint32_t* d = split + 2 + 3 * (size_t)(first + q);
-					d[0] = vb; d[1] = lo + q * part; d[2] = min(lo + (q + 1) * part, lo + t);
+					d[0] = vb; d[1] = lo + q * part; d[2] = min(lo + (q + 1) * part, lo + tk);
 				}
+				first += parts;
+				++b;
 			}
+			lo += tk;
 		}
 	}
 	if (threadIdx.x == 0) { split[0] = c_parts; split[1] = c_sb; }
@@ -645,7 +661,8 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const Scatter
 	}
 	k_sc_scan<<<div_round_up(p.n_buckets, 64), 64 * SCAN_SEG, 0, s>>>(hist, p.n_chunks, p.n_buckets, (uint32_t*)(ws + p.off_cur), (uint32_t*)(ws + p.off_tot));
 	NGP_HIP(hipGetLastError());
-	k_sc_plan<<<1, SC_PLAN_THREADS, 0, s>>>((const uint32_t*)(ws + p.off_tot), p.n_buckets, p.split_limit, p.part,
+	const auto plan = p.n_buckets <= SC_PLAN_THREADS ? k_sc_plan<1> : p.n_buckets <= 8 * SC_PLAN_THREADS ? k_sc_plan<8> : k_sc_plan<32>;
+	plan<<<1, SC_PLAN_THREADS, 0, s>>>((const uint32_t*)(ws + p.off_tot), p.n_buckets, p.split_limit, p.part,
 	                                        (uint32_t*)(ws + p.off_lo), (uint32_t*)(ws + p.off_split), (uint32_t*)(ws + p.off_splitb));
 	NGP_HIP(hipGetLastError());
 }
