@@ -65,6 +65,10 @@ def synthetic_batch(n, seed, device):
     g = np.random.default_rng(seed)
     c = np.zeros((n, 7), np.float32)
     c[:, :3] = g.random((n, 3), dtype=np.float32)
+    if os.environ.get("NGP_BENCH_POINTS") == "blob":  # NeRF-like concentration (hot coarse entries)
+        blob = np.clip(0.5 + 0.06 * g.standard_normal((n, 3)), 0.0, 1.0).astype(np.float32)
+        keep = g.random(n) < 0.8
+        c[keep, :3] = blob[keep]
     c[:, 3] = 0.0
     d = g.standard_normal((n, 3))
     c[:, 4:] = (d / np.linalg.norm(d, axis=1, keepdims=True) + 1) / 2

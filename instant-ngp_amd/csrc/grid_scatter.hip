@@ -42,7 +42,8 @@ constexpr uint32_t SC_BT = 1024;             // bucket/split blocks: 2 per CU by
 // 512-sample chunk) take 1024-sample chunks with 1024 threads, whose runs are twice as long and whose
 // per-(chunk, bucket) histogram and cursor arrays are half the size (C5 backward 385 -> 355 us;
 // 2048-sample chunks measured slower, 372 us).
-constexpr size_t SC_LDS_BYTES = 64 * 1024;   // one bucket's int64 accumulators
+constexpr size_t SC_LDS_BYTES = 64 * 1024;   // one bucket's int64 accumulators (+ one pad entry per feature plane)
+constexpr size_t SC_LDS_PAD_BYTES = 8 * 8;  // up to F = 8 planes
 constexpr float FIX_SCALE = 16777216.0f;     // 2^24: fp16 values are integer multiples of 2^-24
 
 template <uint32_t F> struct ValVec;
@@ -357,8 +358,11 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 		}
 }
 
-// LDS accumulators are feature-major, acc[f * NE + entry]: a wave's lanes hit 2 * (random entry)
-// banks instead of 8 * entry (entry-major int64 x F=4), ~4x fewer bank conflicts.
+// LDS accumulators are feature-major, acc[f * NEP + entry] with NEP = NE + 1: a wave's lanes hit 2 *
+// (random entry) banks instead of 8 * entry (entry-major int64 x F=4), ~4x fewer bank conflicts; the
+// one-entry pad puts the F planes of one entry in different banks. Lane l adds feature (k + l) % F at
+// step k, so lanes that share a hot entry (NeRF batches concentrate on the object: C2's coarse
+// levels) spread their same-address adds over F addresses in F banks instead of serialising on one.
 template <uint32_t F>
 __device__ __forceinline__ void accumulate_items(unsigned long long* acc, uint32_t NE, uint32_t lo, uint32_t hi,
                                                  const uint16_t* __restrict__ item_idx, const f16* __restrict__ item_val,
@@ -376,6 +380,22 @@ __device__ __forceinline__ void accumulate_items(unsigned long long* acc, uint32
 	}
 	// U items per thread in flight: the loop is bound by memory-level parallelism, not LDS
 	constexpr uint32_t U = 8;
+	const uint32_t NEP = NE + 1;
+	const uint32_t rot = (debug & 64) ? 0u : threadIdx.x % F;
+	auto add_item = [&](uint32_t j, const V& vv) {
+#pragma unroll
+		for (uint32_t k = 0; k < F; ++k) {
+			const uint32_t f = (k + rot) & (F - 1);
+			float x;
+			if constexpr (F == 1) x = (float)vv;
+			else {
+				x = (float)vv[0];
+#pragma unroll
+				for (uint32_t q = 1; q < F; ++q) x = f == q ? (float)vv[q] : x;
+			}
+			if (x != 0.f) atomicAdd(&acc[f * NEP + j], (unsigned long long)(long long)(x * FIX_SCALE));
+		}
+	};
 	const uint32_t step = blockDim.x * U;
 	uint32_t t0 = lo;
 	for (; t0 + step <= hi; t0 += step) {
@@ -388,25 +408,9 @@ __device__ __forceinline__ void accumulate_items(unsigned long long* acc, uint32
 			v[u] = *(const V*)(item_val + (size_t)t * F);
 		}
 #pragma unroll
-		for (uint32_t u = 0; u < U; ++u) {
-#pragma unroll
-			for (uint32_t f = 0; f < F; ++f) {
-				float x;
-				if constexpr (F == 1) x = (float)v[u]; else x = (float)v[u][f];
-				if (x != 0.f) atomicAdd(&acc[f * NE + j[u]], (unsigned long long)(long long)(x * FIX_SCALE));
-			}
-		}
+		for (uint32_t u = 0; u < U; ++u) add_item(j[u], v[u]);
 	}
-	for (uint32_t t = t0 + threadIdx.x; t < hi; t += blockDim.x) {
-		const uint32_t jj = item_idx[t];
-		const V vv = *(const V*)(item_val + (size_t)t * F);
-#pragma unroll
-		for (uint32_t f = 0; f < F; ++f) {
-			float x;
-			if constexpr (F == 1) x = (float)vv; else x = (float)vv[f];
-			if (x != 0.f) atomicAdd(&acc[f * NE + jj], (unsigned long long)(long long)(x * FIX_SCALE));
-		}
-	}
+	for (uint32_t t = t0 + threadIdx.x; t < hi; t += blockDim.x) add_item(item_idx[t], *(const V*)(item_val + (size_t)t * F));
 }
 
 __device__ __forceinline__ float fix_to_f32(unsigned long long q) { return (float)((double)(long long)q * (1.0 / FIX_SCALE)); }
@@ -422,7 +426,7 @@ __device__ __forceinline__ void bucket_entries(const GridConst& c, const Levels&
 
 // (entry pair k of a bucket) -> the two accumulator slots (feature-major layout)
 template <uint32_t F>
-__device__ __forceinline__ void pair_slots(uint32_t k, uint32_t NE, uint32_t& a, uint32_t& b) {
+__device__ __forceinline__ void pair_slots(uint32_t k, uint32_t NE, uint32_t& a, uint32_t& b) {  // NE: plane stride
 	if constexpr (F == 1) { a = 2 * k; b = 2 * k + 1; }
 	else {
 		const uint32_t j = k / (F / 2), fp = k % (F / 2);
@@ -443,17 +447,18 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
                                                          const uint32_t* __restrict__ split, unsigned long long* __restrict__ scratch,
                                                          uint32_t debug) {
 	extern __shared__ unsigned long long acc[];
-	const uint32_t NE = 1u << B;
+	const uint32_t NE = 1u << B, NEP = NE + 1;  // feature planes padded by one entry (accumulate_items)
 	if (blockIdx.x < max_parts) {
 		if (blockIdx.x >= split[0]) return;
 		const uint32_t* d = split + 2 + 3 * (size_t)blockIdx.x;
 		const uint32_t lo = d[1], hi = d[2];
-		for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) acc[k] = 0ull;
+		for (uint32_t k = threadIdx.x; k < NEP * F; k += blockDim.x) acc[k] = 0ull;
 		__syncthreads();
 		if (!(debug & 1)) accumulate_items<F>(acc, NE, lo, hi, item_idx, item_val, debug);
 		__syncthreads();
+		// scratch keeps the unpadded layout [f * NE + entry] (k_sc_split_reduce)
 		unsigned long long* dst = scratch + (size_t)blockIdx.x * NE * F;
-		for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) dst[k] = acc[k];
+		for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) dst[k] = acc[(k / NE) * NEP + k % NE];
 		return;
 	}
 	const uint32_t vb = blockIdx.x - max_parts;
@@ -468,14 +473,14 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 		return;
 	}
 	const uint32_t lo = lo_arr[vb];
-	for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) acc[k] = 0ull;
+	for (uint32_t k = threadIdx.x; k < NEP * F; k += blockDim.x) acc[k] = 0ull;
 	__syncthreads();
 	if (!(debug & 1)) accumulate_items<F>(acc, NE, lo, lo + t, item_idx, item_val, debug);
 	__syncthreads();
 	// two fp16 per thread-step (n_e * F is even: levels hold multiples of 8 entries)
 	for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) {
 		uint32_t ia, ib;
-		pair_slots<F>(k, NE, ia, ib);
+		pair_slots<F>(k, NEP, ia, ib);
 		float s0 = fix_to_f32(acc[ia]), s1 = fix_to_f32(acc[ib]);
 		if (!overwrite) {
 			const f16x2 o = ((const f16x2*)g)[k];
@@ -562,8 +567,8 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		ensure_dynamic_lds((const void*)scatter, lds_s);
 		if (!(debug & 4)) scatter<<<grid_s, p.spb == 512 ? 512 : 1024, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, p.n_chunks, xcd_map, cur_t, lo, idx, val, debug);
 		NGP_HIP(hipGetLastError());
-		ensure_dynamic_lds((const void*)accum, SC_LDS_BYTES);
-		accum<<<p.max_split_blocks + p.n_buckets, SC_BT, SC_LDS_BYTES, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
+		ensure_dynamic_lds((const void*)accum, SC_LDS_BYTES + SC_LDS_PAD_BYTES);
+		accum<<<p.max_split_blocks + p.n_buckets, SC_BT, SC_LDS_BYTES + SC_LDS_PAD_BYTES, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
 		                                                                     val, a.grad, overwrite, split, scratch, debug);
 		NGP_HIP(hipGetLastError());
 		const dim3 grid_r(p.max_split_buckets, div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS));
