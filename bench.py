@@ -19,6 +19,7 @@ At N=1 the JSON line also carries (rank 0, after the timed region):
   cpu_baseline  the C oracle's encoding + MLP fwd/bwd on every host core this process may use
   e2e           the full Testbed NeRF step for 30 s on the procedural Lego stand-in: samples/s and PSNR
   c2p           the same training pass at C2' (L=16 F=2 T=2^19), BASELINE's literal "L=16"
+  c5            the SDF training step at C5 (L=16 F=2 T=2^22, 105 M parameters: the HBM-bound config)
 """
 import argparse
 import json
@@ -320,6 +321,25 @@ def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped):
     return summary, rl
 
 
+def c5_pass(pkg, n, rank):
+    """Testbed::train_sdf at C5 (configs/sdf/base.json with T=2^22) on a resident synthetic batch: returns
+    (step, net, trainer)."""
+    cfg = json.loads(json.dumps(pkg.SDF_BASE))
+    cfg["encoding"].update({"log2_hashmap_size": 22, "per_level_scale": 2.0})
+    net = pkg.NetworkWithInputEncoding(3, 1, cfg["encoding"], cfg["network"])
+    trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+    verts = pkg.synthetic.icosphere(4, radius=0.35, bumps=0.3, seed=rank)
+    tris, amin, amax, brad = pkg.sdf.load_mesh(verts)
+    mesh = pkg.sdf.SdfMesh(tris)
+    sdf = pkg.sdf.SdfTraining(net, trainer, mesh, amin, amax, brad, seed=1337 + rank, batch_size=n)
+    sdf.generate_training_samples(n, sdf.positions, sdf.distances)  # resident batch (online regeneration untimed)
+    torch.cuda.synchronize()
+
+    def step():
+        sdf.train_step(get_loss=False, regenerate=False)
+    return step, net, trainer
+
+
 def optimizer_counts(net, trainer, step):
     """Parameters the optimizer updates vs lazily skips (grid entries with a zero gradient) in one step."""
     step()
@@ -341,6 +361,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-seconds", type=float, default=30.0, help="full NeRF step + PSNR sub-record (0: off)")
     ap.add_argument("--no-c2p", action="store_true", help="skip the C2' (L=16) sub-record")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 (SDF, T=2^22) sub-record")
     ap.add_argument("--graph", type=int, default=1, help="1: time the K steps as one captured HIP graph (N=1)")
     ap.add_argument("--overlap", type=int, default=None, help="engine side-stream overlap bitmask (engine.hip)")
     ap.add_argument("--opt", action="append", default=[], help="model option key=value (ngp_model_set_option)")
@@ -363,19 +384,7 @@ def main():
     elif args.variant == "C5":
         if world > 1:
             raise SystemExit("C5 bench is single-GPU")
-        cfg = json.loads(json.dumps(pkg.SDF_BASE))
-        cfg["encoding"].update({"log2_hashmap_size": 22, "per_level_scale": 2.0})
-        net = pkg.NetworkWithInputEncoding(3, 1, cfg["encoding"], cfg["network"])
-        trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
-        verts = pkg.synthetic.icosphere(4, radius=0.35, bumps=0.3, seed=rank)
-        tris, amin, amax, brad = pkg.sdf.load_mesh(verts)
-        mesh = pkg.sdf.SdfMesh(tris)
-        sdf = pkg.sdf.SdfTraining(net, trainer, mesh, amin, amax, brad, seed=1337 + rank, batch_size=n)
-        sdf.generate_training_samples(n, sdf.positions, sdf.distances)  # resident batch (online regeneration untimed)
-        torch.cuda.synchronize()
-
-        def step():
-            sdf.train_step(get_loss=False, regenerate=False)
+        step, net, trainer = c5_pass(pkg, n, rank)
         n_opt = optimizer_counts(net, trainer, step)
         capture = None
     else:  # IMG
@@ -433,6 +442,17 @@ def main():
                 res["c2p"] = {"workload": WORKLOADS["C2p"], "value": n * args.steps / dt2, "unit": "samples/s",
                               "ms_per_step": dt2 / args.steps * 1e3, "launch": launch2, "roofline": rl2, "kernels": ks2}
                 del s2, c2, net2, tr2
+            if not args.no_c5:
+                # BASELINE configs[4]: the HBM-bound SDF step (T=2^22, 105 M parameters), same batch size
+                s5, net5, tr5 = c5_pass(pkg, n, 0)
+                o5 = optimizer_counts(net5, tr5, s5)
+                dt5, launch5, k5 = timed_steps(lib, s5, args.steps, args.warmup, 1, None)
+                ks5, rl5 = roofline("C5", n, k5, *o5)
+                res["c5"] = {"workload": WORKLOADS["C5"], "value": n * args.steps / dt5, "unit": "samples/s",
+                             "ms_per_step": dt5 / args.steps * 1e3, "launch": launch5, "roofline": rl5, "kernels": ks5,
+                             "optimizer_params": {"updated": o5[0], "skipped": o5[1]}}
+                del s5, net5, tr5
+                torch.cuda.empty_cache()
             if args.e2e_seconds > 0:
                 # the metric's full form: the Testbed NeRF step (occupancy grid, sampling, inference,
                 # loss/compaction, training pass, optimizer) for 30 s, then PSNR on held-out views
