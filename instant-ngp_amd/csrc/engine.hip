@@ -158,6 +158,10 @@ struct ngp_model {
 	                                        // and the dW slab reduction with the grid backward
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_frags = nullptr, ev_mlp = nullptr, ev_red = nullptr;
 	f16 *params = nullptr, *inference_params = nullptr, *gradients = nullptr;
+	// lazy-EMA trainer: brings the inference (EMA) parameters up to date before they are read
+	void (*inference_hook)(void*, hipStream_t) = nullptr;
+	void* inference_hook_ctx = nullptr;
+	void sync_inference(hipStream_t s) { if (inference_hook) inference_hook(inference_hook_ctx, s); }
 	float max_level = 1.0f;
 	const float* max_level_per_sample = nullptr;
 	uint64_t generation = 0;
@@ -274,6 +278,7 @@ struct ngp_model {
 	bool fused_training_ok() const { return fuse_train && fused_encoding_ok(); }
 	f16x8* prep(hipStream_t s, bool inference) {
 		f16x8* f = (f16x8*)(inference ? frags_inf : frags).get((size_t)n_all_frags * 1024);
+		if (inference) sync_inference(s);
 		ProfScope ps("prepare_frags", s);
 		prepare_frags(d_descs, n_all_frags, pick(inference), f, s);
 		if (!inference) frags_current = true;
@@ -283,6 +288,7 @@ struct ngp_model {
 	// backward's bucket histogram in the forward kernel (its corner indices are computed anyway).
 	void encode(hipStream_t s, uint32_t n, const float* in, uint32_t stride, f16* out, uint32_t out_stride, uint32_t layout, bool inference,
 	            bool want_hist = false) {
+		if (inference) sync_inference(s);
 		GridFwdArgs a{n, in, stride, pick(inference) + grid_offset(), out, out_stride, layout, max_level, max_level_per_sample};
 		if (enc_width > grid.n_levels * grid.n_features && layout == AoS && !grid_forward_rows_ok(grid, a)) {
 			// zero the padding columns (tcnn pads the encoding output with zeros); the row kernel writes them
@@ -317,6 +323,7 @@ struct ngp_model {
 			a.dL_dout = dL; a.dL_stride = dL_stride; a.dL_denc = dL_denc; a.denc_stride = enc_width; a.dw_slab = slab;
 			a.n_matrix = (uint32_t)n_matrix(); a.density_woff = 0; a.rgb_woff = (uint32_t)mlp0_params;
 			if (mode == MLP_INFER_ENC || mode == MLP_TRAIN_ENC) {
+				if (inference) sync_inference(s);
 				a.table = pick(inference) + grid_offset(); a.max_level = max_level; a.gc = make_grid_const(grid);
 			}
 			ProfScope ps(mode == MLP_TRAIN ? "mlp_train" : mode == MLP_DENSITY ? "mlp_density"
@@ -395,6 +402,21 @@ struct ngp_trainer {
 	float *w32 = nullptr, *m1 = nullptr, *m2 = nullptr, *ema32 = nullptr;
 	f16 *w16 = nullptr, *inf16 = nullptr, *g16 = nullptr;
 	uint32_t* steps = nullptr;
+	// lazy-EMA layout (optimizer.h AdamRec), chosen for large tables: a step touches only the state of
+	// updated parameters; the inference (EMA) parameters are brought up to date when read
+	AdamRec* rec = nullptr;
+	bool inf_stale = false;
+	void materialize(hipStream_t s) {
+		if (!rec || !inf_stale) return;
+		AdamState st{w32, w16, g16, nullptr, nullptr, nullptr, nullptr, inf16, nullptr, nullptr, nullptr, 0, nullptr, rec};
+		ema_materialize(cfg, (uint32_t)n, step, st, s);
+		inf_stale = false;
+	}
+	static void materialize_hook(void* self, hipStream_t s) { ((ngp_trainer*)self)->materialize(s); }
+	void bind_model() {
+		ngp_model_set_params(model, w16, cfg.ema_decay > 0.f ? inf16 : w16, g16);
+		if (rec) { model->inference_hook = materialize_hook; model->inference_hook_ctx = this; }
+	}
 	uint32_t* ctl = nullptr;  // device {optimizer step, block counter, .., AdamConfig at ctl + CTL_CFG}; `step` mirrors ctl[0]
 	ngp_allreduce_fn allreduce = nullptr;  // gradient exchange inside captured steps (ngp_trainer_set_allreduce)
 	void* allreduce_user = nullptr;
@@ -409,9 +431,10 @@ struct ngp_trainer {
 		// launch refreshes with the step: set_learning_rate / set_option reach replayed steps too
 		AdamState st{w32, w16, g16, m1, m2, steps, ema32, inf16,
 		             own && m->frags_current ? (f16*)m->frags.p : nullptr, m->d_fragmap, step_base, step_add,
-		             step_base ? (const AdamConfig*)(ctl + CTL_CFG) : nullptr};
+		             step_base ? (const AdamConfig*)(ctl + CTL_CFG) : nullptr, rec};
 		ProfScope ps("optimizer", s);
 		adam_ema_update(cfg, (uint32_t)n, (uint32_t)m->n_matrix(), loss_scale, st, s);
+		if (rec) inf_stale = true;
 	}
 };
 
@@ -556,6 +579,8 @@ int ngp_model_param_layout(const ngp_model* m, ngp_param_layout* o) {
 int ngp_model_set_params(ngp_model* m, void* params, void* inference_params, void* gradients) {
 	NGP_ARG(m);
 	NGP_TRY({
+		m->inference_hook = nullptr;  // a trainer that binds its own buffers installs its hook afterwards
+		m->inference_hook_ctx = nullptr;
 		m->params = (f16*)params;
 		m->frags_current = false;
 		m->inference_params = (f16*)(inference_params ? inference_params : params);
@@ -765,14 +790,24 @@ int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, 
 		t->n = n;
 		auto al = [](size_t b) { return (b + 255) / 256 * 256; };
 		const size_t b32 = al(n * 4), b16 = al(n * 2);
-		const size_t total = 4 * b32 + 3 * b16 + b32 /*steps*/ + 256 /*ctl*/;
+		// lazy-EMA records for large tables (C5: 105 M parameters, ~28 % updated per step); the eager
+		// arrays otherwise. NGP_LAZY_EMA=0/1 forces the choice.
+		bool lazy = n >= (1ull << 25);
+		if (const char* e = getenv("NGP_LAZY_EMA")) lazy = atoi(e) != 0;
+		lazy = lazy && n % 4 == 0;
+		const size_t brec = al(n / 2 * sizeof(AdamRec));
+		const size_t total = b32 + (lazy ? brec : 4 * b32) + 3 * b16 + 256 /*ctl*/;
 		NGP_HIP(hipMalloc(&t->arena, total));
 		char* p = (char*)t->arena;
 		t->w32 = (float*)p; p += b32;
-		t->m1 = (float*)p; p += b32;
-		t->m2 = (float*)p; p += b32;
-		t->ema32 = (float*)p; p += b32;
-		t->steps = (uint32_t*)p; p += b32;
+		if (lazy) {
+			t->rec = (AdamRec*)p; p += brec;
+		} else {
+			t->m1 = (float*)p; p += b32;
+			t->m2 = (float*)p; p += b32;
+			t->ema32 = (float*)p; p += b32;
+			t->steps = (uint32_t*)p; p += b32;
+		}
 		t->w16 = (f16*)p; p += b16;
 		t->inf16 = (f16*)p; p += b16;
 		t->g16 = (f16*)p; p += b16;
@@ -922,6 +957,7 @@ int ngp_graph_launch(ngp_graph* g, void* stream) {
 		if (g->steps_per_launch) set_device_ctl(g->trainer->ctl, g->trainer->step, g->trainer->cfg, S(stream));
 		NGP_HIP(hipGraphLaunch(g->exec, S(stream)));
 		g->trainer->step += g->steps_per_launch;
+		if (g->steps_per_launch && g->trainer->rec) g->trainer->inf_stale = true;
 	});
 }
 
@@ -929,7 +965,19 @@ void ngp_graph_destroy(ngp_graph* g) { delete g; }
 
 void* ngp_trainer_gradients(ngp_trainer* t) { return t ? t->g16 : nullptr; }
 void* ngp_trainer_params(ngp_trainer* t) { return t ? t->w16 : nullptr; }
-void* ngp_trainer_inference_params(ngp_trainer* t) { return t ? (t->cfg.ema_decay > 0.f ? t->inf16 : t->w16) : nullptr; }
+void* ngp_trainer_inference_params(ngp_trainer* t) {
+	if (!t) return nullptr;
+	if (t->rec && t->inf_stale) {  // lazy EMA: bring the inference parameters up to date before handing them out
+		try {
+			t->materialize(nullptr);
+			NGP_HIP(hipDeviceSynchronize());
+		} catch (const std::exception& e) {
+			g_last_error = e.what();
+			return nullptr;
+		}
+	}
+	return t->cfg.ema_decay > 0.f ? t->inf16 : t->w16;
+}
 float* ngp_trainer_params_full_precision(ngp_trainer* t) { return t ? t->w32 : nullptr; }
 uint32_t ngp_trainer_step(const ngp_trainer* t) { return t ? t->step : 0; }
 float ngp_trainer_learning_rate(const ngp_trainer* t) { return t ? t->cfg.lr_at(t->step) : 0.f; }
@@ -950,7 +998,8 @@ int ngp_trainer_set_params_full_precision(ngp_trainer* t, const float* params_ho
 		k_f32_to_f16<<<div_round_up(n, 256), 256>>>(t->w32, t->w16, t->inf16, n);
 		NGP_HIP(hipGetLastError());
 		NGP_HIP(hipDeviceSynchronize());
-		ngp_model_set_params(t->model, t->w16, t->cfg.ema_decay > 0.f ? t->inf16 : t->w16, t->g16);
+		t->inf_stale = false;  // inference parameters = the new weights, as in the eager layout
+		t->bind_model();
 	});
 }
 
@@ -965,7 +1014,17 @@ int ngp_trainer_serialize(ngp_trainer* t, void* buf, uint64_t* size) {
 		const uint64_t hdr[4] = {0x4e47504d49333535ULL /* "NGPMI355" */, 1, t->n, t->step};
 		memcpy(p, hdr, 32); p += 32;
 		NGP_HIP(hipDeviceSynchronize());
-		for (void* src : {(void*)t->w32, (void*)t->m1, (void*)t->m2, (void*)t->ema32, (void*)t->steps}) {
+		DevBuf soa;
+		float *m1 = t->m1, *m2 = t->m2, *ema32 = t->ema32;
+		uint32_t* steps = t->steps;
+		if (t->rec) {  // lazy layout: every EMA brought up to date, then the eager arrays of the blob
+			t->materialize(nullptr);
+			char* q = (char*)soa.get(t->n * 16);
+			m1 = (float*)q; m2 = (float*)(q + t->n * 4); ema32 = (float*)(q + t->n * 8); steps = (uint32_t*)(q + t->n * 12);
+			adam_rec_to_soa((uint32_t)t->n, t->rec, m1, m2, ema32, steps, nullptr);
+			NGP_HIP(hipDeviceSynchronize());
+		}
+		for (void* src : {(void*)t->w32, (void*)m1, (void*)m2, (void*)ema32, (void*)steps}) {
 			NGP_HIP(hipMemcpy(p, src, t->n * 4, hipMemcpyDeviceToHost));
 			p += t->n * 4;
 		}
@@ -984,10 +1043,19 @@ int ngp_trainer_deserialize(ngp_trainer* t, const void* buf, uint64_t size) {
 		NGP_CHECK(hdr[2] == t->n && size >= 32 + t->n * 20, "deserialize: parameter count mismatch");
 		t->step = (uint32_t)hdr[3];
 		t->sync_device_step();
-		for (void* dst : {(void*)t->w32, (void*)t->m1, (void*)t->m2, (void*)t->ema32, (void*)t->steps}) {
+		DevBuf soa;
+		float *m1 = t->m1, *m2 = t->m2, *ema32 = t->ema32;
+		uint32_t* steps = t->steps;
+		if (t->rec) {
+			char* q = (char*)soa.get(t->n * 16);
+			m1 = (float*)q; m2 = (float*)(q + t->n * 4); ema32 = (float*)(q + t->n * 8); steps = (uint32_t*)(q + t->n * 12);
+		}
+		for (void* dst : {(void*)t->w32, (void*)m1, (void*)m2, (void*)ema32, (void*)steps}) {
 			NGP_HIP(hipMemcpy(dst, p, t->n * 4, hipMemcpyHostToDevice));
 			p += t->n * 4;
 		}
+		if (t->rec) adam_soa_to_rec((uint32_t)t->n, m1, m2, ema32, steps, t->step, t->rec, nullptr);
+		t->inf_stale = false;  // inference parameters = the restored weights (below), as in the eager layout
 		k_f32_to_f16<<<div_round_up(t->n, 256), 256>>>(t->w32, t->w16, t->inf16, t->n);
 		NGP_HIP(hipGetLastError());
 		NGP_HIP(hipDeviceSynchronize());

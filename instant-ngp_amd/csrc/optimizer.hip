@@ -132,6 +132,164 @@ __global__ void __launch_bounds__(256) k_adam_ema4(const uint32_t n4, const uint
 	}
 }
 
+// ---- lazy-EMA layout ------------------------------------------------------------------------
+// The eager EMA of step j: e = d * e + (1 - d) * w (w after step j's update), output e / (1 - d^(j+1)).
+__device__ __forceinline__ float ema_catch_up(float e, float w, float d, uint32_t from, uint32_t to) {
+	for (uint32_t j = from; j < to; ++j) e = d * e + (1.f - d) * w;
+	return e;
+}
+
+// Four parameters (two records) per group; a record none of whose parameters is updated this step is
+// neither read nor written (grid entries without gradient: the bulk of a large table). A thread owns
+// two groups half the table apart and issues both groups' state loads before either computes (the
+// loads depend on the gradient test: two chains in flight instead of one).
+struct LazyGroup {
+	uint32_t i0;
+	bool act[4], any[2];
+	float g[4];
+	f32x4 w;
+	f32x4 q[2][3];
+};
+
+__device__ __forceinline__ void lazy_load(const AdamState& st, uint32_t i0, uint32_t n_matrix, float loss_scale, LazyGroup& G) {
+	G.i0 = i0;
+	const f16x4 gh = *(const f16x4*)(st.g16 + i0);
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		G.g[k] = (float)gh[k] / loss_scale;
+		G.act[k] = !(i0 + k >= n_matrix && G.g[k] == 0.f);
+	}
+	G.any[0] = G.act[0] || G.act[1];
+	G.any[1] = G.act[2] || G.act[3];
+	if (G.any[0] || G.any[1]) G.w = *(const f32x4*)(st.w32 + i0);
+#pragma unroll
+	for (int r = 0; r < 2; ++r) {
+		if (!G.any[r]) continue;
+		const f32x4* rp = (const f32x4*)(st.rec + (i0 >> 1) + r);
+		G.q[r][0] = rp[0]; G.q[r][1] = rp[1]; G.q[r][2] = rp[2];
+	}
+}
+
+__device__ __forceinline__ void lazy_update(const AdamState& st, const AdamConfig& c, uint32_t step, uint32_t n_matrix, LazyGroup& G) {
+	if (!G.any[0] && !G.any[1]) return;
+	const uint32_t i0 = G.i0;
+	const float lr = lr_schedule(c, step);
+	const float d = c.ema_decay;
+	f32x4 w = G.w;
+#pragma unroll
+	for (int r = 0; r < 2; ++r) {
+		if (!G.any[r]) continue;
+		AdamRec rc;
+		rc.m1[0] = G.q[r][0][0]; rc.m1[1] = G.q[r][0][1]; rc.m2[0] = G.q[r][0][2]; rc.m2[1] = G.q[r][0][3];
+		rc.steps[0] = __float_as_uint(G.q[r][1][0]); rc.steps[1] = __float_as_uint(G.q[r][1][1]);
+		rc.ema[0] = G.q[r][1][2]; rc.ema[1] = G.q[r][1][3];
+		rc.done[0] = __float_as_uint(G.q[r][2][0]); rc.done[1] = __float_as_uint(G.q[r][2][1]);
+#pragma unroll
+		for (int k = 0; k < 2; ++k) {
+			const int p = 2 * r + k;
+			if (!G.act[p]) continue;
+			// missing EMA steps first, with the weight those steps saw (unchanged since the last update)
+			if (d > 0.f) rc.ema[k] = ema_catch_up(rc.ema[k], w[p], d, rc.done[k], step);
+			float gk = G.g[p];
+			if (i0 + p < n_matrix) gk += c.l2 * w[p];
+			const float mm = c.beta1 * rc.m1[k] + (1.f - c.beta1) * gk;
+			const float vv = c.beta2 * rc.m2[k] + (1.f - c.beta2) * (gk * gk);
+			rc.m1[k] = mm;
+			rc.m2[k] = vv;
+			const uint32_t sk = rc.steps[k] + 1;
+			rc.steps[k] = sk;
+			const float lr_s = lr * sqrtf(1.f - powf(c.beta2, (float)sk)) / (1.f - powf(c.beta1, (float)sk));
+			w[p] = w[p] - lr_s / (sqrtf(vv) + c.eps) * mm;
+			if (d > 0.f) rc.ema[k] = d * rc.ema[k] + (1.f - d) * w[p];
+			rc.done[k] = step + 1;
+		}
+		f32x4* rp = (f32x4*)(st.rec + (i0 >> 1) + r);
+		rp[0] = f32x4{rc.m1[0], rc.m1[1], rc.m2[0], rc.m2[1]};
+		rp[1] = f32x4{__uint_as_float(rc.steps[0]), __uint_as_float(rc.steps[1]), rc.ema[0], rc.ema[1]};
+		rp[2] = f32x4{__uint_as_float(rc.done[0]), __uint_as_float(rc.done[1]), 0.f, 0.f};
+	}
+	f16x4 wh;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) wh[k] = (f16)w[k];
+	*(f32x4*)(st.w32 + i0) = w;
+	*(f16x4*)(st.w16 + i0) = wh;
+	if (st.frags && i0 < n_matrix) {
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			if (i0 + k >= n_matrix || !G.act[k]) continue;
+			const uint32_t q0 = st.fragmap[2 * (i0 + k)], q1 = st.fragmap[2 * (i0 + k) + 1];
+			if (q0 != ~0u) st.frags[q0] = wh[k];
+			if (q1 != ~0u) st.frags[q1] = wh[k];
+		}
+	}
+}
+
+__global__ void __launch_bounds__(256) k_adam_lazy4(const uint32_t n4, const uint32_t n_matrix, const float loss_scale,
+                                                    const AdamConfig c_arg, const AdamState st) {
+	const uint32_t half = (n4 + 1) / 2;
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= half) return;
+	const AdamConfig c = st.cfg_dev ? *st.cfg_dev : c_arg;
+	const uint32_t step = (st.step_base ? *st.step_base : 0u) + st.step_add;
+	const bool two = t + half < n4;
+	LazyGroup A, B;
+	lazy_load(st, 4 * t, n_matrix, loss_scale, A);
+	if (two) lazy_load(st, 4 * (t + half), n_matrix, loss_scale, B);
+	lazy_update(st, c, step, n_matrix, A);
+	if (two) lazy_update(st, c, step, n_matrix, B);
+}
+
+__global__ void k_ema_materialize(uint32_t n, float d, uint32_t steps_done, const AdamState st) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const float debias = 1.f - powf(d, (float)steps_done);  // on the device, as the eager kernel computes it
+	AdamRec* rp = st.rec + (i >> 1);
+	const uint32_t k = i & 1u;
+	float e = rp->ema[k];
+	const uint32_t done = rp->done[k];
+	if (done < steps_done) {
+		e = ema_catch_up(e, st.w32[i], d, done, steps_done);
+		rp->ema[k] = e;
+		rp->done[k] = steps_done;
+	}
+	st.ema16[i] = (f16)(e / debias);
+}
+
+__global__ void k_rec_to_soa(uint32_t n, const AdamRec* rec, float* m1, float* m2, float* ema32, uint32_t* steps) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	const AdamRec& r = rec[i >> 1];
+	const uint32_t k = i & 1u;
+	m1[i] = r.m1[k]; m2[i] = r.m2[k]; ema32[i] = r.ema[k]; steps[i] = r.steps[k];
+}
+
+__global__ void k_soa_to_rec(uint32_t n, const float* m1, const float* m2, const float* ema32, const uint32_t* steps, uint32_t done,
+                             AdamRec* rec) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	AdamRec& r = rec[i >> 1];
+	const uint32_t k = i & 1u;
+	r.m1[k] = m1[i]; r.m2[k] = m2[i]; r.ema[k] = ema32[i]; r.steps[k] = steps[i]; r.done[k] = done;
+	r.pad[k] = 0;
+}
+
+void ema_materialize(const AdamConfig& c, uint32_t n, uint32_t steps_done, const AdamState& st, hipStream_t s) {
+	if (c.ema_decay <= 0.f || steps_done == 0 || n == 0) return;
+	k_ema_materialize<<<div_round_up(n, 256), 256, 0, s>>>(n, c.ema_decay, steps_done, st);
+	NGP_HIP(hipGetLastError());
+}
+
+void adam_rec_to_soa(uint32_t n, const AdamRec* rec, float* m1, float* m2, float* ema32, uint32_t* steps, hipStream_t s) {
+	if (n) k_rec_to_soa<<<div_round_up(n, 256), 256, 0, s>>>(n, rec, m1, m2, ema32, steps);
+	NGP_HIP(hipGetLastError());
+}
+
+void adam_soa_to_rec(uint32_t n, const float* m1, const float* m2, const float* ema32, const uint32_t* steps, uint32_t done,
+                     AdamRec* rec, hipStream_t s) {
+	if (n) k_soa_to_rec<<<div_round_up(n, 256), 256, 0, s>>>(n, m1, m2, ema32, steps, done, rec);
+	NGP_HIP(hipGetLastError());
+}
+
 __global__ void k_set_ctl(uint32_t* ctl, uint32_t step, const AdamConfig c) {
 	ctl[0] = step;
 	*(AdamConfig*)(ctl + CTL_CFG) = c;
@@ -146,6 +304,13 @@ float AdamConfig::lr_at(uint32_t step) const {
 }
 
 void adam_ema_update(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float loss_scale, const AdamState& st, hipStream_t s) {
+	if (st.rec) {
+		NGP_CHECK(n % 4 == 0 && ((uintptr_t)st.w32 | (uintptr_t)st.w16 | (uintptr_t)st.g16 | (uintptr_t)st.rec) % 16 == 0,
+		          "lazy-EMA optimizer: parameters must be 16-B aligned groups of 4");
+		k_adam_lazy4<<<div_round_up((n / 4 + 1) / 2, 256), 256, 0, s>>>(n / 4, n_matrix, loss_scale, c, st);
+		NGP_HIP(hipGetLastError());
+		return;
+	}
 	AdamState a = st;
 	if (c.ema_decay <= 0.f) a.ema32 = nullptr;
 	const bool aligned = ((uintptr_t)a.w32 | (uintptr_t)a.m1 | (uintptr_t)a.m2 | (uintptr_t)a.steps | (uintptr_t)a.ema32 |

@@ -240,11 +240,19 @@ class Trainer:
         L = lib()
         self.gradients = wrap_device(L.ngp_trainer_gradients(h), n, torch.float16)
         self.params = wrap_device(L.ngp_trainer_params(h), n, torch.float16)
-        self.inference_params = wrap_device(L.ngp_trainer_inference_params(h), n, torch.float16)
         self.params_full_precision = wrap_device(L.ngp_trainer_params_full_precision(h), n, torch.float32)
 
     def __del__(self, _d=_destroy):
         _d(self, "ngp_trainer_destroy")
+
+    @property
+    def inference_params(self):
+        """The EMA (inference) parameters, brought up to date first: a large-table trainer keeps the EMA of
+        untouched entries lazily (optimizer.h AdamRec) and ngp_trainer_inference_params completes it."""
+        p = lib().ngp_trainer_inference_params(self.handle)
+        if not p:
+            raise NgpError(lib().ngp_last_error().decode())
+        return wrap_device(p, self.model.n_params, torch.float16)
 
     def optimizer_step(self, loss_scale=128.0, stream=None):
         check(lib().ngp_trainer_optimizer_step(self.handle, _stream(stream), float(loss_scale)))
