@@ -20,6 +20,7 @@ At N=1 the JSON line also carries (rank 0, after the timed region):
   e2e           the full Testbed NeRF step for 30 s on the procedural Lego stand-in: samples/s and PSNR
   c2p           the same training pass at C2' (L=16 F=2 T=2^19), BASELINE's literal "L=16"
   c5            the SDF training step at C5 (L=16 F=2 T=2^22, 105 M parameters: the HBM-bound config)
+  c3            the fox capture trained for 15 s (samples/s, held-out PSNR), when data/fox is staged
 """
 import argparse
 import json
@@ -362,6 +363,7 @@ def main():
     ap.add_argument("--e2e-seconds", type=float, default=30.0, help="full NeRF step + PSNR sub-record (0: off)")
     ap.add_argument("--no-c2p", action="store_true", help="skip the C2' (L=16) sub-record")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (SDF, T=2^22) sub-record")
+    ap.add_argument("--c3-seconds", type=float, default=15.0, help="fox (C3) training sub-record length (0: off)")
     ap.add_argument("--graph", type=int, default=1, help="1: time the K steps as one captured HIP graph (N=1)")
     ap.add_argument("--overlap", type=int, default=None, help="engine side-stream overlap bitmask (engine.hip)")
     ap.add_argument("--opt", action="append", default=[], help="model option key=value (ngp_model_set_option)")
@@ -461,6 +463,16 @@ def main():
                 e = psnr30.run(pkg, seconds=args.e2e_seconds)
                 res["e2e"] = {k: e[k] for k in ("value", "unit", "psnr", "psnr_views", "train_seconds", "steps", "ms_per_step",
                                                 "data", "config")}
+            if args.c3_seconds > 0:
+                # BASELINE configs[2]: the fox capture (OpenCV lens, aabb_scale 8: 4 cascades), when staged
+                sys.path.insert(0, os.path.join(ROOT, "tools"))
+                import fox_train
+                if os.path.isfile(os.path.join(fox_train.DEFAULT_DATA, "transforms.json")):
+                    f = fox_train.run(pkg, seconds=args.c3_seconds)
+                    res["c3"] = {k: f[k] for k in ("value", "unit", "psnr_heldout", "psnr_views", "psnr_train_views",
+                                                   "train_seconds", "steps", "ms_per_step", "data", "config")}
+                else:
+                    res["c3"] = {"skipped": "data/fox not staged (tools/stage_fox.sh copies it from the reference tree)"}
         if world == 1 and not args.no_cpu_baseline and args.variant in ("C2", "C2p"):
             res["cpu_baseline"] = cpu_baseline(args.variant)
         print(json.dumps(res), flush=True)

@@ -38,29 +38,45 @@ __device__ __forceinline__ float div_min_stepsize(float t) {
 	return t / c;
 }
 
-// testbed_nerf.cu:114-184
-__device__ float to_stepping_space(float t, float cone) {
-	if (cone <= 1e-5f) return div_min_stepsize(t);
-	const float log1p_c = ngp_logf(1.0f + cone);
-	const float a = (ngp_logf(MIN_CONE_STEPSIZE) - ngp_logf(log1p_c)) / log1p_c;
-	const float b = (ngp_logf(MAX_CONE_STEPSIZE) - ngp_logf(log1p_c)) / log1p_c;
-	const float at = ngp_expf(a * log1p_c), bt = ngp_expf(b * log1p_c);
-	if (t <= at) return (t - at) / MIN_CONE_STEPSIZE + a;
-	if (t <= bt) return ngp_logf(t) / log1p_c;
-	return (t - bt) / MAX_CONE_STEPSIZE + b;
+// testbed_nerf.cu:114-184. The constants of a cone angle (log(1 + cone), the two linear segments'
+// bounds) are computed once per ray or thread (make_cone), not at every step: with the shared
+// software logf/expf (ngp_math.h) they are ~10 transcendental evaluations per call. Same operations
+// and values as evaluating them inline.
+struct Cone {
+	float c, log1p_c, a, b, at, bt;
+};
+__device__ __forceinline__ Cone make_cone(float c) {
+	Cone k{c, 0.f, 0.f, 0.f, 0.f, 0.f};
+	if (c <= 1e-5f) return k;
+	k.log1p_c = ngp_logf(1.0f + c);
+	k.a = (ngp_logf(MIN_CONE_STEPSIZE) - ngp_logf(k.log1p_c)) / k.log1p_c;
+	k.b = (ngp_logf(MAX_CONE_STEPSIZE) - ngp_logf(k.log1p_c)) / k.log1p_c;
+	k.at = ngp_expf(k.a * k.log1p_c);
+	k.bt = ngp_expf(k.b * k.log1p_c);
+	return k;
 }
-__device__ float from_stepping_space(float n, float cone) {
-	if (cone <= 1e-5f) return n * MIN_CONE_STEPSIZE;
-	const float log1p_c = ngp_logf(1.0f + cone);
-	const float a = (ngp_logf(MIN_CONE_STEPSIZE) - ngp_logf(log1p_c)) / log1p_c;
-	const float b = (ngp_logf(MAX_CONE_STEPSIZE) - ngp_logf(log1p_c)) / log1p_c;
-	const float at = ngp_expf(a * log1p_c), bt = ngp_expf(b * log1p_c);
-	if (n <= a) return (n - a) * MIN_CONE_STEPSIZE + at;
-	if (n <= b) return ngp_expf(n * log1p_c);
-	return (n - b) * MAX_CONE_STEPSIZE + bt;
+#if NGP_SAMPLER_DIAG == 3  // timing aid only (not bit-exact): hardware log/exp in the stepping space
+#define ngp_logf __logf
+#define ngp_expf __expf
+#endif
+__device__ float to_stepping_space(float t, const Cone& k) {
+	if (k.c <= 1e-5f) return div_min_stepsize(t);
+	if (t <= k.at) return (t - k.at) / MIN_CONE_STEPSIZE + k.a;
+	if (t <= k.bt) return ngp_logf(t) / k.log1p_c;
+	return (t - k.bt) / MAX_CONE_STEPSIZE + k.b;
 }
-__device__ __forceinline__ float advance_n_steps(float t, float cone, float n) { return from_stepping_space(to_stepping_space(t, cone) + n, cone); }
-__device__ __forceinline__ float calc_dt(float t, float cone) { return advance_n_steps(t, cone, 1.0f) - t; }
+__device__ float from_stepping_space(float n, const Cone& k) {
+	if (k.c <= 1e-5f) return n * MIN_CONE_STEPSIZE;
+	if (n <= k.a) return (n - k.a) * MIN_CONE_STEPSIZE + k.at;
+	if (n <= k.b) return ngp_expf(n * k.log1p_c);
+	return (n - k.b) * MAX_CONE_STEPSIZE + k.bt;
+}
+#if NGP_SAMPLER_DIAG == 3
+#undef ngp_logf
+#undef ngp_expf
+#endif
+__device__ __forceinline__ float advance_n_steps(float t, const Cone& k, float n) { return from_stepping_space(to_stepping_space(t, k) + n, k); }
+__device__ __forceinline__ float calc_dt(float t, const Cone& k) { return advance_n_steps(t, k, 1.0f) - t; }
 
 __device__ __forceinline__ float signf_(float v) { return v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f); }  // glm::sign
 
@@ -73,12 +89,15 @@ __device__ float distance_to_next_voxel(V3 pos, V3 dir, V3 idir, float res) {
 	const float t = fminf(fminf(tx, ty), tz);
 	return fmaxf(t * (1.0f / res), 0.0f);  // res is a power of two: same rounding as t / res, no IEEE divide
 }
-__device__ float advance_to_next_voxel(float t, float cone, V3 pos, V3 dir, V3 idir, uint32_t mip) {
+// n_t = to_stepping_space(t): callers that already hold it (the sampler's empty-space march, which
+// also needs it for calc_dt) pass it in.
+__device__ __forceinline__ float advance_to_next_voxel_n(float t, float n_t, const Cone& cone, V3 pos, V3 dir, V3 idir, uint32_t mip) {
 	const float res = scalbnf((float)GRIDSIZE, -(int)mip);
-	float t_target = t + distance_to_next_voxel(pos, dir, idir, res);
-	t = to_stepping_space(t, cone);
-	t_target = to_stepping_space(t_target, cone);
-	return from_stepping_space(t + ceilf(fmaxf(t_target - t, 0.5f)), cone);
+	const float t_target = to_stepping_space(t + distance_to_next_voxel(pos, dir, idir, res), cone);
+	return from_stepping_space(n_t + ceilf(fmaxf(t_target - n_t, 0.5f)), cone);
+}
+__device__ float advance_to_next_voxel(float t, const Cone& cone, V3 pos, V3 dir, V3 idir, uint32_t mip) {
+	return advance_to_next_voxel_n(t, to_stepping_space(t, cone), cone, pos, dir, idir, mip);
 }
 
 // testbed_nerf.cu:614-633
@@ -288,7 +307,7 @@ __device__ RaySetup setup_ray(const Camera* cams, const uint32_t* pixels, uint32
 	aabb_ray_intersect(cfg_aabb(cfg), r.o, r.dn, &tmin, &tmax);
 	r.cone = cfg.cone_angle_constant;
 	tmin = fmaxf(tmin, 0.0f);
-	r.startt = advance_n_steps(tmin, r.cone, pcg_float(rng));
+	r.startt = advance_n_steps(tmin, make_cone(r.cone), pcg_float(rng));
 	r.idir = v3(1.0f / r.dn.x, 1.0f / r.dn.y, 1.0f / r.dn.z);
 	r.valid = true;
 	return r;
@@ -321,7 +340,7 @@ __device__ __forceinline__ bool scan_occupied_2load(V3 p, const uint8_t* bitfiel
 }
 
 template <uint32_t G>
-__device__ float sampling_end_row(V3 o, V3 d, V3 idir, float t_start, float cone, const Aabb& box, const uint8_t* bitfield,
+__device__ float sampling_end_row(V3 o, V3 d, V3 idir, float t_start, const Cone& cone, const Aabb& box, const uint8_t* bitfield,
                                   uint32_t max_cascade, uint32_t L) {
 	static_assert(G >= CASCADES, "one lane per mip");
 	float tmin, tmax;
@@ -390,19 +409,24 @@ struct RayGeo {  // per ray, count pass -> write pass
 template <bool CONE0>
 struct Marcher {
 	V3 o, dn, idir;
-	float cone;
+	Cone cone;
 	uint32_t max_cascade;
 	__device__ __forceinline__ V3 pos(float t) const { return v3(o.x + t * dn.x, o.y + t * dn.y, o.z + t * dn.z); }
-	__device__ __forceinline__ float dt_at(float t) const { return calc_dt(t, CONE0 ? 0.0f : cone); }
+	__device__ __forceinline__ Cone k() const { return CONE0 ? Cone{} : cone; }
+	__device__ __forceinline__ float dt_at(float t) const { return calc_dt(t, k()); }
 	__device__ __forceinline__ uint32_t mip_at(float dt, V3 p) const {
 		if (CONE0) return max_cascade == 0 ? 0u : mip_from_pos(p, max_cascade);
 		return mip_from_dt(dt, p, max_cascade);
 	}
 	__device__ __forceinline__ float step_occupied(float t) const { return t + dt_at(t); }
-	__device__ __forceinline__ float step_empty(float t) const {
+	// advance_to_next_voxel from t, sharing to_stepping_space(t) with calc_dt(t) (same values as
+	// evaluating both separately); *mip_out: the mip the sampler tests t's occupancy at.
+	__device__ __forceinline__ float step_empty(float t, uint32_t* mip_out = nullptr) const {
 		const V3 p = pos(t);
-		const uint32_t mip = mip_at(CONE0 ? 0.0f : dt_at(t), p);
-		return advance_to_next_voxel(t, CONE0 ? 0.0f : cone, p, dn, idir, mip);
+		const float n = to_stepping_space(t, k());
+		const uint32_t mip = mip_at(CONE0 ? 0.0f : from_stepping_space(n + 1.0f, k()) - t, p);
+		if (mip_out) *mip_out = mip;
+		return advance_to_next_voxel_n(t, n, k(), p, dn, idir, mip);
 	}
 };
 
@@ -419,15 +443,15 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 	uint32_t j = 0;
 	if (r.valid) {
 		const Aabb box = cfg_aabb(cfg);
-		const Marcher<CONE0> m{r.o, r.dn, r.idir, r.cone, cfg.max_cascade};
+		const Marcher<CONE0> m{r.o, r.dn, r.idir, make_cone(r.cone), cfg.max_cascade};
 		float t = r.startt;
 #if NGP_SAMPLER_DIAG == 2
 		const float t_end = 3.0e38f;
 #else
-		const float t_end = sampling_end_row<RG>(r.o, r.dn, r.idir, t, r.cone, box, a.bitfield, cfg.max_cascade, L);
+		const float t_end = sampling_end_row<RG>(r.o, r.dn, r.idir, t, m.cone, box, a.bitfield, cfg.max_cascade, L);
 #endif
 #if NGP_SAMPLER_DIAG == 1  // timing aid: sampling_end twice (cost of one = difference to the default build)
-		const float t_end2 = sampling_end_row<RG>(r.o, r.dn, r.idir, t + 0.0f * t_end, r.cone, box, a.bitfield, cfg.max_cascade, L);
+		const float t_end2 = sampling_end_row<RG>(r.o, r.dn, r.idir, t + 0.0f * t_end, m.cone, box, a.bitfield, cfg.max_cascade, L);
 		if (t_end2 != t_end) t = t_end2;
 #endif
 		float* tout = tbuf + (size_t)i * STEPS;
@@ -435,43 +459,49 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 		for (;;) {
 			// lanes [0, nvalid) take the next nvalid states of the sequential march, assuming it stays in
 			// the current mode (all occupied / all empty)
-			float tl, last;
-			uint32_t nvalid = RG;
-			if (CONE0 && occ_mode) {
-				// occupied run, cone 0: t_k ~ (t/MIN + k) * MIN. Guess every state from that lattice and
-				// verify all of them at once (lane L redoes the exact step from lane L-1's guess): the
-				// verified prefix is exact; the first lane that fails holds the exact state from its
-				// verified predecessor. A second round re-guesses the remaining lanes from there.
-				const float n0 = div_min_stepsize(t);
-				float cand = L == 0 ? t : (n0 + (float)L) * MIN_CONE_STEPSIZE;
-				float expct = m.step_occupied(dpp_shr1(cand));
-				uint32_t v = __builtin_ctz(row_ballot(L != 0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
-				if (v < RG) {
+			float tl, last;  // last: the state after lane RG-1's (the march continues there if every lane stays in the mode)
+			uint32_t mipl;   // the mip lane L's state is tested at
+			if (occ_mode) {
+				// Occupied run: t_{k+1} = t_k + calc_dt(t_k) = from(to(t_k) + 1) in stepping space, and
+				// to(from(n)) == n nearly always. Guess state L as from(to(t) + L) and verify every guess at
+				// once (lane L redoes the exact step from lane L-1's state): the verified prefix is exact; the
+				// first lane that fails takes the exact state from its verified predecessor and the lanes
+				// after it are re-guessed from there. Each round verifies at least one more lane, most runs
+				// take one round instead of a chain of RG dependent steps.
+				const float n0 = to_stepping_space(t, m.k());
+				float cand = L == 0 ? t : from_stepping_space(n0 + (float)L, m.k());
+				uint32_t v0 = 1;
+				float dt, nxt;
+				for (;;) {
+					dt = m.dt_at(cand);
+					nxt = cand + dt;  // step_occupied(cand)
+					const float expct = dpp_shr1(nxt);
+					const uint32_t v = __builtin_ctz(row_ballot(L >= v0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
+					if (v >= RG) break;
 					const float tv = __shfl(expct, (int)v, (int)RG);
-					const float nv = div_min_stepsize(tv);
-					cand = L < v ? cand : (L == v ? tv : (nv + (float)(L - v)) * MIN_CONE_STEPSIZE);
-					expct = m.step_occupied(dpp_shr1(cand));
-					v = __builtin_ctz(row_ballot(L > v && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
-					if (v < RG) {
-						if (L == v) cand = expct;
-						nvalid = v + 1;
-					}
+					cand = L < v ? cand : (L == v ? tv : from_stepping_space(to_stepping_space(tv, m.k()) + (float)(L - v), m.k()));
+					v0 = v + 1;
 				}
 				tl = cand;
-				last = 0.f;  // taken by shuffle below
+				mipl = m.mip_at(CONE0 ? 0.0f : dt, m.pos(tl));
+				last = __shfl(nxt, (int)(RG - 1), (int)RG);
 			} else {
-				// chain evaluated in order by every lane of the group; lane L keeps state L
+				// empty space: the chain evaluated in order by every lane of the group; lane L keeps state L
 				float tk = t;
 				tl = t;
+				mipl = 0;
 #pragma unroll
-				for (uint32_t k = 1; k < RG; ++k) {
-					tk = occ_mode ? m.step_occupied(tk) : m.step_empty(tk);
-					if (L == k) tl = tk;
+				for (uint32_t kk = 0; kk < RG; ++kk) {
+					uint32_t mk;
+					const float tn = m.step_empty(tk, &mk);
+					if (L == kk) { tl = tk; mipl = mk; }
+					tk = tn;
 				}
 				last = tk;
 			}
 			const V3 pos = m.pos(tl);
-			const uint32_t mip = m.mip_at(CONE0 ? 0.0f : m.dt_at(tl), pos);
+			const uint32_t mip = mipl;
+			constexpr uint32_t nvalid = RG;
 			const bool inside = L < nvalid && tl <= t_end && aabb_contains(box, pos) && (occ_mode ? j + L : j) < STEPS;
 			const bool occ = inside && density_grid_occupied_at(pos, a.bitfield, mip);
 			const uint32_t cont = row_ballot(inside && occ == occ_mode);
@@ -480,9 +510,8 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				if (L < f) tout[j + L] = tl;
 				j += f;
 			}
-			if (f >= nvalid) {  // every state taken stayed in the mode: continue from the last one
-				if (CONE0 && occ_mode) last = __shfl(tl, (int)(nvalid - 1), (int)RG);
-				t = occ_mode ? m.step_occupied(last) : m.step_empty(last);
+			if (f >= nvalid) {  // every state taken stayed in the mode: continue after the last one
+				t = last;
 				continue;
 			}
 			if (!((row_ballot(inside) >> f) & 1u)) break;  // left the aabb / sampling range / step budget
@@ -538,10 +567,11 @@ __global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg,
 	const V3 diag = v3(box.mx.x - box.mn.x, box.mx.y - box.mn.y, box.mx.z - box.mn.z);
 	const V3 wdir = v3((g.dn[0] + 1.0f) * 0.5f, (g.dn[1] + 1.0f) * 0.5f, (g.dn[2] + 1.0f) * 0.5f);
 	const float* tin = tbuf + (size_t)i * STEPS;
+	const Cone cone = make_cone(g.pad[0]);
 	for (uint32_t jj = L; jj < numsteps; jj += WG) {
 		const float t = tin[jj];
 		const V3 pos = v3(g.o[0] + t * g.dn[0], g.o[1] + t * g.dn[1], g.o[2] + t * g.dn[2]);
-		const float dt = calc_dt(t, g.pad[0]);
+		const float dt = calc_dt(t, cone);
 		float* c = a.coords + (size_t)(b + jj) * 7;
 		c[0] = (pos.x - box.mn.x) / diag.x; c[1] = (pos.y - box.mn.y) / diag.y; c[2] = (pos.z - box.mn.z) / diag.z;
 		c[3] = warp_dt(dt);
@@ -1049,7 +1079,7 @@ __device__ void ld_random_pixel_offset(uint32_t spp, float* ox, float* oy) {  //
 }
 
 // if_unoccupied_advance_to_next_occupied_voxel<MIP_FROM_DT = false> (testbed_nerf.cu:811-842)
-__device__ float advance_to_occupied(float t, float cone, V3 o, V3 d, V3 idir, const uint8_t* bitfield, uint32_t min_mip,
+__device__ float advance_to_occupied(float t, const Cone& cone, V3 o, V3 d, V3 idir, const uint8_t* bitfield, uint32_t min_mip,
                                      uint32_t max_mip, const Aabb& box) {
 	while (true) {
 		const V3 pos = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);
@@ -1101,8 +1131,9 @@ __global__ void k_render_init(RenderArgs a, Payload* __restrict__ pay, float* __
 	if (aabb_contains(box, v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z))) {
 		// advance_pos_nerf (:844-900): jitter the start by a scrambled-Sobol fraction of a step
 		const V3 idir = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-		t = advance_n_steps(t, a.cone_angle_constant, ld_random_val(a.sample_index, i * 786433u));
-		t = advance_to_occupied(t, a.cone_angle_constant, o, d, idir, a.bitfield, 0, a.max_mip, box);
+		const Cone cone = make_cone(a.cone_angle_constant);
+		t = advance_n_steps(t, cone, ld_random_val(a.sample_index, i * 786433u));
+		t = advance_to_occupied(t, cone, o, d, idir, a.bitfield, 0, a.max_mip, box);
 		if (t < 16384.0f) p.alive = 1;
 	}
 	p.t = t;
@@ -1138,7 +1169,7 @@ __global__ void k_render_inputs(RenderArgs a, uint32_t n, uint32_t n_steps, Payl
 	const V3 idir = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 	const Aabb box{v3(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v3(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
 	const V3 diag = v3(box.mx.x - box.mn.x, box.mx.y - box.mn.y, box.mx.z - box.mn.z);
-	const float cone = a.cone_angle_constant;
+	const Cone cone = make_cone(a.cone_angle_constant);
 	float t = p.t;
 	for (uint32_t j = 0; j < n_steps; ++j) {
 		t = advance_to_occupied(t, cone, o, d, idir, a.bitfield, 0, a.max_mip, box);

@@ -17,16 +17,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--data", default=os.path.join(ROOT, "data", "fox"))
-    ap.add_argument("--seconds", type=float, default=30.0)
-    ap.add_argument("--holdout", type=int, default=10, help="every N-th frame is held out for evaluation (0: none)")
-    ap.add_argument("--eval-views", type=int, default=5)
-    ap.add_argument("--spp", type=int, default=1)
-    args = ap.parse_args()
-    from __graft_entry__ import load_package
-    pkg = load_package()
+DEFAULT_DATA = os.path.join(ROOT, "data", "fox")
+
+
+def run(pkg, data=DEFAULT_DATA, seconds=30.0, holdout=10, eval_views=5, spp=1):
+    """Train on the fox capture for `seconds` of wall clock and evaluate; returns the result dict."""
+    args = argparse.Namespace(data=data, seconds=seconds, holdout=holdout, eval_views=eval_views, spp=spp)
     t0 = time.time()
     d = pkg.nerf_data.load_nerf(args.data)
     t_load = time.time() - t0
@@ -69,7 +65,7 @@ def main():
     torch.cuda.synchronize()
     t_render = time.time() - t_render
     h, w = d.rgba8[0].shape[:2]
-    print(json.dumps({
+    return {
         "metric": "training samples/sec + PSNR, NeRF fox (C3) on 1 MI355X",
         "value": samples / t_train, "unit": "samples/s",
         "psnr_heldout": float(np.mean(ps)) if ps else None, "psnr_views": [round(p, 2) for p in ps],
@@ -83,7 +79,20 @@ def main():
                    "batch": 1 << 18},
         "load_seconds": round(t_load, 2), "upload_seconds": round(t_upload, 2), "render_seconds": round(t_render, 2),
         "loss_curve": curve[:40],
-    }), flush=True)
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--data", default=DEFAULT_DATA)
+    ap.add_argument("--seconds", type=float, default=30.0)
+    ap.add_argument("--holdout", type=int, default=10, help="every N-th frame is held out for evaluation (0: none)")
+    ap.add_argument("--eval-views", type=int, default=5)
+    ap.add_argument("--spp", type=int, default=1)
+    args = ap.parse_args()
+    from __graft_entry__ import load_package
+    pkg = load_package()
+    print(json.dumps(run(pkg, args.data, args.seconds, args.holdout, args.eval_views, args.spp)), flush=True)
 
 
 if __name__ == "__main__":

@@ -26,12 +26,18 @@ def main():
     ap.add_argument("--res", type=int, default=800)
     ap.add_argument("--pipeline", type=int, default=1, help="1: next step's sampler under the training pass (default), 0: serial step")
     ap.add_argument("--option", action="append", default=[], help="model option key=value (ngp_model_set_option)")
+    ap.add_argument("--fox", action="store_true", help="the fox capture (data/fox, tools/stage_fox.sh) instead of the stand-in")
     args = ap.parse_args()
     from __graft_entry__ import load_package
     pkg = load_package()
-    S = pkg.synthetic
-    ds = S.lego_like_dataset(n_images=args.images, width=args.res, height=args.res, seed=0, device="cuda")
-    cfg = pkg.nerf.default_config(1.0)
+    if args.fox:
+        d = pkg.nerf_data.load_nerf(os.path.join(ROOT, "data", "fox"))
+        ds = pkg.nerf.NerfDataset(d.images, d.rgba8)
+        cfg = pkg.nerf.default_config(d.aabb_scale)
+    else:
+        S = pkg.synthetic
+        ds = S.lego_like_dataset(n_images=args.images, width=args.res, height=args.res, seed=0, device="cuda")
+        cfg = pkg.nerf.default_config(1.0)
     ncfg = pkg.nerf_config("C2")
     net = pkg.create_nerf_network(ncfg)
     tr = pkg.Trainer(net, ncfg["optimizer"])
