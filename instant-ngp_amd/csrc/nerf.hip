@@ -28,14 +28,25 @@ __device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}
 // t / MIN_CONE_STEPSIZE, correctly rounded, in three instructions: q = t * RN(1/c) and one residual
 // correction. Checked exhaustively against the IEEE quotient for every float t >= 0
 // (tools/microbench/div_check.c): equal for 1.5e-31 <= t <= 5.7e35; outside that the IEEE divide runs.
+// Both the quotient and the residual step are odd in t, so the same holds for -t (the linear segment
+// below `at` divides t - at <= 0).
 __device__ __forceinline__ float div_min_stepsize(float t) {
 	constexpr float c = MIN_CONE_STEPSIZE;
 	const float r = 1.0f / c;  // folded to RN(1/c) at compile time
-	if (__builtin_expect(t >= 1e-30f && t <= 1e35f, 1)) {
+	const float at = fabsf(t);
+	if (__builtin_expect(at >= 1e-30f && at <= 1e35f, 1)) {
 		const float q = t * r;
 		return __builtin_fmaf(__builtin_fmaf(-q, c, t), r, q);
 	}
 	return t / c;
+}
+// x / MAX_CONE_STEPSIZE: MAX = MIN * 2^10 exactly, so (barring subnormals, excluded by the range test)
+// RN(x / MAX) = RN(x / MIN) * 2^-10.
+static_assert(MAX_CONE_STEPSIZE == MIN_CONE_STEPSIZE * 1024.0f, "MAX_CONE_STEPSIZE = MIN * 2^10");
+__device__ __forceinline__ float div_max_stepsize(float t) {
+	const float at = fabsf(t);
+	if (__builtin_expect(at >= 1e-30f && at <= 1e35f, 1)) return div_min_stepsize(t) * (1.0f / 1024.0f);
+	return t / MAX_CONE_STEPSIZE;
 }
 
 // testbed_nerf.cu:114-184. The constants of a cone angle (log(1 + cone), the two linear segments'
@@ -43,12 +54,13 @@ __device__ __forceinline__ float div_min_stepsize(float t) {
 // software logf/expf (ngp_math.h) they are ~10 transcendental evaluations per call. Same operations
 // and values as evaluating them inline.
 struct Cone {
-	float c, log1p_c, a, b, at, bt;
+	float c, log1p_c, a, b, at, bt, rl;  // rl = RN(1 / log1p_c)
 };
 __device__ __forceinline__ Cone make_cone(float c) {
-	Cone k{c, 0.f, 0.f, 0.f, 0.f, 0.f};
+	Cone k{c, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 	if (c <= 1e-5f) return k;
 	k.log1p_c = ngp_logf(1.0f + c);
+	k.rl = 1.0f / k.log1p_c;
 	k.a = (ngp_logf(MIN_CONE_STEPSIZE) - ngp_logf(k.log1p_c)) / k.log1p_c;
 	k.b = (ngp_logf(MAX_CONE_STEPSIZE) - ngp_logf(k.log1p_c)) / k.log1p_c;
 	k.at = ngp_expf(k.a * k.log1p_c);
@@ -61,9 +73,9 @@ __device__ __forceinline__ Cone make_cone(float c) {
 #endif
 __device__ float to_stepping_space(float t, const Cone& k) {
 	if (k.c <= 1e-5f) return div_min_stepsize(t);
-	if (t <= k.at) return (t - k.at) / MIN_CONE_STEPSIZE + k.a;
-	if (t <= k.bt) return ngp_logf(t) / k.log1p_c;
-	return (t - k.bt) / MAX_CONE_STEPSIZE + k.b;
+	if (t <= k.at) return div_min_stepsize(t - k.at) + k.a;
+	if (t <= k.bt) return ngp_div_rc(ngp_logf(t), k.log1p_c, k.rl);
+	return div_max_stepsize(t - k.bt) + k.b;
 }
 __device__ float from_stepping_space(float n, const Cone& k) {
 	if (k.c <= 1e-5f) return n * MIN_CONE_STEPSIZE;
@@ -342,7 +354,7 @@ __device__ __forceinline__ bool scan_occupied_2load(V3 p, const uint8_t* bitfiel
 template <uint32_t G>
 __device__ float sampling_end_row(V3 o, V3 d, V3 idir, float t_start, const Cone& cone, const Aabb& box, const uint8_t* bitfield,
                                   uint32_t max_cascade, uint32_t L) {
-	static_assert(G >= CASCADES, "one lane per mip");
+	static_assert(G >= CASCADES || 2 * G == CASCADES, "one lane per mip, or two");
 	float tmin, tmax;
 	aabb_ray_intersect(box, o, d, &tmin, &tmax);
 	if (!(tmax < 3.0e38f)) return t_start;
@@ -356,7 +368,12 @@ __device__ float sampling_end_row(V3 o, V3 d, V3 idir, float t_start, const Cone
 		const uint32_t mL = mu + L;
 		const bool probe = mL < CASCADES;
 		const bool occ = probe && scan_occupied_2load(p, bitfield, probe ? mL : 0u);
-		const uint32_t bits = (uint32_t)(__ballot(occ) >> shift) & ((1u << G) - 1u);
+		uint32_t bits = (uint32_t)(__ballot(occ) >> shift) & ((1u << G) - 1u);
+		if (G < CASCADES) {  // lanes probe mips mu + L and mu + L + G
+			const bool probe2 = mL + G < CASCADES;
+			const bool occ2 = probe2 && scan_occupied_2load(p, bitfield, probe2 ? mL + G : 0u);
+			bits |= ((uint32_t)(__ballot(occ2) >> shift) & ((1u << G) - 1u)) << G;
+		}
 		if (bits & 1u) return t + 2.0f * SQRT3 / scalbnf((float)GRIDSIZE, -(int)mu);
 		const uint32_t m = bits ? mu + __builtin_ctz(bits) - 1u : CASCADES - 1u;
 		const float res = scalbnf((float)GRIDSIZE, -(int)m);
@@ -384,7 +401,10 @@ __device__ float sampling_end_row(V3 o, V3 d, V3 idir, float t_start, const Cone
 constexpr uint32_t RG = NGP_SAMPLER_RG;  // lanes per ray (16 = one DPP row)
 
 constexpr uint32_t LG = 16;  // lanes per ray in the loss passes: one DPP row
-static_assert(RG >= 8 && RG <= 16 && (RG & (RG - 1)) == 0, "sampler group: 8 or 16 lanes");
+static_assert(RG >= 4 && RG <= 16 && (RG & (RG - 1)) == 0, "sampler group: 4, 8 or 16 lanes");
+#ifndef NGP_SAMPLER_BLOCK
+#define NGP_SAMPLER_BLOCK 256
+#endif
 
 __device__ __forceinline__ uint32_t row_ballot(bool p) {  // this ray's RG lanes of a wave ballot
 	const unsigned long long b = __ballot(p);
@@ -421,14 +441,64 @@ struct Marcher {
 	__device__ __forceinline__ float step_occupied(float t) const { return t + dt_at(t); }
 	// advance_to_next_voxel from t, sharing to_stepping_space(t) with calc_dt(t) (same values as
 	// evaluating both separately); *mip_out: the mip the sampler tests t's occupancy at.
+	// In the exponential segment of the stepping space two of the step's four transcendentals only
+	// decide integers: the mip (the binary exponent of calc_dt(t) * 2 GRIDSIZE) and the number of
+	// stepping-space steps to the next voxel (a ceil). Both are first taken from hardware exp/log
+	// (relative error ~1e-6, bound below) and recomputed exactly only when the approximate value lies
+	// within a margin (>= 10x that error) of a decision boundary: same integers as the exact evaluation.
 	__device__ __forceinline__ float step_empty(float t, uint32_t* mip_out = nullptr) const {
 		const V3 p = pos(t);
 		const float n = to_stepping_space(t, k());
-		const uint32_t mip = mip_at(CONE0 ? 0.0f : from_stepping_space(n + 1.0f, k()) - t, p);
+		uint32_t mip;
+		if (CONE0) {
+			mip = mip_at(0.0f, p);
+		} else {
+			const float n1 = n + 1.0f;
+			float dt;
+			if (n1 > cone.a && n1 <= cone.b) {
+				// from_stepping_space(n1) = ngp_expf(n1 * log1p_c); __expf: v_exp_f32 (~2 ulp) of
+				// the same argument, so dt * 2 GRIDSIZE is off by <= ~3e-7 * t / dt ~ 1e-4 relative
+				dt = __expf(n1 * cone.log1p_c) - t;
+				int e;
+				const float mant = frexpf(dt * (2 * GRIDSIZE), &e);  // boundaries: mantissa 0.5 (= powers of two)
+				if (mant < 0.5005f || mant > 0.9995f) dt = from_stepping_space(n1, cone) - t;
+			} else {
+				dt = from_stepping_space(n1, cone) - t;
+			}
+			mip = mip_at(dt, p);
+		}
 		if (mip_out) *mip_out = mip;
-		return advance_to_next_voxel_n(t, n, k(), p, dn, idir, mip);
+		if (CONE0) return advance_to_next_voxel_n(t, n, k(), p, dn, idir, mip);
+		const float res = scalbnf((float)GRIDSIZE, -(int)mip);
+		const float target = t + distance_to_next_voxel(p, dn, idir, res);
+		float x;
+		if (target > cone.at && target <= cone.bt) {
+			// to_stepping_space(target) = ngp_logf(target) / log1p_c; __logf (v_log_f32) is within
+			// ~1e-6 absolute for target in (at, bt], i.e. ~3e-4 stepping-space units at cone 1/256
+			x = __logf(target) * cone.rl - n;
+			if (fabsf(x - rintf(x)) < 4e-3f) x = to_stepping_space(target, cone) - n;
+		} else {
+			x = to_stepping_space(target, cone) - n;
+		}
+		return from_stepping_space(n + ceilf(fmaxf(x, 0.5f)), cone);
 	}
 };
+
+#if NGP_SAMPLER_DIAG == 4  // instrumentation aid: per-ray march statistics (tools/nerf_step_profile.py --sampler-stats)
+// [0] empty iterations [1] occupied iterations [2] occupied verify rounds [3] rays [4] occupied states
+// [5] max iterations of one ray [6] empty-mode exits (mode switches) [8 + b] rays with 2^b <= iterations < 2^(b+1)
+__device__ unsigned long long g_sampler_stats[48];
+extern "C" __attribute__((visibility("default"))) int ngp_debug_sampler_stats(unsigned long long* out, int n) {
+	if (!out) {
+		static const unsigned long long z[48] = {};
+		return hipMemcpyToSymbol(HIP_SYMBOL(g_sampler_stats), z, sizeof(z)) == hipSuccess ? 0 : -1;
+	}
+	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sampler_stats), sizeof(unsigned long long) * (n < 48 ? n : 48)) == hipSuccess ? 0 : -1;
+}
+#define SAMPLER_STAT(x) x
+#else
+#define SAMPLER_STAT(x)
+#endif
 
 // generate_training_samples_nerf pass 1: count the occupied steps of each ray, keep their t.
 template <bool CONE0>
@@ -456,7 +526,9 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 #endif
 		float* tout = tbuf + (size_t)i * STEPS;
 		bool occ_mode = false;  // rays enter the aabb in empty space far more often than not
+		SAMPLER_STAT(uint32_t st_e = 0; uint32_t st_o = 0; uint32_t st_r = 0; uint32_t st_x = 0;)
 		for (;;) {
+			SAMPLER_STAT(if (occ_mode) ++st_o; else ++st_e;)
 			// lanes [0, nvalid) take the next nvalid states of the sequential march, assuming it stays in
 			// the current mode (all occupied / all empty)
 			float tl, last;  // last: the state after lane RG-1's (the march continues there if every lane stays in the mode)
@@ -473,6 +545,7 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				uint32_t v0 = 1;
 				float dt, nxt;
 				for (;;) {
+					SAMPLER_STAT(++st_r;)
 					dt = m.dt_at(cand);
 					nxt = cand + dt;  // step_occupied(cand)
 					const float expct = dpp_shr1(nxt);
@@ -490,7 +563,7 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				float tk = t;
 				tl = t;
 				mipl = 0;
-#pragma unroll
+#pragma unroll 1  // rolled: the unrolled chain (8 inlined steps) overflowed the instruction cache
 				for (uint32_t kk = 0; kk < RG; ++kk) {
 					uint32_t mk;
 					const float tn = m.step_empty(tk, &mk);
@@ -518,8 +591,19 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			const float tf = __shfl(tl, (int)f, (int)RG);
 			if (occ_mode) t = m.step_empty(tf);  // empty cell at lane f: advance_to_next_voxel
 			else t = tf;                          // occupied cell at lane f: sample it next
+			SAMPLER_STAT(st_x += occ_mode ? 0u : 1u;)
 			occ_mode = !occ_mode;
 		}
+		SAMPLER_STAT(if (L == 0) {
+			atomicAdd(&g_sampler_stats[0], (unsigned long long)st_e);
+			atomicAdd(&g_sampler_stats[1], (unsigned long long)st_o);
+			atomicAdd(&g_sampler_stats[2], (unsigned long long)st_r);
+			atomicAdd(&g_sampler_stats[3], 1ull);
+			atomicAdd(&g_sampler_stats[4], (unsigned long long)j);
+			atomicMax(&g_sampler_stats[5], (unsigned long long)(st_e + st_o));
+			atomicAdd(&g_sampler_stats[6], (unsigned long long)st_x);
+			atomicAdd(&g_sampler_stats[8 + (31 - __builtin_clz(st_e + st_o))], 1ull);
+		})
 	}
 	if (L == 0) {
 		nsteps[i] = j;
@@ -602,13 +686,13 @@ void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs
 	uint32_t* slot = tmp + 3 * (size_t)a.n_rays;
 	float* tbuf = tmpf;
 	RayGeo* geo = (RayGeo*)(tmpf + (size_t)a.n_rays * STEPS);
-	const uint32_t blocks = div_round_up((size_t)a.n_rays * RG, 256);
+	const uint32_t blocks = div_round_up((size_t)a.n_rays * RG, NGP_SAMPLER_BLOCK);
 	{
 		ProfScope ps("sample_count", s);
 		if (cfg.cone_angle_constant <= 1e-5f)
-			k_sample_count<true><<<blocks, 256, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo);
+			k_sample_count<true><<<blocks, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo);
 		else
-			k_sample_count<false><<<blocks, 256, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo);
+			k_sample_count<false><<<blocks, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo);
 		NGP_HIP(hipGetLastError());
 	}
 	{

@@ -99,4 +99,18 @@ NGP_MATH_FN float ngp_logf(float x) {
 	return dk * 6.9313812256e-01f - ((hfsq - (s * (hfsq + R) + dk * 9.0580006145e-06f)) - f);
 }
 
+/* x / c given rc = RN(1/c) (computed once with an IEEE division): q = x rc refined by one fused
+ * residual step (Markstein), three dependent operations instead of the IEEE division sequence. Used for
+ * the stepping-space division by log(1 + cone) (testbed_nerf.cu:114-184), on both sides. Equal to the
+ * IEEE quotient for every x at the default cone 1/256 (tools/microbench/div_check.c, exhaustive over
+ * the range below); outside 2^-100 <= |x| <= 2^100 it is the IEEE division. */
+NGP_MATH_FN float ngp_div_rc(float x, float c, float rc) {
+	const float ax = x < 0.0f ? -x : x;
+	if (ax >= 7.88860905221011805e-31f && ax <= 1.26765060022822940e30f) {
+		const float q = x * rc;
+		return NGP_FMAF(NGP_FMAF(-q, c, x), rc, q);
+	}
+	return x / c;
+}
+
 #endif /* NGP_MATH_H */

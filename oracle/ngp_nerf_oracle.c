@@ -107,7 +107,7 @@ static float to_step(float t, float c) {
 	float a = (ngp_logf(MIN_STEP) - ngp_logf(l)) / l, b = (ngp_logf(MAX_STEP) - ngp_logf(l)) / l;
 	float at = ngp_expf(a * l), bt = ngp_expf(b * l);
 	if (t <= at) return (t - at) / MIN_STEP + a;
-	else if (t <= bt) return ngp_logf(t) / l;
+	else if (t <= bt) return ngp_div_rc(ngp_logf(t), l, 1.0f / l);
 	else return (t - bt) / MAX_STEP + b;
 }
 static float from_step(float n, float c) {

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--pipeline", type=int, default=1, help="1: next step's sampler under the training pass (default), 0: serial step")
     ap.add_argument("--option", action="append", default=[], help="model option key=value (ngp_model_set_option)")
     ap.add_argument("--fox", action="store_true", help="the fox capture (data/fox, tools/stage_fox.sh) instead of the stand-in")
+    ap.add_argument("--sampler-stats", action="store_true",
+                    help="read the march statistics of a -DNGP_SAMPLER_DIAG=4 build (NGP_ENGINE_LIB) over the measured steps")
     args = ap.parse_args()
     from __graft_entry__ import load_package
     pkg = load_package()
@@ -56,6 +58,8 @@ def main():
     t_warm = time.time() - t0
     lib.ngp_profiler_reset()
     lib.ngp_profiler_enable(1)
+    if args.sampler_stats:
+        lib.ngp_debug_sampler_stats(None, 0)
     rays, pre, comp = [], [], []
     t0 = time.time()
     for _ in range(args.measure):
@@ -70,6 +74,15 @@ def main():
     buf = ctypes.create_string_buffer(need)
     lib.ngp_profiler_read(buf, need)
     k = json.loads(buf.value.decode())
+    stats = None
+    if args.sampler_stats:
+        raw = (ctypes.c_uint64 * 48)()
+        lib.ngp_debug_sampler_stats(raw, 48)
+        n = max(raw[3], 1)
+        stats = {"rays": raw[3], "empty_iters_per_ray": raw[0] / n, "occ_iters_per_ray": raw[1] / n,
+                 "occ_rounds_per_occ_iter": raw[2] / max(raw[1], 1), "occ_states_per_ray": raw[4] / n,
+                 "max_iters_one_ray": raw[5], "empty_exits_per_ray": raw[6] / n,
+                 "iters_log2_hist": {f"{1 << b}": raw[8 + b] for b in range(32) if raw[8 + b]}}
     phases = {n: {"calls": v["calls"], "ms_per_call": round(v["ms"] / max(v["calls"], 1), 4),
                   "ms_per_step": round(v["ms"] / args.measure, 4)} for n, v in sorted(k.items())}
     print(json.dumps({
@@ -77,7 +90,7 @@ def main():
         "ms_per_step_wall": round(1e3 * dt / args.measure, 4),
         "rays_per_batch": float(np.mean(rays)), "samples_before_compaction": float(np.mean(pre)),
         "compacted_samples": float(np.mean(comp)),
-        "samples_per_s": float(np.sum(comp) / dt), "phases": phases}, indent=1), flush=True)
+        "samples_per_s": float(np.sum(comp) / dt), "phases": phases, "sampler_stats": stats}, indent=1), flush=True)
 
 
 if __name__ == "__main__":
