@@ -67,10 +67,6 @@ __device__ __forceinline__ Cone make_cone(float c) {
 	k.bt = ngp_expf(k.b * k.log1p_c);
 	return k;
 }
-#if NGP_SAMPLER_DIAG == 3  // timing aid only (not bit-exact): hardware log/exp in the stepping space
-#define ngp_logf __logf
-#define ngp_expf __expf
-#endif
 __device__ float to_stepping_space(float t, const Cone& k) {
 	if (k.c <= 1e-5f) return div_min_stepsize(t);
 	if (t <= k.at) return div_min_stepsize(t - k.at) + k.a;
@@ -83,10 +79,6 @@ __device__ float from_stepping_space(float n, const Cone& k) {
 	if (n <= k.b) return ngp_expf(n * k.log1p_c);
 	return (n - k.b) * MAX_CONE_STEPSIZE + k.bt;
 }
-#if NGP_SAMPLER_DIAG == 3
-#undef ngp_logf
-#undef ngp_expf
-#endif
 __device__ __forceinline__ float advance_n_steps(float t, const Cone& k, float n) { return from_stepping_space(to_stepping_space(t, k) + n, k); }
 __device__ __forceinline__ float calc_dt(float t, const Cone& k) { return advance_n_steps(t, k, 1.0f) - t; }
 
