@@ -71,6 +71,13 @@ def synthetic_batch(n, seed, device):
         blob = np.clip(0.5 + 0.06 * g.standard_normal((n, 3)), 0.0, 1.0).astype(np.float32)
         keep = g.random(n) < 0.8
         c[keep, :3] = blob[keep]
+    if os.environ.get("NGP_BENCH_POINTS") == "sorted":  # experiment: spatially coherent batch (Morton order)
+        q = np.minimum((c[:, :3] * 128).astype(np.uint64), 127)
+        key = np.zeros(n, np.uint64)
+        for b in range(7):
+            for d in range(3):
+                key |= ((q[:, d] >> np.uint64(b)) & np.uint64(1)) << np.uint64(3 * b + d)
+        c[:, :3] = c[np.argsort(key, kind="stable"), :3]
     c[:, 3] = 0.0
     d = g.standard_normal((n, 3))
     c[:, 4:] = (d / np.linalg.norm(d, axis=1, keepdims=True) + 1) / 2
