@@ -151,6 +151,7 @@ struct ngp_model {
 	uint32_t overlap = 0;
 	bool fused_hist = true;                 // option "fused_hist": bucket histogram inside the training forward
 	bool fuse_infer = true;                 // option "fuse_infer": NerfNetwork inference encodes inside the MLP kernel
+	bool fuse_slabs = true;                 // option "fuse_slabs": dW slab reduction inside the grid backward's last kernel
 	bool fuse_train = false;                // option "fuse_train": ... and the training forward_backward too (off: the
 	                                        // training kernel runs 1 wave/SIMD, the gathers are not hidden; C2 0.157 -> 0.161 ms)
 	int grid_forward_mode = 0;              // option "grid_forward_mode": 0 auto, 1 per-sample rows, 2 XCD-partitioned
@@ -349,8 +350,13 @@ struct ngp_model {
 		run_mlp(s, encbuf ? MLP_TRAIN : MLP_TRAIN_ENC, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride,
 		        dL_denc, slab, false);
 		// the dW slab reduction (MLP section of the gradient) and the grid backward (grid section) are
-		// independent: for large batches the reduction runs on the side stream under the grid backward
+		// independent: for large batches the reduction runs in extra blocks of the grid backward's last
+		// kernel (fuse_slabs, default), or on the side stream under it (overlap bit 4)
 		const bool ovl = use_sorted(n) && (overlap & 4);
+		const bool fused = use_sorted(n) && !ovl && fuse_slabs;
+		SlabJob sj;
+		sj.slabs = slab; sj.n_slabs = blocks; sj.n = (uint32_t)n_matrix(); sj.grad = gradients;
+		sj.accumulate = grad_mode == NGP_GRAD_ACCUMULATE;
 		hipStream_t rs = s;
 		if (ovl) {
 			ensure_side_stream();
@@ -358,18 +364,18 @@ struct ngp_model {
 			NGP_HIP(hipStreamWaitEvent(side, ev_mlp, 0));
 			rs = side;
 		}
-		{
+		if (!fused) {
 			ProfScope ps("reduce_slabs", rs);
 			reduce_slabs(slab, blocks, (uint32_t)n_matrix(), gradients, grad_mode == NGP_GRAD_ACCUMULATE, rs);
 		}
 		if (ovl) NGP_HIP(hipEventRecord(ev_red, side));
 		GridBwdArgs b{n, in, stride, dL_denc, enc_width, AoS, gradients + grid_offset(), max_level, max_level_per_sample};
-		scatter_grid_grad(s, b, grad_mode != NGP_GRAD_ACCUMULATE);
+		scatter_grid_grad(s, b, grad_mode != NGP_GRAD_ACCUMULATE, fused ? &sj : nullptr);
 		if (ovl) NGP_HIP(hipStreamWaitEvent(s, ev_red, 0));
 	}
 	// Hash-grid backward: destination-bucketed exact sums (n >= 4096, or mode 3), else tcnn-style direct
 	// packed-f16 atomics (small batches, where the bucket plan costs more than the atomics).
-	void scatter_grid_grad(hipStream_t s, GridBwdArgs b, bool overwrite) {
+	void scatter_grid_grad(hipStream_t s, GridBwdArgs b, bool overwrite, const SlabJob* slab = nullptr) {
 		if (use_sorted(b.n)) {
 			void* ws = sorted_workspace(b.n);
 			if (sc_prepared) {
@@ -381,9 +387,10 @@ struct ngp_model {
 			}
 			sc_hist_done = false;
 			ProfScope ps("grid_backward_sorted", s);
-			grid_backward_sorted(grid, b, sc_plan, ws, s, overwrite, win_debug);
+			grid_backward_sorted(grid, b, sc_plan, ws, s, overwrite, win_debug, slab);
 			return;
 		}
+		NGP_CHECK(!slab, "fused slab reduction needs the sorted grid backward");
 		if (overwrite) {
 			ProfScope ps("grid_grad_zero", s);
 			NGP_HIP(hipMemsetAsync(b.grad, 0, grid_params * sizeof(f16), s));
@@ -626,6 +633,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			m->fuse_infer = value != 0;
 		} else if (k == "fuse_train") {
 			m->fuse_train = value != 0;
+		} else if (k == "fuse_slabs") {
+			m->fuse_slabs = value != 0;
 		} else if (k == "win_debug") {
 			m->win_debug = (uint32_t)value;
 		} else {

@@ -1,6 +1,7 @@
 // grid_scatter.h — destination-bucketed hash-grid backward (see grid_scatter.hip).
 #pragma once
 #include "grid.h"
+#include "slab_reduce.h"
 
 namespace ngp {
 
@@ -32,7 +33,9 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& b, const Scatter
 bool scatter_hist(const GridDesc& g, const ScatterPlan& p, void* workspace, GridHist& h);
 // Phase 2: dL/dy -> gradient. overwrite: b.grad's grid section is fully written (no memset needed);
 // otherwise the sums are added to it. Same level masking as grid_backward.
+// slab (optional): the MLP's dW slab reduction, run in extra blocks of the last backward kernel
+// (same arithmetic as reduce_slabs, no launch of its own).
 void grid_backward_sorted(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace,
-                          hipStream_t s, bool overwrite, uint32_t debug = 0);
+                          hipStream_t s, bool overwrite, uint32_t debug = 0, const SlabJob* slab = nullptr);
 
 }  // namespace ngp

@@ -492,12 +492,20 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 }
 
 // One workgroup per split bucket: sum its parts' int64 partials (exact, so the order is immaterial)
-// and write every entry once — no fp16 atomics, bitwise reproducible.
+// and write every entry once — no fp16 atomics, bitwise reproducible. Columns x >= slab_x0 of the grid
+// run the MLP's dW slab reduction (SlabJob) instead: this kernel leaves most of the chip idle, so the
+// reduction fits beside it.
 template <uint32_t F>
 __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst c, const Levels lv, uint32_t B,
                                                                 const uint32_t* __restrict__ split, const uint32_t* __restrict__ splitb,
                                                                 const unsigned long long* __restrict__ scratch, f16* __restrict__ grad,
-                                                                bool overwrite) {
+                                                                bool overwrite, const SlabJob sj, uint32_t slab_x0) {
+	static_assert(SC_THREADS == SLAB_THREADS, "slab blocks share the split-reduce block shape");
+	if (blockIdx.x >= slab_x0) {
+		const uint32_t blk = blockIdx.y * (gridDim.x - slab_x0) + (blockIdx.x - slab_x0);
+		if (blk < slab_blocks(sj.n)) reduce_slabs_block(sj, blk);
+		return;
+	}
 	// grid (split bucket, 256-pair chunk): one pair per thread, the parts' loads 8 at a time
 	if (blockIdx.x >= split[1]) return;
 	const uint32_t vb = splitb[3 * blockIdx.x], first = splitb[3 * blockIdx.x + 1], parts = splitb[3 * blockIdx.x + 2];
@@ -551,7 +559,7 @@ Levels make_levels(const GridDesc& g, uint32_t B) {
 
 template <uint32_t D>
 void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const GridBwdArgs& a, const ScatterPlan& p, char* ws,
-                     hipStream_t s, bool overwrite, uint32_t debug) {
+                     hipStream_t s, bool overwrite, uint32_t debug, const SlabJob* slab) {
 	const uint32_t* tot = (const uint32_t*)(ws + p.off_tot);
 	const uint32_t* cur_t = (const uint32_t*)(ws + p.off_cur);
 	const uint32_t* split = (const uint32_t*)(ws + p.off_split);
@@ -571,8 +579,11 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		accum<<<p.max_split_blocks + p.n_buckets, SC_BT, SC_LDS_BYTES + SC_LDS_PAD_BYTES, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
 		                                                                     val, a.grad, overwrite, split, scratch, debug);
 		NGP_HIP(hipGetLastError());
-		const dim3 grid_r(p.max_split_buckets, div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS));
-		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite);
+		const uint32_t gy = (uint32_t)div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS);
+		const SlabJob sj = slab ? *slab : SlabJob{};
+		const uint32_t slab_x = slab ? (uint32_t)div_round_up(slab_blocks(sj.n), gy) : 0u;
+		const dim3 grid_r(p.max_split_buckets + slab_x, gy);
+		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets);
 		NGP_HIP(hipGetLastError());
 	};
 	auto by_chunk = [&](auto sc512, auto sc1024, auto accum, auto splitr) {
@@ -673,13 +684,13 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const Scatter
 }
 
 void grid_backward_sorted(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace, hipStream_t s,
-                          bool overwrite, uint32_t debug) {
+                          bool overwrite, uint32_t debug, const SlabJob* slab) {
 	if (b.n == 0) return;
 	NGP_CHECK(b.level_begin == 0, "grid_backward_sorted handles all levels");
 	const GridConst c = make_grid_const(g);
 	const Levels lv = make_levels(g, p.B);
-	if (g.n_dims == 3) launch_backward<3>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug);
-	else launch_backward<2>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug);
+	if (g.n_dims == 3) launch_backward<3>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab);
+	else launch_backward<2>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab);
 }
 
 }  // namespace ngp

@@ -1,6 +1,7 @@
 // mlp.hip — MFMA kernels for the NerfNetwork MLP pair and for a single MLP (see mlp.h for the
 // register/LDS layout contract).
 #include "mlp.h"
+#include "slab_reduce.h"
 
 #include <type_traits>
 
@@ -1251,37 +1252,12 @@ void mlp_run(const MlpPlan& p, MlpMode mode, const MlpArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Block = 32 parameters x 8 slab groups; each thread sums every 8th slab of one parameter, then the 8
-// partial sums are added in a fixed order (deterministic).
-__global__ void __launch_bounds__(256) k_reduce_slabs(const float* __restrict__ slabs, uint32_t n_slabs, uint32_t n,
-                                                      f16* __restrict__ grad, bool accumulate) {
-	__shared__ float part[8][33];
-	const uint32_t p = blockIdx.x * 32 + (threadIdx.x & 31), g = threadIdx.x >> 5;
-	float s = 0.f;
-	if (p < n) {
-		// 8 independent loads in flight per step (the adds stay in slab order: deterministic)
-		uint32_t b = g;
-		for (; b + 56 < n_slabs; b += 64) {
-			float v[8];
-#pragma unroll
-			for (int k = 0; k < 8; ++k) v[k] = slabs[(size_t)(b + 8 * k) * n + p];
-#pragma unroll
-			for (int k = 0; k < 8; ++k) s += v[k];
-		}
-		for (; b < n_slabs; b += 8) s += slabs[(size_t)b * n + p];
-	}
-	part[g][threadIdx.x & 31] = s;
-	__syncthreads();
-	if (g == 0 && p < n) {
-		float t = accumulate ? (float)grad[p] : 0.f;
-#pragma unroll
-		for (int k = 0; k < 8; ++k) t += part[k][threadIdx.x];
-		grad[p] = (f16)t;
-	}
-}
+__global__ void __launch_bounds__(SLAB_THREADS) k_reduce_slabs(const SlabJob j) { reduce_slabs_block(j, blockIdx.x); }
 
 void reduce_slabs(const float* slabs, uint32_t n_slabs, uint32_t n, f16* grad, bool accumulate, hipStream_t s) {
-	k_reduce_slabs<<<div_round_up(n, 32), 256, 0, s>>>(slabs, n_slabs, n, grad, accumulate);
+	SlabJob j;
+	j.slabs = slabs; j.n_slabs = n_slabs; j.n = n; j.grad = grad; j.accumulate = accumulate;
+	k_reduce_slabs<<<slab_blocks(n), SLAB_THREADS, 0, s>>>(j);
 	NGP_HIP(hipGetLastError());
 }
 

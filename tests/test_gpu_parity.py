@@ -451,3 +451,26 @@ def test_fused_encoding_training_matches_unfused(pkg, nerf_setup, n):
         assert torch.equal(res[1][1][nm:], res[0][1][nm:])
     else:
         assert torch.allclose(res[1][1][nm:].float(), res[0][1][nm:].float(), atol=3e-3)
+
+
+@pytest.mark.parametrize("grad_accumulate", [False, True])
+def test_fused_slab_reduction_matches_separate(pkg, nerf_setup, grad_accumulate):
+    """The MLP dW slab reduction run inside the grid backward's last kernel (option fuse_slabs, on by
+    default) writes the same gradients bit for bit as the separate k_reduce_slabs launch, overwriting
+    and accumulating (tcnn's GradientMode::Accumulate)."""
+    net, tr, p16, m = nerf_setup
+    n = 50000
+    c = torch.from_numpy(coords_batch(n, seed=123)).cuda()
+    dL = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
+    dL[:, :4] = torch.rand((n, 4), device="cuda").half() - 0.5
+    res = {}
+    for fuse in (1, 0):
+        net.set_option("fuse_slabs", fuse)
+        net.forward_backward(c, dL)
+        if grad_accumulate:
+            net.forward_backward(c, dL, grad_mode=pkg.GRAD_ACCUMULATE)
+        torch.cuda.synchronize()
+        res[fuse] = tr.gradients.clone()
+    net.set_option("fuse_slabs", 1)
+    assert torch.equal(res[1], res[0])
+    assert res[1][: net.n_matrix_params].abs().sum() > 0
