@@ -91,9 +91,10 @@ REGION_KERNELS = {
     "grid_forward": ["k_grid_forward"],
     "grid_backward": ["k_grid_backward"],
     "grid_backward_total": ["k_sc_scan", "k_sc_plan", "k_sc_scatter", "k_sc_accumulate", "k_sc_split_reduce"],
-    "mlp_train": ["k_nerf_mlp_train<", "k_nerf_mlp<1,", "k_mlp<1,"],
-    "mlp_infer": ["k_nerf_mlp<0,", "k_mlp<0,"],
-    "optimizer": ["k_adam_ema"],
+    # k_nerf_mlp / k_mlp carry the mode as their LAST template argument (1 = training, 0 = inference)
+    "mlp_train": ["k_nerf_mlp_train<", "1>(ngp::NerfMlpArgs)", "1>(ngp::MlpArgs)"],
+    "mlp_infer": ["0>(ngp::NerfMlpArgs)", "0>(ngp::MlpArgs)"],
+    "optimizer": ["k_adam_ema", "k_adam_lazy"],
 }
 # engine profiler phases that make up a roofline region (each runs once per training step)
 REGION_PHASES = {"grid_backward_total": ["grid_bwd_prepare", "grid_backward_sorted"]}
@@ -103,33 +104,44 @@ REGION_PHASES = {"grid_backward_total": ["grid_bwd_prepare", "grid_backward_sort
 OPT_B_UPDATED, OPT_B_SKIPPED = 46, 16
 
 
+def newest_profile(suffix):
+    """profiles/<round>_<suffix> of the latest round tag: r<NN> then a letter sequence that grows like
+    spreadsheet columns (r02z < r02aa < r02br), so plain string order is wrong past z."""
+    import glob
+    import re
+
+    def key(path):
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    files = glob.glob(os.path.join(ROOT, "profiles", f"*_{suffix}"))
+    return max(files, key=key) if files else None
+
+
 def pmc_traffic(variant, region):
     """Bytes per launch of `region` that left L2 for the fabric (Infinity Cache + HBM), from the newest
     committed rocprofv3 summary profiles/<round>_pmc_<variant>.json (tools/pmc_summary.py: reads =
     32/64/128 x TCC_EA0_RDREQ_{32B,64B,128B}, writes = WRITE_SIZE; calibrated against known-byte kernels
     in profiles/r02_hbm_calib.json — FETCH_SIZE alone counts every 128-B request as 64 B). None if absent."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{variant.lower()}.json")))
-    if not files or region not in REGION_KERNELS:
+    path = newest_profile(f"pmc_{variant.lower()}.json")
+    if not path or region not in REGION_KERNELS:
         return None, None
-    summ = json.load(open(files[-1]))
+    summ = json.load(open(path))
     tot, hit = 0.0, False
     for name, v in summ.items():
         compact = name.replace(" ", "")
         if any(k.replace(" ", "") in compact for k in REGION_KERNELS[region]) and "fabric_bytes" in v:
             tot += v["fabric_bytes"]
             hit = True
-    return (tot if hit else None), os.path.relpath(files[-1], ROOT)
+    return (tot if hit else None), os.path.relpath(path, ROOT)
 
 
 def pmc_mfma_util(variant, region):
     """MFMA utilisation of `region`'s kernels (rocprofv3 MfmaUtil = SQ_VALU_MFMA_BUSY_CYCLES over the
     SIMD-cycles of the dispatch) from the newest committed PMC summary; None if absent."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{variant.lower()}.json")))
-    if not files or region not in REGION_KERNELS:
+    path = newest_profile(f"pmc_{variant.lower()}.json")
+    if not path or region not in REGION_KERNELS:
         return None
-    summ = json.load(open(files[-1]))
+    summ = json.load(open(path))
     vals = [v["mfma_util"] for name, v in summ.items()
             if any(k.replace(" ", "") in name.replace(" ", "") for k in REGION_KERNELS[region]) and v.get("mfma_util")]
     return round(max(vals), 4) if vals else None
