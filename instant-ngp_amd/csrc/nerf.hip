@@ -70,13 +70,13 @@ __device__ __forceinline__ Cone make_cone(float c) {
 __device__ float to_stepping_space(float t, const Cone& k) {
 	if (k.c <= 1e-5f) return div_min_stepsize(t);
 	if (t <= k.at) return div_min_stepsize(t - k.at) + k.a;
-	if (t <= k.bt) return ngp_div_rc(ngp_logf(t), k.log1p_c, k.rl);
+	if (t <= k.bt) return ngp_div_rc(ngp_logf_pos(t), k.log1p_c, k.rl);  // at < t <= bt: positive, normal
 	return div_max_stepsize(t - k.bt) + k.b;
 }
 __device__ float from_stepping_space(float n, const Cone& k) {
 	if (k.c <= 1e-5f) return n * MIN_CONE_STEPSIZE;
 	if (n <= k.a) return (n - k.a) * MIN_CONE_STEPSIZE + k.at;
-	if (n <= k.b) return ngp_expf(n * k.log1p_c);
+	if (n <= k.b) return ngp_expf_mid(n * k.log1p_c);  // a l < n l <= b l, i.e. log(at) .. log(bt): |.| << 80
 	return (n - k.b) * MAX_CONE_STEPSIZE + k.bt;
 }
 __device__ __forceinline__ float advance_n_steps(float t, const Cone& k, float n) { return from_stepping_space(to_stepping_space(t, k) + n, k); }

@@ -47,10 +47,8 @@ NGP_MATH_FN float ngp_math_u2f(uint32_t u) {
 /* e^x: x = k ln2 + r (Cody-Waite two-part ln2, |r| <= 0.35), e^r by a degree-7 Taylor polynomial in
  * Horner form (truncation 5e-9 relative), scaled by 2^k through the exponent bits (two factors when
  * the result is subnormal). */
-NGP_MATH_FN float ngp_expf(float x) {
-	if (x != x) return x;
-	if (x > 88.72283935546875f) return ngp_math_u2f(0x7f800000u);
-	if (x < -103.97208404541015625f) return 0.0f;
+/* the polynomial e^r and k of x (x finite, no overflow/underflow checks) */
+NGP_MATH_FN float ngp_expf_poly(float x, float* kout) {
 	const float k = NGP_FLOORF(NGP_FMAF(x, 1.44269502162933349609375f, 0.5f));
 	float r = NGP_FMAF(-k, 0.693145751953125f, x);
 	r = NGP_FMAF(-k, 1.428606765330187045e-06f, r);
@@ -62,6 +60,22 @@ NGP_MATH_FN float ngp_expf(float x) {
 	p = NGP_FMAF(p, r, 0.5f);
 	p = NGP_FMAF(p, r, 1.0f);
 	p = NGP_FMAF(p, r, 1.0f);
+	*kout = k;
+	return p;
+}
+/* e^x for |x| <= 80 (normal result: the scale 2^k is one normal factor): same operations and value as
+ * ngp_expf there, without its range checks (the stepping space's exponential segment) */
+NGP_MATH_FN float ngp_expf_mid(float x) {
+	float k;
+	const float p = ngp_expf_poly(x, &k);
+	return p * ngp_math_u2f((uint32_t)((int)k + 127) << 23);
+}
+NGP_MATH_FN float ngp_expf(float x) {
+	if (x != x) return x;
+	if (x > 88.72283935546875f) return ngp_math_u2f(0x7f800000u);
+	if (x < -103.97208404541015625f) return 0.0f;
+	float k;
+	const float p = ngp_expf_poly(x, &k);
 	const int ki = (int)k;
 	if (ki >= -126 && ki <= 127) return p * ngp_math_u2f((uint32_t)(ki + 127) << 23);
 	/* ki in [-150, -127] or 128: split the scale so both factors are normal */
@@ -71,6 +85,8 @@ NGP_MATH_FN float ngp_expf(float x) {
 
 /* ln x (FreeBSD e_logf.c algorithm): x = 2^e m with m in [sqrt(2)/2, sqrt(2)), f = m - 1,
  * s = f / (2 + f), log(1+f) = f - f^2/2 + s (f^2/2 + R(s^2)), e ln2 added in two parts. */
+/* ln x for x = 2^(e0) m already reduced to ix = its bits (positive, normal) */
+NGP_MATH_FN float ngp_logf_core(uint32_t ix, int e);
 NGP_MATH_FN float ngp_logf(float x) {
 	uint32_t ix = ngp_math_f2u(x);
 	if (x != x) return x;
@@ -83,6 +99,12 @@ NGP_MATH_FN float ngp_logf(float x) {
 		ix = ngp_math_f2u(x);
 		e = -25;
 	}
+	return ngp_logf_core(ix, e);
+}
+/* ln x for positive normal finite x: same operations and value as ngp_logf there, without its
+ * special-case checks (the stepping space's logarithmic segment) */
+NGP_MATH_FN float ngp_logf_pos(float x) { return ngp_logf_core(ngp_math_f2u(x), 0); }
+NGP_MATH_FN float ngp_logf_core(uint32_t ix, int e) {
 	/* m in [sqrt(2)/2, sqrt(2)): bias the mantissa by (1 - sqrt(2)/2) so the exponent step falls there */
 	ix += 0x3f800000u - 0x3f3504f3u;
 	e += (int)(ix >> 23) - 127;
