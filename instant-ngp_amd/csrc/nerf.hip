@@ -191,14 +191,14 @@ __device__ __forceinline__ float unwarp_dt(float dt) {  // :418-421
 __device__ __forceinline__ float srgb_to_linear(float s) { return s <= 0.04045f ? s / 12.92f : powf((s + 0.055f) / 1.055f, 2.4f); }
 __device__ __forceinline__ float linear_to_srgb(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * powf(l, 0.41666f) - 0.055f; }
 
-__device__ __forceinline__ float logistic(float x) { return 1.0f / (1.0f + ngp_expf(-x)); }  // tcnn::logistic
+__device__ __forceinline__ float logistic(float x) { return 1.0f / (1.0f + ngp_expf_fast(-x)); }  // tcnn::logistic
 // testbed_nerf.cu:317-378 (the reference's __expf; ngp_expf here and in the oracle)
 __device__ float network_to_rgb(float v, uint32_t act) {
 	switch (act) {
 		case ACT_NONE: return v;
 		case ACT_RELU: return v > 0.0f ? v : 0.0f;
 		case ACT_LOGISTIC: return logistic(v);
-		case ACT_EXP: return ngp_expf(fminf(fmaxf(v, -10.0f), 10.0f));
+		case ACT_EXP: return ngp_expf_mid(fminf(fmaxf(v, -10.0f), 10.0f));
 	}
 	return 0.0f;
 }
@@ -207,7 +207,7 @@ __device__ float network_to_rgb_derivative(float v, uint32_t act) {
 		case ACT_NONE: return 1.0f;
 		case ACT_RELU: return v > 0.0f ? 1.0f : 0.0f;
 		case ACT_LOGISTIC: { const float d = logistic(v); return d * (1 - d); }
-		case ACT_EXP: return ngp_expf(fminf(fmaxf(v, -10.0f), 10.0f));
+		case ACT_EXP: return ngp_expf_mid(fminf(fmaxf(v, -10.0f), 10.0f));
 	}
 	return 0.0f;
 }
@@ -216,7 +216,7 @@ __device__ float network_to_density(float v, uint32_t act) {
 		case ACT_NONE: return v;
 		case ACT_RELU: return v > 0.0f ? v : 0.0f;
 		case ACT_LOGISTIC: return logistic(v);
-		case ACT_EXP: return ngp_expf(v);
+		case ACT_EXP: return ngp_expf_fast(v);
 	}
 	return 0.0f;
 }
@@ -225,7 +225,7 @@ __device__ float network_to_density_derivative(float v, uint32_t act) {
 		case ACT_NONE: return 1.0f;
 		case ACT_RELU: return v > 0.0f ? 1.0f : 0.0f;
 		case ACT_LOGISTIC: { const float d = logistic(v); return d * (1 - d); }
-		case ACT_EXP: return ngp_expf(fminf(fmaxf(v, -15.0f), 15.0f));
+		case ACT_EXP: return ngp_expf_mid(fminf(fmaxf(v, -15.0f), 15.0f));
 	}
 	return 0.0f;
 }
@@ -757,7 +757,7 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 			const f16x4 o = *(const f16x4*)(out + (size_t)jj * a.out_stride);
 			const float dt = unwarp_dt(ci[(size_t)jj * 7 + 3]);
 			const float density = network_to_density((float)o[3], cfg.density_activation);
-			alpha = 1.f - ngp_expf(-density * dt);
+			alpha = 1.f - ngp_expf_fast(-density * dt);
 			cr = network_to_rgb((float)o[0], cfg.rgb_activation);
 			cg = network_to_rgb((float)o[1], cfg.rgb_activation);
 			cb = network_to_rgb((float)o[2], cfg.rgb_activation);
@@ -857,7 +857,7 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const ngp_nerf_config cfg, L
 			for (int k = 0; k < 3; ++k) rgb[k] = network_to_rgb((float)o[k], cfg.rgb_activation);
 			dt = unwarp_dt(cc[3]);
 			const float density = network_to_density((float)o[3], cfg.density_activation);
-			alpha = 1.f - ngp_expf(-density * dt);
+			alpha = 1.f - ngp_expf_fast(-density * dt);
 		}
 		// compositing in sample order; lane K keeps its weight, transmittance after it and rgb prefix
 		float my_w = 0.f, my_t = 0.f, my_r2[3] = {0.f, 0.f, 0.f};
@@ -1282,7 +1282,7 @@ __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, ui
 		const float o3 = (float)out[r + 3 * (size_t)stride];
 		const float T = 1.f - c[3];
 		const float dt = unwarp_dt(coords[r * 7 + 3]);
-		const float alpha = 1.f - ngp_expf(-network_to_density(o3, a.density_activation) * dt);
+		const float alpha = 1.f - ngp_expf_fast(-network_to_density(o3, a.density_activation) * dt);
 		const float weight = alpha * T;
 		c[0] += network_to_rgb(o0, a.rgb_activation) * weight;
 		c[1] += network_to_rgb(o1, a.rgb_activation) * weight;

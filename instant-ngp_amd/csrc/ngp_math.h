@@ -70,6 +70,14 @@ NGP_MATH_FN float ngp_expf_mid(float x) {
 	const float p = ngp_expf_poly(x, &k);
 	return p * ngp_math_u2f((uint32_t)((int)k + 127) << 23);
 }
+NGP_MATH_FN float ngp_expf(float x);
+/* ngp_expf with the common case |x| <= 80 first (no further checks there; NaN and the rest take the
+ * full path): same value as ngp_expf for every x */
+NGP_MATH_FN float ngp_expf_fast(float x) {
+	const float ax = x < 0.0f ? -x : x;
+	if (ax <= 80.0f) return ngp_expf_mid(x);
+	return ngp_expf(x);
+}
 NGP_MATH_FN float ngp_expf(float x) {
 	if (x != x) return x;
 	if (x > 88.72283935546875f) return ngp_math_u2f(0x7f800000u);
