@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 // Block = 64 consecutive buckets (lanes) x SCAN_SEG chunk segments (waves): each wave sums its segment's
 // counts, the segment offsets come through LDS, then the wave re-reads its segment (L2) and writes the
 // cursors. Reads and writes are 256-B row segments.
-constexpr uint32_t SCAN_SEG = 16;
+constexpr uint32_t SCAN_SEG = 16, SCAN_REG = 32;
 __global__ void __launch_bounds__(64 * SCAN_SEG) k_sc_scan(const uint32_t* __restrict__ hist, uint32_t n_chunks, uint32_t n_vb,
                                                          uint32_t* __restrict__ cur, uint32_t* __restrict__ tot) {
 	__shared__ uint32_t seg_sum[SCAN_SEG][64];
@@ -149,6 +149,30 @@ __global__ void __launch_bounds__(64 * SCAN_SEG) k_sc_scan(const uint32_t* __res
 	const uint32_t vb = blockIdx.x * 64 + lane;
 	const uint32_t per = (n_chunks + SCAN_SEG - 1) / SCAN_SEG;
 	const uint32_t c0 = min(seg * per, n_chunks), c1 = min(c0 + per, n_chunks);
+	if (per <= SCAN_REG) {
+		// the whole segment in registers: one load latency, no second read (C2: 32 chunks per segment)
+		uint32_t v[SCAN_REG], sum = 0;
+#pragma unroll
+		for (uint32_t u = 0; u < SCAN_REG; ++u) v[u] = (vb < n_vb && c0 + u < c1) ? hist[(size_t)(c0 + u) * n_vb + vb] : 0u;
+#pragma unroll
+		for (uint32_t u = 0; u < SCAN_REG; ++u) sum += v[u];
+		seg_sum[seg][lane] = sum;
+		__syncthreads();
+		uint32_t run = 0, total = 0;
+		for (uint32_t q = 0; q < SCAN_SEG; ++q) {
+			const uint32_t x = seg_sum[q][lane];
+			if (q < seg) run += x;
+			total += x;
+		}
+		if (vb >= n_vb) return;
+#pragma unroll
+		for (uint32_t u = 0; u < SCAN_REG; ++u) {
+			if (c0 + u < c1) cur[(size_t)(c0 + u) * n_vb + vb] = run;
+			run += v[u];
+		}
+		if (seg == 0) tot[vb] = total;
+		return;
+	}
 	constexpr uint32_t U = 8;
 	uint32_t sum = 0;
 	if (vb < n_vb) {
