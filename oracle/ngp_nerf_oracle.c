@@ -704,9 +704,22 @@ EXPORT void orc_nerf_render_composite(const ocfg* c, uint32_t n_px, uint32_t max
 	}
 }
 
-/* The shared transcendental (instant-ngp_amd/csrc/ngp_math.h), exported for its accuracy test. */
+/* The shared transcendental (instant-ngp_amd/csrc/ngp_math.h), exported for its accuracy test:
+ * fn 0 ngp_expf, 1 ngp_logf, and the variants the kernels call where the argument is bounded (each
+ * must equal the full function there): 2 ngp_expf_mid, 3 ngp_logf_pos, 4 ngp_expf_fast, 5 the
+ * stepping-space division ngp_div_rc(x, log(1 + 1/256)). */
 EXPORT void orc_math_eval(int fn, size_t n, const float* x, float* y) {
-	for (size_t i = 0; i < n; ++i) y[i] = fn == 0 ? ngp_expf(x[i]) : ngp_logf(x[i]);
+	const float l = ngp_logf(1.0f + 1.0f / 256.0f), rl = 1.0f / l;
+	for (size_t i = 0; i < n; ++i) {
+		switch (fn) {
+			case 0: y[i] = ngp_expf(x[i]); break;
+			case 1: y[i] = ngp_logf(x[i]); break;
+			case 2: y[i] = ngp_expf_mid(x[i]); break;
+			case 3: y[i] = ngp_logf_pos(x[i]); break;
+			case 4: y[i] = ngp_expf_fast(x[i]); break;
+			default: y[i] = ngp_div_rc(x[i], l, rl); break;
+		}
+	}
 }
 
 /* ---- NerfCounters (testbed_nerf.cu:3568-3609) and the step's inference size (:3923-3930) ---------

@@ -188,7 +188,7 @@ def grid_backward(g, pos, dL_dy, max_level=1.0, max_level_per_sample=None, strid
 
 
 def math_eval(fn, x):
-    """ngp_math.h's expf (fn 0) / logf (fn 1) evaluated on the host."""
+    """ngp_math.h evaluated on the host: fn 0 expf, 1 logf, 2 expf_mid, 3 logf_pos, 4 expf_fast, 5 div_rc by log(1+1/256)."""
     x = np.ascontiguousarray(x, dtype=np.float32)
     y = np.empty_like(x)
     lib().orc_math_eval(fn, x.size, ptr(x), ptr(y))

@@ -325,6 +325,25 @@ def test_shared_math_accuracy(orc):
     assert abs(sp[5] - np.log(1e-40)) < 1e-5 * abs(np.log(1e-40))
 
 
+def test_shared_math_fast_variants_equal_full(orc):
+    """The kernels call ngp_math.h's unchecked cores where the argument is bounded (stepping-space
+    segments, clamped activations) and a fast path for |x| <= 80 elsewhere: each returns the same bits
+    as the full function on its domain, and the stepping-space division by log(1 + 1/256) equals IEEE
+    division (tools/microbench/div_check.c checks it exhaustively)."""
+    g = np.random.default_rng(5)
+    x = np.concatenate([g.uniform(-80, 80, 1 << 20), g.uniform(-15, 15, 1 << 18)]).astype(np.float32)
+    assert np.array_equal(orc.math_eval(2, x).view(np.uint32), orc.math_eval(0, x).view(np.uint32))
+    bits = g.integers(0x00800000, 0x7f800000, 1 << 20, dtype=np.uint32)
+    x = np.concatenate([bits.view(np.float32), g.uniform(0.4, 60, 1 << 18).astype(np.float32)])
+    assert np.array_equal(orc.math_eval(3, x).view(np.uint32), orc.math_eval(1, x).view(np.uint32))
+    x = np.concatenate([g.uniform(-200, 200, 1 << 20).astype(np.float32),
+                        np.array([np.nan, np.inf, -np.inf, 80.0, -80.0, 88.7, -103.9, -120.0], np.float32)])
+    assert np.array_equal(orc.math_eval(4, x).view(np.uint32), orc.math_eval(0, x).view(np.uint32))
+    x = np.concatenate([g.uniform(-2, 5, 1 << 20), g.uniform(-1e3, 1e3, 1 << 18)]).astype(np.float32)
+    l = np.float32(orc.math_eval(1, np.array([1 + 1 / 256], np.float32))[0])
+    assert np.array_equal(orc.math_eval(5, x), (x / l).astype(np.float32))
+
+
 def test_grid_backward_exact_vs_double(orc):
     """The contribution-exact backward (per-contribution fp16 rounding, exact sum, one rounding) agrees
     with the float64 backward within the per-contribution rounding it adds: <= sum of half an fp16 ulp
