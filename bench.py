@@ -261,7 +261,7 @@ def timed_steps(lib, step, steps, warmup, world, capture=None):
     return t1 - t0, ("hip_graph" if graph is not None else (graph_note or "eager")), read_profiler(lib)
 
 
-def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None):
+def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None, wire="f32"):
     """NerfNetwork + Trainer for C2/C2' with a resident synthetic batch; returns (step, capture, net, trainer)."""
     cfg = pkg.nerf_config(variant)
     net = pkg.create_nerf_network(cfg)
@@ -278,7 +278,7 @@ def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None):
     if world > 1:
         # the engine's own RCCL communicator: the gradient all-reduce is enqueued by the engine on its
         # stream, between the backward and the optimizer, and captured into the step's graph
-        comm = pkg.dp.EngineComm(rank, world)
+        comm = pkg.dp.EngineComm(rank, world, wire=wire)
         trainer.set_allreduce(comm)
     loss_scale = 128.0
 
@@ -293,8 +293,21 @@ def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None):
     return step, capture, net, trainer, comm
 
 
-def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped):
-    """Per-region achieved rate and fraction of peak; returns (summary dict, dominant region)."""
+def slab_reduction_bytes(lib, net):
+    """Algorithmic bytes of the MLP dW slab reduction that runs inside the grid backward's last kernel
+    (engine option fuse_slabs): every fp32 slab read once [blocks x n_matrix], the fp16 MLP gradient
+    written once. 0 when the model has no slab workspace."""
+    import ctypes
+    p, nb = ctypes.c_void_p(), ctypes.c_uint64()
+    if lib.ngp_model_workspace(net.handle, b"dw_slabs", ctypes.byref(p), ctypes.byref(nb)) != 0:
+        return 0
+    return int(nb.value) + 2 * int(net.n_matrix_params)
+
+
+def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped, slab_bytes=0):
+    """Per-region achieved rate and fraction of peak; returns (summary dict, dominant region).
+    slab_bytes: the fused dW slab reduction's bytes, counted in the grid_backward_total region (its
+    kernel runs them as extra blocks)."""
     a = ALGO[variant]
     per = {k: v["ms"] / max(v["calls"], 1) for k, v in kernels.items()}
     for region, phases in REGION_PHASES.items():
@@ -303,7 +316,7 @@ def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped):
     roof = {
         "grid_forward": ("hbm", a["enc_fwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
         "grid_backward": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
-        "grid_backward_total": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
+        "grid_backward_total": ("hbm", (a["enc_bwd_B"] * n + slab_bytes) / 1e9, HBM_PEAK_GBS, "GB/s"),
         "mlp_train": ("mfma", a["mlp_train_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
         "mlp_infer": ("mfma", a["mlp_fwd_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
     }
@@ -313,13 +326,23 @@ def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped):
     for k, ms in per.items():
         e = {"avg_ms": round(ms, 4)}
         if k in roof:
-            _, w, pk, u = roof[k]
+            b, w, pk, u = roof[k]
             e.update({"achieved": round(w / (ms / 1e3), 1), "unit": u, "frac": round(w / (ms / 1e3) / pk, 4)})
-            if k == "optimizer" and w * 1e9 < IC_BYTES:
-                # the whole optimizer state fits the 256 MiB Infinity Cache and is re-touched every step:
-                # its bytes do not all come from HBM, so an HBM fraction would overstate it (C2: >1)
-                e.update({"bound": "infinity_cache", "frac": None,
-                          "note": "working set < 256 MiB, served on-die; no HBM fraction (HBM spec is not its ceiling)"})
+            if b == "hbm":
+                traffic, _ = pmc_traffic(variant, k)
+                if traffic is not None:
+                    # what actually left L2 for the fabric per launch, and its rate
+                    e["fabric_MB"] = round(traffic / 1e6, 2)
+                    e["fabric_GBs"] = round(traffic / 1e9 / (ms / 1e3), 1)
+                cached = (k == "optimizer" and w * 1e9 < IC_BYTES) or w / (ms / 1e3) > pk
+                if cached:
+                    # the algorithmic bytes were (partly) served on-die (Infinity Cache / L2: the optimizer
+                    # state re-touched every step, hot table entries): the HBM spec is not their ceiling and
+                    # an algorithmic "HBM fraction" above 1 is not physical. Report the fabric rate instead.
+                    e.update({"bound": "infinity_cache", "frac": None,
+                              "fabric_frac": (round(e["fabric_GBs"] / pk, 4) if "fabric_GBs" in e else None),
+                              "note": "algorithmic bytes served partly on-die (working set re-touched every step); no "
+                                      "algorithmic HBM fraction; fabric_GBs = PMC bytes leaving L2 / time"})
         if k in ("mlp_train", "mlp_infer"):
             u = pmc_mfma_util(variant, k)
             if u is not None:
@@ -337,6 +360,8 @@ def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped):
                           "+ WRITE_SIZE)",
           "traffic_source": src,
           "algorithmic": round(work * (1e3 if unit == "GB/s" else 1e6), 2),
+          "algorithmic_includes": ("the fused MLP dW slab reduction: %.2f MB" % (slab_bytes / 1e6)
+                                   if dom == "grid_backward_total" and slab_bytes else None),
           "algorithmic_unit": "MB/launch" if unit == "GB/s" else "MFLOP/launch"}
     return summary, rl
 
@@ -369,6 +394,37 @@ def optimizer_counts(net, trainer, step):
     return nm + nz, net.n_params - nm - nz
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a torch.distributed environment: start N fresh rank processes
+    (torch.distributed.run, rendezvous on 127.0.0.1) running this same command line, and return their exit
+    code. Runs before this process touches the GPU (no HIP call has been made yet): the ranks are children,
+    never an exec of this process."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def check_world(gpus, env=os.environ):
+    """The rank layout bench.py runs with: (needs_launch, world). --gpus N > 1 without WORLD_SIZE means
+    bench.py must start the N ranks itself; with WORLD_SIZE set, it must equal --gpus."""
+    if "WORLD_SIZE" not in env:
+        return gpus > 1, 1
+    world = int(env["WORLD_SIZE"])
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world} (torch.distributed.run --nproc-per-node must match)")
+    return False, world
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -386,19 +442,28 @@ def main():
     ap.add_argument("--graph", type=int, default=1, help="1: time the K steps as one captured HIP graph (N=1)")
     ap.add_argument("--overlap", type=int, default=None, help="engine side-stream overlap bitmask (engine.hip)")
     ap.add_argument("--opt", action="append", default=[], help="model option key=value (ngp_model_set_option)")
+    ap.add_argument("--wire", default="f32", choices=["f32", "f16"],
+                    help="gradient all-reduce wire type (f32: fp16 sums widened, rounded once)")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling sub-record")
     args = ap.parse_args()
+
+    need_launch, _ = check_world(args.gpus)
+    if need_launch:
+        sys.exit(launch_ranks(args.gpus))
 
     from __graft_entry__ import load_package
     pkg = load_package()
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     rank, world, local_rank = pkg.dp.init_from_env()
+    assert world == args.gpus, (world, args.gpus)
     lib = pkg.lib()
 
     n = args.batch if args.scaling == "weak" else args.batch // world
     n_opt = (None, None)
     if args.variant in ("C2", "C2p"):
-        step, capture, net, trainer, comm = nerf_pass(pkg, args.variant, n, rank, world, args.opt, args.overlap)
+        step, capture, net, trainer, comm = nerf_pass(pkg, args.variant, n, rank, world, args.opt, args.overlap,
+                                                      args.wire)
         n_opt = optimizer_counts(net, trainer, step)
         if not args.graph:
             capture = None
@@ -422,14 +487,40 @@ def main():
             it.train_step(get_loss=False)
         capture = None
 
+    n_params_total = net.n_params
     dt, launch, kernels = timed_steps(lib, step, args.steps, args.warmup, world, capture)
+    slab_b = slab_reduction_bytes(lib, net)
     if world > 1:
         t = torch.tensor([dt], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    strong = None
+    if world > 1 and args.variant in ("C2", "C2p") and not args.no_strong:
+        # the other scaling mode in the same line: weak = fixed batch per GPU (headline), strong = one
+        # global --batch sharded over the N ranks
+        n_s = args.batch // world if args.scaling == "weak" else args.batch
+        s_s, c_s, _, _, comm_s = nerf_pass(pkg, args.variant, n_s, rank, world, args.opt, args.overlap, args.wire)
+        dts, launch_s, k_s = timed_steps(lib, s_s, args.steps, args.warmup, world, c_s if args.graph else None)
+        t = torch.tensor([dts], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dts = float(t.item())
+        ar = k_s.get("allreduce")
+        strong = {"scaling": "strong" if args.scaling == "weak" else "weak", "batch_per_gpu": n_s,
+                  "global_batch": n_s * world, "value": n_s * world * args.steps / dts, "unit": "samples/s",
+                  "ms_per_step": dts / args.steps * 1e3, "launch": launch_s,
+                  "allreduce_ms_per_step": None if ar is None else round(ar["ms"] / max(ar["calls"], 1), 4)}
+        del s_s, c_s, comm_s
+    e2e_dp = None
+    if world > 1 and args.variant == "C2" and args.e2e_seconds > 0:
+        # the metric's full form on N GPUs: the Testbed NeRF step data-parallel (rays sharded with their
+        # global ids, RCCL all-reduce of gradients, density-grid maxima and counters), then PSNR on rank 0
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import psnr30
+        e2e_dp = psnr30.run(pkg, seconds=args.e2e_seconds, rank=rank, world=world)
+
     if rank == 0:
-        kern_summary, rl = roofline(args.variant, n, kernels, *n_opt)
+        kern_summary, rl = roofline(args.variant, n, kernels, *n_opt, slab_bytes=slab_b)
         res = {
             "metric": "training samples/sec + PSNR@30s, NeRF Lego at 1/2/4/8 MI355X",
             "value": n * world * args.steps / dt,
@@ -446,20 +537,30 @@ def main():
             "config": {"workload": WORKLOADS[args.variant],
                        "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
                        "launch": launch,
-                       "exchange": "engine RCCL all-reduce of the fp16 gradient buffer per step" if world > 1 else None},
+                       "exchange": (f"engine RCCL all-reduce of the gradient buffer per step ({args.wire} on the wire)"
+                                    if world > 1 else None)},
             "kernel_timing": ("HIP events per kernel on the launch stream, eager replay of the same K steps queued "
                               "behind a graph launch" if launch == "hip_graph" else "HIP events per kernel over the timed region"),
             "roofline": rl,
             "optimizer_params": {"updated": n_opt[0], "skipped": n_opt[1]},
             "kernels": kern_summary,
         }
+        if world > 1:
+            ar = kernels.get("allreduce")
+            res["allreduce_ms_per_step"] = None if ar is None else round(ar["ms"] / max(ar["calls"], 1), 4)
+            res["allreduce_bytes"] = (4 if args.wire == "f32" else 2) * int(n_params_total)
+            if strong is not None:
+                res["strong"] = strong
+            if e2e_dp is not None:
+                res["e2e"] = {k: e2e_dp[k] for k in ("value", "unit", "psnr", "psnr_views", "train_seconds", "steps",
+                                                     "ms_per_step", "n_gpus", "data", "config")}
         if world == 1 and args.variant == "C2":
             if not args.no_c2p:
                 # BASELINE's literal "L=16": the same training pass at C2' (L=16 F=2 T=2^19)
                 s2, c2, net2, tr2, _ = nerf_pass(pkg, "C2p", n, 0, 1)
                 o2 = optimizer_counts(net2, tr2, s2)
                 dt2, launch2, k2 = timed_steps(lib, s2, args.steps, args.warmup, 1, c2)
-                ks2, rl2 = roofline("C2p", n, k2, *o2)
+                ks2, rl2 = roofline("C2p", n, k2, *o2, slab_bytes=slab_reduction_bytes(lib, net2))
                 res["c2p"] = {"workload": WORKLOADS["C2p"], "value": n * args.steps / dt2, "unit": "samples/s",
                               "ms_per_step": dt2 / args.steps * 1e3, "launch": launch2, "roofline": rl2, "kernels": ks2}
                 del s2, c2, net2, tr2
@@ -468,7 +569,7 @@ def main():
                 s5, net5, tr5 = c5_pass(pkg, n, 0)
                 o5 = optimizer_counts(net5, tr5, s5)
                 dt5, launch5, k5 = timed_steps(lib, s5, args.steps, args.warmup, 1, None)
-                ks5, rl5 = roofline("C5", n, k5, *o5)
+                ks5, rl5 = roofline("C5", n, k5, *o5, slab_bytes=slab_reduction_bytes(lib, net5))
                 res["c5"] = {"workload": WORKLOADS["C5"], "value": n * args.steps / dt5, "unit": "samples/s",
                              "ms_per_step": dt5 / args.steps * 1e3, "launch": launch5, "roofline": rl5, "kernels": ks5,
                              "optimizer_params": {"updated": o5[0], "skipped": o5[1]}}

@@ -311,6 +311,11 @@ int ngp_nerf_trainer_create(ngp_model* model, ngp_trainer* trainer, const ngp_ne
 void ngp_nerf_trainer_destroy(ngp_nerf_trainer* t);
 int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_nerf_stats* out);
 int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** density_grid, uint8_t** bitfield, float** mean_density);
+/* The same pointers for READING only: keeps a prelaunched (pipelined) sampler, which reads the bitfield
+ * and writes none of the three. Writes through these pointers are not seen by an already prelaunched
+ * sampler: use ngp_nerf_trainer_buffers to modify them. */
+int ngp_nerf_trainer_buffers_read(const ngp_nerf_trainer* t, const float** density_grid, const uint8_t** bitfield,
+                                  const float** mean_density);
 
 /* Rendering (NerfTracer::init_rays_from_camera + trace + shade, testbed_nerf.cu:2229-2659,
  * 948-1196, 2164-2226; ERenderMode::Shade, pinhole). camera: the view (xform after
@@ -368,6 +373,12 @@ int ngp_dp_comm_unique_id(uint8_t* id_out);
 int ngp_dp_comm_create(uint32_t rank, uint32_t world, const uint8_t* id_in, ngp_dp_comm** out);
 void ngp_dp_comm_destroy(ngp_dp_comm* c);
 int ngp_dp_comm_allreduce(void* user, void* device_buf, uint64_t count, int dtype, int op, void* stream);
+/* Wire type of fp16 sums (default NGP_DTYPE_F32: widened to fp32, all-reduced, rounded to fp16 once —
+ * RCCL's fp16 ring rounds at every hop, so its sum depends on N and ring order; NGP_DTYPE_F16: half the
+ * bytes). ngp_dp_comm_reserve sizes the fp32 staging buffer for `count` elements; it must run outside
+ * graph capture (the trainers call it when the communicator is bound). */
+int ngp_dp_comm_set_wire(ngp_dp_comm* c, int dtype);
+int ngp_dp_comm_reserve(ngp_dp_comm* c, uint64_t count);
 /* Gradient exchange inside the trainer's step (network-level data parallelism, bench.py --gpus N):
  * after every forward_backward captured by ngp_trainer_capture_training_step, and before the
  * optimizer, the fp16 gradient buffer is all-reduced (sum) with `allreduce`; the optimizer divides

@@ -150,6 +150,7 @@ SIGNATURES = {
     "ngp_nerf_trainer_destroy": (None, [P]),
     "ngp_nerf_train_step": (i32, [P, P, i32, C.POINTER(NerfStats)]),
     "ngp_nerf_trainer_buffers": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
+    "ngp_nerf_trainer_buffers_read": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
     "ngp_nerf_trainer_set_pipeline": (i32, [P, i32]),
     "ngp_nerf_trainer_set_data_parallel": (i32, [P, u32, u32, P, P]),
     "ngp_nerf_save_snapshot": (i32, [P, P, C.c_char_p, C.c_char_p, i32, i32]),
@@ -159,6 +160,8 @@ SIGNATURES = {
     "ngp_dp_comm_create": (i32, [u32, u32, P, C.POINTER(P)]),
     "ngp_dp_comm_destroy": (None, [P]),
     "ngp_dp_comm_allreduce": (i32, [P, P, u64, i32, i32, P]),
+    "ngp_dp_comm_set_wire": (i32, [P, i32]),
+    "ngp_dp_comm_reserve": (i32, [P, u64]),
     "ngp_trainer_set_allreduce": (i32, [P, u32, P, P]),
     "ngp_nerf_renderer_create": (i32, [C.POINTER(P)]),
     "ngp_nerf_renderer_destroy": (None, [P]),

@@ -5,6 +5,7 @@
 // is issued here directly on the engine's stream, so a captured training step (forward/backward ->
 // ncclAllReduce -> Adam/EMA) is one HIP graph on one queue: no host callback and no cross-queue graph
 // edge per step. The unique id travels over any host channel (torch.distributed in dp.py).
+// The fp16 gradient sum travels as fp32 by default (ngp_dp_comm_set_wire), so it is rounded once.
 // Links librccl.so.1; inside a PyTorch process that is the RCCL instance torch already loaded (same
 // SONAME), so both communicators live in one library.
 #include <rccl/rccl.h>
@@ -21,7 +22,41 @@ namespace ngp { void set_last_error(const char* msg); }
 struct ngp_dp_comm {
 	ncclComm_t comm = nullptr;
 	int rank = 0, world = 1;
+	// fp16 sums travel as fp32 (default): RCCL's fp16 ring rounds the partial sum to fp16 at every hop,
+	// so the result depends on N and on each rank's ring position. Widened, the N fp16 addends are summed
+	// in fp32 and rounded to fp16 once (ngp_dp_comm_set_wire).
+	int wire = NGP_DTYPE_F32;
+	float* stage = nullptr;  // fp32 staging of the widened buffer
+	uint64_t stage_count = 0;
 };
+
+namespace ngp {
+// fp16 -> fp32 widening and the single fp32 -> fp16 rounding around a widened all-reduce; 8 elements per
+// thread (16-B loads), scalar tail
+__global__ void k_widen_f16(const f16* __restrict__ a, float* __restrict__ b, uint64_t n) {
+	const uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * 8;
+	if (i + 8 <= n) {
+		const f16x8 v = *(const f16x8*)(a + i);
+		f32x4 lo = {(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+		f32x4 hi = {(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+		*(f32x4*)(b + i) = lo;
+		*(f32x4*)(b + i + 4) = hi;
+	} else {
+		for (uint64_t j = i; j < n; ++j) b[j] = (float)a[j];
+	}
+}
+__global__ void k_narrow_f32(const float* __restrict__ b, f16* __restrict__ a, uint64_t n) {
+	const uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * 8;
+	if (i + 8 <= n) {
+		const f32x4 lo = *(const f32x4*)(b + i), hi = *(const f32x4*)(b + i + 4);
+		f16x8 v;
+		for (int k = 0; k < 4; ++k) { v[k] = (f16)lo[k]; v[k + 4] = (f16)hi[k]; }
+		*(f16x8*)(a + i) = v;
+	} else {
+		for (uint64_t j = i; j < n; ++j) a[j] = (f16)b[j];
+	}
+}
+}  // namespace ngp
 
 namespace {
 int fail(const char* what, ncclResult_t r) {
@@ -61,7 +96,30 @@ int ngp_dp_comm_create(uint32_t rank, uint32_t world, const uint8_t* id_in, ngp_
 void ngp_dp_comm_destroy(ngp_dp_comm* c) {
 	if (!c) return;
 	if (c->comm) (void)ncclCommDestroy(c->comm);
+	if (c->stage) (void)hipFree(c->stage);
 	delete c;
+}
+
+int ngp_dp_comm_set_wire(ngp_dp_comm* c, int dtype) {
+	if (!c || (dtype != NGP_DTYPE_F32 && dtype != NGP_DTYPE_F16)) return NGP_INVALID;
+	c->wire = dtype;
+	return NGP_OK;
+}
+
+int ngp_dp_comm_reserve(ngp_dp_comm* c, uint64_t count) {
+	if (!c) return NGP_INVALID;
+	if (count <= c->stage_count) return NGP_OK;
+	hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+	if (hipStreamIsCapturing(nullptr, &st) == hipSuccess && st != hipStreamCaptureStatusNone) return NGP_ERROR;
+	if (c->stage) (void)hipFree(c->stage);
+	c->stage = nullptr;
+	c->stage_count = 0;
+	if (hipMalloc(&c->stage, count * sizeof(float)) != hipSuccess) {
+		ngp::set_last_error("ngp_dp_comm_reserve: hipMalloc of the fp32 staging buffer failed");
+		return NGP_ERROR;
+	}
+	c->stage_count = count;
+	return NGP_OK;
 }
 
 // ngp_allreduce_fn: user = ngp_dp_comm*
@@ -69,10 +127,34 @@ int ngp_dp_comm_allreduce(void* user, void* buf, uint64_t count, int dtype, int 
 	auto* c = (ngp_dp_comm*)user;
 	if (!c || (!buf && count)) return NGP_INVALID;
 	if (count == 0) return NGP_OK;
-	const ncclDataType_t t = dtype == NGP_DTYPE_F16 ? ncclFloat16 : ncclFloat32;
 	const ncclRedOp_t o = op == NGP_REDUCE_MAX ? ncclMax : ncclSum;
-	ngp::ProfScope ps("allreduce", (hipStream_t)stream);
-	const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, t, o, c->comm, (hipStream_t)stream);
+	hipStream_t s = (hipStream_t)stream;
+	ngp::ProfScope ps("allreduce", s);
+	if (dtype == NGP_DTYPE_F16 && op == NGP_REDUCE_SUM && c->wire == NGP_DTYPE_F32) {
+		// widened sum: fp16 -> fp32 staging, fp32 ring all-reduce, one rounding back to fp16. The staging
+		// buffer is sized outside graph capture (ngp_dp_comm_reserve, called when a trainer binds the
+		// communicator); it is grown here only on a stream that is not being captured
+		if (count > c->stage_count) {
+			hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+			if (hipStreamIsCapturing(s, &st) != hipSuccess || st != hipStreamCaptureStatusNone) {
+				ngp::set_last_error("ngp_dp_comm_allreduce: fp32 staging too small inside a graph capture (ngp_dp_comm_reserve first)");
+				return NGP_ERROR;
+			}
+			if (hipStreamSynchronize(s) != hipSuccess) return NGP_ERROR;
+			const int rc = ngp_dp_comm_reserve(c, count);
+			if (rc != NGP_OK) return rc;
+		}
+		const uint32_t blocks = (uint32_t)((count + 8 * 256 - 1) / (8 * 256));
+		ngp::k_widen_f16<<<blocks, 256, 0, s>>>((const ngp::f16*)buf, c->stage, count);
+		if (hipGetLastError() != hipSuccess) return NGP_ERROR;
+		const ncclResult_t r = ncclAllReduce(c->stage, c->stage, (size_t)count, ncclFloat32, o, c->comm, s);
+		if (r != ncclSuccess) return fail("ncclAllReduce", r);
+		ngp::k_narrow_f32<<<blocks, 256, 0, s>>>(c->stage, (ngp::f16*)buf, count);
+		if (hipGetLastError() != hipSuccess) return NGP_ERROR;
+		return NGP_OK;
+	}
+	const ncclDataType_t t = dtype == NGP_DTYPE_F16 ? ncclFloat16 : ncclFloat32;
+	const ncclResult_t r = ncclAllReduce(buf, buf, (size_t)count, t, o, c->comm, s);
 	if (r != ncclSuccess) return fail("ncclAllReduce", r);
 	return NGP_OK;
 }

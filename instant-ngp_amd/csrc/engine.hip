@@ -413,8 +413,8 @@ struct ngp_trainer {
 	// updated parameters; the inference (EMA) parameters are brought up to date when read
 	AdamRec* rec = nullptr;
 	bool inf_stale = false;
-	void materialize(hipStream_t s) {
-		if (!rec || !inf_stale) return;
+	void materialize(hipStream_t s, bool force = false) {
+		if (!rec || (!inf_stale && !force)) return;
 		AdamState st{w32, w16, g16, nullptr, nullptr, nullptr, nullptr, inf16, nullptr, nullptr, nullptr, 0, nullptr, rec};
 		ema_materialize(cfg, (uint32_t)n, step, st, s);
 		inf_stale = false;
@@ -654,8 +654,8 @@ int ngp_model_workspace(ngp_model* m, const char* name, void** ptr, uint64_t* by
 	NGP_ARG(m && name && ptr);
 	NGP_TRY({
 		const std::string k(name);
-		DevBuf* b = k == "encoding" ? &m->enc : k == "dL_dencoding" ? &m->denc : nullptr;
-		NGP_CHECK(b, "ngp_model_workspace: unknown workspace '" + k + "' (encoding, dL_dencoding)");
+		DevBuf* b = k == "encoding" ? &m->enc : k == "dL_dencoding" ? &m->denc : k == "dw_slabs" ? &m->slabs : nullptr;
+		NGP_CHECK(b, "ngp_model_workspace: unknown workspace '" + k + "' (encoding, dL_dencoding, dw_slabs)");
 		*ptr = b->p;
 		if (bytes) *bytes = b->bytes;
 	});
@@ -954,6 +954,9 @@ int ngp_trainer_set_allreduce(ngp_trainer* t, uint32_t world, ngp_allreduce_fn a
 		t->allreduce = allreduce;
 		t->allreduce_user = user;
 		t->world = allreduce ? world : 1;
+		// the engine's communicator widens the fp16 sum to fp32: size its staging now, outside any capture
+		if (allreduce == ngp_dp_comm_allreduce && user)
+			NGP_CHECK(ngp_dp_comm_reserve((ngp_dp_comm*)user, t->n) == NGP_OK, "ngp_dp_comm_reserve failed");
 	});
 }
 
@@ -978,6 +981,7 @@ void* ngp_trainer_inference_params(ngp_trainer* t) {
 	if (!t) return nullptr;
 	if (t->rec && t->inf_stale) {  // lazy EMA: bring the inference parameters up to date before handing them out
 		try {
+			NGP_HIP(hipDeviceSynchronize());  // the optimizer may still run on a caller's non-blocking stream
 			t->materialize(nullptr);
 			NGP_HIP(hipDeviceSynchronize());
 		} catch (const std::exception& e) {
@@ -1003,6 +1007,14 @@ __global__ static void k_f32_to_f16(const float* a, f16* b, f16* c, uint64_t n) 
 int ngp_trainer_set_params_full_precision(ngp_trainer* t, const float* params_host, uint64_t n) {
 	NGP_ARG(t && params_host && n == t->n);
 	NGP_TRY({
+		if (t->rec && t->step > 0) {
+			// lazy EMA: entries skipped since their last update still owe EMA steps on the OLD weight (the eager
+			// layout applied them every step). Replay them before the weights change; the records are then
+			// current (done = step), as every eager EMA is.
+			NGP_HIP(hipDeviceSynchronize());
+			t->materialize(nullptr, true);
+			NGP_HIP(hipDeviceSynchronize());
+		}
 		NGP_HIP(hipMemcpy(t->w32, params_host, n * 4, hipMemcpyHostToDevice));
 		k_f32_to_f16<<<div_round_up(n, 256), 256>>>(t->w32, t->w16, t->inf16, n);
 		NGP_HIP(hipGetLastError());

@@ -438,6 +438,8 @@ struct Marcher {
 	// stepping-space steps to the next voxel (a ceil). Both are first taken from hardware exp/log
 	// (relative error ~1e-6, bound below) and recomputed exactly only when the approximate value lies
 	// within a margin (>= 10x that error) of a decision boundary: same integers as the exact evaluation.
+	// Both errors grow like 1 / log(1 + cone) (= cone.rl): the margins scale with it, so a small cone
+	// (cone_angle_constant down to 1e-5) simply takes the exact path more often, never a wrong integer.
 	__device__ __forceinline__ float step_empty(float t, uint32_t* mip_out = nullptr) const {
 		const V3 p = pos(t);
 		const float n = to_stepping_space(t, k());
@@ -449,11 +451,13 @@ struct Marcher {
 			float dt;
 			if (n1 > cone.a && n1 <= cone.b) {
 				// from_stepping_space(n1) = ngp_expf(n1 * log1p_c); __expf: v_exp_f32 (~2 ulp) of
-				// the same argument, so dt * 2 GRIDSIZE is off by <= ~3e-7 * t / dt ~ 1e-4 relative
+				// the same argument, so dt * 2 GRIDSIZE is off by <= ~3e-7 * t / dt ~ 3e-7 * rl relative
+				// (~8e-5 at cone 1/256). Margin: 13x that, relative to the boundary (mantissa 0.5 = powers of two)
 				dt = __expf(n1 * cone.log1p_c) - t;
 				int e;
-				const float mant = frexpf(dt * (2 * GRIDSIZE), &e);  // boundaries: mantissa 0.5 (= powers of two)
-				if (mant < 0.5005f || mant > 0.9995f) dt = from_stepping_space(n1, cone) - t;
+				const float mant = frexpf(dt * (2 * GRIDSIZE), &e);
+				const float mm = 3.9e-6f * cone.rl;  // 1e-3 at cone 1/256
+				if (mant < 0.5f + 0.5f * mm || mant > 1.0f - mm) dt = from_stepping_space(n1, cone) - t;
 			} else {
 				dt = from_stepping_space(n1, cone) - t;
 			}
@@ -466,9 +470,10 @@ struct Marcher {
 		float x;
 		if (target > cone.at && target <= cone.bt) {
 			// to_stepping_space(target) = ngp_logf(target) / log1p_c; __logf (v_log_f32) is within
-			// ~1e-6 absolute for target in (at, bt], i.e. ~3e-4 stepping-space units at cone 1/256
+			// ~1e-6 absolute for target in (at, bt], i.e. ~1e-6 * rl stepping-space units (~3e-4 at cone
+			// 1/256); margin 15x that (4e-3 at cone 1/256; >= 0.5 below cone ~3e-5: always exact)
 			x = __logf(target) * cone.rl - n;
-			if (fabsf(x - rintf(x)) < 4e-3f) x = to_stepping_space(target, cone) - n;
+			if (fabsf(x - rintf(x)) < 1.5625e-5f * cone.rl) x = to_stepping_space(target, cone) - n;
 		} else {
 			x = to_stepping_space(target, cone) - n;
 		}

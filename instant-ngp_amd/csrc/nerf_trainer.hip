@@ -455,8 +455,17 @@ int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint3
 	t->allreduce_user = user;
 	// an RCCL hook is stream-ordered and graph-capturable; a host callback (gloo) is not
 	t->dp_capturable = allreduce == ngp_dp_comm_allreduce;
+	if (t->dp_capturable && user && ngp_dp_comm_reserve((ngp_dp_comm*)user, ngp_model_n_params(t->model)) != NGP_OK) return NGP_ERROR;
 	if (t->train_graph) ngp_graph_destroy(t->train_graph);  // re-captured with (or without) the exchange
 	t->train_graph = nullptr;
+	return NGP_OK;
+}
+
+int ngp_nerf_trainer_buffers_read(const ngp_nerf_trainer* t, const float** grid, const uint8_t** bitfield, const float** mean) {
+	if (!t) return NGP_INVALID;
+	if (grid) *grid = (const float*)t->grid.p;
+	if (bitfield) *bitfield = (const uint8_t*)t->bitfield.p;
+	if (mean) *mean = (const float*)t->mean.p;
 	return NGP_OK;
 }
 

@@ -1,6 +1,7 @@
 """Data-parallel training over the GPUs of one node: one process per GPU,
 torch.distributed with the "nccl" backend (= RCCL over xGMI on ROCm), one all-reduce of the
-contiguous fp16 gradient buffer per step, the 1/N average folded into the optimizer's loss scale.
+contiguous fp16 gradient buffer per step (widened to fp32 on the wire, rounded once), the 1/N average
+folded into the optimizer's loss scale.
 
 The reference trains on one GPU only (multi-GPU is render replication); this module is
 the new exchange step. Sharding keeps the *global* ray index i so every rank draws exactly the rays
@@ -63,7 +64,7 @@ class EngineComm:
     (ngp_trainer_set_allreduce, ngp_nerf_trainer_set_data_parallel), so the all-reduce is issued by the
     engine on its own stream — inside a captured HIP graph if the step is captured."""
 
-    def __init__(self, rank, world, group=None):
+    def __init__(self, rank, world, group=None, wire="f32"):
         from ._capi import check, lib
         idb = (C.c_uint8 * 128)()
         if rank == 0:
@@ -76,6 +77,9 @@ class EngineComm:
         h = C.c_void_p()
         check(lib().ngp_dp_comm_create(rank, world, idb, C.byref(h)))
         self.handle, self.rank, self.world = h, rank, world
+        # fp16 gradient sums travel widened to fp32 and are rounded once (ngp_dp_comm_set_wire)
+        check(lib().ngp_dp_comm_set_wire(h, {"f32": 0, "f16": 1}[wire]))
+        self.wire = wire
         self.fn = C.cast(lib().ngp_dp_comm_allreduce, C.c_void_p)
 
     def allreduce(self, tensor, op="sum", stream=None):

@@ -205,26 +205,39 @@ class NerfTraining:
                                             C.byref(h)))
         self.handle = h
 
-    def _buffers(self):
-        # ngp_nerf_trainer_buffers discards a prelaunched (pipelined) sampler, so writes through the
-        # returned views are seen by the next step's sampling
+    def _buffers(self, write=False):
+        # reads keep a prelaunched (pipelined) sampler: it reads only the bitfield and writes none of the
+        # three buffers. ngp_nerf_trainer_buffers (write=True) discards it, so writes through the returned
+        # views are seen by the next step's sampling
         g, b, m = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        check(lib().ngp_nerf_trainer_buffers(self.handle, C.byref(g), C.byref(b), C.byref(m)))
+        fn = lib().ngp_nerf_trainer_buffers if write else lib().ngp_nerf_trainer_buffers_read
+        check(fn(self.handle, C.byref(g), C.byref(b), C.byref(m)))
         return g.value, b.value, m.value
+
+    def _views(self, write):
+        g, b, m = self._buffers(write)
+        return (wrap_device(g, N_CELLS * (self.cfg.max_cascade + 1), torch.float32),
+                wrap_device(b, BITFIELD_BYTES // 4, torch.float32).view(torch.uint8),
+                wrap_device(m, 1, torch.float32))
 
     @property
     def density_grid(self):
-        """fp32 [128^3 x (max_cascade + 1)] (testbed_nerf.cu:3412-3420), Morton order per cascade."""
-        return wrap_device(self._buffers()[0], N_CELLS * (self.cfg.max_cascade + 1), torch.float32)
+        """fp32 [128^3 x (max_cascade + 1)] (testbed_nerf.cu:3412-3420), Morton order per cascade. For
+        reading (logging, snapshots); modify through writable_buffers()."""
+        return self._views(False)[0]
 
     @property
     def mean_density(self):
-        return wrap_device(self._buffers()[2], 1, torch.float32)
+        return self._views(False)[2]
 
     @property
     def bitfield(self):
-        words = wrap_device(self._buffers()[1], BITFIELD_BYTES // 4, torch.float32)
-        return words.view(torch.uint8)
+        return self._views(False)[1]
+
+    def writable_buffers(self):
+        """(density_grid, bitfield, mean_density) views for MODIFYING the occupancy state between steps:
+        discards a prelaunched sampler so the next step samples with the caller's writes."""
+        return self._views(True)
 
     def set_data_parallel(self, rank, world, group=None, exchange_at_world_1=False):
         """Shard the rays (global ids kept), the compacted batch and the density-grid evaluation over
@@ -249,8 +262,8 @@ class NerfTraining:
 
     def set_pipeline(self, enable):
         """Launch the next step's ray sampling under this step's training pass (default on; identical
-        samples). Reading density_grid / bitfield / mean_density discards a prelaunched sampler, so
-        writes through them reach the next step."""
+        samples). Reading density_grid / bitfield / mean_density keeps it; writable_buffers() discards it,
+        so writes through those views reach the next step."""
         check(lib().ngp_nerf_trainer_set_pipeline(self.handle, int(enable)))
 
     def save_snapshot(self, path, network_config=None, include_optimizer_state=False, compress=True, stream=None):

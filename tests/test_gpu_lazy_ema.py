@@ -117,3 +117,31 @@ def test_lazy_ema_deserialize_resumes_bitwise(pkg):
     assert tr_l.serialize() == tr_e2.serialize()
     np.testing.assert_array_equal(tr_l.inference_params.cpu().numpy().view(np.uint16),
                                   tr_e2.inference_params.cpu().numpy().view(np.uint16))
+
+
+def test_lazy_ema_set_params_full_precision_bitwise(pkg):
+    """Trainer::set_params_full_precision (testbed.cu:4146) mid-training: the lazy layout must first
+    replay the EMA steps its skipped entries still owe on the OLD weights (the eager layout applied them
+    every step), then take the new weights; training and a serialize afterwards match the eager layout."""
+    runs = {}
+    for lazy in (False, True):
+        net, tr = make_trainer(pkg, "sdf", lazy)
+        for step in range(6):
+            x, dl = batch("sdf", 4096, step)
+            net.forward_backward(x, dl)
+            tr.optimizer_step(128.0)
+        torch.cuda.synchronize()
+        w = tr.params_full_precision.cpu().numpy().copy()
+        w[::3] *= 0.5  # new weights for a third of the parameters
+        tr.set_params_full_precision(w)
+        blob_now = tr.serialize()
+        for step in range(6, 10):
+            x, dl = batch("sdf", 4096, step)
+            net.forward_backward(x, dl)
+            tr.optimizer_step(128.0)
+        torch.cuda.synchronize()
+        runs[lazy] = (blob_now, tr.serialize(), tr.inference_params.cpu().numpy().view(np.uint16).copy())
+        del net, tr
+    assert runs[True][0] == runs[False][0], "serialize right after set_params_full_precision differs"
+    assert runs[True][1] == runs[False][1], "training after set_params_full_precision differs"
+    np.testing.assert_array_equal(runs[True][2], runs[False][2])

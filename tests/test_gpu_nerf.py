@@ -134,6 +134,45 @@ def test_generate_training_samples_cone(pkg, orc, scene, aabb_scale, n_rays, fra
     np.testing.assert_array_equal(got["coords"][:used], ref["coords"][:used])
 
 
+@pytest.mark.parametrize("aabb_scale,cone,n_rays,frac", [
+    (8.0, None, 1 << 16, 0.3), (32.0, None, 1 << 16, 0.15), (128.0, None, 1 << 16, 0.05),
+    (8.0, 1e-4, 1 << 14, 0.3), (8.0, 5e-4, 1 << 14, 0.3), (16.0, 2e-5, 1 << 13, 0.3), (8.0, 0.02, 1 << 14, 0.3)])
+def test_sampler_and_loss_cone_at_scale(pkg, orc, scene, aabb_scale, cone, n_rays, frac):
+    """Fox-scale and larger ray counts (>= 64k rays at aabb_scale 8, 32, 128) and user-set cone angles
+    from 2e-5 to 0.02: the sampler's hardware exp/log speculation in empty space (csrc/nerf.hip
+    step_empty) falls back to the exact path near every integer decision, with margins that scale with
+    1 / log(1 + cone), so sample sets, compacted counts and coordinates stay bit-exact with the oracle."""
+    ds, ims, pix = scene
+    kw = {} if cone is None else {"cone_angle_constant": cone}
+    cfg = pkg.nerf.default_config(aabb_scale, **kw)
+    _, bf = occupancy(orc, seed=int(aabb_scale) + n_rays, frac=frac, max_cascade=cfg.max_cascade)
+    r = rng(pkg, 2024 + n_rays)
+    max_samples = 1 << 22
+    bf_t = torch.from_numpy(bf).cuda()
+    got = pkg.nerf.generate_training_samples(ds, cfg, n_rays, r, max_samples, bf_t, n_rays_total=n_rays)
+    ref = orc.nerf_generate_samples(cfg, ims, pix, n_rays, orc_rng(orc, r), max_samples, bf)
+    gn = {k: v.cpu().numpy() for k, v in got.items()}
+    np.testing.assert_array_equal(gn["counters"].view(np.uint32), ref["counters"])
+    kept = int(ref["counters"][0])
+    assert kept > n_rays // 4
+    np.testing.assert_array_equal(gn["ray_indices"][:kept].view(np.uint32), ref["ray_indices"][:kept])
+    np.testing.assert_array_equal(gn["numsteps"][:kept].view(np.uint32), ref["numsteps"][:kept])
+    used = min(int(ref["counters"][1]), max_samples)
+    assert used > n_rays
+    np.testing.assert_array_equal(gn["coords"][:used], ref["coords"][:used])
+    # compaction of the same samples (testbed_nerf.cu:1660-2012)
+    g = np.random.default_rng(n_rays)
+    out = g.uniform(-3.0, 2.0, (max_samples, 16)).astype(np.float16)
+    mean = torch.tensor([0.003], device="cuda")
+    max_c = 1 << 18
+    gl = pkg.nerf.compute_loss(ds, cfg, n_rays, r, max_c, got, torch.from_numpy(out).cuda(), mean)
+    rl = orc.nerf_compute_loss(cfg, ims, pix, n_rays, orc_rng(orc, r), max_c, ref, out.view(np.uint16), 0.003)
+    cc = int(gl["compacted_counter"].cpu().numpy().view(np.uint32)[0])
+    assert cc == int(rl["compacted_counter"][0]) and cc > 0
+    n_used = min(cc, max_c)
+    np.testing.assert_array_equal(gl["coords_compacted"].cpu().numpy()[:n_used], rl["coords_compacted"][:n_used])
+
+
 @pytest.mark.parametrize("loss_type,act,aabb_scale", [(4, 3, 1.0), (0, 2, 1.0), (1, 3, 1.0), (4, 3, 8.0), (0, 2, 4.0)])
 def test_compute_loss(pkg, orc, scene, loss_type, act, aabb_scale):
     """compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012). Compositing weights use the shared

@@ -31,18 +31,21 @@ if has prof; then
   head -12 "$OUT/kernel_stats.csv"
 fi
 if has pmc; then
-  # separate passes (TCC slots): sized read requests, WRITE_SIZE, MFMA utilisation; eager launches
-  BENCH_PMC="python3 bench.py --no-cpu-baseline --e2e-seconds 0 --c3-seconds 0 --no-c2p --no-c5 --graph 0 --steps 5 --warmup 2 ${PMC_ARGS}"
-  i=0
-  for c in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" "WRITE_SIZE" \
-           "MfmaUtil SQ_INSTS_VALU_MFMA_MOPS_F16"; do
-    i=$((i+1))
-    timeout -k 10 300 rocprofv3 --pmc $c -f csv -d "$OUT/pmc_$i" -o run -- $BENCH_PMC > "$OUT/pmc_$i.json" 2> "$OUT/pmc_$i.err"
-    find "$OUT/pmc_$i" -name '*counter_collection.csv' -exec cp {} "$OUT/counters_$i.csv" \;
-    rm -rf "$OUT/pmc_$i"
+  # separate passes (TCC slots): sized read requests, WRITE_SIZE, MFMA utilisation; eager launches; one
+  # summary per variant (PMC_VARIANTS, default C2 C2p C5) -> $OUT/pmc_summary_<variant>.json
+  for V in ${PMC_VARIANTS:-C2 C2p C5}; do
+    BENCH_PMC="python3 bench.py --variant $V --no-cpu-baseline --e2e-seconds 0 --c3-seconds 0 --no-c2p --no-c5 --graph 0 --steps 5 --warmup 2 ${PMC_ARGS}"
+    i=0
+    for c in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" "WRITE_SIZE" \
+             "MfmaUtil SQ_INSTS_VALU_MFMA_MOPS_F16"; do
+      i=$((i+1))
+      timeout -k 10 300 rocprofv3 --pmc $c -f csv -d "$OUT/pmc_${V}_$i" -o run -- $BENCH_PMC > "$OUT/pmc_${V}_$i.json" 2> "$OUT/pmc_${V}_$i.err"
+      find "$OUT/pmc_${V}_$i" -name '*counter_collection.csv' -exec cp {} "$OUT/counters_${V}_$i.csv" \;
+      rm -rf "$OUT/pmc_${V}_$i"
+    done
+    python3 tools/pmc_summary.py "$OUT"/counters_${V}_[0-9].csv > "$OUT/pmc_summary_$V.json"
+    python3 -c "import json; d=json.load(open('$OUT/pmc_summary_$V.json')); [print('$V', k[:60], {a: round(b, 4) if isinstance(b, float) else b for a, b in v.items()}) for k, v in d.items()]"
   done
-  python3 tools/pmc_summary.py "$OUT"/counters_[0-9].csv > "$OUT/pmc_summary.json"
-  python3 -c "import json; d=json.load(open('$OUT/pmc_summary.json')); [print(k[:60], {a: round(b, 4) if isinstance(b, float) else b for a, b in v.items()}) for k, v in d.items()]"
 fi
 if has pmcx; then
   # extra counters for one pass, e.g. PMCX="TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"

@@ -19,9 +19,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8):
+def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8, rank=0, world=1):
     """Train the full NeRF step for `seconds` of wall clock on the procedural stand-in, then render the
-    held-out views. Returns the result dict (samples/s over the training wall time, mean PSNR)."""
+    held-out views. Returns the result dict (samples/s over the training wall time, mean PSNR).
+    world > 1 (torch.distributed initialised): data-parallel training (NerfTraining.set_data_parallel:
+    rays sharded with their global ids, engine RCCL exchange); every rank stops after the same step
+    (decided jointly every 32 steps) and rank 0 renders the held-out views."""
     S = pkg.synthetic
     t0 = time.time()
     ds = S.lego_like_dataset(n_images=images, width=res, height=res, seed=0, device="cuda")
@@ -31,6 +34,10 @@ def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8):
     net = pkg.create_nerf_network(ncfg)
     tr = pkg.Trainer(net, ncfg["optimizer"])
     run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
+    if world > 1:
+        import torch.distributed as dist
+        run.set_data_parallel(rank, world)
+        dist.barrier()
     torch.cuda.synchronize()
     samples, steps = 0, 0
     t_start = time.time()
@@ -41,10 +48,22 @@ def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8):
         steps += 1
         if steps % 100 == 1:
             curve.append((round(time.time() - t_start, 2), steps, round(st["loss"], 6)))
-        if time.time() - t_start >= seconds:
+        if world > 1:
+            if steps % 32 == 0:  # the ranks must run the same number of steps (collectives inside)
+                flag = torch.tensor([float(time.time() - t_start >= seconds)], device="cuda")
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                if flag.item() > 0:
+                    break
+        elif time.time() - t_start >= seconds:
             break
     torch.cuda.synchronize()
     t_train = time.time() - t_start
+    if world > 1:
+        tt = torch.tensor([t_train], device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_train = float(tt.item())
+        if rank != 0:
+            return {"value": samples / t_train, "steps": steps, "train_seconds": t_train}
     r = pkg.nerf.NerfRenderer()
     poses = S.camera_poses(images + test_views, seed=12345)[-test_views:]
     ps, t_render = [], time.time()
@@ -59,11 +78,12 @@ def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8):
         "metric": "training samples/sec + PSNR@30s, NeRF Lego at 1/2/4/8 MI355X",
         "value": samples / t_train, "unit": "samples/s", "psnr": float(np.mean(ps)), "psnr_views": [round(p, 2) for p in ps],
         "train_seconds": round(t_train, 2), "steps": steps, "ms_per_step": 1e3 * t_train / steps,
-        "n_gpus": 1, "dtype": "f16",
+        "n_gpus": world, "dtype": "f16",
         "data": f"procedural Lego stand-in: {images} views {res}x{res} RGBA8, camera_angle_x of lego "
                 "(nerf_synthetic is not in the image)",
         "config": {"workload": "Testbed NeRF training (configs/nerf/base.json fork, C2) + NerfTracer eval "
-                               f"(black bg, snapped, spp {spp})", "batch": 1 << 18},
+                               f"(black bg, snapped, spp {spp})", "batch": 1 << 18,
+                   "parallelism": f"dp{world}"},
         "dataset_seconds": round(t_data, 2), "render_seconds": round(t_render, 2), "loss_curve": curve[:40],
     }
 
