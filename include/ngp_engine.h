@@ -39,7 +39,7 @@ enum { NGP_LAYOUT_AOS = 0, NGP_LAYOUT_SOA = 1 };
 /* Engine extension for NerfNetwork inference outputs: only the 4 live rows (raw rgb, raw density) as
  * AoS [n x stride >= 4], skipping the 12 padded outputs of padded_output_width 16 (nerf_network.h:463). */
 enum { NGP_LAYOUT_AOS_RGBD = 2 };
-enum { NGP_GRAD_OVERWRITE = 0, NGP_GRAD_ACCUMULATE = 1 }; /* tcnn::EGradientMode */
+enum { NGP_GRAD_OVERWRITE = 0, NGP_GRAD_ACCUMULATE = 1, NGP_GRAD_IGNORE = 2 }; /* tcnn::EGradientMode */
 
 /* ---- library ------------------------------------------------------------------------------ */
 const char* ngp_last_error(void);
@@ -104,7 +104,9 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value);
 int ngp_model_reserve(ngp_model* m, uint32_t n);
 /* Inspection of the last training pass's intermediates (the role of tcnn's forward_activations(ctx),
  * nerf_network.h:502-507): "encoding" = fp16 AoS [n x encoding_width] grid output of the last unfused
- * forward, "dL_dencoding" = fp16 AoS [n x encoding_width] input of the grid backward. Device pointer
+ * forward, "dL_dencoding" = fp16 AoS [n x encoding_width] input of the grid backward, "dL_dsh" = fp16
+ * [n x 16] dL/d(SH encoding) of the last backward with input gradients, "dw_slabs" = the fp32 per-block
+ * MLP weight-gradient partial sums. Device pointer
  * valid until the next call that grows the workspace. */
 int ngp_model_workspace(ngp_model* m, const char* name, void** ptr, uint64_t* bytes);
 /* Counts workspace reallocations. A graph from ngp_trainer_capture_training_step holds workspace
@@ -121,9 +123,30 @@ int ngp_density(ngp_model* m, void* stream, uint32_t n, const float* input, uint
 /* forward_impl (nerf_network.h:179-254) -> context; output may be NULL */
 int ngp_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
                 uint32_t output_stride, int use_inference_params, ngp_ctx** ctx);
-/* backward_impl (nerf_network.h:256-335): param gradients into the gradient buffer given to set_params */
-int ngp_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* dL_doutput, uint32_t dL_stride, int grad_mode);
+/* backward_impl (nerf_network.h:256-335): param gradients into the gradient buffer given to set_params
+ * (grad_mode NGP_GRAD_IGNORE: untouched). dL_dinput (nullable, the reference's `GPUMatrixDynamic<float>*
+ * dL_dinput`): fp32 AoS [n x dL_dinput_stride]; rows 0..n_pos_dims-1 receive dL/dposition through the
+ * grid encoding, a NerfNetwork's rows dir_offset..+2 dL/ddirection through the SH encoding
+ * (nerf_network.h:282-299, 317-333); other rows are not written. */
+int ngp_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* dL_doutput, uint32_t dL_stride, float* dL_dinput,
+                 uint32_t dL_dinput_stride, int grad_mode);
 void ngp_ctx_destroy(ngp_ctx* ctx);
+/* NerfNetwork::density_forward (nerf_network.h:355-382) -> context; output (nullable): the density
+ * network's fp16 output AoS [n x output_stride] (16 rows) */
+int ngp_density_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                        uint32_t output_stride, int use_inference_params, ngp_ctx** ctx);
+/* NerfNetwork::density_backward (nerf_network.h:384-428): dL_doutput = dL/d(density network output),
+ * fp16 AoS [n x dL_stride] (16 rows, stride a multiple of 4). Gradients of the density MLP and the grid
+ * (the rgb MLP's are left as they are); dL_dinput as in ngp_backward (position rows only). */
+int ngp_density_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* dL_doutput, uint32_t dL_stride, float* dL_dinput,
+                         uint32_t dL_dinput_stride, int grad_mode);
+/* tcnn Network::input_gradient(stream, dim, input, d_dinput, backprop_scale) — the reference's normals
+ * (testbed_nerf.cu:2616, dim 3 = density; testbed.cu:4621, SDF dim 0): forward, backward of a one-hot
+ * dL/doutput (row `dim` = backprop_scale) with parameter gradients ignored, result / backprop_scale.
+ * d_dinput fp32 AoS [n x d_dinput_stride] (may alias `input` with the same stride, as the reference
+ * passes positions_matrix for both: only the position/direction rows are written, after every read). */
+int ngp_input_gradient(ngp_model* m, void* stream, uint32_t dim, uint32_t n, const float* input, uint32_t input_stride,
+                       float* d_dinput, uint32_t d_dinput_stride, float backprop_scale);
 /* fused training pass = forward_impl + backward_impl (src/testbed_nerf.cu:4077-4078) in one call */
 int ngp_forward_backward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
                          uint32_t output_stride, const void* dL_doutput, uint32_t dL_stride, int grad_mode);
@@ -131,8 +154,10 @@ int ngp_forward_backward(ngp_model* m, void* stream, uint32_t n, const float* in
 /* Raw position-encoding access (tcnn GridEncoding forward / backward). out fp16 [n x encoding_width]. */
 int ngp_encoding_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
                          uint32_t output_stride, uint32_t output_layout, int use_inference_params);
+/* dL_dinput (nullable; needs dL_layout AoS): fp32 [n x dL_dinput_stride], rows 0..n_pos_dims-1 */
 int ngp_encoding_backward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride,
-                          const void* dL_doutput, uint32_t dL_stride, uint32_t dL_layout, int grad_mode);
+                          const void* dL_doutput, uint32_t dL_stride, uint32_t dL_layout, float* dL_dinput,
+                          uint32_t dL_dinput_stride, int grad_mode);
 
 /* ---- trainer (tcnn::Trainer<float, __half, __half>, src/testbed.cu:4129) -------------------- */
 /* optimizer_json: the "optimizer" config section (Ema / ExponentialDecay / Adam nesting).

@@ -7,8 +7,10 @@
 //   NerfNetwork<__half>                      nerf_network.h:77-578 (ctor :81-112)
 //     inference_mixed_precision(stream, input, output, use_inference_params)   :116-174
 //     forward(stream, input, output, use_inference_params) -> Context          :179-254
-//     backward(stream, ctx, dL_doutput, grad_mode)                              :256-335
+//     backward(stream, ctx, dL_doutput, dL_dinput, grad_mode)                   :256-335
+//     input_gradient(stream, dim, input, d_dinput, backprop_scale)   tcnn Network; testbed_nerf.cu:2616, testbed.cu:4621
 //     density(stream, input, output, use_inference_params)                      :337-353
+//     density_forward / density_backward                                       :355-428
 //     n_params / padded_output_width / input_width / output_width / layer_sizes :459-490
 //   NetworkWithInputEncoding                 src/testbed.cu:4101-4110
 //   Trainer (optimizer_step, params, serialize, set_params_full_precision)      src/testbed.cu:4129-4146,
@@ -42,6 +44,8 @@ struct MatrixView {
 	uint32_t stride = 0;   // elements between consecutive samples (CM) or features (RM)
 	Layout layout = Layout::CM;
 };
+
+enum class GradientMode { Ignore = NGP_GRAD_IGNORE, Overwrite = NGP_GRAD_OVERWRITE, Accumulate = NGP_GRAD_ACCUMULATE };  // tcnn::EGradientMode
 
 class Context {  // tcnn::Context of forward(), consumed by backward()
 public:
@@ -91,11 +95,22 @@ public:
 		      "forward");
 		return std::unique_ptr<Context>(new Context(c));
 	}
-	// backward: parameter gradients into the trainer's gradient buffer (tcnn EGradientMode)
-	void backward(void* stream, const Context& ctx, const MatrixView<const uint16_t>& dL_doutput, bool accumulate = false) {
-		check(ngp_backward(m_, stream, ctx.get(), dL_doutput.data, dL_doutput.stride,
-		                   accumulate ? NGP_GRAD_ACCUMULATE : NGP_GRAD_OVERWRITE),
+	// backward: parameter gradients into the trainer's gradient buffer (tcnn EGradientMode); dL_dinput (CM,
+	// fp32) receives the input gradients when given (nerf_network.h:262, 282-299, 317-333)
+	void backward(void* stream, const Context& ctx, const MatrixView<const uint16_t>& dL_doutput,
+	              MatrixView<float>* dL_dinput = nullptr, GradientMode mode = GradientMode::Overwrite) {
+		if (dL_dinput && dL_dinput->layout != Layout::CM) throw std::runtime_error("backward: dL_dinput must be in column major format");
+		check(ngp_backward(m_, stream, ctx.get(), dL_doutput.data, dL_doutput.stride, dL_dinput ? dL_dinput->data : nullptr,
+		                   dL_dinput ? dL_dinput->stride : 0, (int)mode),
 		      "backward");
+	}
+	// tcnn Network::input_gradient: d output[dim] / d input (the reference's normals). d_dinput may be the
+	// input matrix itself, as testbed_nerf.cu:2616 passes it.
+	void input_gradient(void* stream, uint32_t dim, const MatrixView<const float>& input, const MatrixView<float>& d_dinput,
+	                    float backprop_scale = 128.f) {
+		require_cm(input, "input_gradient");
+		check(ngp_input_gradient(m_, stream, dim, input.n, input.data, input.stride, d_dinput.data, d_dinput.stride, backprop_scale),
+		      "input_gradient");
 	}
 	// GridEncoding::set_max_level / set_max_level_gpu (src/testbed.cu:3856-3864; testbed_nerf.cu:3996,4004)
 	void set_max_level(float max_level, const float* max_level_per_sample_gpu = nullptr) {
@@ -128,6 +143,25 @@ public:
 		check(ngp_density(m_, stream, input.n, input.data, input.stride, output.data, output.stride, (uint32_t)output.layout,
 		                  use_inference_params ? 1 : 0),
 		      "density");
+	}
+	// NerfNetwork::density_forward / density_backward (nerf_network.h:355-428): the density network alone,
+	// its 16-row output CM; backward writes density-MLP and grid gradients (and dL/dposition if asked)
+	std::unique_ptr<Context> density_forward(void* stream, const MatrixView<const float>& input, MatrixView<uint16_t>* output,
+	                                         bool use_inference_params = false) {
+		require_cm(input, "density_forward");
+		ngp_ctx* c = nullptr;
+		check(ngp_density_forward(m_, stream, input.n, input.data, input.stride, output ? output->data : nullptr,
+		                          output ? output->stride : 0, use_inference_params ? 1 : 0, &c),
+		      "density_forward");
+		return std::unique_ptr<Context>(new Context(c));
+	}
+	void density_backward(void* stream, const Context& ctx, const MatrixView<const uint16_t>& dL_doutput,
+	                      MatrixView<float>* dL_dinput = nullptr, GradientMode mode = GradientMode::Overwrite) {
+		if (dL_dinput && dL_dinput->layout != Layout::CM)
+			throw std::runtime_error("NerfNetwork::density_backward input must be in column major format.");
+		check(ngp_density_backward(m_, stream, ctx.get(), dL_doutput.data, dL_doutput.stride, dL_dinput ? dL_dinput->data : nullptr,
+		                           dL_dinput ? dL_dinput->stride : 0, (int)mode),
+		      "density_backward");
 	}
 };
 

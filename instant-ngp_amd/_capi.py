@@ -98,11 +98,14 @@ SIGNATURES = {
     "ngp_inference": (i32, [P, P, u32, P, u32, P, u32, u32, i32]),
     "ngp_density": (i32, [P, P, u32, P, u32, P, u32, u32, i32]),
     "ngp_forward": (i32, [P, P, u32, P, u32, P, u32, i32, C.POINTER(P)]),
-    "ngp_backward": (i32, [P, P, P, P, u32, i32]),
+    "ngp_backward": (i32, [P, P, P, P, u32, P, u32, i32]),
+    "ngp_density_forward": (i32, [P, P, u32, P, u32, P, u32, i32, C.POINTER(P)]),
+    "ngp_density_backward": (i32, [P, P, P, P, u32, P, u32, i32]),
+    "ngp_input_gradient": (i32, [P, P, u32, u32, P, u32, P, u32, f32]),
     "ngp_ctx_destroy": (None, [P]),
     "ngp_forward_backward": (i32, [P, P, u32, P, u32, P, u32, P, u32, i32]),
     "ngp_encoding_forward": (i32, [P, P, u32, P, u32, P, u32, u32, i32]),
-    "ngp_encoding_backward": (i32, [P, P, u32, P, u32, P, u32, u32, i32]),
+    "ngp_encoding_backward": (i32, [P, P, u32, P, u32, P, u32, u32, P, u32, i32]),
     "ngp_trainer_create": (i32, [P, C.c_char_p, u64, C.POINTER(P)]),
     "ngp_trainer_destroy": (None, [P]),
     "ngp_trainer_optimizer_step": (i32, [P, P, f32]),

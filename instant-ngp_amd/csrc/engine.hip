@@ -123,7 +123,20 @@ struct ngp_ctx {
 	uint32_t input_stride;
 	bool use_inference_params;
 	uint64_t generation;  // the model workspace generation the encoding lives in
+	bool density_only = false;  // from ngp_density_forward: only ngp_density_backward may consume it
 };
+
+namespace ngp {
+// Optional parts of a backward pass (ngp_model::train_pass)
+struct BwdExtra {
+	float* dL_dinput = nullptr;     // fp32 AoS [n x dinput_stride]: rows 0..D-1 (+ the direction rows of a NerfNetwork)
+	uint32_t dinput_stride = 0;
+	float dinput_scale = 1.f;
+	bool density_only = false;      // NerfNetwork::density_backward: the density network alone
+	const f16* ddens = nullptr;     // its dL/d(density output), fp16 AoS [n x ddens_stride]
+	uint32_t ddens_stride = 0;
+};
+}  // namespace ngp
 
 struct ngp_model {
 	bool nerf = true;
@@ -137,7 +150,7 @@ struct ngp_model {
 	uint32_t* d_fragmap = nullptr;  // [n_matrix x 2] fragment slot (f16 index) of each matrix param: fwd, bwd
 	bool frags_current = false;     // `frags` holds the fragments of the current `params` (kept by the optimizer)
 	uint32_t n_all_frags = 0;
-	DevBuf frags, frags_inf, enc, denc, slabs, scatter_ws, out_ws, dl_ws;
+	DevBuf frags, frags_inf, enc, denc, slabs, scatter_ws, out_ws, dl_ws, dsh_ws, dl1_ws;
 	int grid_backward_mode = 0;  // 0 auto, 1 direct (tcnn-style), 3 bucketed (grid_scatter.h)
 	uint32_t win_debug = 0;      // timing experiments only (see grid_scatter.h)
 	ScatterPlan sc_plan;
@@ -170,7 +183,7 @@ struct ngp_model {
 	std::unique_ptr<ngp_ctx> last_ctx;
 
 	ngp_model() {
-		for (DevBuf* b : {&frags, &frags_inf, &enc, &denc, &slabs, &scatter_ws, &out_ws, &dl_ws}) b->epoch = &ws_epoch;
+		for (DevBuf* b : {&frags, &frags_inf, &enc, &denc, &slabs, &scatter_ws, &out_ws, &dl_ws, &dsh_ws, &dl1_ws}) b->epoch = &ws_epoch;
 	}
 
 	~ngp_model() {
@@ -306,7 +319,7 @@ struct ngp_model {
 	}
 	void run_mlp(hipStream_t s, MlpMode mode, uint32_t n, const float* in, uint32_t stride, const f16* encbuf, f16* out,
 	             uint32_t out_stride, uint32_t out_layout, const f16* dL, uint32_t dL_stride, f16* dL_denc, float* slab,
-	             bool inference) {
+	             bool inference, const BwdExtra* ex = nullptr, f16* dL_dsh = nullptr) {
 		f16x8* f;
 		if (frags_async && !inference) {
 			f = (f16x8*)frags.p;
@@ -323,12 +336,15 @@ struct ngp_model {
 			a.frags = f; a.n_frags = n_all_frags; a.out = out; a.out_stride = out_stride; a.out_layout = out_layout;
 			a.dL_dout = dL; a.dL_stride = dL_stride; a.dL_denc = dL_denc; a.denc_stride = enc_width; a.dw_slab = slab;
 			a.n_matrix = (uint32_t)n_matrix(); a.density_woff = 0; a.rgb_woff = (uint32_t)mlp0_params;
+			a.dL_dsh = dL_dsh;
+			if (ex) { a.dL_ddens = ex->ddens; a.ddens_stride = ex->ddens_stride; }
 			if (mode == MLP_INFER_ENC || mode == MLP_TRAIN_ENC) {
 				if (inference) sync_inference(s);
 				a.table = pick(inference) + grid_offset(); a.max_level = max_level; a.gc = make_grid_const(grid);
 			}
 			ProfScope ps(mode == MLP_TRAIN ? "mlp_train" : mode == MLP_DENSITY ? "mlp_density"
-			             : mode == MLP_INFER_ENC ? "mlp_infer_enc" : mode == MLP_TRAIN_ENC ? "mlp_train_enc" : "mlp_infer", s);
+			             : mode == MLP_INFER_ENC ? "mlp_infer_enc" : mode == MLP_TRAIN_ENC ? "mlp_train_enc"
+			             : mode == MLP_DENSITY_TRAIN ? "mlp_density_train" : "mlp_infer", s);
 			nerf_mlp_run(nplan, mode, a, s);
 		} else {
 			MlpArgs a{};
@@ -339,23 +355,43 @@ struct ngp_model {
 			mlp_run(mplan, mode == MLP_DENSITY ? MLP_INFER : mode, a, s);
 		}
 	}
-	// backward given the encoding already in `encbuf`: MLP fwd+bwd (+output), dW slabs, grid scatter
+	// backward given the encoding already in `encbuf`: MLP fwd+bwd (+output), dW slabs, grid scatter.
+	// ex (optional): input gradients and the density-only backward (BwdExtra); grad_mode NGP_GRAD_IGNORE
+	// leaves the parameter gradients untouched (tcnn EGradientMode::Ignore, input_gradient).
 	void train_pass(hipStream_t s, uint32_t n, const float* in, uint32_t stride, const f16* encbuf, f16* out, uint32_t out_stride,
-	                const void* dL, uint32_t dL_stride, int grad_mode) {
-		NGP_CHECK(gradients, "model has no gradient buffer: call ngp_model_set_params");
+	                const void* dL, uint32_t dL_stride, int grad_mode, const BwdExtra& ex = BwdExtra{}) {
+		NGP_CHECK(gradients || grad_mode == NGP_GRAD_IGNORE, "model has no gradient buffer: call ngp_model_set_params");
+		NGP_CHECK(!ex.density_only || (nerf && encbuf), "density backward: a NerfNetwork with its encoding");
 		f16* dL_denc = (f16*)denc.get((size_t)n * enc_width * sizeof(f16));
 		const uint32_t blocks = nerf ? nerf_mlp_train_blocks(n) : mlp_train_blocks(n);
 		float* slab = (float*)slabs.get((size_t)blocks * n_matrix() * sizeof(float));
+		f16* dsh = ex.dL_dinput && nerf && !ex.density_only ? (f16*)dsh_ws.get((size_t)n * 16 * sizeof(f16)) : nullptr;
 		// encbuf == nullptr: the MLP kernel encodes the positions itself (fused_training_ok)
-		run_mlp(s, encbuf ? MLP_TRAIN : MLP_TRAIN_ENC, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride,
-		        dL_denc, slab, false);
+		const MlpMode mode = ex.density_only ? MLP_DENSITY_TRAIN : encbuf ? MLP_TRAIN : MLP_TRAIN_ENC;
+		run_mlp(s, mode, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride, dL_denc, slab, false, &ex, dsh);
+		// dL/dinput through the grid (position rows) and the SH encoding (direction rows, NerfNetwork). Run
+		// last: dL_dinput may alias the input (the reference passes positions_matrix for both,
+		// testbed_nerf.cu:2616), which the grid backward still reads
+		auto input_gradient = [&]() {
+			if (!ex.dL_dinput) return;
+			ProfScope ps("input_gradient", s);
+			InputGradArgs ia{n, in, stride, params + grid_offset(), dL_denc, enc_width, max_level, max_level_per_sample, dsh,
+			                 dir_offset, ex.dL_dinput, ex.dinput_stride, ex.dinput_scale};
+			grid_input_gradient(grid, ia, s);
+		};
+		if (grad_mode == NGP_GRAD_IGNORE) {
+			input_gradient();
+			return;
+		}
 		// the dW slab reduction (MLP section of the gradient) and the grid backward (grid section) are
 		// independent: for large batches the reduction runs in extra blocks of the grid backward's last
-		// kernel (fuse_slabs, default), or on the side stream under it (overlap bit 4)
+		// kernel (fuse_slabs, default), or on the side stream under it (overlap bit 4). The density-only
+		// backward reduces the density MLP's leading slice of each slab (the rgb gradients stay untouched).
 		const bool ovl = use_sorted(n) && (overlap & 4);
-		const bool fused = use_sorted(n) && !ovl && fuse_slabs;
+		const bool fused = use_sorted(n) && !ovl && fuse_slabs && !ex.density_only;
+		const uint32_t n_red = ex.density_only ? (uint32_t)mlp0_params : (uint32_t)n_matrix();
 		SlabJob sj;
-		sj.slabs = slab; sj.n_slabs = blocks; sj.n = (uint32_t)n_matrix(); sj.grad = gradients;
+		sj.slabs = slab; sj.n_slabs = blocks; sj.n = n_red; sj.grad = gradients; sj.stride = (uint32_t)n_matrix();
 		sj.accumulate = grad_mode == NGP_GRAD_ACCUMULATE;
 		hipStream_t rs = s;
 		if (ovl) {
@@ -366,12 +402,13 @@ struct ngp_model {
 		}
 		if (!fused) {
 			ProfScope ps("reduce_slabs", rs);
-			reduce_slabs(slab, blocks, (uint32_t)n_matrix(), gradients, grad_mode == NGP_GRAD_ACCUMULATE, rs);
+			reduce_slabs(slab, blocks, n_red, gradients, grad_mode == NGP_GRAD_ACCUMULATE, rs, (uint32_t)n_matrix());
 		}
 		if (ovl) NGP_HIP(hipEventRecord(ev_red, side));
 		GridBwdArgs b{n, in, stride, dL_denc, enc_width, AoS, gradients + grid_offset(), max_level, max_level_per_sample};
 		scatter_grid_grad(s, b, grad_mode != NGP_GRAD_ACCUMULATE, fused ? &sj : nullptr);
 		if (ovl) NGP_HIP(hipStreamWaitEvent(s, ev_red, 0));
+		input_gradient();
 	}
 	// Hash-grid backward: destination-bucketed exact sums (n >= 4096, or mode 3), else tcnn-style direct
 	// packed-f16 atomics (small batches, where the bucket plan costs more than the atomics).
@@ -457,6 +494,16 @@ struct ngp_graph {
 		if (graph) (void)hipGraphDestroy(graph);
 	}
 };
+
+// dL/doutput of tcnn's input_gradient: row `dim` of every sample = scale, every other row 0
+__global__ static void k_one_hot_f16(f16* out, uint32_t n, uint32_t width, uint32_t dim, f16 v) {
+	const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+	if (i < (uint64_t)n * width) out[i] = (i % width) == dim ? v : (f16)0.f;
+}
+static void fill_one_hot_f16(f16* out, uint32_t n, uint32_t width, uint32_t dim, float v, hipStream_t s) {
+	k_one_hot_f16<<<div_round_up((uint64_t)n * width, 256), 256, 0, s>>>(out, n, width, dim, (f16)v);
+	NGP_HIP(hipGetLastError());
+}
 
 // ------------------------------------------------------------------------------------------------
 // C-ABI
@@ -654,8 +701,9 @@ int ngp_model_workspace(ngp_model* m, const char* name, void** ptr, uint64_t* by
 	NGP_ARG(m && name && ptr);
 	NGP_TRY({
 		const std::string k(name);
-		DevBuf* b = k == "encoding" ? &m->enc : k == "dL_dencoding" ? &m->denc : k == "dw_slabs" ? &m->slabs : nullptr;
-		NGP_CHECK(b, "ngp_model_workspace: unknown workspace '" + k + "' (encoding, dL_dencoding, dw_slabs)");
+		DevBuf* b = k == "encoding" ? &m->enc : k == "dL_dencoding" ? &m->denc : k == "dw_slabs" ? &m->slabs
+		          : k == "dL_dsh" ? &m->dsh_ws : nullptr;
+		NGP_CHECK(b, "ngp_model_workspace: unknown workspace '" + k + "' (encoding, dL_dencoding, dL_dsh, dw_slabs)");
 		*ptr = b->p;
 		if (bytes) *bytes = b->bytes;
 	});
@@ -671,9 +719,20 @@ int ngp_encoding_forward(ngp_model* m, void* stream, uint32_t n, const float* in
 }
 
 int ngp_encoding_backward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride,
-                          const void* dL_doutput, uint32_t dL_stride, uint32_t dL_layout, int grad_mode) {
-	NGP_ARG(m && (n == 0 || (input && dL_doutput)) && dL_layout <= 1);
+                          const void* dL_doutput, uint32_t dL_stride, uint32_t dL_layout, float* dL_dinput,
+                          uint32_t dL_dinput_stride, int grad_mode) {
+	NGP_ARG(m && (n == 0 || (input && dL_doutput)) && dL_layout <= 1 && grad_mode >= 0 && grad_mode <= NGP_GRAD_IGNORE);
+	NGP_ARG(!dL_dinput || (dL_layout == NGP_LAYOUT_AOS && dL_dinput_stride >= m->grid.n_dims));
 	NGP_TRY({
+		if (n == 0) return NGP_OK;
+		m->require_params(false);
+		if (dL_dinput) {
+			ProfScope ps("input_gradient", S(stream));
+			InputGradArgs ia{n, input, input_stride, m->params + m->grid_offset(), (const f16*)dL_doutput, dL_stride, m->max_level,
+			                 m->max_level_per_sample, nullptr, 0, dL_dinput, dL_dinput_stride, 1.f};
+			grid_input_gradient(m->grid, ia, S(stream));
+		}
+		if (grad_mode == NGP_GRAD_IGNORE) return NGP_OK;
 		NGP_CHECK(m->gradients, "model has no gradient buffer");
 		GridBwdArgs b{n, input, input_stride, (const f16*)dL_doutput, dL_stride, dL_layout, m->gradients + m->grid_offset(),
 		              m->max_level, m->max_level_per_sample};
@@ -734,14 +793,84 @@ int ngp_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint
 	});
 }
 
-int ngp_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* dL_doutput, uint32_t dL_stride, int grad_mode) {
-	NGP_ARG(m && ctx && (ctx->n == 0 || dL_doutput));
+static int check_dinput(const ngp_model* m, float* dL_dinput, uint32_t stride) {
+	if (!dL_dinput) return NGP_OK;
+	const uint32_t need = m->nerf ? m->dir_offset + 3 : m->n_pos_dims;
+	if (stride < need) {
+		g_last_error = "dL_dinput: stride smaller than the rows the input gradient writes";
+		return NGP_INVALID;
+	}
+	return NGP_OK;
+}
+
+int ngp_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* dL_doutput, uint32_t dL_stride, float* dL_dinput,
+                 uint32_t dL_dinput_stride, int grad_mode) {
+	NGP_ARG(m && ctx && (ctx->n == 0 || dL_doutput) && grad_mode >= 0 && grad_mode <= NGP_GRAD_IGNORE);
+	if (check_dinput(m, dL_dinput, dL_dinput_stride) != NGP_OK) return NGP_INVALID;
 	NGP_TRY({
 		NGP_CHECK(ctx->generation == m->generation,
 		          "backward: the forward context is stale (another forward/inference ran on this model since)");
+		NGP_CHECK(!ctx->density_only, "backward: this context is from density_forward (use density_backward)");
 		if (ctx->n == 0) return NGP_OK;
+		BwdExtra ex;
+		ex.dL_dinput = dL_dinput; ex.dinput_stride = dL_dinput_stride;
 		m->train_pass(S(stream), ctx->n, ctx->input, ctx->input_stride, (const f16*)m->enc.p, nullptr, 0, dL_doutput, dL_stride,
-		              grad_mode);
+		              grad_mode, ex);
+	});
+}
+
+int ngp_density_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                        uint32_t output_stride, int use_inference_params, ngp_ctx** ctx) {
+	NGP_ARG(m && ctx && (n == 0 || input) && (!output || output_stride >= 16));
+	NGP_TRY({
+		NGP_CHECK(m->nerf, "density_forward is a NerfNetwork method");
+		m->require_params(use_inference_params);
+		f16* e = (f16*)m->enc.get((size_t)(n ? n : 1) * m->enc_width * sizeof(f16));
+		m->generation++;
+		if (n) {
+			m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, use_inference_params);
+			if (output)
+				m->run_mlp(S(stream), MLP_DENSITY, n, input, input_stride, e, (f16*)output, output_stride, AoS, nullptr, 0, nullptr,
+				           nullptr, use_inference_params);
+		}
+		*ctx = new ngp_ctx{n, input, input_stride, (bool)use_inference_params, m->generation, true};
+	});
+}
+
+int ngp_density_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* dL_doutput, uint32_t dL_stride, float* dL_dinput,
+                         uint32_t dL_dinput_stride, int grad_mode) {
+	NGP_ARG(m && ctx && (ctx->n == 0 || dL_doutput) && dL_stride >= 16 && dL_stride % 4 == 0 && grad_mode >= 0 &&
+	        grad_mode <= NGP_GRAD_IGNORE && (!dL_dinput || dL_dinput_stride >= 3));
+	NGP_TRY({
+		NGP_CHECK(m->nerf, "density_backward is a NerfNetwork method");
+		NGP_CHECK(ctx->generation == m->generation,
+		          "density_backward: the forward context is stale (another forward/inference ran on this model since)");
+		NGP_CHECK(ctx->density_only, "density_backward: this context is from forward (use backward)");
+		if (ctx->n == 0) return NGP_OK;
+		BwdExtra ex;
+		ex.dL_dinput = dL_dinput; ex.dinput_stride = dL_dinput_stride;
+		ex.density_only = true; ex.ddens = (const f16*)dL_doutput; ex.ddens_stride = dL_stride;
+		m->train_pass(S(stream), ctx->n, ctx->input, ctx->input_stride, (const f16*)m->enc.p, nullptr, 0, nullptr, 0, grad_mode, ex);
+	});
+}
+
+int ngp_input_gradient(ngp_model* m, void* stream, uint32_t dim, uint32_t n, const float* input, uint32_t input_stride,
+                       float* d_dinput, uint32_t d_dinput_stride, float backprop_scale) {
+	NGP_ARG(m && (n == 0 || (input && d_dinput)) && dim < 16 && backprop_scale != 0.f);
+	if (check_dinput(m, d_dinput, d_dinput_stride) != NGP_OK) return NGP_INVALID;
+	NGP_TRY({
+		if (n == 0) return NGP_OK;
+		m->require_params(false);
+		hipStream_t s = S(stream);
+		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
+		f16* dl = (f16*)m->dl1_ws.get((size_t)n * 16 * sizeof(f16));
+		m->generation++;
+		m->encode(s, n, input, input_stride, e, m->enc_width, AoS, false);
+		// one-hot dL/doutput: row `dim` = backprop_scale (fp16), every other row 0
+		fill_one_hot_f16(dl, n, 16, dim, backprop_scale, s);
+		BwdExtra ex;
+		ex.dL_dinput = d_dinput; ex.dinput_stride = d_dinput_stride; ex.dinput_scale = 1.f / backprop_scale;
+		m->train_pass(s, n, input, input_stride, e, nullptr, 0, dl, 16, NGP_GRAD_IGNORE, ex);
 	});
 }
 

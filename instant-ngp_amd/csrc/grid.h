@@ -66,6 +66,26 @@ bool grid_forward_xcd_ok(const GridDesc& g, const GridFwdArgs& a);
 bool grid_forward_rows_ok(const GridDesc& g, const GridFwdArgs& a);
 void grid_backward(const GridDesc& g, const GridBwdArgs& a, hipStream_t stream);
 
+// Input gradients (tcnn Encoding::backward's dL_dinput; NerfNetwork::backward_impl slices them into
+// the pos rows and the direction rows, nerf_network.h:282-299, 317-333). Per sample, fp32:
+//   dL/dx_d = sum_l scale_l * sum_c (dw_c/dx_d / scale_l) * sum_f dL/dy_{l,f} * T[c, f]
+// where w_c is the trilinear weight of corner c (levels the forward zeroes, l >= max_level L + 1e-3,
+// contribute nothing); and, when dL_dsh is given, the direction gradient through the degree-4 SH
+// encoding of d = 2 dir - 1:  dL/ddir_j = 2 * sum_k dL/dSH_k * dSH_k/dd_j.  Both are multiplied by
+// out_scale (tcnn input_gradient divides out its backprop scale).
+struct InputGradArgs {
+	uint32_t n;
+	const float* pos; uint32_t pos_stride;   // encoding input: element (i, d) at pos[i * pos_stride + d]
+	const f16* table;                        // [entries x F]
+	const f16* dL_dy; uint32_t dy_stride;    // dL/d(encoding) AoS: dL_dy[i * dy_stride + l*F + f]
+	float max_level; const float* max_level_per_sample;
+	const f16* dL_dsh;                       // optional: dL/d(SH encoding) [n x 16]
+	uint32_t dir_offset;                     // direction rows of the input (pos + dir_offset) and output
+	float* out; uint32_t out_stride;         // dL/dinput: rows 0..D-1 (and dir_offset..+2) of each sample's row
+	float out_scale;
+};
+void grid_input_gradient(const GridDesc& g, const InputGradArgs& a, hipStream_t stream);
+
 // ---- device-side building blocks (shared with fused kernels) ---------------------------------
 struct GridConst {
 	uint32_t n_levels, n_features;

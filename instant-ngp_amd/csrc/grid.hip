@@ -423,6 +423,130 @@ static void launch_bwd(uint32_t F, const GridConst& c, const GridBwdArgs& a, hip
 	}
 }
 
+// ---- input gradients ------------------------------------------------------------------------------
+// One thread per sample (the NeRF normals / SDF normals path: a render-time query, not the training hot
+// path). Corner order c = 0..2^D-1, feature order f = 0..F-1, fp32 without contraction (the oracle's
+// orc_grid_input_grad restates it in double).
+template <uint32_t D, uint32_t F>
+__global__ void __launch_bounds__(256) k_input_grad(const GridConst c, const InputGradArgs a) {
+	typedef typename FeatVec<F>::T V;
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= a.n) return;
+	const float* xp = a.pos + (size_t)i * a.pos_stride;
+	float x[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) x[d] = xp[d];
+	const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
+	const f16* gy = a.dL_dy + (size_t)i * a.dy_stride;
+	float acc[D];
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) acc[d] = 0.f;
+	for (uint32_t l = 0; l < c.n_levels; ++l) {
+		if ((float)l >= ml + 1e-3f) continue;  // zeroed in the forward: the output does not depend on x
+		float frac[D];
+		uint32_t base[D];
+		level_setup<D>(c, l, x, frac, base);
+		float g[F];
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) g[f] = (float)gy[l * F + f];
+		float la[D];
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) la[d] = 0.f;
+#pragma unroll
+		for (uint32_t k = 0; k < (1u << D); ++k) {
+			const V v = *(const V*)(a.table + (size_t)corner_index<D>(c, l, base, k) * F);
+			float gs = 0.f;
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) {
+				if constexpr (F == 1) gs = gs + g[0] * (float)v;
+				else gs = gs + g[f] * (float)v[f];
+			}
+#pragma unroll
+			for (uint32_t d = 0; d < D; ++d) {
+				float wo = 1.f;  // product of the other dimensions' weights, in dimension order
+#pragma unroll
+				for (uint32_t e = 0; e < D; ++e)
+					if (e != d) wo = wo * (((k >> e) & 1u) ? frac[e] : 1.f - frac[e]);
+				const float t = wo * gs;
+				la[d] = ((k >> d) & 1u) ? la[d] + t : la[d] - t;
+			}
+		}
+#pragma unroll
+		for (uint32_t d = 0; d < D; ++d) acc[d] = acc[d] + c.scale[l] * la[d];
+	}
+	float* o = a.out + (size_t)i * a.out_stride;
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) o[d] = acc[d] * a.out_scale;
+	if (a.dL_dsh) {
+		// d/dd of the 16 degree-4 real SH basis functions (the forward: mlp.hip sh4_frag), d = 2 dir - 1
+		const float* dp = a.pos + (size_t)i * a.pos_stride + a.dir_offset;
+		const float X = dp[0] * 2.f - 1.f, Y = dp[1] * 2.f - 1.f, Z = dp[2] * 2.f - 1.f;
+		float s[16];
+#pragma unroll
+		for (int k = 0; k < 16; ++k) s[k] = (float)a.dL_dsh[(size_t)i * 16 + k];
+		const float A = 0.48860251190291987f, B = 1.0925484305920792f, C = 0.94617469575755997f, E = 0.54627421529603959f,
+		            G = 0.59004358992664352f, H = 2.8906114426405538f, I = 0.45704579946446572f, J = 0.3731763325901154f,
+		            K = 1.4453057213202769f;
+		const float X2 = X * X, Y2 = Y * Y, Z2 = Z * Z;
+		float gx = 0.f, gy2 = 0.f, gz = 0.f;
+		// k: 1 -A y | 2 A z | 3 -A x | 4 B xy | 5 -B yz | 6 C z^2 - c | 7 -B xz | 8 E (x^2 - y^2)
+		//    9 G y (y^2 - 3x^2) | 10 H xyz | 11 I y (1 - 5z^2) | 12 J z (5z^2 - 3) | 13 I x (1 - 5z^2)
+		//    14 K z (x^2 - y^2) | 15 G x (3y^2 - x^2)
+		gx = gx + s[3] * (-A);
+		gx = gx + s[4] * (B * Y);
+		gx = gx + s[7] * (-B * Z);
+		gx = gx + s[8] * (2.f * E * X);
+		gx = gx + s[9] * (-6.f * G * X * Y);
+		gx = gx + s[10] * (H * Y * Z);
+		gx = gx + s[13] * (I * (1.f - 5.f * Z2));
+		gx = gx + s[14] * (2.f * K * X * Z);
+		gx = gx + s[15] * (3.f * G * (Y2 - X2));
+		gy2 = gy2 + s[1] * (-A);
+		gy2 = gy2 + s[4] * (B * X);
+		gy2 = gy2 + s[5] * (-B * Z);
+		gy2 = gy2 + s[8] * (-2.f * E * Y);
+		gy2 = gy2 + s[9] * (3.f * G * (Y2 - X2));
+		gy2 = gy2 + s[10] * (H * X * Z);
+		gy2 = gy2 + s[11] * (I * (1.f - 5.f * Z2));
+		gy2 = gy2 + s[14] * (-2.f * K * Y * Z);
+		gy2 = gy2 + s[15] * (6.f * G * X * Y);
+		gz = gz + s[2] * A;
+		gz = gz + s[5] * (-B * Y);
+		gz = gz + s[6] * (2.f * C * Z);
+		gz = gz + s[7] * (-B * X);
+		gz = gz + s[10] * (H * X * Y);
+		gz = gz + s[11] * (-10.f * I * Y * Z);
+		gz = gz + s[12] * (J * (15.f * Z2 - 3.f));
+		gz = gz + s[13] * (-10.f * I * X * Z);
+		gz = gz + s[14] * (K * (X2 - Y2));
+		float* od = o + a.dir_offset;
+		od[0] = 2.f * gx * a.out_scale;
+		od[1] = 2.f * gy2 * a.out_scale;
+		od[2] = 2.f * gz * a.out_scale;
+	}
+}
+
+template <uint32_t D>
+static void launch_input_grad(uint32_t F, const GridConst& c, const InputGradArgs& a, hipStream_t s) {
+	const dim3 grid(div_round_up(a.n, 256)), block(256);
+	switch (F) {
+		case 1: k_input_grad<D, 1><<<grid, block, 0, s>>>(c, a); break;
+		case 2: k_input_grad<D, 2><<<grid, block, 0, s>>>(c, a); break;
+		case 4: k_input_grad<D, 4><<<grid, block, 0, s>>>(c, a); break;
+		case 8: k_input_grad<D, 8><<<grid, block, 0, s>>>(c, a); break;
+		default: throw Error("GridEncoding: unsupported F");
+	}
+}
+
+void grid_input_gradient(const GridDesc& g, const InputGradArgs& a, hipStream_t stream) {
+	if (a.n == 0) return;
+	NGP_CHECK(!a.dL_dsh || g.n_dims == 3, "input gradient: the SH direction encoding needs a 3D grid");
+	GridConst c = make_grid_const(g);
+	if (g.n_dims == 3) launch_input_grad<3>(g.n_features, c, a, stream);
+	else launch_input_grad<2>(g.n_features, c, a, stream);
+	NGP_HIP(hipGetLastError());
+}
+
 void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist, int mode) {
 	if (a.n == 0) return;
 	GridConst c = make_grid_const(g);

@@ -56,6 +56,12 @@ struct NerfMlpArgs {
 	const f16* table;                             // grid parameters [entries x F]
 	float max_level;                              // tcnn set_max_level (global; per-sample masks not fused)
 	GridConst gc;
+	// input gradients (nerf_network.h:282-299): dL/d(SH encoding) = rows 16..31 of the rgb network's dL/dinput,
+	// fp16 [n x 16] (nullptr: skip)
+	f16* dL_dsh;
+	// MLP_DENSITY_TRAIN (NerfNetwork::density_backward, nerf_network.h:384-428): dL/d(density network output),
+	// fp16 AoS [n x ddens_stride] (16 rows; stride a multiple of 4)
+	const f16* dL_ddens; uint32_t ddens_stride;
 };
 
 struct MlpArgs {  // single MLP behind an encoding (tcnn::NetworkWithInputEncoding): image / SDF
@@ -88,7 +94,8 @@ MlpPlan make_mlp_plan(uint32_t enc_width, uint32_t width, uint32_t hidden, uint3
 
 void prepare_frags(const FragDesc* descs_dev, uint32_t n_frags, const f16* params, f16x8* frags, hipStream_t s);
 
-enum MlpMode : uint32_t { MLP_INFER = 0, MLP_TRAIN = 1, MLP_DENSITY = 2, MLP_INFER_ENC = 3, MLP_TRAIN_ENC = 4 };
+enum MlpMode : uint32_t { MLP_INFER = 0, MLP_TRAIN = 1, MLP_DENSITY = 2, MLP_INFER_ENC = 3, MLP_TRAIN_ENC = 4,
+                          MLP_DENSITY_TRAIN = 5 };  // density network forward + backward only (NeRF)
 // MLP_INFER_ENC / MLP_TRAIN_ENC are fused for 3D grids with 4 levels of 4 features (one 16-wide encoding step: C2)
 bool nerf_mlp_fused_encoding_ok(const GridDesc& g, uint32_t enc_width);
 
@@ -99,6 +106,8 @@ uint32_t mlp_train_blocks(uint32_t n);
 void mlp_run(const MlpPlan& p, MlpMode mode, const MlpArgs& a, hipStream_t s);
 
 // Sum [n_slabs x n] fp32 slabs into fp16 gradients: out = (accumulate ? out : 0) + sum.
-void reduce_slabs(const float* slabs, uint32_t n_slabs, uint32_t n, f16* grad, bool accumulate, hipStream_t s);
+// stride: elements between consecutive slabs (0: n); larger reduces only the leading n of each slab.
+void reduce_slabs(const float* slabs, uint32_t n_slabs, uint32_t n, f16* grad, bool accumulate, hipStream_t s,
+                  uint32_t stride = 0);
 
 }  // namespace ngp

@@ -331,6 +331,14 @@ __device__ __forceinline__ void store_out16(f16* out, uint32_t stride, uint32_t 
 	}
 }
 
+// dL/d(SH encoding) of one sample, fp16 [16]: the upper half (rows 16..31) of the rgb network's
+// dL/dinput tile, lane half h holding SH rows 4h..4h+3 (regs 0..3) and 8+4h..8+4h+3 (regs 4..7)
+__device__ __forceinline__ void store_dsh(f16* dsh_out, uint32_t sample, int h, const f16x8& v) {
+	f16* row = dsh_out + (size_t)sample * 16 + 4 * h;
+	*(f16x4*)(row + 0) = f16x4{v[0], v[1], v[2], v[3]};
+	*(f16x4*)(row + 8) = f16x4{v[4], v[5], v[6], v[7]};
+}
+
 // ------------------------------------------------------------------------------------------------
 // NerfNetwork MLP pair: density (enc -> 64 x DH -> 16) and rgb ([density out | SH] -> 64 x RH -> 16)
 // ------------------------------------------------------------------------------------------------
@@ -376,7 +384,8 @@ struct NerfLayout {
 template <int ES, int DH, int RH, int MODE>
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_nerf_mlp(const NerfMlpArgs a) {
 	using Lay = NerfLayout<ES, DH, RH>;
-	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_TRAIN_ENC;
+	constexpr bool DTRAIN = MODE == MLP_DENSITY_TRAIN;  // density network forward + backward only
+	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_TRAIN_ENC || DTRAIN;
 	constexpr bool DENSITY = MODE == MLP_DENSITY;
 	constexpr bool FUSE = MODE == MLP_INFER_ENC || MODE == MLP_TRAIN_ENC;
 	static_assert(!FUSE || ES == 1, "fused encoding: one 16-wide encoding step");
@@ -414,6 +423,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	f16x8 xe_n[ES];
 	float cd_n[3] = {0.f, 0.f, 0.f};
 	f16x4 dl_n{};
+	f16x8 dd_n{};  // DTRAIN: dL/d(density output) rows (j&3) + 8(j>>2) + 4h, the B-operand order of a packed tile
 	// FUSE (MLP_INFER_ENC, ES == 1, F == 4): lane half h encodes levels 2h and 2h+1 of its sample (the 8
 	// features of its B operand). The next tile's corner gathers are issued with the other prefetches
 	// and blended at the top of the next iteration, so the gather latency hides under this tile's MFMAs.
@@ -477,11 +487,17 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 #pragma unroll
 			for (int s = 0; s < ES; ++s) xe_n[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
 		}
-		if constexpr (!DENSITY) {
+		if constexpr (!DENSITY && !DTRAIN) {
 			const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
 			cd_n[0] = cd[0]; cd_n[1] = cd[1]; cd_n[2] = cd[2];
 		}
-		if constexpr (TRAIN) dl_n = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
+		if constexpr (DTRAIN) {
+			const f16* r = a.dL_ddens + (size_t)ls * a.ddens_stride + 4 * h;
+			const f16x4 lo = *(const f16x4*)r, hi = *(const f16x4*)(r + 8);
+			dd_n = f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+		} else if constexpr (TRAIN) {
+			dl_n = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
+		}
 	};
 	if (blockIdx.x * 4 + wave < n_tiles) {
 		if constexpr (FUSE) load_pos(blockIdx.x * 4 + wave);
@@ -516,6 +532,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		}
 		const float cdx = cd_n[0], cdy = cd_n[1], cdz = cd_n[2];
 		const f16x4 dl_cur = dl_n;
+		const f16x8 dd_cur = dd_n;
 		load_inputs(tile + gridDim.x * 4);  // unconditional (past-the-end tiles read sample 0): no phi copies
 
 		// ---- density forward -------------------------------------------------------------------
@@ -538,6 +555,53 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		pack_tile(dacc[0], dout[0], dout[1], false);  // dout[0] = rows 0..15 (density network output)
 		if constexpr (DENSITY) {
 			if (valid) store_out16(a.out, a.out_stride, a.out_layout, a.n, sample, h, dout[0]);
+			continue;
+		}
+		// density network backward from dL/d(density output) `dd` (the NeRF training pass after
+		// add_density_gradient, or density_backward's own dL/doutput): dW of the density layers, dL/d(encoding)
+		auto density_backward = [&](f16x8 (&dd)[1], f16* dz_img) {
+			f16x8 dz[4];
+			img_store_acc<1>(dz_img, Lay::S_64, dd, lane);
+			dw_accum<1, 4>(dw + Lay::W_DO, dz_img, Lay::S_64, img + Lay::I_HD + (DH - 1) * 32 * Lay::S_64, Lay::S_64, lane);
+			layer_fwd<2, 1>(acc, dd, lfrag + Lay::B_DO * 64, lane);
+			mask_pack<2>(acc, hd[DH - 1], dz);
+#pragma unroll
+			for (int l = DH - 1; l >= 1; --l) {
+				img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
+				dw_accum<4, 4>(dw + Lay::W_DH + 16 * (DH - 1 - l), dz_img, Lay::S_64, img + Lay::I_HD + (l - 1) * 32 * Lay::S_64,
+				               Lay::S_64, lane);
+				layer_fwd<2, 4>(acc, dz, lfrag + (Lay::B_DH + 8 * (DH - 1 - l)) * 64, lane);
+				mask_pack<2>(acc, hd[l - 1], dz);
+			}
+			img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
+			dw_accum<4, ES>(dw + Lay::W_D0, dz_img, Lay::S_64, img + Lay::I_XE, Lay::S_XE, lane);
+			if (a.dL_denc) {
+				// the MFMAs run with the full wave (every lane supplies A rows); only the stores are masked
+				f32x16 ae[Lay::ET];
+				layer_fwd<Lay::ET, 4>(ae, dz, lfrag + Lay::B_D0 * 64, lane);
+#pragma unroll
+				for (int t = 0; t < Lay::ET; ++t) {
+					f16x8 lo, hi;
+					pack_tile(ae[t], lo, hi, false);
+					if (!valid) continue;
+					// rows 32t + 8k + 4h + (0..3): lo holds k = 0,1; hi holds k = 2,3
+					f16* row = a.dL_denc + (size_t)sample * a.denc_stride + 32 * t + 4 * h;
+					*(f16x4*)(row + 0) = f16x4{lo[0], lo[1], lo[2], lo[3]};
+					*(f16x4*)(row + 8) = f16x4{lo[4], lo[5], lo[6], lo[7]};
+					if (32 * t + 16 < 16 * ES) {
+						*(f16x4*)(row + 16) = f16x4{hi[0], hi[1], hi[2], hi[3]};
+						*(f16x4*)(row + 24) = f16x4{hi[4], hi[5], hi[6], hi[7]};
+					}
+				}
+			}
+		};
+		if constexpr (DTRAIN) {
+			// NerfNetwork::density_forward / density_backward (nerf_network.h:355-428)
+			if (a.out && valid) store_out16(a.out, a.out_stride, a.out_layout, a.n, sample, h, dout[0]);
+#pragma unroll
+			for (int l = 0; l < DH; ++l) img_store_acc<4>(img + Lay::I_HD + l * 32 * Lay::S_64, Lay::S_64, hd[l], lane);
+			f16x8 dd[1] = {valid ? dd_cur : f16x8{}};
+			density_backward(dd, img + Lay::I_DZ);
 			continue;
 		}
 
@@ -600,45 +664,15 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 			dw_accum<4, 2>(dw + Lay::W_R0, dz_img, Lay::S_64, img + Lay::I_RIN, Lay::S_RIN, lane);
 			f32x16 a1[1];
 			layer_fwd<1, 4>(a1, dz, lfrag + Lay::B_R0 * 64, lane);
-			// dL/d(density output) = rows 0..15; add_density_gradient (nerf_network.h:63-74) in fp16
-			f16x8 dd[1], unused;
-			pack_tile(a1[0], dd[0], unused, false);
+			// dL/d(rgb input): rows 0..15 = dL/d(density output), rows 16..31 = dL/d(SH encoding);
+			// add_density_gradient (nerf_network.h:63-74) in fp16
+			f16x8 dd[1], dsh;
+			pack_tile(a1[0], dd[0], dsh, false);
 			if (h == 0) dd[0][0] = (f16)((float)dd[0][0] + dsig);
+			if (a.dL_dsh && valid) store_dsh(a.dL_dsh, sample, h, dsh);
 
 			// ---- density backward ------------------------------------------------------------
-			img_store_acc<1>(dz_img, Lay::S_64, dd, lane);
-			dw_accum<1, 4>(dw + Lay::W_DO, dz_img, Lay::S_64, img + Lay::I_HD + (DH - 1) * 32 * Lay::S_64, Lay::S_64, lane);
-			layer_fwd<2, 1>(acc, dd, lfrag + Lay::B_DO * 64, lane);
-			mask_pack<2>(acc, hd[DH - 1], dz);
-#pragma unroll
-			for (int l = DH - 1; l >= 1; --l) {
-				img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
-				dw_accum<4, 4>(dw + Lay::W_DH + 16 * (DH - 1 - l), dz_img, Lay::S_64, img + Lay::I_HD + (l - 1) * 32 * Lay::S_64,
-				               Lay::S_64, lane);
-				layer_fwd<2, 4>(acc, dz, lfrag + (Lay::B_DH + 8 * (DH - 1 - l)) * 64, lane);
-				mask_pack<2>(acc, hd[l - 1], dz);
-			}
-			img_store_acc<4>(dz_img, Lay::S_64, dz, lane);
-			dw_accum<4, ES>(dw + Lay::W_D0, dz_img, Lay::S_64, img + Lay::I_XE, Lay::S_XE, lane);
-			if (a.dL_denc) {
-				// the MFMAs run with the full wave (every lane supplies A rows); only the stores are masked
-				f32x16 ae[Lay::ET];
-				layer_fwd<Lay::ET, 4>(ae, dz, lfrag + Lay::B_D0 * 64, lane);
-#pragma unroll
-				for (int t = 0; t < Lay::ET; ++t) {
-					f16x8 lo, hi;
-					pack_tile(ae[t], lo, hi, false);
-					if (!valid) continue;
-					// rows 32t + 8k + 4h + (0..3): lo holds k = 0,1; hi holds k = 2,3
-					f16* row = a.dL_denc + (size_t)sample * a.denc_stride + 32 * t + 4 * h;
-					*(f16x4*)(row + 0) = f16x4{lo[0], lo[1], lo[2], lo[3]};
-					*(f16x4*)(row + 8) = f16x4{lo[4], lo[5], lo[6], lo[7]};
-					if (32 * t + 16 < 16 * ES) {
-						*(f16x4*)(row + 16) = f16x4{hi[0], hi[1], hi[2], hi[3]};
-						*(f16x4*)(row + 24) = f16x4{hi[4], hi[5], hi[6], hi[7]};
-					}
-				}
-			}
+			density_backward(dd, dz_img);
 		}
 	}
 
@@ -924,9 +958,10 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		img_store_acc<4>(img + T::I_ZR0, Lay::S_64, dz, lane);
 		f32x16 a1[1];
 		layer_fwd_reg<1, 4>(a1, dz, breg, Lay::B_R0 - Lay::N_FWD);
-		f16x8 dd[1], unused;
-		pack_tile(a1[0], dd[0], unused, false);
+		f16x8 dd[1], dsh;
+		pack_tile(a1[0], dd[0], dsh, false);  // dsh: rows 16..31 of dL/d(rgb input) = dL/d(SH encoding)
 		if (h == 0) dd[0][0] = (f16)((float)dd[0][0] + dsig);  // add_density_gradient (:63-74)
+		if (a.dL_dsh && valid) store_dsh(a.dL_dsh, sample, h, dsh);
 		img_store_acc<1>(img + T::I_ZDO, T::S_16, dd, lane);
 		layer_fwd_reg<2, 1>(acc, dd, breg, Lay::B_DO - Lay::N_FWD);
 		mask_pack<2>(acc, hd[DH - 1], dz);
@@ -992,7 +1027,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 template <int ES, int DH, int RH, int MODE>
 static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	using Lay = NerfLayout<ES, DH, RH>;
-	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_TRAIN_ENC;
+	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_TRAIN_ENC || MODE == MLP_DENSITY_TRAIN;
 	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (MODE == MLP_DENSITY ? Lay::F_R0 : Lay::N_FWD);
 	size_t lds = (size_t)NFRAG * 1024 + (TRAIN ? 4 * Lay::IMG_HALVES * sizeof(f16) : 0);
 	uint32_t n_reg = 4;
@@ -1002,7 +1037,7 @@ static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	const uint32_t tiles = (a.n + 31) / 32;
 	uint32_t blocks = TRAIN ? nerf_mlp_train_blocks(a.n) : std::min<uint32_t>(div_round_up(tiles, 4), 8 * device_cu_count());
 	if (blocks == 0) return;
-	if constexpr (TRAIN && NerfTrainLayout<ES, DH, RH>::LDS_BYTES <= 160 * 1024 && Lay::N_ALL <= 44) {
+	if constexpr (TRAIN && MODE != MLP_DENSITY_TRAIN && NerfTrainLayout<ES, DH, RH>::LDS_BYTES <= 160 * 1024 && Lay::N_ALL <= 44) {
 		// weight gradients split across the waves, all fragments in registers (k_nerf_mlp_train)
 		auto kt = k_nerf_mlp_train<ES, DH, RH, MODE == MLP_TRAIN_ENC>;
 		const size_t lt = NerfTrainLayout<ES, DH, RH>::LDS_BYTES;
@@ -1056,6 +1091,7 @@ void nerf_mlp_run(const NerfMlpPlan& p, MlpMode mode, const NerfMlpArgs& a, hipS
 		case MLP_DENSITY: dispatch_nerf<MLP_DENSITY>(p, a, s); break;
 		case MLP_INFER_ENC: dispatch_nerf_fused<MLP_INFER_ENC>(p, a, s); break;
 		case MLP_TRAIN_ENC: dispatch_nerf_fused<MLP_TRAIN_ENC>(p, a, s); break;
+		case MLP_DENSITY_TRAIN: dispatch_nerf<MLP_DENSITY_TRAIN>(p, a, s); break;
 	}
 }
 
@@ -1254,9 +1290,9 @@ void mlp_run(const MlpPlan& p, MlpMode mode, const MlpArgs& a, hipStream_t s) {
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(SLAB_THREADS) k_reduce_slabs(const SlabJob j) { reduce_slabs_block(j, blockIdx.x); }
 
-void reduce_slabs(const float* slabs, uint32_t n_slabs, uint32_t n, f16* grad, bool accumulate, hipStream_t s) {
+void reduce_slabs(const float* slabs, uint32_t n_slabs, uint32_t n, f16* grad, bool accumulate, hipStream_t s, uint32_t stride) {
 	SlabJob j;
-	j.slabs = slabs; j.n_slabs = n_slabs; j.n = n; j.grad = grad; j.accumulate = accumulate;
+	j.slabs = slabs; j.n_slabs = n_slabs; j.n = n; j.grad = grad; j.accumulate = accumulate; j.stride = stride;
 	k_reduce_slabs<<<slab_blocks(n), SLAB_THREADS, 0, s>>>(j);
 	NGP_HIP(hipGetLastError());
 }

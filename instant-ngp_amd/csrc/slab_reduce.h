@@ -12,6 +12,7 @@ struct SlabJob {
 	uint32_t n_slabs = 0, n = 0;
 	f16* grad = nullptr;
 	bool accumulate = false;
+	uint32_t stride = 0;  // elements between consecutive slabs (0: n); > n reduces a leading range only
 };
 constexpr uint32_t SLAB_THREADS = 256;
 __host__ __device__ constexpr uint32_t slab_blocks(uint32_t n) { return (n + 31) / 32; }
@@ -21,6 +22,7 @@ __host__ __device__ constexpr uint32_t slab_blocks(uint32_t n) { return (n + 31)
 __device__ __forceinline__ void reduce_slabs_block(const SlabJob& j, uint32_t blk) {
 	__shared__ float part[8][33];
 	const uint32_t p = blk * 32 + (threadIdx.x & 31), g = threadIdx.x >> 5;
+	const size_t st = j.stride ? j.stride : j.n;
 	float s = 0.f;
 	if (p < j.n) {
 		// 8 independent loads in flight per step (the adds stay in slab order: deterministic)
@@ -28,11 +30,11 @@ __device__ __forceinline__ void reduce_slabs_block(const SlabJob& j, uint32_t bl
 		for (; b + 56 < j.n_slabs; b += 64) {
 			float v[8];
 #pragma unroll
-			for (int k = 0; k < 8; ++k) v[k] = j.slabs[(size_t)(b + 8 * k) * j.n + p];
+			for (int k = 0; k < 8; ++k) v[k] = j.slabs[(size_t)(b + 8 * k) * st + p];
 #pragma unroll
 			for (int k = 0; k < 8; ++k) s += v[k];
 		}
-		for (; b < j.n_slabs; b += 8) s += j.slabs[(size_t)b * j.n + p];
+		for (; b < j.n_slabs; b += 8) s += j.slabs[(size_t)b * st + p];
 	}
 	part[g][threadIdx.x & 31] = s;
 	__syncthreads();

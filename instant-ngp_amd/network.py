@@ -14,7 +14,7 @@ from ._capi import ParamLayout, check, lib
 
 LAYOUT_AOS, LAYOUT_SOA = 0, 1
 LAYOUT_AOS_RGBD = 2  # engine extension: NerfNetwork rows 0..3 only (raw rgb, raw density), [n x 4]
-GRAD_OVERWRITE, GRAD_ACCUMULATE = 0, 1
+GRAD_OVERWRITE, GRAD_ACCUMULATE, GRAD_IGNORE = 0, 1, 2  # tcnn::EGradientMode
 
 
 def _js(cfg):
@@ -127,11 +127,12 @@ class Model:
         check(lib().ngp_model_reserve(self.handle, n))
 
     def workspace(self, name, n):
-        """The last training pass's fp16 intermediates as a [n x encoding_width] view: "encoding" (grid
-        output) or "dL_dencoding" (grid backward input) — tcnn's forward_activations(ctx) role."""
+        """The last training pass's fp16 intermediates as a [n x width] view: "encoding" (grid output) or
+        "dL_dencoding" (grid backward input), width encoding_width — tcnn's forward_activations(ctx) role —
+        or "dL_dsh" (dL/d(SH encoding) of the last backward with input gradients), width 16."""
         p, nb = C.c_void_p(), C.c_uint64()
         check(lib().ngp_model_workspace(self.handle, name.encode(), C.byref(p), C.byref(nb)))
-        w = self.layout().encoding_width
+        w = 16 if name == "dL_dsh" else self.layout().encoding_width
         if n * w * 2 > nb.value:
             raise ValueError(f"workspace {name} holds {nb.value} bytes, fewer than {n} rows")
         return wrap_device(p.value, n * w, torch.float16).view(n, w)
@@ -155,9 +156,24 @@ class Model:
                                 output.stride(0) if output is not None else 0, int(use_inference_params), C.byref(h)))
         return Context(self, h, x.shape[0]), output
 
-    def backward(self, ctx, dL_doutput, grad_mode=GRAD_OVERWRITE, stream=None):
+    def backward(self, ctx, dL_doutput, dL_dinput=None, grad_mode=GRAD_OVERWRITE, stream=None):
+        """backward_impl (nerf_network.h:256-335). dL_dinput: optional fp32 [n x >= input_width] tensor that
+        receives dL/dposition (and dL/ddirection for a NerfNetwork); other columns are not written."""
         assert dL_doutput.dtype == torch.float16 and dL_doutput.shape[1] >= 16
-        check(lib().ngp_backward(self.handle, _stream(stream), ctx.handle, _ptr(dL_doutput), dL_doutput.stride(0), grad_mode))
+        if dL_dinput is not None:
+            assert dL_dinput.dtype == torch.float32 and dL_dinput.shape[0] == ctx.n
+        check(lib().ngp_backward(self.handle, _stream(stream), ctx.handle, _ptr(dL_doutput), dL_doutput.stride(0),
+                                 _ptr(dL_dinput), dL_dinput.stride(0) if dL_dinput is not None else 0, grad_mode))
+
+    def input_gradient(self, dim, x, d_dinput=None, backprop_scale=128.0, stream=None):
+        """tcnn Network::input_gradient (the reference's normals: testbed_nerf.cu:2616, testbed.cu:4621):
+        d output[dim] / d input, fp32 [n x input width] (only the position / direction columns written)."""
+        _check_input(x, self.input_width())
+        if d_dinput is None:
+            d_dinput = torch.zeros((x.shape[0], x.shape[1]), dtype=torch.float32, device=x.device)
+        check(lib().ngp_input_gradient(self.handle, _stream(stream), dim, x.shape[0], _ptr(x), x.stride(0), _ptr(d_dinput),
+                                       d_dinput.stride(0), float(backprop_scale)))
+        return d_dinput
 
     def forward_backward(self, x, dL_doutput, output=None, grad_mode=GRAD_OVERWRITE, stream=None):
         _check_input(x, self.input_width())
@@ -175,9 +191,10 @@ class Model:
                                          layout, int(use_inference_params)))
         return out
 
-    def encoding_backward(self, x, dL_dy, layout=LAYOUT_AOS, grad_mode=GRAD_OVERWRITE, stream=None):
+    def encoding_backward(self, x, dL_dy, layout=LAYOUT_AOS, grad_mode=GRAD_OVERWRITE, dL_dinput=None, stream=None):
         check(lib().ngp_encoding_backward(self.handle, _stream(stream), x.shape[0], _ptr(x), x.stride(0), _ptr(dL_dy),
-                                          dL_dy.stride(0), layout, grad_mode))
+                                          dL_dy.stride(0), layout, _ptr(dL_dinput),
+                                          dL_dinput.stride(0) if dL_dinput is not None else 0, grad_mode))
 
 
 class NerfNetwork(Model):
@@ -199,6 +216,19 @@ class NerfNetwork(Model):
         check(lib().ngp_density(self.handle, _stream(stream), n, _ptr(x), x.stride(0), _ptr(output), output.stride(0), layout,
                                 int(use_inference_params)))
         return output
+
+    def density_forward(self, x, output=None, use_inference_params=False, stream=None):
+        """NerfNetwork::density_forward (nerf_network.h:355-382): (context, density network output [n x 16])."""
+        h = C.c_void_p()
+        check(lib().ngp_density_forward(self.handle, _stream(stream), x.shape[0], _ptr(x), x.stride(0), _ptr(output),
+                                        output.stride(0) if output is not None else 0, int(use_inference_params), C.byref(h)))
+        return Context(self, h, x.shape[0]), output
+
+    def density_backward(self, ctx, dL_doutput, dL_dinput=None, grad_mode=GRAD_OVERWRITE, stream=None):
+        """NerfNetwork::density_backward (nerf_network.h:384-428): dL_doutput = dL/d(density output) fp16 [n x 16]."""
+        assert dL_doutput.dtype == torch.float16 and dL_doutput.shape[1] >= 16
+        check(lib().ngp_density_backward(self.handle, _stream(stream), ctx.handle, _ptr(dL_doutput), dL_doutput.stride(0),
+                                         _ptr(dL_dinput), dL_dinput.stride(0) if dL_dinput is not None else 0, grad_mode))
 
 
 class NetworkWithInputEncoding(Model):

@@ -307,6 +307,14 @@ EXPORT void orc_nerf_generate_samples(const ocfg* c, const oimg* ims, const uint
 	uint32_t total = 0, kept = 0;
 	float diag[3];
 	for (int k = 0; k < 3; ++k) diag[k] = c->aabb_max[k] - c->aabb_min[k];
+	/* The reference marches each ray twice (count, then write) and takes its base from an atomic
+	 * counter; here the slots follow ray order (a prefix over the counts). Pass 1 counts
+	 * every ray's occupied steps (rays are independent: parallel), the prefix runs in ray order, pass 2
+	 * re-marches the kept rays and writes their samples. */
+	uint32_t* cnt = (uint32_t*)calloc(n_rays ? n_rays : 1, sizeof(uint32_t));
+	uint32_t* slot = (uint32_t*)malloc(sizeof(uint32_t) * (n_rays ? n_rays : 1));
+	uint32_t* basev = (uint32_t*)malloc(sizeof(uint32_t) * (n_rays ? n_rays : 1));
+	#pragma omp parallel for schedule(dynamic, 64)
 	for (uint32_t i = 0; i < n_rays; ++i) {
 		uint32_t ig = i + ray_offset;
 		oray r = setup(c, ims, cams, px, n_img, ig, n_div ? n_div : n_rays, rng);
@@ -321,17 +329,30 @@ EXPORT void orc_nerf_generate_samples(const ocfg* c, const oimg* ims, const uint
 			if (occupied(pos, bf, mip)) { ++j; t += dt; }
 			else t = advance_voxel(t, r.cone, pos, r.dn, r.idir, mip);
 		}
+		cnt[i] = j;
+	}
+	for (uint32_t i = 0; i < n_rays; ++i) {
+		slot[i] = 0xffffffffu;
+		const uint32_t j = cnt[i];
 		if (j == 0) continue;
 		uint32_t base = total;
 		total += j;
 		if (base + j > max_samples) continue;
-		uint32_t s = kept++;
+		slot[i] = kept++;
+		basev[i] = base;
+	}
+	#pragma omp parallel for schedule(dynamic, 64)
+	for (uint32_t i = 0; i < n_rays; ++i) {
+		if (slot[i] == 0xffffffffu) continue;
+		uint32_t ig = i + ray_offset;
+		oray r = setup(c, ims, cams, px, n_img, ig, n_div ? n_div : n_rays, rng);
+		const uint32_t s = slot[i], j = cnt[i], base = basev[i];
 		ray_indices[s] = ig;
 		for (int k = 0; k < 3; ++k) { rays[6 * s + k] = r.o[k]; rays[6 * s + 3 + k] = r.d[k]; }
 		numsteps[2 * s] = j;
 		numsteps[2 * s + 1] = base;
 		uint32_t jj = 0;
-		t = r.startt;
+		float t = r.startt, pos[3];
 		for (;;) {
 			for (int k = 0; k < 3; ++k) pos[k] = r.o[k] + t * r.dn[k];
 			if (!(contains(c, pos) && jj < j)) break;
@@ -350,6 +371,7 @@ EXPORT void orc_nerf_generate_samples(const ocfg* c, const oimg* ims, const uint
 			}
 		}
 	}
+	free(cnt); free(slot); free(basev);
 	counters[0] = kept;
 	counters[1] = total;
 	free(cams);

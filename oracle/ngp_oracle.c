@@ -349,6 +349,76 @@ EXPORT void orc_sh4(float dx, float dy, float dz, float* o) {
 }
 
 /* ------------------------------------------------------------------------------------------------
+ * Input gradients (tcnn Encoding::backward's dL_dinput, as NerfNetwork::backward_impl slices them:
+ * include/neural-graphics-primitives/nerf_network.h:282-299 direction, :317-333 position), restated
+ * analytically in double:
+ *   grid: dL/dx_d = sum_l scale_l * sum_c sign_d(c) * prod_{e != d} w_e(c) * sum_f dL/dy_{l,f} T[c, f]
+ *         (w_e(c) = frac_e or 1 - frac_e; levels zeroed by set_max_level contribute nothing);
+ *   SH:   dL/ddir_j = 2 * sum_k dL/dSH_k * dSH_k/dd_j, d = 2 dir - 1 (the degree-4 basis of orc_sh4).
+ * ---------------------------------------------------------------------------------------------- */
+EXPORT void orc_grid_input_grad(const orc_grid* g, size_t n, const float* pos, uint32_t pos_stride, const uint16_t* table,
+                                const float* dL_dy, uint32_t dy_stride, float max_level, double* out) {
+	const uint32_t L = g->n_levels, F = g->n_features, D = g->n_dims;
+	#pragma omp parallel for schedule(static)
+	for (size_t i = 0; i < n; ++i) {
+		const float* x = pos + i * pos_stride;
+		const float ml = max_level * (float)L;
+		double acc[4] = {0, 0, 0, 0};
+		for (uint32_t l = 0; l < L; ++l) {
+			if ((float)l >= ml + 1e-3f) continue;
+			float frac[4]; uint32_t base[4], p[4];
+			grid_corner_setup(g, l, x, frac, base);
+			for (uint32_t c = 0; c < (1u << D); ++c) {
+				corner_weight(g, c, frac, base, p);
+				size_t e = (size_t)g->offsets[l] + grid_index(g, l, p);
+				double gs = 0.0;
+				for (uint32_t f = 0; f < F; ++f) gs += (double)dL_dy[i * dy_stride + l * F + f] * (double)hf(table[e * F + f]);
+				for (uint32_t d = 0; d < D; ++d) {
+					double wo = 1.0;
+					for (uint32_t k = 0; k < D; ++k)
+						if (k != d) wo *= (c >> k) & 1u ? (double)frac[k] : 1.0 - (double)frac[k];
+					acc[d] += (double)g->scale[l] * ((c >> d) & 1u ? wo : -wo) * gs;
+				}
+			}
+		}
+		for (uint32_t d = 0; d < D; ++d) out[i * D + d] = acc[d];
+	}
+}
+
+/* gradient of each SH basis function wrt d = (x, y, z), basis order of orc_sh4 */
+static void sh4_basis_grad(double x, double y, double z, double gr[16][3]) {
+	const double A = 0.48860251190291987, B = 1.0925484305920792, C = 0.94617469575755997, E = 0.54627421529603959,
+	             G = 0.59004358992664352, H = 2.8906114426405538, I = 0.45704579946446572, J = 0.3731763325901154,
+	             K = 1.4453057213202769;
+	memset(gr, 0, sizeof(double) * 48);
+	gr[1][1] = -A;
+	gr[2][2] = A;
+	gr[3][0] = -A;
+	gr[4][0] = B * y; gr[4][1] = B * x;
+	gr[5][1] = -B * z; gr[5][2] = -B * y;
+	gr[6][2] = 2 * C * z;
+	gr[7][0] = -B * z; gr[7][2] = -B * x;
+	gr[8][0] = 2 * E * x; gr[8][1] = -2 * E * y;
+	gr[9][0] = G * y * (-6 * x); gr[9][1] = G * (-3 * x * x + 3 * y * y);
+	gr[10][0] = H * y * z; gr[10][1] = H * x * z; gr[10][2] = H * x * y;
+	gr[11][1] = I * (1 - 5 * z * z); gr[11][2] = I * y * (-10 * z);
+	gr[12][2] = J * (15 * z * z - 3);
+	gr[13][0] = I * (1 - 5 * z * z); gr[13][2] = I * x * (-10 * z);
+	gr[14][0] = K * z * 2 * x; gr[14][1] = -K * z * 2 * y; gr[14][2] = K * (x * x - y * y);
+	gr[15][0] = G * (-3 * x * x + 3 * y * y); gr[15][1] = G * x * 6 * y;
+}
+
+EXPORT void orc_sh4_input_grad(const float* dir, const float* dL_dsh, double* out) {
+	double gr[16][3];
+	sh4_basis_grad(2.0 * dir[0] - 1.0, 2.0 * dir[1] - 1.0, 2.0 * dir[2] - 1.0, gr);
+	for (int j = 0; j < 3; ++j) {
+		double s = 0.0;
+		for (int k = 0; k < 16; ++k) s += (double)dL_dsh[k] * gr[k][j];
+		out[j] = 2.0 * s;
+	}
+}
+
+/* ------------------------------------------------------------------------------------------------
  * Fully-fused MLP (tcnn FullyFusedMLP<half, W>, restated).
  * Layers: in_pad -> W (ReLU) -> [W -> W (ReLU)] x (n_hidden-1) -> out_pad (no activation).
  * Weights fp16 row-major [out x in] per layer, consecutive. Every layer: fp16 operands, fp32 sum,
@@ -570,6 +640,70 @@ EXPORT void orc_nerf_backward(const orc_nerf* m, const uint16_t* params, size_t 
 		float gy[256];
 		for (uint32_t k = 0; k < LF; ++k) gy[k] = denc[k];
 		orc_grid_backward(g, 1, x, m->in_stride, gy, 1.0f, NULL, grads + nd + nr);
+	}
+}
+
+/* NerfNetwork backward with input gradients (nerf_network.h:256-335 with dL_dinput): per sample the
+ * fp16-rounded dL/d(SH) (rows 16..31 of the rgb network's dL/dinput) and dL/d(encoding) as the engine
+ * rounds them, then the analytic position and direction gradients (orc_grid_input_grad,
+ * orc_sh4_input_grad) of those. dinput: float [n x in_stride], rows 0..2 and dir_offset..+2 written,
+ * scaled by `scale`. dsh / denc (optional): [n x 16] / [n x density.in_pad]. */
+EXPORT void orc_nerf_input_grad(const orc_nerf* m, const uint16_t* params, size_t n, const float* in, const float* dL_dout,
+                                float scale, float* dinput, float* dsh_out, float* denc_out) {
+	const orc_grid* g = &m->grid;
+	size_t nd = orc_mlp_n_params(&m->density), nr = orc_mlp_n_params(&m->rgb);
+	const uint16_t* wd = params;
+	const uint16_t* wr = params + nd;
+	const uint16_t* table = wr + nr;
+	#pragma omp parallel
+	{
+		float enc[256], dacts[1024], racts[1024], rin[32], out16[16], drgb[16], drin[32], denc[256], dd[16];
+		double* dW = (double*)calloc(nd + nr, sizeof(double));
+		#pragma omp for schedule(static)
+		for (size_t i = 0; i < n; ++i) {
+			const float* x = in + i * m->in_stride;
+			nerf_forward_one(m, params, x, enc, dacts, racts, rin, out16);
+			for (uint32_t k = 0; k < 16; ++k) drgb[k] = k < 3 ? dL_dout[i * 16 + k] : 0.f;
+			mlp_backward_one(&m->rgb, wr, rin, racts, drgb, dW + nd, drin);
+			for (uint32_t k = 0; k < 16; ++k) dd[k] = drin[k];
+			dd[0] = rh(dd[0] + dL_dout[i * 16 + 3]);
+			mlp_backward_one(&m->density, wd, enc, dacts, dd, dW, denc);
+			double gp[4], gd[3];
+			orc_grid_input_grad(g, 1, x, m->in_stride, table, denc, m->density.in_pad, 1.0f, gp);
+			orc_sh4_input_grad(x + m->dir_offset, drin + 16, gd);
+			float* o = dinput + i * m->in_stride;
+			for (int d = 0; d < 3; ++d) o[d] = (float)(gp[d] * scale);
+			for (int d = 0; d < 3; ++d) o[m->dir_offset + d] = (float)(gd[d] * scale);
+			if (dsh_out) memcpy(dsh_out + i * 16, drin + 16, 16 * sizeof(float));
+			if (denc_out) memcpy(denc_out + i * m->density.in_pad, denc, m->density.in_pad * sizeof(float));
+		}
+		free(dW);
+	}
+}
+
+/* NerfNetwork::density_backward (nerf_network.h:384-428): dL_ddens float [n x 16] = dL/d(density network
+ * output). grads (double [n_params], accumulated; caller zeroes): density MLP and grid sections only.
+ * dinput (optional, float [n x in_stride]): rows 0..2. */
+EXPORT void orc_nerf_density_backward(const orc_nerf* m, const uint16_t* params, size_t n, const float* in,
+                                      const float* dL_ddens, double* grads, float* dinput) {
+	const orc_grid* g = &m->grid;
+	uint32_t LF = g->n_levels * g->n_features;
+	size_t nd = orc_mlp_n_params(&m->density), nr = orc_mlp_n_params(&m->rgb);
+	const uint16_t* table = params + nd + nr;
+	float enc[256], dacts[1024], denc[256], gy[256];
+	for (size_t i = 0; i < n; ++i) {
+		const float* x = in + i * m->in_stride;
+		orc_grid_forward(g, 1, x, m->in_stride, table, 1.0f, NULL, enc);
+		for (uint32_t k = 0; k < m->density.in_pad; ++k) enc[k] = k < LF ? rh(enc[k]) : 0.f;
+		mlp_forward_one(&m->density, params, enc, dacts);
+		mlp_backward_one(&m->density, params, enc, dacts, dL_ddens + i * 16, grads, denc);
+		for (uint32_t k = 0; k < LF; ++k) gy[k] = denc[k];
+		orc_grid_backward(g, 1, x, m->in_stride, gy, 1.0f, NULL, grads + nd + nr);
+		if (dinput) {
+			double gp[4];
+			orc_grid_input_grad(g, 1, x, m->in_stride, table, denc, m->density.in_pad, 1.0f, gp);
+			for (int d = 0; d < 3; ++d) dinput[i * m->in_stride + d] = (float)gp[d];
+		}
 	}
 }
 

@@ -80,6 +80,10 @@ def _declare(L):
     d("orc_grid_indices", None, P, sz, P, u32, P)
     d("orc_grid_backward_exact", None, P, sz, P, u32, P, u32, f32, P, C.c_int, P, P)
     d("orc_sh4", None, f32, f32, f32, P)
+    d("orc_grid_input_grad", None, P, sz, P, u32, P, P, u32, f32, P)
+    d("orc_sh4_input_grad", None, P, P, P)
+    d("orc_nerf_input_grad", None, P, P, sz, P, P, f32, P, P, P)
+    d("orc_nerf_density_backward", None, P, P, sz, P, P, P, P)
     d("orc_mlp_n_params", u32, P)
     d("orc_mlp_forward", None, P, P, sz, P, P)
     d("orc_mlp_backward", None, P, P, sz, P, P, P, P)
@@ -225,6 +229,48 @@ def sh4(d):
     out = np.zeros(16, dtype=np.float32)
     lib().orc_sh4(float(d[0]), float(d[1]), float(d[2]), ptr(out))
     return out
+
+
+def grid_input_grad(g, pos, table16, dL_dy, max_level=1.0, stride=None):
+    """Analytic dL/dposition through the grid (orc_grid_input_grad), float64 [n x D]. dL_dy float [n x W]
+    (W >= L*F, only the first L*F columns read)."""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    dy = np.ascontiguousarray(dL_dy, dtype=np.float32)
+    out = np.zeros((pos.shape[0], g.n_dims), np.float64)
+    lib().orc_grid_input_grad(C.byref(g), pos.shape[0], ptr(pos), stride or pos.shape[1], ptr(np.ascontiguousarray(table16)),
+                              ptr(dy), dy.shape[1], max_level, ptr(out))
+    return out
+
+
+def sh4_input_grad(d, dL_dsh):
+    out = np.zeros(3, np.float64)
+    lib().orc_sh4_input_grad(ptr(np.ascontiguousarray(d, np.float32)), ptr(np.ascontiguousarray(dL_dsh, np.float32)), ptr(out))
+    return out
+
+
+def nerf_input_grad(m, params16, coords, dL_dout, scale=1.0):
+    """NerfNetwork backward with dL_dinput (orc_nerf_input_grad): dict of dinput [n x in_stride] (position and
+    direction rows), dsh [n x 16] and denc [n x encoding width] (the fp16-rounded intermediates)."""
+    coords = np.ascontiguousarray(coords, dtype=np.float32)
+    n = coords.shape[0]
+    r = {"dinput": np.zeros((n, m.in_stride), np.float32), "dsh": np.zeros((n, 16), np.float32),
+         "denc": np.zeros((n, m.density.in_pad), np.float32)}
+    lib().orc_nerf_input_grad(C.byref(m), ptr(np.ascontiguousarray(params16)), n, ptr(coords),
+                              ptr(np.ascontiguousarray(dL_dout, np.float32)), float(scale), ptr(r["dinput"]), ptr(r["dsh"]),
+                              ptr(r["denc"]))
+    return r
+
+
+def nerf_density_backward(m, params16, coords, dL_ddens):
+    """NerfNetwork::density_backward (orc_nerf_density_backward): (grads float64 [n_params] with the density MLP
+    and grid sections, dinput float32 [n x in_stride] position rows)."""
+    coords = np.ascontiguousarray(coords, dtype=np.float32)
+    n = coords.shape[0]
+    grads = np.zeros(nerf_n_params(m), np.float64)
+    dinput = np.zeros((n, m.in_stride), np.float32)
+    lib().orc_nerf_density_backward(C.byref(m), ptr(np.ascontiguousarray(params16)), n, ptr(coords),
+                                    ptr(np.ascontiguousarray(dL_ddens, np.float32)), ptr(grads), ptr(dinput))
+    return grads, dinput
 
 
 def make_mlp(in_pad, width, n_hidden, out_pad):

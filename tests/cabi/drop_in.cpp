@@ -8,7 +8,11 @@
 //          NerfCoordinate), dL.bin (f16 [n x 16])
 //   writes <dir>/params.bin (f16 [n_params], after initialisation), infer.bin (f16 [n x 16] CM),
 //          density.bin (f16 [16 x n] RM), fwd.bin (f16 [n x 16]), grads.bin (f16 [n_params]),
-//          params_after.bin (f16 [n_params] after optimizer_step(128)), meta.json
+//          params_after.bin (f16 [n_params] after optimizer_step(128)), meta.json; then, on the restored
+//          parameters: normals.bin (f32 [n x 7]: input_gradient(dim 3) written over a copy of the
+//          coordinates, as testbed_nerf.cu:2616 does), dinput.bin (f32 [n x 7]: backward's dL_dinput),
+//          dens_out.bin (f16 [n x 16]: density_forward), grads2.bin (f16 [n_params] after backward +
+//          density_backward with dL.bin as dL/d(density output)), dens_dinput.bin (f32 [n x 7])
 // The Testbed's sequence per step (testbed_nerf.cu:3514, 4001, 4077-4078, 3678): density for the
 // occupancy grid, inference over the samples, forward + backward on the batch, optimizer_step.
 #include <cstdio>
@@ -94,6 +98,42 @@ int main(int argc, char** argv) {
 		trainer.deserialize(snap);  // Trainer::deserialize restores the pre-step state
 		const uint32_t step_restored = trainer.step();
 
+		// normals (testbed_nerf.cu:2616): network.input_gradient(stream, 3, positions_matrix, positions_matrix)
+		DevBuf d_pos(coords.size());
+		d_pos.upload(coords.data());
+		net.input_gradient(stream, 3, MatrixView<const float>{(const float*)d_pos.p, 7, n, 7, Layout::CM},
+		                   MatrixView<float>{(float*)d_pos.p, 7, n, 7, Layout::CM});
+		// backward with input gradients (nerf_network.h:262), then density_forward / density_backward (:355-428)
+		const std::vector<float> zeros((size_t)n * 7, 0.f);
+		DevBuf d_din(zeros.size() * 4), d_ddin(zeros.size() * 4), d_dout((size_t)n * 16 * 2);
+		d_din.upload(zeros.data());
+		d_ddin.upload(zeros.data());
+		auto ctx2 = net.forward(stream, in, &fwd, false);
+		MatrixView<float> din{(float*)d_din.p, 7, n, 7, Layout::CM}, ddin{(float*)d_ddin.p, 7, n, 7, Layout::CM};
+		net.backward(stream, *ctx2, MatrixView<const uint16_t>{(const uint16_t*)d_dl.p, 16, n, 16, Layout::CM}, &din);
+		MatrixView<uint16_t> dout{(uint16_t*)d_dout.p, 16, n, 16, Layout::CM};
+		auto dctx = net.density_forward(stream, in, &dout, false);
+		net.density_backward(stream, *dctx, MatrixView<const uint16_t>{(const uint16_t*)d_dl.p, 16, n, 16, Layout::CM}, &ddin);
+		check(ngp_stream_synchronize(stream), "sync");
+		std::vector<float> f32v(zeros.size());
+		d_pos.download(f32v.data(), f32v.size() * 4);
+		dump(dir + "/normals.bin", f32v.data(), f32v.size() * 4);
+		d_din.download(f32v.data(), f32v.size() * 4);
+		dump(dir + "/dinput.bin", f32v.data(), f32v.size() * 4);
+		d_ddin.download(f32v.data(), f32v.size() * 4);
+		dump(dir + "/dens_dinput.bin", f32v.data(), f32v.size() * 4);
+		d_dout.download(o.data(), (size_t)n * 16 * 2);
+		dump(dir + "/dens_out.bin", o.data(), (size_t)n * 16 * 2);
+		check(ngp_memcpy(h16.data(), trainer.gradients(), np * 2, 2), "gradients");
+		dump(dir + "/grads2.bin", h16.data(), np * 2);
+		std::string ctx_err;  // a forward() context handed to density_backward is refused
+		try {
+			auto ctx3 = net.forward(stream, in, &fwd, false);
+			net.density_backward(stream, *ctx3, MatrixView<const uint16_t>{(const uint16_t*)d_dl.p, 16, n, 16, Layout::CM});
+		} catch (const std::runtime_error& e) {
+			ctx_err = e.what();
+		}
+
 		// the reference's error behaviour: a non-CM input throws (nerf_network.h:338-340)
 		std::string err;
 		try {
@@ -107,7 +147,7 @@ int main(int argc, char** argv) {
 		     << ", \"input_width\": " << net.input_width() << ", \"output_width\": " << net.output_width()
 		     << ", \"step_after\": " << step_after << ", \"step_restored\": " << step_restored
 		     << ", \"learning_rate\": " << trainer.learning_rate() << ", \"serialized_bytes\": " << snap.size()
-		     << ", \"rm_input_error\": \"" << err << "\"}";
+		     << ", \"rm_input_error\": \"" << err << "\", \"ctx_kind_error\": \"" << (ctx_err.empty() ? "" : "refused") << "\"}";
 		std::ofstream(dir + "/meta.json") << meta.str();
 	} catch (const std::exception& e) {
 		fprintf(stderr, "drop_in: %s\n", e.what());

@@ -1,8 +1,11 @@
 """The C++ drop-in caller (tests/cabi/drop_in.cpp over include/ngp_tcnn_adapter.hpp, g++ only) runs the
 Testbed's per-step call sequence through the C-ABI — density (testbed_nerf.cu:3514), inference over the
 samples (:4001), forward + backward (:4077-4078), optimizer_step (:3678), Trainer serialize/deserialize
-(src/testbed.cu:4874,5040) — in its own process on the GPU; its outputs are checked against the CPU
-oracle with the parity bars of test_gpu_parity.py (outputs 1e-2 of scale, gradients 2e-2 of scale)."""
+(src/testbed.cu:4874,5040) — and the input-gradient surface: input_gradient for normals written over the
+positions (testbed_nerf.cu:2616), backward with dL_dinput (nerf_network.h:262), density_forward /
+density_backward (:355-428) — in its own process on the GPU; its outputs are checked against the CPU
+oracle with the parity bars of test_gpu_parity.py (outputs 1e-2 of scale, gradients 2e-2 of scale) and
+of test_gpu_input_grad.py (input gradients per element)."""
 import json
 import os
 import subprocess
@@ -65,3 +68,34 @@ def test_cpp_drop_in_matches_oracle(tmp_path, orc):
     after = np.fromfile(tmp_path / "params_after.bin", np.uint16)
     changed = after != p16
     assert changed[:meta["n_matrix_params"]].mean() > 0.9  # every MLP weight with a gradient moves
+
+    # input gradients and the density-only pass, on the restored (initial) parameters. The initial grid
+    # is U(+-1e-4), so dL/dposition is small but not zero; bars per element (as test_gpu_input_grad.py)
+    keep = orc.nerf_train_ex(m, p16, c, dL.astype(np.float32))["margin"] > 1e-4
+    assert keep.mean() > 0.5
+    assert meta["ctx_kind_error"] == "refused"
+
+    def close(a, b, frac=2e-3):
+        bad = np.abs(a - b) > 1e-2 * np.abs(b) + 1e-3 * np.abs(b).max(axis=0) + 1e-9
+        return bad.mean() < frac
+    normals = np.fromfile(tmp_path / "normals.bin", np.float32).reshape(n, 7)
+    np.testing.assert_array_equal(normals[:, 3], c[:, 3])  # written over the coordinates: dt row kept
+    oh = np.zeros((n, 16), np.float32)
+    oh[:, 3] = 128.0
+    r_n = orc.nerf_input_grad(m, p16, c, oh, scale=1.0 / 128.0)
+    assert close(normals[keep, :3], r_n["dinput"][keep, :3])
+    assert np.all(normals[:, 4:] == 0.0)  # the density does not depend on the direction
+    din = np.fromfile(tmp_path / "dinput.bin", np.float32).reshape(n, 7)
+    r_b = orc.nerf_input_grad(m, p16, c, dL.astype(np.float32))
+    assert close(din[keep, :3], r_b["dinput"][keep, :3]) and close(din[keep, 4:], r_b["dinput"][keep, 4:])
+    assert np.all(din[:, 3] == 0.0)
+    dens = np.fromfile(tmp_path / "dens_out.bin", np.float16).reshape(n, 16).astype(np.float32)
+    assert np.abs(dens - ref_d).max() <= 1e-2 * np.abs(ref_d).max()
+    g2 = np.fromfile(tmp_path / "grads2.bin", np.float16).astype(np.float32)
+    ref_dg, ref_ddin = orc.nerf_density_backward(m, p16, c, dL.astype(np.float32))
+    for name, lo, hi, ref in [("density", 0, nd, ref_dg), ("rgb (from backward, untouched)", nd, nd + nr, ref_g),
+                              ("grid", nd + nr, g2.size, ref_dg)]:
+        err = np.abs(g2[lo:hi] - ref[lo:hi]).max()
+        assert err <= 2e-2 * np.abs(ref[lo:hi]).max() + 1e-4, name
+    ddin = np.fromfile(tmp_path / "dens_dinput.bin", np.float32).reshape(n, 7)
+    assert close(ddin[:, :3], ref_ddin[:, :3]) and np.all(ddin[:, 3:] == 0.0)

@@ -135,8 +135,8 @@ def test_generate_training_samples_cone(pkg, orc, scene, aabb_scale, n_rays, fra
 
 
 @pytest.mark.parametrize("aabb_scale,cone,n_rays,frac", [
-    (8.0, None, 1 << 16, 0.3), (32.0, None, 1 << 16, 0.15), (128.0, None, 1 << 16, 0.05),
-    (8.0, 1e-4, 1 << 14, 0.3), (8.0, 5e-4, 1 << 14, 0.3), (16.0, 2e-5, 1 << 13, 0.3), (8.0, 0.02, 1 << 14, 0.3)])
+    (8.0, None, 1 << 16, 0.05), (32.0, None, 1 << 16, 0.03), (128.0, None, 1 << 16, 0.01),
+    (8.0, 1e-4, 1 << 14, 0.05), (8.0, 5e-4, 1 << 14, 0.05), (16.0, 2e-5, 1 << 13, 0.05), (8.0, 0.02, 1 << 14, 0.1)])
 def test_sampler_and_loss_cone_at_scale(pkg, orc, scene, aabb_scale, cone, n_rays, frac):
     """Fox-scale and larger ray counts (>= 64k rays at aabb_scale 8, 32, 128) and user-set cone angles
     from 2e-5 to 0.02: the sampler's hardware exp/log speculation in empty space (csrc/nerf.hip
@@ -154,7 +154,7 @@ def test_sampler_and_loss_cone_at_scale(pkg, orc, scene, aabb_scale, cone, n_ray
     gn = {k: v.cpu().numpy() for k, v in got.items()}
     np.testing.assert_array_equal(gn["counters"].view(np.uint32), ref["counters"])
     kept = int(ref["counters"][0])
-    assert kept > n_rays // 4
+    assert kept > n_rays // 8  # most rays fit the sample budget (the rest are dropped, as the reference does)
     np.testing.assert_array_equal(gn["ray_indices"][:kept].view(np.uint32), ref["ray_indices"][:kept])
     np.testing.assert_array_equal(gn["numsteps"][:kept].view(np.uint32), ref["numsteps"][:kept])
     used = min(int(ref["counters"][1]), max_samples)

@@ -390,3 +390,134 @@ def test_nerf_train_ex_matches_serial(orc):
     gx, absum = orc.grid_backward_exact(m.grid, c[:, :3].copy(), r["denc16"], stride=3, with_abs_sum=True)
     tol = absum * 2.0 ** -11 + np.abs(ref[nm:]) * 2.0 ** -11 + 2.0 ** -24
     assert np.all(np.abs(orc.f16_bits_to_f32(gx) - ref[nm:]) <= tol)
+
+
+# ------------------------------------------------------------------------------------------------
+# Input gradients (orc_grid_input_grad, orc_sh4_input_grad) vs torch float64 autograd
+# ------------------------------------------------------------------------------------------------
+def torch_grid_pos(g, pos, table, max_level=1.0):
+    """The grid forward as a function of the positions (float64 autograd through the trilinear weights;
+    corner indices fixed by the float32 floor, as the forward's). pos: (n, D) float32."""
+    n, D = pos.shape
+    x = torch.from_numpy(pos.astype(np.float64)).requires_grad_(True)
+    outs = []
+    for l in range(g.n_levels):
+        if l >= max_level * g.n_levels + 1e-3:
+            outs.append(torch.zeros((n, g.n_features), dtype=torch.float64))
+            continue
+        scale = float(np.float32(g.scale[l]))
+        res = int(g.resolution[l])
+        T = int(g.offsets[l + 1] - g.offsets[l])
+        # the forward's float32 fractions as values (fmaf: one rounding), d frac / dx = scale as derivative
+        p32 = (pos.astype(np.float64) * scale + 0.5).astype(np.float32)
+        base = np.floor(p32)
+        frac32 = torch.from_numpy((p32 - base).astype(np.float64))
+        frac = frac32 + (x - x.detach()) * scale
+        base = base.astype(np.int64).astype(np.uint64)
+        acc = 0
+        for c in range(1 << D):
+            w = torch.ones(n, dtype=torch.float64)
+            pc = []
+            for d in range(D):
+                if c & (1 << d):
+                    w = w * frac[:, d]
+                    pc.append(base[:, d] + 1)
+                else:
+                    w = w * (1 - frac[:, d])
+                    pc.append(base[:, d])
+            stride, index = 1, np.zeros(n, np.uint64)
+            for d in range(D):
+                if stride > T:
+                    break
+                index = (index + pc[d] * np.uint64(stride)) & np.uint64(0xFFFFFFFF)
+                stride *= res
+            if T < stride:
+                index = np.zeros(n, np.uint64)
+                for d in range(D):
+                    index ^= (pc[d] * np.uint64(PRIMES[d])) & np.uint64(0xFFFFFFFF)
+            index = (index % np.uint64(T)).astype(np.int64) + int(g.offsets[l])
+            acc = acc + w[:, None] * table[torch.from_numpy(index)]
+        outs.append(acc)
+    return x, torch.cat(outs, dim=1)
+
+
+@pytest.mark.parametrize("D,L,F,log2T,max_level", [(3, 4, 4, 19, 1.0), (3, 16, 2, 14, 1.0), (2, 4, 2, 14, 1.0),
+                                                   (3, 8, 1, 12, 0.6), (3, 6, 8, 10, 1.0)])
+def test_grid_input_grad_vs_torch(orc, D, L, F, log2T, max_level):
+    g = orc.make_grid(D, L, F, log2T)
+    rng = np.random.default_rng(7 * D + L)
+    n = 256
+    pos = rng.random((n, D), dtype=np.float32)
+    E = orc.grid_n_entries(g)
+    table32 = (rng.random(E * F, dtype=np.float32) * 2 - 1).astype(np.float16).astype(np.float32)
+    table16 = table32.astype(np.float16).view(np.uint16)
+    dy = rng.standard_normal((n, L * F)).astype(np.float32)
+    got = orc.grid_input_grad(g, pos, table16, dy, max_level)
+    x, y = torch_grid_pos(g, pos, torch.from_numpy(table32.astype(np.float64).reshape(E, F)), max_level)
+    y.backward(torch.from_numpy(dy.astype(np.float64)))
+    ref = x.grad.numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-12 * np.abs(ref).max())
+
+
+def torch_sh4(d):
+    x, y, z = d[:, 0] * 2 - 1, d[:, 1] * 2 - 1, d[:, 2] * 2 - 1
+    xy, xz, yz, x2, y2, z2 = x * y, x * z, y * z, x * x, y * y, z * z
+    return torch.stack([
+        torch.full_like(x, 0.28209479177387814), -0.48860251190291987 * y, 0.48860251190291987 * z,
+        -0.48860251190291987 * x, 1.0925484305920792 * xy, -1.0925484305920792 * yz,
+        0.94617469575755997 * z2 - 0.31539156525251999, -1.0925484305920792 * xz,
+        0.54627421529603959 * x2 - 0.54627421529603959 * y2, 0.59004358992664352 * y * (-3.0 * x2 + y2),
+        2.8906114426405538 * xy * z, 0.45704579946446572 * y * (1.0 - 5.0 * z2), 0.3731763325901154 * z * (5.0 * z2 - 3.0),
+        0.45704579946446572 * x * (1.0 - 5.0 * z2), 1.4453057213202769 * z * (x2 - y2),
+        0.59004358992664352 * x * (-x2 + 3.0 * y2)], dim=1)
+
+
+def test_sh4_matches_torch_and_input_grad(orc):
+    rng = np.random.default_rng(11)
+    n = 200
+    d = rng.standard_normal((n, 3))
+    d = ((d / np.linalg.norm(d, axis=1, keepdims=True)) + 1) / 2
+    d32 = d.astype(np.float32)
+    dt = torch.from_numpy(d32.astype(np.float64)).requires_grad_(True)
+    sh = torch_sh4(dt)
+    np.testing.assert_allclose(np.stack([orc.sh4(v) for v in d32]), sh.detach().numpy(), rtol=1e-5, atol=1e-6)
+    g = rng.standard_normal((n, 16)).astype(np.float32)
+    sh.backward(torch.from_numpy(g.astype(np.float64)))
+    got = np.stack([orc.sh4_input_grad(d32[i], g[i]) for i in range(n)])
+    np.testing.assert_allclose(got, dt.grad.numpy(), rtol=1e-9, atol=1e-9)
+
+
+def test_nerf_input_grad_vs_torch(orc):
+    """The NerfNetwork input gradient (nerf_network.h:256-335 with dL_dinput) vs torch autograd of the
+    composition w.r.t. positions and directions (float64; the oracle rounds intermediates to fp16)."""
+    m = orc.make_nerf(L=4, F=4, log2T=12)
+    p32 = orc.nerf_init(m, 5)
+    rng = np.random.default_rng(5)
+    p32[orc.mlp_n_params(m.density) + orc.mlp_n_params(m.rgb):] = rng.uniform(-0.5, 0.5, orc.grid_n_entries(m.grid) * 4)
+    p16 = orc.f32_to_f16_bits(p32)
+    pq = orc.f16_bits_to_f32(p16).astype(np.float64)
+    n = 128
+    c = np.zeros((n, 7), np.float32)
+    c[:, :3] = rng.random((n, 3))
+    c[:, 3] = 0.01
+    dd = rng.standard_normal((n, 3))
+    c[:, 4:] = (dd / np.linalg.norm(dd, axis=1, keepdims=True) + 1) / 2
+    dL = np.zeros((n, 16), np.float32)
+    dL[:, :4] = rng.uniform(-1, 1, (n, 4)).astype(np.float16)
+    r = orc.nerf_input_grad(m, p16, c, dL)
+    nd, nr = orc.mlp_n_params(m.density), orc.mlp_n_params(m.rgb)
+    table = torch.from_numpy(pq[nd + nr:].reshape(-1, 4))
+    x, enc = torch_grid_pos(m.grid, c[:, :3], table)
+    enc = torch.cat([enc.half().double(), torch.zeros((n, m.density.in_pad - enc.shape[1]), dtype=torch.float64)], 1)
+    dout = torch_mlp(m.density, torch.from_numpy(pq[:nd]), enc)
+    dt = torch.from_numpy(c[:, 4:].astype(np.float64)).requires_grad_(True)
+    rout = torch_mlp(m.rgb, torch.from_numpy(pq[nd:nd + nr]), torch.cat([dout, torch_sh4(dt)], 1))
+    out = torch.cat([rout[:, :3], dout[:, :1]], 1)
+    out.backward(torch.from_numpy(dL[:, :4].astype(np.float64)))
+    # samples with a hidden pre-activation within 1e-4 (relative) of a ReLU switch are excluded: the torch
+    # encoding (float64, rounded once) can differ from the oracle's fp32 blend by one fp16 ulp and flip it
+    keep = orc.nerf_train_ex(m, p16, c, dL)["margin"] > 1e-4
+    assert keep.mean() > 0.5
+    for got, ref in ((r["dinput"][:, :3], x.grad.numpy()), (r["dinput"][:, 4:], dt.grad.numpy())):
+        # the oracle rounds activations and back-propagated gradients to fp16 (the kernel's contract)
+        np.testing.assert_allclose(got[keep], ref[keep], rtol=2e-2, atol=2e-2 * np.abs(ref).max())
