@@ -7,7 +7,7 @@ __graft_entry__.load_package() (tests/conftest.py does the same).
 from . import dp, exr, image, nerf, nerf_data, sdf, synthetic  # noqa: F401
 from ._capi import NgpError, lib  # noqa: F401
 from .config import IMAGE_BASE, NERF_BASE, SDF_BASE, load_config, merge_patch, nerf_config  # noqa: F401
-from .network import (GRAD_ACCUMULATE, GRAD_OVERWRITE, LAYOUT_AOS, LAYOUT_AOS_RGBD, LAYOUT_SOA, Model, NerfNetwork,  # noqa: F401
+from .network import (GRAD_ACCUMULATE, GRAD_IGNORE, GRAD_OVERWRITE, LAYOUT_AOS, LAYOUT_AOS_RGBD, LAYOUT_SOA, Model, NerfNetwork,  # noqa: F401
                       NetworkWithInputEncoding, Trainer, TrainingGraph, loss_evaluate, wrap_device)
 
 

@@ -58,7 +58,7 @@ def nerf_with_params(pkg, orc, log2T=15, L=4, F=4, seed=3, grid_scale=0.5):
 
 
 @pytest.mark.parametrize("D,L,F,log2T,max_level", [(3, 4, 4, 19, 1.0), (3, 16, 2, 19, 1.0), (2, 4, 2, 14, 1.0),
-                                                   (3, 8, 1, 12, 0.6), (3, 6, 8, 10, 1.0), (3, 16, 2, 22, 1.0)])
+                                                   (3, 8, 1, 12, 0.6), (3, 4, 8, 10, 1.0), (3, 16, 2, 22, 1.0)])
 def test_encoding_input_gradient_vs_oracle(pkg, orc, D, L, F, log2T, max_level):
     enc = {"otype": "HashGrid", "n_levels": L, "n_features_per_level": F, "log2_hashmap_size": log2T,
            "base_resolution": 16, "per_level_scale": 2.0}

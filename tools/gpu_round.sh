@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 has() { [[ " $STAGES " == *" $1 "* ]]; }
 
 if has tests; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu ${PYTEST_ARGS:--x} -q --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
   tail -3 "$OUT/gpu_tests.log"
 fi
 if has smoke; then
