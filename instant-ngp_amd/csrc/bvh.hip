@@ -20,6 +20,7 @@
 #include <stack>
 #include <vector>
 
+#include "profiler.h"
 #include "training.h"
 
 namespace ngp {
@@ -46,6 +47,8 @@ void bbox_of(const HostTri* b, const HostTri* e, BvhNode& n) {
 
 void build_bvh4(float* tris, uint32_t n_triangles, uint32_t n_primitives_per_leaf, std::vector<BvhNode>& nodes) {
 	NGP_CHECK(n_triangles >= 4, "bvh: need at least 4 triangles");
+	// device traversal entries pack a leaf as (first triangle, count - 1) in 25 + 6 bits (node_entry)
+	NGP_CHECK(n_primitives_per_leaf <= 64 && n_triangles < (1u << 25), "bvh: at most 64 triangles per leaf and 2^25 triangles");
 	HostTri* T = (HostTri*)tris;
 	nodes.clear();
 	nodes.emplace_back();
@@ -98,6 +101,17 @@ void build_bvh4(float* tris, uint32_t n_triangles, uint32_t n_primitives_per_lea
 		}
 		nodes[cur.node].right = (int32_t)nodes.size();
 	}
+}
+
+uint32_t bvh_depth(const std::vector<BvhNode>& nodes) {
+	std::vector<uint32_t> d(nodes.size(), 0);  // children are stored after their parent (build order)
+	uint32_t deepest = 0;
+	for (size_t i = 0; i < nodes.size(); ++i) {
+		if (nodes[i].left < 0) continue;
+		deepest = std::max(deepest, d[i] + 1);
+		for (int c = 0; c < 4; ++c) d[nodes[i].left + c] = d[i] + 1;
+	}
+	return deepest;
 }
 
 // ---- device -----------------------------------------------------------------------------------
@@ -173,30 +187,57 @@ template <typename K> __device__ __forceinline__ void sort4_desc(K* k, int* id) 
 	cs(0, 2); cs(1, 3); cs(0, 1); cs(2, 3); cs(1, 2);
 }
 
-// closest_triangle (triangle_bvh.cu:286-335): squared distance, or -1 if none within max_sq
-__device__ float closest_dist_sq(V p, const BvhNode* __restrict__ nodes, const float* __restrict__ tris, float max_sq) {
-	int stack[STACK];
+// Traversal state. A stack entry names what the traversal needs next without re-reading the node it
+// came from: an internal node is pushed as the index of its first child (its 4 children are stored
+// consecutively, build_bvh4), a leaf as -(first_triangle * 64 + count - 1) - 1. The per-lane stacks live
+// in LDS, slot-major ([slot][thread]: consecutive lanes hit consecutive banks); as a register array a
+// divergent stack pointer turns every push and pop into a 32-way select chain.
+__device__ __forceinline__ int node_entry(const BvhNode& n) {
+	return n.left >= 0 ? n.left : -(((-n.left - 1) << 6) + (n.left - n.right - 1)) - 1;
+}
+__device__ __forceinline__ void leaf_range(int e, int& first, int& end) {
+	const int v = -e - 1;
+	first = v >> 6;
+	end = first + (v & 63) + 1;
+}
+
+// closest_triangle (triangle_bvh.cu:286-335): squared distance, or -1 if none within max_sq. Same
+// arithmetic, pruning and visiting order as the reference's traversal (children pushed farthest first,
+// pruned at push time against the best distance so far).
+__device__ float closest_dist_sq(V p, const BvhNode* __restrict__ nodes, const float* __restrict__ tris, float max_sq, int* stk,
+                                 int stride) {
+	// the nearest accepted child is visited next straight from a register (the reference pushes it last
+	// and pops it first: the same order); only its farther siblings go through the LDS stack
+	int e = nodes[0].left;  // the root is always internal (build_bvh4 splits it)
 	int sp = 0;
-	stack[sp++] = 0;
 	float best = max_sq;
 	bool found = false;
-	while (sp > 0) {
-		const BvhNode node = nodes[stack[--sp]];
-		if (node.left < 0) {
-			const int end = -node.right - 1;
-			for (int i = -node.left - 1; i < end; ++i) {
+	while (true) {
+		if (e < 0) {
+			int i, end;
+			leaf_range(e, i, end);
+			for (; i < end; ++i) {
 				const float d = tri_dist_sq(tris + 9 * (size_t)i, p);
 				if (d <= best) { best = d; found = true; }
 			}
+			if (sp == 0) break;
+			e = stk[--sp * stride];
 		} else {
 			float k[4];
 			int id[4];
 #pragma unroll
-			for (int c = 0; c < 4; ++c) { id[c] = node.left + c; k[c] = box_dist_sq(nodes[node.left + c], p); }
+			for (int c = 0; c < 4; ++c) {
+				const BvhNode ch = nodes[e + c];
+				id[c] = node_entry(ch);
+				k[c] = box_dist_sq(ch, p);
+			}
 			sort4_desc(k, id);
 #pragma unroll
-			for (int c = 0; c < 4; ++c)
-				if (k[c] <= best && sp < STACK) stack[sp++] = id[c];
+			for (int c = 0; c < 3; ++c)
+				if (k[c] <= best && sp < STACK) stk[sp++ * stride] = id[c];
+			if (k[3] <= best) e = id[3];
+			else if (sp == 0) break;
+			else e = stk[--sp * stride];
 		}
 	}
 	return found ? best : -1.0f;
@@ -236,24 +277,53 @@ __device__ __forceinline__ uint64_t pcg_advanced(uint64_t state, uint64_t inc, u
 	return am * state + ap;
 }
 
+// Slab test of a stab ray against a child box, widened so that it never rejects a box the reference's
+// division-based BoundingBox::ray_intersect (box_ray_t) accepts: the ray's reciprocal direction is
+// computed once, each slab distance (lo - o) * (1/d) is within 3 ulp of the quotient (lo - o) / d, and the
+// overlap and MAX_DIST tests get a slack of 2^-19 of the magnitudes involved (>= 16 ulp). Accepting extra
+// boxes only visits more triangles; the sign is decided by tri_ray_t alone (a triangle hit lies inside
+// every box that contains the triangle), so the outcome is the reference's. Rays with a zero direction
+// component (0 * inf) take the exact test.
+struct StabRay {
+	V o, d, id;
+	bool exact;
+};
+__device__ __forceinline__ float stab_box(const BvhNode& n, const StabRay& r) {  // entry distance, or FMAX if rejected
+	if (r.exact) return box_ray_t(n, r.o, r.d);
+	const float x0 = (n.lo[0] - r.o.x) * r.id.x, x1 = (n.hi[0] - r.o.x) * r.id.x;
+	const float y0 = (n.lo[1] - r.o.y) * r.id.y, y1 = (n.hi[1] - r.o.y) * r.id.y;
+	const float z0 = (n.lo[2] - r.o.z) * r.id.z, z1 = (n.hi[2] - r.o.z) * r.id.z;
+	const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+	const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+	const float slack = (fabsf(tn) + fabsf(tf)) * 1.9073486e-6f + 1e-30f;  // 2^-19
+	return (tn <= tf + slack && tn < MAX_DIST * (1.0f + 1.9073486e-6f)) ? fminf(tn, MAX_DIST * 0.5f) : 3.402823466e+38f;
+}
+
 // signed_distance_raystab_kernel (triangle_bvh.cu:688-703) in two launches. Distance: one thread per
 // point (closest_triangle under the upper bound). Sign: 32 lanes per point, lane k traces stab ray k —
 // the rays of one point traverse similar nodes, so the half-wave stays coherent where one thread would
 // run the 32 traversals back to back; the first lane whose ray escapes raises an LDS flag that stops the
 // others (the sign only asks whether any ray escapes).
-__global__ void __launch_bounds__(128) k_sdf_distance(uint32_t n, const float* __restrict__ pos, const BvhNode* __restrict__ nodes,
-                                                      const float* __restrict__ tris, float* __restrict__ dist, bool upper_bounds) {
+constexpr uint32_t DIST_T = 128;
+__global__ void __launch_bounds__(DIST_T) k_sdf_distance(uint32_t n, const float* __restrict__ pos, const BvhNode* __restrict__ nodes,
+                                                         const float* __restrict__ tris, float* __restrict__ dist, bool upper_bounds) {
+	__shared__ int stk[STACK * DIST_T];
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
 	const float max_d = upper_bounds ? dist[i] : MAX_DIST;
-	const float dsq = closest_dist_sq(vld(pos + 3 * (size_t)i), nodes, tris, max_d * max_d);
+	const float dsq = closest_dist_sq(vld(pos + 3 * (size_t)i), nodes, tris, max_d * max_d, stk + threadIdx.x, DIST_T);
 	dist[i] = dsq < 0.f ? 0.0f : sqrtf(dsq);
 }
 
 constexpr uint32_t SIGN_T = 256;  // 8 points per block
+// per-lane stack: the farther siblings along the current path, at most 3 per internal level, so
+// 3 x depth slots never overflow (the armadillo's BVH: 7 internal levels, 21 slots = 21 KB of LDS per
+// block). Dynamic LDS sized by the host.
 __global__ void __launch_bounds__(SIGN_T) k_sdf_sign(uint32_t n, const float* __restrict__ pos, const BvhNode* __restrict__ nodes,
                                                      const float* __restrict__ tris, float* __restrict__ dist) {
 	__shared__ uint32_t escaped[SIGN_T / 32];
+	extern __shared__ int stk_all[];
+	int* stk = stk_all + threadIdx.x;
 	const uint32_t g = threadIdx.x / 32, k = threadIdx.x % 32;
 	const uint32_t i = blockIdx.x * (SIGN_T / 32) + g;
 	if (k == 0) escaped[g] = 0u;
@@ -263,30 +333,51 @@ __global__ void __launch_bounds__(SIGN_T) k_sdf_sign(uint32_t n, const float* __
 		const uint64_t inc = 0xda3e39cb94b95bdbULL;  // default_rng_t advanced by 2 i
 		uint64_t st = pcg_advanced(0x853c49e6748fea9bULL, inc, 2ull * i);
 		const float ox = pcg_next_float(st, inc), oy = pcg_next_float(st, inc);
-		const V d = fib_dir32(k, ox, oy);
-		// any triangle closer than MAX_DIST along ray k? (stops early once another ray escaped)
-		int stack[STACK];
+		StabRay r;
+		r.o = p;
+		r.d = fib_dir32(k, ox, oy);
+		r.id = V{1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z};
+		r.exact = r.d.x == 0.f || r.d.y == 0.f || r.d.z == 0.f;
+		// any triangle closer than MAX_DIST along ray k? (stops early once another ray escaped). The node
+		// to visit next is kept in a register (`e`): a descent to the nearest accepted child costs no
+		// stack round trip; only its farther siblings are pushed.
+		int e = nodes[0].left;
 		int sp = 0;
-		stack[sp++] = 0;
-		bool hit = false;
-		while (sp > 0 && !hit) {
+		bool hit = false, done = false;
+		while (!done) {
 			if (__hip_atomic_load(&escaped[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-			const BvhNode node = nodes[stack[--sp]];
-			if (node.left < 0) {
-				const int end = -node.right - 1;
-				for (int t = -node.left - 1; t < end && !hit; ++t) hit = tri_ray_t(tris + 9 * (size_t)t, p, d) < MAX_DIST;
+			if (e < 0) {
+				int t, end;
+				leaf_range(e, t, end);
+				for (; t < end && !hit; t += 2) {  // two triangles' loads in flight
+					const bool h0 = tri_ray_t(tris + 9 * (size_t)t, p, r.d) < MAX_DIST;
+					const bool h1 = t + 1 < end && tri_ray_t(tris + 9 * (size_t)(t + 1), p, r.d) < MAX_DIST;
+					hit = h0 || h1;
+				}
+				if (hit) break;
+				if (sp == 0) done = true;
+				else e = stk[--sp * SIGN_T];
 			} else {
 				float kk[4];
 				int id[4];
 #pragma unroll
-				for (int c = 0; c < 4; ++c) { id[c] = node.left + c; kk[c] = box_ray_t(nodes[node.left + c], p, d); }
+				for (int c = 0; c < 4; ++c) {
+					const BvhNode ch = nodes[e + c];
+					id[c] = node_entry(ch);
+					kk[c] = stab_box(ch, r);
+				}
+				// nearest accepted child next, the others pushed farthest first: only how soon a hit is
+				// found depends on the order
 				sort4_desc(kk, id);
 #pragma unroll
-				for (int c = 0; c < 4; ++c)
-					if (kk[c] < MAX_DIST && sp < STACK) stack[sp++] = id[c];
+				for (int c = 0; c < 3; ++c)
+					if (kk[c] < MAX_DIST) stk[sp++ * SIGN_T] = id[c];
+				if (kk[3] < MAX_DIST) e = id[3];
+				else if (sp == 0) done = true;
+				else e = stk[--sp * SIGN_T];
 			}
 		}
-		if (!hit && sp == 0) __hip_atomic_store(&escaped[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+		if (done) __hip_atomic_store(&escaped[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 	}
 	__syncthreads();
 	if (i < n && k == 0 && !escaped[g]) dist[i] = -dist[i];
@@ -296,9 +387,15 @@ __global__ void __launch_bounds__(SIGN_T) k_sdf_sign(uint32_t n, const float* __
 void sdf_signed_distance(const SdfMeshDev& m, uint32_t n, const float* positions, float* distances, bool upper_bounds, hipStream_t s) {
 	if (n == 0) return;
 	NGP_CHECK(m.nodes, "sdf: mesh has no BVH");
-	k_sdf_distance<<<div_round_up(n, 128), 128, 0, s>>>(n, positions, m.nodes, m.tris, distances, upper_bounds);
-	NGP_HIP(hipGetLastError());
-	k_sdf_sign<<<div_round_up(n, SIGN_T / 32), SIGN_T, 0, s>>>(n, positions, m.nodes, m.tris, distances);
+	{
+		ProfScope ps("sdf_distance", s);
+		k_sdf_distance<<<div_round_up(n, DIST_T), DIST_T, 0, s>>>(n, positions, m.nodes, m.tris, distances, upper_bounds);
+		NGP_HIP(hipGetLastError());
+	}
+	ProfScope ps("sdf_sign", s);
+	const size_t lds = (size_t)3 * std::max(m.depth, 1u) * SIGN_T * sizeof(int);
+	NGP_CHECK(lds <= 64 * 1024, "sdf: BVH too deep for the stab-ray stacks");
+	k_sdf_sign<<<div_round_up(n, SIGN_T / 32), SIGN_T, lds, s>>>(n, positions, m.nodes, m.tris, distances);
 	NGP_HIP(hipGetLastError());
 }
 

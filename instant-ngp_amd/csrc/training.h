@@ -49,7 +49,10 @@ struct SdfMeshDev {
 	const float* tris;                // [n x 9] vertices a, b, c, in BVH order
 	const float* cdf;                 // [n] inclusive area CDF normalised to 1 (triangle_cdf)
 	const BvhNode* nodes;             // 4-ary BVH (bvh.hip)
+	uint32_t depth;                   // internal nodes on the longest root-to-leaf path (bvh_depth)
 };
+// internal levels of a build_bvh4 tree (sizes the traversal stacks)
+uint32_t bvh_depth(const std::vector<BvhNode>& nodes);
 // TriangleBvh4::build (triangle_bvh.cu:540-617): reorders tris [n x 9] in place, fills nodes
 void build_bvh4(float* tris, uint32_t n_triangles, uint32_t n_primitives_per_leaf, std::vector<BvhNode>& nodes);
 // signed_distance_gpu, EMeshSdfMode::Raystab (triangle_bvh.cu:436-476): upper_bounds = the distances

@@ -1,6 +1,7 @@
 // training.hip — tcnn losses, image sampling (BASELINE C1) and SDF sampling (BASELINE C5) on gfx950.
 // See training.h for the reference call sites; every kernel cites the code it restates.
 #include "training.h"
+#include "profiler.h"
 
 #include <cmath>
 #include <cstring>
@@ -214,8 +215,11 @@ void sdf_generate_samples(const SdfMeshDev& m, const SdfSampleArgs& a, hipStream
 	NGP_CHECK(a.n % 8 == 0, "sdf: the number of samples must be a multiple of 8");
 	if (a.n == 0) return;
 	const uint32_t base = a.n / 8;
-	k_sdf_samples<<<div_round_up(a.n, 256), 256, 0, s>>>(m, a, 4 * base, 3 * base, base);
-	NGP_HIP(hipGetLastError());
+	{
+		ProfScope ps("sdf_samples", s);
+		k_sdf_samples<<<div_round_up(a.n, 256), 256, 0, s>>>(m, a, 4 * base, 3 * base, base);
+		NGP_HIP(hipGetLastError());
+	}
 	// the distances written above are upper bounds of the true ones (perturbation length / aabb
 	// diagonal x 1.001): signed_distance_gpu(..., use_existing_distances_as_upper_bounds = true)
 	sdf_signed_distance(m, 4 * base, a.positions + 3 * (size_t)(4 * base), a.distances + 4 * base, true, s);

@@ -50,6 +50,7 @@ struct ngp_sdf_mesh {
 	float* cdf = nullptr;   // [n]
 	BvhNode* nodes = nullptr;
 	uint32_t n_nodes = 0;
+	uint32_t depth = 0;
 	std::vector<float> tris_host;
 	Buf perturbations;
 	~ngp_sdf_mesh() {
@@ -57,7 +58,7 @@ struct ngp_sdf_mesh {
 		if (cdf) (void)hipFree(cdf);
 		if (nodes) (void)hipFree(nodes);
 	}
-	SdfMeshDev dev() const { return SdfMeshDev{n_triangles, tris, cdf, nodes}; }
+	SdfMeshDev dev() const { return SdfMeshDev{n_triangles, tris, cdf, nodes, depth}; }
 };
 
 #define TRY(...)                                   \
@@ -157,6 +158,7 @@ int ngp_sdf_mesh_create(uint32_t n_triangles, const float* tris_host, ngp_sdf_me
 		build_bvh4(m->tris_host.data(), n_triangles, 8, nodes);
 		tris_host = m->tris_host.data();
 		m->n_nodes = (uint32_t)nodes.size();
+		m->depth = bvh_depth(nodes);
 		NGP_HIP(hipMalloc(&m->nodes, nodes.size() * sizeof(BvhNode)));
 		NGP_HIP(hipMemcpy(m->nodes, nodes.data(), nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
 		// triangle_distribution.build(surface areas) (testbed_sdf.cu:1167-1172, discrete_distribution.h:20-36)

@@ -556,11 +556,28 @@ EXPORT void orc_nerf_grid_splat_ema(uint32_t n, const uint32_t* indices, const u
 }
 
 /* update_density_grid_mean_and_bitfield (:3538-3567), grid_to_bitfield (:762-786), bitfield_max_pool
- * (:788-809). The mean is order-dependent in the reference (reduce_sum); here it is an input. */
-EXPORT double orc_nerf_grid_mean(const float* grid) {
-	double s = 0.0;
-	for (uint32_t i = 0; i < N_CELLS; ++i) s += (double)(fmaxf(grid[i], 0.f) / (float)N_CELLS);
-	return s;
+ * (:788-809). The reference's mean is reduce_sum(max(v,0)/N) over cascade 0 (:3544-3551), a device
+ * reduction whose float order is unspecified. The contract fixes one order, and this restatement
+ * follows it step for step so the mean (and every bitfield bit that depends on it) is bit-exact:
+ * 512 partials, partial b = a 256-wide pairwise tree over lanes t of the running sums
+ * acc_t = sum_{k = t, t+256, ..} max(v[b*4096+k], 0)/N (in k order); then a 512-wide pairwise tree of
+ * the partials. Both trees add s[t] += s[t+off] for off = width/2 .. 1. */
+EXPORT float orc_nerf_grid_mean(const float* grid) {
+	const uint32_t blocks = 512, threads = 256, per_block = N_CELLS / 512;
+	float partial[512], s[512];
+	for (uint32_t b = 0; b < blocks; ++b) {
+		for (uint32_t t = 0; t < threads; ++t) {
+			float acc = 0.f;
+			for (uint32_t k = t; k < per_block; k += threads) acc += fmaxf(grid[b * per_block + k], 0.f) / (float)N_CELLS;
+			s[t] = acc;
+		}
+		for (uint32_t off = threads / 2; off > 0; off >>= 1)
+			for (uint32_t t = 0; t < off; ++t) s[t] += s[t + off];
+		partial[b] = s[0];
+	}
+	for (uint32_t off = blocks / 2; off > 0; off >>= 1)
+		for (uint32_t t = 0; t < off; ++t) partial[t] += partial[t + off];
+	return partial[0];
 }
 EXPORT void orc_nerf_grid_bitfield(const float* grid, uint32_t max_cascade, float mean, uint8_t* bf) {
 	uint32_t n_bytes = N_CELLS / 8 * CASCADES, n_nz = N_CELLS / 8 * (max_cascade + 1);

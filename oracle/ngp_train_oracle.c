@@ -249,6 +249,7 @@ static F3 fib_dir32(uint32_t i, float ox, float oy) {
 /* signed_distance_raystab_kernel (src/triangle_bvh.cu:688-703) over every triangle (the BVH only
  * prunes): per element i a default pcg32 advanced by 2 i gives the stab-ray offset random_val_2d. */
 EXPORT void orc_sdf_signed_distance(uint32_t n, const float* positions, uint32_t n_tris, const float* tris, float* distances) {
+#pragma omp parallel for schedule(dynamic, 1)
 	for (uint32_t i = 0; i < n; ++i) {
 		orc_pcg32 r0 = {0x853c49e6748fea9bULL, 0xda3e39cb94b95bdbULL};
 		orc_pcg32_advance(&r0, 2 * (int64_t)i);

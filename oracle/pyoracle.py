@@ -405,7 +405,7 @@ def _declare_nerf(L):
     d("orc_nerf_compute_loss", None, P, P, P, u32, u32, u32, Pcg32, u32, u32, P, P, P, P, P, P, P, P, P, f32, f32)
     d("orc_nerf_grid_samples", None, P, u32, Pcg32, u32, P, u32, f32, P, P)
     d("orc_nerf_grid_splat_ema", None, u32, P, P, u32, u32, f32, P)
-    d("orc_nerf_grid_mean", C.c_double, P)
+    d("orc_nerf_grid_mean", C.c_float, P)
     d("orc_nerf_counters_update", u32, u32, u32, u32, u32, f32, P, P, P)
     d("orc_nerf_max_inference", u32, u32, u32)
     d("orc_nerf_grid_bitfield", None, P, u32, f32, P)

@@ -2,7 +2,8 @@
 
 Bars: sample generation (ray indices, per-ray step counts and bases, ray origins/directions, sample
 coordinates) bit-exact with cone_angle 0 (no transcendental on that path; slots from prefix scans
-equal the oracle's ray-order slots); density-grid sample positions/indices and bitfields bit-exact;
+equal the oracle's ray-order slots); density-grid sample positions/indices, splat+EMA grid, mean
+(fixed reduction tree) and bitfields bit-exact;
 rollover bit-exact. Cone-angle stepping and compositing evaluate ngp_math.h's expf/logf on both sides,
 so sample indices, compacted counts, bases and coordinates are bit-exact at every aabb_scale; losses
 agree to 1e-4 relative and fp16 loss gradients to 2 fp16 ulp (sRGB targets use powf).
@@ -245,11 +246,30 @@ def test_density_grid_update(pkg, orc):
     ref_grid = grid.copy()
     orc.nerf_grid_splat_ema(idx_ref, dens[:, 0].copy().view(np.uint16), 3, ref_grid, 0.95)
     got = grid_t.cpu().numpy()
-    np.testing.assert_allclose(got, ref_grid, rtol=1e-5, atol=0)
+    # splat (atomicMax on the uint bits) and the EMA max-filter are exact float operations on the same
+    # density bits: the whole grid is bit-exact
+    np.testing.assert_array_equal(got.view(np.uint32), ref_grid.view(np.uint32))
     mean, bf = pkg.nerf.grid_mean_and_bitfield(grid_t, cfg.max_cascade)
-    m = float(mean[0].item())
-    assert m == pytest.approx(orc.nerf_grid_mean(got), rel=1e-5)
-    np.testing.assert_array_equal(bf.cpu().numpy(), orc.nerf_grid_bitfield(got, cfg.max_cascade, m))
+    m = np.float32(mean[0].item())
+    m_ref = np.float32(orc.nerf_grid_mean(ref_grid))
+    assert m.view(np.uint32) == m_ref.view(np.uint32), (m, m_ref)  # the fixed reduction tree, restated
+    np.testing.assert_array_equal(bf.cpu().numpy(), orc.nerf_grid_bitfield(ref_grid, cfg.max_cascade, float(m_ref)))
+
+
+@pytest.mark.parametrize("seed,frac,scale", [(0, 0.3, 0.02), (1, 1.0, 1e-3), (2, 0.05, 5.0)])
+def test_density_grid_mean_bitfield_bitexact(pkg, orc, seed, frac, scale):
+    """update_density_grid_mean_and_bitfield (testbed_nerf.cu:3538-3567): the mean over cascade 0 and
+    all 8 bitfield mips bit-exact from the grid alone (no GPU-provided mean), with thresholds that land
+    on both sides of min(0.01, mean)."""
+    g = np.random.default_rng(seed)
+    grid = np.where(g.random(128 ** 3 * 8) < frac, g.random(128 ** 3 * 8) * scale, 0.0).astype(np.float32)
+    grid[g.integers(0, grid.size, 5000)] = -1.0
+    for max_cascade in (0, 3, 7):
+        mean, bf = pkg.nerf.grid_mean_and_bitfield(torch.from_numpy(grid).cuda(), max_cascade)
+        m = np.float32(mean[0].item())
+        m_ref = np.float32(orc.nerf_grid_mean(grid))
+        assert m.view(np.uint32) == m_ref.view(np.uint32), (m, m_ref)
+        np.testing.assert_array_equal(bf.cpu().numpy(), orc.nerf_grid_bitfield(grid, max_cascade, float(m_ref)))
 
 
 def test_nerf_training_end_to_end(pkg, orc):
@@ -272,12 +292,16 @@ def test_nerf_training_end_to_end(pkg, orc):
     assert 0 < stats[-1]["measured_batch_size"] <= stats[-1]["measured_batch_size_before_compaction"]
     assert stats[-1]["rays_per_batch"] % 256 == 0
     grid = run.density_grid.cpu().numpy()
-    m = float(run.mean_density.cpu().numpy()[0])
+    m = np.float32(run.mean_density.cpu().numpy()[0])
     bf = run.bitfield.cpu().numpy()
     assert grid.size == 128 ** 3 * (cfg.max_cascade + 1)
     full = np.zeros(128 ** 3 * 8, np.float32)
     full[:grid.size] = grid
-    np.testing.assert_array_equal(bf, orc.nerf_grid_bitfield(full, cfg.max_cascade, m))
+    # the trainer's mean is the oracle's fixed-tree mean of the trainer's grid, bit for bit, and the
+    # bitfield follows from the grid alone
+    m_ref = np.float32(orc.nerf_grid_mean(full))
+    assert m.view(np.uint32) == m_ref.view(np.uint32), (m, m_ref)
+    np.testing.assert_array_equal(bf, orc.nerf_grid_bitfield(full, cfg.max_cascade, float(m_ref)))
     occupied = np.unpackbits(bf[:128 ** 3 // 8]).mean()
     assert 0.0 < occupied < 0.5  # the grid prunes once step >= 256 switches to the 0.01 threshold (:3518)
 

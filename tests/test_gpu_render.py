@@ -18,11 +18,11 @@ def pkg():
     return load_package()
 
 
-def _setup(pkg, orc, seed, grid_frac):
+def _setup(pkg, orc, seed, grid_frac, aabb_scale=1.0):
     S = pkg.synthetic
     c2w = S.camera_poses(3, seed=seed)[1]
     cam = pkg.nerf.make_image(40, 30, pkg.nerf.nerf_matrix_to_ngp(c2w), camera_angle_x=S.LEGO_CAMERA_ANGLE_X)
-    cfg = pkg.nerf.default_config(1.0)
+    cfg = pkg.nerf.default_config(aabb_scale)
     ncfg = pkg.nerf_config("C2")
     ncfg["encoding"]["log2_hashmap_size"] = 14
     net = pkg.create_nerf_network(ncfg)
@@ -41,9 +41,12 @@ def _setup(pkg, orc, seed, grid_frac):
     return cam, cfg, net, p16, bf, m
 
 
-@pytest.mark.parametrize("seed,frac,sample_index", [(0, 1.0, 0), (1, 0.3, 3)])
-def test_render_matches_oracle(pkg, orc, seed, frac, sample_index):
-    cam, cfg, net, p16, bf, m = _setup(pkg, orc, seed, frac)
+@pytest.mark.parametrize("seed,frac,sample_index,aabb_scale", [(0, 1.0, 0, 1.0), (1, 0.3, 3, 1.0), (5, 0.3, 0, 8.0),
+                                                                (6, 0.15, 2, 4.0), (7, 0.05, 1, 16.0)])
+def test_render_matches_oracle(pkg, orc, seed, frac, sample_index, aabb_scale):
+    """aabb_scale > 1 (fox is 8: 4 cascades): the tracer marches with cone stepping through the shared
+    ngp_math.h logf/expf and mips up to max_cascade (testbed_nerf.cu:948-1240,2504-2659)."""
+    cam, cfg, net, p16, bf, m = _setup(pkg, orc, seed, frac, aabb_scale)
     r = pkg.nerf.NerfRenderer()
     bg = (0.1, 0.2, 0.3, 1.0)
     img = r.render(net, cfg, cam, torch.from_numpy(bf).cuda(), spp=1, sample_index=sample_index, min_transmittance=1e-4,

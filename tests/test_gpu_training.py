@@ -6,11 +6,16 @@ targets within 2e-6 (powf of the sRGB curve may differ by an ulp); SDF surface/u
 positions within 1e-6, perturbed ones within 1e-5 (logf), signed distances within 1e-5 (sign equal
 away from the surface); training_step gradients equal forward_backward given the same dL/doutput.
 """
+import os
+import sys
+
 import numpy as np
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARMADILLO = os.path.join(ROOT, "data", "sdf", "armadillo.obj")
 
 
 @pytest.fixture(scope="module")
@@ -180,3 +185,26 @@ def test_sdf_bvh_signed_distance_matches_bruteforce(pkg, orc):
     ref = orc.sdf_signed_distance(pts, mesh.triangles)
     assert np.mean(ref < 0) > 0.1 and np.mean(ref > 0) > 0.1
     np.testing.assert_allclose(got, ref, rtol=0, atol=1e-5)
+
+
+@pytest.mark.skipif(not os.path.isfile(ARMADILLO), reason="data/sdf not staged (tools/stage_sdf.sh)")
+def test_sdf_armadillo_signed_distance_matches_bruteforce(pkg, orc):
+    """C5's mesh (armadillo, ~100k triangles): the online ground truth of the training batch — perturbed
+    surface samples (the hard case for the stab rays: they start next to the surface) and uniform
+    samples — equals the oracle's brute force over every triangle, sign and distance."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import sdf_train
+    tris, amin, amax, brad = pkg.sdf.load_mesh(sdf_train.load_obj_triangles(ARMADILLO))
+    mesh = pkg.sdf.SdfMesh(tris)
+    net = pkg.NetworkWithInputEncoding(3, 1, enc(3, 4, 2, 14), MLP)
+    tr = pkg.Trainer(net, ADAM)
+    st = pkg.sdf.SdfTraining(net, tr, mesh, amin, amax, brad, seed=5, batch_size=1 << 12)
+    pos, dist = st.generate_training_samples(1 << 12)
+    base = (1 << 12) // 8
+    pts = pos.cpu().numpy()[4 * base:]
+    idx = np.concatenate([np.arange(0, 3 * base, 3 * base // 96), np.arange(3 * base, 4 * base, base // 32)])
+    got = mesh.signed_distance(torch.from_numpy(np.ascontiguousarray(pts[idx])).cuda()).cpu().numpy()
+    ref = orc.sdf_signed_distance(pts[idx], mesh.triangles)
+    assert np.mean(ref < 0) > 0.2 and np.mean(ref > 0) > 0.2
+    np.testing.assert_array_equal(np.sign(got), np.sign(ref))
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-6)
