@@ -17,6 +17,8 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <stack>
 #include <vector>
 
@@ -202,23 +204,34 @@ __device__ __forceinline__ void leaf_range(int e, int& first, int& end) {
 }
 
 // closest_triangle (triangle_bvh.cu:286-335): squared distance, or -1 if none within max_sq. Same
-// arithmetic, pruning and visiting order as the reference's traversal (children pushed farthest first,
-// pruned at push time against the best distance so far).
+// arithmetic and pruning as the reference's traversal (children visited nearest first, pruned at push
+// time against the best distance so far), with the root's four subtrees searched by the four lanes of a
+// group (DIST_G) that share their best distance through LDS: a pruning bound can only be one another
+// lane has reached, so the minimum found is the serial search's (the closest triangle is never pruned:
+// its box distance is below its own distance).
 __device__ float closest_dist_sq(V p, const BvhNode* __restrict__ nodes, const float* __restrict__ tris, float max_sq, int* stk,
-                                 int stride) {
+                                 int stride, uint32_t* shared_best, int sub) {
 	// the nearest accepted child is visited next straight from a register (the reference pushes it last
 	// and pops it first: the same order); only its farther siblings go through the LDS stack
-	int e = nodes[0].left;  // the root is always internal (build_bvh4 splits it)
-	int sp = 0;
+	const BvhNode top = nodes[nodes[0].left + sub];  // the root is always internal (build_bvh4 splits it)
 	float best = max_sq;
 	bool found = false;
+	if (box_dist_sq(top, p) > best) return -1.0f;
+	int e = node_entry(top);
+	int sp = 0;
 	while (true) {
+		best = fminf(best, __uint_as_float(__hip_atomic_load(shared_best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)));
 		if (e < 0) {
 			int i, end;
 			leaf_range(e, i, end);
+			float lb = best;
 			for (; i < end; ++i) {
 				const float d = tri_dist_sq(tris + 9 * (size_t)i, p);
-				if (d <= best) { best = d; found = true; }
+				if (d <= lb) { lb = d; found = true; }
+			}
+			if (lb < best) {
+				best = lb;
+				atomicMin(shared_best, __float_as_uint(lb));  // non-negative floats order as their bits
 			}
 			if (sp == 0) break;
 			e = stk[--sp * stride];
@@ -304,24 +317,38 @@ __device__ __forceinline__ float stab_box(const BvhNode& n, const StabRay& r) { 
 // the rays of one point traverse similar nodes, so the half-wave stays coherent where one thread would
 // run the 32 traversals back to back; the first lane whose ray escapes raises an LDS flag that stops the
 // others (the sign only asks whether any ray escapes).
-constexpr uint32_t DIST_T = 128;
+constexpr uint32_t DIST_T = 256, DIST_G = 4;  // 64 points per block, one lane per root subtree
 __global__ void __launch_bounds__(DIST_T) k_sdf_distance(uint32_t n, const float* __restrict__ pos, const BvhNode* __restrict__ nodes,
                                                          const float* __restrict__ tris, float* __restrict__ dist, bool upper_bounds) {
 	__shared__ int stk[STACK * DIST_T];
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= n) return;
-	const float max_d = upper_bounds ? dist[i] : MAX_DIST;
-	const float dsq = closest_dist_sq(vld(pos + 3 * (size_t)i), nodes, tris, max_d * max_d, stk + threadIdx.x, DIST_T);
-	dist[i] = dsq < 0.f ? 0.0f : sqrtf(dsq);
+	__shared__ uint32_t best[DIST_T / DIST_G];
+	__shared__ uint32_t any[DIST_T / DIST_G];
+	const uint32_t g = threadIdx.x / DIST_G, sub = threadIdx.x % DIST_G;
+	const uint32_t i = blockIdx.x * (DIST_T / DIST_G) + g;
+	const float max_d = i < n ? (upper_bounds ? dist[i] : MAX_DIST) : 0.f;
+	if (sub == 0) { best[g] = __float_as_uint(max_d * max_d); any[g] = 0u; }
+	__syncthreads();
+	if (i < n) {
+		const float dsq = closest_dist_sq(vld(pos + 3 * (size_t)i), nodes, tris, max_d * max_d, stk + threadIdx.x, DIST_T, &best[g],
+		                                  (int)sub);
+		if (dsq >= 0.f) atomicOr(&any[g], 1u);
+	}
+	__syncthreads();
+	if (i < n && sub == 0) dist[i] = any[g] ? sqrtf(__uint_as_float(best[g])) : 0.0f;
 }
 
 constexpr uint32_t SIGN_T = 256;  // 8 points per block
 // per-lane stack: the farther siblings along the current path, at most 3 per internal level, so
 // 3 x depth slots never overflow (the armadillo's BVH: 7 internal levels, 21 slots = 21 KB of LDS per
-// block). Dynamic LDS sized by the host.
+// block). Dynamic LDS sized by the host. (A per-block pool of 32 points' rays drawn by idle lanes was
+// measured slower, 4.5 -> 5.1 ms on the armadillo batch: the traversal is bound by the node and
+// triangle fetches, not by lanes idling between a ray's end and its point's. A binned-SAH query tree
+// cut node visits per ray by ~15 % (33 -> 30) and ran no faster; the reference's median-split tree stays.)
 __global__ void __launch_bounds__(SIGN_T) k_sdf_sign(uint32_t n, const float* __restrict__ pos, const BvhNode* __restrict__ nodes,
-                                                     const float* __restrict__ tris, float* __restrict__ dist) {
+                                                     const float* __restrict__ tris, float* __restrict__ dist,
+                                                     unsigned long long* __restrict__ stats) {
 	__shared__ uint32_t escaped[SIGN_T / 32];
+	uint32_t n_inner = 0, n_leaf = 0, n_tri = 0;  // traversal statistics (stats != nullptr: NGP_SDF_STATS)
 	extern __shared__ int stk_all[];
 	int* stk = stk_all + threadIdx.x;
 	const uint32_t g = threadIdx.x / 32, k = threadIdx.x % 32;
@@ -349,6 +376,8 @@ __global__ void __launch_bounds__(SIGN_T) k_sdf_sign(uint32_t n, const float* __
 			if (e < 0) {
 				int t, end;
 				leaf_range(e, t, end);
+				++n_leaf;
+				n_tri += end - t;
 				for (; t < end && !hit; t += 2) {  // two triangles' loads in flight
 					const bool h0 = tri_ray_t(tris + 9 * (size_t)t, p, r.d) < MAX_DIST;
 					const bool h1 = t + 1 < end && tri_ray_t(tris + 9 * (size_t)(t + 1), p, r.d) < MAX_DIST;
@@ -358,6 +387,7 @@ __global__ void __launch_bounds__(SIGN_T) k_sdf_sign(uint32_t n, const float* __
 				if (sp == 0) done = true;
 				else e = stk[--sp * SIGN_T];
 			} else {
+				++n_inner;
 				float kk[4];
 				int id[4];
 #pragma unroll
@@ -381,6 +411,16 @@ __global__ void __launch_bounds__(SIGN_T) k_sdf_sign(uint32_t n, const float* __
 	}
 	__syncthreads();
 	if (i < n && k == 0 && !escaped[g]) dist[i] = -dist[i];
+	if (stats && i < n) {
+		atomicAdd(&stats[0], (unsigned long long)n_inner);
+		atomicAdd(&stats[1], (unsigned long long)n_leaf);
+		atomicAdd(&stats[2], (unsigned long long)n_tri);
+		atomicAdd(&stats[3], 1ull);
+		if (k == 0) {
+			atomicAdd(&stats[5], 1ull);
+			if (!escaped[g]) atomicAdd(&stats[6], 1ull);
+		}
+	}
 }
 }  // namespace
 
@@ -389,14 +429,28 @@ void sdf_signed_distance(const SdfMeshDev& m, uint32_t n, const float* positions
 	NGP_CHECK(m.nodes, "sdf: mesh has no BVH");
 	{
 		ProfScope ps("sdf_distance", s);
-		k_sdf_distance<<<div_round_up(n, DIST_T), DIST_T, 0, s>>>(n, positions, m.nodes, m.tris, distances, upper_bounds);
+		k_sdf_distance<<<div_round_up(n, DIST_T / DIST_G), DIST_T, 0, s>>>(n, positions, m.nodes, m.tris, distances, upper_bounds);
 		NGP_HIP(hipGetLastError());
 	}
 	ProfScope ps("sdf_sign", s);
 	const size_t lds = (size_t)3 * std::max(m.depth, 1u) * SIGN_T * sizeof(int);
 	NGP_CHECK(lds <= 64 * 1024, "sdf: BVH too deep for the stab-ray stacks");
-	k_sdf_sign<<<div_round_up(n, SIGN_T / 32), SIGN_T, lds, s>>>(n, positions, m.nodes, m.tris, distances);
+	static unsigned long long* stats = nullptr;
+	const bool want_stats = getenv("NGP_SDF_STATS") != nullptr;
+	if (want_stats && !stats) NGP_HIP(hipMalloc(&stats, 8 * sizeof(unsigned long long)));
+	if (want_stats) NGP_HIP(hipMemsetAsync(stats, 0, 8 * sizeof(unsigned long long), s));
+	k_sdf_sign<<<div_round_up(n, SIGN_T / 32), SIGN_T, lds, s>>>(n, positions, m.nodes, m.tris, distances,
+	                                                            want_stats ? stats : nullptr);
 	NGP_HIP(hipGetLastError());
+	if (want_stats) {  // diagnostics: traversal work per stab ray and per point
+		unsigned long long h[8];
+		NGP_HIP(hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, s));
+		NGP_HIP(hipStreamSynchronize(s));
+		const double lanes = (double)std::max(h[3], 1ull), groups = (double)std::max(h[5], 1ull);
+		fprintf(stderr, "{\"sdf_sign_stats\": {\"points\": %llu, \"inner_per_ray\": %.2f, \"leaf_per_ray\": %.2f, "
+		        "\"tris_per_ray\": %.2f, \"inside_frac\": %.4f}}\n",
+		        h[5], h[0] / lanes, h[1] / lanes, h[2] / lanes, h[6] / groups);
+	}
 }
 
 }  // namespace ngp
