@@ -788,6 +788,13 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	for (int q = 0; q < Lay::N_FWD; ++q) wreg[q] = a.frags[q * 64 + lane];
 #pragma unroll
 	for (int q = 0; q < T::N_BWD; ++q) breg[q] = a.frags[(Lay::N_FWD + q) * 64 + lane];
+	// The fragments live in the accumulator file (AGPRs can be an MFMA's A operand): left to itself the
+	// register allocator parks them there anyway under VGPR pressure and copies them back with one
+	// v_accvgpr_read per register before each use (~100 VALU per tile); pinned, the MFMAs read them in place.
+#pragma unroll
+	for (int q = 0; q < Lay::N_FWD; ++q) asm volatile("" : "+a"(wreg[q]));
+#pragma unroll
+	for (int q = 0; q < T::N_BWD; ++q) asm volatile("" : "+a"(breg[q]));
 	f32x4 dw[T::N_DW];
 #pragma unroll
 	for (int q = 0; q < T::N_DW; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
