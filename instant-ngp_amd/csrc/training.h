@@ -44,12 +44,28 @@ struct BvhNode {                  // TriangleBvhNode (triangle_bvh.cuh:28-32)
 	float lo[3], hi[3];               // bounding box
 	int32_t left, right;              // children [left, right) or, negative, leaf triangles [-left-1, -right-1)
 };
+// The four children of a BVH node as the signed-distance kernels read them: boxes as fp16 rounded
+// outward (lo down, hi up: every box contains its float box, so pruning tests stay conservative) and
+// the traversal entry of each child (bvh.hip node_entry). 64 B per node instead of 4 x 32 B.
+struct BvhChildBlock {
+	_Float16 lo[4][3], hi[4][3];
+	int32_t entry[4];
+};
+static_assert(sizeof(BvhChildBlock) == 64, "child block: one 64-B read");
+// child blocks of build_bvh4's nodes: block j holds nodes 1 + 4j .. 4 + 4j
+void bvh_child_blocks(const std::vector<BvhNode>& nodes, std::vector<BvhChildBlock>& blocks);
 struct SdfMeshDev {
 	uint32_t n_triangles;
 	const float* tris;                // [n x 9] vertices a, b, c, in BVH order
 	const float* cdf;                 // [n] inclusive area CDF normalised to 1 (triangle_cdf)
 	const BvhNode* nodes;             // 4-ary BVH (bvh.hip)
 	uint32_t depth;                   // internal nodes on the longest root-to-leaf path (bvh_depth)
+	// the query tree the signed-distance kernels traverse: build_bvh4 with 4 triangles per leaf over its
+	// own copy of the triangles (closest triangle and stab-ray hits do not depend on the tree)
+	const BvhNode* qnodes;
+	const float* qtris;
+	uint32_t qdepth;
+	const BvhChildBlock* blocks;      // bvh_child_blocks(qnodes)
 };
 // internal levels of a build_bvh4 tree (sizes the traversal stacks)
 uint32_t bvh_depth(const std::vector<BvhNode>& nodes);

@@ -51,14 +51,21 @@ struct ngp_sdf_mesh {
 	BvhNode* nodes = nullptr;
 	uint32_t n_nodes = 0;
 	uint32_t depth = 0;
+	BvhNode* qnodes = nullptr;  // query tree (4 triangles per leaf) over qtris, and its child blocks
+	float* qtris = nullptr;
+	uint32_t qdepth = 0;
+	BvhChildBlock* blocks = nullptr;
 	std::vector<float> tris_host;
 	Buf perturbations;
 	~ngp_sdf_mesh() {
 		if (tris) (void)hipFree(tris);
 		if (cdf) (void)hipFree(cdf);
 		if (nodes) (void)hipFree(nodes);
+		if (blocks) (void)hipFree(blocks);
+		if (qnodes) (void)hipFree(qnodes);
+		if (qtris) (void)hipFree(qtris);
 	}
-	SdfMeshDev dev() const { return SdfMeshDev{n_triangles, tris, cdf, nodes, depth}; }
+	SdfMeshDev dev() const { return SdfMeshDev{n_triangles, tris, cdf, nodes, depth, qnodes, qtris, qdepth, blocks}; }
 };
 
 #define TRY(...)                                   \
@@ -159,6 +166,24 @@ int ngp_sdf_mesh_create(uint32_t n_triangles, const float* tris_host, ngp_sdf_me
 		tris_host = m->tris_host.data();
 		m->n_nodes = (uint32_t)nodes.size();
 		m->depth = bvh_depth(nodes);
+		{
+			// the query tree: the same median-split build with 4 triangles per leaf over a copy of the
+			// triangles (the reference's 8-triangle tree above keeps ordering them for surface sampling).
+			// Signed distances do not depend on the tree; on the armadillo batch this one is 19 % faster
+			// (ground truth 6.2 -> 5.0 ms, profiles/r03q_sdf_gt_leaf{8,4}.json)
+			std::vector<float> q(m->tris_host);
+			std::vector<BvhNode> qn;
+			build_bvh4(q.data(), n_triangles, 4, qn);
+			m->qdepth = bvh_depth(qn);
+			std::vector<BvhChildBlock> cb;
+			bvh_child_blocks(qn, cb);
+			NGP_HIP(hipMalloc(&m->qnodes, qn.size() * sizeof(BvhNode)));
+			NGP_HIP(hipMemcpy(m->qnodes, qn.data(), qn.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
+			NGP_HIP(hipMalloc(&m->qtris, q.size() * sizeof(float)));
+			NGP_HIP(hipMemcpy(m->qtris, q.data(), q.size() * sizeof(float), hipMemcpyHostToDevice));
+			NGP_HIP(hipMalloc(&m->blocks, cb.size() * sizeof(BvhChildBlock)));
+			NGP_HIP(hipMemcpy(m->blocks, cb.data(), cb.size() * sizeof(BvhChildBlock), hipMemcpyHostToDevice));
+		}
 		NGP_HIP(hipMalloc(&m->nodes, nodes.size() * sizeof(BvhNode)));
 		NGP_HIP(hipMemcpy(m->nodes, nodes.data(), nodes.size() * sizeof(BvhNode), hipMemcpyHostToDevice));
 		// triangle_distribution.build(surface areas) (testbed_sdf.cu:1167-1172, discrete_distribution.h:20-36)
