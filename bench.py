@@ -104,6 +104,10 @@ REGION_PHASES = {"grid_backward_total": ["grid_bwd_prepare", "grid_backward_sort
 # (22 B) + write w32 m1 m2 steps w16 ema32 ema16 (24 B) = 46 B; lazily skipped grid entry (zero
 # gradient) = read g16 w32 ema32 (10 B) + write ema32 ema16 (6 B) = 16 B
 OPT_B_UPDATED, OPT_B_SKIPPED = 46, 16
+# the grid's lazy-layout update fused into the bucketed backward (engine option fuse_opt, C5): per updated
+# parameter w32 read + write (8 B), w16 write (2 B) and its half of a 48-B AdamRec read and written (48 B);
+# skipped parameters are not touched, and no gradient is stored or re-read
+OPT_B_FUSED = 58
 
 
 def newest_profile(suffix):
@@ -306,19 +310,25 @@ def slab_reduction_bytes(lib, net):
     return int(nb.value) + 2 * int(net.n_matrix_params)
 
 
-def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped, slab_bytes=0):
+def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped, slab_bytes=0, fused_grid_updated=None):
     """Per-region achieved rate and fraction of peak; returns (summary dict, dominant region).
     slab_bytes: the fused dW slab reduction's bytes, counted in the grid_backward_total region (its
-    kernel runs them as extra blocks)."""
+    kernel runs them as extra blocks). fused_grid_updated: grid parameters updated by the optimizer fused
+    into the backward (profiler phase grid_backward_adam); their OPT_B_FUSED bytes join that region and
+    the optimizer region covers the MLP alone (n_opt_* are then the MLP's counts)."""
     a = ALGO[variant]
     per = {k: v["ms"] / max(v["calls"], 1) for k, v in kernels.items()}
     for region, phases in REGION_PHASES.items():
         if all(p in per for p in phases):
             per[region] = sum(per[p] for p in phases)
+    fused_b = 0
+    if "grid_backward_adam" in per and "grid_bwd_prepare" in per:
+        per["grid_backward_total"] = per["grid_bwd_prepare"] + per["grid_backward_adam"]
+        fused_b = OPT_B_FUSED * (fused_grid_updated or 0)
     roof = {
         "grid_forward": ("hbm", a["enc_fwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
         "grid_backward": ("hbm", a["enc_bwd_B"] * n / 1e9, HBM_PEAK_GBS, "GB/s"),
-        "grid_backward_total": ("hbm", (a["enc_bwd_B"] * n + slab_bytes) / 1e9, HBM_PEAK_GBS, "GB/s"),
+        "grid_backward_total": ("hbm", (a["enc_bwd_B"] * n + slab_bytes + fused_b) / 1e9, HBM_PEAK_GBS, "GB/s"),
         "mlp_train": ("mfma", a["mlp_train_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
         "mlp_infer": ("mfma", a["mlp_fwd_flop"] * n / 1e12, MFMA_F16_PEAK_TFLOPS, "TFLOP/s"),
     }
@@ -364,8 +374,11 @@ def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped, slab_bytes=0):
                           "+ WRITE_SIZE)",
           "traffic_source": src,
           "algorithmic": round(work * (1e3 if unit == "GB/s" else 1e6), 2),
-          "algorithmic_includes": ("the fused MLP dW slab reduction: %.2f MB" % (slab_bytes / 1e6)
-                                   if dom == "grid_backward_total" and slab_bytes else None),
+          "algorithmic_includes": ("; ".join(x for x in (
+              ("the fused MLP dW slab reduction: %.2f MB" % (slab_bytes / 1e6)) if slab_bytes else "",
+              ("the grid's optimizer update fused into the backward: %.2f MB (%d B per updated parameter)"
+               % (fused_b / 1e6, OPT_B_FUSED)) if fused_b else "") if x)
+                                   if dom == "grid_backward_total" and (slab_bytes or fused_b) else None),
           "algorithmic_unit": "MB/launch" if unit == "GB/s" else "MFLOP/launch"}
     return summary, rl
 
@@ -400,13 +413,22 @@ def c5_pass(pkg, n, rank, mesh_path=None, online=False):
     return step, net, trainer
 
 
-def optimizer_counts(net, trainer, step):
-    """Parameters the optimizer updates vs lazily skips (grid entries with a zero gradient) in one step."""
+def optimizer_counts(net, trainer, step, fused=False):
+    """Parameters the optimizer updates vs lazily skips (grid entries with a zero gradient) in one step.
+    fused: the step is Trainer::training_step, whose grid update runs inside the backward without storing
+    the gradient (engine option fuse_opt); the counts come from one step with it off. Returns
+    (updated, skipped) for the optimizer launch and the number of grid parameters the fused update
+    touches (None when not fused)."""
+    if fused:
+        net.set_option("fuse_opt", 0)
     step()
     torch.cuda.synchronize()
     nm = net.n_matrix_params
     nz = int(torch.count_nonzero(trainer.gradients[nm:]).item())
-    return nm + nz, net.n_params - nm - nz
+    if fused:
+        net.set_option("fuse_opt", 1)
+        return nm, 0, nz
+    return nm + nz, net.n_params - nm - nz, None
 
 
 def free_port():
@@ -462,6 +484,9 @@ def main():
     ap.add_argument("--wire", default="f32", choices=["f32", "f16"],
                     help="gradient all-reduce wire type (f32: fp16 sums widened, rounded once)")
     ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling sub-record")
+    ap.add_argument("--no-opt-count", action="store_true",
+                    help="skip the untimed step that counts updated parameters (PMC passes: at C5 that step runs "
+                         "unfused and would mix into the per-dispatch counter averages)")
     args = ap.parse_args()
 
     need_launch, _ = check_world(args.gpus)
@@ -478,17 +503,19 @@ def main():
 
     n = args.batch if args.scaling == "weak" else args.batch // world
     n_opt = (None, None)
+    c5_fused = None
     if args.variant in ("C2", "C2p"):
         step, capture, net, trainer, comm = nerf_pass(pkg, args.variant, n, rank, world, args.opt, args.overlap,
                                                       args.wire)
-        n_opt = optimizer_counts(net, trainer, step)
+        n_opt = optimizer_counts(net, trainer, step)[:2]
         if not args.graph:
             capture = None
     elif args.variant == "C5":
         if world > 1:
             raise SystemExit("C5 bench is single-GPU")
         step, net, trainer = c5_pass(pkg, n, rank)
-        n_opt = optimizer_counts(net, trainer, step)
+        if not args.no_opt_count:
+            *n_opt, c5_fused = optimizer_counts(net, trainer, step, fused=True)
         capture = None
     else:  # IMG
         if world > 1:
@@ -537,7 +564,7 @@ def main():
         e2e_dp = psnr30.run(pkg, seconds=args.e2e_seconds, rank=rank, world=world)
 
     if rank == 0:
-        kern_summary, rl = roofline(args.variant, n, kernels, *n_opt, slab_bytes=slab_b)
+        kern_summary, rl = roofline(args.variant, n, kernels, *n_opt, slab_bytes=slab_b, fused_grid_updated=c5_fused)
         res = {
             "metric": "training samples/sec + PSNR@30s, NeRF Lego at 1/2/4/8 MI355X",
             "value": n * world * args.steps / dt,
@@ -559,7 +586,8 @@ def main():
             "kernel_timing": ("HIP events per kernel on the launch stream, eager replay of the same K steps queued "
                               "behind a graph launch" if launch == "hip_graph" else "HIP events per kernel over the timed region"),
             "roofline": rl,
-            "optimizer_params": {"updated": n_opt[0], "skipped": n_opt[1]},
+            "optimizer_params": ({"updated": n_opt[0], "skipped": n_opt[1]} if c5_fused is None else
+                                 {"mlp_updated": n_opt[0], "grid_updated_in_backward": c5_fused}),
             "kernels": kern_summary,
         }
         if world > 1:
@@ -575,7 +603,7 @@ def main():
             if not args.no_c2p:
                 # BASELINE's literal "L=16": the same training pass at C2' (L=16 F=2 T=2^19)
                 s2, c2, net2, tr2, _ = nerf_pass(pkg, "C2p", n, 0, 1)
-                o2 = optimizer_counts(net2, tr2, s2)
+                o2 = optimizer_counts(net2, tr2, s2)[:2]
                 dt2, launch2, k2 = timed_steps(lib, s2, args.steps, args.warmup, 1, c2)
                 ks2, rl2 = roofline("C2p", n, k2, *o2, slab_bytes=slab_reduction_bytes(lib, net2))
                 res["c2p"] = {"workload": WORKLOADS["C2p"], "value": n * args.steps / dt2, "unit": "samples/s",
@@ -584,12 +612,12 @@ def main():
             if not args.no_c5:
                 # BASELINE configs[4]: the HBM-bound SDF step (T=2^22, 105 M parameters), same batch size
                 s5, net5, tr5 = c5_pass(pkg, n, 0)
-                o5 = optimizer_counts(net5, tr5, s5)
+                *o5, f5 = optimizer_counts(net5, tr5, s5, fused=True)
                 dt5, launch5, k5 = timed_steps(lib, s5, args.steps, args.warmup, 1, None)
-                ks5, rl5 = roofline("C5", n, k5, *o5, slab_bytes=slab_reduction_bytes(lib, net5))
+                ks5, rl5 = roofline("C5", n, k5, *o5, slab_bytes=slab_reduction_bytes(lib, net5), fused_grid_updated=f5)
                 res["c5"] = {"workload": WORKLOADS["C5"], "value": n * args.steps / dt5, "unit": "samples/s",
                              "ms_per_step": dt5 / args.steps * 1e3, "launch": launch5, "roofline": rl5, "kernels": ks5,
-                             "optimizer_params": {"updated": o5[0], "skipped": o5[1]}}
+                             "optimizer_params": {"mlp_updated": o5[0], "grid_updated_in_backward": f5}}
                 del s5, net5, tr5
                 torch.cuda.empty_cache()
             if not args.no_c5 and args.c5_online_steps > 0 and os.path.isfile(ARMADILLO):

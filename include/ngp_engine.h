@@ -206,7 +206,9 @@ int ngp_loss_evaluate(int loss_type, void* stream, uint32_t n, uint32_t dims, co
                       float* values, float* loss_sum);
 /* tcnn::Trainer::training_step(stream, input, target, data_pdf = nullptr, run_optimizer)
  * (src/testbed_image.cu:276, src/testbed_sdf.cu:1304): forward, loss over the model's output_width
- * columns, backward into the gradient buffer (overwrite) and, if run_optimizer, optimizer_step. */
+ * columns, backward into the gradient buffer (overwrite) and, if run_optimizer, optimizer_step. With
+ * run_optimizer on the lazy-EMA layout and model option "fuse_opt" (default), the grid's update runs
+ * inside the backward (bit-identical) and the grid part of the gradient buffer is not written. */
 int ngp_trainer_training_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
                               const float* target, uint32_t target_stride, int loss_type, float loss_scale, int run_optimizer,
                               float* loss_sum);

@@ -165,6 +165,7 @@ struct ngp_model {
 	bool fused_hist = true;                 // option "fused_hist": bucket histogram inside the training forward
 	bool fuse_infer = true;                 // option "fuse_infer": NerfNetwork inference encodes inside the MLP kernel
 	bool fuse_slabs = true;                 // option "fuse_slabs": dW slab reduction inside the grid backward's last kernel
+	bool fuse_opt = true;                   // option "fuse_opt": lazy-layout optimizer update inside the grid backward (training_step)
 	bool fuse_train = false;                // option "fuse_train": ... and the training forward_backward too (off: the
 	                                        // training kernel runs 1 wave/SIMD, the gathers are not hidden; C2 0.157 -> 0.161 ms)
 	int grid_forward_mode = 0;              // option "grid_forward_mode": 0 auto, 1 per-sample rows, 2 XCD-partitioned
@@ -359,7 +360,7 @@ struct ngp_model {
 	// ex (optional): input gradients and the density-only backward (BwdExtra); grad_mode NGP_GRAD_IGNORE
 	// leaves the parameter gradients untouched (tcnn EGradientMode::Ignore, input_gradient).
 	void train_pass(hipStream_t s, uint32_t n, const float* in, uint32_t stride, const f16* encbuf, f16* out, uint32_t out_stride,
-	                const void* dL, uint32_t dL_stride, int grad_mode, const BwdExtra& ex = BwdExtra{}) {
+	                const void* dL, uint32_t dL_stride, int grad_mode, const BwdExtra& ex = BwdExtra{}, const FusedAdam* fopt = nullptr) {
 		NGP_CHECK(gradients || grad_mode == NGP_GRAD_IGNORE, "model has no gradient buffer: call ngp_model_set_params");
 		NGP_CHECK(!ex.density_only || (nerf && encbuf), "density backward: a NerfNetwork with its encoding");
 		f16* dL_denc = (f16*)denc.get((size_t)n * enc_width * sizeof(f16));
@@ -406,13 +407,13 @@ struct ngp_model {
 		}
 		if (ovl) NGP_HIP(hipEventRecord(ev_red, side));
 		GridBwdArgs b{n, in, stride, dL_denc, enc_width, AoS, gradients + grid_offset(), max_level, max_level_per_sample};
-		scatter_grid_grad(s, b, grad_mode != NGP_GRAD_ACCUMULATE, fused ? &sj : nullptr);
+		scatter_grid_grad(s, b, grad_mode != NGP_GRAD_ACCUMULATE, fused ? &sj : nullptr, fopt);
 		if (ovl) NGP_HIP(hipStreamWaitEvent(s, ev_red, 0));
 		input_gradient();
 	}
 	// Hash-grid backward: destination-bucketed exact sums (n >= 4096, or mode 3), else tcnn-style direct
 	// packed-f16 atomics (small batches, where the bucket plan costs more than the atomics).
-	void scatter_grid_grad(hipStream_t s, GridBwdArgs b, bool overwrite, const SlabJob* slab = nullptr) {
+	void scatter_grid_grad(hipStream_t s, GridBwdArgs b, bool overwrite, const SlabJob* slab = nullptr, const FusedAdam* fopt = nullptr) {
 		if (use_sorted(b.n)) {
 			void* ws = sorted_workspace(b.n);
 			if (sc_prepared) {
@@ -423,11 +424,11 @@ struct ngp_model {
 				grid_scatter_prepare(grid, b, sc_plan, ws, s, sc_hist_done);
 			}
 			sc_hist_done = false;
-			ProfScope ps("grid_backward_sorted", s);
-			grid_backward_sorted(grid, b, sc_plan, ws, s, overwrite, win_debug, slab);
+			ProfScope ps(fopt ? "grid_backward_adam" : "grid_backward_sorted", s);  // _adam: with the grid's optimizer update
+			grid_backward_sorted(grid, b, sc_plan, ws, s, overwrite, win_debug, slab, fopt);
 			return;
 		}
-		NGP_CHECK(!slab, "fused slab reduction needs the sorted grid backward");
+		NGP_CHECK(!slab && !fopt, "fused slab reduction / optimizer need the sorted grid backward");
 		if (overwrite) {
 			ProfScope ps("grid_grad_zero", s);
 			NGP_HIP(hipMemsetAsync(b.grad, 0, grid_params * sizeof(f16), s));
@@ -468,7 +469,8 @@ struct ngp_trainer {
 	~ngp_trainer() { if (arena) (void)hipFree(arena); }
 	void sync_device_step() { NGP_HIP(hipMemcpy(ctl, &step, sizeof(uint32_t), hipMemcpyHostToDevice)); }
 	// One optimizer step on stream s. step_base/step_add: see AdamState (optimizer.h).
-	void run_step(hipStream_t s, float loss_scale, const uint32_t* step_base, uint32_t step_add) {
+	// n_first: parameters [0, n_first) only (the MLP, when the grid's update ran fused in the backward)
+	void run_step(hipStream_t s, float loss_scale, const uint32_t* step_base, uint32_t step_add, uint64_t n_first = 0) {
 		ngp_model* m = model;
 		const bool own = m->params == w16;
 		// captured steps (step_base = ctl) read the hyperparameters from the ctl block, which every graph
@@ -477,8 +479,23 @@ struct ngp_trainer {
 		             own && m->frags_current ? (f16*)m->frags.p : nullptr, m->d_fragmap, step_base, step_add,
 		             step_base ? (const AdamConfig*)(ctl + CTL_CFG) : nullptr, rec};
 		ProfScope ps("optimizer", s);
-		adam_ema_update(cfg, (uint32_t)n, (uint32_t)m->n_matrix(), loss_scale, st, s);
+		adam_ema_update(cfg, (uint32_t)(n_first ? n_first : n), (uint32_t)m->n_matrix(), loss_scale, st, s);
 		if (rec) inf_stale = true;
+	}
+	// The grid's lazy update fused into the backward (model option fuse_opt): lazy layout, no gradient
+	// exchange (the all-reduce needs the stored gradients), the sorted backward, F >= 2, and an MLP
+	// section that is a whole number of 4-parameter groups (k_adam_lazy4 then runs on it alone).
+	bool fused_update_ok(uint32_t n_batch) const {
+		const ngp_model* m = model;
+		return rec && !allreduce && m->fuse_opt && m->use_sorted(n_batch) && m->grid.n_features >= 2 && m->n_matrix() % 4 == 0 &&
+		       m->grid_offset() % 2 == 0 && m->params == w16 && m->gradients == g16;
+	}
+	FusedAdam fused_update(float loss_scale) const {
+		FusedAdam fa;
+		const uint64_t go = model->grid_offset();
+		fa.w32 = w32 + go; fa.w16 = w16 + go; fa.rec = rec + go / 2;
+		fa.loss_scale = loss_scale; fa.cfg = cfg; fa.step_add = step;
+		return fa;
 	}
 };
 
@@ -682,6 +699,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			m->fuse_train = value != 0;
 		} else if (k == "fuse_slabs") {
 			m->fuse_slabs = value != 0;
+		} else if (k == "fuse_opt") {
+			m->fuse_opt = value != 0;
 		} else if (k == "win_debug") {
 			m->win_debug = (uint32_t)value;
 		} else {
@@ -1009,9 +1028,13 @@ int ngp_trainer_training_step(ngp_trainer* t, void* stream, uint32_t n, const fl
 			ProfScope ps("loss", s);
 			loss_evaluate((uint32_t)loss_type, la, s);
 		}
-		m->train_pass(s, n, input, input_stride, e, nullptr, 0, dl, W, NGP_GRAD_OVERWRITE);
+		// the grid's optimizer update runs inside the backward where possible (fused_update_ok): its
+		// gradient is then not stored, and the optimizer launch covers the MLP section alone
+		const bool fuse = run_optimizer && t->fused_update_ok(n);
+		const FusedAdam fa = fuse ? t->fused_update(loss_scale) : FusedAdam{};
+		m->train_pass(s, n, input, input_stride, e, nullptr, 0, dl, W, NGP_GRAD_OVERWRITE, BwdExtra{}, fuse ? &fa : nullptr);
 		if (run_optimizer) {
-			t->run_step(s, loss_scale, nullptr, t->step);
+			t->run_step(s, loss_scale, nullptr, t->step, fuse ? m->n_matrix() : 0);
 			t->step++;
 		}
 	});

@@ -1,6 +1,7 @@
 // grid_scatter.h — destination-bucketed hash-grid backward (see grid_scatter.hip).
 #pragma once
 #include "grid.h"
+#include "optimizer.h"
 #include "slab_reduce.h"
 
 namespace ngp {
@@ -35,7 +36,11 @@ bool scatter_hist(const GridDesc& g, const ScatterPlan& p, void* workspace, Grid
 // otherwise the sums are added to it. Same level masking as grid_backward.
 // slab (optional): the MLP's dW slab reduction, run in extra blocks of the last backward kernel
 // (same arithmetic as reduce_slabs, no launch of its own).
+// fused (optional, overwrite only): apply the lazy optimizer update to every entry with a nonzero
+// gradient instead of storing the gradient (optimizer.h FusedAdam); the grid part of b.grad is then
+// left unwritten.
 void grid_backward_sorted(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace,
-                          hipStream_t s, bool overwrite, uint32_t debug = 0, const SlabJob* slab = nullptr);
+                          hipStream_t s, bool overwrite, uint32_t debug = 0, const SlabJob* slab = nullptr,
+                          const FusedAdam* fused = nullptr);
 
 }  // namespace ngp

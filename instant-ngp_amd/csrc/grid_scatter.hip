@@ -469,7 +469,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
                                                          uint32_t max_parts, const uint16_t* __restrict__ item_idx,
                                                          const f16* __restrict__ item_val, f16* __restrict__ grad, bool overwrite,
                                                          const uint32_t* __restrict__ split, unsigned long long* __restrict__ scratch,
-                                                         uint32_t debug) {
+                                                         uint32_t debug, const FusedAdam fa) {
 	extern __shared__ unsigned long long acc[];
 	const uint32_t NE = 1u << B, NEP = NE + 1;  // feature planes padded by one entry (accumulate_items)
 	if (blockIdx.x < max_parts) {
@@ -491,8 +491,8 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 	uint32_t e0, n_e;
 	bucket_entries(c, lv, B, vb, e0, n_e);
 	f16* g = grad + (size_t)e0 * F;
-	if (t == 0) {
-		if (overwrite)
+	if (t == 0) {  // no contribution: gradient 0 (fused update: every entry of the bucket is skipped)
+		if (overwrite && !fa.rec)
 			for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) ((uint32_t*)g)[k] = 0u;
 		return;
 	}
@@ -501,11 +501,16 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 	__syncthreads();
 	if (!(debug & 1)) accumulate_items<F>(acc, NE, lo, lo + t, item_idx, item_val, debug);
 	__syncthreads();
-	// two fp16 per thread-step (n_e * F is even: levels hold multiples of 8 entries)
+	// two fp16 per thread-step (n_e * F is even: levels hold multiples of 8 entries); pair k of the
+	// bucket is parameter pair (e0 F) / 2 + k of the grid
 	for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) {
 		uint32_t ia, ib;
 		pair_slots<F>(k, NEP, ia, ib);
 		float s0 = fix_to_f32(acc[ia]), s1 = fix_to_f32(acc[ib]);
+		if (fa.rec) {  // (issuing several pairs' state loads before the first update measured slower: 1.58 -> 1.97 ms at C5)
+			fused_adam_pair(fa, e0 * F / 2 + k, (f16)s0, (f16)s1);
+			continue;
+		}
 		if (!overwrite) {
 			const f16x2 o = ((const f16x2*)g)[k];
 			s0 += (float)o[0];
@@ -523,7 +528,7 @@ template <uint32_t F>
 __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst c, const Levels lv, uint32_t B,
                                                                 const uint32_t* __restrict__ split, const uint32_t* __restrict__ splitb,
                                                                 const unsigned long long* __restrict__ scratch, f16* __restrict__ grad,
-                                                                bool overwrite, const SlabJob sj, uint32_t slab_x0) {
+                                                                bool overwrite, const SlabJob sj, uint32_t slab_x0, const FusedAdam fa) {
 	static_assert(SC_THREADS == SLAB_THREADS, "slab blocks share the split-reduce block shape");
 	if (blockIdx.x >= slab_x0) {
 		const uint32_t blk = blockIdx.y * (gridDim.x - slab_x0) + (blockIdx.x - slab_x0);
@@ -554,6 +559,10 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
 		}
 		for (; p < parts; ++p) { q0 += src[p * pstride + ia]; q1 += src[p * pstride + ib]; }
 		float s0 = fix_to_f32(q0), s1 = fix_to_f32(q1);
+		if (fa.rec) {
+			fused_adam_pair(fa, e0 * F / 2 + k, (f16)s0, (f16)s1);
+			return;
+		}
 		if (!overwrite) {
 			const f16x2 o = ((const f16x2*)g)[k];
 			s0 += (float)o[0];
@@ -583,7 +592,7 @@ Levels make_levels(const GridDesc& g, uint32_t B) {
 
 template <uint32_t D>
 void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const GridBwdArgs& a, const ScatterPlan& p, char* ws,
-                     hipStream_t s, bool overwrite, uint32_t debug, const SlabJob* slab) {
+                     hipStream_t s, bool overwrite, uint32_t debug, const SlabJob* slab, const FusedAdam& fa) {
 	const uint32_t* tot = (const uint32_t*)(ws + p.off_tot);
 	const uint32_t* cur_t = (const uint32_t*)(ws + p.off_cur);
 	const uint32_t* split = (const uint32_t*)(ws + p.off_split);
@@ -601,13 +610,13 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		NGP_HIP(hipGetLastError());
 		ensure_dynamic_lds((const void*)accum, SC_LDS_BYTES + SC_LDS_PAD_BYTES);
 		accum<<<p.max_split_blocks + p.n_buckets, SC_BT, SC_LDS_BYTES + SC_LDS_PAD_BYTES, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
-		                                                                     val, a.grad, overwrite, split, scratch, debug);
+		                                                                     val, a.grad, overwrite, split, scratch, debug, fa);
 		NGP_HIP(hipGetLastError());
 		const uint32_t gy = (uint32_t)div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS);
 		const SlabJob sj = slab ? *slab : SlabJob{};
 		const uint32_t slab_x = slab ? (uint32_t)div_round_up(slab_blocks(sj.n), gy) : 0u;
 		const dim3 grid_r(p.max_split_buckets + slab_x, gy);
-		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets);
+		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets, fa);
 		NGP_HIP(hipGetLastError());
 	};
 	auto by_chunk = [&](auto sc512, auto sc1024, auto accum, auto splitr) {
@@ -708,13 +717,15 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const Scatter
 }
 
 void grid_backward_sorted(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace, hipStream_t s,
-                          bool overwrite, uint32_t debug, const SlabJob* slab) {
+                          bool overwrite, uint32_t debug, const SlabJob* slab, const FusedAdam* fused) {
 	if (b.n == 0) return;
 	NGP_CHECK(b.level_begin == 0, "grid_backward_sorted handles all levels");
+	NGP_CHECK(!fused || (overwrite && g.n_features >= 2), "fused optimizer: overwrite mode, F >= 2");
 	const GridConst c = make_grid_const(g);
 	const Levels lv = make_levels(g, p.B);
-	if (g.n_dims == 3) launch_backward<3>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab);
-	else launch_backward<2>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab);
+	const FusedAdam fa = fused ? *fused : FusedAdam{};
+	if (g.n_dims == 3) launch_backward<3>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab, fa);
+	else launch_backward<2>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab, fa);
 }
 
 }  // namespace ngp

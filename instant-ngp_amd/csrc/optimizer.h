@@ -41,6 +41,96 @@ struct AdamState {
 	const AdamConfig* cfg_dev;  // non-null (captured steps): hyperparameters read from device memory
 	AdamRec* rec = nullptr;     // non-null: lazy-EMA layout (m1/m2/steps/ema32 unused)
 };
+// ---- device helpers shared by optimizer.hip and the fused update in the grid backward ----------
+// Learning rate of optimizer step `step` (ExponentialDecay wrapper).
+__device__ __forceinline__ float lr_schedule(const AdamConfig& c, uint32_t step) {
+	float r = c.lr;
+	if (c.decay_interval == 0 || step < c.decay_start) return r;
+	const uint32_t k = (step - c.decay_start) / c.decay_interval + 1;
+	for (uint32_t i = 0; i < k; ++i) r *= c.decay_base;
+	return r;
+}
+// The eager EMA of step j: e = d * e + (1 - d) * w (w after step j's update), output e / (1 - d^(j+1)).
+__device__ __forceinline__ float ema_catch_up(float e, float w, float d, uint32_t from, uint32_t to) {
+	for (uint32_t j = from; j < to; ++j) e = d * e + (1.f - d) * w;
+	return e;
+}
+
+// The lazy-layout update applied inside the hash-grid backward (engine option fuse_opt): the bucket
+// accumulation holds each grid entry's final fp16 gradient, so it updates that parameter pair's record
+// directly instead of storing the gradient for k_adam_lazy4 to read back (C5: 210 MB written and 210 MB
+// read per step). Pointers are offset to the grid's first parameter (an even index: records are pairs).
+// Same fp32 operations, in the same order, as k_adam_lazy4's lazy_update for a non-matrix pair.
+struct FusedAdam {
+	float* w32 = nullptr;
+	f16* w16 = nullptr;
+	AdamRec* rec = nullptr;  // null: no fused update (the backward stores the gradient)
+	float loss_scale = 1.f;
+	AdamConfig cfg;
+	const AdamConfig* cfg_dev = nullptr;
+	const uint32_t* step_base = nullptr;
+	uint32_t step_add = 0;
+};
+// One parameter pair's state between the load and the update (callers issue several pairs' loads
+// before the first update: the record reads are the latency to hide).
+struct FusedPair {
+	float g[2];
+	bool act[2];
+	f32x4 q0, q1, q2;
+	float w[2];
+};
+__device__ __forceinline__ bool fused_adam_load(const FusedAdam& fa, uint32_t r, f16 g0h, f16 g1h, FusedPair& p) {
+	p.g[0] = (float)g0h / fa.loss_scale;
+	p.g[1] = (float)g1h / fa.loss_scale;
+	p.act[0] = p.g[0] != 0.f;  // grid parameters: a zero gradient skips the parameter
+	p.act[1] = p.g[1] != 0.f;
+	if (!p.act[0] && !p.act[1]) return false;
+	typedef float f32x2 __attribute__((ext_vector_type(2)));
+	const f32x2 w = *(const f32x2*)(fa.w32 + 2 * (size_t)r);
+	p.w[0] = w[0];
+	p.w[1] = w[1];
+	const f32x4* rp = (const f32x4*)(fa.rec + r);
+	p.q0 = rp[0]; p.q1 = rp[1]; p.q2 = rp[2];
+	return true;
+}
+__device__ __forceinline__ void fused_adam_store(const FusedAdam& fa, uint32_t r, FusedPair& p) {
+	const AdamConfig c = fa.cfg_dev ? *fa.cfg_dev : fa.cfg;
+	const uint32_t step = (fa.step_base ? *fa.step_base : 0u) + fa.step_add;
+	const float lr = lr_schedule(c, step);
+	const float d = c.ema_decay;
+	float m1[2] = {p.q0[0], p.q0[1]}, m2[2] = {p.q0[2], p.q0[3]}, ema[2] = {p.q1[2], p.q1[3]};
+	uint32_t steps[2] = {__float_as_uint(p.q1[0]), __float_as_uint(p.q1[1])};
+	uint32_t done[2] = {__float_as_uint(p.q2[0]), __float_as_uint(p.q2[1])};
+	float w[2] = {p.w[0], p.w[1]};
+#pragma unroll
+	for (int k = 0; k < 2; ++k) {
+		if (!p.act[k]) continue;
+		if (d > 0.f) ema[k] = ema_catch_up(ema[k], w[k], d, done[k], step);
+		const float gk = p.g[k];
+		const float mm = c.beta1 * m1[k] + (1.f - c.beta1) * gk;
+		const float vv = c.beta2 * m2[k] + (1.f - c.beta2) * (gk * gk);
+		m1[k] = mm;
+		m2[k] = vv;
+		const uint32_t sk = steps[k] + 1;
+		steps[k] = sk;
+		const float lr_s = lr * sqrtf(1.f - powf(c.beta2, (float)sk)) / (1.f - powf(c.beta1, (float)sk));
+		w[k] = w[k] - lr_s / (sqrtf(vv) + c.eps) * mm;
+		if (d > 0.f) ema[k] = d * ema[k] + (1.f - d) * w[k];
+		done[k] = step + 1;
+	}
+	f32x4* rp = (f32x4*)(fa.rec + r);
+	rp[0] = f32x4{m1[0], m1[1], m2[0], m2[1]};
+	rp[1] = f32x4{__uint_as_float(steps[0]), __uint_as_float(steps[1]), ema[0], ema[1]};
+	rp[2] = f32x4{__uint_as_float(done[0]), __uint_as_float(done[1]), 0.f, 0.f};
+	typedef float f32x2 __attribute__((ext_vector_type(2)));
+	*(f32x2*)(fa.w32 + 2 * (size_t)r) = f32x2{w[0], w[1]};
+	*(f16x2*)(fa.w16 + 2 * (size_t)r) = f16x2{(f16)w[0], (f16)w[1]};
+}
+__device__ __forceinline__ void fused_adam_pair(const FusedAdam& fa, uint32_t r, f16 g0h, f16 g1h) {
+	FusedPair p;
+	if (fused_adam_load(fa, r, g0h, g1h, p)) fused_adam_store(fa, r, p);
+}
+
 // The trainer's device control block: ctl[0] optimizer step, ctl[1] block counter, AdamConfig at
 // ctl + CTL_CFG. A graph launch rewrites step and config (set_device_ctl), so replayed steps follow
 // set_learning_rate / set_option like eager ones.

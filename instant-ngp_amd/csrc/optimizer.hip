@@ -13,14 +13,7 @@ namespace ngp {
 
 // The optimizer step: eager launches pass it by value; a HIP graph of K captured steps reads a base
 // from device memory (written once per graph launch by k_set_step) plus the step's index in the graph,
-// so no per-step counter kernel is needed.
-__device__ __forceinline__ float lr_schedule(const AdamConfig& c, uint32_t step) {
-	float r = c.lr;
-	if (c.decay_interval == 0 || step < c.decay_start) return r;
-	const uint32_t k = (step - c.decay_start) / c.decay_interval + 1;
-	for (uint32_t i = 0; i < k; ++i) r *= c.decay_base;
-	return r;
-}
+// so no per-step counter kernel is needed. lr_schedule, ema_catch_up: optimizer.h.
 
 __global__ void k_adam_ema(const uint32_t i0, const uint32_t n, const uint32_t n_matrix, const float loss_scale, const AdamConfig c_arg,
                            const AdamState st) {
@@ -133,11 +126,6 @@ __global__ void __launch_bounds__(256) k_adam_ema4(const uint32_t n4, const uint
 }
 
 // ---- lazy-EMA layout ------------------------------------------------------------------------
-// The eager EMA of step j: e = d * e + (1 - d) * w (w after step j's update), output e / (1 - d^(j+1)).
-__device__ __forceinline__ float ema_catch_up(float e, float w, float d, uint32_t from, uint32_t to) {
-	for (uint32_t j = from; j < to; ++j) e = d * e + (1.f - d) * w;
-	return e;
-}
 
 // Four parameters (two records) per group; a record none of whose parameters is updated this step is
 // neither read nor written (grid entries without gradient: the bulk of a large table). A thread owns

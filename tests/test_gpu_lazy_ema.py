@@ -145,3 +145,36 @@ def test_lazy_ema_set_params_full_precision_bitwise(pkg):
     assert runs[True][0] == runs[False][0], "serialize right after set_params_full_precision differs"
     assert runs[True][1] == runs[False][1], "training after set_params_full_precision differs"
     np.testing.assert_array_equal(runs[True][2], runs[False][2])
+
+
+def test_fused_optimizer_training_step_bitwise(pkg):
+    """Trainer::training_step with the optimizer (train_sdf's call, testbed_sdf.cu:1304) on the lazy
+    layout runs the grid's update inside the bucketed backward (model option fuse_opt, default on): it
+    must train bit for bit like the separate k_adam_lazy4 launch and like the eager layout, with steps
+    whose batches leave most entries untouched and steps whose coarse buckets split into parts."""
+    runs = {}
+    for name, lazy, fuse in (("eager", False, 0), ("lazy", True, 0), ("fused", True, 1)):
+        net, tr = make_trainer(pkg, "sdf", lazy)
+        net.set_option("fuse_opt", fuse)
+        snaps = []
+        for step in range(20):
+            n = 4096 if step % 3 else 1 << 16
+            x, _ = batch("sdf", n, step)
+            tgt = torch.from_numpy(np.random.default_rng(500 + step).uniform(-0.1, 0.1, (n, 1)).astype(np.float32)).cuda()
+            tr.training_step(x, tgt, "MAPE", run_optimizer=True)
+            if step == 9:
+                torch.cuda.synchronize()
+                snaps.append(tr.inference_params.cpu().numpy().view(np.uint16).copy())
+        torch.cuda.synchronize()
+        snaps.append(tr.inference_params.cpu().numpy().view(np.uint16).copy())
+        runs[name] = (tr.params_full_precision.cpu().numpy().view(np.uint32).copy(),
+                      tr.params.cpu().numpy().view(np.uint16).copy(), snaps, tr.serialize(), tr.step)
+        del net, tr
+    for name in ("lazy", "fused"):
+        w, p, s, b, st = runs[name]
+        np.testing.assert_array_equal(w, runs["eager"][0])
+        np.testing.assert_array_equal(p, runs["eager"][1])
+        for a, e in zip(s, runs["eager"][2]):
+            np.testing.assert_array_equal(a, e)
+        assert b == runs["eager"][3], f"{name}: serialized optimizer state differs"
+        assert st == runs["eager"][4] == 20

@@ -34,7 +34,7 @@ if has pmc; then
   # separate passes (TCC slots): sized read requests, WRITE_SIZE, MFMA utilisation; eager launches; one
   # summary per variant (PMC_VARIANTS, default C2 C2p C5) -> $OUT/pmc_summary_<variant>.json
   for V in ${PMC_VARIANTS:-C2 C2p C5}; do
-    BENCH_PMC="python3 bench.py --variant $V --no-cpu-baseline --e2e-seconds 0 --c3-seconds 0 --no-c2p --no-c5 --graph 0 --steps 5 --warmup 2 ${PMC_ARGS}"
+    BENCH_PMC="python3 bench.py --variant $V --no-cpu-baseline --e2e-seconds 0 --c3-seconds 0 --no-c2p --no-c5 --graph 0 --steps 5 --warmup 2 --no-opt-count ${PMC_ARGS}"
     i=0
     for c in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" "WRITE_SIZE" \
              "MfmaUtil SQ_INSTS_VALU_MFMA_MOPS_F16"; do
