@@ -391,6 +391,9 @@ __device__ float sampling_end_row(V3 o, V3 d, V3 idir, float t_start, const Cone
 #define NGP_SAMPLER_RG 8
 #endif
 constexpr uint32_t RG = NGP_SAMPLER_RG;  // lanes per ray (16 = one DPP row)
+#ifndef NGP_SAMPLER_EMPTY_SPEC
+#define NGP_SAMPLER_EMPTY_SPEC 1  // cone stepping: one guess-and-verify loop for both modes (0: occupied guess-and-verify, empty chain in every lane)
+#endif
 
 constexpr uint32_t LG = 16;  // lanes per ray in the loss passes: one DPP row
 static_assert(RG >= 4 && RG <= 16 && (RG & (RG - 1)) == 0, "sampler group: 4, 8 or 16 lanes");
@@ -446,25 +449,32 @@ struct Marcher {
 		uint32_t mip;
 		if (CONE0) {
 			mip = mip_at(0.0f, p);
-		} else {
-			const float n1 = n + 1.0f;
-			float dt;
-			if (n1 > cone.a && n1 <= cone.b) {
-				// from_stepping_space(n1) = ngp_expf(n1 * log1p_c); __expf: v_exp_f32 (~2 ulp) of
-				// the same argument, so dt * 2 GRIDSIZE is off by <= ~3e-7 * t / dt ~ 3e-7 * rl relative
-				// (~8e-5 at cone 1/256). Margin: 13x that, relative to the boundary (mantissa 0.5 = powers of two)
-				dt = __expf(n1 * cone.log1p_c) - t;
-				int e;
-				const float mant = frexpf(dt * (2 * GRIDSIZE), &e);
-				const float mm = 3.9e-6f * cone.rl;  // 1e-3 at cone 1/256
-				if (mant < 0.5f + 0.5f * mm || mant > 1.0f - mm) dt = from_stepping_space(n1, cone) - t;
-			} else {
-				dt = from_stepping_space(n1, cone) - t;
-			}
-			mip = mip_at(dt, p);
+			if (mip_out) *mip_out = mip;
+			return advance_to_next_voxel_n(t, n, k(), p, dn, idir, mip);
 		}
+		const float c = empty_steps(t, n, p, &mip);
 		if (mip_out) *mip_out = mip;
-		if (CONE0) return advance_to_next_voxel_n(t, n, k(), p, dn, idir, mip);
+		return from_stepping_space(n + c, cone);
+	}
+	// Cone stepping: the number of stepping-space steps advance_to_next_voxel takes from t (n = to(t),
+	// p = pos(t)), ceil(max(to(target) - n, 0.5)), and t's mip.
+	__device__ __forceinline__ float empty_steps(float t, float n, V3 p, uint32_t* mip_out) const {
+		const float n1 = n + 1.0f;
+		float dt;
+		if (n1 > cone.a && n1 <= cone.b) {
+			// from_stepping_space(n1) = ngp_expf(n1 * log1p_c); __expf: v_exp_f32 (~2 ulp) of
+			// the same argument, so dt * 2 GRIDSIZE is off by <= ~3e-7 * t / dt ~ 3e-7 * rl relative
+			// (~8e-5 at cone 1/256). Margin: 13x that, relative to the boundary (mantissa 0.5 = powers of two)
+			dt = __expf(n1 * cone.log1p_c) - t;
+			int e;
+			const float mant = frexpf(dt * (2 * GRIDSIZE), &e);
+			const float mm = 3.9e-6f * cone.rl;  // 1e-3 at cone 1/256
+			if (mant < 0.5f + 0.5f * mm || mant > 1.0f - mm) dt = from_stepping_space(n1, cone) - t;
+		} else {
+			dt = from_stepping_space(n1, cone) - t;
+		}
+		const uint32_t mip = mip_at(dt, p);
+		*mip_out = mip;
 		const float res = scalbnf((float)GRIDSIZE, -(int)mip);
 		const float target = t + distance_to_next_voxel(p, dn, idir, res);
 		float x;
@@ -477,7 +487,64 @@ struct Marcher {
 		} else {
 			x = to_stepping_space(target, cone) - n;
 		}
-		return from_stepping_space(n + ceilf(fmaxf(x, 0.5f)), cone);
+		return ceilf(fmaxf(x, 0.5f));
+	}
+	// Cone stepping, either mode: the state after t and t's mip. occ: t + calc_dt(t) (calc_dt = from(n + 1)
+	// - t); empty: advance_to_next_voxel = from(n + empty_steps). One to() and one from() either way, so
+	// a wave whose rays are in different modes evaluates the two software transcendentals once.
+	__device__ __forceinline__ float step_any(float t, bool occ, uint32_t* mip_out) const {
+		const V3 p = pos(t);
+		const float n = to_stepping_space(t, cone);
+		uint32_t mip = 0;
+		float c = 1.0f;
+		if (!occ) c = empty_steps(t, n, p, &mip);
+		const float e = from_stepping_space(n + c, cone);
+		if (!occ) {
+			*mip_out = mip;
+			return e;
+		}
+		const float dt = e - t;
+		*mip_out = mip_at(dt, p);
+		return t + dt;
+	}
+	// Guesses only (the speculative empty-space march verifies every state they lead to): the
+	// stepping-space conversions with hardware exp/log in the exponential segment.
+	__device__ __forceinline__ float to_fast(float t) const {
+		if (t <= cone.at) return div_min_stepsize(t - cone.at) + cone.a;
+		if (t <= cone.bt) return __logf(t) * cone.rl;
+		return div_max_stepsize(t - cone.bt) + cone.b;
+	}
+	__device__ __forceinline__ float from_fast(float n) const {
+		if (n <= cone.a) return (n - cone.a) * MIN_CONE_STEPSIZE + cone.at;
+		if (n <= cone.b) return __expf(n * cone.log1p_c);
+		return (n - cone.b) * MAX_CONE_STEPSIZE + cone.bt;
+	}
+	// Guess of the state j >= 1 empty-space steps after the exact state (tb, nb = to(tb)), assuming each
+	// step crosses one voxel boundary at tb's mip: b_j, the j-th boundary crossing of the ray's DDA from
+	// pos(tb), then state j = from(nb + ceil(to(b_j) - nb)); returns that ceil (advance_to_next_voxel from inside the cell
+	// before b_j lands on the first lattice point past it; nb plus an integer is exact). No dependency
+	// between the lanes' guesses; wrong ones (a mip change, two crossings in one step, a tie at a cell
+	// corner) only cost a verify round.
+	__device__ __forceinline__ float guess_empty_steps(float tb, float nb, uint32_t j) const {
+		const V3 p = pos(tb);
+		const float res = scalbnf((float)GRIDSIZE, -(int)mip_at(from_fast(nb + 1.0f) - tb, p));
+		const float qx = res * (p.x - 0.5f), qy = res * (p.y - 0.5f), qz = res * (p.z - 0.5f);
+		float sx = (floorf(qx + 0.5f + 0.5f * signf_(dn.x)) - qx) * idir.x;
+		float sy = (floorf(qy + 0.5f + 0.5f * signf_(dn.y)) - qy) * idir.y;
+		float sz = (floorf(qz + 0.5f + 0.5f * signf_(dn.z)) - qz) * idir.z;
+		const float ax = fabsf(idir.x), ay = fabsf(idir.y), az = fabsf(idir.z);
+		float s = 0.0f;
+#pragma unroll
+		for (uint32_t k = 0; k + 1 < RG; ++k) {
+			if (k < j) {
+				s = fminf(fminf(sx, sy), sz);
+				if (sx == s) sx += ax;
+				else if (sy == s) sy += ay;
+				else sz += az;
+			}
+		}
+		const float b = tb + fmaxf(s, 0.0f) * (1.0f / res);
+		return ceilf(fmaxf(to_fast(b) - nb, 0.5f));
 	}
 };
 
@@ -523,14 +590,44 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 #endif
 		float* tout = tbuf + (size_t)i * STEPS;
 		bool occ_mode = false;  // rays enter the aabb in empty space far more often than not
-		SAMPLER_STAT(uint32_t st_e = 0; uint32_t st_o = 0; uint32_t st_r = 0; uint32_t st_x = 0;)
+		SAMPLER_STAT(uint32_t st_e = 0; uint32_t st_o = 0; uint32_t st_r = 0; uint32_t st_x = 0; uint32_t st_q = 0;)
 		for (;;) {
 			SAMPLER_STAT(if (occ_mode) ++st_o; else ++st_e;)
 			// lanes [0, nvalid) take the next nvalid states of the sequential march, assuming it stays in
 			// the current mode (all occupied / all empty)
 			float tl, last;  // last: the state after lane RG-1's (the march continues there if every lane stays in the mode)
 			uint32_t mipl;   // the mip lane L's state is tested at
-			if (occ_mode) {
+			if (!CONE0 && NGP_SAMPLER_EMPTY_SPEC) {
+				// Cone stepping, both modes in one guess-and-verify loop. Every state is from(n + c) with n =
+				// to(previous state): c = 1 in an occupied run (t + calc_dt(t)), c = the ceil of
+				// advance_to_next_voxel in an empty one. Lane L guesses state L as from(to(t) + C_L): C_L = L
+				// when occupied (to(from(n)) == n nearly always), the voxel DDA's estimate when empty
+				// (guess_empty_steps). All lanes verify at once: lane L redoes the exact step from lane L-1's
+				// guess. The verified prefix is exact; the first lane that fails takes the exact state from its
+				// predecessor and the lanes after it are re-guessed from there. The rays of a wave sit in
+				// different modes most of the time; sharing the loop (and its exact to()/from() per lane and
+				// round) means the wave no longer runs one mode's loop after the other's.
+				const float n0 = to_stepping_space(t, m.cone);
+				const float c0 = occ_mode ? (float)L : m.guess_empty_steps(t, n0, L);
+				float cand = L == 0 ? t : from_stepping_space(n0 + c0, m.cone);
+				uint32_t v0 = 1, mk = 0;
+				float nxt;
+				for (;;) {
+					SAMPLER_STAT(if (occ_mode) ++st_r; else ++st_q;)
+					nxt = m.step_any(cand, occ_mode, &mk);
+					const float expct = dpp_shr1(nxt);
+					const uint32_t v = __builtin_ctz(row_ballot(L >= v0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
+					if (v >= RG) break;
+					const float tv = __shfl(expct, (int)v, (int)RG);
+					const float nv = to_stepping_space(tv, m.cone);
+					const float cv = occ_mode ? (float)(L - v) : m.guess_empty_steps(tv, nv, L - v);
+					cand = L < v ? cand : (L == v ? tv : from_stepping_space(nv + cv, m.cone));
+					v0 = v + 1;
+				}
+				tl = cand;
+				mipl = mk;
+				last = __shfl(nxt, (int)(RG - 1), (int)RG);
+			} else if (occ_mode) {
 				// Occupied run: t_{k+1} = t_k + calc_dt(t_k) = from(to(t_k) + 1) in stepping space, and
 				// to(from(n)) == n nearly always. Guess state L as from(to(t) + L) and verify every guess at
 				// once (lane L redoes the exact step from lane L-1's state): the verified prefix is exact; the
@@ -599,6 +696,7 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			atomicAdd(&g_sampler_stats[4], (unsigned long long)j);
 			atomicMax(&g_sampler_stats[5], (unsigned long long)(st_e + st_o));
 			atomicAdd(&g_sampler_stats[6], (unsigned long long)st_x);
+			atomicAdd(&g_sampler_stats[7], (unsigned long long)st_q);
 			atomicAdd(&g_sampler_stats[8 + (31 - __builtin_clz(st_e + st_o))], 1ull);
 		})
 	}

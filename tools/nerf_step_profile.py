@@ -82,6 +82,7 @@ def main():
         stats = {"rays": raw[3], "empty_iters_per_ray": raw[0] / n, "occ_iters_per_ray": raw[1] / n,
                  "occ_rounds_per_occ_iter": raw[2] / max(raw[1], 1), "occ_states_per_ray": raw[4] / n,
                  "max_iters_one_ray": raw[5], "empty_exits_per_ray": raw[6] / n,
+                 "empty_rounds_per_empty_iter": raw[7] / max(raw[0], 1),
                  "iters_log2_hist": {f"{1 << b}": raw[8 + b] for b in range(32) if raw[8 + b]}}
     phases = {n: {"calls": v["calls"], "ms_per_call": round(v["ms"] / max(v["calls"], 1), 4),
                   "ms_per_step": round(v["ms"] / args.measure, 4)} for n, v in sorted(k.items())}
