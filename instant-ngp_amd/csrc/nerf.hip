@@ -394,6 +394,9 @@ constexpr uint32_t RG = NGP_SAMPLER_RG;  // lanes per ray (16 = one DPP row)
 #ifndef NGP_SAMPLER_EMPTY_SPEC
 #define NGP_SAMPLER_EMPTY_SPEC 1  // cone stepping: one guess-and-verify loop for both modes (0: occupied guess-and-verify, empty chain in every lane)
 #endif
+#ifndef NGP_SAMPLER_UNIFIED0
+#define NGP_SAMPLER_UNIFIED0 0  // the same for cone 0 (measured neutral on the Lego stand-in, r03ab: off)
+#endif
 
 constexpr uint32_t LG = 16;  // lanes per ray in the loss passes: one DPP row
 static_assert(RG >= 4 && RG <= 16 && (RG & (RG - 1)) == 0, "sampler group: 4, 8 or 16 lanes");
@@ -489,23 +492,28 @@ struct Marcher {
 		}
 		return ceilf(fmaxf(x, 0.5f));
 	}
-	// Cone stepping, either mode: the state after t and t's mip. occ: t + calc_dt(t) (calc_dt = from(n + 1)
+	// Either mode: the state after t and t's mip. occ: t + calc_dt(t) (calc_dt = from(n + 1)
 	// - t); empty: advance_to_next_voxel = from(n + empty_steps). One to() and one from() either way, so
 	// a wave whose rays are in different modes evaluates the two software transcendentals once.
 	__device__ __forceinline__ float step_any(float t, bool occ, uint32_t* mip_out) const {
 		const V3 p = pos(t);
-		const float n = to_stepping_space(t, cone);
-		uint32_t mip = 0;
+		const float n = to_stepping_space(t, k());
+		uint32_t mip = CONE0 ? mip_at(0.0f, p) : 0u;
 		float c = 1.0f;
-		if (!occ) c = empty_steps(t, n, p, &mip);
-		const float e = from_stepping_space(n + c, cone);
+		if (!occ) c = CONE0 ? empty_steps0(t, n, p, mip) : empty_steps(t, n, p, &mip);
+		const float e = from_stepping_space(n + c, k());
 		if (!occ) {
 			*mip_out = mip;
 			return e;
 		}
 		const float dt = e - t;
-		*mip_out = mip_at(dt, p);
+		*mip_out = CONE0 ? mip : mip_at(dt, p);
 		return t + dt;
+	}
+	// cone 0: the steps of advance_to_next_voxel_n (mip: mip_at(0, p))
+	__device__ __forceinline__ float empty_steps0(float t, float n, V3 p, uint32_t mip) const {
+		const float target = t + distance_to_next_voxel(p, dn, idir, scalbnf((float)GRIDSIZE, -(int)mip));
+		return ceilf(fmaxf(to_stepping_space(target, Cone{}) - n, 0.5f));
 	}
 	// Guesses only (the speculative empty-space march verifies every state they lead to): the
 	// stepping-space conversions with hardware exp/log in the exponential segment.
@@ -527,7 +535,7 @@ struct Marcher {
 	// corner) only cost a verify round.
 	__device__ __forceinline__ float guess_empty_steps(float tb, float nb, uint32_t j) const {
 		const V3 p = pos(tb);
-		const float res = scalbnf((float)GRIDSIZE, -(int)mip_at(from_fast(nb + 1.0f) - tb, p));
+		const float res = scalbnf((float)GRIDSIZE, -(int)mip_at(CONE0 ? 0.0f : from_fast(nb + 1.0f) - tb, p));
 		const float qx = res * (p.x - 0.5f), qy = res * (p.y - 0.5f), qz = res * (p.z - 0.5f);
 		float sx = (floorf(qx + 0.5f + 0.5f * signf_(dn.x)) - qx) * idir.x;
 		float sy = (floorf(qy + 0.5f + 0.5f * signf_(dn.y)) - qy) * idir.y;
@@ -544,7 +552,7 @@ struct Marcher {
 			}
 		}
 		const float b = tb + fmaxf(s, 0.0f) * (1.0f / res);
-		return ceilf(fmaxf(to_fast(b) - nb, 0.5f));
+		return ceilf(fmaxf((CONE0 ? to_stepping_space(b, Cone{}) : to_fast(b)) - nb, 0.5f));
 	}
 };
 
@@ -597,8 +605,8 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			// the current mode (all occupied / all empty)
 			float tl, last;  // last: the state after lane RG-1's (the march continues there if every lane stays in the mode)
 			uint32_t mipl;   // the mip lane L's state is tested at
-			if (!CONE0 && NGP_SAMPLER_EMPTY_SPEC) {
-				// Cone stepping, both modes in one guess-and-verify loop. Every state is from(n + c) with n =
+			if (CONE0 ? NGP_SAMPLER_UNIFIED0 : NGP_SAMPLER_EMPTY_SPEC) {
+				// Both modes in one guess-and-verify loop. Every state is from(n + c) with n =
 				// to(previous state): c = 1 in an occupied run (t + calc_dt(t)), c = the ceil of
 				// advance_to_next_voxel in an empty one. Lane L guesses state L as from(to(t) + C_L): C_L = L
 				// when occupied (to(from(n)) == n nearly always), the voxel DDA's estimate when empty
@@ -607,9 +615,9 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				// predecessor and the lanes after it are re-guessed from there. The rays of a wave sit in
 				// different modes most of the time; sharing the loop (and its exact to()/from() per lane and
 				// round) means the wave no longer runs one mode's loop after the other's.
-				const float n0 = to_stepping_space(t, m.cone);
+				const float n0 = to_stepping_space(t, m.k());
 				const float c0 = occ_mode ? (float)L : m.guess_empty_steps(t, n0, L);
-				float cand = L == 0 ? t : from_stepping_space(n0 + c0, m.cone);
+				float cand = L == 0 ? t : from_stepping_space(n0 + c0, m.k());
 				uint32_t v0 = 1, mk = 0;
 				float nxt;
 				for (;;) {
@@ -619,9 +627,9 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 					const uint32_t v = __builtin_ctz(row_ballot(L >= v0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
 					if (v >= RG) break;
 					const float tv = __shfl(expct, (int)v, (int)RG);
-					const float nv = to_stepping_space(tv, m.cone);
+					const float nv = to_stepping_space(tv, m.k());
 					const float cv = occ_mode ? (float)(L - v) : m.guess_empty_steps(tv, nv, L - v);
-					cand = L < v ? cand : (L == v ? tv : from_stepping_space(nv + cv, m.cone));
+					cand = L < v ? cand : (L == v ? tv : from_stepping_space(nv + cv, m.k()));
 					v0 = v + 1;
 				}
 				tl = cand;

@@ -92,7 +92,13 @@ NGP_MATH_FN float ngp_expf(float x) {
 }
 
 /* ln x (FreeBSD e_logf.c algorithm): x = 2^e m with m in [sqrt(2)/2, sqrt(2)), f = m - 1,
- * s = f / (2 + f), log(1+f) = f - f^2/2 + s (f^2/2 + R(s^2)), e ln2 added in two parts. */
+ * s = f / (2 + f), log(1+f) = f - f^2/2 + s (f^2/2 + R(s^2)), e ln2 added in two parts.
+ * The polynomial constants Lg1..Lg4 and the ln2 hi/lo split below are those of fdlibm's e_logf.c,
+ * which carries this notice:
+ *   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+ *   Developed at SunPro, a Sun Microsystems, Inc. business.
+ *   Permission to use, copy, modify, and distribute this software is freely granted,
+ *   provided that this notice is preserved. */
 /* ln x for x = 2^(e0) m already reduced to ix = its bits (positive, normal) */
 NGP_MATH_FN float ngp_logf_core(uint32_t ix, int e);
 NGP_MATH_FN float ngp_logf(float x) {
