@@ -463,7 +463,9 @@ __device__ __forceinline__ void pair_slots(uint32_t k, uint32_t NE, uint32_t& a,
 // sums to their scratch slot, added by k_sc_split_reduce), blocks max_parts + vb the other buckets:
 // exact sum, written once per entry with plain stores (overwrite: every entry, untouched ones get 0
 // — no separate memset; accumulate: old + sum).
-template <uint32_t F>
+// FUSED: the grid's optimizer update (FusedAdam) replaces the gradient store; a template parameter so
+// that the plain instantiation keeps its register allocation (the runtime branch cost C2' 25 %).
+template <uint32_t F, bool FUSED>
 __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, const Levels lv, const uint32_t* __restrict__ tot,
                                                          const uint32_t* __restrict__ lo_arr, uint32_t B, uint32_t split_limit,
                                                          uint32_t max_parts, const uint16_t* __restrict__ item_idx,
@@ -492,7 +494,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 	bucket_entries(c, lv, B, vb, e0, n_e);
 	f16* g = grad + (size_t)e0 * F;
 	if (t == 0) {  // no contribution: gradient 0 (fused update: every entry of the bucket is skipped)
-		if (overwrite && !fa.rec)
+		if (overwrite && !FUSED)
 			for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) ((uint32_t*)g)[k] = 0u;
 		return;
 	}
@@ -507,7 +509,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 		uint32_t ia, ib;
 		pair_slots<F>(k, NEP, ia, ib);
 		float s0 = fix_to_f32(acc[ia]), s1 = fix_to_f32(acc[ib]);
-		if (fa.rec) {  // (issuing several pairs' state loads before the first update measured slower: 1.58 -> 1.97 ms at C5)
+		if (FUSED) {  // (issuing several pairs' state loads before the first update measured slower: 1.58 -> 1.97 ms at C5)
 			fused_adam_pair(fa, e0 * F / 2 + k, (f16)s0, (f16)s1);
 			continue;
 		}
@@ -524,7 +526,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 // and write every entry once — no fp16 atomics, bitwise reproducible. Columns x >= slab_x0 of the grid
 // run the MLP's dW slab reduction (SlabJob) instead: this kernel leaves most of the chip idle, so the
 // reduction fits beside it.
-template <uint32_t F>
+template <uint32_t F, bool FUSED>
 __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst c, const Levels lv, uint32_t B,
                                                                 const uint32_t* __restrict__ split, const uint32_t* __restrict__ splitb,
                                                                 const unsigned long long* __restrict__ scratch, f16* __restrict__ grad,
@@ -559,7 +561,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
 		}
 		for (; p < parts; ++p) { q0 += src[p * pstride + ia]; q1 += src[p * pstride + ib]; }
 		float s0 = fix_to_f32(q0), s1 = fix_to_f32(q1);
-		if (fa.rec) {
+		if (FUSED) {
 			fused_adam_pair(fa, e0 * F / 2 + k, (f16)s0, (f16)s1);
 			return;
 		}
@@ -623,7 +625,11 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		if (p.spb == 512) go(sc512, accum, splitr);
 		else go(sc1024, accum, splitr);
 	};
-#define NGP_SC_F(FF) by_chunk(k_sc_scatter<D, FF, 512, 512>, k_sc_scatter<D, FF, 1024, 1024>, k_sc_accumulate<FF>, k_sc_split_reduce<FF>)
+#define NGP_SC_F(FF)                                                                                                 \
+	if (fa.rec) by_chunk(k_sc_scatter<D, FF, 512, 512>, k_sc_scatter<D, FF, 1024, 1024>, k_sc_accumulate<FF, true>,   \
+	                     k_sc_split_reduce<FF, true>);                                                               \
+	else by_chunk(k_sc_scatter<D, FF, 512, 512>, k_sc_scatter<D, FF, 1024, 1024>, k_sc_accumulate<FF, false>,         \
+	              k_sc_split_reduce<FF, false>)
 	switch (F) {
 		case 1: NGP_SC_F(1); break;
 		case 2: NGP_SC_F(2); break;
