@@ -558,7 +558,10 @@ struct Marcher {
 
 #if NGP_SAMPLER_DIAG == 4  // instrumentation aid: per-ray march statistics (tools/nerf_step_profile.py --sampler-stats)
 // [0] empty iterations [1] occupied iterations [2] occupied verify rounds [3] rays [4] occupied states
-// [5] max iterations of one ray [6] empty-mode exits (mode switches) [8 + b] rays with 2^b <= iterations < 2^(b+1)
+// [5] max iterations of one ray [6] empty-mode exits (mode switches) [7] empty verify rounds
+// [8 + b] rays with 2^b <= iterations < 2^(b+1); wall_clock64 ticks summed over rays: [40] setup_ray
+// [41] sampling_end [42] guess + verify [43] occupancy test [44] whole march loop; [45] max ticks of one ray;
+// [46] the initial guesses of the unified loop (part of [42])
 __device__ unsigned long long g_sampler_stats[48];
 extern "C" __attribute__((visibility("default"))) int ngp_debug_sampler_stats(unsigned long long* out, int n) {
 	if (!out) {
@@ -567,9 +570,16 @@ extern "C" __attribute__((visibility("default"))) int ngp_debug_sampler_stats(un
 	}
 	return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sampler_stats), sizeof(unsigned long long) * (n < 48 ? n : 48)) == hipSuccess ? 0 : -1;
 }
-#define SAMPLER_STAT(x) x
+#define SAMPLER_STAT(...) __VA_ARGS__
+// a timestamp the scheduler keeps in program order
+__device__ __forceinline__ unsigned long long sampler_clock() {
+	__builtin_amdgcn_sched_barrier(0);
+	const unsigned long long t = wall_clock64();
+	__builtin_amdgcn_sched_barrier(0);
+	return t;
+}
 #else
-#define SAMPLER_STAT(x)
+#define SAMPLER_STAT(...)
 #endif
 
 // generate_training_samples_nerf pass 1: count the occupied steps of each ray, keep their t.
@@ -581,7 +591,9 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t i = gid / RG, L = gid % RG;
 	if (i >= a.n_rays) return;  // whole rows
+	SAMPLER_STAT(const unsigned long long ck0 = sampler_clock();)
 	const RaySetup r = setup_ray(cams, pixels, n_images, cfg, i + a.ray_offset, a.n_rays_total_for_image_idx, a.rng);
+	SAMPLER_STAT(const unsigned long long ck1 = sampler_clock(); unsigned long long ck2 = ck1, ck_g = 0, ck_o = 0, ck_q = 0;)
 	uint32_t j = 0;
 	if (r.valid) {
 		const Aabb box = cfg_aabb(cfg);
@@ -598,9 +610,10 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 #endif
 		float* tout = tbuf + (size_t)i * STEPS;
 		bool occ_mode = false;  // rays enter the aabb in empty space far more often than not
+		SAMPLER_STAT(ck2 = sampler_clock();)
 		SAMPLER_STAT(uint32_t st_e = 0; uint32_t st_o = 0; uint32_t st_r = 0; uint32_t st_x = 0; uint32_t st_q = 0;)
 		for (;;) {
-			SAMPLER_STAT(if (occ_mode) ++st_o; else ++st_e;)
+			SAMPLER_STAT(if (occ_mode) ++st_o; else ++st_e; const unsigned long long cka = sampler_clock();)
 			// lanes [0, nvalid) take the next nvalid states of the sequential march, assuming it stays in
 			// the current mode (all occupied / all empty)
 			float tl, last;  // last: the state after lane RG-1's (the march continues there if every lane stays in the mode)
@@ -618,6 +631,7 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				const float n0 = to_stepping_space(t, m.k());
 				const float c0 = occ_mode ? (float)L : m.guess_empty_steps(t, n0, L);
 				float cand = L == 0 ? t : from_stepping_space(n0 + c0, m.k());
+				SAMPLER_STAT(ck_q += sampler_clock() - cka;)
 				uint32_t v0 = 1, mk = 0;
 				float nxt;
 				for (;;) {
@@ -674,6 +688,7 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				}
 				last = tk;
 			}
+			SAMPLER_STAT(const unsigned long long ckb = sampler_clock(); ck_g += ckb - cka;)
 			const V3 pos = m.pos(tl);
 			const uint32_t mip = mipl;
 			constexpr uint32_t nvalid = RG;
@@ -681,8 +696,13 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			const bool occ = inside && density_grid_occupied_at(pos, a.bitfield, mip);
 			const uint32_t cont = row_ballot(inside && occ == occ_mode);
 			const uint32_t f = __builtin_ctz(~cont | (1u << RG));  // first lane the sequential march leaves the mode at
+			SAMPLER_STAT(ck_o += sampler_clock() - ckb;)
 			if (occ_mode) {
+#if NGP_SAMPLER_DIAG == 5  // timing aid: every occupied state stored twice (mirrored copy; cost of the stores)
+				if (L < f) { tout[j + L] = tl; tout[STEPS - 1 - (j + L)] = tl; }
+#else
 				if (L < f) tout[j + L] = tl;
+#endif
 				j += f;
 			}
 			if (f >= nvalid) {  // every state taken stayed in the mode: continue after the last one
@@ -706,6 +726,14 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			atomicAdd(&g_sampler_stats[6], (unsigned long long)st_x);
 			atomicAdd(&g_sampler_stats[7], (unsigned long long)st_q);
 			atomicAdd(&g_sampler_stats[8 + (31 - __builtin_clz(st_e + st_o))], 1ull);
+			const unsigned long long ck3 = sampler_clock();
+			atomicAdd(&g_sampler_stats[40], ck1 - ck0);
+			atomicAdd(&g_sampler_stats[41], ck2 - ck1);
+			atomicAdd(&g_sampler_stats[42], ck_g);
+			atomicAdd(&g_sampler_stats[43], ck_o);
+			atomicAdd(&g_sampler_stats[44], ck3 - ck2);
+			atomicMax(&g_sampler_stats[45], ck3 - ck0);
+			atomicAdd(&g_sampler_stats[46], ck_q);
 		})
 	}
 	if (L == 0) {

@@ -83,6 +83,10 @@ def main():
                  "occ_rounds_per_occ_iter": raw[2] / max(raw[1], 1), "occ_states_per_ray": raw[4] / n,
                  "max_iters_one_ray": raw[5], "empty_exits_per_ray": raw[6] / n,
                  "empty_rounds_per_empty_iter": raw[7] / max(raw[0], 1),
+                 "wall_ticks_per_ray": {"setup_ray": raw[40] / n, "sampling_end": raw[41] / n, "guess_verify": raw[42] / n,
+                                        "occupancy_test": raw[43] / n, "march_loop": raw[44] / n,
+                                        "initial_guess": raw[46] / n},
+                 "max_wall_ticks_one_ray": raw[45],
                  "iters_log2_hist": {f"{1 << b}": raw[8 + b] for b in range(32) if raw[8 + b]}}
     phases = {n: {"calls": v["calls"], "ms_per_call": round(v["ms"] / max(v["calls"], 1), 4),
                   "ms_per_step": round(v["ms"] / args.measure, 4)} for n, v in sorted(k.items())}
