@@ -394,8 +394,11 @@ constexpr uint32_t RG = NGP_SAMPLER_RG;  // lanes per ray (16 = one DPP row)
 #ifndef NGP_SAMPLER_EMPTY_SPEC
 #define NGP_SAMPLER_EMPTY_SPEC 1  // cone stepping: one guess-and-verify loop for both modes (0: occupied guess-and-verify, empty chain in every lane)
 #endif
+#ifndef NGP_SAMPLER_ROUND_CAP
+#define NGP_SAMPLER_ROUND_CAP 1  // verify rounds per march iteration (0: until every lane is verified)
+#endif
 #ifndef NGP_SAMPLER_UNIFIED0
-#define NGP_SAMPLER_UNIFIED0 0  // the same for cone 0 (measured neutral on the Lego stand-in, r03ab: off)
+#define NGP_SAMPLER_UNIFIED0 1  // the same for cone 0 (0: occupied guess-and-verify, empty chain)
 #endif
 
 constexpr uint32_t LG = 16;  // lanes per ray in the loss passes: one DPP row
@@ -616,8 +619,9 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			SAMPLER_STAT(if (occ_mode) ++st_o; else ++st_e; const unsigned long long cka = sampler_clock();)
 			// lanes [0, nvalid) take the next nvalid states of the sequential march, assuming it stays in
 			// the current mode (all occupied / all empty)
-			float tl, last;  // last: the state after lane RG-1's (the march continues there if every lane stays in the mode)
+			float tl, last;  // last: the state after lane nvalid-1's (the march continues there if every lane stays in the mode)
 			uint32_t mipl;   // the mip lane L's state is tested at
+			uint32_t nvalid = RG;  // lanes holding verified states
 			if (CONE0 ? NGP_SAMPLER_UNIFIED0 : NGP_SAMPLER_EMPTY_SPEC) {
 				// Both modes in one guess-and-verify loop. Every state is from(n + c) with n =
 				// to(previous state): c = 1 in an occupied run (t + calc_dt(t)), c = the ceil of
@@ -632,8 +636,8 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				const float c0 = occ_mode ? (float)L : m.guess_empty_steps(t, n0, L);
 				float cand = L == 0 ? t : from_stepping_space(n0 + c0, m.k());
 				SAMPLER_STAT(ck_q += sampler_clock() - cka;)
-				uint32_t v0 = 1, mk = 0;
-				float nxt;
+				uint32_t v0 = 1, mk = 0, rounds = 0;
+				float nxt, tcap = 0.0f;
 				for (;;) {
 					SAMPLER_STAT(if (occ_mode) ++st_r; else ++st_q;)
 					nxt = m.step_any(cand, occ_mode, &mk);
@@ -641,6 +645,14 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 					const uint32_t v = __builtin_ctz(row_ballot(L >= v0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
 					if (v >= RG) break;
 					const float tv = __shfl(expct, (int)v, (int)RG);
+					// The wave runs the loop until its slowest ray is verified. After NGP_SAMPLER_ROUND_CAP rounds a
+					// ray keeps its verified prefix (lanes < v) and continues from tv (the exact state after it)
+					// in the next iteration.
+					if (NGP_SAMPLER_ROUND_CAP && ++rounds >= NGP_SAMPLER_ROUND_CAP) {
+						nvalid = v;
+						tcap = tv;
+						break;
+					}
 					const float nv = to_stepping_space(tv, m.k());
 					const float cv = occ_mode ? (float)(L - v) : m.guess_empty_steps(tv, nv, L - v);
 					cand = L < v ? cand : (L == v ? tv : from_stepping_space(nv + cv, m.k()));
@@ -649,6 +661,7 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				tl = cand;
 				mipl = mk;
 				last = __shfl(nxt, (int)(RG - 1), (int)RG);
+				if (nvalid < RG) last = tcap;
 			} else if (occ_mode) {
 				// Occupied run: t_{k+1} = t_k + calc_dt(t_k) = from(to(t_k) + 1) in stepping space, and
 				// to(from(n)) == n nearly always. Guess state L as from(to(t) + L) and verify every guess at
@@ -691,7 +704,6 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			SAMPLER_STAT(const unsigned long long ckb = sampler_clock(); ck_g += ckb - cka;)
 			const V3 pos = m.pos(tl);
 			const uint32_t mip = mipl;
-			constexpr uint32_t nvalid = RG;
 			const bool inside = L < nvalid && tl <= t_end && aabb_contains(box, pos) && (occ_mode ? j + L : j) < STEPS;
 			const bool occ = inside && density_grid_occupied_at(pos, a.bitfield, mip);
 			const uint32_t cont = row_ballot(inside && occ == occ_mode);
