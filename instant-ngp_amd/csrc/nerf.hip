@@ -819,9 +819,134 @@ size_t scan_temp_bytes(uint32_t n) {
 	return bytes;
 }
 
+// Single-workgroup scans for the per-ray arrays of one step (~9-25 K rays): one launch of 1024 threads
+// instead of the device-wide scan's chain of launches. Tiles of 4096 elements, 4 consecutive ones per
+// thread (16-B coalesced loads and stores, all tiles loaded up front); one block scan per tile. Above
+// SCAN1_MAX elements (rays_per_batch can grow to 2^18) the device-wide scan.
+constexpr uint32_t SCAN1_THREADS = 1024, SCAN1_TILE = 4 * SCAN1_THREADS, SCAN1_NT = 8;
+constexpr uint32_t SCAN1_MAX = SCAN1_NT * SCAN1_TILE;
+// exclusive sum of one value per thread over the block, and the block total; lds: 32 words
+__device__ __forceinline__ uint32_t block_exclusive_sum(uint32_t v, uint32_t* lds, uint32_t* total) {
+	constexpr uint32_t NW = SCAN1_THREADS / 64;
+	const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+	uint32_t x = v;
+#pragma unroll
+	for (uint32_t d = 1; d < 64; d <<= 1) {
+		const uint32_t y = __shfl_up(x, d, 64);
+		if (lane >= d) x += y;
+	}
+	if (lane == 63) lds[w] = x;
+	__syncthreads();
+	if (w == 0) {
+		uint32_t y = lane < NW ? lds[lane] : 0u;
+#pragma unroll
+		for (uint32_t d = 1; d < NW; d <<= 1) {
+			const uint32_t z = __shfl_up(y, d, 64);
+			if (lane >= d) y += z;
+		}
+		if (lane < NW) lds[NW + lane] = y;  // inclusive
+	}
+	__syncthreads();
+	const uint32_t r = (w ? lds[NW + w - 1] : 0u) + x - v;
+	*total = lds[2 * NW - 1];
+	__syncthreads();
+	return r;
+}
+__device__ __forceinline__ void scan1_load(const uint32_t* in, uint32_t n, uint32_t i, uint32_t v[4]) {
+	if (i + 3 < n && ((uintptr_t)in & 15) == 0) {
+		const uint4 q = *(const uint4*)(in + i);
+		v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+	} else {
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) v[k] = i + k < n ? in[i + k] : 0u;
+	}
+}
+__device__ __forceinline__ void scan1_store(uint32_t* out, uint32_t n, uint32_t i, const uint32_t v[4]) {
+	if (i + 3 < n && ((uintptr_t)out & 15) == 0) {
+		*(uint4*)(out + i) = uint4{v[0], v[1], v[2], v[3]};
+	} else {
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k)
+			if (i + k < n) out[i + k] = v[k];
+	}
+}
+__global__ void __launch_bounds__(SCAN1_THREADS) k_scan1(uint32_t n, const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
+	__shared__ uint32_t lds[32];
+	const uint32_t nt = (n + SCAN1_TILE - 1) / SCAN1_TILE;
+	uint32_t x[SCAN1_NT][4];
+#pragma unroll
+	for (uint32_t tl = 0; tl < SCAN1_NT; ++tl)
+		if (tl < nt) scan1_load(in, n, tl * SCAN1_TILE + 4 * threadIdx.x, x[tl]);
+	uint32_t run = 0;
+#pragma unroll
+	for (uint32_t tl = 0; tl < SCAN1_NT; ++tl) {
+		if (tl >= nt) break;
+		uint32_t tot;
+		uint32_t b = run + block_exclusive_sum(x[tl][0] + x[tl][1] + x[tl][2] + x[tl][3], lds, &tot);
+		uint32_t o[4];
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) {
+			o[k] = b;
+			b += x[tl][k];
+		}
+		scan1_store(out, n, tl * SCAN1_TILE + 4 * threadIdx.x, o);
+		run += tot;
+	}
+}
 static void exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* tmp, size_t bytes, hipStream_t s) {
+	if (n <= SCAN1_MAX) {
+		k_scan1<<<1, SCAN1_THREADS, 0, s>>>(n, in, out);
+		NGP_HIP(hipGetLastError());
+		return;
+	}
 	size_t need = bytes;
 	NGP_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, need, in, out, (int)n, s));
+}
+// The sampler's base = exclusive scan of nsteps, keep (the ray's samples fit under max_samples,
+// testbed_nerf.cu:1616-1619 atomicAdd guard, in ray order), slot = exclusive scan of keep: one launch.
+__global__ void __launch_bounds__(SCAN1_THREADS) k_sample_scan1(uint32_t n, const uint32_t* __restrict__ nsteps, uint32_t max_samples,
+                                                                 uint32_t* __restrict__ base, uint32_t* __restrict__ keep,
+                                                                 uint32_t* __restrict__ slot) {
+	__shared__ uint32_t lds[32];
+	const uint32_t nt = (n + SCAN1_TILE - 1) / SCAN1_TILE;
+	uint32_t x[SCAN1_NT][4];
+#pragma unroll
+	for (uint32_t tl = 0; tl < SCAN1_NT; ++tl)
+		if (tl < nt) scan1_load(nsteps, n, tl * SCAN1_TILE + 4 * threadIdx.x, x[tl]);
+	uint32_t run = 0;
+#pragma unroll
+	for (uint32_t tl = 0; tl < SCAN1_NT; ++tl) {
+		if (tl >= nt) break;
+		uint32_t tot;
+		uint32_t b = run + block_exclusive_sum(x[tl][0] + x[tl][1] + x[tl][2] + x[tl][3], lds, &tot);
+		uint32_t o[4];
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) {
+			o[k] = b;
+			const uint32_t ns = x[tl][k];
+			b += ns;
+			x[tl][k] = (ns > 0 && b <= max_samples) ? 1u : 0u;  // keep
+		}
+		const uint32_t i = tl * SCAN1_TILE + 4 * threadIdx.x;
+		scan1_store(base, n, i, o);
+		scan1_store(keep, n, i, x[tl]);
+		run += tot;
+	}
+	run = 0;
+#pragma unroll
+	for (uint32_t tl = 0; tl < SCAN1_NT; ++tl) {
+		if (tl >= nt) break;
+		uint32_t tot;
+		uint32_t b = run + block_exclusive_sum(x[tl][0] + x[tl][1] + x[tl][2] + x[tl][3], lds, &tot);
+		uint32_t o[4];
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) {
+			o[k] = b;
+			b += x[tl][k];
+		}
+		scan1_store(slot, n, tl * SCAN1_TILE + 4 * threadIdx.x, o);
+		run += tot;
+	}
 }
 
 size_t sample_tmp_f32(uint32_t n_rays) { return (size_t)n_rays * (STEPS + sizeof(RayGeo) / 4); }
@@ -847,9 +972,14 @@ void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs
 	}
 	{
 		ProfScope ps("sample_scans", s);
-		exclusive_scan(nsteps, base, a.n_rays, scan_tmp, scan_bytes, s);
-		k_sample_keep<<<div_round_up(a.n_rays, 256), 256, 0, s>>>(a.n_rays, nsteps, base, a.max_samples, keep);
-		exclusive_scan(keep, slot, a.n_rays, scan_tmp, scan_bytes, s);
+		if (a.n_rays <= SCAN1_MAX) {
+			k_sample_scan1<<<1, SCAN1_THREADS, 0, s>>>(a.n_rays, nsteps, a.max_samples, base, keep, slot);
+			NGP_HIP(hipGetLastError());
+		} else {
+			exclusive_scan(nsteps, base, a.n_rays, scan_tmp, scan_bytes, s);
+			k_sample_keep<<<div_round_up(a.n_rays, 256), 256, 0, s>>>(a.n_rays, nsteps, base, a.max_samples, keep);
+			exclusive_scan(keep, slot, a.n_rays, scan_tmp, scan_bytes, s);
+		}
 	}
 	ProfScope ps("sample_write", s);
 	k_sample_write<<<div_round_up((size_t)a.n_rays * WG, 256), 256, 0, s>>>(cfg, a, nsteps, base, keep, slot, tbuf, geo);
