@@ -56,7 +56,8 @@ __device__ __forceinline__ float div_max_stepsize(float t) {
 struct Cone {
 	float c, log1p_c, a, b, at, bt, rl;  // rl = RN(1 / log1p_c)
 };
-__device__ __forceinline__ Cone make_cone(float c) {
+// host and device: the sampler computes it once per launch on the host (same ngp_math.h operations)
+__host__ __device__ inline Cone make_cone(float c) {
 	Cone k{c, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 	if (c <= 1e-5f) return k;
 	k.log1p_c = ngp_logf(1.0f + c);
@@ -286,7 +287,7 @@ struct RaySetup {
 };
 
 __device__ RaySetup setup_ray(const Camera* cams, const uint32_t* pixels, uint32_t n_images, const ngp_nerf_config& cfg,
-                              uint32_t ig, uint32_t n_rays_div, Rng rng) {
+                              uint32_t ig, uint32_t n_rays_div, Rng rng, const Cone& cone) {
 	RaySetup r;
 	r.valid = false;
 	const uint32_t img = image_idx(ig, n_rays_div, n_images);
@@ -311,7 +312,7 @@ __device__ RaySetup setup_ray(const Camera* cams, const uint32_t* pixels, uint32
 	aabb_ray_intersect(cfg_aabb(cfg), r.o, r.dn, &tmin, &tmax);
 	r.cone = cfg.cone_angle_constant;
 	tmin = fmaxf(tmin, 0.0f);
-	r.startt = advance_n_steps(tmin, make_cone(r.cone), pcg_float(rng));
+	r.startt = advance_n_steps(tmin, cone, pcg_float(rng));
 	r.idir = v3(1.0f / r.dn.x, 1.0f / r.dn.y, 1.0f / r.dn.z);
 	r.valid = true;
 	return r;
@@ -593,17 +594,17 @@ template <bool CONE0>
 __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
                                                       uint32_t n_images, const ngp_nerf_config cfg, SampleArgs a,
                                                       uint32_t* __restrict__ nsteps, float* __restrict__ tbuf,
-                                                      RayGeo* __restrict__ geo) {
+                                                      RayGeo* __restrict__ geo, const Cone cone) {
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t i = gid / RG, L = gid % RG;
 	if (i >= a.n_rays) return;  // whole rows
 	SAMPLER_STAT(const unsigned long long ck0 = sampler_clock();)
-	const RaySetup r = setup_ray(cams, pixels, n_images, cfg, i + a.ray_offset, a.n_rays_total_for_image_idx, a.rng);
+	const RaySetup r = setup_ray(cams, pixels, n_images, cfg, i + a.ray_offset, a.n_rays_total_for_image_idx, a.rng, cone);
 	SAMPLER_STAT(const unsigned long long ck1 = sampler_clock(); unsigned long long ck2 = ck1, ck_g = 0, ck_o = 0, ck_q = 0;)
 	uint32_t j = 0;
 	if (r.valid) {
 		const Aabb box = cfg_aabb(cfg);
-		const Marcher<CONE0> m{r.o, r.dn, r.idir, make_cone(r.cone), cfg.max_cascade};
+		const Marcher<CONE0> m{r.o, r.dn, r.idir, cone, cfg.max_cascade};
 		float t = r.startt;
 #if NGP_SAMPLER_DIAG == 2
 		const float t_end = 3.0e38f;
@@ -780,7 +781,7 @@ constexpr uint32_t WG = 64;
 __global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg, SampleArgs a, const uint32_t* __restrict__ nsteps,
                                                       const uint32_t* __restrict__ base, const uint32_t* __restrict__ keep,
                                                       const uint32_t* __restrict__ slot, const float* __restrict__ tbuf,
-                                                      const RayGeo* __restrict__ geo) {
+                                                      const RayGeo* __restrict__ geo, const Cone cone) {
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t i = gid / WG, L = gid % WG;
 	if (gid == 0) {  // counters: rays kept, total steps of every ray that found samples
@@ -801,7 +802,6 @@ __global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg,
 	const V3 diag = v3(box.mx.x - box.mn.x, box.mx.y - box.mn.y, box.mx.z - box.mn.z);
 	const V3 wdir = v3((g.dn[0] + 1.0f) * 0.5f, (g.dn[1] + 1.0f) * 0.5f, (g.dn[2] + 1.0f) * 0.5f);
 	const float* tin = tbuf + (size_t)i * STEPS;
-	const Cone cone = make_cone(g.pad[0]);
 	for (uint32_t jj = L; jj < numsteps; jj += WG) {
 		const float t = tin[jj];
 		const V3 pos = v3(g.o[0] + t * g.dn[0], g.o[1] + t * g.dn[1], g.o[2] + t * g.dn[2]);
@@ -962,12 +962,13 @@ void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs
 	float* tbuf = tmpf;
 	RayGeo* geo = (RayGeo*)(tmpf + (size_t)a.n_rays * STEPS);
 	const uint32_t blocks = div_round_up((size_t)a.n_rays * RG, NGP_SAMPLER_BLOCK);
+	const Cone cone = make_cone(cfg.cone_angle_constant);  // every ray's cone (setup_ray: r.cone)
 	{
 		ProfScope ps("sample_count", s);
 		if (cfg.cone_angle_constant <= 1e-5f)
-			k_sample_count<true><<<blocks, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo);
+			k_sample_count<true><<<blocks, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo, cone);
 		else
-			k_sample_count<false><<<blocks, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo);
+			k_sample_count<false><<<blocks, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo, cone);
 		NGP_HIP(hipGetLastError());
 	}
 	{
@@ -982,7 +983,7 @@ void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs
 		}
 	}
 	ProfScope ps("sample_write", s);
-	k_sample_write<<<div_round_up((size_t)a.n_rays * WG, 256), 256, 0, s>>>(cfg, a, nsteps, base, keep, slot, tbuf, geo);
+	k_sample_write<<<div_round_up((size_t)a.n_rays * WG, 256), 256, 0, s>>>(cfg, a, nsteps, base, keep, slot, tbuf, geo, cone);
 	NGP_HIP(hipGetLastError());
 }
 
