@@ -1229,22 +1229,28 @@ __global__ void k_rollover_f32(uint32_t n_elements, uint32_t stride, const uint3
 	data[i] = data[i % (n_in * stride)];
 }
 // both rollovers of the training batch in one launch (dL/doutput rescaled, coordinates copied)
+// Grid-stride over the rollover range only (a full batch leaves nothing to fill; launching one thread per
+// element cost ~16 K empty blocks per step).
 __global__ void k_rollover_pair(uint32_t n_elements, uint32_t stride16, uint32_t stride32, const uint32_t* n_input_ptr, f16* d16,
                                 float* d32) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t n_in = *n_input_ptr;
-	if (n_in == 0) return;
-	if (i >= n_in * stride16 && i < n_elements * stride16) {
-		f16 r = d16[i % (n_in * stride16)];
-		r = (f16)((float)r * n_in / n_elements);
-		d16[i] = r;
+	if (n_in == 0 || n_in >= n_elements) return;
+	const uint32_t lo = n_in * (stride16 < stride32 ? stride16 : stride32);
+	const uint32_t hi = n_elements * (stride16 > stride32 ? stride16 : stride32);
+	for (uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += gridDim.x * blockDim.x) {
+		if (i >= n_in * stride16 && i < n_elements * stride16) {
+			f16 r = d16[i % (n_in * stride16)];
+			r = (f16)((float)r * n_in / n_elements);
+			d16[i] = r;
+		}
+		if (i >= n_in * stride32 && i < n_elements * stride32) d32[i] = d32[i % (n_in * stride32)];
 	}
-	if (i >= n_in * stride32 && i < n_elements * stride32) d32[i] = d32[i % (n_in * stride32)];
 }
 void fill_rollover_pair(uint32_t n_elements, const uint32_t* n_input, f16* dloss, uint32_t stride16, float* coords,
                         uint32_t stride32, hipStream_t s) {
 	const uint64_t n = (uint64_t)n_elements * (stride16 > stride32 ? stride16 : stride32);
-	k_rollover_pair<<<div_round_up(n, 256), 256, 0, s>>>(n_elements, stride16, stride32, n_input, dloss, coords);
+	const uint32_t blocks = (uint32_t)std::min<uint64_t>(div_round_up(n, 256), 1024);
+	k_rollover_pair<<<blocks, 256, 0, s>>>(n_elements, stride16, stride32, n_input, dloss, coords);
 	NGP_HIP(hipGetLastError());
 }
 void fill_rollover_f16(uint32_t n_elements, uint32_t stride, const uint32_t* n_input, f16* data, bool rescale, hipStream_t s) {
