@@ -80,6 +80,7 @@ struct LossArgs {
 	float* coords_out;         // [max_samples_compacted x 7]
 	f16* dloss_doutput;        // [max_samples_compacted x 16]
 	float* loss;               // [n_rays]
+	bool zero_loss;            // pass 1 zeroes loss[0, n_rays) (the Testbed step's memset, testbed_nerf.cu:3579)
 	uint32_t* compacted_counter;  // [1]
 	const float* mean_density;    // [1]
 	float loss_scale;

@@ -1015,6 +1015,7 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t i = gid / LG, L = gid % LG;
 	if (i >= a.n_rays) return;
+	if (L == 0 && a.zero_loss && a.loss) a.loss[i] = 0.0f;  // pass 2 writes the compacted rays' loss after it
 	if (i >= *a.ray_counter) { if (L == 0) craw[i] = 0; return; }
 	const uint32_t numsteps = a.numsteps[2 * i], base = a.numsteps[2 * i + 1];
 	const f16* out = a.network_output + (size_t)base * a.out_stride;

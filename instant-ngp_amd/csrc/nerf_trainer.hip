@@ -304,7 +304,7 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
                              uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
                              const void* network_output, uint32_t out_stride, const uint32_t* ray_indices, const float* rays,
                              uint32_t* numsteps, const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
-                             uint32_t* compacted_counter, const float* mean_density, float loss_scale);
+                             uint32_t* compacted_counter, const float* mean_density, float loss_scale, bool zero_loss = false);
 
 int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
                           uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
@@ -320,7 +320,7 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
                              uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
                              const void* network_output, uint32_t out_stride, const uint32_t* ray_indices, const float* rays,
                              uint32_t* numsteps, const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
-                             uint32_t* compacted_counter, const float* mean_density, float loss_scale) {
+                             uint32_t* compacted_counter, const float* mean_density, float loss_scale, bool zero_loss) {
 	if (!ds || !cfg || !ray_counter || !network_output || !numsteps || !coords_in || !coords_out || !dloss_doutput ||
 	    !compacted_counter || !mean_density)
 		return NGP_INVALID;
@@ -331,7 +331,7 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
 		a.out_stride = out_stride;
 		a.ray_indices = ray_indices; a.rays = rays; a.numsteps = numsteps; a.coords_in = coords_in; a.coords_out = coords_out;
 		a.dloss_doutput = (f16*)dloss_doutput; a.loss = loss; a.compacted_counter = compacted_counter;
-		a.mean_density = mean_density; a.loss_scale = loss_scale;
+		a.mean_density = mean_density; a.loss_scale = loss_scale; a.zero_loss = zero_loss;
 		if (n_rays == 0) { NGP_HIP(hipMemsetAsync(compacted_counter, 0, 4, S(stream))); return NGP_OK; }
 		static thread_local Buf scan, tmp, tmpf;
 		const size_t sb = scan_temp_bytes(n_rays);
@@ -660,7 +660,6 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		f16* dloss = t->dloss.get<f16>((size_t)Bl * 16);
 		float* coords_c = t->coords_c.get<float>((size_t)Bl * 7);
 		float* loss = t->loss.get<float>(Ra);
-		NGP_HIP(hipMemsetAsync(loss, 0, (size_t)Ra * 4, s));
 		ngp_rng rng{t->rng.state, t->rng.inc};
 		// global ray ids (rng.advance(i * 16), image_idx(i, R)) so the shards draw the 1-GPU rays;
 		// dL/doutput is scaled by 128 / R (global), so the summed gradient is the 1-GPU gradient
@@ -680,7 +679,7 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		{
 		ProfScope ps("nerf_loss", s);
 		check_rc(nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, 4, ray_indices, rays, numsteps, coords, coords_c,
-		                               dloss, loss, ctr + 2, (const float*)t->mean.p, dp ? loss_scale_local : 128.0f));
+		                               dloss, loss, ctr + 2, (const float*)t->mean.p, dp ? loss_scale_local : 128.0f, true));
 		fill_rollover_pair(Bl, ctr + 2, dloss, 16, coords_c, 7, s);  // fill_rollover_and_rescale + fill_rollover
 		}
 		// the step's counters are final here (the training pass does not touch them): publish them before
