@@ -1040,12 +1040,24 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 	float rr = 0.f, rg = 0.f, rb = 0.f;
 	uint32_t cn = 0;
 	bool stop = false;
+	// the next chunk's loads are issued before this chunk's compositing chain (software pipelining)
+	f16x4 o_next = {(f16)0.f, (f16)0.f, (f16)0.f, (f16)0.f};
+	float dtw_next = 0.f;
+	if (L < numsteps) {
+		o_next = *(const f16x4*)(out + (size_t)L * a.out_stride);
+		dtw_next = ci[(size_t)L * 7 + 3];
+	}
 	for (uint32_t c = 0; c < numsteps && !stop; c += LG) {
 		const uint32_t jj = c + L;
+		const f16x4 o = o_next;
+		const float dtw = dtw_next;
+		if (jj + LG < numsteps) {
+			o_next = *(const f16x4*)(out + (size_t)(jj + LG) * a.out_stride);
+			dtw_next = ci[(size_t)(jj + LG) * 7 + 3];
+		}
 		float alpha = 0.f, cr = 0.f, cg = 0.f, cb = 0.f;
 		if (jj < numsteps) {
-			const f16x4 o = *(const f16x4*)(out + (size_t)jj * a.out_stride);
-			const float dt = unwarp_dt(ci[(size_t)jj * 7 + 3]);
+			const float dt = unwarp_dt(dtw);
 			const float density = network_to_density((float)o[3], cfg.density_activation);
 			alpha = 1.f - ngp_expf_fast(-density * dt);
 			cr = network_to_rgb((float)o[0], cfg.rgb_activation);
@@ -1134,16 +1146,28 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const ngp_nerf_config cfg, L
 	f16* dl = a.dloss_doutput + (size_t)compacted_base * 16;
 	float r2[3] = {0.f, 0.f, 0.f};
 	float t = 1.0f;
+	// the next chunk's loads are issued before this chunk's compositing chain (software pipelining)
+	float cc_next[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+	f16x4 o_next = {(f16)0.f, (f16)0.f, (f16)0.f, (f16)0.f};
+	if (L < cn) {
+#pragma unroll
+		for (int k = 0; k < 7; ++k) cc_next[k] = ci[(size_t)L * 7 + k];
+		o_next = *(const f16x4*)(out + (size_t)L * a.out_stride);
+	}
 	for (uint32_t c0 = 0; c0 < cn; c0 += LG) {
 		const uint32_t jj = c0 + L;
 		const bool valid = jj < cn;
-		float cc[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-		f16x4 o = {(f16)0.f, (f16)0.f, (f16)0.f, (f16)0.f};
+		float cc[7];
+#pragma unroll
+		for (int k = 0; k < 7; ++k) cc[k] = cc_next[k];
+		const f16x4 o = o_next;
+		if (jj + LG < cn) {
+#pragma unroll
+			for (int k = 0; k < 7; ++k) cc_next[k] = ci[(size_t)(jj + LG) * 7 + k];
+			o_next = *(const f16x4*)(out + (size_t)(jj + LG) * a.out_stride);
+		}
 		float rgb[3] = {0.f, 0.f, 0.f}, alpha = 0.f, dt = 0.f;
 		if (valid) {
-#pragma unroll
-			for (int k = 0; k < 7; ++k) cc[k] = ci[(size_t)jj * 7 + k];
-			o = *(const f16x4*)(out + (size_t)jj * a.out_stride);
 			for (int k = 0; k < 3; ++k) rgb[k] = network_to_rgb((float)o[k], cfg.rgb_activation);
 			dt = unwarp_dt(cc[3]);
 			const float density = network_to_density((float)o[3], cfg.density_activation);
