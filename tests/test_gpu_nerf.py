@@ -137,9 +137,12 @@ def test_generate_training_samples_cone(pkg, orc, scene, aabb_scale, n_rays, fra
 
 @pytest.mark.parametrize("aabb_scale,cone,n_rays,frac", [
     (8.0, None, 1 << 16, 0.05), (32.0, None, 1 << 16, 0.03), (128.0, None, 1 << 16, 0.01),
-    (8.0, 1e-4, 1 << 14, 0.05), (8.0, 5e-4, 1 << 14, 0.05), (16.0, 2e-5, 1 << 13, 0.05), (8.0, 0.02, 1 << 14, 0.1)])
+    (8.0, 1e-4, 1 << 14, 0.05), (8.0, 5e-4, 1 << 14, 0.05), (16.0, 2e-5, 1 << 13, 0.05), (8.0, 0.02, 1 << 14, 0.1),
+    # the single-workgroup scans at their largest size (8 tiles of 4096) and a ragged cone-0 batch
+    (8.0, None, 1 << 15, 0.05), (1.0, None, 30001, 0.1)])
 def test_sampler_and_loss_cone_at_scale(pkg, orc, scene, aabb_scale, cone, n_rays, frac):
-    """Fox-scale and larger ray counts (>= 64k rays at aabb_scale 8, 32, 128) and user-set cone angles
+    """Fox-scale and larger ray counts (>= 64k rays at aabb_scale 8, 32, 128: the device-wide scans; 32k
+    and 30001 rays: the single-workgroup scans) and user-set cone angles
     from 2e-5 to 0.02: the sampler's hardware exp/log speculation in empty space (csrc/nerf.hip
     step_empty) falls back to the exact path near every integer decision, with margins that scale with
     1 / log(1 + cone), so sample sets, compacted counts and coordinates stay bit-exact with the oracle."""
