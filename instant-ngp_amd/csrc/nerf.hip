@@ -406,6 +406,12 @@ constexpr uint32_t RG = NGP_SAMPLER_RG;  // lanes per ray (16 = one DPP row)
 #endif
 
 constexpr uint32_t LG = 16;  // lanes per ray in the loss passes: one DPP row
+#ifndef NGP_LOSS_PF
+#define NGP_LOSS_PF 2  // loss pass 1: chunks of 16 samples whose loads are in flight ahead of the compositing
+#endif
+#ifndef NGP_LOSS2_PF
+#define NGP_LOSS2_PF 1  // loss pass 2: depth 2 takes 86 VGPRs (5 waves/SIMD) and measured 41 -> 45 us (Lego stand-in)
+#endif
 static_assert(RG >= 4 && RG <= 16 && (RG & (RG - 1)) == 0, "sampler group: 4, 8 or 16 lanes");
 #ifndef NGP_SAMPLER_BLOCK
 #define NGP_SAMPLER_BLOCK 256
@@ -777,6 +783,9 @@ __global__ void k_sample_keep(uint32_t n, const uint32_t* __restrict__ nsteps, c
 // pass 2: write the ray records and the NerfCoordinates of kept rays from the stored t values; one
 // wave per ray (most rays take one or two iterations, consecutive lanes write consecutive samples).
 constexpr uint32_t WG = 64;
+#ifndef NGP_SW_STAGE
+#define NGP_SW_STAGE 1  // records staged in LDS, written as contiguous wave stores
+#endif
 // pass 2: write the ray records and the NerfCoordinates of kept rays from the stored t values.
 __global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg, SampleArgs a, const uint32_t* __restrict__ nsteps,
                                                       const uint32_t* __restrict__ base, const uint32_t* __restrict__ keep,
@@ -802,6 +811,35 @@ __global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg,
 	const V3 diag = v3(box.mx.x - box.mn.x, box.mx.y - box.mn.y, box.mx.z - box.mn.z);
 	const V3 wdir = v3((g.dn[0] + 1.0f) * 0.5f, (g.dn[1] + 1.0f) * 0.5f, (g.dn[2] + 1.0f) * 0.5f);
 	const float* tin = tbuf + (size_t)i * STEPS;
+#if NGP_SW_STAGE
+	// a wave's 64 records (7 floats each, 28-B stride) are staged in LDS and written back as 7 contiguous
+	// 256-B wave stores instead of 7 stores that each touch 14 lines
+	__shared__ float stage[256 / WG][WG * 7];
+	float* st = stage[threadIdx.x / WG];
+	for (uint32_t j0 = 0; j0 < numsteps; j0 += WG) {
+		const uint32_t jj = j0 + L;
+		if (jj < numsteps) {
+			const float t = tin[jj];
+			const V3 pos = v3(g.o[0] + t * g.dn[0], g.o[1] + t * g.dn[1], g.o[2] + t * g.dn[2]);
+			const float dt = calc_dt(t, cone);
+			float* c = st + L * 7;  // stride 7 words: conflict-free
+			c[0] = (pos.x - box.mn.x) / diag.x; c[1] = (pos.y - box.mn.y) / diag.y; c[2] = (pos.z - box.mn.z) / diag.z;
+			c[3] = warp_dt(dt);
+			c[4] = wdir.x; c[5] = wdir.y; c[6] = wdir.z;
+		}
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+		const uint32_t nf = min(WG, numsteps - j0) * 7;
+		float* dst = a.coords + (size_t)(b + j0) * 7;
+#pragma unroll
+		for (uint32_t k = 0; k < 7; ++k)
+			if (L + k * WG < nf) dst[L + k * WG] = st[L + k * WG];
+		__builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+		__builtin_amdgcn_wave_barrier();
+		__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+	}
+#else
 	for (uint32_t jj = L; jj < numsteps; jj += WG) {
 		const float t = tin[jj];
 		const V3 pos = v3(g.o[0] + t * g.dn[0], g.o[1] + t * g.dn[1], g.o[2] + t * g.dn[2]);
@@ -811,6 +849,7 @@ __global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg,
 		c[3] = warp_dt(dt);
 		c[4] = wdir.x; c[5] = wdir.y; c[6] = wdir.z;
 	}
+#endif
 }
 
 size_t scan_temp_bytes(uint32_t n) {
@@ -1030,9 +1069,13 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 	float u, v;
 	random_image_pos(rng, cam.width, cam.height, cfg.snap_to_pixel_centers != 0, &u, &v);
 	pcg_advance(rng, 1);  // motionblur_time
+	// The per-ray colour work (12 powf in the default configuration) is split over the row: lane ch < 3
+	// finishes colour channel ch with the reference's per-channel operations, and lane 0 gathers the
+	// three results (the other lanes repeat channel 2).
+	const uint32_t ch = L < 3 ? L : 2;
 	float bg[3] = {cfg.background_color[0], cfg.background_color[1], cfg.background_color[2]};
 	if (cfg.random_bg_color) { bg[0] = pcg_float(rng); bg[1] = pcg_float(rng); bg[2] = pcg_float(rng); }
-	for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear(bg[k]);
+	float bgc = srgb_to_linear(ch == 0 ? bg[0] : ch == 1 ? bg[1] : bg[2]);
 	// read_rgba, Byte images (common_device.cuh:885-904)
 	const uint32_t raw = pixels[cam.pixel_offset + pixel_index(u, v, cam.width, cam.height)];
 	float t = 1.f;
@@ -1040,20 +1083,30 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 	float rr = 0.f, rg = 0.f, rb = 0.f;
 	uint32_t cn = 0;
 	bool stop = false;
-	// the next chunk's loads are issued before this chunk's compositing chain (software pipelining)
-	f16x4 o_next = {(f16)0.f, (f16)0.f, (f16)0.f, (f16)0.f};
-	float dtw_next = 0.f;
-	if (L < numsteps) {
-		o_next = *(const f16x4*)(out + (size_t)L * a.out_stride);
-		dtw_next = ci[(size_t)L * 7 + 3];
+	// software pipelining: the loads of the next NGP_LOSS_PF chunks are in flight while a chunk's
+	// compositing chain runs (the chunk loop is unrolled by the depth, so every buffer keeps its registers)
+	f16x4 ob[NGP_LOSS_PF];
+	float db[NGP_LOSS_PF];
+#pragma unroll
+	for (uint32_t d = 0; d < NGP_LOSS_PF; ++d) {
+		ob[d] = f16x4{(f16)0.f, (f16)0.f, (f16)0.f, (f16)0.f};
+		db[d] = 0.f;
+		if (L + d * LG < numsteps) {
+			ob[d] = *(const f16x4*)(out + (size_t)(L + d * LG) * a.out_stride);
+			db[d] = ci[(size_t)(L + d * LG) * 7 + 3];
+		}
 	}
-	for (uint32_t c = 0; c < numsteps && !stop; c += LG) {
+	for (uint32_t c0 = 0; c0 < numsteps && !stop; c0 += NGP_LOSS_PF * LG)
+#pragma unroll
+	for (uint32_t d = 0; d < NGP_LOSS_PF; ++d) {
+		const uint32_t c = c0 + d * LG;
+		if (c >= numsteps || stop) break;
 		const uint32_t jj = c + L;
-		const f16x4 o = o_next;
-		const float dtw = dtw_next;
-		if (jj + LG < numsteps) {
-			o_next = *(const f16x4*)(out + (size_t)(jj + LG) * a.out_stride);
-			dtw_next = ci[(size_t)(jj + LG) * 7 + 3];
+		const f16x4 o = ob[d];
+		const float dtw = db[d];
+		if (jj + NGP_LOSS_PF * LG < numsteps) {
+			ob[d] = *(const f16x4*)(out + (size_t)(jj + NGP_LOSS_PF * LG) * a.out_stride);
+			db[d] = ci[(size_t)(jj + NGP_LOSS_PF * LG) * 7 + 3];
 		}
 		float alpha = 0.f, cr = 0.f, cg = 0.f, cb = 0.f;
 		if (jj < numsteps) {
@@ -1080,39 +1133,35 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 		NGP_ROW_UNROLL16(NGP_LOSS1_STEP)
 #undef NGP_LOSS1_STEP
 	}
-	if (L != 0) return;
-	float tex[4];
-	if (raw == 0x00FF00FFu) { tex[0] = tex[1] = tex[2] = tex[3] = -1.0f; }
+	// channel ch of the target, the background and the loss (every lane of the row holds rr, rg, rb, t, cn)
+	float texc, tex3;
+	if (raw == 0x00FF00FFu) { texc = tex3 = -1.0f; }
 	else {
 		const float alpha = (float)(raw >> 24) * (1.0f / 255.0f);
-		tex[0] = srgb_to_linear((float)(raw & 0xff) * (1.0f / 255.0f)) * alpha;
-		tex[1] = srgb_to_linear((float)((raw >> 8) & 0xff) * (1.0f / 255.0f)) * alpha;
-		tex[2] = srgb_to_linear((float)((raw >> 16) & 0xff) * (1.0f / 255.0f)) * alpha;
-		tex[3] = alpha;
+		texc = srgb_to_linear((float)((raw >> (8 * ch)) & 0xff) * (1.0f / 255.0f)) * alpha;
+		tex3 = alpha;
 	}
 	const float exposure_scale = expf(0.6931471805599453f * 0.0f);
-	float target[3];
+	float target;
 	if (cfg.linear_colors || cfg.color_space_linear) {
-		for (int k = 0; k < 3; ++k) target[k] = exposure_scale * tex[k] + (1.0f - tex[3]) * bg[k];
-		if (!cfg.linear_colors)
-			for (int k = 0; k < 3; ++k) { target[k] = linear_to_srgb(target[k]); bg[k] = linear_to_srgb(bg[k]); }
+		target = exposure_scale * texc + (1.0f - tex3) * bgc;
+		if (!cfg.linear_colors) { target = linear_to_srgb(target); bgc = linear_to_srgb(bgc); }
 	} else {
-		for (int k = 0; k < 3; ++k) bg[k] = linear_to_srgb(bg[k]);
-		if (tex[3] > 0)
-			for (int k = 0; k < 3; ++k) target[k] = linear_to_srgb(exposure_scale * tex[k] / tex[3]) * tex[3] + (1.0f - tex[3]) * bg[k];
-		else
-			for (int k = 0; k < 3; ++k) target[k] = bg[k];
+		bgc = linear_to_srgb(bgc);
+		target = tex3 > 0 ? linear_to_srgb(exposure_scale * texc / tex3) * tex3 + (1.0f - tex3) * bgc : bgc;
 	}
-	if (cn == numsteps) { rr += t * bg[0]; rg += t * bg[1]; rb += t * bg[2]; }
-	float l[3], g[3];
-	loss_channel(target[0], rr, cfg.loss_type, &l[0], &g[0]);
-	loss_channel(target[1], rg, cfg.loss_type, &l[1], &g[1]);
-	loss_channel(target[2], rb, cfg.loss_type, &l[2], &g[2]);
+	float pred = ch == 0 ? rr : ch == 1 ? rg : rb;
+	if (cn == numsteps) pred += t * bgc;
+	float lc, gc;
+	loss_channel(target, pred, cfg.loss_type, &lc, &gc);
+	const float l1 = row_bcast<1>(lc), l2 = row_bcast<2>(lc), g1 = row_bcast<1>(gc), g2 = row_bcast<2>(gc);
+	const float p1 = row_bcast<1>(pred), p2 = row_bcast<2>(pred);
+	if (L != 0) return;
 	craw[i] = cn;
 	LossRay q;
-	q.mean_loss = (l[0] + l[1] + l[2]) / 3.0f;
-	q.grad[0] = g[0]; q.grad[1] = g[1]; q.grad[2] = g[2];
-	q.rgb_ray[0] = rr; q.rgb_ray[1] = rg; q.rgb_ray[2] = rb;
+	q.mean_loss = (lc + l1 + l2) / 3.0f;
+	q.grad[0] = gc; q.grad[1] = g1; q.grad[2] = g2;
+	q.rgb_ray[0] = pred; q.rgb_ray[1] = p1; q.rgb_ray[2] = p2;
 	q.pad = 0.f;
 	lr[i] = q;
 }
@@ -1146,25 +1195,35 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const ngp_nerf_config cfg, L
 	f16* dl = a.dloss_doutput + (size_t)compacted_base * 16;
 	float r2[3] = {0.f, 0.f, 0.f};
 	float t = 1.0f;
-	// the next chunk's loads are issued before this chunk's compositing chain (software pipelining)
-	float cc_next[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-	f16x4 o_next = {(f16)0.f, (f16)0.f, (f16)0.f, (f16)0.f};
-	if (L < cn) {
+	// software pipelining as in pass 1: NGP_LOSS2_PF chunks' loads in flight ahead of the compositing
+	float cb[NGP_LOSS2_PF][7];
+	f16x4 ob[NGP_LOSS2_PF];
 #pragma unroll
-		for (int k = 0; k < 7; ++k) cc_next[k] = ci[(size_t)L * 7 + k];
-		o_next = *(const f16x4*)(out + (size_t)L * a.out_stride);
+	for (uint32_t d = 0; d < NGP_LOSS2_PF; ++d) {
+		ob[d] = f16x4{(f16)0.f, (f16)0.f, (f16)0.f, (f16)0.f};
+#pragma unroll
+		for (int k = 0; k < 7; ++k) cb[d][k] = 0.f;
+		if (L + d * LG < cn) {
+#pragma unroll
+			for (int k = 0; k < 7; ++k) cb[d][k] = ci[(size_t)(L + d * LG) * 7 + k];
+			ob[d] = *(const f16x4*)(out + (size_t)(L + d * LG) * a.out_stride);
+		}
 	}
-	for (uint32_t c0 = 0; c0 < cn; c0 += LG) {
+	for (uint32_t cq = 0; cq < cn; cq += NGP_LOSS2_PF * LG)
+#pragma unroll
+	for (uint32_t d = 0; d < NGP_LOSS2_PF; ++d) {
+		const uint32_t c0 = cq + d * LG;
+		if (c0 >= cn) break;
 		const uint32_t jj = c0 + L;
 		const bool valid = jj < cn;
 		float cc[7];
 #pragma unroll
-		for (int k = 0; k < 7; ++k) cc[k] = cc_next[k];
-		const f16x4 o = o_next;
-		if (jj + LG < cn) {
+		for (int k = 0; k < 7; ++k) cc[k] = cb[d][k];
+		const f16x4 o = ob[d];
+		if (jj + NGP_LOSS2_PF * LG < cn) {
 #pragma unroll
-			for (int k = 0; k < 7; ++k) cc_next[k] = ci[(size_t)(jj + LG) * 7 + k];
-			o_next = *(const f16x4*)(out + (size_t)(jj + LG) * a.out_stride);
+			for (int k = 0; k < 7; ++k) cb[d][k] = ci[(size_t)(jj + NGP_LOSS2_PF * LG) * 7 + k];
+			ob[d] = *(const f16x4*)(out + (size_t)(jj + NGP_LOSS2_PF * LG) * a.out_stride);
 		}
 		float rgb[3] = {0.f, 0.f, 0.f}, alpha = 0.f, dt = 0.f;
 		if (valid) {
