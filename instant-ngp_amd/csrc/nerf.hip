@@ -1232,20 +1232,24 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const ngp_nerf_config cfg, L
 			const float density = network_to_density((float)o[3], cfg.density_activation);
 			alpha = 1.f - ngp_expf_fast(-density * dt);
 		}
-		// compositing in sample order; lane K keeps its weight, transmittance after it and rgb prefix
-		float my_w = 0.f, my_t = 0.f, my_r2[3] = {0.f, 0.f, 0.f};
+		// compositing in sample order; lane L stops after its own sample, so it ends with its weight, the
+		// transmittance after it and the rgb prefix through it; the chunk's totals come from lane 15
+		float my_w = 0.f;
 #define NGP_LOSS2_STEP(K)                                                                              \
 		{                                                                                              \
 			const float ak = row_bcast<K>(alpha), rk = row_bcast<K>(rgb[0]), gk = row_bcast<K>(rgb[1]), bk = row_bcast<K>(rgb[2]); \
-			if (c0 + K < cn) {                                                                         \
+			if (c0 + K < cn && K <= L) {                                                               \
 				const float weight = ak * t;                                                           \
 				r2[0] += weight * rk; r2[1] += weight * gk; r2[2] += weight * bk;                      \
 				t *= (1.0f - ak);                                                                      \
-				if (L == K) { my_w = weight; my_t = t; my_r2[0] = r2[0]; my_r2[1] = r2[1]; my_r2[2] = r2[2]; } \
+				my_w = weight;                                                                         \
 			}                                                                                          \
 		}
 		NGP_ROW_UNROLL16(NGP_LOSS2_STEP)
 #undef NGP_LOSS2_STEP
+		const float my_t = t, my_r2[3] = {r2[0], r2[1], r2[2]};
+		t = row_bcast<15>(t);  // a next chunk exists only if this one is full: lane 15 then took all 16 samples
+		r2[0] = row_bcast<15>(r2[0]); r2[1] = row_bcast<15>(r2[1]); r2[2] = row_bcast<15>(r2[2]);
 		if (!valid) continue;
 #pragma unroll
 		for (int k = 0; k < 7; ++k) co[(size_t)jj * 7 + k] = cc[k];
