@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--pipeline", type=int, default=1, help="1: next step's sampler under the training pass (default), 0: serial step")
     ap.add_argument("--option", action="append", default=[], help="model option key=value (ngp_model_set_option)")
     ap.add_argument("--fox", action="store_true", help="the fox capture (data/fox, tools/stage_fox.sh) instead of the stand-in")
+    ap.add_argument("--profiler", type=int, default=1, help="0: no engine HIP-event profiler in the measured steps (wall time only)")
     ap.add_argument("--sampler-stats", action="store_true",
                     help="read the march statistics of a -DNGP_SAMPLER_DIAG=4 build (NGP_ENGINE_LIB) over the measured steps")
     args = ap.parse_args()
@@ -57,7 +58,7 @@ def main():
     torch.cuda.synchronize()
     t_warm = time.time() - t0
     lib.ngp_profiler_reset()
-    lib.ngp_profiler_enable(1)
+    lib.ngp_profiler_enable(args.profiler)
     if args.sampler_stats:
         lib.ngp_debug_sampler_stats(None, 0)
     rays, pre, comp = [], [], []
