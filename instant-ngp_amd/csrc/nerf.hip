@@ -409,6 +409,10 @@ constexpr uint32_t LG = 16;  // lanes per ray in the loss passes: one DPP row
 #ifndef NGP_LOSS_PF
 #define NGP_LOSS_PF 2  // loss pass 1: chunks of 16 samples whose loads are in flight ahead of the compositing
 #endif
+#ifndef NGP_LOSS_SELECT
+#define NGP_LOSS_SELECT 1  // loss pass 1: compositing steps committed with selects instead of branches (pass 2
+                           // measured slower that way: its steps already run under a per-lane mask)
+#endif
 #ifndef NGP_LOSS2_PF
 #define NGP_LOSS2_PF 1  // loss pass 2: depth 2 takes 86 VGPRs (5 waves/SIMD) and measured 41 -> 45 us (Lego stand-in)
 #endif
@@ -1117,6 +1121,22 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 			cg = network_to_rgb((float)o[1], cfg.rgb_activation);
 			cb = network_to_rgb((float)o[2], cfg.rgb_activation);
 		}
+#if NGP_LOSS_SELECT
+		// branch-free step: the same operations, committed with selects (no exec-mask branch per sample)
+#define NGP_LOSS1_STEP(K)                                                                              \
+		{                                                                                              \
+			const float ak = row_bcast<K>(alpha), rk = row_bcast<K>(cr), gk = row_bcast<K>(cg), bk = row_bcast<K>(cb); \
+			const bool act = !stop && c + K < numsteps;                                                \
+			const bool low = t < eps;                                                                  \
+			stop = stop || (act && low);                                                               \
+			const bool upd = act && !low;                                                              \
+			const float weight = ak * t;                                                               \
+			const float nr = rr + weight * rk, ng = rg + weight * gk, nb = rb + weight * bk;           \
+			const float nt = t * (1.f - ak);                                                           \
+			rr = upd ? nr : rr; rg = upd ? ng : rg; rb = upd ? nb : rb; t = upd ? nt : t;              \
+			cn += upd ? 1u : 0u;                                                                       \
+		}
+#else
 #define NGP_LOSS1_STEP(K)                                                                              \
 		{                                                                                              \
 			const float ak = row_bcast<K>(alpha), rk = row_bcast<K>(cr), gk = row_bcast<K>(cg), bk = row_bcast<K>(cb); \
@@ -1130,6 +1150,7 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 				}                                                                                      \
 			}                                                                                          \
 		}
+#endif
 		NGP_ROW_UNROLL16(NGP_LOSS1_STEP)
 #undef NGP_LOSS1_STEP
 	}
