@@ -143,6 +143,33 @@ __device__ __forceinline__ uint32_t corner_index(const GridConst& c, uint32_t l,
 	return c.offsets[l] + idx;
 }
 
+// All 2^D corner indices of one level. A dense level with res^D <= T whose cell is in range (base < res:
+// positions in [0, 1]) has every corner index below 2 T, so index % T is min(id, id - T), and the corners
+// are corner 0's index plus constants: one branch per level instead of a modulo test per corner. Other
+// cells and levels take corner_index (the same integers).
+template <uint32_t D>
+__device__ __forceinline__ void corner_indices(const GridConst& c, uint32_t l, const uint32_t* base, uint32_t* idx) {
+	const uint32_t res = c.resolution[l], T = c.offsets[l + 1] - c.offsets[l];
+	uint64_t vol = res;
+#pragma unroll
+	for (uint32_t d = 1; d < D; ++d) vol *= res;
+	bool fast = !((c.hashed >> l) & 1u) && vol <= T;
+#pragma unroll
+	for (uint32_t d = 0; d < D; ++d) fast = fast && base[d] < res;
+	if (__builtin_expect(fast, 1)) {
+		const uint32_t r2 = res * res;
+		const uint32_t i0 = D == 3 ? base[0] + res * (base[1] + res * base[2]) : base[0] + res * base[1];
+#pragma unroll
+		for (uint32_t k = 0; k < (1u << D); ++k) {
+			const uint32_t id = i0 + (k & 1u) + (((k >> 1) & 1u) ? res : 0u) + ((D == 3 && ((k >> 2) & 1u)) ? r2 : 0u);
+			idx[k] = c.offsets[l] + min(id, id - T);
+		}
+	} else {
+#pragma unroll
+		for (uint32_t k = 0; k < (1u << D); ++k) idx[k] = corner_index<D>(c, l, base, k);
+	}
+}
+
 // Gather the 2^D corner entries of one level. The two corners of an x-edge are adjacent entries on
 // dense levels, and on hashed levels when base x is even (the hash's x prime is 1, so x+1 flips bit
 // 0 only): then both come from one 2F-wide load — half the gather requests of a dense level.
@@ -179,6 +206,35 @@ __device__ __forceinline__ void gather_corners(const GridConst& c, uint32_t l, c
 	} else {
 #pragma unroll
 		for (uint32_t k = 0; k < (1u << D); ++k) v[k] = *(const V*)(table + (size_t)corner_index<D>(c, l, base, k) * F);
+	}
+}
+// the same gather from precomputed corner indices (corner_indices)
+template <uint32_t D, uint32_t F>
+__device__ __forceinline__ void gather_corners_at(const uint32_t* idx, const f16* __restrict__ table, typename GridVec<F>::T* v) {
+	typedef typename GridVec<F>::T V;
+	typedef typename GridVec<F>::P P;
+	if constexpr (F == 2 || F == 4) {
+#pragma unroll
+		for (uint32_t k = 0; k < (1u << D); k += 2) {
+			const uint32_t i0 = idx[k], i1 = idx[k + 1];
+			// dense: i1 == i0 + 1 (unless wrapped); hashed with even base x: i1 == i0 ^ 1
+			const uint32_t lo_i = min(i0, i1);
+			if (max(i0, i1) == lo_i + 1u) {
+				const P p = *(const P*)(table + (size_t)lo_i * F);
+				V lo, hi;
+#pragma unroll
+				for (uint32_t f = 0; f < F; ++f) { lo[f] = p[f]; hi[f] = p[F + f]; }
+				const bool swap = i1 < i0;
+				v[k] = swap ? hi : lo;
+				v[k + 1] = swap ? lo : hi;
+			} else {
+				v[k] = *(const V*)(table + (size_t)i0 * F);
+				v[k + 1] = *(const V*)(table + (size_t)i1 * F);
+			}
+		}
+	} else {
+#pragma unroll
+		for (uint32_t k = 0; k < (1u << D); ++k) v[k] = *(const V*)(table + (size_t)idx[k] * F);
 	}
 }
 

@@ -122,6 +122,11 @@ __global__ void __launch_bounds__(256) k_grid_forward(const GridConst c, const G
 // zero-padded past L*F) is written with back-to-back 16-B stores, so each 64-B segment is filled by
 // one wave within a few cycles. Per-level 8-B stores spaced a level's gathers apart reach HBM as
 // partial segments (rocprof WRITE_SIZE 3.6x the 8.4 MB of a C2 batch, profiles/r01b_pmc_c2.json).
+#ifndef NGP_FWD_FASTIDX
+#define NGP_FWD_FASTIDX 1  // corner indices once per level (corner_indices), shared by the histogram and the gather;
+                           // F >= 4 only (C2 forward 28.9 -> 27.3 us; with 16 levels of F = 2 the index arrays cost
+                           // registers: C2' step 350 -> 393 us, profiles/r03bp)
+#endif
 template <uint32_t D, uint32_t F, bool HIST>
 __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const GridConst c, const GridFwdArgs a, const GridHist h) {
 	typedef typename FeatVec<F>::T V;
@@ -155,13 +160,23 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 		if (active) {
 			float frac[D]; uint32_t base[D];
 			level_setup<D>(c, l, x, frac, base);
-			if constexpr (HIST) {
-#pragma unroll
-				for (uint32_t k = 0; k < (1u << D); ++k)
-					atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
-			}
 			V v[1u << D];
-			gather_corners<D, F>(c, l, base, a.table, v);
+			if constexpr (NGP_FWD_FASTIDX && F >= 4) {
+				uint32_t cidx[1u << D];
+				corner_indices<D>(c, l, base, cidx);
+				if constexpr (HIST) {
+#pragma unroll
+					for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&hl[h.vb_base[l] + ((cidx[k] - c.offsets[l]) >> h.B)], 1u);
+				}
+				gather_corners_at<D, F>(cidx, a.table, v);
+			} else {
+				if constexpr (HIST) {
+#pragma unroll
+					for (uint32_t k = 0; k < (1u << D); ++k)
+						atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
+				}
+				gather_corners<D, F>(c, l, base, a.table, v);
+			}
 #pragma unroll
 			for (uint32_t k = 0; k < (1u << D); ++k) {
 				const float w = corner_weight<D>(frac, k);

@@ -35,6 +35,12 @@ namespace ngp {
 
 namespace {
 
+#ifndef NGP_SC_FASTIDX
+#define NGP_SC_FASTIDX 1  // scatter: corner indices of an in-range dense cell without a modulo test per corner
+#endif
+#ifndef NGP_ACC_SKIP0
+#define NGP_ACC_SKIP0 1   // accumulate: skip the LDS atomic of a zero contribution (a branch per feature)
+#endif
 constexpr uint32_t SC_THREADS = 256;
 constexpr uint32_t SC_BT = 1024;             // bucket/split blocks: 2 per CU by LDS, 32 waves to hide latency
 // (chunk, level) blocks: 512 samples with 512 threads where a chunk fills each bucket with long runs
@@ -344,9 +350,17 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 		}
 		float frac[D]; uint32_t base[D];
 		level_setup<D>(c, l, x, frac, base);
+#if NGP_SC_FASTIDX
+		uint32_t cidx[NC];
+		corner_indices<D>(c, l, base, cidx);
+#endif
 #pragma unroll
 		for (uint32_t k = 0; k < NC; ++k) {
+#if NGP_SC_FASTIDX
+			e[q][k] = cidx[k] - off_l;
+#else
 			e[q][k] = corner_index<D>(c, l, base, k) - off_l;
+#endif
 			r[q][k] = bucket_rank(lh, e[q][k] >> B, few_bits);
 			const float w = corner_weight<D>(frac, k);
 			if constexpr (F == 1) val[q][k] = to_f16(w * g[0]);
@@ -417,7 +431,11 @@ __device__ __forceinline__ void accumulate_items(unsigned long long* acc, uint32
 #pragma unroll
 				for (uint32_t q = 1; q < F; ++q) x = f == q ? (float)vv[q] : x;
 			}
+#if NGP_ACC_SKIP0
 			if (x != 0.f) atomicAdd(&acc[f * NEP + j], (unsigned long long)(long long)(x * FIX_SCALE));
+#else
+			atomicAdd(&acc[f * NEP + j], (unsigned long long)(long long)(x * FIX_SCALE));  // adding 0 is exact
+#endif
 		}
 	};
 	const uint32_t step = blockDim.x * U;
