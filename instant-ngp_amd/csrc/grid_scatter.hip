@@ -136,8 +136,10 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 		load_pos<D>(a, i, x);
 		float frac[D]; uint32_t base[D];
 		level_setup<D>(c, l, x, frac, base);
+		uint32_t cidx[1u << D];
+		corner_indices<D>(c, l, base, cidx);
 #pragma unroll
-		for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&h[(corner_index<D>(c, l, base, k) - off_l) >> B], 1u);
+		for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&h[(cidx[k] - off_l) >> B], 1u);
 	}
 	__syncthreads();
 	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) hist[(size_t)chunk * lv.vb_base[c.n_levels] + lv.vb_base[l] + j] = h[j];
