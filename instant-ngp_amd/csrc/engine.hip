@@ -447,6 +447,7 @@ struct ngp_trainer {
 	float *w32 = nullptr, *m1 = nullptr, *m2 = nullptr, *ema32 = nullptr;
 	f16 *w16 = nullptr, *inf16 = nullptr, *g16 = nullptr;
 	uint32_t* steps = nullptr;
+	float* bias_tab = nullptr;  // adam_bias_table for cfg.beta1/beta2 (built at creation)
 	// lazy-EMA layout (optimizer.h AdamRec), chosen for large tables: a step touches only the state of
 	// updated parameters; the inference (EMA) parameters are brought up to date when read
 	AdamRec* rec = nullptr;
@@ -466,7 +467,10 @@ struct ngp_trainer {
 	ngp_allreduce_fn allreduce = nullptr;  // gradient exchange inside captured steps (ngp_trainer_set_allreduce)
 	void* allreduce_user = nullptr;
 	uint32_t world = 1;
-	~ngp_trainer() { if (arena) (void)hipFree(arena); }
+	~ngp_trainer() {
+		if (arena) (void)hipFree(arena);
+		if (bias_tab) (void)hipFree(bias_tab);
+	}
 	void sync_device_step() { NGP_HIP(hipMemcpy(ctl, &step, sizeof(uint32_t), hipMemcpyHostToDevice)); }
 	// One optimizer step on stream s. step_base/step_add: see AdamState (optimizer.h).
 	// n_first: parameters [0, n_first) only (the MLP, when the grid's update ran fused in the backward)
@@ -477,7 +481,7 @@ struct ngp_trainer {
 		// launch refreshes with the step: set_learning_rate / set_option reach replayed steps too
 		AdamState st{w32, w16, g16, m1, m2, steps, ema32, inf16,
 		             own && m->frags_current ? (f16*)m->frags.p : nullptr, m->d_fragmap, step_base, step_add,
-		             step_base ? (const AdamConfig*)(ctl + CTL_CFG) : nullptr, rec};
+		             step_base ? (const AdamConfig*)(ctl + CTL_CFG) : nullptr, rec, bias_tab};
 		ProfScope ps("optimizer", s);
 		adam_ema_update(cfg, (uint32_t)(n_first ? n_first : n), (uint32_t)m->n_matrix(), loss_scale, st, s);
 		if (rec) inf_stale = true;
@@ -495,6 +499,7 @@ struct ngp_trainer {
 		const uint64_t go = model->grid_offset();
 		fa.w32 = w32 + go; fa.w16 = w16 + go; fa.rec = rec + go / 2;
 		fa.loss_scale = loss_scale; fa.cfg = cfg; fa.step_add = step;
+		fa.bias_tab = bias_tab;
 		return fa;
 	}
 };
@@ -943,6 +948,10 @@ int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, 
 		auto t = std::make_unique<ngp_trainer>();
 		t->model = m;
 		if (optimizer_json) parse_optimizer(Json::parse(optimizer_json), t->cfg);
+		// the betas are fixed for the trainer's lifetime (only the learning rate has a setter)
+		NGP_HIP(hipMalloc(&t->bias_tab, (size_t)BIAS_TAB_CAP * 2 * sizeof(float)));
+		adam_bias_table(t->bias_tab, t->cfg.beta1, t->cfg.beta2, nullptr);
+		NGP_HIP(hipDeviceSynchronize());
 		const uint64_t n = m->n_params;
 		t->n = n;
 		auto al = [](size_t b) { return (b + 255) / 256 * 256; };

@@ -40,8 +40,24 @@ struct AdamState {
 	const uint32_t* step_base; uint32_t step_add;
 	const AdamConfig* cfg_dev;  // non-null (captured steps): hyperparameters read from device memory
 	AdamRec* rec = nullptr;     // non-null: lazy-EMA layout (m1/m2/steps/ema32 unused)
+	const float* bias_tab = nullptr;  // adam_bias_table (nullable)
 };
 // ---- device helpers shared by optimizer.hip and the fused update in the grid backward ----------
+// Adam's bias correction depends on the parameter's own step s only: the factors sqrtf(1 - beta2^s) and
+// 1 - beta1^s are tabulated once per trainer for s < BIAS_TAB_CAP by the same device powf/sqrtf
+// (adam_bias_table), so the per-parameter update reads two floats instead of evaluating two powf; the
+// step size lr * A / B keeps its operations and order, so the result is bit-identical. Layout: float2
+// per s; entry 0 holds the betas the table was built for (a mismatch falls back to powf).
+constexpr uint32_t BIAS_TAB_CAP = 1u << 20;
+__device__ __forceinline__ float adam_step_size(const AdamConfig& c, float lr, uint32_t sk, const float* tab) {
+	typedef float f32x2_t __attribute__((ext_vector_type(2)));
+	if (tab && sk < BIAS_TAB_CAP && tab[0] == c.beta1 && tab[1] == c.beta2) {
+		const f32x2_t q = ((const f32x2_t*)tab)[sk];
+		return lr * q[0] / q[1];
+	}
+	return lr * sqrtf(1.f - powf(c.beta2, (float)sk)) / (1.f - powf(c.beta1, (float)sk));
+}
+void adam_bias_table(float* tab, float beta1, float beta2, hipStream_t s);
 // Learning rate of optimizer step `step` (ExponentialDecay wrapper).
 __device__ __forceinline__ float lr_schedule(const AdamConfig& c, uint32_t step) {
 	float r = c.lr;
@@ -70,6 +86,7 @@ struct FusedAdam {
 	const AdamConfig* cfg_dev = nullptr;
 	const uint32_t* step_base = nullptr;
 	uint32_t step_add = 0;
+	const float* bias_tab = nullptr;
 };
 // One parameter pair's state between the load and the update (callers issue several pairs' loads
 // before the first update: the record reads are the latency to hide).
@@ -113,7 +130,7 @@ __device__ __forceinline__ void fused_adam_store(const FusedAdam& fa, uint32_t r
 		m2[k] = vv;
 		const uint32_t sk = steps[k] + 1;
 		steps[k] = sk;
-		const float lr_s = lr * sqrtf(1.f - powf(c.beta2, (float)sk)) / (1.f - powf(c.beta1, (float)sk));
+		const float lr_s = adam_step_size(c, lr, sk, fa.bias_tab);
 		w[k] = w[k] - lr_s / (sqrtf(vv) + c.eps) * mm;
 		if (d > 0.f) ema[k] = d * ema[k] + (1.f - d) * w[k];
 		done[k] = step + 1;

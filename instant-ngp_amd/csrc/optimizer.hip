@@ -15,6 +15,18 @@ namespace ngp {
 // from device memory (written once per graph launch by k_set_step) plus the step's index in the graph,
 // so no per-step counter kernel is needed. lr_schedule, ema_catch_up: optimizer.h.
 
+__global__ void k_adam_bias_table(float* __restrict__ tab, float beta1, float beta2) {
+	const uint32_t sk = blockIdx.x * blockDim.x + threadIdx.x;
+	if (sk >= BIAS_TAB_CAP) return;
+	if (sk == 0) { tab[0] = beta1; tab[1] = beta2; return; }
+	tab[2 * sk] = sqrtf(1.f - powf(beta2, (float)sk));
+	tab[2 * sk + 1] = 1.f - powf(beta1, (float)sk);
+}
+void adam_bias_table(float* tab, float beta1, float beta2, hipStream_t s) {
+	k_adam_bias_table<<<BIAS_TAB_CAP / 256, 256, 0, s>>>(tab, beta1, beta2);
+	NGP_HIP(hipGetLastError());
+}
+
 __global__ void k_adam_ema(const uint32_t i0, const uint32_t n, const uint32_t n_matrix, const float loss_scale, const AdamConfig c_arg,
                            const AdamState st) {
 	const AdamConfig c = st.cfg_dev ? *st.cfg_dev : c_arg;
@@ -32,7 +44,7 @@ __global__ void k_adam_ema(const uint32_t i0, const uint32_t n, const uint32_t n
 			st.m2[i] = vv;
 			const uint32_t s = st.steps[i] + 1;
 			st.steps[i] = s;
-			const float lr_s = lr * sqrtf(1.f - powf(c.beta2, (float)s)) / (1.f - powf(c.beta1, (float)s));
+			const float lr_s = adam_step_size(c, lr, s, st.bias_tab);
 			w = w - lr_s / (sqrtf(vv) + c.eps) * mm;
 			st.w32[i] = w;
 			const f16 h = (f16)w;
@@ -91,7 +103,7 @@ __global__ void __launch_bounds__(256) k_adam_ema4(const uint32_t n4, const uint
 				m2[k] = vv;
 				const uint32_t sk = sv[k] + 1;
 				sv[k] = sk;
-				const float lr_s = lr * sqrtf(1.f - powf(c.beta2, (float)sk)) / (1.f - powf(c.beta1, (float)sk));
+				const float lr_s = adam_step_size(c, lr, sk, st.bias_tab);
 				w[k] = w[k] - lr_s / (sqrtf(vv) + c.eps) * mm;
 			}
 			wh[k] = (f16)w[k];
@@ -186,7 +198,7 @@ __device__ __forceinline__ void lazy_update(const AdamState& st, const AdamConfi
 			rc.m2[k] = vv;
 			const uint32_t sk = rc.steps[k] + 1;
 			rc.steps[k] = sk;
-			const float lr_s = lr * sqrtf(1.f - powf(c.beta2, (float)sk)) / (1.f - powf(c.beta1, (float)sk));
+			const float lr_s = adam_step_size(c, lr, sk, st.bias_tab);
 			w[p] = w[p] - lr_s / (sqrtf(vv) + c.eps) * mm;
 			if (d > 0.f) rc.ema[k] = d * rc.ema[k] + (1.f - d) * w[p];
 			rc.done[k] = step + 1;
