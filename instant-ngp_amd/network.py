@@ -270,10 +270,19 @@ class Trainer:
         L = lib()
         self.gradients = wrap_device(L.ngp_trainer_gradients(h), n, torch.float16)
         self.params = wrap_device(L.ngp_trainer_params(h), n, torch.float16)
-        self.params_full_precision = wrap_device(L.ngp_trainer_params_full_precision(h), n, torch.float32)
 
     def __del__(self, _d=_destroy):
         _d(self, "ngp_trainer_destroy")
+
+    @property
+    def params_full_precision(self):
+        """The fp32 master weights. A large-table trainer keeps them in its optimizer records (optimizer.h
+        AdamRec::w) and ngp_trainer_params_full_precision refreshes this mirror first; write new weights with
+        set_params_full_precision (tcnn's Trainer::set_params_full_precision, testbed.cu:4146)."""
+        p = lib().ngp_trainer_params_full_precision(self.handle)
+        if not p:
+            raise NgpError(lib().ngp_last_error().decode())
+        return wrap_device(p, self.model.n_params, torch.float32)
 
     @property
     def inference_params(self):
