@@ -170,7 +170,9 @@ int ngp_trainer_optimizer_step(ngp_trainer* t, void* stream, float loss_scale);
 void* ngp_trainer_gradients(ngp_trainer* t);               /* fp16 [n_params], the DP all-reduce buffer */
 void* ngp_trainer_params(ngp_trainer* t);                  /* fp16 [n_params] */
 void* ngp_trainer_inference_params(ngp_trainer* t);        /* fp16 [n_params] (EMA when configured) */
-float* ngp_trainer_params_full_precision(ngp_trainer* t);  /* fp32 [n_params] */
+/* fp32 [n_params]; large-table trainers keep the master weights in their optimizer records and refresh this
+   mirror on each call (synchronizes the device; NULL + ngp_last_error on failure) */
+float* ngp_trainer_params_full_precision(ngp_trainer* t);
 uint32_t ngp_trainer_step(const ngp_trainer* t);
 float ngp_trainer_learning_rate(const ngp_trainer* t);     /* optimizer->learning_rate() (testbed_nerf.cu:3771) */
 int ngp_trainer_set_learning_rate(ngp_trainer* t, float lr);

@@ -452,6 +452,15 @@ struct ngp_trainer {
 	// updated parameters; the inference (EMA) parameters are brought up to date when read
 	AdamRec* rec = nullptr;
 	bool inf_stale = false;
+	// lazy layout: the fp32 weights live in the records (AdamRec::w); w32 is their mirror, stale after a step
+	bool w32_stale = false;
+	void sync_w32() {
+		if (!rec || !w32_stale) return;
+		NGP_HIP(hipDeviceSynchronize());  // the optimizer may still run on a caller's non-blocking stream
+		adam_rec_weights((uint32_t)n, rec, w32, false, nullptr);
+		NGP_HIP(hipDeviceSynchronize());
+		w32_stale = false;
+	}
 	void materialize(hipStream_t s, bool force = false) {
 		if (!rec || (!inf_stale && !force)) return;
 		AdamState st{w32, w16, g16, nullptr, nullptr, nullptr, nullptr, inf16, nullptr, nullptr, nullptr, 0, nullptr, rec};
@@ -484,7 +493,7 @@ struct ngp_trainer {
 		             step_base ? (const AdamConfig*)(ctl + CTL_CFG) : nullptr, rec, bias_tab};
 		ProfScope ps("optimizer", s);
 		adam_ema_update(cfg, (uint32_t)(n_first ? n_first : n), (uint32_t)m->n_matrix(), loss_scale, st, s);
-		if (rec) inf_stale = true;
+		if (rec) inf_stale = w32_stale = true;
 	}
 	// The grid's lazy update fused into the backward (model option fuse_opt): lazy layout, no gradient
 	// exchange (the all-reduce needs the stored gradients), the sorted backward, F >= 2, and an MLP
@@ -497,7 +506,7 @@ struct ngp_trainer {
 	FusedAdam fused_update(float loss_scale) const {
 		FusedAdam fa;
 		const uint64_t go = model->grid_offset();
-		fa.w32 = w32 + go; fa.w16 = w16 + go; fa.rec = rec + go / 2;
+		fa.w16 = w16 + go; fa.rec = rec + go / 2;
 		fa.loss_scale = loss_scale; fa.cfg = cfg; fa.step_add = step;
 		fa.bias_tab = bias_tab;
 		return fa;
@@ -1130,7 +1139,7 @@ int ngp_graph_launch(ngp_graph* g, void* stream) {
 		if (g->steps_per_launch) set_device_ctl(g->trainer->ctl, g->trainer->step, g->trainer->cfg, S(stream));
 		NGP_HIP(hipGraphLaunch(g->exec, S(stream)));
 		g->trainer->step += g->steps_per_launch;
-		if (g->steps_per_launch && g->trainer->rec) g->trainer->inf_stale = true;
+		if (g->steps_per_launch && g->trainer->rec) g->trainer->inf_stale = g->trainer->w32_stale = true;
 	});
 }
 
@@ -1152,7 +1161,18 @@ void* ngp_trainer_inference_params(ngp_trainer* t) {
 	}
 	return t->cfg.ema_decay > 0.f ? t->inf16 : t->w16;
 }
-float* ngp_trainer_params_full_precision(ngp_trainer* t) { return t ? t->w32 : nullptr; }
+// Lazy layout: the mirror of the records' weights, refreshed here (a read accessor: writes into it do not reach
+// the records; set_params_full_precision does, as in tcnn).
+float* ngp_trainer_params_full_precision(ngp_trainer* t) {
+	if (!t) return nullptr;
+	try {
+		t->sync_w32();
+	} catch (const std::exception& e) {
+		g_last_error = e.what();
+		return nullptr;
+	}
+	return t->w32;
+}
 uint32_t ngp_trainer_step(const ngp_trainer* t) { return t ? t->step : 0; }
 float ngp_trainer_learning_rate(const ngp_trainer* t) { return t ? t->cfg.lr_at(t->step) : 0.f; }
 int ngp_trainer_set_learning_rate(ngp_trainer* t, float lr) {
@@ -1179,8 +1199,9 @@ int ngp_trainer_set_params_full_precision(ngp_trainer* t, const float* params_ho
 		NGP_HIP(hipMemcpy(t->w32, params_host, n * 4, hipMemcpyHostToDevice));
 		k_f32_to_f16<<<div_round_up(n, 256), 256>>>(t->w32, t->w16, t->inf16, n);
 		NGP_HIP(hipGetLastError());
+		if (t->rec) adam_rec_weights((uint32_t)n, t->rec, t->w32, true, nullptr);
 		NGP_HIP(hipDeviceSynchronize());
-		t->inf_stale = false;  // inference parameters = the new weights, as in the eager layout
+		t->inf_stale = t->w32_stale = false;  // inference parameters = the new weights, as in the eager layout
 		t->bind_model();
 	});
 }
@@ -1196,6 +1217,7 @@ int ngp_trainer_serialize(ngp_trainer* t, void* buf, uint64_t* size) {
 		const uint64_t hdr[4] = {0x4e47504d49333535ULL /* "NGPMI355" */, 1, t->n, t->step};
 		memcpy(p, hdr, 32); p += 32;
 		NGP_HIP(hipDeviceSynchronize());
+		t->sync_w32();
 		DevBuf soa;
 		float *m1 = t->m1, *m2 = t->m2, *ema32 = t->ema32;
 		uint32_t* steps = t->steps;
@@ -1236,8 +1258,11 @@ int ngp_trainer_deserialize(ngp_trainer* t, const void* buf, uint64_t size) {
 			NGP_HIP(hipMemcpy(dst, p, t->n * 4, hipMemcpyHostToDevice));
 			p += t->n * 4;
 		}
-		if (t->rec) adam_soa_to_rec((uint32_t)t->n, m1, m2, ema32, steps, t->step, t->rec, nullptr);
-		t->inf_stale = false;  // inference parameters = the restored weights (below), as in the eager layout
+		if (t->rec) {
+			adam_soa_to_rec((uint32_t)t->n, m1, m2, ema32, steps, t->step, t->rec, nullptr);
+			adam_rec_weights((uint32_t)t->n, t->rec, t->w32, true, nullptr);
+		}
+		t->inf_stale = t->w32_stale = false;  // inference parameters = the restored weights (below), as in the eager layout
 		k_f32_to_f16<<<div_round_up(t->n, 256), 256>>>(t->w32, t->w16, t->inf16, t->n);
 		NGP_HIP(hipGetLastError());
 		NGP_HIP(hipDeviceSynchronize());

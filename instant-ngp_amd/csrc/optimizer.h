@@ -23,12 +23,15 @@ struct AdamConfig {
 // grid gradient) keeps its weight, so its missing EMA steps are the same recurrence on the same
 // weight and are applied, in order and with the same fp32 operations, when it is next updated or when
 // the inference (EMA) parameters are read (ema_materialize): bit-identical to the eager update.
+// The fp32 master weights of the pair live in the record too (`w`): an update then reads and writes one
+// record instead of the record plus a separate line of the w32 array. The trainer's w32 array is a
+// mirror in this layout, refreshed when it is read (adam_rec_weights).
 struct AdamRec {
 	float m1[2], m2[2];
 	uint32_t steps[2];
 	float ema[2];
 	uint32_t done[2];
-	uint32_t pad[2];
+	float w[2];
 };
 static_assert(sizeof(AdamRec) == 48, "AdamRec is three 16-B words (64-B records measured slower: 976 -> 1019 us at C5)");
 
@@ -78,9 +81,8 @@ __device__ __forceinline__ float ema_catch_up(float e, float w, float d, uint32_
 // read per step). Pointers are offset to the grid's first parameter (an even index: records are pairs).
 // Same fp32 operations, in the same order, as k_adam_lazy4's lazy_update for a non-matrix pair.
 struct FusedAdam {
-	float* w32 = nullptr;
 	f16* w16 = nullptr;
-	AdamRec* rec = nullptr;  // null: no fused update (the backward stores the gradient)
+	AdamRec* rec = nullptr;  // null: no fused update (the backward stores the gradient); holds the fp32 weights
 	float loss_scale = 1.f;
 	AdamConfig cfg;
 	const AdamConfig* cfg_dev = nullptr;
@@ -94,7 +96,6 @@ struct FusedPair {
 	float g[2];
 	bool act[2];
 	f32x4 q0, q1, q2;
-	float w[2];
 };
 __device__ __forceinline__ bool fused_adam_load(const FusedAdam& fa, uint32_t r, f16 g0h, f16 g1h, FusedPair& p) {
 	p.g[0] = (float)g0h / fa.loss_scale;
@@ -102,10 +103,6 @@ __device__ __forceinline__ bool fused_adam_load(const FusedAdam& fa, uint32_t r,
 	p.act[0] = p.g[0] != 0.f;  // grid parameters: a zero gradient skips the parameter
 	p.act[1] = p.g[1] != 0.f;
 	if (!p.act[0] && !p.act[1]) return false;
-	typedef float f32x2 __attribute__((ext_vector_type(2)));
-	const f32x2 w = *(const f32x2*)(fa.w32 + 2 * (size_t)r);
-	p.w[0] = w[0];
-	p.w[1] = w[1];
 	const f32x4* rp = (const f32x4*)(fa.rec + r);
 	p.q0 = rp[0]; p.q1 = rp[1]; p.q2 = rp[2];
 	return true;
@@ -118,7 +115,7 @@ __device__ __forceinline__ void fused_adam_store(const FusedAdam& fa, uint32_t r
 	float m1[2] = {p.q0[0], p.q0[1]}, m2[2] = {p.q0[2], p.q0[3]}, ema[2] = {p.q1[2], p.q1[3]};
 	uint32_t steps[2] = {__float_as_uint(p.q1[0]), __float_as_uint(p.q1[1])};
 	uint32_t done[2] = {__float_as_uint(p.q2[0]), __float_as_uint(p.q2[1])};
-	float w[2] = {p.w[0], p.w[1]};
+	float w[2] = {p.q2[2], p.q2[3]};
 #pragma unroll
 	for (int k = 0; k < 2; ++k) {
 		if (!p.act[k]) continue;
@@ -138,9 +135,7 @@ __device__ __forceinline__ void fused_adam_store(const FusedAdam& fa, uint32_t r
 	f32x4* rp = (f32x4*)(fa.rec + r);
 	rp[0] = f32x4{m1[0], m1[1], m2[0], m2[1]};
 	rp[1] = f32x4{__uint_as_float(steps[0]), __uint_as_float(steps[1]), ema[0], ema[1]};
-	rp[2] = f32x4{__uint_as_float(done[0]), __uint_as_float(done[1]), 0.f, 0.f};
-	typedef float f32x2 __attribute__((ext_vector_type(2)));
-	*(f32x2*)(fa.w32 + 2 * (size_t)r) = f32x2{w[0], w[1]};
+	rp[2] = f32x4{__uint_as_float(done[0]), __uint_as_float(done[1]), w[0], w[1]};
 	*(f16x2*)(fa.w16 + 2 * (size_t)r) = f16x2{(f16)w[0], (f16)w[1]};
 }
 __device__ __forceinline__ void fused_adam_pair(const FusedAdam& fa, uint32_t r, f16 g0h, f16 g1h) {
@@ -161,5 +156,7 @@ void ema_materialize(const AdamConfig& c, uint32_t n, uint32_t steps_done, const
 void adam_rec_to_soa(uint32_t n, const AdamRec* rec, float* m1, float* m2, float* ema32, uint32_t* steps, hipStream_t s);
 void adam_soa_to_rec(uint32_t n, const float* m1, const float* m2, const float* ema32, const uint32_t* steps, uint32_t done,
                      AdamRec* rec, hipStream_t s);
+// Lazy layout: the records' fp32 weights to the w32 mirror (to_rec false) or from it (to_rec true).
+void adam_rec_weights(uint32_t n, AdamRec* rec, float* w32, bool to_rec, hipStream_t s);
 
 }  // namespace ngp

@@ -147,7 +147,6 @@ struct LazyGroup {
 	uint32_t i0;
 	bool act[4], any[2];
 	float g[4];
-	f32x4 w;
 	f32x4 q[2][3];
 };
 
@@ -161,7 +160,6 @@ __device__ __forceinline__ void lazy_load(const AdamState& st, uint32_t i0, uint
 	}
 	G.any[0] = G.act[0] || G.act[1];
 	G.any[1] = G.act[2] || G.act[3];
-	if (G.any[0] || G.any[1]) G.w = *(const f32x4*)(st.w32 + i0);
 #pragma unroll
 	for (int r = 0; r < 2; ++r) {
 		if (!G.any[r]) continue;
@@ -175,10 +173,12 @@ __device__ __forceinline__ void lazy_update(const AdamState& st, const AdamConfi
 	const uint32_t i0 = G.i0;
 	const float lr = lr_schedule(c, step);
 	const float d = c.ema_decay;
-	f32x4 w = G.w;
+	float w[4];
 #pragma unroll
 	for (int r = 0; r < 2; ++r) {
 		if (!G.any[r]) continue;
+		w[2 * r] = G.q[r][2][2];  // the pair's fp32 weights (AdamRec::w)
+		w[2 * r + 1] = G.q[r][2][3];
 		AdamRec rc;
 		rc.m1[0] = G.q[r][0][0]; rc.m1[1] = G.q[r][0][1]; rc.m2[0] = G.q[r][0][2]; rc.m2[1] = G.q[r][0][3];
 		rc.steps[0] = __float_as_uint(G.q[r][1][0]); rc.steps[1] = __float_as_uint(G.q[r][1][1]);
@@ -206,20 +206,17 @@ __device__ __forceinline__ void lazy_update(const AdamState& st, const AdamConfi
 		f32x4* rp = (f32x4*)(st.rec + (i0 >> 1) + r);
 		rp[0] = f32x4{rc.m1[0], rc.m1[1], rc.m2[0], rc.m2[1]};
 		rp[1] = f32x4{__uint_as_float(rc.steps[0]), __uint_as_float(rc.steps[1]), rc.ema[0], rc.ema[1]};
-		rp[2] = f32x4{__uint_as_float(rc.done[0]), __uint_as_float(rc.done[1]), 0.f, 0.f};
+		rp[2] = f32x4{__uint_as_float(rc.done[0]), __uint_as_float(rc.done[1]), w[2 * r], w[2 * r + 1]};
+		*(f16x2*)(st.w16 + i0 + 2 * r) = f16x2{(f16)w[2 * r], (f16)w[2 * r + 1]};
 	}
-	f16x4 wh;
-#pragma unroll
-	for (int k = 0; k < 4; ++k) wh[k] = (f16)w[k];
-	*(f32x4*)(st.w32 + i0) = w;
-	*(f16x4*)(st.w16 + i0) = wh;
 	if (st.frags && i0 < n_matrix) {
 #pragma unroll
 		for (int k = 0; k < 4; ++k) {
 			if (i0 + k >= n_matrix || !G.act[k]) continue;
 			const uint32_t q0 = st.fragmap[2 * (i0 + k)], q1 = st.fragmap[2 * (i0 + k) + 1];
-			if (q0 != ~0u) st.frags[q0] = wh[k];
-			if (q1 != ~0u) st.frags[q1] = wh[k];
+			const f16 wh = (f16)w[k];
+			if (q0 != ~0u) st.frags[q0] = wh;
+			if (q1 != ~0u) st.frags[q1] = wh;
 		}
 	}
 }
@@ -248,7 +245,7 @@ __global__ void k_ema_materialize(uint32_t n, float d, uint32_t steps_done, cons
 	float e = rp->ema[k];
 	const uint32_t done = rp->done[k];
 	if (done < steps_done) {
-		e = ema_catch_up(e, st.w32[i], d, done, steps_done);
+		e = ema_catch_up(e, rp->w[k], d, done, steps_done);
 		rp->ema[k] = e;
 		rp->done[k] = steps_done;
 	}
@@ -270,7 +267,13 @@ __global__ void k_soa_to_rec(uint32_t n, const float* m1, const float* m2, const
 	AdamRec& r = rec[i >> 1];
 	const uint32_t k = i & 1u;
 	r.m1[k] = m1[i]; r.m2[k] = m2[i]; r.ema[k] = ema32[i]; r.steps[k] = steps[i]; r.done[k] = done;
-	r.pad[k] = 0;
+}
+
+__global__ void k_rec_weights(uint32_t n, AdamRec* rec, float* w32, bool to_rec) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i >= n) return;
+	if (to_rec) rec[i >> 1].w[i & 1u] = w32[i];
+	else w32[i] = rec[i >> 1].w[i & 1u];
 }
 
 void ema_materialize(const AdamConfig& c, uint32_t n, uint32_t steps_done, const AdamState& st, hipStream_t s) {
@@ -287,6 +290,11 @@ void adam_rec_to_soa(uint32_t n, const AdamRec* rec, float* m1, float* m2, float
 void adam_soa_to_rec(uint32_t n, const float* m1, const float* m2, const float* ema32, const uint32_t* steps, uint32_t done,
                      AdamRec* rec, hipStream_t s) {
 	if (n) k_soa_to_rec<<<div_round_up(n, 256), 256, 0, s>>>(n, m1, m2, ema32, steps, done, rec);
+	NGP_HIP(hipGetLastError());
+}
+
+void adam_rec_weights(uint32_t n, AdamRec* rec, float* w32, bool to_rec, hipStream_t s) {
+	if (n) k_rec_weights<<<div_round_up(n, 256), 256, 0, s>>>(n, rec, w32, to_rec);
 	NGP_HIP(hipGetLastError());
 }
 
