@@ -911,6 +911,16 @@ void ngp_ctx_destroy(ngp_ctx* ctx) { delete ctx; }
 
 int ngp_forward_backward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
                          uint32_t output_stride, const void* dL_doutput, uint32_t dL_stride, int grad_mode) {
+	return ngp::forward_backward_with(m, stream, n, input, input_stride, output, output_stride, dL_doutput, dL_stride, grad_mode,
+	                                  nullptr);
+}
+}  // extern "C"
+
+// ngp_forward_backward, optionally with the grid's lazy optimizer update fused into the backward (fopt:
+// captured training steps, ngp_trainer_fused_update)
+int ngp::forward_backward_with(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                               uint32_t output_stride, const void* dL_doutput, uint32_t dL_stride, int grad_mode,
+                               const FusedAdam* fopt) {
 	NGP_ARG(m && (n == 0 || (input && dL_doutput)));
 	NGP_TRY({
 		if (n == 0) return NGP_OK;
@@ -921,13 +931,16 @@ int ngp_forward_backward(ngp_model* m, void* stream, uint32_t n, const float* in
 		if (m->fused_training_ok()) {
 			// no encoding pass: the MLP kernel encodes, the sorted backward counts its own histogram
 			m->sc_hist_done = false;
-			m->train_pass(S(stream), n, input, input_stride, nullptr, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode);
+			m->train_pass(S(stream), n, input, input_stride, nullptr, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode,
+			              BwdExtra{}, fopt);
 		} else {
 			m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, false, true);
-			m->train_pass(S(stream), n, input, input_stride, e, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode);
+			m->train_pass(S(stream), n, input, input_stride, e, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode,
+			              BwdExtra{}, fopt);
 		}
 	});
 }
+extern "C" {
 
 // ---- trainer ------------------------------------------------------------------------------
 static void parse_optimizer(const Json& j, AdamConfig& c) {
@@ -965,9 +978,10 @@ int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, 
 		t->n = n;
 		auto al = [](size_t b) { return (b + 255) / 256 * 256; };
 		const size_t b32 = al(n * 4), b16 = al(n * 2);
-		// lazy-EMA records for large tables (C5: 105 M parameters, ~28 % updated per step); the eager
-		// arrays otherwise. NGP_LAZY_EMA=0/1 forces the choice.
-		bool lazy = n >= (1ull << 25);
+		// lazy-EMA records for large tables (C5: 105 M parameters, ~28 % updated per step; C2' 13 M: captured
+		// step 351 -> 330 us with the fused update, profiles/r03bw); the eager arrays otherwise (C2, 3.3 M
+		// parameters, ~96 % updated: 143.5 -> 145.5 us lazy). NGP_LAZY_EMA=0/1 forces the choice.
+		bool lazy = n >= (1ull << 23);
 		if (const char* e = getenv("NGP_LAZY_EMA")) lazy = atoi(e) != 0;
 		lazy = lazy && n % 4 == 0;
 		const size_t brec = al(n / 2 * sizeof(AdamRec));
@@ -1085,10 +1099,20 @@ int ngp::capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, co
 		auto g = std::make_unique<ngp_graph>();
 		g->trainer = t;
 		g->steps_per_launch = with_optimizer ? n_steps : 0;
+		// the grid's update inside the backward where possible (lazy layout, no exchange): as training_step
+		const bool fuse = with_optimizer && !allreduce && t->fused_update_ok(n);
 		NGP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
 		int rc = NGP_OK;
 		for (uint32_t k = 0; k < n_steps && rc == NGP_OK; ++k) {
-			rc = ngp_forward_backward(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE);
+			FusedAdam fa;
+			if (fuse) {
+				fa = t->fused_update(loss_scale * (float)world);
+				fa.step_base = t->ctl;  // step = device base (set per launch) + k, hyperparameters from the ctl block
+				fa.step_add = k;
+				fa.cfg_dev = (const AdamConfig*)(t->ctl + CTL_CFG);
+			}
+			rc = forward_backward_with(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE,
+			                           fuse ? &fa : nullptr);
 			if (rc == NGP_OK && allreduce) {
 				rc = allreduce(allreduce_user, t->g16, t->n, NGP_DTYPE_F16, NGP_REDUCE_SUM, stream);
 				if (rc != NGP_OK && g_last_error.empty()) g_last_error = "gradient all-reduce failed";
@@ -1096,7 +1120,7 @@ int ngp::capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, co
 			if (rc == NGP_OK && with_optimizer) {
 				try {
 					// the summed gradient of `world` ranks: mean via the loss scale
-					t->run_step(s, loss_scale * (float)world, t->ctl, k);  // step = device base (set per launch) + k
+					t->run_step(s, loss_scale * (float)world, t->ctl, k, fuse ? m->n_matrix() : 0);  // step = device base + k
 				} catch (const std::exception& e) {
 					g_last_error = e.what();
 					rc = NGP_ERROR;

@@ -1,7 +1,7 @@
 """The lazy-EMA optimizer layout (optimizer.h AdamRec: per-pair records, EMA of untouched entries
 completed when next updated or when the inference parameters are read) must train bit for bit like the
 eager Ema(ExponentialDecay(Adam)) update of tcnn's chain (configs/nerf/base.json:5-22;
-configs/sdf/base.json). Large tables (>= 2^25 parameters, BASELINE C5) use it by default; NGP_LAZY_EMA
+configs/sdf/base.json). Large tables (>= 2^23 parameters: BASELINE C5, C2') use it by default; NGP_LAZY_EMA
 forces either layout here, on tables small enough to compare quickly, with batches small enough that
 most grid entries get no gradient in a step (the lazy path's whole point)."""
 import os
@@ -178,3 +178,41 @@ def test_fused_optimizer_training_step_bitwise(pkg):
             np.testing.assert_array_equal(a, e)
         assert b == runs["eager"][3], f"{name}: serialized optimizer state differs"
         assert st == runs["eager"][4] == 20
+
+
+@pytest.mark.parametrize("kind", ["nerf", "sdf"])
+def test_fused_optimizer_captured_steps_bitwise(pkg, kind):
+    """Captured training steps (ngp_trainer_capture_training_step: forward_backward + optimizer_step replayed
+    as one HIP graph) on the lazy layout run the grid's update inside the bucketed backward too, with the step
+    and hyperparameters read from the trainer's device block: bit for bit the eager layout's graph, across
+    launches, a learning-rate change between launches, and a mid-run read of the inference parameters."""
+    runs = {}
+    for name, lazy, fuse in (("eager", False, 0), ("lazy", True, 0), ("fused", True, 1)):
+        net, tr = make_trainer(pkg, kind, lazy)
+        net.set_option("fuse_opt", fuse)
+        s = torch.cuda.Stream()
+        snaps = []
+        graphs = []
+        for n, step in ((1 << 15, 1), (4096, 0)):  # the larger batch first: its workspaces serve both graphs
+            x, dl = batch(kind, n, step)
+            with torch.cuda.stream(s):
+                graphs.append((tr.capture_training_step(x, dl, 128.0, n_steps=2, stream=s), x, dl))
+        for it in range(6):
+            graphs[it % 3 == 2][0].launch(s)
+            if it == 3:
+                s.synchronize()
+                snaps.append(tr.inference_params.cpu().numpy().view(np.uint16).copy())
+                tr.learning_rate = tr.learning_rate * 0.5
+        s.synchronize()
+        snaps.append(tr.inference_params.cpu().numpy().view(np.uint16).copy())
+        runs[name] = (tr.params_full_precision.cpu().numpy().view(np.uint32).copy(),
+                      tr.params.cpu().numpy().view(np.uint16).copy(), snaps, tr.serialize(), tr.step)
+        del graphs, net, tr
+    for name in ("lazy", "fused"):
+        w, p, sn, b, st = runs[name]
+        np.testing.assert_array_equal(w, runs["eager"][0])
+        np.testing.assert_array_equal(p, runs["eager"][1])
+        for a, e in zip(sn, runs["eager"][2]):
+            np.testing.assert_array_equal(a, e)
+        assert b == runs["eager"][3], f"{name}: serialized optimizer state differs"
+        assert st == runs["eager"][4] == 12
