@@ -50,6 +50,7 @@ constexpr uint32_t SC_BT = 1024;             // bucket/split blocks: 2 per CU by
 // 2048-sample chunks measured slower, 372 us).
 constexpr size_t SC_LDS_BYTES = 64 * 1024;   // one bucket's int64 accumulators (+ one pad entry per feature plane)
 constexpr size_t SC_LDS_PAD_BYTES = 8 * 8;  // up to F = 8 planes
+constexpr size_t SC_LIST_BYTES = 4096 * 2;  // fused update: u16 list of a bucket's updated pairs (NE * F / 2 <= 4096)
 constexpr float FIX_SCALE = 16777216.0f;     // 2^24: fp16 values are integer multiples of 2^-24
 
 template <uint32_t F> struct ValVec;
@@ -525,14 +526,53 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 	__syncthreads();
 	// two fp16 per thread-step (n_e * F is even: levels hold multiples of 8 entries); pair k of the
 	// bucket is parameter pair (e0 F) / 2 + k of the grid
+	if constexpr (FUSED) {
+		// the pairs with a gradient (about a quarter at C5) are listed first (wave ballots, one LDS atomic per
+		// wave), then updated densely: a block runs ~1 round of record load -> update -> store instead of one
+		// per 1024 pairs with most lanes idle. Pairs are independent, so the list order does not matter.
+		// Only for sparse buckets (fewer than 2 items per entry: C5's hashed levels); dense ones (C2', ~4 per
+		// entry) update in place, where the list pass measured slower (r03bz: C2' 329 -> 335 us; r03ca/cb:
+		// threshold 1 vs 2 items per entry, C5 1.262 vs 1.20 ms on a faster box, C2' unchanged).
+		if (t >= 2 * n_e) {
+			for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) {
+				uint32_t ia, ib;
+				pair_slots<F>(k, NEP, ia, ib);
+				fused_adam_pair(fa, e0 * F / 2 + k, (f16)fix_to_f32(acc[ia]), (f16)fix_to_f32(acc[ib]));
+			}
+			return;
+		}
+		__shared__ uint32_t n_list;
+		uint16_t* list = (uint16_t*)(acc + NEP * F);
+		if (threadIdx.x == 0) n_list = 0;
+		__syncthreads();
+		const uint32_t lane = threadIdx.x & 63;
+		for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) {
+			uint32_t ia, ib;
+			pair_slots<F>(k, NEP, ia, ib);
+			const f16 h0 = (f16)fix_to_f32(acc[ia]), h1 = (f16)fix_to_f32(acc[ib]);
+			const bool act = (float)h0 / fa.loss_scale != 0.f || (float)h1 / fa.loss_scale != 0.f;  // fused_adam_load's test
+			const unsigned long long m = __ballot(act);
+			if (m == 0ull) continue;
+			const uint32_t leader = __ffsll((long long)m) - 1;
+			uint32_t base = 0;
+			if (lane == leader) base = atomicAdd(&n_list, (uint32_t)__popcll(m));
+			base = __shfl(base, leader);
+			if (act) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)k;
+		}
+		__syncthreads();
+		const uint32_t na = n_list;
+		for (uint32_t i = threadIdx.x; i < na; i += blockDim.x) {
+			const uint32_t k = list[i];
+			uint32_t ia, ib;
+			pair_slots<F>(k, NEP, ia, ib);
+			fused_adam_pair(fa, e0 * F / 2 + k, (f16)fix_to_f32(acc[ia]), (f16)fix_to_f32(acc[ib]));
+		}
+		return;
+	}
 	for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) {
 		uint32_t ia, ib;
 		pair_slots<F>(k, NEP, ia, ib);
 		float s0 = fix_to_f32(acc[ia]), s1 = fix_to_f32(acc[ib]);
-		if (FUSED) {  // (issuing several pairs' state loads before the first update measured slower: 1.58 -> 1.97 ms at C5)
-			fused_adam_pair(fa, e0 * F / 2 + k, (f16)s0, (f16)s1);
-			continue;
-		}
 		if (!overwrite) {
 			const f16x2 o = ((const f16x2*)g)[k];
 			s0 += (float)o[0];
@@ -630,8 +670,9 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		ensure_dynamic_lds((const void*)scatter, lds_s);
 		if (!(debug & 4)) scatter<<<grid_s, p.spb == 512 ? 512 : 1024, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, p.n_chunks, xcd_map, cur_t, lo, idx, val, debug);
 		NGP_HIP(hipGetLastError());
-		ensure_dynamic_lds((const void*)accum, SC_LDS_BYTES + SC_LDS_PAD_BYTES);
-		accum<<<p.max_split_blocks + p.n_buckets, SC_BT, SC_LDS_BYTES + SC_LDS_PAD_BYTES, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
+		const size_t lds_a = SC_LDS_BYTES + SC_LDS_PAD_BYTES + (fa.rec ? SC_LIST_BYTES : 0);
+		ensure_dynamic_lds((const void*)accum, lds_a);
+		accum<<<p.max_split_blocks + p.n_buckets, SC_BT, lds_a, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
 		                                                                     val, a.grad, overwrite, split, scratch, debug, fa);
 		NGP_HIP(hipGetLastError());
 		const uint32_t gy = (uint32_t)div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS);
