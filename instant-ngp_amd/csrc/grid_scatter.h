@@ -18,6 +18,7 @@ struct ScatterPlan {
 	uint32_t max_split_blocks = 0;
 	uint32_t max_split_buckets = 0;
 	uint32_t xcd_map = 2;    // scatter block order: 2 = a chunk's level blocks and neighbouring chunks share an XCD
+	uint32_t bt = 1024;      // bucket accumulation block threads (experiment knob NGP_SC_BT)
 	// workspace layout (bytes)
 	size_t off_hist = 0, off_cur = 0, off_tot = 0, off_split = 0, off_lo = 0, off_splitb = 0, off_scratch = 0, off_idx = 0, off_val = 0,
 	       total = 0;

@@ -670,9 +670,9 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		ensure_dynamic_lds((const void*)scatter, lds_s);
 		if (!(debug & 4)) scatter<<<grid_s, p.spb == 512 ? 512 : 1024, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, p.n_chunks, xcd_map, cur_t, lo, idx, val, debug);
 		NGP_HIP(hipGetLastError());
-		const size_t lds_a = SC_LDS_BYTES + SC_LDS_PAD_BYTES + (fa.rec ? SC_LIST_BYTES : 0);
+		const size_t lds_a = ((size_t)8 << p.B) * c.n_features + SC_LDS_PAD_BYTES + (fa.rec ? SC_LIST_BYTES : 0);
 		ensure_dynamic_lds((const void*)accum, lds_a);
-		accum<<<p.max_split_blocks + p.n_buckets, SC_BT, lds_a, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
+		accum<<<p.max_split_blocks + p.n_buckets, p.bt, lds_a, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
 		                                                                     val, a.grad, overwrite, split, scratch, debug, fa);
 		NGP_HIP(hipGetLastError());
 		const uint32_t gy = (uint32_t)div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS);
@@ -708,7 +708,9 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	const uint32_t F = g.n_features;
 	// bucket = 2^B entries of one level whose F int64 accumulators fill SC_LDS_BYTES
 	p.B = 0;
-	while (((size_t)2 << p.B) * F * 8 <= SC_LDS_BYTES && p.B < 16) ++p.B;
+	size_t lds_budget = SC_LDS_BYTES;  // experiment knob NGP_SC_LDS_KB (<= 64)
+	if (const char* e = getenv("NGP_SC_LDS_KB")) lds_budget = std::min<size_t>(SC_LDS_BYTES, (size_t)atoi(e) * 1024);
+	while (((size_t)2 << p.B) * F * 8 <= lds_budget && p.B < 16) ++p.B;
 	const Levels lv = make_levels(g, p.B);
 	p.n_buckets = lv.vb_base[g.n_levels];
 	p.max_lb = 0;
@@ -733,6 +735,11 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	p.max_split_buckets = (uint32_t)(div_round_up(p.n_items, (uint64_t)p.split_limit) + 1);
 	p.xcd_map = 2;
 	if (const char* e = getenv("NGP_SC_XCD")) p.xcd_map = (uint32_t)atoi(e);
+	// accumulation block: 512 threads for F = 2 (4 blocks per CU by waves; C2' 328 -> 315 us, C5 1.250 ->
+	// 1.235 ms), 1024 for F = 4 (C2: 144 -> 151 us at 512) (profiles/r03ce)
+	p.bt = F == 2 ? 512 : 1024;
+	if (const char* e = getenv("NGP_SC_BT")) p.bt = (uint32_t)atoi(e);
+	NGP_CHECK(p.bt >= 64 && p.bt <= SC_BT && p.bt % 64 == 0, "grid backward: NGP_SC_BT must be a multiple of 64 up to 1024");
 	const uint64_t len = (uint64_t)p.n_buckets * p.n_chunks;
 	NGP_CHECK(len < (1ull << 31), "grid backward: bucket histogram too large");
 	auto align = [](size_t v) { return (v + 255) / 256 * 256; };
