@@ -2,7 +2,7 @@
 # under the last variant's environment, then each variant twice. Variants: "name:VAR=val,VAR=val".
 set -e -o pipefail
 T=$1; shift; mkdir -p gpurun_out/$T; export TMPDIR=/tmp
-apply() { unset NGP_SC_BT NGP_SC_LDS_KB; local kv=${1#*:}; [ "$kv" = "$1" ] && return 0; for a in ${kv//,/ }; do export "$a"; done; }
+apply() { unset NGP_SC_BT NGP_SC_LDS_KB NGP_SC_CHUNK NGP_SC_PART NGP_SC_LIMIT; local kv=${1#*:}; [ "$kv" = "$1" ] && return 0; for a in ${kv//,/ }; do export "$a"; done; }
 last=${@: -1}; apply "$last"
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_lazy_ema.py tests/test_gpu_grid_exact.py tests/test_gpu_network_full.py > gpurun_out/$T/tests.log 2>&1
 tail -1 gpurun_out/$T/tests.log
