@@ -104,10 +104,13 @@ REGION_PHASES = {"grid_backward_total": ["grid_bwd_prepare", "grid_backward_sort
 # (22 B) + write w32 m1 m2 steps w16 ema32 ema16 (24 B) = 46 B; lazily skipped grid entry (zero
 # gradient) = read g16 w32 ema32 (10 B) + write ema32 ema16 (6 B) = 16 B
 OPT_B_UPDATED, OPT_B_SKIPPED = 46, 16
-# the grid's lazy-layout update fused into the bucketed backward (engine option fuse_opt, C5): per updated
-# parameter w32 read + write (8 B), w16 write (2 B) and its half of a 48-B AdamRec read and written (48 B);
-# skipped parameters are not touched, and no gradient is stored or re-read
-OPT_B_FUSED = 58
+# the grid's lazy-layout update fused into the bucketed backward (engine option fuse_opt: C5, C2'): a parameter
+# pair's optimizer state AND fp32 master weights are one AdamRec (optimizer.h: {m1, m2, steps, ema, w, done}
+# for two parameters, static_assert sizeof == 48), so an updated parameter reads and writes its half of the
+# record and writes its fp16 weight; skipped parameters are not touched, no gradient is stored or re-read
+ADAMREC_BYTES, ADAMREC_PARAMS = 48, 2
+OPT_B_FUSED = ADAMREC_BYTES // ADAMREC_PARAMS * 2 + 2  # = 50 B per updated parameter
+L2_PEAK_GBS = 34500.0  # aggregate L2 bandwidth (MI355X_MICROARCH.md, L2): no fabric rate can exceed it
 
 
 def newest_profile(suffix):
@@ -219,11 +222,14 @@ def read_profiler(lib):
     return json.loads(cbuf.value.decode())
 
 
-def timed_steps(lib, step, steps, warmup, world, capture=None):
+def timed_steps(lib, step, steps, warmup, world, capture=None, comm=None):
     """W untimed warmup steps, then K steps between barrier + synchronize on both sides (one captured
     HIP graph of K steps when `capture` gives one), then the same K steps replayed eagerly with the
     engine's per-kernel HIP events (queued behind graph launches so the events bracket kernels only).
-    Returns (seconds for the K timed steps, launch mode, per-phase profiler dict)."""
+    `step` must run what the graph runs (Trainer.train_step is the eager form of a captured step).
+    comm: a host-side exchange (dp.HostComm) whose own round-trip timer stands in for the engine
+    profiler's "allreduce" region. Returns (seconds for the K timed steps, launch mode, per-phase
+    profiler dict)."""
     stream = torch.cuda.Stream()
     graph_note = None
     with torch.cuda.stream(stream):
@@ -242,6 +248,8 @@ def timed_steps(lib, step, steps, warmup, world, capture=None):
         if graph is None:
             lib.ngp_profiler_reset()
             lib.ngp_profiler_enable(1)
+        if hasattr(comm, "reset_timer"):
+            comm.reset_timer()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -264,11 +272,17 @@ def timed_steps(lib, step, steps, warmup, world, capture=None):
                 step()
             torch.cuda.synchronize()
         lib.ngp_profiler_enable(0)
-    return t1 - t0, ("hip_graph" if graph is not None else (graph_note or "eager")), read_profiler(lib)
+    prof = read_profiler(lib)
+    if hasattr(comm, "reset_timer") and comm.calls and "allreduce" not in prof:
+        prof["allreduce"] = {"ms": comm.ms, "calls": comm.calls, "timer": "host round trip (gloo)"}
+    return t1 - t0, ("hip_graph" if graph is not None else (graph_note or "eager")), prof
 
 
 def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None, wire="f32"):
-    """NerfNetwork + Trainer for C2/C2' with a resident synthetic batch; returns (step, capture, net, trainer)."""
+    """NerfNetwork + Trainer for C2/C2' with a resident synthetic batch; returns (step, capture, net, trainer,
+    comm). step() is Trainer.train_step, the eager form of the captured step (the grid's update fused into
+    the backward on the lazy layout, the exchange hook, the optimizer), so the per-kernel replay profiles
+    the path the graph times. capture is None when the exchange is a host round trip (gloo)."""
     cfg = pkg.nerf_config(variant)
     net = pkg.create_nerf_network(cfg)
     if overlap is not None:
@@ -279,24 +293,21 @@ def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None, wire="f32"):
     trainer = pkg.Trainer(net, cfg["optimizer"], seed=1337)
     net.reserve(n)
     x, dL = synthetic_batch(n, 1337 + rank, "cuda")
-    grads = trainer.gradients
     comm = None
     if world > 1:
-        # the engine's own RCCL communicator: the gradient all-reduce is enqueued by the engine on its
-        # stream, between the backward and the optimizer, and captured into the step's graph
-        comm = pkg.dp.EngineComm(rank, world, wire=wire)
+        # nccl: the engine's own RCCL communicator, the gradient all-reduce enqueued by the engine on its
+        # stream between the backward and the optimizer and captured into the step's graph; gloo (ranks
+        # sharing one GPU): a host round trip through torch.distributed, eager steps only
+        comm = pkg.dp.make_comm(rank, world, wire=wire)
         trainer.set_allreduce(comm)
     loss_scale = 128.0
 
     def step():
-        net.forward_backward(x, dL)
-        if comm is not None:
-            comm.allreduce(grads)  # RCCL over xGMI; 1/N folded into the loss scale
-        trainer.optimizer_step(loss_scale * world)
+        trainer.train_step(x, dL, loss_scale)  # 1/N of the all-reduced sum folded into the loss scale
 
     def capture(k):
         return trainer.capture_training_step(x, dL, loss_scale, n_steps=k)
-    return step, capture, net, trainer, comm
+    return step, (None if isinstance(comm, pkg.dp.HostComm) else capture), net, trainer, comm
 
 
 def slab_reduction_bytes(lib, net):
@@ -341,22 +352,23 @@ def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped, slab_bytes=0, fu
             b, w, pk, u = roof[k]
             e.update({"achieved": round(w / (ms / 1e3), 1), "unit": u, "frac": round(w / (ms / 1e3) / pk, 4)})
             if b == "hbm":
-                traffic, _ = pmc_traffic(variant, k)
+                traffic, src = pmc_traffic(variant, k)
                 if traffic is not None:
                     # what actually left L2 for the fabric per launch, and its rate
                     e["fabric_MB"] = round(traffic / 1e6, 2)
                     e["fabric_GBs"] = round(traffic / 1e9 / (ms / 1e3), 1)
-                cached = (k == "optimizer" and w * 1e9 < IC_BYTES) or w / (ms / 1e3) > pk
-                if cached:
-                    # the algorithmic bytes were (partly) served on-die (Infinity Cache / L2: the optimizer
-                    # state re-touched every step, hot table entries; L2 write-back absorbs stores that
-                    # drain during the next kernel): the HBM spec is not their ceiling, so no fraction of
-                    # it is printed (neither algorithmic nor fabric: both can exceed 1 here). fabric_GBs
-                    # stays as the measured rate.
+                    if e["fabric_GBs"] > L2_PEAK_GBS:
+                        # more bytes per second leaving L2 than L2 can deliver: the committed PMC summary
+                        # describes other kernels than the ones timed here (stale profile or a different path)
+                        raise RuntimeError(f"roofline {variant}/{k}: {e['fabric_MB']} MB per launch from {src} in "
+                                           f"{ms * 1e3:.1f} us = {e['fabric_GBs']} GB/s > L2 {L2_PEAK_GBS} GB/s")
+                if k == "optimizer" and w * 1e9 < IC_BYTES:
+                    # the optimizer's whole working set is re-touched every step and fits the Infinity Cache:
+                    # its bytes are served on-die, so the HBM spec is not their ceiling and no fraction of it
+                    # is printed. fabric_GBs stays as the measured rate.
                     e.update({"bound": "infinity_cache", "frac": None,
-                              "note": "algorithmic bytes served partly on-die (working set re-touched every step, "
-                                      "stores absorbed by the L2 write-back); no HBM fraction; fabric_GBs = PMC "
-                                      "bytes leaving L2 / time"})
+                              "note": "working set < Infinity Cache, re-touched every step: no HBM fraction; "
+                                      "fabric_GBs = PMC bytes leaving L2 / time"})
         if k in ("mlp_train", "mlp_infer"):
             u = pmc_mfma_util(variant, k)
             if u is not None:
@@ -431,6 +443,16 @@ def optimizer_counts(net, trainer, step, fused=False):
     return nm + nz, net.n_params - nm - nz, None
 
 
+# engine profiler phases that enclose other phases (the NeRF step's outer scopes; not added in kernels_sum_ms)
+NESTED_PHASES = {"nerf_sample", "nerf_density_grid", "nerf_inference", "nerf_loss", "nerf_train_pass"}
+
+
+def kernels_sum_ms(kernels):
+    """Sum of the per-step averages of the engine profiler's top-level phases: the device time of one step
+    as the per-kernel replay saw it, to compare with ms_per_step."""
+    return round(sum(v["ms"] / max(v["calls"], 1) for k, v in kernels.items() if k not in NESTED_PHASES), 4)
+
+
 def free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
@@ -484,6 +506,13 @@ def main():
     ap.add_argument("--wire", default="f32", choices=["f32", "f16"],
                     help="gradient all-reduce wire type (f32: fp16 sums widened, rounded once)")
     ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling sub-record")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo"],
+                    help="N > 1 exchange: rccl (engine RCCL communicator, one GPU per rank) or gloo (host round "
+                         "trip through torch.distributed: ranks may share a GPU, eager steps only)")
+    ap.add_argument("--device", type=int, default=None, help="GPU index for every rank (default: LOCAL_RANK)")
+    ap.add_argument("--e2e-images", type=int, default=100, help="views of the e2e procedural scene")
+    ap.add_argument("--e2e-res", type=int, default=800, help="resolution of the e2e procedural scene")
+    ap.add_argument("--no-vs1", action="store_true", help="N > 1: skip the in-job 1-GPU reference pass")
     ap.add_argument("--no-opt-count", action="store_true",
                     help="skip the untimed step that counts updated parameters (PMC passes: at C5 that step runs "
                          "unfused and would mix into the per-dispatch counter averages)")
@@ -496,18 +525,33 @@ def main():
     from __graft_entry__ import load_package
     pkg = load_package()
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    rank, world, local_rank = pkg.dp.init_from_env()
+    torch.cuda.set_device(local_rank if args.device is None else args.device)
+    rank, world, local_rank = pkg.dp.init_from_env("gloo" if args.comm == "gloo" else None)
     assert world == args.gpus, (world, args.gpus)
     lib = pkg.lib()
+
+    vs1 = None
+    if world > 1 and args.variant in ("C2", "C2p") and not args.no_vs1:
+        # the 1-GPU reference for the N-vs-1 ratios, measured in this job: rank 0 alone trains the same
+        # --batch per step with no exchange, launched like the N-rank passes; the other ranks wait
+        if rank == 0:
+            s1, c1, _, _, _ = nerf_pass(pkg, args.variant, args.batch, 0, 1, args.opt, args.overlap)
+            use_graph = args.graph and args.comm == "rccl"
+            dt1, launch1, _ = timed_steps(lib, s1, args.steps, args.warmup, 1, c1 if use_graph else None)
+            vs1 = {"value": args.batch * args.steps / dt1, "ms_per_step": dt1 / args.steps * 1e3, "launch": launch1,
+                   "batch": args.batch}
+            del s1, c1
+            torch.cuda.synchronize()
+        dist.barrier()
 
     n = args.batch if args.scaling == "weak" else args.batch // world
     n_opt = (None, None)
     c5_fused = None
+    comm = None
     if args.variant in ("C2", "C2p"):
         step, capture, net, trainer, comm = nerf_pass(pkg, args.variant, n, rank, world, args.opt, args.overlap,
                                                       args.wire)
-        n_opt = optimizer_counts(net, trainer, step)[:2]
+        *n_opt, c5_fused = optimizer_counts(net, trainer, step, fused=trainer.fused_update_active(n))
         if not args.graph:
             capture = None
     elif args.variant == "C5":
@@ -532,12 +576,16 @@ def main():
         capture = None
 
     n_params_total = net.n_params
-    dt, launch, kernels = timed_steps(lib, step, args.steps, args.warmup, world, capture)
+    dt, launch, kernels = timed_steps(lib, step, args.steps, args.warmup, world, capture, comm)
     slab_b = slab_reduction_bytes(lib, net)
+    param_hashes = None
     if world > 1:
-        t = torch.tensor([dt], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = pkg.dp.reduce_scalar(dt, "max")
+        # data parallelism keeps every rank's parameters identical (same all-reduced gradient, same update)
+        import hashlib
+        torch.cuda.synchronize()
+        param_hashes = [None] * world
+        dist.all_gather_object(param_hashes, hashlib.sha1(trainer.params.cpu().numpy().tobytes()).hexdigest())
 
     strong = None
     if world > 1 and args.variant in ("C2", "C2p") and not args.no_strong:
@@ -545,10 +593,8 @@ def main():
         # global --batch sharded over the N ranks
         n_s = args.batch // world if args.scaling == "weak" else args.batch
         s_s, c_s, _, _, comm_s = nerf_pass(pkg, args.variant, n_s, rank, world, args.opt, args.overlap, args.wire)
-        dts, launch_s, k_s = timed_steps(lib, s_s, args.steps, args.warmup, world, c_s if args.graph else None)
-        t = torch.tensor([dts], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dts = float(t.item())
+        dts, launch_s, k_s = timed_steps(lib, s_s, args.steps, args.warmup, world, c_s if args.graph else None, comm_s)
+        dts = pkg.dp.reduce_scalar(dts, "max")
         ar = k_s.get("allreduce")
         strong = {"scaling": "strong" if args.scaling == "weak" else "weak", "batch_per_gpu": n_s,
                   "global_batch": n_s * world, "value": n_s * world * args.steps / dts, "unit": "samples/s",
@@ -561,7 +607,8 @@ def main():
         # global ids, RCCL all-reduce of gradients, density-grid maxima and counters), then PSNR on rank 0
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import psnr30
-        e2e_dp = psnr30.run(pkg, seconds=args.e2e_seconds, rank=rank, world=world)
+        e2e_dp = psnr30.run(pkg, seconds=args.e2e_seconds, images=args.e2e_images, res=args.e2e_res, rank=rank,
+                            world=world)
 
     if rank == 0:
         kern_summary, rl = roofline(args.variant, n, kernels, *n_opt, slab_bytes=slab_b, fused_grid_updated=c5_fused)
@@ -581,13 +628,16 @@ def main():
             "config": {"workload": WORKLOADS[args.variant],
                        "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
                        "launch": launch,
-                       "exchange": (f"engine RCCL all-reduce of the gradient buffer per step ({args.wire} on the wire)"
+                       "exchange": ((f"engine RCCL all-reduce of the gradient buffer per step ({args.wire} on the wire)"
+                                     if args.comm == "rccl" else
+                                     "gloo all-reduce of the gradient buffer per step (host round trip, fp32)")
                                     if world > 1 else None)},
             "kernel_timing": ("HIP events per kernel on the launch stream, eager replay of the same K steps queued "
                               "behind a graph launch" if launch == "hip_graph" else "HIP events per kernel over the timed region"),
             "roofline": rl,
             "optimizer_params": ({"updated": n_opt[0], "skipped": n_opt[1]} if c5_fused is None else
                                  {"mlp_updated": n_opt[0], "grid_updated_in_backward": c5_fused}),
+            "kernels_sum_ms": kernels_sum_ms(kernels),
             "kernels": kern_summary,
         }
         if world > 1:
@@ -596,6 +646,15 @@ def main():
             res["allreduce_bytes"] = (4 if args.wire == "f32" else 2) * int(n_params_total)
             if strong is not None:
                 res["strong"] = strong
+            res["param_sha1_per_rank"] = param_hashes
+            if vs1 is not None:
+                # N-vs-1 from this job's own 1-GPU pass: weak = N x batch per step over N GPUs, strong = one
+                # batch per step over N GPUs, both against one GPU training one batch per step
+                res["vs_1gpu"] = {"one_gpu": vs1, "weak_ratio": None, "strong_ratio": None}
+                for mode, v in ((args.scaling, res["value"]),
+                                (strong["scaling"] if strong else None, strong["value"] if strong else None)):
+                    if mode is not None:
+                        res["vs_1gpu"][f"{mode}_ratio"] = round(v / vs1["value"], 4)
             if e2e_dp is not None:
                 res["e2e"] = {k: e2e_dp[k] for k in ("value", "unit", "psnr", "psnr_views", "train_seconds", "steps",
                                                      "ms_per_step", "n_gpus", "data", "config")}
@@ -603,11 +662,14 @@ def main():
             if not args.no_c2p:
                 # BASELINE's literal "L=16": the same training pass at C2' (L=16 F=2 T=2^19)
                 s2, c2, net2, tr2, _ = nerf_pass(pkg, "C2p", n, 0, 1)
-                o2 = optimizer_counts(net2, tr2, s2)[:2]
+                *o2, f2 = optimizer_counts(net2, tr2, s2, fused=tr2.fused_update_active(n))
                 dt2, launch2, k2 = timed_steps(lib, s2, args.steps, args.warmup, 1, c2)
-                ks2, rl2 = roofline("C2p", n, k2, *o2, slab_bytes=slab_reduction_bytes(lib, net2))
+                ks2, rl2 = roofline("C2p", n, k2, *o2, slab_bytes=slab_reduction_bytes(lib, net2), fused_grid_updated=f2)
                 res["c2p"] = {"workload": WORKLOADS["C2p"], "value": n * args.steps / dt2, "unit": "samples/s",
-                              "ms_per_step": dt2 / args.steps * 1e3, "launch": launch2, "roofline": rl2, "kernels": ks2}
+                              "ms_per_step": dt2 / args.steps * 1e3, "launch": launch2, "roofline": rl2, "kernels": ks2,
+                              "kernels_sum_ms": kernels_sum_ms(k2),
+                              "optimizer_params": ({"updated": o2[0], "skipped": o2[1]} if f2 is None else
+                                                   {"mlp_updated": o2[0], "grid_updated_in_backward": f2})}
                 del s2, c2, net2, tr2
             if not args.no_c5:
                 # BASELINE configs[4]: the HBM-bound SDF step (T=2^22, 105 M parameters), same batch size
@@ -617,6 +679,7 @@ def main():
                 ks5, rl5 = roofline("C5", n, k5, *o5, slab_bytes=slab_reduction_bytes(lib, net5), fused_grid_updated=f5)
                 res["c5"] = {"workload": WORKLOADS["C5"], "value": n * args.steps / dt5, "unit": "samples/s",
                              "ms_per_step": dt5 / args.steps * 1e3, "launch": launch5, "roofline": rl5, "kernels": ks5,
+                             "kernels_sum_ms": kernels_sum_ms(k5),
                              "optimizer_params": {"mlp_updated": o5[0], "grid_updated_in_backward": f5}}
                 del s5, net5, tr5
                 torch.cuda.empty_cache()

@@ -127,7 +127,9 @@ int ngp_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint
  * (grad_mode NGP_GRAD_IGNORE: untouched). dL_dinput (nullable, the reference's `GPUMatrixDynamic<float>*
  * dL_dinput`): fp32 AoS [n x dL_dinput_stride]; rows 0..n_pos_dims-1 receive dL/dposition through the
  * grid encoding, a NerfNetwork's rows dir_offset..+2 dL/ddirection through the SH encoding
- * (nerf_network.h:282-299, 317-333); other rows are not written. */
+ * (nerf_network.h:282-299, 317-333); other rows are not written. A context from a forward with
+ * use_inference_params runs the backward on the inference (EMA) parameters too (backward_impl's
+ * use_inference_params, nerf_network.h:256-335). */
 int ngp_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* dL_doutput, uint32_t dL_stride, float* dL_dinput,
                  uint32_t dL_dinput_stride, int grad_mode);
 void ngp_ctx_destroy(ngp_ctx* ctx);
@@ -171,7 +173,9 @@ void* ngp_trainer_gradients(ngp_trainer* t);               /* fp16 [n_params], t
 void* ngp_trainer_params(ngp_trainer* t);                  /* fp16 [n_params] */
 void* ngp_trainer_inference_params(ngp_trainer* t);        /* fp16 [n_params] (EMA when configured) */
 /* fp32 [n_params]; large-table trainers keep the master weights in their optimizer records and refresh this
-   mirror on each call (synchronizes the device; NULL + ngp_last_error on failure) */
+   mirror on each call (synchronizes the device; NULL + ngp_last_error on failure). For those trainers the
+   buffer is read-only: writes into it never reach training or serialize (which reads the records); change
+   weights with ngp_trainer_set_params_full_precision. For eager-layout trainers it is the live master copy. */
 float* ngp_trainer_params_full_precision(ngp_trainer* t);
 uint32_t ngp_trainer_step(const ngp_trainer* t);
 float ngp_trainer_learning_rate(const ngp_trainer* t);     /* optimizer->learning_rate() (testbed_nerf.cu:3771) */
@@ -191,6 +195,15 @@ typedef struct ngp_graph ngp_graph;
 int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
                                       const void* dL_doutput, uint32_t dL_stride, float loss_scale, uint32_t n_steps,
                                       int with_optimizer, ngp_graph** out);
+/* Engine extension: ONE step of exactly what a captured step runs, launched eagerly: forward_backward
+ * (with the grid's lazy update fused into the backward when ngp_trainer_fused_update_active), the
+ * trainer's gradient exchange hook if set (ngp_trainer_set_allreduce), then optimizer_step(loss_scale x
+ * world). The per-kernel profile of this call is the profile of a replayed graph step. */
+int ngp_trainer_train_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                           const void* dL_doutput, uint32_t dL_stride, float loss_scale);
+/* 1 when a training step of n_batch samples runs the grid's optimizer update inside the backward (lazy-EMA
+ * layout, model option fuse_opt, no exchange hook): the grid part of the gradient buffer is then not written. */
+int ngp_trainer_fused_update_active(const ngp_trainer* t, uint32_t n_batch);
 int ngp_graph_launch(ngp_graph* g, void* stream);
 void ngp_graph_destroy(ngp_graph* g);
 

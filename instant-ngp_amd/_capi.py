@@ -120,6 +120,8 @@ SIGNATURES = {
     "ngp_trainer_serialize": (i32, [P, P, C.POINTER(u64)]),
     "ngp_trainer_deserialize": (i32, [P, P, u64]),
     "ngp_trainer_capture_training_step": (i32, [P, P, u32, P, u32, P, u32, f32, u32, i32, C.POINTER(P)]),
+    "ngp_trainer_train_step": (i32, [P, P, u32, P, u32, P, u32, f32]),
+    "ngp_trainer_fused_update_active": (i32, [P, u32]),
     "ngp_graph_launch": (i32, [P, P]),
     "ngp_graph_destroy": (None, [P]),
     "ngp_loss_evaluate": (i32, [i32, P, u32, u32, P, u32, P, u32, f32, P, u32, P, P]),

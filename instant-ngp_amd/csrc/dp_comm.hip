@@ -32,28 +32,28 @@ struct ngp_dp_comm {
 
 namespace ngp {
 // fp16 -> fp32 widening and the single fp32 -> fp16 rounding around a widened all-reduce; 8 elements per
-// thread (16-B loads), scalar tail
-__global__ void k_widen_f16(const f16* __restrict__ a, float* __restrict__ b, uint64_t n) {
+// thread (16-B loads when the fp16 buffer is 16-B aligned, else 8 scalar ones), scalar tail
+__global__ void k_widen_f16(const f16* __restrict__ a, float* __restrict__ b, uint64_t n, bool vec) {
 	const uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * 8;
-	if (i + 8 <= n) {
+	if (vec && i + 8 <= n) {
 		const f16x8 v = *(const f16x8*)(a + i);
 		f32x4 lo = {(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 		f32x4 hi = {(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
 		*(f32x4*)(b + i) = lo;
 		*(f32x4*)(b + i + 4) = hi;
 	} else {
-		for (uint64_t j = i; j < n; ++j) b[j] = (float)a[j];
+		for (uint64_t j = i; j < n && j < i + 8; ++j) b[j] = (float)a[j];
 	}
 }
-__global__ void k_narrow_f32(const float* __restrict__ b, f16* __restrict__ a, uint64_t n) {
+__global__ void k_narrow_f32(const float* __restrict__ b, f16* __restrict__ a, uint64_t n, bool vec) {
 	const uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * 8;
-	if (i + 8 <= n) {
+	if (vec && i + 8 <= n) {
 		const f32x4 lo = *(const f32x4*)(b + i), hi = *(const f32x4*)(b + i + 4);
 		f16x8 v;
 		for (int k = 0; k < 4; ++k) { v[k] = (f16)lo[k]; v[k + 4] = (f16)hi[k]; }
 		*(f16x8*)(a + i) = v;
 	} else {
-		for (uint64_t j = i; j < n; ++j) a[j] = (f16)b[j];
+		for (uint64_t j = i; j < n && j < i + 8; ++j) a[j] = (f16)b[j];
 	}
 }
 }  // namespace ngp
@@ -145,11 +145,12 @@ int ngp_dp_comm_allreduce(void* user, void* buf, uint64_t count, int dtype, int 
 			if (rc != NGP_OK) return rc;
 		}
 		const uint32_t blocks = (uint32_t)((count + 8 * 256 - 1) / (8 * 256));
-		ngp::k_widen_f16<<<blocks, 256, 0, s>>>((const ngp::f16*)buf, c->stage, count);
+		const bool vec = (uintptr_t)buf % 16 == 0;  // any tensor view may come in (EngineComm.allreduce)
+		ngp::k_widen_f16<<<blocks, 256, 0, s>>>((const ngp::f16*)buf, c->stage, count, vec);
 		if (hipGetLastError() != hipSuccess) return NGP_ERROR;
 		const ncclResult_t r = ncclAllReduce(c->stage, c->stage, (size_t)count, ncclFloat32, o, c->comm, s);
 		if (r != ncclSuccess) return fail("ncclAllReduce", r);
-		ngp::k_narrow_f32<<<blocks, 256, 0, s>>>(c->stage, (ngp::f16*)buf, count);
+		ngp::k_narrow_f32<<<blocks, 256, 0, s>>>(c->stage, (ngp::f16*)buf, count, vec);
 		if (hipGetLastError() != hipSuccess) return NGP_ERROR;
 		return NGP_OK;
 	}

@@ -135,6 +135,7 @@ struct BwdExtra {
 	bool density_only = false;      // NerfNetwork::density_backward: the density network alone
 	const f16* ddens = nullptr;     // its dL/d(density output), fp16 AoS [n x ddens_stride]
 	uint32_t ddens_stride = 0;
+	bool inference = false;         // the forward context ran on the inference (EMA) parameters: so does the backward
 };
 }  // namespace ngp
 
@@ -369,14 +370,16 @@ struct ngp_model {
 		f16* dsh = ex.dL_dinput && nerf && !ex.density_only ? (f16*)dsh_ws.get((size_t)n * 16 * sizeof(f16)) : nullptr;
 		// encbuf == nullptr: the MLP kernel encodes the positions itself (fused_training_ok)
 		const MlpMode mode = ex.density_only ? MLP_DENSITY_TRAIN : encbuf ? MLP_TRAIN : MLP_TRAIN_ENC;
-		run_mlp(s, mode, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride, dL_denc, slab, false, &ex, dsh);
+		run_mlp(s, mode, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride, dL_denc, slab, ex.inference, &ex,
+		        dsh);
 		// dL/dinput through the grid (position rows) and the SH encoding (direction rows, NerfNetwork). Run
 		// last: dL_dinput may alias the input (the reference passes positions_matrix for both,
 		// testbed_nerf.cu:2616), which the grid backward still reads
 		auto input_gradient = [&]() {
 			if (!ex.dL_dinput) return;
 			ProfScope ps("input_gradient", s);
-			InputGradArgs ia{n, in, stride, params + grid_offset(), dL_denc, enc_width, max_level, max_level_per_sample, dsh,
+			if (ex.inference) sync_inference(s);
+			InputGradArgs ia{n, in, stride, pick(ex.inference) + grid_offset(), dL_denc, enc_width, max_level, max_level_per_sample, dsh,
 			                 dir_offset, ex.dL_dinput, ex.dinput_stride, ex.dinput_scale};
 			grid_input_gradient(grid, ia, s);
 		};
@@ -759,17 +762,19 @@ int ngp_encoding_backward(ngp_model* m, void* stream, uint32_t n, const float* i
 	NGP_TRY({
 		if (n == 0) return NGP_OK;
 		m->require_params(false);
+		if (grad_mode != NGP_GRAD_IGNORE) {
+			NGP_CHECK(m->gradients, "model has no gradient buffer");
+			GridBwdArgs b{n, input, input_stride, (const f16*)dL_doutput, dL_stride, dL_layout, m->gradients + m->grid_offset(),
+			              m->max_level, m->max_level_per_sample};
+			m->scatter_grid_grad(S(stream), b, grad_mode != NGP_GRAD_ACCUMULATE);
+		}
+		// last: dL_dinput may alias the input, which the parameter backward above still reads
 		if (dL_dinput) {
 			ProfScope ps("input_gradient", S(stream));
 			InputGradArgs ia{n, input, input_stride, m->params + m->grid_offset(), (const f16*)dL_doutput, dL_stride, m->max_level,
 			                 m->max_level_per_sample, nullptr, 0, dL_dinput, dL_dinput_stride, 1.f};
 			grid_input_gradient(m->grid, ia, S(stream));
 		}
-		if (grad_mode == NGP_GRAD_IGNORE) return NGP_OK;
-		NGP_CHECK(m->gradients, "model has no gradient buffer");
-		GridBwdArgs b{n, input, input_stride, (const f16*)dL_doutput, dL_stride, dL_layout, m->gradients + m->grid_offset(),
-		              m->max_level, m->max_level_per_sample};
-		m->scatter_grid_grad(S(stream), b, grad_mode != NGP_GRAD_ACCUMULATE);
 	});
 }
 
@@ -847,6 +852,7 @@ int ngp_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* dL_doutpu
 		if (ctx->n == 0) return NGP_OK;
 		BwdExtra ex;
 		ex.dL_dinput = dL_dinput; ex.dinput_stride = dL_dinput_stride;
+		ex.inference = ctx->use_inference_params;  // backward_impl passes use_inference_params to every sub-backward
 		m->train_pass(S(stream), ctx->n, ctx->input, ctx->input_stride, (const f16*)m->enc.p, nullptr, 0, dL_doutput, dL_stride,
 		              grad_mode, ex);
 	});
@@ -883,6 +889,7 @@ int ngp_density_backward(ngp_model* m, void* stream, ngp_ctx* ctx, const void* d
 		BwdExtra ex;
 		ex.dL_dinput = dL_dinput; ex.dinput_stride = dL_dinput_stride;
 		ex.density_only = true; ex.ddens = (const f16*)dL_doutput; ex.ddens_stride = dL_stride;
+		ex.inference = ctx->use_inference_params;
 		m->train_pass(S(stream), ctx->n, ctx->input, ctx->input_stride, (const f16*)m->enc.p, nullptr, 0, nullptr, 0, grad_mode, ex);
 	});
 }
@@ -1081,6 +1088,65 @@ int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, 
 }
 }  // extern "C"
 
+// One training step as the captured graph runs it: forward_backward (the grid's lazy update fused into the
+// backward when `fuse`), [gradient exchange], optimizer. step_base = the trainer's ctl block (captured: the
+// step is the device base + k, hyperparameters read from the ctl block) or nullptr (eager: host step + k).
+static int train_step_body(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                           const void* dL_doutput, uint32_t dL_stride, float loss_scale, int with_optimizer,
+                           ngp_allreduce_fn allreduce, void* allreduce_user, uint32_t world, bool fuse,
+                           const uint32_t* step_base, uint32_t k) {
+	ngp_model* m = t->model;
+	FusedAdam fa;
+	if (fuse) {
+		fa = t->fused_update(loss_scale * (float)world);
+		if (step_base) {
+			fa.step_base = step_base;
+			fa.step_add = k;
+			fa.cfg_dev = (const AdamConfig*)(t->ctl + CTL_CFG);
+		} else {
+			fa.step_add = t->step + k;
+		}
+	}
+	int rc = forward_backward_with(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE,
+	                               fuse ? &fa : nullptr);
+	if (rc == NGP_OK && allreduce) {
+		rc = allreduce(allreduce_user, t->g16, t->n, NGP_DTYPE_F16, NGP_REDUCE_SUM, stream);
+		if (rc != NGP_OK && g_last_error.empty()) g_last_error = "gradient all-reduce failed";
+	}
+	if (rc == NGP_OK && with_optimizer) {
+		try {
+			// the summed gradient of `world` ranks: mean via the loss scale
+			t->run_step(S(stream), loss_scale * (float)world, step_base, step_base ? k : t->step + k,
+			            fuse ? m->n_matrix() : 0);
+		} catch (const std::exception& e) {
+			g_last_error = e.what();
+			rc = NGP_ERROR;
+		}
+	}
+	return rc;
+}
+
+extern "C" {
+int ngp_trainer_train_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                           const void* dL_doutput, uint32_t dL_stride, float loss_scale) {
+	NGP_ARG(t && n > 0 && input && dL_doutput && loss_scale > 0.f);
+	NGP_TRY({
+		ngp_model* m = t->model;
+		m->require_params(false);
+		NGP_CHECK(m->gradients == t->g16, "train_step: the model's gradient buffer must be this trainer's");
+		const bool fuse = !t->allreduce && t->fused_update_ok(n);
+		if (train_step_body(t, stream, n, input, input_stride, dL_doutput, dL_stride, loss_scale, 1, t->allreduce,
+		                    t->allreduce_user, t->world, fuse, nullptr, 0) != NGP_OK)
+			throw Error(g_last_error);
+		t->step++;
+	});
+}
+
+int ngp_trainer_fused_update_active(const ngp_trainer* t, uint32_t n_batch) {
+	return t && !t->allreduce && t->fused_update_ok(n_batch) ? 1 : 0;
+}
+}  // extern "C"
+
 // The capture with an explicit gradient exchange hook and world factor (ngp_trainer_capture_training_step
 // passes the trainer's own; the data-parallel NeRF trainer passes its communicator with world factor 1,
 // because its shards' dL/doutput is already scaled by 128 / R_global, so the summed gradient is the
@@ -1103,30 +1169,9 @@ int ngp::capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, co
 		const bool fuse = with_optimizer && !allreduce && t->fused_update_ok(n);
 		NGP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
 		int rc = NGP_OK;
-		for (uint32_t k = 0; k < n_steps && rc == NGP_OK; ++k) {
-			FusedAdam fa;
-			if (fuse) {
-				fa = t->fused_update(loss_scale * (float)world);
-				fa.step_base = t->ctl;  // step = device base (set per launch) + k, hyperparameters from the ctl block
-				fa.step_add = k;
-				fa.cfg_dev = (const AdamConfig*)(t->ctl + CTL_CFG);
-			}
-			rc = forward_backward_with(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE,
-			                           fuse ? &fa : nullptr);
-			if (rc == NGP_OK && allreduce) {
-				rc = allreduce(allreduce_user, t->g16, t->n, NGP_DTYPE_F16, NGP_REDUCE_SUM, stream);
-				if (rc != NGP_OK && g_last_error.empty()) g_last_error = "gradient all-reduce failed";
-			}
-			if (rc == NGP_OK && with_optimizer) {
-				try {
-					// the summed gradient of `world` ranks: mean via the loss scale
-					t->run_step(s, loss_scale * (float)world, t->ctl, k, fuse ? m->n_matrix() : 0);  // step = device base + k
-				} catch (const std::exception& e) {
-					g_last_error = e.what();
-					rc = NGP_ERROR;
-				}
-			}
-		}
+		for (uint32_t k = 0; k < n_steps && rc == NGP_OK; ++k)
+			rc = train_step_body(t, stream, n, input, input_stride, dL_doutput, dL_stride, loss_scale, with_optimizer, allreduce,
+			                     allreduce_user, world, fuse, t->ctl, k);  // step = device base (set per launch) + k
 		hipGraph_t graph = nullptr;
 		const hipError_t end = hipStreamEndCapture(s, &graph);
 		g->ws_epoch = m->ws_epoch;
@@ -1191,6 +1236,9 @@ float* ngp_trainer_params_full_precision(ngp_trainer* t) {
 	if (!t) return nullptr;
 	try {
 		t->sync_w32();
+		// the caller may write into the mirror: it is not the master copy, so the next reader (serialize, this
+		// accessor) refreshes it from the records again instead of trusting it
+		if (t->rec) t->w32_stale = true;
 	} catch (const std::exception& e) {
 		g_last_error = e.what();
 		return nullptr;
@@ -1241,6 +1289,7 @@ int ngp_trainer_serialize(ngp_trainer* t, void* buf, uint64_t* size) {
 		const uint64_t hdr[4] = {0x4e47504d49333535ULL /* "NGPMI355" */, 1, t->n, t->step};
 		memcpy(p, hdr, 32); p += 32;
 		NGP_HIP(hipDeviceSynchronize());
+		if (t->rec) t->w32_stale = true;  // lazy layout: the blob's weights always come from the records
 		t->sync_w32();
 		DevBuf soa;
 		float *m1 = t->m1, *m2 = t->m2, *ema32 = t->ema32;

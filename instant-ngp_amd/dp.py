@@ -100,13 +100,24 @@ class EngineComm:
             self.handle = None
 
 
-def make_allreduce_callback(group=None):
+def _host_allreduce(t, op, group, stream):
+    """All-reduce a device tensor through torch.distributed on the host: wait for `stream`, sum (or max)
+    a float32 host copy, write it back and wait for the copy (gloo: CPU tests, ranks sharing a GPU)."""
+    (torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()).synchronize()
+    h = t.float().cpu()
+    dist.all_reduce(h, op=op, group=group)
+    t.copy_(h.to(t.dtype))
+    torch.cuda.synchronize()
+
+
+def make_allreduce_callback(group=None, timer=None):
     """The engine's exchange hook (ngp_nerf_trainer_set_data_parallel) over torch.distributed.
 
     nccl (= RCCL over xGMI): the all-reduce is enqueued on the engine's stream. gloo (CPU tests, or
-    several ranks sharing one GPU): host round trip, summed in fp32. Keep the returned object alive
-    while the engine may call it."""
+    several ranks sharing one GPU): host round trip, summed in fp32. `timer` (optional) gets
+    `add(ms)` per host round trip. Keep the returned object alive while the engine may call it."""
     from .network import wrap_device
+    import time
 
     def cb(user, ptr, count, dtype, op, stream):
         try:
@@ -117,14 +128,59 @@ def make_allreduce_callback(group=None):
                 with torch.cuda.stream(s):
                     dist.all_reduce(t, op=rop, group=group)
             else:
-                (torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()).synchronize()
-                h = t.float().cpu()
-                dist.all_reduce(h, op=rop, group=group)
-                t.copy_(h.to(t.dtype))
-                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                _host_allreduce(t, rop, group, stream)
+                if timer is not None:
+                    timer.add(1e3 * (time.perf_counter() - t0))
             return 0
         except Exception:
             traceback.print_exc(file=sys.stderr)
             return -1
 
     return ALLREDUCE_FN(cb)
+
+
+class HostComm:
+    """Gradient exchange through torch.distributed with a host round trip (gloo backend): the same
+    interface as EngineComm (`world`, `fn`/`handle` for the engine's exchange hooks, `allreduce(tensor)`)
+    for ranks that share one GPU or run without RCCL. Not capturable into a HIP graph (the hook
+    synchronises the stream). Times its own round trips (`ms`, `calls`): the engine profiler sees only
+    device work."""
+
+    def __init__(self, rank, world, group=None):
+        self.rank, self.world, self.group = rank, world, group
+        self.ms, self.calls = 0.0, 0
+        self._cb = make_allreduce_callback(group, timer=self)
+        self.fn = C.cast(self._cb, C.c_void_p)
+        self.handle = None
+        self.wire = "f32"
+
+    def add(self, ms):
+        self.ms += ms
+        self.calls += 1
+
+    def reset_timer(self):
+        self.ms, self.calls = 0.0, 0
+
+    def allreduce(self, tensor, op="sum", stream=None):
+        import time
+        t0 = time.perf_counter()
+        _host_allreduce(tensor, dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX, self.group,
+                        stream if stream is not None else torch.cuda.current_stream().cuda_stream)
+        self.add(1e3 * (time.perf_counter() - t0))
+
+
+def make_comm(rank, world, group=None, wire="f32"):
+    """The gradient exchange for this process group: the engine's RCCL communicator under the nccl
+    backend, a host round trip (HostComm) under gloo."""
+    if dist.get_backend(group) == "nccl":
+        return EngineComm(rank, world, group, wire=wire)
+    return HostComm(rank, world, group)
+
+
+def reduce_scalar(value, op="max", group=None):
+    """All-reduce one float over the ranks (a device tensor under nccl, a host tensor under gloo)."""
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op={"max": dist.ReduceOp.MAX, "sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN}[op], group=group)
+    return float(t.item())

@@ -344,6 +344,18 @@ class Trainer:
             check(lib().ngp_trainer_set_allreduce(self.handle, comm.world, comm.fn, comm.handle))
         self._comm = comm
 
+    def train_step(self, x, dL_doutput, loss_scale=128.0, stream=None):
+        """Engine extension: one eager step of what capture_training_step records (forward_backward with the
+        grid's update fused into the backward where possible, the exchange hook, optimizer_step)."""
+        _check_input(x, self.model.input_width())
+        check(lib().ngp_trainer_train_step(self.handle, _stream(stream), x.shape[0], _ptr(x), x.stride(0),
+                                           _ptr(dL_doutput), dL_doutput.stride(0), float(loss_scale)))
+
+    def fused_update_active(self, n_batch):
+        """True when a training step of n_batch samples updates the grid inside the backward (the grid part
+        of the gradient buffer is then not written)."""
+        return bool(lib().ngp_trainer_fused_update_active(self.handle, int(n_batch)))
+
     def capture_training_step(self, x, dL_doutput, loss_scale=128.0, n_steps=1, with_optimizer=True, stream=None):
         """Engine extension: n_steps of forward_backward(x, dL_doutput) [+ optimizer_step] captured into
         one HIP graph (TrainingGraph.launch replays it). `stream` must not be the null stream."""

@@ -111,6 +111,14 @@ def _engine_comm_run(_rank, port, out_dir):
             tr.optimizer_step(128.0)
         torch.cuda.synchronize()
         hashes.append(hashlib.sha1(tr.params.cpu().numpy().tobytes()).hexdigest())
+    # a tensor view that is only 2-byte aligned: the widened path takes scalar loads there; at
+    # world 1 the widened sum is the identity, bit for bit
+    buf = torch.randn(4099, device="cuda").half()
+    view = buf[1:]
+    before = view.clone()
+    comm.allreduce(view)
+    torch.cuda.synchronize()
+    hashes.append(bool(torch.equal(view.view(torch.int16), before.view(torch.int16))))
     del comm
     dist.destroy_process_group()
     with open(os.path.join(out_dir, "comm.json"), "w") as f:
@@ -122,8 +130,9 @@ def test_engine_rccl_allreduce_in_captured_step(tmp_path):
         pytest.skip("no GPU")
     import torch.multiprocessing as mp
     mp.spawn(_engine_comm_run, args=(29400 + os.getpid() % 1000, str(tmp_path)), nprocs=1, join=True)
-    a, b = json.load(open(tmp_path / "comm.json"))
+    a, b, unaligned_ok = json.load(open(tmp_path / "comm.json"))
     assert a == b
+    assert unaligned_ok
 
 
 def _nerf_rccl_world1(_rank, port, out_dir):

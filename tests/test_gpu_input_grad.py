@@ -199,3 +199,123 @@ def test_density_forward_backward(pkg, orc):
     ctx2, _ = net.forward(x, torch.zeros((n, 16), dtype=torch.float16, device="cuda"))
     with pytest.raises(RuntimeError):
         net.density_backward(ctx2, torch.from_numpy(dL).cuda())
+
+
+def _sh4_np(d):
+    """Real spherical harmonics of degree 4 (16 values) of unit-cube-warped directions in float64: the
+    published closed forms tcnn's SH encoding evaluates on d = 2 in - 1 (independent of the engine and of
+    the oracle's derivative code)."""
+    x, y, z = (2.0 * d[..., k] - 1.0 for k in range(3))
+    xy, xz, yz, x2, y2, z2 = x * y, x * z, y * z, x * x, y * y, z * z
+    return np.stack([
+        np.full_like(x, 0.28209479177387814), -0.48860251190291987 * y, 0.48860251190291987 * z,
+        -0.48860251190291987 * x, 1.0925484305920792 * xy, -1.0925484305920792 * yz,
+        0.94617469575755997 * z2 - 0.31539156525251999, -1.0925484305920792 * xz,
+        0.54627421529603959 * x2 - 0.54627421529603959 * y2, 0.59004358992664352 * y * (-3.0 * x2 + y2),
+        2.8906114426405538 * xy * z, 0.45704579946446572 * y * (1.0 - 5.0 * z2),
+        0.3731763325901154 * z * (5.0 * z2 - 3.0), 0.45704579946446572 * x * (1.0 - 5.0 * z2),
+        1.4453057213202769 * z * (x2 - y2), 0.59004358992664352 * x * (-x2 + 3.0 * y2)], axis=-1)
+
+
+def test_input_gradients_against_finite_differences(pkg, orc):
+    """An independent check of the input-gradient formulas (the oracle restates the same ones).
+
+    Grid rows: the encoding is trilinear inside a cell, so for points whose cells at every level are the
+    same at x - h and x + h the central difference of sum_f dy_f enc_f(x) (enc from the GPU forward, fp16) is
+    the exact derivative up to the fp16 rounding of the features, which bounds the difference element by
+    element. SH rows: the central difference (float64, h = 1e-4) of sum_j dL/dsh_j SH_j(2 dir - 1) with the
+    published degree-4 closed forms, against the direction rows of the NerfNetwork backward (its own dL/dsh):
+    the factor 2 of d = 2 dir - 1 and every polynomial term."""
+    L, F, D = 4, 2, 3
+    enc = {"otype": "HashGrid", "n_levels": L, "n_features_per_level": F, "log2_hashmap_size": 19,
+           "base_resolution": 16, "per_level_scale": 2.0}
+    net = pkg.NetworkWithInputEncoding(D, 1, enc, {"otype": "FullyFusedMLP", "activation": "ReLU",
+                                                   "output_activation": "None", "n_neurons": 64, "n_hidden_layers": 1})
+    rng = np.random.default_rng(21)
+    nm = net.n_matrix_params
+    p16 = np.zeros(net.n_params, np.float16)
+    p16[nm:] = rng.uniform(-1, 1, net.n_params - nm).astype(np.float16)
+    params = torch.from_numpy(p16).cuda()
+    net.set_params(params, params, torch.zeros_like(params))
+    n, h = 8192, np.float32(2.0 ** -12)
+    pos = rng.uniform(0.05, 0.95, (n, D)).astype(np.float32)
+    W = net.layout().encoding_width
+    dy = np.zeros((n, W), np.float16)
+    dy[:, :L * F] = rng.standard_normal((n, L * F)).astype(np.float16)
+    got = torch.zeros((n, D), device="cuda")
+    net.encoding_backward(torch.from_numpy(pos).cuda(), torch.from_numpy(dy).cuda(), grad_mode=pkg.GRAD_IGNORE, dL_dinput=got)
+    got = got.cpu().numpy().astype(np.float64)
+    scales = np.float32(16.0) * np.float32(2.0) ** np.arange(L, dtype=np.float32) - np.float32(1.0)
+    dyf = dy[:, :L * F].astype(np.float64)
+    checked = 0
+    for d in range(D):
+        xs = []
+        for sgn in (1, -1):
+            x = pos.copy()
+            x[:, d] = pos[:, d] + np.float32(sgn) * h
+            xs.append(x)
+        # cells of every level at both points (pos = scale * x + 0.5, floor: the engine's grid arithmetic)
+        same = np.ones(n, bool)
+        for sc in scales:
+            same &= np.all(np.floor(xs[0] * sc + np.float32(0.5)) == np.floor(xs[1] * sc + np.float32(0.5)), axis=1)
+        e = [net.encode(torch.from_numpy(x).cuda()).cpu().numpy()[:, :L * F] for x in xs]
+        step = (xs[0][:, d].astype(np.float64) - xs[1][:, d].astype(np.float64))
+        fd = ((e[0].astype(np.float64) - e[1].astype(np.float64)) * dyf).sum(1) / step
+        ulp = lambda a: np.spacing(np.abs(a).astype(np.float16)).astype(np.float64)
+        bound = (np.abs(dyf) * (ulp(e[0]) + ulp(e[1])) / 2).sum(1) / step + 1e-4 * np.abs(got[:, d]) + 1e-6
+        err = np.abs(fd - got[:, d])
+        assert np.all(err[same] <= bound[same]), (d, float((err / bound)[same].max()))
+        checked += int(same.sum())
+    assert checked > n  # most points stay inside their cells at every level
+
+    # SH rows through the NerfNetwork backward
+    net2, m, p16b, params2, grads2 = nerf_with_params(pkg, orc, seed=8)
+    c = coords(3000, 8)
+    g = np.random.default_rng(8)
+    dL = np.zeros((3000, 16), np.float16)
+    dL[:, :4] = g.uniform(-1, 1, (3000, 4))
+    x = torch.from_numpy(c).cuda()
+    ctx, _ = net2.forward(x, torch.zeros((3000, 16), dtype=torch.float16, device="cuda"))
+    din = torch.zeros((3000, 7), device="cuda")
+    net2.backward(ctx, torch.from_numpy(dL).cuda(), dL_dinput=din)
+    torch.cuda.synchronize()
+    dsh = net2.workspace("dL_dsh", 3000).cpu().numpy().astype(np.float64)
+    dirs = c[:, 4:].astype(np.float64)
+    assert np.allclose(_sh4_np(dirs[:5]), np.stack([orc.sh4(2.0 * d - 1.0) for d in c[:5, 4:]]), atol=1e-6)
+    hh = 1e-4
+    fd = np.zeros((3000, 3))
+    for k in range(3):
+        dp, dm = dirs.copy(), dirs.copy()
+        dp[:, k] += hh
+        dm[:, k] -= hh
+        fd[:, k] = ((_sh4_np(dp) - _sh4_np(dm)) * dsh).sum(1) / (2 * hh)
+    gd = din.cpu().numpy()[:, 4:].astype(np.float64)
+    scale = (np.abs(dsh).sum(1) * 12.0)[:, None]
+    assert np.all(np.abs(gd - fd) <= 1e-5 * scale + 1e-6), float(np.abs(gd - fd).max())
+
+
+def test_backward_honours_inference_params(pkg, orc):
+    """nerf_network.h:256-335: backward_impl runs every sub-backward with the forward's use_inference_params.
+    A forward on the inference parameters followed by backward must give the input and parameter gradients
+    of a network whose training parameters ARE those inference parameters, bit for bit."""
+    net, m, p16, params, grads = nerf_with_params(pkg, orc, seed=11)
+    g = np.random.default_rng(11)
+    other = torch.from_numpy((p16.view(np.float16).astype(np.float32) *
+                              g.uniform(0.5, 1.5, p16.size).astype(np.float32)).astype(np.float16)).cuda()
+    n = 5000
+    c = torch.from_numpy(coords(n, 11)).cuda()
+    dL = np.zeros((n, 16), np.float16)
+    dL[:, :4] = g.uniform(-1, 1, (n, 4))
+    dL = torch.from_numpy(dL).cuda()
+    res = []
+    for train_p, inf_p, use_inf in ((other, params, True), (params, params, False)):
+        gr = torch.zeros_like(params)
+        net.set_params(train_p, inf_p, gr)
+        out = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
+        ctx, _ = net.forward(c, out, use_inference_params=use_inf)
+        din = torch.zeros((n, 7), device="cuda")
+        net.backward(ctx, dL, dL_dinput=din)
+        torch.cuda.synchronize()
+        res.append((out.cpu().numpy().view(np.uint16), din.cpu().numpy(), gr.cpu().numpy().view(np.uint16)))
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(a, b)

@@ -216,3 +216,51 @@ def test_fused_optimizer_captured_steps_bitwise(pkg, kind):
             np.testing.assert_array_equal(a, e)
         assert b == runs["eager"][3], f"{name}: serialized optimizer state differs"
         assert st == runs["eager"][4] == 12
+
+
+def test_lazy_mirror_is_read_only():
+    """ngp_trainer_params_full_precision on the lazy layout hands out a mirror of the records' weights:
+    writing into it reaches neither training nor serialize (which read the records), and the next read of
+    the accessor shows the records again (the mirror used to be trusted once synced)."""
+    from __graft_entry__ import load_package
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    pkg = load_package()
+    net, tr = make_trainer(pkg, "sdf", True)
+    for step in range(4):
+        x, dl = batch("sdf", 4096, step)
+        net.forward_backward(x, dl)
+        tr.optimizer_step(128.0)
+    torch.cuda.synchronize()
+    blob = tr.serialize()
+    w = tr.params_full_precision
+    before = w.cpu().numpy().copy()
+    w.mul_(2.0)  # a caller's write into the mirror
+    torch.cuda.synchronize()
+    assert tr.serialize() == blob
+    np.testing.assert_array_equal(tr.params_full_precision.cpu().numpy(), before)
+
+
+@pytest.mark.parametrize("lazy", [False, True])
+def test_eager_train_step_equals_captured_step(pkg, lazy):
+    """ngp_trainer_train_step (what bench.py's per-kernel replay runs) is one captured step launched eagerly:
+    K eager steps and one K-step graph train bit for bit alike, with the grid's update fused into the
+    backward on the lazy layout."""
+    runs = []
+    for mode in ("eager", "graph"):
+        net, tr = make_trainer(pkg, "nerf", lazy)
+        x, dl = batch("nerf", 1 << 15, 0)
+        assert tr.fused_update_active(x.shape[0]) == lazy
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            if mode == "eager":
+                for _ in range(3):
+                    tr.train_step(x, dl, 128.0, stream=s)
+            else:
+                tr.capture_training_step(x, dl, 128.0, n_steps=3, stream=s).launch(s)
+        s.synchronize()
+        runs.append((tr.serialize(), tr.params.cpu().numpy().view(np.uint16).copy(), tr.step))
+        del net, tr
+    assert runs[0][0] == runs[1][0]
+    np.testing.assert_array_equal(runs[0][1], runs[1][1])
+    assert runs[0][2] == runs[1][2] == 3

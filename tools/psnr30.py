@@ -39,7 +39,7 @@ def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8, rank=0, wor
         run.set_data_parallel(rank, world)
         dist.barrier()
     torch.cuda.synchronize()
-    samples, steps = 0, 0
+    samples, steps = 0, 0  # measured_batch_size is the global count under data parallelism (all-reduced)
     t_start = time.time()
     curve = []
     while True:
@@ -50,18 +50,14 @@ def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8, rank=0, wor
             curve.append((round(time.time() - t_start, 2), steps, round(st["loss"], 6)))
         if world > 1:
             if steps % 32 == 0:  # the ranks must run the same number of steps (collectives inside)
-                flag = torch.tensor([float(time.time() - t_start >= seconds)], device="cuda")
-                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-                if flag.item() > 0:
+                if pkg.dp.reduce_scalar(float(time.time() - t_start >= seconds), "max") > 0:
                     break
         elif time.time() - t_start >= seconds:
             break
     torch.cuda.synchronize()
     t_train = time.time() - t_start
     if world > 1:
-        tt = torch.tensor([t_train], device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_train = float(tt.item())
+        t_train = pkg.dp.reduce_scalar(t_train, "max")
         if rank != 0:
             return {"value": samples / t_train, "steps": steps, "train_seconds": t_train}
     r = pkg.nerf.NerfRenderer()
