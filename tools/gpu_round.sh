@@ -25,7 +25,7 @@ if has bench; then
 fi
 if has prof; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/prof" -o run -- \
-      python3 bench.py --no-cpu-baseline --e2e-seconds 0 --c3-seconds 0 --no-c5 ${PMC_ARGS} > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+      python3 bench.py --no-cpu-baseline --e2e-seconds 0 --c3-seconds 0 --no-c5 --pmc-collect ${PMC_ARGS} > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
   find "$OUT/prof" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
   rm -rf "$OUT/prof"
   head -12 "$OUT/kernel_stats.csv"
@@ -34,7 +34,7 @@ if has pmc; then
   # separate passes (TCC slots): sized read requests, WRITE_SIZE, MFMA utilisation; eager launches; one
   # summary per variant (PMC_VARIANTS, default C2 C2p C5) -> $OUT/pmc_summary_<variant>.json
   for V in ${PMC_VARIANTS:-C2 C2p C5}; do
-    BENCH_PMC="python3 bench.py --variant $V --no-cpu-baseline --e2e-seconds 0 --c3-seconds 0 --no-c2p --no-c5 --graph 0 --steps 5 --warmup 2 --no-opt-count ${PMC_ARGS}"
+    BENCH_PMC="python3 bench.py --variant $V --no-cpu-baseline --e2e-seconds 0 --c3-seconds 0 --no-c2p --no-c5 --graph 0 --steps 5 --warmup 2 --no-opt-count --pmc-collect ${PMC_ARGS}"
     i=0
     for c in "TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" "WRITE_SIZE" \
              "MfmaUtil SQ_INSTS_VALU_MFMA_MOPS_F16"; do
@@ -50,7 +50,7 @@ fi
 if has pmcx; then
   # extra counters for one pass, e.g. PMCX="TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"
   timeout -k 10 300 rocprofv3 --pmc ${PMCX} -f csv -d "$OUT/pmcx" -o run -- \
-      python3 bench.py --no-cpu-baseline --e2e-seconds 0 --c3-seconds 0 --no-c2p --no-c5 --graph 0 --steps 5 --warmup 2 ${PMC_ARGS} > "$OUT/pmcx.json" 2> "$OUT/pmcx.err"
+      python3 bench.py --no-cpu-baseline --e2e-seconds 0 --c3-seconds 0 --no-c2p --no-c5 --graph 0 --steps 5 --warmup 2 --pmc-collect ${PMC_ARGS} > "$OUT/pmcx.json" 2> "$OUT/pmcx.err"
   find "$OUT/pmcx" -name '*counter_collection.csv' -exec cp {} "$OUT/counters_x.csv" \;
   rm -rf "$OUT/pmcx"
   python3 tools/pmc_table.py "$OUT/counters_x.csv" | tee "$OUT/pmcx_table.txt"
