@@ -351,6 +351,11 @@ int ngp_nerf_grid_mean_and_bitfield(void* stream, const float* grid, uint32_t ma
 int ngp_nerf_trainer_create(ngp_model* model, ngp_trainer* trainer, const ngp_nerf_dataset* ds,
                             const ngp_nerf_config* cfg, uint64_t seed, ngp_nerf_trainer** out);
 void ngp_nerf_trainer_destroy(ngp_nerf_trainer* t);
+/* The training knobs of a live trainer (Testbed::Nerf::Training members the pybind surface writes, e.g.
+ * random_bg_color, loss_type, near_distance, target batch size). max_cascade and the aabb size the density
+ * grid and cannot change (recreate the trainer). */
+int ngp_nerf_trainer_get_config(const ngp_nerf_trainer* t, ngp_nerf_config* out);
+int ngp_nerf_trainer_set_config(ngp_nerf_trainer* t, const ngp_nerf_config* cfg);
 int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_nerf_stats* out);
 int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** density_grid, uint8_t** bitfield, float** mean_density);
 /* The same pointers for READING only: keeps a prelaunched (pipelined) sampler, which reads the bitfield

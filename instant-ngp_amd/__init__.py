@@ -15,3 +15,15 @@ def create_nerf_network(cfg, n_pos_dims=3, n_dir_dims=3, n_extra_dims=0, dir_off
     """Testbed::reset_network's NerfNetwork construction (src/testbed.cu:4029-4042)."""
     return NerfNetwork(n_pos_dims, n_dir_dims, n_extra_dims, dir_offset, cfg["encoding"], cfg.get("dir_encoding"),
                        cfg["network"], cfg["rgb_network"])
+
+
+def pyngp():
+    """The pybind11 Testbed module (csrc/python_api.cpp, built into lib/ by build()): the reference's
+    `import pyngp as ngp` surface (src/python_api.cu)."""
+    import importlib
+    import os
+    import sys
+    lib_dir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+    if lib_dir not in sys.path:
+        sys.path.insert(0, lib_dir)
+    return importlib.import_module("pyngp")

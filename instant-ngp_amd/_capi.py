@@ -153,6 +153,8 @@ SIGNATURES = {
     "ngp_nerf_grid_mean_and_bitfield": (i32, [P, P, u32, P, P]),
     "ngp_nerf_trainer_create": (i32, [P, P, P, C.POINTER(NerfConfig), u64, C.POINTER(P)]),
     "ngp_nerf_trainer_destroy": (None, [P]),
+    "ngp_nerf_trainer_get_config": (i32, [P, C.POINTER(NerfConfig)]),
+    "ngp_nerf_trainer_set_config": (i32, [P, C.POINTER(NerfConfig)]),
     "ngp_nerf_train_step": (i32, [P, P, i32, C.POINTER(NerfStats)]),
     "ngp_nerf_trainer_buffers": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
     "ngp_nerf_trainer_buffers_read": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),

@@ -2,6 +2,7 @@
 // e.g. configs/image/base.json, carry // comments, which are accepted).
 #pragma once
 #include <cctype>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <memory>
@@ -27,6 +28,45 @@ struct Json {
 	}
 	double number_or(const std::string& k, double d) const { return contains(k) ? (*this)[k].num : d; }
 	std::string string_or(const std::string& k, const std::string& d) const { return contains(k) ? (*this)[k].str : d; }
+
+	// compact JSON text (numbers with enough digits to round-trip a double)
+	std::string dump() const {
+		switch (type) {
+		case Null: return "null";
+		case Bool: return b ? "true" : "false";
+		case Number: {
+			char buf[32];
+			snprintf(buf, sizeof(buf), "%.17g", num);
+			return buf;
+		}
+		case String: return quote(str);
+		case Array: {
+			std::string o = "[";
+			for (size_t i = 0; i < arr.size(); ++i) o += (i ? "," : "") + arr[i].dump();
+			return o + "]";
+		}
+		case Object: {
+			std::string o = "{";
+			bool first = true;
+			for (const auto& kv : obj) {
+				o += (first ? "" : ",") + quote(kv.first) + ":" + kv.second.dump();
+				first = false;
+			}
+			return o + "}";
+		}
+		}
+		return "null";
+	}
+	static std::string quote(const std::string& s) {
+		std::string o = "\"";
+		for (char c : s) {
+			if (c == '"' || c == '\\') { o += '\\'; o += c; }
+			else if (c == '\n') o += "\\n";
+			else if (c == '\t') o += "\\t";
+			else o += c;
+		}
+		return o + "\"";
+	}
 
 	static Json parse(const std::string& s) {
 		size_t i = 0;

@@ -386,6 +386,25 @@ int ngp_nerf_trainer_create(ngp_model* model, ngp_trainer* trainer, const ngp_ne
 
 void ngp_nerf_trainer_destroy(ngp_nerf_trainer* t) { delete t; }
 
+int ngp_nerf_trainer_get_config(const ngp_nerf_trainer* t, ngp_nerf_config* out) {
+	if (!t || !out) return NGP_INVALID;
+	*out = t->cfg;
+	return NGP_OK;
+}
+
+int ngp_nerf_trainer_set_config(ngp_nerf_trainer* t, const ngp_nerf_config* cfg) {
+	if (!t || !cfg) return NGP_INVALID;
+	NERF_TRY({
+		NGP_CHECK(cfg->max_cascade == t->cfg.max_cascade, "set_config: max_cascade sizes the density grid (reset the trainer)");
+		for (int k = 0; k < 3; ++k)
+			NGP_CHECK(cfg->aabb_min[k] == t->cfg.aabb_min[k] && cfg->aabb_max[k] == t->cfg.aabb_max[k],
+			          "set_config: the aabb is fixed for the trainer's lifetime (reset the trainer)");
+		NGP_CHECK(cfg->target_batch_size > 0 && cfg->target_batch_size % 256 == 0, "set_config: target_batch_size");
+		t->drain();  // a prelaunched sampler ran with the old knobs
+		t->cfg = *cfg;
+	});
+}
+
 static void check_rc(int rc) { if (rc != NGP_OK) throw Error(ngp_last_error()); }
 
 // ---- rendering ---------------------------------------------------------------------------------

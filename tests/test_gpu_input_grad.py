@@ -281,7 +281,7 @@ def test_input_gradients_against_finite_differences(pkg, orc):
     torch.cuda.synchronize()
     dsh = net2.workspace("dL_dsh", 3000).cpu().numpy().astype(np.float64)
     dirs = c[:, 4:].astype(np.float64)
-    assert np.allclose(_sh4_np(dirs[:5]), np.stack([orc.sh4(2.0 * d - 1.0) for d in c[:5, 4:]]), atol=1e-6)
+    assert np.allclose(_sh4_np(dirs[:5]), np.stack([orc.sh4(d) for d in c[:5, 4:]]), atol=1e-6)
     hh = 1e-4
     fd = np.zeros((3000, 3))
     for k in range(3):

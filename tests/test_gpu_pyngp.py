@@ -1,0 +1,129 @@
+"""The pybind11 Testbed (`pyngp`, csrc/python_api.cpp over csrc/testbed_host.hpp) on the GPU: the reference's
+scripting flow (scripts/run.py: Testbed(), load_training_data, shall_train, `while testbed.frame()`,
+save_snapshot / load_snapshot, render) on a procedural NeRF scene written to disk as transforms.json + PNGs.
+
+* 200 frames train the scene; the C++ Testbed trains bit for bit like the package's Python Testbed mirror
+  (nerf.NerfTraining) on the same files and seeds: the renders of the two networks are identical.
+* A snapshot written by one Testbed and loaded by another gives the same training step and the same render.
+* SDF (armadillo.obj, when staged) and image (.npy) Testbeds train through the same surface."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    from __graft_entry__ import load_package
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return load_package()
+
+
+@pytest.fixture(scope="module")
+def scene_dir(pkg, tmp_path_factory):
+    from PIL import Image
+    S = pkg.synthetic
+    d = tmp_path_factory.mktemp("standin")
+    frames = []
+    for i, c2w in enumerate(S.camera_poses(16, seed=4)):
+        Image.fromarray(S.render(c2w, 96, 96)).save(d / f"r_{i}.png")
+        frames.append({"file_path": f"./r_{i}", "transform_matrix": np.asarray(c2w, np.float64).tolist()})
+    (d / "transforms.json").write_text(json.dumps({"camera_angle_x": S.LEGO_CAMERA_ANGLE_X, "frames": frames}))
+    return str(d)
+
+
+def test_testbed_trains_like_the_python_mirror_and_round_trips_a_snapshot(pkg, scene_dir, tmp_path):
+    ngp = pkg.pyngp()
+    tb = ngp.Testbed()
+    tb.load_training_data(scene_dir)
+    assert tb.mode == ngp.TestbedMode.Nerf
+    assert tb.nerf.training.dataset.n_images == 16
+    tb.shall_train = True
+    losses = []
+    while tb.frame():
+        if tb.training_step % 16 == 1:  # the loss is read back every 16 steps (testbed.cu:4346)
+            losses.append(tb.loss)
+        if tb.training_step >= 200:
+            break
+    assert tb.training_step == 200
+    assert tb.n_params() == 3302400 and tb.n_encoding_params() == 3293184
+    assert all(np.isfinite(losses)) and np.mean(losses[-3:]) < 0.5 * losses[0]
+    tb.set_camera_to_training_view(3)
+    img = tb.render(64, 48, spp=1, linear=True)
+    assert img.shape == (48, 64, 4) and np.isfinite(img).all() and img[..., :3].max() > 0.05
+
+    # the Python Testbed mirror on the same files and seeds (Trainer / NerfTraining seed 1337)
+    d = pkg.nerf_data.load_nerf(scene_dir)
+    ds = pkg.nerf.NerfDataset(d.images, d.rgba8)
+    cfg = pkg.nerf.default_config(d.aabb_scale)
+    ncfg = pkg.nerf_config("C2")
+    net = pkg.create_nerf_network(ncfg)
+    tr = pkg.Trainer(net, ncfg["optimizer"], seed=1337)
+    run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
+    for k in range(200):
+        run.train_step(get_loss=(k % 16 == 0))
+    im3 = d.images[3]
+    # the Testbed's float arithmetic: relative focal length (set_camera_to_training_view) x the render height
+    f32 = np.float32
+    focal = tuple(float(f32(f32(im3.focal_length[k]) / f32(im3.height)) * f32(48)) for k in range(2))
+    cam = pkg.nerf.make_image(64, 48, list(im3.xform), focal=focal, principal=tuple(im3.principal_point))
+    ref = pkg.nerf.NerfRenderer().render(net, cfg, cam, run.bitfield, spp=1, background=(0, 0, 0, 1)).cpu().numpy()
+    np.testing.assert_array_equal(img, ref)
+
+    # snapshot round trip into a fresh Testbed
+    snap = str(tmp_path / "standin.ingp")
+    tb.save_snapshot(snap, include_optimizer_state=True, compress=True)
+    tb2 = ngp.Testbed()
+    tb2.load_training_data(scene_dir)
+    tb2.load_snapshot(snap)
+    assert tb2.training_step == 200
+    tb2.set_camera_to_training_view(3)
+    np.testing.assert_array_equal(tb2.render(64, 48, spp=1, linear=True), img)
+    # shall_train off: frame() renders nothing and trains nothing
+    tb2.shall_train = False
+    tb2.frame()
+    assert tb2.training_step == 200
+    # a live knob reaches the trainer: no random background, then training continues
+    tb.nerf.training.random_bg_color = False
+    assert tb.nerf.training.random_bg_color == 0
+    tb.train(1 << 18)
+    assert tb.training_step == 201
+    tb.reset()
+    assert tb.training_step == 0
+
+
+def test_testbed_sdf_and_image_modes(pkg, tmp_path):
+    ngp = pkg.pyngp()
+    arm = os.path.join(ROOT, "data", "sdf", "armadillo.obj")
+    if os.path.isfile(arm):
+        tb = ngp.Testbed()
+        tb.load_training_data(arm)
+        assert tb.mode == ngp.TestbedMode.Sdf
+        tb.shall_train = True
+        tb.training_batch_size = 1 << 16
+        for _ in range(33):
+            tb.frame()
+        assert tb.training_step == 33 and np.isfinite(tb.loss) and tb.loss > 0
+    img = pkg.synthetic.synthetic_image(64, 48, seed=2)
+    path = tmp_path / "img.npy"
+    np.save(path, img.astype(np.float32))
+    tb = ngp.Testbed()
+    tb.load_training_data(str(path))
+    assert tb.mode == ngp.TestbedMode.Image
+    tb.reload_network_from_json({**pkg.IMAGE_BASE, "encoding": {**pkg.IMAGE_BASE["encoding"], "log2_hashmap_size": 14}})
+    tb.shall_train = True
+    tb.training_batch_size = 1 << 14
+    first = None
+    for _ in range(200):
+        tb.frame()
+        if tb.training_step == 1:
+            first = tb.loss
+    out = tb.render(64, 48, spp=1, linear=True)
+    assert out.shape == (48, 64, 4) and np.isfinite(out).all()
+    assert tb.loss < first
