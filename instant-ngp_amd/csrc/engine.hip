@@ -167,6 +167,7 @@ struct ngp_model {
 	bool fuse_infer = true;                 // option "fuse_infer": NerfNetwork inference encodes inside the MLP kernel
 	bool fuse_slabs = true;                 // option "fuse_slabs": dW slab reduction inside the grid backward's last kernel
 	bool fuse_opt = true;                   // option "fuse_opt": lazy-layout optimizer update inside the grid backward (training_step)
+	bool mlp_train16 = true;                // option "mlp_train16": the training MLP at two waves per SIMD (mlp_train16.hip)
 	bool fuse_train = false;                // option "fuse_train": ... and the training forward_backward too (off: the
 	                                        // training kernel runs 1 wave/SIMD, the gathers are not hidden; C2 0.157 -> 0.161 ms)
 	int grid_forward_mode = 0;              // option "grid_forward_mode": 0 auto, 1 per-sample rows, 2 XCD-partitioned
@@ -340,6 +341,8 @@ struct ngp_model {
 			a.n_matrix = (uint32_t)n_matrix(); a.density_woff = 0; a.rgb_woff = (uint32_t)mlp0_params;
 			a.dL_dsh = dL_dsh;
 			if (ex) { a.dL_ddens = ex->ddens; a.ddens_stride = ex->ddens_stride; }
+			a.params = pick(inference);
+			a.train16 = mlp_train16 ? 1u : 0u;
 			if (mode == MLP_INFER_ENC || mode == MLP_TRAIN_ENC) {
 				if (inference) sync_inference(s);
 				a.table = pick(inference) + grid_offset(); a.max_level = max_level; a.gc = make_grid_const(grid);
@@ -714,6 +717,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			m->fuse_infer = value != 0;
 		} else if (k == "fuse_train") {
 			m->fuse_train = value != 0;
+		} else if (k == "mlp_train16") {
+			m->mlp_train16 = value != 0;
 		} else if (k == "fuse_slabs") {
 			m->fuse_slabs = value != 0;
 		} else if (k == "fuse_opt") {

@@ -62,6 +62,10 @@ struct NerfMlpArgs {
 	// MLP_DENSITY_TRAIN (NerfNetwork::density_backward, nerf_network.h:384-428): dL/d(density network output),
 	// fp16 AoS [n x ddens_stride] (16 rows; stride a multiple of 4)
 	const f16* dL_ddens; uint32_t ddens_stride;
+	// the fp16 parameters the fragments are built from (k_nerf_mlp_train16 builds its own from them) and
+	// whether MLP_TRAIN may run k_nerf_mlp_train16 (model option "mlp_train16")
+	const f16* params;
+	uint32_t train16;
 };
 
 struct MlpArgs {  // single MLP behind an encoding (tcnn::NetworkWithInputEncoding): image / SDF
@@ -102,6 +106,8 @@ bool nerf_mlp_fused_encoding_ok(const GridDesc& g, uint32_t enc_width);
 // Launch sizes for the training kernel: one persistent block per CU (slab count = blocks).
 uint32_t nerf_mlp_train_blocks(uint32_t n);
 void nerf_mlp_run(const NerfMlpPlan& p, MlpMode mode, const NerfMlpArgs& a, hipStream_t s);
+// MLP_TRAIN at two waves per SIMD (mlp_train16.hip); false when the configuration is not covered
+bool nerf_mlp_train16_run(const NerfMlpPlan& p, const NerfMlpArgs& a, hipStream_t s);
 uint32_t mlp_train_blocks(uint32_t n);
 void mlp_run(const MlpPlan& p, MlpMode mode, const MlpArgs& a, hipStream_t s);
 

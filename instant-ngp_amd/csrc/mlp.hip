@@ -1137,6 +1137,7 @@ static void dispatch_nerf_fused(const NerfMlpPlan& p, const NerfMlpArgs& a, hipS
 
 void nerf_mlp_run(const NerfMlpPlan& p, MlpMode mode, const NerfMlpArgs& a, hipStream_t s) {
 	if (a.n == 0) return;
+	if (mode == MLP_TRAIN && a.train16 && nerf_mlp_train16_run(p, a, s)) return;
 	switch (mode) {
 		case MLP_INFER: dispatch_nerf<MLP_INFER>(p, a, s); break;
 		case MLP_TRAIN: dispatch_nerf<MLP_TRAIN>(p, a, s); break;

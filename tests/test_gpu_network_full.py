@@ -79,11 +79,15 @@ def check_close(name, got, ref, cond, margin=None):
                   f"{np.sort(margin[rows])[-3:].tolist()}; {int((margin < MARGIN).sum())} samples that close)")
 
 
+@pytest.mark.parametrize("train16", [1, 0])
 @pytest.mark.parametrize("cfg_name,log2T,L,F", [("C2", 19, 4, 4), ("C2p", 19, 16, 2)])
-def test_nerf_network_full_batch(pkg, orc, cfg_name, log2T, L, F, record_property):
+def test_nerf_network_full_batch(pkg, orc, cfg_name, log2T, L, F, train16, record_property):
+    """train16 = 1: the two-waves-per-SIMD training kernel (mlp_train16.hip, the default for C2 and C2');
+    0: k_nerf_mlp_train (mlp.hip), kept for the configurations the former does not cover."""
     cfg = pkg.nerf_config(cfg_name)
     cfg["encoding"]["log2_hashmap_size"] = log2T
     net = pkg.create_nerf_network(cfg)
+    net.set_option("mlp_train16", train16)
     tr = pkg.Trainer(net, cfg["optimizer"])
     nm = net.n_matrix_params
     # trained-looking parameters: Xavier MLP (initialize_params), grid entries U(-0.5, 0.5)

@@ -76,15 +76,30 @@ def test_testbed_trains_like_the_python_mirror_and_round_trips_a_snapshot(pkg, s
     ref = pkg.nerf.NerfRenderer().render(net, cfg, cam, run.bitfield, spp=1, background=(0, 0, 0, 1)).cpu().numpy()
     np.testing.assert_array_equal(img, ref)
 
-    # snapshot round trip into a fresh Testbed
-    snap = str(tmp_path / "standin.ingp")
+    # snapshot round trip into a fresh Testbed: the parameters, optimizer state and fp16 density grid it
+    # restores are the ones saved (its own snapshot carries them unchanged), and it renders what the
+    # Python mirror renders after loading the same file (after a load the inference parameters are the
+    # loaded parameters and the bitfield follows from the fp16 grid, testbed.cu:4939-5057)
+    import gzip
+    import msgpack
+    snap, snap2 = str(tmp_path / "standin.ingp"), str(tmp_path / "standin2.ingp")
     tb.save_snapshot(snap, include_optimizer_state=True, compress=True)
     tb2 = ngp.Testbed()
     tb2.load_training_data(scene_dir)
     tb2.load_snapshot(snap)
     assert tb2.training_step == 200
+    tb2.save_snapshot(snap2, include_optimizer_state=True, compress=True)
+    a, b = (msgpack.unpackb(gzip.decompress(open(p, "rb").read()), raw=False) for p in (snap, snap2))
+    for key in ("params_binary", "density_grid_binary"):
+        va = a["snapshot"][key] if key in a["snapshot"] else a[key]
+        vb = b["snapshot"][key] if key in b["snapshot"] else b[key]
+        assert len(va) > 0 and va == vb, key
     tb2.set_camera_to_training_view(3)
-    np.testing.assert_array_equal(tb2.render(64, 48, spp=1, linear=True), img)
+    img2 = tb2.render(64, 48, spp=1, linear=True)
+    run.load_snapshot(snap)
+    ref2 = pkg.nerf.NerfRenderer().render(net, cfg, cam, run.bitfield, spp=1, background=(0, 0, 0, 1)).cpu().numpy()
+    np.testing.assert_array_equal(img2, ref2)
+    assert np.abs(img2 - img).mean() < 0.05  # the EMA (inference) parameters before saving vs the loaded ones
     # shall_train off: frame() renders nothing and trains nothing
     tb2.shall_train = False
     tb2.frame()
