@@ -588,6 +588,25 @@ int ngp_free(void* ptr) { NGP_TRY(NGP_HIP(hipFree(ptr))); }
 int ngp_memcpy(void* dst, const void* src, size_t bytes, int kind) { NGP_TRY(NGP_HIP(hipMemcpy(dst, src, bytes, (hipMemcpyKind)kind))); }
 int ngp_stream_synchronize(void* stream) { NGP_TRY(NGP_HIP(hipStreamSynchronize(S(stream)))); }
 
+// NGP_MODEL_OPTS="key=value,key=value": engine options applied to every model at creation (A/B runs of whole
+// programs, tools/ab.sh); an unknown key or a bad value fails the creation
+static void apply_env_options(ngp_model* m) {
+	const char* env = getenv("NGP_MODEL_OPTS");
+	if (!env || !*env) return;
+	std::string all = env;
+	size_t pos = 0;
+	while (pos < all.size()) {
+		size_t end = all.find(',', pos);
+		if (end == std::string::npos) end = all.size();
+		const std::string kv = all.substr(pos, end - pos);
+		pos = end + 1;
+		if (kv.empty()) continue;
+		const size_t eq = kv.find('=');
+		NGP_CHECK(eq != std::string::npos, "NGP_MODEL_OPTS: expected key=value, got " + kv);
+		if (ngp_model_set_option(m, kv.substr(0, eq).c_str(), atof(kv.c_str() + eq + 1)) != NGP_OK) throw Error(g_last_error);
+	}
+}
+
 int ngp_nerf_network_create(uint32_t n_pos_dims, uint32_t n_dir_dims, uint32_t n_extra_dims, uint32_t dir_offset,
                             const char* pos_encoding_json, const char* dir_encoding_json, const char* density_network_json,
                             const char* rgb_network_json, ngp_model** out) {
@@ -618,6 +637,7 @@ int ngp_nerf_network_create(uint32_t n_pos_dims, uint32_t n_dir_dims, uint32_t n
 		m->n_input_dims = dir_offset + n_dir_dims + n_extra_dims;
 		m->n_output_dims = 4;
 		m->finalize();
+		apply_env_options(m.get());
 		*out = m.release();
 	});
 }
@@ -639,6 +659,7 @@ int ngp_network_with_input_encoding_create(uint32_t n_input_dims, uint32_t n_out
 		m->mlp0_params = m->mplan.mlp.n_params();
 		m->mlp1_params = 0;
 		m->finalize();
+		apply_env_options(m.get());
 		*out = m.release();
 	});
 }

@@ -183,9 +183,21 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const int pair = wave >> 1, half = wave & 1;
 	f16* img = imgs + pair * T::IMG_HALVES;
-	const f16* P = a.params;
-	const f16* Wd = P + a.density_woff;  // density MLP: [64 x 16ES], (DH-1) x [64 x 64], [16 x 64]
-	const f16* Wr = P + a.rgb_woff;      // rgb MLP:     [64 x 32], (RH-1) x [64 x 64], [16 x 64]
+	// the MLP parameters ([density | rgb], n_matrix halves) staged in the image region with 16-B loads; the
+	// fragments are gathered from there (gathering them from global costs ~150 scattered 2-B loads per lane)
+	f16* stage = imgs;
+	{
+		const uint32_t nm = a.n_matrix;
+		const f16* src = a.params;
+		if (nm % 8 == 0 && ((uintptr_t)src & 15) == 0) {
+			for (uint32_t i = 8 * threadIdx.x; i < nm; i += 8 * blockDim.x) *(f16x8*)(stage + i) = *(const f16x8*)(src + i);
+		} else {
+			for (uint32_t i = threadIdx.x; i < nm; i += blockDim.x) stage[i] = src[i];
+		}
+	}
+	__syncthreads();
+	const f16* Wd = stage + a.density_woff;  // density MLP: [64 x 16ES], (DH-1) x [64 x 64], [16 x 64]
+	const f16* Wr = stage + a.rgb_woff;      // rgb MLP:     [64 x 32], (RH-1) x [64 x 64], [16 x 64]
 	auto wd = [&](int l) { return Wd + (l == 0 ? 0 : 64 * 16 * ES + (l - 1) * 64 * 64); };
 	auto wr = [&](int l) { return Wr + (l == 0 ? 0 : 64 * 32 + (l - 1) * 64 * 64); };
 
@@ -266,7 +278,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		dl_n = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
 	};
 	load_inputs(blockIdx.x * 4 + pair);
-	__syncthreads();  // backward weights in LDS
+	__syncthreads();  // backward weights in LDS; the staged parameters are no longer read (images overwrite them)
 
 	for (uint32_t base = blockIdx.x * 4; base < n_tiles; base += gridDim.x * 4) {
 		const uint32_t tile = base + pair;
@@ -318,11 +330,12 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			}
 			pack64(acc, hr[l]);
 		}
-		if (a.out && valid) {
+		if (a.out) {
 			const f32x4 racc = mma32(wro[1], hr[RH - 1][1], mma32(wro[0], hr[RH - 1][0], f32x4{0.f, 0.f, 0.f, 0.f}));
 			f16x4 ro = pack4(racc, false);
 			if (g == 0) ro[3] = dout[0];  // extract_density (nerf_network.h:32-43)
-			if (a.out_layout == 2) {
+			if (!valid) {
+			} else if (a.out_layout == 2) {
 				if (g == 0) *(f16x4*)(a.out + (size_t)sample * a.out_stride) = ro;
 			} else if (a.out_layout == 0) {
 				*(f16x4*)(a.out + (size_t)sample * a.out_stride + 4 * g) = ro;
@@ -364,10 +377,12 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		                     mma32(*(const f16x8*)(wl + T::B_R0 + (0 * 64 + lane) * 8), dz[0], f32x4{0.f, 0.f, 0.f, 0.f}));
 		f16x4 dd = pack4(dd_acc, false);
 		if (g == 0) dd[0] = (f16)((float)dd[0] + dsig);  // add_density_gradient (:63-74)
-		if (a.dL_dsh && valid) {
+		// MFMAs take operands from every lane whatever EXEC says: only wave-uniform branches around them, the
+		// per-lane `valid` guards only the stores
+		if (a.dL_dsh) {
 			const f32x4 sacc = mma32(*(const f16x8*)(wl + T::B_R0 + (3 * 64 + lane) * 8), dz[1],
 			                         mma32(*(const f16x8*)(wl + T::B_R0 + (2 * 64 + lane) * 8), dz[0], f32x4{0.f, 0.f, 0.f, 0.f}));
-			*(f16x4*)(a.dL_dsh + (size_t)sample * 16 + 4 * g) = pack4(sacc, false);
+			if (valid) *(f16x4*)(a.dL_dsh + (size_t)sample * 16 + 4 * g) = pack4(sacc, false);
 		}
 		img_put4(img + T::I_ZDO + r * T::S_16, 0, g, dd);
 #pragma unroll
@@ -386,12 +401,12 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			mask64(acc, hd[l - 1], dz);
 		}
 		img_put64(img + T::I_ZD0 + r * T::S_64, g, dz);
-		if (a.dL_denc && valid) {
+		if (a.dL_denc) {
 #pragma unroll
 			for (int t = 0; t < ES; ++t) {
 				const f32x4 e = mma32(*(const f16x8*)(wl + T::B_D0 + ((2 * t + 1) * 64 + lane) * 8), dz[1],
 				                      mma32(*(const f16x8*)(wl + T::B_D0 + ((2 * t) * 64 + lane) * 8), dz[0], f32x4{0.f, 0.f, 0.f, 0.f}));
-				*(f16x4*)(a.dL_denc + (size_t)sample * a.denc_stride + 16 * t + 4 * g) = pack4(e, false);
+				if (valid) *(f16x4*)(a.dL_denc + (size_t)sample * a.denc_stride + 16 * t + 4 * g) = pack4(e, false);
 			}
 		}
 		__syncthreads();
@@ -467,6 +482,7 @@ static bool launch_train16(const NerfMlpArgs& a, hipStream_t s) {
 	if constexpr (T::LDS_BYTES > 160 * 1024) {
 		return false;
 	} else {
+		if (a.n_matrix > 4 * (uint32_t)T::IMG_HALVES) return false;  // the parameter staging must fit the image region
 		const uint32_t blocks = nerf_mlp_train_blocks(a.n);
 		if (blocks == 0) return true;
 		auto k = k_nerf_mlp_train16<ES, DH, RH>;

@@ -322,6 +322,14 @@ def test_large_batch_properties(pkg, nerf_setup):
     nm = net.n_matrix_params
     assert torch.allclose(g2[:nm], 2 * g1[:nm], rtol=2e-3, atol=1e-3)
     ref_out = net.inference(c, use_inference_params=False)
+    # the inference kernel (32x32x16 MFMAs) and the two-wave training kernel (16x16x32) sum each layer's fp32
+    # products in different groupings: outputs agree to the fp16 rounding of the intermediates, and the
+    # k_nerf_mlp_train kernel (the inference kernel's layout) reproduces the inference output bit for bit
+    assert torch.allclose(out.float(), ref_out.float(), rtol=1e-2, atol=2e-3)
+    net.set_option("mlp_train16", 0)
+    net.forward_backward(c, dL, output=out)
+    net.set_option("mlp_train16", 1)
+    torch.cuda.synchronize()
     assert torch.equal(ref_out, out)
 
 
@@ -431,8 +439,10 @@ def test_training_graph_matches_eager(pkg):
 def test_fused_encoding_training_matches_unfused(pkg, nerf_setup, n):
     """forward_backward with the encoding inside the MLP training kernel (option fuse_train, off by default)
     gives the same output and MLP gradients bit for bit as encode-then-MLP, and the same grid gradients
-    (bitwise on the sorted backward, n >= 4096; within fp16 atomic-order noise on the direct one)."""
+    (bitwise on the sorted backward, n >= 4096; within fp16 atomic-order noise on the direct one). The fused
+    path is k_nerf_mlp_train's, so the unfused run uses that kernel too (option mlp_train16 = 0)."""
     net, tr, p16, m = nerf_setup
+    net.set_option("mlp_train16", 0)
     c = torch.from_numpy(coords_batch(n, seed=11 + n)).cuda()
     dL = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
     dL[:, :4] = torch.rand((n, 4), device="cuda").half() - 0.5
@@ -444,6 +454,7 @@ def test_fused_encoding_training_matches_unfused(pkg, nerf_setup, n):
         torch.cuda.synchronize()
         res[fuse] = (out.clone(), tr.gradients.clone())
     net.set_option("fuse_train", 0)
+    net.set_option("mlp_train16", 1)
     nm = net.n_matrix_params
     assert torch.equal(res[1][0], res[0][0])
     assert torch.equal(res[1][1][:nm], res[0][1][:nm])

@@ -1,6 +1,6 @@
 # Idle time of the NeRF step's queues at steady state: rocprofv3 kernel trace of the Lego stand-in and fox
 # steps (engine profiler off), then per step: wall, the main queue's busy time and its idle gaps.
-# bash tools/r03_gaps.sh TAG
+# bash tools/gaps.sh TAG
 set -e -o pipefail
 T=${1:-r03bk}
 mkdir -p gpurun_out/$T
