@@ -74,25 +74,30 @@ __device__ __forceinline__ void mask64(const f32x4 (&acc)[4], const f16x8 (&act)
 
 // k of element j in K=32 step s of lane group g: permuted (a packed 64-row activation) or standard
 __device__ __forceinline__ uint32_t kperm(uint32_t s, uint32_t j, uint32_t g) { return 32 * s + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4)); }
-// One weight fragment read straight from the fp16 parameters (row-major W[out x in] at w):
-// transposed = false: A = W (m = output unit, k = input unit); true: A = W^T (m = input unit, k = output unit)
-__device__ __forceinline__ f16 wval(const f16* w, uint32_t out_dim, uint32_t in_dim, bool tr, uint32_t m, uint32_t k) {
+// A layer's weights W[out x in] staged in LDS with a padded row stride (in + 2 halves: the 16 rows a
+// fragment reads at one column fall into 16 different banks)
+struct LW {
+	const f16* w;
+	uint32_t out, in, stride;
+};
+// One weight fragment element: transposed = false: A = W (m = output unit, k = input unit); true: A = W^T
+// (m = input unit, k = output unit)
+__device__ __forceinline__ f16 wval(const LW& L, bool tr, uint32_t m, uint32_t k) {
 	const uint32_t o = tr ? k : m, i = tr ? m : k;
-	return o < out_dim && i < in_dim ? w[o * in_dim + i] : (f16)0.f;
+	return o < L.out && i < L.in ? L.w[o * L.stride + i] : (f16)0.f;
 }
-__device__ __forceinline__ f16x8 wfrag32(const f16* w, uint32_t out_dim, uint32_t in_dim, bool tr, uint32_t t, uint32_t s, bool perm,
-                                         uint32_t lane) {
+__device__ __forceinline__ f16x8 wfrag32(const LW& L, bool tr, uint32_t t, uint32_t s, bool perm, uint32_t lane) {
 	const uint32_t m = 16 * t + (lane & 15), g = lane >> 4;
 	f16x8 v;
 #pragma unroll
-	for (uint32_t j = 0; j < 8; ++j) v[j] = wval(w, out_dim, in_dim, tr, m, perm ? kperm(s, j, g) : 32 * s + 8 * g + j);
+	for (uint32_t j = 0; j < 8; ++j) v[j] = wval(L, tr, m, perm ? kperm(s, j, g) : 32 * s + 8 * g + j);
 	return v;
 }
-__device__ __forceinline__ f16x4 wfrag16(const f16* w, uint32_t out_dim, uint32_t in_dim, bool tr, uint32_t t, uint32_t lane) {
+__device__ __forceinline__ f16x4 wfrag16(const LW& L, bool tr, uint32_t t, uint32_t lane) {
 	const uint32_t m = 16 * t + (lane & 15), g = lane >> 4;
 	f16x4 v;
 #pragma unroll
-	for (uint32_t j = 0; j < 4; ++j) v[j] = wval(w, out_dim, in_dim, tr, m, 4 * g + j);
+	for (uint32_t j = 0; j < 4; ++j) v[j] = wval(L, tr, m, 4 * g + j);
 	return v;
 }
 
@@ -171,6 +176,16 @@ struct Train16Layout {
 	static constexpr int B_D0 = B_DH + (DH - 1) * 8 * 64 * 8;    // W_d0^T: ES tiles x 2 steps   (f16x8)
 	static constexpr int W_HALVES = B_D0 + ES * 2 * 64 * 8;
 	static constexpr size_t LDS_BYTES = (4 * (size_t)IMG_HALVES + W_HALVES) * sizeof(f16);
+	// staged parameters (kernel start, in the image region): each layer [out x (in + 2)]
+	__host__ __device__ static constexpr uint32_t stage_d(int l) {
+		return l == 0 ? 0u : 64u * (16 * ES + 2) + (uint32_t)(l - 1) * 64u * 66u;
+	}
+	static constexpr uint32_t STAGE_D = 64u * (16 * ES + 2) + (DH - 1) * 64u * 66u + 16u * 66u;
+	__host__ __device__ static constexpr uint32_t stage_r(int l) {
+		return STAGE_D + (l == 0 ? 0u : 64u * 34u + (uint32_t)(l - 1) * 64u * 66u);
+	}
+	static constexpr uint32_t STAGE_HALVES = STAGE_D + 64u * 34u + (RH - 1) * 64u * 66u + 16u * 66u;
+	static_assert(STAGE_HALVES <= 4 * IMG_HALVES, "parameter staging must fit the image region");
 };
 
 template <int ES, int DH, int RH>
@@ -183,74 +198,80 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 	const int pair = wave >> 1, half = wave & 1;
 	f16* img = imgs + pair * T::IMG_HALVES;
-	// the MLP parameters ([density | rgb], n_matrix halves) staged in the image region with 16-B loads; the
-	// fragments are gathered from there (gathering them from global costs ~150 scattered 2-B loads per lane)
+	// the MLP parameters staged in the image region, layer by layer with padded rows (T::stage_*); the
+	// fragments are gathered from there (from global they cost ~150 scattered 2-B loads per lane, and from an
+	// unpadded copy 16-way bank conflicts)
 	f16* stage = imgs;
+	auto wd = [&](int l) {  // density MLP: [64 x 16ES], (DH-1) x [64 x 64], [16 x 64]
+		return LW{stage + T::stage_d(l), l == DH ? 16u : 64u, l == 0 ? 16u * ES : 64u, (l == 0 ? 16u * ES : 64u) + 2u};
+	};
+	auto wr = [&](int l) {  // rgb MLP: [64 x 32], (RH-1) x [64 x 64], [16 x 64]
+		return LW{stage + T::stage_r(l), l == RH ? 16u : 64u, l == 0 ? 32u : 64u, (l == 0 ? 32u : 64u) + 2u};
+	};
 	{
-		const uint32_t nm = a.n_matrix;
-		const f16* src = a.params;
-		if (nm % 8 == 0 && ((uintptr_t)src & 15) == 0) {
-			for (uint32_t i = 8 * threadIdx.x; i < nm; i += 8 * blockDim.x) *(f16x8*)(stage + i) = *(const f16x8*)(src + i);
-		} else {
-			for (uint32_t i = threadIdx.x; i < nm; i += blockDim.x) stage[i] = src[i];
-		}
+		auto copy = [&](const LW& L, const f16* src) {
+			for (uint32_t i = threadIdx.x; i < L.out * L.in; i += blockDim.x)
+				((f16*)L.w)[(i / L.in) * L.stride + i % L.in] = src[i];
+		};
+		const f16* pd = a.params + a.density_woff;
+		const f16* pr = a.params + a.rgb_woff;
+#pragma unroll
+		for (int l = 0; l <= DH; ++l) copy(wd(l), pd + (l == 0 ? 0 : 64 * 16 * ES + (l - 1) * 64 * 64));
+#pragma unroll
+		for (int l = 0; l <= RH; ++l) copy(wr(l), pr + (l == 0 ? 0 : 64 * 32 + (l - 1) * 64 * 64));
 	}
 	__syncthreads();
-	const f16* Wd = stage + a.density_woff;  // density MLP: [64 x 16ES], (DH-1) x [64 x 64], [16 x 64]
-	const f16* Wr = stage + a.rgb_woff;      // rgb MLP:     [64 x 32], (RH-1) x [64 x 64], [16 x 64]
-	auto wd = [&](int l) { return Wd + (l == 0 ? 0 : 64 * 16 * ES + (l - 1) * 64 * 64); };
-	auto wr = [&](int l) { return Wr + (l == 0 ? 0 : 64 * 32 + (l - 1) * 64 * 64); };
 
 	// backward (transposed) weights -> LDS, one copy per block
 	for (int t = threadIdx.x; t < 4 * 64; t += blockDim.x) {  // K=16 fragments: W_ro^T and W_do^T, 4 tiles each
 		const int tile = t >> 6, l = t & 63;
-		*(f16x4*)(wl + T::B_RO + t * 4) = wfrag16(wr(RH), 16, 64, true, tile, l);
-		*(f16x4*)(wl + T::B_DO + t * 4) = wfrag16(wd(DH), 16, 64, true, tile, l);
+		*(f16x4*)(wl + T::B_RO + t * 4) = wfrag16(wr(RH), true, tile, l);
+		*(f16x4*)(wl + T::B_DO + t * 4) = wfrag16(wd(DH), true, tile, l);
 	}
 	for (int t = threadIdx.x; t < (RH - 1) * 8 * 64; t += blockDim.x) {
 		const int j = t / 512, f = (t >> 6) & 7, l = t & 63;  // j-th = layer RH-1-j; f = tile * 2 + step
-		*(f16x8*)(wl + T::B_RH + t * 8) = wfrag32(wr(RH - 1 - j), 64, 64, true, f >> 1, f & 1, true, l);
+		*(f16x8*)(wl + T::B_RH + t * 8) = wfrag32(wr(RH - 1 - j), true, f >> 1, f & 1, true, l);
 	}
 	for (int t = threadIdx.x; t < 4 * 64; t += blockDim.x) {
 		const int f = t >> 6, l = t & 63;
-		*(f16x8*)(wl + T::B_R0 + t * 8) = wfrag32(wr(0), 64, 32, true, f >> 1, f & 1, true, l);
+		*(f16x8*)(wl + T::B_R0 + t * 8) = wfrag32(wr(0), true, f >> 1, f & 1, true, l);
 	}
 	for (int t = threadIdx.x; t < (DH - 1) * 8 * 64; t += blockDim.x) {
 		const int j = t / 512, f = (t >> 6) & 7, l = t & 63;
-		*(f16x8*)(wl + T::B_DH + t * 8) = wfrag32(wd(DH - 1 - j), 64, 64, true, f >> 1, f & 1, true, l);
+		*(f16x8*)(wl + T::B_DH + t * 8) = wfrag32(wd(DH - 1 - j), true, f >> 1, f & 1, true, l);
 	}
 	for (int t = threadIdx.x; t < ES * 2 * 64; t += blockDim.x) {
 		const int f = t >> 6, l = t & 63;
-		*(f16x8*)(wl + T::B_D0 + t * 8) = wfrag32(wd(0), 64, 16 * ES, true, f >> 1, f & 1, true, l);
+		*(f16x8*)(wl + T::B_D0 + t * 8) = wfrag32(wd(0), true, f >> 1, f & 1, true, l);
 	}
 	// forward weights in registers
 	f16x4 wd0_16[ES == 1 ? 4 : 1];
 	f16x8 wd0_32[ES == 2 ? 4 : 1];
 	if constexpr (ES == 1) {
 #pragma unroll
-		for (int t = 0; t < 4; ++t) wd0_16[t] = wfrag16(wd(0), 64, 16, false, t, lane);
+		for (int t = 0; t < 4; ++t) wd0_16[t] = wfrag16(wd(0), false, t, lane);
 	} else {
 #pragma unroll
-		for (int t = 0; t < 4; ++t) wd0_32[t] = wfrag32(wd(0), 64, 32, false, t, 0, false, lane);
+		for (int t = 0; t < 4; ++t) wd0_32[t] = wfrag32(wd(0), false, t, 0, false, lane);
 	}
 	f16x8 wdh[DH > 1 ? DH - 1 : 1][8];
 #pragma unroll
 	for (int l = 1; l < DH; ++l)
 #pragma unroll
-		for (int f = 0; f < 8; ++f) wdh[l - 1][f] = wfrag32(wd(l), 64, 64, false, f >> 1, f & 1, true, lane);
+		for (int f = 0; f < 8; ++f) wdh[l - 1][f] = wfrag32(wd(l), false, f >> 1, f & 1, true, lane);
 	f16x8 wdo[2], wr0[4], wro[2];
 	f16x8 wrh[RH > 1 ? RH - 1 : 1][8];
 #pragma unroll
-	for (int s = 0; s < 2; ++s) wdo[s] = wfrag32(wd(DH), 16, 64, false, 0, s, true, lane);
+	for (int s = 0; s < 2; ++s) wdo[s] = wfrag32(wd(DH), false, 0, s, true, lane);
 	// rgb layer 0: k = [density output rows 0..15 (the dout tile's own order) | SH 0..15]
 #pragma unroll
-	for (int t = 0; t < 4; ++t) wr0[t] = wfrag32(wr(0), 64, 32, false, t, 0, true, lane);
+	for (int t = 0; t < 4; ++t) wr0[t] = wfrag32(wr(0), false, t, 0, true, lane);
 #pragma unroll
 	for (int l = 1; l < RH; ++l)
 #pragma unroll
-		for (int f = 0; f < 8; ++f) wrh[l - 1][f] = wfrag32(wr(l), 64, 64, false, f >> 1, f & 1, true, lane);
+		for (int f = 0; f < 8; ++f) wrh[l - 1][f] = wfrag32(wr(l), false, f >> 1, f & 1, true, lane);
 #pragma unroll
-	for (int s = 0; s < 2; ++s) wro[s] = wfrag32(wr(RH), 16, 64, false, 0, s, true, lane);
+	for (int s = 0; s < 2; ++s) wro[s] = wfrag32(wr(RH), false, 0, s, true, lane);
 
 	// this wave's dW tiles (16x16 fp32): waves 0-3 the rgb hidden layers (m = wave, n 0..3 per layer),
 	// waves 4-7 (v = wave - 4) the output layers' column v, rgb layer 0 row v, density layer 0 row v
@@ -352,6 +373,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		for (int l = 0; l < RH; ++l) img_put64(img + T::I_HR + l * 32 * T::S_64 + r * T::S_64, g, hr[l]);
 
 		// ---- backward dX chain, every dZ kept in the pair image ------------------------------------
+#ifndef NGP_T16_SKIP_BWD  // timing experiments only (phase costs)
 		const float dsig = (float)dl_cur[3];
 		const f16x4 dz1 = g == 0 ? f16x4{dl_cur[0], dl_cur[1], dl_cur[2], (f16)0.f} : f16x4{};  // extract_rgb (:46-60)
 		img_put4(img + T::I_ZRO + r * T::S_16, 0, g, dz1);
@@ -409,9 +431,11 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 				if (valid) *(f16x4*)(a.dL_denc + (size_t)sample * a.denc_stride + 16 * t + 4 * g) = pack4(e, false);
 			}
 		}
+#endif
 		__syncthreads();
 
 		// ---- dW over the four pair images (K = 32 samples per MFMA), images in a fixed order ---------
+#ifndef NGP_T16_SKIP_B
 #pragma unroll
 		for (int p = 0; p < 4; ++p) {
 			const f16* im = imgs + p * T::IMG_HALVES;
@@ -445,6 +469,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 				for (int n = 0; n < ES; ++n) dw[4 + n] = mma32(d0, img_frag(im + T::I_XE, T::S_XE, 16 * n, lane), dw[4 + n]);
 			}
 		}
+#endif
 		__syncthreads();
 	}
 
@@ -482,7 +507,6 @@ static bool launch_train16(const NerfMlpArgs& a, hipStream_t s) {
 	if constexpr (T::LDS_BYTES > 160 * 1024) {
 		return false;
 	} else {
-		if (a.n_matrix > 4 * (uint32_t)T::IMG_HALVES) return false;  // the parameter staging must fit the image region
 		const uint32_t blocks = nerf_mlp_train_blocks(a.n);
 		if (blocks == 0) return true;
 		auto k = k_nerf_mlp_train16<ES, DH, RH>;
