@@ -273,43 +273,55 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
 	for (int s = 0; s < 2; ++s) wro[s] = wfrag32(wr(RH), false, 0, s, true, lane);
 
-	// this wave's dW tiles (16x16 fp32): waves 0-3 the rgb hidden layers (m = wave, n 0..3 per layer),
-	// waves 4-7 (v = wave - 4) the output layers' column v, rgb layer 0 row v, density layer 0 row v
+	// this wave's dW tiles (16x16 fp32): waves 0-3 row block m = wave of the hidden layers (n 0..3 per layer)
+	// and of density layer 0 (n 0..ES-1); waves 4-7 (v = wave - 4) the output layers' column v and rgb layer
+	// 0's row block v (n 0, 1): 4 + ES and 4 tiles at C2, 7 operand fragments per image either way
 	constexpr int NH = (RH - 1) + (DH - 1);      // 64x64 hidden layers
-	constexpr int NT_A = 4 * NH > 0 ? 4 * NH : 1; // tiles of waves 0-3
-	constexpr int NT_B = 1 + 2 + 1 + ES;          // tiles of waves 4-7
+	constexpr int NT_A = 4 * NH + ES;            // tiles of waves 0-3
+	constexpr int NT_B = 4;                      // tiles of waves 4-7
 	constexpr int NT = NT_A > NT_B ? NT_A : NT_B;
 	f32x4 dw[NT];
 #pragma unroll
 	for (int q = 0; q < NT; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 	const uint32_t n_tiles = (a.n + 31) / 32;
-	// inputs of this lane's sample, prefetched one iteration ahead
-	f16x4 xe16_n;
-	f16x8 xe32_n;
-	float cd_n[3];
-	f16x4 dl_n;
-	auto load_inputs = [&](uint32_t tile) {
-		const uint32_t smp = tile * 32 + 16 * half + sn;
-		const uint32_t ls = smp < a.n ? smp : 0;
-		if constexpr (ES == 1) xe16_n = *(const f16x4*)(a.enc + (size_t)ls * a.enc_stride + 4 * g);
-		else xe32_n = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 8 * g);
-		const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
-		cd_n[0] = cd[0]; cd_n[1] = cd[1]; cd_n[2] = cd[2];
-		dl_n = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
+	// inputs of this lane's sample, prefetched PF iterations ahead: at one iteration the loop waited on their
+	// HBM latency (phase costs in DESIGN §6)
+#ifndef NGP_T16_PF
+#define NGP_T16_PF 2
+#endif
+	constexpr int PF = NGP_T16_PF;
+	struct In {
+		f16x4 xe16;
+		f16x8 xe32;
+		float cd[3];
+		f16x4 dl;
 	};
-	load_inputs(blockIdx.x * 4 + pair);
+	In pf[PF];
+	auto load_inputs = [&](In& d, uint32_t tile) {
+		const uint32_t smp = tile * 32 + 16 * half + sn;
+		const uint32_t ls = smp < a.n ? smp : 0;  // past-the-end tiles read sample 0 (unconditional loads)
+		if constexpr (ES == 1) d.xe16 = *(const f16x4*)(a.enc + (size_t)ls * a.enc_stride + 4 * g);
+		else d.xe32 = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 8 * g);
+		const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
+		d.cd[0] = cd[0]; d.cd[1] = cd[1]; d.cd[2] = cd[2];
+		d.dl = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
+	};
+#pragma unroll
+	for (int k = 0; k < PF; ++k) load_inputs(pf[k], blockIdx.x * 4 + pair + k * gridDim.x * 4);
 	__syncthreads();  // backward weights in LDS; the staged parameters are no longer read (images overwrite them)
 
 	for (uint32_t base = blockIdx.x * 4; base < n_tiles; base += gridDim.x * 4) {
 		const uint32_t tile = base + pair;
 		const uint32_t sample = tile * 32 + 16 * half + sn;
 		const bool valid = sample < a.n;
-		const f16x4 xe16 = valid ? xe16_n : f16x4{};
-		const f16x8 xe32 = valid ? xe32_n : f16x8{};
-		const float cdx = cd_n[0], cdy = cd_n[1], cdz = cd_n[2];
-		const f16x4 dl_cur = valid ? dl_n : f16x4{};
-		load_inputs(tile + gridDim.x * 4);  // unconditional (past-the-end tiles read sample 0)
+		const f16x4 xe16 = valid ? pf[0].xe16 : f16x4{};
+		const f16x8 xe32 = valid ? pf[0].xe32 : f16x8{};
+		const float cdx = pf[0].cd[0], cdy = pf[0].cd[1], cdz = pf[0].cd[2];
+		const f16x4 dl_cur = valid ? pf[0].dl : f16x4{};
+#pragma unroll
+		for (int k = 0; k + 1 < PF; ++k) pf[k] = pf[k + 1];
+		load_inputs(pf[PF - 1], tile + PF * gridDim.x * 4);
 		const int r = 16 * half + sn;       // this lane's row in the pair images
 
 		// ---- forward -----------------------------------------------------------------------------
@@ -455,6 +467,9 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 					for (int n = 0; n < 4; ++n, ++q)
 						dw[q] = mma32(am, img_frag(im + T::I_HD + (DH - 2 - j) * 32 * T::S_64, T::S_64, 16 * n, lane), dw[q]);
 				}
+				const f16x8 d0 = img_frag(im + T::I_ZD0, T::S_64, 16 * wave, lane);
+#pragma unroll
+				for (int n = 0; n < ES; ++n, ++q) dw[q] = mma32(d0, img_frag(im + T::I_XE, T::S_XE, 16 * n, lane), dw[q]);
 			} else {
 				const int v = wave - 4;
 				dw[0] = mma32(img_frag(im + T::I_ZRO, T::S_16, 0, lane),
@@ -464,9 +479,6 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 				dw[2] = mma32(a0, img_frag(im + T::I_RIN, T::S_RIN, 16, lane), dw[2]);
 				dw[3] = mma32(img_frag(im + T::I_ZDO, T::S_16, 0, lane),
 				              img_frag(im + T::I_HD + (DH - 1) * 32 * T::S_64, T::S_64, 16 * v, lane), dw[3]);
-				const f16x8 d0 = img_frag(im + T::I_ZD0, T::S_64, 16 * v, lane);
-#pragma unroll
-				for (int n = 0; n < ES; ++n) dw[4 + n] = mma32(d0, img_frag(im + T::I_XE, T::S_XE, 16 * n, lane), dw[4 + n]);
 			}
 		}
 #endif
@@ -490,14 +502,14 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		for (int j = 0; j < DH - 1; ++j)
 #pragma unroll
 			for (int n = 0; n < 4; ++n, ++q) put(dw[q], dw0 + 64 * 16 * ES + 64 * 64 * (DH - 2 - j), 64, wave, n);
+#pragma unroll
+		for (int n = 0; n < ES; ++n, ++q) put(dw[q], dw0, 16 * ES, wave, n);
 	} else {
 		const int v = wave - 4;
 		put(dw[0], rw0 + 64 * 32 + 64 * 64 * (RH - 1), 64, 0, v);
 		put(dw[1], rw0, 32, v, 0);
 		put(dw[2], rw0, 32, v, 1);
 		put(dw[3], dw0 + 64 * 16 * ES + 64 * 64 * (DH - 1), 64, 0, v);
-#pragma unroll
-		for (int n = 0; n < ES; ++n) put(dw[4 + n], dw0, 16 * ES, v, n);
 	}
 }
 
