@@ -97,9 +97,13 @@ int ngp_model_initialize_params(const ngp_model* m, uint64_t seed, float* params
 /* GridEncoding::set_max_level / set_max_level_gpu (src/testbed.cu:3856-3864; testbed_nerf.cu:3996,4004) */
 int ngp_model_set_max_level(ngp_model* m, float max_level, const float* max_level_per_sample);
 /* engine knobs: "grid_backward_mode" = 0 auto, 1 direct packed-f16 atomics (tcnn-style),
- * 3 destination-bucketed exact sums (auto picks 3 for n >= 4096); "fuse_infer", "fuse_train",
+ * 3 destination-bucketed exact sums (auto picks 3 for n >= 4096); "grid_bricks" (bucketed backward: dense
+ * levels summed per brick where that moves fewer bytes, default 1); "fuse_infer", "fuse_train",
  * "fused_hist", "overlap", "grid_forward_mode"  */
 int ngp_model_set_option(ngp_model* m, const char* key, double value);
+/* engine state for tests and tools: "grid_brick_levels" = dense levels the bucketed backward sums per brick
+ * in its plan for the last batch size (0: all levels through items) */
+int ngp_model_query(const ngp_model* m, const char* key, double* value);
 /* pre-size internal workspaces for batches up to n (lets callers capture steps into HIP graphs) */
 int ngp_model_reserve(ngp_model* m, uint32_t n);
 /* Inspection of the last training pass's intermediates (the role of tcnn's forward_activations(ctx),

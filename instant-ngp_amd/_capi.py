@@ -92,6 +92,7 @@ SIGNATURES = {
     "ngp_model_initialize_params": (i32, [P, u64, P, f32]),
     "ngp_model_set_max_level": (i32, [P, f32, P]),
     "ngp_model_set_option": (i32, [P, C.c_char_p, C.c_double]),
+    "ngp_model_query": (i32, [P, C.c_char_p, C.POINTER(C.c_double)]),
     "ngp_model_reserve": (i32, [P, u32]),
     "ngp_model_workspace": (i32, [P, C.c_char_p, C.POINTER(P), C.POINTER(u64)]),
     "ngp_model_workspace_epoch": (u64, [P]),

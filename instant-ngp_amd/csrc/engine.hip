@@ -45,6 +45,7 @@ struct DevBuf {
 			if (p) NGP_HIP(hipFree(p));
 			p = nullptr;
 			NGP_HIP(hipMalloc(&p, need));
+			NGP_HIP(hipMemset(p, 0, need));  // workspaces that must start zeroed (the grid backward's brick fallback table)
 			bytes = need;
 			if (epoch) ++*epoch;
 		}
@@ -168,6 +169,7 @@ struct ngp_model {
 	bool fuse_slabs = true;                 // option "fuse_slabs": dW slab reduction inside the grid backward's last kernel
 	bool fuse_opt = true;                   // option "fuse_opt": lazy-layout optimizer update inside the grid backward (training_step)
 	bool mlp_train16 = true;                // option "mlp_train16": the training MLP at two waves per SIMD (mlp_train16.hip)
+	bool grid_bricks = true;                // option "grid_bricks": dense levels of the bucketed backward summed per brick
 	bool fuse_train = false;                // option "fuse_train": ... and the training forward_backward too (off: the
 	                                        // training kernel runs 1 wave/SIMD, the gathers are not hidden; C2 0.157 -> 0.161 ms)
 	int grid_forward_mode = 0;              // option "grid_forward_mode": 0 auto, 1 per-sample rows, 2 XCD-partitioned
@@ -221,7 +223,7 @@ struct ngp_model {
 	bool use_sorted(uint32_t n) const { return grid_backward_mode == 3 || (grid_backward_mode == 0 && n >= 4096); }
 	bool side_prepare(uint32_t n) const { return use_sorted(n) && (overlap & 1); }
 	const ScatterPlan& sc_plan_for(uint32_t n) {
-		if (sc_plan_n != n) { sc_plan = make_scatter_plan(grid, n); sc_plan_n = n; }
+		if (sc_plan_n != n) { sc_plan = make_scatter_plan(grid, n, grid_bricks); sc_plan_n = n; }
 		return sc_plan;
 	}
 	void* sorted_workspace(uint32_t n) { return scatter_ws.get(sc_plan_for(n).total); }
@@ -744,11 +746,23 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			m->fuse_slabs = value != 0;
 		} else if (k == "fuse_opt") {
 			m->fuse_opt = value != 0;
+		} else if (k == "grid_bricks") {
+			m->grid_bricks = value != 0;
+			m->sc_plan_n = 0;  // re-plan at the next batch
 		} else if (k == "win_debug") {
 			m->win_debug = (uint32_t)value;
 		} else {
 			throw Error("unknown model option: " + k);
 		}
+	});
+}
+
+int ngp_model_query(const ngp_model* m, const char* key, double* value) {
+	NGP_ARG(m && key && value);
+	NGP_TRY({
+		const std::string k = key;
+		if (k == "grid_brick_levels") *value = m->sc_plan_n ? (double)m->sc_plan.bk.LD : 0.0;
+		else throw Error("unknown model query: " + k);
 	});
 }
 

@@ -52,10 +52,13 @@ struct GridBwdArgs {
 // Optional by-product of the training forward: the bucket histogram of the sorted backward
 // (grid_scatter.hip k_sc_hist), counted from the corner indices the forward computes anyway.
 // hist[chunk * vb_base[L] + vb_base[l] + bucket]; one forward block = one chunk of `chunk` samples.
+// With bricks (grid_scatter.h ScatterPlan::LD > 0) the leading LD dense levels are not counted per corner:
+// each sample counts once in its brick's bucket (vbs [0, n_bricks), brick_of).
 struct GridHist {
 	uint32_t* hist;
 	uint32_t B, n_chunks, chunk;
 	uint32_t vb_base[33];
+	uint32_t brick_levels = 0, n_bricks = 0, brick_cells = 8, bricks_per_dim = 0;
 };
 
 // mode: 0/1 per-sample kernels, 2 XCD-partitioned (level, chunk) kernel (L2-local tables; measured
@@ -255,6 +258,22 @@ __device__ __forceinline__ void level_setup(const GridConst& c, uint32_t l, cons
 		base[d] = (uint32_t)(int)t;
 		frac[d] = p - t;
 	}
+}
+
+// The brick of a 3D sample for the brick-summed dense levels 0..LD-1 (grid_scatter.hip): its cell at the
+// finest of them, f = LD - 1 (level_setup's arithmetic), divided by the brick edge in cells, clamped to the
+// brick grid (positions outside [0, 1] land in an edge brick; their corners outside its region take the
+// exact global fallback).
+__device__ __forceinline__ uint32_t brick_of(const GridConst& c, uint32_t f, uint32_t K, uint32_t NB, const float* x) {
+	uint32_t id = 0, mul = 1;
+#pragma unroll
+	for (uint32_t d = 0; d < 3; ++d) {
+		const int cell = (int)floorf(__builtin_fmaf(c.scale[f], x[d], 0.5f));
+		const int b = cell < 0 ? 0 : min(cell / (int)K, (int)NB - 1);
+		id += (uint32_t)b * mul;
+		mul *= NB;
+	}
+	return id;
 }
 
 GridConst make_grid_const(const GridDesc& g);

@@ -142,6 +142,9 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 #pragma unroll
 	for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * a.pos_stride + d];
 	const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
+	if constexpr (HIST && D == 3) {
+		if (h.brick_levels) atomicAdd(&hl[brick_of(c, h.brick_levels - 1, h.brick_cells, h.bricks_per_dim, x)], 1u);
+	}
 	f16 row[32];
 #pragma unroll
 	for (uint32_t l = 0; l < MAXL; ++l) {
@@ -149,7 +152,8 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) acc[f] = 0.f;
 		const bool active = l < c.n_levels && !((float)l >= ml + 1e-3f);
-		if (HIST && l < c.n_levels && !active) {
+		const bool count = HIST && l >= h.brick_levels;  // brick levels: counted once per sample above
+		if (count && l < c.n_levels && !active) {
 			// the backward stages items for masked levels too (with zero values): count them
 			float frac[D]; uint32_t base[D];
 			level_setup<D>(c, l, x, frac, base);
@@ -164,13 +168,13 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 			if constexpr (NGP_FWD_FASTIDX && F >= 4) {
 				uint32_t cidx[1u << D];
 				corner_indices<D>(c, l, base, cidx);
-				if constexpr (HIST) {
+				if (count) {
 #pragma unroll
 					for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&hl[h.vb_base[l] + ((cidx[k] - c.offsets[l]) >> h.B)], 1u);
 				}
 				gather_corners_at<D, F>(cidx, a.table, v);
 			} else {
-				if constexpr (HIST) {
+				if (count) {
 #pragma unroll
 					for (uint32_t k = 0; k < (1u << D); ++k)
 						atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
@@ -297,9 +301,12 @@ __global__ void __launch_bounds__(256) k_grid_forward_xcd(const GridConst c, con
 	if (m.reps == 1) { l = slot + XCD_SLOTS * (r / m.n_chunks); chunk = r % m.n_chunks; }
 	else { l = slot % c.n_levels; chunk = r * m.reps + slot / c.n_levels; }
 	if (l >= c.n_levels || chunk >= m.n_chunks) return;
-	uint32_t nvb = 0;
+	uint32_t nvb = 0, vb0 = 0;
+	// bricks: the block of the finest brick level counts each sample's brick, coarser brick levels nothing
+	const bool brick_counter = HIST && D == 3 && l + 1 == h.brick_levels;
 	if constexpr (HIST) {
-		nvb = h.vb_base[l + 1] - h.vb_base[l];
+		nvb = l < h.brick_levels ? (brick_counter ? h.n_bricks : 0u) : h.vb_base[l + 1] - h.vb_base[l];
+		vb0 = l < h.brick_levels ? 0u : h.vb_base[l];
 		for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) hl[j] = 0;
 		__syncthreads();
 	}
@@ -318,8 +325,13 @@ __global__ void __launch_bounds__(256) k_grid_forward_xcd(const GridConst c, con
 		float frac[D]; uint32_t base[D];
 		level_setup<D>(c, l, x, frac, base);
 		if constexpr (HIST) {
+			if constexpr (D == 3) {
+				if (brick_counter) atomicAdd(&hl[brick_of(c, l, h.brick_cells, h.bricks_per_dim, x)], 1u);
+			}
+			if (l >= h.brick_levels) {
 #pragma unroll
-			for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&hl[(corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B], 1u);
+				for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&hl[(corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B], 1u);
+			}
 		}
 		if (active) {
 			V v[1u << D];
@@ -351,7 +363,7 @@ __global__ void __launch_bounds__(256) k_grid_forward_xcd(const GridConst c, con
 	}
 	if constexpr (HIST) {
 		__syncthreads();
-		for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) h.hist[(size_t)chunk * h.vb_base[c.n_levels] + h.vb_base[l] + j] = hl[j];
+		for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) h.hist[(size_t)chunk * h.vb_base[c.n_levels] + vb0 + j] = hl[j];
 	}
 }
 
@@ -367,6 +379,7 @@ static void launch_fwd_xcd(uint32_t F, const GridConst& c, const GridFwdArgs& a,
 	if (h) NGP_CHECK(h->chunk == XCD_CHUNK && h->n_chunks == m.n_chunks, "grid forward histogram: chunk mismatch");
 	uint32_t max_lb = 0;
 	if (h) for (uint32_t l = 0; l < c.n_levels; ++l) max_lb = std::max(max_lb, h->vb_base[l + 1] - h->vb_base[l]);
+	if (h) max_lb = std::max(max_lb, h->n_bricks);
 	const size_t lds = (size_t)max_lb * 4;
 	const GridHist none{};
 	auto go = [&](auto kern_nohist, auto kern_hist) {

@@ -6,6 +6,18 @@
 
 namespace ngp {
 
+// Brick-summed dense levels (3D grids): the leading LD dense levels are not sent through items. Samples are
+// counting-sorted by brick (K^3 cells of the finest of those levels, f = LD - 1; one item per sample: its
+// index), each brick part sums its samples' contributions to levels 0..LD-1 in LDS over the brick's region
+// (a box of corners per level, W[l]^3 entries at regoff[l]) and stores the exact int64 sums as a slab; the
+// finalize adds, per entry, the slabs of every brick whose region holds it. Corners outside the region
+// (positions outside [0, 1]) go to an int64 fallback table with global atomics.
+struct BrickConst {
+	uint32_t LD = 0, K = 8, NB = 0, NBK = 0, R = 0;
+	uint32_t W[4] = {}, regoff[4] = {};
+	uint16_t lo[4][32] = {};  // region's first corner coordinate per level and brick coordinate
+};
+
 struct ScatterPlan {
 	uint32_t B = 0;          // log2 entries per bucket (a bucket's accumulators fill one LDS tile)
 	uint32_t n_buckets = 0;  // buckets are level-aligned: a bucket never spans two levels
@@ -19,12 +31,17 @@ struct ScatterPlan {
 	uint32_t max_split_buckets = 0;
 	uint32_t xcd_map = 2;    // scatter block order: 2 = a chunk's level blocks and neighbouring chunks share an XCD
 	uint32_t bt = 1024;      // bucket accumulation block threads (experiment knob NGP_SC_BT)
+	BrickConst bk;           // bk.LD = 0: every level through items
+	uint32_t brick_part = 1024;  // samples per brick part (parts of one brick each store a slab)
 	// workspace layout (bytes)
 	size_t off_hist = 0, off_cur = 0, off_tot = 0, off_split = 0, off_lo = 0, off_splitb = 0, off_scratch = 0, off_idx = 0, off_val = 0,
+	       off_bp = 0,    // bricks: {first part, parts} per brick
+	       off_fb = 0,    // bricks: int64 fallback table [offsets[LD] x F] + flag; zero between steps
 	       total = 0;
 };
 
-ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n);
+// bricks: allow the brick-summed dense levels (ScatterPlan::bk; chosen only where they move fewer bytes)
+ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n, bool bricks = true);
 // Phase 1 (positions only, so it can run on a side stream while the forward pass and the MLP run):
 // bucket histogram per block of samples + per-bucket scans.
 // hist_done: the histogram was produced by the training forward (scatter_hist, grid_forward).

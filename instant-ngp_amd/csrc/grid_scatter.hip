@@ -26,9 +26,19 @@
 //     k_sc_accumulate per part of an oversized bucket (int64 partial sums to scratch), then per bucket:
 //                     zero LDS, accumulate, store every entry once (no memset, no atomics)
 //     k_sc_split_reduce  per oversized bucket: sum its parts (exact), write every entry once
+//
+// Bricks (ScatterPlan::bk, 3D grids): the leading dense levels (C2: 0-2 of 4) do not go through items. The
+// histogram counts each sample once in its brick (K^3 cells of the finest of those levels), the scatter's
+// brick slot writes the sample's index as its one item, every non-empty brick is a "split" bucket whose
+// parts (brick_part samples each) sum levels 0..LD-1 of their samples in LDS over the brick's region and
+// store the exact int64 sums (a slab, in the split scratch), and extra blocks of k_sc_split_reduce add, per
+// dense entry, the slabs of the bricks whose regions hold it. The contributions and their fixed-point sums
+// are those of the item path, so the gradient is the same to the bit. C2: 3 of 4 levels' items (63 MB
+// written and read) become 4 B per sample plus ~24 MB of slabs.
 #include "grid_scatter.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 namespace ngp {
@@ -117,14 +127,49 @@ __device__ __forceinline__ void load_pos(const GridBwdArgs& a, uint32_t i, float
 }
 
 struct Levels {
-	uint32_t vb_base[33];  // first bucket of each level; vb_base[L] = number of buckets
+	uint32_t vb_base[33];  // first bucket of each level; vb_base[L] = number of buckets (bricks first: vbs [0, NBK))
+};
+
+// sample index as a brick item: low 16 bits in the idx slot, high 16 in the first value element
+template <uint32_t F>
+__device__ __forceinline__ typename ValVec<F>::T brick_item_hi(uint32_t i) {
+	typename ValVec<F>::T v{};
+	const f16 h = __builtin_bit_cast(f16, (uint16_t)(i >> 16));
+	if constexpr (F == 1) v = h; else v[0] = h;
+	return v;
+}
+template <uint32_t F>
+__device__ __forceinline__ uint32_t brick_item(const uint16_t* item_idx, const f16* item_val, uint32_t t) {
+	return (uint32_t)item_idx[t] | ((uint32_t)__builtin_bit_cast(uint16_t, item_val[(size_t)t * F]) << 16);
+}
+// global fallback table of the brick levels: int64 [offsets[LD] * F], then the "used" flag
+struct BrickFallback {
+	unsigned long long* fix;
+	uint32_t* flag;
 };
 
 template <uint32_t D, uint32_t CHUNK>
-__global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const Levels lv, const GridBwdArgs a, uint32_t B,
-                                                        uint32_t n_chunks, uint32_t* __restrict__ hist) {
+__global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const Levels lv, const BrickConst bk, const GridBwdArgs a,
+                                                        uint32_t B, uint32_t n_chunks, uint32_t* __restrict__ hist) {
 	extern __shared__ uint32_t h[];
 	const uint32_t chunk = blockIdx.x, l = blockIdx.y;
+	if (l < bk.LD) {  // brick levels: the finest one's block counts each sample's brick
+		if constexpr (D == 3) {
+			if (l + 1 != bk.LD) return;
+			for (uint32_t j = threadIdx.x; j < bk.NBK; j += blockDim.x) h[j] = 0;
+			__syncthreads();
+			for (uint32_t q = 0; q < CHUNK / SC_THREADS; ++q) {
+				const uint32_t i = chunk * CHUNK + q * SC_THREADS + threadIdx.x;
+				if (i >= a.n) continue;
+				float x[3];
+				load_pos<3>(a, i, x);
+				atomicAdd(&h[brick_of(c, l, bk.K, bk.NB, x)], 1u);
+			}
+			__syncthreads();
+			for (uint32_t j = threadIdx.x; j < bk.NBK; j += blockDim.x) hist[(size_t)chunk * lv.vb_base[c.n_levels] + j] = h[j];
+		}
+		return;
+	}
 	const uint32_t nvb = lv.vb_base[l + 1] - lv.vb_base[l];
 	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) h[j] = 0;
 	__syncthreads();
@@ -233,7 +278,12 @@ constexpr uint32_t SC_PLAN_THREADS = 1024;
 template <uint32_t SC_PLAN_K>
 __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __restrict__ tot, uint32_t n_vb, uint32_t split_limit,
                                                              uint32_t part, uint32_t* __restrict__ lo_out,
-                                                             uint32_t* __restrict__ split, uint32_t* __restrict__ splitb) {
+                                                             uint32_t* __restrict__ split, uint32_t* __restrict__ splitb,
+                                                             uint32_t n_bricks, uint32_t brick_part, uint32_t* __restrict__ bp,
+                                                             uint32_t* __restrict__ fb_flag) {
+	// bricks (vbs [0, n_bricks)): every non-empty one is summed in parts of brick_part samples, each storing a
+	// slab; bp[2 b] = first part, bp[2 b + 1] = parts. They are not split buckets of k_sc_split_reduce.
+	if (fb_flag && threadIdx.x == 0) *fb_flag = 0u;  // the previous step's finalize has read and cleared the fallback
 	__shared__ uint32_t wsum[3][SC_PLAN_THREADS / 64];
 	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 	const uint32_t K = min(SC_PLAN_K, (n_vb + SC_PLAN_THREADS - 1) / SC_PLAN_THREADS);
@@ -246,8 +296,10 @@ __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __r
 		uint32_t s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll
 		for (uint32_t k = 0; k < SC_PLAN_K; ++k) {
-			const uint32_t sp = t[k] > split_limit ? 1u : 0u;
-			s0 += t[k]; s1 += sp ? (t[k] + part - 1) / part : 0u; s2 += sp;
+			const bool brick = v0 + k < n_bricks;
+			const uint32_t sp = (brick ? t[k] > 0 : t[k] > split_limit) ? 1u : 0u;
+			const uint32_t pk = brick ? brick_part : part;
+			s0 += t[k]; s1 += sp ? (t[k] + pk - 1) / pk : 0u; s2 += brick ? 0u : sp;
 		}
 		const uint32_t i0 = wave_inclusive_scan(s0), i1 = wave_inclusive_scan(s1), i2 = wave_inclusive_scan(s2);
 		if (lane == 63) { wsum[0][wave] = i0; wsum[1][wave] = i1; wsum[2][wave] = i2; }
@@ -264,7 +316,15 @@ __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __r
 			if (k >= K || v0 + k >= n_vb) break;
 			const uint32_t vb = v0 + k, tk = t[k];
 			lo_out[vb] = lo;
-			if (tk > split_limit) {
+			if (vb < n_bricks) {
+				const uint32_t parts = (tk + brick_part - 1) / brick_part;
+				bp[2 * vb] = first; bp[2 * vb + 1] = parts;
+				for (uint32_t q = 0; q < parts; ++q) {
+					uint32_t* d = split + 2 + 3 * (size_t)(first + q);
+					d[0] = vb; d[1] = lo + q * brick_part; d[2] = min(lo + (q + 1) * brick_part, lo + tk);
+				}
+				first += parts;
+			} else if (tk > split_limit) {
 				const uint32_t parts = (tk + part - 1) / part;
 				splitb[3 * b] = vb; splitb[3 * b + 1] = first; splitb[3 * b + 2] = parts;
 				for (uint32_t q = 0; q < parts; ++q) {
@@ -280,8 +340,58 @@ __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __r
 	if (threadIdx.x == 0) { split[0] = c_parts; split[1] = c_sb; }
 }
 
+// The brick slot of a chunk: one item per sample (its index) in its brick's bucket, ranked, staged and
+// written out like the level items.
+template <uint32_t F, uint32_t SC_CHUNK, uint32_t SC_ST>
+__device__ void scatter_bricks(const GridConst& c, const BrickConst& bk, const GridBwdArgs& a, uint32_t n_vb, uint32_t chunk,
+                               const uint32_t* __restrict__ cur_t, const uint32_t* __restrict__ lo_vb,
+                               uint16_t* __restrict__ item_idx, f16* __restrict__ item_val, uint32_t* lds, uint32_t* wsum) {
+	typedef typename ValVec<F>::T V;
+	constexpr uint32_t SC_SSPT = SC_CHUNK / SC_ST;
+	const uint32_t nvb = bk.NBK;
+	uint32_t* cur = lds;
+	uint32_t* lh = cur + nvb;
+	uint32_t* loff = lh + nvb;
+	uint16_t* st_b = (uint16_t*)(loff + nvb + 1);
+	uint32_t* st_i = (uint32_t*)(((uintptr_t)(st_b + SC_CHUNK) + 15) & ~(uintptr_t)15);
+	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) {
+		cur[j] = lo_vb[j] + cur_t[(size_t)chunk * n_vb + j];
+		lh[j] = 0;
+	}
+	__syncthreads();
+	uint32_t e[SC_SSPT], r[SC_SSPT];
+#pragma unroll
+	for (uint32_t q = 0; q < SC_SSPT; ++q) {
+		const uint32_t i = chunk * SC_CHUNK + q * SC_ST + threadIdx.x;
+		if (i >= a.n) continue;
+		float x[3];
+		load_pos<3>(a, i, x);
+		e[q] = brick_of(c, bk.LD - 1, bk.K, bk.NB, x);
+		r[q] = atomicAdd(&lh[e[q]], 1u);
+	}
+	__syncthreads();
+	block_exclusive_scan<SC_ST>(lh, loff, nvb, wsum);
+	__syncthreads();
+#pragma unroll
+	for (uint32_t q = 0; q < SC_SSPT; ++q) {
+		const uint32_t i = chunk * SC_CHUNK + q * SC_ST + threadIdx.x;
+		if (i >= a.n) continue;
+		const uint32_t slot = loff[e[q]] + r[q];
+		st_b[slot] = (uint16_t)e[q];
+		st_i[slot] = i;
+	}
+	__syncthreads();
+	const uint32_t n_it = loff[nvb];
+	for (uint32_t t = threadIdx.x; t < n_it; t += blockDim.x) {
+		const uint32_t j = st_b[t], i = st_i[t];
+		const uint32_t gpos = cur[j] + (t - loff[j]);
+		item_idx[gpos] = (uint16_t)(i & 0xffffu);
+		*(V*)(item_val + (size_t)gpos * F) = brick_item_hi<F>(i);
+	}
+}
+
 template <uint32_t D, uint32_t F, uint32_t SC_CHUNK, uint32_t SC_ST>
-__global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const Levels lv, const GridBwdArgs a, uint32_t B,
+__global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const Levels lv, const BrickConst bk, const GridBwdArgs a, uint32_t B,
                                                       uint32_t n_vb, uint32_t n_chunks, uint32_t xcd_map, const uint32_t* __restrict__ cur_t,
                                                       const uint32_t* __restrict__ lo_vb, uint16_t* __restrict__ item_idx,
                                                       f16* __restrict__ item_val, uint32_t debug) {
@@ -291,24 +401,35 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 	constexpr uint32_t SC_SSPT = SC_CHUNK / SC_ST;  // samples per thread
 	extern __shared__ uint32_t lds[];
 	__shared__ uint32_t wsum[SC_ST / 64];
+	// slots per chunk: the brick slot (slot 0 when bk.LD > 0), then one per item level
+	const uint32_t n_slots = c.n_levels - bk.LD + (bk.LD ? 1u : 0u);
 	// XCD-aware order: blocks b and b + 8 share an XCD (round-robin dispatch), so the L level blocks of a
 	// chunk run back to back on one XCD and its positions and dL/dy rows leave HBM once, not L times
 	uint32_t chunk, l;
 	if (xcd_map == 1) {
 		const uint32_t slot = blockIdx.x >> 3;
-		l = slot % c.n_levels;
-		chunk = (slot / c.n_levels) * 8 + (blockIdx.x & 7);
+		l = slot % n_slots;
+		chunk = (slot / n_slots) * 8 + (blockIdx.x & 7);
 	} else if (xcd_map == 2) {
 		// and each XCD owns a contiguous range of chunks: neighbouring runs of a bucket meet in one L2
 		const uint32_t slot = blockIdx.x >> 3, cpx = (n_chunks + 7) >> 3;
-		l = slot % c.n_levels;
-		chunk = (blockIdx.x & 7) * cpx + slot / c.n_levels;
-		if (slot / c.n_levels >= cpx) return;
+		l = slot % n_slots;
+		chunk = (blockIdx.x & 7) * cpx + slot / n_slots;
+		if (slot / n_slots >= cpx) return;
 	} else {
 		chunk = blockIdx.x % n_chunks;
 		l = blockIdx.x / n_chunks;
 	}
 	if (chunk >= n_chunks) return;
+	if (bk.LD) {
+		if constexpr (D == 3) {
+			if (l == 0) {
+				scatter_bricks<F, SC_CHUNK, SC_ST>(c, bk, a, n_vb, chunk, cur_t, lo_vb, item_idx, item_val, lds, wsum);
+				return;
+			}
+		}
+		l = l - 1 + bk.LD;
+	}
 	const uint32_t nvb = lv.vb_base[l + 1] - lv.vb_base[l];
 	uint32_t* cur = lds;                                   // [nvb] this block's global cursor per bucket
 	uint32_t* lh = cur + nvb;                              // [nvb] counts
@@ -460,6 +581,136 @@ __device__ __forceinline__ void accumulate_items(unsigned long long* acc, uint32
 
 __device__ __forceinline__ float fix_to_f32(unsigned long long q) { return (float)((double)(long long)q * (1.0 / FIX_SCALE)); }
 
+// One part of brick vb (items [lo, hi) = sample indices): the contributions of its samples to levels
+// 0..LD-1, to_f16(w * dL/dy) as the scatter forms them, summed exactly in LDS over the brick's region
+// (acc[f * (R + 1) + local]), then stored as the part's slab dst[f * NE + local]. Work item = (level,
+// sample), level-major, so a wave's lanes share the level. Lane l starts at feature l % F (as
+// accumulate_items: spreads a hot entry's same-address adds). Corners outside the region (positions
+// outside [0, 1]) are added to the global fallback table instead.
+template <uint32_t F>
+__device__ void accumulate_brick(const GridConst& c, const BrickConst& bk, const GridBwdArgs& a, uint32_t vb, uint32_t lo, uint32_t hi,
+                                 const uint16_t* __restrict__ item_idx, const f16* __restrict__ item_val, unsigned long long* acc,
+                                 unsigned long long* __restrict__ dst, uint32_t NE, const BrickFallback& fb) {
+	typedef typename ValVec<F>::T V;
+	const uint32_t RP = bk.R + 1;
+	for (uint32_t k = threadIdx.x; k < RP * F; k += blockDim.x) acc[k] = 0ull;
+	__syncthreads();
+	const uint32_t b3[3] = {vb % bk.NB, (vb / bk.NB) % bk.NB, vb / (bk.NB * bk.NB)};
+	const uint32_t ns = hi - lo, rot = threadIdx.x % F;
+	for (uint32_t w = threadIdx.x; w < ns * bk.LD; w += blockDim.x) {
+		const uint32_t l = w / ns, i = brick_item<F>(item_idx, item_val, lo + w % ns);
+		float x[3];
+		load_pos<3>(a, i, x);
+		const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
+		if ((float)l > ml + 1e-3f) continue;  // tcnn backward: masked levels contribute zeros
+		float g[F];
+		if (a.dy_layout == AoS) {
+			const V gv = *(const V*)(a.dL_dy + (size_t)i * a.dy_stride + l * F);
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) {
+				if constexpr (F == 1) g[f] = (float)gv; else g[f] = (float)gv[f];
+			}
+		} else {
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) g[f] = (float)a.dL_dy[(size_t)(l * F + f) * a.dy_stride + i];
+		}
+		float frac[3]; uint32_t base[3];
+		level_setup<3>(c, l, x, frac, base);
+		const uint32_t W = bk.W[l];
+		uint32_t r0[3];
+#pragma unroll
+		for (uint32_t d = 0; d < 3; ++d) r0[d] = base[d] - bk.lo[l][b3[d]];
+#pragma unroll
+		for (uint32_t k = 0; k < 8; ++k) {
+			const uint32_t rx = r0[0] + (k & 1u), ry = r0[1] + ((k >> 1) & 1u), rz = r0[2] + ((k >> 2) & 1u);
+			const float wk = corner_weight<3>(frac, k);
+			const bool in = rx < W && ry < W && rz < W;
+			const uint32_t local = bk.regoff[l] + rx + W * (ry + W * rz);
+#pragma unroll
+			for (uint32_t q = 0; q < F; ++q) {
+				const uint32_t f = (q + rot) & (F - 1);
+				float gf = g[0];
+#pragma unroll
+				for (uint32_t u = 1; u < F; ++u) gf = f == u ? g[u] : gf;
+				const float v = (float)to_f16(wk * gf);
+				if (v == 0.f) continue;
+				const unsigned long long fx = (unsigned long long)(long long)(v * FIX_SCALE);
+				if (__builtin_expect(in, 1)) atomicAdd(&acc[f * RP + local], fx);
+				else {
+					atomicAdd(&fb.fix[(size_t)corner_index<3>(c, l, base, k) * F + f], fx);
+					*fb.flag = 1u;
+				}
+			}
+		}
+	}
+	__syncthreads();
+	for (uint32_t k = threadIdx.x; k < bk.R * F; k += blockDim.x) dst[(k / bk.R) * NE + k % bk.R] = acc[(k / bk.R) * RP + k % bk.R];
+}
+
+// Sum of one brick-level entry's feature f: the slabs of every part of every brick whose region holds a
+// corner that indexes it, plus the fallback table (then cleared; read only when the flag is set). A dense
+// level's corner coordinates run 0..res (a cell's upper corner at coordinate res is tcnn's index
+// x + res (y + res z) unclamped, modulo T = res^3), so entry (x, y, z) is also the corner (x + res, y - 1, z)
+// when x = 0, and so on with the borrow through y and z: at most 2 candidates per coordinate.
+__device__ __forceinline__ unsigned long long brick_entry_sum(const GridConst& c, const BrickConst& bk, uint32_t e, uint32_t f, uint32_t F,
+                                                              uint32_t NE, const uint32_t* __restrict__ bp,
+                                                              const unsigned long long* __restrict__ scratch, const BrickFallback& fb,
+                                                              bool fb_used) {
+	uint32_t l = 0;
+	while (c.offsets[l + 1] <= e) ++l;
+	const int res = (int)c.resolution[l], idx = (int)(e - c.offsets[l]);
+	const int cc[3] = {idx % res, (idx / res) % res, idx / (res * res)};
+	const uint32_t W = bk.W[l];
+	unsigned long long q = 0;
+	// bricks whose region holds coordinate v along one dimension: lo <= v < lo + W, a contiguous range
+	auto range = [&](int v, uint32_t& b0, uint32_t& b1) {
+		b0 = bk.NB; b1 = 0;
+		for (uint32_t b = 0; b < bk.NB; ++b) {
+			const int lb = bk.lo[l][b];
+			if (lb <= v && v < lb + (int)W) { b0 = min(b0, b); b1 = b + 1; }
+		}
+	};
+	// corner coordinate candidates of a coordinate t - borrow: (value, borrow out)
+	auto cands = [&](int t, int* v, int* bo) {
+		int n = 0;
+		if (t >= 0) { v[n] = t; bo[n] = 0; ++n; }
+		if (t == 0) { v[n] = res; bo[n] = 1; ++n; }
+		if (t == -1) { v[n] = res - 1; bo[n] = 1; ++n; }
+		return n;
+	};
+	int va[2], ba[2];
+	const int na = cands(cc[0], va, ba);
+	for (int ia = 0; ia < na; ++ia) {
+		int vb_[2], bb[2];
+		const int nb = cands(cc[1] - ba[ia], vb_, bb);
+		for (int ib = 0; ib < nb; ++ib) {
+			int vc[2], bc[2];
+			const int nc = cands(cc[2] - bb[ib], vc, bc);  // a borrow out of z wraps modulo T = res^3
+			for (int ic = 0; ic < nc; ++ic) {
+				const int v3[3] = {va[ia], vb_[ib], vc[ic]};
+				uint32_t b0[3], b1[3];
+#pragma unroll
+				for (int d = 0; d < 3; ++d) range(v3[d], b0[d], b1[d]);
+				for (uint32_t bz = b0[2]; bz < b1[2]; ++bz)
+					for (uint32_t by = b0[1]; by < b1[1]; ++by)
+						for (uint32_t bx = b0[0]; bx < b1[0]; ++bx) {
+							const uint32_t b = bx + bk.NB * (by + bk.NB * bz);
+							const uint32_t first = bp[2 * b], parts = bp[2 * b + 1];
+							const uint32_t local = bk.regoff[l] + (uint32_t)(v3[0] - bk.lo[l][bx]) +
+							                       W * ((uint32_t)(v3[1] - bk.lo[l][by]) + W * (uint32_t)(v3[2] - bk.lo[l][bz]));
+							for (uint32_t p = 0; p < parts; ++p) q += scratch[(size_t)(first + p) * NE * F + (size_t)f * NE + local];
+						}
+			}
+		}
+	}
+	if (fb_used) {
+		unsigned long long* src = fb.fix + (size_t)e * F + f;
+		const unsigned long long v = *src;
+		if (v) { q += v; *src = 0ull; }
+	}
+	return q;
+}
+
 // bucket vb -> (first entry, entries)
 __device__ __forceinline__ void bucket_entries(const GridConst& c, const Levels& lv, uint32_t B, uint32_t vb, uint32_t& e0, uint32_t& n_e) {
 	uint32_t l = 0;
@@ -487,18 +738,23 @@ __device__ __forceinline__ void pair_slots(uint32_t k, uint32_t NE, uint32_t& a,
 // FUSED: the grid's optimizer update (FusedAdam) replaces the gradient store; a template parameter so
 // that the plain instantiation keeps its register allocation (the runtime branch cost C2' 25 %).
 template <uint32_t F, bool FUSED>
-__global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, const Levels lv, const uint32_t* __restrict__ tot,
+__global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, const Levels lv, const BrickConst bk, const GridBwdArgs a,
+                                                         const uint32_t* __restrict__ tot,
                                                          const uint32_t* __restrict__ lo_arr, uint32_t B, uint32_t split_limit,
                                                          uint32_t max_parts, const uint16_t* __restrict__ item_idx,
                                                          const f16* __restrict__ item_val, f16* __restrict__ grad, bool overwrite,
                                                          const uint32_t* __restrict__ split, unsigned long long* __restrict__ scratch,
-                                                         uint32_t debug, const FusedAdam fa) {
+                                                         uint32_t debug, const FusedAdam fa, const BrickFallback fb) {
 	extern __shared__ unsigned long long acc[];
 	const uint32_t NE = 1u << B, NEP = NE + 1;  // feature planes padded by one entry (accumulate_items)
 	if (blockIdx.x < max_parts) {
 		if (blockIdx.x >= split[0]) return;
 		const uint32_t* d = split + 2 + 3 * (size_t)blockIdx.x;
 		const uint32_t lo = d[1], hi = d[2];
+		if (d[0] < bk.NBK) {
+			accumulate_brick<F>(c, bk, a, d[0], lo, hi, item_idx, item_val, acc, scratch + (size_t)blockIdx.x * NE * F, NE, fb);
+			return;
+		}
 		for (uint32_t k = threadIdx.x; k < NEP * F; k += blockDim.x) acc[k] = 0ull;
 		__syncthreads();
 		if (!(debug & 1)) accumulate_items<F>(acc, NE, lo, hi, item_idx, item_val, debug);
@@ -509,6 +765,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 		return;
 	}
 	const uint32_t vb = blockIdx.x - max_parts;
+	if (vb < bk.NBK) return;  // bricks: parts only
 	const uint32_t t = tot[vb];
 	if (t > split_limit) return;
 	uint32_t e0, n_e;
@@ -586,14 +843,46 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 // and write every entry once — no fp16 atomics, bitwise reproducible. Columns x >= slab_x0 of the grid
 // run the MLP's dW slab reduction (SlabJob) instead: this kernel leaves most of the chip idle, so the
 // reduction fits beside it.
+// Columns [fin_x0, gridDim.x) finalize the brick levels: one parameter pair per thread (pair k = entry
+// features 2k, 2k + 1 of the grid's leading entries), summed over the bricks' slabs (brick_entry_sum).
 template <uint32_t F, bool FUSED>
 __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst c, const Levels lv, uint32_t B,
                                                                 const uint32_t* __restrict__ split, const uint32_t* __restrict__ splitb,
                                                                 const unsigned long long* __restrict__ scratch, f16* __restrict__ grad,
-                                                                bool overwrite, const SlabJob sj, uint32_t slab_x0, const FusedAdam fa) {
+                                                                bool overwrite, const SlabJob sj, uint32_t slab_x0, const FusedAdam fa,
+                                                                const BrickConst bk, const uint32_t* __restrict__ bp, const BrickFallback fb,
+                                                                uint32_t fin_x0) {
 	static_assert(SC_THREADS == SLAB_THREADS, "slab blocks share the split-reduce block shape");
+	if (blockIdx.x >= fin_x0) {
+		const uint32_t blk = blockIdx.y * (gridDim.x - fin_x0) + (blockIdx.x - fin_x0);
+		const uint32_t k = blk * blockDim.x + threadIdx.x;
+		if (k >= c.offsets[bk.LD] * F / 2) return;
+		const uint32_t NE = 1u << B;
+		const bool used = *fb.flag != 0u;
+		unsigned long long q0, q1;
+		if constexpr (F == 1) {
+			q0 = brick_entry_sum(c, bk, 2 * k, 0, F, NE, bp, scratch, fb, used);
+			q1 = brick_entry_sum(c, bk, 2 * k + 1, 0, F, NE, bp, scratch, fb, used);
+		} else {
+			const uint32_t e = k / (F / 2), fp = k % (F / 2);
+			q0 = brick_entry_sum(c, bk, e, 2 * fp, F, NE, bp, scratch, fb, used);
+			q1 = brick_entry_sum(c, bk, e, 2 * fp + 1, F, NE, bp, scratch, fb, used);
+		}
+		float s0 = fix_to_f32(q0), s1 = fix_to_f32(q1);
+		if (FUSED) {
+			fused_adam_pair(fa, k, (f16)s0, (f16)s1);
+			return;
+		}
+		if (!overwrite) {
+			const f16x2 o = ((const f16x2*)grad)[k];
+			s0 += (float)o[0];
+			s1 += (float)o[1];
+		}
+		((f16x2*)grad)[k] = f16x2{(f16)s0, (f16)s1};
+		return;
+	}
 	if (blockIdx.x >= slab_x0) {
-		const uint32_t blk = blockIdx.y * (gridDim.x - slab_x0) + (blockIdx.x - slab_x0);
+		const uint32_t blk = blockIdx.y * (fin_x0 - slab_x0) + (blockIdx.x - slab_x0);
 		if (blk < slab_blocks(sj.n)) reduce_slabs_block(sj, blk);
 		return;
 	}
@@ -641,12 +930,12 @@ size_t scatter_lds_bytes(uint32_t max_lb, uint32_t chunk, uint32_t D, uint32_t F
 	return (size_t)(3 * max_lb + 1) * 4 + nit * 4 + 16 + nit * F * 2;
 }
 
-Levels make_levels(const GridDesc& g, uint32_t B) {
+Levels make_levels(const GridDesc& g, uint32_t B, const BrickConst& bk) {
 	Levels lv{};
-	uint32_t vb = 0;
+	uint32_t vb = bk.NBK;  // bricks first; brick levels have no buckets
 	for (uint32_t l = 0; l < g.n_levels; ++l) {
 		lv.vb_base[l] = vb;
-		vb += (g.offsets[l + 1] - g.offsets[l] + (1u << B) - 1) >> B;
+		if (l >= bk.LD) vb += (g.offsets[l + 1] - g.offsets[l] + (1u << B) - 1) >> B;
 	}
 	for (uint32_t l = g.n_levels; l <= 32; ++l) lv.vb_base[l] = vb;
 	return lv;
@@ -663,23 +952,31 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 	unsigned long long* scratch = (unsigned long long*)(ws + p.off_scratch);
 	uint16_t* idx = (uint16_t*)(ws + p.off_idx);
 	f16* val = (f16*)(ws + p.off_val);
+	const uint32_t* bp = (const uint32_t*)(ws + p.off_bp);
+	const BrickFallback fb{(unsigned long long*)(ws + p.off_fb), (uint32_t*)(ws + p.off_fb + (size_t)c.offsets[p.bk.LD] * c.n_features * 8)};
 	const size_t lds_s = scatter_lds_bytes(p.max_lb, p.spb, D, F);
 	const uint32_t xcd_map = p.xcd_map;
-	const dim3 grid_s(xcd_map ? (uint32_t)div_round_up(p.n_chunks, 8) * 8 * c.n_levels : p.n_chunks * c.n_levels);
+	const uint32_t n_slots = c.n_levels - p.bk.LD + (p.bk.LD ? 1u : 0u);
+	const dim3 grid_s(xcd_map ? (uint32_t)div_round_up(p.n_chunks, 8) * 8 * n_slots : p.n_chunks * n_slots);
 	auto go = [&](auto scatter, auto accum, auto splitr) {
 		ensure_dynamic_lds((const void*)scatter, lds_s);
-		if (!(debug & 4)) scatter<<<grid_s, p.spb == 512 ? 512 : 1024, lds_s, s>>>(c, lv, a, p.B, p.n_buckets, p.n_chunks, xcd_map, cur_t, lo, idx, val, debug);
+		if (!(debug & 4))
+			scatter<<<grid_s, p.spb == 512 ? 512 : 1024, lds_s, s>>>(c, lv, p.bk, a, p.B, p.n_buckets, p.n_chunks, xcd_map, cur_t, lo, idx, val,
+			                                                          debug);
 		NGP_HIP(hipGetLastError());
 		const size_t lds_a = ((size_t)8 << p.B) * c.n_features + SC_LDS_PAD_BYTES + (fa.rec ? SC_LIST_BYTES : 0);
 		ensure_dynamic_lds((const void*)accum, lds_a);
-		accum<<<p.max_split_blocks + p.n_buckets, p.bt, lds_a, s>>>(c, lv, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
-		                                                                     val, a.grad, overwrite, split, scratch, debug, fa);
+		accum<<<p.max_split_blocks + p.n_buckets, p.bt, lds_a, s>>>(c, lv, p.bk, a, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
+		                                                                     val, a.grad, overwrite, split, scratch, debug, fa, fb);
 		NGP_HIP(hipGetLastError());
 		const uint32_t gy = (uint32_t)div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS);
 		const SlabJob sj = slab ? *slab : SlabJob{};
 		const uint32_t slab_x = slab ? (uint32_t)div_round_up(slab_blocks(sj.n), gy) : 0u;
-		const dim3 grid_r(p.max_split_buckets + slab_x, gy);
-		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets, fa);
+		const size_t fin_pairs = (size_t)c.offsets[p.bk.LD] * c.n_features / 2;
+		const uint32_t fin_x = (uint32_t)div_round_up(div_round_up(fin_pairs, SC_THREADS), gy);
+		const dim3 grid_r(p.max_split_buckets + slab_x + fin_x, gy);
+		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets, fa, p.bk, bp, fb,
+		                                     p.max_split_buckets + slab_x);
 		NGP_HIP(hipGetLastError());
 	};
 	auto by_chunk = [&](auto sc512, auto sc1024, auto accum, auto splitr) {
@@ -701,9 +998,70 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 #undef NGP_SC_F
 }
 
+// Brick geometry for the leading LD dense levels (3D). Finest level f = LD - 1: brick b covers cells
+// [K b, K b + K) and so corners [K b, K b + K]. A coarser level l gets, per brick coordinate, the corners of
+// every cell a position of that range can fall in (computed in double, one cell of margin each side for the
+// float rounding of the samples' own level_setup), W[l] = the widest such range. Returns bk.LD = 0 when no
+// LD fits the bucket's LDS tile (R <= NE) or saves bytes: the slabs (one per non-empty brick and part, R * F
+// int64, written and read once) must cost under 3/4 of the items they replace (LD * 2^D per sample, also
+// written and read once). C2 (2^18 samples): 24 MB of slabs for 63 MB of items; not at 2^16 samples.
+static BrickConst make_bricks(const GridDesc& g, uint32_t n, uint32_t B, uint32_t brick_part) {
+	BrickConst best;
+	if (g.n_dims != 3) return best;
+	if (const char* e = getenv("NGP_SC_BRICKS")) { if (atoi(e) == 0) return best; }
+	const uint32_t F = g.n_features, NE = 1u << B;
+	// dense levels with T = res^3 exactly (even res: the unclamped upper corners alias modulo res^3 only,
+	// brick_entry_sum), at most 4
+	uint32_t dense = 0;
+	while (dense < g.n_levels && dense < 4) {
+		const uint64_t r = g.resolution[dense];
+		if (r * r * r != g.offsets[dense + 1] - g.offsets[dense]) break;
+		++dense;
+	}
+	double best_save = 0.0;
+	for (uint32_t LD = 1; LD <= dense; ++LD) {
+		BrickConst bk;
+		bk.LD = LD; bk.K = 8;
+		const uint32_t f = LD - 1, cells = g.resolution[f];  // positions in [0, 1]: cells 0..res-1
+		bk.NB = (cells + bk.K - 1) / bk.K;
+		if (bk.NB < 2 || bk.NB > 32) continue;
+		bk.NBK = bk.NB * bk.NB * bk.NB;
+		bool ok = true;
+		for (uint32_t l = 0; l < LD && ok; ++l) {
+			uint32_t W = 0;
+			for (uint32_t b = 0; b < bk.NB; ++b) {
+				int64_t c_lo, c_hi;
+				if (l == f) { c_lo = (int64_t)bk.K * b; c_hi = c_lo + bk.K; }
+				else {
+					const double sl = g.scale[l], sf = g.scale[f];
+					const double lower = sl * ((double)bk.K * b - 0.5) / sf + 0.5, upper = sl * ((double)bk.K * b + bk.K - 0.5) / sf + 0.5;
+					c_lo = (int64_t)std::floor(lower) - 1;
+					c_hi = (int64_t)std::floor(upper) + 2;  // last cell (+ margin) + its upper corner
+				}
+				c_lo = std::max<int64_t>(c_lo, 0);
+				c_hi = std::min<int64_t>(c_hi, (int64_t)g.resolution[l]);  // the last cell's upper corner is coordinate res
+				bk.lo[l][b] = (uint16_t)c_lo;
+				W = std::max<uint32_t>(W, (uint32_t)(c_hi - c_lo + 1));
+			}
+			bk.W[l] = W;
+			bk.regoff[l] = bk.R;
+			bk.R += W * W * W;
+			ok = bk.R <= NE;
+		}
+		if (!ok) continue;
+		// parts: one per non-empty brick, more where bricks hold over brick_part samples
+		const double parts = std::max((double)std::min<uint64_t>(bk.NBK, n), (double)n / brick_part);
+		const double slabs = parts * bk.R * F * 8;
+		const double items = (double)n * LD * 8 * (2 + 2 * F);
+		const double save = 0.75 * items - slabs;
+		if (save > best_save) { best_save = save; best = bk; }
+	}
+	return best;
+}
+
 }  // namespace
 
-ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
+ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n, bool bricks) {
 	ScatterPlan p;
 	const uint32_t F = g.n_features;
 	// bucket = 2^B entries of one level whose F int64 accumulators fill SC_LDS_BYTES
@@ -711,27 +1069,30 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	size_t lds_budget = SC_LDS_BYTES;  // experiment knob NGP_SC_LDS_KB (<= 64)
 	if (const char* e = getenv("NGP_SC_LDS_KB")) lds_budget = std::min<size_t>(SC_LDS_BYTES, (size_t)atoi(e) * 1024);
 	while (((size_t)2 << p.B) * F * 8 <= lds_budget && p.B < 16) ++p.B;
-	const Levels lv = make_levels(g, p.B);
+	if (const char* e = getenv("NGP_SC_BRICK_PART")) p.brick_part = std::max(1, atoi(e));
+	if (bricks) p.bk = make_bricks(g, n, p.B, p.brick_part);
+	const Levels lv = make_levels(g, p.B, p.bk);
 	p.n_buckets = lv.vb_base[g.n_levels];
-	p.max_lb = 0;
+	p.max_lb = p.bk.NBK;
 	for (uint32_t l = 0; l < g.n_levels; ++l) p.max_lb = std::max(p.max_lb, lv.vb_base[l + 1] - lv.vb_base[l]);
 	NGP_CHECK((size_t)p.max_lb * 4 <= 32 * 1024, "grid backward: level too large for the bucket histogram");
 	// samples per chunk: 1024 when 512-sample chunks would average fewer than 16 items per (chunk,
 	// bucket) and the scatter block's LDS allows it
-	const uint64_t items_per_sample = (uint64_t)g.n_levels << g.n_dims;
+	const uint64_t items_per_sample = ((uint64_t)(g.n_levels - p.bk.LD) << g.n_dims) + (p.bk.LD ? 1u : 0u);
 	p.spb = 512;
 	if (512ull * items_per_sample < 16ull * p.n_buckets && scatter_lds_bytes(p.max_lb, 1024, g.n_dims, F) <= 160 * 1024) p.spb = 1024;
 	if (const char* e = getenv("NGP_SC_CHUNK")) p.spb = (uint32_t)atoi(e);
 	NGP_CHECK(p.spb == 512 || p.spb == 1024, "grid backward: chunk must be 512 or 1024 samples");
 	NGP_CHECK(scatter_lds_bytes(p.max_lb, p.spb, g.n_dims, F) <= 160 * 1024, "grid backward: scatter chunk exceeds LDS");
 	p.n_chunks = (uint32_t)div_round_up(n, p.spb);
-	p.n_items = (uint64_t)n * g.n_levels * (1u << g.n_dims);
+	p.n_items = (uint64_t)n * items_per_sample;
 	NGP_CHECK(p.n_items < (1ull << 32), "grid backward: too many contributions for 32-bit offsets");
 	p.split_limit = 49152;
 	p.part = 49152;
 	if (const char* e = getenv("NGP_SC_PART")) p.part = (uint32_t)atoi(e);
 	if (const char* e = getenv("NGP_SC_LIMIT")) p.split_limit = (uint32_t)atoi(e);
 	p.max_split_blocks = (uint32_t)(div_round_up(p.n_items, (uint64_t)p.part) + div_round_up(p.n_items, (uint64_t)p.split_limit) + 1);
+	if (p.bk.LD) p.max_split_blocks += (uint32_t)(std::min<uint64_t>(p.bk.NBK, n) + div_round_up((uint64_t)n, (uint64_t)p.brick_part));
 	p.max_split_buckets = (uint32_t)(div_round_up(p.n_items, (uint64_t)p.split_limit) + 1);
 	p.xcd_map = 2;
 	if (const char* e = getenv("NGP_SC_XCD")) p.xcd_map = (uint32_t)atoi(e);
@@ -752,16 +1113,19 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n) {
 	p.off_scratch = align(p.off_splitb + 3 * (size_t)p.max_split_buckets * 4);
 	p.off_idx = align(p.off_scratch + (size_t)p.max_split_blocks * ((size_t)1 << p.B) * g.n_features * 8);
 	p.off_val = align(p.off_idx + p.n_items * 2);
-	p.total = align(p.off_val + p.n_items * F * 2);
+	p.off_bp = align(p.off_val + p.n_items * F * 2);
+	p.off_fb = align(p.off_bp + (size_t)p.bk.NBK * 8);
+	p.total = align(p.off_fb + (size_t)g.offsets[p.bk.LD] * F * 8 + 4);
 	return p;
 }
 
 bool scatter_hist(const GridDesc& g, const ScatterPlan& p, void* workspace, GridHist& h) {
 	if ((size_t)p.n_buckets * 4 > 48 * 1024 || p.spb != 512) return false;
-	const Levels lv = make_levels(g, p.B);
+	const Levels lv = make_levels(g, p.B, p.bk);
 	h.hist = (uint32_t*)((char*)workspace + p.off_hist);
 	h.B = p.B; h.n_chunks = p.n_chunks; h.chunk = p.spb;
 	for (int l = 0; l <= 32; ++l) h.vb_base[l] = lv.vb_base[l];
+	h.brick_levels = p.bk.LD; h.n_bricks = p.bk.NBK; h.brick_cells = p.bk.K; h.bricks_per_dim = p.bk.NB;
 	return true;
 }
 
@@ -771,12 +1135,12 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const Scatter
 	uint32_t* hist = (uint32_t*)(ws + p.off_hist);
 	if (!hist_done) {
 		const GridConst c = make_grid_const(g);
-		const Levels lv = make_levels(g, p.B);
+		const Levels lv = make_levels(g, p.B, p.bk);
 		const dim3 grid_h(p.n_chunks, g.n_levels);
 		const size_t lds_h = (size_t)p.max_lb * 4;
 		auto go = [&](auto k3, auto k2) {
-			if (g.n_dims == 3) k3<<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
-			else k2<<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, a, p.B, p.n_chunks, hist);
+			if (g.n_dims == 3) k3<<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, p.bk, a, p.B, p.n_chunks, hist);
+			else k2<<<grid_h, SC_THREADS, lds_h, s>>>(c, lv, p.bk, a, p.B, p.n_chunks, hist);
 		};
 		if (p.spb == 512) go(k_sc_hist<3, 512>, k_sc_hist<2, 512>);
 		else go(k_sc_hist<3, 1024>, k_sc_hist<2, 1024>);
@@ -786,7 +1150,9 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const Scatter
 	NGP_HIP(hipGetLastError());
 	const auto plan = p.n_buckets <= SC_PLAN_THREADS ? k_sc_plan<1> : p.n_buckets <= 8 * SC_PLAN_THREADS ? k_sc_plan<8> : k_sc_plan<32>;
 	plan<<<1, SC_PLAN_THREADS, 0, s>>>((const uint32_t*)(ws + p.off_tot), p.n_buckets, p.split_limit, p.part,
-	                                        (uint32_t*)(ws + p.off_lo), (uint32_t*)(ws + p.off_split), (uint32_t*)(ws + p.off_splitb));
+	                                        (uint32_t*)(ws + p.off_lo), (uint32_t*)(ws + p.off_split), (uint32_t*)(ws + p.off_splitb),
+	                                        p.bk.NBK, p.brick_part, (uint32_t*)(ws + p.off_bp),
+	                                        p.bk.LD ? (uint32_t*)(ws + p.off_fb + (size_t)g.offsets[p.bk.LD] * g.n_features * 8) : nullptr);
 	NGP_HIP(hipGetLastError());
 }
 
@@ -796,7 +1162,7 @@ void grid_backward_sorted(const GridDesc& g, const GridBwdArgs& b, const Scatter
 	NGP_CHECK(b.level_begin == 0, "grid_backward_sorted handles all levels");
 	NGP_CHECK(!fused || (overwrite && g.n_features >= 2), "fused optimizer: overwrite mode, F >= 2");
 	const GridConst c = make_grid_const(g);
-	const Levels lv = make_levels(g, p.B);
+	const Levels lv = make_levels(g, p.B, p.bk);
 	const FusedAdam fa = fused ? *fused : FusedAdam{};
 	if (g.n_dims == 3) launch_backward<3>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab, fa);
 	else launch_backward<2>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab, fa);

@@ -86,8 +86,16 @@ __device__ __forceinline__ f16 wval(const LW& L, bool tr, uint32_t m, uint32_t k
 	const uint32_t o = tr ? k : m, i = tr ? m : k;
 	return o < L.out && i < L.in ? L.w[o * L.stride + i] : (f16)0.f;
 }
+// Non-transposed fragments read whole dwords (k runs of 4 or 8 along a padded row, 4-B aligned: the rows are
+// (in + 2) halves apart, in even), in range at every call site (m < out, k < in); transposed ones gather
+// 2-B elements down a column.
+__device__ __forceinline__ uint32_t wpair(const LW& L, uint32_t m, uint32_t k) { return *(const uint32_t*)(L.w + m * L.stride + k); }
 __device__ __forceinline__ f16x8 wfrag32(const LW& L, bool tr, uint32_t t, uint32_t s, bool perm, uint32_t lane) {
 	const uint32_t m = 16 * t + (lane & 15), g = lane >> 4;
+	if (!tr) {
+		const uint32_t k0 = perm ? 32 * s + 4 * g : 32 * s + 8 * g, k1 = perm ? k0 + 16 : k0 + 4;
+		return __builtin_bit_cast(f16x8, u32x4v{wpair(L, m, k0), wpair(L, m, k0 + 2), wpair(L, m, k1), wpair(L, m, k1 + 2)});
+	}
 	f16x8 v;
 #pragma unroll
 	for (uint32_t j = 0; j < 8; ++j) v[j] = wval(L, tr, m, perm ? kperm(s, j, g) : 32 * s + 8 * g + j);
@@ -95,6 +103,7 @@ __device__ __forceinline__ f16x8 wfrag32(const LW& L, bool tr, uint32_t t, uint3
 }
 __device__ __forceinline__ f16x4 wfrag16(const LW& L, bool tr, uint32_t t, uint32_t lane) {
 	const uint32_t m = 16 * t + (lane & 15), g = lane >> 4;
+	if (!tr) return __builtin_bit_cast(f16x4, u32x2{wpair(L, m, 4 * g), wpair(L, m, 4 * g + 2)});
 	f16x4 v;
 #pragma unroll
 	for (uint32_t j = 0; j < 4; ++j) v[j] = wval(L, tr, m, 4 * g + j);
@@ -188,6 +197,16 @@ struct Train16Layout {
 	static_assert(STAGE_HALVES <= 4 * IMG_HALVES, "parameter staging must fit the image region");
 };
 
+// Timing experiments only (-DNGP_T16_CLOCK, DESIGN §6 phase costs): block 0..1023's thread 0 stamps the
+// 100-MHz wall clock at the phase boundaries (slots: 0 entry, 1 staged, 2 loop entry, 3 + 3i / 4 + 3i / 5 + 3i
+// iteration i's forward / backward / dW ends, 31 exit); ngp_debug_t16_clock copies them out.
+#ifdef NGP_T16_CLOCK
+__device__ uint64_t g_t16_clock[1024 * 32];
+#define T16_MARK(i) do { if (threadIdx.x == 0 && blockIdx.x < 1024 && (i) < 32) g_t16_clock[blockIdx.x * 32 + (i)] = wall_clock64(); } while (0)
+#else
+#define T16_MARK(i) do {} while (0)
+#endif
+
 template <int ES, int DH, int RH>
 __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 2))) k_nerf_mlp_train16(const NerfMlpArgs a) {
 	using T = Train16Layout<ES, DH, RH>;
@@ -202,6 +221,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 	// fragments are gathered from there (from global they cost ~150 scattered 2-B loads per lane, and from an
 	// unpadded copy 16-way bank conflicts)
 	f16* stage = imgs;
+	T16_MARK(0);
 	auto wd = [&](int l) {  // density MLP: [64 x 16ES], (DH-1) x [64 x 64], [16 x 64]
 		return LW{stage + T::stage_d(l), l == DH ? 16u : 64u, l == 0 ? 16u * ES : 64u, (l == 0 ? 16u * ES : 64u) + 2u};
 	};
@@ -209,18 +229,48 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		return LW{stage + T::stage_r(l), l == RH ? 16u : 64u, l == 0 ? 32u : 64u, (l == 0 ? 32u : 64u) + 2u};
 	};
 	{
-		auto copy = [&](const LW& L, const f16* src) {
-			for (uint32_t i = threadIdx.x; i < L.out * L.in; i += blockDim.x)
-				((f16*)L.w)[(i / L.in) * L.stride + i % L.in] = src[i];
-		};
+		// 16-B chunks (8 halves of one row: every row length is a multiple of 8), all loads issued before the
+		// first store; a scalar copy loop waited on one L2 round trip per iteration (~20 of them)
+		constexpr uint32_t ND = 64 * 16 * ES + (DH - 1) * 64 * 64 + 16 * 64, NR = 64 * 32 + (RH - 1) * 64 * 64 + 16 * 64;
+		constexpr uint32_t NCH = (ND + NR) / 8, PER = (NCH + 511) / 512;
 		const f16* pd = a.params + a.density_woff;
 		const f16* pr = a.params + a.rgb_woff;
+		f16x8 v[PER];
 #pragma unroll
-		for (int l = 0; l <= DH; ++l) copy(wd(l), pd + (l == 0 ? 0 : 64 * 16 * ES + (l - 1) * 64 * 64));
+		for (uint32_t k = 0; k < PER; ++k) {
+			const uint32_t c = threadIdx.x + 512 * k;
+			if (c < NCH) v[k] = *(const f16x8*)(c < ND / 8 ? pd + 8 * c : pr + 8 * (c - ND / 8));
+		}
+		auto put8 = [&](const LW& L, uint32_t h, f16x8 x) {  // h = the chunk's first element in [out x in]
+			uint32_t* d = (uint32_t*)(L.w + (h / L.in) * L.stride + h % L.in);
+			const u32x4v u = __builtin_bit_cast(u32x4v, x);
+			d[0] = u[0]; d[1] = u[1]; d[2] = u[2]; d[3] = u[3];
+		};
 #pragma unroll
-		for (int l = 0; l <= RH; ++l) copy(wr(l), pr + (l == 0 ? 0 : 64 * 32 + (l - 1) * 64 * 64));
+		for (uint32_t k = 0; k < PER; ++k) {
+			const uint32_t c = threadIdx.x + 512 * k;
+			if (c >= NCH) continue;
+			if (c < ND / 8) {
+				uint32_t h = 8 * c;
+#pragma unroll
+				for (int l = 0; l <= DH; ++l) {
+					const LW L = wd(l);
+					if (h < L.out * L.in) { put8(L, h, v[k]); break; }
+					h -= L.out * L.in;
+				}
+			} else {
+				uint32_t h = 8 * c - ND;
+#pragma unroll
+				for (int l = 0; l <= RH; ++l) {
+					const LW L = wr(l);
+					if (h < L.out * L.in) { put8(L, h, v[k]); break; }
+					h -= L.out * L.in;
+				}
+			}
+		}
 	}
 	__syncthreads();
+	T16_MARK(1);
 
 	// backward (transposed) weights -> LDS, one copy per block
 	for (int t = threadIdx.x; t < 4 * 64; t += blockDim.x) {  // K=16 fragments: W_ro^T and W_do^T, 4 tiles each
@@ -310,6 +360,8 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
 	for (int k = 0; k < PF; ++k) load_inputs(pf[k], blockIdx.x * 4 + pair + k * gridDim.x * 4);
 	__syncthreads();  // backward weights in LDS; the staged parameters are no longer read (images overwrite them)
+	T16_MARK(2);
+	[[maybe_unused]] uint32_t it = 0;
 
 	for (uint32_t base = blockIdx.x * 4; base < n_tiles; base += gridDim.x * 4) {
 		const uint32_t tile = base + pair;
@@ -384,6 +436,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
 		for (int l = 0; l < RH; ++l) img_put64(img + T::I_HR + l * 32 * T::S_64 + r * T::S_64, g, hr[l]);
 
+		T16_MARK(3 + 3 * it);
 		// ---- backward dX chain, every dZ kept in the pair image ------------------------------------
 #ifndef NGP_T16_SKIP_BWD  // timing experiments only (phase costs)
 		const float dsig = (float)dl_cur[3];
@@ -445,6 +498,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		}
 #endif
 		__syncthreads();
+		T16_MARK(4 + 3 * it);
 
 		// ---- dW over the four pair images (K = 32 samples per MFMA), images in a fixed order ---------
 #ifndef NGP_T16_SKIP_B
@@ -483,6 +537,8 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		}
 #endif
 		__syncthreads();
+		T16_MARK(5 + 3 * it);
+		++it;
 	}
 
 	// this wave's dW tiles -> the block's slab at their parameter-slice positions [out x in]
@@ -511,6 +567,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		put(dw[2], rw0, 32, v, 1);
 		put(dw[3], dw0 + 64 * 16 * ES + 64 * 64 * (DH - 1), 64, 0, v);
 	}
+	T16_MARK(31);
 }
 
 template <int ES, int DH, int RH>
@@ -531,6 +588,8 @@ static bool launch_train16(const NerfMlpArgs& a, hipStream_t s) {
 
 bool nerf_mlp_train16_run(const NerfMlpPlan& p, const NerfMlpArgs& a, hipStream_t s) {
 	if (!a.params || a.n == 0) return false;
+	// the parameter staging reads 16-B chunks
+	if (((uintptr_t)(a.params + a.density_woff) | (uintptr_t)(a.params + a.rgb_woff)) % 16) return false;
 	const uint32_t key = p.enc_steps * 100 + p.d_hidden * 10 + p.r_hidden;
 	switch (key) {
 		case 112: return launch_train16<1, 1, 2>(a, s);
@@ -542,3 +601,9 @@ bool nerf_mlp_train16_run(const NerfMlpPlan& p, const NerfMlpArgs& a, hipStream_
 }
 
 }  // namespace ngp
+
+#ifdef NGP_T16_CLOCK
+extern "C" __attribute__((visibility("default"))) int ngp_debug_t16_clock(uint64_t* out, uint32_t n) {
+	return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ngp::g_t16_clock), (size_t)(n < 1024 * 32 ? n : 1024 * 32) * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif

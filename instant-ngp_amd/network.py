@@ -123,6 +123,12 @@ class Model:
     def set_option(self, key, value):
         check(lib().ngp_model_set_option(self.handle, key.encode(), float(value)))
 
+    def query(self, key):
+        """engine state (ngp_model_query): "grid_brick_levels" """
+        v = C.c_double()
+        check(lib().ngp_model_query(self.handle, key.encode(), C.byref(v)))
+        return v.value
+
     def reserve(self, n):
         check(lib().ngp_model_reserve(self.handle, n))
 

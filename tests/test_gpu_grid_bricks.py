@@ -1,0 +1,69 @@
+"""Brick-summed dense levels of the bucketed grid backward (csrc/grid_scatter.hip, ScatterPlan::bk).
+
+At 2^18 samples the C2 (L4 F4) and C2' (L16 F2) grids send their leading dense levels 0-2 through bricks
+(each sample's index sorted by brick, its contributions summed in LDS over the brick's region, the exact
+int64 slabs added per entry) instead of 8 items per sample and level. The contributions and their
+fixed-point sums are those of the item path, so training must be bit for bit the same with the bricks
+switched off (model option grid_bricks = 0): the NeRF training step with
+the forward-fused histogram, on the eager layout (C2) and with the grid's optimizer update fused into the
+backward (C2', lazy layout), on uniform and on concentrated sample clouds whose bricks split into parts,
+with positions on and past the unit cube's faces (the exact global fallback). The oracle comparison of the
+same path is tests/test_gpu_grid_exact.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+N = 1 << 18
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    from __graft_entry__ import load_package
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return load_package()
+
+
+def batch(kind, n, seed):
+    g = np.random.default_rng(seed)
+    c = np.zeros((n, 7), np.float32)
+    c[:, :3] = g.random((n, 3), dtype=np.float32)
+    if kind == "blob":  # NeRF-like: 80 % of the samples in a small blob -> a few bricks of thousands of samples
+        blob = np.clip(0.5 + 0.05 * g.standard_normal((n, 3)), 0.0, 1.0).astype(np.float32)
+        keep = g.random(n) < 0.8
+        c[keep, :3] = blob[keep]
+    c[:64, :3] = np.round(c[:64, :3] * 8) / 8   # brick and cell boundaries
+    c[64:72, :3] = 1.0                          # the upper faces
+    c[72:80, :3] = np.float32(1.0 + 2e-2)       # past the cube: corners outside every brick region
+    c[80:88, :3] = np.float32(-1e-2)
+    d = g.standard_normal((n, 3))
+    c[:, 4:] = (d / np.linalg.norm(d, axis=1, keepdims=True) + 1) / 2
+    dL = np.zeros((n, 16), np.float16)
+    dL[:, :4] = g.uniform(-1e-2, 1e-2, (n, 4))
+    return torch.from_numpy(c).cuda(), torch.from_numpy(dL).cuda()
+
+
+def train(pkg, variant, kind, bricks, steps=4):
+    cfg = pkg.nerf_config(variant)
+    net = pkg.create_nerf_network(cfg)
+    net.set_option("grid_bricks", 1 if bricks else 0)
+    tr = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+    net.reserve(N)
+    for s in range(steps):
+        x, dL = batch(kind, N, 100 + s)
+        tr.train_step(x, dL, 128.0)
+    torch.cuda.synchronize()
+    assert net.query("grid_brick_levels") == (3 if bricks else 0)  # C2 and C2': levels 0-2 of res 16, 32, 64
+    return tr.params.cpu().numpy().view(np.uint16).copy(), tr.params_full_precision.cpu().numpy().view(np.uint32).copy()
+
+
+@pytest.mark.parametrize("variant", ["C2", "C2p"])
+@pytest.mark.parametrize("kind", ["uniform", "blob"])
+def test_bricks_train_bitwise_like_items(pkg, variant, kind):
+    p1, w1 = train(pkg, variant, kind, True)
+    p0, w0 = train(pkg, variant, kind, False)
+    assert np.isfinite(p1.view(np.float16).astype(np.float32)).all()
+    np.testing.assert_array_equal(p1, p0)
+    np.testing.assert_array_equal(w1, w0)
