@@ -378,6 +378,10 @@ int ngp_nerf_trainer_buffers_read(const ngp_nerf_trainer* t, const float** densi
 typedef struct ngp_nerf_renderer ngp_nerf_renderer;
 int ngp_nerf_renderer_create(ngp_nerf_renderer** out);
 void ngp_nerf_renderer_destroy(ngp_nerf_renderer* r);
+/* ERenderMode of the following renders (common.h:110-119): 1 Shade (default), 2 Normals (testbed_nerf.cu:
+ * 1183-1188, 2179-2181, 2615-2617: the density output's input gradient per step, ngp_input_gradient with
+ * backprop_scale 128, composited as normalize(-density'(raw) * gradient), shaded as (0.5 n + 0.5) * alpha) */
+int ngp_nerf_renderer_set_mode(ngp_nerf_renderer* r, int render_mode);
 int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_config* cfg, void* stream, const ngp_nerf_image* camera,
                     const uint8_t* bitfield, uint32_t spp, uint32_t sample_index, float min_transmittance,
                     const float* background_rgba, int use_inference_params, float* out_rgba);

@@ -173,6 +173,7 @@ SIGNATURES = {
     "ngp_trainer_set_allreduce": (i32, [P, u32, P, P]),
     "ngp_nerf_renderer_create": (i32, [C.POINTER(P)]),
     "ngp_nerf_renderer_destroy": (None, [P]),
+    "ngp_nerf_renderer_set_mode": (i32, [P, i32]),
     "ngp_nerf_render": (i32, [P, P, C.POINTER(NerfConfig), P, C.POINTER(NerfImage), P, u32, u32, f32, P, i32, P]),
 }
 

@@ -198,13 +198,24 @@ struct Train16Layout {
 };
 
 // Timing experiments only (-DNGP_T16_CLOCK, DESIGN §6 phase costs): block 0..1023's thread 0 stamps the
-// 100-MHz wall clock at the phase boundaries (slots: 0 entry, 1 staged, 2 loop entry, 3 + 3i / 4 + 3i / 5 + 3i
-// iteration i's forward / backward / dW ends, 31 exit); ngp_debug_t16_clock copies them out.
+// 100-MHz wall clock at the phase boundaries (slots: 0 entry, 1 staged, 2 loop entry, then per iteration i
+// 3 + 12 i + k for k = 0 inputs read, 1 density layer 0, 2 density output + SH, 3 rgb layer 0, 4 rgb hidden,
+// 5 images written, 6 rgb backward chain, 7 density backward chain, 8 dL/denc stored, 9 barrier, 10 dW,
+// 11 barrier; 127 exit); ngp_debug_t16_clock copies them out. Scheduling barriers around each stamp keep
+// the phases apart (the stamped kernel is slower than the plain one).
 #ifdef NGP_T16_CLOCK
-__device__ uint64_t g_t16_clock[1024 * 32];
-#define T16_MARK(i) do { if (threadIdx.x == 0 && blockIdx.x < 1024 && (i) < 32) g_t16_clock[blockIdx.x * 32 + (i)] = wall_clock64(); } while (0)
+constexpr int T16_SLOTS = 128;
+__device__ uint64_t g_t16_clock[1024 * T16_SLOTS];
+#define T16_MARK(i)                                                                                     \
+	do {                                                                                                \
+		__builtin_amdgcn_sched_barrier(0);                                                              \
+		if (threadIdx.x == 0 && blockIdx.x < 1024 && (i) < T16_SLOTS) g_t16_clock[blockIdx.x * T16_SLOTS + (i)] = wall_clock64(); \
+		__builtin_amdgcn_sched_barrier(0);                                                              \
+	} while (0)
+#define T16_IT(k) T16_MARK(3 + 12 * it + (k))
 #else
 #define T16_MARK(i) do {} while (0)
+#define T16_IT(k) do {} while (0)
 #endif
 
 template <int ES, int DH, int RH>
@@ -375,6 +386,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		for (int k = 0; k + 1 < PF; ++k) pf[k] = pf[k + 1];
 		load_inputs(pf[PF - 1], tile + PF * gridDim.x * 4);
 		const int r = 16 * half + sn;       // this lane's row in the pair images
+		T16_IT(0);
 
 		// ---- forward -----------------------------------------------------------------------------
 		if constexpr (ES == 1) img_put4(img + T::I_XE + r * T::S_XE, 0, g, xe16);
@@ -389,6 +401,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			else acc[t] = mma32(wd0_32[t], xe32, f32x4{0.f, 0.f, 0.f, 0.f});
 		}
 		pack64(acc, hd[0]);
+		T16_IT(1);
 #pragma unroll
 		for (int l = 1; l < DH; ++l) {
 #pragma unroll
@@ -402,10 +415,12 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		const f16x4 dout = pack4(dacc, false);                                          // density network output rows 4g..4g+3
 		const f16x4 sh = valid ? sh4_quad(cdx, cdy, cdz, g) : f16x4{};
 		const f16x8 rin = cat(dout, sh);                                                // [density out | SH], permuted k
+		T16_IT(2);
 #pragma unroll
 		for (int t = 0; t < 4; ++t) acc[t] = mma32(wr0[t], rin, f32x4{0.f, 0.f, 0.f, 0.f});
 		f16x8 hr[RH][2];
 		pack64(acc, hr[0]);
+		T16_IT(3);
 #pragma unroll
 		for (int l = 1; l < RH; ++l) {
 #pragma unroll
@@ -415,6 +430,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			}
 			pack64(acc, hr[l]);
 		}
+		T16_IT(4);
 		if (a.out) {
 			const f32x4 racc = mma32(wro[1], hr[RH - 1][1], mma32(wro[0], hr[RH - 1][0], f32x4{0.f, 0.f, 0.f, 0.f}));
 			f16x4 ro = pack4(racc, false);
@@ -436,7 +452,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
 		for (int l = 0; l < RH; ++l) img_put64(img + T::I_HR + l * 32 * T::S_64 + r * T::S_64, g, hr[l]);
 
-		T16_MARK(3 + 3 * it);
+		T16_IT(5);
 		// ---- backward dX chain, every dZ kept in the pair image ------------------------------------
 #ifndef NGP_T16_SKIP_BWD  // timing experiments only (phase costs)
 		const float dsig = (float)dl_cur[3];
@@ -459,6 +475,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			mask64(acc, hr[l - 1], dz);
 		}
 		img_put64(img + T::I_ZR0 + r * T::S_64, g, dz);
+		T16_IT(6);
 		// dL/d(rgb input): tile 0 = the density output rows, tile 1 = the SH rows (input gradients only)
 		f32x4 dd_acc = mma32(*(const f16x8*)(wl + T::B_R0 + (1 * 64 + lane) * 8), dz[1],
 		                     mma32(*(const f16x8*)(wl + T::B_R0 + (0 * 64 + lane) * 8), dz[0], f32x4{0.f, 0.f, 0.f, 0.f}));
@@ -488,6 +505,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			mask64(acc, hd[l - 1], dz);
 		}
 		img_put64(img + T::I_ZD0 + r * T::S_64, g, dz);
+		T16_IT(7);
 		if (a.dL_denc) {
 #pragma unroll
 			for (int t = 0; t < ES; ++t) {
@@ -497,8 +515,9 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			}
 		}
 #endif
+		T16_IT(8);
 		__syncthreads();
-		T16_MARK(4 + 3 * it);
+		T16_IT(9);
 
 		// ---- dW over the four pair images (K = 32 samples per MFMA), images in a fixed order ---------
 #ifndef NGP_T16_SKIP_B
@@ -536,8 +555,9 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			}
 		}
 #endif
+		T16_IT(10);
 		__syncthreads();
-		T16_MARK(5 + 3 * it);
+		T16_IT(11);
 		++it;
 	}
 
@@ -567,7 +587,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		put(dw[2], rw0, 32, v, 1);
 		put(dw[3], dw0 + 64 * 16 * ES + 64 * 64 * (DH - 1), 64, 0, v);
 	}
-	T16_MARK(31);
+	T16_MARK(127);
 }
 
 template <int ES, int DH, int RH>
@@ -604,6 +624,7 @@ bool nerf_mlp_train16_run(const NerfMlpPlan& p, const NerfMlpArgs& a, hipStream_
 
 #ifdef NGP_T16_CLOCK
 extern "C" __attribute__((visibility("default"))) int ngp_debug_t16_clock(uint64_t* out, uint32_t n) {
-	return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ngp::g_t16_clock), (size_t)(n < 1024 * 32 ? n : 1024 * 32) * 8, 0, hipMemcpyDeviceToHost);
+	return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ngp::g_t16_clock), (size_t)(n < 1024 * ngp::T16_SLOTS ? n : 1024 * ngp::T16_SLOTS) * 8, 0,
+	                                hipMemcpyDeviceToHost);
 }
 #endif

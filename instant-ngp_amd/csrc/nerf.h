@@ -122,7 +122,9 @@ struct RenderArgs {
 	uint32_t rgb_activation, density_activation;
 	float min_transmittance;
 	float background[4];           // linear rgba
+	uint32_t render_mode;          // ERenderMode (common.h:110-119): 1 Shade, 2 Normals
 };
+enum : uint32_t { RENDER_SHADE = 1, RENDER_NORMALS = 2 };
 struct RenderWorkspace {
 	void* payload[2]; void* payload_hit;
 	float* rgba[2]; float* rgba_hit;
@@ -134,9 +136,12 @@ struct RenderWorkspace {
 };
 size_t render_payload_bytes();
 // spp samples of one view, averaged into out (linear RGBA [H x W x 4]); infer(n, coords, out_rm)
-// evaluates the network on n NerfCoordinates (output RM, row stride n).
+// evaluates the network on n NerfCoordinates (output RM, row stride n). Normals: grad(n, coords) then
+// overwrites the coordinates' position rows with d(density output)/d(position) (Network::input_gradient,
+// testbed_nerf.cu:2615-2617).
 void render_frame(const RenderArgs& a, uint32_t spp, RenderWorkspace& ws,
-                  const std::function<void(uint32_t, const float*, f16*)>& infer, float* out, hipStream_t s);
+                  const std::function<void(uint32_t, const float*, f16*)>& infer, float* out, hipStream_t s,
+                  const std::function<void(uint32_t, float*)>& grad = nullptr);
 
 }  // namespace nerf
 }  // namespace ngp

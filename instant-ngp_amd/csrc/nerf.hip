@@ -1687,7 +1687,9 @@ __global__ void k_render_inputs(RenderArgs a, uint32_t n, uint32_t n_steps, Payl
 	p.n_steps = n_steps;
 }
 
-// composite_kernel_nerf (:1016-1196), ERenderMode::Shade; network output RM [16 x stride]
+// composite_kernel_nerf (:1016-1196), ERenderMode::Shade and Normals; network output RM [16 x stride]. Normals
+// (:1183-1188): the colour of a step is normalize(-density'(raw) * d(raw density)/d(position)), the gradient
+// in the coordinates' position rows (render_frame's grad).
 __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, uint32_t current_step, uint32_t n_steps,
                                    Payload* __restrict__ pay, float* __restrict__ rgba, const float* __restrict__ coords,
                                    const f16* __restrict__ out) {
@@ -1706,9 +1708,20 @@ __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, ui
 		const float dt = unwarp_dt(coords[r * 7 + 3]);
 		const float alpha = 1.f - ngp_expf_fast(-network_to_density(o3, a.density_activation) * dt);
 		const float weight = alpha * T;
-		c[0] += network_to_rgb(o0, a.rgb_activation) * weight;
-		c[1] += network_to_rgb(o1, a.rgb_activation) * weight;
-		c[2] += network_to_rgb(o2, a.rgb_activation) * weight;
+		float rgb[3];
+		if (a.render_mode == RENDER_NORMALS) {
+			const float dd = -network_to_density_derivative(o3, a.density_activation);
+			const float nx = dd * coords[r * 7 + 0], ny = dd * coords[r * 7 + 1], nz = dd * coords[r * 7 + 2];
+			const float inv = 1.0f / sqrtf(nx * nx + ny * ny + nz * nz);  // glm normalize (0 -> NaN, as the reference)
+			rgb[0] = nx * inv; rgb[1] = ny * inv; rgb[2] = nz * inv;
+		} else {
+			rgb[0] = network_to_rgb(o0, a.rgb_activation);
+			rgb[1] = network_to_rgb(o1, a.rgb_activation);
+			rgb[2] = network_to_rgb(o2, a.rgb_activation);
+		}
+		c[0] += rgb[0] * weight;
+		c[1] += rgb[1] * weight;
+		c[2] += rgb[2] * weight;
 		c[3] += weight;
 		if (weight > p.max_weight) p.max_weight = weight;
 		if (c[3] > (1.0f - a.min_transmittance)) {
@@ -1726,12 +1739,17 @@ __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, ui
 
 // shade_kernel_nerf (:2164-2196) into the frame (pre-filled with the linear background), then the
 // spp average (the render buffer's accumulation)
-__global__ void k_render_shade(uint32_t n_hit, uint32_t linear_colors, const Payload* __restrict__ hit, const float* __restrict__ hit_rgba,
-                               float* __restrict__ frame) {
+__global__ void k_render_shade(uint32_t n_hit, uint32_t linear_colors, uint32_t mode, const Payload* __restrict__ hit,
+                               const float* __restrict__ hit_rgba, float* __restrict__ frame) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n_hit) return;
 	f32x4 c = *(const f32x4*)(hit_rgba + 4 * (size_t)i);
-	if (!linear_colors) { c[0] = srgb_to_linear(c[0]); c[1] = srgb_to_linear(c[1]); c[2] = srgb_to_linear(c[2]); }
+	if (mode == RENDER_NORMALS) {  // (0.5 n + 0.5) * a with n = normalize(rgb)
+		const float inv = 1.0f / sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+		for (int k = 0; k < 3; ++k) c[k] = (0.5f * (c[k] * inv) + 0.5f) * c[3];
+	} else if (!linear_colors) {
+		c[0] = srgb_to_linear(c[0]); c[1] = srgb_to_linear(c[1]); c[2] = srgb_to_linear(c[2]);
+	}
 	float* f = frame + 4 * (size_t)hit[i].idx;
 	for (int k = 0; k < 4; ++k) f[k] = c[k] + f[k] * (1.0f - c[3]);
 }
@@ -1745,7 +1763,8 @@ __global__ void k_render_accumulate(uint32_t n4, float w, const float* __restric
 }
 
 void render_frame(const RenderArgs& a, uint32_t spp, RenderWorkspace& ws, const std::function<void(uint32_t, const float*, f16*)>& infer,
-                  float* out, hipStream_t s) {
+                  float* out, hipStream_t s, const std::function<void(uint32_t, float*)>& grad) {
+	NGP_CHECK(a.render_mode == RENDER_SHADE || (a.render_mode == RENDER_NORMALS && grad), "render: Shade and Normals are implemented");
 	const uint32_t n_px = a.width * a.height;
 	if (n_px == 0) return;
 	const uint32_t MARCH_ITER = 10000, MIN_STEPS = 1, MAX_STEPS = 8, TARGET_QUERIES = 2 * 1024 * 1024;
@@ -1779,12 +1798,13 @@ void render_frame(const RenderArgs& a, uint32_t spp, RenderWorkspace& ws, const 
 			NGP_HIP(hipGetLastError());
 			const uint32_t n_el = next_multiple(n_alive * n_steps, 256);
 			infer(n_el, ws.coords, ws.out);
+			if (a.render_mode == RENDER_NORMALS) grad(n_el, ws.coords);
 			k_render_composite<<<div_round_up(n_alive, 128), 128, 0, s>>>(r, n_alive, n_el, it, n_steps, dst, dst_c, ws.coords, ws.out);
 			NGP_HIP(hipGetLastError());
 			it += n_steps;
 		}
 		const uint32_t n_hit = ws.host_counters[1];
-		if (n_hit) k_render_shade<<<div_round_up(n_hit, 256), 256, 0, s>>>(n_hit, a.linear_colors, hit, ws.rgba_hit, ws.frame);
+		if (n_hit) k_render_shade<<<div_round_up(n_hit, 256), 256, 0, s>>>(n_hit, a.linear_colors, a.render_mode, hit, ws.rgba_hit, ws.frame);
 		k_render_accumulate<<<div_round_up(4 * n_px, 256), 256, 0, s>>>(4 * n_px, 1.0f / (float)spp, ws.frame, out, sidx == 0);
 		NGP_HIP(hipGetLastError());
 	}

@@ -83,6 +83,7 @@ extern "C" const char* ngp_last_error(void);
 struct ngp_nerf_renderer {
 	Buf pay0, pay1, payh, rgba0, rgba1, rgbah, coords, out, frame, counters;
 	uint32_t* host_counters = nullptr;
+	uint32_t render_mode = RENDER_SHADE;  // ngp_nerf_renderer_set_mode
 	~ngp_nerf_renderer() { if (host_counters) (void)hipHostFree(host_counters); }
 };
 
@@ -413,6 +414,11 @@ int ngp_nerf_renderer_create(ngp_nerf_renderer** out) {
 	NERF_TRY({ *out = new ngp_nerf_renderer(); });
 }
 void ngp_nerf_renderer_destroy(ngp_nerf_renderer* r) { delete r; }
+int ngp_nerf_renderer_set_mode(ngp_nerf_renderer* r, int render_mode) {
+	if (!r || (render_mode != RENDER_SHADE && render_mode != RENDER_NORMALS)) return NGP_INVALID;
+	r->render_mode = (uint32_t)render_mode;
+	return NGP_OK;
+}
 
 int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_config* cfg, void* stream, const ngp_nerf_image* camera,
                     const uint8_t* bitfield, uint32_t spp, uint32_t sample_index, float min_transmittance, const float* background_rgba,
@@ -458,10 +464,15 @@ int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_confi
 		ws.counters = r->counters.get<uint32_t>(2);
 		if (!r->host_counters) NGP_HIP(hipHostMalloc(&r->host_counters, 16));
 		ws.host_counters = r->host_counters;
+		a.render_mode = r->render_mode;
 		auto infer = [&](uint32_t n, const float* coords, f16* out) {
 			check_rc(ngp_inference(model, s, n, coords, 7, out, n, NGP_LAYOUT_SOA, use_inference_params));
 		};
-		render_frame(a, spp, ws, infer, out_rgba, s);
+		// Normals: tcnn input_gradient's default backprop_scale (128); it reads the inference parameters
+		auto grad = [&](uint32_t n, float* coords) {
+			check_rc(ngp_input_gradient(model, s, 3, n, coords, 7, coords, 7, 128.0f));
+		};
+		render_frame(a, spp, ws, infer, out_rgba, s, grad);
 	});
 }
 

@@ -472,9 +472,11 @@ public:
 		if (!m_model) throw std::runtime_error("render: no network (train or load a snapshot first)");
 		std::vector<float> out((size_t)width * height * 4);
 		if (m_testbed_mode == ETestbedMode::Nerf) {
-			if (m_render_mode != ERenderMode::Shade) throw std::runtime_error("render: only ERenderMode::Shade is implemented");
+			if (m_render_mode != ERenderMode::Shade && m_render_mode != ERenderMode::Normals)
+				throw std::runtime_error("render: ERenderMode Shade and Normals are implemented");
 			require_nerf_trainer("render");
 			if (!m_renderer) check(ngp_nerf_renderer_create(&m_renderer), "ngp_nerf_renderer_create");
+			check(ngp_nerf_renderer_set_mode(m_renderer, (int)m_render_mode), "ngp_nerf_renderer_set_mode");
 			ngp_nerf_image cam{};
 			cam.width = width;
 			cam.height = height;

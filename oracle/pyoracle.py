@@ -594,3 +594,46 @@ def nerf_render(cfg, cam, model, params16, bitfield, sample_index=0, min_transmi
     lib().orc_nerf_render_composite(C.byref(cfg), W * H, max_per_ray, ptr(coords), ptr(counts), ptr(out16),
                                     min_transmittance, ptr(bgv), ptr(frame))
     return frame.reshape(H, W, 4), counts
+
+
+def nerf_render_normals(cfg, cam, model, params16, bitfield, sample_index=0, min_transmittance=0.01, bg=(0, 0, 0, 0),
+                        max_per_ray=1024):
+    """ERenderMode::Normals restated (testbed_nerf.cu:2615-2617 input_gradient(3, positions) with backprop scale
+    128; composite :1183-1188 normal = normalize(-density'(raw) * d raw / d position); shade :2179-2181
+    (0.5 n + 0.5) * alpha, composited over bg). The same march as nerf_render. Linear rgba [H, W, 4], counts."""
+    W, H = cam.width, cam.height
+    coords = np.zeros((W * H, max_per_ray, 7), np.float32)
+    counts = np.zeros(W * H, np.int32)
+    bfp = ptr(bitfield) if bitfield is not None else None
+    lib().orc_nerf_render_march(C.byref(cfg), C.byref(cam), bfp, sample_index, max_per_ray, ptr(coords), ptr(counts))
+    mask = np.arange(max_per_ray)[None, :] < counts[:, None]
+    raw = np.zeros((W * H, max_per_ray), np.float32)
+    grad = np.zeros((W * H, max_per_ray, 3), np.float32)
+    if mask.any():
+        c = np.ascontiguousarray(coords[mask])
+        raw[mask] = f16_bits_to_f32(f32_to_f16_bits(nerf_forward(model, params16, c)[:, 3]))
+        dL = np.zeros((c.shape[0], 16), np.float32)
+        dL[:, 3] = 128.0
+        grad[mask] = nerf_input_grad(model, params16, c, dL, scale=1.0 / 128.0)["dinput"][:, :3]
+    act = cfg.density_activation
+    dens = {0: lambda v: v, 1: lambda v: np.maximum(v, 0), 2: lambda v: 1 / (1 + np.exp(-v)), 3: np.exp}[act]
+    ddens = {0: lambda v: np.ones_like(v), 1: lambda v: (v > 0).astype(np.float32),
+             2: lambda v: (1 / (1 + np.exp(-v))) * (1 - 1 / (1 + np.exp(-v))), 3: lambda v: np.exp(np.clip(v, -15, 15))}[act]
+    min_step = np.sqrt(3.0) / 1024
+    frame = np.tile(np.asarray(bg, np.float64), (W * H, 1))
+    for i in range(W * H):
+        rgba = np.zeros(4)
+        for k in range(counts[i]):
+            dt = coords[i, k, 3] * (min_step * (1 << 7) - min_step) + min_step
+            w = (1.0 - np.exp(-dens(np.float64(raw[i, k])) * dt)) * (1.0 - rgba[3])
+            nrm = -ddens(np.float64(raw[i, k])) * grad[i, k].astype(np.float64)
+            rgba[:3] += nrm / np.linalg.norm(nrm) * w
+            rgba[3] += w
+            if rgba[3] > 1.0 - min_transmittance:
+                rgba /= rgba[3]
+                break
+        if rgba[3] > 0.001:  # the tracer's hit list (compact_kernel_nerf)
+            n = rgba[:3] / np.linalg.norm(rgba[:3])
+            rgba[:3] = (0.5 * n + 0.5) * rgba[3]
+            frame[i] = rgba + frame[i] * (1.0 - rgba[3])
+    return frame.reshape(H, W, 4).astype(np.float32), counts

@@ -76,6 +76,31 @@ def test_render_with_lens_matches_oracle(pkg, orc, mode, k):
     assert d.mean() < 2e-3, d.mean()
 
 
+@pytest.mark.parametrize("seed,frac", [(3, 1.0), (8, 0.3)])
+def test_render_normals_matches_oracle(pkg, orc, seed, frac):
+    """ERenderMode::Normals (testbed_nerf.cu:1183-1188, 2179-2181, 2615-2617): per step the density output's
+    input gradient (ngp_input_gradient, backprop scale 128) composited as normalize(-density'(raw) * gradient),
+    shaded (0.5 n + 0.5) * alpha. The gradient goes through fp16 intermediates whose fp32 sums are ordered
+    differently from the oracle's and each step's normal is normalised, so a step whose gradient nearly
+    vanishes can turn: pixels are compared within 2e-2, 98 % of them, mean 5e-3."""
+    cam, cfg, net, p16, bf, m = _setup(pkg, orc, seed, frac)
+    r = pkg.nerf.NerfRenderer()
+    bg = (0.1, 0.2, 0.3, 1.0)
+    img = r.render(net, cfg, cam, torch.from_numpy(bf).cuda(), spp=1, min_transmittance=1e-4, background=bg,
+                   use_inference_params=False, render_mode="Normals").cpu().numpy()
+    ref, counts = orc.nerf_render_normals(cfg, cam, m, p16, bf, min_transmittance=1e-4, bg=bg)
+    assert (counts > 0).mean() > 0.2
+    assert np.isfinite(img).all()
+    d = np.abs(img - ref).max(axis=2)
+    assert (d < 2e-2).mean() > 0.98, (d < 2e-2).mean()
+    assert d.mean() < 5e-3, d.mean()
+    # a Shade render with the same renderer afterwards is unaffected by the mode switch
+    shade = r.render(net, cfg, cam, torch.from_numpy(bf).cuda(), spp=1, min_transmittance=1e-4, background=bg,
+                     use_inference_params=False).cpu().numpy()
+    ref_s, _ = orc.nerf_render(cfg, cam, m, p16, bf, min_transmittance=1e-4, bg=bg)
+    assert np.abs(shade - ref_s).max() < 2e-2
+
+
 def test_render_spp_average_and_background(pkg, orc):
     cam, cfg, net, p16, bf, m = _setup(pkg, orc, 2, 0.0)  # empty grid: every ray misses -> background
     r = pkg.nerf.NerfRenderer()

@@ -33,21 +33,23 @@ def main():
     lib = pkg._capi.lib()
     f = lib.ngp_debug_t16_clock
     f.argtypes = [C.c_void_p, C.c_uint32]
-    buf = np.zeros(1024 * 32, np.uint64)
+    S = 128
+    buf = np.zeros(1024 * S, np.uint64)
     assert f(buf.ctypes.data, buf.size) == 0
-    t = buf.reshape(1024, 32).astype(np.int64)
+    t = buf.reshape(1024, S).astype(np.int64)
     blocks = int((t[:, 0] > 0).sum())
     t = t[:blocks]
     t0 = t[:, 0:1]
     rel = (t - t0) * 0.01  # 100 MHz ticks -> us
     names = {0: "entry", 1: "staged", 2: "loop"}
-    for i in range(3, 31):
-        names[i] = f"it{(i - 3) // 3}.{['fwd', 'bwd', 'dW'][(i - 3) % 3]}"
-    names[31] = "exit"
+    ks = ["inputs", "d0", "dout_sh", "r0", "rh", "img", "bwd_rgb", "bwd_density", "denc", "sync1", "dW", "sync2"]
+    for i in range(3, S - 1):
+        names[i] = f"it{(i - 3) // 12}.{ks[(i - 3) % 12]}"
+    names[S - 1] = "exit"
     out = {"blocks": blocks, "n": n}
     prev = 0.0
     phases = {}
-    for i in range(32):
+    for i in range(S):
         col = t[:, i]
         ok = col >= t0[:, 0]
         if i > 0 and (col == 0).all():
@@ -57,7 +59,7 @@ def main():
         prev = m
     out["phases"] = phases
     start = (t[:, 0] - t[:, 0].min()) * 0.01
-    end = (t[:, 31] - t[:, 0].min()) * 0.01
+    end = (t[:, S - 1] - t[:, 0].min()) * 0.01
     out["entry_spread_us"] = [round(float(np.percentile(start, q)), 3) for q in (0, 50, 100)]
     out["exit_spread_us"] = [round(float(np.percentile(end, q)), 3) for q in (0, 50, 100)]
     print(json.dumps(out, indent=1))
