@@ -98,7 +98,7 @@ int ngp_model_initialize_params(const ngp_model* m, uint64_t seed, float* params
 int ngp_model_set_max_level(ngp_model* m, float max_level, const float* max_level_per_sample);
 /* engine knobs: "grid_backward_mode" = 0 auto, 1 direct packed-f16 atomics (tcnn-style),
  * 3 destination-bucketed exact sums (auto picks 3 for n >= 4096); "grid_bricks" (bucketed backward: dense
- * levels summed per brick where that moves fewer bytes, default 1); "fuse_infer", "fuse_train",
+ * levels summed per brick where that moves fewer bytes, default 0); "fuse_infer", "fuse_train",
  * "fused_hist", "overlap", "grid_forward_mode"  */
 int ngp_model_set_option(ngp_model* m, const char* key, double value);
 /* engine state for tests and tools: "grid_brick_levels" = dense levels the bucketed backward sums per brick

@@ -616,15 +616,21 @@ __device__ void accumulate_brick(const GridConst& c, const BrickConst& bk, const
 		}
 		float frac[3]; uint32_t base[3];
 		level_setup<3>(c, l, x, frac, base);
-		const uint32_t W = bk.W[l];
+		const uint32_t W = bk.W[l], res = c.resolution[l];
 		uint32_t r0[3];
+		bool lo_in[3], hi_in[3];  // corner coordinate base + bit in 0..res (what the finalize's preimages cover)
 #pragma unroll
-		for (uint32_t d = 0; d < 3; ++d) r0[d] = base[d] - bk.lo[l][b3[d]];
+		for (uint32_t d = 0; d < 3; ++d) {
+			r0[d] = base[d] - bk.lo[l][b3[d]];
+			lo_in[d] = base[d] <= res;
+			hi_in[d] = base[d] + 1u <= res;
+		}
 #pragma unroll
 		for (uint32_t k = 0; k < 8; ++k) {
 			const uint32_t rx = r0[0] + (k & 1u), ry = r0[1] + ((k >> 1) & 1u), rz = r0[2] + ((k >> 2) & 1u);
 			const float wk = corner_weight<3>(frac, k);
-			const bool in = rx < W && ry < W && rz < W;
+			const bool in = rx < W && ry < W && rz < W && ((k & 1u) ? hi_in[0] : lo_in[0]) && ((k & 2u) ? hi_in[1] : lo_in[1]) &&
+			                ((k & 4u) ? hi_in[2] : lo_in[2]);
 			const uint32_t local = bk.regoff[l] + rx + W * (ry + W * rz);
 #pragma unroll
 			for (uint32_t q = 0; q < F; ++q) {
@@ -647,21 +653,22 @@ __device__ void accumulate_brick(const GridConst& c, const BrickConst& bk, const
 	for (uint32_t k = threadIdx.x; k < bk.R * F; k += blockDim.x) dst[(k / bk.R) * NE + k % bk.R] = acc[(k / bk.R) * RP + k % bk.R];
 }
 
-// Sum of one brick-level entry's feature f: the slabs of every part of every brick whose region holds a
+// Sums of one brick-level entry's F features: the slabs of every part of every brick whose region holds a
 // corner that indexes it, plus the fallback table (then cleared; read only when the flag is set). A dense
 // level's corner coordinates run 0..res (a cell's upper corner at coordinate res is tcnn's index
 // x + res (y + res z) unclamped, modulo T = res^3), so entry (x, y, z) is also the corner (x + res, y - 1, z)
 // when x = 0, and so on with the borrow through y and z: at most 2 candidates per coordinate.
-__device__ __forceinline__ unsigned long long brick_entry_sum(const GridConst& c, const BrickConst& bk, uint32_t e, uint32_t f, uint32_t F,
-                                                              uint32_t NE, const uint32_t* __restrict__ bp,
-                                                              const unsigned long long* __restrict__ scratch, const BrickFallback& fb,
-                                                              bool fb_used) {
+template <uint32_t F>
+__device__ __forceinline__ void brick_entry_sums(const GridConst& c, const BrickConst& bk, uint32_t e, uint32_t NE,
+                                                 const uint32_t* __restrict__ bp, const unsigned long long* __restrict__ scratch,
+                                                 const BrickFallback& fb, bool fb_used, unsigned long long (&q)[F]) {
+#pragma unroll
+	for (uint32_t f = 0; f < F; ++f) q[f] = 0ull;
 	uint32_t l = 0;
 	while (c.offsets[l + 1] <= e) ++l;
 	const int res = (int)c.resolution[l], idx = (int)(e - c.offsets[l]);
 	const int cc[3] = {idx % res, (idx / res) % res, idx / (res * res)};
 	const uint32_t W = bk.W[l];
-	unsigned long long q = 0;
 	// bricks whose region holds coordinate v along one dimension: lo <= v < lo + W, a contiguous range
 	auto range = [&](int v, uint32_t& b0, uint32_t& b1) {
 		b0 = bk.NB; b1 = 0;
@@ -698,17 +705,23 @@ __device__ __forceinline__ unsigned long long brick_entry_sum(const GridConst& c
 							const uint32_t first = bp[2 * b], parts = bp[2 * b + 1];
 							const uint32_t local = bk.regoff[l] + (uint32_t)(v3[0] - bk.lo[l][bx]) +
 							                       W * ((uint32_t)(v3[1] - bk.lo[l][by]) + W * (uint32_t)(v3[2] - bk.lo[l][bz]));
-							for (uint32_t p = 0; p < parts; ++p) q += scratch[(size_t)(first + p) * NE * F + (size_t)f * NE + local];
+							for (uint32_t p = 0; p < parts; ++p) {
+								const unsigned long long* src = scratch + (size_t)(first + p) * NE * F + local;
+#pragma unroll
+								for (uint32_t f = 0; f < F; ++f) q[f] += src[(size_t)f * NE];
+							}
 						}
 			}
 		}
 	}
 	if (fb_used) {
-		unsigned long long* src = fb.fix + (size_t)e * F + f;
-		const unsigned long long v = *src;
-		if (v) { q += v; *src = 0ull; }
+		unsigned long long* src = fb.fix + (size_t)e * F;
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) {
+			const unsigned long long v = src[f];
+			if (v) { q[f] += v; src[f] = 0ull; }
+		}
 	}
-	return q;
 }
 
 // bucket vb -> (first entry, entries)
@@ -843,8 +856,9 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 // and write every entry once — no fp16 atomics, bitwise reproducible. Columns x >= slab_x0 of the grid
 // run the MLP's dW slab reduction (SlabJob) instead: this kernel leaves most of the chip idle, so the
 // reduction fits beside it.
-// Columns [fin_x0, gridDim.x) finalize the brick levels: one parameter pair per thread (pair k = entry
-// features 2k, 2k + 1 of the grid's leading entries), summed over the bricks' slabs (brick_entry_sum).
+// Columns [fin_x0, gridDim.x) finalize the brick levels: one entry per thread (two for F = 1), every feature
+// summed over the bricks' slabs in one pass over the geometry (brick_entry_sums), written as parameter pairs
+// (pair k = features 2k, 2k + 1 of the grid's leading entries).
 template <uint32_t F, bool FUSED>
 __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst c, const Levels lv, uint32_t B,
                                                                 const uint32_t* __restrict__ split, const uint32_t* __restrict__ splitb,
@@ -854,31 +868,36 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
                                                                 uint32_t fin_x0) {
 	static_assert(SC_THREADS == SLAB_THREADS, "slab blocks share the split-reduce block shape");
 	if (blockIdx.x >= fin_x0) {
+		constexpr uint32_t EPT = F == 1 ? 2 : 1;  // entries per thread: whole parameter pairs
 		const uint32_t blk = blockIdx.y * (gridDim.x - fin_x0) + (blockIdx.x - fin_x0);
-		const uint32_t k = blk * blockDim.x + threadIdx.x;
-		if (k >= c.offsets[bk.LD] * F / 2) return;
+		const uint32_t e0 = (blk * blockDim.x + threadIdx.x) * EPT;
+		if (e0 >= c.offsets[bk.LD]) return;
 		const uint32_t NE = 1u << B;
 		const bool used = *fb.flag != 0u;
-		unsigned long long q0, q1;
-		if constexpr (F == 1) {
-			q0 = brick_entry_sum(c, bk, 2 * k, 0, F, NE, bp, scratch, fb, used);
-			q1 = brick_entry_sum(c, bk, 2 * k + 1, 0, F, NE, bp, scratch, fb, used);
-		} else {
-			const uint32_t e = k / (F / 2), fp = k % (F / 2);
-			q0 = brick_entry_sum(c, bk, e, 2 * fp, F, NE, bp, scratch, fb, used);
-			q1 = brick_entry_sum(c, bk, e, 2 * fp + 1, F, NE, bp, scratch, fb, used);
+		float s[EPT * F];
+#pragma unroll
+		for (uint32_t u = 0; u < EPT; ++u) {
+			unsigned long long q[F];
+			brick_entry_sums<F>(c, bk, e0 + u, NE, bp, scratch, fb, used, q);
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) s[u * F + f] = fix_to_f32(q[f]);
 		}
-		float s0 = fix_to_f32(q0), s1 = fix_to_f32(q1);
-		if (FUSED) {
-			fused_adam_pair(fa, k, (f16)s0, (f16)s1);
-			return;
+		// pairs (e0 F) / 2 .. of the grid (brick levels start at entry 0)
+#pragma unroll
+		for (uint32_t h = 0; h < EPT * F / 2; ++h) {
+			const uint32_t k = e0 * F / 2 + h;
+			float s0 = s[2 * h], s1 = s[2 * h + 1];
+			if (FUSED) {
+				fused_adam_pair(fa, k, (f16)s0, (f16)s1);
+				continue;
+			}
+			if (!overwrite) {
+				const f16x2 o = ((const f16x2*)grad)[k];
+				s0 += (float)o[0];
+				s1 += (float)o[1];
+			}
+			((f16x2*)grad)[k] = f16x2{(f16)s0, (f16)s1};
 		}
-		if (!overwrite) {
-			const f16x2 o = ((const f16x2*)grad)[k];
-			s0 += (float)o[0];
-			s1 += (float)o[1];
-		}
-		((f16x2*)grad)[k] = f16x2{(f16)s0, (f16)s1};
 		return;
 	}
 	if (blockIdx.x >= slab_x0) {
@@ -972,8 +991,8 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		const uint32_t gy = (uint32_t)div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS);
 		const SlabJob sj = slab ? *slab : SlabJob{};
 		const uint32_t slab_x = slab ? (uint32_t)div_round_up(slab_blocks(sj.n), gy) : 0u;
-		const size_t fin_pairs = (size_t)c.offsets[p.bk.LD] * c.n_features / 2;
-		const uint32_t fin_x = (uint32_t)div_round_up(div_round_up(fin_pairs, SC_THREADS), gy);
+		const size_t fin_threads = c.n_features == 1 ? div_round_up(c.offsets[p.bk.LD], 2) : (size_t)c.offsets[p.bk.LD];
+		const uint32_t fin_x = (uint32_t)div_round_up(div_round_up(fin_threads, SC_THREADS), gy);
 		const dim3 grid_r(p.max_split_buckets + slab_x + fin_x, gy);
 		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets, fa, p.bk, bp, fb,
 		                                     p.max_split_buckets + slab_x);

@@ -345,11 +345,48 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
 	for (int q = 0; q < NT; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+	// phase B operands of one pair image: waves 0-3 per hidden layer {dZ rows 16 wave, inputs n = 0..3} (rgb
+	// layers RH-1..1, then density DH-1..1), then {dZ density layer 0, encoding n = 0..ES-1}; waves 4-7 {dZ rgb
+	// output, rgb last hidden v, dZ rgb layer 0 rows 16 v, [density out | SH] 0, 16, dZ density output,
+	// density last hidden v}
+	constexpr int NOPS_A = 5 * ((RH - 1) + (DH - 1)) + 1 + ES;
+	constexpr int NOPS = NOPS_A > 7 ? NOPS_A : 7;
+	auto load_ops = [&](int p, f16x8 (&o)[NOPS]) {
+		const f16* im = imgs + p * T::IMG_HALVES;
+		if (wave < 4) {
+			int k = 0;
+#pragma unroll
+			for (int j = 0; j < RH - 1; ++j, k += 5) {
+				o[k] = img_frag(im + T::I_ZRH + j * 32 * T::S_64, T::S_64, 16 * wave, lane);
+#pragma unroll
+				for (int n = 0; n < 4; ++n) o[k + 1 + n] = img_frag(im + T::I_HR + (RH - 2 - j) * 32 * T::S_64, T::S_64, 16 * n, lane);
+			}
+#pragma unroll
+			for (int j = 0; j < DH - 1; ++j, k += 5) {
+				o[k] = img_frag(im + T::I_ZDH + j * 32 * T::S_64, T::S_64, 16 * wave, lane);
+#pragma unroll
+				for (int n = 0; n < 4; ++n) o[k + 1 + n] = img_frag(im + T::I_HD + (DH - 2 - j) * 32 * T::S_64, T::S_64, 16 * n, lane);
+			}
+			o[k] = img_frag(im + T::I_ZD0, T::S_64, 16 * wave, lane);
+#pragma unroll
+			for (int n = 0; n < ES; ++n) o[k + 1 + n] = img_frag(im + T::I_XE, T::S_XE, 16 * n, lane);
+		} else {
+			const int v = wave - 4;
+			o[0] = img_frag(im + T::I_ZRO, T::S_16, 0, lane);
+			o[1] = img_frag(im + T::I_HR + (RH - 1) * 32 * T::S_64, T::S_64, 16 * v, lane);
+			o[2] = img_frag(im + T::I_ZR0, T::S_64, 16 * v, lane);
+			o[3] = img_frag(im + T::I_RIN, T::S_RIN, 0, lane);
+			o[4] = img_frag(im + T::I_RIN, T::S_RIN, 16, lane);
+			o[5] = img_frag(im + T::I_ZDO, T::S_16, 0, lane);
+			o[6] = img_frag(im + T::I_HD + (DH - 1) * 32 * T::S_64, T::S_64, 16 * v, lane);
+		}
+	};
+
 	const uint32_t n_tiles = (a.n + 31) / 32;
-	// inputs of this lane's sample, prefetched PF iterations ahead: at one iteration the loop waited on their
-	// HBM latency (phase costs in DESIGN §6)
+	// inputs of this lane's sample, prefetched PF iterations ahead (one: a deeper ring measured no faster and
+	// its registers are needed by phase B's double buffer)
 #ifndef NGP_T16_PF
-#define NGP_T16_PF 2
+#define NGP_T16_PF 1
 #endif
 	constexpr int PF = NGP_T16_PF;
 	struct In {
@@ -445,6 +482,19 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 				for (int j = 0; j < 4; ++j) a.out[(size_t)(4 * g + j) * a.out_stride + sample] = ro[j];
 			}
 		}
+		// the backward chain's weight fragments, requested before the image writes (a wave's LDS requests are
+		// served in order: reads queued behind the writes wait for them) and a layer or more ahead of their
+		// MFMAs; the scheduling barrier keeps the compiler from sinking them next to their uses, where each
+		// MFMA waited out an LDS round trip (phase clock)
+		f16x4 b_ro[4], b_do[4];
+		f16x8 b_rh[RH > 1 ? 8 : 1], b_r0[2];
+#pragma unroll
+		for (int t = 0; t < 4; ++t) b_ro[t] = *(const f16x4*)(wl + T::B_RO + (t * 64 + lane) * 4);
+		if constexpr (RH > 1) {
+#pragma unroll
+			for (int f = 0; f < 8; ++f) b_rh[f] = *(const f16x8*)(wl + T::B_RH + (f * 64 + lane) * 8);
+		}
+		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (int l = 0; l < DH; ++l) img_put64(img + T::I_HD + l * 32 * T::S_64 + r * T::S_64, g, hd[l]);
 		img_put4(img + T::I_RIN + r * T::S_RIN, 0, g, dout);
@@ -459,9 +509,16 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		const f16x4 dz1 = g == 0 ? f16x4{dl_cur[0], dl_cur[1], dl_cur[2], (f16)0.f} : f16x4{};  // extract_rgb (:46-60)
 		img_put4(img + T::I_ZRO + r * T::S_16, 0, g, dz1);
 #pragma unroll
-		for (int t = 0; t < 4; ++t) acc[t] = mma16(*(const f16x4*)(wl + T::B_RO + (t * 64 + lane) * 4), dz1, f32x4{0.f, 0.f, 0.f, 0.f});
+		for (int t = 0; t < 4; ++t) acc[t] = mma16(b_ro[t], dz1, f32x4{0.f, 0.f, 0.f, 0.f});
 		f16x8 dz[2];
 		mask64(acc, hr[RH - 1], dz);
+		// the density layer 0 fragments of dL/denc, a chain ahead
+		f16x8 b_d0[2 * ES];
+#pragma unroll
+		for (int f = 0; f < 2; ++f) b_r0[f] = *(const f16x8*)(wl + T::B_R0 + (f * 64 + lane) * 8);
+#pragma unroll
+		for (int t = 0; t < 4; ++t) b_do[t] = *(const f16x4*)(wl + T::B_DO + (t * 64 + lane) * 4);
+		__builtin_amdgcn_sched_barrier(0);
 #pragma unroll
 		for (int l = RH - 1; l >= 1; --l) {
 			const int j = RH - 1 - l;
@@ -469,16 +526,18 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			const f16* wb = wl + T::B_RH + j * 8 * 64 * 8;
 #pragma unroll
 			for (int t = 0; t < 4; ++t) {
-				f32x4 c = mma32(*(const f16x8*)(wb + ((2 * t) * 64 + lane) * 8), dz[0], f32x4{0.f, 0.f, 0.f, 0.f});
-				acc[t] = mma32(*(const f16x8*)(wb + ((2 * t + 1) * 64 + lane) * 8), dz[1], c);
+				// layer RH-1's fragments were requested with the forward's image writes
+				const f16x8 w0 = j == 0 ? b_rh[2 * t] : *(const f16x8*)(wb + ((2 * t) * 64 + lane) * 8);
+				const f16x8 w1 = j == 0 ? b_rh[2 * t + 1] : *(const f16x8*)(wb + ((2 * t + 1) * 64 + lane) * 8);
+				f32x4 c = mma32(w0, dz[0], f32x4{0.f, 0.f, 0.f, 0.f});
+				acc[t] = mma32(w1, dz[1], c);
 			}
 			mask64(acc, hr[l - 1], dz);
 		}
 		img_put64(img + T::I_ZR0 + r * T::S_64, g, dz);
 		T16_IT(6);
 		// dL/d(rgb input): tile 0 = the density output rows, tile 1 = the SH rows (input gradients only)
-		f32x4 dd_acc = mma32(*(const f16x8*)(wl + T::B_R0 + (1 * 64 + lane) * 8), dz[1],
-		                     mma32(*(const f16x8*)(wl + T::B_R0 + (0 * 64 + lane) * 8), dz[0], f32x4{0.f, 0.f, 0.f, 0.f}));
+		f32x4 dd_acc = mma32(b_r0[1], dz[1], mma32(b_r0[0], dz[0], f32x4{0.f, 0.f, 0.f, 0.f}));
 		f16x4 dd = pack4(dd_acc, false);
 		if (g == 0) dd[0] = (f16)((float)dd[0] + dsig);  // add_density_gradient (:63-74)
 		// MFMAs take operands from every lane whatever EXEC says: only wave-uniform branches around them, the
@@ -488,9 +547,12 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			                         mma32(*(const f16x8*)(wl + T::B_R0 + (2 * 64 + lane) * 8), dz[0], f32x4{0.f, 0.f, 0.f, 0.f}));
 			if (valid) *(f16x4*)(a.dL_dsh + (size_t)sample * 16 + 4 * g) = pack4(sacc, false);
 		}
+#pragma unroll
+		for (int f = 0; f < 2 * ES; ++f) b_d0[f] = *(const f16x8*)(wl + T::B_D0 + (f * 64 + lane) * 8);
+		__builtin_amdgcn_sched_barrier(0);
 		img_put4(img + T::I_ZDO + r * T::S_16, 0, g, dd);
 #pragma unroll
-		for (int t = 0; t < 4; ++t) acc[t] = mma16(*(const f16x4*)(wl + T::B_DO + (t * 64 + lane) * 4), dd, f32x4{0.f, 0.f, 0.f, 0.f});
+		for (int t = 0; t < 4; ++t) acc[t] = mma16(b_do[t], dd, f32x4{0.f, 0.f, 0.f, 0.f});
 		mask64(acc, hd[DH - 1], dz);
 #pragma unroll
 		for (int l = DH - 1; l >= 1; --l) {
@@ -509,8 +571,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		if (a.dL_denc) {
 #pragma unroll
 			for (int t = 0; t < ES; ++t) {
-				const f32x4 e = mma32(*(const f16x8*)(wl + T::B_D0 + ((2 * t + 1) * 64 + lane) * 8), dz[1],
-				                      mma32(*(const f16x8*)(wl + T::B_D0 + ((2 * t) * 64 + lane) * 8), dz[0], f32x4{0.f, 0.f, 0.f, 0.f}));
+				const f32x4 e = mma32(b_d0[2 * t + 1], dz[1], mma32(b_d0[2 * t], dz[0], f32x4{0.f, 0.f, 0.f, 0.f}));
 				if (valid) *(f16x4*)(a.dL_denc + (size_t)sample * a.denc_stride + 16 * t + 4 * g) = pack4(e, false);
 			}
 		}
@@ -521,37 +582,26 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 
 		// ---- dW over the four pair images (K = 32 samples per MFMA), images in a fixed order ---------
 #ifndef NGP_T16_SKIP_B
+		// operands of image p + 1 requested before image p's MFMAs (two register buffers)
+		f16x8 ops[2][NOPS];
+		load_ops(0, ops[0]);
 #pragma unroll
 		for (int p = 0; p < 4; ++p) {
-			const f16* im = imgs + p * T::IMG_HALVES;
+			if (p < 3) load_ops(p + 1, ops[(p + 1) & 1]);
+			const f16x8(&o)[NOPS] = ops[p & 1];
 			if (wave < 4) {
-				int q = 0;
+				int q = 0, k = 0;
 #pragma unroll
-				for (int j = 0; j < RH - 1; ++j) {  // rgb hidden layer RH-1-j: dZ rows 16*wave.., inputs HR[RH-2-j]
-					const f16x8 am = img_frag(im + T::I_ZRH + j * 32 * T::S_64, T::S_64, 16 * wave, lane);
+				for (int j = 0; j < (RH - 1) + (DH - 1); ++j, k += 5)
 #pragma unroll
-					for (int n = 0; n < 4; ++n, ++q)
-						dw[q] = mma32(am, img_frag(im + T::I_HR + (RH - 2 - j) * 32 * T::S_64, T::S_64, 16 * n, lane), dw[q]);
-				}
+					for (int n = 0; n < 4; ++n, ++q) dw[q] = mma32(o[k], o[k + 1 + n], dw[q]);
 #pragma unroll
-				for (int j = 0; j < DH - 1; ++j) {
-					const f16x8 am = img_frag(im + T::I_ZDH + j * 32 * T::S_64, T::S_64, 16 * wave, lane);
-#pragma unroll
-					for (int n = 0; n < 4; ++n, ++q)
-						dw[q] = mma32(am, img_frag(im + T::I_HD + (DH - 2 - j) * 32 * T::S_64, T::S_64, 16 * n, lane), dw[q]);
-				}
-				const f16x8 d0 = img_frag(im + T::I_ZD0, T::S_64, 16 * wave, lane);
-#pragma unroll
-				for (int n = 0; n < ES; ++n, ++q) dw[q] = mma32(d0, img_frag(im + T::I_XE, T::S_XE, 16 * n, lane), dw[q]);
+				for (int n = 0; n < ES; ++n, ++q) dw[q] = mma32(o[k], o[k + 1 + n], dw[q]);
 			} else {
-				const int v = wave - 4;
-				dw[0] = mma32(img_frag(im + T::I_ZRO, T::S_16, 0, lane),
-				              img_frag(im + T::I_HR + (RH - 1) * 32 * T::S_64, T::S_64, 16 * v, lane), dw[0]);
-				const f16x8 a0 = img_frag(im + T::I_ZR0, T::S_64, 16 * v, lane);
-				dw[1] = mma32(a0, img_frag(im + T::I_RIN, T::S_RIN, 0, lane), dw[1]);
-				dw[2] = mma32(a0, img_frag(im + T::I_RIN, T::S_RIN, 16, lane), dw[2]);
-				dw[3] = mma32(img_frag(im + T::I_ZDO, T::S_16, 0, lane),
-				              img_frag(im + T::I_HD + (DH - 1) * 32 * T::S_64, T::S_64, 16 * v, lane), dw[3]);
+				dw[0] = mma32(o[0], o[1], dw[0]);
+				dw[1] = mma32(o[2], o[3], dw[1]);
+				dw[2] = mma32(o[2], o[4], dw[2]);
+				dw[3] = mma32(o[5], o[6], dw[3]);
 			}
 		}
 #endif
