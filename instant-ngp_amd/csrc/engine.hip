@@ -169,6 +169,7 @@ struct ngp_model {
 	bool fuse_slabs = true;                 // option "fuse_slabs": dW slab reduction inside the grid backward's last kernel
 	bool fuse_opt = true;                   // option "fuse_opt": lazy-layout optimizer update inside the grid backward (training_step)
 	bool mlp_train16 = true;                // option "mlp_train16": the training MLP at two waves per SIMD (mlp_train16.hip)
+	bool grid_stage0 = true;                // option "grid_stage0": the training forward stages level 0 in LDS (grid.hip STAGE0)
 	bool grid_bricks = false;               // option "grid_bricks": dense levels of the bucketed backward summed per brick (off: measured slower)
 	bool fuse_train = false;                // option "fuse_train": ... and the training forward_backward too (off: the
 	                                        // training kernel runs 1 wave/SIMD, the gathers are not hidden; C2 0.157 -> 0.161 ms)
@@ -318,6 +319,7 @@ struct ngp_model {
 		const bool xcd = grid_forward_mode == 2;  // auto = per-sample rows: measured faster (DESIGN.md §Grid forward)
 		const bool fuse = want_hist && fused_hist && use_sorted(n) && !sc_prepared && (xcd || grid_forward_rows_ok(grid, a)) &&
 		                  scatter_hist(grid, sc_plan_for(n), sorted_workspace(n), h);
+		h.stage0 = grid_stage0 ? 1u : 0u;
 		ProfScope ps("grid_forward", s);
 		grid_forward(grid, a, s, fuse ? &h : nullptr, xcd ? 2 : 1);
 		sc_hist_done = fuse;
@@ -746,6 +748,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			m->fuse_slabs = value != 0;
 		} else if (k == "fuse_opt") {
 			m->fuse_opt = value != 0;
+		} else if (k == "grid_stage0") {
+			m->grid_stage0 = value != 0;
 		} else if (k == "grid_bricks") {
 			m->grid_bricks = value != 0;
 			m->sc_plan_n = 0;  // re-plan at the next batch

@@ -59,6 +59,7 @@ struct GridHist {
 	uint32_t B, n_chunks, chunk;
 	uint32_t vb_base[33];
 	uint32_t brick_levels = 0, n_bricks = 0, brick_cells = 8, bricks_per_dim = 0;
+	uint32_t stage0 = 1;  // row kernel: level 0's table staged in LDS when dense and <= 32 KB
 };
 
 // mode: 0/1 per-sample kernels, 2 XCD-partitioned (level, chunk) kernel (L2-local tables; measured
@@ -274,6 +275,19 @@ __device__ __forceinline__ uint32_t brick_of(const GridConst& c, uint32_t f, uin
 		mul *= NB;
 	}
 	return id;
+}
+
+// Histogram add of one corner's bucket j (< 2^few_bits buckets in the level, few_bits <= 4): the lanes with
+// the same bucket are found with ballots and their leader adds their count once. C2's coarse levels have 2
+// and 16 buckets, so a plain per-lane LDS atomic serialised up to 64 lanes on one counter per corner.
+__device__ __forceinline__ void hist_add(uint32_t* h, uint32_t j, uint32_t few_bits) {
+	if (few_bits > 4) { atomicAdd(&h[j], 1u); return; }
+	uint64_t peers = __ballot(1);
+	for (uint32_t b = 0; b < few_bits; ++b) {
+		const uint64_t m = __ballot((j >> b) & 1u);
+		peers &= ((j >> b) & 1u) ? m : ~m;
+	}
+	if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)peers) - 1)) atomicAdd(&h[j], (uint32_t)__popcll(peers));
 }
 
 GridConst make_grid_const(const GridDesc& g);

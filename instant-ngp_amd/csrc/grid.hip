@@ -127,15 +127,25 @@ __global__ void __launch_bounds__(256) k_grid_forward(const GridConst c, const G
                            // F >= 4 only (C2 forward 28.9 -> 27.3 us; with 16 levels of F = 2 the index arrays cost
                            // registers: C2' step 350 -> 393 us, profiles/r03bp)
 #endif
-template <uint32_t D, uint32_t F, bool HIST>
+// STAGE0 (training forward, dense level 0 of at most 32 KB: C2's 4096 x 4 fp16): the block copies level
+// 0's table into LDS with coalesced 16-B loads and gathers its corners there, so 512 samples cost the L2 256
+// line requests instead of 2048 scattered corner-pair requests (the forward is bound by the L2's request
+// rate). Same values, same arithmetic: bit-identical.
+template <uint32_t D, uint32_t F, bool HIST, bool STAGE0 = false>
 __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const GridConst c, const GridFwdArgs a, const GridHist h) {
 	typedef typename FeatVec<F>::T V;
 	constexpr uint32_t MAXL = 32 / F;
-	extern __shared__ uint32_t hl[];  // HIST: [vb_base[L]] bucket counts of this chunk
+	extern __shared__ __attribute__((aligned(16))) uint32_t hl[];  // HIST: [vb_base[L]] bucket counts of this chunk
+	f16* t0 = nullptr;  // STAGE0: level 0's table, after the counts (16-B aligned)
 	if constexpr (HIST) {
 		for (uint32_t j = threadIdx.x; j < h.vb_base[c.n_levels]; j += blockDim.x) hl[j] = 0;
-		__syncthreads();
 	}
+	if constexpr (STAGE0) {
+		t0 = (f16*)(hl + ((h.vb_base[c.n_levels] + 3u) & ~3u));
+		const uint32_t n16 = c.offsets[1] * F / 8;  // 16-B chunks (level sizes are multiples of 8 entries)
+		for (uint32_t j = threadIdx.x; j < n16; j += blockDim.x) ((f16x8*)t0)[j] = ((const f16x8*)a.table)[j];
+	}
+	if constexpr (HIST || STAGE0) __syncthreads();
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i < a.n) {
 	float x[D];
@@ -153,13 +163,18 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 		for (uint32_t f = 0; f < F; ++f) acc[f] = 0.f;
 		const bool active = l < c.n_levels && !((float)l >= ml + 1e-3f);
 		const bool count = HIST && l >= h.brick_levels;  // brick levels: counted once per sample above
+		uint32_t few_bits = 32;
+		if constexpr (HIST) {
+			const uint32_t nvb = l < c.n_levels ? h.vb_base[l + 1] - h.vb_base[l] : 0u;
+			few_bits = nvb <= 1 ? 0u : nvb <= 2 ? 1u : nvb <= 4 ? 2u : nvb <= 8 ? 3u : nvb <= 16 ? 4u : 32u;
+		}
 		if (count && l < c.n_levels && !active) {
 			// the backward stages items for masked levels too (with zero values): count them
 			float frac[D]; uint32_t base[D];
 			level_setup<D>(c, l, x, frac, base);
 #pragma unroll
 			for (uint32_t k = 0; k < (1u << D); ++k)
-				atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
+				hist_add(hl + h.vb_base[l], (corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B, few_bits);
 		}
 		if (active) {
 			float frac[D]; uint32_t base[D];
@@ -170,16 +185,16 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 				corner_indices<D>(c, l, base, cidx);
 				if (count) {
 #pragma unroll
-					for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&hl[h.vb_base[l] + ((cidx[k] - c.offsets[l]) >> h.B)], 1u);
+					for (uint32_t k = 0; k < (1u << D); ++k) hist_add(hl + h.vb_base[l], (cidx[k] - c.offsets[l]) >> h.B, few_bits);
 				}
-				gather_corners_at<D, F>(cidx, a.table, v);
+				gather_corners_at<D, F>(cidx, (STAGE0 && l == 0) ? t0 : a.table, v);
 			} else {
 				if (count) {
 #pragma unroll
 					for (uint32_t k = 0; k < (1u << D); ++k)
-						atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
+						hist_add(hl + h.vb_base[l], (corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B, few_bits);
 				}
-				gather_corners<D, F>(c, l, base, a.table, v);
+				gather_corners<D, F>(c, l, base, (STAGE0 && l == 0) ? t0 : a.table, v);
 			}
 #pragma unroll
 			for (uint32_t k = 0; k < (1u << D); ++k) {
@@ -406,16 +421,24 @@ static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hip
 		NGP_CHECK(rows && h->chunk == 512, "grid forward histogram: needs the row kernel and 512-sample chunks");
 		const dim3 grid_h(div_round_up(a.n, 512));
 		NGP_CHECK(grid_h.x == h->n_chunks, "grid forward histogram: chunk count mismatch");
-		const size_t lds = (size_t)h->vb_base[c.n_levels] * 4;
-		auto go = [&](auto kern) {
-			ensure_dynamic_lds((const void*)kern, lds);
-			kern<<<grid_h, 512, lds, s>>>(c, a, *h);
+		// level 0 staged in LDS when dense and <= 32 KB (engine option grid_stage0, default on)
+		const size_t t0_bytes = (size_t)c.offsets[1] * F * 2;
+		const bool stage0 = h->stage0 && !(c.hashed & 1u) && t0_bytes <= 32 * 1024;
+		const size_t lds = (((size_t)h->vb_base[c.n_levels] + 3) & ~(size_t)3) * 4 + (stage0 ? t0_bytes : 0);
+		auto go = [&](auto kern, auto kern_s) {
+			if (stage0) {
+				ensure_dynamic_lds((const void*)kern_s, lds);
+				kern_s<<<grid_h, 512, lds, s>>>(c, a, *h);
+			} else {
+				ensure_dynamic_lds((const void*)kern, lds);
+				kern<<<grid_h, 512, lds, s>>>(c, a, *h);
+			}
 		};
 		switch (F) {
-			case 1: go(k_grid_forward_rows<D, 1, true>); return;
-			case 2: go(k_grid_forward_rows<D, 2, true>); return;
-			case 4: go(k_grid_forward_rows<D, 4, true>); return;
-			case 8: go(k_grid_forward_rows<D, 8, true>); return;
+			case 1: go(k_grid_forward_rows<D, 1, true>, k_grid_forward_rows<D, 1, true, true>); return;
+			case 2: go(k_grid_forward_rows<D, 2, true>, k_grid_forward_rows<D, 2, true, true>); return;
+			case 4: go(k_grid_forward_rows<D, 4, true>, k_grid_forward_rows<D, 4, true, true>); return;
+			case 8: go(k_grid_forward_rows<D, 8, true>, k_grid_forward_rows<D, 8, true, true>); return;
 			default: throw Error("GridEncoding: unsupported F");
 		}
 	}

@@ -171,6 +171,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 		return;
 	}
 	const uint32_t nvb = lv.vb_base[l + 1] - lv.vb_base[l];
+	const uint32_t few_bits = nvb <= 1 ? 0u : nvb <= 2 ? 1u : nvb <= 4 ? 2u : nvb <= 8 ? 3u : nvb <= 16 ? 4u : 32u;
 	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) h[j] = 0;
 	__syncthreads();
 	const uint32_t off_l = c.offsets[l];
@@ -185,7 +186,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 		uint32_t cidx[1u << D];
 		corner_indices<D>(c, l, base, cidx);
 #pragma unroll
-		for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&h[(cidx[k] - off_l) >> B], 1u);
+		for (uint32_t k = 0; k < (1u << D); ++k) hist_add(h, (cidx[k] - off_l) >> B, few_bits);
 	}
 	__syncthreads();
 	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) hist[(size_t)chunk * lv.vb_base[c.n_levels] + lv.vb_base[l] + j] = h[j];

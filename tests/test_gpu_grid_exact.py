@@ -47,8 +47,10 @@ def positions(kind, n, D, seed):
     return x
 
 
-def run_backward(pkg, D, L, F, T, x, dy16, grad_mode=None, init=None):
+def run_backward(pkg, D, L, F, T, x, dy16, grad_mode=None, init=None, bricks=None):
     net = pkg.NetworkWithInputEncoding(D, 1, enc_cfg(L, F, T), MLP2)
+    if bricks is not None:
+        net.set_option("grid_bricks", bricks)
     tr = pkg.Trainer(net, ADAM)
     nm = net.n_matrix_params
     if init is not None:
@@ -92,6 +94,27 @@ def test_grid_backward_bitexact_full_batch(pkg, orc, name, D, L, F, T, kind):
     detail = [(int(i), hex(got[i]), hex(ref[i])) for i in bad[:6]]
     assert bad.size == 0, f"{name}/{kind}: {bad.size} of {ref.size} gradient entries differ: {detail}"
     assert np.count_nonzero(ref) > 0
+
+
+@pytest.mark.parametrize("name,L,F,T,kind", [("C2", 4, 4, 19, "uniform"), ("C2", 4, 4, 19, "nerf"),
+                                              ("C2p", 16, 2, 19, "nerf"), ("C5", 16, 2, 22, "uniform")])
+def test_grid_backward_bricks_bitexact(pkg, orc, name, L, F, T, kind):
+    """The brick-summed dense levels (model option grid_bricks): the same table as the oracle, with points on
+    the unit cube's faces (the upper corners at coordinate res) and outside it (the global fallback)."""
+    n = 1 << 18
+    x = positions(kind, n, 3, seed=zlib.crc32(f"bricks/{name}/{kind}".encode()) & 0xffff)
+    x[80:88] = np.float32(1.0 + 2e-2)
+    x[88:96] = np.float32(-1e-2)
+    W = encoding_width(L, F)
+    g = np.random.default_rng(n + L + 1)
+    dy = np.zeros((n, W), np.float16)
+    dy[:, :L * F] = g.uniform(-1, 1, (n, L * F)).astype(np.float16)
+    net, _, got = run_backward(pkg, 3, L, F, T, x, dy, bricks=1)
+    assert net.query("grid_brick_levels") == 3
+    ref = orc.grid_backward_exact(orc.make_grid(3, L, F, T), x, dy)
+    bad = np.nonzero(got != ref)[0]
+    detail = [(int(i), hex(got[i]), hex(ref[i])) for i in bad[:6]]
+    assert bad.size == 0, f"{name}/{kind}: {bad.size} of {ref.size} gradient entries differ: {detail}"
 
 
 def test_grid_backward_bitexact_small_values(pkg, orc):
