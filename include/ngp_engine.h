@@ -101,8 +101,8 @@ int ngp_model_set_max_level(ngp_model* m, float max_level, const float* max_leve
  * levels summed per brick where that moves fewer bytes, default 0); "fuse_infer", "fuse_train",
  * "fused_hist", "overlap", "grid_forward_mode"  */
 int ngp_model_set_option(ngp_model* m, const char* key, double value);
-/* engine state for tests and tools: "grid_brick_levels" = dense levels the bucketed backward sums per brick
- * in its plan for the last batch size (0: all levels through items) */
+/* engine state for tests and tools: "grid_brick_levels" = how many dense levels the bucketed backward sums
+ * per brick in its plan for the last batch size (0: all levels through items) */
 int ngp_model_query(const ngp_model* m, const char* key, double* value);
 /* pre-size internal workspaces for batches up to n (lets callers capture steps into HIP graphs) */
 int ngp_model_reserve(ngp_model* m, uint32_t n);

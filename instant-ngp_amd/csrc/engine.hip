@@ -765,7 +765,7 @@ int ngp_model_query(const ngp_model* m, const char* key, double* value) {
 	NGP_ARG(m && key && value);
 	NGP_TRY({
 		const std::string k = key;
-		if (k == "grid_brick_levels") *value = m->sc_plan_n ? (double)m->sc_plan.bk.LD : 0.0;
+		if (k == "grid_brick_levels") *value = m->sc_plan_n ? (double)(m->sc_plan.bk.LD - m->sc_plan.bk.LB) : 0.0;
 		else throw Error("unknown model query: " + k);
 	});
 }

@@ -58,7 +58,7 @@ struct GridHist {
 	uint32_t* hist;
 	uint32_t B, n_chunks, chunk;
 	uint32_t vb_base[33];
-	uint32_t brick_levels = 0, n_bricks = 0, brick_cells = 8, bricks_per_dim = 0;
+	uint32_t brick_first = 0, brick_levels = 0, n_bricks = 0, brick_cells = 8, bricks_per_dim = 0, brick_vb0 = 0;  // levels [first, levels)
 	uint32_t stage0 = 1;  // row kernel: level 0's table staged in LDS when dense and <= 32 KB
 };
 

@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 	for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * a.pos_stride + d];
 	const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
 	if constexpr (HIST && D == 3) {
-		if (h.brick_levels) atomicAdd(&hl[brick_of(c, h.brick_levels - 1, h.brick_cells, h.bricks_per_dim, x)], 1u);
+		if (h.brick_levels) atomicAdd(&hl[h.brick_vb0 + brick_of(c, h.brick_levels - 1, h.brick_cells, h.bricks_per_dim, x)], 1u);
 	}
 	f16 row[32];
 #pragma unroll
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) acc[f] = 0.f;
 		const bool active = l < c.n_levels && !((float)l >= ml + 1e-3f);
-		const bool count = HIST && l >= h.brick_levels;  // brick levels: counted once per sample above
+		const bool count = HIST && !(l >= h.brick_first && l < h.brick_levels);  // brick levels: counted once per sample above
 		uint32_t few_bits = 32;
 		if constexpr (HIST) {
 			const uint32_t nvb = l < c.n_levels ? h.vb_base[l + 1] - h.vb_base[l] : 0u;
@@ -319,9 +319,10 @@ __global__ void __launch_bounds__(256) k_grid_forward_xcd(const GridConst c, con
 	uint32_t nvb = 0, vb0 = 0;
 	// bricks: the block of the finest brick level counts each sample's brick, coarser brick levels nothing
 	const bool brick_counter = HIST && D == 3 && l + 1 == h.brick_levels;
+	const bool brick_level = l >= h.brick_first && l < h.brick_levels;
 	if constexpr (HIST) {
-		nvb = l < h.brick_levels ? (brick_counter ? h.n_bricks : 0u) : h.vb_base[l + 1] - h.vb_base[l];
-		vb0 = l < h.brick_levels ? 0u : h.vb_base[l];
+		nvb = brick_level ? (brick_counter ? h.n_bricks : 0u) : h.vb_base[l + 1] - h.vb_base[l];
+		vb0 = brick_level ? h.brick_vb0 : h.vb_base[l];
 		for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) hl[j] = 0;
 		__syncthreads();
 	}
@@ -343,7 +344,7 @@ __global__ void __launch_bounds__(256) k_grid_forward_xcd(const GridConst c, con
 			if constexpr (D == 3) {
 				if (brick_counter) atomicAdd(&hl[brick_of(c, l, h.brick_cells, h.bricks_per_dim, x)], 1u);
 			}
-			if (l >= h.brick_levels) {
+			if (!brick_level) {
 #pragma unroll
 				for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&hl[(corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B], 1u);
 			}

@@ -6,14 +6,16 @@
 
 namespace ngp {
 
-// Brick-summed dense levels (3D grids): the leading LD dense levels are not sent through items. Samples are
+// Brick-summed dense levels (3D grids): dense levels LB..LD-1 are not sent through items. Samples are
 // counting-sorted by brick (K^3 cells of the finest of those levels, f = LD - 1; one item per sample: its
 // index), each brick part sums its samples' contributions to levels 0..LD-1 in LDS over the brick's region
 // (a box of corners per level, W[l]^3 entries at regoff[l]) and stores the exact int64 sums as a slab; the
 // finalize adds, per entry, the slabs of every brick whose region holds it. Corners outside the region
 // (positions outside [0, 1]) go to an int64 fallback table with global atomics.
 struct BrickConst {
-	uint32_t LD = 0, K = 8, NB = 0, NBK = 0, R = 0;
+	uint32_t LB = 0, LD = 0;  // brick levels [LB, LD) (coarser ones stay items: too few corners per brick, LDS contention)
+	uint32_t vb0 = 0;         // bricks are vbs [vb0, vb0 + NBK), owned by level LB's range
+	uint32_t K = 8, NB = 0, NBK = 0, R = 0;
 	uint32_t W[4] = {}, regoff[4] = {};
 	uint16_t lo[4][32] = {};  // region's first corner coordinate per level and brick coordinate
 };

@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
                                                         uint32_t B, uint32_t n_chunks, uint32_t* __restrict__ hist) {
 	extern __shared__ uint32_t h[];
 	const uint32_t chunk = blockIdx.x, l = blockIdx.y;
-	if (l < bk.LD) {  // brick levels: the finest one's block counts each sample's brick
+	if (l >= bk.LB && l < bk.LD) {  // brick levels: the finest one's block counts each sample's brick
 		if constexpr (D == 3) {
 			if (l + 1 != bk.LD) return;
 			for (uint32_t j = threadIdx.x; j < bk.NBK; j += blockDim.x) h[j] = 0;
@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_hist(const GridConst c, const
 				atomicAdd(&h[brick_of(c, l, bk.K, bk.NB, x)], 1u);
 			}
 			__syncthreads();
-			for (uint32_t j = threadIdx.x; j < bk.NBK; j += blockDim.x) hist[(size_t)chunk * lv.vb_base[c.n_levels] + j] = h[j];
+			for (uint32_t j = threadIdx.x; j < bk.NBK; j += blockDim.x) hist[(size_t)chunk * lv.vb_base[c.n_levels] + bk.vb0 + j] = h[j];
 		}
 		return;
 	}
@@ -280,9 +280,9 @@ template <uint32_t SC_PLAN_K>
 __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __restrict__ tot, uint32_t n_vb, uint32_t split_limit,
                                                              uint32_t part, uint32_t* __restrict__ lo_out,
                                                              uint32_t* __restrict__ split, uint32_t* __restrict__ splitb,
-                                                             uint32_t n_bricks, uint32_t brick_part, uint32_t* __restrict__ bp,
+                                                             uint32_t brick_vb0, uint32_t n_bricks, uint32_t brick_part, uint32_t* __restrict__ bp,
                                                              uint32_t* __restrict__ fb_flag) {
-	// bricks (vbs [0, n_bricks)): every non-empty one is summed in parts of brick_part samples, each storing a
+	// bricks (vbs [brick_vb0, + n_bricks)): every non-empty one is summed in parts of brick_part samples, each storing a
 	// slab; bp[2 b] = first part, bp[2 b + 1] = parts. They are not split buckets of k_sc_split_reduce.
 	if (fb_flag && threadIdx.x == 0) *fb_flag = 0u;  // the previous step's finalize has read and cleared the fallback
 	__shared__ uint32_t wsum[3][SC_PLAN_THREADS / 64];
@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __r
 		uint32_t s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll
 		for (uint32_t k = 0; k < SC_PLAN_K; ++k) {
-			const bool brick = v0 + k < n_bricks;
+			const bool brick = v0 + k - brick_vb0 < n_bricks;
 			const uint32_t sp = (brick ? t[k] > 0 : t[k] > split_limit) ? 1u : 0u;
 			const uint32_t pk = brick ? brick_part : part;
 			s0 += t[k]; s1 += sp ? (t[k] + pk - 1) / pk : 0u; s2 += brick ? 0u : sp;
@@ -317,9 +317,9 @@ __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __r
 			if (k >= K || v0 + k >= n_vb) break;
 			const uint32_t vb = v0 + k, tk = t[k];
 			lo_out[vb] = lo;
-			if (vb < n_bricks) {
+			if (vb - brick_vb0 < n_bricks) {
 				const uint32_t parts = (tk + brick_part - 1) / brick_part;
-				bp[2 * vb] = first; bp[2 * vb + 1] = parts;
+				bp[2 * (vb - brick_vb0)] = first; bp[2 * (vb - brick_vb0) + 1] = parts;
 				for (uint32_t q = 0; q < parts; ++q) {
 					uint32_t* d = split + 2 + 3 * (size_t)(first + q);
 					d[0] = vb; d[1] = lo + q * brick_part; d[2] = min(lo + (q + 1) * brick_part, lo + tk);
@@ -356,7 +356,7 @@ __device__ void scatter_bricks(const GridConst& c, const BrickConst& bk, const G
 	uint16_t* st_b = (uint16_t*)(loff + nvb + 1);
 	uint32_t* st_i = (uint32_t*)(((uintptr_t)(st_b + SC_CHUNK) + 15) & ~(uintptr_t)15);
 	for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) {
-		cur[j] = lo_vb[j] + cur_t[(size_t)chunk * n_vb + j];
+		cur[j] = lo_vb[bk.vb0 + j] + cur_t[(size_t)chunk * n_vb + bk.vb0 + j];
 		lh[j] = 0;
 	}
 	__syncthreads();
@@ -402,8 +402,8 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 	constexpr uint32_t SC_SSPT = SC_CHUNK / SC_ST;  // samples per thread
 	extern __shared__ uint32_t lds[];
 	__shared__ uint32_t wsum[SC_ST / 64];
-	// slots per chunk: the brick slot (slot 0 when bk.LD > 0), then one per item level
-	const uint32_t n_slots = c.n_levels - bk.LD + (bk.LD ? 1u : 0u);
+	// slots per chunk: one per item level, the brick slot in place of the brick levels (slot LB)
+	const uint32_t n_slots = c.n_levels - (bk.LD - bk.LB) + (bk.LD ? 1u : 0u);
 	// XCD-aware order: blocks b and b + 8 share an XCD (round-robin dispatch), so the L level blocks of a
 	// chunk run back to back on one XCD and its positions and dL/dy rows leave HBM once, not L times
 	uint32_t chunk, l;
@@ -422,14 +422,14 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 		l = blockIdx.x / n_chunks;
 	}
 	if (chunk >= n_chunks) return;
-	if (bk.LD) {
+	if (bk.LD && l >= bk.LB) {
 		if constexpr (D == 3) {
-			if (l == 0) {
+			if (l == bk.LB) {
 				scatter_bricks<F, SC_CHUNK, SC_ST>(c, bk, a, n_vb, chunk, cur_t, lo_vb, item_idx, item_val, lds, wsum);
 				return;
 			}
 		}
-		l = l - 1 + bk.LD;
+		l = l - bk.LB - 1 + bk.LD;
 	}
 	const uint32_t nvb = lv.vb_base[l + 1] - lv.vb_base[l];
 	uint32_t* cur = lds;                                   // [nvb] this block's global cursor per bucket
@@ -598,8 +598,8 @@ __device__ void accumulate_brick(const GridConst& c, const BrickConst& bk, const
 	__syncthreads();
 	const uint32_t b3[3] = {vb % bk.NB, (vb / bk.NB) % bk.NB, vb / (bk.NB * bk.NB)};
 	const uint32_t ns = hi - lo, rot = threadIdx.x % F;
-	for (uint32_t w = threadIdx.x; w < ns * bk.LD; w += blockDim.x) {
-		const uint32_t l = w / ns, i = brick_item<F>(item_idx, item_val, lo + w % ns);
+	for (uint32_t w = threadIdx.x; w < ns * (bk.LD - bk.LB); w += blockDim.x) {
+		const uint32_t l = bk.LB + w / ns, i = brick_item<F>(item_idx, item_val, lo + w % ns);
 		float x[3];
 		load_pos<3>(a, i, x);
 		const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
@@ -765,8 +765,8 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 		if (blockIdx.x >= split[0]) return;
 		const uint32_t* d = split + 2 + 3 * (size_t)blockIdx.x;
 		const uint32_t lo = d[1], hi = d[2];
-		if (d[0] < bk.NBK) {
-			accumulate_brick<F>(c, bk, a, d[0], lo, hi, item_idx, item_val, acc, scratch + (size_t)blockIdx.x * NE * F, NE, fb);
+		if (d[0] - bk.vb0 < bk.NBK) {
+			accumulate_brick<F>(c, bk, a, d[0] - bk.vb0, lo, hi, item_idx, item_val, acc, scratch + (size_t)blockIdx.x * NE * F, NE, fb);
 			return;
 		}
 		for (uint32_t k = threadIdx.x; k < NEP * F; k += blockDim.x) acc[k] = 0ull;
@@ -779,7 +779,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 		return;
 	}
 	const uint32_t vb = blockIdx.x - max_parts;
-	if (vb < bk.NBK) return;  // bricks: parts only
+	if (vb - bk.vb0 < bk.NBK) return;  // bricks: parts only
 	const uint32_t t = tot[vb];
 	if (t > split_limit) return;
 	uint32_t e0, n_e;
@@ -871,7 +871,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
 	if (blockIdx.x >= fin_x0) {
 		constexpr uint32_t EPT = F == 1 ? 2 : 1;  // entries per thread: whole parameter pairs
 		const uint32_t blk = blockIdx.y * (gridDim.x - fin_x0) + (blockIdx.x - fin_x0);
-		const uint32_t e0 = (blk * blockDim.x + threadIdx.x) * EPT;
+		const uint32_t e0 = c.offsets[bk.LB] + (blk * blockDim.x + threadIdx.x) * EPT;
 		if (e0 >= c.offsets[bk.LD]) return;
 		const uint32_t NE = 1u << B;
 		const bool used = *fb.flag != 0u;
@@ -883,7 +883,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
 #pragma unroll
 			for (uint32_t f = 0; f < F; ++f) s[u * F + f] = fix_to_f32(q[f]);
 		}
-		// pairs (e0 F) / 2 .. of the grid (brick levels start at entry 0)
+		// pairs (e0 F) / 2 .. of the grid
 #pragma unroll
 		for (uint32_t h = 0; h < EPT * F / 2; ++h) {
 			const uint32_t k = e0 * F / 2 + h;
@@ -952,10 +952,11 @@ size_t scatter_lds_bytes(uint32_t max_lb, uint32_t chunk, uint32_t D, uint32_t F
 
 Levels make_levels(const GridDesc& g, uint32_t B, const BrickConst& bk) {
 	Levels lv{};
-	uint32_t vb = bk.NBK;  // bricks first; brick levels have no buckets
+	uint32_t vb = 0;  // level LB's range holds the bricks [bk.vb0, + NBK); levels LB+1..LD-1 own no buckets
 	for (uint32_t l = 0; l < g.n_levels; ++l) {
 		lv.vb_base[l] = vb;
-		if (l >= bk.LD) vb += (g.offsets[l + 1] - g.offsets[l] + (1u << B) - 1) >> B;
+		if (bk.LD && l == bk.LB) vb += bk.NBK;
+		else if (!(l >= bk.LB && l < bk.LD)) vb += (g.offsets[l + 1] - g.offsets[l] + (1u << B) - 1) >> B;
 	}
 	for (uint32_t l = g.n_levels; l <= 32; ++l) lv.vb_base[l] = vb;
 	return lv;
@@ -976,7 +977,7 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 	const BrickFallback fb{(unsigned long long*)(ws + p.off_fb), (uint32_t*)(ws + p.off_fb + (size_t)c.offsets[p.bk.LD] * c.n_features * 8)};
 	const size_t lds_s = scatter_lds_bytes(p.max_lb, p.spb, D, F);
 	const uint32_t xcd_map = p.xcd_map;
-	const uint32_t n_slots = c.n_levels - p.bk.LD + (p.bk.LD ? 1u : 0u);
+	const uint32_t n_slots = c.n_levels - (p.bk.LD - p.bk.LB) + (p.bk.LD ? 1u : 0u);
 	const dim3 grid_s(xcd_map ? (uint32_t)div_round_up(p.n_chunks, 8) * 8 * n_slots : p.n_chunks * n_slots);
 	auto go = [&](auto scatter, auto accum, auto splitr) {
 		ensure_dynamic_lds((const void*)scatter, lds_s);
@@ -992,7 +993,8 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		const uint32_t gy = (uint32_t)div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS);
 		const SlabJob sj = slab ? *slab : SlabJob{};
 		const uint32_t slab_x = slab ? (uint32_t)div_round_up(slab_blocks(sj.n), gy) : 0u;
-		const size_t fin_threads = c.n_features == 1 ? div_round_up(c.offsets[p.bk.LD], 2) : (size_t)c.offsets[p.bk.LD];
+		const size_t fin_entries = (size_t)c.offsets[p.bk.LD] - c.offsets[p.bk.LB];
+		const size_t fin_threads = c.n_features == 1 ? div_round_up(fin_entries, 2) : fin_entries;
 		const uint32_t fin_x = (uint32_t)div_round_up(div_round_up(fin_threads, SC_THREADS), gy);
 		const dim3 grid_r(p.max_split_buckets + slab_x + fin_x, gy);
 		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets, fa, p.bk, bp, fb,
@@ -1018,20 +1020,25 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 #undef NGP_SC_F
 }
 
-// Brick geometry for the leading LD dense levels (3D). Finest level f = LD - 1: brick b covers cells
+// Brick geometry for dense levels LB..LD-1 (3D). Finest level f = LD - 1: brick b covers cells
 // [K b, K b + K) and so corners [K b, K b + K]. A coarser level l gets, per brick coordinate, the corners of
 // every cell a position of that range can fall in (computed in double, one cell of margin each side for the
-// float rounding of the samples' own level_setup), W[l] = the widest such range. Returns bk.LD = 0 when no
-// LD fits the bucket's LDS tile (R <= NE) or saves bytes: the slabs (one per non-empty brick and part, R * F
-// int64, written and read once) must cost under 3/4 of the items they replace (LD * 2^D per sample, also
-// written and read once). C2 (2^18 samples): 24 MB of slabs for 63 MB of items; not at 2^16 samples.
+// float rounding of the samples' own level_setup), W[l] = the widest such range. A level joins only if a
+// brick spans at least MIN_CELLS of its cells per dimension: coarser ones put a brick's thousands of
+// contributions on a few dozen LDS counters (C2's level 0: ~2 cells, ~170 adds per counter and brick),
+// which serialised the first version (r04j: backward 72 -> 164 us with levels 0-2). Returns LD = 0 when no
+// range fits the bucket's LDS tile (R <= NE) or saves bytes: the slabs (one per non-empty brick and part, R * F
+// int64, written and read once) must cost under 3/4 of the items they replace (2^D per sample and level, also
+// written and read once).
 static BrickConst make_bricks(const GridDesc& g, uint32_t n, uint32_t B, uint32_t brick_part) {
 	BrickConst best;
 	if (g.n_dims != 3) return best;
 	if (const char* e = getenv("NGP_SC_BRICKS")) { if (atoi(e) == 0) return best; }
+	double min_cells = 3.0;
+	if (const char* e = getenv("NGP_SC_BRICK_MIN_CELLS")) min_cells = atof(e);
 	const uint32_t F = g.n_features, NE = 1u << B;
 	// dense levels with T = res^3 exactly (even res: the unclamped upper corners alias modulo res^3 only,
-	// brick_entry_sum), at most 4
+	// brick_entry_sums), at most 4
 	uint32_t dense = 0;
 	while (dense < g.n_levels && dense < 4) {
 		const uint64_t r = g.resolution[dense];
@@ -1039,43 +1046,48 @@ static BrickConst make_bricks(const GridDesc& g, uint32_t n, uint32_t B, uint32_
 		++dense;
 	}
 	double best_save = 0.0;
-	for (uint32_t LD = 1; LD <= dense; ++LD) {
-		BrickConst bk;
-		bk.LD = LD; bk.K = 8;
-		const uint32_t f = LD - 1, cells = g.resolution[f];  // positions in [0, 1]: cells 0..res-1
-		bk.NB = (cells + bk.K - 1) / bk.K;
-		if (bk.NB < 2 || bk.NB > 32) continue;
-		bk.NBK = bk.NB * bk.NB * bk.NB;
-		bool ok = true;
-		for (uint32_t l = 0; l < LD && ok; ++l) {
-			uint32_t W = 0;
-			for (uint32_t b = 0; b < bk.NB; ++b) {
-				int64_t c_lo, c_hi;
-				if (l == f) { c_lo = (int64_t)bk.K * b; c_hi = c_lo + bk.K; }
-				else {
-					const double sl = g.scale[l], sf = g.scale[f];
-					const double lower = sl * ((double)bk.K * b - 0.5) / sf + 0.5, upper = sl * ((double)bk.K * b + bk.K - 0.5) / sf + 0.5;
-					c_lo = (int64_t)std::floor(lower) - 1;
-					c_hi = (int64_t)std::floor(upper) + 2;  // last cell (+ margin) + its upper corner
+	for (uint32_t LD = 1; LD <= dense; ++LD)
+		for (uint32_t LB = 0; LB < LD; ++LB) {
+			BrickConst bk;
+			bk.LB = LB; bk.LD = LD; bk.K = 8;
+			const uint32_t f = LD - 1, cells = g.resolution[f];  // positions in [0, 1]: cells 0..res-1
+			bk.NB = (cells + bk.K - 1) / bk.K;
+			if (bk.NB < 2 || bk.NB > 32) continue;
+			if ((double)bk.K * g.scale[LB] / g.scale[f] < min_cells) continue;
+			bk.NBK = bk.NB * bk.NB * bk.NB;
+			bool ok = true;
+			for (uint32_t l = LB; l < LD && ok; ++l) {
+				uint32_t W = 0;
+				for (uint32_t b = 0; b < bk.NB; ++b) {
+					int64_t c_lo, c_hi;
+					if (l == f) { c_lo = (int64_t)bk.K * b; c_hi = c_lo + bk.K; }
+					else {
+						const double sl = g.scale[l], sf = g.scale[f];
+						const double lower = sl * ((double)bk.K * b - 0.5) / sf + 0.5, upper = sl * ((double)bk.K * b + bk.K - 0.5) / sf + 0.5;
+						c_lo = (int64_t)std::floor(lower) - 1;
+						c_hi = (int64_t)std::floor(upper) + 2;  // last cell (+ margin) + its upper corner
+					}
+					c_lo = std::max<int64_t>(c_lo, 0);
+					c_hi = std::min<int64_t>(c_hi, (int64_t)g.resolution[l]);  // the last cell's upper corner is coordinate res
+					bk.lo[l][b] = (uint16_t)c_lo;
+					W = std::max<uint32_t>(W, (uint32_t)(c_hi - c_lo + 1));
 				}
-				c_lo = std::max<int64_t>(c_lo, 0);
-				c_hi = std::min<int64_t>(c_hi, (int64_t)g.resolution[l]);  // the last cell's upper corner is coordinate res
-				bk.lo[l][b] = (uint16_t)c_lo;
-				W = std::max<uint32_t>(W, (uint32_t)(c_hi - c_lo + 1));
+				bk.W[l] = W;
+				bk.regoff[l] = bk.R;
+				bk.R += W * W * W;
+				ok = bk.R <= NE;
 			}
-			bk.W[l] = W;
-			bk.regoff[l] = bk.R;
-			bk.R += W * W * W;
-			ok = bk.R <= NE;
+			if (!ok) continue;
+			// parts: one per non-empty brick, more where bricks hold over brick_part samples
+			const double parts = std::max((double)std::min<uint64_t>(bk.NBK, n), (double)n / brick_part);
+			const double slabs = parts * bk.R * F * 8;
+			const double items = (double)n * (LD - LB) * 8 * (2 + 2 * F);
+			const double save = 0.75 * items - slabs;
+			if (save > best_save) { best_save = save; best = bk; }
 		}
-		if (!ok) continue;
-		// parts: one per non-empty brick, more where bricks hold over brick_part samples
-		const double parts = std::max((double)std::min<uint64_t>(bk.NBK, n), (double)n / brick_part);
-		const double slabs = parts * bk.R * F * 8;
-		const double items = (double)n * LD * 8 * (2 + 2 * F);
-		const double save = 0.75 * items - slabs;
-		if (save > best_save) { best_save = save; best = bk; }
-	}
+	// the bricks sit in level LB's bucket range: after the buckets of levels 0..LB-1
+	if (best.LD)
+		for (uint32_t l = 0; l < best.LB; ++l) best.vb0 += (g.offsets[l + 1] - g.offsets[l] + NE - 1) >> B;
 	return best;
 }
 
@@ -1098,7 +1110,7 @@ ScatterPlan make_scatter_plan(const GridDesc& g, uint32_t n, bool bricks) {
 	NGP_CHECK((size_t)p.max_lb * 4 <= 32 * 1024, "grid backward: level too large for the bucket histogram");
 	// samples per chunk: 1024 when 512-sample chunks would average fewer than 16 items per (chunk,
 	// bucket) and the scatter block's LDS allows it
-	const uint64_t items_per_sample = ((uint64_t)(g.n_levels - p.bk.LD) << g.n_dims) + (p.bk.LD ? 1u : 0u);
+	const uint64_t items_per_sample = ((uint64_t)(g.n_levels - (p.bk.LD - p.bk.LB)) << g.n_dims) + (p.bk.LD ? 1u : 0u);
 	p.spb = 512;
 	if (512ull * items_per_sample < 16ull * p.n_buckets && scatter_lds_bytes(p.max_lb, 1024, g.n_dims, F) <= 160 * 1024) p.spb = 1024;
 	if (const char* e = getenv("NGP_SC_CHUNK")) p.spb = (uint32_t)atoi(e);
@@ -1145,7 +1157,8 @@ bool scatter_hist(const GridDesc& g, const ScatterPlan& p, void* workspace, Grid
 	h.hist = (uint32_t*)((char*)workspace + p.off_hist);
 	h.B = p.B; h.n_chunks = p.n_chunks; h.chunk = p.spb;
 	for (int l = 0; l <= 32; ++l) h.vb_base[l] = lv.vb_base[l];
-	h.brick_levels = p.bk.LD; h.n_bricks = p.bk.NBK; h.brick_cells = p.bk.K; h.bricks_per_dim = p.bk.NB;
+	h.brick_first = p.bk.LB; h.brick_levels = p.bk.LD; h.n_bricks = p.bk.NBK; h.brick_cells = p.bk.K; h.bricks_per_dim = p.bk.NB;
+	h.brick_vb0 = p.bk.vb0;
 	return true;
 }
 
@@ -1171,7 +1184,7 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const Scatter
 	const auto plan = p.n_buckets <= SC_PLAN_THREADS ? k_sc_plan<1> : p.n_buckets <= 8 * SC_PLAN_THREADS ? k_sc_plan<8> : k_sc_plan<32>;
 	plan<<<1, SC_PLAN_THREADS, 0, s>>>((const uint32_t*)(ws + p.off_tot), p.n_buckets, p.split_limit, p.part,
 	                                        (uint32_t*)(ws + p.off_lo), (uint32_t*)(ws + p.off_split), (uint32_t*)(ws + p.off_splitb),
-	                                        p.bk.NBK, p.brick_part, (uint32_t*)(ws + p.off_bp),
+	                                        p.bk.vb0, p.bk.NBK, p.brick_part, (uint32_t*)(ws + p.off_bp),
 	                                        p.bk.LD ? (uint32_t*)(ws + p.off_fb + (size_t)g.offsets[p.bk.LD] * g.n_features * 8) : nullptr);
 	NGP_HIP(hipGetLastError());
 }

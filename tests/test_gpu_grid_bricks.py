@@ -1,6 +1,6 @@
 """Brick-summed dense levels of the bucketed grid backward (csrc/grid_scatter.hip, ScatterPlan::bk).
 
-At 2^18 samples the C2 (L4 F4) and C2' (L16 F2) grids send their leading dense levels 0-2 through bricks
+At 2^18 samples the C2 (L4 F4) and C2' (L16 F2) grids send their dense levels 1-2 through bricks
 (each sample's index sorted by brick, its contributions summed in LDS over the brick's region, the exact
 int64 slabs added per entry) instead of 8 items per sample and level. The contributions and their
 fixed-point sums are those of the item path, so training must be bit for bit the same with the bricks
@@ -55,7 +55,7 @@ def train(pkg, variant, kind, bricks, steps=4):
         x, dL = batch(kind, N, 100 + s)
         tr.train_step(x, dL, 128.0)
     torch.cuda.synchronize()
-    assert net.query("grid_brick_levels") == (3 if bricks else 0)  # C2 and C2': levels 0-2 of res 16, 32, 64
+    assert net.query("grid_brick_levels") == (2 if bricks else 0)  # C2 and C2': levels 1-2 (res 32, 64)
     return tr.params.cpu().numpy().view(np.uint16).copy(), tr.params_full_precision.cpu().numpy().view(np.uint32).copy()
 
 

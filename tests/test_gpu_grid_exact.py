@@ -110,7 +110,7 @@ def test_grid_backward_bricks_bitexact(pkg, orc, name, L, F, T, kind):
     dy = np.zeros((n, W), np.float16)
     dy[:, :L * F] = g.uniform(-1, 1, (n, L * F)).astype(np.float16)
     net, _, got = run_backward(pkg, 3, L, F, T, x, dy, bricks=1)
-    assert net.query("grid_brick_levels") == 3
+    assert net.query("grid_brick_levels") == 2  # levels 1-2 (C5: res 32, 64; level 0 has too few cells per brick)
     ref = orc.grid_backward_exact(orc.make_grid(3, L, F, T), x, dy)
     bad = np.nonzero(got != ref)[0]
     detail = [(int(i), hex(got[i]), hex(ref[i])) for i in bad[:6]]
