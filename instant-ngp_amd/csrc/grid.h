@@ -183,12 +183,22 @@ template <> struct GridVec<2> { typedef f16x2 T; typedef f16 __attribute__((ext_
 template <> struct GridVec<4> { typedef f16x4 T; typedef f16 __attribute__((ext_vector_type(8), aligned(8))) P; };
 template <> struct GridVec<8> { typedef f16x8 T; typedef f16x8 P; };
 
+#ifndef NGP_GATHER16
+#define NGP_GATHER16 1  // F = 2 gathers by aligned 16-B groups (gather_pairs_f2)
+#endif
+template <uint32_t D>
+__device__ __forceinline__ void gather_pairs_f2(const uint32_t* idx, const f16* __restrict__ table, f16x2* v);
 template <uint32_t D, uint32_t F>
 __device__ __forceinline__ void gather_corners(const GridConst& c, uint32_t l, const uint32_t* base, const f16* __restrict__ table,
                                                typename GridVec<F>::T* v) {
 	typedef typename GridVec<F>::T V;
 	typedef typename GridVec<F>::P P;
-	if constexpr (F == 2 || F == 4) {
+	if constexpr (F == 2 && NGP_GATHER16) {
+		uint32_t idx[1u << D];
+#pragma unroll
+		for (uint32_t k = 0; k < (1u << D); ++k) idx[k] = corner_index<D>(c, l, base, k);
+		gather_pairs_f2<D>(idx, table, v);
+	} else if constexpr (F == 2 || F == 4) {
 #pragma unroll
 		for (uint32_t k = 0; k < (1u << D); k += 2) {
 			const uint32_t i0 = corner_index<D>(c, l, base, k), i1 = corner_index<D>(c, l, base, k + 1);
@@ -212,12 +222,49 @@ __device__ __forceinline__ void gather_corners(const GridConst& c, uint32_t l, c
 		for (uint32_t k = 0; k < (1u << D); ++k) v[k] = *(const V*)(table + (size_t)corner_index<D>(c, l, base, k) * F);
 	}
 }
+// F = 2: an x-edge pair whose entries share an aligned group of 4 (16 B) is one 16-B load even when the
+// two are not adjacent: on a hashed level with base x = 1 mod 4 the pair is (4m, 4m + 3) or (4m + 3, 4m)
+// half of the time, two requests with 8-B loads. The gathers are bound by the L2's request rate (§5), so
+// a hashed level's expected requests per pair fall from ~1.31 to ~1.19.
+__device__ __forceinline__ f16x2 pick4(const uint32_t (&g)[4], uint32_t i) {
+	const uint32_t lo = (i & 1u) ? g[1] : g[0], hi = (i & 1u) ? g[3] : g[2];
+	return __builtin_bit_cast(f16x2, (i & 2u) ? hi : lo);
+}
+template <uint32_t D>
+__device__ __forceinline__ void gather_pairs_f2(const uint32_t* idx, const f16* __restrict__ table, f16x2* v) {
+	typedef GridVec<2>::P P;
+#pragma unroll
+	for (uint32_t k = 0; k < (1u << D); k += 2) {
+		const uint32_t i0 = idx[k], i1 = idx[k + 1];
+		const uint32_t lo_i = min(i0, i1);
+		if ((i0 >> 2) == (i1 >> 2)) {
+			const uint32_t* gp = (const uint32_t*)(table + (size_t)(i0 & ~3u) * 2);
+			typedef uint32_t u32x4g __attribute__((ext_vector_type(4)));
+			const u32x4g q = *(const u32x4g*)gp;
+			const uint32_t g[4] = {q[0], q[1], q[2], q[3]};
+			v[k] = pick4(g, i0 & 3u);
+			v[k + 1] = pick4(g, i1 & 3u);
+		} else if (max(i0, i1) == lo_i + 1u) {
+			const P p = *(const P*)(table + (size_t)lo_i * 2);
+			const f16x2 a{p[0], p[1]}, b{p[2], p[3]};
+			const bool swap = i1 < i0;
+			v[k] = swap ? b : a;
+			v[k + 1] = swap ? a : b;
+		} else {
+			v[k] = *(const f16x2*)(table + (size_t)i0 * 2);
+			v[k + 1] = *(const f16x2*)(table + (size_t)i1 * 2);
+		}
+	}
+}
+
 // the same gather from precomputed corner indices (corner_indices)
 template <uint32_t D, uint32_t F>
 __device__ __forceinline__ void gather_corners_at(const uint32_t* idx, const f16* __restrict__ table, typename GridVec<F>::T* v) {
 	typedef typename GridVec<F>::T V;
 	typedef typename GridVec<F>::P P;
-	if constexpr (F == 2 || F == 4) {
+	if constexpr (F == 2 && NGP_GATHER16) {
+		gather_pairs_f2<D>(idx, table, v);
+	} else if constexpr (F == 2 || F == 4) {
 #pragma unroll
 		for (uint32_t k = 0; k < (1u << D); k += 2) {
 			const uint32_t i0 = idx[k], i1 = idx[k + 1];

@@ -194,7 +194,17 @@ struct Train16Layout {
 		return STAGE_D + (l == 0 ? 0u : 64u * 34u + (uint32_t)(l - 1) * 64u * 66u);
 	}
 	static constexpr uint32_t STAGE_HALVES = STAGE_D + 64u * 34u + (RH - 1) * 64u * 66u + 16u * 66u;
-	static_assert(STAGE_HALVES <= 4 * IMG_HALVES, "parameter staging must fit the image region");
+	// the same layers transposed ([in x (out + 2)]), for the backward fragments: their A = W^T rows are then
+	// dword runs too instead of 2-B gathers down a column
+	__host__ __device__ static constexpr uint32_t stage_dt(int l) {
+		return STAGE_HALVES + (l == 0 ? 0u : 16u * ES * 66u + (uint32_t)(l - 1) * 64u * 66u);
+	}
+	static constexpr uint32_t STAGE_DT = STAGE_HALVES + 16u * ES * 66u + (DH - 1) * 64u * 66u + 64u * 18u;
+	__host__ __device__ static constexpr uint32_t stage_rt(int l) {
+		return STAGE_DT + (l == 0 ? 0u : 32u * 66u + (uint32_t)(l - 1) * 64u * 66u);
+	}
+	static constexpr uint32_t STAGE_ALL = STAGE_DT + 32u * 66u + (RH - 1) * 64u * 66u + 64u * 18u;
+	static_assert(STAGE_ALL <= 4 * IMG_HALVES, "parameter staging must fit the image region");
 };
 
 // Timing experiments only (-DNGP_T16_CLOCK, DESIGN §6 phase costs): block 0..1023's thread 0 stamps the
@@ -239,6 +249,12 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 	auto wr = [&](int l) {  // rgb MLP: [64 x 32], (RH-1) x [64 x 64], [16 x 64]
 		return LW{stage + T::stage_r(l), l == RH ? 16u : 64u, l == 0 ? 32u : 64u, (l == 0 ? 32u : 64u) + 2u};
 	};
+	auto wdt = [&](int l) {  // transposed copies: [in x out]
+		return LW{stage + T::stage_dt(l), l == 0 ? 16u * ES : 64u, l == DH ? 16u : 64u, (l == DH ? 16u : 64u) + 2u};
+	};
+	auto wrt = [&](int l) {
+		return LW{stage + T::stage_rt(l), l == 0 ? 32u : 64u, l == RH ? 16u : 64u, (l == RH ? 16u : 64u) + 2u};
+	};
 	{
 		// 16-B chunks (8 halves of one row: every row length is a multiple of 8), all loads issued before the
 		// first store; a scalar copy loop waited on one L2 round trip per iteration (~20 of them)
@@ -252,10 +268,14 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 			const uint32_t c = threadIdx.x + 512 * k;
 			if (c < NCH) v[k] = *(const f16x8*)(c < ND / 8 ? pd + 8 * c : pr + 8 * (c - ND / 8));
 		}
-		auto put8 = [&](const LW& L, uint32_t h, f16x8 x) {  // h = the chunk's first element in [out x in]
-			uint32_t* d = (uint32_t*)(L.w + (h / L.in) * L.stride + h % L.in);
+		auto put8 = [&](const LW& L, const LW& Lt, uint32_t h, f16x8 x) {  // h = the chunk's first element in [out x in]
+			const uint32_t o = h / L.in, i = h % L.in;
+			uint32_t* d = (uint32_t*)(L.w + o * L.stride + i);
 			const u32x4v u = __builtin_bit_cast(u32x4v, x);
 			d[0] = u[0]; d[1] = u[1]; d[2] = u[2]; d[3] = u[3];
+			f16* t = (f16*)Lt.w + i * Lt.stride + o;
+#pragma unroll
+			for (int j = 0; j < 8; ++j) t[j * Lt.stride] = x[j];
 		};
 #pragma unroll
 		for (uint32_t k = 0; k < PER; ++k) {
@@ -266,7 +286,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
 				for (int l = 0; l <= DH; ++l) {
 					const LW L = wd(l);
-					if (h < L.out * L.in) { put8(L, h, v[k]); break; }
+					if (h < L.out * L.in) { put8(L, wdt(l), h, v[k]); break; }
 					h -= L.out * L.in;
 				}
 			} else {
@@ -274,7 +294,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 #pragma unroll
 				for (int l = 0; l <= RH; ++l) {
 					const LW L = wr(l);
-					if (h < L.out * L.in) { put8(L, h, v[k]); break; }
+					if (h < L.out * L.in) { put8(L, wrt(l), h, v[k]); break; }
 					h -= L.out * L.in;
 				}
 			}
@@ -283,27 +303,27 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 	__syncthreads();
 	T16_MARK(1);
 
-	// backward (transposed) weights -> LDS, one copy per block
+	// backward (transposed) weights -> LDS, one copy per block: A = W^T, read as rows of the transposed copies
 	for (int t = threadIdx.x; t < 4 * 64; t += blockDim.x) {  // K=16 fragments: W_ro^T and W_do^T, 4 tiles each
 		const int tile = t >> 6, l = t & 63;
-		*(f16x4*)(wl + T::B_RO + t * 4) = wfrag16(wr(RH), true, tile, l);
-		*(f16x4*)(wl + T::B_DO + t * 4) = wfrag16(wd(DH), true, tile, l);
+		*(f16x4*)(wl + T::B_RO + t * 4) = wfrag16(wrt(RH), false, tile, l);
+		*(f16x4*)(wl + T::B_DO + t * 4) = wfrag16(wdt(DH), false, tile, l);
 	}
 	for (int t = threadIdx.x; t < (RH - 1) * 8 * 64; t += blockDim.x) {
 		const int j = t / 512, f = (t >> 6) & 7, l = t & 63;  // j-th = layer RH-1-j; f = tile * 2 + step
-		*(f16x8*)(wl + T::B_RH + t * 8) = wfrag32(wr(RH - 1 - j), true, f >> 1, f & 1, true, l);
+		*(f16x8*)(wl + T::B_RH + t * 8) = wfrag32(wrt(RH - 1 - j), false, f >> 1, f & 1, true, l);
 	}
 	for (int t = threadIdx.x; t < 4 * 64; t += blockDim.x) {
 		const int f = t >> 6, l = t & 63;
-		*(f16x8*)(wl + T::B_R0 + t * 8) = wfrag32(wr(0), true, f >> 1, f & 1, true, l);
+		*(f16x8*)(wl + T::B_R0 + t * 8) = wfrag32(wrt(0), false, f >> 1, f & 1, true, l);
 	}
 	for (int t = threadIdx.x; t < (DH - 1) * 8 * 64; t += blockDim.x) {
 		const int j = t / 512, f = (t >> 6) & 7, l = t & 63;
-		*(f16x8*)(wl + T::B_DH + t * 8) = wfrag32(wd(DH - 1 - j), true, f >> 1, f & 1, true, l);
+		*(f16x8*)(wl + T::B_DH + t * 8) = wfrag32(wdt(DH - 1 - j), false, f >> 1, f & 1, true, l);
 	}
 	for (int t = threadIdx.x; t < ES * 2 * 64; t += blockDim.x) {
 		const int f = t >> 6, l = t & 63;
-		*(f16x8*)(wl + T::B_D0 + t * 8) = wfrag32(wd(0), true, f >> 1, f & 1, true, l);
+		*(f16x8*)(wl + T::B_D0 + t * 8) = wfrag32(wdt(0), false, f >> 1, f & 1, true, l);
 	}
 	// forward weights in registers
 	f16x4 wd0_16[ES == 1 ? 4 : 1];
