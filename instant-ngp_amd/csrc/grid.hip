@@ -424,7 +424,7 @@ static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hip
 		NGP_CHECK(grid_h.x == h->n_chunks, "grid forward histogram: chunk count mismatch");
 		// level 0 staged in LDS when dense and <= 32 KB (engine option grid_stage0, default on)
 		const size_t t0_bytes = (size_t)c.offsets[1] * F * 2;
-		const bool stage0 = h->stage0 && !(c.hashed & 1u) && t0_bytes <= 32 * 1024;
+		const bool stage0 = h->stage0 && !(c.hashed & 1u) && t0_bytes <= 32 * 1024 && ((uintptr_t)a.table & 15u) == 0;
 		const size_t lds = (((size_t)h->vb_base[c.n_levels] + 3) & ~(size_t)3) * 4 + (stage0 ? t0_bytes : 0);
 		auto go = [&](auto kern, auto kern_s) {
 			if (stage0) {
