@@ -59,7 +59,7 @@ struct GridHist {
 	uint32_t B, n_chunks, chunk;
 	uint32_t vb_base[33];
 	uint32_t brick_first = 0, brick_levels = 0, n_bricks = 0, brick_cells = 8, bricks_per_dim = 0, brick_vb0 = 0;  // levels [first, levels)
-	uint32_t stage0 = 1;  // row kernel: level 0's table staged in LDS when dense and <= 32 KB
+	uint32_t stage0 = 0;  // row kernel: level 0's table staged in LDS when dense and <= 32 KB
 };
 
 // mode: 0/1 per-sample kernels, 2 XCD-partitioned (level, chunk) kernel (L2-local tables; measured
@@ -184,7 +184,7 @@ template <> struct GridVec<4> { typedef f16x4 T; typedef f16 __attribute__((ext_
 template <> struct GridVec<8> { typedef f16x8 T; typedef f16x8 P; };
 
 #ifndef NGP_GATHER16
-#define NGP_GATHER16 1  // F = 2 gathers by aligned 16-B groups (gather_pairs_f2)
+#define NGP_GATHER16 0  // 1: F = 2 gathers by aligned 16-B groups (gather_pairs_f2; measured slower at C2')
 #endif
 template <uint32_t D>
 __device__ __forceinline__ void gather_pairs_f2(const uint32_t* idx, const f16* __restrict__ table, f16x2* v);
@@ -325,8 +325,8 @@ __device__ __forceinline__ uint32_t brick_of(const GridConst& c, uint32_t f, uin
 }
 
 // Histogram add of one corner's bucket j (< 2^few_bits buckets in the level, few_bits <= 4): the lanes with
-// the same bucket are found with ballots and their leader adds their count once. C2's coarse levels have 2
-// and 16 buckets, so a plain per-lane LDS atomic serialised up to 64 lanes on one counter per corner.
+// the same bucket are found with ballots and their leader adds their count once (k_sc_hist; the forward's
+// fused histogram keeps per-lane atomics, where the ballots measured no faster).
 __device__ __forceinline__ void hist_add(uint32_t* h, uint32_t j, uint32_t few_bits) {
 	if (few_bits > 4) { atomicAdd(&h[j], 1u); return; }
 	uint64_t peers = __ballot(1);

@@ -163,18 +163,13 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 		for (uint32_t f = 0; f < F; ++f) acc[f] = 0.f;
 		const bool active = l < c.n_levels && !((float)l >= ml + 1e-3f);
 		const bool count = HIST && !(l >= h.brick_first && l < h.brick_levels);  // brick levels: counted once per sample above
-		uint32_t few_bits = 32;
-		if constexpr (HIST) {
-			const uint32_t nvb = l < c.n_levels ? h.vb_base[l + 1] - h.vb_base[l] : 0u;
-			few_bits = nvb <= 1 ? 0u : nvb <= 2 ? 1u : nvb <= 4 ? 2u : nvb <= 8 ? 3u : nvb <= 16 ? 4u : 32u;
-		}
 		if (count && l < c.n_levels && !active) {
 			// the backward stages items for masked levels too (with zero values): count them
 			float frac[D]; uint32_t base[D];
 			level_setup<D>(c, l, x, frac, base);
 #pragma unroll
 			for (uint32_t k = 0; k < (1u << D); ++k)
-				hist_add(hl + h.vb_base[l], (corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B, few_bits);
+				atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
 		}
 		if (active) {
 			float frac[D]; uint32_t base[D];
@@ -185,14 +180,14 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 				corner_indices<D>(c, l, base, cidx);
 				if (count) {
 #pragma unroll
-					for (uint32_t k = 0; k < (1u << D); ++k) hist_add(hl + h.vb_base[l], (cidx[k] - c.offsets[l]) >> h.B, few_bits);
+					for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&hl[h.vb_base[l] + ((cidx[k] - c.offsets[l]) >> h.B)], 1u);
 				}
 				gather_corners_at<D, F>(cidx, (STAGE0 && l == 0) ? t0 : a.table, v);
 			} else {
 				if (count) {
 #pragma unroll
 					for (uint32_t k = 0; k < (1u << D); ++k)
-						hist_add(hl + h.vb_base[l], (corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B, few_bits);
+						atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
 				}
 				gather_corners<D, F>(c, l, base, (STAGE0 && l == 0) ? t0 : a.table, v);
 			}
