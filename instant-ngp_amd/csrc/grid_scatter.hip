@@ -48,6 +48,9 @@ namespace {
 #ifndef NGP_SC_FASTIDX
 #define NGP_SC_FASTIDX 1  // scatter: corner indices of an in-range dense cell without a modulo test per corner
 #endif
+#ifndef NGP_SC_PAIR_RANK
+#define NGP_SC_PAIR_RANK 1  // scatter: one rank add per x-edge pair of corners in one bucket (bucket_rank_cnt)
+#endif
 #ifndef NGP_ACC_SKIP0
 #define NGP_ACC_SKIP0 1   // accumulate: skip the LDS atomic of a zero contribution (a branch per feature)
 #endif
@@ -118,6 +121,27 @@ __device__ __forceinline__ uint32_t bucket_rank(uint32_t* lh, uint32_t j, uint32
 	if (lane == leader) base = atomicAdd(&lh[j], (uint32_t)__popcll(peers));
 	base = __shfl(base, leader);
 	return base + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+}
+
+// The same for cnt (0, 1 or 2) consecutive items of bucket j: the first of their ranks. The two corners of an
+// x-edge usually share a bucket (adjacent entries on a dense level; entries i and i ^ 1 on a hashed level
+// with even base x), so the scatter ranks them with one add of 2 instead of two adds of 1.
+__device__ __forceinline__ uint32_t bucket_rank_cnt(uint32_t* lh, uint32_t j, uint32_t cnt, uint32_t few_bits) {
+	if (few_bits > 4) return cnt ? atomicAdd(&lh[j], cnt) : 0u;
+	uint64_t peers = __ballot(cnt != 0);
+	if (peers == 0ull) return 0u;  // wave-uniform
+	for (uint32_t b = 0; b < few_bits; ++b) {
+		const uint64_t m = __ballot((j >> b) & 1u);
+		peers &= ((j >> b) & 1u) ? m : ~m;
+	}
+	const uint64_t two = __ballot(cnt == 2);
+	const uint32_t lane = __lane_id();
+	const uint32_t leader = peers ? (uint32_t)(__ffsll((unsigned long long)peers) - 1) : lane;
+	uint32_t base = 0;
+	if (cnt && lane == leader) base = atomicAdd(&lh[j], (uint32_t)(__popcll(peers) + __popcll(peers & two)));
+	base = __shfl(base, leader);
+	const uint64_t below = peers & ((1ull << lane) - 1ull);
+	return base + (uint32_t)(__popcll(below) + __popcll(below & two));
 }
 
 template <uint32_t D>
@@ -486,7 +510,18 @@ __global__ void __launch_bounds__(SC_ST) k_sc_scatter(const GridConst c, const L
 #else
 			e[q][k] = corner_index<D>(c, l, base, k) - off_l;
 #endif
+#if NGP_SC_PAIR_RANK
+			if (k & 1u) {  // ranks of the x-edge pair (k - 1, k)
+				const uint32_t j0 = e[q][k - 1] >> B, j1 = e[q][k] >> B;
+				const bool same = j0 == j1;
+				const uint32_t r0 = bucket_rank_cnt(lh, j0, same ? 2u : 1u, few_bits);
+				const uint32_t r1 = bucket_rank_cnt(lh, j1, same ? 0u : 1u, few_bits);
+				r[q][k - 1] = r0;
+				r[q][k] = same ? r0 + 1u : r1;
+			}
+#else
 			r[q][k] = bucket_rank(lh, e[q][k] >> B, few_bits);
+#endif
 			const float w = corner_weight<D>(frac, k);
 			if constexpr (F == 1) val[q][k] = to_f16(w * g[0]);
 			else {
