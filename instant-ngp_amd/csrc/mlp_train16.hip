@@ -431,6 +431,14 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 	T16_MARK(2);
 	[[maybe_unused]] uint32_t it = 0;
 
+#ifndef NGP_T16_SH_AHEAD
+#define NGP_T16_SH_AHEAD 0  // 1: the next tile's SH computed in the dW phase (VALU idle there, LDS-bound)
+#endif
+	f16x4 sh_next{};  // NGP_T16_SH_AHEAD: SH of this lane's sample in the next tile
+	if constexpr (NGP_T16_SH_AHEAD) {
+		const uint32_t s0 = (blockIdx.x * 4 + pair) * 32 + 16 * half + sn;
+		if (s0 < a.n) sh_next = sh4_quad(pf[0].cd[0], pf[0].cd[1], pf[0].cd[2], g);
+	}
 	for (uint32_t base = blockIdx.x * 4; base < n_tiles; base += gridDim.x * 4) {
 		const uint32_t tile = base + pair;
 		const uint32_t sample = tile * 32 + 16 * half + sn;
@@ -470,7 +478,7 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		}
 		f32x4 dacc = mma32(wdo[1], hd[DH - 1][1], mma32(wdo[0], hd[DH - 1][0], f32x4{0.f, 0.f, 0.f, 0.f}));
 		const f16x4 dout = pack4(dacc, false);                                          // density network output rows 4g..4g+3
-		const f16x4 sh = valid ? sh4_quad(cdx, cdy, cdz, g) : f16x4{};
+		const f16x4 sh = NGP_T16_SH_AHEAD ? sh_next : (valid ? sh4_quad(cdx, cdy, cdz, g) : f16x4{});
 		const f16x8 rin = cat(dout, sh);                                                // [density out | SH], permuted k
 		T16_IT(2);
 #pragma unroll
@@ -599,6 +607,10 @@ __global__ void __launch_bounds__(512, 1) __attribute__((amdgpu_waves_per_eu(2, 
 		T16_IT(8);
 		__syncthreads();
 		T16_IT(9);
+		if constexpr (NGP_T16_SH_AHEAD) {  // pf[0] holds the next tile's inputs (requested at this iteration's start)
+			const uint32_t s1 = (tile + gridDim.x * 4) * 32 + 16 * half + sn;
+			sh_next = s1 < a.n ? sh4_quad(pf[0].cd[0], pf[0].cd[1], pf[0].cd[2], g) : f16x4{};
+		}
 
 		// ---- dW over the four pair images (K = 32 samples per MFMA), images in a fixed order ---------
 #ifndef NGP_T16_SKIP_B
