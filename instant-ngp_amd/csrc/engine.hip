@@ -168,7 +168,7 @@ struct ngp_model {
 	bool fuse_infer = true;                 // option "fuse_infer": NerfNetwork inference encodes inside the MLP kernel
 	bool fuse_slabs = true;                 // option "fuse_slabs": dW slab reduction inside the grid backward's last kernel
 	bool fuse_opt = true;                   // option "fuse_opt": lazy-layout optimizer update inside the grid backward (training_step)
-	bool mlp_train16 = true;                // option "mlp_train16": the training MLP at two waves per SIMD (mlp_train16.hip)
+	bool mlp_train16 = false;               // option "mlp_train16": the training MLP at two waves per SIMD (mlp_train16.hip; off: no faster at C2, 3x slower at C2p)
 	bool grid_stage0 = false;               // option "grid_stage0": the training forward stages level 0 in LDS (grid.hip STAGE0; off: measured slower)
 	bool grid_bricks = false;               // option "grid_bricks": dense levels of the bucketed backward summed per brick (off: measured slower)
 	bool fuse_train = false;                // option "fuse_train": ... and the training forward_backward too (off: the

@@ -49,7 +49,7 @@ namespace {
 #define NGP_SC_FASTIDX 1  // scatter: corner indices of an in-range dense cell without a modulo test per corner
 #endif
 #ifndef NGP_SC_PAIR_RANK
-#define NGP_SC_PAIR_RANK 0  // 1: scatter ranks an x-edge pair of corners in one bucket with one add (bucket_rank_cnt)
+#define NGP_SC_PAIR_RANK 1  // scatter: one rank add per x-edge pair of corners in one bucket (bucket_rank_cnt; C2 backward -2.2 us)
 #endif
 #ifndef NGP_ACC_SKIP0
 #define NGP_ACC_SKIP0 1   // accumulate: skip the LDS atomic of a zero contribution (a branch per feature)

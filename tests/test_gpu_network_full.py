@@ -82,8 +82,8 @@ def check_close(name, got, ref, cond, margin=None):
 @pytest.mark.parametrize("train16", [1, 0])
 @pytest.mark.parametrize("cfg_name,log2T,L,F", [("C2", 19, 4, 4), ("C2p", 19, 16, 2)])
 def test_nerf_network_full_batch(pkg, orc, cfg_name, log2T, L, F, train16, record_property):
-    """train16 = 1: the two-waves-per-SIMD training kernel (mlp_train16.hip, the default for C2 and C2');
-    0: k_nerf_mlp_train (mlp.hip), kept for the configurations the former does not cover."""
+    """train16 = 1: the two-waves-per-SIMD training kernel (mlp_train16.hip, option mlp_train16);
+    0: k_nerf_mlp_train (mlp.hip), the default."""
     cfg = pkg.nerf_config(cfg_name)
     cfg["encoding"]["log2_hashmap_size"] = log2T
     net = pkg.create_nerf_network(cfg)

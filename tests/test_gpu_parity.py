@@ -313,6 +313,7 @@ def test_large_batch_properties(pkg, nerf_setup):
     dL = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
     dL[:, :4] = (torch.rand((n, 4), device="cuda") - 0.5).half() * 0.01
     out = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
+    net.set_option("mlp_train16", 1)  # the two-waves-per-SIMD kernel (option, off by default)
     net.forward_backward(c, dL, output=out)
     g1 = tr.gradients.float().clone()
     net.forward_backward(c, dL * 2, output=out)
@@ -326,9 +327,8 @@ def test_large_batch_properties(pkg, nerf_setup):
     # products in different groupings: outputs agree to the fp16 rounding of the intermediates, and the
     # k_nerf_mlp_train kernel (the inference kernel's layout) reproduces the inference output bit for bit
     assert torch.allclose(out.float(), ref_out.float(), rtol=1e-2, atol=2e-3)
-    net.set_option("mlp_train16", 0)
+    net.set_option("mlp_train16", 0)  # the default kernel
     net.forward_backward(c, dL, output=out)
-    net.set_option("mlp_train16", 1)
     torch.cuda.synchronize()
     assert torch.equal(ref_out, out)
 
@@ -454,7 +454,6 @@ def test_fused_encoding_training_matches_unfused(pkg, nerf_setup, n):
         torch.cuda.synchronize()
         res[fuse] = (out.clone(), tr.gradients.clone())
     net.set_option("fuse_train", 0)
-    net.set_option("mlp_train16", 1)
     nm = net.n_matrix_params
     assert torch.equal(res[1][0], res[0][0])
     assert torch.equal(res[1][1][:nm], res[0][1][:nm])

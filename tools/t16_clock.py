@@ -26,7 +26,7 @@ def main():
     from __graft_entry__ import load_package
     pkg = load_package()
     n = bench.B
-    step, _, net, trainer, _ = bench.nerf_pass(pkg, args.variant, n, 0, 1)
+    step, _, net, trainer, _ = bench.nerf_pass(pkg, args.variant, n, 0, 1, opts=("mlp_train16=1",))
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
