@@ -398,6 +398,9 @@ constexpr uint32_t RG = NGP_SAMPLER_RG;  // lanes per ray (16 = one DPP row)
 #ifndef NGP_SAMPLER_ROUND_CAP
 #define NGP_SAMPLER_ROUND_CAP 1  // verify rounds per march iteration (0: until every lane is verified)
 #endif
+#ifndef NGP_SAMPLER_PRIO
+#define NGP_SAMPLER_PRIO 0  // s_setprio of the cone-stepping count pass (it shares the SIMDs with the training pass)
+#endif
 #ifndef NGP_SAMPLER_END_CONE
 #define NGP_SAMPLER_END_CONE 0  // sampling_end under cone stepping (off: measured slower with the speculative march)
 #endif
@@ -608,6 +611,7 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t i = gid / RG, L = gid % RG;
 	if (i >= a.n_rays) return;  // whole rows
+	if (!CONE0 && NGP_SAMPLER_PRIO) __builtin_amdgcn_s_setprio(NGP_SAMPLER_PRIO);
 	SAMPLER_STAT(const unsigned long long ck0 = sampler_clock();)
 	const RaySetup r = setup_ray(cams, pixels, n_images, cfg, i + a.ray_offset, a.n_rays_total_for_image_idx, a.rng, cone);
 	SAMPLER_STAT(const unsigned long long ck1 = sampler_clock(); unsigned long long ck2 = ck1, ck_g = 0, ck_o = 0, ck_q = 0;)
