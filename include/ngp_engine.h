@@ -338,6 +338,15 @@ int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg
                           const void* network_output, const uint32_t* ray_indices, const float* rays, uint32_t* numsteps,
                           const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
                           uint32_t* compacted_counter, const float* mean_density, float loss_scale);
+/* The same with the training error map (testbed_nerf.cu:1869-1899, the kernel's error_map argument): every
+ * compacted ray adds its mean loss, split bilinearly around uv * res - 0.5, into error_map
+ * [n_images][em_height][em_width] (device floats, float atomics as in the reference). */
+int ngp_nerf_compute_loss_error_map(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
+                                    uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted,
+                                    const uint32_t* ray_counter, const void* network_output, const uint32_t* ray_indices,
+                                    const float* rays, uint32_t* numsteps, const float* coords_in, float* coords_out,
+                                    void* dloss_doutput, float* loss, uint32_t* compacted_counter, const float* mean_density,
+                                    float loss_scale, float* error_map, uint32_t em_width, uint32_t em_height);
 /* tcnn fill_rollover / fill_rollover_and_rescale (testbed_nerf.cu:4061-4069); dtype 0 f32, 1 f16 */
 int ngp_nerf_fill_rollover(void* stream, uint32_t n_elements, uint32_t stride, const uint32_t* n_input, void* data,
                            int dtype, int rescale);
@@ -402,6 +411,24 @@ int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint3
 // grid or bitfield between steps (ngp_nerf_trainer_buffers discards a prelaunched sampler). No reference counterpart (the
 // Testbed runs the step serially, testbed_nerf.cu:3867-4132).
 int ngp_nerf_trainer_set_pipeline(ngp_nerf_trainer* t, int enable);
+
+/* The training error map (Testbed::Nerf::Training::ErrorMap, testbed.h:668-677, 736-738). Every step
+ * deposits the compacted rays' losses into it (accumulate_error, testbed_nerf.cu:3951-3953, 4044); it is
+ * zeroed and resized to min(3.5 (n_steps_between * rays_per_batch / n_images)^(1/4), image size) when a
+ * window starts (:3659-3666), and after n_steps_between steps its CDFs are built (construct_cdf_2d/1d and
+ * the host pass over the per-image totals, :3700-3748) and the window grows by 1.5x. which: 0 data
+ * [n_images][height][width], 1 cdf_x_cond_y (cdf resolution), 2 cdf_y [n_images][cdf_height], 3 cdf_img
+ * [n_images] (the normalised image CDF), 4 pmf_img [n_images] (host). Copies min(cap, size) floats to
+ * host memory `out` (NULL: only *info) after the trainer's stream work. */
+typedef struct {
+	uint32_t width, height;          /* error_map.resolution */
+	uint32_t cdf_width, cdf_height;  /* error_map.cdf_resolution */
+	uint32_t n_images;
+	uint32_t cdf_valid;              /* error_map.is_cdf_valid */
+	uint32_t n_steps_since_update, n_steps_between_updates;
+	uint64_t size;                   /* floats held by the requested array */
+} ngp_nerf_error_map_info;
+int ngp_nerf_trainer_error_map(ngp_nerf_trainer* t, int which, float* out, uint64_t cap, ngp_nerf_error_map_info* info);
 
 /* Snapshots (Testbed::save_snapshot / load_snapshot, src/testbed.cu:4873-5057; python_api.cu:446-447):
  * msgpack of the network config (network_config_json, the Testbed's m_network_config; NULL = {}) with

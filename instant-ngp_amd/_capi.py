@@ -64,6 +64,12 @@ class NerfStats(C.Structure):
                 ("measured_batch_size_before_compaction", C.c_uint32), ("loss", C.c_float)]
 
 
+class NerfErrorMapInfo(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("cdf_width", C.c_uint32), ("cdf_height", C.c_uint32),
+                ("n_images", C.c_uint32), ("cdf_valid", C.c_uint32), ("n_steps_since_update", C.c_uint32),
+                ("n_steps_between_updates", C.c_uint32), ("size", C.c_uint64)]
+
+
 P = C.c_void_p
 u32, u64, f32, i32, sz = C.c_uint32, C.c_uint64, C.c_float, C.c_int, C.c_size_t
 
@@ -147,6 +153,8 @@ SIGNATURES = {
                                                  P]),
     "ngp_nerf_compute_loss": (i32, [P, C.POINTER(NerfConfig), P, u32, u32, Rng, u32, P, P, P, P, P, P, P, P, P, P, P,
                                     f32]),
+    "ngp_nerf_compute_loss_error_map": (i32, [P, C.POINTER(NerfConfig), P, u32, u32, Rng, u32, P, P, P, P, P, P, P, P,
+                                              P, P, P, f32, P, u32, u32]),
     "ngp_nerf_fill_rollover": (i32, [P, u32, u32, P, P, i32, i32]),
     "ngp_nerf_grid_generate_samples": (i32, [P, C.POINTER(NerfConfig), u32, Rng, u32, P, u32, f32, P, P]),
     "ngp_nerf_grid_splat_max": (i32, [P, u32, P, P, u32, P]),
@@ -160,6 +168,7 @@ SIGNATURES = {
     "ngp_nerf_trainer_buffers": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
     "ngp_nerf_trainer_buffers_read": (i32, [P, C.POINTER(P), C.POINTER(P), C.POINTER(P)]),
     "ngp_nerf_trainer_set_pipeline": (i32, [P, i32]),
+    "ngp_nerf_trainer_error_map": (i32, [P, i32, P, u64, C.POINTER(NerfErrorMapInfo)]),
     "ngp_nerf_trainer_set_data_parallel": (i32, [P, u32, u32, P, P]),
     "ngp_nerf_save_snapshot": (i32, [P, P, C.c_char_p, C.c_char_p, i32, i32]),
     "ngp_nerf_load_snapshot": (i32, [P, P, C.c_char_p]),

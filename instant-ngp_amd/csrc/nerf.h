@@ -85,6 +85,10 @@ struct LossArgs {
 	const float* mean_density;    // [1]
 	float loss_scale;
 	float bg[3];
+	// training error map (testbed_nerf.cu:1869-1899): each compacted ray adds its mean loss, bilinearly
+	// split, into [n_images][em_h][em_w] floats; null: off
+	float* error_map;
+	uint32_t em_w, em_h;
 };
 
 // The kernels (each cites its reference kernel in nerf.hip).
@@ -105,6 +109,9 @@ void grid_mean_bitfield(const float* grid, uint32_t max_cascade, float* mean_out
 size_t scan_temp_bytes(uint32_t n);
 size_t sample_tmp_f32(uint32_t n_rays);  // floats of sample_rays' tmp_f32 (stored t per step + ray geometry)
 size_t loss_tmp_f32(uint32_t n_rays);    // floats of compute_loss' tmp_f32 (per-ray pass-1 results)
+// construct_cdf_2d / construct_cdf_1d (testbed_nerf.cu:2356-2410) over the error map
+void error_map_cdfs(uint32_t n_images, uint32_t w, uint32_t h, const float* data, float* cdf_x_cond_y, float* cdf_y,
+                    float* cdf_img, hipStream_t s);
 
 // ---- rendering (NerfTracer) ------------------------------------------------------------------
 struct RenderArgs {

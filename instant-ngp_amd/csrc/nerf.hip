@@ -1037,8 +1037,9 @@ void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs
 
 // ------------------------------------------------------------------------------------------------
 // compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012), split at its atomicAdd into two passes
-// around a prefix scan. Error map / sharpness / envmap / exposure / depth supervision are off in the
-// reference's default training and not implemented.
+// around a prefix scan. The error map deposit (:1869-1899, always on in the reference's training) is
+// done in pass 2 after the compaction early-out, as there; sharpness / envmap / exposure / depth
+// supervision are off in the reference's default training and not implemented.
 // A ray owns one DPP row: lanes load and activate 16 samples at once (network output, dt, exp), and
 // the compositing recurrence (T *= 1 - alpha, rgb += alpha T c) runs over the row in sample order
 // with row_newbcast broadcasts, i.e. with the reference's float ops in the reference's order.
@@ -1047,7 +1048,9 @@ struct LossRay {  // pass-1 results kept for pass 2
 	float grad[3];
 	float rgb_ray[3];
 	float mean_loss;
-	float pad;
+	float u, v;    // the ray's image position and image (the error map deposit)
+	uint32_t img;
+	float pad[2];
 };
 
 __device__ __forceinline__ V3 unwarp_pos(const float* c, const Aabb& b) {
@@ -1187,12 +1190,33 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 	q.mean_loss = (lc + l1 + l2) / 3.0f;
 	q.grad[0] = gc; q.grad[1] = g1; q.grad[2] = g2;
 	q.rgb_ray[0] = pred; q.rgb_ray[1] = p1; q.rgb_ray[2] = p2;
-	q.pad = 0.f;
+	q.u = u; q.v = v; q.img = img;
+	q.pad[0] = q.pad[1] = 0.f;
 	lr[i] = q;
 }
 
-__global__ void __launch_bounds__(256) k_loss_pass2(const ngp_nerf_config cfg, LossArgs a, const uint32_t* __restrict__ craw,
-                                                    const uint32_t* __restrict__ cbase, const LossRay* __restrict__ lr) {
+// error map deposit of one compacted ray (testbed_nerf.cu:1869-1899 without the sharpness factor,
+// include_sharpness_in_error is off by default): mean loss split bilinearly over the 4 texels around
+// uv * res - 0.5, float atomics as in the reference (the map only steers importance sampling)
+__device__ __forceinline__ void deposit_error(const LossArgs& a, const Camera* __restrict__ cams, const LossRay& q) {
+	const float rx = (float)a.em_w, ry = (float)a.em_h;
+	const float px = fminf(fmaxf(q.u * rx - 0.5f, 0.0f), rx - (1.0f + 1e-4f));
+	const float py = fminf(fmaxf(q.v * ry - 0.5f, 0.0f), ry - (1.0f + 1e-4f));
+	const int ix0 = (int)px, iy0 = (int)py;
+	const float wx = px - (float)ix0, wy = py - (float)iy0;
+	// clamp(pos_int, 0, resolution - 2) with the image's resolution, as the reference writes it
+	const int ix = min(max(ix0, 0), (int)cams[q.img].width - 2), iy = min(max(iy0, 0), (int)cams[q.img].height - 2);
+	float* em = a.error_map + (size_t)q.img * a.em_w * a.em_h;
+	const float ml = q.mean_loss;
+	atomicAdd(em + (size_t)iy * a.em_w + ix, (1 - wx) * (1 - wy) * ml);
+	atomicAdd(em + (size_t)iy * a.em_w + ix + 1, wx * (1 - wy) * ml);
+	atomicAdd(em + (size_t)(iy + 1) * a.em_w + ix, (1 - wx) * wy * ml);
+	atomicAdd(em + (size_t)(iy + 1) * a.em_w + ix + 1, wx * wy * ml);
+}
+
+__global__ void __launch_bounds__(256) k_loss_pass2(const Camera* __restrict__ cams, const ngp_nerf_config cfg, LossArgs a,
+                                                    const uint32_t* __restrict__ craw, const uint32_t* __restrict__ cbase,
+                                                    const LossRay* __restrict__ lr) {
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t i = gid / LG, L = gid % LG;
 	if (gid == 0) *a.compacted_counter = cbase[a.n_rays - 1] + craw[a.n_rays - 1];
@@ -1208,6 +1232,7 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const ngp_nerf_config cfg, L
 	if (cn == 0) return;
 	const LossRay q = lr[i];
 	if (L == 0 && a.loss) a.loss[i] = q.mean_loss / (float)a.n_rays;  // written after the compaction early-out (:1836-1866)
+	if (L == 0 && a.error_map) deposit_error(a, cams, q);
 	const float loss_scale = a.loss_scale / (float)a.n_rays;
 	const float output_l2_reg = cfg.rgb_activation == ACT_EXP ? 1e-4f : 0.0f;
 	const float output_l1_reg_density = *a.mean_density < MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
@@ -1319,7 +1344,49 @@ void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs&
 		exclusive_scan(craw, cbase, a.n_rays, scan_tmp, scan_bytes, s);
 	}
 	ProfScope ps("loss_pass2", s);
-	k_loss_pass2<<<blocks, 256, 0, s>>>(cfg, a, craw, cbase, lr);
+	k_loss_pass2<<<blocks, 256, 0, s>>>(ds.d_cams, cfg, a, craw, cbase, lr);
+	NGP_HIP(hipGetLastError());
+}
+
+// construct_cdf_2d (testbed_nerf.cu:2356-2382): one thread per (image, row), running sums along x
+constexpr float ERROR_MAP_MIN_PDF = 0.01f;
+__global__ void k_cdf_2d(uint32_t n_images, uint32_t h, uint32_t w, const float* __restrict__ data, float* __restrict__ cdf_x_cond_y,
+                         float* __restrict__ cdf_y) {
+	const uint32_t y = blockIdx.x * blockDim.x + threadIdx.x, img = blockIdx.y;
+	if (y >= h || img >= n_images) return;
+	const size_t off = ((size_t)img * h + y) * w;
+	float cum = 0.f;
+	for (uint32_t x = 0; x < w; ++x) {
+		cum += data[off + x] + 1e-10f;
+		cdf_x_cond_y[off + x] = cum;
+	}
+	cdf_y[(size_t)img * h + y] = cum;
+	const float norm = 1.0f / cum;  // __frcp_rn: the correctly rounded reciprocal
+	for (uint32_t x = 0; x < w; ++x)
+		cdf_x_cond_y[off + x] = (1.0f - ERROR_MAP_MIN_PDF) * cdf_x_cond_y[off + x] * norm + ERROR_MAP_MIN_PDF * (float)(x + 1) / (float)w;
+}
+// construct_cdf_1d (:2384-2410): one thread per image, running sums over the rows' totals
+__global__ void k_cdf_1d(uint32_t n_images, uint32_t h, float* __restrict__ cdf_y, float* __restrict__ cdf_img) {
+	const uint32_t img = blockIdx.x * blockDim.x + threadIdx.x;
+	if (img >= n_images) return;
+	float* c = cdf_y + (size_t)img * h;
+	float cum = 0.f;
+	for (uint32_t y = 0; y < h; ++y) {
+		cum += c[y];
+		c[y] = cum;
+	}
+	cdf_img[img] = cum;
+	const float norm = 1.0f / cum;
+	for (uint32_t y = 0; y < h; ++y) c[y] = (1.0f - ERROR_MAP_MIN_PDF) * c[y] * norm + ERROR_MAP_MIN_PDF * (float)(y + 1) / (float)h;
+}
+
+void error_map_cdfs(uint32_t n_images, uint32_t w, uint32_t h, const float* data, float* cdf_x_cond_y, float* cdf_y,
+                    float* cdf_img, hipStream_t s) {
+	if (!n_images || !w || !h) return;
+	ProfScope ps("nerf_error_map_cdf", s);
+	k_cdf_2d<<<dim3(div_round_up(h, 64u), n_images), 64, 0, s>>>(n_images, h, w, data, cdf_x_cond_y, cdf_y);
+	NGP_HIP(hipGetLastError());
+	k_cdf_1d<<<div_round_up(n_images, 64u), 64, 0, s>>>(n_images, h, cdf_y, cdf_img);
 	NGP_HIP(hipGetLastError());
 }
 

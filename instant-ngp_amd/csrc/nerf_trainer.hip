@@ -145,6 +145,12 @@ struct ngp_nerf_trainer {
 	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens;
 	// training workspaces
 	Buf ray_indices, rays, numsteps, coords, mlp_out, dloss, coords_c, loss, counters, scan_tmp, tmp_u32, tmp_f32;
+	// training error map (Testbed::Nerf::Training::ErrorMap and its update window, testbed.h:668-677, 736-738)
+	Buf em_data, em_cdf_x, em_cdf_y, em_cdf_img;
+	uint32_t em_w = 0, em_h = 0, em_cdf_w = 0, em_cdf_h = 0;
+	uint32_t em_steps_since = 0, em_steps_between = 128;
+	bool em_cdf_valid = false;
+	std::vector<float> em_pmf_img;  // pmf_img_cpu
 };
 
 static hipStream_t S(void* s) { return (hipStream_t)s; }
@@ -305,7 +311,8 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
                              uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
                              const void* network_output, uint32_t out_stride, const uint32_t* ray_indices, const float* rays,
                              uint32_t* numsteps, const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
-                             uint32_t* compacted_counter, const float* mean_density, float loss_scale, bool zero_loss = false);
+                             uint32_t* compacted_counter, const float* mean_density, float loss_scale, bool zero_loss = false,
+                             float* error_map = nullptr, uint32_t em_w = 0, uint32_t em_h = 0);
 
 int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
                           uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
@@ -317,11 +324,24 @@ int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg
 	                         loss_scale);
 }
 
+int ngp_nerf_compute_loss_error_map(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
+                                    uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted,
+                                    const uint32_t* ray_counter, const void* network_output, const uint32_t* ray_indices,
+                                    const float* rays, uint32_t* numsteps, const float* coords_in, float* coords_out,
+                                    void* dloss_doutput, float* loss, uint32_t* compacted_counter, const float* mean_density,
+                                    float loss_scale, float* error_map, uint32_t em_width, uint32_t em_height) {
+	if (error_map && (em_width < 2 || em_height < 2)) return NGP_INVALID;  // the bilinear deposit needs a 2x2 texel block
+	return nerf_compute_loss(ds, cfg, stream, n_rays, n_rays_total, rng, max_samples_compacted, ray_counter, network_output, 16,
+	                         ray_indices, rays, numsteps, coords_in, coords_out, dloss_doutput, loss, compacted_counter, mean_density,
+	                         loss_scale, false, error_map, em_width, em_height);
+}
+
 static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
                              uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
                              const void* network_output, uint32_t out_stride, const uint32_t* ray_indices, const float* rays,
                              uint32_t* numsteps, const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
-                             uint32_t* compacted_counter, const float* mean_density, float loss_scale, bool zero_loss) {
+                             uint32_t* compacted_counter, const float* mean_density, float loss_scale, bool zero_loss,
+                             float* error_map, uint32_t em_w, uint32_t em_h) {
 	if (!ds || !cfg || !ray_counter || !network_output || !numsteps || !coords_in || !coords_out || !dloss_doutput ||
 	    !compacted_counter || !mean_density)
 		return NGP_INVALID;
@@ -333,6 +353,7 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
 		a.ray_indices = ray_indices; a.rays = rays; a.numsteps = numsteps; a.coords_in = coords_in; a.coords_out = coords_out;
 		a.dloss_doutput = (f16*)dloss_doutput; a.loss = loss; a.compacted_counter = compacted_counter;
 		a.mean_density = mean_density; a.loss_scale = loss_scale; a.zero_loss = zero_loss;
+		a.error_map = error_map; a.em_w = em_w; a.em_h = em_h;
 		if (n_rays == 0) { NGP_HIP(hipMemsetAsync(compacted_counter, 0, 4, S(stream))); return NGP_OK; }
 		static thread_local Buf scan, tmp, tmpf;
 		const size_t sb = scan_temp_bytes(n_rays);
@@ -649,6 +670,90 @@ static bool density_grid_update_due(uint32_t step) {
 	return step % skip == 0;
 }
 
+// Testbed::train_nerf's error map window (testbed_nerf.cu:3659-3666): at its first step the map is
+// resized to min(3.5 (n_steps_between * rays_per_batch / n_images)^(1/4), image 0's size) per image and
+// zeroed (uint32 arithmetic as in the reference). Returns the map the step's loss pass deposits into.
+static float* error_map_window(ngp_nerf_trainer* t, hipStream_t s) {
+	const Dataset& ds = t->data->ds;
+	if (ds.n_images == 0 || ds.cams.empty()) return nullptr;
+	if (t->em_steps_since == 0) {
+		const uint32_t n_samples_per_image = (t->em_steps_between * t->rays_per_batch) / ds.n_images;
+		const int k = (int)(std::sqrt(std::sqrt((float)n_samples_per_image)) * 3.5f);
+		t->em_w = (uint32_t)std::min(k, (int)ds.cams[0].width);
+		t->em_h = (uint32_t)std::min(k, (int)ds.cams[0].height);
+		const size_t n = (size_t)t->em_w * t->em_h * ds.n_images;
+		NGP_HIP(hipMemsetAsync(t->em_data.get<float>(std::max<size_t>(n, 1)), 0, n * sizeof(float), s));
+	}
+	return t->em_w >= 2 && t->em_h >= 2 ? (float*)t->em_data.p : nullptr;
+}
+
+// After the step (testbed_nerf.cu:3700-3748): when the window is full, the CDFs of the map
+// (construct_cdf_2d/1d on the stream; with data parallelism the ranks' maps are summed first), the
+// host pass over the per-image totals, then a 1.5x longer window.
+static void error_map_step_done(ngp_nerf_trainer* t, hipStream_t s) {
+	const Dataset& ds = t->data->ds;
+	if (ds.n_images == 0 || ds.cams.empty()) return;
+	t->em_steps_since += 1;
+	if (t->em_steps_since < t->em_steps_between) return;
+	t->em_cdf_w = t->em_w;
+	t->em_cdf_h = t->em_h;
+	const uint32_t n_img = ds.n_images, w = t->em_cdf_w, h = t->em_cdf_h;
+	float* data = (float*)t->em_data.p;
+	if (t->dp() && data && w && h)
+		NGP_CHECK(t->allreduce(t->allreduce_user, data, (uint64_t)w * h * n_img, NGP_DTYPE_F32, NGP_REDUCE_SUM, s) == 0,
+		          "data parallel: error map all-reduce failed");
+	float* cdf_x = t->em_cdf_x.get<float>(std::max<size_t>((size_t)w * h * n_img, 1));
+	float* cdf_y = t->em_cdf_y.get<float>(std::max<size_t>((size_t)h * n_img, 1));
+	float* cdf_img = t->em_cdf_img.get<float>(n_img);
+	error_map_cdfs(n_img, w, h, data, cdf_x, cdf_y, cdf_img, s);
+	// the image CDF on the host (single-threaded in the reference too)
+	std::vector<float> pmf(n_img), cdf(n_img);
+	NGP_HIP(hipMemcpyAsync(pmf.data(), cdf_img, n_img * sizeof(float), hipMemcpyDeviceToHost, s));
+	NGP_HIP(hipStreamSynchronize(s));
+	float cum = 0.f;
+	for (uint32_t i = 0; i < n_img; ++i) cdf[i] = cum += pmf[i];
+	const float norm = 1.0f / cum;
+	constexpr float MIN_PMF = 0.1f;
+	for (uint32_t i = 0; i < n_img; ++i) {
+		pmf[i] = (1.0f - MIN_PMF) * pmf[i] * norm + MIN_PMF / (float)n_img;
+		cdf[i] = (1.0f - MIN_PMF) * cdf[i] * norm + MIN_PMF * (float)(i + 1) / (float)n_img;
+	}
+	NGP_HIP(hipMemcpyAsync(cdf_img, cdf.data(), n_img * sizeof(float), hipMemcpyHostToDevice, s));
+	NGP_HIP(hipStreamSynchronize(s));
+	t->em_pmf_img = std::move(pmf);
+	t->em_steps_since = 0;
+	t->em_cdf_valid = true;
+	t->em_steps_between = (uint32_t)(t->em_steps_between * 1.5f);
+}
+
+int ngp_nerf_trainer_error_map(ngp_nerf_trainer* t, int which, float* out, uint64_t cap, ngp_nerf_error_map_info* info) {
+	if (!t || which < 0 || which > 4) return NGP_INVALID;
+	NERF_TRY({
+		const uint32_t n_img = t->data->ds.n_images;
+		const uint64_t sizes[5] = {(uint64_t)t->em_w * t->em_h * n_img, (uint64_t)t->em_cdf_w * t->em_cdf_h * n_img,
+		                           (uint64_t)t->em_cdf_h * n_img, t->em_cdf_valid ? n_img : 0u, t->em_pmf_img.size()};
+		const void* src[5] = {t->em_data.p, t->em_cdf_x.p, t->em_cdf_y.p, t->em_cdf_img.p, t->em_pmf_img.data()};
+		if (info) {
+			info->width = t->em_w; info->height = t->em_h;
+			info->cdf_width = t->em_cdf_w; info->cdf_height = t->em_cdf_h;
+			info->n_images = n_img;
+			info->cdf_valid = t->em_cdf_valid ? 1u : 0u;
+			info->n_steps_since_update = t->em_steps_since;
+			info->n_steps_between_updates = t->em_steps_between;
+			info->size = sizes[which];
+		}
+		const uint64_t n = std::min(cap, sizes[which]);
+		if (out && n) {
+			if (which == 4) {
+				memcpy(out, src[4], n * sizeof(float));
+			} else {
+				NGP_HIP(hipDeviceSynchronize());
+				NGP_HIP(hipMemcpy(out, src[which], n * sizeof(float), hipMemcpyDeviceToHost));
+			}
+		}
+	});
+}
+
 int ngp_nerf_trainer_set_pipeline(ngp_nerf_trainer* t, int enable) {
 	if (!t) return NGP_INVALID;
 	NERF_TRY({
@@ -706,10 +811,12 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		}
 		const bool dp = t->dp();
 		const float loss_scale_local = 128.0f * (float)Rl / (float)R;
+		float* error_map = error_map_window(t, s);
 		{
 		ProfScope ps("nerf_loss", s);
 		check_rc(nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, 4, ray_indices, rays, numsteps, coords, coords_c,
-		                               dloss, loss, ctr + 2, (const float*)t->mean.p, dp ? loss_scale_local : 128.0f, true));
+		                               dloss, loss, ctr + 2, (const float*)t->mean.p, dp ? loss_scale_local : 128.0f, true,
+		                               error_map, t->em_w, t->em_h));
 		fill_rollover_pair(Bl, ctr + 2, dloss, 16, coords_c, 7, s);  // fill_rollover_and_rescale + fill_rollover
 		}
 		// the step's counters are final here (the training pass does not touch them): publish them before
@@ -807,6 +914,7 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			uint32_t r = (uint32_t)((float)t->rays_per_batch * (float)B / (float)t->measured_batch_size);
 			t->rays_per_batch = std::min(next_multiple(r, 256), 1u << 18);
 		}
+		error_map_step_done(t, s);
 		// next step's sampler, concurrent with this step's training pass (no density-grid update due first)
 		if (can_pipeline && t->measured_batch_size > 0 && !density_grid_update_due(t->training_step)) {
 			const SamplePlan np = sample_plan(t);

@@ -13,7 +13,7 @@ import os
 import numpy as np
 import torch
 
-from ._capi import NerfConfig, NerfImage, NerfStats, Rng, check, lib
+from ._capi import NerfConfig, NerfErrorMapInfo, NerfImage, NerfStats, Rng, check, lib
 from .network import _ptr, _stream, wrap_device
 
 NERF_GRIDSIZE = 128
@@ -135,9 +135,10 @@ def generate_training_samples(ds, cfg, n_rays, rng, max_samples, bitfield, ray_o
 
 
 def compute_loss(ds, cfg, n_rays, rng, max_compacted, samples, network_output, mean_density, loss_scale=128.0,
-                 n_rays_total=None, stream=None):
+                 n_rays_total=None, stream=None, error_map=None):
     """compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012). `samples` is the dict returned by
-    generate_training_samples (its numsteps is rewritten to the compacted {n, base})."""
+    generate_training_samples (its numsteps is rewritten to the compacted {n, base}). error_map: a
+    float32 device tensor [n_images, h, w] the compacted rays' losses are added into (:1869-1899)."""
     dev = network_output.device
     # the kernel reads one output row per sample; samples never exceed the sampler's coords buffer
     if network_output.shape[0] < samples["coords"].shape[0]:
@@ -149,11 +150,16 @@ def compute_loss(ds, cfg, n_rays, rng, max_compacted, samples, network_output, m
         "loss": torch.zeros(n_rays, dtype=torch.float32, device=dev),
         "compacted_counter": torch.zeros(1, dtype=torch.int32, device=dev),
     }
-    check(lib().ngp_nerf_compute_loss(
-        ds.handle, C.byref(cfg), _stream(stream), n_rays, n_rays_total or n_rays, rng, max_compacted,
-        _ptr(samples["counters"]), _ptr(network_output), _ptr(samples["ray_indices"]), _ptr(samples["rays"]),
-        _ptr(samples["numsteps"]), _ptr(samples["coords"]), _ptr(out["coords_compacted"]), _ptr(out["dloss_doutput"]),
-        _ptr(out["loss"]), _ptr(out["compacted_counter"]), _ptr(mean_density), float(loss_scale)))
+    args = (ds.handle, C.byref(cfg), _stream(stream), n_rays, n_rays_total or n_rays, rng, max_compacted,
+            _ptr(samples["counters"]), _ptr(network_output), _ptr(samples["ray_indices"]), _ptr(samples["rays"]),
+            _ptr(samples["numsteps"]), _ptr(samples["coords"]), _ptr(out["coords_compacted"]), _ptr(out["dloss_doutput"]),
+            _ptr(out["loss"]), _ptr(out["compacted_counter"]), _ptr(mean_density), float(loss_scale))
+    if error_map is None:
+        check(lib().ngp_nerf_compute_loss(*args))
+    else:
+        if error_map.dtype != torch.float32 or error_map.dim() != 3 or not error_map.is_contiguous():
+            raise ValueError("error_map: a contiguous float32 tensor [n_images, h, w]")
+        check(lib().ngp_nerf_compute_loss_error_map(*args, _ptr(error_map), error_map.shape[2], error_map.shape[1]))
     return out
 
 
@@ -276,6 +282,28 @@ class NerfTraining:
     def load_snapshot(self, path, stream=None):
         """Testbed::load_snapshot (testbed.cu:4939-5057) into this trainer's network/optimizer/grid."""
         check(lib().ngp_nerf_load_snapshot(self.handle, _stream(stream), os.fsencode(path)))
+
+    ERROR_MAP_ARRAYS = ("data", "cdf_x_cond_y", "cdf_y", "cdf_img", "pmf_img")
+
+    def error_map(self):
+        """The training error map (Testbed::Nerf::Training::ErrorMap, testbed.h:668-677): the rays' losses
+        deposited since the current window started ("data", [n_images, h, w]) and, once a window has closed,
+        its CDFs ("cdf_x_cond_y" [n_images, cdf_h, cdf_w], "cdf_y" [n_images, cdf_h], "cdf_img", "pmf_img"
+        [n_images]), plus the window state (testbed_nerf.cu:3659-3666, 3700-3748)."""
+        info = NerfErrorMapInfo()
+        check(lib().ngp_nerf_trainer_error_map(self.handle, 0, None, 0, C.byref(info)))
+        out = {k: getattr(info, k) for k, _ in NerfErrorMapInfo._fields_ if k != "size"}
+        shapes = {"data": (info.n_images, info.height, info.width),
+                  "cdf_x_cond_y": (info.n_images, info.cdf_height, info.cdf_width),
+                  "cdf_y": (info.n_images, info.cdf_height), "cdf_img": (info.n_images,), "pmf_img": (info.n_images,)}
+        for which, name in enumerate(self.ERROR_MAP_ARRAYS):
+            check(lib().ngp_nerf_trainer_error_map(self.handle, which, None, 0, C.byref(info)))
+            a = np.zeros(int(info.size), np.float32)
+            if a.size:
+                check(lib().ngp_nerf_trainer_error_map(self.handle, which, a.ctypes.data, a.size, C.byref(info)))
+                a = a.reshape(shapes[name])
+            out[name] = a
+        return out
 
     def train_step(self, get_loss=True, stream=None):
         st = NerfStats()

@@ -413,13 +413,31 @@ static void lossg(float tgt, float p, uint32_t type, float* l, float* g) {
 	}
 }
 
+/* The error map deposit of one compacted ray (testbed_nerf.cu:1869-1899, no sharpness factor): the mean
+ * loss split bilinearly over the texels around uv * res - 0.5; idx clamped with the image's resolution. */
+static void deposit_error(float* em, uint32_t w, uint32_t h, const oimg* im, uint32_t img, float u, float v, float ml) {
+	const float rx = (float)w, ry = (float)h;
+	const float px = fminf(fmaxf(u * rx - 0.5f, 0.0f), rx - (1.0f + 1e-4f));
+	const float py = fminf(fmaxf(v * ry - 0.5f, 0.0f), ry - (1.0f + 1e-4f));
+	const int ix0 = (int)px, iy0 = (int)py;
+	const float wx = px - (float)ix0, wy = py - (float)iy0;
+	int ix = ix0 < 0 ? 0 : ix0, iy = iy0 < 0 ? 0 : iy0;
+	if (ix > (int)im->width - 2) ix = (int)im->width - 2;
+	if (iy > (int)im->height - 2) iy = (int)im->height - 2;
+	float* e = em + (size_t)img * w * h;
+	e[(size_t)iy * w + ix] += (1 - wx) * (1 - wy) * ml;
+	e[(size_t)iy * w + ix + 1] += wx * (1 - wy) * ml;
+	e[(size_t)(iy + 1) * w + ix] += (1 - wx) * wy * ml;
+	e[(size_t)(iy + 1) * w + ix + 1] += wx * wy * ml;
+}
+
 /* compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012); network_output fp16 bits [n x 16];
- * dloss fp16 bits [max_c x 16] (rows 0..3 written). */
-EXPORT void orc_nerf_compute_loss(const ocfg* c, const oimg* ims, const uint32_t* const* px, uint32_t n_img, uint32_t n_rays,
-                                  uint32_t n_div, orc_pcg32 rng0, uint32_t max_c, uint32_t ray_counter, const uint16_t* out16,
-                                  const uint32_t* ray_indices, const float* rays, uint32_t* numsteps, const float* coords_in,
-                                  float* coords_out, uint16_t* dloss, float* loss, uint32_t* compacted_counter, float mean_density,
-                                  float loss_scale) {
+ * dloss fp16 bits [max_c x 16] (rows 0..3 written); error_map [n_img][em_h][em_w] or NULL. */
+EXPORT void orc_nerf_compute_loss_em(const ocfg* c, const oimg* ims, const uint32_t* const* px, uint32_t n_img, uint32_t n_rays,
+                                     uint32_t n_div, orc_pcg32 rng0, uint32_t max_c, uint32_t ray_counter, const uint16_t* out16,
+                                     const uint32_t* ray_indices, const float* rays, uint32_t* numsteps, const float* coords_in,
+                                     float* coords_out, uint16_t* dloss, float* loss, uint32_t* compacted_counter, float mean_density,
+                                     float loss_scale, float* error_map, uint32_t em_w, uint32_t em_h) {
 	uint32_t ctotal = 0;
 	float diag[3];
 	for (int k = 0; k < 3; ++k) diag[k] = c->aabb_max[k] - c->aabb_min[k];
@@ -477,6 +495,7 @@ EXPORT void orc_nerf_compute_loss(const ocfg* c, const oimg* ims, const uint32_t
 		float l[3], g[3];
 		for (int k = 0; k < 3; ++k) lossg(tgt[k], rgb_ray[k], c->loss_type, &l[k], &g[k]);
 		if (loss) loss[i] = ((l[0] + l[1] + l[2]) / 3.0f) / (float)n_rays;
+		if (error_map) deposit_error(error_map, em_w, em_h, im, img, u, v, (l[0] + l[1] + l[2]) / 3.0f);
 		float ls = loss_scale / (float)n_rays;
 		float l2reg = c->rgb_activation == 3 ? 1e-4f : 0.0f, l1d = mean_density < MIN_OPT ? 1e-4f : 0.0f;
 		const float* ray = rays + (size_t)i * 6;
@@ -507,6 +526,14 @@ EXPORT void orc_nerf_compute_loss(const ocfg* c, const oimg* ims, const uint32_t
 		}
 	}
 	*compacted_counter = ctotal;
+}
+EXPORT void orc_nerf_compute_loss(const ocfg* c, const oimg* ims, const uint32_t* const* px, uint32_t n_img, uint32_t n_rays,
+                                  uint32_t n_div, orc_pcg32 rng0, uint32_t max_c, uint32_t ray_counter, const uint16_t* out16,
+                                  const uint32_t* ray_indices, const float* rays, uint32_t* numsteps, const float* coords_in,
+                                  float* coords_out, uint16_t* dloss, float* loss, uint32_t* compacted_counter, float mean_density,
+                                  float loss_scale) {
+	orc_nerf_compute_loss_em(c, ims, px, n_img, n_rays, n_div, rng0, max_c, ray_counter, out16, ray_indices, rays, numsteps,
+	                         coords_in, coords_out, dloss, loss, compacted_counter, mean_density, loss_scale, NULL, 0, 0);
 }
 
 /* generate_grid_samples_nerf_nonuniform (testbed_nerf.cu:635-676) */

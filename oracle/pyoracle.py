@@ -403,6 +403,8 @@ def _declare_nerf(L):
     d("orc_camera_matrix", None, P, P)
     d("orc_nerf_generate_samples", None, P, P, P, u32, u32, u32, u32, Pcg32, u32, P, P, P, P, P, P)
     d("orc_nerf_compute_loss", None, P, P, P, u32, u32, u32, Pcg32, u32, u32, P, P, P, P, P, P, P, P, P, f32, f32)
+    d("orc_nerf_compute_loss_em", None, P, P, P, u32, u32, u32, Pcg32, u32, u32, P, P, P, P, P, P, P, P, P, f32, f32, P,
+      u32, u32)
     d("orc_nerf_grid_samples", None, P, u32, Pcg32, u32, P, u32, f32, P, P)
     d("orc_nerf_grid_splat_ema", None, u32, P, P, u32, u32, f32, P)
     d("orc_nerf_grid_mean", C.c_float, P)
@@ -455,8 +457,10 @@ def nerf_generate_samples(cfg, images, pixels, n_rays, rng, max_samples, bitfiel
 
 
 def nerf_compute_loss(cfg, images, pixels, n_rays, rng, max_compacted, samples, out16, mean_density, loss_scale=128.0,
-                      n_div=None):
-    """samples: dict from nerf_generate_samples (numpy; its numsteps is rewritten in place)."""
+                      n_div=None, error_map_res=None):
+    """samples: dict from nerf_generate_samples (numpy; its numsteps is rewritten in place). error_map_res
+    (w, h): also deposit every compacted ray's mean loss into a zeroed error map, res["error_map"]
+    [n_images, h, w] (testbed_nerf.cu:1869-1899)."""
     ims = _images_arg(images)
     keep, pix = _pixels_arg(pixels)
     res = {
@@ -464,13 +468,52 @@ def nerf_compute_loss(cfg, images, pixels, n_rays, rng, max_compacted, samples, 
         "dloss_doutput": np.zeros((max_compacted, 16), np.uint16),
         "loss": np.zeros(n_rays, np.float32), "compacted_counter": np.zeros(1, np.uint32),
     }
-    lib().orc_nerf_compute_loss(C.byref(cfg), ims, pix, len(images), n_rays, n_div or n_rays, rng, max_compacted,
-                                int(samples["counters"][0]), ptr(np.ascontiguousarray(out16, np.uint16)),
-                                ptr(samples["ray_indices"]), ptr(samples["rays"]), ptr(samples["numsteps"]),
-                                ptr(samples["coords"]), ptr(res["coords_compacted"]), ptr(res["dloss_doutput"]),
-                                ptr(res["loss"]), ptr(res["compacted_counter"]), float(mean_density), float(loss_scale))
+    em_w, em_h = error_map_res or (0, 0)
+    em = np.zeros((len(images), em_h, em_w), np.float32) if error_map_res else None
+    lib().orc_nerf_compute_loss_em(C.byref(cfg), ims, pix, len(images), n_rays, n_div or n_rays, rng, max_compacted,
+                                   int(samples["counters"][0]), ptr(np.ascontiguousarray(out16, np.uint16)),
+                                   ptr(samples["ray_indices"]), ptr(samples["rays"]), ptr(samples["numsteps"]),
+                                   ptr(samples["coords"]), ptr(res["coords_compacted"]), ptr(res["dloss_doutput"]),
+                                   ptr(res["loss"]), ptr(res["compacted_counter"]), float(mean_density), float(loss_scale),
+                                   ptr(em) if em is not None else None, em_w, em_h)
+    if em is not None:
+        res["error_map"] = em
     del keep
     return res
+
+
+ERROR_MAP_MIN_PDF = np.float32(0.01)
+
+
+def error_map_cdfs(data):
+    """construct_cdf_2d + construct_cdf_1d (testbed_nerf.cu:2356-2410) in float32, sequential running sums
+    like the kernels' loops (np.cumsum accumulates in order). data [n_images, h, w] -> (cdf_x_cond_y,
+    cdf_y, cdf_img)."""
+    data = np.asarray(data, np.float32)
+    n, h, w = data.shape
+    one, mp = np.float32(1.0), ERROR_MAP_MIN_PDF
+    cum = np.cumsum(data + np.float32(1e-10), axis=2, dtype=np.float32)
+    cdf_y_raw = cum[:, :, -1].copy()
+    norm = one / cdf_y_raw
+    xs = (mp * np.arange(1, w + 1, dtype=np.float32)) / np.float32(w)
+    cdf_x = (one - mp) * cum * norm[:, :, None] + xs
+    cy = np.cumsum(cdf_y_raw, axis=1, dtype=np.float32)
+    cdf_img = cy[:, -1].copy()
+    ys = (mp * np.arange(1, h + 1, dtype=np.float32)) / np.float32(h)
+    cdf_y = (one - mp) * cy * (one / cdf_img)[:, None] + ys
+    return cdf_x.astype(np.float32), cdf_y.astype(np.float32), cdf_img
+
+
+def error_map_image_pmf(cdf_img):
+    """The host pass over construct_cdf_1d's per-image totals (testbed_nerf.cu:3730-3745): (pmf, cdf)."""
+    tot = np.asarray(cdf_img, np.float32)
+    n = tot.size
+    cum = np.cumsum(tot, dtype=np.float32)
+    norm = np.float32(1.0) / cum[-1]
+    mp = np.float32(0.1)
+    pmf = (np.float32(1.0) - mp) * tot * norm + mp / np.float32(n)
+    cdf = (np.float32(1.0) - mp) * cum * norm + (mp * np.arange(1, n + 1, dtype=np.float32)) / np.float32(n)
+    return pmf.astype(np.float32), cdf.astype(np.float32)
 
 
 def nerf_grid_samples(cfg, n, rng, step, grid, n_cascades, thresh):

@@ -196,9 +196,15 @@ def test_compute_loss(pkg, orc, scene, loss_type, act, aabb_scale):
     out_t = torch.from_numpy(out).cuda()
     mean = torch.tensor([0.003], device="cuda")
     max_c = 1 << 15
-    got = pkg.nerf.compute_loss(ds, cfg, n_rays, r, max_c, samples, out_t, mean)
-    ref = orc.nerf_compute_loss(cfg, ims, pix, n_rays, orc_rng(orc, r), max_c, ref_s, out.view(np.uint16), 0.003)
+    em = torch.zeros((len(ims), 11, 13), dtype=torch.float32, device="cuda")
+    got = pkg.nerf.compute_loss(ds, cfg, n_rays, r, max_c, samples, out_t, mean, error_map=em)
+    ref = orc.nerf_compute_loss(cfg, ims, pix, n_rays, orc_rng(orc, r), max_c, ref_s, out.view(np.uint16), 0.003,
+                                error_map_res=(13, 11))
     kept = int(ref_s["counters"][0])
+    # error map deposit (:1869-1899): float atomics in any order, losses to rtol 1e-4 (powf, see above)
+    em_ref = ref["error_map"]
+    assert em_ref.sum() > 0
+    np.testing.assert_allclose(em.cpu().numpy(), em_ref, rtol=1e-4, atol=1e-6 * float(em_ref.max()))
     cc = int(got["compacted_counter"].cpu().numpy().view(np.uint32)[0])
     assert cc == int(ref["compacted_counter"][0])
     assert cc > 0
@@ -307,6 +313,47 @@ def test_nerf_training_end_to_end(pkg, orc):
     np.testing.assert_array_equal(bf, orc.nerf_grid_bitfield(full, cfg.max_cascade, float(m_ref)))
     occupied = np.unpackbits(bf[:128 ** 3 // 8]).mean()
     assert 0.0 < occupied < 0.5  # the grid prunes once step >= 256 switches to the 0.01 threshold (:3518)
+
+
+def test_training_error_map_window(pkg, orc):
+    """The trainer's error map (testbed_nerf.cu:3659-3666, 1869-1899, 3700-3748): the first window is
+    sized from 128 steps of the initial 4096 rays, its CDFs after step 128 equal the oracle's
+    construct_cdf_2d/1d and host pass of the same map bit for bit, the next window is 1.5x longer and is
+    sized from the current ray count, and a step deposits exactly its rays' losses."""
+    n_img, W = 8, 96
+    ds = pkg.synthetic.lego_like_dataset(n_images=n_img, width=W, height=W, seed=5)
+    cfg = pkg.nerf.default_config(1.0)
+    net = pkg.create_nerf_network(pkg.nerf_config("C2"))
+    tr = pkg.Trainer(net, pkg.nerf_config("C2")["optimizer"])
+    run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
+    f = np.float32
+
+    def side(between, rays):
+        n = (between * rays) // n_img
+        return min(int(f(np.sqrt(f(np.sqrt(f(n))))) * f(3.5)), W)
+
+    stats = [run.train_step(get_loss=False) for _ in range(128)]
+    em = run.error_map()
+    k0 = side(128, 4096)
+    assert (em["width"], em["height"], em["cdf_width"], em["cdf_height"]) == (k0, k0, k0, k0)
+    assert em["cdf_valid"] == 1 and em["n_steps_since_update"] == 0 and em["n_steps_between_updates"] == 192
+    data = em["data"]
+    assert data.shape == (n_img, k0, k0) and (data >= 0).all() and data.sum() > 0
+    cx, cy, ci = orc.error_map_cdfs(data)
+    np.testing.assert_array_equal(em["cdf_x_cond_y"], cx)
+    np.testing.assert_array_equal(em["cdf_y"], cy)
+    pmf, cdf = orc.error_map_image_pmf(ci)
+    np.testing.assert_array_equal(em["pmf_img"], pmf)
+    np.testing.assert_array_equal(em["cdf_img"], cdf)
+    R = stats[-1]["rays_per_batch"]
+    s = run.train_step(get_loss=True)
+    em = run.error_map()
+    k1 = side(192, R)
+    assert (em["width"], em["height"], em["n_steps_since_update"]) == (k1, k1, 1)
+    # loss_scalar = sum_i(mean_loss_i / R) * measured / B (testbed_nerf.cu:3583-3609): the map holds sum_i mean_loss_i
+    B = cfg.target_batch_size
+    want = s["loss"] * B / s["measured_batch_size"] * R
+    np.testing.assert_allclose(em["data"].sum(dtype=np.float64), want, rtol=1e-4)
 
 
 def test_counters_follow_oracle_recurrence(pkg, orc):

@@ -125,3 +125,45 @@ def test_counters_update_oracle_hand_cases(orc):
     assert orc.nerf_max_inference(0, 1 << 22) == 1 << 22
     assert orc.nerf_max_inference(300001, 1 << 22) == 300032
     assert orc.nerf_max_inference(5 << 22, 1 << 22) == 1 << 22
+
+
+def test_oracle_error_map_deposit_and_cdfs(pkg, orc):
+    """The error map (testbed_nerf.cu:1869-1899, 2356-2410, 3730-3745) in the oracle: every compacted ray's
+    mean loss is split over 4 texels with weights summing to 1, so the map's total is the sum of the per-ray
+    losses; the CDF restatement equals a scalar float32 loop of the kernels; the image pmf sums to 1."""
+    ims, pix = _scene(pkg, n=3, w=40, h=30)
+    cfg = pkg.nerf.default_config(1.0)
+    full = np.full(128 ** 3, 1.0, np.float32)
+    bf = orc.nerf_grid_bitfield(np.concatenate([full] + [np.zeros_like(full)] * 7), 0, 0.005)
+    n_rays = 256
+    s = orc.nerf_generate_samples(cfg, ims, pix, n_rays, orc.pcg(*_st(pkg.nerf.pcg32(5))), 1 << 16, bf)
+    out = np.random.default_rng(1).uniform(-2, 2, (1 << 16, 16)).astype(np.float16)
+    res = orc.nerf_compute_loss(cfg, ims, pix, n_rays, orc.pcg(*_st(pkg.nerf.pcg32(5))), 1 << 15, s, out.view(np.uint16),
+                                0.01, error_map_res=(9, 7))
+    em = res["error_map"]
+    assert em.shape == (3, 7, 9) and (em >= 0).all() and em.sum() > 0
+    np.testing.assert_allclose(em.sum(dtype=np.float64), res["loss"].sum(dtype=np.float64) * n_rays, rtol=1e-5)
+    cx, cy, ci = orc.error_map_cdfs(em)
+    n, h, w = em.shape
+    f = np.float32
+    for i in range(n):
+        cum_y = f(0)
+        rows = []
+        for y in range(h):
+            cum = f(0)
+            row = []
+            for x in range(w):
+                cum = f(cum + f(em[i, y, x] + f(1e-10)))
+                row.append(cum)
+            rows.append(cum)
+            norm = f(1) / cum
+            for x in range(w):
+                want = f(f(f(f(1) - f(0.01)) * row[x]) * norm) + f(f(f(0.01) * f(x + 1)) / f(w))
+                assert cx[i, y, x] == want
+        for y in range(h):
+            cum_y = f(cum_y + rows[y])
+            assert cy[i, y] == f(f(f(f(1) - f(0.01)) * cum_y) * (f(1) / ci[i])) + f(f(f(0.01) * f(y + 1)) / f(h))
+        assert ci[i] == cum_y
+    assert (np.diff(cx, axis=2) > 0).all() and np.allclose(cx[:, :, -1], 1.0) and np.allclose(cy[:, -1], 1.0)
+    pmf, cdf = orc.error_map_image_pmf(ci)
+    assert abs(float(pmf.sum(dtype=np.float64)) - 1.0) < 1e-6 and abs(float(cdf[-1]) - 1.0) < 1e-6
