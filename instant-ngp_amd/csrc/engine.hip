@@ -168,6 +168,7 @@ struct ngp_model {
 	bool fuse_infer = true;                 // option "fuse_infer": NerfNetwork inference encodes inside the MLP kernel
 	bool fuse_slabs = true;                 // option "fuse_slabs": dW slab reduction inside the grid backward's last kernel
 	bool fuse_opt = true;                   // option "fuse_opt": lazy-layout optimizer update inside the grid backward (training_step)
+	bool fuse_mlp_opt = true;               // option "fuse_mlp_opt": ... and the MLP section's update in its dW slab blocks (no optimizer launch)
 	bool mlp_train16 = false;               // option "mlp_train16": the training MLP at two waves per SIMD (mlp_train16.hip; off: no faster at C2, 3x slower at C2p)
 	bool grid_stage0 = false;               // option "grid_stage0": the training forward stages level 0 in LDS (grid.hip STAGE0; off: measured slower)
 	bool grid_bricks = false;               // option "grid_bricks": dense levels of the bucketed backward summed per brick (off: measured slower)
@@ -417,6 +418,16 @@ struct ngp_model {
 		}
 		if (ovl) NGP_HIP(hipEventRecord(ev_red, side));
 		GridBwdArgs b{n, in, stride, dL_denc, enc_width, AoS, gradients + grid_offset(), max_level, max_level_per_sample};
+		FusedAdam fmlp;
+		if (fopt && fopt->mlp_n) {
+			// the MLP's update in the slab blocks (trainer: mlp_opt_in_backward): the fragment slots are written
+			// in place when they hold the current parameters, as the optimizer launch would (run_step)
+			NGP_CHECK(fused && grad_mode == NGP_GRAD_OVERWRITE && fopt->mlp_n == n_matrix(), "fused MLP update: slab reduction not fused");
+			fmlp = *fopt;
+			fmlp.frags = frags_current ? (f16*)frags.p : nullptr;
+			fmlp.fragmap = d_fragmap;
+			fopt = &fmlp;
+		}
 		scatter_grid_grad(s, b, grad_mode != NGP_GRAD_ACCUMULATE, fused ? &sj : nullptr, fopt);
 		if (ovl) NGP_HIP(hipStreamWaitEvent(s, ev_red, 0));
 		input_gradient();
@@ -513,13 +524,28 @@ struct ngp_trainer {
 		return rec && !allreduce && m->fuse_opt && m->use_sorted(n_batch) && m->grid.n_features >= 2 && m->n_matrix() % 4 == 0 &&
 		       m->grid_offset() % 2 == 0 && m->params == w16 && m->gradients == g16;
 	}
-	FusedAdam fused_update(float loss_scale) const {
+	FusedAdam fused_update(float loss_scale, uint32_t n_batch) const {
 		FusedAdam fa;
 		const uint64_t go = model->grid_offset();
 		fa.w16 = w16 + go; fa.rec = rec + go / 2;
 		fa.loss_scale = loss_scale; fa.cfg = cfg; fa.step_add = step;
 		fa.bias_tab = bias_tab;
+		if (mlp_opt_in_backward(n_batch)) {
+			fa.mlp_n = (uint32_t)model->n_matrix();
+			fa.mlp_w16 = w16;
+			fa.mlp_rec = rec;
+		}
 		return fa;
+	}
+	// With the grid's update fused (fused_update_ok), the MLP section's update runs in the dW slab blocks of
+	// the grid backward's last kernel when the slab reduction is fused there (model options fuse_slabs,
+	// fuse_mlp_opt; not under the side-stream reduction, overlap bit 4): no optimizer launch.
+	bool mlp_opt_in_backward(uint32_t n_batch) const {
+		const ngp_model* m = model;
+		return m->fuse_mlp_opt && m->fuse_slabs && !(m->overlap & 4) && m->use_sorted(n_batch) && m->n_matrix() > 0;
+	}
+	void mlp_step_done() {  // run_step's bookkeeping when the update ran in the backward
+		if (rec) inf_stale = w32_stale = true;
 	}
 };
 
@@ -748,6 +774,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			m->fuse_slabs = value != 0;
 		} else if (k == "fuse_opt") {
 			m->fuse_opt = value != 0;
+		} else if (k == "fuse_mlp_opt") {
+			m->fuse_mlp_opt = value != 0;
 		} else if (k == "grid_stage0") {
 			m->grid_stage0 = value != 0;
 		} else if (k == "grid_bricks") {
@@ -1114,10 +1142,11 @@ int ngp_trainer_training_step(ngp_trainer* t, void* stream, uint32_t n, const fl
 		// the grid's optimizer update runs inside the backward where possible (fused_update_ok): its
 		// gradient is then not stored, and the optimizer launch covers the MLP section alone
 		const bool fuse = run_optimizer && t->fused_update_ok(n);
-		const FusedAdam fa = fuse ? t->fused_update(loss_scale) : FusedAdam{};
+		const FusedAdam fa = fuse ? t->fused_update(loss_scale, n) : FusedAdam{};
 		m->train_pass(s, n, input, input_stride, e, nullptr, 0, dl, W, NGP_GRAD_OVERWRITE, BwdExtra{}, fuse ? &fa : nullptr);
 		if (run_optimizer) {
-			t->run_step(s, loss_scale, nullptr, t->step, fuse ? m->n_matrix() : 0);
+			if (fa.mlp_n) t->mlp_step_done();
+			else t->run_step(s, loss_scale, nullptr, t->step, fuse ? m->n_matrix() : 0);
 			t->step++;
 		}
 	});
@@ -1142,7 +1171,7 @@ static int train_step_body(ngp_trainer* t, void* stream, uint32_t n, const float
 	ngp_model* m = t->model;
 	FusedAdam fa;
 	if (fuse) {
-		fa = t->fused_update(loss_scale * (float)world);
+		fa = t->fused_update(loss_scale * (float)world, n);
 		if (step_base) {
 			fa.step_base = step_base;
 			fa.step_add = k;
@@ -1160,8 +1189,9 @@ static int train_step_body(ngp_trainer* t, void* stream, uint32_t n, const float
 	if (rc == NGP_OK && with_optimizer) {
 		try {
 			// the summed gradient of `world` ranks: mean via the loss scale
-			t->run_step(S(stream), loss_scale * (float)world, step_base, step_base ? k : t->step + k,
-			            fuse ? m->n_matrix() : 0);
+			if (fa.mlp_n) t->mlp_step_done();
+			else t->run_step(S(stream), loss_scale * (float)world, step_base, step_base ? k : t->step + k,
+			                 fuse ? m->n_matrix() : 0);
 		} catch (const std::exception& e) {
 			g_last_error = e.what();
 			rc = NGP_ERROR;

@@ -938,7 +938,36 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
 	}
 	if (blockIdx.x >= slab_x0) {
 		const uint32_t blk = blockIdx.y * (fin_x0 - slab_x0) + (blockIdx.x - slab_x0);
-		if (blk < slab_blocks(sj.n)) reduce_slabs_block(sj, blk);
+		if (blk >= slab_blocks(sj.n)) return;
+		if (!FUSED || fa.mlp_n == 0) {
+			reduce_slabs_block(sj, blk);
+			return;
+		}
+		// the MLP's optimizer update for this block's 32 parameters (8 groups of 4), from the gradients
+		// just reduced: k_adam_lazy4's lazy_update on [0, mlp_n) without a launch of its own
+		__shared__ f16 gsh[32];
+		reduce_slabs_block(sj, blk, gsh);
+		__syncthreads();
+		const uint32_t i0 = blk * 32 + 4 * threadIdx.x;
+		if (threadIdx.x >= 8 || i0 >= fa.mlp_n) return;
+		AdamState st{};
+		st.w16 = fa.mlp_w16; st.rec = fa.mlp_rec; st.frags = fa.frags; st.fragmap = fa.fragmap; st.bias_tab = fa.bias_tab;
+		const AdamConfig cfg = fa.cfg_dev ? *fa.cfg_dev : fa.cfg;
+		const uint32_t step = (fa.step_base ? *fa.step_base : 0u) + fa.step_add;
+		LazyGroup G;
+		G.i0 = i0;
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			G.g[k] = (float)gsh[4 * threadIdx.x + k] / fa.loss_scale;
+			G.act[k] = true;  // matrix parameters: updated every step
+		}
+		G.any[0] = G.any[1] = true;
+#pragma unroll
+		for (int r = 0; r < 2; ++r) {
+			const f32x4* rp = (const f32x4*)(fa.mlp_rec + (i0 >> 1) + r);
+			G.q[r][0] = rp[0]; G.q[r][1] = rp[1]; G.q[r][2] = rp[2];
+		}
+		lazy_update(st, cfg, step, fa.mlp_n, G);
 		return;
 	}
 	// grid (split bucket, 256-pair chunk): one pair per thread, the parts' loads 8 at a time

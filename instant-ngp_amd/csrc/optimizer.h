@@ -75,6 +75,70 @@ __device__ __forceinline__ float ema_catch_up(float e, float w, float d, uint32_
 	return e;
 }
 
+// Four parameters (two records) per group; a record none of whose parameters is updated this step is
+// neither read nor written (grid entries without gradient: the bulk of a large table). A thread owns
+// two groups half the table apart and issues both groups' state loads before either computes (the
+// loads depend on the gradient test: two chains in flight instead of one).
+struct LazyGroup {
+	uint32_t i0;
+	bool act[4], any[2];
+	float g[4];
+	f32x4 q[2][3];
+};
+
+__device__ __forceinline__ void lazy_update(const AdamState& st, const AdamConfig& c, uint32_t step, uint32_t n_matrix, LazyGroup& G) {
+	if (!G.any[0] && !G.any[1]) return;
+	const uint32_t i0 = G.i0;
+	const float lr = lr_schedule(c, step);
+	const float d = c.ema_decay;
+	float w[4];
+#pragma unroll
+	for (int r = 0; r < 2; ++r) {
+		if (!G.any[r]) continue;
+		w[2 * r] = G.q[r][2][2];  // the pair's fp32 weights (AdamRec::w)
+		w[2 * r + 1] = G.q[r][2][3];
+		AdamRec rc;
+		rc.m1[0] = G.q[r][0][0]; rc.m1[1] = G.q[r][0][1]; rc.m2[0] = G.q[r][0][2]; rc.m2[1] = G.q[r][0][3];
+		rc.steps[0] = __float_as_uint(G.q[r][1][0]); rc.steps[1] = __float_as_uint(G.q[r][1][1]);
+		rc.ema[0] = G.q[r][1][2]; rc.ema[1] = G.q[r][1][3];
+		rc.done[0] = __float_as_uint(G.q[r][2][0]); rc.done[1] = __float_as_uint(G.q[r][2][1]);
+#pragma unroll
+		for (int k = 0; k < 2; ++k) {
+			const int p = 2 * r + k;
+			if (!G.act[p]) continue;
+			// missing EMA steps first, with the weight those steps saw (unchanged since the last update)
+			if (d > 0.f) rc.ema[k] = ema_catch_up(rc.ema[k], w[p], d, rc.done[k], step);
+			float gk = G.g[p];
+			if (i0 + p < n_matrix) gk += c.l2 * w[p];
+			const float mm = c.beta1 * rc.m1[k] + (1.f - c.beta1) * gk;
+			const float vv = c.beta2 * rc.m2[k] + (1.f - c.beta2) * (gk * gk);
+			rc.m1[k] = mm;
+			rc.m2[k] = vv;
+			const uint32_t sk = rc.steps[k] + 1;
+			rc.steps[k] = sk;
+			const float lr_s = adam_step_size(c, lr, sk, st.bias_tab);
+			w[p] = w[p] - lr_s / (sqrtf(vv) + c.eps) * mm;
+			if (d > 0.f) rc.ema[k] = d * rc.ema[k] + (1.f - d) * w[p];
+			rc.done[k] = step + 1;
+		}
+		f32x4* rp = (f32x4*)(st.rec + (i0 >> 1) + r);
+		rp[0] = f32x4{rc.m1[0], rc.m1[1], rc.m2[0], rc.m2[1]};
+		rp[1] = f32x4{__uint_as_float(rc.steps[0]), __uint_as_float(rc.steps[1]), rc.ema[0], rc.ema[1]};
+		rp[2] = f32x4{__uint_as_float(rc.done[0]), __uint_as_float(rc.done[1]), w[2 * r], w[2 * r + 1]};
+		*(f16x2*)(st.w16 + i0 + 2 * r) = f16x2{(f16)w[2 * r], (f16)w[2 * r + 1]};
+	}
+	if (st.frags && i0 < n_matrix) {
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			if (i0 + k >= n_matrix || !G.act[k]) continue;
+			const uint32_t q0 = st.fragmap[2 * (i0 + k)], q1 = st.fragmap[2 * (i0 + k) + 1];
+			const f16 wh = (f16)w[k];
+			if (q0 != ~0u) st.frags[q0] = wh;
+			if (q1 != ~0u) st.frags[q1] = wh;
+		}
+	}
+}
+
 // The lazy-layout update applied inside the hash-grid backward (engine option fuse_opt): the bucket
 // accumulation holds each grid entry's final fp16 gradient, so it updates that parameter pair's record
 // directly instead of storing the gradient for k_adam_lazy4 to read back (C5: 210 MB written and 210 MB
@@ -89,6 +153,14 @@ struct FusedAdam {
 	const uint32_t* step_base = nullptr;
 	uint32_t step_add = 0;
 	const float* bias_tab = nullptr;
+	// The MLP section's update too (mlp_n = its parameter count, a multiple of 4; 0: the optimizer launch
+	// does it): the dW slab blocks of the grid backward's last kernel hold those parameters' final
+	// gradients, so they run k_adam_lazy4's lazy_update on them (whole-model pointers; option fuse_mlp_opt)
+	uint32_t mlp_n = 0;
+	f16* mlp_w16 = nullptr;
+	AdamRec* mlp_rec = nullptr;
+	f16* frags = nullptr;
+	const uint32_t* fragmap = nullptr;
 };
 // One parameter pair's state between the load and the update (callers issue several pairs' loads
 // before the first update: the record reads are the latency to hide).

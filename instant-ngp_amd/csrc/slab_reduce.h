@@ -19,7 +19,8 @@ __host__ __device__ constexpr uint32_t slab_blocks(uint32_t n) { return (n + 31)
 
 // Block `blk` (256 threads) = 32 parameters x 8 slab groups; each thread sums every 8th slab of one
 // parameter, then the 8 partial sums are added in a fixed order (deterministic).
-__device__ __forceinline__ void reduce_slabs_block(const SlabJob& j, uint32_t blk) {
+// gsh (optional, 32 entries of LDS): also receives the block's fp16 gradients (the fused MLP update).
+__device__ __forceinline__ void reduce_slabs_block(const SlabJob& j, uint32_t blk, f16* gsh = nullptr) {
 	__shared__ float part[8][33];
 	const uint32_t p = blk * 32 + (threadIdx.x & 31), g = threadIdx.x >> 5;
 	const size_t st = j.stride ? j.stride : j.n;
@@ -43,6 +44,7 @@ __device__ __forceinline__ void reduce_slabs_block(const SlabJob& j, uint32_t bl
 #pragma unroll
 		for (int k = 0; k < 8; ++k) t += part[k][threadIdx.x];
 		j.grad[p] = (f16)t;
+		if (gsh) gsh[threadIdx.x] = (f16)t;
 	}
 }
 

@@ -149,13 +149,14 @@ def test_lazy_ema_set_params_full_precision_bitwise(pkg):
 
 def test_fused_optimizer_training_step_bitwise(pkg):
     """Trainer::training_step with the optimizer (train_sdf's call, testbed_sdf.cu:1304) on the lazy
-    layout runs the grid's update inside the bucketed backward (model option fuse_opt, default on): it
-    must train bit for bit like the separate k_adam_lazy4 launch and like the eager layout, with steps
+    layout runs the grid's update inside the bucketed backward (model option fuse_opt, default on), and the
+    MLP's in the backward's dW slab blocks (fuse_mlp_opt, default on): it must train bit for bit like the separate k_adam_lazy4 launch and like the eager layout, with steps
     whose batches leave most entries untouched and steps whose coarse buckets split into parts."""
     runs = {}
-    for name, lazy, fuse in (("eager", False, 0), ("lazy", True, 0), ("fused", True, 1)):
+    for name, lazy, fuse, mlp in (("eager", False, 0, 1), ("lazy", True, 0, 1), ("fused", True, 1, 1), ("fused_mlp_launch", True, 1, 0)):
         net, tr = make_trainer(pkg, "sdf", lazy)
         net.set_option("fuse_opt", fuse)
+        net.set_option("fuse_mlp_opt", mlp)  # the MLP's update in the slab blocks (1) or its own launch (0)
         snaps = []
         for step in range(20):
             n = 4096 if step % 3 else 1 << 16
@@ -170,7 +171,7 @@ def test_fused_optimizer_training_step_bitwise(pkg):
         runs[name] = (tr.params_full_precision.cpu().numpy().view(np.uint32).copy(),
                       tr.params.cpu().numpy().view(np.uint16).copy(), snaps, tr.serialize(), tr.step)
         del net, tr
-    for name in ("lazy", "fused"):
+    for name in ("lazy", "fused", "fused_mlp_launch"):
         w, p, s, b, st = runs[name]
         np.testing.assert_array_equal(w, runs["eager"][0])
         np.testing.assert_array_equal(p, runs["eager"][1])
@@ -187,9 +188,10 @@ def test_fused_optimizer_captured_steps_bitwise(pkg, kind):
     and hyperparameters read from the trainer's device block: bit for bit the eager layout's graph, across
     launches, a learning-rate change between launches, and a mid-run read of the inference parameters."""
     runs = {}
-    for name, lazy, fuse in (("eager", False, 0), ("lazy", True, 0), ("fused", True, 1)):
+    for name, lazy, fuse, mlp in (("eager", False, 0, 1), ("lazy", True, 0, 1), ("fused", True, 1, 1), ("fused_mlp_launch", True, 1, 0)):
         net, tr = make_trainer(pkg, kind, lazy)
         net.set_option("fuse_opt", fuse)
+        net.set_option("fuse_mlp_opt", mlp)
         s = torch.cuda.Stream()
         snaps = []
         graphs = []
@@ -208,7 +210,7 @@ def test_fused_optimizer_captured_steps_bitwise(pkg, kind):
         runs[name] = (tr.params_full_precision.cpu().numpy().view(np.uint32).copy(),
                       tr.params.cpu().numpy().view(np.uint16).copy(), snaps, tr.serialize(), tr.step)
         del graphs, net, tr
-    for name in ("lazy", "fused"):
+    for name in ("lazy", "fused", "fused_mlp_launch"):
         w, p, sn, b, st = runs[name]
         np.testing.assert_array_equal(w, runs["eager"][0])
         np.testing.assert_array_equal(p, runs["eager"][1])
