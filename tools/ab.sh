@@ -17,14 +17,15 @@ done
 shift $((OPTIND - 1))
 mkdir -p gpurun_out/$T
 export TMPDIR=/tmp
-apply() {  # reset, then export the variant's settings
-  unset NGP_ENGINE_LIB NGP_MODEL_OPTS NGP_SC_BT NGP_SC_LDS_KB NGP_SC_CHUNK NGP_SC_PART NGP_SC_LIMIT
+SET_KEYS=""
+apply() {  # reset (every variable an earlier variant exported), then export the variant's settings
+  unset NGP_ENGINE_LIB NGP_MODEL_OPTS NGP_SC_BT NGP_SC_LDS_KB NGP_SC_CHUNK NGP_SC_PART NGP_SC_LIMIT $SET_KEYS
   local kv=${1#*:}
   [ "$kv" = "$1" ] && return 0
   IFS=',' read -ra pairs <<< "$kv"
   for a in "${pairs[@]}"; do
     if [[ $a == lib=* ]]; then export NGP_ENGINE_LIB=$PWD/build/${a#lib=}/libngp_engine.so
-    else export "${a//;/,}"; fi
+    else export "${a//;/,}"; SET_KEYS="$SET_KEYS ${a%%=*}"; fi
   done
 }
 if [ -n "$TESTS" ]; then
