@@ -46,8 +46,8 @@ def test_bench_two_ranks_gloo_line():
     # N-vs-1 ratios against this job's own 1-GPU pass
     v1 = res["vs_1gpu"]
     assert v1["one_gpu"]["value"] > 0
-    assert v1["weak_ratio"] == pytest.approx(res["value"] / v1["one_gpu"]["value"], rel=1e-3)
-    assert v1["strong_ratio"] == pytest.approx(st["value"] / v1["one_gpu"]["value"], rel=1e-3)
+    assert v1["weak_ratio"] == pytest.approx(res["value"] / v1["one_gpu"]["value"], rel=1e-3, abs=6e-5)  # printed to 4 decimals
+    assert v1["strong_ratio"] == pytest.approx(st["value"] / v1["one_gpu"]["value"], rel=1e-3, abs=6e-5)
     # the data-parallel Testbed NeRF step (e2e over the two ranks) and its held-out PSNR on rank 0
     e = res["e2e"]
     assert e["n_gpus"] == 2 and e["steps"] > 0 and e["value"] > 0 and e["psnr"] > 10.0
