@@ -311,13 +311,30 @@ __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __r
 	if (fb_flag && threadIdx.x == 0) *fb_flag = 0u;  // the previous step's finalize has read and cleared the fallback
 	__shared__ uint32_t wsum[3][SC_PLAN_THREADS / 64];
 	const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-	const uint32_t K = min(SC_PLAN_K, (n_vb + SC_PLAN_THREADS - 1) / SC_PLAN_THREADS);
+	// buckets per thread; a multiple of 4 when SC_PLAN_K is, so totals and starts move as 16-B vectors
+	// (the workspace arrays are 256-B aligned, every thread's first bucket a multiple of 4)
+	constexpr bool VEC = SC_PLAN_K % 4 == 0;
+	uint32_t K = min(SC_PLAN_K, (n_vb + SC_PLAN_THREADS - 1) / SC_PLAN_THREADS);
+	if (VEC) K = (K + 3) & ~3u;
 	uint32_t c_lo = 0, c_parts = 0, c_sb = 0;
 	for (uint32_t b0 = 0; b0 < n_vb; b0 += SC_PLAN_THREADS * K) {
 		const uint32_t v0 = b0 + threadIdx.x * K;
 		uint32_t t[SC_PLAN_K];
+		if (VEC) {
 #pragma unroll
-		for (uint32_t k = 0; k < SC_PLAN_K; ++k) t[k] = (k < K && v0 + k < n_vb) ? tot[v0 + k] : 0u;
+			for (uint32_t k = 0; k < SC_PLAN_K; k += 4) {
+				if (k < K && v0 + k + 3 < n_vb) {
+					const uint4 q = *(const uint4*)(tot + v0 + k);
+					t[k] = q.x; t[k + 1] = q.y; t[k + 2] = q.z; t[k + 3] = q.w;
+				} else {
+#pragma unroll
+					for (uint32_t j = 0; j < 4; ++j) t[k + j] = (k + j < K && v0 + k + j < n_vb) ? tot[v0 + k + j] : 0u;
+				}
+			}
+		} else {
+#pragma unroll
+			for (uint32_t k = 0; k < SC_PLAN_K; ++k) t[k] = (k < K && v0 + k < n_vb) ? tot[v0 + k] : 0u;
+		}
 		uint32_t s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll
 		for (uint32_t k = 0; k < SC_PLAN_K; ++k) {
@@ -336,11 +353,27 @@ __global__ void __launch_bounds__(SC_PLAN_THREADS) k_sc_plan(const uint32_t* __r
 		}
 		__syncthreads();
 		uint32_t lo = p0 + i0 - s0, first = p1 + i1 - s1, b = p2 + i2 - s2;
+		if (VEC) {  // the bucket starts as 16-B stores; the split / brick lists below as before
+			uint32_t l = lo;
+#pragma unroll
+			for (uint32_t k = 0; k < SC_PLAN_K; k += 4) {
+				const uint32_t l0 = l, l1 = l0 + t[k], l2 = l1 + t[k + 1], l3 = l2 + t[k + 2];
+				l = l3 + t[k + 3];
+				if (k < K && v0 + k + 3 < n_vb) {
+					*(uint4*)(lo_out + v0 + k) = uint4{l0, l1, l2, l3};
+				} else {
+					const uint32_t lv[4] = {l0, l1, l2, l3};
+#pragma unroll
+					for (uint32_t j = 0; j < 4; ++j)
+						if (k + j < K && v0 + k + j < n_vb) lo_out[v0 + k + j] = lv[j];
+				}
+			}
+		}
 #pragma unroll
 		for (uint32_t k = 0; k < SC_PLAN_K; ++k) {
 			if (k >= K || v0 + k >= n_vb) break;
 			const uint32_t vb = v0 + k, tk = t[k];
-			lo_out[vb] = lo;
+			if (!VEC) lo_out[vb] = lo;
 			if (vb - brick_vb0 < n_bricks) {
 				const uint32_t parts = (tk + brick_part - 1) / brick_part;
 				bp[2 * (vb - brick_vb0)] = first; bp[2 * (vb - brick_vb0) + 1] = parts;
