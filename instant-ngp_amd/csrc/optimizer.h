@@ -70,7 +70,18 @@ __device__ __forceinline__ float lr_schedule(const AdamConfig& c, uint32_t step)
 	return r;
 }
 // The eager EMA of step j: e = d * e + (1 - d) * w (w after step j's update), output e / (1 - d^(j+1)).
+// A parameter skipped for k steps kept its weight w, so its EMA is owed k applications of that recurrence.
+// Up to EMA_CATCH_UP_LOOP of them are replayed one by one (bit-identical to the eager layout); a longer
+// gap uses the closed form d^k e + (1 - d^k) w, which differs from the replay by rounding only. Replaying
+// every step made a rarely touched entry loop over its whole gap (NeRF: tens of thousands of steps for
+// entries at the edge of the occupied space), and the kernel waited for that thread.
+constexpr uint32_t EMA_CATCH_UP_LOOP = 32;
 __device__ __forceinline__ float ema_catch_up(float e, float w, float d, uint32_t from, uint32_t to) {
+	if (to <= from) return e;
+	if (to - from > EMA_CATCH_UP_LOOP) {
+		const float dk = powf(d, (float)(to - from));
+		return dk * e + (1.f - dk) * w;
+	}
 	for (uint32_t j = from; j < to; ++j) e = d * e + (1.f - d) * w;
 	return e;
 }
