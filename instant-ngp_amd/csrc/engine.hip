@@ -1057,12 +1057,12 @@ int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, 
 		t->n = n;
 		auto al = [](size_t b) { return (b + 255) / 256 * 256; };
 		const size_t b32 = al(n * 4), b16 = al(n * 2);
-		// lazy-EMA records for large tables (C5: 105 M parameters, ~28 % updated per step; C2' 13 M: captured
-		// step 351 -> 330 us with the fused update, profiles/r03bw). C2 (3.3 M parameters, ~96 % updated) keeps
-		// the eager arrays: its pass is faster lazy since the MLP's update runs in the backward (141.3 -> 135 us,
-		// gpurun_out/r04lz), but the NeRF training steps were not measured with the EMA's closed-form catch-up
-		// yet. NGP_LAZY_EMA=0/1 forces the choice.
-		bool lazy = n >= (1ull << 23);
+		// lazy-EMA records from 2^20 parameters (C5: 105 M parameters, ~28 % updated per step; C2' 13 M: captured
+		// step 351 -> 330 us with the fused update, profiles/r03bw; C2, 3.3 M parameters, ~96 % updated: pass
+		// 140.6-142.8 -> 136.0 us since the MLP's update runs in the backward, NeRF steps unchanged with the
+		// EMA's closed-form catch-up, gpurun_out/r04cg); the eager arrays for small models. NGP_LAZY_EMA=0/1
+		// forces the choice.
+		bool lazy = n >= (1ull << 20);
 		if (const char* e = getenv("NGP_LAZY_EMA")) lazy = atoi(e) != 0;
 		lazy = lazy && n % 4 == 0;
 		const size_t brec = al(n / 2 * sizeof(AdamRec));
