@@ -240,8 +240,16 @@ def timed_steps(lib, step, steps, warmup, world, capture=None, comm=None):
         if capture is not None:
             try:
                 graph = capture(steps)
-                graph.launch()  # untimed replay: graph upload / first-launch costs
-                torch.cuda.synchronize()
+                # untimed replays: graph upload / first-launch costs, then at least ~25 ms of GPU work before the
+                # timed launch. A short warmup leaves the clocks ramping into the timed region: at K = 20 after 5
+                # warmup steps the first timed launch ran 146 us/step and every later one 135-138
+                # (tools/graph_probe.py, profiles/r05e_graph_probe.jsonl)
+                t_w = time.perf_counter()
+                for i in range(16):
+                    graph.launch()
+                    torch.cuda.synchronize()
+                    if i >= 1 and time.perf_counter() - t_w > 0.025:
+                        break
             except Exception as e:  # same HIP kernels, launched one by one
                 graph, graph_note = None, f"graph capture failed ({e}); eager launches"
                 print(f"[bench] {graph_note}", file=sys.stderr, flush=True)

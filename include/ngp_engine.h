@@ -184,6 +184,10 @@ float* ngp_trainer_params_full_precision(ngp_trainer* t);
 uint32_t ngp_trainer_step(const ngp_trainer* t);
 float ngp_trainer_learning_rate(const ngp_trainer* t);     /* optimizer->learning_rate() (testbed_nerf.cu:3771) */
 int ngp_trainer_set_learning_rate(ngp_trainer* t, float lr);
+/* Engine extension: trainer options. "ema_closed_form" 0 (default) / 1: how the large-table (lazy-EMA) layout
+ * applies the EMA steps a skipped parameter owes: exact replay to the recurrence's fixed point, bit for bit the
+ * per-step Ema of tcnn's chain (configs/nerf/base.json:5-8), or a closed form past 32 steps (within 1 fp16 ulp). */
+int ngp_trainer_set_option(ngp_trainer* t, const char* key, double value);
 /* set_params_full_precision (src/testbed.cu:4146): host fp32 -> master, fp16 params and inference params */
 int ngp_trainer_set_params_full_precision(ngp_trainer* t, const float* params_host, uint64_t n);
 /* serialize / deserialize (src/testbed.cu:4874,5040): flat little-endian blob, size query with buf=NULL */

@@ -123,6 +123,7 @@ SIGNATURES = {
     "ngp_trainer_step": (u32, [P]),
     "ngp_trainer_learning_rate": (f32, [P]),
     "ngp_trainer_set_learning_rate": (i32, [P, f32]),
+    "ngp_trainer_set_option": (i32, [P, C.c_char_p, C.c_double]),
     "ngp_trainer_set_params_full_precision": (i32, [P, P, u64]),
     "ngp_trainer_serialize": (i32, [P, P, C.POINTER(u64)]),
     "ngp_trainer_deserialize": (i32, [P, P, u64]),

@@ -98,6 +98,7 @@ def nerf_config(variant="C2"):
     cfg = json.loads(json.dumps(NERF_BASE))
     if variant == "C2p":
         cfg["encoding"].update({"n_levels": 16, "n_features_per_level": 2, "log2_hashmap_size": 19})
-    # the fork forces per_level_scale = 2.0 in reset_network (src/testbed.cu:3991)
+    # base.json has no per_level_scale: the grid gets tcnn's default 2.0 (the fork's reset_network sets only its
+    # log member to 2.0, src/testbed.cu:3991, and passes the encoding config on unchanged, :4037)
     cfg["encoding"]["per_level_scale"] = 2.0
     return cfg

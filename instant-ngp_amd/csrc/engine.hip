@@ -92,15 +92,21 @@ static void init_mlp(const MlpDims& d, Pcg32& rng, float* p, float scale) {
 	}
 }
 
+// tcnn's GridEncoding otypes: HashGrid (= Grid with type Hash) and DenseGrid (= Grid with type Dense, e.g.
+// configs/nerf/densegrid.json). A dense level holds res^D entries (rounded to 8) with no hashmap cap, so its
+// stride never exceeds its size and grid_index never hashes: the hash-grid kernels run it unchanged with the
+// cap lifted (GRID_LOG2_DENSE). TiledGrid is not implemented.
 static GridDesc parse_grid(uint32_t n_dims, const Json& j) {
 	const std::string ot = j.string_or("otype", "HashGrid");
-	NGP_CHECK(iequals(ot, "HashGrid") || iequals(ot, "Grid"), "encoding: only HashGrid is implemented (got " + ot + ")");
-	NGP_CHECK(iequals(j.string_or("type", "Hash"), "Hash"), "encoding: only hash grids are implemented");
+	NGP_CHECK(iequals(ot, "HashGrid") || iequals(ot, "DenseGrid") || iequals(ot, "Grid"),
+	          "encoding: HashGrid and DenseGrid are implemented (got " + ot + ")");
+	const std::string type = j.string_or("type", iequals(ot, "DenseGrid") ? "Dense" : "Hash");
+	NGP_CHECK(iequals(type, "Hash") || iequals(type, "Dense"), "encoding: grid type Hash or Dense (got " + type + ")");
 	NGP_CHECK(iequals(j.string_or("interpolation", "Linear"), "Linear"), "encoding: only linear interpolation is implemented");
 	GridDesc g;
 	grid_desc_init(g, n_dims, (uint32_t)j.number_or("n_levels", 16), (uint32_t)j.number_or("n_features_per_level", 2),
-	               (uint32_t)j.number_or("log2_hashmap_size", 19), (uint32_t)j.number_or("base_resolution", 16),
-	               (float)j.number_or("per_level_scale", 2.0));
+	               iequals(type, "Dense") ? GRID_LOG2_DENSE : (uint32_t)j.number_or("log2_hashmap_size", 19),
+	               (uint32_t)j.number_or("base_resolution", 16), (float)j.number_or("per_level_scale", 2.0));
 	return g;
 }
 
@@ -225,8 +231,21 @@ struct ngp_model {
 	bool use_sorted(uint32_t n) const { return grid_backward_mode == 3 || (grid_backward_mode == 0 && n >= 4096); }
 	bool side_prepare(uint32_t n) const { return use_sorted(n) && (overlap & 1); }
 	const ScatterPlan& sc_plan_for(uint32_t n) {
-		if (sc_plan_n != n) { sc_plan = make_scatter_plan(grid, n, grid_bricks); sc_plan_n = n; }
+		if (sc_plan_n != n) {
+			sc_plan = make_scatter_plan(grid, n, grid_bricks);
+			sc_plan_n = n;
+			fb_dirty = true;  // the brick fallback table may now lie over bytes the previous plan used (items)
+		}
 		return sc_plan;
+	}
+	// The brick levels' fallback table must be zero when a backward adds into it (each finalize clears the
+	// entries it reads, so it stays zero between steps of one plan). A new plan moves it (its offset follows
+	// the item regions, sized by the batch): zero it once on the stream before the plan's first backward.
+	bool fb_dirty = true;
+	void clear_brick_fallback(hipStream_t s, void* ws) {
+		if (!fb_dirty) return;
+		if (sc_plan.bk.LD) NGP_HIP(hipMemsetAsync((char*)ws + sc_plan.off_fb, 0, sc_plan.total - sc_plan.off_fb, s));
+		fb_dirty = false;
 	}
 	void* sorted_workspace(uint32_t n) { return scatter_ws.get(sc_plan_for(n).total); }
 	// Phase 1 of the bucketed grid backward on a side stream: it only needs the positions, so it runs
@@ -235,6 +254,7 @@ struct ngp_model {
 		if (!side_prepare(n)) return;
 		ensure_side_stream();
 		void* ws = sorted_workspace(n);
+		clear_brick_fallback(s, ws);  // on s, before the fork: the side stream's plan kernel writes the flag after it
 		GridBwdArgs b{n, in, stride, nullptr, 0, AoS, nullptr, max_level, max_level_per_sample};
 		NGP_HIP(hipEventRecord(ev_fork, s));
 		NGP_HIP(hipStreamWaitEvent(side, ev_fork, 0));
@@ -437,6 +457,7 @@ struct ngp_model {
 	void scatter_grid_grad(hipStream_t s, GridBwdArgs b, bool overwrite, const SlabJob* slab = nullptr, const FusedAdam* fopt = nullptr) {
 		if (use_sorted(b.n)) {
 			void* ws = sorted_workspace(b.n);
+			clear_brick_fallback(s, ws);
 			if (sc_prepared) {
 				NGP_HIP(hipStreamWaitEvent(s, ev_join, 0));
 				sc_prepared = false;
@@ -1049,6 +1070,7 @@ int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, 
 		auto t = std::make_unique<ngp_trainer>();
 		t->model = m;
 		if (optimizer_json) parse_optimizer(Json::parse(optimizer_json), t->cfg);
+		if (const char* e = getenv("NGP_EMA_CLOSED_FORM")) t->cfg.ema_closed_form = atoi(e) != 0;  // A/B runs
 		// the betas are fixed for the trainer's lifetime (only the learning rate has a setter)
 		NGP_HIP(hipMalloc(&t->bias_tab, (size_t)BIAS_TAB_CAP * 2 * sizeof(float)));
 		adam_bias_table(t->bias_tab, t->cfg.beta1, t->cfg.beta2, nullptr);
@@ -1326,6 +1348,20 @@ float ngp_trainer_learning_rate(const ngp_trainer* t) { return t ? t->cfg.lr_at(
 int ngp_trainer_set_learning_rate(ngp_trainer* t, float lr) {
 	NGP_ARG(t && lr >= 0.f);
 	NGP_TRY({ t->cfg.lr = lr; });
+}
+// Trainer options (engine extension). "ema_closed_form": 0 (default) = the lazy layout's owed EMA steps are
+// replayed exactly (optimizer.h ema_catch_up: bit for bit the eager layout), 1 = closed form for gaps of more
+// than 32 steps (A/B and the tolerance test only).
+int ngp_trainer_set_option(ngp_trainer* t, const char* key, double value) {
+	NGP_ARG(t && key);
+	NGP_TRY({
+		const std::string k = key;
+		if (k == "ema_closed_form") {
+			t->cfg.ema_closed_form = value != 0 ? 1u : 0u;
+		} else {
+			throw Error("ngp_trainer_set_option: unknown option " + k);
+		}
+	});
 }
 
 __global__ static void k_f32_to_f16(const float* a, f16* b, f16* c, uint64_t n) {

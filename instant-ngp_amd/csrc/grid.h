@@ -20,6 +20,8 @@ struct GridDesc {
 };
 
 // Host: offset table identical to tcnn's (dense level rounded up to 8 entries, clamped to 2^log2T).
+// log2T = GRID_LOG2_DENSE: a dense grid (tcnn DenseGrid), every level res^D entries with no hashmap cap
+constexpr uint32_t GRID_LOG2_DENSE = 31;
 void grid_desc_init(GridDesc& g, uint32_t D, uint32_t L, uint32_t F, uint32_t log2T, uint32_t Nmin, float b);
 
 enum Layout : uint32_t { AoS = 0, SoA = 1 };

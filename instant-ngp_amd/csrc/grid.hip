@@ -19,7 +19,7 @@ void grid_desc_init(GridDesc& g, uint32_t D, uint32_t L, uint32_t F, uint32_t lo
 	NGP_CHECK(D == 2 || D == 3, "GridEncoding: n_dims must be 2 or 3");
 	NGP_CHECK(L >= 1 && L <= 32, "GridEncoding: n_levels must be in [1, 32]");
 	NGP_CHECK(F == 1 || F == 2 || F == 4 || F == 8, "GridEncoding: n_features_per_level must be 1, 2, 4 or 8");
-	NGP_CHECK(log2T >= 4 && log2T <= 28, "GridEncoding: log2_hashmap_size out of range");
+	NGP_CHECK((log2T >= 4 && log2T <= 28) || log2T == GRID_LOG2_DENSE, "GridEncoding: log2_hashmap_size out of range");
 	g = GridDesc{};
 	g.n_dims = D; g.n_levels = L; g.n_features = F; g.log2_hashmap = log2T; g.base_resolution = Nmin;
 	g.per_level_scale = b;

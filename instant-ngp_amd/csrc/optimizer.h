@@ -9,6 +9,9 @@ struct AdamConfig {
 	float ema_decay = 0.f;  // 0 => no Ema wrapper
 	uint32_t decay_start = 0, decay_interval = 0;  // 0 interval => no ExponentialDecay wrapper
 	float decay_base = 1.f;
+	// lazy layout: how a skipped parameter's owed EMA steps are applied (ema_catch_up). 0 = exact replay (bit
+	// for bit the eager layout), 1 = closed form past EMA_CATCH_UP_LOOP steps (trainer option "ema_closed_form")
+	uint32_t ema_closed_form = 0;
 	float lr_at(uint32_t step) const;  // learning rate used by optimizer step `step` (0-based)
 };
 
@@ -22,7 +25,7 @@ struct AdamConfig {
 // number of optimizer steps whose EMA the parameter has received; a parameter that is skipped (zero
 // grid gradient) keeps its weight, so its missing EMA steps are the same recurrence on the same
 // weight and are applied, in order and with the same fp32 operations, when it is next updated or when
-// the inference (EMA) parameters are read (ema_materialize): bit-identical to the eager update.
+// the inference (EMA) parameters are read (ema_materialize): bit-identical to the eager update (ema_catch_up).
 // The fp32 master weights of the pair live in the record too (`w`): an update then reads and writes one
 // record instead of the record plus a separate line of the w32 array. The trainer's w32 array is a
 // mirror in this layout, refreshed when it is read (adam_rec_weights).
@@ -69,20 +72,36 @@ __device__ __forceinline__ float lr_schedule(const AdamConfig& c, uint32_t step)
 	for (uint32_t i = 0; i < k; ++i) r *= c.decay_base;
 	return r;
 }
-// The eager EMA of step j: e = d * e + (1 - d) * w (w after step j's update), output e / (1 - d^(j+1)).
-// A parameter skipped for k steps kept its weight w, so its EMA is owed k applications of that recurrence.
-// Up to EMA_CATCH_UP_LOOP of them are replayed one by one (bit-identical to the eager layout); a longer
-// gap uses the closed form d^k e + (1 - d^k) w, which differs from the replay by rounding only. Replaying
-// every step made a rarely touched entry loop over its whole gap (NeRF: tens of thousands of steps for
-// entries at the edge of the occupied space), and the kernel waited for that thread.
+// The eager EMA of step j: e = d * e + (1 - d) * w (w after step j's update), output e / (1 - d^(j+1)). Every
+// site evaluates the recurrence as ema_step, RN(RN(d e) + RN((1 - d) w)) (the engine builds with
+// -ffp-contract=off, as the oracle does), so the eager kernels, the lazy update and the catch-up below round
+// identically.
+__device__ __forceinline__ float ema_step(float e, float d, float dw) { return d * e + dw; }
+// A parameter skipped for k steps kept its weight w, so its EMA is owed k applications of that recurrence
+// with a constant addend. The map e -> RN(RN(d e) + RN((1 - d) w)) is non-decreasing in e (d > 0, RN is
+// monotone), so the replayed sequence is monotone and, on the finite set of floats, reaches a fixed point
+// after which every step leaves it unchanged. The exact catch-up therefore replays until the gap is
+// exhausted or a step changes nothing: bit for bit the eager layout's value whatever the gap, in at most a
+// few hundred steps (d = 0.95: the distance to w shrinks by 0.95 per step until one step's change rounds
+// away; 200-600 steps from random float starts). Replaying the whole gap made a rarely touched entry loop
+// over tens of thousands of steps (NeRF: entries at the edge of the occupied space) while the kernel waited
+// for that thread. closed != 0 (AdamConfig::ema_closed_form): past EMA_CATCH_UP_LOOP steps use
+// d^k e + (1 - d^k) w instead, which differs from the replay by rounding (tests/test_gpu_ema_gaps.py).
 constexpr uint32_t EMA_CATCH_UP_LOOP = 32;
-__device__ __forceinline__ float ema_catch_up(float e, float w, float d, uint32_t from, uint32_t to) {
+__device__ __forceinline__ float ema_catch_up(float e, float w, float d, uint32_t from, uint32_t to, uint32_t closed = 0) {
 	if (to <= from) return e;
-	if (to - from > EMA_CATCH_UP_LOOP) {
-		const float dk = powf(d, (float)(to - from));
+	uint32_t k = to - from;
+	if (closed && k > EMA_CATCH_UP_LOOP) {
+		const float dk = powf(d, (float)k);
 		return dk * e + (1.f - dk) * w;
 	}
-	for (uint32_t j = from; j < to; ++j) e = d * e + (1.f - d) * w;
+	const float dw = (1.f - d) * w;
+	for (; k >= 4; k -= 4) {
+		const float e1 = ema_step(e, d, dw), e2 = ema_step(e1, d, dw), e3 = ema_step(e2, d, dw), e4 = ema_step(e3, d, dw);
+		if (e4 == e3) return e4;  // fixed point: the rest of the gap leaves it unchanged
+		e = e4;
+	}
+	for (; k; --k) e = ema_step(e, d, dw);
 	return e;
 }
 
@@ -118,7 +137,7 @@ __device__ __forceinline__ void lazy_update(const AdamState& st, const AdamConfi
 			const int p = 2 * r + k;
 			if (!G.act[p]) continue;
 			// missing EMA steps first, with the weight those steps saw (unchanged since the last update)
-			if (d > 0.f) rc.ema[k] = ema_catch_up(rc.ema[k], w[p], d, rc.done[k], step);
+			if (d > 0.f) rc.ema[k] = ema_catch_up(rc.ema[k], w[p], d, rc.done[k], step, c.ema_closed_form);
 			float gk = G.g[p];
 			if (i0 + p < n_matrix) gk += c.l2 * w[p];
 			const float mm = c.beta1 * rc.m1[k] + (1.f - c.beta1) * gk;
@@ -129,7 +148,7 @@ __device__ __forceinline__ void lazy_update(const AdamState& st, const AdamConfi
 			rc.steps[k] = sk;
 			const float lr_s = adam_step_size(c, lr, sk, st.bias_tab);
 			w[p] = w[p] - lr_s / (sqrtf(vv) + c.eps) * mm;
-			if (d > 0.f) rc.ema[k] = d * rc.ema[k] + (1.f - d) * w[p];
+			if (d > 0.f) rc.ema[k] = ema_step(rc.ema[k], d, (1.f - d) * w[p]);
 			rc.done[k] = step + 1;
 		}
 		f32x4* rp = (f32x4*)(st.rec + (i0 >> 1) + r);
@@ -202,7 +221,7 @@ __device__ __forceinline__ void fused_adam_store(const FusedAdam& fa, uint32_t r
 #pragma unroll
 	for (int k = 0; k < 2; ++k) {
 		if (!p.act[k]) continue;
-		if (d > 0.f) ema[k] = ema_catch_up(ema[k], w[k], d, done[k], step);
+		if (d > 0.f) ema[k] = ema_catch_up(ema[k], w[k], d, done[k], step, c.ema_closed_form);
 		const float gk = p.g[k];
 		const float mm = c.beta1 * m1[k] + (1.f - c.beta1) * gk;
 		const float vv = c.beta2 * m2[k] + (1.f - c.beta2) * (gk * gk);
@@ -212,7 +231,7 @@ __device__ __forceinline__ void fused_adam_store(const FusedAdam& fa, uint32_t r
 		steps[k] = sk;
 		const float lr_s = adam_step_size(c, lr, sk, fa.bias_tab);
 		w[k] = w[k] - lr_s / (sqrtf(vv) + c.eps) * mm;
-		if (d > 0.f) ema[k] = d * ema[k] + (1.f - d) * w[k];
+		if (d > 0.f) ema[k] = ema_step(ema[k], d, (1.f - d) * w[k]);
 		done[k] = step + 1;
 	}
 	f32x4* rp = (f32x4*)(fa.rec + r);

@@ -57,7 +57,7 @@ __global__ void k_adam_ema(const uint32_t i0, const uint32_t n, const uint32_t n
 		}
 		if (st.ema32) {
 			const float debias = 1.f - powf(c.ema_decay, (float)(step + 1));
-			const float v = c.ema_decay * st.ema32[i] + (1.f - c.ema_decay) * w;
+			const float v = ema_step(st.ema32[i], c.ema_decay, (1.f - c.ema_decay) * w);
 			st.ema32[i] = v;
 			st.ema16[i] = (f16)(v / debias);
 		}
@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(256) k_adam_ema4(const uint32_t n4, const uint
 		f16x4 eh;
 #pragma unroll
 		for (int k = 0; k < 4; ++k) {
-			e[k] = c.ema_decay * e[k] + (1.f - c.ema_decay) * w[k];
+			e[k] = ema_step(e[k], c.ema_decay, (1.f - c.ema_decay) * w[k]);
 			eh[k] = (f16)(e[k] / debias);
 		}
 		*(f32x4*)(st.ema32 + i0) = e;
@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(256) k_adam_lazy4(const uint32_t n4, const uin
 	if (two) lazy_update(st, c, step, n_matrix, B);
 }
 
-__global__ void k_ema_materialize(uint32_t n, float d, uint32_t steps_done, const AdamState st) {
+__global__ void k_ema_materialize(uint32_t n, float d, uint32_t steps_done, uint32_t closed, const AdamState st) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
 	const float debias = 1.f - powf(d, (float)steps_done);  // on the device, as the eager kernel computes it
@@ -181,7 +181,7 @@ __global__ void k_ema_materialize(uint32_t n, float d, uint32_t steps_done, cons
 	float e = rp->ema[k];
 	const uint32_t done = rp->done[k];
 	if (done < steps_done) {
-		e = ema_catch_up(e, rp->w[k], d, done, steps_done);
+		e = ema_catch_up(e, rp->w[k], d, done, steps_done, closed);
 		rp->ema[k] = e;
 		rp->done[k] = steps_done;
 	}
@@ -214,7 +214,7 @@ __global__ void k_rec_weights(uint32_t n, AdamRec* rec, float* w32, bool to_rec)
 
 void ema_materialize(const AdamConfig& c, uint32_t n, uint32_t steps_done, const AdamState& st, hipStream_t s) {
 	if (c.ema_decay <= 0.f || steps_done == 0 || n == 0) return;
-	k_ema_materialize<<<div_round_up(n, 256), 256, 0, s>>>(n, c.ema_decay, steps_done, st);
+	k_ema_materialize<<<div_round_up(n, 256), 256, 0, s>>>(n, c.ema_decay, steps_done, c.ema_closed_form, st);
 	NGP_HIP(hipGetLastError());
 }
 

@@ -318,9 +318,16 @@ public:
 		free_network();
 		m_training_step = 0;
 		m_loss_scalar = 0.f;
+		// testbed.cu:3975-3997: a missing base_resolution becomes 2^(log2_hashmap_size / n_pos) and is written
+		// into the config. per_level_scale: the fork sets only its log member to 2.0 (:3991), so the auto-scale
+		// branch never runs and the encoding config reaches the network unchanged (:4037): a config's own value
+		// stays (configs/nerf/densegrid.json 1.405), an absent key is tcnn's default 2.0 (parse_grid)
 		Json enc = m_network_config["encoding"];
-		enc.obj["per_level_scale"].type = Json::Number;  // the fork forces 2.0 for every grid (testbed.cu:3991)
-		enc.obj["per_level_scale"].num = 2.0;
+		const uint32_t n_pos = m_testbed_mode == ETestbedMode::Image ? 2u : 3u;
+		if (enc.number_or("base_resolution", 0.0) == 0.0) {
+			enc.obj["base_resolution"].type = Json::Number;
+			enc.obj["base_resolution"].num = (double)(1u << ((uint32_t)enc.number_or("log2_hashmap_size", 15.0) / n_pos));
+		}
 		const std::string opt = m_network_config["optimizer"].dump();
 		switch (m_testbed_mode) {
 		case ETestbedMode::Nerf: {

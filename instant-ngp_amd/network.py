@@ -314,6 +314,10 @@ class Trainer:
     def learning_rate(self, lr):
         check(lib().ngp_trainer_set_learning_rate(self.handle, float(lr)))
 
+    def set_option(self, key, value):
+        """Engine trainer option (ngp_trainer_set_option), e.g. "ema_closed_form"."""
+        check(lib().ngp_trainer_set_option(self.handle, key.encode(), float(value)))
+
     def set_params_full_precision(self, params_host):
         import numpy as np
         a = np.ascontiguousarray(params_host, dtype=np.float32)

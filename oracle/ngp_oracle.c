@@ -864,6 +864,18 @@ EXPORT float orc_lr_at_step(const orc_adam_cfg* c, uint32_t step) {
 	return lr;
 }
 
+/* tcnn Ema: after the nested optimizer's step `step` (0-based), every parameter's EMA takes the new weight,
+ * skipped parameters included: e = d e + (1 - d) w, and the inference parameter is e debiased by 1 - d^(step+1).
+ * The lazy-EMA layout of the engine must equal this per-step recurrence (tests/test_gpu_ema_gaps.py). */
+static inline void ema_one(float d, float debias, float w, float* e32, uint16_t* e16) {
+	float v = *e32 = d * *e32 + (1.f - d) * w;
+	*e16 = fh(v / debias);
+}
+EXPORT void orc_ema_step(float d, uint32_t step, size_t n, const float* w32, float* ema32, uint16_t* ema16) {
+	float debias = 1.f - powf(d, (float)(step + 1));
+	for (size_t i = 0; i < n; ++i) ema_one(d, debias, w32[i], ema32 + i, ema16 + i);
+}
+
 EXPORT void orc_adam_step(const orc_adam_cfg* c, uint32_t step, size_t n, size_t n_matrix, float loss_scale,
                           float* w32, uint16_t* w16, const uint16_t* g16, float* m1, float* m2, uint32_t* steps,
                           float* ema32, uint16_t* ema16) {
@@ -884,12 +896,7 @@ EXPORT void orc_adam_step(const orc_adam_cfg* c, uint32_t step, size_t n, size_t
 			w16[i] = fh(nw);
 		}
 	ema:
-		if (c->ema_decay > 0.f && ema32) {
-			float d = c->ema_decay;
-			float v = ema32[i] = d * ema32[i] + (1.f - d) * w32[i];
-			float debias = 1.f - powf(d, (float)(step + 1));
-			ema16[i] = fh(v / debias);
-		}
+		if (c->ema_decay > 0.f && ema32) ema_one(c->ema_decay, 1.f - powf(c->ema_decay, (float)(step + 1)), w32[i], ema32 + i, ema16 + i);
 	}
 }
 

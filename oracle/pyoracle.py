@@ -98,6 +98,7 @@ def _declare(L):
     d("orc_nerf_init", None, P, u64, P)
     d("orc_lr_at_step", f32, P, u32)
     d("orc_adam_step", None, P, u32, sz, sz, f32, P, P, P, P, P, P, P, P)
+    d("orc_ema_step", None, f32, u32, sz, P, P, P)
     d("orc_morton3D", u32, u32, u32, u32)
     d("orc_srgb_to_linear", f32, f32)
     d("orc_linear_to_srgb", f32, f32)
@@ -387,6 +388,11 @@ def net_train_ex(grid, mlp, params16, pos, dL_dout, stride=None):
 def adam_step(cfg, step, n_matrix, loss_scale, w32, w16, g16, m1, m2, steps, ema32=None, ema16=None):
     lib().orc_adam_step(C.byref(cfg), step, w32.size, n_matrix, loss_scale, ptr(w32), ptr(w16), ptr(g16), ptr(m1),
                         ptr(m2), ptr(steps), ptr(ema32), ptr(ema16))
+
+
+def ema_step(decay, step, w32, ema32, ema16):
+    """tcnn Ema after optimizer step `step`: ema32 = d ema32 + (1 - d) w32, ema16 = fp16(ema32 / (1 - d^(step+1)))."""
+    lib().orc_ema_step(decay, step, w32.size, ptr(np.ascontiguousarray(w32, np.float32)), ptr(ema32), ptr(ema16))
 
 
 # ---------------------------------------------------------------------------------------------

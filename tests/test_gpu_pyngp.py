@@ -142,3 +142,41 @@ def test_testbed_sdf_and_image_modes(pkg, tmp_path):
     out = tb.render(64, 48, spp=1, linear=True)
     assert out.shape == (48, 64, 4) and np.isfinite(out).all()
     assert tb.loss < first
+
+
+def _dense_entries(levels, b, nmin=16, d=3):
+    """tcnn's offset table for a DenseGrid: res^D rounded to 8 per level, no hashmap cap (float32 as the engine)."""
+    f32 = np.float32
+    total = 0
+    for l in range(levels):
+        s = f32(np.exp2(f32(l) * np.log2(f32(b)))) * f32(nmin) - f32(1)
+        res = int(np.ceil(s)) + 1
+        total += (res ** d + 7) // 8 * 8
+    return total
+
+
+def test_reload_network_keeps_the_configs_per_level_scale(pkg, scene_dir, tmp_path):
+    """reset_network (testbed.cu:3975-3997, 4037): the fork writes 2.0 only into its log member, so a config's own
+    per_level_scale reaches the encoding (configs/nerf/densegrid.json: DenseGrid, 8 levels, b = 1.405), and a
+    missing base_resolution becomes 2^(log2_hashmap_size / 3)."""
+    ngp = pkg.pyngp()
+    (tmp_path / "base.json").write_text(ngp.default_network_config(ngp.TestbedMode.Nerf))
+    (tmp_path / "densegrid.json").write_text(
+        '{\t// multiresolution dense grid - 8 levels, from res 16 to 173\n\t"parent" : "base.json",\n'
+        '\t"encoding": {"otype": "DenseGrid", "n_levels": 8, "base_resolution": 16, "per_level_scale": 1.405}\n}\n')
+    tb = ngp.Testbed()
+    tb.load_training_data(scene_dir)
+    tb.reload_network_from_file(str(tmp_path / "densegrid.json"))
+    assert tb.n_encoding_params() == 4 * _dense_entries(8, 1.405)  # base.json's 4 features per level
+    tb.shall_train = True
+    for _ in range(3):
+        tb.frame()
+    assert tb.training_step == 3 and np.isfinite(tb.loss)
+    # a hash grid with its own scale and no base_resolution: N_min = 2^(15 / 3) = 32 with the default T = 2^15
+    (tmp_path / "own.json").write_text('{"parent": "base.json", "encoding": {"otype": "HashGrid", "n_levels": 2, '
+                                       '"n_features_per_level": 2, "log2_hashmap_size": 15, "base_resolution": 0, '
+                                       '"per_level_scale": 1.5}}')
+    tb.reload_network_from_file(str(tmp_path / "own.json"))
+    res = [32, int(np.ceil(np.float32(1.5) * np.float32(32) - np.float32(1))) + 1]
+    assert tb.n_encoding_params() == 2 * sum(min((r ** 3 + 7) // 8 * 8, 1 << 15) for r in res)
+    assert json.loads(tb.network_config)["encoding"]["per_level_scale"] == 1.5
