@@ -286,7 +286,7 @@ def timed_steps(lib, step, steps, warmup, world, capture=None, comm=None):
     return t1 - t0, ("hip_graph" if graph is not None else (graph_note or "eager")), prof
 
 
-def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None, wire="f32"):
+def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None, wire="f32", shard=True, exchange_at_world_1=False):
     """NerfNetwork + Trainer for C2/C2' with a resident synthetic batch; returns (step, capture, net, trainer,
     comm). step() is Trainer.train_step, the eager form of the captured step (the grid's update fused into
     the backward on the lazy layout, the exchange hook, the optimizer), so the per-kernel replay profiles
@@ -302,12 +302,16 @@ def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None, wire="f32"):
     net.reserve(n)
     x, dL = synthetic_batch(n, 1337 + rank, "cuda")
     comm = None
-    if world > 1:
-        # nccl: the engine's own RCCL communicator, the gradient all-reduce enqueued by the engine on its
+    if world > 1 or exchange_at_world_1:
+        # nccl: the engine's own RCCL communicator, the gradient exchange enqueued by the engine on its
         # stream between the backward and the optimizer and captured into the step's graph; gloo (ranks
-        # sharing one GPU): a host round trip through torch.distributed, eager steps only
-        comm = pkg.dp.make_comm(rank, world, wire=wire)
-        trainer.set_allreduce(comm)
+        # sharing one GPU): a host round trip through torch.distributed, eager steps only. A world of one
+        # (exchange_at_world_1, no process group): the engine communicator alone, for the dp1_overhead record
+        comm = pkg.dp.EngineComm(0, 1, wire=wire) if world == 1 else pkg.dp.make_comm(rank, world, wire=wire)
+        if shard:
+            trainer.set_data_parallel(comm)  # sharded optimizer: reduce-scatter, slice update, all-gather
+        else:
+            trainer.set_allreduce(comm)
     loss_scale = 128.0
 
     def step():
@@ -454,6 +458,13 @@ def optimizer_counts(net, trainer, step, fused=False):
     return nm + nz, net.n_params - nm - nz, None
 
 
+def exchange_ms(kernels):
+    """Per-step time of the gradient exchange: the engine profiler's RCCL phases (allreduce, or reduce_scatter +
+    all_gather) or, for gloo ranks, the host round-trip timer reported as "allreduce"."""
+    ph = [kernels[k] for k in ("allreduce", "reduce_scatter", "all_gather") if k in kernels]
+    return round(sum(v["ms"] / max(v["calls"], 1) for v in ph), 4) if ph else None
+
+
 # engine profiler phases that enclose other phases (the NeRF step's outer scopes; not added in kernels_sum_ms)
 NESTED_PHASES = {"nerf_sample", "nerf_density_grid", "nerf_inference", "nerf_loss", "nerf_train_pass"}
 
@@ -517,6 +528,10 @@ def main():
     ap.add_argument("--wire", default="f32", choices=["f32", "f16"],
                     help="gradient all-reduce wire type (f32: fp16 sums widened, rounded once)")
     ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling sub-record")
+    ap.add_argument("--dp-shard", type=int, default=1,
+                    help="N > 1: 1 = sharded optimizer (reduce-scatter fp32, slice update, all-gather fp16 weights), "
+                         "0 = one fp32 all-reduce of the gradients and a replicated update")
+    ap.add_argument("--no-dp1", action="store_true", help="N = 1: skip the dp1_overhead sub-record")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo"],
                     help="N > 1 exchange: rccl (engine RCCL communicator, one GPU per rank) or gloo (host round "
                          "trip through torch.distributed: ranks may share a GPU, eager steps only)")
@@ -566,7 +581,7 @@ def main():
     comm = None
     if args.variant in ("C2", "C2p"):
         step, capture, net, trainer, comm = nerf_pass(pkg, args.variant, n, rank, world, args.opt, args.overlap,
-                                                      args.wire)
+                                                      args.wire, shard=bool(args.dp_shard))
         if not args.no_opt_count:
             *n_opt, c5_fused = optimizer_counts(net, trainer, step, fused=trainer.fused_update_active(n))
         if not args.graph:
@@ -609,14 +624,14 @@ def main():
         # the other scaling mode in the same line: weak = fixed batch per GPU (headline), strong = one
         # global --batch sharded over the N ranks
         n_s = args.batch // world if args.scaling == "weak" else args.batch
-        s_s, c_s, _, _, comm_s = nerf_pass(pkg, args.variant, n_s, rank, world, args.opt, args.overlap, args.wire)
+        s_s, c_s, _, _, comm_s = nerf_pass(pkg, args.variant, n_s, rank, world, args.opt, args.overlap, args.wire,
+                                           shard=bool(args.dp_shard))
         dts, launch_s, k_s = timed_steps(lib, s_s, args.steps, args.warmup, world, c_s if args.graph else None, comm_s)
         dts = pkg.dp.reduce_scalar(dts, "max")
-        ar = k_s.get("allreduce")
         strong = {"scaling": "strong" if args.scaling == "weak" else "weak", "batch_per_gpu": n_s,
                   "global_batch": n_s * world, "value": n_s * world * args.steps / dts, "unit": "samples/s",
                   "ms_per_step": dts / args.steps * 1e3, "launch": launch_s,
-                  "allreduce_ms_per_step": None if ar is None else round(ar["ms"] / max(ar["calls"], 1), 4)}
+                  "exchange_ms_per_step": exchange_ms(k_s)}
         del s_s, c_s, comm_s
     e2e_dp = None
     if world > 1 and args.variant == "C2" and args.e2e_seconds > 0:
@@ -645,9 +660,11 @@ def main():
             "config": {"workload": WORKLOADS[args.variant],
                        "batch_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
                        "launch": launch,
-                       "exchange": ((f"engine RCCL all-reduce of the gradient buffer per step ({args.wire} on the wire)"
-                                     if args.comm == "rccl" else
-                                     "gloo all-reduce of the gradient buffer per step (host round trip, fp32)")
+                       "exchange": (("sharded optimizer: fp32 reduce-scatter of the widened gradients, 1/N of the "
+                                     "optimizer records updated per rank, fp16 all-gather of the weights" if args.dp_shard else
+                                     f"all-reduce of the gradient buffer ({args.wire} on the wire), replicated update")
+                                    + (" (engine RCCL communicator, inside the step's graph)" if args.comm == "rccl" else
+                                       " (gloo host round trips)")
                                     if world > 1 else None)},
             "kernel_timing": ("HIP events per kernel on the launch stream, eager replay of the same K steps queued "
                               "behind a graph launch" if launch == "hip_graph" else "HIP events per kernel over the timed region"),
@@ -658,9 +675,11 @@ def main():
             "kernels": kern_summary,
         }
         if world > 1:
-            ar = kernels.get("allreduce")
-            res["allreduce_ms_per_step"] = None if ar is None else round(ar["ms"] / max(ar["calls"], 1), 4)
-            res["allreduce_bytes"] = (4 if args.wire == "f32" else 2) * int(n_params_total)
+            res["exchange_ms_per_step"] = exchange_ms(kernels)
+            q = 8 * world
+            n_pad = (int(n_params_total) + q - 1) // q * q
+            res["exchange_bytes"] = ({"reduce_scatter_f32": 4 * n_pad, "all_gather_f16": 2 * n_pad} if args.dp_shard else
+                                     {"all_reduce": (4 if args.wire == "f32" else 2) * int(n_params_total)})
             if strong is not None:
                 res["strong"] = strong
             res["param_sha1_per_rank"] = param_hashes
@@ -675,6 +694,24 @@ def main():
             if e2e_dp is not None:
                 res["e2e"] = {k: e2e_dp[k] for k in ("value", "unit", "psnr", "psnr_views", "train_seconds", "steps",
                                                      "ms_per_step", "n_gpus", "data", "config")}
+        if world == 1 and args.variant in ("C2", "C2p") and not args.no_dp1 and args.comm == "rccl":
+            # the data-parallel step's own cost, measured where it can be (one GPU): the same pass with the
+            # engine's RCCL communicator attached at world 1, timed like the headline (one graph of K steps),
+            # sharded (reduce-scatter + slice update + all-gather) and all-reduce, against the fused N = 1 step
+            res["dp1_overhead"] = {"note": "world-1 RCCL exchange attached, vs the fused single-GPU step above. shard: "
+                                           "the backward stores the fp32 gradient itself, reduce-scatter, the rank's "
+                                           "slice of the optimizer (here all of it), all-gather of the fp16 weights; "
+                                           "allreduce: fp16 gradient, widen, all-reduce, narrow, replicated update"}
+            for mode in ("shard", "allreduce"):
+                sd, cd, _, _, commd = nerf_pass(pkg, args.variant, n, 0, 1, args.opt, args.overlap, args.wire,
+                                                shard=mode == "shard", exchange_at_world_1=True)
+                dtd, launchd, kd = timed_steps(lib, sd, args.steps, args.warmup, 1, cd if args.graph else None)
+                res["dp1_overhead"][mode] = {
+                    "ms_per_step": dtd / args.steps * 1e3, "launch": launchd,
+                    "overhead_us": round((dtd - dt) / args.steps * 1e6, 2),
+                    "phases_us": {k: round(v["ms"] / max(v["calls"], 1) * 1e3, 2) for k, v in kd.items()}}
+                del sd, cd, commd
+            torch.cuda.synchronize()
         if world == 1 and args.variant == "C2":
             if not args.no_c2p:
                 # BASELINE's literal "L=16": the same training pass at C2' (L=16 F=2 T=2^19)

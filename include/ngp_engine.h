@@ -186,7 +186,8 @@ float ngp_trainer_learning_rate(const ngp_trainer* t);     /* optimizer->learnin
 int ngp_trainer_set_learning_rate(ngp_trainer* t, float lr);
 /* Engine extension: trainer options. "ema_closed_form" 0 (default) / 1: how the large-table (lazy-EMA) layout
  * applies the EMA steps a skipped parameter owes: exact replay to the recurrence's fixed point, bit for bit the
- * per-step Ema of tcnn's chain (configs/nerf/base.json:5-8), or a closed form past 32 steps (within 1 fp16 ulp). */
+ * per-step Ema of tcnn's chain (configs/nerf/base.json:5-8), or a closed form past 32 steps (within 1 fp16 ulp).
+ * "shard_opt" 1 (default) / 0: the sharded optimizer under ngp_trainer_set_data_parallel (see there). */
 int ngp_trainer_set_option(ngp_trainer* t, const char* key, double value);
 /* set_params_full_precision (src/testbed.cu:4146): host fp32 -> master, fp16 params and inference params */
 int ngp_trainer_set_params_full_precision(ngp_trainer* t, const float* params_host, uint64_t n);
@@ -406,6 +407,11 @@ int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_confi
  * rays [R r / N, R (r+1) / N) with their global ids and compacts to B / N samples. */
 enum { NGP_DTYPE_F32 = 0, NGP_DTYPE_F16 = 1 };
 enum { NGP_REDUCE_SUM = 0, NGP_REDUCE_MAX = 1 };
+/* Collectives of the sharded optimizer (ngp_trainer_set_data_parallel), passed in `op` of the same hook. `count`
+ * is the whole buffer, a multiple of world; rank r's slice is [r count / world, (r + 1) count / world).
+ * NGP_REDUCE_SCATTER_SUM: every rank's buffer summed, the sum of rank r's slice left in rank r's slice (other
+ * slices undefined afterwards). NGP_ALL_GATHER: every rank's slice copied into that slice of every rank. */
+enum { NGP_REDUCE_SCATTER_SUM = 2, NGP_ALL_GATHER = 3 };
 typedef int (*ngp_allreduce_fn)(void* user, void* device_buf, uint64_t count, int dtype, int op, void* stream);
 int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn allreduce, void* user);
 // Sampler pipelining (default on, single GPU): when no density-grid update is due before the next
@@ -470,6 +476,18 @@ int ngp_dp_comm_reserve(ngp_dp_comm* c, uint64_t count);
  * optimizer, the fp16 gradient buffer is all-reduced (sum) with `allreduce`; the optimizer divides
  * by `world` (mean gradient) on top of its loss scale. allreduce = NULL turns it off. */
 int ngp_trainer_set_allreduce(ngp_trainer* t, uint32_t world, ngp_allreduce_fn allreduce, void* user);
+/* The same exchange with this process's rank, so that large-table (lazy-EMA) trainers shard the optimizer
+ * (trainer option "shard_opt", default 1): the fp16 gradients, widened to fp32, are reduce-scattered; rank r
+ * updates the optimizer records of its 1/world slice of the parameters from the fp32 sums rounded to fp16
+ * once (bit for bit the all-reduce path's update) and the fp16 weights are all-gathered: half the wire bytes
+ * of an fp32 all-reduce and 1/world of the update per rank. Other trainers, and shard_opt 0, all-reduce.
+ * With world > 1 the records of other ranks' slices are stale on this rank after a sharded step: the EMA
+ * (inference) parameters, the full-precision weights and serialize need ngp_trainer_gather_shards first,
+ * called on every rank (they fail otherwise); the fp16 training parameters are always complete. */
+int ngp_trainer_set_data_parallel(ngp_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn fn, void* user);
+/* Collective (every rank, same order): all-gather the sharded optimizer records so that every rank holds the
+ * whole optimizer state again. A no-op unless a sharded step left them partial. */
+int ngp_trainer_gather_shards(ngp_trainer* t, void* stream);
 
 #pragma GCC visibility pop
 #ifdef __cplusplus

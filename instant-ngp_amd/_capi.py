@@ -181,6 +181,8 @@ SIGNATURES = {
     "ngp_dp_comm_set_wire": (i32, [P, i32]),
     "ngp_dp_comm_reserve": (i32, [P, u64]),
     "ngp_trainer_set_allreduce": (i32, [P, u32, P, P]),
+    "ngp_trainer_set_data_parallel": (i32, [P, u32, u32, P, P]),
+    "ngp_trainer_gather_shards": (i32, [P, P]),
     "ngp_nerf_renderer_create": (i32, [C.POINTER(P)]),
     "ngp_nerf_renderer_destroy": (None, [P]),
     "ngp_nerf_renderer_set_mode": (i32, [P, i32]),

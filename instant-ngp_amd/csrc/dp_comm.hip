@@ -56,6 +56,11 @@ __global__ void k_narrow_f32(const float* __restrict__ b, f16* __restrict__ a, u
 		for (uint64_t j = i; j < n && j < i + 8; ++j) a[j] = (f16)b[j];
 	}
 }
+void widen_f16(const f16* a, float* b, uint64_t n, hipStream_t s) {
+	if (n == 0) return;
+	k_widen_f16<<<(uint32_t)((n + 8 * 256 - 1) / (8 * 256)), 256, 0, s>>>(a, b, n, (uintptr_t)a % 16 == 0 && (uintptr_t)b % 16 == 0);
+	NGP_HIP(hipGetLastError());
+}
 }  // namespace ngp
 
 namespace {
@@ -129,6 +134,24 @@ int ngp_dp_comm_allreduce(void* user, void* buf, uint64_t count, int dtype, int 
 	if (count == 0) return NGP_OK;
 	const ncclRedOp_t o = op == NGP_REDUCE_MAX ? ncclMax : ncclSum;
 	hipStream_t s = (hipStream_t)stream;
+	if (op == NGP_REDUCE_SCATTER_SUM || op == NGP_ALL_GATHER) {
+		// in place: rank r's slice [r c, (r + 1) c) of the count = world c elements
+		if (count % (uint64_t)c->world) {
+			ngp::set_last_error("ngp_dp_comm_allreduce: reduce-scatter / all-gather count must be a multiple of world");
+			return NGP_INVALID;
+		}
+		const size_t per = (size_t)(count / (uint64_t)c->world), esz = dtype == NGP_DTYPE_F16 ? 2 : 4;
+		const ncclDataType_t t = dtype == NGP_DTYPE_F16 ? ncclFloat16 : ncclFloat32;
+		char* mine = (char*)buf + (size_t)c->rank * per * esz;
+		if (op == NGP_REDUCE_SCATTER_SUM) {
+			ngp::ProfScope ps("reduce_scatter", s);
+			const ncclResult_t r = ncclReduceScatter(buf, mine, per, t, ncclSum, c->comm, s);
+			return r == ncclSuccess ? NGP_OK : fail("ncclReduceScatter", r);
+		}
+		ngp::ProfScope ps("all_gather", s);
+		const ncclResult_t r = ncclAllGather(mine, buf, per, t, c->comm, s);
+		return r == ncclSuccess ? NGP_OK : fail("ncclAllGather", r);
+	}
 	ngp::ProfScope ps("allreduce", s);
 	if (dtype == NGP_DTYPE_F16 && op == NGP_REDUCE_SUM && c->wire == NGP_DTYPE_F32) {
 		// widened sum: fp16 -> fp32 staging, fp32 ring all-reduce, one rounding back to fp16. The staging

@@ -229,6 +229,9 @@ struct ngp_model {
 		NGP_HIP(hipEventCreateWithFlags(&ev_red, hipEventDisableTiming));
 	}
 	bool use_sorted(uint32_t n) const { return grid_backward_mode == 3 || (grid_backward_mode == 0 && n >= 4096); }
+	// the backward can store the whole gradient as fp32 itself (FusedAdam::g32): bucketed grid backward with the
+	// dW slab reduction in its last kernel
+	bool grad32_ok(uint32_t n) const { return use_sorted(n) && fuse_slabs && !(overlap & 4) && grid.n_features >= 2; }
 	bool side_prepare(uint32_t n) const { return use_sorted(n) && (overlap & 1); }
 	const ScatterPlan& sc_plan_for(uint32_t n) {
 		if (sc_plan_n != n) {
@@ -425,6 +428,14 @@ struct ngp_model {
 		SlabJob sj;
 		sj.slabs = slab; sj.n_slabs = blocks; sj.n = n_red; sj.grad = gradients; sj.stride = (uint32_t)n_matrix();
 		sj.accumulate = grad_mode == NGP_GRAD_ACCUMULATE;
+		FusedAdam f32store;
+		if (fopt && fopt->g32) {
+			// the sharded optimizer's input: the whole gradient stored widened to fp32 by the backward itself
+			NGP_CHECK(fused && grad_mode == NGP_GRAD_OVERWRITE && !fopt->rec, "fp32 gradient store: fused slab reduction");
+			sj.grad32 = fopt->g32;
+			f32store.g32 = fopt->g32 + grid_offset();
+			fopt = &f32store;
+		}
 		hipStream_t rs = s;
 		if (ovl) {
 			ensure_side_stream();
@@ -466,7 +477,8 @@ struct ngp_model {
 				grid_scatter_prepare(grid, b, sc_plan, ws, s, sc_hist_done);
 			}
 			sc_hist_done = false;
-			ProfScope ps(fopt ? "grid_backward_adam" : "grid_backward_sorted", s);  // _adam: with the grid's optimizer update
+			// _adam: with the grid's optimizer update
+			ProfScope ps(fopt && fopt->rec ? "grid_backward_adam" : "grid_backward_sorted", s);
 			grid_backward_sorted(grid, b, sc_plan, ws, s, overwrite, win_debug, slab, fopt);
 			return;
 		}
@@ -498,6 +510,7 @@ struct ngp_trainer {
 	bool w32_stale = false;
 	void sync_w32() {
 		if (!rec || !w32_stale) return;
+		require_full_state("full-precision weights");
 		NGP_HIP(hipDeviceSynchronize());  // the optimizer may still run on a caller's non-blocking stream
 		adam_rec_weights((uint32_t)n, rec, w32, false, nullptr);
 		NGP_HIP(hipDeviceSynchronize());
@@ -505,6 +518,7 @@ struct ngp_trainer {
 	}
 	void materialize(hipStream_t s, bool force = false) {
 		if (!rec || (!inf_stale && !force)) return;
+		require_full_state("inference (EMA) parameters");
 		AdamState st{w32, w16, g16, nullptr, nullptr, nullptr, nullptr, inf16, nullptr, nullptr, nullptr, 0, nullptr, rec};
 		ema_materialize(cfg, (uint32_t)n, step, st, s);
 		inf_stale = false;
@@ -518,9 +532,60 @@ struct ngp_trainer {
 	ngp_allreduce_fn allreduce = nullptr;  // gradient exchange inside captured steps (ngp_trainer_set_allreduce)
 	void* allreduce_user = nullptr;
 	uint32_t world = 1;
+	// sharded optimizer (ngp_trainer_set_data_parallel): this rank, the fp32 gradient staging of the
+	// reduce-scatter [n_pad] and the parameter count padded to a multiple of 8 world (w16 and the records
+	// are allocated with SHARD_PAD spare parameters for it)
+	static constexpr uint64_t SHARD_PAD = 2048;
+	uint32_t dp_rank = 0;
+	bool dp_rank_known = false;
+	bool shard_opt = true;       // trainer option "shard_opt"
+	bool shards_valid = true;    // false: a sharded step left other ranks' records stale here (gather_shards)
+	float* g32 = nullptr;
+	uint64_t n_pad = 0;
 	~ngp_trainer() {
 		if (arena) (void)hipFree(arena);
 		if (bias_tab) (void)hipFree(bias_tab);
+		if (g32) (void)hipFree(g32);
+	}
+	ngp::Exchange exchange() const {
+		ngp::Exchange e;
+		e.fn = allreduce; e.user = allreduce_user; e.rank = dp_rank; e.world = world; e.world_factor = (float)world;
+		e.rank_known = dp_rank_known;
+		return e;
+	}
+	// the sharded optimizer applies to this exchange: the lazy layout owning the model's buffers, rank known
+	bool sharded(const ngp::Exchange& e) const {
+		return e.fn && e.rank_known && shard_opt && rec && g32 && e.world == world && model->params == w16 &&
+		       model->gradients == g16;
+	}
+	void require_full_state(const char* what) const {
+		if (!shards_valid)
+			throw Error(std::string(what) + ": the optimizer state is sharded over the data-parallel ranks; call "
+			            "ngp_trainer_gather_shards on every rank first");
+	}
+	// Sharded exchange + update: fp16 gradients widened to fp32, reduce-scattered; this rank's slice of the
+	// records updated from the sums (rounded to fp16 once, as the all-reduce path narrows); fp16 weights
+	// all-gathered; the MLP's weight fragments rebuilt where another rank updated the MLP section.
+	int shard_step(hipStream_t s, float loss_scale, const ngp::Exchange& e, const uint32_t* step_base, uint32_t step_add,
+	               bool stored32) {
+		ngp_model* m = model;
+		const uint64_t c = n_pad / e.world;
+		if (!stored32) widen_f16(g16, g32, n, s);  // the backward did not write the fp32 input itself
+		if (e.fn(e.user, g32, n_pad, NGP_DTYPE_F32, NGP_REDUCE_SCATTER_SUM, s) != NGP_OK) return NGP_ERROR;
+		const uint64_t lo = std::min<uint64_t>((uint64_t)e.rank * c, n), hi = std::min<uint64_t>(lo + c, n);
+		const bool mlp_here = lo == 0 && hi >= m->n_matrix();
+		AdamState st{w32, w16, g16, nullptr, nullptr, nullptr, nullptr, inf16,
+		             mlp_here && m->frags_current ? (f16*)m->frags.p : nullptr, m->d_fragmap, step_base, step_add,
+		             step_base ? (const AdamConfig*)(ctl + CTL_CFG) : nullptr, rec, bias_tab, g32};
+		{
+			ProfScope ps("optimizer", s);
+			adam_lazy_range(cfg, (uint32_t)lo, (uint32_t)hi, (uint32_t)m->n_matrix(), loss_scale, st, s);
+		}
+		if (e.fn(e.user, w16, n_pad, NGP_DTYPE_F16, NGP_ALL_GATHER, s) != NGP_OK) return NGP_ERROR;
+		if (!mlp_here && m->n_matrix() > 0) m->prep(s, false);  // fragments of the gathered MLP weights
+		inf_stale = w32_stale = true;
+		if (e.world > 1) shards_valid = false;
+		return NGP_OK;
 	}
 	void sync_device_step() { NGP_HIP(hipMemcpy(ctl, &step, sizeof(uint32_t), hipMemcpyHostToDevice)); }
 	// One optimizer step on stream s. step_base/step_add: see AdamState (optimizer.h).
@@ -1078,7 +1143,8 @@ int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, 
 		const uint64_t n = m->n_params;
 		t->n = n;
 		auto al = [](size_t b) { return (b + 255) / 256 * 256; };
-		const size_t b32 = al(n * 4), b16 = al(n * 2);
+		// w16 and the records carry SHARD_PAD spare parameters: the sharded optimizer pads to a multiple of 8 world
+		const size_t b32 = al(n * 4), b16 = al((n + ngp_trainer::SHARD_PAD) * 2);
 		// lazy-EMA records from 2^20 parameters (C5: 105 M parameters, ~28 % updated per step; C2' 13 M: captured
 		// step 351 -> 330 us with the fused update, profiles/r03bw; C2, 3.3 M parameters, ~96 % updated: pass
 		// 140.6-142.8 -> 136.0 us since the MLP's update runs in the backward, NeRF steps unchanged with the
@@ -1087,7 +1153,7 @@ int ngp_trainer_create(ngp_model* m, const char* optimizer_json, uint64_t seed, 
 		bool lazy = n >= (1ull << 20);
 		if (const char* e = getenv("NGP_LAZY_EMA")) lazy = atoi(e) != 0;
 		lazy = lazy && n % 4 == 0;
-		const size_t brec = al(n / 2 * sizeof(AdamRec));
+		const size_t brec = al((n + ngp_trainer::SHARD_PAD) / 2 * sizeof(AdamRec));
 		const size_t total = b32 + (lazy ? brec : 4 * b32) + 3 * b16 + 256 /*ctl*/;
 		NGP_HIP(hipMalloc(&t->arena, total));
 		char* p = (char*)t->arena;
@@ -1181,21 +1247,21 @@ int ngp_trainer_capture_training_step(ngp_trainer* t, void* stream, uint32_t n, 
                                       int with_optimizer, ngp_graph** out) {
 	NGP_ARG(t);
 	return ngp::capture_training_step_with(t, stream, n, input, input_stride, dL_doutput, dL_stride, loss_scale, n_steps,
-	                                       with_optimizer, t->allreduce, t->allreduce_user, t->world, out);
+	                                       with_optimizer, t->exchange(), out);
 }
 }  // extern "C"
 
 // One training step as the captured graph runs it: forward_backward (the grid's lazy update fused into the
-// backward when `fuse`), [gradient exchange], optimizer. step_base = the trainer's ctl block (captured: the
-// step is the device base + k, hyperparameters read from the ctl block) or nullptr (eager: host step + k).
+// backward when `fuse`), [gradient exchange: one all-reduce, or the sharded reduce-scatter / slice update /
+// all-gather], optimizer. step_base = the trainer's ctl block (captured: the step is the device base + k,
+// hyperparameters read from the ctl block) or nullptr (eager: host step + k).
 static int train_step_body(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
                            const void* dL_doutput, uint32_t dL_stride, float loss_scale, int with_optimizer,
-                           ngp_allreduce_fn allreduce, void* allreduce_user, uint32_t world, bool fuse,
-                           const uint32_t* step_base, uint32_t k) {
+                           const Exchange& ex, bool fuse, const uint32_t* step_base, uint32_t k) {
 	ngp_model* m = t->model;
 	FusedAdam fa;
 	if (fuse) {
-		fa = t->fused_update(loss_scale * (float)world, n);
+		fa = t->fused_update(loss_scale * ex.world_factor, n);
 		if (step_base) {
 			fa.step_base = step_base;
 			fa.step_add = k;
@@ -1204,17 +1270,27 @@ static int train_step_body(ngp_trainer* t, void* stream, uint32_t n, const float
 			fa.step_add = t->step + k;
 		}
 	}
+	const bool shard = with_optimizer && t->sharded(ex);
+	// sharded: the backward writes the fp32 reduce-scatter input itself where it can (no widening pass)
+	const bool direct32 = shard && m->grad32_ok(n);
+	if (direct32) fa.g32 = t->g32;
 	int rc = forward_backward_with(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE,
-	                               fuse ? &fa : nullptr);
-	if (rc == NGP_OK && allreduce) {
-		rc = allreduce(allreduce_user, t->g16, t->n, NGP_DTYPE_F16, NGP_REDUCE_SUM, stream);
-		if (rc != NGP_OK && g_last_error.empty()) g_last_error = "gradient all-reduce failed";
-	}
-	if (rc == NGP_OK && with_optimizer) {
+	                               fuse || direct32 ? &fa : nullptr);
+	if (rc == NGP_OK && ex.fn) {
 		try {
-			// the summed gradient of `world` ranks: mean via the loss scale
+			// the summed gradient of the ranks: the mean (or, NeRF, the 1-GPU gradient) via the loss scale
+			rc = shard ? t->shard_step(S(stream), loss_scale * ex.world_factor, ex, step_base, step_base ? k : t->step + k, direct32)
+			           : ex.fn(ex.user, t->g16, t->n, NGP_DTYPE_F16, NGP_REDUCE_SUM, stream);
+		} catch (const std::exception& e) {
+			g_last_error = e.what();
+			rc = NGP_ERROR;
+		}
+		if (rc != NGP_OK && g_last_error.empty()) g_last_error = "gradient exchange failed";
+	}
+	if (rc == NGP_OK && with_optimizer && !shard) {
+		try {
 			if (fa.mlp_n) t->mlp_step_done();
-			else t->run_step(S(stream), loss_scale * (float)world, step_base, step_base ? k : t->step + k,
+			else t->run_step(S(stream), loss_scale * ex.world_factor, step_base, step_base ? k : t->step + k,
 			                 fuse ? m->n_matrix() : 0);
 		} catch (const std::exception& e) {
 			g_last_error = e.what();
@@ -1224,20 +1300,25 @@ static int train_step_body(ngp_trainer* t, void* stream, uint32_t n, const float
 	return rc;
 }
 
-extern "C" {
-int ngp_trainer_train_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
-                           const void* dL_doutput, uint32_t dL_stride, float loss_scale) {
+int ngp::train_step_with(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                         const void* dL_doutput, uint32_t dL_stride, float loss_scale, const Exchange& ex) {
 	NGP_ARG(t && n > 0 && input && dL_doutput && loss_scale > 0.f);
 	NGP_TRY({
 		ngp_model* m = t->model;
 		m->require_params(false);
 		NGP_CHECK(m->gradients == t->g16, "train_step: the model's gradient buffer must be this trainer's");
-		const bool fuse = !t->allreduce && t->fused_update_ok(n);
-		if (train_step_body(t, stream, n, input, input_stride, dL_doutput, dL_stride, loss_scale, 1, t->allreduce,
-		                    t->allreduce_user, t->world, fuse, nullptr, 0) != NGP_OK)
+		const bool fuse = !ex.fn && t->fused_update_ok(n);
+		if (train_step_body(t, stream, n, input, input_stride, dL_doutput, dL_stride, loss_scale, 1, ex, fuse, nullptr, 0) != NGP_OK)
 			throw Error(g_last_error);
 		t->step++;
 	});
+}
+
+extern "C" {
+int ngp_trainer_train_step(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
+                           const void* dL_doutput, uint32_t dL_stride, float loss_scale) {
+	NGP_ARG(t);
+	return ngp::train_step_with(t, stream, n, input, input_stride, dL_doutput, dL_stride, loss_scale, t->exchange());
 }
 
 int ngp_trainer_fused_update_active(const ngp_trainer* t, uint32_t n_batch) {
@@ -1251,9 +1332,8 @@ int ngp_trainer_fused_update_active(const ngp_trainer* t, uint32_t n_batch) {
 // 1-GPU gradient).
 int ngp::capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
                                     const void* dL_doutput, uint32_t dL_stride, float loss_scale, uint32_t n_steps,
-                                    int with_optimizer, ngp_allreduce_fn allreduce, void* allreduce_user, uint32_t world,
-                                    ngp_graph** out) {
-	NGP_ARG(t && out && stream && n > 0 && input && dL_doutput && loss_scale > 0.f && n_steps >= 1 && world >= 1);
+                                    int with_optimizer, const Exchange& ex, ngp_graph** out) {
+	NGP_ARG(t && out && stream && n > 0 && input && dL_doutput && loss_scale > 0.f && n_steps >= 1 && ex.world >= 1);
 	NGP_TRY({
 		ngp_model* m = t->model;
 		m->require_params(false);
@@ -1264,12 +1344,12 @@ int ngp::capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, co
 		g->trainer = t;
 		g->steps_per_launch = with_optimizer ? n_steps : 0;
 		// the grid's update inside the backward where possible (lazy layout, no exchange): as training_step
-		const bool fuse = with_optimizer && !allreduce && t->fused_update_ok(n);
+		const bool fuse = with_optimizer && !ex.fn && t->fused_update_ok(n);
 		NGP_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
 		int rc = NGP_OK;
 		for (uint32_t k = 0; k < n_steps && rc == NGP_OK; ++k)
-			rc = train_step_body(t, stream, n, input, input_stride, dL_doutput, dL_stride, loss_scale, with_optimizer, allreduce,
-			                     allreduce_user, world, fuse, t->ctl, k);  // step = device base (set per launch) + k
+			rc = train_step_body(t, stream, n, input, input_stride, dL_doutput, dL_stride, loss_scale, with_optimizer, ex, fuse,
+			                     t->ctl, k);  // step = device base (set per launch) + k
 		hipGraph_t graph = nullptr;
 		const hipError_t end = hipStreamEndCapture(s, &graph);
 		g->ws_epoch = m->ws_epoch;
@@ -1285,12 +1365,58 @@ int ngp::capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, co
 }
 extern "C" {
 
+// The sharded optimizer's buffers for `world` ranks: the fp32 gradient staging of the reduce-scatter, sized
+// outside any capture (the records and w16 carry SHARD_PAD spare parameters for the padding)
+static void trainer_prepare_shards(ngp_trainer* t, uint32_t world) {
+	if (!t->rec) return;
+	const uint64_t q = 8ull * world, n_pad = (t->n + q - 1) / q * q;
+	NGP_CHECK(n_pad - t->n <= ngp_trainer::SHARD_PAD, "sharded optimizer: too many ranks for the parameter padding");
+	if (t->g32 && t->n_pad == n_pad) return;
+	if (t->g32) NGP_HIP(hipFree(t->g32));
+	t->g32 = nullptr;
+	NGP_HIP(hipMalloc(&t->g32, n_pad * sizeof(float)));
+	NGP_HIP(hipMemset(t->g32, 0, n_pad * sizeof(float)));  // the padding stays 0: it sums to 0 in the reduce-scatter
+	t->n_pad = n_pad;
+}
+
+int ngp_trainer_set_data_parallel(ngp_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn fn, void* user) {
+	NGP_ARG(t && world >= 1 && rank < world && (fn || world == 1));
+	NGP_TRY({
+		NGP_CHECK(t->shards_valid, "set_data_parallel: gather the sharded optimizer state first (ngp_trainer_gather_shards)");
+		t->allreduce = fn;
+		t->allreduce_user = user;
+		t->world = fn ? world : 1;
+		t->dp_rank = fn ? rank : 0;
+		t->dp_rank_known = fn != nullptr;
+		if (fn) trainer_prepare_shards(t, world);
+		// the engine's communicator widens fp16 all-reduces to fp32 (the unsharded path): staging sized now
+		if (fn == ngp_dp_comm_allreduce && user)
+			NGP_CHECK(ngp_dp_comm_reserve((ngp_dp_comm*)user, t->n) == NGP_OK, "ngp_dp_comm_reserve failed");
+	});
+}
+
+int ngp_trainer_gather_shards(ngp_trainer* t, void* stream) {
+	NGP_ARG(t);
+	NGP_TRY({
+		if (t->shards_valid) return NGP_OK;
+		NGP_CHECK(t->allreduce && t->rec && t->n_pad, "gather_shards: no sharded exchange attached");
+		// records of n_pad / 2 pairs, 12 floats each: rank r's slice holds the pairs of its parameter slice
+		if (t->allreduce(t->allreduce_user, t->rec, t->n_pad / 2 * 12, NGP_DTYPE_F32, NGP_ALL_GATHER, stream) != NGP_OK)
+			throw Error(g_last_error.empty() ? "gather_shards: all-gather failed" : g_last_error);
+		NGP_HIP(hipStreamSynchronize(S(stream)));
+		t->shards_valid = true;
+	});
+}
+
 int ngp_trainer_set_allreduce(ngp_trainer* t, uint32_t world, ngp_allreduce_fn allreduce, void* user) {
 	NGP_ARG(t && world >= 1);
 	NGP_TRY({
+		NGP_CHECK(t->shards_valid, "set_allreduce: gather the sharded optimizer state first (ngp_trainer_gather_shards)");
 		t->allreduce = allreduce;
 		t->allreduce_user = user;
 		t->world = allreduce ? world : 1;
+		t->dp_rank = 0;
+		t->dp_rank_known = false;
 		// the engine's communicator widens the fp16 sum to fp32: size its staging now, outside any capture
 		if (allreduce == ngp_dp_comm_allreduce && user)
 			NGP_CHECK(ngp_dp_comm_reserve((ngp_dp_comm*)user, t->n) == NGP_OK, "ngp_dp_comm_reserve failed");
@@ -1358,6 +1484,9 @@ int ngp_trainer_set_option(ngp_trainer* t, const char* key, double value) {
 		const std::string k = key;
 		if (k == "ema_closed_form") {
 			t->cfg.ema_closed_form = value != 0 ? 1u : 0u;
+		} else if (k == "shard_opt") {
+			NGP_CHECK(t->shards_valid, "shard_opt: gather the sharded optimizer state first (ngp_trainer_gather_shards)");
+			t->shard_opt = value != 0;
 		} else {
 			throw Error("ngp_trainer_set_option: unknown option " + k);
 		}
@@ -1372,6 +1501,7 @@ __global__ static void k_f32_to_f16(const float* a, f16* b, f16* c, uint64_t n) 
 int ngp_trainer_set_params_full_precision(ngp_trainer* t, const float* params_host, uint64_t n) {
 	NGP_ARG(t && params_host && n == t->n);
 	NGP_TRY({
+		t->require_full_state("set_params_full_precision");
 		if (t->rec && t->step > 0) {
 			// lazy EMA: entries skipped since their last update still owe EMA steps on the OLD weight (the eager
 			// layout applied them every step). Replay them before the weights change; the records are then
@@ -1396,6 +1526,7 @@ int ngp_trainer_serialize(ngp_trainer* t, void* buf, uint64_t* size) {
 	NGP_TRY({
 		const uint64_t need = 32 + t->n * 4 * 5;
 		if (!buf) { *size = need; return NGP_OK; }
+		t->require_full_state("serialize");
 		NGP_CHECK(*size >= need, "serialize: buffer too small");
 		char* p = (char*)buf;
 		const uint64_t hdr[4] = {0x4e47504d49333535ULL /* "NGPMI355" */, 1, t->n, t->step};
@@ -1448,6 +1579,7 @@ int ngp_trainer_deserialize(ngp_trainer* t, const void* buf, uint64_t size) {
 			adam_rec_weights((uint32_t)t->n, t->rec, t->w32, true, nullptr);
 		}
 		t->inf_stale = t->w32_stale = false;  // inference parameters = the restored weights (below), as in the eager layout
+		t->shards_valid = true;              // every record restored on every rank
 		k_f32_to_f16<<<div_round_up(t->n, 256), 256>>>(t->w32, t->w16, t->inf16, t->n);
 		NGP_HIP(hipGetLastError());
 		NGP_HIP(hipDeviceSynchronize());

@@ -6,6 +6,9 @@
 
 namespace ngp {
 
+// gradient store modes of the bucketed backward's last kernels (template parameter MODE)
+enum : uint32_t { SC_STORE_F16 = 0, SC_FUSED_ADAM = 1, SC_STORE_F32 = 2 };
+
 // Brick-summed dense levels (3D grids): dense levels LB..LD-1 are not sent through items. Samples are
 // counting-sorted by brick (K^3 cells of the finest of those levels, f = LD - 1; one item per sample: its
 // index), each brick part sums its samples' contributions to levels 0..LD-1 in LDS over the brick's region

@@ -812,14 +812,28 @@ __device__ __forceinline__ void pair_slots(uint32_t k, uint32_t NE, uint32_t& a,
 	}
 }
 
+// The gradient store of parameter pair k (of the grid) in the non-fused modes: fp16 into `grad`, or (G32) the
+// same fp16-rounded values widened into g32.
+template <bool G32>
+__device__ __forceinline__ void store_pair(f16* grad, float* g32, size_t k, float s0, float s1) {
+	if constexpr (G32) {
+		typedef float f32x2 __attribute__((ext_vector_type(2)));
+		((f32x2*)g32)[k] = f32x2{(float)(f16)s0, (float)(f16)s1};
+	} else {
+		((f16x2*)grad)[k] = f16x2{(f16)s0, (f16)s1};
+	}
+}
+
 // One workgroup per work unit, heaviest first: blocks [0, max_parts) are the parts of oversized
 // buckets (coarse levels, where thousands of samples share a handful of entries; exact int64 partial
 // sums to their scratch slot, added by k_sc_split_reduce), blocks max_parts + vb the other buckets:
 // exact sum, written once per entry with plain stores (overwrite: every entry, untouched ones get 0
 // — no separate memset; accumulate: old + sum).
-// FUSED: the grid's optimizer update (FusedAdam) replaces the gradient store; a template parameter so
-// that the plain instantiation keeps its register allocation (the runtime branch cost C2' 25 %).
-template <uint32_t F, bool FUSED>
+// MODE (a template parameter, so that the plain instantiation keeps its register allocation: a runtime
+// branch for the fused update cost C2' 25 %): SC_STORE_F16 the fp16 gradient store; SC_FUSED_ADAM the grid's
+// optimizer update (FusedAdam) instead of the store; SC_STORE_F32 the fp16-rounded gradient widened to fp32
+// into fa.g32 (the sharded optimizer's reduce-scatter input: no separate widening pass).
+template <uint32_t F, uint32_t MODE>
 __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, const Levels lv, const BrickConst bk, const GridBwdArgs a,
                                                          const uint32_t* __restrict__ tot,
                                                          const uint32_t* __restrict__ lo_arr, uint32_t B, uint32_t split_limit,
@@ -827,6 +841,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
                                                          const f16* __restrict__ item_val, f16* __restrict__ grad, bool overwrite,
                                                          const uint32_t* __restrict__ split, unsigned long long* __restrict__ scratch,
                                                          uint32_t debug, const FusedAdam fa, const BrickFallback fb) {
+	constexpr bool FUSED = MODE == SC_FUSED_ADAM, G32 = MODE == SC_STORE_F32;
 	extern __shared__ unsigned long long acc[];
 	const uint32_t NE = 1u << B, NEP = NE + 1;  // feature planes padded by one entry (accumulate_items)
 	if (blockIdx.x < max_parts) {
@@ -855,7 +870,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 	f16* g = grad + (size_t)e0 * F;
 	if (t == 0) {  // no contribution: gradient 0 (fused update: every entry of the bucket is skipped)
 		if (overwrite && !FUSED)
-			for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) ((uint32_t*)g)[k] = 0u;
+			for (uint32_t k = threadIdx.x; k < n_e * F / 2; k += blockDim.x) store_pair<G32>(grad, fa.g32, (size_t)e0 * F / 2 + k, 0.f, 0.f);
 		return;
 	}
 	const uint32_t lo = lo_arr[vb];
@@ -912,12 +927,12 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 		uint32_t ia, ib;
 		pair_slots<F>(k, NEP, ia, ib);
 		float s0 = fix_to_f32(acc[ia]), s1 = fix_to_f32(acc[ib]);
-		if (!overwrite) {
+		if (!G32 && !overwrite) {
 			const f16x2 o = ((const f16x2*)g)[k];
 			s0 += (float)o[0];
 			s1 += (float)o[1];
 		}
-		((f16x2*)g)[k] = f16x2{(f16)s0, (f16)s1};
+		store_pair<G32>(grad, fa.g32, (size_t)e0 * F / 2 + k, s0, s1);
 	}
 }
 
@@ -928,7 +943,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 // Columns [fin_x0, gridDim.x) finalize the brick levels: one entry per thread (two for F = 1), every feature
 // summed over the bricks' slabs in one pass over the geometry (brick_entry_sums), written as parameter pairs
 // (pair k = features 2k, 2k + 1 of the grid's leading entries).
-template <uint32_t F, bool FUSED>
+template <uint32_t F, uint32_t MODE>
 __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst c, const Levels lv, uint32_t B,
                                                                 const uint32_t* __restrict__ split, const uint32_t* __restrict__ splitb,
                                                                 const unsigned long long* __restrict__ scratch, f16* __restrict__ grad,
@@ -936,6 +951,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
                                                                 const BrickConst bk, const uint32_t* __restrict__ bp, const BrickFallback fb,
                                                                 uint32_t fin_x0) {
 	static_assert(SC_THREADS == SLAB_THREADS, "slab blocks share the split-reduce block shape");
+	constexpr bool FUSED = MODE == SC_FUSED_ADAM, G32 = MODE == SC_STORE_F32;
 	if (blockIdx.x >= fin_x0) {
 		constexpr uint32_t EPT = F == 1 ? 2 : 1;  // entries per thread: whole parameter pairs
 		const uint32_t blk = blockIdx.y * (gridDim.x - fin_x0) + (blockIdx.x - fin_x0);
@@ -960,12 +976,12 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
 				fused_adam_pair(fa, k, (f16)s0, (f16)s1);
 				continue;
 			}
-			if (!overwrite) {
+			if (!G32 && !overwrite) {
 				const f16x2 o = ((const f16x2*)grad)[k];
 				s0 += (float)o[0];
 				s1 += (float)o[1];
 			}
-			((f16x2*)grad)[k] = f16x2{(f16)s0, (f16)s1};
+			store_pair<G32>(grad, fa.g32, k, s0, s1);
 		}
 		return;
 	}
@@ -1031,12 +1047,12 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
 			fused_adam_pair(fa, e0 * F / 2 + k, (f16)s0, (f16)s1);
 			return;
 		}
-		if (!overwrite) {
+		if (!G32 && !overwrite) {
 			const f16x2 o = ((const f16x2*)g)[k];
 			s0 += (float)o[0];
 			s1 += (float)o[1];
 		}
-		((f16x2*)g)[k] = f16x2{(f16)s0, (f16)s1};
+		store_pair<G32>(grad, fa.g32, (size_t)e0 * F / 2 + k, s0, s1);
 	}
 }
 
@@ -1103,10 +1119,12 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		else go(sc1024, accum, splitr);
 	};
 #define NGP_SC_F(FF)                                                                                                 \
-	if (fa.rec) by_chunk(k_sc_scatter<D, FF, 512, 512>, k_sc_scatter<D, FF, 1024, 1024>, k_sc_accumulate<FF, true>,   \
-	                     k_sc_split_reduce<FF, true>);                                                               \
-	else by_chunk(k_sc_scatter<D, FF, 512, 512>, k_sc_scatter<D, FF, 1024, 1024>, k_sc_accumulate<FF, false>,         \
-	              k_sc_split_reduce<FF, false>)
+	if (fa.rec) by_chunk(k_sc_scatter<D, FF, 512, 512>, k_sc_scatter<D, FF, 1024, 1024>, k_sc_accumulate<FF, SC_FUSED_ADAM>, \
+	                     k_sc_split_reduce<FF, SC_FUSED_ADAM>);                                                      \
+	else if (fa.g32) by_chunk(k_sc_scatter<D, FF, 512, 512>, k_sc_scatter<D, FF, 1024, 1024>,                       \
+	                          k_sc_accumulate<FF, SC_STORE_F32>, k_sc_split_reduce<FF, SC_STORE_F32>);              \
+	else by_chunk(k_sc_scatter<D, FF, 512, 512>, k_sc_scatter<D, FF, 1024, 1024>, k_sc_accumulate<FF, SC_STORE_F16>,  \
+	              k_sc_split_reduce<FF, SC_STORE_F16>)
 	switch (F) {
 		case 1: NGP_SC_F(1); break;
 		case 2: NGP_SC_F(2); break;

@@ -141,6 +141,14 @@ struct ngp_nerf_trainer {
 	bool dp_capturable = false;  // the hook is the engine's RCCL communicator: the DP training pass is a graph
 	Buf dp_scalars;
 	bool dp() const { return allreduce != nullptr; }
+	// the training pass's exchange: the shards' dL/doutput is already scaled by 128 / R_global, so the summed
+	// gradient is the 1-GPU gradient (world factor 1)
+	ngp::Exchange exchange() const {
+		ngp::Exchange e;
+		e.fn = allreduce; e.user = allreduce_user; e.rank = rank; e.world = world; e.world_factor = 1.f;
+		e.rank_known = allreduce != nullptr;
+		return e;
+	}
 	// occupancy grid
 	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens;
 	// training workspaces
@@ -507,6 +515,10 @@ int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint3
 	// an RCCL hook is stream-ordered and graph-capturable; a host callback (gloo) is not
 	t->dp_capturable = allreduce == ngp_dp_comm_allreduce;
 	if (t->dp_capturable && user && ngp_dp_comm_reserve((ngp_dp_comm*)user, ngp_model_n_params(t->model)) != NGP_OK) return NGP_ERROR;
+	// the trainer's exchange with this rank: large tables shard the optimizer (reduce-scatter, slice update,
+	// all-gather of the weights; trainer option shard_opt)
+	const int rc = ngp_trainer_set_data_parallel(t->trainer, allreduce ? rank : 0, allreduce ? world : 1, allreduce, user);
+	if (rc != NGP_OK) return rc;
 	if (t->train_graph) ngp_graph_destroy(t->train_graph);  // re-captured with (or without) the exchange
 	t->train_graph = nullptr;
 	return NGP_OK;
@@ -862,10 +874,10 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			    t->graph_epoch != ngp_model_workspace_epoch(t->model)) {
 				if (t->train_graph) ngp_graph_destroy(t->train_graph);
 				t->train_graph = nullptr;
-				// data parallel: the shards' dL/doutput is scaled by 128 / R_global, so the summed gradient is
-				// the 1-GPU gradient: world factor 1 in the optimizer
-				check_rc(capture_training_step_with(t->trainer, s, Bl, coords_c, 7, dloss, 16, 128.0f, 1, 1,
-				                                    dp ? t->allreduce : nullptr, t->allreduce_user, 1, &t->train_graph));
+				// data parallel: the shards' dL/doutput is scaled by 128 / R_global, so the summed gradient is the
+				// 1-GPU gradient: world factor 1 in the optimizer
+				check_rc(capture_training_step_with(t->trainer, s, Bl, coords_c, 7, dloss, 16, 128.0f, 1, 1, t->exchange(),
+				                                    &t->train_graph));
 				t->graph_in = coords_c;
 				t->graph_dl = dloss;
 				t->graph_n = Bl;
@@ -873,12 +885,8 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			}
 			check_rc(ngp_graph_launch(t->train_graph, s));
 		} else {
-			// host-callback exchange (gloo): not capturable
-			check_rc(ngp_forward_backward(t->model, s, Bl, coords_c, 7, nullptr, 0, dloss, 16, NGP_GRAD_OVERWRITE));
-			NGP_CHECK(t->allreduce(t->allreduce_user, ngp_trainer_gradients(t->trainer), ngp_model_n_params(t->model), NGP_DTYPE_F16,
-			                       NGP_REDUCE_SUM, s) == 0,
-			          "data parallel: gradient all-reduce failed");
-			check_rc(ngp_trainer_optimizer_step(t->trainer, s, 128.0f));
+			// host-callback exchange (gloo): not capturable; the same step body, launched eagerly
+			check_rc(train_step_with(t->trainer, s, Bl, coords_c, 7, dloss, 16, 128.0f, t->exchange()));
 		}
 		t->rng.advance();  // m_rng.advance() (testbed_nerf.cu:4127)
 		}

@@ -47,6 +47,9 @@ struct AdamState {
 	const AdamConfig* cfg_dev;  // non-null (captured steps): hyperparameters read from device memory
 	AdamRec* rec = nullptr;     // non-null: lazy-EMA layout (m1/m2/steps/ema32 unused)
 	const float* bias_tab = nullptr;  // adam_bias_table (nullable)
+	// lazy layout, sharded data parallelism: the gradient is the ranks' fp32 sum of their fp16 gradients
+	// (reduce-scatter); it is rounded to fp16 once here, as the all-reduce path narrows it (dp_comm.hip)
+	const float* g32 = nullptr;
 };
 // ---- device helpers shared by optimizer.hip and the fused update in the grid backward ----------
 // Adam's bias correction depends on the parameter's own step s only: the factors sqrtf(1 - beta2^s) and
@@ -188,6 +191,10 @@ struct FusedAdam {
 	// gradients, so they run k_adam_lazy4's lazy_update on them (whole-model pointers; option fuse_mlp_opt)
 	uint32_t mlp_n = 0;
 	f16* mlp_w16 = nullptr;
+	// no update (rec null), the gradient stored widened: the fp16-rounded sums as fp32 at g32 (grid-relative in
+	// the grid backward, the whole model's buffer at the engine boundary) — the sharded optimizer's
+	// reduce-scatter input written by the backward itself
+	float* g32 = nullptr;
 	AdamRec* mlp_rec = nullptr;
 	f16* frags = nullptr;
 	const uint32_t* fragmap = nullptr;
@@ -250,6 +257,10 @@ __device__ __forceinline__ void fused_adam_pair(const FusedAdam& fa, uint32_t r,
 // set_learning_rate / set_option like eager ones.
 constexpr uint32_t CTL_CFG = 16;
 void adam_ema_update(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float loss_scale, const AdamState& st, hipStream_t s);
+// Lazy layout: the update of parameters [lo, hi) only (multiples of 4): one rank's slice under the sharded
+// optimizer (st.g32 = the reduce-scattered fp32 gradient sums, indexed like the parameters)
+void adam_lazy_range(const AdamConfig& c, uint32_t lo, uint32_t hi, uint32_t n_matrix, float loss_scale, const AdamState& st,
+                     hipStream_t s);
 void set_device_ctl(uint32_t* ctl, uint32_t step, const AdamConfig& c, hipStream_t s);
 // Lazy layout: bring every parameter's EMA up to `steps_done` optimizer steps and write ema16 (the
 // inference parameters) debiased as the eager update would have after step steps_done - 1.

@@ -141,7 +141,13 @@ __global__ void __launch_bounds__(256) k_adam_ema4(const uint32_t n4, const uint
 
 __device__ __forceinline__ void lazy_load(const AdamState& st, uint32_t i0, uint32_t n_matrix, float loss_scale, LazyGroup& G) {
 	G.i0 = i0;
-	const f16x4 gh = *(const f16x4*)(st.g16 + i0);
+	f16x4 gh;
+	if (st.g32) {  // the ranks' fp32 sum, rounded to fp16 once (= the all-reduce path's narrowing)
+		const f32x4 g = *(const f32x4*)(st.g32 + i0);
+		gh = f16x4{(f16)g[0], (f16)g[1], (f16)g[2], (f16)g[3]};
+	} else {
+		gh = *(const f16x4*)(st.g16 + i0);
+	}
 #pragma unroll
 	for (int k = 0; k < 4; ++k) {
 		G.g[k] = (float)gh[k] / loss_scale;
@@ -157,7 +163,8 @@ __device__ __forceinline__ void lazy_load(const AdamState& st, uint32_t i0, uint
 	}
 }
 
-__global__ void __launch_bounds__(256) k_adam_lazy4(const uint32_t n4, const uint32_t n_matrix, const float loss_scale,
+// groups [g0, g0 + n4) of 4 parameters
+__global__ void __launch_bounds__(256) k_adam_lazy4(const uint32_t g0, const uint32_t n4, const uint32_t n_matrix, const float loss_scale,
                                                     const AdamConfig c_arg, const AdamState st) {
 	const uint32_t half = (n4 + 1) / 2;
 	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -166,8 +173,8 @@ __global__ void __launch_bounds__(256) k_adam_lazy4(const uint32_t n4, const uin
 	const uint32_t step = (st.step_base ? *st.step_base : 0u) + st.step_add;
 	const bool two = t + half < n4;
 	LazyGroup A, B;
-	lazy_load(st, 4 * t, n_matrix, loss_scale, A);
-	if (two) lazy_load(st, 4 * (t + half), n_matrix, loss_scale, B);
+	lazy_load(st, 4 * (g0 + t), n_matrix, loss_scale, A);
+	if (two) lazy_load(st, 4 * (g0 + t + half), n_matrix, loss_scale, B);
 	lazy_update(st, c, step, n_matrix, A);
 	if (two) lazy_update(st, c, step, n_matrix, B);
 }
@@ -251,7 +258,7 @@ void adam_ema_update(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float l
 	if (st.rec) {
 		NGP_CHECK(n % 4 == 0 && ((uintptr_t)st.w32 | (uintptr_t)st.w16 | (uintptr_t)st.g16 | (uintptr_t)st.rec) % 16 == 0,
 		          "lazy-EMA optimizer: parameters must be 16-B aligned groups of 4");
-		k_adam_lazy4<<<div_round_up((n / 4 + 1) / 2, 256), 256, 0, s>>>(n / 4, n_matrix, loss_scale, c, st);
+		k_adam_lazy4<<<div_round_up((n / 4 + 1) / 2, 256), 256, 0, s>>>(0, n / 4, n_matrix, loss_scale, c, st);
 		NGP_HIP(hipGetLastError());
 		return;
 	}
@@ -262,6 +269,16 @@ void adam_ema_update(const AdamConfig& c, uint32_t n, uint32_t n_matrix, float l
 	const uint32_t n4 = aligned ? n / 4 : 0;
 	if (n4) k_adam_ema4<<<div_round_up(n4, 256), 256, 0, s>>>(n4, n_matrix, loss_scale, c, a);
 	if (4 * n4 < n) k_adam_ema<<<div_round_up(n - 4 * n4, 256), 256, 0, s>>>(4 * n4, n, n_matrix, loss_scale, c, a);
+	NGP_HIP(hipGetLastError());
+}
+
+void adam_lazy_range(const AdamConfig& c, uint32_t lo, uint32_t hi, uint32_t n_matrix, float loss_scale, const AdamState& st,
+                     hipStream_t s) {
+	NGP_CHECK(st.rec && lo % 4 == 0 && hi % 4 == 0 && lo <= hi, "lazy range update: record layout, groups of 4");
+	NGP_CHECK(((uintptr_t)st.w16 | (uintptr_t)st.rec | (uintptr_t)(st.g32 ? (const void*)st.g32 : (const void*)st.g16)) % 16 == 0,
+	          "lazy range update: 16-B aligned buffers");
+	const uint32_t n4 = (hi - lo) / 4;
+	if (n4) k_adam_lazy4<<<div_round_up((n4 + 1) / 2, 256), 256, 0, s>>>(lo / 4, n4, n_matrix, loss_scale, c, st);
 	NGP_HIP(hipGetLastError());
 }
 

@@ -11,6 +11,7 @@ struct SlabJob {
 	const float* slabs = nullptr;
 	uint32_t n_slabs = 0, n = 0;
 	f16* grad = nullptr;
+	float* grad32 = nullptr;  // set: the fp16-rounded sums widened into it instead (the sharded optimizer's input)
 	bool accumulate = false;
 	uint32_t stride = 0;  // elements between consecutive slabs (0: n); > n reduces a leading range only
 };
@@ -43,7 +44,8 @@ __device__ __forceinline__ void reduce_slabs_block(const SlabJob& j, uint32_t bl
 		float t = j.accumulate ? (float)j.grad[p] : 0.f;
 #pragma unroll
 		for (int k = 0; k < 8; ++k) t += part[k][threadIdx.x];
-		j.grad[p] = (f16)t;
+		if (j.grad32) j.grad32[p] = (float)(f16)t;
+		else j.grad[p] = (f16)t;
 		if (gsh) gsh[threadIdx.x] = (f16)t;
 	}
 }

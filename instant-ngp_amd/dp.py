@@ -58,6 +58,20 @@ def allreduce_counters(values, world):
     return t.cpu().tolist()
 
 
+class _stdout_to_stderr:
+    """Redirect file descriptor 1 to 2 (native libraries write there directly, below sys.stdout)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 class EngineComm:
     """The engine's own RCCL communicator (ngp_dp_comm_*): rank 0 makes the unique id, torch.distributed
     broadcasts it, every rank joins. `fn`/`user` plug into the engine's exchange hooks
@@ -66,14 +80,19 @@ class EngineComm:
 
     def __init__(self, rank, world, group=None, wire="f32"):
         from ._capi import check, lib
+        with _stdout_to_stderr():  # RCCL prints its version banner to stdout: keep bench.py's one JSON line clean
+            self._init(rank, world, group, wire, check, lib)
+
+    def _init(self, rank, world, group, wire, check, lib):
         idb = (C.c_uint8 * 128)()
         if rank == 0:
             check(lib().ngp_dp_comm_unique_id(idb))
-        t = torch.tensor(list(idb), dtype=torch.uint8)
-        if dist.get_backend(group) == "nccl":
-            t = t.cuda()
-        dist.broadcast(t, src=0, group=group)
-        idb = (C.c_uint8 * 128)(*t.cpu().tolist())
+        if world > 1 or dist.is_initialized():
+            t = torch.tensor(list(idb), dtype=torch.uint8)
+            if dist.get_backend(group) == "nccl":
+                t = t.cuda()
+            dist.broadcast(t, src=0, group=group)
+            idb = (C.c_uint8 * 128)(*t.cpu().tolist())  # else a world of one: no process group needed
         h = C.c_void_p()
         check(lib().ngp_dp_comm_create(rank, world, idb, C.byref(h)))
         self.handle, self.rank, self.world = h, rank, world
@@ -110,6 +129,38 @@ def _host_allreduce(t, op, group, stream):
     torch.cuda.synchronize()
 
 
+REDUCE_SCATTER_SUM, ALL_GATHER = 2, 3  # ngp_engine.h: the sharded optimizer's hook ops
+
+
+def _host_shard_collective(t, op, group, stream):
+    """NGP_REDUCE_SCATTER_SUM / NGP_ALL_GATHER on a device tensor, in place (rank r's slice is the r-th of world
+    equal slices). nccl: torch.distributed's collectives on `stream`; gloo: host round trip (the reduce-scatter as
+    a float32 all-reduce of the whole buffer, which leaves every slice summed; the all-gather bit-exact)."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    c = t.numel() // world
+    if dist.get_backend(group) == "nccl":
+        s = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()
+        with torch.cuda.stream(s):
+            if op == REDUCE_SCATTER_SUM:
+                out = torch.empty(c, dtype=t.dtype, device=t.device)
+                dist.reduce_scatter_tensor(out, t, group=group)
+                t[rank * c:(rank + 1) * c].copy_(out)
+            else:
+                dist.all_gather_into_tensor(t, t[rank * c:(rank + 1) * c].clone(), group=group)
+        return
+    (torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()).synchronize()
+    if op == REDUCE_SCATTER_SUM:
+        h = t.float().cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h.to(t.dtype))
+    else:
+        # gloo gathers float32 (not 16-bit types): fp16 slices travel widened, which is exact both ways
+        parts = [torch.empty(c, dtype=torch.float32) for _ in range(world)]
+        dist.all_gather(parts, t[rank * c:(rank + 1) * c].float().cpu().contiguous(), group=group)
+        t.copy_(torch.cat(parts).to(t.device, t.dtype))
+    torch.cuda.synchronize()
+
+
 def make_allreduce_callback(group=None, timer=None):
     """The engine's exchange hook (ngp_nerf_trainer_set_data_parallel) over torch.distributed.
 
@@ -122,6 +173,12 @@ def make_allreduce_callback(group=None, timer=None):
     def cb(user, ptr, count, dtype, op, stream):
         try:
             t = wrap_device(ptr, int(count), torch.float32 if dtype == 0 else torch.float16)
+            if op in (REDUCE_SCATTER_SUM, ALL_GATHER):  # the sharded optimizer's collectives (in place)
+                t0 = time.perf_counter()
+                _host_shard_collective(t, op, group, stream)
+                if timer is not None:
+                    timer.add(1e3 * (time.perf_counter() - t0))
+                return 0
             rop = dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX
             if dist.get_backend(group) == "nccl":
                 s = torch.cuda.ExternalStream(stream) if stream else torch.cuda.current_stream()

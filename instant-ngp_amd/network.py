@@ -10,7 +10,7 @@ import json
 
 import torch
 
-from ._capi import ParamLayout, check, lib
+from ._capi import NgpError, ParamLayout, check, lib
 
 LAYOUT_AOS, LAYOUT_SOA = 0, 1
 LAYOUT_AOS_RGBD = 2  # engine extension: NerfNetwork rows 0..3 only (raw rgb, raw density), [n x 4]
@@ -353,6 +353,21 @@ class Trainer:
         else:
             check(lib().ngp_trainer_set_allreduce(self.handle, comm.world, comm.fn, comm.handle))
         self._comm = comm
+
+    def set_data_parallel(self, comm):
+        """Engine extension: the exchange of set_allreduce with this rank (comm.rank), so that large-table trainers
+        shard the optimizer (reduce-scatter of the fp32-widened gradients, this rank's slice of the update,
+        all-gather of the fp16 weights; option shard_opt). None: off. With world > 1, call gather_shards() on every
+        rank before reading inference_params / params_full_precision or serializing."""
+        if comm is None:
+            check(lib().ngp_trainer_set_data_parallel(self.handle, 0, 1, None, None))
+        else:
+            check(lib().ngp_trainer_set_data_parallel(self.handle, comm.rank, comm.world, comm.fn, comm.handle))
+        self._comm = comm
+
+    def gather_shards(self, stream=None):
+        """Collective: every rank gets the whole (sharded) optimizer state again (ngp_trainer_gather_shards)."""
+        check(lib().ngp_trainer_gather_shards(self.handle, _stream(stream)))
 
     def train_step(self, x, dL_doutput, loss_scale=128.0, stream=None):
         """Engine extension: one eager step of what capture_training_step records (forward_backward with the

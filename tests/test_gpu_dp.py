@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 STEPS = 80
 
 
-def _run(rank, world, port, out_dir):
+def _run(rank, world, port, out_dir, shard=True):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank), "WORLD_SIZE": str(world)})
     import torch.distributed as dist
     from __graft_entry__ import load_package
@@ -31,18 +31,20 @@ def _run(rank, world, port, out_dir):
     net = pkg.create_nerf_network(ncfg)
     tr = pkg.Trainer(net, ncfg["optimizer"])
     run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
+    tag = f"w{world}" + ("" if shard else "_ar")
     if world > 1:
+        tr.set_option("shard_opt", int(shard))  # sharded optimizer (default) or one all-reduce per step
         run.set_data_parallel(rank, world)
     log = []
     for k in range(STEPS):
         s = run.train_step(get_loss=True)
         torch.cuda.synchronize()
-        if k == 0:  # the step's gradient (all-reduced across the ranks when sharded)
-            np.save(os.path.join(out_dir, f"grad0_w{world}_r{rank}.npy"), tr.gradients.float().cpu().numpy())
+        if k == 0:  # the step's gradient (all-reduced across the ranks on the all-reduce path)
+            np.save(os.path.join(out_dir, f"grad0_{tag}_r{rank}.npy"), tr.gradients.float().cpu().numpy())
         log.append({"loss": s["loss"], "rays": s["rays_per_batch"], "measured": s["measured_batch_size"],
                     "params": hashlib.sha1(tr.params.cpu().numpy().tobytes()).hexdigest(),
                     "grid": hashlib.sha1(run.density_grid.cpu().numpy().tobytes()).hexdigest()})
-    with open(os.path.join(out_dir, f"w{world}_r{rank}.json"), "w") as f:
+    with open(os.path.join(out_dir, f"{tag}_r{rank}.json"), "w") as f:
         json.dump(log, f)
     if world > 1:
         dist.destroy_process_group()
@@ -54,13 +56,17 @@ def test_nerf_data_parallel_two_ranks(tmp_path):
     import torch.multiprocessing as mp
     port = 29500 + os.getpid() % 1000
     mp.spawn(_run, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_run, args=(2, port + 2, str(tmp_path), False), nprocs=2, join=True)
     mp.spawn(_run, args=(1, port + 1, str(tmp_path)), nprocs=1, join=True)
     r0 = json.load(open(tmp_path / "w2_r0.json"))
     r1 = json.load(open(tmp_path / "w2_r1.json"))
+    ar0 = json.load(open(tmp_path / "w2_ar_r0.json"))
     single = json.load(open(tmp_path / "w1_r0.json"))
-    # every rank holds the same all-reduced gradient (the batches differ from the 1-GPU step's wherever
-    # compaction truncates or rolls over per shard, so the sum is compared on a fixed batch below)
-    assert np.array_equal(np.load(tmp_path / "grad0_w2_r0.npy"), np.load(tmp_path / "grad0_w2_r1.npy"))
+    # all-reduce path: every rank holds the same summed gradient (the batches differ from the 1-GPU step's
+    # wherever compaction truncates or rolls over per shard, so the sum is compared on a fixed batch below)
+    assert np.array_equal(np.load(tmp_path / "grad0_w2_ar_r0.npy"), np.load(tmp_path / "grad0_w2_ar_r1.npy"))
+    # the sharded optimizer trains bit for bit like the all-reduce path: same parameters, grid and counters
+    assert r0 == ar0
     for a, b in zip(r0, r1):
         assert a["params"] == b["params"] and a["grid"] == b["grid"]
         assert a["rays"] == b["rays"] and a["measured"] == b["measured"]

@@ -58,6 +58,7 @@ def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8, rank=0, wor
     t_train = time.time() - t_start
     if world > 1:
         t_train = pkg.dp.reduce_scalar(t_train, "max")
+        tr.gather_shards()  # collective: the sharded optimizer state (EMA records) whole on every rank
         if rank != 0:
             return {"value": samples / t_train, "steps": steps, "train_seconds": t_train}
     r = pkg.nerf.NerfRenderer()
