@@ -182,6 +182,7 @@ void* ngp_trainer_inference_params(ngp_trainer* t);        /* fp16 [n_params] (E
    weights with ngp_trainer_set_params_full_precision. For eager-layout trainers it is the live master copy. */
 float* ngp_trainer_params_full_precision(ngp_trainer* t);
 uint32_t ngp_trainer_step(const ngp_trainer* t);
+uint64_t ngp_trainer_n_params(const ngp_trainer* t);
 float ngp_trainer_learning_rate(const ngp_trainer* t);     /* optimizer->learning_rate() (testbed_nerf.cu:3771) */
 int ngp_trainer_set_learning_rate(ngp_trainer* t, float lr);
 /* Engine extension: trainer options. "ema_closed_form" 0 (default) / 1: how the large-table (lazy-EMA) layout
@@ -394,8 +395,12 @@ int ngp_nerf_renderer_create(ngp_nerf_renderer** out);
 void ngp_nerf_renderer_destroy(ngp_nerf_renderer* r);
 /* ERenderMode of the following renders (common.h:110-119): 1 Shade (default), 2 Normals (testbed_nerf.cu:
  * 1183-1188, 2179-2181, 2615-2617: the density output's input gradient per step, ngp_input_gradient with
- * backprop_scale 128, composited as normalize(-density'(raw) * gradient), shaded as (0.5 n + 0.5) * alpha) */
+ * backprop_scale 128, composited as normalize(-density'(raw) * gradient), shaded as (0.5 n + 0.5) * alpha),
+ * 0 AO (each step's alpha), 3 Positions ((pos - 0.5) / 2 + 0.5, show_accel off), 4 Depth (dot(camera forward,
+ * pos - ray origin) * depth_scale): :1189-1208, composited like Shade, no sRGB decoding in the shade step (:2183).
+ * depth_scale: 1 / the dataset's scale (render_nerf, testbed_nerf.cu:2822); default 1. */
 int ngp_nerf_renderer_set_mode(ngp_nerf_renderer* r, int render_mode);
+int ngp_nerf_renderer_set_depth_scale(ngp_nerf_renderer* r, float depth_scale);
 int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_config* cfg, void* stream, const ngp_nerf_image* camera,
                     const uint8_t* bitfield, uint32_t spp, uint32_t sample_index, float min_transmittance,
                     const float* background_rgba, int use_inference_params, float* out_rgba);
@@ -451,6 +456,18 @@ int ngp_nerf_trainer_error_map(ngp_nerf_trainer* t, int which, float* out, uint6
 int ngp_nerf_save_snapshot(ngp_nerf_trainer* t, void* stream, const char* path, const char* network_config_json,
                            int include_optimizer_state, int compress);
 int ngp_nerf_load_snapshot(ngp_nerf_trainer* t, void* stream, const char* path);
+/* Testbed::save_snapshot / load_snapshot for the image and SDF testbeds (testbed.cu:4873-5057): the trainer's
+ * Trainer::serialize members (as in the NeRF snapshot), version, mode (e.g. "sdf", "image"), training_step, loss,
+ * aabb {min, max} and bounding_radius. Loading restores the parameters (and the optimizer state if present; an
+ * optimizer member lacking some arrays fills them from the parameters / zeros) and returns the scalars (each output
+ * nullable; bounding_radius keeps its value when the snapshot has none). ngp_snapshot_mode: the snapshot's mode
+ * (a NeRF snapshot without one: "nerf"), for a Testbed to switch mode before reset_network. */
+int ngp_save_snapshot(ngp_trainer* t, void* stream, const char* path, const char* network_config_json, const char* mode,
+                      const float* aabb_min, const float* aabb_max, float bounding_radius, uint32_t training_step, float loss,
+                      int include_optimizer_state, int compress);
+int ngp_load_snapshot(ngp_trainer* t, void* stream, const char* path, uint32_t* training_step, float* loss, float* aabb_min,
+                      float* aabb_max, float* bounding_radius);
+int ngp_snapshot_mode(const char* path, char* mode_buf, uint64_t cap);
 /* Testbed::load_network_config (testbed.cu:246) of a snapshot: the config as JSON text without the
  * "snapshot" member (binaries as {"binary_bytes": n}); size query with json_buf = NULL. */
 int ngp_snapshot_network_config(const char* path, char* json_buf, uint64_t* size);

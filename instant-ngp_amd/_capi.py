@@ -182,6 +182,11 @@ SIGNATURES = {
     "ngp_dp_comm_reserve": (i32, [P, u64]),
     "ngp_trainer_set_allreduce": (i32, [P, u32, P, P]),
     "ngp_trainer_set_data_parallel": (i32, [P, u32, u32, P, P]),
+    "ngp_nerf_renderer_set_depth_scale": (i32, [P, f32]),
+    "ngp_trainer_n_params": (u64, [P]),
+    "ngp_save_snapshot": (i32, [P, P, C.c_char_p, C.c_char_p, C.c_char_p, P, P, f32, u32, f32, i32, i32]),
+    "ngp_load_snapshot": (i32, [P, P, C.c_char_p, P, P, P, P, P]),
+    "ngp_snapshot_mode": (i32, [C.c_char_p, C.c_char_p, u64]),
     "ngp_trainer_gather_shards": (i32, [P, P]),
     "ngp_nerf_renderer_create": (i32, [C.POINTER(P)]),
     "ngp_nerf_renderer_destroy": (None, [P]),

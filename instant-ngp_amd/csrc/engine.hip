@@ -1470,6 +1470,7 @@ float* ngp_trainer_params_full_precision(ngp_trainer* t) {
 	return t->w32;
 }
 uint32_t ngp_trainer_step(const ngp_trainer* t) { return t ? t->step : 0; }
+uint64_t ngp_trainer_n_params(const ngp_trainer* t) { return t ? t->n : 0; }
 float ngp_trainer_learning_rate(const ngp_trainer* t) { return t ? t->cfg.lr_at(t->step) : 0.f; }
 int ngp_trainer_set_learning_rate(ngp_trainer* t, float lr) {
 	NGP_ARG(t && lr >= 0.f);

@@ -129,9 +129,10 @@ struct RenderArgs {
 	uint32_t rgb_activation, density_activation;
 	float min_transmittance;
 	float background[4];           // linear rgba
-	uint32_t render_mode;          // ERenderMode (common.h:110-119): 1 Shade, 2 Normals
+	uint32_t render_mode;          // ERenderMode (common.h:110-119): 0 AO, 1 Shade, 2 Normals, 3 Positions, 4 Depth
+	float depth_scale;             // ERenderMode::Depth: 1 / dataset scale (testbed_nerf.cu:2822)
 };
-enum : uint32_t { RENDER_SHADE = 1, RENDER_NORMALS = 2 };
+enum : uint32_t { RENDER_AO = 0, RENDER_SHADE = 1, RENDER_NORMALS = 2, RENDER_POSITIONS = 3, RENDER_DEPTH = 4 };
 struct RenderWorkspace {
 	void* payload[2]; void* payload_hit;
 	float* rgba[2]; float* rgba_hit;

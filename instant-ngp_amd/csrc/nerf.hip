@@ -1758,9 +1758,11 @@ __global__ void k_render_inputs(RenderArgs a, uint32_t n, uint32_t n_steps, Payl
 	p.n_steps = n_steps;
 }
 
-// composite_kernel_nerf (:1016-1196), ERenderMode::Shade and Normals; network output RM [16 x stride]. Normals
-// (:1183-1188): the colour of a step is normalize(-density'(raw) * d(raw density)/d(position)), the gradient
-// in the coordinates' position rows (render_frame's grad).
+// composite_kernel_nerf (:1016-1196); network output RM [16 x stride]. The colour of a step by ERenderMode
+// (:1183-1208): Shade the network's rgb; Normals normalize(-density'(raw) * d(raw density)/d(position)), the
+// gradient in the coordinates' position rows (render_frame's grad); Positions (pos - 0.5) / 2 + 0.5 (show_accel
+// off); Depth dot(camera forward, pos - ray origin) * depth_scale; AO the step's alpha. pos = unwarp_position of
+// the step's coordinate over the aabb the inputs were warped with.
 __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, uint32_t current_step, uint32_t n_steps,
                                    Payload* __restrict__ pay, float* __restrict__ rgba, const float* __restrict__ coords,
                                    const f16* __restrict__ out) {
@@ -1785,6 +1787,19 @@ __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, ui
 			const float nx = dd * coords[r * 7 + 0], ny = dd * coords[r * 7 + 1], nz = dd * coords[r * 7 + 2];
 			const float inv = 1.0f / sqrtf(nx * nx + ny * ny + nz * nz);  // glm normalize (0 -> NaN, as the reference)
 			rgb[0] = nx * inv; rgb[1] = ny * inv; rgb[2] = nz * inv;
+		} else if (a.render_mode == RENDER_POSITIONS || a.render_mode == RENDER_DEPTH) {
+			float pos[3];
+#pragma unroll
+			for (int k = 0; k < 3; ++k) pos[k] = coords[r * 7 + k] * (a.aabb_max[k] - a.aabb_min[k]) + a.aabb_min[k];
+			if (a.render_mode == RENDER_POSITIONS) {
+#pragma unroll
+				for (int k = 0; k < 3; ++k) rgb[k] = (pos[k] - 0.5f) / 2.0f + 0.5f;
+			} else {
+				const float z = (a.cam[6] * (pos[0] - p.o[0]) + a.cam[7] * (pos[1] - p.o[1]) + a.cam[8] * (pos[2] - p.o[2])) * a.depth_scale;
+				rgb[0] = rgb[1] = rgb[2] = z;
+			}
+		} else if (a.render_mode == RENDER_AO) {
+			rgb[0] = rgb[1] = rgb[2] = alpha;
 		} else {
 			rgb[0] = network_to_rgb(o0, a.rgb_activation);
 			rgb[1] = network_to_rgb(o1, a.rgb_activation);
@@ -1818,7 +1833,7 @@ __global__ void k_render_shade(uint32_t n_hit, uint32_t linear_colors, uint32_t 
 	if (mode == RENDER_NORMALS) {  // (0.5 n + 0.5) * a with n = normalize(rgb)
 		const float inv = 1.0f / sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
 		for (int k = 0; k < 3; ++k) c[k] = (0.5f * (c[k] * inv) + 0.5f) * c[3];
-	} else if (!linear_colors) {
+	} else if (!linear_colors && mode == RENDER_SHADE) {  // only Shade (and Slice) accumulate in linear colours
 		c[0] = srgb_to_linear(c[0]); c[1] = srgb_to_linear(c[1]); c[2] = srgb_to_linear(c[2]);
 	}
 	float* f = frame + 4 * (size_t)hit[i].idx;
@@ -1835,7 +1850,8 @@ __global__ void k_render_accumulate(uint32_t n4, float w, const float* __restric
 
 void render_frame(const RenderArgs& a, uint32_t spp, RenderWorkspace& ws, const std::function<void(uint32_t, const float*, f16*)>& infer,
                   float* out, hipStream_t s, const std::function<void(uint32_t, float*)>& grad) {
-	NGP_CHECK(a.render_mode == RENDER_SHADE || (a.render_mode == RENDER_NORMALS && grad), "render: Shade and Normals are implemented");
+	NGP_CHECK(a.render_mode <= RENDER_DEPTH && (a.render_mode != RENDER_NORMALS || grad),
+	          "render: AO, Shade, Normals, Positions and Depth are implemented");
 	const uint32_t n_px = a.width * a.height;
 	if (n_px == 0) return;
 	const uint32_t MARCH_ITER = 10000, MIN_STEPS = 1, MAX_STEPS = 8, TARGET_QUERIES = 2 * 1024 * 1024;

@@ -84,6 +84,7 @@ struct ngp_nerf_renderer {
 	Buf pay0, pay1, payh, rgba0, rgba1, rgbah, coords, out, frame, counters;
 	uint32_t* host_counters = nullptr;
 	uint32_t render_mode = RENDER_SHADE;  // ngp_nerf_renderer_set_mode
+	float depth_scale = 1.0f;             // ngp_nerf_renderer_set_depth_scale
 	~ngp_nerf_renderer() { if (host_counters) (void)hipHostFree(host_counters); }
 };
 
@@ -444,8 +445,13 @@ int ngp_nerf_renderer_create(ngp_nerf_renderer** out) {
 }
 void ngp_nerf_renderer_destroy(ngp_nerf_renderer* r) { delete r; }
 int ngp_nerf_renderer_set_mode(ngp_nerf_renderer* r, int render_mode) {
-	if (!r || (render_mode != RENDER_SHADE && render_mode != RENDER_NORMALS)) return NGP_INVALID;
+	if (!r || render_mode < (int)RENDER_AO || render_mode > (int)RENDER_DEPTH) return NGP_INVALID;
 	r->render_mode = (uint32_t)render_mode;
+	return NGP_OK;
+}
+int ngp_nerf_renderer_set_depth_scale(ngp_nerf_renderer* r, float depth_scale) {
+	if (!r) return NGP_INVALID;
+	r->depth_scale = depth_scale;
 	return NGP_OK;
 }
 
@@ -494,6 +500,7 @@ int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_confi
 		if (!r->host_counters) NGP_HIP(hipHostMalloc(&r->host_counters, 16));
 		ws.host_counters = r->host_counters;
 		a.render_mode = r->render_mode;
+		a.depth_scale = r->depth_scale;
 		auto infer = [&](uint32_t n, const float* coords, f16* out) {
 			check_rc(ngp_inference(model, s, n, coords, 7, out, n, NGP_LAYOUT_SOA, use_inference_params));
 		};
@@ -1022,6 +1029,90 @@ template <typename T> std::vector<T> device_to_host(const void* d, size_t n) {
 	if (n) NGP_HIP(hipMemcpy(h.data(), d, n * sizeof(T), hipMemcpyDeviceToHost));
 	return h;
 }
+
+void check_ok(int rc) {
+	if (rc != NGP_OK) throw ngp::Error(ngp_last_error());
+}
+
+const char* const OPT_NAMES[5] = {"full_precision_params_binary", "first_moments_binary", "second_moments_binary",
+                                  "ema_params_binary", "param_steps_binary"};
+
+// tcnn Trainer::serialize(include_optimizer_state) (testbed.cu:4874): n_params, params_type, params_binary (the fp16
+// parameters) and, with the optimizer state, an "optimizer" member: the Adam moments and per-parameter steps, the
+// EMA weights and the fp32 master weights under tcnn-style names (tcnn absent: the member names are a restatement,
+// parity unpinned)
+void trainer_to_snapshot(ngp_trainer* tr, uint64_t n, bool include_optimizer_state, Value& snap) {
+	snap["n_params"] = Value::uint(n);
+	snap["params_type"] = Value::str("__half");
+	{
+		auto p = device_to_host<uint16_t>(ngp_trainer_params(tr), n);
+		snap["params_binary"] = Value::bin(p.data(), p.size() * 2);
+	}
+	if (!include_optimizer_state) return;
+	uint64_t bytes = 0;
+	check_ok(ngp_trainer_serialize(tr, nullptr, &bytes));
+	std::string blob(bytes, '\0');
+	check_ok(ngp_trainer_serialize(tr, blob.data(), &bytes));
+	uint64_t hdr[4];
+	memcpy(hdr, blob.data(), 32);
+	Value opt = Value::object();
+	opt["otype"] = Value::str("Ema(ExponentialDecay(Adam))");
+	opt["current_step"] = Value::uint(hdr[3]);
+	for (int k = 0; k < 5; ++k) opt[OPT_NAMES[k]] = Value::bin(blob.data() + 32 + (size_t)k * n * 4, (size_t)n * 4);
+	snap["optimizer"] = opt;
+}
+
+// tcnn Trainer::deserialize (testbed.cu:5040): the parameters, then the optimizer state when the snapshot has one.
+// An optimizer member without some of this engine's arrays (one written by another implementation of the chain)
+// fills them from what is there: fp32 master weights and EMA from the parameters, moments and steps from 0.
+void trainer_from_snapshot(ngp_trainer* tr, uint64_t n, const Value& snap) {
+	NGP_CHECK((uint64_t)snap.at("n_params").number() == n, "snapshot: parameter count differs from this network");
+	const Value& pb = snap.at("params_binary");
+	const std::string type = snap.find("params_type") ? snap.at("params_type").s : std::string("__half");
+	std::vector<float> w(n);
+	if (type == "float") {
+		NGP_CHECK(pb.s.size() == n * 4, "snapshot: params_binary size");
+		memcpy(w.data(), pb.s.data(), n * 4);
+	} else {
+		NGP_CHECK(type == "__half" && pb.s.size() == n * 2, "snapshot: params_binary size/type");
+		const ngp::f16* h = (const ngp::f16*)pb.s.data();
+		for (uint64_t k = 0; k < n; ++k) w[k] = (float)h[k];
+	}
+	check_ok(ngp_trainer_set_params_full_precision(tr, w.data(), n));
+	const Value* opt = snap.find("optimizer");
+	if (!opt) return;
+	std::string blob(32 + (size_t)n * 20, '\0');
+	const uint64_t hdr[4] = {0x4e47504d49333535ULL, 1, n, (uint64_t)opt->number_or("current_step", 0.0)};
+	memcpy(blob.data(), hdr, 32);
+	for (int k = 0; k < 5; ++k) {
+		char* dst = blob.data() + 32 + (size_t)k * n * 4;
+		if (const Value* b = opt->find(OPT_NAMES[k])) {
+			NGP_CHECK(b->s.size() == n * 4, std::string("snapshot: optimizer ") + OPT_NAMES[k] + " size");
+			memcpy(dst, b->s.data(), n * 4);
+		} else if (k == 0 || k == 3) {
+			memcpy(dst, w.data(), n * 4);  // master weights / EMA: the parameters
+		}  // moments, steps: 0
+	}
+	check_ok(ngp_trainer_deserialize(tr, blob.data(), blob.size()));
+}
+
+void write_snapshot(const char* path, Value& root, Value& snap, int compress) {
+	root["snapshot"] = snap;
+	std::string bytes;
+	ngp::mp::encode(root, bytes);
+	if (ends_with_ci(path, ".ingp")) bytes = gzip_bytes(bytes, compress ? Z_DEFAULT_COMPRESSION : Z_NO_COMPRESSION);
+	std::ofstream f(path, std::ios::binary);
+	NGP_CHECK(f.good(), std::string("snapshot: cannot write '") + path + "'");
+	f.write(bytes.data(), (std::streamsize)bytes.size());
+	NGP_CHECK(f.good(), "snapshot: write failed");
+}
+
+Value snapshot_root(const char* network_config_json) {
+	Value root = network_config_json && *network_config_json ? ngp::mp::from_json(ngp::Json::parse(network_config_json))
+	                                                          : Value::object();
+	root.erase("snapshot");
+	return root;
+}
 }  // namespace
 
 extern "C" {
@@ -1031,33 +1122,9 @@ int ngp_nerf_save_snapshot(ngp_nerf_trainer* t, void* stream, const char* path, 
 	if (!t || !path) return NGP_INVALID;
 	NERF_TRY({
 		NGP_HIP(hipStreamSynchronize(S(stream)));
-		Value root = network_config_json && *network_config_json ? ngp::mp::from_json(ngp::Json::parse(network_config_json))
-		                                                          : Value::object();
-		root.erase("snapshot");
+		Value root = snapshot_root(network_config_json);
 		Value snap = Value::object();
-		// tcnn Trainer::serialize
-		const uint64_t n = ngp_model_n_params(t->model);
-		snap["n_params"] = Value::uint(n);
-		snap["params_type"] = Value::str("__half");
-		{
-			auto p = device_to_host<uint16_t>(ngp_trainer_params(t->trainer), n);
-			snap["params_binary"] = Value::bin(p.data(), p.size() * 2);
-		}
-		if (include_optimizer_state) {
-			uint64_t bytes = 0;
-			check_rc(ngp_trainer_serialize(t->trainer, nullptr, &bytes));
-			std::string blob(bytes, '\0');
-			check_rc(ngp_trainer_serialize(t->trainer, blob.data(), &bytes));
-			uint64_t hdr[4];
-			memcpy(hdr, blob.data(), 32);
-			Value opt = Value::object();
-			opt["otype"] = Value::str("Ema(ExponentialDecay(Adam))");
-			opt["current_step"] = Value::uint(hdr[3]);
-			const char* names[5] = {"full_precision_params_binary", "first_moments_binary", "second_moments_binary",
-			                        "ema_params_binary", "param_steps_binary"};
-			for (int k = 0; k < 5; ++k) opt[names[k]] = Value::bin(blob.data() + 32 + (size_t)k * n * 4, (size_t)n * 4);
-			snap["optimizer"] = opt;
-		}
+		trainer_to_snapshot(t->trainer, ngp_model_n_params(t->model), include_optimizer_state != 0, snap);
 		snap["version"] = Value::uint(SNAPSHOT_FORMAT_VERSION);
 		snap["mode"] = Value::str("nerf");
 		snap["density_grid_size"] = Value::uint(GRIDSIZE);
@@ -1078,14 +1145,7 @@ int ngp_nerf_save_snapshot(ngp_nerf_trainer* t, void* stream, const char* path, 
 		snap["aabb"]["min"] = vec3(t->cfg.aabb_min);
 		snap["aabb"]["max"] = vec3(t->cfg.aabb_max);
 		snap["density_grid_ema_step"] = Value::uint(t->ema_step);
-		root["snapshot"] = snap;
-		std::string bytes;
-		ngp::mp::encode(root, bytes);
-		if (ends_with_ci(path, ".ingp")) bytes = gzip_bytes(bytes, compress ? Z_DEFAULT_COMPRESSION : Z_NO_COMPRESSION);
-		std::ofstream f(path, std::ios::binary);
-		NGP_CHECK(f.good(), std::string("snapshot: cannot write '") + path + "'");
-		f.write(bytes.data(), (std::streamsize)bytes.size());
-		NGP_CHECK(f.good(), "snapshot: write failed");
+		write_snapshot(path, root, snap, compress);
 	});
 }
 
@@ -1101,34 +1161,7 @@ int ngp_nerf_load_snapshot(ngp_nerf_trainer* t, void* stream, const char* path) 
 		NGP_CHECK(snap.number_or("version", 0) >= SNAPSHOT_FORMAT_VERSION, "Snapshot uses an old format and can not be loaded.");
 		if (const Value* m = snap.find("mode")) NGP_CHECK(m->type == Value::Str && m->s == "nerf", "snapshot: not a NeRF snapshot");
 		NGP_CHECK((uint32_t)snap.at("density_grid_size").number() == GRIDSIZE, "Incompatible grid size.");
-		// tcnn Trainer::deserialize
-		const uint64_t n = ngp_model_n_params(t->model);
-		NGP_CHECK((uint64_t)snap.at("n_params").number() == n, "snapshot: parameter count differs from this network");
-		const Value& pb = snap.at("params_binary");
-		const std::string type = snap.find("params_type") ? snap.at("params_type").s : std::string("__half");
-		std::vector<float> w(n);
-		if (type == "float") {
-			NGP_CHECK(pb.s.size() == n * 4, "snapshot: params_binary size");
-			memcpy(w.data(), pb.s.data(), n * 4);
-		} else {
-			NGP_CHECK(type == "__half" && pb.s.size() == n * 2, "snapshot: params_binary size/type");
-			const f16* h = (const f16*)pb.s.data();
-			for (uint64_t k = 0; k < n; ++k) w[k] = (float)h[k];
-		}
-		check_rc(ngp_trainer_set_params_full_precision(t->trainer, w.data(), n));
-		if (const Value* opt = snap.find("optimizer")) {
-			const char* names[5] = {"full_precision_params_binary", "first_moments_binary", "second_moments_binary",
-			                        "ema_params_binary", "param_steps_binary"};
-			std::string blob(32 + (size_t)n * 20, '\0');
-			const uint64_t hdr[4] = {0x4e47504d49333535ULL, 1, n, (uint64_t)opt->at("current_step").number()};
-			memcpy(blob.data(), hdr, 32);
-			for (int k = 0; k < 5; ++k) {
-				const Value& b = opt->at(names[k]);
-				NGP_CHECK(b.s.size() == n * 4, "snapshot: optimizer state size");
-				memcpy(blob.data() + 32 + (size_t)k * n * 4, b.s.data(), n * 4);
-			}
-			check_rc(ngp_trainer_deserialize(t->trainer, blob.data(), blob.size()));
-		}
+		trainer_from_snapshot(t->trainer, ngp_model_n_params(t->model), snap);  // tcnn Trainer::deserialize
 		// density grid (fp16 in the file)
 		const Value& gb = snap.at("density_grid_binary");
 		const uint32_t n_el = GRID_N_CELLS * (t->cfg.max_cascade + 1);
@@ -1152,6 +1185,68 @@ int ngp_nerf_load_snapshot(ngp_nerf_trainer* t, void* stream, const char* path) 
 		t->loss_scalar = (float)snap.number_or("loss", 0.0);
 		t->ema_step = (uint32_t)snap.number_or("density_grid_ema_step", (double)t->training_step);
 		NGP_HIP(hipStreamSynchronize(s));
+	});
+}
+
+// Testbed::save_snapshot / load_snapshot for the image and SDF testbeds (testbed.cu:4873-4937, 4939-5057): the
+// mode-independent members (Trainer::serialize, version, mode, training_step, loss, aabb, bounding_radius).
+int ngp_save_snapshot(ngp_trainer* t, void* stream, const char* path, const char* network_config_json, const char* mode,
+                      const float* aabb_min, const float* aabb_max, float bounding_radius, uint32_t training_step, float loss,
+                      int include_optimizer_state, int compress) {
+	if (!t || !path || !mode) return NGP_INVALID;
+	NERF_TRY({
+		NGP_HIP(hipStreamSynchronize(S(stream)));
+		Value root = snapshot_root(network_config_json);
+		Value snap = Value::object();
+		trainer_to_snapshot(t, ngp_trainer_n_params(t), include_optimizer_state != 0, snap);
+		snap["version"] = Value::uint(SNAPSHOT_FORMAT_VERSION);
+		snap["mode"] = Value::str(mode);
+		snap["training_step"] = Value::uint(training_step);
+		snap["loss"] = Value::real(loss);
+		const float zero[3] = {0.f, 0.f, 0.f}, one[3] = {1.f, 1.f, 1.f};
+		snap["aabb"]["min"] = vec3(aabb_min ? aabb_min : zero);
+		snap["aabb"]["max"] = vec3(aabb_max ? aabb_max : one);
+		snap["bounding_radius"] = Value::real(bounding_radius);
+		write_snapshot(path, root, snap, compress);
+	});
+}
+
+int ngp_load_snapshot(ngp_trainer* t, void* stream, const char* path, uint32_t* training_step, float* loss, float* aabb_min,
+                      float* aabb_max, float* bounding_radius) {
+	if (!t || !path) return NGP_INVALID;
+	NERF_TRY({
+		NGP_HIP(hipStreamSynchronize(S(stream)));
+		const Value root = load_network_config(path);
+		NGP_CHECK(root.find("snapshot"), std::string("File '") + path + "' does not contain a snapshot.");
+		const Value& snap = root.at("snapshot");
+		NGP_CHECK(snap.number_or("version", 0) >= SNAPSHOT_FORMAT_VERSION, "Snapshot uses an old format and can not be loaded.");
+		trainer_from_snapshot(t, ngp_trainer_n_params(t), snap);
+		if (training_step) *training_step = (uint32_t)snap.number_or("training_step", 0.0);
+		if (loss) *loss = (float)snap.number_or("loss", 0.0);
+		if (bounding_radius) *bounding_radius = (float)snap.number_or("bounding_radius", (double)*bounding_radius);
+		if (const Value* a = snap.find("aabb")) {
+			for (int d = 0; d < 3; ++d) {
+				if (aabb_min) aabb_min[d] = (float)a->at("min").arr.at(d).number();
+				if (aabb_max) aabb_max[d] = (float)a->at("max").arr.at(d).number();
+			}
+		}
+	});
+}
+
+// The snapshot's mode ("nerf", "sdf", "image", ...; testbed.cu:4950-4957: a snapshot without one but with a "nerf"
+// member is a NeRF snapshot), so that a Testbed can switch mode before reset_network
+int ngp_snapshot_mode(const char* path, char* mode_buf, uint64_t cap) {
+	if (!path || !mode_buf || cap == 0) return NGP_INVALID;
+	NERF_TRY({
+		const Value root = load_network_config(path);
+		NGP_CHECK(root.find("snapshot"), std::string("File '") + path + "' does not contain a snapshot.");
+		const Value& snap = root.at("snapshot");
+		std::string m;
+		if (const Value* v = snap.find("mode")) m = v->s;
+		else if (snap.find("nerf")) m = "nerf";
+		NGP_CHECK(!m.empty(), "Unknown snapshot mode. Snapshot must be regenerated with a new version of instant-ngp.");
+		NGP_CHECK(m.size() + 1 <= cap, "snapshot mode: buffer too small");
+		memcpy(mode_buf, m.c_str(), m.size() + 1);
 	});
 }
 

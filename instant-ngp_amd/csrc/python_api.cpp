@@ -67,8 +67,9 @@ void load_training_data(Testbed& tb, const std::string& path) {
 			ptrs.push_back(keep.back().data());
 		}
 		const float aabb_scale = d.attr("aabb_scale").cast<float>();
+		const float scale = py::hasattr(d, "scale") ? d.attr("scale").cast<float>() : 1.0f;
 		py::gil_scoped_release nogil;
-		tb.load_nerf(meta, ptrs, aabb_scale);
+		tb.load_nerf(meta, ptrs, aabb_scale, scale);
 		break;
 	}
 	case ETestbedMode::Image: {

@@ -59,6 +59,17 @@ inline ETestbedMode mode_from_scene(const std::string& scene) {
 	return ETestbedMode::Image;
 }
 
+// to_string(ETestbedMode) (common.cu:175-184)
+inline const char* mode_name(ETestbedMode m) {
+	switch (m) {
+	case ETestbedMode::Nerf: return "nerf";
+	case ETestbedMode::Sdf: return "sdf";
+	case ETestbedMode::Image: return "image";
+	case ETestbedMode::Volume: return "volume";
+	default: return "none";
+	}
+}
+
 // mode_from_string (common.cu:161-173)
 inline ETestbedMode mode_from_string(const std::string& s) {
 	if (ngp::iequals(s, "nerf")) return ETestbedMode::Nerf;
@@ -229,7 +240,8 @@ public:
 	// ---- training data ------------------------------------------------------------------------------
 	// Testbed::load_nerf + load_nerf_post (testbed_nerf.cu:3093-3109): decoded images (RGBA8 sRGB) with their
 	// metadata after nerf_matrix_to_ngp, and the dataset's aabb_scale
-	void load_nerf(const std::vector<ngp_nerf_image>& images, const std::vector<const void*>& rgba8, float aabb_scale) {
+	void load_nerf(const std::vector<ngp_nerf_image>& images, const std::vector<const void*>& rgba8, float aabb_scale,
+	               float dataset_scale = 1.0f) {
 		set_mode(ETestbedMode::Nerf);
 		if (images.empty() || images.size() != rgba8.size()) throw std::runtime_error("load_nerf: one RGBA8 buffer per image");
 		free_network();
@@ -237,6 +249,7 @@ public:
 		check(ngp_nerf_dataset_create((uint32_t)images.size(), images.data(), rgba8.data(), &m_nerf_dataset), "ngp_nerf_dataset_create");
 		m_nerf_images = images;
 		m_aabb_scale = aabb_scale;
+		m_dataset_scale = dataset_scale;  // NerfDataset::scale (nerf_loader.cu:388): Depth renders in its units
 		check(ngp_nerf_default_config(aabb_scale, &m_nerf_cfg), "ngp_nerf_default_config");
 		m_training_data_available = true;
 		set_camera_to_training_view(0);
@@ -434,16 +447,34 @@ public:
 	float loss() const { return m_loss_scalar; }
 	uint32_t training_step() const { return m_training_step; }
 
-	// ---- snapshots (NeRF: the .ingp / msgpack format of testbed.cu:4873-5057) -------------------------
+	// ---- snapshots (the .ingp / msgpack format of testbed.cu:4873-5057, every mode) -----------------------
 	void save_snapshot(const std::string& path, bool include_optimizer_state, bool compress) {
-		require_nerf_trainer("save_snapshot");
-		check(ngp_nerf_save_snapshot(m_nerf_trainer, nullptr, path.c_str(), m_network_config.dump().c_str(),
-		                             include_optimizer_state ? 1 : 0, compress ? 1 : 0),
-		      "ngp_nerf_save_snapshot");
+		if (m_testbed_mode == ETestbedMode::Nerf) {
+			require_nerf_trainer("save_snapshot");
+			check(ngp_nerf_save_snapshot(m_nerf_trainer, nullptr, path.c_str(), m_network_config.dump().c_str(),
+			                             include_optimizer_state ? 1 : 0, compress ? 1 : 0),
+			      "ngp_nerf_save_snapshot");
+			return;
+		}
+		if (!m_trainer) throw std::runtime_error("save_snapshot: no network (train first)");
+		const float img_min[3] = {0.f, 0.f, 0.f}, img_max[3] = {1.f, 1.f, 1.f};
+		const bool sdf = m_testbed_mode == ETestbedMode::Sdf;
+		check(ngp_save_snapshot(m_trainer, nullptr, path.c_str(), m_network_config.dump().c_str(), mode_name(m_testbed_mode),
+		                        sdf ? m_sdf_aabb_min : img_min, sdf ? m_sdf_aabb_max : img_max, m_bounding_radius, m_training_step,
+		                        m_loss_scalar, include_optimizer_state ? 1 : 0, compress ? 1 : 0),
+		      "ngp_save_snapshot");
 	}
+	// Testbed::load_snapshot (testbed.cu:4939-5057): the snapshot's mode (a different one drops the loaded data, as
+	// set_mode does), its network config, then the trainer state and the mode's members
 	void load_snapshot(const std::string& path) {
-		if (m_testbed_mode != ETestbedMode::Nerf || !m_nerf_dataset)
-			throw std::runtime_error("load_snapshot: load the NeRF training data first (snapshots are implemented for NeRF)");
+		char mode[32];
+		check(ngp_snapshot_mode(path.c_str(), mode, sizeof mode), "ngp_snapshot_mode");
+		const ETestbedMode m = mode_from_string(mode);
+		if (m == ETestbedMode::None || m == ETestbedMode::Volume)
+			throw std::runtime_error(std::string("load_snapshot: unsupported snapshot mode '") + mode + "'");
+		set_mode(m);
+		if (m == ETestbedMode::Nerf && !m_nerf_dataset)
+			throw std::runtime_error("load_snapshot: load the NeRF training data first (the snapshot's dataset member is not read)");
 		uint64_t size = 0;
 		check(ngp_snapshot_network_config(path.c_str(), nullptr, &size), "ngp_snapshot_network_config");
 		std::string cfg(size, '\0');
@@ -451,8 +482,18 @@ public:
 		cfg.resize(strlen(cfg.c_str()));
 		m_network_config = Json::parse(cfg);
 		reset_network();
-		check(ngp_nerf_load_snapshot(m_nerf_trainer, nullptr, path.c_str()), "ngp_nerf_load_snapshot");
-		m_training_step = ngp_trainer_step(m_trainer);  // one optimizer step per training step
+		if (m == ETestbedMode::Nerf) {
+			check(ngp_nerf_load_snapshot(m_nerf_trainer, nullptr, path.c_str()), "ngp_nerf_load_snapshot");
+			m_training_step = ngp_trainer_step(m_trainer);  // one optimizer step per training step
+			return;
+		}
+		float amin[3], amax[3];
+		check(ngp_load_snapshot(m_trainer, nullptr, path.c_str(), &m_training_step, &m_loss_scalar, amin, amax, &m_bounding_radius),
+		      "ngp_load_snapshot");
+		if (m == ETestbedMode::Sdf) {
+			std::memcpy(m_sdf_aabb_min, amin, sizeof amin);
+			std::memcpy(m_sdf_aabb_max, amax, sizeof amax);
+		}
 	}
 
 	// ---- camera and rendering -----------------------------------------------------------------------
@@ -479,11 +520,13 @@ public:
 		if (!m_model) throw std::runtime_error("render: no network (train or load a snapshot first)");
 		std::vector<float> out((size_t)width * height * 4);
 		if (m_testbed_mode == ETestbedMode::Nerf) {
-			if (m_render_mode != ERenderMode::Shade && m_render_mode != ERenderMode::Normals)
-				throw std::runtime_error("render: ERenderMode Shade and Normals are implemented");
+			if ((int)m_render_mode > (int)ERenderMode::Depth)
+				throw std::runtime_error("render: ERenderMode AO, Shade, Normals, Positions and Depth are implemented");
 			require_nerf_trainer("render");
 			if (!m_renderer) check(ngp_nerf_renderer_create(&m_renderer), "ngp_nerf_renderer_create");
 			check(ngp_nerf_renderer_set_mode(m_renderer, (int)m_render_mode), "ngp_nerf_renderer_set_mode");
+			// depth_scale = 1 / m_nerf.training.dataset.scale (render_nerf, testbed_nerf.cu:2822)
+			check(ngp_nerf_renderer_set_depth_scale(m_renderer, 1.0f / m_dataset_scale), "ngp_nerf_renderer_set_depth_scale");
 			ngp_nerf_image cam{};
 			cam.width = width;
 			cam.height = height;
@@ -622,6 +665,7 @@ private:
 	ngp_nerf_config m_nerf_cfg{};
 	std::vector<ngp_nerf_image> m_nerf_images;
 	float m_aabb_scale = 1.f;
+	float m_dataset_scale = 1.f;
 	uint32_t m_lens_mode = 0;
 	float m_lens_params[4] = {0, 0, 0, 0};
 	// image

@@ -744,9 +744,17 @@ EXPORT void orc_nerf_render_march(const ocfg* c, const oimg* cam, const uint8_t*
 	}
 }
 
-/* out16: network outputs [W*H x max_per_ray x 16] (AoS, half bits); frame: [W*H x 4] linear rgba */
-EXPORT void orc_nerf_render_composite(const ocfg* c, uint32_t n_px, uint32_t max_per_ray, const float* coords, const int32_t* counts,
-                                      const uint16_t* out16, float min_transmittance, const float* bg, float* frame) {
+/* out16: network outputs [W*H x max_per_ray x 16] (AoS, half bits); frame: [W*H x 4] linear rgba.
+ * mode: ERenderMode (common.h:110-119) 0 AO, 1 Shade, 3 Positions, 4 Depth: the step colour of composite_kernel_nerf
+ * (testbed_nerf.cu:1189-1208; pos = unwarp_position over the aabb; Depth: dot(camera forward, pos - ray origin) *
+ * depth_scale with the origin the render's camera position, m_render_near_distance 0); shade_kernel_nerf
+ * (:2164-2196) decodes sRGB for Shade only. cam: the view (its camera matrix, for Depth). */
+EXPORT void orc_nerf_render_composite_mode(const ocfg* c, const oimg* cam, uint32_t n_px, uint32_t max_per_ray, const float* coords,
+                                           const int32_t* counts, const uint16_t* out16, float min_transmittance, const float* bg,
+                                           int mode, float depth_scale, float* frame) {
+	float m[12];
+	orc_camera_matrix(cam->xform, m);
+	const float diag[3] = {c->aabb_max[0] - c->aabb_min[0], c->aabb_max[1] - c->aabb_min[1], c->aabb_max[2] - c->aabb_min[2]};
 	for (uint32_t i = 0; i < n_px; ++i) {
 		float r = 0, g = 0, b = 0, a = 0;
 		for (int32_t k = 0; k < counts[i]; ++k) {
@@ -755,19 +763,39 @@ EXPORT void orc_nerf_render_composite(const ocfg* c, uint32_t n_px, uint32_t max
 			const float dt = coords[((size_t)i * max_per_ray + k) * 7 + 3] * (MIN_STEP * (1 << (CASCADES - 1)) - MIN_STEP) + MIN_STEP;
 			const float alpha = 1.f - ngp_expf(-to_dens(orc_f16_to_f32(o[3]), c->density_activation) * dt);
 			const float w = alpha * T;
-			r += to_rgb(orc_f16_to_f32(o[0]), c->rgb_activation) * w;
-			g += to_rgb(orc_f16_to_f32(o[1]), c->rgb_activation) * w;
-			b += to_rgb(orc_f16_to_f32(o[2]), c->rgb_activation) * w;
+			float rgb[3];
+			if (mode == 1) {
+				for (int q = 0; q < 3; ++q) rgb[q] = to_rgb(orc_f16_to_f32(o[q]), c->rgb_activation);
+			} else if (mode == 0) {
+				rgb[0] = rgb[1] = rgb[2] = alpha;
+			} else {
+				const float* wp = coords + ((size_t)i * max_per_ray + k) * 7;
+				float pos[3];
+				for (int q = 0; q < 3; ++q) pos[q] = wp[q] * diag[q] + c->aabb_min[q];
+				if (mode == 3) {
+					for (int q = 0; q < 3; ++q) rgb[q] = (pos[q] - 0.5f) / 2.0f + 0.5f;
+				} else {
+					const float z = (m[6] * (pos[0] - m[9]) + m[7] * (pos[1] - m[10]) + m[8] * (pos[2] - m[11])) * depth_scale;
+					rgb[0] = rgb[1] = rgb[2] = z;
+				}
+			}
+			r += rgb[0] * w;
+			g += rgb[1] * w;
+			b += rgb[2] * w;
 			a += w;
 			if (a > 1.0f - min_transmittance) { const float inv = 1.0f / a; r *= inv; g *= inv; b *= inv; a *= inv; break; }
 		}
 		float* f = frame + 4 * (size_t)i;
 		f[0] = bg[0]; f[1] = bg[1]; f[2] = bg[2]; f[3] = bg[3];
 		if (counts[i] < 0 || !(a > 0.001f)) continue;
-		if (!c->linear_colors) { r = s2l(r); g = s2l(g); b = s2l(b); }
+		if (!c->linear_colors && mode == 1) { r = s2l(r); g = s2l(g); b = s2l(b); }
 		const float cc[4] = {r, g, b, a};
 		for (int k = 0; k < 4; ++k) f[k] = cc[k] + f[k] * (1.0f - a);
 	}
+}
+EXPORT void orc_nerf_render_composite(const ocfg* c, const oimg* cam, uint32_t n_px, uint32_t max_per_ray, const float* coords,
+                                      const int32_t* counts, const uint16_t* out16, float min_transmittance, const float* bg, float* frame) {
+	orc_nerf_render_composite_mode(c, cam, n_px, max_per_ray, coords, counts, out16, min_transmittance, bg, 1, 1.0f, frame);
 }
 
 /* The shared transcendental (instant-ngp_amd/csrc/ngp_math.h), exported for its accuracy test:

@@ -421,7 +421,8 @@ def _declare_nerf(L):
     d("orc_fill_rollover_f16", None, u32, u32, u32, P, C.c_int)
     d("orc_ld_random_val", f32, u32, u32, u32)
     d("orc_nerf_render_march", None, P, P, P, u32, u32, P, P)
-    d("orc_nerf_render_composite", None, P, u32, u32, P, P, P, f32, P, P)
+    d("orc_nerf_render_composite", None, P, P, u32, u32, P, P, P, f32, P, P)
+    d("orc_nerf_render_composite_mode", None, P, P, u32, u32, P, P, P, f32, P, C.c_int, f32, P)
 
 
 N_CELLS = 128 ** 3
@@ -624,10 +625,14 @@ def sdf_signed_distance(pos, tris):
     return out
 
 
+RENDER_MODES = {"AO": 0, "Shade": 1, "Positions": 3, "Depth": 4}  # ERenderMode (common.h:110-119)
+
+
 def nerf_render(cfg, cam, model, params16, bitfield, sample_index=0, min_transmittance=0.01, bg=(0, 0, 0, 0),
-                max_per_ray=1024):
-    """NerfTracer restated per ray: march, oracle NerfNetwork on every sample, composite, shade.
-    Returns linear rgba [H, W, 4] and the per-pixel sample counts."""
+                max_per_ray=1024, render_mode="Shade", depth_scale=1.0):
+    """NerfTracer restated per ray: march, oracle NerfNetwork on every sample, composite (the step colour of
+    render_mode: AO, Shade, Positions or Depth), shade. Returns linear rgba [H, W, 4] and the per-pixel sample
+    counts."""
     W, H = cam.width, cam.height
     coords = np.zeros((W * H, max_per_ray, 7), np.float32)
     counts = np.zeros(W * H, np.int32)
@@ -640,8 +645,9 @@ def nerf_render(cfg, cam, model, params16, bitfield, sample_index=0, min_transmi
         out16[mask] = f32_to_f16_bits(o)
     frame = np.zeros((W * H, 4), np.float32)
     bgv = np.asarray(bg, np.float32)
-    lib().orc_nerf_render_composite(C.byref(cfg), W * H, max_per_ray, ptr(coords), ptr(counts), ptr(out16),
-                                    min_transmittance, ptr(bgv), ptr(frame))
+    lib().orc_nerf_render_composite_mode(C.byref(cfg), C.byref(cam), W * H, max_per_ray, ptr(coords), ptr(counts),
+                                         ptr(out16), min_transmittance, ptr(bgv), RENDER_MODES[render_mode],
+                                         float(depth_scale), ptr(frame))
     return frame.reshape(H, W, 4), counts
 
 

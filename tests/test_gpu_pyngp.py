@@ -75,6 +75,15 @@ def test_testbed_trains_like_the_python_mirror_and_round_trips_a_snapshot(pkg, s
     cam = pkg.nerf.make_image(64, 48, list(im3.xform), focal=focal, principal=tuple(im3.principal_point))
     ref = pkg.nerf.NerfRenderer().render(net, cfg, cam, run.bitfield, spp=1, background=(0, 0, 0, 1)).cpu().numpy()
     np.testing.assert_array_equal(img, ref)
+    # ERenderMode::Depth through the Testbed: depth in the dataset's units (depth_scale = 1 / dataset scale,
+    # testbed_nerf.cu:2822), the same frame as the renderer called directly
+    tb.render_mode = ngp.RenderMode.Depth
+    depth = tb.render(64, 48, spp=1, linear=True)
+    tb.render_mode = ngp.RenderMode.Shade
+    ref_d = pkg.nerf.NerfRenderer().render(net, cfg, cam, run.bitfield, spp=1, background=(0, 0, 0, 1), render_mode="Depth",
+                                           depth_scale=1.0 / d.scale).cpu().numpy()
+    np.testing.assert_array_equal(depth, ref_d)
+    assert np.isfinite(depth).all() and depth[..., 0].max() > 0.1
 
     # snapshot round trip into a fresh Testbed: the parameters, optimizer state and fp16 density grid it
     # restores are the ones saved (its own snapshot carries them unchanged), and it renders what the
@@ -125,6 +134,7 @@ def test_testbed_sdf_and_image_modes(pkg, tmp_path):
         for _ in range(33):
             tb.frame()
         assert tb.training_step == 33 and np.isfinite(tb.loss) and tb.loss > 0
+        _snapshot_round_trip(ngp, tb, tmp_path / "arm.ingp", ngp.TestbedMode.Sdf, arm)
     img = pkg.synthetic.synthetic_image(64, 48, seed=2)
     path = tmp_path / "img.npy"
     np.save(path, img.astype(np.float32))
@@ -142,6 +152,40 @@ def test_testbed_sdf_and_image_modes(pkg, tmp_path):
     out = tb.render(64, 48, spp=1, linear=True)
     assert out.shape == (48, 64, 4) and np.isfinite(out).all()
     assert tb.loss < first
+    _snapshot_round_trip(ngp, tb, tmp_path / "img.ingp", ngp.TestbedMode.Image, str(path))
+    # after a load the inference parameters are the loaded parameters (testbed.cu:5040): a fresh Testbed and the
+    # first one reloading its own snapshot render the same frame
+    tb3 = ngp.Testbed()
+    tb3.load_training_data(str(path))
+    tb3.load_snapshot(str(tmp_path / "img.ingp"))
+    tb.load_snapshot(str(tmp_path / "img.ingp"))
+    np.testing.assert_array_equal(tb3.render(64, 48, spp=1, linear=True), tb.render(64, 48, spp=1, linear=True))
+
+
+def _snapshot_round_trip(ngp, tb, path, mode, data):
+    """Testbed::save_snapshot / load_snapshot for the SDF and image testbeds (testbed.cu:4873-5057): a fresh Testbed
+    loads the file (its mode from the snapshot), holds the same training step and network, writes the same
+    parameters and optimizer state back, and trains on."""
+    import gzip
+    import msgpack
+    tb.save_snapshot(str(path), include_optimizer_state=True, compress=True)
+    tb2 = ngp.Testbed()
+    tb2.load_training_data(data)
+    tb2.load_snapshot(str(path))
+    assert tb2.mode == mode and tb2.training_step == tb.training_step and tb2.n_params() == tb.n_params()
+    path2 = str(path) + ".2.ingp"
+    tb2.save_snapshot(path2, include_optimizer_state=True, compress=True)
+    a, b = (msgpack.unpackb(gzip.decompress(open(p, "rb").read()), raw=False)["snapshot"] for p in (str(path), path2))
+    assert a["mode"] == b["mode"] == {ngp.TestbedMode.Sdf: "sdf", ngp.TestbedMode.Image: "image"}[mode]
+    assert a["params_binary"] == b["params_binary"] and len(a["params_binary"]) == 2 * tb.n_params()
+    for k, v in a["optimizer"].items():
+        assert b["optimizer"][k] == v, k
+    assert a["aabb"] == b["aabb"] and a["training_step"] == b["training_step"]
+    tb2.shall_train = True
+    for _ in range(3):
+        tb2.frame()
+    assert tb2.training_step == tb.training_step + 3 and np.isfinite(tb2.loss)
+    return tb2
 
 
 def _dense_entries(levels, b, nmin=16, d=3):

@@ -130,3 +130,27 @@ def test_psnr_after_training(pkg):
         ref = pkg.nerf.ground_truth_linear(S.render(c2w, 96, 96))
         ps.append(pkg.nerf.psnr(img, ref)[0])
     assert np.mean(ps) > 20.0, ps
+
+
+@pytest.mark.parametrize("mode,seed,frac,aabb_scale", [("Depth", 3, 1.0, 1.0), ("Positions", 8, 0.3, 1.0), ("AO", 6, 0.3, 4.0),
+                                                        ("Depth", 5, 0.3, 8.0)])
+def test_render_modes_match_oracle(pkg, orc, mode, seed, frac, aabb_scale):
+    """ERenderMode AO, Positions and Depth (testbed_nerf.cu:1189-1208: each step's alpha, (pos - 0.5) / 2 + 0.5,
+    dot(camera forward, pos - origin) * depth_scale with depth_scale = 1 / dataset scale, :2822), composited like
+    Shade and shaded without sRGB decoding (:2183-2186). Same march and bars as the Shade comparison."""
+    cam, cfg, net, p16, bf, m = _setup(pkg, orc, seed, frac, aabb_scale)
+    r = pkg.nerf.NerfRenderer()
+    bg = (0.1, 0.2, 0.3, 1.0)
+    ds = 1.0 / 0.33  # nerf_synthetic's scale (nerf_loader.cu:388)
+    img = r.render(net, cfg, cam, torch.from_numpy(bf).cuda(), spp=1, min_transmittance=1e-4, background=bg,
+                   use_inference_params=False, render_mode=mode, depth_scale=ds).cpu().numpy()
+    ref, counts = orc.nerf_render(cfg, cam, m, p16, bf, min_transmittance=1e-4, bg=bg, render_mode=mode, depth_scale=ds)
+    assert (counts > 0).mean() > 0.2
+    assert np.isfinite(img).all()
+    scale = max(1.0, float(np.abs(ref).max()))  # depth values grow with the scene's size
+    d = np.abs(img - ref)
+    assert d.max() < 2e-2 * scale, (d.max(), scale)
+    assert d.mean() < 2e-3 * scale, d.mean()
+    if mode == "Positions":  # a hit pixel's colour is a weighted mean of positions inside the unit cube
+        hit = counts > 0
+        assert np.all(img.reshape(-1, 4)[hit, :3] > -0.5)

@@ -35,3 +35,11 @@ print(f"steps {n}: wall {sum(walls) / n:.1f} us, main-queue busy {sum(busy) / n:
 top = sorted(gaps.items(), key=lambda kv: -sum(kv[1]))[:12]
 for (p, q), v in top:
     print(f"  gap {sum(v) / n:6.1f} us/step ({len(v)}x, mean {sum(v) / len(v):.1f})  {p} -> {q}")
+# per-kernel device time per step over the same steps (all queues), largest first
+per = defaultdict(float)
+for a, b in list(zip(starts, starts[1:]))[-args.last:]:
+    for r in rows[a:b]:
+        per[(r["Queue_Id"], r["Kernel_Name"][:70])] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+print("per-kernel us/step (queue, kernel):")
+for (q, k), v in sorted(per.items(), key=lambda kv: -kv[1])[:25]:
+    print(f"  {v / n:7.1f}  q{q}  {k}")
