@@ -1107,8 +1107,14 @@ static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 }
 
 uint32_t nerf_mlp_train_blocks(uint32_t n) {
+	// NGP_MLP_TRAIN_BLOCKS: blocks per CU x 100 (experiment knob; default 100 = one block per CU)
+	static const uint32_t per_cu100 = [] {
+		const char* v = getenv("NGP_MLP_TRAIN_BLOCKS");
+		const int x = v ? atoi(v) : 100;
+		return (uint32_t)(x >= 25 && x <= 1600 ? x : 100);
+	}();
 	const uint32_t tiles = (n + 31) / 32;
-	return std::max<uint32_t>(1, std::min<uint32_t>(div_round_up(tiles, 4), device_cu_count()));
+	return std::max<uint32_t>(1, std::min<uint32_t>(div_round_up(tiles, 4), device_cu_count() * per_cu100 / 100));
 }
 
 template <int MODE>

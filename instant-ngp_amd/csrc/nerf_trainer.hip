@@ -781,12 +781,48 @@ int ngp_nerf_trainer_set_pipeline(ngp_nerf_trainer* t, int enable) {
 	});
 }
 
+// The pipelined sampler's stream. Experiment knobs (A/B): NGP_SAMPLER_PRIO / NGP_MAIN_PRIO -1 low,
+// 1 high (HSA queue priority: which queue's workgroups the dispatcher places first); NGP_SAMPLER_CU_KEEP k in 1..7:
+// the sampler's queue may use k of every 8 CUs (CU mask), so the training pass's one-block-per-CU MLP kernel
+// finds whole CUs free on the rest.
+static int env_prio(const char* name) {
+	const char* v = getenv(name);
+	if (!v || !*v) return 0;
+	const int p = atoi(v);
+	int least = 0, greatest = 0;
+	NGP_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+	return p < 0 ? least : (p > 0 ? greatest : 0);  // lower number = higher priority
+}
+static hipStream_t make_sampler_stream() {
+	hipStream_t s = nullptr;
+	const char* keep = getenv("NGP_SAMPLER_CU_KEEP");
+	const int k = keep ? atoi(keep) : 0;
+	if (k > 0 && k < 8) {
+		int dev = 0, n_cu = 0;
+		NGP_HIP(hipGetDevice(&dev));
+		NGP_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+		std::vector<uint32_t> mask((n_cu + 31) / 32, 0u);
+		for (int c = 0; c < n_cu; ++c)
+			if (c % 8 < k) mask[c / 32] |= 1u << (c % 32);
+		NGP_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+		return s;
+	}
+	const int prio = env_prio("NGP_SAMPLER_PRIO");
+	if (prio) NGP_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio));
+	else NGP_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+	return s;
+}
+
 int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_nerf_stats* st) {
 	if (!t) return NGP_INVALID;
 	NERF_TRY({
 		hipStream_t s = S(stream);
 		if (!s) {  // a private blocking stream (ordered after the null stream's earlier work)
-			if (!t->own_stream) NGP_HIP(hipStreamCreate(&t->own_stream));
+			if (!t->own_stream) {
+				const int prio = env_prio("NGP_MAIN_PRIO");
+				if (prio) NGP_HIP(hipStreamCreateWithPriority(&t->own_stream, hipStreamDefault, prio));
+				else NGP_HIP(hipStreamCreate(&t->own_stream));
+			}
 			s = t->own_stream;
 		}
 		const ngp_nerf_config& cfg = t->cfg;
@@ -865,7 +901,7 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		const bool can_pipeline = t->pipeline && (!dp || t->dp_capturable);
 		if (can_pipeline) {
 			if (!t->sample_stream) {
-				NGP_HIP(hipStreamCreateWithFlags(&t->sample_stream, hipStreamNonBlocking));
+				t->sample_stream = make_sampler_stream();
 				NGP_HIP(hipEventCreateWithFlags(&t->ev_free, hipEventDisableTiming));
 				NGP_HIP(hipEventCreateWithFlags(&t->ev_samp, hipEventDisableTiming));
 			}
