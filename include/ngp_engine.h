@@ -56,6 +56,11 @@ int ngp_stream_synchronize(void* stream);
 int ngp_profiler_enable(int enable);
 int ngp_profiler_reset(void);
 int ngp_profiler_read(char* json_buf, size_t len);
+/* Verification (engine extension): the device forms of the shared math (csrc/ngp_math.h) against the reference
+ * operations they replace, over the whole input range, on the GPU. which 0: ngp_div_2pf (the logf's f / (2 + f),
+ * reciprocal + Newton + residual step) against the IEEE quotient for all 2^23 reduced arguments. *mismatches =
+ * the number of inputs whose results differ in any bit (0 is the contract the sampler's bit-exactness rests on). */
+int ngp_debug_math_check(int which, void* stream, uint64_t* mismatches);
 
 /* ---- models (tcnn::Network<float, __half> surface) ------------------------------------------ */
 /* NerfNetwork ctor (nerf_network.h:81-112); JSON strings are the config sections the Testbed passes

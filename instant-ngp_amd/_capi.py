@@ -85,6 +85,7 @@ SIGNATURES = {
     "ngp_profiler_enable": (i32, [i32]),
     "ngp_profiler_reset": (i32, []),
     "ngp_profiler_read": (i32, [C.c_char_p, sz]),
+    "ngp_debug_math_check": (i32, [i32, P, C.POINTER(C.c_uint64)]),
     "ngp_nerf_network_create": (i32, [u32, u32, u32, u32, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(P)]),
     "ngp_network_with_input_encoding_create": (i32, [u32, u32, C.c_char_p, C.c_char_p, C.POINTER(P)]),
     "ngp_model_destroy": (None, [P]),

@@ -602,6 +602,35 @@ __device__ __forceinline__ unsigned long long sampler_clock() {
 #define SAMPLER_STAT(...)
 #endif
 
+// ngp_debug_math_check: the device forms of the shared math against their reference operations, over whole
+// input ranges. which 0: ngp_div_2pf(f) vs the IEEE f / (2 + f) for all 2^23 reduced logf arguments f.
+__global__ void k_check_div_2pf(unsigned long long* bad) {
+	const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+	if (m >= (1u << 23)) return;
+	const float f = __uint_as_float(m + 0x3f3504f3u) - 1.0f;
+	const float want = f / (2.0f + f);
+	if (__float_as_uint(ngp_div_2pf(f)) != __float_as_uint(want)) atomicAdd(bad, 1ull);
+}
+extern "C" __attribute__((visibility("default"))) int ngp_debug_math_check(int which, void* stream, uint64_t* mismatches) {
+	if (!mismatches || which != 0) return NGP_INVALID;
+	hipStream_t s = (hipStream_t)stream;
+	unsigned long long* d = nullptr;
+	if (hipMallocAsync((void**)&d, 8, s) != hipSuccess) return NGP_ERROR;
+	int rc = NGP_OK;
+	if (hipMemsetAsync(d, 0, 8, s) != hipSuccess) rc = NGP_ERROR;
+	if (rc == NGP_OK) {
+		k_check_div_2pf<<<(1u << 23) / 256, 256, 0, s>>>(d);
+		if (hipGetLastError() != hipSuccess) rc = NGP_ERROR;
+	}
+	unsigned long long h = 0;
+	if (rc == NGP_OK && hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, s) != hipSuccess) rc = NGP_ERROR;
+	if (hipStreamSynchronize(s) != hipSuccess) rc = NGP_ERROR;
+	hipFreeAsync(d, s);
+	hipStreamSynchronize(s);
+	*mismatches = h;
+	return rc;
+}
+
 // generate_training_samples_nerf pass 1: count the occupied steps of each ray, keep their t.
 template <bool CONE0>
 __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,

@@ -22,6 +22,10 @@
 
 #include <stdint.h>
 
+#ifndef NGP_LOGF_FASTDIV
+#define NGP_LOGF_FASTDIV 1  /* device: the logf's f / (2 + f) without the IEEE division sequence (ngp_div_2pf) */
+#endif
+
 #if defined(__HIPCC__)
 #define NGP_MATH_FN static __host__ __device__ __forceinline__
 #define NGP_FMAF(a, b, c) __builtin_fmaf((a), (b), (c))
@@ -99,6 +103,22 @@ NGP_MATH_FN float ngp_expf(float x) {
  *   Developed at SunPro, a Sun Microsystems, Inc. business.
  *   Permission to use, copy, modify, and distribute this software is freely granted,
  *   provided that this notice is preserved. */
+/* f / (2 + f) for the reduced argument of ngp_logf_core, f = m - 1 with m in [sqrt(2)/2, sqrt(2)) (2^23
+ * values): the IEEE quotient. On the device it is a reciprocal, one Newton step and one fused residual
+ * step (six dependent operations instead of the eleven of the IEEE division sequence), which equals the
+ * IEEE quotient for every one of those f: ngp_debug_math_check compares the two over the whole range on
+ * the GPU (tests/test_gpu_math.py). The host keeps the division. */
+NGP_MATH_FN float ngp_div_2pf(float f) {
+#if defined(__HIP_DEVICE_COMPILE__) && NGP_LOGF_FASTDIV
+	const float b = 2.0f + f;
+	float r = __builtin_amdgcn_rcpf(b);
+	r = NGP_FMAF(NGP_FMAF(-b, r, 1.0f), r, r);
+	const float q = f * r;
+	return NGP_FMAF(NGP_FMAF(-b, q, f), r, q);
+#else
+	return f / (2.0f + f);
+#endif
+}
 /* ln x for x = 2^(e0) m already reduced to ix = its bits (positive, normal) */
 NGP_MATH_FN float ngp_logf_core(uint32_t ix, int e);
 NGP_MATH_FN float ngp_logf(float x) {
@@ -124,7 +144,7 @@ NGP_MATH_FN float ngp_logf_core(uint32_t ix, int e) {
 	e += (int)(ix >> 23) - 127;
 	ix = (ix & 0x007fffffu) + 0x3f3504f3u;
 	const float f = ngp_math_u2f(ix) - 1.0f;
-	const float s = f / (2.0f + f);
+	const float s = ngp_div_2pf(f);
 	const float z = s * s, w = z * z;
 	const float t1 = w * NGP_FMAF(w, 0.24279078841f, 0.40000972152f);
 	const float t2 = z * NGP_FMAF(w, 0.28498786688f, 0.66666662693f);
