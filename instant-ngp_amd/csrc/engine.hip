@@ -1363,6 +1363,22 @@ int ngp::capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, co
 		*out = g.release();
 	});
 }
+void ngp::trainer_ctl_values(const ngp_trainer* t, uint32_t** ctl, uint32_t* step, uint32_t* cfg_off, uint32_t* cfg_words, uint32_t* cfg) {
+	static_assert(sizeof(AdamConfig) % 4 == 0 && sizeof(AdamConfig) <= 32 * 4, "AdamConfig as at most 32 words");
+	*ctl = t->ctl;
+	*step = t->step;
+	*cfg_off = CTL_CFG;
+	*cfg_words = sizeof(AdamConfig) / 4;
+	memcpy(cfg, &t->cfg, sizeof(AdamConfig));
+}
+void ngp::graph_launch_ctl_written(ngp_graph* g, void* stream) {
+	NGP_CHECK(g && g->exec, "graph launch: no graph");
+	NGP_CHECK(g->ws_epoch == g->trainer->model->ws_epoch, "graph launch: the model's workspaces were reallocated since capture");
+	NGP_HIP(hipGraphLaunch(g->exec, S(stream)));
+	g->trainer->step += g->steps_per_launch;
+	if (g->steps_per_launch && g->trainer->rec) g->trainer->inf_stale = g->trainer->w32_stale = true;
+}
+
 extern "C" {
 
 // The sharded optimizer's buffers for `world` ranks: the fp32 gradient staging of the reduce-scatter, sized

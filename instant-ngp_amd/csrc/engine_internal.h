@@ -26,6 +26,11 @@ int forward_backward_with(ngp_model* m, void* stream, uint32_t n, const float* i
 int capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride,
                                const void* dL_doutput, uint32_t dL_stride, float loss_scale, uint32_t n_steps, int with_optimizer,
                                const Exchange& ex, ngp_graph** out);
+// The values ngp_graph_launch writes into the trainer's device control block before a launch of its graph (set_device_ctl:
+// step at ctl[0], the AdamConfig at ctl + CTL_CFG), for a caller that writes them in a kernel of its own, and
+// the launch without that write (the rest of ngp_graph_launch: workspace check, step and staleness bookkeeping).
+void trainer_ctl_values(const ngp_trainer* t, uint32_t** ctl, uint32_t* step, uint32_t* cfg_off, uint32_t* cfg_words, uint32_t* cfg);
+void graph_launch_ctl_written(ngp_graph* g, void* stream);
 // One eager step of what capture_training_step_with records (the host-callback exchange of gloo ranks)
 int train_step_with(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride, const void* dL_doutput,
                     uint32_t dL_stride, float loss_scale, const Exchange& ex);

@@ -100,6 +100,15 @@ void fill_rollover_f16(uint32_t n_elements, uint32_t stride, const uint32_t* n_i
 void fill_rollover_f32(uint32_t n_elements, uint32_t stride, const uint32_t* n_input, float* data, hipStream_t s);
 void fill_rollover_pair(uint32_t n_elements, const uint32_t* n_input, f16* dloss, uint32_t stride16, float* coords,
                         uint32_t stride32, hipStream_t s);
+// What the single-GPU NeRF step does right after the rollover, in the same launch (block 0, thread 0): publish the
+// step's counters ctr[0..3] to host-mapped memory (then seq, after a system-scope fence), and write the optimizer
+// control block the training graph reads ({ctl[0] = step, ctl[CTL_CFG..] = cfg}, set_device_ctl). bytes: cfg.
+struct StepPublish {
+	const uint32_t* ctr; volatile uint32_t* host; uint32_t seq;
+	uint32_t* ctl; uint32_t step; uint32_t cfg_off, cfg_words; uint32_t cfg[32];  // cfg at ctl + cfg_off (words)
+};
+void fill_rollover_pair_publish(uint32_t n_elements, const uint32_t* n_input, f16* dloss, uint32_t stride16, float* coords,
+                                uint32_t stride32, const StepPublish& pub, hipStream_t s);
 void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_config& cfg, const float* grid_in,
                            uint32_t n_cascades, float thresh, float* positions, uint32_t* indices, hipStream_t s);
 void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t density_activation, float* grid_tmp,

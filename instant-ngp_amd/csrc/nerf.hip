@@ -1455,6 +1455,38 @@ __global__ void k_rollover_pair(uint32_t n_elements, uint32_t stride16, uint32_t
 		if (i >= n_in * stride32 && i < n_elements * stride32) d32[i] = d32[i % (n_in * stride32)];
 	}
 }
+// k_rollover_pair plus the step's publish and control-block writes (StepPublish): two launches less per NeRF step
+__global__ void k_rollover_pair_publish(uint32_t n_elements, uint32_t stride16, uint32_t stride32, const uint32_t* n_input_ptr, f16* d16,
+                                        float* d32, const StepPublish pub) {
+	if (blockIdx.x == 0 && threadIdx.x == 0) {
+		volatile uint32_t* host = pub.host;
+		host[0] = pub.ctr[0]; host[1] = pub.ctr[1]; host[2] = pub.ctr[2]; host[3] = pub.ctr[3];
+		__threadfence_system();
+		host[4] = pub.seq;
+		pub.ctl[0] = pub.step;
+		for (uint32_t k = 0; k < pub.cfg_words; ++k) pub.ctl[pub.cfg_off + k] = pub.cfg[k];
+	}
+	const uint32_t n_in = *n_input_ptr;
+	if (n_in == 0 || n_in >= n_elements) return;
+	const uint32_t lo = n_in * (stride16 < stride32 ? stride16 : stride32);
+	const uint32_t hi = n_elements * (stride16 > stride32 ? stride16 : stride32);
+	for (uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += gridDim.x * blockDim.x) {
+		if (i >= n_in * stride16 && i < n_elements * stride16) {
+			f16 r = d16[i % (n_in * stride16)];
+			r = (f16)((float)r * n_in / n_elements);
+			d16[i] = r;
+		}
+		if (i >= n_in * stride32 && i < n_elements * stride32) d32[i] = d32[i % (n_in * stride32)];
+	}
+}
+void fill_rollover_pair_publish(uint32_t n_elements, const uint32_t* n_input, f16* dloss, uint32_t stride16, float* coords,
+                                uint32_t stride32, const StepPublish& pub, hipStream_t s) {
+	NGP_CHECK(pub.host && pub.ctl && pub.cfg_words <= 32, "rollover publish: host counters, control block and config required");
+	const uint64_t n = (uint64_t)n_elements * (stride16 > stride32 ? stride16 : stride32);
+	const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(div_round_up(n, 256), 1024));
+	k_rollover_pair_publish<<<blocks, 256, 0, s>>>(n_elements, stride16, stride32, n_input, dloss, coords, pub);
+	NGP_HIP(hipGetLastError());
+}
 void fill_rollover_pair(uint32_t n_elements, const uint32_t* n_input, f16* dloss, uint32_t stride16, float* coords,
                         uint32_t stride32, hipStream_t s) {
 	const uint64_t n = (uint64_t)n_elements * (stride16 > stride32 ? stride16 : stride32);

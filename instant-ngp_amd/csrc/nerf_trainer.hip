@@ -591,14 +591,6 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	grid_mean_bitfield(grid, cfg.max_cascade, (float*)t->mean.p, (uint8_t*)t->bitfield.p, s);
 }
 
-__global__ void k_publish_counters(const uint32_t* __restrict__ ctr, volatile uint32_t* host, uint32_t seq) {
-	if (threadIdx.x == 0) {
-		host[0] = ctr[0]; host[1] = ctr[1]; host[2] = ctr[2]; host[3] = ctr[3];
-		__threadfence_system();
-		host[4] = seq;
-	}
-}
-
 // Data parallel: this shard's counters and loss as five floats for one all-reduce (sum). The u32
 // counters travel as 16-bit halves so their sums stay exact in fp32 for up to 256 ranks; the per-ray
 // losses are normalised by the shard's ray count (compute_loss), rescaled here to 1 / R_global.
@@ -631,7 +623,8 @@ __global__ void k_dp_publish(const float* __restrict__ red, const uint32_t* __re
 	}
 }
 
-// Wait until the step's k_publish_counters has run (or the stream failed / stalled for a minute).
+// Wait until the step's counters are published (k_rollover_pair_publish, or k_dp_publish; or the stream failed /
+// stalled for a minute).
 static void wait_published(volatile uint32_t* host, uint32_t seq, hipStream_t s) {
 	const auto t0 = std::chrono::steady_clock::now();
 	for (uint64_t spin = 0;; ++spin) {
@@ -872,7 +865,6 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		check_rc(nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, 4, ray_indices, rays, numsteps, coords, coords_c,
 		                               dloss, loss, ctr + 2, (const float*)t->mean.p, dp ? loss_scale_local : 128.0f, true,
 		                               error_map, t->em_w, t->em_h));
-		fill_rollover_pair(Bl, ctr + 2, dloss, 16, coords_c, 7, s);  // fill_rollover_and_rescale + fill_rollover
 		}
 		// the step's counters are final here (the training pass does not touch them): publish them before
 		// the training pass so the host can size the next step while it runs
@@ -881,6 +873,19 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			NGP_HIP(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
 			t->host_ctr = (volatile uint32_t*)p;
 			memset(p, 0, 64);
+		}
+		if (!dp) {
+			// single GPU: the rollover launch (fill_rollover_and_rescale + fill_rollover) also publishes the counters
+			// and writes the optimizer control block the training graph reads (a separate publish kernel and
+			// ngp_graph_launch's k_set_ctl before: two launches less per step)
+			StepPublish pub{};
+			pub.ctr = ctr;
+			pub.host = t->host_ctr;
+			pub.seq = ++t->publish_seq;
+			trainer_ctl_values(t->trainer, &pub.ctl, &pub.step, &pub.cfg_off, &pub.cfg_words, pub.cfg);
+			fill_rollover_pair_publish(Bl, ctr + 2, dloss, 16, coords_c, 7, pub, s);
+		} else {
+			fill_rollover_pair(Bl, ctr + 2, dloss, 16, coords_c, 7, s);  // fill_rollover_and_rescale + fill_rollover
 		}
 		if (dp) {
 			// NerfCounters::update_after_training on the global batch: this shard's counters and loss
@@ -892,8 +897,6 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			NGP_CHECK(t->allreduce(t->allreduce_user, d, 5, NGP_DTYPE_F32, NGP_REDUCE_SUM, s) == 0,
 			          "data parallel: counter all-reduce failed");
 			k_dp_publish<<<1, 64, 0, s>>>(d, ctr, t->host_ctr, ++t->publish_seq);
-		} else {
-			k_publish_counters<<<1, 64, 0, s>>>(ctr, t->host_ctr, ++t->publish_seq);
 		}
 		NGP_HIP(hipGetLastError());
 		// the next step's sampler may run under this step's training pass when the exchange is
@@ -926,7 +929,8 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 				t->graph_n = Bl;
 				t->graph_epoch = ngp_model_workspace_epoch(t->model);
 			}
-			check_rc(ngp_graph_launch(t->train_graph, s));
+			if (dp) check_rc(ngp_graph_launch(t->train_graph, s));
+			else graph_launch_ctl_written(t->train_graph, s);  // the control block was written by the rollover launch
 		} else {
 			// host-callback exchange (gloo): not capturable; the same step body, launched eagerly
 			check_rc(train_step_with(t->trainer, s, Bl, coords_c, 7, dloss, 16, 128.0f, t->exchange()));
