@@ -467,8 +467,11 @@ struct Marcher {
 	// Both errors grow like 1 / log(1 + cone) (= cone.rl): the margins scale with it, so a small cone
 	// (cone_angle_constant down to 1e-5) simply takes the exact path more often, never a wrong integer.
 	__device__ __forceinline__ float step_empty(float t, uint32_t* mip_out = nullptr) const {
+		return step_empty_n(t, to_stepping_space(t, k()), mip_out);
+	}
+	// step_empty given n = to(t) (the verify step has it for every candidate)
+	__device__ __forceinline__ float step_empty_n(float t, float n, uint32_t* mip_out = nullptr) const {
 		const V3 p = pos(t);
-		const float n = to_stepping_space(t, k());
 		uint32_t mip;
 		if (CONE0) {
 			mip = mip_at(0.0f, p);
@@ -515,9 +518,10 @@ struct Marcher {
 	// Either mode: the state after t and t's mip. occ: t + calc_dt(t) (calc_dt = from(n + 1)
 	// - t); empty: advance_to_next_voxel = from(n + empty_steps). One to() and one from() either way, so
 	// a wave whose rays are in different modes evaluates the two software transcendentals once.
-	__device__ __forceinline__ float step_any(float t, bool occ, uint32_t* mip_out) const {
+	__device__ __forceinline__ float step_any(float t, bool occ, uint32_t* mip_out, float* n_out = nullptr) const {
 		const V3 p = pos(t);
 		const float n = to_stepping_space(t, k());
+		if (n_out) *n_out = n;
 		uint32_t mip = CONE0 ? mip_at(0.0f, p) : 0u;
 		float c = 1.0f;
 		if (!occ) c = CONE0 ? empty_steps0(t, n, p, mip) : empty_steps(t, n, p, &mip);
@@ -625,8 +629,8 @@ extern "C" __attribute__((visibility("default"))) int ngp_debug_math_check(int w
 	unsigned long long h = 0;
 	if (rc == NGP_OK && hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, s) != hipSuccess) rc = NGP_ERROR;
 	if (hipStreamSynchronize(s) != hipSuccess) rc = NGP_ERROR;
-	hipFreeAsync(d, s);
-	hipStreamSynchronize(s);
+	(void)hipFreeAsync(d, s);
+	(void)hipStreamSynchronize(s);
 	*mismatches = h;
 	return rc;
 }
@@ -664,6 +668,8 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 #endif
 		float* tout = tbuf + (size_t)i * STEPS;
 		bool occ_mode = false;  // rays enter the aabb in empty space far more often than not
+		bool have_n0 = false;   // unified loop: n0_next = to(t) is known (the verify step computed it for the new state)
+		float n0_next = 0.f;
 		SAMPLER_STAT(ck2 = sampler_clock();)
 		SAMPLER_STAT(uint32_t st_e = 0; uint32_t st_o = 0; uint32_t st_r = 0; uint32_t st_x = 0; uint32_t st_q = 0;)
 		for (;;) {
@@ -672,6 +678,7 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			// the current mode (all occupied / all empty)
 			float tl, last;  // last: the state after lane nvalid-1's (the march continues there if every lane stays in the mode)
 			uint32_t mipl;   // the mip lane L's state is tested at
+			float nk = 0.f;  // unified loop: to(tl), from its verify step (reused when the ray leaves an occupied run at this lane)
 			uint32_t nvalid = RG;  // lanes holding verified states
 			if (CONE0 ? NGP_SAMPLER_UNIFIED0 : NGP_SAMPLER_EMPTY_SPEC) {
 				// Both modes in one guess-and-verify loop. Every state is from(n + c) with n =
@@ -683,7 +690,8 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				// predecessor and the lanes after it are re-guessed from there. The rays of a wave sit in
 				// different modes most of the time; sharing the loop (and its exact to()/from() per lane and
 				// round) means the wave no longer runs one mode's loop after the other's.
-				const float n0 = to_stepping_space(t, m.k());
+				const float n0 = have_n0 ? n0_next : to_stepping_space(t, m.k());
+				have_n0 = false;
 				const float c0 = occ_mode ? (float)L : m.guess_empty_steps(t, n0, L);
 				float cand = L == 0 ? t : from_stepping_space(n0 + c0, m.k());
 				SAMPLER_STAT(ck_q += sampler_clock() - cka;)
@@ -691,7 +699,7 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				float nxt, tcap = 0.0f;
 				for (;;) {
 					SAMPLER_STAT(if (occ_mode) ++st_r; else ++st_q;)
-					nxt = m.step_any(cand, occ_mode, &mk);
+					nxt = m.step_any(cand, occ_mode, &mk, &nk);
 					const float expct = dpp_shr1(nxt);
 					const uint32_t v = __builtin_ctz(row_ballot(L >= v0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
 					if (v >= RG) break;
@@ -774,8 +782,18 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			}
 			if (!((row_ballot(inside) >> f) & 1u)) break;  // left the aabb / sampling range / step budget
 			const float tf = __shfl(tl, (int)f, (int)RG);
-			if (occ_mode) t = m.step_empty(tf);  // empty cell at lane f: advance_to_next_voxel
-			else t = tf;                          // occupied cell at lane f: sample it next
+			if (occ_mode) {  // empty cell at lane f: advance_to_next_voxel
+				// cone stepping: lane f's to() from its verify step (at cone 0 to() is a multiply, cheaper than the shuffle)
+				if (!CONE0 && NGP_SAMPLER_EMPTY_SPEC) t = m.step_empty_n(tf, __shfl(nk, (int)f, (int)RG));
+				else t = m.step_empty(tf);
+			}
+			else {  // occupied cell at lane f: sample it next
+				t = tf;
+				if (!CONE0 && NGP_SAMPLER_EMPTY_SPEC) {
+					n0_next = __shfl(nk, (int)f, (int)RG);
+					have_n0 = true;
+				}
+			}
 			SAMPLER_STAT(st_x += occ_mode ? 0u : 1u;)
 			occ_mode = !occ_mode;
 		}
