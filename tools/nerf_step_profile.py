@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--option", action="append", default=[], help="model option key=value (ngp_model_set_option)")
     ap.add_argument("--fox", action="store_true", help="the fox capture (data/fox, tools/stage_fox.sh) instead of the stand-in")
     ap.add_argument("--profiler", type=int, default=1, help="0: no engine HIP-event profiler in the measured steps (wall time only)")
+    ap.add_argument("--env-after-warmup", action="append", default=[],
+                    help="KEY=VALUE set in the environment after the warm-up steps (engine timing switches read per step)")
     ap.add_argument("--sampler-stats", action="store_true",
                     help="read the march statistics of a -DNGP_SAMPLER_DIAG=4 build (NGP_ENGINE_LIB) over the measured steps")
     args = ap.parse_args()
@@ -57,6 +59,9 @@ def main():
             print(f"step {i} {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t_warm = time.time() - t0
+    for kv in args.env_after_warmup:
+        key, value = kv.split("=", 1)
+        os.environ[key] = value
     lib.ngp_profiler_reset()
     lib.ngp_profiler_enable(args.profiler)
     if args.sampler_stats:
