@@ -28,6 +28,7 @@ import argparse
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -126,7 +127,12 @@ def newest_profile(suffix):
     return max(files, key=key) if files else None
 
 
-def pmc_traffic(variant, region):
+# the bucketed backward's store mode (grid_scatter.h: 0 fp16 gradient, 1 fused optimizer update, 2 fp32 gradient)
+# is the second template argument of k_sc_accumulate / k_sc_split_reduce: ...ILj<F>ELj<MODE>E...
+_SC_MODE = re.compile(r"k_sc_(?:accumulate|split_reduce)ILj\d+ELj(\d+)E")
+
+
+def pmc_traffic(variant, region, sc_mode=None):
     """Bytes per launch of `region` that left L2 for the fabric (Infinity Cache + HBM), from the newest
     committed rocprofv3 summary profiles/<round>_pmc_<variant>.json (tools/pmc_summary.py: reads =
     32/64/128 x TCC_EA0_RDREQ_{32B,64B,128B}, writes = WRITE_SIZE; calibrated against known-byte kernels
@@ -138,6 +144,9 @@ def pmc_traffic(variant, region):
     tot, hit = 0.0, False
     for name, v in summ.items():
         compact = name.replace(" ", "")
+        m = _SC_MODE.search(compact)
+        if m and sc_mode is not None and int(m.group(1)) != sc_mode:
+            continue  # another store mode's instantiation (a different path than the one timed)
         if any(k.replace(" ", "") in compact for k in REGION_KERNELS[region]) and "fabric_bytes" in v:
             tot += v["fabric_bytes"]
             hit = True
@@ -348,6 +357,7 @@ def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped, slab_bytes=0, fu
         if all(p in per for p in phases):
             per[region] = sum(per[p] for p in phases)
     fused_b = 0
+    sc_mode = 1 if "grid_backward_adam" in per else 0  # the timed step's bucketed-backward store mode
     if "grid_backward_adam" in per and "grid_bwd_prepare" in per:
         per["grid_backward_total"] = per["grid_bwd_prepare"] + per["grid_backward_adam"]
         fused_b = OPT_B_FUSED * (fused_grid_updated or 0)
@@ -373,7 +383,7 @@ def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped, slab_bytes=0, fu
                 e.update({"achieved_incl_fused_update": round(wf / (ms / 1e3), 1),
                           "frac_incl_fused_update": round(wf / (ms / 1e3) / pk, 4)})
             if b == "hbm":
-                traffic, src = pmc_traffic(variant, k)
+                traffic, src = pmc_traffic(variant, k, sc_mode)
                 if traffic is not None:
                     # what actually left L2 for the fabric per launch, and its rate
                     e["fabric_MB"] = round(traffic / 1e6, 2)
@@ -400,7 +410,7 @@ def roofline(variant, n, kernels, n_opt_updated, n_opt_skipped, slab_bytes=0, fu
     dom = max(cands, key=lambda k: per[k])
     bound, work, peak, unit = roof[dom]
     achieved = work / (per[dom] / 1e3)
-    traffic, src = pmc_traffic(variant, dom)
+    traffic, src = pmc_traffic(variant, dom, sc_mode)
     rl = {"kernel": dom, "bound": bound, "achieved": round(achieved, 1), "peak": peak, "unit": unit,
           "frac": round(achieved / peak, 4), "traffic": None if traffic is None else round(traffic / 1e6, 2),
           "traffic_unit": "MB/launch leaving L2 for the fabric (Infinity Cache + HBM; rocprofv3 sized read requests "
@@ -707,7 +717,8 @@ def main():
             if e2e_dp is not None:
                 res["e2e"] = {k: e2e_dp[k] for k in ("value", "unit", "psnr", "psnr_views", "train_seconds", "steps",
                                                      "ms_per_step", "n_gpus", "data", "config")}
-        if world == 1 and args.variant in ("C2", "C2p") and not args.no_dp1 and args.comm == "rccl":
+        if world == 1 and args.variant in ("C2", "C2p") and not args.no_dp1 and not args.pmc_collect and args.comm == "rccl":
+            # (not in counter-collection runs: their summaries describe the headline step's kernels alone)
             # the data-parallel step's own cost, measured where it can be (one GPU): the same pass with the
             # engine's RCCL communicator attached at world 1, timed like the headline (one graph of K steps),
             # sharded (reduce-scatter + slice update + all-gather) and all-reduce, against the fused N = 1 step
