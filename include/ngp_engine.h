@@ -352,6 +352,16 @@ int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg
 /* The same with the training error map (testbed_nerf.cu:1869-1899, the kernel's error_map argument): every
  * compacted ray adds its mean loss, split bilinearly around uv * res - 0.5, into error_map
  * [n_images][em_height][em_width] (device floats, float atomics as in the reference). */
+/* Engine extension: ngp_nerf_compute_loss with pass 1 keeping each composited sample's state (weight, transmittance
+ * after it, rgb prefix through it) in sample_state ([5][state_capacity] floats, indexed like the samples: state_capacity
+ * at least the sample buffer's length) for pass 2, which then does not composite each ray again. The same float
+ * operations: outputs equal ngp_nerf_compute_loss's bit for bit. The training step uses this form. */
+int ngp_nerf_compute_loss_state(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
+                                uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
+                                const void* network_output, const uint32_t* ray_indices, const float* rays, uint32_t* numsteps,
+                                const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
+                                uint32_t* compacted_counter, const float* mean_density, float loss_scale, float* sample_state,
+                                uint64_t state_capacity);
 int ngp_nerf_compute_loss_error_map(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
                                     uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted,
                                     const uint32_t* ray_counter, const void* network_output, const uint32_t* ray_indices,

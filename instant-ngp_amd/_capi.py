@@ -157,6 +157,8 @@ SIGNATURES = {
                                     f32]),
     "ngp_nerf_compute_loss_error_map": (i32, [P, C.POINTER(NerfConfig), P, u32, u32, Rng, u32, P, P, P, P, P, P, P, P,
                                               P, P, P, f32, P, u32, u32]),
+    "ngp_nerf_compute_loss_state": (i32, [P, C.POINTER(NerfConfig), P, u32, u32, Rng, u32, P, P, P, P, P, P, P, P, P, P, P,
+                                          f32, P, C.c_uint64]),
     "ngp_nerf_fill_rollover": (i32, [P, u32, u32, P, P, i32, i32]),
     "ngp_nerf_grid_generate_samples": (i32, [P, C.POINTER(NerfConfig), u32, Rng, u32, P, u32, f32, P, P]),
     "ngp_nerf_grid_splat_max": (i32, [P, u32, P, P, u32, P]),

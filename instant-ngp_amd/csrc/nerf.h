@@ -89,6 +89,11 @@ struct LossArgs {
 	// split, into [n_images][em_h][em_w] floats; null: off
 	float* error_map;
 	uint32_t em_w, em_h;
+	// optional (null: off): pass 1 stores, per sample it composites, the weight, the transmittance after it and
+	// the rgb prefix through it ([5][state_cap] floats, indexed by the pre-compaction sample), and pass 2 reads
+	// them instead of compositing each ray again. Same float operations, so the same bits either way.
+	float* state;
+	uint64_t state_cap;
 };
 
 // The kernels (each cites its reference kernel in nerf.hip).

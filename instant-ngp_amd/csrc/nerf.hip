@@ -1141,6 +1141,7 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 	float rr = 0.f, rg = 0.f, rb = 0.f;
 	uint32_t cn = 0;
 	bool stop = false;
+	const bool keep_state = NGP_LOSS_SELECT && a.state != nullptr;
 	// software pipelining: the loads of the next NGP_LOSS_PF chunks are in flight while a chunk's
 	// compositing chain runs (the chunk loop is unrolled by the depth, so every buffer keeps its registers)
 	f16x4 ob[NGP_LOSS_PF];
@@ -1189,6 +1190,7 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 			const float nt = t * (1.f - ak);                                                           \
 			rr = upd ? nr : rr; rg = upd ? ng : rg; rb = upd ? nb : rb; t = upd ? nt : t;              \
 			cn += upd ? 1u : 0u;                                                                       \
+			if (keep_state && L == K) { sw = weight; sT = nt; sr = nr; sg = ng; sb = nb; su = upd; }   \
 		}
 #else
 #define NGP_LOSS1_STEP(K)                                                                              \
@@ -1205,8 +1207,15 @@ __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ c
 			}                                                                                          \
 		}
 #endif
+		float sw = 0.f, sT = 0.f, sr = 0.f, sg = 0.f, sb = 0.f;
+		bool su = false;
 		NGP_ROW_UNROLL16(NGP_LOSS1_STEP)
 #undef NGP_LOSS1_STEP
+		if (keep_state && su && (size_t)base + jj < a.state_cap) {  // composited: pass 2 reads its state instead of compositing again
+			const size_t si = (size_t)base + jj;
+			a.state[si] = sw; a.state[a.state_cap + si] = sT;
+			a.state[2 * a.state_cap + si] = sr; a.state[3 * a.state_cap + si] = sg; a.state[4 * a.state_cap + si] = sb;
+		}
 	}
 	// channel ch of the target, the background and the loss (every lane of the row holds rr, rg, rb, t, cn)
 	float texc, tex3;
@@ -1290,6 +1299,47 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const Camera* __restrict__ c
 	const float* ci = a.coords_in + (size_t)base * 7;
 	float* co = a.coords_out + (size_t)compacted_base * 7;
 	f16* dl = a.dloss_doutput + (size_t)compacted_base * 16;
+	// the gradient of compacted sample jj (cc its coordinates, o its network output, its weight my_w, the
+	// transmittance after it my_t and the rgb prefix through it my_r2), written with its coordinates
+	auto emit = [&](uint32_t jj, const float (&cc)[7], const f16x4& o, const float (&rgb)[3], float dt, float my_w, float my_t,
+	                const float (&my_r2)[3]) __attribute__((always_inline)) {
+#pragma unroll
+		for (int k = 0; k < 7; ++k) co[(size_t)jj * 7 + k] = cc[k];
+		const V3 pos = unwarp_pos(cc, box);
+		const float ddx = pos.x - ro0, ddy = pos.y - ro1, ddz = pos.z - ro2;
+		const float depth = sqrtf(ddx * ddx + ddy * ddy + ddz * ddz);
+		float suffix[3];
+		for (int k = 0; k < 3; ++k) suffix[k] = q.rgb_ray[k] - my_r2[k];
+		f16x4 g;
+		for (int k = 0; k < 3; ++k) {
+			const float dloss_by_drgb = my_w * q.grad[k];
+			g[k] = (f16)(loss_scale * (dloss_by_drgb * network_to_rgb_derivative((float)o[k], cfg.rgb_activation) +
+			                           fmaxf(0.0f, output_l2_reg * (float)o[k])));
+		}
+		const float density_derivative = network_to_density_derivative((float)o[3], cfg.density_activation);
+		const float dotv = q.grad[0] * (my_t * rgb[0] - suffix[0]) + q.grad[1] * (my_t * rgb[1] - suffix[1]) +
+		                   q.grad[2] * (my_t * rgb[2] - suffix[2]);
+		const float dloss_by_dmlp = density_derivative * (dt * (dotv + 0.0f));
+		const float o3 = (float)o[3];
+		g[3] = (f16)(loss_scale * dloss_by_dmlp + (o3 < 0.0f ? -output_l1_reg_density : 0.0f) +
+		             (o3 > -10.0f && depth < cfg.near_distance ? 1e-4f : 0.0f));
+		*(f16x4*)(dl + (size_t)jj * 16) = g;
+	};
+	if (a.state) {  // pass 1 kept every composited sample's state: no sequential compositing here
+		for (uint32_t jj = L; jj < cn; jj += LG) {
+			float cc[7];
+#pragma unroll
+			for (int k = 0; k < 7; ++k) cc[k] = ci[(size_t)jj * 7 + k];
+			const f16x4 o = *(const f16x4*)(out + (size_t)jj * a.out_stride);
+			const size_t si = (size_t)base + jj;
+			const float my_w = a.state[si], my_t = a.state[a.state_cap + si];
+			const float my_r2[3] = {a.state[2 * a.state_cap + si], a.state[3 * a.state_cap + si], a.state[4 * a.state_cap + si]};
+			float rgb[3];
+			for (int k = 0; k < 3; ++k) rgb[k] = network_to_rgb((float)o[k], cfg.rgb_activation);
+			emit(jj, cc, o, rgb, unwarp_dt(cc[3]), my_w, my_t, my_r2);
+		}
+		return;
+	}
 	float r2[3] = {0.f, 0.f, 0.f};
 	float t = 1.0f;
 	// software pipelining as in pass 1: NGP_LOSS2_PF chunks' loads in flight ahead of the compositing
@@ -1348,27 +1398,7 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const Camera* __restrict__ c
 		t = row_bcast<15>(t);  // a next chunk exists only if this one is full: lane 15 then took all 16 samples
 		r2[0] = row_bcast<15>(r2[0]); r2[1] = row_bcast<15>(r2[1]); r2[2] = row_bcast<15>(r2[2]);
 		if (!valid) continue;
-#pragma unroll
-		for (int k = 0; k < 7; ++k) co[(size_t)jj * 7 + k] = cc[k];
-		const V3 pos = unwarp_pos(cc, box);
-		const float ddx = pos.x - ro0, ddy = pos.y - ro1, ddz = pos.z - ro2;
-		const float depth = sqrtf(ddx * ddx + ddy * ddy + ddz * ddz);
-		float suffix[3];
-		for (int k = 0; k < 3; ++k) suffix[k] = q.rgb_ray[k] - my_r2[k];
-		f16x4 g;
-		for (int k = 0; k < 3; ++k) {
-			const float dloss_by_drgb = my_w * q.grad[k];
-			g[k] = (f16)(loss_scale * (dloss_by_drgb * network_to_rgb_derivative((float)o[k], cfg.rgb_activation) +
-			                           fmaxf(0.0f, output_l2_reg * (float)o[k])));
-		}
-		const float density_derivative = network_to_density_derivative((float)o[3], cfg.density_activation);
-		const float dotv = q.grad[0] * (my_t * rgb[0] - suffix[0]) + q.grad[1] * (my_t * rgb[1] - suffix[1]) +
-		                   q.grad[2] * (my_t * rgb[2] - suffix[2]);
-		const float dloss_by_dmlp = density_derivative * (dt * (dotv + 0.0f));
-		const float o3 = (float)o[3];
-		g[3] = (f16)(loss_scale * dloss_by_dmlp + (o3 < 0.0f ? -output_l1_reg_density : 0.0f) +
-		             (o3 > -10.0f && depth < cfg.near_distance ? 1e-4f : 0.0f));
-		*(f16x4*)(dl + (size_t)jj * 16) = g;
+		emit(jj, cc, o, rgb, dt, my_w, my_t, my_r2);
 	}
 }
 

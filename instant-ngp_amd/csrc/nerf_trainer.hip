@@ -154,6 +154,7 @@ struct ngp_nerf_trainer {
 	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens;
 	// training workspaces
 	Buf ray_indices, rays, numsteps, coords, mlp_out, dloss, coords_c, loss, counters, scan_tmp, tmp_u32, tmp_f32;
+	Buf loss_state;  // compute_loss: pass 1's per-sample compositing state for pass 2 (LossArgs::state)
 	// training error map (Testbed::Nerf::Training::ErrorMap and its update window, testbed.h:668-677, 736-738)
 	Buf em_data, em_cdf_x, em_cdf_y, em_cdf_img;
 	uint32_t em_w = 0, em_h = 0, em_cdf_w = 0, em_cdf_h = 0;
@@ -321,7 +322,8 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
                              const void* network_output, uint32_t out_stride, const uint32_t* ray_indices, const float* rays,
                              uint32_t* numsteps, const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
                              uint32_t* compacted_counter, const float* mean_density, float loss_scale, bool zero_loss = false,
-                             float* error_map = nullptr, uint32_t em_w = 0, uint32_t em_h = 0);
+                             float* error_map = nullptr, uint32_t em_w = 0, uint32_t em_h = 0, float* state = nullptr,
+                             uint64_t state_cap = 0);
 
 int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
                           uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
@@ -345,12 +347,24 @@ int ngp_nerf_compute_loss_error_map(const ngp_nerf_dataset* ds, const ngp_nerf_c
 	                         loss_scale, false, error_map, em_width, em_height);
 }
 
+int ngp_nerf_compute_loss_state(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
+                                uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
+                                const void* network_output, const uint32_t* ray_indices, const float* rays, uint32_t* numsteps,
+                                const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
+                                uint32_t* compacted_counter, const float* mean_density, float loss_scale, float* sample_state,
+                                uint64_t state_capacity) {
+	if (!sample_state || state_capacity == 0) return NGP_INVALID;
+	return nerf_compute_loss(ds, cfg, stream, n_rays, n_rays_total, rng, max_samples_compacted, ray_counter, network_output, 16,
+	                         ray_indices, rays, numsteps, coords_in, coords_out, dloss_doutput, loss, compacted_counter, mean_density,
+	                         loss_scale, false, nullptr, 0, 0, sample_state, state_capacity);
+}
+
 static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
                              uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
                              const void* network_output, uint32_t out_stride, const uint32_t* ray_indices, const float* rays,
                              uint32_t* numsteps, const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
                              uint32_t* compacted_counter, const float* mean_density, float loss_scale, bool zero_loss,
-                             float* error_map, uint32_t em_w, uint32_t em_h) {
+                             float* error_map, uint32_t em_w, uint32_t em_h, float* state, uint64_t state_cap) {
 	if (!ds || !cfg || !ray_counter || !network_output || !numsteps || !coords_in || !coords_out || !dloss_doutput ||
 	    !compacted_counter || !mean_density)
 		return NGP_INVALID;
@@ -363,6 +377,7 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
 		a.dloss_doutput = (f16*)dloss_doutput; a.loss = loss; a.compacted_counter = compacted_counter;
 		a.mean_density = mean_density; a.loss_scale = loss_scale; a.zero_loss = zero_loss;
 		a.error_map = error_map; a.em_w = em_w; a.em_h = em_h;
+		a.state = state; a.state_cap = state ? state_cap : 0;
 		if (n_rays == 0) { NGP_HIP(hipMemsetAsync(compacted_counter, 0, 4, S(stream))); return NGP_OK; }
 		static thread_local Buf scan, tmp, tmpf;
 		const size_t sb = scan_temp_bytes(n_rays);
@@ -862,9 +877,12 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		float* error_map = error_map_window(t, s);
 		{
 		ProfScope ps("nerf_loss", s);
+		// pass 1 keeps each composited sample's state for pass 2 (indexed like the sampler's samples, at most max_samples)
+		static const bool keep_state = !getenv("NGP_LOSS_STATE") || atoi(getenv("NGP_LOSS_STATE")) != 0;  // A/B knob
+		float* lstate = keep_state ? t->loss_state.get<float>((size_t)5 * sp.max_samples) : nullptr;
 		check_rc(nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, 4, ray_indices, rays, numsteps, coords, coords_c,
 		                               dloss, loss, ctr + 2, (const float*)t->mean.p, dp ? loss_scale_local : 128.0f, true,
-		                               error_map, t->em_w, t->em_h));
+		                               error_map, t->em_w, t->em_h, lstate, sp.max_samples));
 		}
 		// the step's counters are final here (the training pass does not touch them): publish them before
 		// the training pass so the host can size the next step while it runs

@@ -135,10 +135,12 @@ def generate_training_samples(ds, cfg, n_rays, rng, max_samples, bitfield, ray_o
 
 
 def compute_loss(ds, cfg, n_rays, rng, max_compacted, samples, network_output, mean_density, loss_scale=128.0,
-                 n_rays_total=None, stream=None, error_map=None):
+                 n_rays_total=None, stream=None, error_map=None, keep_state=False):
     """compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012). `samples` is the dict returned by
     generate_training_samples (its numsteps is rewritten to the compacted {n, base}). error_map: a
-    float32 device tensor [n_images, h, w] the compacted rays' losses are added into (:1869-1899)."""
+    float32 device tensor [n_images, h, w] the compacted rays' losses are added into (:1869-1899).
+    keep_state: pass 1 keeps each composited sample's state for pass 2 (ngp_nerf_compute_loss_state, the
+    training step's form; same outputs bit for bit)."""
     dev = network_output.device
     # the kernel reads one output row per sample; samples never exceed the sampler's coords buffer
     if network_output.shape[0] < samples["coords"].shape[0]:
@@ -154,7 +156,13 @@ def compute_loss(ds, cfg, n_rays, rng, max_compacted, samples, network_output, m
             _ptr(samples["counters"]), _ptr(network_output), _ptr(samples["ray_indices"]), _ptr(samples["rays"]),
             _ptr(samples["numsteps"]), _ptr(samples["coords"]), _ptr(out["coords_compacted"]), _ptr(out["dloss_doutput"]),
             _ptr(out["loss"]), _ptr(out["compacted_counter"]), _ptr(mean_density), float(loss_scale))
-    if error_map is None:
+    if keep_state:
+        if error_map is not None:
+            raise ValueError("keep_state: without error_map (the C-ABI form has no error-map argument)")
+        cap = samples["coords"].shape[0]
+        state = torch.empty((5, cap), dtype=torch.float32, device=dev)
+        check(lib().ngp_nerf_compute_loss_state(*args, _ptr(state), cap))
+    elif error_map is None:
         check(lib().ngp_nerf_compute_loss(*args))
     else:
         if error_map.dtype != torch.float32 or error_map.dim() != 3 or not error_map.is_contiguous():

@@ -221,6 +221,32 @@ def test_compute_loss(pkg, orc, scene, loss_type, act, aabb_scale):
     assert not bad.any(), (int(bad.sum()), dl_got[bad][:5], dl_ref[bad][:5])
 
 
+@pytest.mark.parametrize("loss_type,act,aabb_scale", [(4, 3, 1.0), (0, 2, 4.0)])
+def test_compute_loss_kept_state_is_bitwise_equal(pkg, scene, orc, loss_type, act, aabb_scale):
+    """The training step's form of the loss (pass 1 keeps each composited sample's weight, transmittance and
+    rgb prefix; pass 2 reads them instead of compositing each ray again) gives the same bits as the two
+    compositing passes: compacted count, {n, base}, coordinates, losses and dL/doutput."""
+    ds, ims, pix = scene
+    cfg = pkg.nerf.default_config(aabb_scale, loss_type=loss_type, rgb_activation=act, density_activation=3)
+    _, bf = occupancy(orc, seed=3, frac=0.5, max_cascade=cfg.max_cascade)
+    n_rays, max_samples, max_c = 2000, 1 << 17, 1 << 15
+    r = rng(pkg, 11)
+    g = np.random.default_rng(loss_type + 7)
+    out_t = torch.from_numpy(g.uniform(-3.0, 2.0, (max_samples, 16)).astype(np.float16)).cuda()
+    mean = torch.tensor([0.003], device="cuda")
+    res = []
+    for keep in (False, True):
+        samples = pkg.nerf.generate_training_samples(ds, cfg, n_rays, r, max_samples, torch.from_numpy(bf).cuda())
+        got = pkg.nerf.compute_loss(ds, cfg, n_rays, r, max_c, samples, out_t, mean, keep_state=keep)
+        torch.cuda.synchronize()
+        res.append({"ns": samples["numsteps"].cpu().numpy(), **{k: v.cpu().numpy() for k, v in got.items()}})
+    a, b = res
+    assert int(a["compacted_counter"][0]) > 0
+    for k in ("ns", "compacted_counter", "coords_compacted", "loss"):
+        np.testing.assert_array_equal(a[k].view(np.uint32), b[k].view(np.uint32), err_msg=k)
+    np.testing.assert_array_equal(a["dloss_doutput"].view(np.uint16), b["dloss_doutput"].view(np.uint16))
+
+
 @pytest.mark.parametrize("dtype,rescale", [(torch.float32, False), (torch.float16, False), (torch.float16, True)])
 def test_fill_rollover(pkg, orc, dtype, rescale):
     g = np.random.default_rng(1)
