@@ -175,6 +175,7 @@ struct ngp_model {
 	bool fuse_slabs = true;                 // option "fuse_slabs": dW slab reduction inside the grid backward's last kernel
 	bool fuse_opt = true;                   // option "fuse_opt": lazy-layout optimizer update inside the grid backward (training_step)
 	bool fuse_mlp_opt = true;               // option "fuse_mlp_opt": ... and the MLP section's update in its dW slab blocks (no optimizer launch)
+	bool mlp_pipe = false;                  // option "mlp_pipe": the training MLP software-pipelined across tiles (k_nerf_mlp_train_pipe)
 	bool mlp_train16 = false;               // option "mlp_train16": the training MLP at two waves per SIMD (mlp_train16.hip; off: no faster at C2, 3x slower at C2p)
 	bool grid_stage0 = false;               // option "grid_stage0": the training forward stages level 0 in LDS (grid.hip STAGE0; off: measured slower)
 	bool grid_bricks = false;               // option "grid_bricks": dense levels of the bucketed backward summed per brick (off: measured slower)
@@ -371,6 +372,7 @@ struct ngp_model {
 			if (ex) { a.dL_ddens = ex->ddens; a.ddens_stride = ex->ddens_stride; }
 			a.params = pick(inference);
 			a.train16 = mlp_train16 ? 1u : 0u;
+			a.pipe = mlp_pipe ? 1u : 0u;
 			if (mode == MLP_INFER_ENC || mode == MLP_TRAIN_ENC) {
 				if (inference) sync_inference(s);
 				a.table = pick(inference) + grid_offset(); a.max_level = max_level; a.gc = make_grid_const(grid);
@@ -854,6 +856,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			m->fuse_infer = value != 0;
 		} else if (k == "fuse_train") {
 			m->fuse_train = value != 0;
+		} else if (k == "mlp_pipe") {
+			m->mlp_pipe = value != 0;
 		} else if (k == "mlp_train16") {
 			m->mlp_train16 = value != 0;
 		} else if (k == "fuse_slabs") {

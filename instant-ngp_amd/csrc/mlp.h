@@ -66,6 +66,8 @@ struct NerfMlpArgs {
 	// whether MLP_TRAIN may run k_nerf_mlp_train16 (model option "mlp_train16")
 	const f16* params;
 	uint32_t train16;
+	// whether MLP_TRAIN runs the software-pipelined k_nerf_mlp_train_pipe (model option "mlp_pipe")
+	uint32_t pipe;
 };
 
 struct MlpArgs {  // single MLP behind an encoding (tcnn::NetworkWithInputEncoding): image / SDF

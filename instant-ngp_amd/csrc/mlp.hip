@@ -144,19 +144,40 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // two fp32 -> packed fp16, round to nearest even (v_cvt_pk_f16_f32 on gfx950)
 __device__ __forceinline__ f16x2 cvt2(float a, float b) { return __builtin_convertvector(f32x2{a, b}, f16x2); }
-// ReLU on a packed pair (v_pk_max_f16)
-__device__ __forceinline__ f16x2 relu2(f16x2 x) { return __builtin_elementwise_max(x, f16x2{(f16)0.f, (f16)0.f}); }
+#ifndef NGP_RELU_INT
+#define NGP_RELU_INT 1
+#endif
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+// ReLU on a packed pair. NGP_RELU_INT: as a signed 16-bit max (v_pk_max_i16): a negative half, -0
+// included, has its sign bit set and becomes +0; a non-negative one orders like its integer bits.
+// Equal to max(x, 0) for every non-NaN x, and never yields -0, so the backward mask needs no sign
+// clear. (A NaN with the sign bit clear passes through instead of becoming 0.)
+__device__ __forceinline__ f16x2 relu2(f16x2 x) {
+#if NGP_RELU_INT
+	return __builtin_bit_cast(f16x2, __builtin_elementwise_max(__builtin_bit_cast(s16x2, x), s16x2{0, 0}));
+#else
+	return __builtin_elementwise_max(x, f16x2{(f16)0.f, (f16)0.f});
+#endif
+}
 // backward ReLU: g where the (already ReLU'd, so >= 0) activation is nonzero, else 0, on packed bits:
-// (a & 0x7fff) min 1 is 1 or 0 per half, times g's bits (v_pk_min_u16 + v_pk_mul_lo_u16). Keeps no
-// per-element lane masks alive between the forward and the backward pass.
+// a min 1 is 1 or 0 per half, times g's bits (v_pk_min_u16 + v_pk_mul_lo_u16). Keeps no per-element
+// lane masks alive between the forward and the backward pass.
 __device__ __forceinline__ uint32_t relu_mask_bits(uint32_t a, uint32_t g) {
 	// written out: the compiler otherwise turns the idiom back into per-half compares and selects
 	uint32_t t, r;
+#if NGP_RELU_INT
+	asm("v_pk_min_u16 %0, %2, %3\n\t"
+	    "v_pk_mul_lo_u16 %1, %4, %0"
+	    : "=&v"(t), "=v"(r)
+	    : "v"(a), "v"(0x00010001u), "v"(g));
+#else
+	// v_pk_max_f16 may return -0 for a -0 input: clear the sign first
 	asm("v_and_b32 %0, 0x7fff7fff, %2\n\t"
 	    "v_pk_min_u16 %0, %0, %3\n\t"
 	    "v_pk_mul_lo_u16 %1, %4, %0"
 	    : "=&v"(t), "=v"(r)
 	    : "v"(a), "v"(0x00010001u), "v"(g));
+#endif
 	return r;
 }
 __device__ __forceinline__ f16x8 cat4(f16x2 a, f16x2 b, f16x2 c, f16x2 d) {
@@ -211,6 +232,43 @@ __device__ __forceinline__ void img_store_acc(f16* img, int stride, const f16x8*
 		const int base = 32 * (q >> 1) + 16 * (q & 1);
 		*(f16x4*)(row + base) = f16x4{f[q][0], f[q][1], f[q][2], f[q][3]};
 		*(f16x4*)(row + base + 8) = f16x4{f[q][4], f[q][5], f[q][6], f[q][7]};
+	}
+}
+
+// k_nerf_mlp_train_pipe variants (experiment knobs): NGP_PIPE_FENCE, a scheduling fence between its
+// pairs of layers (no instruction moves across it); NGP_PIPE_RELOAD, the backward reads the tile's
+// activations back from its image instead of keeping them in registers
+#ifndef NGP_PIPE_FENCE
+#define NGP_PIPE_FENCE 1
+#endif
+#ifndef NGP_PIPE_RELOAD
+#define NGP_PIPE_RELOAD 1
+#endif
+#if NGP_PIPE_FENCE
+#define NGP_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define NGP_SCHED_FENCE() do {} while (0)
+#endif
+#if NGP_PIPE_RELOAD
+#define NGP_PIPE_ACT(act, reg, im) img_load_acc<4>(im, Lay::S_64, act, lane)
+#else
+#define NGP_PIPE_ACT(act, reg, im) do { for (int q_ = 0; q_ < 4; ++q_) act[q_] = reg[q_]; } while (0)
+#endif
+
+// Read back what img_store_acc wrote: the packed accumulator-layout fragments of one sample column.
+// The address is laundered so the compiler cannot forward the stored registers (which would keep them
+// live: the point of reading back is to free them).
+template <int NFRAG>
+__device__ __forceinline__ void img_load_acc(const f16* img, int stride, f16x8* f, int lane) {
+	const int smp = lane & 31, h = lane >> 5;
+	int idx = smp * stride + 4 * h;
+	asm volatile("" : "+v"(idx));
+	const f16* row = img + idx;
+#pragma unroll
+	for (int q = 0; q < NFRAG; ++q) {
+		const int base = 32 * (q >> 1) + 16 * (q & 1);
+		const f16x4 lo = *(const f16x4*)(row + base), hi = *(const f16x4*)(row + base + 8);
+		f[q] = f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 	}
 }
 
@@ -782,6 +840,82 @@ struct PhaseBOps {
 	f16x8 d0_a, d0_b[ES];
 };
 
+// Phase B: this wave's quarter of dW over the block's four images (NerfTrainLayout W_*), between the
+// two barriers of an iteration.
+// DB: the next image's operands are requested before this image's MFMAs (two operand sets live)
+template <int ES, int DH, int RH, bool DB = true>
+__device__ __forceinline__ void train_phase_b(f32x4* dw, const f16* img_all, int wave, int lane) {
+	using Lay = NerfLayout<ES, DH, RH>;
+	using T = NerfTrainLayout<ES, DH, RH>;
+	// The operands of image w + 1 (28 ds_read_b64_tr_b16) are requested before image w's 9 MFMA tiles,
+	// which lets the scheduler keep more reads in flight (30.9 -> 30.5 us at C2; pinning that order
+	// with sched_barrier measured 31.4 us: at most 15 LDS reads can be outstanding per wave). Same
+	// products in the same order as dw_part: the gradients are unchanged bit for bit.
+	PhaseBOps<ES, DH, RH> ops[DB ? 2 : 1];
+	auto load_ops = [&](int w, PhaseBOps<ES, DH, RH>& o) {
+		const f16* im = img_all + w * T::IMG_HALVES;
+		o.ro_a = img_frag(im + T::I_ZRO, T::S_16, 0, lane);
+		o.ro_b = img_frag(im + T::I_HR + (RH - 1) * 32 * Lay::S_64, Lay::S_64, 16 * wave, lane);
+#pragma unroll
+		for (int j = 0; j < RH - 1; ++j) {
+			o.rh_a[j] = img_frag(im + T::I_ZRH + j * 32 * Lay::S_64, Lay::S_64, 16 * wave, lane);
+#pragma unroll
+			for (int n = 0; n < 4; ++n) o.rh_b[j][n] = img_frag(im + T::I_HR + (RH - 2 - j) * 32 * Lay::S_64, Lay::S_64, 16 * n, lane);
+		}
+		o.r0_a = img_frag(im + T::I_ZR0, Lay::S_64, 16 * wave, lane);
+#pragma unroll
+		for (int n = 0; n < 2; ++n) o.r0_b[n] = img_frag(im + T::I_RIN, Lay::S_RIN, 16 * n, lane);
+		o.do_a = img_frag(im + T::I_ZDO, T::S_16, 0, lane);
+		o.do_b = img_frag(im + T::I_HD + (DH - 1) * 32 * Lay::S_64, Lay::S_64, 16 * wave, lane);
+#pragma unroll
+		for (int j = 0; j < DH - 1; ++j) {
+			o.dh_a[j] = img_frag(im + T::I_ZDH + j * 32 * Lay::S_64, Lay::S_64, 16 * wave, lane);
+#pragma unroll
+			for (int n = 0; n < 4; ++n) o.dh_b[j][n] = img_frag(im + T::I_HD + (DH - 2 - j) * 32 * Lay::S_64, Lay::S_64, 16 * n, lane);
+		}
+		o.d0_a = img_frag(im + T::I_ZD0, Lay::S_64, 16 * wave, lane);
+#pragma unroll
+		for (int n = 0; n < ES; ++n) o.d0_b[n] = img_frag(im + T::I_XE, Lay::S_XE, 16 * n, lane);
+	};
+	if (DB) load_ops(0, ops[0]);
+#pragma unroll
+	for (int w = 0; w < 4; ++w) {
+		if (!DB) load_ops(w, ops[0]);
+		else if (w < 3) load_ops(w + 1, ops[(w + 1) & (DB ? 1 : 0)]);
+		const PhaseBOps<ES, DH, RH>& o = ops[w & (DB ? 1 : 0)];
+		dw[T::W_RO] = mfma16(o.ro_a, o.ro_b, dw[T::W_RO]);
+#pragma unroll
+		for (int j = 0; j < RH - 1; ++j)
+#pragma unroll
+			for (int n = 0; n < 4; ++n) dw[T::W_RH + 4 * j + n] = mfma16(o.rh_a[j], o.rh_b[j][n], dw[T::W_RH + 4 * j + n]);
+#pragma unroll
+		for (int n = 0; n < 2; ++n) dw[T::W_R0 + n] = mfma16(o.r0_a, o.r0_b[n], dw[T::W_R0 + n]);
+		dw[T::W_DO] = mfma16(o.do_a, o.do_b, dw[T::W_DO]);
+#pragma unroll
+		for (int j = 0; j < DH - 1; ++j)
+#pragma unroll
+			for (int n = 0; n < 4; ++n) dw[T::W_DH + 4 * j + n] = mfma16(o.dh_a[j], o.dh_b[j][n], dw[T::W_DH + 4 * j + n]);
+#pragma unroll
+		for (int n = 0; n < ES; ++n) dw[T::W_D0 + n] = mfma16(o.d0_a, o.d0_b[n], dw[T::W_D0 + n]);
+	}
+}
+
+// this wave's dW tiles -> the block's slab (parameter-slice layout; the waves' tiles are disjoint)
+template <int ES, int DH, int RH>
+__device__ __forceinline__ void train_store_dw(const f32x4* dw, const NerfMlpArgs& a, int wave, int lane) {
+	using T = NerfTrainLayout<ES, DH, RH>;
+	float* slab = a.dw_slab + (size_t)blockIdx.x * a.n_matrix;
+	const uint32_t dw0 = a.density_woff, rw0 = a.rgb_woff;
+	dw_store<1, 1>(dw + T::W_RO, slab, rw0 + 64 * 32 + 64 * 64 * (RH - 1), 64, 0, wave, lane);
+#pragma unroll
+	for (int j = 0; j < RH - 1; ++j) dw_store<1, 4>(dw + T::W_RH + 4 * j, slab, rw0 + 64 * 32 + 64 * 64 * (RH - 2 - j), 64, wave, 0, lane);
+	dw_store<1, 2>(dw + T::W_R0, slab, rw0, 32, wave, 0, lane);
+	dw_store<1, 1>(dw + T::W_DO, slab, dw0 + 64 * 16 * ES + 64 * 64 * (DH - 1), 64, 0, wave, lane);
+#pragma unroll
+	for (int j = 0; j < DH - 1; ++j) dw_store<1, 4>(dw + T::W_DH + 4 * j, slab, dw0 + 64 * 16 * ES + 64 * 64 * (DH - 2 - j), 64, wave, 0, lane);
+	dw_store<1, ES>(dw + T::W_D0, slab, dw0, 16 * ES, wave, 0, lane);
+}
+
 template <int ES, int DH, int RH, bool FUSE>
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_nerf_mlp_train(const NerfMlpArgs a) {
 	static_assert(!FUSE || ES == 1, "fused encoding: one 16-wide encoding step");
@@ -1010,70 +1144,272 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		__syncthreads();
 
 		// ---- phase B: this wave's quarter of dW over the four images ---------------------------
-		// The operands of image w + 1 (28 ds_read_b64_tr_b16) are requested before image w's 9 MFMA tiles,
-		// which lets the scheduler keep more reads in flight (30.9 -> 30.5 us at C2; pinning that order
-		// with sched_barrier measured 31.4 us: at most 15 LDS reads can be outstanding per wave). Same
-		// products in the same order as dw_part: the gradients are unchanged bit for bit.
-		PhaseBOps<ES, DH, RH> ops[2];
-		auto load_ops = [&](int w, PhaseBOps<ES, DH, RH>& o) {
-			const f16* im = img_all + w * T::IMG_HALVES;
-			o.ro_a = img_frag(im + T::I_ZRO, T::S_16, 0, lane);
-			o.ro_b = img_frag(im + T::I_HR + (RH - 1) * 32 * Lay::S_64, Lay::S_64, 16 * wave, lane);
-#pragma unroll
-			for (int j = 0; j < RH - 1; ++j) {
-				o.rh_a[j] = img_frag(im + T::I_ZRH + j * 32 * Lay::S_64, Lay::S_64, 16 * wave, lane);
-#pragma unroll
-				for (int n = 0; n < 4; ++n) o.rh_b[j][n] = img_frag(im + T::I_HR + (RH - 2 - j) * 32 * Lay::S_64, Lay::S_64, 16 * n, lane);
-			}
-			o.r0_a = img_frag(im + T::I_ZR0, Lay::S_64, 16 * wave, lane);
-#pragma unroll
-			for (int n = 0; n < 2; ++n) o.r0_b[n] = img_frag(im + T::I_RIN, Lay::S_RIN, 16 * n, lane);
-			o.do_a = img_frag(im + T::I_ZDO, T::S_16, 0, lane);
-			o.do_b = img_frag(im + T::I_HD + (DH - 1) * 32 * Lay::S_64, Lay::S_64, 16 * wave, lane);
-#pragma unroll
-			for (int j = 0; j < DH - 1; ++j) {
-				o.dh_a[j] = img_frag(im + T::I_ZDH + j * 32 * Lay::S_64, Lay::S_64, 16 * wave, lane);
-#pragma unroll
-				for (int n = 0; n < 4; ++n) o.dh_b[j][n] = img_frag(im + T::I_HD + (DH - 2 - j) * 32 * Lay::S_64, Lay::S_64, 16 * n, lane);
-			}
-			o.d0_a = img_frag(im + T::I_ZD0, Lay::S_64, 16 * wave, lane);
-#pragma unroll
-			for (int n = 0; n < ES; ++n) o.d0_b[n] = img_frag(im + T::I_XE, Lay::S_XE, 16 * n, lane);
-		};
-		load_ops(0, ops[0]);
-#pragma unroll
-		for (int w = 0; w < 4; ++w) {
-			if (w < 3) load_ops(w + 1, ops[(w + 1) & 1]);
-			const PhaseBOps<ES, DH, RH>& o = ops[w & 1];
-			dw[T::W_RO] = mfma16(o.ro_a, o.ro_b, dw[T::W_RO]);
-#pragma unroll
-			for (int j = 0; j < RH - 1; ++j)
-#pragma unroll
-				for (int n = 0; n < 4; ++n) dw[T::W_RH + 4 * j + n] = mfma16(o.rh_a[j], o.rh_b[j][n], dw[T::W_RH + 4 * j + n]);
-#pragma unroll
-			for (int n = 0; n < 2; ++n) dw[T::W_R0 + n] = mfma16(o.r0_a, o.r0_b[n], dw[T::W_R0 + n]);
-			dw[T::W_DO] = mfma16(o.do_a, o.do_b, dw[T::W_DO]);
-#pragma unroll
-			for (int j = 0; j < DH - 1; ++j)
-#pragma unroll
-				for (int n = 0; n < 4; ++n) dw[T::W_DH + 4 * j + n] = mfma16(o.dh_a[j], o.dh_b[j][n], dw[T::W_DH + 4 * j + n]);
-#pragma unroll
-			for (int n = 0; n < ES; ++n) dw[T::W_D0 + n] = mfma16(o.d0_a, o.d0_b[n], dw[T::W_D0 + n]);
-		}
+		train_phase_b<ES, DH, RH>(dw, img_all, wave, lane);
 		__syncthreads();
 	}
+	train_store_dw<ES, DH, RH>(dw, a, wave, lane);
+}
 
-	// this wave's dW tiles -> the block's slab (parameter-slice layout; the waves' tiles are disjoint)
-	float* slab = a.dw_slab + (size_t)blockIdx.x * a.n_matrix;
-	const uint32_t dw0 = a.density_woff, rw0 = a.rgb_woff;
-	dw_store<1, 1>(dw + T::W_RO, slab, rw0 + 64 * 32 + 64 * 64 * (RH - 1), 64, 0, wave, lane);
+// ------------------------------------------------------------------------------------------------
+// The same training pass, software-pipelined across tiles (option mlp_pipe, NGP_MLP_PIPE)
+// ------------------------------------------------------------------------------------------------
+// In k_nerf_mlp_train a wave's phase A is one dependent chain (layer MFMAs -> fp16 pack -> next
+// layer) at one wave per SIMD, so every MFMA result latency and every pack sits on the critical path.
+// Here phase A of iteration i runs the backward dX chain of tile i and the forward chain of the wave's
+// next tile, i + 1, as two independent chains written layer by layer in alternation, so one chain's
+// packs issue while the other's MFMAs run. Tile i + 1's forward activations stay in registers until
+// the next iteration stores them to the (then free) image. Per tile the operations and the image
+// contents are those of k_nerf_mlp_train, and phase B is the same function: dW, dL/dinput and the
+// outputs are bit-identical.
+template <int ES, int DH, int RH>
+struct TrainTileFwd {
+	f16x8 xe[ES];      // encoding (B-operand order)
+	f16x8 hd[DH][4];   // density hidden activations
+	f16x8 dout;        // density network output rows 0..15 (rgb input rows 0..15)
+	f16x8 sh;          // SH encoding (rgb input rows 16..31)
+	f16x8 hr[RH][4];   // rgb hidden activations
+	f16x4 dl;          // dL/d(output) of the tile's sample
+};
+
+template <int ES, int DH, int RH>
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_nerf_mlp_train_pipe(const NerfMlpArgs a) {
+	using Lay = NerfLayout<ES, DH, RH>;
+	using T = NerfTrainLayout<ES, DH, RH>;
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	const int lane = threadIdx.x & 63, h = lane >> 5;
+	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	f16* img_all = (f16*)smem;
+	f16* img = img_all + wave * T::IMG_HALVES;
+
+	f16x8 wreg[Lay::N_FWD], breg[T::N_BWD];
 #pragma unroll
-	for (int j = 0; j < RH - 1; ++j) dw_store<1, 4>(dw + T::W_RH + 4 * j, slab, rw0 + 64 * 32 + 64 * 64 * (RH - 2 - j), 64, wave, 0, lane);
-	dw_store<1, 2>(dw + T::W_R0, slab, rw0, 32, wave, 0, lane);
-	dw_store<1, 1>(dw + T::W_DO, slab, dw0 + 64 * 16 * ES + 64 * 64 * (DH - 1), 64, 0, wave, lane);
+	for (int q = 0; q < Lay::N_FWD; ++q) wreg[q] = a.frags[q * 64 + lane];
 #pragma unroll
-	for (int j = 0; j < DH - 1; ++j) dw_store<1, 4>(dw + T::W_DH + 4 * j, slab, dw0 + 64 * 16 * ES + 64 * 64 * (DH - 2 - j), 64, wave, 0, lane);
-	dw_store<1, ES>(dw + T::W_D0, slab, dw0, 16 * ES, wave, 0, lane);
+	for (int q = 0; q < T::N_BWD; ++q) breg[q] = a.frags[(Lay::N_FWD + q) * 64 + lane];
+#pragma unroll
+	for (int q = 0; q < Lay::N_FWD; ++q) asm volatile("" : "+a"(wreg[q]));
+#pragma unroll
+	for (int q = 0; q < T::N_BWD; ++q) asm volatile("" : "+a"(breg[q]));
+	f32x4 dw[T::N_DW];
+#pragma unroll
+	for (int q = 0; q < T::N_DW; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+	const uint32_t n_tiles = (a.n + 31) / 32;
+	const uint32_t stride = gridDim.x * 4;
+	f16x8 xe_n[ES];
+	float cd_n[3];
+	f16x4 dl_n;
+	f16x8 sh_n;  // SH encoding of the prefetched tile, computed once its directions arrive (make_sh)
+	auto load_inputs = [&](uint32_t tile) {
+		const uint32_t smp = tile * 32 + (lane & 31);
+		const uint32_t ls = smp < a.n ? smp : 0;
+#pragma unroll
+		for (int s = 0; s < ES; ++s) xe_n[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
+		const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
+		cd_n[0] = cd[0]; cd_n[1] = cd[1]; cd_n[2] = cd[2];
+		dl_n = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
+	};
+	// forward layer steps of one tile (each a layer's MFMAs and its pack), called in alternation with
+	// the backward steps of the previous tile
+	// sh4_frag branches on the lane half; it runs outside phase A so that phase A stays one region
+	auto make_sh = [&](uint32_t tile) {
+		sh_n = tile * 32 + (lane & 31) < a.n ? sh4_frag(cd_n[0], cd_n[1], cd_n[2], h) : f16x8{};
+	};
+	auto take_inputs = [&](TrainTileFwd<ES, DH, RH>& f, uint32_t tile) {
+		const bool valid = tile * 32 + (lane & 31) < a.n;
+#pragma unroll
+		for (int s = 0; s < ES; ++s) f.xe[s] = valid ? xe_n[s] : f16x8{};
+		f.sh = sh_n;
+		f.dl = dl_n;
+	};
+	auto fwd_d0 = [&](TrainTileFwd<ES, DH, RH>& f) {
+		f32x16 acc[2];
+		layer_fwd_reg<2, ES>(acc, f.xe, wreg, Lay::F_D0);
+		pack_tiles<2>(acc, f.hd[0], true);
+	};
+	auto fwd_dh = [&](TrainTileFwd<ES, DH, RH>& f, int l) {
+		f32x16 acc[2];
+		layer_fwd_reg<2, 4>(acc, f.hd[l - 1], wreg, Lay::F_DH + 8 * (l - 1));
+		pack_tiles<2>(acc, f.hd[l], true);
+	};
+	auto fwd_do = [&](TrainTileFwd<ES, DH, RH>& f) {
+		f32x16 dacc[1];
+		layer_fwd_reg<1, 4>(dacc, f.hd[DH - 1], wreg, Lay::F_DO);
+		f16x8 hi;
+		pack_tile(dacc[0], f.dout, hi, false);
+	};
+	auto fwd_r0 = [&](TrainTileFwd<ES, DH, RH>& f) {
+		f32x16 acc[2];
+		const f16x8 rin[2] = {f.dout, f.sh};
+		layer_fwd_reg<2, 2>(acc, rin, wreg, Lay::F_R0);
+		pack_tiles<2>(acc, f.hr[0], true);
+	};
+	auto fwd_rh = [&](TrainTileFwd<ES, DH, RH>& f, int l) {
+		f32x16 acc[2];
+		layer_fwd_reg<2, 4>(acc, f.hr[l - 1], wreg, Lay::F_RH + 8 * (l - 1));
+		pack_tiles<2>(acc, f.hr[l], true);
+	};
+	// the rgb output rows 0..15 with the density in row 3 (extract_density, nerf_network.h:32-43)
+	auto fwd_ro = [&](TrainTileFwd<ES, DH, RH>& f) {
+		f32x16 racc[1];
+		layer_fwd_reg<1, 4>(racc, f.hr[RH - 1], wreg, Lay::F_RO);
+		f16x8 ro, ro_hi;
+		pack_tile(racc[0], ro, ro_hi, false);
+		ro[3] = h == 0 ? f.dout[0] : ro[3];
+		return ro;
+	};
+
+	TrainTileFwd<ES, DH, RH> t_a, t_b;
+	{
+		TrainTileFwd<ES, DH, RH>& cur = t_a;
+		// prologue: the wave's first tile's forward, and the inputs of its second tile requested
+		const uint32_t t0 = blockIdx.x * 4 + wave;
+		load_inputs(t0);
+		make_sh(t0);
+		take_inputs(cur, t0);
+		load_inputs(t0 + stride);
+		fwd_d0(cur);
+#pragma unroll
+		for (int l = 1; l < DH; ++l) fwd_dh(cur, l);
+		fwd_do(cur);
+		fwd_r0(cur);
+#pragma unroll
+		for (int l = 1; l < RH; ++l) fwd_rh(cur, l);
+		const f16x8 ro = fwd_ro(cur);
+		const uint32_t s0 = t0 * 32 + (lane & 31);
+		if (a.out && s0 < a.n) store_out16(a.out, a.out_stride, a.out_layout, a.n, s0, h, ro);
+		make_sh(t0 + stride);
+	}
+	// one iteration: tile `base + wave` (forward done, in `cur`) and the next tile's forward into `nxt`.
+	// Every wave runs the same number of iterations (the barriers need all four); tiles past the end
+	// run on zero inputs and zero output gradients, so their dW contribution is exactly zero.
+	// Phase A has no branch (its global stores wait until the end), so the two chains form one
+	// scheduling region; the backward reads the tile's activations back from its image (conflict-free
+	// ds_read_b64) instead of keeping them in registers.
+	auto step = [&](TrainTileFwd<ES, DH, RH>& cur, TrainTileFwd<ES, DH, RH>& nxt, uint32_t base) {
+		const uint32_t tile = base + wave, ntile = tile + stride;
+		const uint32_t sample = tile * 32 + (lane & 31), nsample = ntile * 32 + (lane & 31);
+		const bool valid = sample < a.n;
+
+		// ---- tile's forward images (its activations were computed last iteration) ------------------
+#pragma unroll
+		for (int s = 0; s < ES; ++s) img_store_std(img + T::I_XE, Lay::S_XE, cur.xe[s], s, lane);
+#pragma unroll
+		for (int l = 0; l < DH; ++l) img_store_acc<4>(img + T::I_HD + l * 32 * Lay::S_64, Lay::S_64, cur.hd[l], lane);
+		{
+			f16x8 d1[1] = {cur.dout};
+			img_store_acc<1>(img + T::I_RIN, Lay::S_RIN, d1, lane);
+			img_store_std(img + T::I_RIN, Lay::S_RIN, cur.sh, 1, lane);
+		}
+#pragma unroll
+		for (int l = 0; l < RH; ++l) img_store_acc<4>(img + T::I_HR + l * 32 * Lay::S_64, Lay::S_64, cur.hr[l], lane);
+		const f16x4 dl_cur = valid ? cur.dl : f16x4{};
+
+		// the next tile's inputs (requested last iteration), and the one after requested now
+		take_inputs(nxt, ntile);
+		load_inputs(ntile + stride);  // unconditional (past-the-end tiles read sample 0)
+
+		// ---- phase A: tile's backward dX chain || next tile's forward chain -------------------------
+		// sched_barrier between the pairs of layers: the scheduler interleaves the two chains within a
+		// pair but does not hoist later loads and MFMAs, which would raise the register pressure past the
+		// file (spills)
+		f32x16 acc[2];
+		f16x8 dz[4], act[4];
+		const float dsig = (float)dl_cur[3];
+		NGP_SCHED_FENCE();
+		{
+			f16x8 dz1[1];
+			dz1[0] = h == 0 ? f16x8{dl_cur[0], dl_cur[1], dl_cur[2], (f16)0.f, 0, 0, 0, 0} : f16x8{};  // extract_rgb (:46-60)
+			img_store_acc<1>(img + T::I_ZRO, T::S_16, dz1, lane);
+			NGP_PIPE_ACT(act, cur.hr[RH - 1], img + T::I_HR + (RH - 1) * 32 * Lay::S_64);
+			layer_fwd_reg<2, 1>(acc, dz1, breg, Lay::B_RO - Lay::N_FWD);
+			mask_pack<2>(acc, act, dz);
+		}
+		fwd_d0(nxt);
+		NGP_SCHED_FENCE();
+#pragma unroll
+		for (int l = RH - 1; l >= 1; --l) {
+			img_store_acc<4>(img + T::I_ZRH + (RH - 1 - l) * 32 * Lay::S_64, Lay::S_64, dz, lane);
+			NGP_PIPE_ACT(act, cur.hr[l - 1], img + T::I_HR + (l - 1) * 32 * Lay::S_64);
+			layer_fwd_reg<2, 4>(acc, dz, breg, Lay::B_RH - Lay::N_FWD + 8 * (RH - 1 - l));
+			mask_pack<2>(acc, act, dz);
+			if (RH - 1 - l + 1 < DH) fwd_dh(nxt, RH - 1 - l + 1);
+			NGP_SCHED_FENCE();
+		}
+#pragma unroll
+		for (int l = RH; l < DH; ++l) fwd_dh(nxt, l);
+		f16x8 dd[1], dsh;
+		{
+			img_store_acc<4>(img + T::I_ZR0, Lay::S_64, dz, lane);
+			f32x16 a1[1];
+			layer_fwd_reg<1, 4>(a1, dz, breg, Lay::B_R0 - Lay::N_FWD);
+			pack_tile(a1[0], dd[0], dsh, false);  // dsh: rows 16..31 of dL/d(rgb input) = dL/d(SH encoding)
+			dd[0][0] = h == 0 ? (f16)((float)dd[0][0] + dsig) : dd[0][0];  // add_density_gradient (:63-74)
+			img_store_acc<1>(img + T::I_ZDO, T::S_16, dd, lane);
+		}
+		fwd_do(nxt);
+		NGP_SCHED_FENCE();
+		NGP_PIPE_ACT(act, cur.hd[DH - 1], img + T::I_HD + (DH - 1) * 32 * Lay::S_64);
+		layer_fwd_reg<2, 1>(acc, dd, breg, Lay::B_DO - Lay::N_FWD);
+		mask_pack<2>(acc, act, dz);
+		fwd_r0(nxt);
+		NGP_SCHED_FENCE();
+#pragma unroll
+		for (int l = DH - 1; l >= 1; --l) {
+			img_store_acc<4>(img + T::I_ZDH + (DH - 1 - l) * 32 * Lay::S_64, Lay::S_64, dz, lane);
+			NGP_PIPE_ACT(act, cur.hd[l - 1], img + T::I_HD + (l - 1) * 32 * Lay::S_64);
+			layer_fwd_reg<2, 4>(acc, dz, breg, Lay::B_DH - Lay::N_FWD + 8 * (DH - 1 - l));
+			mask_pack<2>(acc, act, dz);
+			if (DH - l < RH) fwd_rh(nxt, DH - l);
+			NGP_SCHED_FENCE();
+		}
+#pragma unroll
+		for (int l = DH; l < RH; ++l) {
+			fwd_rh(nxt, l);
+			NGP_SCHED_FENCE();
+		}
+		img_store_acc<4>(img + T::I_ZD0, Lay::S_64, dz, lane);
+		f16x8 de[2 * Lay::ET];  // dL/d(encoding): tile t's rows in de[2t] (lo) and de[2t + 1] (hi)
+		{
+			f32x16 ae[Lay::ET];
+			layer_fwd_reg<Lay::ET, 4>(ae, dz, breg, Lay::B_D0 - Lay::N_FWD);
+#pragma unroll
+			for (int t = 0; t < Lay::ET; ++t) pack_tile(ae[t], de[2 * t], de[2 * t + 1], false);
+		}
+		const f16x8 ro = fwd_ro(nxt);
+		NGP_SCHED_FENCE();
+
+		// ---- global stores of phase A; the SH of the tile after next ----------------------------------
+		make_sh(ntile + stride);
+		if (a.out && nsample < a.n) store_out16(a.out, a.out_stride, a.out_layout, a.n, nsample, h, ro);
+		if (a.dL_dsh && valid) store_dsh(a.dL_dsh, sample, h, dsh);
+		if (a.dL_denc && valid) {
+#pragma unroll
+			for (int t = 0; t < Lay::ET; ++t) {
+				f16* row = a.dL_denc + (size_t)sample * a.denc_stride + 32 * t + 4 * h;
+				const f16x8 lo = de[2 * t], hi = de[2 * t + 1];
+				*(f16x4*)(row + 0) = f16x4{lo[0], lo[1], lo[2], lo[3]};
+				*(f16x4*)(row + 8) = f16x4{lo[4], lo[5], lo[6], lo[7]};
+				if (32 * t + 16 < 16 * ES) {
+					*(f16x4*)(row + 16) = f16x4{hi[0], hi[1], hi[2], hi[3]};
+					*(f16x4*)(row + 24) = f16x4{hi[4], hi[5], hi[6], hi[7]};
+				}
+			}
+		}
+		__syncthreads();
+
+		// ---- phase B: this wave's quarter of dW over the four images (one operand set: the next tile's
+		// forward record is live across it) ---------------------------------------------------------------
+		train_phase_b<ES, DH, RH, false>(dw, img_all, wave, lane);
+		__syncthreads();
+	};
+	// (the record copy is free: the register allocator coalesces it; unrolling by two with the roles
+	// swapped instead measured 145 more live registers and spills)
+	for (uint32_t base = blockIdx.x * 4; base < n_tiles; base += stride) {
+		step(t_a, t_b, base);
+		t_a = t_b;
+	}
+	train_store_dw<ES, DH, RH>(dw, a, wave, lane);
 }
 
 template <int ES, int DH, int RH, int MODE>
@@ -1091,7 +1427,8 @@ static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	if (blocks == 0) return;
 	if constexpr (TRAIN && MODE != MLP_DENSITY_TRAIN && NerfTrainLayout<ES, DH, RH>::LDS_BYTES <= 160 * 1024 && Lay::N_ALL <= 44) {
 		// weight gradients split across the waves, all fragments in registers (k_nerf_mlp_train)
-		auto kt = k_nerf_mlp_train<ES, DH, RH, MODE == MLP_TRAIN_ENC>;
+		void (*kt)(const NerfMlpArgs) = k_nerf_mlp_train<ES, DH, RH, MODE == MLP_TRAIN_ENC>;
+		if (MODE == MLP_TRAIN && a.pipe) kt = k_nerf_mlp_train_pipe<ES, DH, RH>;
 		const size_t lt = NerfTrainLayout<ES, DH, RH>::LDS_BYTES;
 		ensure_dynamic_lds((const void*)kt, lt);
 		kt<<<blocks, 256, lt, s>>>(a);
