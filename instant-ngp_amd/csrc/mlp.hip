@@ -397,6 +397,40 @@ __device__ __forceinline__ void store_dsh(f16* dsh_out, uint32_t sample, int h, 
 	*(f16x4*)(row + 8) = f16x4{v[4], v[5], v[6], v[7]};
 }
 
+// The fused-encoding paths' gather of one level's 8 corners (F = 4) given the cell's base corner: the
+// integers of corner_index (grid.h; tcnn grid_index), dense and hashed indices both formed and selected so
+// the two lane halves (different levels) do not diverge. A dense index is reduced with min(id, id - T),
+// which is id % T for id < 2 T (every in-range cell); a lane with a larger one (a position far outside
+// [0, 1]) takes the modulo in a branch that is almost never entered. The loads are unconditional (the
+// index is in the level's table either way) and an inactive level's values are zeroed afterwards, so
+// the 8 loads issue back to back.
+__device__ __forceinline__ void fuse_gather_level(const f16* tab, const uint32_t (&base)[3], uint32_t res, uint32_t T, bool hashed,
+                                                  bool active, f16x4 (&g)[8]) {
+	uint32_t idx[8];
+	bool wrap = false;
+#pragma unroll
+	for (uint32_t k = 0; k < 8; ++k) {
+		const uint32_t cx = base[0] + (k & 1u), cy = base[1] + ((k >> 1) & 1u), cz = base[2] + ((k >> 2) & 1u);
+		const uint32_t ih = (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (T - 1u);
+		const uint32_t id = cx + res * (cy + res * cz);
+		const uint32_t im = min(id, id - T);
+		wrap |= !hashed && im >= T;
+		idx[k] = hashed ? ih : im;
+	}
+	if (__builtin_expect(wrap, 0)) {
+#pragma unroll
+		for (uint32_t k = 0; k < 8; ++k) {
+			const uint32_t cx = base[0] + (k & 1u), cy = base[1] + ((k >> 1) & 1u), cz = base[2] + ((k >> 2) & 1u);
+			idx[k] = (cx + res * (cy + res * cz)) % T;
+		}
+	}
+	f16x4 v[8];
+#pragma unroll
+	for (uint32_t k = 0; k < 8; ++k) v[k] = *(const f16x4*)(tab + (size_t)idx[k] * 4);
+#pragma unroll
+	for (uint32_t k = 0; k < 8; ++k) g[k] = active ? v[k] : f16x4{};
+}
+
 // ------------------------------------------------------------------------------------------------
 // NerfNetwork MLP pair: density (enc -> 64 x DH -> 16) and rgb ([density out | SH] -> 64 x RH -> 16)
 // ------------------------------------------------------------------------------------------------
@@ -530,16 +564,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 					base[d] = (uint32_t)(int)t;
 					gfrac[j][d] = p - t;
 				}
-				const f16* tab = a.table + (size_t)lv_off[j] * 4;
-#pragma unroll
-				for (uint32_t k = 0; k < 8; ++k) {
-					const uint32_t cx = base[0] + (k & 1u), cy = base[1] + ((k >> 1) & 1u), cz = base[2] + ((k >> 2) & 1u);
-					const uint32_t ih = (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (lv_T[j] - 1u);
-					uint32_t id = cx + lv_res[j] * (cy + lv_res[j] * cz);
-					if (__builtin_expect(!lv_hashed[j] && id >= lv_T[j], 0)) id %= lv_T[j];
-					const uint32_t idx = lv_hashed[j] ? ih : id;
-					graw[j][k] = lv_active[j] ? *(const f16x4*)(tab + (size_t)idx * 4) : f16x4{};
-				}
+				fuse_gather_level(a.table + (size_t)lv_off[j] * 4, base, lv_res[j], lv_T[j], lv_hashed[j], lv_active[j], graw[j]);
 			}
 		} else {
 #pragma unroll
@@ -990,16 +1015,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 					gb[d] = (uint32_t)(int)t;
 					gfrac[j][d] = p - t;
 				}
-				const f16* tab = a.table + (size_t)lv_off[j] * 4;
-#pragma unroll
-				for (uint32_t k = 0; k < 8; ++k) {
-					const uint32_t cx = gb[0] + (k & 1u), cy = gb[1] + ((k >> 1) & 1u), cz = gb[2] + ((k >> 2) & 1u);
-					const uint32_t ih = (cx ^ (cy * 2654435761u) ^ (cz * 805459861u)) & (lv_T[j] - 1u);
-					uint32_t id = cx + lv_res[j] * (cy + lv_res[j] * cz);
-					if (__builtin_expect(!lv_hashed[j] && id >= lv_T[j], 0)) id %= lv_T[j];
-					const uint32_t idx = lv_hashed[j] ? ih : id;
-					graw[j][k] = lv_active[j] ? *(const f16x4*)(tab + (size_t)idx * 4) : f16x4{};
-				}
+				fuse_gather_level(a.table + (size_t)lv_off[j] * 4, gb, lv_res[j], lv_T[j], lv_hashed[j], lv_active[j], graw[j]);
 			}
 		} else {
 #pragma unroll
