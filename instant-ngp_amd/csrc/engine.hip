@@ -21,6 +21,8 @@
 #include "profiler.h"
 #include "training.h"
 
+static_assert(ngp::DENSITY_LAYOUT_ROW0 == ngp::MLP_LAYOUT_ROW0, "the row-0 density layout of mlp.h and engine_internal.h");
+
 namespace ngp {
 
 int device_cu_count() {
@@ -172,6 +174,8 @@ struct ngp_model {
 	uint32_t overlap = 0;
 	bool fused_hist = true;                 // option "fused_hist": bucket histogram inside the training forward
 	bool fuse_infer = true;                 // option "fuse_infer": NerfNetwork inference encodes inside the MLP kernel
+	bool fuse_density = false;              // option "fuse_density": NerfNetwork::density encodes inside the MLP kernel (off: at the
+	                                        // MLP kernel's occupancy the gathers are slower than the grid forward's)
 	bool fuse_slabs = true;                 // option "fuse_slabs": dW slab reduction inside the grid backward's last kernel
 	bool fuse_opt = true;                   // option "fuse_opt": lazy-layout optimizer update inside the grid backward (training_step)
 	bool fuse_mlp_opt = true;               // option "fuse_mlp_opt": ... and the MLP section's update in its dW slab blocks (no optimizer launch)
@@ -320,6 +324,7 @@ struct ngp_model {
 		       nplan.d_hidden == 1 && nplan.r_hidden >= 1 && nplan.r_hidden <= 3;
 	}
 	bool fused_inference_ok() const { return fuse_infer && fused_encoding_ok(); }
+	bool fused_density_ok() const { return fuse_density && fused_encoding_ok(); }
 	bool fused_training_ok() const { return fuse_train && fused_encoding_ok(); }
 	f16x8* prep(hipStream_t s, bool inference) {
 		f16x8* f = (f16x8*)(inference ? frags_inf : frags).get((size_t)n_all_frags * 1024);
@@ -373,12 +378,13 @@ struct ngp_model {
 			a.params = pick(inference);
 			a.train16 = mlp_train16 ? 1u : 0u;
 			a.pipe = mlp_pipe ? 1u : 0u;
-			if (mode == MLP_INFER_ENC || mode == MLP_TRAIN_ENC) {
+			if (mode == MLP_INFER_ENC || mode == MLP_TRAIN_ENC || mode == MLP_DENSITY_ENC) {
 				if (inference) sync_inference(s);
 				a.table = pick(inference) + grid_offset(); a.max_level = max_level; a.gc = make_grid_const(grid);
 			}
 			ProfScope ps(mode == MLP_TRAIN ? "mlp_train" : mode == MLP_DENSITY ? "mlp_density"
 			             : mode == MLP_INFER_ENC ? "mlp_infer_enc" : mode == MLP_TRAIN_ENC ? "mlp_train_enc"
+			             : mode == MLP_DENSITY_ENC ? "mlp_density_enc"
 			             : mode == MLP_DENSITY_TRAIN ? "mlp_density_train" : "mlp_infer", s);
 			nerf_mlp_run(nplan, mode, a, s);
 		} else {
@@ -854,6 +860,8 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 			m->fused_hist = value != 0;
 		} else if (k == "fuse_infer") {
 			m->fuse_infer = value != 0;
+		} else if (k == "fuse_density") {
+			m->fuse_density = value != 0;
 		} else if (k == "fuse_train") {
 			m->fuse_train = value != 0;
 		} else if (k == "mlp_pipe") {
@@ -940,6 +948,31 @@ int ngp_encoding_backward(ngp_model* m, void* stream, uint32_t n, const float* i
 	});
 }
 
+}  // extern "C"
+// NerfNetwork::density (ngp_density's body): the density network's output rows in `output_layout` (AoS, SoA, or
+// MLP_LAYOUT_ROW0 for the density grid update, which reads row 0 only). With the fused encoding the MLP kernel
+// gathers the grid levels itself (k_nerf_mlp<MLP_DENSITY_ENC>: the integers and the blend of the grid forward,
+// so the same bits).
+int ngp::density_impl(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                      uint32_t output_stride, uint32_t output_layout, int use_inference_params) {
+	NGP_TRY({
+		NGP_CHECK(m->nerf, "density() is a NerfNetwork method");
+		if (n == 0) return NGP_OK;
+		m->require_params(use_inference_params);
+		if (m->fused_density_ok()) {
+			m->run_mlp(S(stream), MLP_DENSITY_ENC, n, input, input_stride, nullptr, (f16*)output, output_stride, output_layout, nullptr,
+			           0, nullptr, nullptr, use_inference_params);
+		} else {
+			f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
+			m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, use_inference_params);
+			m->run_mlp(S(stream), MLP_DENSITY, n, input, input_stride, e, (f16*)output, output_stride, output_layout, nullptr, 0,
+			           nullptr, nullptr, use_inference_params);
+		}
+		m->generation++;
+	});
+}
+extern "C" {
+
 int ngp_inference(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
                   uint32_t output_stride, uint32_t output_layout, int use_inference_params) {
 	NGP_ARG(m && (n == 0 || (input && output)) && (output_layout <= 1 || (output_layout == NGP_LAYOUT_AOS_RGBD && m->nerf &&
@@ -964,16 +997,7 @@ int ngp_inference(ngp_model* m, void* stream, uint32_t n, const float* input, ui
 int ngp_density(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
                 uint32_t output_stride, uint32_t output_layout, int use_inference_params) {
 	NGP_ARG(m && (n == 0 || (input && output)) && output_layout <= 1);
-	NGP_TRY({
-		NGP_CHECK(m->nerf, "density() is a NerfNetwork method");
-		if (n == 0) return NGP_OK;
-		m->require_params(use_inference_params);
-		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
-		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, use_inference_params);
-		m->run_mlp(S(stream), MLP_DENSITY, n, input, input_stride, e, (f16*)output, output_stride, output_layout, nullptr, 0,
-		           nullptr, nullptr, use_inference_params);
-		m->generation++;
-	});
+	return ngp::density_impl(m, stream, n, input, input_stride, output, output_stride, output_layout, use_inference_params);
 }
 
 int ngp_forward(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,

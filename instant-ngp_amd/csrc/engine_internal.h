@@ -31,6 +31,11 @@ int capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, const f
 // the launch without that write (the rest of ngp_graph_launch: workspace check, step and staleness bookkeeping).
 void trainer_ctl_values(const ngp_trainer* t, uint32_t** ctl, uint32_t* step, uint32_t* cfg_off, uint32_t* cfg_words, uint32_t* cfg);
 void graph_launch_ctl_written(ngp_graph* g, void* stream);
+// ngp_density with the internal output layout DENSITY_LAYOUT_ROW0 allowed besides AoS / SoA: row 0 only, a flat
+// array of n (the density grid update reads nothing else)
+constexpr uint32_t DENSITY_LAYOUT_ROW0 = 3;  // == MLP_LAYOUT_ROW0 (mlp.h)
+int density_impl(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
+                 uint32_t output_stride, uint32_t output_layout, int use_inference_params);
 // One eager step of what capture_training_step_with records (the host-callback exchange of gloo ranks)
 int train_step_with(ngp_trainer* t, void* stream, uint32_t n, const float* input, uint32_t input_stride, const void* dL_doutput,
                     uint32_t dL_stride, float loss_scale, const Exchange& ex);

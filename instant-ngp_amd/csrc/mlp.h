@@ -101,8 +101,13 @@ MlpPlan make_mlp_plan(uint32_t enc_width, uint32_t width, uint32_t hidden, uint3
 void prepare_frags(const FragDesc* descs_dev, uint32_t n_frags, const f16* params, f16x8* frags, hipStream_t s);
 
 enum MlpMode : uint32_t { MLP_INFER = 0, MLP_TRAIN = 1, MLP_DENSITY = 2, MLP_INFER_ENC = 3, MLP_TRAIN_ENC = 4,
-                          MLP_DENSITY_TRAIN = 5 };  // density network forward + backward only (NeRF)
-// MLP_INFER_ENC / MLP_TRAIN_ENC are fused for 3D grids with 4 levels of 4 features (one 16-wide encoding step: C2)
+                          MLP_DENSITY_TRAIN = 5,   // density network forward + backward only (NeRF)
+                          MLP_DENSITY_ENC = 6 };   // MLP_DENSITY with the encoding gathered in the kernel
+// MLP_INFER_ENC / MLP_TRAIN_ENC / MLP_DENSITY_ENC are fused for 3D grids with 4 levels of 4 features (one 16-wide
+// encoding step: C2)
+// internal output layout of the density network: row 0 only, as a flat array of n (the density grid update
+// reads nothing else)
+constexpr uint32_t MLP_LAYOUT_ROW0 = 3;  // == DENSITY_LAYOUT_ROW0 (engine_internal.h)
 bool nerf_mlp_fused_encoding_ok(const GridDesc& g, uint32_t enc_width);
 
 // Launch sizes for the training kernel: one persistent block per CU (slab count = blocks).

@@ -377,7 +377,9 @@ __device__ __forceinline__ f16x8 sh4_frag(float dx, float dy, float dz, int h) {
 // rows 4h..4h+3 (regs 0..3) and 8+4h..8+4h+3 (regs 4..7).
 __device__ __forceinline__ void store_out16(f16* out, uint32_t stride, uint32_t layout, uint32_t n, uint32_t sample, int h,
                                             const f16x8& v) {
-	if (layout == 2) {  // NGP_LAYOUT_AOS_RGBD: rows 0..3 only (lane half 0 holds them)
+	if (layout == MLP_LAYOUT_ROW0) {  // row 0 only (lane half 0, register 0)
+		if (h == 0) out[sample] = v[0];
+	} else if (layout == 2) {  // NGP_LAYOUT_AOS_RGBD: rows 0..3 only (lane half 0 holds them)
 		if (h == 0) *(f16x4*)(out + (size_t)sample * stride) = f16x4{v[0], v[1], v[2], v[3]};
 	} else if (layout == 0) {
 		f16* row = out + (size_t)sample * stride;
@@ -478,8 +480,8 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	using Lay = NerfLayout<ES, DH, RH>;
 	constexpr bool DTRAIN = MODE == MLP_DENSITY_TRAIN;  // density network forward + backward only
 	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_TRAIN_ENC || DTRAIN;
-	constexpr bool DENSITY = MODE == MLP_DENSITY;
-	constexpr bool FUSE = MODE == MLP_INFER_ENC || MODE == MLP_TRAIN_ENC;
+	constexpr bool DENSITY = MODE == MLP_DENSITY || MODE == MLP_DENSITY_ENC;
+	constexpr bool FUSE = MODE == MLP_INFER_ENC || MODE == MLP_TRAIN_ENC || MODE == MLP_DENSITY_ENC;
 	static_assert(!FUSE || ES == 1, "fused encoding: one 16-wide encoding step");
 	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (DENSITY ? Lay::F_R0 : Lay::N_FWD);
 	extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1432,7 +1434,7 @@ template <int ES, int DH, int RH, int MODE>
 static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	using Lay = NerfLayout<ES, DH, RH>;
 	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_TRAIN_ENC || MODE == MLP_DENSITY_TRAIN;
-	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (MODE == MLP_DENSITY ? Lay::F_R0 : Lay::N_FWD);
+	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (MODE == MLP_DENSITY || MODE == MLP_DENSITY_ENC ? Lay::F_R0 : Lay::N_FWD);
 	size_t lds = (size_t)NFRAG * 1024 + (TRAIN ? 4 * Lay::IMG_HALVES * sizeof(f16) : 0);
 	uint32_t n_reg = 4;
 	while (n_reg > 1 && (size_t)n_reg * a.n_matrix * sizeof(float) > 160 * 1024) n_reg /= 2;
@@ -1504,6 +1506,7 @@ void nerf_mlp_run(const NerfMlpPlan& p, MlpMode mode, const NerfMlpArgs& a, hipS
 		case MLP_INFER_ENC: dispatch_nerf_fused<MLP_INFER_ENC>(p, a, s); break;
 		case MLP_TRAIN_ENC: dispatch_nerf_fused<MLP_TRAIN_ENC>(p, a, s); break;
 		case MLP_DENSITY_TRAIN: dispatch_nerf<MLP_DENSITY_TRAIN>(p, a, s); break;
+		case MLP_DENSITY_ENC: dispatch_nerf_fused<MLP_DENSITY_ENC>(p, a, s); break;
 	}
 }
 

@@ -593,7 +593,8 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	const uint32_t ns = hi - lo;
 	f16* dens = t->gdens.get<f16>((size_t)std::max(ns, 1u) * 16);
 	if (ns) {
-		check_rc(ngp_density(t->model, s, ns, pos + (size_t)lo * 3, 3, dens, ns, NGP_LAYOUT_SOA, 0));  // row 0 = raw density
+		// row 0 (raw density) only: the other 15 rows of the density network's output are not read
+		check_rc(ngp::density_impl(t->model, s, ns, pos + (size_t)lo * 3, 3, dens, ns, ngp::DENSITY_LAYOUT_ROW0, 0));
 		grid_splat_max(ns, idx + lo, dens, cfg.density_activation, tmp, s);
 	}
 	if (t->world > 1) {

@@ -141,6 +141,25 @@ def test_nerf_density(pkg, orc, nerf_setup):
     assert np.array_equal(soa.T, out)
 
 
+@pytest.mark.parametrize("n", [1, 33, 2000, 70001])
+def test_nerf_density_fused_bitwise(pkg, nerf_setup, n):
+    """NerfNetwork::density with the encoding gathered inside the MLP kernel (option fuse_density, on by
+    default) against encode-then-MLP (fuse_density 0): both layouts, bit for bit, including positions
+    outside [0, 1] (the dense levels' index wraps like tcnn's index % T)."""
+    net, tr, p16, m = nerf_setup
+    c = coords_batch(n, seed=40 + n)
+    c[::7, :3] = c[::7, :3] * 9.0 - 4.0  # far out of the unit cube: dense indices beyond 2 T take the modulo branch
+    x = torch.from_numpy(c).cuda()
+    res = {}
+    for fused in (0, 1):
+        net.set_option("fuse_density", fused)
+        for layout in (pkg.LAYOUT_AOS, pkg.LAYOUT_SOA):
+            res[fused, layout] = net.density(x, layout=layout, use_inference_params=False).clone()
+    net.set_option("fuse_density", 1)
+    for layout in (pkg.LAYOUT_AOS, pkg.LAYOUT_SOA):
+        assert torch.equal(res[0, layout].view(torch.int16), res[1, layout].view(torch.int16)), layout
+
+
 @pytest.mark.parametrize("n", [32, 777, 4096])
 def test_nerf_forward_backward(pkg, orc, nerf_setup, n):
     net, tr, p16, m = nerf_setup
