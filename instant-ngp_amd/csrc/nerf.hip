@@ -412,6 +412,9 @@ constexpr uint32_t LG = 16;  // lanes per ray in the loss passes: one DPP row
 #ifndef NGP_LOSS_PF
 #define NGP_LOSS_PF 2  // loss pass 1: chunks of 16 samples whose loads are in flight ahead of the compositing
 #endif
+#ifndef NGP_LOSS2_LANES
+#define NGP_LOSS2_LANES 64  // loss pass 2 with pass 1's kept state: lanes per ray (k_loss_pass2)
+#endif
 #ifndef NGP_LOSS_SELECT
 #define NGP_LOSS_SELECT 1  // loss pass 1: compositing steps committed with selects instead of branches (pass 2
                            // measured slower that way: its steps already run under a per-lane mask)
@@ -1270,11 +1273,15 @@ __device__ __forceinline__ void deposit_error(const LossArgs& a, const Camera* _
 	atomicAdd(em + (size_t)(iy + 1) * a.em_w + ix + 1, wx * wy * ml);
 }
 
+// LANES per ray: LG (one DPP row) when pass 2 composites again; a whole wave when it reads pass 1's kept state,
+// where the samples are independent: a ray's samples then take ceil(cn / 64) rounds of loads instead of
+// ceil(cn / 16), and the long rays, each round a memory latency, set the kernel's time (fox: up to ~26 rounds)
+template <uint32_t LANES>
 __global__ void __launch_bounds__(256) k_loss_pass2(const Camera* __restrict__ cams, const ngp_nerf_config cfg, LossArgs a,
                                                     const uint32_t* __restrict__ craw, const uint32_t* __restrict__ cbase,
                                                     const LossRay* __restrict__ lr) {
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-	const uint32_t i = gid / LG, L = gid % LG;
+	const uint32_t i = gid / LANES, L = gid % LANES;
 	if (gid == 0) *a.compacted_counter = cbase[a.n_rays - 1] + craw[a.n_rays - 1];
 	if (i >= a.n_rays || i >= *a.ray_counter) return;
 	const uint32_t base = a.numsteps[2 * i + 1];
@@ -1325,8 +1332,8 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const Camera* __restrict__ c
 		             (o3 > -10.0f && depth < cfg.near_distance ? 1e-4f : 0.0f));
 		*(f16x4*)(dl + (size_t)jj * 16) = g;
 	};
-	if (a.state) {  // pass 1 kept every composited sample's state: no sequential compositing here
-		for (uint32_t jj = L; jj < cn; jj += LG) {
+	if (LANES != LG || a.state) {  // pass 1 kept every composited sample's state: no sequential compositing here
+		for (uint32_t jj = L; jj < cn; jj += LANES) {
 			float cc[7];
 #pragma unroll
 			for (int k = 0; k < 7; ++k) cc[k] = ci[(size_t)jj * 7 + k];
@@ -1340,6 +1347,7 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const Camera* __restrict__ c
 		}
 		return;
 	}
+	if constexpr (LANES == LG) {
 	float r2[3] = {0.f, 0.f, 0.f};
 	float t = 1.0f;
 	// software pipelining as in pass 1: NGP_LOSS2_PF chunks' loads in flight ahead of the compositing
@@ -1400,6 +1408,7 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const Camera* __restrict__ c
 		if (!valid) continue;
 		emit(jj, cc, o, rgb, dt, my_w, my_t, my_r2);
 	}
+	}
 }
 
 size_t loss_tmp_f32(uint32_t n_rays) { return (size_t)n_rays * (sizeof(LossRay) / 4); }
@@ -1421,7 +1430,12 @@ void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs&
 		exclusive_scan(craw, cbase, a.n_rays, scan_tmp, scan_bytes, s);
 	}
 	ProfScope ps("loss_pass2", s);
-	k_loss_pass2<<<blocks, 256, 0, s>>>(ds.d_cams, cfg, a, craw, cbase, lr);
+	if (a.state) {
+		constexpr uint32_t W = NGP_LOSS2_LANES;  // a wave per ray: see k_loss_pass2
+		k_loss_pass2<W><<<div_round_up((size_t)a.n_rays * W, 256), 256, 0, s>>>(ds.d_cams, cfg, a, craw, cbase, lr);
+	} else {
+		k_loss_pass2<LG><<<blocks, 256, 0, s>>>(ds.d_cams, cfg, a, craw, cbase, lr);
+	}
 	NGP_HIP(hipGetLastError());
 }
 
