@@ -415,6 +415,9 @@ constexpr uint32_t LG = 16;  // lanes per ray in the loss passes: one DPP row
 #ifndef NGP_LOSS2_LANES
 #define NGP_LOSS2_LANES 64  // loss pass 2 with pass 1's kept state: lanes per ray (k_loss_pass2)
 #endif
+// a ray's lanes must be one wave: lane 0 overwrites numsteps[2i + 1] after every lane has read it in the same
+// wave instruction (128 or 256 lanes per ray let a second wave read the overwritten value: wrong samples)
+static_assert(NGP_LOSS2_LANES >= 16 && NGP_LOSS2_LANES <= 64, "loss pass 2: at most one wave per ray");
 #ifndef NGP_LOSS_SELECT
 #define NGP_LOSS_SELECT 1  // loss pass 1: compositing steps committed with selects instead of branches (pass 2
                            // measured slower that way: its steps already run under a per-lane mask)
