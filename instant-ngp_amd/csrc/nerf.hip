@@ -412,6 +412,9 @@ constexpr uint32_t LG = 16;  // lanes per ray in the loss passes: one DPP row
 #ifndef NGP_LOSS_PF
 #define NGP_LOSS_PF 2  // loss pass 1: chunks of 16 samples whose loads are in flight ahead of the compositing
 #endif
+#ifndef NGP_LOSS_XCD
+#define NGP_LOSS_XCD 1  // loss pass 1 reads its rays on the XCD that wrote their samples (k_loss_pass1)
+#endif
 #ifndef NGP_LOSS2_LANES
 #define NGP_LOSS2_LANES 64  // loss pass 2 with pass 1's kept state: lanes per ray (k_loss_pass2)
 #endif
@@ -1115,8 +1118,17 @@ __device__ __forceinline__ V3 unwarp_pos(const float* c, const Aabb& b) {
 __global__ void __launch_bounds__(256) k_loss_pass1(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
                                                     uint32_t n_images, const ngp_nerf_config cfg, LossArgs a,
                                                     uint32_t* __restrict__ craw, LossRay* __restrict__ lr) {
-	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-	const uint32_t i = gid / LG, L = gid % LG;
+	// XCD-aware ray order (NGP_LOSS_XCD): the block on XCD x = blockIdx % 8 takes the rays whose samples
+	// k_sample_write wrote from XCD x (a wave per ray there: ray i on XCD (i / 4) % 8), so their coordinates
+	// can still be in that XCD's L2: rays 128 m + 32 q + 4 x + j (q, j in 0..3) for block 8 m + x
+	uint32_t i;
+	const uint32_t L = threadIdx.x % LG;
+	if (NGP_LOSS_XCD) {
+		const uint32_t m = blockIdx.x / 8, x = blockIdx.x % 8, r = threadIdx.x / LG;
+		i = 128 * m + 32 * (r / 4) + 4 * x + (r % 4);
+	} else {
+		i = (blockIdx.x * blockDim.x + threadIdx.x) / LG;
+	}
 	if (i >= a.n_rays) return;
 	if (L == 0 && a.zero_loss && a.loss) a.loss[i] = 0.0f;  // pass 2 writes the compacted rays' loss after it
 	if (i >= *a.ray_counter) { if (L == 0) craw[i] = 0; return; }
@@ -1425,7 +1437,9 @@ void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs&
 	const uint32_t blocks = div_round_up((size_t)a.n_rays * LG, 256);
 	{
 		ProfScope ps("loss_pass1", s);
-		k_loss_pass1<<<blocks, 256, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, craw, lr);
+		static_assert(256 / LG == 16, "k_loss_pass1's XCD-aware order assumes 16 rays per block");
+		const uint32_t b1 = NGP_LOSS_XCD ? 8 * div_round_up(a.n_rays, 128) : blocks;
+		k_loss_pass1<<<b1, 256, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, craw, lr);
 		NGP_HIP(hipGetLastError());
 	}
 	{
