@@ -17,6 +17,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--keep-state", type=int, default=1, help="pass 1 keeps the compositing state (the training step's form)")
+    ap.add_argument("--flush-mb", type=int, default=0, help="write this many MB between launches (evicts the L2s)")
     args = ap.parse_args()
     from __graft_entry__ import load_package
     pkg = load_package()
@@ -38,21 +40,29 @@ def main():
     kept = int(got["counters"].cpu().numpy().view(np.uint32)[0])
     ns = got["numsteps"].cpu().numpy().view(np.uint32).reshape(-1)[: 2 * kept].reshape(-1, 2)[:, 0].astype(np.int64)
     out = net.inference(got["coords"], layout=pkg.LAYOUT_AOS, use_inference_params=False)
-    gl = pkg.nerf.compute_loss(ds, cfg, R, r, B, got, out, mean[:1].contiguous())
+    ks = bool(args.keep_state)
+    ns0 = got["numsteps"].clone()  # compute_loss rewrites numsteps to the compacted {n, base}: restored per launch
+    gl = pkg.nerf.compute_loss(ds, cfg, R, r, B, got, out, mean[:1].contiguous(), keep_state=ks)
+    flush = torch.empty(max(args.flush_mb, 1) * (1 << 18), dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
+    tot = 0.0
     for _ in range(args.reps):
-        pkg.nerf.compute_loss(ds, cfg, R, r, B, got, out, mean[:1].contiguous())
-    ev1.record()
-    torch.cuda.synchronize()
+        got["numsteps"].copy_(ns0)
+        if args.flush_mb:
+            flush.fill_(1.0)
+        ev0.record()
+        pkg.nerf.compute_loss(ds, cfg, R, r, B, got, out, mean[:1].contiguous(), keep_state=ks)
+        ev1.record()
+        torch.cuda.synchronize()
+        tot += ev0.elapsed_time(ev1)
     q = np.percentile(ns, [50, 90, 99, 99.9]).tolist()
     chunks = (ns + 15) // 16
     print(json.dumps({"rays": R, "kept": kept, "samples": int(ns.sum()), "numsteps_mean": float(ns.mean()),
                       "numsteps_p50_p90_p99_p999": q, "numsteps_max": int(ns.max()),
                       "chunks_max": int(chunks.max()), "chunks_mean": float(chunks.mean()),
                       "rays_over_256": int((ns > 256).sum()), "rays_over_512": int((ns > 512).sum()),
-                      "compute_loss_ms": ev0.elapsed_time(ev1) / args.reps}))
+                      "keep_state": ks, "flush_mb": args.flush_mb, "compute_loss_ms": tot / args.reps}))
 
 
 if __name__ == "__main__":
