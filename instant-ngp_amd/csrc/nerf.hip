@@ -429,13 +429,22 @@ static_assert(NGP_LOSS2_LANES >= 16 && NGP_LOSS2_LANES <= 64, "loss pass 2: at m
 #define NGP_LOSS2_PF 1  // loss pass 2: depth 2 takes 86 VGPRs (5 waves/SIMD) and measured 41 -> 45 us (Lego stand-in)
 #endif
 static_assert(RG >= 4 && RG <= 16 && (RG & (RG - 1)) == 0, "sampler group: 4, 8 or 16 lanes");
+#ifndef NGP_SAMPLER_RG0
+#define NGP_SAMPLER_RG0 4  // lanes per ray at cone 0 (k_sample_count<true>, the Lego stand-in): 8 -> 4 measured
+                           // Lego 0.451-0.453 -> 0.443-0.446 ms per step; the cone-stepping march (fox) stays at
+                           // RG (4 there: 0.546 -> 0.605 ms, gpurun_out/r05zzg)
+#endif
+static_assert(NGP_SAMPLER_RG0 >= 4 && NGP_SAMPLER_RG0 <= 16 && (NGP_SAMPLER_RG0 & (NGP_SAMPLER_RG0 - 1)) == 0,
+              "sampler group: 4, 8 or 16 lanes");
+template <bool CONE0> constexpr uint32_t sampler_rg() { return CONE0 ? NGP_SAMPLER_RG0 : RG; }
 #ifndef NGP_SAMPLER_BLOCK
 #define NGP_SAMPLER_BLOCK 256
 #endif
 
-__device__ __forceinline__ uint32_t row_ballot(bool p) {  // this ray's RG lanes of a wave ballot
+template <uint32_t G>
+__device__ __forceinline__ uint32_t row_ballot(bool p) {  // this ray's G lanes of a wave ballot
 	const unsigned long long b = __ballot(p);
-	return (uint32_t)(b >> (__lane_id() & (64u - RG))) & ((1u << RG) - 1u);
+	return (uint32_t)(b >> (__lane_id() & (64u - G))) & ((1u << G) - 1u);
 }
 __device__ __forceinline__ float dpp_shr1(float v) {  // lane l - 1 of the same DPP row (lane 0 of a row: 0)
 	return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));
@@ -576,7 +585,7 @@ struct Marcher {
 		const float ax = fabsf(idir.x), ay = fabsf(idir.y), az = fabsf(idir.z);
 		float s = 0.0f;
 #pragma unroll
-		for (uint32_t k = 0; k + 1 < RG; ++k) {
+		for (uint32_t k = 0; k + 1 < sampler_rg<CONE0>(); ++k) {
 			if (k < j) {
 				s = fminf(fminf(sx, sy), sz);
 				if (sx == s) sx += ax;
@@ -650,8 +659,9 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
                                                       uint32_t n_images, const ngp_nerf_config cfg, SampleArgs a,
                                                       uint32_t* __restrict__ nsteps, float* __restrict__ tbuf,
                                                       RayGeo* __restrict__ geo, const Cone cone) {
+	constexpr uint32_t RGk = sampler_rg<CONE0>();
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-	const uint32_t i = gid / RG, L = gid % RG;
+	const uint32_t i = gid / RGk, L = gid % RGk;
 	if (i >= a.n_rays) return;  // whole rows
 	if (!CONE0 && NGP_SAMPLER_PRIO) __builtin_amdgcn_s_setprio(NGP_SAMPLER_PRIO);
 	SAMPLER_STAT(const unsigned long long ck0 = sampler_clock();)
@@ -668,11 +678,11 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 		// Under cone stepping the speculative march crosses trailing empty space faster than the backward
 		// scan finds its start (fox: 0.356 ms with it, 0.334 without, profiles/r03ak); at cone 0 it pays.
 		const float t_end = (CONE0 || NGP_SAMPLER_END_CONE)
-		                        ? sampling_end_row<RG>(r.o, r.dn, r.idir, t, m.cone, box, a.bitfield, cfg.max_cascade, L)
+		                        ? sampling_end_row<RGk>(r.o, r.dn, r.idir, t, m.cone, box, a.bitfield, cfg.max_cascade, L)
 		                        : 3.0e38f;
 #endif
 #if NGP_SAMPLER_DIAG == 1  // timing aid: sampling_end twice (cost of one = difference to the default build)
-		const float t_end2 = sampling_end_row<RG>(r.o, r.dn, r.idir, t + 0.0f * t_end, m.cone, box, a.bitfield, cfg.max_cascade, L);
+		const float t_end2 = sampling_end_row<RGk>(r.o, r.dn, r.idir, t + 0.0f * t_end, m.cone, box, a.bitfield, cfg.max_cascade, L);
 		if (t_end2 != t_end) t = t_end2;
 #endif
 		float* tout = tbuf + (size_t)i * STEPS;
@@ -688,7 +698,7 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			float tl, last;  // last: the state after lane nvalid-1's (the march continues there if every lane stays in the mode)
 			uint32_t mipl;   // the mip lane L's state is tested at
 			float nk = 0.f;  // unified loop: to(tl), from its verify step (reused when the ray leaves an occupied run at this lane)
-			uint32_t nvalid = RG;  // lanes holding verified states
+			uint32_t nvalid = RGk;  // lanes holding verified states
 			if (CONE0 ? NGP_SAMPLER_UNIFIED0 : NGP_SAMPLER_EMPTY_SPEC) {
 				// Both modes in one guess-and-verify loop. Every state is from(n + c) with n =
 				// to(previous state): c = 1 in an occupied run (t + calc_dt(t)), c = the ceil of
@@ -710,9 +720,9 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 					SAMPLER_STAT(if (occ_mode) ++st_r; else ++st_q;)
 					nxt = m.step_any(cand, occ_mode, &mk, &nk);
 					const float expct = dpp_shr1(nxt);
-					const uint32_t v = __builtin_ctz(row_ballot(L >= v0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
-					if (v >= RG) break;
-					const float tv = __shfl(expct, (int)v, (int)RG);
+					const uint32_t v = __builtin_ctz(row_ballot<RGk>(L >= v0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RGk));
+					if (v >= RGk) break;
+					const float tv = __shfl(expct, (int)v, (int)RGk);
 					// The wave runs the loop until its slowest ray is verified. After NGP_SAMPLER_ROUND_CAP rounds a
 					// ray keeps its verified prefix (lanes < v) and continues from tv (the exact state after it)
 					// in the next iteration.
@@ -728,15 +738,15 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				}
 				tl = cand;
 				mipl = mk;
-				last = __shfl(nxt, (int)(RG - 1), (int)RG);
-				if (nvalid < RG) last = tcap;
+				last = __shfl(nxt, (int)(RGk - 1), (int)RGk);
+				if (nvalid < RGk) last = tcap;
 			} else if (occ_mode) {
 				// Occupied run: t_{k+1} = t_k + calc_dt(t_k) = from(to(t_k) + 1) in stepping space, and
 				// to(from(n)) == n nearly always. Guess state L as from(to(t) + L) and verify every guess at
 				// once (lane L redoes the exact step from lane L-1's state): the verified prefix is exact; the
 				// first lane that fails takes the exact state from its verified predecessor and the lanes
 				// after it are re-guessed from there. Each round verifies at least one more lane, most runs
-				// take one round instead of a chain of RG dependent steps.
+				// take one round instead of a chain of RGk dependent steps.
 				const float n0 = to_stepping_space(t, m.k());
 				float cand = L == 0 ? t : from_stepping_space(n0 + (float)L, m.k());
 				uint32_t v0 = 1;
@@ -746,22 +756,22 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 					dt = m.dt_at(cand);
 					nxt = cand + dt;  // step_occupied(cand)
 					const float expct = dpp_shr1(nxt);
-					const uint32_t v = __builtin_ctz(row_ballot(L >= v0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RG));
-					if (v >= RG) break;
-					const float tv = __shfl(expct, (int)v, (int)RG);
+					const uint32_t v = __builtin_ctz(row_ballot<RGk>(L >= v0 && __float_as_uint(expct) != __float_as_uint(cand)) | (1u << RGk));
+					if (v >= RGk) break;
+					const float tv = __shfl(expct, (int)v, (int)RGk);
 					cand = L < v ? cand : (L == v ? tv : from_stepping_space(to_stepping_space(tv, m.k()) + (float)(L - v), m.k()));
 					v0 = v + 1;
 				}
 				tl = cand;
 				mipl = m.mip_at(CONE0 ? 0.0f : dt, m.pos(tl));
-				last = __shfl(nxt, (int)(RG - 1), (int)RG);
+				last = __shfl(nxt, (int)(RGk - 1), (int)RGk);
 			} else {
 				// empty space: the chain evaluated in order by every lane of the group; lane L keeps state L
 				float tk = t;
 				tl = t;
 				mipl = 0;
 #pragma unroll 1  // rolled: the unrolled chain (8 inlined steps) overflowed the instruction cache
-				for (uint32_t kk = 0; kk < RG; ++kk) {
+				for (uint32_t kk = 0; kk < RGk; ++kk) {
 					uint32_t mk;
 					const float tn = m.step_empty(tk, &mk);
 					if (L == kk) { tl = tk; mipl = mk; }
@@ -774,8 +784,8 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 			const uint32_t mip = mipl;
 			const bool inside = L < nvalid && tl <= t_end && aabb_contains(box, pos) && (occ_mode ? j + L : j) < STEPS;
 			const bool occ = inside && density_grid_occupied_at(pos, a.bitfield, mip);
-			const uint32_t cont = row_ballot(inside && occ == occ_mode);
-			const uint32_t f = __builtin_ctz(~cont | (1u << RG));  // first lane the sequential march leaves the mode at
+			const uint32_t cont = row_ballot<RGk>(inside && occ == occ_mode);
+			const uint32_t f = __builtin_ctz(~cont | (1u << RGk));  // first lane the sequential march leaves the mode at
 			SAMPLER_STAT(ck_o += sampler_clock() - ckb;)
 			if (occ_mode) {
 #if NGP_SAMPLER_DIAG == 5  // timing aid: every occupied state stored twice (mirrored copy; cost of the stores)
@@ -789,17 +799,17 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 				t = last;
 				continue;
 			}
-			if (!((row_ballot(inside) >> f) & 1u)) break;  // left the aabb / sampling range / step budget
-			const float tf = __shfl(tl, (int)f, (int)RG);
+			if (!((row_ballot<RGk>(inside) >> f) & 1u)) break;  // left the aabb / sampling range / step budget
+			const float tf = __shfl(tl, (int)f, (int)RGk);
 			if (occ_mode) {  // empty cell at lane f: advance_to_next_voxel
 				// cone stepping: lane f's to() from its verify step (at cone 0 to() is a multiply, cheaper than the shuffle)
-				if (!CONE0 && NGP_SAMPLER_EMPTY_SPEC) t = m.step_empty_n(tf, __shfl(nk, (int)f, (int)RG));
+				if (!CONE0 && NGP_SAMPLER_EMPTY_SPEC) t = m.step_empty_n(tf, __shfl(nk, (int)f, (int)RGk));
 				else t = m.step_empty(tf);
 			}
 			else {  // occupied cell at lane f: sample it next
 				t = tf;
 				if (!CONE0 && NGP_SAMPLER_EMPTY_SPEC) {
-					n0_next = __shfl(nk, (int)f, (int)RG);
+					n0_next = __shfl(nk, (int)f, (int)RGk);
 					have_n0 = true;
 				}
 			}
@@ -1065,11 +1075,12 @@ void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs
 	float* tbuf = tmpf;
 	RayGeo* geo = (RayGeo*)(tmpf + (size_t)a.n_rays * STEPS);
 	const uint32_t blocks = div_round_up((size_t)a.n_rays * RG, NGP_SAMPLER_BLOCK);
+	const uint32_t blocks0 = div_round_up((size_t)a.n_rays * sampler_rg<true>(), NGP_SAMPLER_BLOCK);
 	const Cone cone = make_cone(cfg.cone_angle_constant);  // every ray's cone (setup_ray: r.cone)
 	{
 		ProfScope ps("sample_count", s);
 		if (cfg.cone_angle_constant <= 1e-5f)
-			k_sample_count<true><<<blocks, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo, cone);
+			k_sample_count<true><<<blocks0, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo, cone);
 		else
 			k_sample_count<false><<<blocks, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo, cone);
 		NGP_HIP(hipGetLastError());
