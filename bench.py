@@ -95,7 +95,7 @@ REGION_KERNELS = {
     "grid_backward": ["k_grid_backward"],
     "grid_backward_total": ["k_sc_scan", "k_sc_plan", "k_sc_scatter", "k_sc_accumulate", "k_sc_split_reduce"],
     # k_nerf_mlp / k_mlp carry the mode as their LAST template argument (1 = training, 0 = inference)
-    "mlp_train": ["k_nerf_mlp_train<", "k_nerf_mlp_train16<", "1>(ngp::NerfMlpArgs)", "1>(ngp::MlpArgs)"],
+    "mlp_train": ["k_nerf_mlp_train<", "1>(ngp::NerfMlpArgs)", "1>(ngp::MlpArgs)"],
     "mlp_infer": ["0>(ngp::NerfMlpArgs)", "0>(ngp::MlpArgs)"],
     "optimizer": ["k_adam_ema", "k_adam_lazy"],
 }

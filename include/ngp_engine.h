@@ -103,8 +103,8 @@ int ngp_model_initialize_params(const ngp_model* m, uint64_t seed, float* params
 int ngp_model_set_max_level(ngp_model* m, float max_level, const float* max_level_per_sample);
 /* engine knobs: "grid_backward_mode" = 0 auto, 1 direct packed-f16 atomics (tcnn-style),
  * 3 destination-bucketed exact sums (auto picks 3 for n >= 4096); "grid_bricks" (bucketed backward: dense
- * levels summed per brick where that moves fewer bytes, default 0); "fuse_infer", "fuse_train",
- * "fused_hist", "overlap", "grid_forward_mode"  */
+ * levels summed per brick where that moves fewer bytes, default 0); "fuse_infer", "fused_hist",
+ * "fuse_slabs", "fuse_opt", "fuse_mlp_opt", "overlap", "win_debug"  */
 int ngp_model_set_option(ngp_model* m, const char* key, double value);
 /* engine state for tests and tools: "grid_brick_levels" = how many dense levels the bucketed backward sums
  * per brick in its plan for the last batch size (0: all levels through items) */
@@ -179,6 +179,12 @@ void ngp_trainer_destroy(ngp_trainer* t);
 /* Trainer::optimizer_step(stream, loss_scale) (src/testbed_nerf.cu:3678) */
 int ngp_trainer_optimizer_step(ngp_trainer* t, void* stream, float loss_scale);
 void* ngp_trainer_gradients(ngp_trainer* t);               /* fp16 [n_params], the DP all-reduce buffer */
+/* 1 when the gradient buffer holds the last training pass's whole gradient. 0 after a step whose backward did
+ * not write it: the grid's optimizer update fused into the backward (ngp_trainer_fused_update_active, captured
+ * or training_step steps on the lazy layout) or the sharded data-parallel step, whose backward stores the
+ * gradient as fp32 for the reduce-scatter. The buffer then holds an older gradient. ngp_forward_backward and
+ * steps without the fused update write it again (engine extension; tcnn's gradients() is always current) */
+int ngp_trainer_gradients_valid(const ngp_trainer* t);
 void* ngp_trainer_params(ngp_trainer* t);                  /* fp16 [n_params] */
 void* ngp_trainer_inference_params(ngp_trainer* t);        /* fp16 [n_params] (EMA when configured) */
 /* fp32 [n_params]; large-table trainers keep the master weights in their optimizer records and refresh this

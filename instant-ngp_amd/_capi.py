@@ -118,6 +118,7 @@ SIGNATURES = {
     "ngp_trainer_destroy": (None, [P]),
     "ngp_trainer_optimizer_step": (i32, [P, P, f32]),
     "ngp_trainer_gradients": (P, [P]),
+    "ngp_trainer_gradients_valid": (i32, [P]),
     "ngp_trainer_params": (P, [P]),
     "ngp_trainer_inference_params": (P, [P]),
     "ngp_trainer_params_full_precision": (P, [P]),

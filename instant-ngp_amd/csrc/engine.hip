@@ -174,18 +174,10 @@ struct ngp_model {
 	uint32_t overlap = 0;
 	bool fused_hist = true;                 // option "fused_hist": bucket histogram inside the training forward
 	bool fuse_infer = true;                 // option "fuse_infer": NerfNetwork inference encodes inside the MLP kernel
-	bool fuse_density = false;              // option "fuse_density": NerfNetwork::density encodes inside the MLP kernel (off: at the
-	                                        // MLP kernel's occupancy the gathers are slower than the grid forward's)
 	bool fuse_slabs = true;                 // option "fuse_slabs": dW slab reduction inside the grid backward's last kernel
 	bool fuse_opt = true;                   // option "fuse_opt": lazy-layout optimizer update inside the grid backward (training_step)
 	bool fuse_mlp_opt = true;               // option "fuse_mlp_opt": ... and the MLP section's update in its dW slab blocks (no optimizer launch)
-	bool mlp_pipe = false;                  // option "mlp_pipe": the training MLP software-pipelined across tiles (k_nerf_mlp_train_pipe)
-	bool mlp_train16 = false;               // option "mlp_train16": the training MLP at two waves per SIMD (mlp_train16.hip; off: no faster at C2, 3x slower at C2p)
-	bool grid_stage0 = false;               // option "grid_stage0": the training forward stages level 0 in LDS (grid.hip STAGE0; off: measured slower)
 	bool grid_bricks = false;               // option "grid_bricks": dense levels of the bucketed backward summed per brick (off: measured slower)
-	bool fuse_train = false;                // option "fuse_train": ... and the training forward_backward too (off: the
-	                                        // training kernel runs 1 wave/SIMD, the gathers are not hidden; C2 0.157 -> 0.161 ms)
-	int grid_forward_mode = 0;              // option "grid_forward_mode": 0 auto, 1 per-sample rows, 2 XCD-partitioned
 	hipStream_t side = nullptr;             // overlaps fragments + bucket histogram with forward + MLP,
 	                                        // and the dW slab reduction with the grid backward
 	hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_frags = nullptr, ev_mlp = nullptr, ev_red = nullptr;
@@ -196,6 +188,9 @@ struct ngp_model {
 	void sync_inference(hipStream_t s) { if (inference_hook) inference_hook(inference_hook_ctx, s); }
 	float max_level = 1.0f;
 	const float* max_level_per_sample = nullptr;
+	// false: the last training pass did not write the fp16 gradient buffer (the grid's update ran inside the
+	// backward, or the backward stored the gradient as fp32 for the sharded exchange): ngp_trainer_gradients_valid
+	bool grads_valid = true;
 	uint64_t generation = 0;
 	uint64_t ws_epoch = 0;  // bumped by every workspace reallocation (DevBuf::epoch)
 	std::unique_ptr<ngp_ctx> last_ctx;
@@ -324,8 +319,6 @@ struct ngp_model {
 		       nplan.d_hidden == 1 && nplan.r_hidden >= 1 && nplan.r_hidden <= 3;
 	}
 	bool fused_inference_ok() const { return fuse_infer && fused_encoding_ok(); }
-	bool fused_density_ok() const { return fuse_density && fused_encoding_ok(); }
-	bool fused_training_ok() const { return fuse_train && fused_encoding_ok(); }
 	f16x8* prep(hipStream_t s, bool inference) {
 		f16x8* f = (f16x8*)(inference ? frags_inf : frags).get((size_t)n_all_frags * 1024);
 		if (inference) sync_inference(s);
@@ -346,12 +339,10 @@ struct ngp_model {
 		}
 		sc_hist_done = false;
 		GridHist h;
-		const bool xcd = grid_forward_mode == 2;  // auto = per-sample rows: measured faster (DESIGN.md §Grid forward)
-		const bool fuse = want_hist && fused_hist && use_sorted(n) && !sc_prepared && (xcd || grid_forward_rows_ok(grid, a)) &&
+		const bool fuse = want_hist && fused_hist && use_sorted(n) && !sc_prepared && grid_forward_rows_ok(grid, a) &&
 		                  scatter_hist(grid, sc_plan_for(n), sorted_workspace(n), h);
-		h.stage0 = grid_stage0 ? 1u : 0u;
 		ProfScope ps("grid_forward", s);
-		grid_forward(grid, a, s, fuse ? &h : nullptr, xcd ? 2 : 1);
+		grid_forward(grid, a, s, fuse ? &h : nullptr);
 		sc_hist_done = fuse;
 	}
 	void run_mlp(hipStream_t s, MlpMode mode, uint32_t n, const float* in, uint32_t stride, const f16* encbuf, f16* out,
@@ -375,16 +366,12 @@ struct ngp_model {
 			a.n_matrix = (uint32_t)n_matrix(); a.density_woff = 0; a.rgb_woff = (uint32_t)mlp0_params;
 			a.dL_dsh = dL_dsh;
 			if (ex) { a.dL_ddens = ex->ddens; a.ddens_stride = ex->ddens_stride; }
-			a.params = pick(inference);
-			a.train16 = mlp_train16 ? 1u : 0u;
-			a.pipe = mlp_pipe ? 1u : 0u;
-			if (mode == MLP_INFER_ENC || mode == MLP_TRAIN_ENC || mode == MLP_DENSITY_ENC) {
+			if (mode == MLP_INFER_ENC) {
 				if (inference) sync_inference(s);
 				a.table = pick(inference) + grid_offset(); a.max_level = max_level; a.gc = make_grid_const(grid);
 			}
 			ProfScope ps(mode == MLP_TRAIN ? "mlp_train" : mode == MLP_DENSITY ? "mlp_density"
-			             : mode == MLP_INFER_ENC ? "mlp_infer_enc" : mode == MLP_TRAIN_ENC ? "mlp_train_enc"
-			             : mode == MLP_DENSITY_ENC ? "mlp_density_enc"
+			             : mode == MLP_INFER_ENC ? "mlp_infer_enc"
 			             : mode == MLP_DENSITY_TRAIN ? "mlp_density_train" : "mlp_infer", s);
 			nerf_mlp_run(nplan, mode, a, s);
 		} else {
@@ -407,8 +394,8 @@ struct ngp_model {
 		const uint32_t blocks = nerf ? nerf_mlp_train_blocks(n) : mlp_train_blocks(n);
 		float* slab = (float*)slabs.get((size_t)blocks * n_matrix() * sizeof(float));
 		f16* dsh = ex.dL_dinput && nerf && !ex.density_only ? (f16*)dsh_ws.get((size_t)n * 16 * sizeof(f16)) : nullptr;
-		// encbuf == nullptr: the MLP kernel encodes the positions itself (fused_training_ok)
-		const MlpMode mode = ex.density_only ? MLP_DENSITY_TRAIN : encbuf ? MLP_TRAIN : MLP_TRAIN_ENC;
+		NGP_CHECK(encbuf, "train_pass: the encoding buffer");
+		const MlpMode mode = ex.density_only ? MLP_DENSITY_TRAIN : MLP_TRAIN;
 		run_mlp(s, mode, n, in, stride, encbuf, out, out_stride, AoS, (const f16*)dL, dL_stride, dL_denc, slab, ex.inference, &ex,
 		        dsh);
 		// dL/dinput through the grid (position rows) and the SH encoding (direction rows, NerfNetwork). Run
@@ -426,6 +413,7 @@ struct ngp_model {
 			input_gradient();
 			return;
 		}
+		grads_valid = !(fopt && (fopt->rec || fopt->g32));
 		// the dW slab reduction (MLP section of the gradient) and the grid backward (grid section) are
 		// independent: for large batches the reduction runs in extra blocks of the grid backward's last
 		// kernel (fuse_slabs, default), or on the side stream under it (overlap bit 4). The density-only
@@ -650,6 +638,17 @@ struct ngp_graph {
 	ngp_trainer* trainer = nullptr;
 	uint32_t steps_per_launch = 1;
 	uint64_t ws_epoch = 0;  // the model's workspace epoch at capture
+	// the graph holds a sharded exchange over world > 1 ranks: every launch leaves the other ranks' optimizer
+	// records stale on this rank again (ngp_trainer_gather_shards)
+	bool shards_stale = false;
+	// the graph's backward writes the gradient for the sharded exchange as fp32 only: g16 is not written
+	bool g16_stale = false;
+	void launched() {
+		trainer->step += steps_per_launch;
+		if (steps_per_launch && trainer->rec) trainer->inf_stale = trainer->w32_stale = true;
+		if (shards_stale) trainer->shards_valid = false;
+		if (g16_stale) trainer->model->grads_valid = false;
+	}
 	~ngp_graph() {
 		if (exec) (void)hipGraphExecDestroy(exec);
 		if (graph) (void)hipGraphDestroy(graph);
@@ -853,29 +852,16 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 		} else if (k == "overlap") {
 			NGP_CHECK(value >= 0 && value <= 15, "overlap is a bitmask in [0, 15]");
 			m->overlap = (uint32_t)value;
-		} else if (k == "grid_forward_mode") {
-			NGP_CHECK(value == 0 || value == 1 || value == 2, "grid_forward_mode must be 0 (auto), 1 (rows), 2 (XCD-partitioned)");
-			m->grid_forward_mode = (int)value;
 		} else if (k == "fused_hist") {
 			m->fused_hist = value != 0;
 		} else if (k == "fuse_infer") {
 			m->fuse_infer = value != 0;
-		} else if (k == "fuse_density") {
-			m->fuse_density = value != 0;
-		} else if (k == "fuse_train") {
-			m->fuse_train = value != 0;
-		} else if (k == "mlp_pipe") {
-			m->mlp_pipe = value != 0;
-		} else if (k == "mlp_train16") {
-			m->mlp_train16 = value != 0;
 		} else if (k == "fuse_slabs") {
 			m->fuse_slabs = value != 0;
 		} else if (k == "fuse_opt") {
 			m->fuse_opt = value != 0;
 		} else if (k == "fuse_mlp_opt") {
 			m->fuse_mlp_opt = value != 0;
-		} else if (k == "grid_stage0") {
-			m->grid_stage0 = value != 0;
 		} else if (k == "grid_bricks") {
 			m->grid_bricks = value != 0;
 			m->sc_plan_n = 0;  // re-plan at the next batch
@@ -950,24 +936,17 @@ int ngp_encoding_backward(ngp_model* m, void* stream, uint32_t n, const float* i
 
 }  // extern "C"
 // NerfNetwork::density (ngp_density's body): the density network's output rows in `output_layout` (AoS, SoA, or
-// MLP_LAYOUT_ROW0 for the density grid update, which reads row 0 only). With the fused encoding the MLP kernel
-// gathers the grid levels itself (k_nerf_mlp<MLP_DENSITY_ENC>: the integers and the blend of the grid forward,
-// so the same bits).
+// MLP_LAYOUT_ROW0 for the density grid update, which reads row 0 only).
 int ngp::density_impl(ngp_model* m, void* stream, uint32_t n, const float* input, uint32_t input_stride, void* output,
                       uint32_t output_stride, uint32_t output_layout, int use_inference_params) {
 	NGP_TRY({
 		NGP_CHECK(m->nerf, "density() is a NerfNetwork method");
 		if (n == 0) return NGP_OK;
 		m->require_params(use_inference_params);
-		if (m->fused_density_ok()) {
-			m->run_mlp(S(stream), MLP_DENSITY_ENC, n, input, input_stride, nullptr, (f16*)output, output_stride, output_layout, nullptr,
-			           0, nullptr, nullptr, use_inference_params);
-		} else {
-			f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
-			m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, use_inference_params);
-			m->run_mlp(S(stream), MLP_DENSITY, n, input, input_stride, e, (f16*)output, output_stride, output_layout, nullptr, 0,
-			           nullptr, nullptr, use_inference_params);
-		}
+		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
+		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, use_inference_params);
+		m->run_mlp(S(stream), MLP_DENSITY, n, input, input_stride, e, (f16*)output, output_stride, output_layout, nullptr, 0,
+		           nullptr, nullptr, use_inference_params);
 		m->generation++;
 	});
 }
@@ -1121,16 +1100,9 @@ int ngp::forward_backward_with(ngp_model* m, void* stream, uint32_t n, const flo
 		f16* e = (f16*)m->enc.get((size_t)n * m->enc_width * sizeof(f16));
 		m->generation++;
 		m->prepare_grid_backward_async(S(stream), n, input, input_stride);
-		if (m->fused_training_ok()) {
-			// no encoding pass: the MLP kernel encodes, the sorted backward counts its own histogram
-			m->sc_hist_done = false;
-			m->train_pass(S(stream), n, input, input_stride, nullptr, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode,
-			              BwdExtra{}, fopt);
-		} else {
-			m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, false, true);
-			m->train_pass(S(stream), n, input, input_stride, e, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode,
-			              BwdExtra{}, fopt);
-		}
+		m->encode(S(stream), n, input, input_stride, e, m->enc_width, AoS, false, true);
+		m->train_pass(S(stream), n, input, input_stride, e, (f16*)output, output_stride, dL_doutput, dL_stride, grad_mode,
+		              BwdExtra{}, fopt);
 	});
 }
 extern "C" {
@@ -1381,6 +1353,8 @@ int ngp::capture_training_step_with(ngp_trainer* t, void* stream, uint32_t n, co
 		hipGraph_t graph = nullptr;
 		const hipError_t end = hipStreamEndCapture(s, &graph);
 		g->ws_epoch = m->ws_epoch;
+		g->shards_stale = with_optimizer && t->sharded(ex) && ex.world > 1;
+		g->g16_stale = !m->grads_valid;
 		if (rc != NGP_OK) {
 			if (graph) (void)hipGraphDestroy(graph);
 			throw Error(g_last_error);
@@ -1403,8 +1377,7 @@ void ngp::graph_launch_ctl_written(ngp_graph* g, void* stream) {
 	NGP_CHECK(g && g->exec, "graph launch: no graph");
 	NGP_CHECK(g->ws_epoch == g->trainer->model->ws_epoch, "graph launch: the model's workspaces were reallocated since capture");
 	NGP_HIP(hipGraphLaunch(g->exec, S(stream)));
-	g->trainer->step += g->steps_per_launch;
-	if (g->steps_per_launch && g->trainer->rec) g->trainer->inf_stale = g->trainer->w32_stale = true;
+	g->launched();
 }
 
 extern "C" {
@@ -1475,14 +1448,16 @@ int ngp_graph_launch(ngp_graph* g, void* stream) {
 		          "pass grew them); capture again (ngp_model_workspace_epoch tells when)");
 		if (g->steps_per_launch) set_device_ctl(g->trainer->ctl, g->trainer->step, g->trainer->cfg, S(stream));
 		NGP_HIP(hipGraphLaunch(g->exec, S(stream)));
-		g->trainer->step += g->steps_per_launch;
-		if (g->steps_per_launch && g->trainer->rec) g->trainer->inf_stale = g->trainer->w32_stale = true;
+		g->launched();
 	});
 }
 
 void ngp_graph_destroy(ngp_graph* g) { delete g; }
 
 void* ngp_trainer_gradients(ngp_trainer* t) { return t ? t->g16 : nullptr; }
+int ngp_trainer_gradients_valid(const ngp_trainer* t) {
+	return t && t->model->gradients == t->g16 && t->model->grads_valid ? 1 : 0;
+}
 void* ngp_trainer_params(ngp_trainer* t) { return t ? t->w16 : nullptr; }
 void* ngp_trainer_inference_params(ngp_trainer* t) {
 	if (!t) return nullptr;

@@ -61,13 +61,11 @@ struct GridHist {
 	uint32_t B, n_chunks, chunk;
 	uint32_t vb_base[33];
 	uint32_t brick_first = 0, brick_levels = 0, n_bricks = 0, brick_cells = 8, bricks_per_dim = 0, brick_vb0 = 0;  // levels [first, levels)
-	uint32_t stage0 = 0;  // row kernel: level 0's table staged in LDS when dense and <= 32 KB
 };
 
 // mode: 0/1 per-sample kernels, 2 XCD-partitioned (level, chunk) kernel (L2-local tables; measured
 // slower than the per-sample row kernel on C2 and C2p, kept as an option)
-void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist = nullptr, int mode = 0);
-bool grid_forward_xcd_ok(const GridDesc& g, const GridFwdArgs& a);
+void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist = nullptr);
 // true when grid_forward writes whole AoS rows (padding columns included: no memset needed)
 bool grid_forward_rows_ok(const GridDesc& g, const GridFwdArgs& a);
 void grid_backward(const GridDesc& g, const GridBwdArgs& a, hipStream_t stream);

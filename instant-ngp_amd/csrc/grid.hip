@@ -127,25 +127,15 @@ __global__ void __launch_bounds__(256) k_grid_forward(const GridConst c, const G
                            // F >= 4 only (C2 forward 28.9 -> 27.3 us; with 16 levels of F = 2 the index arrays cost
                            // registers: C2' step 350 -> 393 us, profiles/r03bp)
 #endif
-// STAGE0 (training forward, dense level 0 of at most 32 KB: C2's 4096 x 4 fp16): the block copies level
-// 0's table into LDS with coalesced 16-B loads and gathers its corners there, so 512 samples cost the L2 256
-// line requests instead of 2048 scattered corner-pair requests (the forward is bound by the L2's request
-// rate). Same values, same arithmetic: bit-identical.
-template <uint32_t D, uint32_t F, bool HIST, bool STAGE0 = false>
+template <uint32_t D, uint32_t F, bool HIST>
 __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const GridConst c, const GridFwdArgs a, const GridHist h) {
 	typedef typename FeatVec<F>::T V;
 	constexpr uint32_t MAXL = 32 / F;
 	extern __shared__ __attribute__((aligned(16))) uint32_t hl[];  // HIST: [vb_base[L]] bucket counts of this chunk
-	f16* t0 = nullptr;  // STAGE0: level 0's table, after the counts (16-B aligned)
 	if constexpr (HIST) {
 		for (uint32_t j = threadIdx.x; j < h.vb_base[c.n_levels]; j += blockDim.x) hl[j] = 0;
+		__syncthreads();
 	}
-	if constexpr (STAGE0) {
-		t0 = (f16*)(hl + ((h.vb_base[c.n_levels] + 3u) & ~3u));
-		const uint32_t n16 = c.offsets[1] * F / 8;  // 16-B chunks (level sizes are multiples of 8 entries)
-		for (uint32_t j = threadIdx.x; j < n16; j += blockDim.x) ((f16x8*)t0)[j] = ((const f16x8*)a.table)[j];
-	}
-	if constexpr (HIST || STAGE0) __syncthreads();
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i < a.n) {
 	float x[D];
@@ -182,14 +172,14 @@ __global__ void __launch_bounds__(HIST ? 512 : 256) k_grid_forward_rows(const Gr
 #pragma unroll
 					for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&hl[h.vb_base[l] + ((cidx[k] - c.offsets[l]) >> h.B)], 1u);
 				}
-				gather_corners_at<D, F>(cidx, (STAGE0 && l == 0) ? t0 : a.table, v);
+				gather_corners_at<D, F>(cidx, a.table, v);
 			} else {
 				if (count) {
 #pragma unroll
 					for (uint32_t k = 0; k < (1u << D); ++k)
 						atomicAdd(&hl[h.vb_base[l] + ((corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B)], 1u);
 				}
-				gather_corners<D, F>(c, l, base, (STAGE0 && l == 0) ? t0 : a.table, v);
+				gather_corners<D, F>(c, l, base, a.table, v);
 			}
 #pragma unroll
 			for (uint32_t k = 0; k < (1u << D); ++k) {
@@ -276,140 +266,6 @@ bool grid_forward_rows_ok(const GridDesc& g, const GridFwdArgs& a) {
 	       ((uintptr_t)a.out & 15) == 0;
 }
 
-// XCD-partitioned forward: work = (level, chunk of 512 samples) blocks, ordered so that every block
-// of a level runs on the same XCD slot (blocks are dealt round-robin over the 8 XCDs: b % 8 names a
-// slot, MI355X_MICROARCH §Workgroup dispatch — for speed only, never correctness). Each XCD's 4 MiB L2
-// then holds the tables of its own levels instead of all of them: the gathers hit in L2 instead of
-// the Infinity Cache. L >= 8: slot x owns levels x, x + 8, ... (level-major, all chunks); L < 8
-// (8 % L == 0): slot x owns level x % L and every (8 / L)-th chunk.
-constexpr uint32_t XCD_SLOTS = 8;
-constexpr uint32_t XCD_CHUNK = 512;
-
-struct XcdMap {
-	uint32_t n_chunks, rounds, lpx, reps;  // lpx: levels per slot (L >= 8); reps: slots per level (L < 8)
-};
-
-__host__ __device__ inline XcdMap make_xcd_map(uint32_t n, uint32_t L) {
-	XcdMap m;
-	m.n_chunks = (n + XCD_CHUNK - 1) / XCD_CHUNK;
-	if (L >= XCD_SLOTS) {
-		m.lpx = (L + XCD_SLOTS - 1) / XCD_SLOTS; m.reps = 1;
-		m.rounds = m.lpx * m.n_chunks;
-	} else {
-		m.lpx = 1; m.reps = XCD_SLOTS / L;
-		m.rounds = (m.n_chunks + m.reps - 1) / m.reps;
-	}
-	return m;
-}
-
-template <uint32_t D, uint32_t F, bool HIST>
-__global__ void __launch_bounds__(256) k_grid_forward_xcd(const GridConst c, const GridFwdArgs a, const XcdMap m, const GridHist h) {
-	typedef typename FeatVec<F>::T V;
-	extern __shared__ uint32_t hl[];  // HIST: this (level, chunk)'s bucket counts
-	const uint32_t slot = blockIdx.x % XCD_SLOTS, r = blockIdx.x / XCD_SLOTS;
-	uint32_t l, chunk;
-	if (m.reps == 1) { l = slot + XCD_SLOTS * (r / m.n_chunks); chunk = r % m.n_chunks; }
-	else { l = slot % c.n_levels; chunk = r * m.reps + slot / c.n_levels; }
-	if (l >= c.n_levels || chunk >= m.n_chunks) return;
-	uint32_t nvb = 0, vb0 = 0;
-	// bricks: the block of the finest brick level counts each sample's brick, coarser brick levels nothing
-	const bool brick_counter = HIST && D == 3 && l + 1 == h.brick_levels;
-	const bool brick_level = l >= h.brick_first && l < h.brick_levels;
-	if constexpr (HIST) {
-		nvb = brick_level ? (brick_counter ? h.n_bricks : 0u) : h.vb_base[l + 1] - h.vb_base[l];
-		vb0 = brick_level ? h.brick_vb0 : h.vb_base[l];
-		for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) hl[j] = 0;
-		__syncthreads();
-	}
-#pragma unroll
-	for (uint32_t q = 0; q < XCD_CHUNK / 256; ++q) {
-		const uint32_t i = chunk * XCD_CHUNK + q * 256 + threadIdx.x;
-		if (i >= a.n) break;
-		float x[D];
-#pragma unroll
-		for (uint32_t d = 0; d < D; ++d) x[d] = a.pos[(size_t)i * a.pos_stride + d];
-		const float ml = (a.max_level_per_sample ? a.max_level_per_sample[i] : a.max_level) * (float)c.n_levels;
-		const bool active = !((float)l >= ml + 1e-3f);
-		float acc[F];
-#pragma unroll
-		for (uint32_t f = 0; f < F; ++f) acc[f] = 0.f;
-		float frac[D]; uint32_t base[D];
-		level_setup<D>(c, l, x, frac, base);
-		if constexpr (HIST) {
-			if constexpr (D == 3) {
-				if (brick_counter) atomicAdd(&hl[brick_of(c, l, h.brick_cells, h.bricks_per_dim, x)], 1u);
-			}
-			if (!brick_level) {
-#pragma unroll
-				for (uint32_t k = 0; k < (1u << D); ++k) atomicAdd(&hl[(corner_index<D>(c, l, base, k) - c.offsets[l]) >> h.B], 1u);
-			}
-		}
-		if (active) {
-			V v[1u << D];
-			gather_corners<D, F>(c, l, base, a.table, v);
-#pragma unroll
-			for (uint32_t k = 0; k < (1u << D); ++k) {
-				const float w = corner_weight<D>(frac, k);
-				if constexpr (F == 1) acc[0] = __builtin_fmaf(w, (float)v[k], acc[0]);
-				else {
-#pragma unroll
-					for (uint32_t f = 0; f < F; ++f) acc[f] = __builtin_fmaf(w, (float)v[k][f], acc[f]);
-				}
-			}
-		}
-#pragma unroll
-		for (uint32_t f = 0; f < F; ++f) asm volatile("" : "+v"(acc[f]));
-		if (a.out_layout == AoS) {
-			V o;
-			if constexpr (F == 1) o = (f16)acc[0];
-			else {
-#pragma unroll
-				for (uint32_t f = 0; f < F; ++f) o[f] = (f16)acc[f];
-			}
-			*(V*)(a.out + (size_t)i * a.out_stride + l * F) = o;
-		} else {
-#pragma unroll
-			for (uint32_t f = 0; f < F; ++f) a.out[(size_t)(l * F + f) * a.out_stride + i] = (f16)acc[f];
-		}
-	}
-	if constexpr (HIST) {
-		__syncthreads();
-		for (uint32_t j = threadIdx.x; j < nvb; j += blockDim.x) h.hist[(size_t)chunk * h.vb_base[c.n_levels] + vb0 + j] = hl[j];
-	}
-}
-
-bool grid_forward_xcd_ok(const GridDesc& g, const GridFwdArgs& a) {
-	return a.n >= 16384 && (g.n_levels >= XCD_SLOTS || XCD_SLOTS % g.n_levels == 0) &&
-	       (a.out_layout != AoS || a.out_stride == g.n_levels * g.n_features);
-}
-
-template <uint32_t D>
-static void launch_fwd_xcd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hipStream_t s, const GridHist* h) {
-	const XcdMap m = make_xcd_map(a.n, c.n_levels);
-	const dim3 grid(XCD_SLOTS * m.rounds);
-	if (h) NGP_CHECK(h->chunk == XCD_CHUNK && h->n_chunks == m.n_chunks, "grid forward histogram: chunk mismatch");
-	uint32_t max_lb = 0;
-	if (h) for (uint32_t l = 0; l < c.n_levels; ++l) max_lb = std::max(max_lb, h->vb_base[l + 1] - h->vb_base[l]);
-	if (h) max_lb = std::max(max_lb, h->n_bricks);
-	const size_t lds = (size_t)max_lb * 4;
-	const GridHist none{};
-	auto go = [&](auto kern_nohist, auto kern_hist) {
-		if (h) {
-			ensure_dynamic_lds((const void*)kern_hist, lds);
-			kern_hist<<<grid, 256, lds, s>>>(c, a, m, *h);
-		} else {
-			kern_nohist<<<grid, 256, 0, s>>>(c, a, m, none);
-		}
-	};
-	switch (F) {
-		case 1: go(k_grid_forward_xcd<D, 1, false>, k_grid_forward_xcd<D, 1, true>); return;
-		case 2: go(k_grid_forward_xcd<D, 2, false>, k_grid_forward_xcd<D, 2, true>); return;
-		case 4: go(k_grid_forward_xcd<D, 4, false>, k_grid_forward_xcd<D, 4, true>); return;
-		case 8: go(k_grid_forward_xcd<D, 8, false>, k_grid_forward_xcd<D, 8, true>); return;
-		default: throw Error("GridEncoding: unsupported F");
-	}
-}
-
 template <uint32_t D>
 static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hipStream_t s, bool rows, const GridHist* h) {
 	const dim3 grid(div_round_up(a.n, 256)), block(256);
@@ -417,24 +273,16 @@ static void launch_fwd(uint32_t F, const GridConst& c, const GridFwdArgs& a, hip
 		NGP_CHECK(rows && h->chunk == 512, "grid forward histogram: needs the row kernel and 512-sample chunks");
 		const dim3 grid_h(div_round_up(a.n, 512));
 		NGP_CHECK(grid_h.x == h->n_chunks, "grid forward histogram: chunk count mismatch");
-		// level 0 staged in LDS when dense and <= 32 KB (engine option grid_stage0, default on)
-		const size_t t0_bytes = (size_t)c.offsets[1] * F * 2;
-		const bool stage0 = h->stage0 && !(c.hashed & 1u) && t0_bytes <= 32 * 1024 && ((uintptr_t)a.table & 15u) == 0;
-		const size_t lds = (((size_t)h->vb_base[c.n_levels] + 3) & ~(size_t)3) * 4 + (stage0 ? t0_bytes : 0);
-		auto go = [&](auto kern, auto kern_s) {
-			if (stage0) {
-				ensure_dynamic_lds((const void*)kern_s, lds);
-				kern_s<<<grid_h, 512, lds, s>>>(c, a, *h);
-			} else {
-				ensure_dynamic_lds((const void*)kern, lds);
-				kern<<<grid_h, 512, lds, s>>>(c, a, *h);
-			}
+		const size_t lds = (size_t)h->vb_base[c.n_levels] * 4;
+		auto go = [&](auto kern) {
+			ensure_dynamic_lds((const void*)kern, lds);
+			kern<<<grid_h, 512, lds, s>>>(c, a, *h);
 		};
 		switch (F) {
-			case 1: go(k_grid_forward_rows<D, 1, true>, k_grid_forward_rows<D, 1, true, true>); return;
-			case 2: go(k_grid_forward_rows<D, 2, true>, k_grid_forward_rows<D, 2, true, true>); return;
-			case 4: go(k_grid_forward_rows<D, 4, true>, k_grid_forward_rows<D, 4, true, true>); return;
-			case 8: go(k_grid_forward_rows<D, 8, true>, k_grid_forward_rows<D, 8, true, true>); return;
+			case 1: go(k_grid_forward_rows<D, 1, true>); return;
+			case 2: go(k_grid_forward_rows<D, 2, true>); return;
+			case 4: go(k_grid_forward_rows<D, 4, true>); return;
+			case 8: go(k_grid_forward_rows<D, 8, true>); return;
 			default: throw Error("GridEncoding: unsupported F");
 		}
 	}
@@ -594,16 +442,9 @@ void grid_input_gradient(const GridDesc& g, const InputGradArgs& a, hipStream_t 
 	NGP_HIP(hipGetLastError());
 }
 
-void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist, int mode) {
+void grid_forward(const GridDesc& g, const GridFwdArgs& a, hipStream_t stream, const GridHist* hist) {
 	if (a.n == 0) return;
 	GridConst c = make_grid_const(g);
-	if (mode == 2) {
-		NGP_CHECK(grid_forward_xcd_ok(g, a), "grid forward: the XCD-partitioned kernel does not apply");
-		if (g.n_dims == 3) launch_fwd_xcd<3>(g.n_features, c, a, stream, hist);
-		else launch_fwd_xcd<2>(g.n_features, c, a, stream, hist);
-		NGP_HIP(hipGetLastError());
-		return;
-	}
 	const bool rows = grid_forward_rows_ok(g, a);
 	if (g.n_dims == 3) launch_fwd<3>(g.n_features, c, a, stream, rows, hist);
 	else launch_fwd<2>(g.n_features, c, a, stream, rows, hist);

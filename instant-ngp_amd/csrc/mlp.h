@@ -51,7 +51,7 @@ struct NerfMlpArgs {
 	uint32_t n_matrix;                            // matrix params = density MLP + rgb MLP
 	uint32_t n_reg;                               // LDS regions of the dW block reduction (set at launch)
 	uint32_t density_woff, rgb_woff;              // parameter offsets of the two MLPs
-	// MLP_INFER_ENC / MLP_TRAIN_ENC: the density network's input is encoded in the kernel (hash-grid gather and
+	// MLP_INFER_ENC: the density network's input is encoded in the kernel (hash-grid gather and
 	// trilinear blend of the sample's levels, same arithmetic as k_grid_forward_rows) instead of read
 	const f16* table;                             // grid parameters [entries x F]
 	float max_level;                              // tcnn set_max_level (global; per-sample masks not fused)
@@ -62,12 +62,6 @@ struct NerfMlpArgs {
 	// MLP_DENSITY_TRAIN (NerfNetwork::density_backward, nerf_network.h:384-428): dL/d(density network output),
 	// fp16 AoS [n x ddens_stride] (16 rows; stride a multiple of 4)
 	const f16* dL_ddens; uint32_t ddens_stride;
-	// the fp16 parameters the fragments are built from (k_nerf_mlp_train16 builds its own from them) and
-	// whether MLP_TRAIN may run k_nerf_mlp_train16 (model option "mlp_train16")
-	const f16* params;
-	uint32_t train16;
-	// whether MLP_TRAIN runs the software-pipelined k_nerf_mlp_train_pipe (model option "mlp_pipe")
-	uint32_t pipe;
 };
 
 struct MlpArgs {  // single MLP behind an encoding (tcnn::NetworkWithInputEncoding): image / SDF
@@ -100,11 +94,9 @@ MlpPlan make_mlp_plan(uint32_t enc_width, uint32_t width, uint32_t hidden, uint3
 
 void prepare_frags(const FragDesc* descs_dev, uint32_t n_frags, const f16* params, f16x8* frags, hipStream_t s);
 
-enum MlpMode : uint32_t { MLP_INFER = 0, MLP_TRAIN = 1, MLP_DENSITY = 2, MLP_INFER_ENC = 3, MLP_TRAIN_ENC = 4,
-                          MLP_DENSITY_TRAIN = 5,   // density network forward + backward only (NeRF)
-                          MLP_DENSITY_ENC = 6 };   // MLP_DENSITY with the encoding gathered in the kernel
-// MLP_INFER_ENC / MLP_TRAIN_ENC / MLP_DENSITY_ENC are fused for 3D grids with 4 levels of 4 features (one 16-wide
-// encoding step: C2)
+enum MlpMode : uint32_t { MLP_INFER = 0, MLP_TRAIN = 1, MLP_DENSITY = 2, MLP_INFER_ENC = 3,
+                          MLP_DENSITY_TRAIN = 5 };  // density network forward + backward only (NeRF)
+// MLP_INFER_ENC is fused for 3D grids with 4 levels of 4 features (one 16-wide encoding step: C2)
 // internal output layout of the density network: row 0 only, as a flat array of n (the density grid update
 // reads nothing else)
 constexpr uint32_t MLP_LAYOUT_ROW0 = 3;  // == DENSITY_LAYOUT_ROW0 (engine_internal.h)
@@ -113,8 +105,6 @@ bool nerf_mlp_fused_encoding_ok(const GridDesc& g, uint32_t enc_width);
 // Launch sizes for the training kernel: one persistent block per CU (slab count = blocks).
 uint32_t nerf_mlp_train_blocks(uint32_t n);
 void nerf_mlp_run(const NerfMlpPlan& p, MlpMode mode, const NerfMlpArgs& a, hipStream_t s);
-// MLP_TRAIN at two waves per SIMD (mlp_train16.hip); false when the configuration is not covered
-bool nerf_mlp_train16_run(const NerfMlpPlan& p, const NerfMlpArgs& a, hipStream_t s);
 uint32_t mlp_train_blocks(uint32_t n);
 void mlp_run(const MlpPlan& p, MlpMode mode, const MlpArgs& a, hipStream_t s);
 

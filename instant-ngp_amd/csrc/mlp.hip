@@ -235,43 +235,6 @@ __device__ __forceinline__ void img_store_acc(f16* img, int stride, const f16x8*
 	}
 }
 
-// k_nerf_mlp_train_pipe variants (experiment knobs): NGP_PIPE_FENCE, a scheduling fence between its
-// pairs of layers (no instruction moves across it); NGP_PIPE_RELOAD, the backward reads the tile's
-// activations back from its image instead of keeping them in registers
-#ifndef NGP_PIPE_FENCE
-#define NGP_PIPE_FENCE 1
-#endif
-#ifndef NGP_PIPE_RELOAD
-#define NGP_PIPE_RELOAD 1
-#endif
-#if NGP_PIPE_FENCE
-#define NGP_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define NGP_SCHED_FENCE() do {} while (0)
-#endif
-#if NGP_PIPE_RELOAD
-#define NGP_PIPE_ACT(act, reg, im) img_load_acc<4>(im, Lay::S_64, act, lane)
-#else
-#define NGP_PIPE_ACT(act, reg, im) do { for (int q_ = 0; q_ < 4; ++q_) act[q_] = reg[q_]; } while (0)
-#endif
-
-// Read back what img_store_acc wrote: the packed accumulator-layout fragments of one sample column.
-// The address is laundered so the compiler cannot forward the stored registers (which would keep them
-// live: the point of reading back is to free them).
-template <int NFRAG>
-__device__ __forceinline__ void img_load_acc(const f16* img, int stride, f16x8* f, int lane) {
-	const int smp = lane & 31, h = lane >> 5;
-	int idx = smp * stride + 4 * h;
-	asm volatile("" : "+v"(idx));
-	const f16* row = img + idx;
-#pragma unroll
-	for (int q = 0; q < NFRAG; ++q) {
-		const int base = 32 * (q >> 1) + 16 * (q & 1);
-		const f16x4 lo = *(const f16x4*)(row + base), hi = *(const f16x4*)(row + base + 8);
-		f[q] = f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-	}
-}
-
 // Standard-order fragment (lane half h holds features 16s + 8h + 0..7) into the image.
 __device__ __forceinline__ void img_store_std(f16* img, int stride, const f16x8& f, int s, int lane) {
 	const int smp = lane & 31, h = lane >> 5;
@@ -479,9 +442,9 @@ template <int ES, int DH, int RH, int MODE>
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_nerf_mlp(const NerfMlpArgs a) {
 	using Lay = NerfLayout<ES, DH, RH>;
 	constexpr bool DTRAIN = MODE == MLP_DENSITY_TRAIN;  // density network forward + backward only
-	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_TRAIN_ENC || DTRAIN;
-	constexpr bool DENSITY = MODE == MLP_DENSITY || MODE == MLP_DENSITY_ENC;
-	constexpr bool FUSE = MODE == MLP_INFER_ENC || MODE == MLP_TRAIN_ENC || MODE == MLP_DENSITY_ENC;
+	constexpr bool TRAIN = MODE == MLP_TRAIN || DTRAIN;
+	constexpr bool DENSITY = MODE == MLP_DENSITY;
+	constexpr bool FUSE = MODE == MLP_INFER_ENC;
 	static_assert(!FUSE || ES == 1, "fused encoding: one 16-wide encoding step");
 	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (DENSITY ? Lay::F_R0 : Lay::N_FWD);
 	extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -943,9 +906,8 @@ __device__ __forceinline__ void train_store_dw(const f32x4* dw, const NerfMlpArg
 	dw_store<1, ES>(dw + T::W_D0, slab, dw0, 16 * ES, wave, 0, lane);
 }
 
-template <int ES, int DH, int RH, bool FUSE>
+template <int ES, int DH, int RH>
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_nerf_mlp_train(const NerfMlpArgs a) {
-	static_assert(!FUSE || ES == 1, "fused encoding: one 16-wide encoding step");
 	using Lay = NerfLayout<ES, DH, RH>;
 	using T = NerfTrainLayout<ES, DH, RH>;
 	extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -975,59 +937,15 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	f16x8 xe_n[ES];
 	float cd_n[3];
 	f16x4 dl_n;
-	// FUSE (MLP_TRAIN_ENC): the encoding is gathered here, as in k_nerf_mlp's MLP_INFER_ENC path (lane
-	// half h blends levels 2h, 2h+1 with k_grid_forward_rows' arithmetic, one tile ahead)
-	f16x4 graw[FUSE ? 2 : 1][8];
-	float gfrac[FUSE ? 2 : 1][3];
-	float px_n[3];
-	uint32_t lv_off[2], lv_T[2], lv_res[2];
-	float lv_scale[2];
-	bool lv_hashed[2], lv_active[2];
-	if constexpr (FUSE) {
-		const float ml = a.max_level * (float)a.gc.n_levels;
-#pragma unroll
-		for (int j = 0; j < 2; ++j) {
-			const uint32_t l0 = j, l1 = 2 + j;
-			lv_off[j] = h ? a.gc.offsets[l1] : a.gc.offsets[l0];
-			lv_T[j] = h ? a.gc.offsets[l1 + 1] - a.gc.offsets[l1] : a.gc.offsets[l0 + 1] - a.gc.offsets[l0];
-			lv_res[j] = h ? a.gc.resolution[l1] : a.gc.resolution[l0];
-			lv_scale[j] = h ? a.gc.scale[l1] : a.gc.scale[l0];
-			lv_hashed[j] = (a.gc.hashed >> (h ? l1 : l0)) & 1u;
-			lv_active[j] = !((float)(h ? l1 : l0) >= ml + 1e-3f);
-		}
-	}
-	auto load_pos = [&](uint32_t tile) {
-		const uint32_t smp = tile * 32 + (lane & 31);
-		const float* cp = a.coords + (size_t)(smp < a.n ? smp : 0) * a.coord_stride;
-		px_n[0] = cp[0]; px_n[1] = cp[1]; px_n[2] = cp[2];
-	};
 	auto load_inputs = [&](uint32_t tile) {
 		const uint32_t smp = tile * 32 + (lane & 31);
 		const uint32_t ls = smp < a.n ? smp : 0;
-		if constexpr (FUSE) {
-			const float x[3] = {px_n[0], px_n[1], px_n[2]};
-			load_pos(tile + gridDim.x * 4);
 #pragma unroll
-			for (int j = 0; j < 2; ++j) {
-				uint32_t gb[3];
-#pragma unroll
-				for (int d = 0; d < 3; ++d) {
-					const float p = __builtin_fmaf(lv_scale[j], x[d], 0.5f);
-					const float t = floorf(p);
-					gb[d] = (uint32_t)(int)t;
-					gfrac[j][d] = p - t;
-				}
-				fuse_gather_level(a.table + (size_t)lv_off[j] * 4, gb, lv_res[j], lv_T[j], lv_hashed[j], lv_active[j], graw[j]);
-			}
-		} else {
-#pragma unroll
-			for (int s = 0; s < ES; ++s) xe_n[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
-		}
+		for (int s = 0; s < ES; ++s) xe_n[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
 		const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
 		cd_n[0] = cd[0]; cd_n[1] = cd[1]; cd_n[2] = cd[2];
 		dl_n = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
 	};
-	if constexpr (FUSE) load_pos(blockIdx.x * 4 + wave);
 	load_inputs(blockIdx.x * 4 + wave);
 	// every wave runs the same number of iterations (the barriers need all four); tiles past the end
 	// run on zero inputs and zero output gradients, so their dW contribution is exactly zero
@@ -1036,29 +954,8 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		const uint32_t sample = tile * 32 + (lane & 31);
 		const bool valid = sample < a.n;
 		f16x8 xe[ES];
-		if constexpr (FUSE) {
-			// trilinear blend in k_grid_forward_rows' order (fp32 FMAs, one RNE rounding per feature)
-			f16x8 r;
 #pragma unroll
-			for (int j = 0; j < 2; ++j) {
-				float acc4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-				for (uint32_t k = 0; k < 8; ++k) {
-					const float w = corner_weight<3>(gfrac[j], k);
-#pragma unroll
-					for (int f = 0; f < 4; ++f) acc4[f] = __builtin_fmaf(w, (float)graw[j][k][f], acc4[f]);
-				}
-#pragma unroll
-				for (int f = 0; f < 4; ++f) {
-					asm volatile("" : "+v"(acc4[f]));
-					r[4 * j + f] = (f16)acc4[f];
-				}
-			}
-			xe[0] = valid ? r : f16x8{};
-		} else {
-#pragma unroll
-			for (int s = 0; s < ES; ++s) xe[s] = valid ? xe_n[s] : f16x8{};
-		}
+		for (int s = 0; s < ES; ++s) xe[s] = valid ? xe_n[s] : f16x8{};
 		const float cdx = cd_n[0], cdy = cd_n[1], cdz = cd_n[2];
 		const f16x4 dl_cur = dl_n;
 		load_inputs(tile + gridDim.x * 4);  // unconditional (past-the-end tiles read sample 0)
@@ -1168,273 +1065,11 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	train_store_dw<ES, DH, RH>(dw, a, wave, lane);
 }
 
-// ------------------------------------------------------------------------------------------------
-// The same training pass, software-pipelined across tiles (option mlp_pipe, NGP_MLP_PIPE)
-// ------------------------------------------------------------------------------------------------
-// In k_nerf_mlp_train a wave's phase A is one dependent chain (layer MFMAs -> fp16 pack -> next
-// layer) at one wave per SIMD, so every MFMA result latency and every pack sits on the critical path.
-// Here phase A of iteration i runs the backward dX chain of tile i and the forward chain of the wave's
-// next tile, i + 1, as two independent chains written layer by layer in alternation, so one chain's
-// packs issue while the other's MFMAs run. Tile i + 1's forward activations stay in registers until
-// the next iteration stores them to the (then free) image. Per tile the operations and the image
-// contents are those of k_nerf_mlp_train, and phase B is the same function: dW, dL/dinput and the
-// outputs are bit-identical.
-template <int ES, int DH, int RH>
-struct TrainTileFwd {
-	f16x8 xe[ES];      // encoding (B-operand order)
-	f16x8 hd[DH][4];   // density hidden activations
-	f16x8 dout;        // density network output rows 0..15 (rgb input rows 0..15)
-	f16x8 sh;          // SH encoding (rgb input rows 16..31)
-	f16x8 hr[RH][4];   // rgb hidden activations
-	f16x4 dl;          // dL/d(output) of the tile's sample
-};
-
-template <int ES, int DH, int RH>
-__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_nerf_mlp_train_pipe(const NerfMlpArgs a) {
-	using Lay = NerfLayout<ES, DH, RH>;
-	using T = NerfTrainLayout<ES, DH, RH>;
-	extern __shared__ __attribute__((aligned(16))) char smem[];
-	const int lane = threadIdx.x & 63, h = lane >> 5;
-	const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	f16* img_all = (f16*)smem;
-	f16* img = img_all + wave * T::IMG_HALVES;
-
-	f16x8 wreg[Lay::N_FWD], breg[T::N_BWD];
-#pragma unroll
-	for (int q = 0; q < Lay::N_FWD; ++q) wreg[q] = a.frags[q * 64 + lane];
-#pragma unroll
-	for (int q = 0; q < T::N_BWD; ++q) breg[q] = a.frags[(Lay::N_FWD + q) * 64 + lane];
-#pragma unroll
-	for (int q = 0; q < Lay::N_FWD; ++q) asm volatile("" : "+a"(wreg[q]));
-#pragma unroll
-	for (int q = 0; q < T::N_BWD; ++q) asm volatile("" : "+a"(breg[q]));
-	f32x4 dw[T::N_DW];
-#pragma unroll
-	for (int q = 0; q < T::N_DW; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-	const uint32_t n_tiles = (a.n + 31) / 32;
-	const uint32_t stride = gridDim.x * 4;
-	f16x8 xe_n[ES];
-	float cd_n[3];
-	f16x4 dl_n;
-	f16x8 sh_n;  // SH encoding of the prefetched tile, computed once its directions arrive (make_sh)
-	auto load_inputs = [&](uint32_t tile) {
-		const uint32_t smp = tile * 32 + (lane & 31);
-		const uint32_t ls = smp < a.n ? smp : 0;
-#pragma unroll
-		for (int s = 0; s < ES; ++s) xe_n[s] = *(const f16x8*)(a.enc + (size_t)ls * a.enc_stride + 16 * s + 8 * h);
-		const float* cd = a.coords + (size_t)ls * a.coord_stride + a.dir_offset;
-		cd_n[0] = cd[0]; cd_n[1] = cd[1]; cd_n[2] = cd[2];
-		dl_n = *(const f16x4*)(a.dL_dout + (size_t)ls * a.dL_stride);
-	};
-	// forward layer steps of one tile (each a layer's MFMAs and its pack), called in alternation with
-	// the backward steps of the previous tile
-	// sh4_frag branches on the lane half; it runs outside phase A so that phase A stays one region
-	auto make_sh = [&](uint32_t tile) {
-		sh_n = tile * 32 + (lane & 31) < a.n ? sh4_frag(cd_n[0], cd_n[1], cd_n[2], h) : f16x8{};
-	};
-	auto take_inputs = [&](TrainTileFwd<ES, DH, RH>& f, uint32_t tile) {
-		const bool valid = tile * 32 + (lane & 31) < a.n;
-#pragma unroll
-		for (int s = 0; s < ES; ++s) f.xe[s] = valid ? xe_n[s] : f16x8{};
-		f.sh = sh_n;
-		f.dl = dl_n;
-	};
-	auto fwd_d0 = [&](TrainTileFwd<ES, DH, RH>& f) {
-		f32x16 acc[2];
-		layer_fwd_reg<2, ES>(acc, f.xe, wreg, Lay::F_D0);
-		pack_tiles<2>(acc, f.hd[0], true);
-	};
-	auto fwd_dh = [&](TrainTileFwd<ES, DH, RH>& f, int l) {
-		f32x16 acc[2];
-		layer_fwd_reg<2, 4>(acc, f.hd[l - 1], wreg, Lay::F_DH + 8 * (l - 1));
-		pack_tiles<2>(acc, f.hd[l], true);
-	};
-	auto fwd_do = [&](TrainTileFwd<ES, DH, RH>& f) {
-		f32x16 dacc[1];
-		layer_fwd_reg<1, 4>(dacc, f.hd[DH - 1], wreg, Lay::F_DO);
-		f16x8 hi;
-		pack_tile(dacc[0], f.dout, hi, false);
-	};
-	auto fwd_r0 = [&](TrainTileFwd<ES, DH, RH>& f) {
-		f32x16 acc[2];
-		const f16x8 rin[2] = {f.dout, f.sh};
-		layer_fwd_reg<2, 2>(acc, rin, wreg, Lay::F_R0);
-		pack_tiles<2>(acc, f.hr[0], true);
-	};
-	auto fwd_rh = [&](TrainTileFwd<ES, DH, RH>& f, int l) {
-		f32x16 acc[2];
-		layer_fwd_reg<2, 4>(acc, f.hr[l - 1], wreg, Lay::F_RH + 8 * (l - 1));
-		pack_tiles<2>(acc, f.hr[l], true);
-	};
-	// the rgb output rows 0..15 with the density in row 3 (extract_density, nerf_network.h:32-43)
-	auto fwd_ro = [&](TrainTileFwd<ES, DH, RH>& f) {
-		f32x16 racc[1];
-		layer_fwd_reg<1, 4>(racc, f.hr[RH - 1], wreg, Lay::F_RO);
-		f16x8 ro, ro_hi;
-		pack_tile(racc[0], ro, ro_hi, false);
-		ro[3] = h == 0 ? f.dout[0] : ro[3];
-		return ro;
-	};
-
-	TrainTileFwd<ES, DH, RH> t_a, t_b;
-	{
-		TrainTileFwd<ES, DH, RH>& cur = t_a;
-		// prologue: the wave's first tile's forward, and the inputs of its second tile requested
-		const uint32_t t0 = blockIdx.x * 4 + wave;
-		load_inputs(t0);
-		make_sh(t0);
-		take_inputs(cur, t0);
-		load_inputs(t0 + stride);
-		fwd_d0(cur);
-#pragma unroll
-		for (int l = 1; l < DH; ++l) fwd_dh(cur, l);
-		fwd_do(cur);
-		fwd_r0(cur);
-#pragma unroll
-		for (int l = 1; l < RH; ++l) fwd_rh(cur, l);
-		const f16x8 ro = fwd_ro(cur);
-		const uint32_t s0 = t0 * 32 + (lane & 31);
-		if (a.out && s0 < a.n) store_out16(a.out, a.out_stride, a.out_layout, a.n, s0, h, ro);
-		make_sh(t0 + stride);
-	}
-	// one iteration: tile `base + wave` (forward done, in `cur`) and the next tile's forward into `nxt`.
-	// Every wave runs the same number of iterations (the barriers need all four); tiles past the end
-	// run on zero inputs and zero output gradients, so their dW contribution is exactly zero.
-	// Phase A has no branch (its global stores wait until the end), so the two chains form one
-	// scheduling region; the backward reads the tile's activations back from its image (conflict-free
-	// ds_read_b64) instead of keeping them in registers.
-	auto step = [&](TrainTileFwd<ES, DH, RH>& cur, TrainTileFwd<ES, DH, RH>& nxt, uint32_t base) {
-		const uint32_t tile = base + wave, ntile = tile + stride;
-		const uint32_t sample = tile * 32 + (lane & 31), nsample = ntile * 32 + (lane & 31);
-		const bool valid = sample < a.n;
-
-		// ---- tile's forward images (its activations were computed last iteration) ------------------
-#pragma unroll
-		for (int s = 0; s < ES; ++s) img_store_std(img + T::I_XE, Lay::S_XE, cur.xe[s], s, lane);
-#pragma unroll
-		for (int l = 0; l < DH; ++l) img_store_acc<4>(img + T::I_HD + l * 32 * Lay::S_64, Lay::S_64, cur.hd[l], lane);
-		{
-			f16x8 d1[1] = {cur.dout};
-			img_store_acc<1>(img + T::I_RIN, Lay::S_RIN, d1, lane);
-			img_store_std(img + T::I_RIN, Lay::S_RIN, cur.sh, 1, lane);
-		}
-#pragma unroll
-		for (int l = 0; l < RH; ++l) img_store_acc<4>(img + T::I_HR + l * 32 * Lay::S_64, Lay::S_64, cur.hr[l], lane);
-		const f16x4 dl_cur = valid ? cur.dl : f16x4{};
-
-		// the next tile's inputs (requested last iteration), and the one after requested now
-		take_inputs(nxt, ntile);
-		load_inputs(ntile + stride);  // unconditional (past-the-end tiles read sample 0)
-
-		// ---- phase A: tile's backward dX chain || next tile's forward chain -------------------------
-		// sched_barrier between the pairs of layers: the scheduler interleaves the two chains within a
-		// pair but does not hoist later loads and MFMAs, which would raise the register pressure past the
-		// file (spills)
-		f32x16 acc[2];
-		f16x8 dz[4], act[4];
-		const float dsig = (float)dl_cur[3];
-		NGP_SCHED_FENCE();
-		{
-			f16x8 dz1[1];
-			dz1[0] = h == 0 ? f16x8{dl_cur[0], dl_cur[1], dl_cur[2], (f16)0.f, 0, 0, 0, 0} : f16x8{};  // extract_rgb (:46-60)
-			img_store_acc<1>(img + T::I_ZRO, T::S_16, dz1, lane);
-			NGP_PIPE_ACT(act, cur.hr[RH - 1], img + T::I_HR + (RH - 1) * 32 * Lay::S_64);
-			layer_fwd_reg<2, 1>(acc, dz1, breg, Lay::B_RO - Lay::N_FWD);
-			mask_pack<2>(acc, act, dz);
-		}
-		fwd_d0(nxt);
-		NGP_SCHED_FENCE();
-#pragma unroll
-		for (int l = RH - 1; l >= 1; --l) {
-			img_store_acc<4>(img + T::I_ZRH + (RH - 1 - l) * 32 * Lay::S_64, Lay::S_64, dz, lane);
-			NGP_PIPE_ACT(act, cur.hr[l - 1], img + T::I_HR + (l - 1) * 32 * Lay::S_64);
-			layer_fwd_reg<2, 4>(acc, dz, breg, Lay::B_RH - Lay::N_FWD + 8 * (RH - 1 - l));
-			mask_pack<2>(acc, act, dz);
-			if (RH - 1 - l + 1 < DH) fwd_dh(nxt, RH - 1 - l + 1);
-			NGP_SCHED_FENCE();
-		}
-#pragma unroll
-		for (int l = RH; l < DH; ++l) fwd_dh(nxt, l);
-		f16x8 dd[1], dsh;
-		{
-			img_store_acc<4>(img + T::I_ZR0, Lay::S_64, dz, lane);
-			f32x16 a1[1];
-			layer_fwd_reg<1, 4>(a1, dz, breg, Lay::B_R0 - Lay::N_FWD);
-			pack_tile(a1[0], dd[0], dsh, false);  // dsh: rows 16..31 of dL/d(rgb input) = dL/d(SH encoding)
-			dd[0][0] = h == 0 ? (f16)((float)dd[0][0] + dsig) : dd[0][0];  // add_density_gradient (:63-74)
-			img_store_acc<1>(img + T::I_ZDO, T::S_16, dd, lane);
-		}
-		fwd_do(nxt);
-		NGP_SCHED_FENCE();
-		NGP_PIPE_ACT(act, cur.hd[DH - 1], img + T::I_HD + (DH - 1) * 32 * Lay::S_64);
-		layer_fwd_reg<2, 1>(acc, dd, breg, Lay::B_DO - Lay::N_FWD);
-		mask_pack<2>(acc, act, dz);
-		fwd_r0(nxt);
-		NGP_SCHED_FENCE();
-#pragma unroll
-		for (int l = DH - 1; l >= 1; --l) {
-			img_store_acc<4>(img + T::I_ZDH + (DH - 1 - l) * 32 * Lay::S_64, Lay::S_64, dz, lane);
-			NGP_PIPE_ACT(act, cur.hd[l - 1], img + T::I_HD + (l - 1) * 32 * Lay::S_64);
-			layer_fwd_reg<2, 4>(acc, dz, breg, Lay::B_DH - Lay::N_FWD + 8 * (DH - 1 - l));
-			mask_pack<2>(acc, act, dz);
-			if (DH - l < RH) fwd_rh(nxt, DH - l);
-			NGP_SCHED_FENCE();
-		}
-#pragma unroll
-		for (int l = DH; l < RH; ++l) {
-			fwd_rh(nxt, l);
-			NGP_SCHED_FENCE();
-		}
-		img_store_acc<4>(img + T::I_ZD0, Lay::S_64, dz, lane);
-		f16x8 de[2 * Lay::ET];  // dL/d(encoding): tile t's rows in de[2t] (lo) and de[2t + 1] (hi)
-		{
-			f32x16 ae[Lay::ET];
-			layer_fwd_reg<Lay::ET, 4>(ae, dz, breg, Lay::B_D0 - Lay::N_FWD);
-#pragma unroll
-			for (int t = 0; t < Lay::ET; ++t) pack_tile(ae[t], de[2 * t], de[2 * t + 1], false);
-		}
-		const f16x8 ro = fwd_ro(nxt);
-		NGP_SCHED_FENCE();
-
-		// ---- global stores of phase A; the SH of the tile after next ----------------------------------
-		make_sh(ntile + stride);
-		if (a.out && nsample < a.n) store_out16(a.out, a.out_stride, a.out_layout, a.n, nsample, h, ro);
-		if (a.dL_dsh && valid) store_dsh(a.dL_dsh, sample, h, dsh);
-		if (a.dL_denc && valid) {
-#pragma unroll
-			for (int t = 0; t < Lay::ET; ++t) {
-				f16* row = a.dL_denc + (size_t)sample * a.denc_stride + 32 * t + 4 * h;
-				const f16x8 lo = de[2 * t], hi = de[2 * t + 1];
-				*(f16x4*)(row + 0) = f16x4{lo[0], lo[1], lo[2], lo[3]};
-				*(f16x4*)(row + 8) = f16x4{lo[4], lo[5], lo[6], lo[7]};
-				if (32 * t + 16 < 16 * ES) {
-					*(f16x4*)(row + 16) = f16x4{hi[0], hi[1], hi[2], hi[3]};
-					*(f16x4*)(row + 24) = f16x4{hi[4], hi[5], hi[6], hi[7]};
-				}
-			}
-		}
-		__syncthreads();
-
-		// ---- phase B: this wave's quarter of dW over the four images (one operand set: the next tile's
-		// forward record is live across it) ---------------------------------------------------------------
-		train_phase_b<ES, DH, RH, false>(dw, img_all, wave, lane);
-		__syncthreads();
-	};
-	// (the record copy is free: the register allocator coalesces it; unrolling by two with the roles
-	// swapped instead measured 145 more live registers and spills)
-	for (uint32_t base = blockIdx.x * 4; base < n_tiles; base += stride) {
-		step(t_a, t_b, base);
-		t_a = t_b;
-	}
-	train_store_dw<ES, DH, RH>(dw, a, wave, lane);
-}
-
 template <int ES, int DH, int RH, int MODE>
 static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	using Lay = NerfLayout<ES, DH, RH>;
-	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_TRAIN_ENC || MODE == MLP_DENSITY_TRAIN;
-	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (MODE == MLP_DENSITY || MODE == MLP_DENSITY_ENC ? Lay::F_R0 : Lay::N_FWD);
+	constexpr bool TRAIN = MODE == MLP_TRAIN || MODE == MLP_DENSITY_TRAIN;
+	constexpr int NFRAG = TRAIN ? Lay::N_ALL : (MODE == MLP_DENSITY ? Lay::F_R0 : Lay::N_FWD);
 	size_t lds = (size_t)NFRAG * 1024 + (TRAIN ? 4 * Lay::IMG_HALVES * sizeof(f16) : 0);
 	uint32_t n_reg = 4;
 	while (n_reg > 1 && (size_t)n_reg * a.n_matrix * sizeof(float) > 160 * 1024) n_reg /= 2;
@@ -1445,8 +1080,7 @@ static void launch_nerf(const NerfMlpArgs& a, hipStream_t s) {
 	if (blocks == 0) return;
 	if constexpr (TRAIN && MODE != MLP_DENSITY_TRAIN && NerfTrainLayout<ES, DH, RH>::LDS_BYTES <= 160 * 1024 && Lay::N_ALL <= 44) {
 		// weight gradients split across the waves, all fragments in registers (k_nerf_mlp_train)
-		void (*kt)(const NerfMlpArgs) = k_nerf_mlp_train<ES, DH, RH, MODE == MLP_TRAIN_ENC>;
-		if (MODE == MLP_TRAIN && a.pipe) kt = k_nerf_mlp_train_pipe<ES, DH, RH>;
+		void (*kt)(const NerfMlpArgs) = k_nerf_mlp_train<ES, DH, RH>;
 		const size_t lt = NerfTrainLayout<ES, DH, RH>::LDS_BYTES;
 		ensure_dynamic_lds((const void*)kt, lt);
 		kt<<<blocks, 256, lt, s>>>(a);
@@ -1498,15 +1132,12 @@ static void dispatch_nerf_fused(const NerfMlpPlan& p, const NerfMlpArgs& a, hipS
 
 void nerf_mlp_run(const NerfMlpPlan& p, MlpMode mode, const NerfMlpArgs& a, hipStream_t s) {
 	if (a.n == 0) return;
-	if (mode == MLP_TRAIN && a.train16 && nerf_mlp_train16_run(p, a, s)) return;
 	switch (mode) {
 		case MLP_INFER: dispatch_nerf<MLP_INFER>(p, a, s); break;
 		case MLP_TRAIN: dispatch_nerf<MLP_TRAIN>(p, a, s); break;
 		case MLP_DENSITY: dispatch_nerf<MLP_DENSITY>(p, a, s); break;
 		case MLP_INFER_ENC: dispatch_nerf_fused<MLP_INFER_ENC>(p, a, s); break;
-		case MLP_TRAIN_ENC: dispatch_nerf_fused<MLP_TRAIN_ENC>(p, a, s); break;
 		case MLP_DENSITY_TRAIN: dispatch_nerf<MLP_DENSITY_TRAIN>(p, a, s); break;
-		case MLP_DENSITY_ENC: dispatch_nerf_fused<MLP_DENSITY_ENC>(p, a, s); break;
 	}
 }
 

@@ -1359,17 +1359,37 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const Camera* __restrict__ c
 		*(f16x4*)(dl + (size_t)jj * 16) = g;
 	};
 	if (LANES != LG || a.state) {  // pass 1 kept every composited sample's state: no sequential compositing here
-		for (uint32_t jj = L; jj < cn; jj += LANES) {
+		if ((size_t)base + cn <= a.state_cap) {
+			for (uint32_t jj = L; jj < cn; jj += LANES) {
+				float cc[7];
+#pragma unroll
+				for (int k = 0; k < 7; ++k) cc[k] = ci[(size_t)jj * 7 + k];
+				const f16x4 o = *(const f16x4*)(out + (size_t)jj * a.out_stride);
+				const size_t si = (size_t)base + jj;
+				const float my_w = a.state[si], my_t = a.state[a.state_cap + si];
+				const float my_r2[3] = {a.state[2 * a.state_cap + si], a.state[3 * a.state_cap + si], a.state[4 * a.state_cap + si]};
+				float rgb[3];
+				for (int k = 0; k < 3; ++k) rgb[k] = network_to_rgb((float)o[k], cfg.rgb_activation);
+				emit(jj, cc, o, rgb, unwarp_dt(cc[3]), my_w, my_t, my_r2);
+			}
+			return;
+		}
+		// the ray's samples reach past the caller's state capacity (pass 1 kept no state there): every lane
+		// composites the ray in sample order itself, with pass 1's operations, and emits its own samples
+		float t = 1.f, r2[3] = {0.f, 0.f, 0.f};
+		for (uint32_t jj = 0; jj < cn; ++jj) {
 			float cc[7];
 #pragma unroll
 			for (int k = 0; k < 7; ++k) cc[k] = ci[(size_t)jj * 7 + k];
 			const f16x4 o = *(const f16x4*)(out + (size_t)jj * a.out_stride);
-			const size_t si = (size_t)base + jj;
-			const float my_w = a.state[si], my_t = a.state[a.state_cap + si];
-			const float my_r2[3] = {a.state[2 * a.state_cap + si], a.state[3 * a.state_cap + si], a.state[4 * a.state_cap + si]};
 			float rgb[3];
 			for (int k = 0; k < 3; ++k) rgb[k] = network_to_rgb((float)o[k], cfg.rgb_activation);
-			emit(jj, cc, o, rgb, unwarp_dt(cc[3]), my_w, my_t, my_r2);
+			const float dt = unwarp_dt(cc[3]);
+			const float alpha = 1.f - ngp_expf_fast(-network_to_density((float)o[3], cfg.density_activation) * dt);
+			const float weight = alpha * t;
+			r2[0] = r2[0] + weight * rgb[0]; r2[1] = r2[1] + weight * rgb[1]; r2[2] = r2[2] + weight * rgb[2];
+			t = t * (1.f - alpha);
+			if (jj % LANES == L) emit(jj, cc, o, rgb, dt, weight, t, r2);
 		}
 		return;
 	}
@@ -1458,6 +1478,7 @@ void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs&
 		exclusive_scan(craw, cbase, a.n_rays, scan_tmp, scan_bytes, s);
 	}
 	ProfScope ps("loss_pass2", s);
+	static_assert(NGP_LOSS_SELECT, "pass 1 keeps the compositing state pass 2 reads only in its select form");
 	if (a.state) {
 		constexpr uint32_t W = NGP_LOSS2_LANES;  // a wave per ray: see k_loss_pass2
 		k_loss_pass2<W><<<div_round_up((size_t)a.n_rays * W, 256), 256, 0, s>>>(ds.d_cams, cfg, a, craw, cbase, lr);

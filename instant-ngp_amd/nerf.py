@@ -135,12 +135,13 @@ def generate_training_samples(ds, cfg, n_rays, rng, max_samples, bitfield, ray_o
 
 
 def compute_loss(ds, cfg, n_rays, rng, max_compacted, samples, network_output, mean_density, loss_scale=128.0,
-                 n_rays_total=None, stream=None, error_map=None, keep_state=False):
+                 n_rays_total=None, stream=None, error_map=None, keep_state=False, state_capacity=None):
     """compute_loss_kernel_train_nerf (testbed_nerf.cu:1660-2012). `samples` is the dict returned by
     generate_training_samples (its numsteps is rewritten to the compacted {n, base}). error_map: a
     float32 device tensor [n_images, h, w] the compacted rays' losses are added into (:1869-1899).
     keep_state: pass 1 keeps each composited sample's state for pass 2 (ngp_nerf_compute_loss_state, the
-    training step's form; same outputs bit for bit)."""
+    training step's form; same outputs bit for bit). state_capacity: samples the kept state holds (default: every
+    sample slot); rays reaching past it are composited again by pass 2, with the same result."""
     dev = network_output.device
     # the kernel reads one output row per sample; samples never exceed the sampler's coords buffer
     if network_output.shape[0] < samples["coords"].shape[0]:
@@ -159,7 +160,7 @@ def compute_loss(ds, cfg, n_rays, rng, max_compacted, samples, network_output, m
     if keep_state:
         if error_map is not None:
             raise ValueError("keep_state: without error_map (the C-ABI form has no error-map argument)")
-        cap = samples["coords"].shape[0]
+        cap = samples["coords"].shape[0] if state_capacity is None else int(state_capacity)
         state = torch.empty((5, cap), dtype=torch.float32, device=dev)
         check(lib().ngp_nerf_compute_loss_state(*args, _ptr(state), cap))
     elif error_map is None:

@@ -381,6 +381,12 @@ class Trainer:
         of the gradient buffer is then not written)."""
         return bool(lib().ngp_trainer_fused_update_active(self.handle, int(n_batch)))
 
+    @property
+    def gradients_valid(self):
+        """False when the last step did not write `gradients` (the fused grid update or the sharded
+        data-parallel step took the gradient without storing it as fp16): the buffer is an older one."""
+        return bool(lib().ngp_trainer_gradients_valid(self.handle))
+
     def capture_training_step(self, x, dL_doutput, loss_scale=128.0, n_steps=1, with_optimizer=True, stream=None):
         """Engine extension: n_steps of forward_backward(x, dL_doutput) [+ optimizer_step] captured into
         one HIP graph (TrainingGraph.launch replays it). `stream` must not be the null stream."""

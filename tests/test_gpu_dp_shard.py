@@ -25,6 +25,14 @@ pytestmark = pytest.mark.gpu
 STEPS = 6
 
 
+@pytest.fixture(scope="module")
+def pkg():
+    from __graft_entry__ import load_package
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return load_package()
+
+
 def _h(t):
     return hashlib.sha1(t.cpu().numpy().tobytes()).hexdigest()
 
@@ -146,3 +154,44 @@ def test_sharded_optimizer_rccl_world1_equals_fused_step(tmp_path):
     r = json.load(open(tmp_path / "w1.json"))
     assert r["plain"] == r["shard"]
     assert r["shard"][3] == 11
+
+
+class _NoopComm:
+    """A world-2 exchange that moves nothing (rank 0 of 2): capturable, so it drives the captured sharded step's
+    host bookkeeping on one GPU. Numerically meaningless; only the staleness rules are checked with it."""
+
+    def __init__(self, pkg):
+        self.rank, self.world, self.handle = 0, 2, None
+        self.fn = pkg.dp.ALLREDUCE_FN(lambda user, buf, count, dtype, op, stream: 0)
+
+
+def test_captured_sharded_step_invalidates_state_at_every_launch(pkg):
+    """A captured sharded step over world > 1 leaves the other ranks' records stale at EVERY launch, not only
+    while it is recorded: after gather_shards, a further launch must make serialize / the EMA parameters fail
+    again. Its backward stores the gradient as fp32 only, so gradients_valid is False after it and
+    True again after a plain forward_backward."""
+    n = 1 << 14
+    x, dl = _batch(0, 0, n)
+    cfg = pkg.nerf_config("C2")
+    net = pkg.create_nerf_network(cfg)
+    tr = pkg.Trainer(net, cfg["optimizer"], seed=1337)
+    net.reserve(n)
+    comm = _NoopComm(pkg)
+    tr.set_data_parallel(comm)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        g = tr.capture_training_step(x, dl, 128.0, n_steps=1, stream=s)
+    for _ in range(2):
+        with torch.cuda.stream(s):
+            g.launch(s)
+        s.synchronize()
+        with pytest.raises(pkg.NgpError, match="gather_shards"):
+            tr.serialize()
+        assert not tr.gradients_valid
+        tr.gather_shards()  # the no-op all-gather "restores" the records: the reads are allowed again
+        tr.serialize()
+    net.forward_backward(x, dl)
+    torch.cuda.synchronize()
+    assert tr.gradients_valid
+    del g
+    tr.set_data_parallel(None)

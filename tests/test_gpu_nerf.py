@@ -225,7 +225,9 @@ def test_compute_loss(pkg, orc, scene, loss_type, act, aabb_scale):
 def test_compute_loss_kept_state_is_bitwise_equal(pkg, scene, orc, loss_type, act, aabb_scale):
     """The training step's form of the loss (pass 1 keeps each composited sample's weight, transmittance and
     rgb prefix; pass 2 reads them instead of compositing each ray again) gives the same bits as the two
-    compositing passes: compacted count, {n, base}, coordinates, losses and dL/doutput."""
+    compositing passes: compacted count, {n, base}, coordinates, losses and dL/doutput. Also with a state
+    capacity shorter than the samples (a C-ABI caller's smaller buffer): pass 2 composites the rays past it
+    again instead of reading unwritten state, with the same bits."""
     ds, ims, pix = scene
     cfg = pkg.nerf.default_config(aabb_scale, loss_type=loss_type, rgb_activation=act, density_activation=3)
     _, bf = occupancy(orc, seed=3, frac=0.5, max_cascade=cfg.max_cascade)
@@ -235,16 +237,19 @@ def test_compute_loss_kept_state_is_bitwise_equal(pkg, scene, orc, loss_type, ac
     out_t = torch.from_numpy(g.uniform(-3.0, 2.0, (max_samples, 16)).astype(np.float16)).cuda()
     mean = torch.tensor([0.003], device="cuda")
     res = []
-    for keep in (False, True):
+    for keep, cap in ((False, None), (True, None), (True, "short")):
         samples = pkg.nerf.generate_training_samples(ds, cfg, n_rays, r, max_samples, torch.from_numpy(bf).cuda())
-        got = pkg.nerf.compute_loss(ds, cfg, n_rays, r, max_c, samples, out_t, mean, keep_state=keep)
+        if cap == "short":  # about a third of the generated samples
+            cap = max(1, int(samples["counters"][1].item()) // 3)  # counters = {rays kept, samples}
+        got = pkg.nerf.compute_loss(ds, cfg, n_rays, r, max_c, samples, out_t, mean, keep_state=keep, state_capacity=cap)
         torch.cuda.synchronize()
         res.append({"ns": samples["numsteps"].cpu().numpy(), **{k: v.cpu().numpy() for k, v in got.items()}})
-    a, b = res
+    a = res[0]
     assert int(a["compacted_counter"][0]) > 0
-    for k in ("ns", "compacted_counter", "coords_compacted", "loss"):
-        np.testing.assert_array_equal(a[k].view(np.uint32), b[k].view(np.uint32), err_msg=k)
-    np.testing.assert_array_equal(a["dloss_doutput"].view(np.uint16), b["dloss_doutput"].view(np.uint16))
+    for b in res[1:]:
+        for k in ("ns", "compacted_counter", "coords_compacted", "loss"):
+            np.testing.assert_array_equal(a[k].view(np.uint32), b[k].view(np.uint32), err_msg=k)
+        np.testing.assert_array_equal(a["dloss_doutput"].view(np.uint16), b["dloss_doutput"].view(np.uint16))
 
 
 @pytest.mark.parametrize("dtype,rescale", [(torch.float32, False), (torch.float16, False), (torch.float16, True)])

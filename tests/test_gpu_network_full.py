@@ -79,15 +79,12 @@ def check_close(name, got, ref, cond, margin=None):
                   f"{np.sort(margin[rows])[-3:].tolist()}; {int((margin < MARGIN).sum())} samples that close)")
 
 
-@pytest.mark.parametrize("train16", [1, 0])
 @pytest.mark.parametrize("cfg_name,log2T,L,F", [("C2", 19, 4, 4), ("C2p", 19, 16, 2)])
-def test_nerf_network_full_batch(pkg, orc, cfg_name, log2T, L, F, train16, record_property):
-    """train16 = 1: the two-waves-per-SIMD training kernel (mlp_train16.hip, option mlp_train16);
-    0: k_nerf_mlp_train (mlp.hip), the default."""
+def test_nerf_network_full_batch(pkg, orc, cfg_name, log2T, L, F, record_property):
+    """The training kernel k_nerf_mlp_train (mlp.hip) at full size against the oracle."""
     cfg = pkg.nerf_config(cfg_name)
     cfg["encoding"]["log2_hashmap_size"] = log2T
     net = pkg.create_nerf_network(cfg)
-    net.set_option("mlp_train16", train16)
     tr = pkg.Trainer(net, cfg["optimizer"])
     nm = net.n_matrix_params
     # trained-looking parameters: Xavier MLP (initialize_params), grid entries U(-0.5, 0.5)
@@ -167,35 +164,3 @@ def test_sdf_training_step_c5_full_batch(pkg, orc, log2T):
     ref_grid = orc.grid_backward_exact(grid, x, got_denc.view(np.uint16))
     np.testing.assert_array_equal(got_g[nm:].view(np.uint16), ref_grid)
     print("\n".join(msgs))
-
-
-@pytest.mark.parametrize("n", [1 << 18, (1 << 18) - 37, 4096 + 37, 1000, 33])
-@pytest.mark.parametrize("cfg_name", ["C2", "C2p"])
-def test_mlp_pipe_bitwise(pkg, cfg_name, n):
-    """Option mlp_pipe (k_nerf_mlp_train_pipe: each wave's next tile forward interleaved with its current
-    tile's backward) against k_nerf_mlp_train: output, dL/d(encoding) and the MLP gradients bit for bit,
-    at full size, ragged batches and batches of at most one tile per wave; the grid gradients too where
-    the grid backward is the sorted (deterministic) one, n >= 4096 (below, its fp16 atomics make two
-    runs of the same kernel differ)."""
-    cfg = pkg.nerf_config(cfg_name)
-    net = pkg.create_nerf_network(cfg)
-    tr = pkg.Trainer(net, cfg["optimizer"])
-    nm = net.n_matrix_params
-    p = net.initialize_params(1337)
-    p[nm:] = np.random.default_rng(3).uniform(-0.5, 0.5, p.size - nm).astype(np.float32)
-    tr.set_params_full_precision(p)
-    c = torch.from_numpy(coords_batch(n, seed=21)).cuda()
-    dL = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
-    dL[:, :4] = torch.from_numpy(np.random.default_rng(22).uniform(-1, 1, (n, 4)).astype(np.float16)).cuda()
-    res = []
-    for pipe in (0, 1):
-        net.set_option("mlp_pipe", pipe)
-        out = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
-        net.forward_backward(c, dL, output=out)
-        torch.cuda.synchronize()
-        res.append((out.clone(), net.workspace("dL_dencoding", n).clone(), tr.gradients.clone()))
-    net.set_option("mlp_pipe", 0)
-    for name, a, b in zip(("output", "dL/dencoding", "gradients"), res[0], res[1]):
-        if name == "gradients" and n < 4096:
-            a, b = a[:nm], b[:nm]
-        assert torch.equal(a.view(torch.int16), b.view(torch.int16)), name

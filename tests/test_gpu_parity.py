@@ -141,25 +141,6 @@ def test_nerf_density(pkg, orc, nerf_setup):
     assert np.array_equal(soa.T, out)
 
 
-@pytest.mark.parametrize("n", [1, 33, 2000, 70001])
-def test_nerf_density_fused_bitwise(pkg, nerf_setup, n):
-    """NerfNetwork::density with the encoding gathered inside the MLP kernel (option fuse_density, on by
-    default) against encode-then-MLP (fuse_density 0): both layouts, bit for bit, including positions
-    outside [0, 1] (the dense levels' index wraps like tcnn's index % T)."""
-    net, tr, p16, m = nerf_setup
-    c = coords_batch(n, seed=40 + n)
-    c[::7, :3] = c[::7, :3] * 9.0 - 4.0  # far out of the unit cube: dense indices beyond 2 T take the modulo branch
-    x = torch.from_numpy(c).cuda()
-    res = {}
-    for fused in (0, 1):
-        net.set_option("fuse_density", fused)
-        for layout in (pkg.LAYOUT_AOS, pkg.LAYOUT_SOA):
-            res[fused, layout] = net.density(x, layout=layout, use_inference_params=False).clone()
-    net.set_option("fuse_density", 1)
-    for layout in (pkg.LAYOUT_AOS, pkg.LAYOUT_SOA):
-        assert torch.equal(res[0, layout].view(torch.int16), res[1, layout].view(torch.int16)), layout
-
-
 @pytest.mark.parametrize("n", [32, 777, 4096])
 def test_nerf_forward_backward(pkg, orc, nerf_setup, n):
     net, tr, p16, m = nerf_setup
@@ -332,7 +313,6 @@ def test_large_batch_properties(pkg, nerf_setup):
     dL = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
     dL[:, :4] = (torch.rand((n, 4), device="cuda") - 0.5).half() * 0.01
     out = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
-    net.set_option("mlp_train16", 1)  # the two-waves-per-SIMD kernel (option, off by default)
     net.forward_backward(c, dL, output=out)
     g1 = tr.gradients.float().clone()
     net.forward_backward(c, dL * 2, output=out)
@@ -341,13 +321,8 @@ def test_large_batch_properties(pkg, nerf_setup):
     assert torch.isfinite(out).all()
     nm = net.n_matrix_params
     assert torch.allclose(g2[:nm], 2 * g1[:nm], rtol=2e-3, atol=1e-3)
+    # k_nerf_mlp_train lays out and sums each layer like the inference kernel: the same output bit for bit
     ref_out = net.inference(c, use_inference_params=False)
-    # the inference kernel (32x32x16 MFMAs) and the two-wave training kernel (16x16x32) sum each layer's fp32
-    # products in different groupings: outputs agree to the fp16 rounding of the intermediates, and the
-    # k_nerf_mlp_train kernel (the inference kernel's layout) reproduces the inference output bit for bit
-    assert torch.allclose(out.float(), ref_out.float(), rtol=1e-2, atol=2e-3)
-    net.set_option("mlp_train16", 0)  # the default kernel
-    net.forward_backward(c, dL, output=out)
     torch.cuda.synchronize()
     assert torch.equal(ref_out, out)
 
@@ -452,34 +427,6 @@ def test_training_graph_matches_eager(pkg):
         runs.append((tr.params_full_precision.cpu().numpy().copy(), tr.inference_params.float().cpu().numpy().copy()))
     np.testing.assert_array_equal(runs[1][0], runs[0][0])
     np.testing.assert_array_equal(runs[1][1], runs[0][1])
-
-
-@pytest.mark.parametrize("n", [777, 4096, 50000])
-def test_fused_encoding_training_matches_unfused(pkg, nerf_setup, n):
-    """forward_backward with the encoding inside the MLP training kernel (option fuse_train, off by default)
-    gives the same output and MLP gradients bit for bit as encode-then-MLP, and the same grid gradients
-    (bitwise on the sorted backward, n >= 4096; within fp16 atomic-order noise on the direct one). The fused
-    path is k_nerf_mlp_train's, so the unfused run uses that kernel too (option mlp_train16 = 0)."""
-    net, tr, p16, m = nerf_setup
-    net.set_option("mlp_train16", 0)
-    c = torch.from_numpy(coords_batch(n, seed=11 + n)).cuda()
-    dL = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
-    dL[:, :4] = torch.rand((n, 4), device="cuda").half() - 0.5
-    res = {}
-    for fuse in (1, 0):
-        net.set_option("fuse_train", fuse)
-        out = torch.zeros((n, 16), dtype=torch.float16, device="cuda")
-        net.forward_backward(c, dL, output=out)
-        torch.cuda.synchronize()
-        res[fuse] = (out.clone(), tr.gradients.clone())
-    net.set_option("fuse_train", 0)
-    nm = net.n_matrix_params
-    assert torch.equal(res[1][0], res[0][0])
-    assert torch.equal(res[1][1][:nm], res[0][1][:nm])
-    if n >= 4096:
-        assert torch.equal(res[1][1][nm:], res[0][1][nm:])
-    else:
-        assert torch.allclose(res[1][1][nm:].float(), res[0][1][nm:].float(), atol=3e-3)
 
 
 @pytest.mark.parametrize("grad_accumulate", [False, True])

@@ -7,7 +7,7 @@
 # sets engine options on every model, NGP_SC_* the grid-backward plan knobs, ...), or lib=DIR to load
 # build/DIR/libngp_engine.so instead of the in-tree engine. -t runs the tests under the LAST variant's
 # settings first; -n adds the Lego stand-in and fox step profiles (tools/nerf_step_profile.py). Outputs go to
-# gpurun_out/TAG/.  Example: bash tools/ab.sh r04x -t tests/test_gpu_network_full.py new old:NGP_MODEL_OPTS="mlp_train16=0"
+# gpurun_out/TAG/.  Example: bash tools/ab.sh r04x -t tests/test_gpu_network_full.py new old:NGP_MODEL_OPTS="fuse_slabs=0"
 set -e -o pipefail
 T=$1; shift
 TESTS=""; BENCH="--no-cpu-baseline --e2e-seconds 0 --c3-seconds 0"; NERF=""
