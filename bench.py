@@ -295,7 +295,8 @@ def timed_steps(lib, step, steps, warmup, world, capture=None, comm=None):
     return t1 - t0, ("hip_graph" if graph is not None else (graph_note or "eager")), prof
 
 
-def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None, wire="f32", shard=True, exchange_at_world_1=False):
+def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None, wire="f32", shard=True, exchange_at_world_1=False,
+              dp_parts=None, dp_wire16=False):
     """NerfNetwork + Trainer for C2/C2' with a resident synthetic batch; returns (step, capture, net, trainer,
     comm). step() is Trainer.train_step, the eager form of the captured step (the grid's update fused into
     the backward on the lazy layout, the exchange hook, the optimizer), so the per-kernel replay profiles
@@ -318,6 +319,9 @@ def nerf_pass(pkg, variant, n, rank, world, opts=(), overlap=None, wire="f32", s
         # (exchange_at_world_1, no process group): the engine communicator alone, for the dp1_overhead record
         comm = pkg.dp.EngineComm(0, 1, wire=wire) if world == 1 else pkg.dp.make_comm(rank, world, wire=wire)
         if shard:
+            if dp_parts is not None:
+                trainer.set_option("dp_parts", dp_parts)  # the exchange in parameter parts, overlapping the backward
+            trainer.set_option("dp_wire16", int(dp_wire16))
             trainer.set_data_parallel(comm)  # sharded optimizer: reduce-scatter, slice update, all-gather
         else:
             trainer.set_allreduce(comm)
@@ -555,6 +559,11 @@ def main():
                     help="N > 1: 1 = sharded optimizer (reduce-scatter fp32, slice update, all-gather fp16 weights), "
                          "0 = one fp32 all-reduce of the gradients and a replicated update")
     ap.add_argument("--no-dp1", action="store_true", help="N = 1: skip the dp1_overhead sub-record")
+    ap.add_argument("--dp-parts", type=int, default=None,
+                    help="sharded exchange: parameter parts, each reduce-scattered / updated / all-gathered while the "
+                         "backward sums the next (trainer option dp_parts; default: the engine's)")
+    ap.add_argument("--dp-wire16", type=int, default=0,
+                    help="sharded exchange: 1 = reduce-scatter the fp16 gradient (half the bytes; per-hop fp16 sums)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo"],
                     help="N > 1 exchange: rccl (engine RCCL communicator, one GPU per rank) or gloo (host round "
                          "trip through torch.distributed: ranks may share a GPU, eager steps only)")
@@ -604,7 +613,8 @@ def main():
     comm = None
     if args.variant in ("C2", "C2p"):
         step, capture, net, trainer, comm = nerf_pass(pkg, args.variant, n, rank, world, args.opt, args.overlap,
-                                                      args.wire, shard=bool(args.dp_shard))
+                                                      args.wire, shard=bool(args.dp_shard), dp_parts=args.dp_parts,
+                                                      dp_wire16=bool(args.dp_wire16))
         if not args.no_opt_count:
             *n_opt, c5_fused = optimizer_counts(net, trainer, step, fused=trainer.fused_update_active(n))
         if not args.graph:
@@ -648,7 +658,8 @@ def main():
         # global --batch sharded over the N ranks
         n_s = args.batch // world if args.scaling == "weak" else args.batch
         s_s, c_s, _, _, comm_s = nerf_pass(pkg, args.variant, n_s, rank, world, args.opt, args.overlap, args.wire,
-                                           shard=bool(args.dp_shard))
+                                           shard=bool(args.dp_shard), dp_parts=args.dp_parts,
+                                           dp_wire16=bool(args.dp_wire16))
         dts, launch_s, k_s = timed_steps(lib, s_s, args.steps, args.warmup, world, c_s if args.graph else None, comm_s)
         dts = pkg.dp.reduce_scalar(dts, "max")
         strong = {"scaling": "strong" if args.scaling == "weak" else "weak", "batch_per_gpu": n_s,
@@ -701,7 +712,8 @@ def main():
             res["exchange_ms_per_step"] = exchange_ms(kernels)
             q = 8 * world
             n_pad = (int(n_params_total) + q - 1) // q * q
-            res["exchange_bytes"] = ({"reduce_scatter_f32": 4 * n_pad, "all_gather_f16": 2 * n_pad} if args.dp_shard else
+            res["exchange_bytes"] = ({"reduce_scatter_f16" if args.dp_wire16 else "reduce_scatter_f32":
+                                      (2 if args.dp_wire16 else 4) * n_pad, "all_gather_f16": 2 * n_pad} if args.dp_shard else
                                      {"all_reduce": (4 if args.wire == "f32" else 2) * int(n_params_total)})
             if strong is not None:
                 res["strong"] = strong
@@ -723,12 +735,17 @@ def main():
             # engine's RCCL communicator attached at world 1, timed like the headline (one graph of K steps),
             # sharded (reduce-scatter + slice update + all-gather) and all-reduce, against the fused N = 1 step
             res["dp1_overhead"] = {"note": "world-1 RCCL exchange attached, vs the fused single-GPU step above. shard: "
-                                           "the backward stores the fp32 gradient itself, reduce-scatter, the rank's "
-                                           "slice of the optimizer (here all of it), all-gather of the fp16 weights; "
+                                           "the backward stores the fp32 gradient itself, and each of the engine's "
+                                           "default parameter parts is reduce-scattered, its slice of the optimizer "
+                                           "updated (here all of it) and its fp16 weights all-gathered on an exchange "
+                                           "stream while the backward sums the next part; shard_p1: the same in one "
+                                           "part after the backward; shard_wire16: default parts, fp16 reduce-scatter; "
                                            "allreduce: fp16 gradient, widen, all-reduce, narrow, replicated update"}
-            for mode in ("shard", "allreduce"):
+            for mode in ("shard", "shard_p1", "shard_wire16", "allreduce"):
                 sd, cd, _, _, commd = nerf_pass(pkg, args.variant, n, 0, 1, args.opt, args.overlap, args.wire,
-                                                shard=mode == "shard", exchange_at_world_1=True)
+                                                shard=mode != "allreduce", exchange_at_world_1=True,
+                                                dp_parts=1 if mode == "shard_p1" else args.dp_parts,
+                                                dp_wire16=mode == "shard_wire16")
                 dtd, launchd, kd = timed_steps(lib, sd, args.steps, args.warmup, 1, cd if args.graph else None)
                 res["dp1_overhead"][mode] = {
                     "ms_per_step": dtd / args.steps * 1e3, "launch": launchd,

@@ -191,6 +191,12 @@ struct ngp_model {
 	// false: the last training pass did not write the fp16 gradient buffer (the grid's update ran inside the
 	// backward, or the backward stored the gradient as fp32 for the sharded exchange): ngp_trainer_gradients_valid
 	bool grads_valid = true;
+	// the sharded exchange's consumer of the grid backward's parts (BwdParts): set by the trainer around one
+	// training pass, used when the bucketed backward runs without bricks or the fused update
+	const BwdParts* bwd_parts = nullptr;
+	bool parts_ok(uint32_t n) const {
+		return use_sorted(n) && fuse_slabs && !(overlap & 4) && !grid_bricks && grid.n_features >= 2;
+	}
 	uint64_t generation = 0;
 	uint64_t ws_epoch = 0;  // bumped by every workspace reallocation (DevBuf::epoch)
 	std::unique_ptr<ngp_ctx> last_ctx;
@@ -475,7 +481,8 @@ struct ngp_model {
 			sc_hist_done = false;
 			// _adam: with the grid's optimizer update
 			ProfScope ps(fopt && fopt->rec ? "grid_backward_adam" : "grid_backward_sorted", s);
-			grid_backward_sorted(grid, b, sc_plan, ws, s, overwrite, win_debug, slab, fopt);
+			grid_backward_sorted(grid, b, sc_plan, ws, s, overwrite, win_debug, slab, fopt,
+			                     bwd_parts && !sc_plan.bk.LD && !(fopt && fopt->rec) ? bwd_parts : nullptr);
 			return;
 		}
 		NGP_CHECK(!slab && !fopt, "fused slab reduction / optimizer need the sorted grid backward");
@@ -537,11 +544,36 @@ struct ngp_trainer {
 	bool shard_opt = true;       // trainer option "shard_opt"
 	bool shards_valid = true;    // false: a sharded step left other ranks' records stale here (gather_shards)
 	float* g32 = nullptr;
+	uint64_t g32_count = 0;
 	uint64_t n_pad = 0;
+	// The exchange in parameter parts (trainer option "dp_parts"): part j = parameters [pb[j], pb[j + 1]), multiples
+	// of 8 world; rank r owns the r-th of the world equal slices of every part. Each part is reduce-scattered,
+	// its slice updated and all-gathered as soon as the backward has summed it (BwdParts), on the exchange
+	// stream xs, while the backward sums the next part.
+	uint32_t dp_parts = 2;
+	bool dp_wire16 = false;      // option "dp_wire16": reduce-scatter the fp16 gradient (half the bytes; rounded per hop)
+	std::vector<uint64_t> pb;
+	hipStream_t xs = nullptr;
+	hipEvent_t ev_part[BwdParts::MAX] = {}, ev_xs = nullptr;
+	struct PartStep {  // one sharded step's exchange state (issue_part)
+		hipStream_t s = nullptr;
+		ngp::Exchange e;
+		float loss_scale = 1.f;
+		const uint32_t* step_base = nullptr;
+		uint32_t step_add = 0;
+		bool wire16 = false, overlap = false;
+		uint32_t issued = 0;
+		int rc = NGP_OK;
+	} ps_;
+	BwdParts bparts;
 	~ngp_trainer() {
 		if (arena) (void)hipFree(arena);
 		if (bias_tab) (void)hipFree(bias_tab);
 		if (g32) (void)hipFree(g32);
+		for (hipEvent_t ev : ev_part)
+			if (ev) (void)hipEventDestroy(ev);
+		if (ev_xs) (void)hipEventDestroy(ev_xs);
+		if (xs) (void)hipStreamDestroy(xs);
 	}
 	ngp::Exchange exchange() const {
 		ngp::Exchange e;
@@ -552,35 +584,116 @@ struct ngp_trainer {
 	// the sharded optimizer applies to this exchange: the lazy layout owning the model's buffers, rank known
 	bool sharded(const ngp::Exchange& e) const {
 		return e.fn && e.rank_known && shard_opt && rec && g32 && e.world == world && model->params == w16 &&
-		       model->gradients == g16;
+		       model->gradients == g16 && !pb.empty();
 	}
 	void require_full_state(const char* what) const {
 		if (!shards_valid)
 			throw Error(std::string(what) + ": the optimizer state is sharded over the data-parallel ranks; call "
 			            "ngp_trainer_gather_shards on every rank first");
 	}
-	// Sharded exchange + update: fp16 gradients widened to fp32, reduce-scattered; this rank's slice of the
-	// records updated from the sums (rounded to fp16 once, as the all-reduce path narrows); fp16 weights
-	// all-gathered; the MLP's weight fragments rebuilt where another rank updated the MLP section.
-	int shard_step(hipStream_t s, float loss_scale, const ngp::Exchange& e, const uint32_t* step_base, uint32_t step_add,
-	               bool stored32) {
+	// part bounds for `world` ranks: dp_parts parts of about n_pad / dp_parts, multiples of 8 world
+	void make_part_bounds(uint32_t w) {
+		const uint64_t q = 8ull * w;
+		pb.assign(1, 0);
+		for (uint32_t j = 1; j < dp_parts; ++j) {
+			const uint64_t b = (n_pad * j / dp_parts) / q * q;
+			if (b > pb.back() && b < n_pad) pb.push_back(b);
+		}
+		pb.push_back(n_pad);
+	}
+	void ensure_exchange_stream() {
+		if (xs) return;
+		NGP_HIP(hipStreamCreateWithFlags(&xs, hipStreamNonBlocking));
+		for (hipEvent_t& ev : ev_part) NGP_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+		NGP_HIP(hipEventCreateWithFlags(&ev_xs, hipEventDisableTiming));
+	}
+	// this rank's slice of part j, clamped to the parameters
+	void part_slice(uint32_t j, uint64_t& lo, uint64_t& hi) const {
+		const uint64_t c = (pb[j + 1] - pb[j]) / world;
+		lo = std::min<uint64_t>(pb[j] + (uint64_t)dp_rank * c, n);
+		hi = std::min<uint64_t>(lo + c, n);
+	}
+	// the MLP section lies in this rank's slice of part 0: the update keeps its weight fragments current
+	bool mlp_owned() const {
+		uint64_t lo, hi;
+		part_slice(0, lo, hi);
+		return lo == 0 && hi >= model->n_matrix();
+	}
+	// Exchange + update of part j (sharded step): reduce-scatter of the summed gradient, this rank's slice of the
+	// records updated from the sums (fp32 wire: rounded to fp16 once, as the all-reduce path narrows; fp16 wire:
+	// RCCL's per-hop fp16 sum), all-gather of the slice's fp16 weights. On xs behind an event when the backward
+	// hands the parts over while it runs, else on the step's stream.
+	void issue_part(uint32_t j) {
+		PartStep& q = ps_;
+		if (q.rc != NGP_OK || j != q.issued || j + 1 >= pb.size()) { q.rc = NGP_ERROR; return; }
+		hipStream_t x = q.s;
+		if (q.overlap) {
+			NGP_HIP(hipEventRecord(ev_part[j], q.s));
+			NGP_HIP(hipStreamWaitEvent(xs, ev_part[j], 0));
+			x = xs;
+		}
+		const uint64_t a = pb[j], len = pb[j + 1] - pb[j];
+		const ngp::Exchange& e = q.e;
+		if (e.fn(e.user, q.wire16 ? (void*)(g16 + a) : (void*)(g32 + a), len, q.wire16 ? NGP_DTYPE_F16 : NGP_DTYPE_F32,
+		         NGP_REDUCE_SCATTER_SUM, x) != NGP_OK) { q.rc = NGP_ERROR; return; }
+		uint64_t lo, hi;
+		part_slice(j, lo, hi);
 		ngp_model* m = model;
-		const uint64_t c = n_pad / e.world;
-		if (!stored32) widen_f16(g16, g32, n, s);  // the backward did not write the fp32 input itself
-		if (e.fn(e.user, g32, n_pad, NGP_DTYPE_F32, NGP_REDUCE_SCATTER_SUM, s) != NGP_OK) return NGP_ERROR;
-		const uint64_t lo = std::min<uint64_t>((uint64_t)e.rank * c, n), hi = std::min<uint64_t>(lo + c, n);
 		const bool mlp_here = lo == 0 && hi >= m->n_matrix();
 		AdamState st{w32, w16, g16, nullptr, nullptr, nullptr, nullptr, inf16,
-		             mlp_here && m->frags_current ? (f16*)m->frags.p : nullptr, m->d_fragmap, step_base, step_add,
-		             step_base ? (const AdamConfig*)(ctl + CTL_CFG) : nullptr, rec, bias_tab, g32};
+		             mlp_here && m->frags_current ? (f16*)m->frags.p : nullptr, m->d_fragmap, q.step_base, q.step_add,
+		             q.step_base ? (const AdamConfig*)(ctl + CTL_CFG) : nullptr, rec, bias_tab, q.wire16 ? nullptr : g32};
 		{
-			ProfScope ps("optimizer", s);
-			adam_lazy_range(cfg, (uint32_t)lo, (uint32_t)hi, (uint32_t)m->n_matrix(), loss_scale, st, s);
+			ProfScope ps("optimizer", x);
+			adam_lazy_range(cfg, (uint32_t)lo, (uint32_t)hi, (uint32_t)m->n_matrix(), q.loss_scale, st, x);
 		}
-		if (e.fn(e.user, w16, n_pad, NGP_DTYPE_F16, NGP_ALL_GATHER, s) != NGP_OK) return NGP_ERROR;
-		if (!mlp_here && m->n_matrix() > 0) m->prep(s, false);  // fragments of the gathered MLP weights
+		if (e.fn(e.user, w16 + a, len, NGP_DTYPE_F16, NGP_ALL_GATHER, x) != NGP_OK) { q.rc = NGP_ERROR; return; }
+		++q.issued;
+	}
+	static void part_done(void* self, uint32_t j, hipStream_t) { ((ngp_trainer*)self)->issue_part(j); }
+	// Before a sharded step's training pass: the exchange state, and the backward's parts when it can hand them
+	// over (bucketed backward storing the fp32 gradient, or the fp16 one for the fp16 wire): returns them for
+	// ngp_model::bwd_parts, or nullptr (then every part is exchanged after the backward).
+	// stores_input: the backward writes the wire's input itself (fp32 wire: the fp32 store, FusedAdam::g32).
+	const BwdParts* begin_shard_step(hipStream_t s, float loss_scale, const ngp::Exchange& e, const uint32_t* step_base,
+	                                 uint32_t step_add, uint32_t n_batch, bool stores_input) {
+		ps_ = PartStep{};
+		ps_.s = s; ps_.e = e; ps_.loss_scale = loss_scale; ps_.step_base = step_base; ps_.step_add = step_add;
+		ps_.wire16 = dp_wire16;
+		ngp_model* m = model;
+		if (pb.size() < 3 || !m->parts_ok(n_batch) || !(stores_input || dp_wire16)) return nullptr;
+		ensure_exchange_stream();
+		ps_.overlap = true;
+		const ScatterPlan& p = m->sc_plan_for(n_batch);
+		if (p.bk.LD) { ps_.overlap = false; return nullptr; }
+		bparts = BwdParts{};
+		bparts.k = (uint32_t)pb.size() - 1;
+		const uint64_t go = m->grid_offset();
+		for (uint32_t j = 0; j < bparts.k; ++j)
+			bparts.vb_end[j] = j + 1 == bparts.k ? p.n_buckets : scatter_bucket_at_param(m->grid, p, pb[j + 1] > go ? pb[j + 1] - go : 0);
+		bparts.after = part_done;
+		bparts.user = this;
+		return &bparts;
+	}
+	// After the training pass: the parts the backward did not hand over, the join of the exchange stream, the MLP's
+	// fragments from the gathered weights where another rank updated them.
+	int shard_step(bool stored) {
+		PartStep& q = ps_;
+		hipStream_t s = q.s;
+		ngp_model* m = model;
+		if (q.issued == 0) {
+			q.overlap = false;  // nothing handed over (not the bucketed backward): every part here, on s
+			if (!stored && !q.wire16) widen_f16(g16, g32, n, s);  // the backward did not write the fp32 input itself
+		}
+		while (q.rc == NGP_OK && q.issued + 1 < pb.size()) issue_part(q.issued);
+		if (q.rc != NGP_OK) return NGP_ERROR;
+		if (q.overlap) {
+			NGP_HIP(hipEventRecord(ev_xs, xs));
+			NGP_HIP(hipStreamWaitEvent(s, ev_xs, 0));
+		}
+		if (!mlp_owned() && m->n_matrix() > 0) m->prep(s, false);  // fragments of the gathered MLP weights
 		inf_stale = w32_stale = true;
-		if (e.world > 1) shards_valid = false;
+		if (q.e.world > 1) shards_valid = false;
 		return NGP_OK;
 	}
 	void sync_device_step() { NGP_HIP(hipMemcpy(ctl, &step, sizeof(uint32_t), hipMemcpyHostToDevice)); }
@@ -1271,16 +1384,29 @@ static int train_step_body(ngp_trainer* t, void* stream, uint32_t n, const float
 		}
 	}
 	const bool shard = with_optimizer && t->sharded(ex);
-	// sharded: the backward writes the fp32 reduce-scatter input itself where it can (no widening pass)
-	const bool direct32 = shard && m->grad32_ok(n);
+	// sharded: the backward writes the fp32 reduce-scatter input itself where it can (no widening pass); with the
+	// fp16 wire it stores the fp16 gradient as usual
+	const bool direct32 = shard && !t->dp_wire16 && m->grad32_ok(n);
 	if (direct32) fa.g32 = t->g32;
-	int rc = forward_backward_with(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE,
-	                               fuse || direct32 ? &fa : nullptr);
+	int rc = NGP_OK;
+	if (shard) {
+		try {
+			// the exchange of each part starts as soon as the backward has summed it (BwdParts)
+			m->bwd_parts = t->begin_shard_step(S(stream), loss_scale * ex.world_factor, ex, step_base, step_base ? k : t->step + k,
+			                                   n, direct32);
+		} catch (const std::exception& e) {
+			g_last_error = e.what();
+			rc = NGP_ERROR;
+		}
+	}
+	if (rc == NGP_OK)
+		rc = forward_backward_with(m, stream, n, input, input_stride, nullptr, 0, dL_doutput, dL_stride, NGP_GRAD_OVERWRITE,
+		                           fuse || direct32 ? &fa : nullptr);
+	m->bwd_parts = nullptr;
 	if (rc == NGP_OK && ex.fn) {
 		try {
 			// the summed gradient of the ranks: the mean (or, NeRF, the 1-GPU gradient) via the loss scale
-			rc = shard ? t->shard_step(S(stream), loss_scale * ex.world_factor, ex, step_base, step_base ? k : t->step + k, direct32)
-			           : ex.fn(ex.user, t->g16, t->n, NGP_DTYPE_F16, NGP_REDUCE_SUM, stream);
+			rc = shard ? t->shard_step(direct32) : ex.fn(ex.user, t->g16, t->n, NGP_DTYPE_F16, NGP_REDUCE_SUM, stream);
 		} catch (const std::exception& e) {
 			g_last_error = e.what();
 			rc = NGP_ERROR;
@@ -1388,12 +1514,14 @@ static void trainer_prepare_shards(ngp_trainer* t, uint32_t world) {
 	if (!t->rec) return;
 	const uint64_t q = 8ull * world, n_pad = (t->n + q - 1) / q * q;
 	NGP_CHECK(n_pad - t->n <= ngp_trainer::SHARD_PAD, "sharded optimizer: too many ranks for the parameter padding");
-	if (t->g32 && t->n_pad == n_pad) return;
+	t->n_pad = n_pad;
+	t->make_part_bounds(world);
+	if (t->g32 && t->g32_count == n_pad) return;
 	if (t->g32) NGP_HIP(hipFree(t->g32));
 	t->g32 = nullptr;
 	NGP_HIP(hipMalloc(&t->g32, n_pad * sizeof(float)));
 	NGP_HIP(hipMemset(t->g32, 0, n_pad * sizeof(float)));  // the padding stays 0: it sums to 0 in the reduce-scatter
-	t->n_pad = n_pad;
+	t->g32_count = n_pad;
 }
 
 int ngp_trainer_set_data_parallel(ngp_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn fn, void* user) {
@@ -1416,10 +1544,14 @@ int ngp_trainer_gather_shards(ngp_trainer* t, void* stream) {
 	NGP_ARG(t);
 	NGP_TRY({
 		if (t->shards_valid) return NGP_OK;
-		NGP_CHECK(t->allreduce && t->rec && t->n_pad, "gather_shards: no sharded exchange attached");
-		// records of n_pad / 2 pairs, 12 floats each: rank r's slice holds the pairs of its parameter slice
-		if (t->allreduce(t->allreduce_user, t->rec, t->n_pad / 2 * 12, NGP_DTYPE_F32, NGP_ALL_GATHER, stream) != NGP_OK)
-			throw Error(g_last_error.empty() ? "gather_shards: all-gather failed" : g_last_error);
+		NGP_CHECK(t->allreduce && t->rec && t->n_pad && t->pb.size() >= 2, "gather_shards: no sharded exchange attached");
+		// records of each part's parameter pairs, 12 floats each: rank r's slice of the part holds the pairs of its
+		// parameter slice
+		static_assert(sizeof(AdamRec) == 12 * sizeof(float), "AdamRec: 12 floats");
+		for (size_t j = 0; j + 1 < t->pb.size(); ++j)
+			if (t->allreduce(t->allreduce_user, t->rec + t->pb[j] / 2, (t->pb[j + 1] - t->pb[j]) / 2 * 12, NGP_DTYPE_F32, NGP_ALL_GATHER,
+			                 stream) != NGP_OK)
+				throw Error(g_last_error.empty() ? "gather_shards: all-gather failed" : g_last_error);
 		NGP_HIP(hipStreamSynchronize(S(stream)));
 		t->shards_valid = true;
 	});
@@ -1507,6 +1639,13 @@ int ngp_trainer_set_option(ngp_trainer* t, const char* key, double value) {
 		} else if (k == "shard_opt") {
 			NGP_CHECK(t->shards_valid, "shard_opt: gather the sharded optimizer state first (ngp_trainer_gather_shards)");
 			t->shard_opt = value != 0;
+		} else if (k == "dp_parts") {
+			NGP_CHECK(t->shards_valid, "dp_parts: gather the sharded optimizer state first (ngp_trainer_gather_shards)");
+			NGP_CHECK(value >= 1 && value <= BwdParts::MAX, "dp_parts: 1 to 8");
+			t->dp_parts = (uint32_t)value;
+			if (t->n_pad) t->make_part_bounds(t->world);
+		} else if (k == "dp_wire16") {
+			t->dp_wire16 = value != 0;
 		} else {
 			throw Error("ngp_trainer_set_option: unknown option " + k);
 		}

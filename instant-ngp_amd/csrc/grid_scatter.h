@@ -62,8 +62,23 @@ bool scatter_hist(const GridDesc& g, const ScatterPlan& p, void* workspace, Grid
 // fused (optional, overwrite only): apply the lazy optimizer update to every entry with a nonzero
 // gradient instead of storing the gradient (optimizer.h FusedAdam); the grid part of b.grad is then
 // left unwritten.
+// parts (optional): the bucket accumulation in table order, so that a consumer of the gradient (the sharded
+// data-parallel exchange) can start on its leading parameters while the rest is still summed. The split
+// buckets' parts, then k_sc_split_reduce (split buckets, the MLP's dW slabs), then the other buckets in
+// `k` launches: launch j covers the buckets [j ? vb_end[j - 1] : 0, vb_end[j]), and after it `after(user, j, s)`
+// is called (every gradient of the grid's entries below entry_end(vb_end[j]), and the MLP's, is then final
+// on s). Integer sums: the gradient is bit-identical to the one-launch form. Not with bricks or a fused update.
+struct BwdParts {
+	static constexpr uint32_t MAX = 8;
+	uint32_t k = 0;
+	uint32_t vb_end[MAX] = {};
+	void (*after)(void* user, uint32_t part, hipStream_t s) = nullptr;
+	void* user = nullptr;
+};
+// first bucket whose first grid parameter (entry * F, grid-relative) is >= param (n_buckets when none)
+uint32_t scatter_bucket_at_param(const GridDesc& g, const ScatterPlan& p, uint64_t param);
 void grid_backward_sorted(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace,
                           hipStream_t s, bool overwrite, uint32_t debug = 0, const SlabJob* slab = nullptr,
-                          const FusedAdam* fused = nullptr);
+                          const FusedAdam* fused = nullptr, const BwdParts* parts = nullptr);
 
 }  // namespace ngp

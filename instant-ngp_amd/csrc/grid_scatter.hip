@@ -840,7 +840,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
                                                          uint32_t max_parts, const uint16_t* __restrict__ item_idx,
                                                          const f16* __restrict__ item_val, f16* __restrict__ grad, bool overwrite,
                                                          const uint32_t* __restrict__ split, unsigned long long* __restrict__ scratch,
-                                                         uint32_t debug, const FusedAdam fa, const BrickFallback fb) {
+                                                         uint32_t debug, const FusedAdam fa, const BrickFallback fb, uint32_t vb_off) {
 	constexpr bool FUSED = MODE == SC_FUSED_ADAM, G32 = MODE == SC_STORE_F32;
 	extern __shared__ unsigned long long acc[];
 	const uint32_t NE = 1u << B, NEP = NE + 1;  // feature planes padded by one entry (accumulate_items)
@@ -861,7 +861,7 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
 		for (uint32_t k = threadIdx.x; k < NE * F; k += blockDim.x) dst[k] = acc[(k / NE) * NEP + k % NE];
 		return;
 	}
-	const uint32_t vb = blockIdx.x - max_parts;
+	const uint32_t vb = blockIdx.x - max_parts + vb_off;  // vb_off: a launch over buckets [vb_off, ..) (BwdParts)
 	if (vb - bk.vb0 < bk.NBK) return;  // bricks: parts only
 	const uint32_t t = tot[vb];
 	if (t > split_limit) return;
@@ -1077,7 +1077,7 @@ Levels make_levels(const GridDesc& g, uint32_t B, const BrickConst& bk) {
 
 template <uint32_t D>
 void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const GridBwdArgs& a, const ScatterPlan& p, char* ws,
-                     hipStream_t s, bool overwrite, uint32_t debug, const SlabJob* slab, const FusedAdam& fa) {
+                     hipStream_t s, bool overwrite, uint32_t debug, const SlabJob* slab, const FusedAdam& fa, const BwdParts* parts) {
 	const uint32_t* tot = (const uint32_t*)(ws + p.off_tot);
 	const uint32_t* cur_t = (const uint32_t*)(ws + p.off_cur);
 	const uint32_t* split = (const uint32_t*)(ws + p.off_split);
@@ -1100,8 +1100,11 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		NGP_HIP(hipGetLastError());
 		const size_t lds_a = ((size_t)8 << p.B) * c.n_features + SC_LDS_PAD_BYTES + (fa.rec ? SC_LIST_BYTES : 0);
 		ensure_dynamic_lds((const void*)accum, lds_a);
-		accum<<<p.max_split_blocks + p.n_buckets, p.bt, lds_a, s>>>(c, lv, p.bk, a, tot, lo, p.B, p.split_limit, p.max_split_blocks, idx,
-		                                                                     val, a.grad, overwrite, split, scratch, debug, fa, fb);
+		const bool parted = parts && parts->k > 0;
+		// parted: the split buckets' parts alone first (k_sc_split_reduce needs them), the other buckets after it
+		accum<<<p.max_split_blocks + (parted ? 0u : p.n_buckets), p.bt, lds_a, s>>>(c, lv, p.bk, a, tot, lo, p.B, p.split_limit,
+		                                                                             p.max_split_blocks, idx, val, a.grad, overwrite,
+		                                                                             split, scratch, debug, fa, fb, 0u);
 		NGP_HIP(hipGetLastError());
 		const uint32_t gy = (uint32_t)div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS);
 		const SlabJob sj = slab ? *slab : SlabJob{};
@@ -1113,6 +1116,19 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets, fa, p.bk, bp, fb,
 		                                     p.max_split_buckets + slab_x);
 		NGP_HIP(hipGetLastError());
+		if (!parted) return;
+		uint32_t v0 = 0;
+		for (uint32_t j = 0; j < parts->k; ++j) {
+			const uint32_t v1 = std::min(parts->vb_end[j], p.n_buckets);
+			if (v1 > v0) {
+				accum<<<v1 - v0, p.bt, lds_a, s>>>(c, lv, p.bk, a, tot, lo, p.B, p.split_limit, 0u, idx, val, a.grad, overwrite, split,
+				                                   scratch, debug, fa, fb, v0);
+				NGP_HIP(hipGetLastError());
+			}
+			v0 = std::max(v0, v1);
+			if (parts->after) parts->after(parts->user, j, s);
+		}
+		NGP_CHECK(v0 == p.n_buckets, "grid backward parts: the last part must end at the last bucket");
 	};
 	auto by_chunk = [&](auto sc512, auto sc1024, auto accum, auto splitr) {
 		if (p.spb == 512) go(sc512, accum, splitr);
@@ -1304,16 +1320,29 @@ void grid_scatter_prepare(const GridDesc& g, const GridBwdArgs& a, const Scatter
 	NGP_HIP(hipGetLastError());
 }
 
+uint32_t scatter_bucket_at_param(const GridDesc& g, const ScatterPlan& p, uint64_t param) {
+	const Levels lv = make_levels(g, p.B, p.bk);
+	for (uint32_t vb = 0; vb < p.n_buckets; ++vb) {
+		uint32_t l = 0;
+		while (lv.vb_base[l + 1] <= vb) ++l;
+		const uint64_t e0 = (uint64_t)g.offsets[l] + ((uint64_t)(vb - lv.vb_base[l]) << p.B);
+		if (e0 * g.n_features >= param) return vb;
+	}
+	return p.n_buckets;
+}
+
 void grid_backward_sorted(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace, hipStream_t s,
-                          bool overwrite, uint32_t debug, const SlabJob* slab, const FusedAdam* fused) {
+                          bool overwrite, uint32_t debug, const SlabJob* slab, const FusedAdam* fused, const BwdParts* parts) {
 	if (b.n == 0) return;
 	NGP_CHECK(b.level_begin == 0, "grid_backward_sorted handles all levels");
 	NGP_CHECK(!fused || (overwrite && g.n_features >= 2), "fused optimizer: overwrite mode, F >= 2");
+	NGP_CHECK(!parts || !parts->k || (!p.bk.LD && !(fused && fused->rec) && parts->k <= BwdParts::MAX),
+	          "grid backward parts: not with bricks or the fused update");
 	const GridConst c = make_grid_const(g);
 	const Levels lv = make_levels(g, p.B, p.bk);
 	const FusedAdam fa = fused ? *fused : FusedAdam{};
-	if (g.n_dims == 3) launch_backward<3>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab, fa);
-	else launch_backward<2>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab, fa);
+	if (g.n_dims == 3) launch_backward<3>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab, fa, parts);
+	else launch_backward<2>(g.n_features, c, lv, b, p, (char*)workspace, s, overwrite, debug, slab, fa, parts);
 }
 
 }  // namespace ngp

@@ -12,6 +12,12 @@ rank updating every record) rounds the same sums the same way, so the two must t
 * one rank over the engine's RCCL communicator (world 1), captured steps: the sharded step trains bit for bit
   like the fused single-GPU step.
 
+Both in every form of the exchange: in 1, 2 (the default) or 4 parameter parts, each exchanged on the exchange
+stream as soon as the backward has summed it (trainer option dp_parts), and with the fp16 wire (dp_wire16: the
+reduce-scatter sums fp16 gradients). gloo's reduce-scatter sums the fp16 values in fp32 and rounds once, and at
+world 1 nothing is summed, so the fp16 wire is bit-exact here; RCCL's fp16 ring at world >= 3 rounds per hop
+(DESIGN §7 gives that bar).
+
 Reading the EMA parameters, the full-precision weights or serializing before the gather must fail loudly."""
 import hashlib
 import json
@@ -51,6 +57,14 @@ def _batch(rank, step, n=1 << 14):
     return torch.from_numpy(x).cuda(), torch.from_numpy(dl).cuda()
 
 
+SHARD_MODES = ("shard", "shard_p1", "shard_p4", "shard_widen", "shard_wire16")
+
+
+def _shard_options(tr, mode):
+    tr.set_option("dp_parts", {"shard_p1": 1, "shard_p4": 4}.get(mode, 2))
+    tr.set_option("dp_wire16", int(mode == "shard_wire16"))
+
+
 def _gloo_rank(rank, world, port, out_dir):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank), "WORLD_SIZE": str(world)})
     import torch.distributed as dist
@@ -59,7 +73,7 @@ def _gloo_rank(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     out = {}
-    for mode in ("shard", "shard_widen", "allreduce"):
+    for mode in SHARD_MODES + ("allreduce",):
         cfg = pkg.nerf_config("C2")
         net = pkg.create_nerf_network(cfg)
         if mode == "shard_widen":  # dW slab reduction in its own launch: the backward cannot store fp32 itself
@@ -67,6 +81,7 @@ def _gloo_rank(rank, world, port, out_dir):
         tr = pkg.Trainer(net, cfg["optimizer"], seed=1337)
         comm = pkg.dp.HostComm(rank, world)
         if mode.startswith("shard"):
+            _shard_options(tr, mode)
             tr.set_data_parallel(comm)
         else:
             tr.set_allreduce(comm)
@@ -105,7 +120,7 @@ def test_sharded_optimizer_gloo_world2_equals_allreduce(tmp_path):
     r0, r1 = (json.load(open(tmp_path / f"r{r}.json")) for r in (0, 1))
     for r in (r0, r1):
         assert r["shard"]["errors"] == []
-        for mode in ("shard", "shard_widen"):
+        for mode in SHARD_MODES:
             assert r[mode]["params"] == r["allreduce"]["params"], mode  # fp16 weights after every step
             for key in ("blob", "inf", "w32"):
                 assert r[mode][key] == r["allreduce"][key], (mode, key)
@@ -120,14 +135,15 @@ def _rccl_world1(_rank, out_dir):
     x, dl = _batch(0, 0, n)
     x1, dl1 = _batch(0, 1, n)
     res = {}
-    for mode in ("plain", "shard"):
+    for mode in ("plain", "shard", "shard_p1", "shard_p4", "shard_wire16"):
         cfg = pkg.nerf_config("C2")
         net = pkg.create_nerf_network(cfg)
         tr = pkg.Trainer(net, cfg["optimizer"], seed=1337)
         net.reserve(n)
         comm = None
-        if mode == "shard":
+        if mode != "plain":
             comm = pkg.dp.EngineComm(0, 1)  # a world of one: no process group
+            _shard_options(tr, mode)
             tr.set_data_parallel(comm)
         assert tr.fused_update_active(n) == (mode == "plain")
         s = torch.cuda.Stream()
@@ -152,7 +168,8 @@ def test_sharded_optimizer_rccl_world1_equals_fused_step(tmp_path):
     import torch.multiprocessing as mp
     mp.spawn(_rccl_world1, args=(str(tmp_path),), nprocs=1, join=True)
     r = json.load(open(tmp_path / "w1.json"))
-    assert r["plain"] == r["shard"]
+    for mode in ("shard", "shard_p1", "shard_p4", "shard_wire16"):
+        assert r["plain"] == r[mode], mode
     assert r["shard"][3] == 11
 
 
