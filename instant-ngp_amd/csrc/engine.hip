@@ -625,7 +625,8 @@ struct ngp_trainer {
 	// hands the parts over while it runs, else on the step's stream.
 	void issue_part(uint32_t j) {
 		PartStep& q = ps_;
-		if (q.rc != NGP_OK || j != q.issued || j + 1 >= pb.size()) { q.rc = NGP_ERROR; return; }
+		// parts go out from the last to the first (the order the parted backward finishes them), on every rank
+		if (q.rc != NGP_OK || j + 1 >= pb.size() || j + 2 + q.issued != pb.size()) { q.rc = NGP_ERROR; return; }
 		hipStream_t x = q.s;
 		if (q.overlap) {
 			NGP_HIP(hipEventRecord(ev_part[j], q.s));
@@ -665,7 +666,8 @@ struct ngp_trainer {
 		ensure_exchange_stream();
 		ps_.overlap = true;
 		const ScatterPlan& p = m->sc_plan_for(n_batch);
-		if (p.bk.LD) { ps_.overlap = false; return nullptr; }
+		// the MLP's gradient (slab reduction with bucket range 0) must lie in part 0
+		if (p.bk.LD || pb[1] < m->grid_offset()) { ps_.overlap = false; return nullptr; }
 		bparts = BwdParts{};
 		bparts.k = (uint32_t)pb.size() - 1;
 		const uint64_t go = m->grid_offset();
@@ -685,7 +687,7 @@ struct ngp_trainer {
 			q.overlap = false;  // nothing handed over (not the bucketed backward): every part here, on s
 			if (!stored && !q.wire16) widen_f16(g16, g32, n, s);  // the backward did not write the fp32 input itself
 		}
-		while (q.rc == NGP_OK && q.issued + 1 < pb.size()) issue_part(q.issued);
+		while (q.rc == NGP_OK && q.issued + 1 < pb.size()) issue_part((uint32_t)pb.size() - 2 - q.issued);
 		if (q.rc != NGP_OK) return NGP_ERROR;
 		if (q.overlap) {
 			NGP_HIP(hipEventRecord(ev_xs, xs));

@@ -62,12 +62,13 @@ bool scatter_hist(const GridDesc& g, const ScatterPlan& p, void* workspace, Grid
 // fused (optional, overwrite only): apply the lazy optimizer update to every entry with a nonzero
 // gradient instead of storing the gradient (optimizer.h FusedAdam); the grid part of b.grad is then
 // left unwritten.
-// parts (optional): the bucket accumulation in table order, so that a consumer of the gradient (the sharded
-// data-parallel exchange) can start on its leading parameters while the rest is still summed. The split
-// buckets' parts, then k_sc_split_reduce (split buckets, the MLP's dW slabs), then the other buckets in
-// `k` launches: launch j covers the buckets [j ? vb_end[j - 1] : 0, vb_end[j]), and after it `after(user, j, s)`
-// is called (every gradient of the grid's entries below entry_end(vb_end[j]), and the MLP's, is then final
-// on s). Integer sums: the gradient is bit-identical to the one-launch form. Not with bricks or a fused update.
+// parts (optional): the bucket accumulation in bucket ranges, so that a consumer of the gradient (the sharded
+// data-parallel exchange) can start on some parameters while the rest is still summed. Range j = buckets
+// [j ? vb_end[j - 1] : 0, vb_end[j]) (the last one ends at the last bucket); the ranges run from the last to the
+// first, each as a k_sc_accumulate launch (its split buckets' parts and its other buckets) and a k_sc_split_reduce
+// launch (its split buckets; range 0 also the MLP's dW slabs), then `after(user, j, s)` is called: every gradient
+// of the range's entries (range 0: and the MLP's) is final on s. Integer sums: bit-identical to the one-launch
+// form. Not with bricks or a fused update.
 struct BwdParts {
 	static constexpr uint32_t MAX = 8;
 	uint32_t k = 0;

@@ -840,13 +840,15 @@ __global__ void __launch_bounds__(SC_BT) k_sc_accumulate(const GridConst c, cons
                                                          uint32_t max_parts, const uint16_t* __restrict__ item_idx,
                                                          const f16* __restrict__ item_val, f16* __restrict__ grad, bool overwrite,
                                                          const uint32_t* __restrict__ split, unsigned long long* __restrict__ scratch,
-                                                         uint32_t debug, const FusedAdam fa, const BrickFallback fb, uint32_t vb_off) {
+                                                         uint32_t debug, const FusedAdam fa, const BrickFallback fb, uint32_t vb_off,
+                                                         uint32_t part_lo, uint32_t part_hi) {
 	constexpr bool FUSED = MODE == SC_FUSED_ADAM, G32 = MODE == SC_STORE_F32;
 	extern __shared__ unsigned long long acc[];
 	const uint32_t NE = 1u << B, NEP = NE + 1;  // feature planes padded by one entry (accumulate_items)
 	if (blockIdx.x < max_parts) {
 		if (blockIdx.x >= split[0]) return;
 		const uint32_t* d = split + 2 + 3 * (size_t)blockIdx.x;
+		if (d[0] < part_lo || d[0] >= part_hi) return;  // BwdParts: a split part of a bucket of another range
 		const uint32_t lo = d[1], hi = d[2];
 		if (d[0] - bk.vb0 < bk.NBK) {
 			accumulate_brick<F>(c, bk, a, d[0] - bk.vb0, lo, hi, item_idx, item_val, acc, scratch + (size_t)blockIdx.x * NE * F, NE, fb);
@@ -949,7 +951,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
                                                                 const unsigned long long* __restrict__ scratch, f16* __restrict__ grad,
                                                                 bool overwrite, const SlabJob sj, uint32_t slab_x0, const FusedAdam fa,
                                                                 const BrickConst bk, const uint32_t* __restrict__ bp, const BrickFallback fb,
-                                                                uint32_t fin_x0) {
+                                                                uint32_t fin_x0, uint32_t part_lo, uint32_t part_hi) {
 	static_assert(SC_THREADS == SLAB_THREADS, "slab blocks share the split-reduce block shape");
 	constexpr bool FUSED = MODE == SC_FUSED_ADAM, G32 = MODE == SC_STORE_F32;
 	if (blockIdx.x >= fin_x0) {
@@ -1022,6 +1024,7 @@ __global__ void __launch_bounds__(SC_THREADS) k_sc_split_reduce(const GridConst 
 	// grid (split bucket, 256-pair chunk): one pair per thread, the parts' loads 8 at a time
 	if (blockIdx.x >= split[1]) return;
 	const uint32_t vb = splitb[3 * blockIdx.x], first = splitb[3 * blockIdx.x + 1], parts = splitb[3 * blockIdx.x + 2];
+	if (vb < part_lo || vb >= part_hi) return;  // BwdParts: a split bucket of another range
 	const uint32_t NE = 1u << B;
 	uint32_t e0, n_e;
 	bucket_entries(c, lv, B, vb, e0, n_e);
@@ -1101,34 +1104,44 @@ void launch_backward(uint32_t F, const GridConst& c, const Levels& lv, const Gri
 		const size_t lds_a = ((size_t)8 << p.B) * c.n_features + SC_LDS_PAD_BYTES + (fa.rec ? SC_LIST_BYTES : 0);
 		ensure_dynamic_lds((const void*)accum, lds_a);
 		const bool parted = parts && parts->k > 0;
-		// parted: the split buckets' parts alone first (k_sc_split_reduce needs them), the other buckets after it
-		accum<<<p.max_split_blocks + (parted ? 0u : p.n_buckets), p.bt, lds_a, s>>>(c, lv, p.bk, a, tot, lo, p.B, p.split_limit,
-		                                                                             p.max_split_blocks, idx, val, a.grad, overwrite,
-		                                                                             split, scratch, debug, fa, fb, 0u);
-		NGP_HIP(hipGetLastError());
 		const uint32_t gy = (uint32_t)div_round_up(((size_t)1 << p.B) * c.n_features / 2, SC_THREADS);
 		const SlabJob sj = slab ? *slab : SlabJob{};
 		const uint32_t slab_x = slab ? (uint32_t)div_round_up(slab_blocks(sj.n), gy) : 0u;
 		const size_t fin_entries = (size_t)c.offsets[p.bk.LD] - c.offsets[p.bk.LB];
 		const size_t fin_threads = c.n_features == 1 ? div_round_up(fin_entries, 2) : fin_entries;
 		const uint32_t fin_x = (uint32_t)div_round_up(div_round_up(fin_threads, SC_THREADS), gy);
-		const dim3 grid_r(p.max_split_buckets + slab_x + fin_x, gy);
-		splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets, fa, p.bk, bp, fb,
-		                                     p.max_split_buckets + slab_x);
-		NGP_HIP(hipGetLastError());
-		if (!parted) return;
-		uint32_t v0 = 0;
-		for (uint32_t j = 0; j < parts->k; ++j) {
-			const uint32_t v1 = std::min(parts->vb_end[j], p.n_buckets);
-			if (v1 > v0) {
-				accum<<<v1 - v0, p.bt, lds_a, s>>>(c, lv, p.bk, a, tot, lo, p.B, p.split_limit, 0u, idx, val, a.grad, overwrite, split,
-				                                   scratch, debug, fa, fb, v0);
-				NGP_HIP(hipGetLastError());
-			}
-			v0 = std::max(v0, v1);
+		if (!parted) {
+			accum<<<p.max_split_blocks + p.n_buckets, p.bt, lds_a, s>>>(c, lv, p.bk, a, tot, lo, p.B, p.split_limit, p.max_split_blocks,
+			                                                             idx, val, a.grad, overwrite, split, scratch, debug, fa, fb, 0u,
+			                                                             0u, ~0u);
+			NGP_HIP(hipGetLastError());
+			const dim3 grid_r(p.max_split_buckets + slab_x + fin_x, gy);
+			splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets, fa, p.bk, bp,
+			                                     fb, p.max_split_buckets + slab_x, 0u, ~0u);
+			NGP_HIP(hipGetLastError());
+			return;
+		}
+		// parted (no bricks): the bucket ranges from the last to the first, each with its own split parts and split
+		// buckets, so a range's gradient is final when its two launches are; the MLP's slabs with range 0, which
+		// holds the MLP's parameters. The highest ranges (the hashed levels) rarely hold a split bucket: their
+		// exchange starts while the heavy coarse levels are still summed.
+		NGP_CHECK(!p.bk.LD, "grid backward parts: not with bricks");
+		for (uint32_t jj = 0; jj < parts->k; ++jj) {
+			const uint32_t j = parts->k - 1 - jj;
+			const uint32_t v0 = j ? std::min(parts->vb_end[j - 1], p.n_buckets) : 0u;
+			const uint32_t v1 = j + 1 == parts->k ? p.n_buckets : std::min(parts->vb_end[j], p.n_buckets);
+			NGP_CHECK(v0 <= v1, "grid backward parts: bucket ranges out of order");
+			accum<<<p.max_split_blocks + (v1 - v0), p.bt, lds_a, s>>>(c, lv, p.bk, a, tot, lo, p.B, p.split_limit, p.max_split_blocks,
+			                                                           idx, val, a.grad, overwrite, split, scratch, debug, fa, fb, v0,
+			                                                           v0, v1);
+			NGP_HIP(hipGetLastError());
+			const uint32_t sx = j == 0 ? slab_x : 0u;
+			const dim3 grid_r(p.max_split_buckets + sx, gy);
+			splitr<<<grid_r, SC_THREADS, 0, s>>>(c, lv, p.B, split, splitb, scratch, a.grad, overwrite, sj, p.max_split_buckets, fa, p.bk, bp,
+			                                     fb, p.max_split_buckets + sx, v0, v1);
+			NGP_HIP(hipGetLastError());
 			if (parts->after) parts->after(parts->user, j, s);
 		}
-		NGP_CHECK(v0 == p.n_buckets, "grid backward parts: the last part must end at the last bucket");
 	};
 	auto by_chunk = [&](auto sc512, auto sc1024, auto accum, auto splitr) {
 		if (p.spb == 512) go(sc512, accum, splitr);

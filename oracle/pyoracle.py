@@ -109,6 +109,10 @@ def _declare(L):
     d("orc_triangle_cdf", None, u32, P, P)
     d("orc_sdf_samples", None, u32, P, u32, P, P, P, P, f32, P, P)
     d("orc_sdf_signed_distance", None, u32, P, u32, P, P)
+    d("orc_grid_forward_tcnn", None, P, sz, P, u32, P, P, P)
+    d("orc_nerf_tcnn", None, P, P, sz, P, P, P, P, P)
+    d("orc_net_tcnn", None, P, P, P, sz, P, u32, P, P, P)
+    d("orc_grid_backward_tcnn", None, P, sz, P, u32, P, u32, P, P)
     _declare_nerf(L)
 
 
@@ -383,6 +387,59 @@ def net_train_ex(grid, mlp, params16, pos, dL_dout, stride=None):
                            ptr(r["out_abs"]), ptr(r["grads"]), ptr(r["grads_abs"]), ptr(r["denc16"]), ptr(r["denc_abs"]),
                            ptr(r["margin"]))
     return r
+
+
+# ---------------------------------------------------------------------------------------------
+# tcnn mode (oracle/ngp_tcnn_mode.c): the reference's fp16 arithmetic (half FMAs in the grid blend, fp16 WMMA
+# accumulators in the MLP, fp16 atomics in the grid backward), to bound the engine against it
+# ---------------------------------------------------------------------------------------------
+def grid_forward_tcnn(g, pos, table16, stride=None):
+    """(out float32 [n x L*F] fp16 values, bound float32 [n x L*F]: the fp16 chain's own rounding-error bound)."""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    n = pos.shape[0]
+    out = np.zeros((n, g.n_levels * g.n_features), np.float32)
+    bound = np.zeros_like(out)
+    lib().orc_grid_forward_tcnn(C.byref(g), n, ptr(pos), stride or pos.shape[1], ptr(np.ascontiguousarray(table16)), ptr(out),
+                                ptr(bound))
+    return out, bound
+
+
+def nerf_tcnn(m, params16, coords, dL_dout=None):
+    """NerfNetwork forward (and dL/d(encoding) when dL_dout is given) in tcnn's arithmetic: dict out [n x 16],
+    enc [n x encoding width], denc [n x encoding width] or None."""
+    coords = np.ascontiguousarray(coords, dtype=np.float32)
+    n = coords.shape[0]
+    r = {"out": np.zeros((n, 16), np.float32), "enc": np.zeros((n, m.density.in_pad), np.float32),
+         "denc": None if dL_dout is None else np.zeros((n, m.density.in_pad), np.float32)}
+    dl = None if dL_dout is None else np.ascontiguousarray(dL_dout, np.float32)
+    lib().orc_nerf_tcnn(C.byref(m), ptr(np.ascontiguousarray(params16)), n, ptr(coords), ptr(dl), ptr(r["out"]), ptr(r["denc"]),
+                        ptr(r["enc"]))
+    return r
+
+
+def net_tcnn(grid, mlp, params16, pos, dL_dout=None, stride=None):
+    """NetworkWithInputEncoding forward (and dL/d(encoding)) in tcnn's arithmetic: (out, denc or None)."""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    n = pos.shape[0]
+    out = np.zeros((n, mlp.out_pad), np.float32)
+    denc = None if dL_dout is None else np.zeros((n, mlp.in_pad), np.float32)
+    dl = None if dL_dout is None else np.ascontiguousarray(dL_dout, np.float32)
+    lib().orc_net_tcnn(C.byref(grid), C.byref(mlp), ptr(np.ascontiguousarray(params16)), n, ptr(pos), stride or pos.shape[1],
+                       ptr(dl), ptr(out), ptr(denc))
+    return out, denc
+
+
+def grid_backward_tcnn(g, pos, dL_dy16, stride=None):
+    """tcnn's fp16-atomic grid backward in sample order: (grad16 uint16 [entries*F], bound float64: half a spacing
+    per add, summed)."""
+    pos = np.ascontiguousarray(pos, dtype=np.float32)
+    dy = np.ascontiguousarray(dL_dy16).view(np.uint16)
+    np_ = grid_n_entries(g) * g.n_features
+    out = np.zeros(np_, np.uint16)
+    bound = np.zeros(np_, np.float64)
+    lib().orc_grid_backward_tcnn(C.byref(g), pos.shape[0], ptr(pos), stride or pos.shape[1], ptr(dy), dy.shape[1], ptr(out),
+                                 ptr(bound))
+    return out, bound
 
 
 def adam_step(cfg, step, n_matrix, loss_scale, w32, w16, g16, m1, m2, steps, ema32=None, ema16=None):
