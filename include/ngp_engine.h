@@ -422,6 +422,11 @@ void ngp_nerf_renderer_destroy(ngp_nerf_renderer* r);
  * depth_scale: 1 / the dataset's scale (render_nerf, testbed_nerf.cu:2822); default 1. */
 int ngp_nerf_renderer_set_mode(ngp_nerf_renderer* r, int render_mode);
 int ngp_nerf_renderer_set_depth_scale(ngp_nerf_renderer* r, float depth_scale);
+/* render_mode 9 = ERenderMode::EncodingVis (common.h:120): each step's warped position, the network's input
+ * (testbed_nerf.cu:1202-1203). show_accel (Testbed::Nerf::show_accel, testbed.cu:1678; -1 = off, else 0..7): the
+ * march tests the occupancy grid from that mip up (:2497, 2594), every step is opaque (:1078-1080), and Positions
+ * colours the step's occupancy cell (:1190-1199) */
+int ngp_nerf_renderer_set_show_accel(ngp_nerf_renderer* r, int show_accel);
 int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_config* cfg, void* stream, const ngp_nerf_image* camera,
                     const uint8_t* bitfield, uint32_t spp, uint32_t sample_index, float min_transmittance,
                     const float* background_rgba, int use_inference_params, float* out_rgba);

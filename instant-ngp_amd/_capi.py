@@ -187,6 +187,7 @@ SIGNATURES = {
     "ngp_trainer_set_allreduce": (i32, [P, u32, P, P]),
     "ngp_trainer_set_data_parallel": (i32, [P, u32, u32, P, P]),
     "ngp_nerf_renderer_set_depth_scale": (i32, [P, f32]),
+    "ngp_nerf_renderer_set_show_accel": (i32, [P, i32]),
     "ngp_trainer_n_params": (u64, [P]),
     "ngp_save_snapshot": (i32, [P, P, C.c_char_p, C.c_char_p, C.c_char_p, P, P, f32, u32, f32, i32, i32]),
     "ngp_load_snapshot": (i32, [P, P, C.c_char_p, P, P, P, P, P]),

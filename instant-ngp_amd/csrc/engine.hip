@@ -671,6 +671,8 @@ struct ngp_trainer {
 		bparts = BwdParts{};
 		bparts.k = (uint32_t)pb.size() - 1;
 		const uint64_t go = m->grid_offset();
+		// range j ends at the bucket holding part j + 1's first parameter: that bucket is summed with range j + 1,
+		// before part j + 1 goes out, so every part is final when its exchange starts
 		for (uint32_t j = 0; j < bparts.k; ++j)
 			bparts.vb_end[j] = j + 1 == bparts.k ? p.n_buckets : scatter_bucket_at_param(m->grid, p, pb[j + 1] > go ? pb[j + 1] - go : 0);
 		bparts.after = part_done;

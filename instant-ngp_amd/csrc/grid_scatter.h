@@ -67,8 +67,8 @@ bool scatter_hist(const GridDesc& g, const ScatterPlan& p, void* workspace, Grid
 // [j ? vb_end[j - 1] : 0, vb_end[j]) (the last one ends at the last bucket); the ranges run from the last to the
 // first, each as a k_sc_accumulate launch (its split buckets' parts and its other buckets) and a k_sc_split_reduce
 // launch (its split buckets; range 0 also the MLP's dW slabs), then `after(user, j, s)` is called: every gradient
-// of the range's entries (range 0: and the MLP's) is final on s. Integer sums: bit-identical to the one-launch
-// form. Not with bricks or a fused update.
+// of the range's entries and of every higher range's (range 0: and the MLP's) is final on s. Integer sums:
+// bit-identical to the one-launch form. Not with bricks or a fused update.
 struct BwdParts {
 	static constexpr uint32_t MAX = 8;
 	uint32_t k = 0;
@@ -76,7 +76,9 @@ struct BwdParts {
 	void (*after)(void* user, uint32_t part, hipStream_t s) = nullptr;
 	void* user = nullptr;
 };
-// first bucket whose first grid parameter (entry * F, grid-relative) is >= param (n_buckets when none)
+// the first bucket whose entries reach past grid parameter `param` (entry * F, grid-relative): the bucket holding
+// it (n_buckets when none). A range boundary there puts a bucket that straddles a part boundary in the higher
+// range, which the parted backward sums first (BwdParts)
 uint32_t scatter_bucket_at_param(const GridDesc& g, const ScatterPlan& p, uint64_t param);
 void grid_backward_sorted(const GridDesc& g, const GridBwdArgs& b, const ScatterPlan& p, void* workspace,
                           hipStream_t s, bool overwrite, uint32_t debug = 0, const SlabJob* slab = nullptr,

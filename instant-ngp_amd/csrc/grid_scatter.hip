@@ -1338,8 +1338,8 @@ uint32_t scatter_bucket_at_param(const GridDesc& g, const ScatterPlan& p, uint64
 	for (uint32_t vb = 0; vb < p.n_buckets; ++vb) {
 		uint32_t l = 0;
 		while (lv.vb_base[l + 1] <= vb) ++l;
-		const uint64_t e0 = (uint64_t)g.offsets[l] + ((uint64_t)(vb - lv.vb_base[l]) << p.B);
-		if (e0 * g.n_features >= param) return vb;
+		const uint64_t e1 = std::min<uint64_t>((uint64_t)g.offsets[l] + ((uint64_t)(vb - lv.vb_base[l] + 1) << p.B), g.offsets[l + 1]);
+		if (e1 * g.n_features > param) return vb;
 	}
 	return p.n_buckets;
 }

@@ -143,10 +143,11 @@ struct RenderArgs {
 	uint32_t rgb_activation, density_activation;
 	float min_transmittance;
 	float background[4];           // linear rgba
-	uint32_t render_mode;          // ERenderMode (common.h:110-119): 0 AO, 1 Shade, 2 Normals, 3 Positions, 4 Depth
+	uint32_t render_mode;          // ERenderMode (common.h:110-121): 0 AO, 1 Shade, 2 Normals, 3 Positions, 4 Depth, 9 EncodingVis
 	float depth_scale;             // ERenderMode::Depth: 1 / dataset scale (testbed_nerf.cu:2822)
+	int32_t show_accel;            // Testbed::Nerf::show_accel (-1 off): the march's minimum mip, alpha 1, Positions by cell
 };
-enum : uint32_t { RENDER_AO = 0, RENDER_SHADE = 1, RENDER_NORMALS = 2, RENDER_POSITIONS = 3, RENDER_DEPTH = 4 };
+enum : uint32_t { RENDER_AO = 0, RENDER_SHADE = 1, RENDER_NORMALS = 2, RENDER_POSITIONS = 3, RENDER_DEPTH = 4, RENDER_ENCODING_VIS = 9 };
 struct RenderWorkspace {
 	void* payload[2]; void* payload_hit;
 	float* rgba[2]; float* rgba_hit;

@@ -1856,7 +1856,8 @@ __global__ void k_render_init(RenderArgs a, Payload* __restrict__ pay, float* __
 		const V3 idir = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 		const Cone cone = make_cone(a.cone_angle_constant);
 		t = advance_n_steps(t, cone, ld_random_val(a.sample_index, i * 786433u));
-		t = advance_to_occupied(t, cone, o, d, idir, a.bitfield, 0, a.max_mip, box);
+		// min_mip = show_accel >= 0 ? show_accel : 0 (testbed_nerf.cu:2497)
+		t = advance_to_occupied(t, cone, o, d, idir, a.bitfield, a.show_accel >= 0 ? (uint32_t)a.show_accel : 0u, a.max_mip, box);
 		if (t < 16384.0f) p.alive = 1;
 	}
 	p.t = t;
@@ -1913,7 +1914,7 @@ __global__ void k_render_inputs(RenderArgs a, uint32_t n, uint32_t n_steps, Payl
 	const Cone cone = make_cone(a.cone_angle_constant);
 	float t = p.t;
 	for (uint32_t j = 0; j < n_steps; ++j) {
-		t = advance_to_occupied(t, cone, o, d, idir, a.bitfield, 0, a.max_mip, box);
+		t = advance_to_occupied(t, cone, o, d, idir, a.bitfield, a.show_accel >= 0 ? (uint32_t)a.show_accel : 0u, a.max_mip, box);
 		if (t >= 16384.0f) {
 			p.n_steps = j;
 			return;
@@ -1932,9 +1933,11 @@ __global__ void k_render_inputs(RenderArgs a, uint32_t n, uint32_t n_steps, Payl
 
 // composite_kernel_nerf (:1016-1196); network output RM [16 x stride]. The colour of a step by ERenderMode
 // (:1183-1208): Shade the network's rgb; Normals normalize(-density'(raw) * d(raw density)/d(position)), the
-// gradient in the coordinates' position rows (render_frame's grad); Positions (pos - 0.5) / 2 + 0.5 (show_accel
-// off); Depth dot(camera forward, pos - ray origin) * depth_scale; AO the step's alpha. pos = unwarp_position of
-// the step's coordinate over the aabb the inputs were warped with.
+// gradient in the coordinates' position rows (render_frame's grad); Positions (pos - 0.5) / 2 + 0.5, or with
+// show_accel >= 0 the step's occupancy cell (mip = max(show_accel, mip_from_pos), red 1 - mip / 7, green and blue
+// two pcg32 draws seeded by the cell); EncodingVis the warped position (the network's input); Depth dot(camera
+// forward, pos - ray origin) * depth_scale; AO the step's alpha. pos = unwarp_position of the step's coordinate over
+// the aabb the inputs were warped with. show_accel >= 0 also makes every step opaque (alpha 1, :1078-1080).
 __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, uint32_t current_step, uint32_t n_steps,
                                    Payload* __restrict__ pay, float* __restrict__ rgba, const float* __restrict__ coords,
                                    const f16* __restrict__ out) {
@@ -1951,7 +1954,7 @@ __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, ui
 		const float o3 = (float)out[r + 3 * (size_t)stride];
 		const float T = 1.f - c[3];
 		const float dt = unwarp_dt(coords[r * 7 + 3]);
-		const float alpha = 1.f - ngp_expf_fast(-network_to_density(o3, a.density_activation) * dt);
+		const float alpha = a.show_accel >= 0 ? 1.f : 1.f - ngp_expf_fast(-network_to_density(o3, a.density_activation) * dt);
 		const float weight = alpha * T;
 		float rgb[3];
 		if (a.render_mode == RENDER_NORMALS) {
@@ -1963,7 +1966,19 @@ __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, ui
 			float pos[3];
 #pragma unroll
 			for (int k = 0; k < 3; ++k) pos[k] = coords[r * 7 + k] * (a.aabb_max[k] - a.aabb_min[k]) + a.aabb_min[k];
-			if (a.render_mode == RENDER_POSITIONS) {
+			if (a.render_mode == RENDER_POSITIONS && a.show_accel >= 0) {
+				// :1190-1199: the cell of the cascade the march tested, coloured by its mip and a seeded pcg32
+				const uint32_t mip = max((uint32_t)a.show_accel, mip_from_pos(v3(pos[0], pos[1], pos[2]), CASCADES - 1));
+				const uint32_t res = GRIDSIZE >> mip;
+				const int ix = (int)(pos[0] * (float)res), iy = (int)(pos[1] * (float)res), iz = (int)(pos[2] * (float)res);
+				Pcg32Dev rng{0u, (1ull << 1u) | 1u};  // pcg32(initstate, initseq = 1)
+				pcg_next(rng);
+				rng.state += (uint64_t)(int64_t)(ix + iy * 232323 + iz * 727272);
+				pcg_next(rng);
+				rgb[0] = 1.f - (float)mip * (1.f / (float)(CASCADES - 1));
+				rgb[1] = pcg_float(rng);
+				rgb[2] = pcg_float(rng);
+			} else if (a.render_mode == RENDER_POSITIONS) {
 #pragma unroll
 				for (int k = 0; k < 3; ++k) rgb[k] = (pos[k] - 0.5f) / 2.0f + 0.5f;
 			} else {
@@ -1972,6 +1987,9 @@ __global__ void k_render_composite(RenderArgs a, uint32_t n, uint32_t stride, ui
 			}
 		} else if (a.render_mode == RENDER_AO) {
 			rgb[0] = rgb[1] = rgb[2] = alpha;
+		} else if (a.render_mode == RENDER_ENCODING_VIS) {
+#pragma unroll
+			for (int k = 0; k < 3; ++k) rgb[k] = coords[r * 7 + k];  // warped_pos
 		} else {
 			rgb[0] = network_to_rgb(o0, a.rgb_activation);
 			rgb[1] = network_to_rgb(o1, a.rgb_activation);
@@ -2022,8 +2040,8 @@ __global__ void k_render_accumulate(uint32_t n4, float w, const float* __restric
 
 void render_frame(const RenderArgs& a, uint32_t spp, RenderWorkspace& ws, const std::function<void(uint32_t, const float*, f16*)>& infer,
                   float* out, hipStream_t s, const std::function<void(uint32_t, float*)>& grad) {
-	NGP_CHECK(a.render_mode <= RENDER_DEPTH && (a.render_mode != RENDER_NORMALS || grad),
-	          "render: AO, Shade, Normals, Positions and Depth are implemented");
+	NGP_CHECK((a.render_mode <= RENDER_DEPTH || a.render_mode == RENDER_ENCODING_VIS) && (a.render_mode != RENDER_NORMALS || grad),
+	          "render: AO, Shade, Normals, Positions, Depth and EncodingVis are implemented");
 	const uint32_t n_px = a.width * a.height;
 	if (n_px == 0) return;
 	const uint32_t MARCH_ITER = 10000, MIN_STEPS = 1, MAX_STEPS = 8, TARGET_QUERIES = 2 * 1024 * 1024;

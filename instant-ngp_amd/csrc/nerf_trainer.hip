@@ -84,6 +84,7 @@ struct ngp_nerf_renderer {
 	Buf pay0, pay1, payh, rgba0, rgba1, rgbah, coords, out, frame, counters;
 	uint32_t* host_counters = nullptr;
 	uint32_t render_mode = RENDER_SHADE;  // ngp_nerf_renderer_set_mode
+	int32_t show_accel = -1;             // ngp_nerf_renderer_set_show_accel
 	float depth_scale = 1.0f;             // ngp_nerf_renderer_set_depth_scale
 	~ngp_nerf_renderer() { if (host_counters) (void)hipHostFree(host_counters); }
 };
@@ -460,8 +461,14 @@ int ngp_nerf_renderer_create(ngp_nerf_renderer** out) {
 }
 void ngp_nerf_renderer_destroy(ngp_nerf_renderer* r) { delete r; }
 int ngp_nerf_renderer_set_mode(ngp_nerf_renderer* r, int render_mode) {
-	if (!r || render_mode < (int)RENDER_AO || render_mode > (int)RENDER_DEPTH) return NGP_INVALID;
+	if (!r || render_mode < (int)RENDER_AO || (render_mode > (int)RENDER_DEPTH && render_mode != (int)RENDER_ENCODING_VIS))
+		return NGP_INVALID;
 	r->render_mode = (uint32_t)render_mode;
+	return NGP_OK;
+}
+int ngp_nerf_renderer_set_show_accel(ngp_nerf_renderer* r, int show_accel) {
+	if (!r || show_accel < -1 || show_accel >= (int)CASCADES) return NGP_INVALID;
+	r->show_accel = show_accel;
 	return NGP_OK;
 }
 int ngp_nerf_renderer_set_depth_scale(ngp_nerf_renderer* r, float depth_scale) {
@@ -516,6 +523,7 @@ int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_confi
 		ws.host_counters = r->host_counters;
 		a.render_mode = r->render_mode;
 		a.depth_scale = r->depth_scale;
+		a.show_accel = r->show_accel;
 		auto infer = [&](uint32_t n, const float* coords, f16* out) {
 			check_rc(ngp_inference(model, s, n, coords, 7, out, n, NGP_LAYOUT_SOA, use_inference_params));
 		};

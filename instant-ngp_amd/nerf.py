@@ -349,13 +349,15 @@ class NerfRenderer:
         check(lib().ngp_nerf_renderer_create(C.byref(h)))
         self.handle = h
 
-    RENDER_MODES = {"AO": 0, "Shade": 1, "Normals": 2, "Positions": 3, "Depth": 4}  # ERenderMode (common.h:110-119)
+    RENDER_MODES = {"AO": 0, "Shade": 1, "Normals": 2, "Positions": 3, "Depth": 4, "EncodingVis": 9}  # ERenderMode (common.h:110-121)
 
     def render(self, network, cfg, camera, bitfield=None, spp=1, sample_index=0, min_transmittance=0.01,
                background=(0.0, 0.0, 0.0, 0.0), use_inference_params=True, stream=None, render_mode="Shade",
-               depth_scale=1.0):
-        """render_mode: an ERenderMode name; depth_scale (Depth): 1 / the dataset's scale (testbed_nerf.cu:2822)."""
+               depth_scale=1.0, show_accel=-1):
+        """render_mode: an ERenderMode name; depth_scale (Depth): 1 / the dataset's scale (testbed_nerf.cu:2822);
+        show_accel: Testbed::Nerf::show_accel (-1 off; 0..7: the march's minimum mip, opaque steps, Positions by cell)."""
         check(lib().ngp_nerf_renderer_set_mode(self.handle, self.RENDER_MODES[render_mode]))
+        check(lib().ngp_nerf_renderer_set_show_accel(self.handle, int(show_accel)))
         check(lib().ngp_nerf_renderer_set_depth_scale(self.handle, float(depth_scale)))
         out = torch.empty((camera.height, camera.width, 4), dtype=torch.float32, device="cuda")
         bg = (C.c_float * 4)(*[float(v) for v in background])

@@ -18,6 +18,7 @@ typedef struct { uint64_t state, inc; } orc_pcg32;
 uint32_t orc_pcg32_next_uint(orc_pcg32* r);
 float orc_pcg32_next_float(orc_pcg32* r);
 void orc_pcg32_advance(orc_pcg32* r, int64_t delta);
+void orc_pcg32_seed(orc_pcg32* r, uint64_t initstate, uint64_t initseq);
 float orc_f16_to_f32(uint16_t h);
 uint16_t orc_f32_to_f16(float f);
 
@@ -684,12 +685,14 @@ static void pixel_offset(uint32_t spp, float* ox, float* oy) {
 	*oy = fractf_(0.5f - ay + by);
 }
 
+/* if_unoccupied_advance_to_next_occupied_voxel (testbed_nerf.cu:811-842): mip = clamp(mip_from_pos, min_mip, max_mip) */
 static float adv_occupied(float t, float cone, const float* o, const float* d, const float* idir, const uint8_t* bf,
-                          uint32_t max_mip, const ocfg* c) {
+                          uint32_t min_mip, uint32_t max_mip, const ocfg* c) {
 	for (;;) {
 		float pos[3] = {o[0] + t * d[0], o[1] + t * d[1], o[2] + t * d[2]};
 		if (t >= 16384.0f || !contains(c, pos)) return 16384.0f;
 		uint32_t mip = mip_pos(pos, CASCADES - 1);
+		if (mip < min_mip) mip = min_mip;
 		if (mip > max_mip) mip = max_mip;
 		if (!bf || occupied(pos, bf, mip)) return t;
 		while (mip < max_mip && !occupied(pos, bf, mip + 1)) ++mip;
@@ -699,7 +702,8 @@ static float adv_occupied(float t, float cone, const float* o, const float* d, c
 
 /* coords: [W*H x max_per_ray x 7]; counts: [W*H] (-1 when the ray misses the aabb) */
 EXPORT void orc_nerf_render_march(const ocfg* c, const oimg* cam, const uint8_t* bf, uint32_t sample_index, uint32_t max_per_ray,
-                                  float* coords, int32_t* counts) {
+                                  float* coords, int32_t* counts, int show_accel) {
+	const uint32_t min_mip = show_accel >= 0 ? (uint32_t)show_accel : 0u;  /* testbed_nerf.cu:2497, 2594 */
 	float m[12];
 	orc_camera_matrix(cam->xform, m);
 	const uint32_t W = cam->width, H = cam->height;
@@ -730,7 +734,7 @@ EXPORT void orc_nerf_render_march(const ocfg* c, const oimg* cam, const uint8_t*
 		t = from_step(to_step(t, cone) + orc_ld_random_val(sample_index, i * 786433u, 0), cone);
 		uint32_t k = 0;
 		for (; k < max_per_ray; ++k) {
-			t = adv_occupied(t, cone, o, d, idir, bf, c->max_cascade, c);
+			t = adv_occupied(t, cone, o, d, idir, bf, min_mip, c->max_cascade, c);
 			if (t >= 16384.0f) break;
 			const float dt = calc_dt(t, cone);
 			const float pos[3] = {o[0] + d[0] * t, o[1] + d[1] * t, o[2] + d[2] * t};
@@ -751,7 +755,7 @@ EXPORT void orc_nerf_render_march(const ocfg* c, const oimg* cam, const uint8_t*
  * (:2164-2196) decodes sRGB for Shade only. cam: the view (its camera matrix, for Depth). */
 EXPORT void orc_nerf_render_composite_mode(const ocfg* c, const oimg* cam, uint32_t n_px, uint32_t max_per_ray, const float* coords,
                                            const int32_t* counts, const uint16_t* out16, float min_transmittance, const float* bg,
-                                           int mode, float depth_scale, float* frame) {
+                                           int mode, float depth_scale, int show_accel, float* frame) {
 	float m[12];
 	orc_camera_matrix(cam->xform, m);
 	const float diag[3] = {c->aabb_max[0] - c->aabb_min[0], c->aabb_max[1] - c->aabb_min[1], c->aabb_max[2] - c->aabb_min[2]};
@@ -761,18 +765,32 @@ EXPORT void orc_nerf_render_composite_mode(const ocfg* c, const oimg* cam, uint3
 			const uint16_t* o = out16 + ((size_t)i * max_per_ray + k) * 16;
 			const float T = 1.f - a;
 			const float dt = coords[((size_t)i * max_per_ray + k) * 7 + 3] * (MIN_STEP * (1 << (CASCADES - 1)) - MIN_STEP) + MIN_STEP;
-			const float alpha = 1.f - ngp_expf(-to_dens(orc_f16_to_f32(o[3]), c->density_activation) * dt);
+			/* show_accel >= 0: every step opaque (testbed_nerf.cu:1078-1080) */
+			const float alpha = show_accel >= 0 ? 1.f : 1.f - ngp_expf(-to_dens(orc_f16_to_f32(o[3]), c->density_activation) * dt);
 			const float w = alpha * T;
 			float rgb[3];
 			if (mode == 1) {
 				for (int q = 0; q < 3; ++q) rgb[q] = to_rgb(orc_f16_to_f32(o[q]), c->rgb_activation);
 			} else if (mode == 0) {
 				rgb[0] = rgb[1] = rgb[2] = alpha;
+			} else if (mode == 9) {  /* EncodingVis: the warped position (:1202-1203) */
+				const float* wp = coords + ((size_t)i * max_per_ray + k) * 7;
+				for (int q = 0; q < 3; ++q) rgb[q] = wp[q];
 			} else {
 				const float* wp = coords + ((size_t)i * max_per_ray + k) * 7;
 				float pos[3];
 				for (int q = 0; q < 3; ++q) pos[q] = wp[q] * diag[q] + c->aabb_min[q];
-				if (mode == 3) {
+				if (mode == 3 && show_accel >= 0) {  /* :1190-1199 */
+					uint32_t mip = mip_pos(pos, CASCADES - 1);
+					if (mip < (uint32_t)show_accel) mip = (uint32_t)show_accel;
+					const uint32_t res = GRIDSIZE >> mip;
+					const int ix = (int)(pos[0] * (float)res), iy = (int)(pos[1] * (float)res), iz = (int)(pos[2] * (float)res);
+					orc_pcg32 rng;
+					orc_pcg32_seed(&rng, (uint64_t)(int64_t)(ix + iy * 232323 + iz * 727272), 1u);
+					rgb[0] = 1.f - (float)mip * (1.f / (float)(CASCADES - 1));
+					rgb[1] = orc_pcg32_next_float(&rng);
+					rgb[2] = orc_pcg32_next_float(&rng);
+				} else if (mode == 3) {
 					for (int q = 0; q < 3; ++q) rgb[q] = (pos[q] - 0.5f) / 2.0f + 0.5f;
 				} else {
 					const float z = (m[6] * (pos[0] - m[9]) + m[7] * (pos[1] - m[10]) + m[8] * (pos[2] - m[11])) * depth_scale;
@@ -795,7 +813,7 @@ EXPORT void orc_nerf_render_composite_mode(const ocfg* c, const oimg* cam, uint3
 }
 EXPORT void orc_nerf_render_composite(const ocfg* c, const oimg* cam, uint32_t n_px, uint32_t max_per_ray, const float* coords,
                                       const int32_t* counts, const uint16_t* out16, float min_transmittance, const float* bg, float* frame) {
-	orc_nerf_render_composite_mode(c, cam, n_px, max_per_ray, coords, counts, out16, min_transmittance, bg, 1, 1.0f, frame);
+	orc_nerf_render_composite_mode(c, cam, n_px, max_per_ray, coords, counts, out16, min_transmittance, bg, 1, 1.0f, -1, frame);
 }
 
 /* The shared transcendental (instant-ngp_amd/csrc/ngp_math.h), exported for its accuracy test:

@@ -477,9 +477,9 @@ def _declare_nerf(L):
     d("orc_fill_rollover_f32", None, u32, u32, u32, P)
     d("orc_fill_rollover_f16", None, u32, u32, u32, P, C.c_int)
     d("orc_ld_random_val", f32, u32, u32, u32)
-    d("orc_nerf_render_march", None, P, P, P, u32, u32, P, P)
+    d("orc_nerf_render_march", None, P, P, P, u32, u32, P, P, C.c_int)
     d("orc_nerf_render_composite", None, P, P, u32, u32, P, P, P, f32, P, P)
-    d("orc_nerf_render_composite_mode", None, P, P, u32, u32, P, P, P, f32, P, C.c_int, f32, P)
+    d("orc_nerf_render_composite_mode", None, P, P, u32, u32, P, P, P, f32, P, C.c_int, f32, C.c_int, P)
 
 
 N_CELLS = 128 ** 3
@@ -682,19 +682,20 @@ def sdf_signed_distance(pos, tris):
     return out
 
 
-RENDER_MODES = {"AO": 0, "Shade": 1, "Positions": 3, "Depth": 4}  # ERenderMode (common.h:110-119)
+RENDER_MODES = {"AO": 0, "Shade": 1, "Positions": 3, "Depth": 4, "EncodingVis": 9}  # ERenderMode (common.h:110-121)
 
 
 def nerf_render(cfg, cam, model, params16, bitfield, sample_index=0, min_transmittance=0.01, bg=(0, 0, 0, 0),
-                max_per_ray=1024, render_mode="Shade", depth_scale=1.0):
+                max_per_ray=1024, render_mode="Shade", depth_scale=1.0, show_accel=-1):
     """NerfTracer restated per ray: march, oracle NerfNetwork on every sample, composite (the step colour of
-    render_mode: AO, Shade, Positions or Depth), shade. Returns linear rgba [H, W, 4] and the per-pixel sample
-    counts."""
+    render_mode: AO, Shade, Positions, Depth or EncodingVis; show_accel >= 0: the march from that mip up, opaque
+    steps, Positions by occupancy cell), shade. Returns linear rgba [H, W, 4] and the per-pixel sample counts."""
     W, H = cam.width, cam.height
     coords = np.zeros((W * H, max_per_ray, 7), np.float32)
     counts = np.zeros(W * H, np.int32)
     bfp = ptr(bitfield) if bitfield is not None else None
-    lib().orc_nerf_render_march(C.byref(cfg), C.byref(cam), bfp, sample_index, max_per_ray, ptr(coords), ptr(counts))
+    lib().orc_nerf_render_march(C.byref(cfg), C.byref(cam), bfp, sample_index, max_per_ray, ptr(coords), ptr(counts),
+                                int(show_accel))
     mask = np.arange(max_per_ray)[None, :] < counts[:, None]
     out16 = np.zeros((W * H, max_per_ray, 16), np.uint16)
     if mask.any():
@@ -704,7 +705,7 @@ def nerf_render(cfg, cam, model, params16, bitfield, sample_index=0, min_transmi
     bgv = np.asarray(bg, np.float32)
     lib().orc_nerf_render_composite_mode(C.byref(cfg), C.byref(cam), W * H, max_per_ray, ptr(coords), ptr(counts),
                                          ptr(out16), min_transmittance, ptr(bgv), RENDER_MODES[render_mode],
-                                         float(depth_scale), ptr(frame))
+                                         float(depth_scale), int(show_accel), ptr(frame))
     return frame.reshape(H, W, 4), counts
 
 
@@ -717,7 +718,7 @@ def nerf_render_normals(cfg, cam, model, params16, bitfield, sample_index=0, min
     coords = np.zeros((W * H, max_per_ray, 7), np.float32)
     counts = np.zeros(W * H, np.int32)
     bfp = ptr(bitfield) if bitfield is not None else None
-    lib().orc_nerf_render_march(C.byref(cfg), C.byref(cam), bfp, sample_index, max_per_ray, ptr(coords), ptr(counts))
+    lib().orc_nerf_render_march(C.byref(cfg), C.byref(cam), bfp, sample_index, max_per_ray, ptr(coords), ptr(counts), -1)
     mask = np.arange(max_per_ray)[None, :] < counts[:, None]
     raw = np.zeros((W * H, max_per_ray), np.float32)
     grad = np.zeros((W * H, max_per_ray, 3), np.float32)

@@ -132,19 +132,25 @@ def test_psnr_after_training(pkg):
     assert np.mean(ps) > 20.0, ps
 
 
-@pytest.mark.parametrize("mode,seed,frac,aabb_scale", [("Depth", 3, 1.0, 1.0), ("Positions", 8, 0.3, 1.0), ("AO", 6, 0.3, 4.0),
-                                                        ("Depth", 5, 0.3, 8.0)])
-def test_render_modes_match_oracle(pkg, orc, mode, seed, frac, aabb_scale):
-    """ERenderMode AO, Positions and Depth (testbed_nerf.cu:1189-1208: each step's alpha, (pos - 0.5) / 2 + 0.5,
-    dot(camera forward, pos - origin) * depth_scale with depth_scale = 1 / dataset scale, :2822), composited like
-    Shade and shaded without sRGB decoding (:2183-2186). Same march and bars as the Shade comparison."""
+@pytest.mark.parametrize("mode,seed,frac,aabb_scale,show_accel", [
+    ("Depth", 3, 1.0, 1.0, -1), ("Positions", 8, 0.3, 1.0, -1), ("AO", 6, 0.3, 4.0, -1), ("Depth", 5, 0.3, 8.0, -1),
+    ("EncodingVis", 7, 0.3, 1.0, -1), ("EncodingVis", 4, 0.3, 8.0, -1),
+    ("Positions", 9, 0.3, 1.0, 0), ("Positions", 10, 0.3, 8.0, 2), ("Shade", 11, 0.3, 4.0, 1)])
+def test_render_modes_match_oracle(pkg, orc, mode, seed, frac, aabb_scale, show_accel):
+    """ERenderMode AO, Positions, Depth and EncodingVis (testbed_nerf.cu:1189-1208: each step's alpha, (pos - 0.5) / 2
+    + 0.5, dot(camera forward, pos - origin) * depth_scale with depth_scale = 1 / dataset scale, :2822, the warped
+    position), composited like Shade and shaded without sRGB decoding (:2183-2186). show_accel >= 0 (the GUI's
+    "Show acceleration", testbed.cu:1678): the march from that mip up (:2497, 2594), opaque steps (:1078-1080) and
+    Positions coloured by the step's occupancy cell (:1190-1199: 1 - mip / 7 and two pcg32 draws seeded by the
+    cell). Same march and bars as the Shade comparison."""
     cam, cfg, net, p16, bf, m = _setup(pkg, orc, seed, frac, aabb_scale)
     r = pkg.nerf.NerfRenderer()
     bg = (0.1, 0.2, 0.3, 1.0)
     ds = 1.0 / 0.33  # nerf_synthetic's scale (nerf_loader.cu:388)
     img = r.render(net, cfg, cam, torch.from_numpy(bf).cuda(), spp=1, min_transmittance=1e-4, background=bg,
-                   use_inference_params=False, render_mode=mode, depth_scale=ds).cpu().numpy()
-    ref, counts = orc.nerf_render(cfg, cam, m, p16, bf, min_transmittance=1e-4, bg=bg, render_mode=mode, depth_scale=ds)
+                   use_inference_params=False, render_mode=mode, depth_scale=ds, show_accel=show_accel).cpu().numpy()
+    ref, counts = orc.nerf_render(cfg, cam, m, p16, bf, min_transmittance=1e-4, bg=bg, render_mode=mode, depth_scale=ds,
+                                  show_accel=show_accel)
     assert (counts > 0).mean() > 0.2
     assert np.isfinite(img).all()
     scale = max(1.0, float(np.abs(ref).max()))  # depth values grow with the scene's size

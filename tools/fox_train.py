@@ -38,11 +38,12 @@ def run(pkg, data=DEFAULT_DATA, seconds=30.0, holdout=10, eval_views=5, spp=1):
     tr = pkg.Trainer(net, ncfg["optimizer"])
     run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
     torch.cuda.synchronize()
-    samples, steps, curve = 0, 0, []
+    samples, steps, curve, trained = 0, 0, [], 0
     t_start = time.time()
     while True:
         st = run.train_step(get_loss=(steps % 100 == 0))
         samples += st["measured_batch_size"]
+        trained += min(st["measured_batch_size"], 1 << 18)  # the batch the step trains on (rollover truncates)
         steps += 1
         if steps % 100 == 1:
             curve.append((round(time.time() - t_start, 2), steps, round(st["loss"], 6)))
@@ -68,6 +69,7 @@ def run(pkg, data=DEFAULT_DATA, seconds=30.0, holdout=10, eval_views=5, spp=1):
     return {
         "metric": "training samples/sec + PSNR, NeRF fox (C3) on 1 MI355X",
         "value": samples / t_train, "unit": "samples/s",
+        "value_trained": trained / t_train,  # min(measured_batch_size, B) per step: the samples actually trained
         "psnr_heldout": float(np.mean(ps)) if ps else None, "psnr_views": [round(p, 2) for p in ps],
         "psnr_train_views": [round(p, 2) for p in ps_train],
         "train_seconds": round(t_train, 2), "steps": steps, "ms_per_step": 1e3 * t_train / steps,
