@@ -735,16 +735,16 @@ def main():
             # engine's RCCL communicator attached at world 1, timed like the headline (one graph of K steps),
             # sharded (reduce-scatter + slice update + all-gather) and all-reduce, against the fused N = 1 step
             res["dp1_overhead"] = {"note": "world-1 RCCL exchange attached, vs the fused single-GPU step above. shard: "
-                                           "the backward stores the fp32 gradient itself, and each of the engine's "
-                                           "default parameter parts is reduce-scattered, its slice of the optimizer "
-                                           "updated (here all of it) and its fp16 weights all-gathered on an exchange "
-                                           "stream while the backward sums the next part; shard_p1: the same in one "
-                                           "part after the backward; shard_wire16: default parts, fp16 reduce-scatter; "
-                                           "allreduce: fp16 gradient, widen, all-reduce, narrow, replicated update"}
-            for mode in ("shard", "shard_p1", "shard_wire16", "allreduce"):
+                                           "the backward stores the fp32 gradient itself, reduce-scatter, the rank's "
+                                           "slice of the optimizer (here all of it), all-gather of the fp16 weights; "
+                                           "shard_p2: the same in two parameter parts, the higher one exchanged on a "
+                                           "second stream while the backward sums the lower one (trainer option "
+                                           "dp_parts); shard_wire16: fp16 reduce-scatter; allreduce: fp16 gradient, "
+                                           "widen, all-reduce, narrow, replicated update"}
+            for mode in ("shard", "shard_p2", "shard_wire16", "allreduce"):
                 sd, cd, _, _, commd = nerf_pass(pkg, args.variant, n, 0, 1, args.opt, args.overlap, args.wire,
                                                 shard=mode != "allreduce", exchange_at_world_1=True,
-                                                dp_parts=1 if mode == "shard_p1" else args.dp_parts,
+                                                dp_parts=2 if mode == "shard_p2" else args.dp_parts,
                                                 dp_wire16=mode == "shard_wire16")
                 dtd, launchd, kd = timed_steps(lib, sd, args.steps, args.warmup, 1, cd if args.graph else None)
                 res["dp1_overhead"][mode] = {

@@ -549,8 +549,10 @@ struct ngp_trainer {
 	// The exchange in parameter parts (trainer option "dp_parts"): part j = parameters [pb[j], pb[j + 1]), multiples
 	// of 8 world; rank r owns the r-th of the world equal slices of every part. Each part is reduce-scattered,
 	// its slice updated and all-gathered as soon as the backward has summed it (BwdParts), on the exchange
-	// stream xs, while the backward sums the next part.
-	uint32_t dp_parts = 2;
+	// stream xs, while the backward sums the next part. Default 1 part: measured at world 1 the parted
+	// step costs 35-40 us more (the bucket ranges' own launches, and the step's graph runs the two streams' work in
+	// sequence), more than the overlap could hide at N = 8 under DESIGN §7's bandwidth model.
+	uint32_t dp_parts = 1;
 	bool dp_wire16 = false;      // option "dp_wire16": reduce-scatter the fp16 gradient (half the bytes; rounded per hop)
 	std::vector<uint64_t> pb;
 	hipStream_t xs = nullptr;
@@ -603,7 +605,13 @@ struct ngp_trainer {
 	}
 	void ensure_exchange_stream() {
 		if (xs) return;
-		NGP_HIP(hipStreamCreateWithFlags(&xs, hipStreamNonBlocking));
+		// the exchange stream at the highest priority: a stream of the default priority may share a hardware queue
+		// with the step's stream (GPU_MAX_HW_QUEUES), which would run its work in submission order, after the step's
+		// next launches. NGP_XS_PRIORITY=0: the default priority (A/B)
+		int lo = 0, hi = 0;
+		NGP_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+		const char* e = getenv("NGP_XS_PRIORITY");
+		NGP_HIP(hipStreamCreateWithPriority(&xs, hipStreamNonBlocking, e && atoi(e) == 0 ? 0 : hi));
 		for (hipEvent_t& ev : ev_part) NGP_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
 		NGP_HIP(hipEventCreateWithFlags(&ev_xs, hipEventDisableTiming));
 	}

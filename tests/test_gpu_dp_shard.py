@@ -12,7 +12,7 @@ rank updating every record) rounds the same sums the same way, so the two must t
 * one rank over the engine's RCCL communicator (world 1), captured steps: the sharded step trains bit for bit
   like the fused single-GPU step.
 
-Both in every form of the exchange: in 1, 2 (the default) or 4 parameter parts, each exchanged on the exchange
+Both in every form of the exchange: in 1 (the default), 2 or 4 parameter parts, each exchanged on the exchange
 stream as soon as the backward has summed it (trainer option dp_parts), and with the fp16 wire (dp_wire16: the
 reduce-scatter sums fp16 gradients). gloo's reduce-scatter sums the fp16 values in fp32 and rounds once, and at
 world 1 nothing is summed, so the fp16 wire is bit-exact here; RCCL's fp16 ring at world >= 3 rounds per hop
@@ -57,11 +57,11 @@ def _batch(rank, step, n=1 << 14):
     return torch.from_numpy(x).cuda(), torch.from_numpy(dl).cuda()
 
 
-SHARD_MODES = ("shard", "shard_p1", "shard_p4", "shard_widen", "shard_wire16")
+SHARD_MODES = ("shard", "shard_p2", "shard_p4", "shard_widen", "shard_wire16")
 
 
 def _shard_options(tr, mode):
-    tr.set_option("dp_parts", {"shard_p1": 1, "shard_p4": 4}.get(mode, 2))
+    tr.set_option("dp_parts", {"shard_p2": 2, "shard_p4": 4}.get(mode, 1))
     tr.set_option("dp_wire16", int(mode == "shard_wire16"))
 
 
@@ -135,7 +135,7 @@ def _rccl_world1(_rank, out_dir):
     x, dl = _batch(0, 0, n)
     x1, dl1 = _batch(0, 1, n)
     res = {}
-    for mode in ("plain", "shard", "shard_p1", "shard_p4", "shard_wire16"):
+    for mode in ("plain", "shard", "shard_p2", "shard_p4", "shard_wire16"):
         cfg = pkg.nerf_config("C2")
         net = pkg.create_nerf_network(cfg)
         tr = pkg.Trainer(net, cfg["optimizer"], seed=1337)
@@ -168,7 +168,7 @@ def test_sharded_optimizer_rccl_world1_equals_fused_step(tmp_path):
     import torch.multiprocessing as mp
     mp.spawn(_rccl_world1, args=(str(tmp_path),), nprocs=1, join=True)
     r = json.load(open(tmp_path / "w1.json"))
-    for mode in ("shard", "shard_p1", "shard_p4", "shard_wire16"):
+    for mode in ("shard", "shard_p2", "shard_p4", "shard_wire16"):
         assert r["plain"] == r[mode], mode
     assert r["shard"][3] == 11
 

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--wire16", type=int, default=0)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--steps-per-launch", type=int, default=4)
+    ap.add_argument("--eager", type=int, default=0, help="1: time eager train_step calls instead of a captured graph")
     args = ap.parse_args()
     import bench
     from __graft_entry__ import load_package
@@ -30,16 +31,22 @@ def main():
     with torch.cuda.stream(s):
         for _ in range(3):
             step()
-        g = capture(args.steps_per_launch)
+        g = None if args.eager else capture(args.steps_per_launch)
         torch.cuda.synchronize()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record(s)
         for _ in range(args.launches):
-            g.launch()
+            if g is None:
+                for _ in range(args.steps_per_launch):
+                    step()
+            else:
+                g.launch()
         ev1.record(s)
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / (args.launches * args.steps_per_launch)
-    print(f"sharded C2 step, world 1, {args.parts} parts, wire16={args.wire16}: {ms * 1e3:.1f} us per step")
+    print(f"sharded C2 step, world 1, {args.parts} parts, wire16={args.wire16}, {'eager' if args.eager else 'graph'} "
+          f"(DEBUG_CLR_GRAPH_PACKET_CAPTURE={os.environ.get('DEBUG_CLR_GRAPH_PACKET_CAPTURE')}, "
+          f"DEBUG_HIP_FORCE_GRAPH_QUEUES={os.environ.get('DEBUG_HIP_FORCE_GRAPH_QUEUES')}): {ms * 1e3:.1f} us per step")
 
 
 if __name__ == "__main__":
