@@ -906,8 +906,29 @@ __device__ __forceinline__ void train_store_dw(const f32x4* dw, const NerfMlpArg
 	dw_store<1, ES>(dw + T::W_D0, slab, dw0, 16 * ES, wave, 0, lane);
 }
 
+// Timing experiments only (-DNGP_TRAIN_CLOCK, DESIGN §6 phase costs; tools/train_clock.py): thread 0 of blocks
+// 0..1023 (wave 0) stamps the 100-MHz wall clock at the phase boundaries: slot 0 entry, 1 weights loaded, then per
+// iteration i slots 2 + 10 i + k for k = 0 inputs taken, 1 density forward, 2 rgb forward (+ output store),
+// 3 images written, 4 rgb backward chain, 5 density backward chain, 6 dL/denc stored, 7 barrier, 8 dW, 9 barrier;
+// slot 127 exit. Scheduling barriers keep the phases apart, so the stamped kernel is slower than the plain one.
+#ifdef NGP_TRAIN_CLOCK
+constexpr int TRC_SLOTS = 128;
+__device__ uint64_t g_train_clock[1024 * TRC_SLOTS];
+#define TRC_MARK(i)                                                                                               \
+	do {                                                                                                          \
+		__builtin_amdgcn_sched_barrier(0);                                                                        \
+		if (threadIdx.x == 0 && blockIdx.x < 1024 && (i) < TRC_SLOTS) g_train_clock[blockIdx.x * TRC_SLOTS + (i)] = wall_clock64(); \
+		__builtin_amdgcn_sched_barrier(0);                                                                        \
+	} while (0)
+#define TRC_IT(k) TRC_MARK(2 + 10 * (int)trc_it + (k))
+#else
+#define TRC_MARK(i) do {} while (0)
+#define TRC_IT(k) do {} while (0)
+#endif
+
 template <int ES, int DH, int RH>
 __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) k_nerf_mlp_train(const NerfMlpArgs a) {
+	TRC_MARK(0);
 	using Lay = NerfLayout<ES, DH, RH>;
 	using T = NerfTrainLayout<ES, DH, RH>;
 	extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -932,6 +953,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	f32x4 dw[T::N_DW];
 #pragma unroll
 	for (int q = 0; q < T::N_DW; ++q) dw[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+	TRC_MARK(1);
 
 	const uint32_t n_tiles = (a.n + 31) / 32;
 	f16x8 xe_n[ES];
@@ -949,6 +971,9 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 	load_inputs(blockIdx.x * 4 + wave);
 	// every wave runs the same number of iterations (the barriers need all four); tiles past the end
 	// run on zero inputs and zero output gradients, so their dW contribution is exactly zero
+#ifdef NGP_TRAIN_CLOCK
+	uint32_t trc_it = 0;
+#endif
 	for (uint32_t base = blockIdx.x * 4; base < n_tiles; base += gridDim.x * 4) {
 		const uint32_t tile = base + wave;
 		const uint32_t sample = tile * 32 + (lane & 31);
@@ -959,6 +984,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		const float cdx = cd_n[0], cdy = cd_n[1], cdz = cd_n[2];
 		const f16x4 dl_cur = dl_n;
 		load_inputs(tile + gridDim.x * 4);  // unconditional (past-the-end tiles read sample 0)
+		TRC_IT(0);
 
 		// ---- phase A: forward ----------------------------------------------------------------
 #pragma unroll
@@ -976,6 +1002,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		layer_fwd_reg<1, 4>(dacc, hd[DH - 1], wreg, Lay::F_DO);
 		f16x8 dout[2];
 		pack_tile(dacc[0], dout[0], dout[1], false);
+		TRC_IT(1);
 		f16x8 rin[2] = {dout[0], sh4_frag(cdx, cdy, cdz, h)};
 		if (!valid) rin[1] = f16x8{};
 		f16x8 hr[RH][4];
@@ -994,6 +1021,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 			if (h == 0) ro[3] = dout[0][0];  // extract_density (nerf_network.h:32-43)
 			store_out16(a.out, a.out_stride, a.out_layout, a.n, sample, h, ro);
 		}
+		TRC_IT(2);
 #pragma unroll
 		for (int l = 0; l < DH; ++l) img_store_acc<4>(img + T::I_HD + l * 32 * Lay::S_64, Lay::S_64, hd[l], lane);
 		{
@@ -1003,6 +1031,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		}
 #pragma unroll
 		for (int l = 0; l < RH; ++l) img_store_acc<4>(img + T::I_HR + l * 32 * Lay::S_64, Lay::S_64, hr[l], lane);
+		TRC_IT(3);
 
 		// ---- phase A: backward dX chain, every dZ kept in LDS ---------------------------------
 		float dsig;
@@ -1029,6 +1058,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 		pack_tile(a1[0], dd[0], dsh, false);  // dsh: rows 16..31 of dL/d(rgb input) = dL/d(SH encoding)
 		if (h == 0) dd[0][0] = (f16)((float)dd[0][0] + dsig);  // add_density_gradient (:63-74)
 		if (a.dL_dsh && valid) store_dsh(a.dL_dsh, sample, h, dsh);
+		TRC_IT(4);
 		img_store_acc<1>(img + T::I_ZDO, T::S_16, dd, lane);
 		layer_fwd_reg<2, 1>(acc, dd, breg, Lay::B_DO - Lay::N_FWD);
 		mask_pack<2>(acc, hd[DH - 1], dz);
@@ -1039,6 +1069,7 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 			mask_pack<2>(acc, hd[l - 1], dz);
 		}
 		img_store_acc<4>(img + T::I_ZD0, Lay::S_64, dz, lane);
+		TRC_IT(5);
 		if (a.dL_denc) {
 			f32x16 ae[Lay::ET];
 			layer_fwd_reg<Lay::ET, 4>(ae, dz, breg, Lay::B_D0 - Lay::N_FWD);
@@ -1056,13 +1087,21 @@ __global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 
 				}
 			}
 		}
+		TRC_IT(6);
 		__syncthreads();
+		TRC_IT(7);
 
 		// ---- phase B: this wave's quarter of dW over the four images ---------------------------
 		train_phase_b<ES, DH, RH>(dw, img_all, wave, lane);
+		TRC_IT(8);
 		__syncthreads();
+		TRC_IT(9);
+#ifdef NGP_TRAIN_CLOCK
+		++trc_it;
+#endif
 	}
 	train_store_dw<ES, DH, RH>(dw, a, wave, lane);
+	TRC_MARK(127);
 }
 
 template <int ES, int DH, int RH, int MODE>
@@ -1344,3 +1383,10 @@ void reduce_slabs(const float* slabs, uint32_t n_slabs, uint32_t n, f16* grad, b
 }
 
 }  // namespace ngp
+
+#ifdef NGP_TRAIN_CLOCK
+extern "C" __attribute__((visibility("default"))) int ngp_debug_train_clock(uint64_t* out, uint32_t n) {
+	return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(ngp::g_train_clock),
+	                                (size_t)(n < 1024 * ngp::TRC_SLOTS ? n : 1024 * ngp::TRC_SLOTS) * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
