@@ -544,6 +544,8 @@ def main():
                     help="weak: --batch samples per GPU; strong: --batch samples per step over all GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-seconds", type=float, default=30.0, help="full NeRF step + PSNR sub-record (0: off)")
+    ap.add_argument("--e2e-weak-seconds", type=float, default=15.0,
+                    help="N > 1: the e2e NeRF step with 2^18 samples per rank (weak scaling) for this long (0: off)")
     ap.add_argument("--no-c2p", action="store_true", help="skip the C2' (L=16) sub-record")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 (SDF, T=2^22) sub-records")
     ap.add_argument("--c5-online-steps", type=int, default=10,
@@ -562,8 +564,10 @@ def main():
     ap.add_argument("--dp-parts", type=int, default=None,
                     help="sharded exchange: parameter parts, each reduce-scattered / updated / all-gathered while the "
                          "backward sums the next (trainer option dp_parts; default: the engine's)")
-    ap.add_argument("--dp-wire16", type=int, default=0,
-                    help="sharded exchange: 1 = reduce-scatter the fp16 gradient (half the bytes; per-hop fp16 sums)")
+    ap.add_argument("--dp-wire16", type=int, default=1,
+                    help="sharded exchange: 1 = reduce-scatter the fp16 gradient buffer as fp16, the gradients' own "
+                         "precision (half the wire bytes of fp32; RCCL rounds each hop's partial sum to fp16), 0 = "
+                         "widened to fp32 (sums rounded once)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "gloo"],
                     help="N > 1 exchange: rccl (engine RCCL communicator, one GPU per rank) or gloo (host round "
                          "trip through torch.distributed: ranks may share a GPU, eager steps only)")
@@ -667,14 +671,18 @@ def main():
                   "ms_per_step": dts / args.steps * 1e3, "launch": launch_s,
                   "exchange_ms_per_step": exchange_ms(k_s)}
         del s_s, c_s, comm_s
-    e2e_dp = None
+    e2e_dp = e2e_dp_weak = None
     if world > 1 and args.variant == "C2" and args.e2e_seconds > 0:
         # the metric's full form on N GPUs: the Testbed NeRF step data-parallel (rays sharded with their
-        # global ids, RCCL all-reduce of gradients, density-grid maxima and counters), then PSNR on rank 0
+        # global ids, RCCL all-reduce of gradients, density-grid maxima and counters), then PSNR on rank 0.
+        # strong: the 1-GPU batch over N ranks (the 1-GPU ray set); weak: 2^18 samples per rank
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import psnr30
         e2e_dp = psnr30.run(pkg, seconds=args.e2e_seconds, images=args.e2e_images, res=args.e2e_res, rank=rank,
-                            world=world)
+                            world=world, dp_wire16=bool(args.dp_wire16))
+        if args.e2e_weak_seconds > 0:
+            e2e_dp_weak = psnr30.run(pkg, seconds=args.e2e_weak_seconds, images=args.e2e_images, res=args.e2e_res,
+                                     rank=rank, world=world, scaling="weak", dp_wire16=bool(args.dp_wire16))
 
     if rank == 0:
         kern_summary, rl = roofline(args.variant, n, kernels, *n_opt, slab_bytes=slab_b, fused_grid_updated=c5_fused)
@@ -726,6 +734,9 @@ def main():
                                 (strong["scaling"] if strong else None, strong["value"] if strong else None)):
                     if mode is not None:
                         res["vs_1gpu"][f"{mode}_ratio"] = round(v / vs1["value"], 4)
+            if e2e_dp_weak is not None:
+                res["e2e_weak"] = {k: e2e_dp_weak[k] for k in ("value", "value_trained", "unit", "psnr", "psnr_views",
+                                                               "train_seconds", "steps", "ms_per_step", "n_gpus", "config")}
             if e2e_dp is not None:
                 res["e2e"] = {k: e2e_dp[k] for k in ("value", "unit", "psnr", "psnr_views", "train_seconds", "steps",
                                                      "ms_per_step", "n_gpus", "data", "config")}

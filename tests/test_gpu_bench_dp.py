@@ -22,7 +22,7 @@ def test_bench_two_ranks_gloo_line():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--comm", "gloo", "--device", "0", "--graph", "0",
-           "--steps", "3", "--warmup", "1", "--e2e-seconds", "2", "--e2e-images", "8", "--e2e-res", "128",
+           "--steps", "3", "--warmup", "1", "--e2e-seconds", "2", "--e2e-weak-seconds", "2", "--e2e-images", "8", "--e2e-res", "128",
            "--c3-seconds", "0", "--no-cpu-baseline"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
     env.pop("WORLD_SIZE", None)
@@ -39,8 +39,8 @@ def test_bench_two_ranks_gloo_line():
     assert st is not None and st["scaling"] == "strong" and st["global_batch"] == res["config"]["batch_per_gpu"]
     assert st["exchange_ms_per_step"] is not None and st["exchange_ms_per_step"] > 0
     assert res["exchange_ms_per_step"] is not None and res["exchange_ms_per_step"] > 0
-    # the sharded optimizer (default): C2's gradients as fp32 reduce-scattered, the fp16 weights all-gathered
-    assert res["exchange_bytes"] == {"reduce_scatter_f32": 4 * 3302400, "all_gather_f16": 2 * 3302400}
+    # the sharded optimizer (default): C2's fp16 gradients reduce-scattered as fp16, the fp16 weights all-gathered
+    assert res["exchange_bytes"] == {"reduce_scatter_f16": 2 * 3302400, "all_gather_f16": 2 * 3302400}
     # every rank ends with the same parameters (same summed gradient; each slice updated once, then gathered)
     h = res["param_sha1_per_rank"]
     assert len(h) == 2 and h[0] == h[1]
@@ -52,3 +52,6 @@ def test_bench_two_ranks_gloo_line():
     # the data-parallel Testbed NeRF step (e2e over the two ranks) and its held-out PSNR on rank 0
     e = res["e2e"]
     assert e["n_gpus"] == 2 and e["steps"] > 0 and e["value"] > 0 and e["psnr"] > 10.0
+    # the same with 2^18 samples per rank (weak scaling: global batch 2 x 2^18)
+    w = res["e2e_weak"]
+    assert w["n_gpus"] == 2 and w["steps"] > 0 and w["value"] > 0 and w["config"]["batch"] == 2 << 18

@@ -19,23 +19,29 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8, rank=0, world=1):
+def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8, rank=0, world=1, scaling="strong", dp_wire16=True):
     """Train the full NeRF step for `seconds` of wall clock on the procedural stand-in, then render the
     held-out views. Returns the result dict (samples/s over the training wall time, mean PSNR).
     world > 1 (torch.distributed initialised): data-parallel training (NerfTraining.set_data_parallel:
     rays sharded with their global ids, engine RCCL exchange); every rank stops after the same step
-    (decided jointly every 32 steps) and rank 0 renders the held-out views."""
+    (decided jointly every 32 steps) and rank 0 renders the held-out views. scaling "strong" (SURVEY §8e): the
+    1-GPU batch of 2^18 samples split over the ranks, the 1-GPU ray set; "weak": 2^18 samples per rank (the global
+    batch, target_batch_size, N x 2^18)."""
     S = pkg.synthetic
     t0 = time.time()
     ds = S.lego_like_dataset(n_images=images, width=res, height=res, seed=0, device="cuda")
     t_data = time.time() - t0
     cfg = pkg.nerf.default_config(1.0)
+    if scaling == "weak":
+        cfg.target_batch_size = (1 << 18) * world
+    batch = int(cfg.target_batch_size)
     ncfg = pkg.nerf_config("C2")
     net = pkg.create_nerf_network(ncfg)
     tr = pkg.Trainer(net, ncfg["optimizer"])
     run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
     if world > 1:
         import torch.distributed as dist
+        tr.set_option("dp_wire16", int(dp_wire16))  # the fp16 gradient buffer reduce-scattered as fp16 (DESIGN §7)
         run.set_data_parallel(rank, world)
         dist.barrier()
     torch.cuda.synchronize()
@@ -45,7 +51,7 @@ def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8, rank=0, wor
     while True:
         st = run.train_step(get_loss=(steps % 100 == 0))
         samples += st["measured_batch_size"]
-        trained += min(st["measured_batch_size"], 1 << 18)  # the batch the step trains on (rollover truncates)
+        trained += min(st["measured_batch_size"], batch)  # the batch the step trains on (rollover truncates)
         steps += 1
         if steps % 100 == 1:
             curve.append((round(time.time() - t_start, 2), steps, round(st["loss"], 6)))
@@ -82,8 +88,8 @@ def run(pkg, seconds=30.0, images=100, res=800, test_views=8, spp=8, rank=0, wor
         "data": f"procedural Lego stand-in: {images} views {res}x{res} RGBA8, camera_angle_x of lego "
                 "(nerf_synthetic is not in the image)",
         "config": {"workload": "Testbed NeRF training (configs/nerf/base.json fork, C2) + NerfTracer eval "
-                               f"(black bg, snapped, spp {spp})", "batch": 1 << 18,
-                   "parallelism": f"dp{world}"},
+                               f"(black bg, snapped, spp {spp})", "batch": batch,
+                   "parallelism": f"dp{world}", "scaling": scaling},
         "dataset_seconds": round(t_data, 2), "render_seconds": round(t_render, 2), "loss_curve": curve[:40],
     }
 
