@@ -97,10 +97,9 @@ struct LossArgs {
 };
 
 // The kernels (each cites its reference kernel in nerf.hip).
-void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs& a, void* scan_tmp, size_t scan_bytes,
-                 uint32_t* tmp_u32, float* tmp_f32, hipStream_t s);
-void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs& a, void* scan_tmp, size_t scan_bytes,
-                  uint32_t* tmp_u32, float* tmp_f32, hipStream_t s);
+void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs& a, uint32_t* tmp_u32, float* tmp_f32, hipStream_t s);
+size_t sample_tmp_u32(uint32_t n_rays);  // u32 of sample_rays' tmp_u32 (counts, count-wave sums and prefixes)
+void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs& a, uint32_t* tmp_u32, float* tmp_f32, hipStream_t s);
 void fill_rollover_f16(uint32_t n_elements, uint32_t stride, const uint32_t* n_input, f16* data, bool rescale, hipStream_t s);
 void fill_rollover_f32(uint32_t n_elements, uint32_t stride, const uint32_t* n_input, float* data, hipStream_t s);
 void fill_rollover_pair(uint32_t n_elements, const uint32_t* n_input, f16* dloss, uint32_t stride16, float* coords,
@@ -120,7 +119,6 @@ void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, 
                     hipStream_t s);
 void grid_ema(uint32_t n, float decay, float* grid, const float* grid_tmp, hipStream_t s);
 void grid_mean_bitfield(const float* grid, uint32_t max_cascade, float* mean_out, uint8_t* bitfield, hipStream_t s);
-size_t scan_temp_bytes(uint32_t n);
 size_t sample_tmp_f32(uint32_t n_rays);  // floats of sample_rays' tmp_f32 (stored t per step + ray geometry)
 size_t loss_tmp_f32(uint32_t n_rays);    // floats of compute_loss' tmp_f32 (per-ray pass-1 results)
 // construct_cdf_2d / construct_cdf_1d (testbed_nerf.cu:2356-2410) over the error map

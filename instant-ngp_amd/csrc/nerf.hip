@@ -5,7 +5,6 @@
 // instruction sequence the oracle runs, so sample indices, coordinates and compacted counts match the
 // oracle bit for bit at every cone angle (the reference's libdevice logf/expf/__expf are <= 2-ulp
 // approximations of the same functions).
-#include <hipcub/hipcub.hpp>
 
 #include <cmath>
 #include <functional>
@@ -653,16 +652,14 @@ extern "C" __attribute__((visibility("default"))) int ngp_debug_math_check(int w
 	return rc;
 }
 
-// generate_training_samples_nerf pass 1: count the occupied steps of each ray, keep their t.
+// generate_training_samples_nerf pass 1: count the occupied steps of ray i (lane L of its group), keep their t;
+// returns the count (uniform over the group).
 template <bool CONE0>
-__global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
-                                                      uint32_t n_images, const ngp_nerf_config cfg, SampleArgs a,
-                                                      uint32_t* __restrict__ nsteps, float* __restrict__ tbuf,
-                                                      RayGeo* __restrict__ geo, const Cone cone) {
+__device__ __forceinline__ uint32_t count_ray(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels, uint32_t n_images,
+                                              const ngp_nerf_config& cfg, const SampleArgs& a, uint32_t* __restrict__ nsteps,
+                                              float* __restrict__ tbuf, RayGeo* __restrict__ geo, const Cone& cone, uint32_t i,
+                                              uint32_t L) {
 	constexpr uint32_t RGk = sampler_rg<CONE0>();
-	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-	const uint32_t i = gid / RGk, L = gid % RGk;
-	if (i >= a.n_rays) return;  // whole rows
 	if (!CONE0 && NGP_SAMPLER_PRIO) __builtin_amdgcn_s_setprio(NGP_SAMPLER_PRIO);
 	SAMPLER_STAT(const unsigned long long ck0 = sampler_clock();)
 	const RaySetup r = setup_ray(cams, pixels, n_images, cfg, i + a.ray_offset, a.n_rays_total_for_image_idx, a.rng, cone);
@@ -845,13 +842,37 @@ __global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__
 		g.pad[0] = r.cone; g.pad[1] = g.pad[2] = 0.f;
 		geo[i] = g;
 	}
+	return j;
 }
 
-__global__ void k_sample_keep(uint32_t n, const uint32_t* __restrict__ nsteps, const uint32_t* __restrict__ base,
-                              uint32_t max_samples, uint32_t* __restrict__ keep) {
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= n) return;
-	keep[i] = (nsteps[i] > 0 && base[i] + nsteps[i] <= max_samples) ? 1u : 0u;
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+	return v;
+}
+
+// The count pass, and per wave the sum of its rays' counts and the number of its rays with samples (wsum[2 w],
+// wsum[2 w + 1]): the sampler's prefix sums over rays become a scan over waves (k_sample_bscan, ~2 K values at
+// the Lego stand-in's ~32 K rays) plus an in-wave prefix in k_sample_write, instead of a scan over the rays.
+template <bool CONE0>
+__global__ void __launch_bounds__(256) k_sample_count(const Camera* __restrict__ cams, const uint32_t* __restrict__ pixels,
+                                                      uint32_t n_images, const ngp_nerf_config cfg, SampleArgs a,
+                                                      uint32_t* __restrict__ nsteps, float* __restrict__ tbuf,
+                                                      RayGeo* __restrict__ geo, const Cone cone, uint32_t* __restrict__ wsum) {
+	constexpr uint32_t RGk = sampler_rg<CONE0>();
+	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t i = gid / RGk, L = gid % RGk;
+	const bool live = i < a.n_rays;  // whole rows
+	uint32_t j = 0;
+	if (live) j = count_ray<CONE0>(cams, pixels, n_images, cfg, a, nsteps, tbuf, geo, cone, i, L);
+	const bool head = live && L == 0;
+	const uint32_t sum = wave_sum(head ? j : 0u);
+	const uint32_t nz = (uint32_t)__popcll(__ballot(head && j > 0));
+	if ((threadIdx.x & 63) == 0) {
+		const uint32_t w = gid / 64;
+		wsum[2 * w] = sum;
+		wsum[2 * w + 1] = nz;
+	}
 }
 
 // pass 2: write the ray records and the NerfCoordinates of kept rays from the stored t values; one
@@ -861,18 +882,25 @@ constexpr uint32_t WG = 64;
 #define NGP_SW_STAGE 1  // records staged in LDS, written as contiguous wave stores
 #endif
 // pass 2: write the ray records and the NerfCoordinates of kept rays from the stored t values.
+// The ray's sample base (exclusive prefix of the counts, the reference's atomicAdd on numsteps_counter in ray order)
+// and its slot among the kept rays: bpre (the count wave's prefixes, k_sample_bscan) plus the prefix over the
+// rays of its count wave before it (rpw rays per count wave). A ray is kept when it has samples and they fit
+// under max_samples (testbed_nerf.cu:1616-1619); the inclusive prefix grows with the ray index, so the kept
+// rays are the rays with samples before the first that does not fit, and a kept ray's slot counts every ray
+// with samples before it.
 __global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg, SampleArgs a, const uint32_t* __restrict__ nsteps,
-                                                      const uint32_t* __restrict__ base, const uint32_t* __restrict__ keep,
-                                                      const uint32_t* __restrict__ slot, const float* __restrict__ tbuf,
+                                                      const uint32_t* __restrict__ bpre, uint32_t rpw, const float* __restrict__ tbuf,
                                                       const RayGeo* __restrict__ geo, const Cone cone) {
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t i = gid / WG, L = gid % WG;
-	if (gid == 0) {  // counters: rays kept, total steps of every ray that found samples
-		a.counters[0] = slot[a.n_rays - 1] + keep[a.n_rays - 1];
-		a.counters[1] = base[a.n_rays - 1] + nsteps[a.n_rays - 1];
-	}
-	if (i >= a.n_rays || !keep[i]) return;
-	const uint32_t s = slot[i], numsteps = nsteps[i], b = base[i];
+	if (i >= a.n_rays) return;  // whole waves
+	const uint32_t w = i / rpw, r0 = w * rpw;
+	const uint32_t nl = (r0 + L < i) ? nsteps[r0 + L] : 0u;  // the count wave's rays before ray i
+	const uint32_t before = wave_sum(nl);
+	const uint32_t nz_before = (uint32_t)__popcll(__ballot(nl > 0));
+	const uint32_t numsteps = nsteps[i], b = bpre[2 * w] + before;
+	if (numsteps == 0 || b + numsteps > a.max_samples) return;
+	const uint32_t s = bpre[2 * w + 1] + nz_before;
 	const RayGeo g = geo[i];
 	if (L == 0) {
 		a.ray_indices[s] = i + a.ray_offset;
@@ -926,18 +954,12 @@ __global__ void __launch_bounds__(256) k_sample_write(const ngp_nerf_config cfg,
 #endif
 }
 
-size_t scan_temp_bytes(uint32_t n) {
-	size_t bytes = 0;
-	NGP_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n));
-	return bytes;
-}
-
-// Single-workgroup scans for the per-ray arrays of one step (~9-25 K rays): one launch of 1024 threads
-// instead of the device-wide scan's chain of launches. Tiles of 4096 elements, 4 consecutive ones per
-// thread (16-B coalesced loads and stores, all tiles loaded up front); one block scan per tile. Above
-// SCAN1_MAX elements (rays_per_batch can grow to 2^18) the device-wide scan.
-constexpr uint32_t SCAN1_THREADS = 1024, SCAN1_TILE = 4 * SCAN1_THREADS, SCAN1_NT = 8;
-constexpr uint32_t SCAN1_MAX = SCAN1_NT * SCAN1_TILE;
+// Single-workgroup scans of one step's per-wave / per-group sums (the sampler's count waves, the loss's groups of
+// 4 rays: ~2-8 K values at ~32 K rays): one launch of 1024 threads, tiles of 4096 values, 4 consecutive ones per
+// thread (16-B coalesced loads and stores), one block scan per tile. Round 6: they replaced scans over every
+// ray (one single-block scan of up to 8 tiles, or above 32 K rays a device-wide hipcub scan: 2 launches per
+// scan, and 3 scans per step).
+constexpr uint32_t SCAN1_THREADS = 1024, SCAN1_TILE = 4 * SCAN1_THREADS;
 // exclusive sum of one value per thread over the block, and the block total; lds: 32 words
 __device__ __forceinline__ uint32_t block_exclusive_sum(uint32_t v, uint32_t* lds, uint32_t* total) {
 	constexpr uint32_t NW = SCAN1_THREADS / 64;
@@ -983,95 +1005,108 @@ __device__ __forceinline__ void scan1_store(uint32_t* out, uint32_t n, uint32_t 
 			if (i + k < n) out[i + k] = v[k];
 	}
 }
-__global__ void __launch_bounds__(SCAN1_THREADS) k_scan1(uint32_t n, const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
+// Exclusive prefix sums of the sums of groups of 4 consecutive values (gpre[g] = in[0] + .. + in[4 g - 1]) and the
+// total, one block: a quarter of the block scans of a per-element scan (the loss's compaction: ~32 K rays, two
+// tiles instead of eight); a consumer adds the at most 3 values of its group before it.
+__global__ void __launch_bounds__(SCAN1_THREADS) k_scan4(uint32_t n, const uint32_t* __restrict__ in, uint32_t* __restrict__ gpre,
+                                                         uint32_t* __restrict__ total) {
 	__shared__ uint32_t lds[32];
-	const uint32_t nt = (n + SCAN1_TILE - 1) / SCAN1_TILE;
-	uint32_t x[SCAN1_NT][4];
-#pragma unroll
-	for (uint32_t tl = 0; tl < SCAN1_NT; ++tl)
-		if (tl < nt) scan1_load(in, n, tl * SCAN1_TILE + 4 * threadIdx.x, x[tl]);
+	const uint32_t ng = (n + 3) / 4;
 	uint32_t run = 0;
+	for (uint32_t g0 = 0; g0 < ng; g0 += SCAN1_TILE) {
+		uint32_t gs[4];
 #pragma unroll
-	for (uint32_t tl = 0; tl < SCAN1_NT; ++tl) {
-		if (tl >= nt) break;
+		for (uint32_t k = 0; k < 4; ++k) {
+			uint32_t v[4];
+			scan1_load(in, n, 4 * (g0 + 4 * threadIdx.x + k), v);
+			gs[k] = v[0] + v[1] + v[2] + v[3];
+		}
 		uint32_t tot;
-		uint32_t b = run + block_exclusive_sum(x[tl][0] + x[tl][1] + x[tl][2] + x[tl][3], lds, &tot);
+		uint32_t b = run + block_exclusive_sum(gs[0] + gs[1] + gs[2] + gs[3], lds, &tot);
 		uint32_t o[4];
 #pragma unroll
 		for (uint32_t k = 0; k < 4; ++k) {
 			o[k] = b;
-			b += x[tl][k];
+			b += gs[k];
 		}
-		scan1_store(out, n, tl * SCAN1_TILE + 4 * threadIdx.x, o);
+		scan1_store(gpre, ng, g0 + 4 * threadIdx.x, o);
 		run += tot;
 	}
+	if (threadIdx.x == 0) *total = run;
 }
-static void exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, void* tmp, size_t bytes, hipStream_t s) {
-	if (n <= SCAN1_MAX) {
-		k_scan1<<<1, SCAN1_THREADS, 0, s>>>(n, in, out);
-		NGP_HIP(hipGetLastError());
-		return;
-	}
-	size_t need = bytes;
-	NGP_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, need, in, out, (int)n, s));
-}
-// The sampler's base = exclusive scan of nsteps, keep (the ray's samples fit under max_samples,
-// testbed_nerf.cu:1616-1619 atomicAdd guard, in ray order), slot = exclusive scan of keep: one launch.
-__global__ void __launch_bounds__(SCAN1_THREADS) k_sample_scan1(uint32_t n, const uint32_t* __restrict__ nsteps, uint32_t max_samples,
-                                                                 uint32_t* __restrict__ base, uint32_t* __restrict__ keep,
-                                                                 uint32_t* __restrict__ slot) {
+// The count waves' exclusive prefixes (bpre[2 w]: samples before wave w, bpre[2 w + 1]: rays with samples
+// before it) from their sums, one block; and the counters: rays kept, and the total count of every ray (the
+// reference's numsteps_counter, dropped rays included). The one wave whose rays cross max_samples is found
+// here and its rays counted in order.
+__global__ void __launch_bounds__(SCAN1_THREADS) k_sample_bscan(uint32_t nw, const uint32_t* __restrict__ wsum, uint32_t* __restrict__ bpre,
+                                                                const uint32_t* __restrict__ nsteps, uint32_t n_rays, uint32_t rpw,
+                                                                uint32_t max_samples, uint32_t* __restrict__ counters) {
 	__shared__ uint32_t lds[32];
-	const uint32_t nt = (n + SCAN1_TILE - 1) / SCAN1_TILE;
-	uint32_t x[SCAN1_NT][4];
-#pragma unroll
-	for (uint32_t tl = 0; tl < SCAN1_NT; ++tl)
-		if (tl < nt) scan1_load(nsteps, n, tl * SCAN1_TILE + 4 * threadIdx.x, x[tl]);
-	uint32_t run = 0;
-#pragma unroll
-	for (uint32_t tl = 0; tl < SCAN1_NT; ++tl) {
-		if (tl >= nt) break;
-		uint32_t tot;
-		uint32_t b = run + block_exclusive_sum(x[tl][0] + x[tl][1] + x[tl][2] + x[tl][3], lds, &tot);
-		uint32_t o[4];
+	__shared__ uint32_t cross[3];  // the crossing wave, its prefixes
+	if (threadIdx.x == 0) cross[0] = nw;
+	uint32_t run_s = 0, run_z = 0;
+	for (uint32_t t0 = 0; t0 < nw; t0 += SCAN1_TILE) {
+		uint32_t sv[4], zv[4];
 #pragma unroll
 		for (uint32_t k = 0; k < 4; ++k) {
-			o[k] = b;
-			const uint32_t ns = x[tl][k];
-			b += ns;
-			x[tl][k] = (ns > 0 && b <= max_samples) ? 1u : 0u;  // keep
+			const uint32_t w = t0 + 4 * threadIdx.x + k;
+			sv[k] = w < nw ? wsum[2 * w] : 0u;
+			zv[k] = w < nw ? wsum[2 * w + 1] : 0u;
 		}
-		const uint32_t i = tl * SCAN1_TILE + 4 * threadIdx.x;
-		scan1_store(base, n, i, o);
-		scan1_store(keep, n, i, x[tl]);
-		run += tot;
+		uint32_t ts, tz;
+		uint32_t bs = run_s + block_exclusive_sum(sv[0] + sv[1] + sv[2] + sv[3], lds, &ts);
+		uint32_t bz = run_z + block_exclusive_sum(zv[0] + zv[1] + zv[2] + zv[3], lds, &tz);
+#pragma unroll
+		for (uint32_t k = 0; k < 4; ++k) {
+			const uint32_t w = t0 + 4 * threadIdx.x + k;
+			if (w < nw) {
+				bpre[2 * w] = bs;
+				bpre[2 * w + 1] = bz;
+				if (bs <= max_samples && bs + sv[k] > max_samples) {  // at most one wave
+					cross[0] = w; cross[1] = bs; cross[2] = bz;
+				}
+			}
+			bs += sv[k];
+			bz += zv[k];
+		}
+		run_s += ts;
+		run_z += tz;
 	}
-	run = 0;
-#pragma unroll
-	for (uint32_t tl = 0; tl < SCAN1_NT; ++tl) {
-		if (tl >= nt) break;
-		uint32_t tot;
-		uint32_t b = run + block_exclusive_sum(x[tl][0] + x[tl][1] + x[tl][2] + x[tl][3], lds, &tot);
-		uint32_t o[4];
-#pragma unroll
-		for (uint32_t k = 0; k < 4; ++k) {
-			o[k] = b;
-			b += x[tl][k];
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		uint32_t kept = run_z;
+		if (cross[0] < nw) {
+			uint32_t b = cross[1];
+			kept = cross[2];
+			for (uint32_t r = cross[0] * rpw; r < min(n_rays, (cross[0] + 1) * rpw); ++r) {
+				const uint32_t n = nsteps[r];
+				if (b + n > max_samples) break;
+				kept += n > 0 ? 1u : 0u;
+				b += n;
+			}
 		}
-		scan1_store(slot, n, tl * SCAN1_TILE + 4 * threadIdx.x, o);
-		run += tot;
+		counters[0] = kept;
+		counters[1] = run_s;
 	}
 }
 
 size_t sample_tmp_f32(uint32_t n_rays) { return (size_t)n_rays * (STEPS + sizeof(RayGeo) / 4); }
 
-void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs& a, void* scan_tmp, size_t scan_bytes,
-                 uint32_t* tmp, float* tmpf, hipStream_t s) {
+// count waves of the sampler's count pass: whole blocks of NGP_SAMPLER_BLOCK threads, RGk lanes per ray
+static uint32_t sample_count_waves(uint32_t n_rays, uint32_t rgk) {
+	return (uint32_t)(div_round_up((size_t)n_rays * rgk, NGP_SAMPLER_BLOCK) * (NGP_SAMPLER_BLOCK / 64));
+}
+size_t sample_tmp_u32(uint32_t n_rays) { return n_rays + 4 * (size_t)sample_count_waves(n_rays, std::max(RG, sampler_rg<true>())); }
+
+void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs& a, uint32_t* tmp, float* tmpf, hipStream_t s) {
 	if (a.n_rays == 0) return;
 	NGP_CHECK(tmpf != nullptr, "sample_rays: float scratch of sample_tmp_f32(n_rays) floats required");
+	const bool cone0 = cfg.cone_angle_constant <= 1e-5f;
+	const uint32_t rgk = cone0 ? sampler_rg<true>() : RG;
+	const uint32_t nw = sample_count_waves(a.n_rays, rgk);
 	uint32_t* nsteps = tmp;
-	uint32_t* base = tmp + a.n_rays;
-	uint32_t* keep = tmp + 2 * (size_t)a.n_rays;
-	uint32_t* slot = tmp + 3 * (size_t)a.n_rays;
+	uint32_t* wsum = tmp + a.n_rays;    // 2 per count wave
+	uint32_t* bpre = wsum + 2 * (size_t)nw;
 	float* tbuf = tmpf;
 	RayGeo* geo = (RayGeo*)(tmpf + (size_t)a.n_rays * STEPS);
 	const uint32_t blocks = div_round_up((size_t)a.n_rays * RG, NGP_SAMPLER_BLOCK);
@@ -1079,25 +1114,22 @@ void sample_rays(const Dataset& ds, const ngp_nerf_config& cfg, const SampleArgs
 	const Cone cone = make_cone(cfg.cone_angle_constant);  // every ray's cone (setup_ray: r.cone)
 	{
 		ProfScope ps("sample_count", s);
-		if (cfg.cone_angle_constant <= 1e-5f)
-			k_sample_count<true><<<blocks0, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo, cone);
+		if (cone0)
+			k_sample_count<true><<<blocks0, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo, cone,
+			                                                          wsum);
 		else
-			k_sample_count<false><<<blocks, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo, cone);
+			k_sample_count<false><<<blocks, NGP_SAMPLER_BLOCK, 0, s>>>(ds.d_cams, ds.d_pixels, ds.n_images, cfg, a, nsteps, tbuf, geo, cone,
+			                                                           wsum);
 		NGP_HIP(hipGetLastError());
 	}
+	NGP_CHECK(nw == (cone0 ? blocks0 : blocks) * (NGP_SAMPLER_BLOCK / 64) && 64 % rgk == 0, "sampler: count waves");
 	{
 		ProfScope ps("sample_scans", s);
-		if (a.n_rays <= SCAN1_MAX) {
-			k_sample_scan1<<<1, SCAN1_THREADS, 0, s>>>(a.n_rays, nsteps, a.max_samples, base, keep, slot);
-			NGP_HIP(hipGetLastError());
-		} else {
-			exclusive_scan(nsteps, base, a.n_rays, scan_tmp, scan_bytes, s);
-			k_sample_keep<<<div_round_up(a.n_rays, 256), 256, 0, s>>>(a.n_rays, nsteps, base, a.max_samples, keep);
-			exclusive_scan(keep, slot, a.n_rays, scan_tmp, scan_bytes, s);
-		}
+		k_sample_bscan<<<1, SCAN1_THREADS, 0, s>>>(nw, wsum, bpre, nsteps, a.n_rays, 64 / rgk, a.max_samples, a.counters);
+		NGP_HIP(hipGetLastError());
 	}
 	ProfScope ps("sample_write", s);
-	k_sample_write<<<div_round_up((size_t)a.n_rays * WG, 256), 256, 0, s>>>(cfg, a, nsteps, base, keep, slot, tbuf, geo, cone);
+	k_sample_write<<<div_round_up((size_t)a.n_rays * WG, 256), 256, 0, s>>>(cfg, a, nsteps, bpre, 64 / rgk, tbuf, geo, cone);
 	NGP_HIP(hipGetLastError());
 }
 
@@ -1304,14 +1336,15 @@ __device__ __forceinline__ void deposit_error(const LossArgs& a, const Camera* _
 // ceil(cn / 16), and the long rays, each round a memory latency, set the kernel's time (fox: up to ~26 rounds)
 template <uint32_t LANES>
 __global__ void __launch_bounds__(256) k_loss_pass2(const Camera* __restrict__ cams, const ngp_nerf_config cfg, LossArgs a,
-                                                    const uint32_t* __restrict__ craw, const uint32_t* __restrict__ cbase,
+                                                    const uint32_t* __restrict__ craw, const uint32_t* __restrict__ gpre,
                                                     const LossRay* __restrict__ lr) {
 	const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t i = gid / LANES, L = gid % LANES;
-	if (gid == 0) *a.compacted_counter = cbase[a.n_rays - 1] + craw[a.n_rays - 1];
 	if (i >= a.n_rays || i >= *a.ray_counter) return;
 	const uint32_t base = a.numsteps[2 * i + 1];
-	const uint32_t compacted_base = cbase[i];
+	// the exclusive prefix of the compacted counts: the ray's group of 4 (k_scan4) plus the rays of the group before it
+	uint32_t compacted_base = gpre[i / 4];
+	for (uint32_t r = i & ~3u; r < i; ++r) compacted_base += craw[r];
 	const uint32_t mx = a.max_samples_compacted;
 	const uint32_t cn = min(mx - min(mx, compacted_base), craw[i]);
 	if (L == 0) {  // every lane of the row has read numsteps[2i + 1] above (one wave instruction)
@@ -1459,11 +1492,10 @@ __global__ void __launch_bounds__(256) k_loss_pass2(const Camera* __restrict__ c
 
 size_t loss_tmp_f32(uint32_t n_rays) { return (size_t)n_rays * (sizeof(LossRay) / 4); }
 
-void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs& a, void* scan_tmp, size_t scan_bytes,
-                  uint32_t* tmp, float* tmpf, hipStream_t s) {
+void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs& a, uint32_t* tmp, float* tmpf, hipStream_t s) {
 	if (a.n_rays == 0) return;
 	uint32_t* craw = tmp;
-	uint32_t* cbase = tmp + a.n_rays;
+	uint32_t* gpre = tmp + a.n_rays;  // per group of 4 rays
 	LossRay* lr = (LossRay*)tmpf;
 	const uint32_t blocks = div_round_up((size_t)a.n_rays * LG, 256);
 	{
@@ -1475,15 +1507,16 @@ void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs&
 	}
 	{
 		ProfScope ps("loss_scan", s);
-		exclusive_scan(craw, cbase, a.n_rays, scan_tmp, scan_bytes, s);
+		k_scan4<<<1, SCAN1_THREADS, 0, s>>>(a.n_rays, craw, gpre, a.compacted_counter);
+		NGP_HIP(hipGetLastError());
 	}
 	ProfScope ps("loss_pass2", s);
 	static_assert(NGP_LOSS_SELECT, "pass 1 keeps the compositing state pass 2 reads only in its select form");
 	if (a.state) {
 		constexpr uint32_t W = NGP_LOSS2_LANES;  // a wave per ray: see k_loss_pass2
-		k_loss_pass2<W><<<div_round_up((size_t)a.n_rays * W, 256), 256, 0, s>>>(ds.d_cams, cfg, a, craw, cbase, lr);
+		k_loss_pass2<W><<<div_round_up((size_t)a.n_rays * W, 256), 256, 0, s>>>(ds.d_cams, cfg, a, craw, gpre, lr);
 	} else {
-		k_loss_pass2<LG><<<blocks, 256, 0, s>>>(ds.d_cams, cfg, a, craw, cbase, lr);
+		k_loss_pass2<LG><<<blocks, 256, 0, s>>>(ds.d_cams, cfg, a, craw, gpre, lr);
 	}
 	NGP_HIP(hipGetLastError());
 }

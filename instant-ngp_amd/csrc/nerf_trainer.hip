@@ -310,11 +310,9 @@ int ngp_nerf_generate_training_samples(const ngp_nerf_dataset* ds, const ngp_ner
 		a.n_rays = n_rays; a.ray_offset = ray_offset; a.n_rays_total_for_image_idx = n_rays_total ? n_rays_total : n_rays;
 		a.max_samples = max_samples; a.rng = Rng{rng.state, rng.inc}; a.bitfield = bitfield;
 		a.ray_indices = ray_indices; a.rays = rays; a.numsteps = numsteps; a.coords = coords; a.counters = counters;
-		static thread_local Buf scan, tmp, tmpf;
-		const size_t sb = scan_temp_bytes(n_rays);
+		static thread_local Buf tmp, tmpf;
 		if (n_rays == 0) { NGP_HIP(hipMemsetAsync(counters, 0, 8, S(stream))); return NGP_OK; }
-		sample_rays(ds->ds, *cfg, a, scan.get<char>(sb), sb, tmp.get<uint32_t>(4 * (size_t)n_rays),
-		            tmpf.get<float>(sample_tmp_f32(n_rays)), S(stream));
+		sample_rays(ds->ds, *cfg, a, tmp.get<uint32_t>(sample_tmp_u32(n_rays)), tmpf.get<float>(sample_tmp_f32(n_rays)), S(stream));
 	});
 }
 
@@ -380,10 +378,8 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
 		a.error_map = error_map; a.em_w = em_w; a.em_h = em_h;
 		a.state = state; a.state_cap = state ? state_cap : 0;
 		if (n_rays == 0) { NGP_HIP(hipMemsetAsync(compacted_counter, 0, 4, S(stream))); return NGP_OK; }
-		static thread_local Buf scan, tmp, tmpf;
-		const size_t sb = scan_temp_bytes(n_rays);
-		compute_loss(ds->ds, *cfg, a, scan.get<char>(sb), sb, tmp.get<uint32_t>(2 * (size_t)n_rays), tmpf.get<float>(loss_tmp_f32(n_rays)),
-		             S(stream));
+		static thread_local Buf tmp, tmpf;
+		compute_loss(ds->ds, *cfg, a, tmp.get<uint32_t>(2 * (size_t)n_rays), tmpf.get<float>(loss_tmp_f32(n_rays)), S(stream));
 	});
 }
 

@@ -91,6 +91,32 @@ def test_generate_training_samples_bitexact(pkg, orc, scene, n_rays, max_samples
     np.testing.assert_array_equal(got["coords"][:used], ref["coords"][:used])
 
 
+@pytest.mark.parametrize("aabb_scale,n_rays,max_samples", [
+    (1.0, 1, 2), (1.0, 3, 40), (1.0, 17, 300), (1.0, 1 << 16, 1 << 17), (1.0, 50001, 123457),
+    (8.0, 5, 100), (8.0, 1 << 16, 1 << 17), (8.0, 40000, 99999)])
+def test_sampler_sample_budget(pkg, orc, scene, aabb_scale, n_rays, max_samples):
+    """The sample budget cuts the batch inside a count wave (k_sample_bscan finds the crossing wave and counts
+    its rays; k_sample_write keeps a ray only while its inclusive prefix fits): counters, kept rays, bases and
+    coordinates bit-exact with the oracle's sequential atomicAdd order (testbed_nerf.cu:1616-1619), at cone 0 (16
+    rays per count wave) and with cone stepping (8), ragged and tiny batches included."""
+    ds, ims, pix = scene
+    cfg = pkg.nerf.default_config(aabb_scale)
+    _, bf = occupancy(orc, seed=n_rays % 1000 + 3, frac=0.3, max_cascade=cfg.max_cascade)
+    r = rng(pkg, 77 + n_rays)
+    got = pkg.nerf.generate_training_samples(ds, cfg, n_rays, r, max_samples, torch.from_numpy(bf).cuda(), n_rays_total=n_rays)
+    ref = orc.nerf_generate_samples(cfg, ims, pix, n_rays, orc_rng(orc, r), max_samples, bf)
+    got = {k: v.cpu().numpy() for k, v in got.items()}
+    np.testing.assert_array_equal(got["counters"].view(np.uint32), ref["counters"])
+    kept = int(ref["counters"][0])
+    if n_rays > 100:
+        assert int(ref["counters"][1]) > max_samples and kept < n_rays  # the budget cuts the batch
+    np.testing.assert_array_equal(got["ray_indices"][:kept].view(np.uint32), ref["ray_indices"][:kept])
+    np.testing.assert_array_equal(got["numsteps"][:kept].view(np.uint32), ref["numsteps"][:kept])
+    np.testing.assert_array_equal(got["rays"][:kept], ref["rays"][:kept])
+    used = int(ref["numsteps"][kept - 1][0] + ref["numsteps"][kept - 1][1]) if kept else 0
+    np.testing.assert_array_equal(got["coords"][:used], ref["coords"][:used])
+
+
 @pytest.mark.parametrize("n_rays,frac", [(2048, 0.4), (4096, 1.0)])
 def test_generate_training_samples_opencv_lens(pkg, orc, scene_lens, n_rays, frac):
     """uv_to_ray with OpenCV undistortion (iterative Newton, common_device.cuh:330-369): no
@@ -138,11 +164,11 @@ def test_generate_training_samples_cone(pkg, orc, scene, aabb_scale, n_rays, fra
 @pytest.mark.parametrize("aabb_scale,cone,n_rays,frac", [
     (8.0, None, 1 << 16, 0.05), (32.0, None, 1 << 16, 0.03), (128.0, None, 1 << 16, 0.01),
     (8.0, 1e-4, 1 << 14, 0.05), (8.0, 5e-4, 1 << 14, 0.05), (16.0, 2e-5, 1 << 13, 0.05), (8.0, 0.02, 1 << 14, 0.1),
-    # the single-workgroup scans at their largest size (8 tiles of 4096) and a ragged cone-0 batch
+    # a ragged cone-0 batch
     (8.0, None, 1 << 15, 0.05), (1.0, None, 30001, 0.1)])
 def test_sampler_and_loss_cone_at_scale(pkg, orc, scene, aabb_scale, cone, n_rays, frac):
-    """Fox-scale and larger ray counts (>= 64k rays at aabb_scale 8, 32, 128: the device-wide scans; 32k
-    and 30001 rays: the single-workgroup scans) and user-set cone angles
+    """Fox-scale and larger ray counts (64k rays at aabb_scale 8, 32, 128: 2-4 K count waves and 4 tiles of the
+    loss's group scan; 32k and 30001 rays) and user-set cone angles
     from 2e-5 to 0.02: the sampler's hardware exp/log speculation in empty space (csrc/nerf.hip
     step_empty) falls back to the exact path near every integer decision, with margins that scale with
     1 / log(1 + cone), so sample sets, compacted counts and coordinates stay bit-exact with the oracle."""
