@@ -122,6 +122,21 @@ struct ngp_nerf_trainer {
 	uint32_t pre_R = 0, pre_max_inference = 0;
 	hipStream_t sample_stream = nullptr;
 	hipEvent_t ev_free = nullptr, ev_samp = nullptr;
+	// The two queues' handoffs (sampler done -> inference; sample buffers released -> next sampler) as
+	// hipStreamWriteValue32 / hipStreamWaitValue32 on signal memory: a queue idling on a pending event wait starts
+	// its next kernel ~10 us after the event's work ends, on a pending value wait ~1-3 us
+	// (tools/microbench/queue_handoff.hip, profiles/r06s_queue_handoff.jsonl): Lego step 0.4337 -> 0.4257 ms, fox
+	// 0.5440 -> 0.5397 ms (gpurun_out/r06r). NGP_NERF_WAITVAL=0: the events (A/B)
+	uint32_t* sig_samp = nullptr;
+	uint32_t* sig_free = nullptr;
+	uint32_t seq_samp = 0, seq_free = 0;
+	void ensure_signals() {
+		if (sig_samp) return;
+		NGP_HIP(hipExtMallocWithFlags((void**)&sig_samp, 8, hipMallocSignalMemory));
+		NGP_HIP(hipExtMallocWithFlags((void**)&sig_free, 8, hipMallocSignalMemory));
+		NGP_HIP(hipMemset(sig_samp, 0, 8));
+		NGP_HIP(hipMemset(sig_free, 0, 8));
+	}
 	void drain() {  // the prelaunched sampler finished and discarded (state is about to change)
 		if (sample_stream) (void)hipStreamSynchronize(sample_stream);
 		prelaunched = false;
@@ -133,6 +148,8 @@ struct ngp_nerf_trainer {
 		if (sample_stream) (void)hipStreamDestroy(sample_stream);
 		for (hipEvent_t e : {ev_free, ev_samp})
 			if (e) (void)hipEventDestroy(e);
+		for (uint32_t* p : {sig_samp, sig_free})
+			if (p) (void)hipFree(p);
 		if (host_ctr) (void)hipHostFree((void*)host_ctr);
 	}
 	// data parallelism: rank r traces global rays [R r / N, R (r+1) / N), compacts to B / N,
@@ -826,6 +843,11 @@ static hipStream_t make_sampler_stream() {
 	return s;
 }
 
+static bool nerf_waitval() {
+	static const bool v = !getenv("NGP_NERF_WAITVAL") || atoi(getenv("NGP_NERF_WAITVAL")) != 0;
+	return v;
+}
+
 int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_nerf_stats* st) {
 	if (!t) return NGP_INVALID;
 	NERF_TRY({
@@ -868,7 +890,8 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		// dL/doutput is scaled by 128 / R (global), so the summed gradient is the 1-GPU gradient
 		if (pre) {
 			NGP_CHECK(sp.R == t->pre_R && sp.max_inference == t->pre_max_inference, "nerf: prelaunched sampler is stale");
-			NGP_HIP(hipStreamWaitEvent(s, t->ev_samp, 0));
+			if (nerf_waitval()) NGP_HIP(hipStreamWaitValue32(s, t->sig_samp, t->seq_samp, hipStreamWaitValueGte, 0xFFFFFFFFu));
+			else NGP_HIP(hipStreamWaitEvent(s, t->ev_samp, 0));
 		} else {
 			launch_sampler(t, sp, s);
 		}
@@ -931,7 +954,12 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 				NGP_HIP(hipEventCreateWithFlags(&t->ev_free, hipEventDisableTiming));
 				NGP_HIP(hipEventCreateWithFlags(&t->ev_samp, hipEventDisableTiming));
 			}
-			NGP_HIP(hipEventRecord(t->ev_free, s));  // sample buffers and counters released
+			if (nerf_waitval()) {  // sample buffers and counters released
+				t->ensure_signals();
+				NGP_HIP(hipStreamWriteValue32(s, t->sig_free, ++t->seq_free, 0));
+			} else {
+				NGP_HIP(hipEventRecord(t->ev_free, s));
+			}
 		}
 		{
 		ProfScope ps("nerf_train_pass", s);
@@ -996,9 +1024,11 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		// next step's sampler, concurrent with this step's training pass (no density-grid update due first)
 		if (can_pipeline && t->measured_batch_size > 0 && !density_grid_update_due(t->training_step)) {
 			const SamplePlan np = sample_plan(t);
-			NGP_HIP(hipStreamWaitEvent(t->sample_stream, t->ev_free, 0));
+			if (nerf_waitval()) NGP_HIP(hipStreamWaitValue32(t->sample_stream, t->sig_free, t->seq_free, hipStreamWaitValueGte, 0xFFFFFFFFu));
+			else NGP_HIP(hipStreamWaitEvent(t->sample_stream, t->ev_free, 0));
 			launch_sampler(t, np, t->sample_stream);
-			NGP_HIP(hipEventRecord(t->ev_samp, t->sample_stream));
+			if (nerf_waitval()) NGP_HIP(hipStreamWriteValue32(t->sample_stream, t->sig_samp, ++t->seq_samp, 0));
+			else NGP_HIP(hipEventRecord(t->ev_samp, t->sample_stream));
 			t->pre_R = np.R;
 			t->pre_max_inference = np.max_inference;
 			t->prelaunched = true;
