@@ -122,11 +122,12 @@ struct ngp_nerf_trainer {
 	uint32_t pre_R = 0, pre_max_inference = 0;
 	hipStream_t sample_stream = nullptr;
 	hipEvent_t ev_free = nullptr, ev_samp = nullptr;
-	// The two queues' handoffs (sampler done -> inference; sample buffers released -> next sampler) as
-	// hipStreamWriteValue32 / hipStreamWaitValue32 on signal memory: a queue idling on a pending event wait starts
-	// its next kernel ~10 us after the event's work ends, on a pending value wait ~1-3 us
-	// (tools/microbench/queue_handoff.hip, profiles/r06s_queue_handoff.jsonl): Lego step 0.4337 -> 0.4257 ms, fox
-	// 0.5440 -> 0.5397 ms (gpurun_out/r06r). NGP_NERF_WAITVAL=0: the events (A/B)
+	// The sampler -> inference handoff as hipStreamWriteValue32 / hipStreamWaitValue32 on signal memory: a queue
+	// idling on a pending event wait starts its next kernel ~10 us after the event's work ends, on a pending value
+	// wait ~6 us
+	// (tools/microbench/queue_handoff.hip, profiles/r06s_queue_handoff.jsonl): Lego step 0.433 -> 0.428 ms, fox
+	// 0.542 -> 0.535 ms (gpurun_out/r06t; the release handoff by value too, NGP_NERF_WAITVAL=2: Lego 0.427, fox 0.538).
+	// NGP_NERF_WAITVAL=0: the events (A/B)
 	uint32_t* sig_samp = nullptr;
 	uint32_t* sig_free = nullptr;
 	uint32_t seq_samp = 0, seq_free = 0;
@@ -843,8 +844,9 @@ static hipStream_t make_sampler_stream() {
 	return s;
 }
 
-static bool nerf_waitval() {
-	static const bool v = !getenv("NGP_NERF_WAITVAL") || atoi(getenv("NGP_NERF_WAITVAL")) != 0;
+// 1: the sampler -> inference handoff by value (default); 2: the buffer release too; 0: events only (A/B)
+static int nerf_waitval() {
+	static const int v = getenv("NGP_NERF_WAITVAL") ? atoi(getenv("NGP_NERF_WAITVAL")) : 1;
 	return v;
 }
 
@@ -954,7 +956,9 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 				NGP_HIP(hipEventCreateWithFlags(&t->ev_free, hipEventDisableTiming));
 				NGP_HIP(hipEventCreateWithFlags(&t->ev_samp, hipEventDisableTiming));
 			}
-			if (nerf_waitval()) {  // sample buffers and counters released
+			// sample buffers and counters released: an event (by the time the host launches the next sampler this
+			// is long done, and a completed event's wait costs ~1.3 us against ~3.6 for a value wait)
+			if (nerf_waitval() == 2) {
 				t->ensure_signals();
 				NGP_HIP(hipStreamWriteValue32(s, t->sig_free, ++t->seq_free, 0));
 			} else {
@@ -1024,11 +1028,15 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		// next step's sampler, concurrent with this step's training pass (no density-grid update due first)
 		if (can_pipeline && t->measured_batch_size > 0 && !density_grid_update_due(t->training_step)) {
 			const SamplePlan np = sample_plan(t);
-			if (nerf_waitval()) NGP_HIP(hipStreamWaitValue32(t->sample_stream, t->sig_free, t->seq_free, hipStreamWaitValueGte, 0xFFFFFFFFu));
+			if (nerf_waitval() == 2) NGP_HIP(hipStreamWaitValue32(t->sample_stream, t->sig_free, t->seq_free, hipStreamWaitValueGte, 0xFFFFFFFFu));
 			else NGP_HIP(hipStreamWaitEvent(t->sample_stream, t->ev_free, 0));
 			launch_sampler(t, np, t->sample_stream);
-			if (nerf_waitval()) NGP_HIP(hipStreamWriteValue32(t->sample_stream, t->sig_samp, ++t->seq_samp, 0));
-			else NGP_HIP(hipEventRecord(t->ev_samp, t->sample_stream));
+			if (nerf_waitval()) {
+				t->ensure_signals();
+				NGP_HIP(hipStreamWriteValue32(t->sample_stream, t->sig_samp, ++t->seq_samp, 0));
+			} else {
+				NGP_HIP(hipEventRecord(t->ev_samp, t->sample_stream));
+			}
 			t->pre_R = np.R;
 			t->pre_max_inference = np.max_inference;
 			t->prelaunched = true;
