@@ -114,7 +114,8 @@ struct StepPublish {
 void fill_rollover_pair_publish(uint32_t n_elements, const uint32_t* n_input, f16* dloss, uint32_t stride16, float* coords,
                                 uint32_t stride32, const StepPublish& pub, hipStream_t s);
 void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_config& cfg, const float* grid_in,
-                           uint32_t n_cascades, float thresh, float* positions, uint32_t* indices, hipStream_t s);
+                           uint32_t n_cascades, float thresh, float* positions, uint32_t* indices, uint32_t* mask, hipStream_t s);
+size_t grid_mask_words(uint32_t n_cascades);  // u32 of grid_generate_samples' cell mask
 void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t density_activation, float* grid_tmp,
                     hipStream_t s);
 void grid_ema(uint32_t n, float decay, float* grid, const float* grid_tmp, hipStream_t s);

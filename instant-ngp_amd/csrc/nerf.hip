@@ -1651,18 +1651,42 @@ void fill_rollover_f32(uint32_t n_elements, uint32_t stride, const uint32_t* n_i
 // occupancy grid
 // ------------------------------------------------------------------------------------------------
 // generate_grid_samples_nerf_nonuniform (testbed_nerf.cu:635-676)
-__global__ void k_grid_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_config cfg, const float* __restrict__ grid_in,
-                               uint32_t n_cascades, float thresh, float* __restrict__ out, uint32_t* __restrict__ indices) {
+// The candidate test of generate_grid_samples_nerf_nonuniform (grid_in[idx] > thresh) for every cell of the
+// sampled cascades as one bit per cell: a linear pass over the grid (32 cells -> one word, 128-B coalesced reads),
+// so the samples' up-to-10 candidates are tested against a 256-KB-per-cascade mask that stays in L2 instead of
+// one scattered 4-B grid read (a 64-B transaction) per candidate, in a chain.
+__global__ void k_grid_mask(uint32_t n_words, const float* __restrict__ grid, float thresh, uint32_t* __restrict__ mask) {
+	const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+	if (w >= n_words) return;
+	const float4* g = (const float4*)(grid + (size_t)w * 32);
+	uint32_t bits = 0;
+#pragma unroll
+	for (uint32_t q = 0; q < 8; ++q) {
+		const float4 v = g[q];
+		bits |= (v.x > thresh ? 1u : 0u) << (4 * q) | (v.y > thresh ? 1u : 0u) << (4 * q + 1) |
+		        (v.z > thresh ? 1u : 0u) << (4 * q + 2) | (v.w > thresh ? 1u : 0u) << (4 * q + 3);
+	}
+	mask[w] = bits;
+}
+
+__global__ void k_grid_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_config cfg, const uint32_t* __restrict__ mask,
+                               uint32_t n_cascades, float* __restrict__ out, uint32_t* __restrict__ indices) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
 	pcg_advance(rng, (uint64_t)i * 4);
 	const uint32_t level = (uint32_t)(pcg_float(rng) * n_cascades) % n_cascades;
-	uint32_t idx = 0;
+	// the 10 candidates' mask words loaded at once (L2 hits), then the first candidate that passes, as the
+	// reference's loop takes it (its last candidate when none passes)
+	uint32_t cand[10], word[10];
+#pragma unroll
 	for (uint32_t j = 0; j < 10; ++j) {
-		idx = ((i + step * n) * 56924617u + j * 19349663u + 96925573u) % GRID_N_CELLS;
-		idx += level * GRID_N_CELLS;
-		if (grid_in[idx] > thresh) break;
+		cand[j] = ((i + step * n) * 56924617u + j * 19349663u + 96925573u) % GRID_N_CELLS + level * GRID_N_CELLS;
+		word[j] = mask[cand[j] >> 5];
 	}
+	uint32_t idx = cand[9];
+#pragma unroll
+	for (int j = 9; j >= 0; --j)
+		if ((word[j] >> (cand[j] & 31u)) & 1u) idx = cand[j];
 	const uint32_t pos_idx = idx % GRID_N_CELLS;
 	const uint32_t x = morton3D_invert(pos_idx >> 0), y = morton3D_invert(pos_idx >> 1), z = morton3D_invert(pos_idx >> 2);
 	const float r0 = pcg_float(rng), r1 = pcg_float(rng), r2 = pcg_float(rng);
@@ -1746,10 +1770,13 @@ __global__ void k_bitfield_max_pool(uint32_t n, const uint8_t* __restrict__ prev
 	next[morton3D(x, y, z)] |= bits;
 }
 
+size_t grid_mask_words(uint32_t n_cascades) { return (size_t)n_cascades * GRID_N_CELLS / 32; }
 void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_config& cfg, const float* grid_in,
-                           uint32_t n_cascades, float thresh, float* positions, uint32_t* indices, hipStream_t s) {
+                           uint32_t n_cascades, float thresh, float* positions, uint32_t* indices, uint32_t* mask, hipStream_t s) {
 	if (n == 0) return;
-	k_grid_samples<<<div_round_up(n, 128), 128, 0, s>>>(n, rng, step, cfg, grid_in, n_cascades, thresh, positions, indices);
+	const uint32_t nw = (uint32_t)grid_mask_words(n_cascades);
+	k_grid_mask<<<div_round_up(nw, 256), 256, 0, s>>>(nw, grid_in, thresh, mask);
+	k_grid_samples<<<div_round_up(n, 128), 128, 0, s>>>(n, rng, step, cfg, mask, n_cascades, positions, indices);
 	NGP_HIP(hipGetLastError());
 }
 void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t act, float* grid_tmp, hipStream_t s) {

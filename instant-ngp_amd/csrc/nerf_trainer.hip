@@ -170,7 +170,7 @@ struct ngp_nerf_trainer {
 		return e;
 	}
 	// occupancy grid
-	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens;
+	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens, grid_mask;
 	// training workspaces
 	Buf ray_indices, rays, numsteps, coords, mlp_out, dloss, coords_c, loss, counters, scan_tmp, tmp_u32, tmp_f32;
 	Buf loss_state;  // compute_loss: pass 1's per-sample compositing state for pass 2 (LossArgs::state)
@@ -413,7 +413,11 @@ int ngp_nerf_fill_rollover(void* stream, uint32_t n_elements, uint32_t stride, c
 int ngp_nerf_grid_generate_samples(void* stream, const ngp_nerf_config* cfg, uint32_t n, ngp_rng rng, uint32_t step,
                                    const float* grid, uint32_t n_cascades, float thresh, float* positions, uint32_t* indices) {
 	if (!cfg || !grid || !positions || !indices) return NGP_INVALID;
-	NERF_TRY(grid_generate_samples(n, Rng{rng.state, rng.inc}, step, *cfg, grid, n_cascades, thresh, positions, indices, S(stream)));
+	NERF_TRY({
+		static thread_local Buf mask;
+		grid_generate_samples(n, Rng{rng.state, rng.inc}, step, *cfg, grid, n_cascades, thresh, positions, indices,
+		                      mask.get<uint32_t>(grid_mask_words(n_cascades)), S(stream));
+	});
 }
 int ngp_nerf_grid_splat_max(void* stream, uint32_t n, const uint32_t* indices, const void* density_rm, uint32_t act, float* tmp) {
 	if (!indices || !density_rm || !tmp) return NGP_INVALID;
@@ -606,10 +610,11 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	// every rank generates the same sample set (same density rng); each evaluates its 1/N shard
 	float* pos = t->gpos.get<float>((size_t)n * 3);
 	uint32_t* idx = t->gidx.get<uint32_t>(n);
-	grid_generate_samples(n_uniform, t->grid_rng.dev(), t->ema_step, cfg, grid, n_cascades, -0.01f, pos, idx, s);
+	uint32_t* mask = t->grid_mask.get<uint32_t>(grid_mask_words(n_cascades));
+	grid_generate_samples(n_uniform, t->grid_rng.dev(), t->ema_step, cfg, grid, n_cascades, -0.01f, pos, idx, mask, s);
 	t->grid_rng.advance();
 	grid_generate_samples(n_nonuniform, t->grid_rng.dev(), t->ema_step, cfg, grid, n_cascades, MIN_OPTICAL_THICKNESS,
-	                      pos + (size_t)n_uniform * 3, idx + n_uniform, s);
+	                      pos + (size_t)n_uniform * 3, idx + n_uniform, mask, s);
 	t->grid_rng.advance();
 	const uint32_t lo = (uint32_t)((uint64_t)n * t->rank / t->world), hi = (uint32_t)((uint64_t)n * (t->rank + 1) / t->world);
 	const uint32_t ns = hi - lo;
