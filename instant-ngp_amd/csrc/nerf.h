@@ -120,6 +120,9 @@ void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, 
                     hipStream_t s);
 void grid_ema(uint32_t n, float decay, float* grid, const float* grid_tmp, hipStream_t s);
 void grid_mean_bitfield(const float* grid, uint32_t max_cascade, float* mean_out, uint8_t* bitfield, hipStream_t s);
+// grid_ema then grid_mean_bitfield in three launches (the density grid update's finalization; n_el >= GRID_N_CELLS)
+void grid_ema_mean_bitfield(uint32_t n_el, float decay, float* grid, const float* tmp, uint32_t max_cascade, float* mean_out,
+                            uint8_t* bitfield, hipStream_t s);
 size_t sample_tmp_f32(uint32_t n_rays);  // floats of sample_rays' tmp_f32 (stored t per step + ray geometry)
 size_t loss_tmp_f32(uint32_t n_rays);    // floats of compute_loss' tmp_f32 (per-ray pass-1 results)
 // construct_cdf_2d / construct_cdf_1d (testbed_nerf.cu:2356-2410) over the error map

@@ -1784,6 +1784,100 @@ void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, 
 	k_grid_splat<<<div_round_up(n, 128), 128, 0, s>>>(n, indices, density_rm, act, grid_tmp);
 	NGP_HIP(hipGetLastError());
 }
+// The update step's finalization in three launches instead of ten (the reference's ema_grid_samples_nerf,
+// update_density_grid_mean_and_bitfield and 7 bitfield_max_pool launches), the same float operations in the same
+// order, so the same bits:
+//   k_grid_ema_mean: the EMA of every cell; blocks [0, 512) take cascade 0 in k_grid_mean_partial's mapping and
+//     accumulate its mean partials from the values they just wrote;
+//   k_grid_bitfield: every block reduces the 512 partials in k_grid_mean_final's tree (block 0 stores the mean),
+//     then writes 8 bitfield bytes per thread;
+//   the pools into mips 1 .. max_cascade + 1 (full grids), then k_bitfield_pool_tail: one block for the mips above,
+//     whose sources are zero outside a central region that halves per mip (max_cascade + 1: 64^3 cells, ...).
+__global__ void __launch_bounds__(256) k_grid_ema_mean(uint32_t n, float decay, float* __restrict__ grid, const float* __restrict__ tmp,
+                                                       float* __restrict__ partial) {
+	__shared__ float sh[256];
+	if (blockIdx.x >= 512) {
+		const uint32_t i = GRID_N_CELLS + (blockIdx.x - 512) * 256 + threadIdx.x;
+		if (i >= n) return;
+		const float prev = grid[i];
+		grid[i] = prev < 0.f ? prev : fmaxf(prev * decay, tmp[i]);
+		return;
+	}
+	const uint32_t per_block = GRID_N_CELLS / 512;
+	const uint32_t base = blockIdx.x * per_block;
+	float acc = 0.f;
+	for (uint32_t k = threadIdx.x; k < per_block; k += 256) {
+		const float prev = grid[base + k];
+		const float v = prev < 0.f ? prev : fmaxf(prev * decay, tmp[base + k]);
+		grid[base + k] = v;
+		acc += fmaxf(v, 0.f) / (float)GRID_N_CELLS;
+	}
+	sh[threadIdx.x] = acc;
+	__syncthreads();
+	for (uint32_t off = 128; off > 0; off >>= 1) {
+		if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) partial[blockIdx.x] = sh[0];
+}
+__global__ void __launch_bounds__(512) k_grid_bitfield(uint32_t n_bytes, uint32_t n_nonzero, const float* __restrict__ grid,
+                                                       uint8_t* __restrict__ bitfield, const float* __restrict__ partial,
+                                                       float* __restrict__ mean_out) {
+	__shared__ float sh[512];
+	sh[threadIdx.x] = partial[threadIdx.x];
+	__syncthreads();
+	for (uint32_t off = 256; off > 0; off >>= 1) {
+		if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+		__syncthreads();
+	}
+	const float mean = sh[0];
+	if (blockIdx.x == 0 && threadIdx.x == 0) *mean_out = mean;
+	const float thresh = fminf(MIN_OPTICAL_THICKNESS, mean);
+#pragma unroll
+	for (uint32_t q = 0; q < 8; ++q) {
+		const uint32_t i = (blockIdx.x * 8 + q) * 512 + threadIdx.x;
+		if (i >= n_bytes) return;
+		if (i >= n_nonzero) { bitfield[i] = 0; continue; }
+		uint8_t bits = 0;
+#pragma unroll
+		for (uint8_t j = 0; j < 8; ++j) bits |= grid[i * 8 + j] > thresh ? ((uint8_t)1 << j) : 0;
+		bitfield[i] = bits;
+	}
+}
+__global__ void __launch_bounds__(1024) k_bitfield_pool_tail(uint32_t first, uint8_t* __restrict__ bitfield) {
+	for (uint32_t m = first; m + 1 < CASCADES; ++m) {
+		// mip m is zero outside cells [64 - h, 64 + h): h = 32 at m = first, halving per mip; in 4-cell blocks [lo, hi)
+		const uint32_t h = 32u >> (m - first);
+		const uint32_t lo = (64 - h) / 4, hi = (64 + h + 3) / 4, w = hi - lo;
+		const uint8_t* prev = bitfield + (size_t)m * GRID_N_CELLS / 8;
+		uint8_t* next = bitfield + (size_t)(m + 1) * GRID_N_CELLS / 8;
+		for (uint32_t t = threadIdx.x; t < w * w * w; t += blockDim.x) {
+			const uint32_t x = lo + t % w, y = lo + (t / w) % w, z = lo + t / (w * w);
+			const uint32_t i = morton3D(x, y, z);
+			uint8_t bits = 0;
+#pragma unroll
+			for (uint8_t j = 0; j < 8; ++j) bits |= prev[i * 8 + j] > 0 ? ((uint8_t)1 << j) : 0;
+			next[morton3D(x + GRIDSIZE / 8, y + GRIDSIZE / 8, z + GRIDSIZE / 8)] |= bits;
+		}
+		__syncthreads();
+	}
+}
+void grid_ema_mean_bitfield(uint32_t n_el, float decay, float* grid, const float* tmp, uint32_t max_cascade, float* mean_out,
+                            uint8_t* bitfield, hipStream_t s) {
+	float* partial = mean_out + 1;  // [1 + 512] floats
+	k_grid_ema_mean<<<512 + div_round_up(n_el - GRID_N_CELLS, 256), 256, 0, s>>>(n_el, decay, grid, tmp, partial);
+	const uint32_t n_bytes = GRID_N_CELLS / 8 * CASCADES;
+	k_grid_bitfield<<<div_round_up(n_bytes, 8 * 512), 512, 0, s>>>(n_bytes, GRID_N_CELLS / 8 * (max_cascade + 1), grid, bitfield, partial,
+	                                                              mean_out);
+	const uint32_t full = std::min(max_cascade + 1, CASCADES - 1);  // mips 1 .. full from whole grids
+	for (uint32_t level = 1; level <= full; ++level) {
+		const uint32_t n = GRID_N_CELLS / 64;
+		k_bitfield_max_pool<<<div_round_up(n, 256), 256, 0, s>>>(n, bitfield + (size_t)(level - 1) * GRID_N_CELLS / 8,
+		                                                          bitfield + (size_t)level * GRID_N_CELLS / 8);
+	}
+	if (full + 1 < CASCADES) k_bitfield_pool_tail<<<1, 1024, 0, s>>>(full, bitfield);
+	NGP_HIP(hipGetLastError());
+}
 void grid_ema(uint32_t n, float decay, float* grid, const float* tmp, hipStream_t s) {
 	k_grid_ema<<<div_round_up(n, 256), 256, 0, s>>>(n, decay, grid, tmp);
 	NGP_HIP(hipGetLastError());

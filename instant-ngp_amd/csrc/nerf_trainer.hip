@@ -629,9 +629,14 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 		NGP_CHECK(t->allreduce(t->allreduce_user, tmp, n_el, NGP_DTYPE_F32, NGP_REDUCE_MAX, s) == 0,
 		          "data parallel: density-grid all-reduce failed");
 	}
-	grid_ema(n_el, decay, grid, tmp, s);
+	static const bool fused = !getenv("NGP_GRID_FINAL_FUSED") || atoi(getenv("NGP_GRID_FINAL_FUSED")) != 0;  // A/B knob
+	if (fused) {
+		grid_ema_mean_bitfield(n_el, decay, grid, tmp, cfg.max_cascade, (float*)t->mean.p, (uint8_t*)t->bitfield.p, s);
+	} else {
+		grid_ema(n_el, decay, grid, tmp, s);
+		grid_mean_bitfield(grid, cfg.max_cascade, (float*)t->mean.p, (uint8_t*)t->bitfield.p, s);
+	}
 	++t->ema_step;
-	grid_mean_bitfield(grid, cfg.max_cascade, (float*)t->mean.p, (uint8_t*)t->bitfield.p, s);
 }
 
 // Data parallel: this shard's counters and loss as five floats for one all-reduce (sum). The u32
