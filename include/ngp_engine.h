@@ -383,6 +383,11 @@ int ngp_nerf_grid_generate_samples(void* stream, const ngp_nerf_config* cfg, uin
                                    uint32_t* indices);
 int ngp_nerf_grid_splat_max(void* stream, uint32_t n, const uint32_t* indices, const void* density_rm,
                             uint32_t density_activation, float* grid_tmp);
+// The reference's memset(grid_tmp, 0) + splat_grid_samples_nerf_max_nearest_neighbor (testbed_nerf.cu:3476, :678-702)
+// in one call: grid_tmp[c] = the max over the samples in cell c (0 where none) for all n_cells cells (a multiple of
+// 8192), computed as a counting sort by cell bin instead of scattered atomics; bit-identical.
+int ngp_nerf_grid_splat_max_cells(void* stream, uint32_t n, const uint32_t* indices, const void* density_rm,
+                                  uint32_t density_activation, float* grid_tmp, uint32_t n_cells);
 int ngp_nerf_grid_ema(void* stream, uint32_t n, float decay, float* grid, const float* grid_tmp);
 int ngp_nerf_grid_mean_and_bitfield(void* stream, const float* grid, uint32_t max_cascade, float* mean, uint8_t* bitfield);
 

@@ -163,6 +163,7 @@ SIGNATURES = {
     "ngp_nerf_fill_rollover": (i32, [P, u32, u32, P, P, i32, i32]),
     "ngp_nerf_grid_generate_samples": (i32, [P, C.POINTER(NerfConfig), u32, Rng, u32, P, u32, f32, P, P]),
     "ngp_nerf_grid_splat_max": (i32, [P, u32, P, P, u32, P]),
+    "ngp_nerf_grid_splat_max_cells": (i32, [P, u32, P, P, u32, P, u32]),
     "ngp_nerf_grid_ema": (i32, [P, u32, f32, P, P]),
     "ngp_nerf_grid_mean_and_bitfield": (i32, [P, P, u32, P, P]),
     "ngp_nerf_trainer_create": (i32, [P, P, P, C.POINTER(NerfConfig), u64, C.POINTER(P)]),

@@ -118,6 +118,11 @@ void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_co
 size_t grid_mask_words(uint32_t n_cascades);  // u32 of grid_generate_samples' cell mask
 void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t density_activation, float* grid_tmp,
                     hipStream_t s);
+// memset(grid_tmp, 0) + grid_splat_max as a counting sort by cell bin: writes all n_cells of grid_tmp; scratch holds
+// grid_splat_scratch_u32(n, n_cells) words
+size_t grid_splat_scratch_u32(uint32_t n, uint32_t n_cells);
+void grid_splat_max_binned(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t density_activation,
+                           float* grid_tmp, uint32_t n_cells, uint32_t* scratch, hipStream_t s);
 void grid_ema(uint32_t n, float decay, float* grid, const float* grid_tmp, hipStream_t s);
 void grid_mean_bitfield(const float* grid, uint32_t max_cascade, float* mean_out, uint8_t* bitfield, hipStream_t s);
 // grid_ema then grid_mean_bitfield in three launches (the density grid update's finalization; n_el >= GRID_N_CELLS)

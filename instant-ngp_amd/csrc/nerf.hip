@@ -1669,24 +1669,39 @@ __global__ void k_grid_mask(uint32_t n_words, const float* __restrict__ grid, fl
 	mask[w] = bits;
 }
 
+#ifndef NGP_GRID_CAND_FIRST
+#define NGP_GRID_CAND_FIRST 2  // k_grid_samples: candidates whose mask words every lane loads (10: all at once)
+#endif
+static_assert(NGP_GRID_CAND_FIRST >= 1 && NGP_GRID_CAND_FIRST <= 10, "grid sample candidates");
 __global__ void k_grid_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_config cfg, const uint32_t* __restrict__ mask,
                                uint32_t n_cascades, float* __restrict__ out, uint32_t* __restrict__ indices) {
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
 	pcg_advance(rng, (uint64_t)i * 4);
 	const uint32_t level = (uint32_t)(pcg_float(rng) * n_cascades) % n_cascades;
-	// the 10 candidates' mask words loaded at once (L2 hits), then the first candidate that passes, as the
-	// reference's loop takes it (its last candidate when none passes)
+	// the candidates' mask words (L2 hits) in batches of GRID_CAND_FIRST and the rest, the second batch only for the
+	// lanes whose first batch has no passing cell: the first candidate that passes, as the reference's loop takes it
+	// (its last candidate when none passes). The kernel is bound by the L2 request rate, and in the uniform pass nearly
+	// every first candidate passes.
+	constexpr uint32_t NA = NGP_GRID_CAND_FIRST;
 	uint32_t cand[10], word[10];
+	const uint32_t base = (i + step * n) * 56924617u + 96925573u;
 #pragma unroll
-	for (uint32_t j = 0; j < 10; ++j) {
-		cand[j] = ((i + step * n) * 56924617u + j * 19349663u + 96925573u) % GRID_N_CELLS + level * GRID_N_CELLS;
-		word[j] = mask[cand[j] >> 5];
-	}
-	uint32_t idx = cand[9];
+	for (uint32_t j = 0; j < 10; ++j) cand[j] = (base + j * 19349663u) % GRID_N_CELLS + level * GRID_N_CELLS;
 #pragma unroll
-	for (int j = 9; j >= 0; --j)
+	for (uint32_t j = 0; j < NA; ++j) word[j] = mask[cand[j] >> 5];
+	uint32_t idx = ~0u;
+#pragma unroll
+	for (int j = (int)NA - 1; j >= 0; --j)
 		if ((word[j] >> (cand[j] & 31u)) & 1u) idx = cand[j];
+	if (idx == ~0u) {
+#pragma unroll
+		for (uint32_t j = NA; j < 10; ++j) word[j] = mask[cand[j] >> 5];
+		idx = cand[9];
+#pragma unroll
+		for (int j = 9; j >= (int)NA; --j)
+			if ((word[j] >> (cand[j] & 31u)) & 1u) idx = cand[j];
+	}
 	const uint32_t pos_idx = idx % GRID_N_CELLS;
 	const uint32_t x = morton3D_invert(pos_idx >> 0), y = morton3D_invert(pos_idx >> 1), z = morton3D_invert(pos_idx >> 2);
 	const float r0 = pcg_float(rng), r1 = pcg_float(rng), r2 = pcg_float(rng);
@@ -1779,9 +1794,142 @@ void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_co
 	k_grid_samples<<<div_round_up(n, 128), 128, 0, s>>>(n, rng, step, cfg, mask, n_cascades, positions, indices);
 	NGP_HIP(hipGetLastError());
 }
+// The splat as a counting sort by cell bin (fox: 5.2 M samples into 10.5 M cells). The direct splat's atomics are
+// scattered over the whole grid and run at ~32 G/s whatever their locality (an XCD-sliced variant that kept each
+// XCD's cells L2-resident measured no faster): here each sample costs two LDS atomics and 8 B of
+// coalesced-ish traffic instead. Bins of 8192 cells (32 KB of LDS):
+//   k_splat_hist: per-block LDS histogram of the samples' bins, added to the global counts (one atomic per bin and
+//     block);
+//   k_splat_scan: the bins' offsets (one block);
+//   k_splat_scatter: each block reserves its range in every bin (cursor atomics), ranks its samples in LDS and writes
+//     (cell in bin << 16 | density bits) there;
+//   k_splat_bins: a block per bin takes the max of its samples in LDS with the same uint compare as the atomics, then
+//     writes all 8192 cells (so no memset of grid_tmp).
+// Max does not depend on the order, so grid_tmp is bit-identical to memset(0) + k_grid_splat.
+#ifndef NGP_SPLAT_THREADS
+#define NGP_SPLAT_THREADS 1024
+#endif
+constexpr uint32_t SPLAT_THREADS = NGP_SPLAT_THREADS;  // k_splat_hist / k_splat_scatter block size
+constexpr uint32_t SPLAT_BIN_SHIFT = 13, SPLAT_BIN = 1u << SPLAT_BIN_SHIFT, SPLAT_MAX_BINS = 8 * GRID_N_CELLS / SPLAT_BIN;
+__device__ __forceinline__ void splat_chunk(uint32_t n, uint32_t nb, uint32_t* s0, uint32_t* s1) {
+	*s0 = (uint32_t)((uint64_t)n * blockIdx.x / nb);
+	*s1 = (uint32_t)((uint64_t)n * (blockIdx.x + 1) / nb);
+}
+__global__ void __launch_bounds__(SPLAT_THREADS) k_splat_hist(uint32_t n, const uint32_t* __restrict__ indices, uint32_t n_bins,
+                                                   uint32_t* __restrict__ counts) {
+	__shared__ uint32_t h[SPLAT_MAX_BINS];
+	for (uint32_t b = threadIdx.x; b < n_bins; b += SPLAT_THREADS) h[b] = 0;
+	__syncthreads();
+	uint32_t s0, s1;
+	splat_chunk(n, gridDim.x, &s0, &s1);
+	for (uint32_t i = s0 + threadIdx.x; i < s1; i += 4 * SPLAT_THREADS) {
+		uint32_t k[4];
+#pragma unroll
+		for (uint32_t u = 0; u < 4; ++u) k[u] = i + u * SPLAT_THREADS < s1 ? indices[i + u * SPLAT_THREADS] : ~0u;
+#pragma unroll
+		for (uint32_t u = 0; u < 4; ++u)
+			if (k[u] != ~0u) atomicAdd(&h[k[u] >> SPLAT_BIN_SHIFT], 1u);
+	}
+	__syncthreads();
+	for (uint32_t b = threadIdx.x; b < n_bins; b += SPLAT_THREADS)
+		if (h[b]) atomicAdd(&counts[b], h[b]);
+}
+__global__ void __launch_bounds__(1024) k_splat_scan(uint32_t n_bins, const uint32_t* __restrict__ counts,
+                                                    uint32_t* __restrict__ offsets, uint32_t* __restrict__ cursor) {
+	__shared__ uint32_t sh[1024];
+	const uint32_t b0 = 2 * threadIdx.x;  // two bins per thread (n_bins <= 2048)
+	const uint32_t c0 = b0 < n_bins ? counts[b0] : 0u, c1 = b0 + 1 < n_bins ? counts[b0 + 1] : 0u;
+	sh[threadIdx.x] = c0 + c1;
+	__syncthreads();
+	for (uint32_t off = 1; off < 1024; off <<= 1) {  // inclusive scan (Hillis-Steele)
+		const uint32_t v = threadIdx.x >= off ? sh[threadIdx.x - off] : 0u;
+		__syncthreads();
+		sh[threadIdx.x] += v;
+		__syncthreads();
+	}
+	const uint32_t ex = sh[threadIdx.x] - c0 - c1;
+	if (b0 < n_bins) { offsets[b0] = ex; cursor[b0] = ex; }
+	if (b0 + 1 < n_bins) { offsets[b0 + 1] = ex + c0; cursor[b0 + 1] = ex + c0; }
+	if (threadIdx.x == 1023) offsets[n_bins] = sh[1023];
+}
+__global__ void __launch_bounds__(SPLAT_THREADS) k_splat_scatter(uint32_t n, const uint32_t* __restrict__ indices,
+                                                      const f16* __restrict__ density, uint32_t n_bins,
+                                                      uint32_t* __restrict__ cursor, uint32_t* __restrict__ packed) {
+	__shared__ uint32_t h[SPLAT_MAX_BINS], base[SPLAT_MAX_BINS];
+	for (uint32_t b = threadIdx.x; b < n_bins; b += SPLAT_THREADS) h[b] = 0;
+	__syncthreads();
+	uint32_t s0, s1;
+	splat_chunk(n, gridDim.x, &s0, &s1);
+	for (uint32_t i = s0 + threadIdx.x; i < s1; i += 4 * SPLAT_THREADS) {
+		uint32_t k[4];
+#pragma unroll
+		for (uint32_t u = 0; u < 4; ++u) k[u] = i + u * SPLAT_THREADS < s1 ? indices[i + u * SPLAT_THREADS] : ~0u;
+#pragma unroll
+		for (uint32_t u = 0; u < 4; ++u)
+			if (k[u] != ~0u) atomicAdd(&h[k[u] >> SPLAT_BIN_SHIFT], 1u);
+	}
+	__syncthreads();
+	for (uint32_t b = threadIdx.x; b < n_bins; b += SPLAT_THREADS) {
+		if (h[b]) base[b] = atomicAdd(&cursor[b], h[b]);
+		h[b] = 0;
+	}
+	__syncthreads();
+	for (uint32_t i = s0 + threadIdx.x; i < s1; i += 4 * SPLAT_THREADS) {
+		uint32_t k[4];
+		uint16_t d[4];
+#pragma unroll
+		for (uint32_t u = 0; u < 4; ++u) {
+			const bool ok = i + u * SPLAT_THREADS < s1;
+			k[u] = ok ? indices[i + u * SPLAT_THREADS] : ~0u;
+			d[u] = ok ? __builtin_bit_cast(uint16_t, density[i + u * SPLAT_THREADS]) : (uint16_t)0;
+		}
+#pragma unroll
+		for (uint32_t u = 0; u < 4; ++u) {
+			if (k[u] == ~0u) continue;
+			const uint32_t b = k[u] >> SPLAT_BIN_SHIFT;
+			const uint32_t r = atomicAdd(&h[b], 1u);
+			packed[base[b] + r] = (k[u] & (SPLAT_BIN - 1)) << 16 | d[u];
+		}
+	}
+}
+__global__ void __launch_bounds__(1024) k_splat_bins(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ packed,
+                                                    uint32_t act, float* __restrict__ grid_out) {
+	__shared__ uint32_t m[SPLAT_BIN];
+	for (uint32_t c = threadIdx.x; c < SPLAT_BIN; c += 1024) m[c] = 0;
+	__syncthreads();
+	const uint32_t b = blockIdx.x, e = offsets[b + 1];
+	for (uint32_t k = offsets[b] + threadIdx.x; k < e; k += 1024) {
+		const uint32_t v = packed[k];
+		const float mlp = network_to_density((float)__builtin_bit_cast(f16, (uint16_t)(v & 0xffffu)), act);
+		const float thickness = mlp * scalbnf(MIN_CONE_STEPSIZE, 0);
+		atomicMax(&m[v >> 16], __float_as_uint(thickness));
+	}
+	__syncthreads();
+	uint4* out = (uint4*)(grid_out + (size_t)b * SPLAT_BIN);
+	for (uint32_t q = threadIdx.x; q < SPLAT_BIN / 4; q += 1024) out[q] = make_uint4(m[4 * q], m[4 * q + 1], m[4 * q + 2], m[4 * q + 3]);
+}
+
+size_t grid_splat_scratch_u32(uint32_t n, uint32_t n_cells) { return 3 * ((size_t)(n_cells >> SPLAT_BIN_SHIFT) + 1) + n; }
+
 void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t act, float* grid_tmp, hipStream_t s) {
 	if (n == 0) return;
 	k_grid_splat<<<div_round_up(n, 128), 128, 0, s>>>(n, indices, density_rm, act, grid_tmp);
+	NGP_HIP(hipGetLastError());
+}
+void grid_splat_max_binned(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t act, float* grid_tmp,
+                           uint32_t n_cells, uint32_t* scratch, hipStream_t s) {
+	const uint32_t n_bins = n_cells >> SPLAT_BIN_SHIFT;
+	NGP_CHECK(n_cells % SPLAT_BIN == 0 && n_bins <= SPLAT_MAX_BINS, "grid splat: bad cell count");
+	uint32_t* counts = scratch;
+	uint32_t* offsets = counts + n_bins + 1;
+	uint32_t* cursor = offsets + n_bins + 1;
+	uint32_t* packed = cursor + n_bins + 1;
+	NGP_HIP(hipMemsetAsync(counts, 0, (size_t)n_bins * 4, s));
+	const uint32_t nb = std::max(1u, std::min(128u, div_round_up(n, 16384)));
+	if (n) k_splat_hist<<<nb, SPLAT_THREADS, 0, s>>>(n, indices, n_bins, counts);
+	k_splat_scan<<<1, 1024, 0, s>>>(n_bins, counts, offsets, cursor);
+	if (n) k_splat_scatter<<<nb, SPLAT_THREADS, 0, s>>>(n, indices, density_rm, n_bins, cursor, packed);
+	k_splat_bins<<<n_bins, 1024, 0, s>>>(offsets, packed, act, grid_tmp);
 	NGP_HIP(hipGetLastError());
 }
 // The update step's finalization in three launches instead of ten (the reference's ema_grid_samples_nerf,

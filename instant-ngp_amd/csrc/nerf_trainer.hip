@@ -170,7 +170,7 @@ struct ngp_nerf_trainer {
 		return e;
 	}
 	// occupancy grid
-	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens, grid_mask;
+	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens, grid_mask, splat_scratch;
 	// training workspaces
 	Buf ray_indices, rays, numsteps, coords, mlp_out, dloss, coords_c, loss, counters, scan_tmp, tmp_u32, tmp_f32;
 	Buf loss_state;  // compute_loss: pass 1's per-sample compositing state for pass 2 (LossArgs::state)
@@ -423,6 +423,15 @@ int ngp_nerf_grid_splat_max(void* stream, uint32_t n, const uint32_t* indices, c
 	if (!indices || !density_rm || !tmp) return NGP_INVALID;
 	NERF_TRY(grid_splat_max(n, indices, (const f16*)density_rm, act, tmp, S(stream)));
 }
+int ngp_nerf_grid_splat_max_cells(void* stream, uint32_t n, const uint32_t* indices, const void* density_rm, uint32_t act,
+                                  float* tmp, uint32_t n_cells) {
+	if ((n && (!indices || !density_rm)) || !tmp || n_cells == 0 || n_cells % 8192 || n_cells > 8 * GRID_N_CELLS) return NGP_INVALID;
+	NERF_TRY({
+		static thread_local Buf scratch;
+		grid_splat_max_binned(n, indices, (const f16*)density_rm, act, tmp, n_cells,
+		                      scratch.get<uint32_t>(grid_splat_scratch_u32(n, n_cells)), S(stream));
+	});
+}
 int ngp_nerf_grid_ema(void* stream, uint32_t n, float decay, float* grid, const float* tmp) {
 	if (!grid || !tmp) return NGP_INVALID;
 	NERF_TRY(grid_ema(n, decay, grid, tmp, S(stream)));
@@ -606,7 +615,9 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	}
 	const uint32_t n = n_uniform + n_nonuniform;
 	float* tmp = t->grid_tmp.get<float>(n_el);
-	NGP_HIP(hipMemsetAsync(tmp, 0, (size_t)n_el * 4, s));
+	// the splat as a counting sort by cell bin, which writes every cell (A/B knob NGP_SPLAT_BINNED=0: memset + atomics)
+	static const bool binned = !getenv("NGP_SPLAT_BINNED") || atoi(getenv("NGP_SPLAT_BINNED")) != 0;
+	if (!binned) NGP_HIP(hipMemsetAsync(tmp, 0, (size_t)n_el * 4, s));
 	// every rank generates the same sample set (same density rng); each evaluates its 1/N shard
 	float* pos = t->gpos.get<float>((size_t)n * 3);
 	uint32_t* idx = t->gidx.get<uint32_t>(n);
@@ -622,8 +633,11 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	if (ns) {
 		// row 0 (raw density) only: the other 15 rows of the density network's output are not read
 		check_rc(ngp::density_impl(t->model, s, ns, pos + (size_t)lo * 3, 3, dens, ns, ngp::DENSITY_LAYOUT_ROW0, 0));
-		grid_splat_max(ns, idx + lo, dens, cfg.density_activation, tmp, s);
+		if (!binned) grid_splat_max(ns, idx + lo, dens, cfg.density_activation, tmp, s);
 	}
+	if (binned)
+		grid_splat_max_binned(ns, idx + lo, dens, cfg.density_activation, tmp, n_el,
+		                      t->splat_scratch.get<uint32_t>(grid_splat_scratch_u32(ns, n_el)), s);
 	if (t->world > 1) {
 		// splatted maxima of all shards (values are >= 0: float max == max of the shards' atomicMax)
 		NGP_CHECK(t->allreduce(t->allreduce_user, tmp, n_el, NGP_DTYPE_F32, NGP_REDUCE_MAX, s) == 0,

@@ -188,9 +188,15 @@ def grid_generate_samples(cfg, n, rng, step, grid, n_cascades, thresh, stream=No
     return pos, idx
 
 
-def grid_splat_max(indices, density_out, density_activation, grid_tmp, stream=None):
+def grid_splat_max(indices, density_out, density_activation, grid_tmp, stream=None, binned=False):
     """splat_grid_samples_nerf_max_nearest_neighbor (testbed_nerf.cu:678-702). density_out: the density
-    network's fp16 output, row-major [16 x n] (feature-major), density in row 0."""
+    network's fp16 output, row-major [16 x n] (feature-major), density in row 0. binned: the memset of grid_tmp
+    and the splat in one call (ngp_nerf_grid_splat_max_cells, a counting sort by cell bin): grid_tmp is
+    overwritten, every cell of it."""
+    if binned:
+        check(lib().ngp_nerf_grid_splat_max_cells(_stream(stream), indices.shape[0], _ptr(indices), _ptr(density_out),
+                                                  density_activation, _ptr(grid_tmp), grid_tmp.numel()))
+        return
     check(lib().ngp_nerf_grid_splat_max(_stream(stream), indices.shape[0], _ptr(indices), _ptr(density_out),
                                         density_activation, _ptr(grid_tmp)))
 

@@ -84,8 +84,8 @@ def test_fox_capture_density_update_sampler_compaction(pkg, orc, fox):
     pos = torch.cat([pos_u, pos_n]).contiguous()
     idx = torch.cat([idx_u, idx_n]).contiguous()
     dens = net.density(pos, layout=pkg.LAYOUT_SOA, use_inference_params=False)  # [16 x n], density in row 0
-    tmp = torch.zeros_like(grid_t)
-    pkg.nerf.grid_splat_max(idx, dens, cfg.density_activation, tmp)
+    tmp = torch.full_like(grid_t, float("nan"))  # the trainer's binned splat writes every cell
+    pkg.nerf.grid_splat_max(idx, dens, cfg.density_activation, tmp, binned=True)
     pkg.nerf.grid_ema(0.95, grid_t, tmp)
     ref_grid = grid.copy()
     orc.nerf_grid_splat_ema(np.concatenate([ref_iu, ref_in]), dens[0].cpu().numpy().view(np.uint16).copy(),

@@ -291,7 +291,10 @@ def test_fill_rollover(pkg, orc, dtype, rescale):
     np.testing.assert_array_equal(got if dtype == torch.float32 else got.view(np.uint16), ref)
 
 
-def test_density_grid_update(pkg, orc):
+@pytest.mark.parametrize("binned", [False, True])
+def test_density_grid_update(pkg, orc, binned):
+    """binned: the memset + splat as one counting sort by cell bin (ngp_nerf_grid_splat_max_cells, what the
+    trainer's update runs); tmp starts as garbage there, since every cell is written."""
     cfg = pkg.nerf.default_config(4.0)
     g = np.random.default_rng(3)
     grid = np.where(g.random(128 ** 3 * 8) < 0.5, g.random(128 ** 3 * 8) * 0.02, 0.0).astype(np.float32)
@@ -305,9 +308,9 @@ def test_density_grid_update(pkg, orc):
     np.testing.assert_array_equal(idx.cpu().numpy().view(np.uint32), idx_ref)
     np.testing.assert_array_equal(pos.cpu().numpy(), pos_ref)
     dens = g.uniform(-8, 3, (n, 16)).astype(np.float16)
-    tmp = torch.zeros_like(grid_t)
+    tmp = torch.full_like(grid_t, float("nan")) if binned else torch.zeros_like(grid_t)
     # the density network output is row-major [16 x n] (feature-major), density in row 0 (testbed_nerf.cu:3488-3496)
-    pkg.nerf.grid_splat_max(idx, torch.from_numpy(np.ascontiguousarray(dens.T)).cuda(), 3, tmp)
+    pkg.nerf.grid_splat_max(idx, torch.from_numpy(np.ascontiguousarray(dens.T)).cuda(), 3, tmp, binned=binned)
     pkg.nerf.grid_ema(0.95, grid_t, tmp)
     ref_grid = grid.copy()
     orc.nerf_grid_splat_ema(idx_ref, dens[:, 0].copy().view(np.uint16), 3, ref_grid, 0.95)
