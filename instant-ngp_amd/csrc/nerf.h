@@ -123,6 +123,16 @@ void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, 
 size_t grid_splat_scratch_u32(uint32_t n, uint32_t n_cells);
 void grid_splat_max_binned(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t density_activation,
                            float* grid_tmp, uint32_t n_cells, uint32_t* scratch, hipStream_t s);
+// The update's samples in bin order before the density evaluation (which then runs ~1.8x faster on grouped positions):
+// grid_sort_samples writes 16-B records (x, y, z, cell within the bin) sorted by 8192-cell bin (order within a bin
+// arbitrary; recs: 4 n floats) and keeps the bins' offsets in scratch (grid_sort_scratch_u32 words); the density reads
+// the records with stride 4; grid_splat_sorted then writes every cell of grid_tmp from the densities of the sorted
+// samples [lo, hi) (density_rm[k - lo]) = memset + splat of those samples.
+size_t grid_sort_scratch_u32(uint32_t n, uint32_t n_cells);
+void grid_sort_samples(uint32_t n, const float* positions, const uint32_t* indices, uint32_t n_cells, uint32_t* scratch,
+                       float* recs, hipStream_t s);
+void grid_splat_sorted(uint32_t n_cells, const uint32_t* scratch, const float* recs, const f16* density_rm, uint32_t lo, uint32_t hi,
+                       uint32_t density_activation, float* grid_tmp, hipStream_t s);
 void grid_ema(uint32_t n, float decay, float* grid, const float* grid_tmp, hipStream_t s);
 void grid_mean_bitfield(const float* grid, uint32_t max_cascade, float* mean_out, uint8_t* bitfield, hipStream_t s);
 // grid_ema then grid_mean_bitfield in three launches (the density grid update's finalization; n_el >= GRID_N_CELLS)

@@ -1811,6 +1811,10 @@ void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_co
 #endif
 constexpr uint32_t SPLAT_THREADS = NGP_SPLAT_THREADS;  // k_splat_hist / k_splat_scatter block size
 constexpr uint32_t SPLAT_BIN_SHIFT = 13, SPLAT_BIN = 1u << SPLAT_BIN_SHIFT, SPLAT_MAX_BINS = 8 * GRID_N_CELLS / SPLAT_BIN;
+#ifndef NGP_SPLAT_MAX_BLOCKS
+#define NGP_SPLAT_MAX_BLOCKS 128
+#endif
+static uint32_t splat_blocks(uint32_t n) { return std::max(1u, std::min((uint32_t)NGP_SPLAT_MAX_BLOCKS, div_round_up(n, 16384))); }
 __device__ __forceinline__ void splat_chunk(uint32_t n, uint32_t nb, uint32_t* s0, uint32_t* s1) {
 	*s0 = (uint32_t)((uint64_t)n * blockIdx.x / nb);
 	*s1 = (uint32_t)((uint64_t)n * (blockIdx.x + 1) / nb);
@@ -1852,9 +1856,15 @@ __global__ void __launch_bounds__(1024) k_splat_scan(uint32_t n_bins, const uint
 	if (b0 + 1 < n_bins) { offsets[b0 + 1] = ex + c0; cursor[b0 + 1] = ex + c0; }
 	if (threadIdx.x == 1023) offsets[n_bins] = sh[1023];
 }
+// SORT: the samples themselves into bin order before the density evaluation, one 16-B record per sample (x, y, z and
+// the cell within the bin as the 4th word: one store request per sample); else the (cell in bin, density bits) pairs
+// after it.
+template <bool SORT>
 __global__ void __launch_bounds__(SPLAT_THREADS) k_splat_scatter(uint32_t n, const uint32_t* __restrict__ indices,
-                                                      const f16* __restrict__ density, uint32_t n_bins,
-                                                      uint32_t* __restrict__ cursor, uint32_t* __restrict__ packed) {
+                                                                const f16* __restrict__ density,
+                                                                const float* __restrict__ positions, uint32_t n_bins,
+                                                                uint32_t* __restrict__ cursor, uint32_t* __restrict__ packed,
+                                                                float4* __restrict__ pos_out) {
 	__shared__ uint32_t h[SPLAT_MAX_BINS], base[SPLAT_MAX_BINS];
 	for (uint32_t b = threadIdx.x; b < n_bins; b += SPLAT_THREADS) h[b] = 0;
 	__syncthreads();
@@ -1877,32 +1887,58 @@ __global__ void __launch_bounds__(SPLAT_THREADS) k_splat_scatter(uint32_t n, con
 	for (uint32_t i = s0 + threadIdx.x; i < s1; i += 4 * SPLAT_THREADS) {
 		uint32_t k[4];
 		uint16_t d[4];
+		float px[4], py[4], pz[4];
 #pragma unroll
 		for (uint32_t u = 0; u < 4; ++u) {
 			const bool ok = i + u * SPLAT_THREADS < s1;
-			k[u] = ok ? indices[i + u * SPLAT_THREADS] : ~0u;
-			d[u] = ok ? __builtin_bit_cast(uint16_t, density[i + u * SPLAT_THREADS]) : (uint16_t)0;
+			const uint32_t j = i + u * SPLAT_THREADS;
+			k[u] = ok ? indices[j] : ~0u;
+			if (SORT) {
+				px[u] = ok ? positions[(size_t)j * 3 + 0] : 0.f;
+				py[u] = ok ? positions[(size_t)j * 3 + 1] : 0.f;
+				pz[u] = ok ? positions[(size_t)j * 3 + 2] : 0.f;
+			} else {
+				d[u] = ok ? __builtin_bit_cast(uint16_t, density[j]) : (uint16_t)0;
+			}
 		}
 #pragma unroll
 		for (uint32_t u = 0; u < 4; ++u) {
 			if (k[u] == ~0u) continue;
 			const uint32_t b = k[u] >> SPLAT_BIN_SHIFT;
-			const uint32_t r = atomicAdd(&h[b], 1u);
-			packed[base[b] + r] = (k[u] & (SPLAT_BIN - 1)) << 16 | d[u];
+			const uint32_t slot = base[b] + atomicAdd(&h[b], 1u);
+			if (SORT) {
+				pos_out[slot] = make_float4(px[u], py[u], pz[u], __uint_as_float(k[u] & (SPLAT_BIN - 1)));
+			} else {
+				packed[slot] = (k[u] & (SPLAT_BIN - 1)) << 16 | d[u];
+			}
 		}
 	}
 }
+// SORT: bin b's samples are [offsets[b], offsets[b + 1]) of the sorted records (cell in the 4th word), their densities
+// density[k - lo] for the shard [lo, hi) this rank evaluated
+template <bool SORT>
 __global__ void __launch_bounds__(1024) k_splat_bins(const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ packed,
-                                                    uint32_t act, float* __restrict__ grid_out) {
+                                                    const float4* __restrict__ recs, const f16* __restrict__ density,
+                                                    uint32_t lo, uint32_t hi, uint32_t act, float* __restrict__ grid_out) {
 	__shared__ uint32_t m[SPLAT_BIN];
 	for (uint32_t c = threadIdx.x; c < SPLAT_BIN; c += 1024) m[c] = 0;
 	__syncthreads();
-	const uint32_t b = blockIdx.x, e = offsets[b + 1];
-	for (uint32_t k = offsets[b] + threadIdx.x; k < e; k += 1024) {
-		const uint32_t v = packed[k];
-		const float mlp = network_to_density((float)__builtin_bit_cast(f16, (uint16_t)(v & 0xffffu)), act);
+	const uint32_t b = blockIdx.x;
+	const uint32_t k0 = SORT ? std::max(offsets[b], lo) : offsets[b], e = SORT ? std::min(offsets[b + 1], hi) : offsets[b + 1];
+	for (uint32_t k = k0 + threadIdx.x; k < e; k += 1024) {
+		uint32_t c;
+		f16 d;
+		if (SORT) {
+			c = __float_as_uint(recs[k].w);
+			d = density[k - lo];
+		} else {
+			const uint32_t v = packed[k];
+			c = v >> 16;
+			d = __builtin_bit_cast(f16, (uint16_t)(v & 0xffffu));
+		}
+		const float mlp = network_to_density((float)d, act);
 		const float thickness = mlp * scalbnf(MIN_CONE_STEPSIZE, 0);
-		atomicMax(&m[v >> 16], __float_as_uint(thickness));
+		atomicMax(&m[c], __float_as_uint(thickness));
 	}
 	__syncthreads();
 	uint4* out = (uint4*)(grid_out + (size_t)b * SPLAT_BIN);
@@ -1916,20 +1952,41 @@ void grid_splat_max(uint32_t n, const uint32_t* indices, const f16* density_rm, 
 	k_grid_splat<<<div_round_up(n, 128), 128, 0, s>>>(n, indices, density_rm, act, grid_tmp);
 	NGP_HIP(hipGetLastError());
 }
-void grid_splat_max_binned(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t act, float* grid_tmp,
-                           uint32_t n_cells, uint32_t* scratch, hipStream_t s) {
+// the histogram, offsets and cursors of n samples' bins (scratch: counts, offsets, cursor of n_bins + 1 words each)
+static uint32_t splat_bin_offsets(uint32_t n, const uint32_t* indices, uint32_t n_cells, uint32_t* scratch, hipStream_t s) {
 	const uint32_t n_bins = n_cells >> SPLAT_BIN_SHIFT;
 	NGP_CHECK(n_cells % SPLAT_BIN == 0 && n_bins <= SPLAT_MAX_BINS, "grid splat: bad cell count");
 	uint32_t* counts = scratch;
-	uint32_t* offsets = counts + n_bins + 1;
-	uint32_t* cursor = offsets + n_bins + 1;
-	uint32_t* packed = cursor + n_bins + 1;
 	NGP_HIP(hipMemsetAsync(counts, 0, (size_t)n_bins * 4, s));
-	const uint32_t nb = std::max(1u, std::min(128u, div_round_up(n, 16384)));
-	if (n) k_splat_hist<<<nb, SPLAT_THREADS, 0, s>>>(n, indices, n_bins, counts);
-	k_splat_scan<<<1, 1024, 0, s>>>(n_bins, counts, offsets, cursor);
-	if (n) k_splat_scatter<<<nb, SPLAT_THREADS, 0, s>>>(n, indices, density_rm, n_bins, cursor, packed);
-	k_splat_bins<<<n_bins, 1024, 0, s>>>(offsets, packed, act, grid_tmp);
+	if (n) k_splat_hist<<<splat_blocks(n), SPLAT_THREADS, 0, s>>>(n, indices, n_bins, counts);
+	k_splat_scan<<<1, 1024, 0, s>>>(n_bins, counts, counts + n_bins + 1, counts + 2 * (n_bins + 1));
+	return n_bins;
+}
+void grid_splat_max_binned(uint32_t n, const uint32_t* indices, const f16* density_rm, uint32_t act, float* grid_tmp,
+                           uint32_t n_cells, uint32_t* scratch, hipStream_t s) {
+	const uint32_t n_bins = splat_bin_offsets(n, indices, n_cells, scratch, s);
+	const uint32_t* offsets = scratch + n_bins + 1;
+	uint32_t* cursor = scratch + 2 * (n_bins + 1);
+	uint32_t* packed = cursor + n_bins + 1;
+	if (n) k_splat_scatter<false><<<splat_blocks(n), SPLAT_THREADS, 0, s>>>(n, indices, density_rm, nullptr, n_bins, cursor, packed,
+	                                                                       nullptr);
+	k_splat_bins<false><<<n_bins, 1024, 0, s>>>(offsets, packed, nullptr, nullptr, 0, 0, act, grid_tmp);
+	NGP_HIP(hipGetLastError());
+}
+size_t grid_sort_scratch_u32(uint32_t n, uint32_t n_cells) { return 3 * ((size_t)(n_cells >> SPLAT_BIN_SHIFT) + 1); }
+void grid_sort_samples(uint32_t n, const float* positions, const uint32_t* indices, uint32_t n_cells, uint32_t* scratch,
+                       float* recs, hipStream_t s) {
+	const uint32_t n_bins = splat_bin_offsets(n, indices, n_cells, scratch, s);
+	uint32_t* cursor = scratch + 2 * (n_bins + 1);
+	if (n) k_splat_scatter<true><<<splat_blocks(n), SPLAT_THREADS, 0, s>>>(n, indices, nullptr, positions, n_bins, cursor, nullptr,
+	                                                                      (float4*)recs);
+	NGP_HIP(hipGetLastError());
+}
+void grid_splat_sorted(uint32_t n_cells, const uint32_t* scratch, const float* recs, const f16* density_rm, uint32_t lo,
+                       uint32_t hi, uint32_t act, float* grid_tmp, hipStream_t s) {
+	const uint32_t n_bins = n_cells >> SPLAT_BIN_SHIFT;
+	const uint32_t* offsets = scratch + n_bins + 1;
+	k_splat_bins<true><<<n_bins, 1024, 0, s>>>(offsets, nullptr, (const float4*)recs, density_rm, lo, hi, act, grid_tmp);
 	NGP_HIP(hipGetLastError());
 }
 // The update step's finalization in three launches instead of ten (the reference's ema_grid_samples_nerf,

@@ -170,7 +170,7 @@ struct ngp_nerf_trainer {
 		return e;
 	}
 	// occupancy grid
-	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens, grid_mask, splat_scratch;
+	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens, grid_mask, splat_scratch, gpos_sorted;
 	// training workspaces
 	Buf ray_indices, rays, numsteps, coords, mlp_out, dloss, coords_c, loss, counters, scan_tmp, tmp_u32, tmp_f32;
 	Buf loss_state;  // compute_loss: pass 1's per-sample compositing state for pass 2 (LossArgs::state)
@@ -615,9 +615,13 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	}
 	const uint32_t n = n_uniform + n_nonuniform;
 	float* tmp = t->grid_tmp.get<float>(n_el);
-	// the splat as a counting sort by cell bin, which writes every cell (A/B knob NGP_SPLAT_BINNED=0: memset + atomics)
-	static const bool binned = !getenv("NGP_SPLAT_BINNED") || atoi(getenv("NGP_SPLAT_BINNED")) != 0;
-	if (!binned) NGP_HIP(hipMemsetAsync(tmp, 0, (size_t)n_el * 4, s));
+	// One GPU: the samples sorted by cell bin before the density evaluation, and the splat from the sorted order, which
+	// writes every cell. Data parallel: the order within a bin is not deterministic, so the ranks' shards of it would
+	// not partition the samples; there each rank evaluates its shard of the generated order and splats it by the binned
+	// counting sort (every cell too). A/B knob NGP_SPLAT_SORT=0: memset, generated order, atomics.
+	static const int splat_mode = getenv("NGP_SPLAT_SORT") ? atoi(getenv("NGP_SPLAT_SORT")) : 1;
+	const bool sorted = splat_mode != 0 && t->world == 1, binned = splat_mode != 0 && t->world > 1;
+	if (splat_mode == 0) NGP_HIP(hipMemsetAsync(tmp, 0, (size_t)n_el * 4, s));
 	// every rank generates the same sample set (same density rng); each evaluates its 1/N shard
 	float* pos = t->gpos.get<float>((size_t)n * 3);
 	uint32_t* idx = t->gidx.get<uint32_t>(n);
@@ -630,11 +634,21 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	const uint32_t lo = (uint32_t)((uint64_t)n * t->rank / t->world), hi = (uint32_t)((uint64_t)n * (t->rank + 1) / t->world);
 	const uint32_t ns = hi - lo;
 	f16* dens = t->gdens.get<f16>((size_t)std::max(ns, 1u) * 16);
+	uint32_t* scratch = sorted ? t->splat_scratch.get<uint32_t>(grid_sort_scratch_u32(n, n_el)) : nullptr;
+	const float* dpos = pos;
+	uint32_t dstride = 3;
+	if (sorted) {
+		float* recs = t->gpos_sorted.get<float>((size_t)n * 4);
+		grid_sort_samples(n, pos, idx, n_el, scratch, recs, s);
+		dpos = recs;
+		dstride = 4;
+	}
 	if (ns) {
 		// row 0 (raw density) only: the other 15 rows of the density network's output are not read
-		check_rc(ngp::density_impl(t->model, s, ns, pos + (size_t)lo * 3, 3, dens, ns, ngp::DENSITY_LAYOUT_ROW0, 0));
-		if (!binned) grid_splat_max(ns, idx + lo, dens, cfg.density_activation, tmp, s);
+		check_rc(ngp::density_impl(t->model, s, ns, dpos + (size_t)lo * dstride, dstride, dens, ns, ngp::DENSITY_LAYOUT_ROW0, 0));
+		if (splat_mode == 0) grid_splat_max(ns, idx + lo, dens, cfg.density_activation, tmp, s);
 	}
+	if (sorted) grid_splat_sorted(n_el, scratch, dpos, dens, lo, hi, cfg.density_activation, tmp, s);
 	if (binned)
 		grid_splat_max_binned(ns, idx + lo, dens, cfg.density_activation, tmp, n_el,
 		                      t->splat_scratch.get<uint32_t>(grid_splat_scratch_u32(ns, n_el)), s);
