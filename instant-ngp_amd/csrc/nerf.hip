@@ -1812,9 +1812,14 @@ void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_co
 constexpr uint32_t SPLAT_THREADS = NGP_SPLAT_THREADS;  // k_splat_hist / k_splat_scatter block size
 constexpr uint32_t SPLAT_BIN_SHIFT = 13, SPLAT_BIN = 1u << SPLAT_BIN_SHIFT, SPLAT_MAX_BINS = 8 * GRID_N_CELLS / SPLAT_BIN;
 #ifndef NGP_SPLAT_MAX_BLOCKS
-#define NGP_SPLAT_MAX_BLOCKS 128
+#define NGP_SPLAT_MAX_BLOCKS 256  // 128 -> 256: fox scatter 88.5 -> 63.5 us (gpurun_out/r06as_256)
 #endif
-static uint32_t splat_blocks(uint32_t n) { return std::max(1u, std::min((uint32_t)NGP_SPLAT_MAX_BLOCKS, div_round_up(n, 16384))); }
+#ifndef NGP_SPLAT_CHUNK
+#define NGP_SPLAT_CHUNK 4096  // samples per k_splat_hist / k_splat_scatter block at least (Lego: 256 blocks, not 64)
+#endif
+static uint32_t splat_blocks(uint32_t n) {
+	return std::max(1u, std::min((uint32_t)NGP_SPLAT_MAX_BLOCKS, div_round_up(n, NGP_SPLAT_CHUNK)));
+}
 __device__ __forceinline__ void splat_chunk(uint32_t n, uint32_t nb, uint32_t* s0, uint32_t* s1) {
 	*s0 = (uint32_t)((uint64_t)n * blockIdx.x / nb);
 	*s1 = (uint32_t)((uint64_t)n * (blockIdx.x + 1) / nb);
