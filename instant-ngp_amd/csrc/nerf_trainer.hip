@@ -138,16 +138,25 @@ struct ngp_nerf_trainer {
 		NGP_HIP(hipMemset(sig_samp, 0, 8));
 		NGP_HIP(hipMemset(sig_free, 0, 8));
 	}
+	// Density-grid update pipelining: when the next step is due an update, its sample generation and bin sort read
+	// only the grid (unchanged until that update) and the grid rng, so they run on `sample_stream` under this step's
+	// training pass; the update then starts at the density evaluation (ev_gen). Discarding them restores the rng.
+	bool grid_pregen = false;
+	uint32_t pregen_nu = 0, pregen_nn = 0;
+	hipEvent_t ev_gen = nullptr;
+	HostPcg pregen_rng{1};  // grid_rng before the pregenerated samples
 	void drain() {  // the prelaunched sampler finished and discarded (state is about to change)
 		if (sample_stream) (void)hipStreamSynchronize(sample_stream);
 		prelaunched = false;
+		if (grid_pregen) grid_rng = pregen_rng;
+		grid_pregen = false;
 	}
 	~ngp_nerf_trainer() {
 		drain();
 		if (train_graph) ngp_graph_destroy(train_graph);
 		if (own_stream) (void)hipStreamDestroy(own_stream);
 		if (sample_stream) (void)hipStreamDestroy(sample_stream);
-		for (hipEvent_t e : {ev_free, ev_samp})
+		for (hipEvent_t e : {ev_free, ev_samp, ev_gen})
 			if (e) (void)hipEventDestroy(e);
 		for (uint32_t* p : {sig_samp, sig_free})
 			if (p) (void)hipFree(p);
@@ -601,27 +610,22 @@ int ngp_nerf_trainer_buffers(ngp_nerf_trainer* t, float** grid, uint8_t** bitfie
 }
 
 
-// update_density_grid_nerf (testbed_nerf.cu:3412-3536)
-static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay, uint32_t n_uniform, uint32_t n_nonuniform) {
+// update_density_grid_nerf (testbed_nerf.cu:3412-3536), in two parts: the samples (generation and, on one GPU, the
+// sort by cell bin: they read only the grid and the grid rng), then their density, splat, EMA, mean and bitfield.
+// One GPU: the samples sorted by cell bin before the density evaluation, and the splat from the sorted order, which
+// writes every cell. Data parallel: the order within a bin is not deterministic, so the ranks' shards of it would not
+// partition the samples; there each rank evaluates its shard of the generated order and splats it by the binned
+// counting sort (every cell too). A/B knob NGP_SPLAT_SORT=0: memset, generated order, atomics.
+static int splat_mode() {
+	static const int m = getenv("NGP_SPLAT_SORT") ? atoi(getenv("NGP_SPLAT_SORT")) : 1;
+	return m;
+}
+static void grid_update_samples(ngp_nerf_trainer* t, hipStream_t s, uint32_t n_uniform, uint32_t n_nonuniform) {
 	const ngp_nerf_config& cfg = t->cfg;
 	const uint32_t n_cascades = cfg.max_cascade + 1;
 	const uint32_t n_el = GRID_N_CELLS * n_cascades;
-	float* grid = (float*)t->grid.p;
-	if (t->training_step == 0) {
-		t->ema_step = 0;
-		const Dataset& ds = t->data->ds;
-		k_mark_untrained<<<div_round_up(n_el, 128), 128, 0, s>>>(n_el, grid, ds.n_images, ds.d_cams, raw_xforms(ds), true);
-		NGP_HIP(hipGetLastError());
-	}
 	const uint32_t n = n_uniform + n_nonuniform;
-	float* tmp = t->grid_tmp.get<float>(n_el);
-	// One GPU: the samples sorted by cell bin before the density evaluation, and the splat from the sorted order, which
-	// writes every cell. Data parallel: the order within a bin is not deterministic, so the ranks' shards of it would
-	// not partition the samples; there each rank evaluates its shard of the generated order and splats it by the binned
-	// counting sort (every cell too). A/B knob NGP_SPLAT_SORT=0: memset, generated order, atomics.
-	static const int splat_mode = getenv("NGP_SPLAT_SORT") ? atoi(getenv("NGP_SPLAT_SORT")) : 1;
-	const bool sorted = splat_mode != 0 && t->world == 1, binned = splat_mode != 0 && t->world > 1;
-	if (splat_mode == 0) NGP_HIP(hipMemsetAsync(tmp, 0, (size_t)n_el * 4, s));
+	const float* grid = (const float*)t->grid.p;
 	// every rank generates the same sample set (same density rng); each evaluates its 1/N shard
 	float* pos = t->gpos.get<float>((size_t)n * 3);
 	uint32_t* idx = t->gidx.get<uint32_t>(n);
@@ -631,24 +635,33 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 	grid_generate_samples(n_nonuniform, t->grid_rng.dev(), t->ema_step, cfg, grid, n_cascades, MIN_OPTICAL_THICKNESS,
 	                      pos + (size_t)n_uniform * 3, idx + n_uniform, mask, s);
 	t->grid_rng.advance();
+	if (splat_mode() != 0 && t->world == 1)
+		grid_sort_samples(n, pos, idx, n_el, t->splat_scratch.get<uint32_t>(grid_sort_scratch_u32(n, n_el)),
+		                  t->gpos_sorted.get<float>((size_t)n * 4), s);
+}
+static void grid_update_finish(ngp_nerf_trainer* t, hipStream_t s, float decay, uint32_t n_uniform, uint32_t n_nonuniform) {
+	const ngp_nerf_config& cfg = t->cfg;
+	const uint32_t n_cascades = cfg.max_cascade + 1;
+	const uint32_t n_el = GRID_N_CELLS * n_cascades;
+	const uint32_t n = n_uniform + n_nonuniform;
+	float* grid = (float*)t->grid.p;
+	float* tmp = t->grid_tmp.get<float>(n_el);
+	const bool sorted = splat_mode() != 0 && t->world == 1, binned = splat_mode() != 0 && t->world > 1;
+	if (splat_mode() == 0) NGP_HIP(hipMemsetAsync(tmp, 0, (size_t)n_el * 4, s));
+	const uint32_t* idx = t->gidx.get<uint32_t>(n);
 	const uint32_t lo = (uint32_t)((uint64_t)n * t->rank / t->world), hi = (uint32_t)((uint64_t)n * (t->rank + 1) / t->world);
 	const uint32_t ns = hi - lo;
 	f16* dens = t->gdens.get<f16>((size_t)std::max(ns, 1u) * 16);
-	uint32_t* scratch = sorted ? t->splat_scratch.get<uint32_t>(grid_sort_scratch_u32(n, n_el)) : nullptr;
-	const float* dpos = pos;
-	uint32_t dstride = 3;
-	if (sorted) {
-		float* recs = t->gpos_sorted.get<float>((size_t)n * 4);
-		grid_sort_samples(n, pos, idx, n_el, scratch, recs, s);
-		dpos = recs;
-		dstride = 4;
-	}
+	const float* dpos = sorted ? t->gpos_sorted.get<float>((size_t)n * 4) : t->gpos.get<float>((size_t)n * 3);
+	const uint32_t dstride = sorted ? 4 : 3;
 	if (ns) {
 		// row 0 (raw density) only: the other 15 rows of the density network's output are not read
 		check_rc(ngp::density_impl(t->model, s, ns, dpos + (size_t)lo * dstride, dstride, dens, ns, ngp::DENSITY_LAYOUT_ROW0, 0));
-		if (splat_mode == 0) grid_splat_max(ns, idx + lo, dens, cfg.density_activation, tmp, s);
+		if (splat_mode() == 0) grid_splat_max(ns, idx + lo, dens, cfg.density_activation, tmp, s);
 	}
-	if (sorted) grid_splat_sorted(n_el, scratch, dpos, dens, lo, hi, cfg.density_activation, tmp, s);
+	if (sorted)
+		grid_splat_sorted(n_el, t->splat_scratch.get<uint32_t>(grid_sort_scratch_u32(n, n_el)), dpos, dens, lo, hi,
+		                  cfg.density_activation, tmp, s);
 	if (binned)
 		grid_splat_max_binned(ns, idx + lo, dens, cfg.density_activation, tmp, n_el,
 		                      t->splat_scratch.get<uint32_t>(grid_splat_scratch_u32(ns, n_el)), s);
@@ -665,6 +678,23 @@ static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay,
 		grid_mean_bitfield(grid, cfg.max_cascade, (float*)t->mean.p, (uint8_t*)t->bitfield.p, s);
 	}
 	++t->ema_step;
+}
+static void update_density_grid(ngp_nerf_trainer* t, hipStream_t s, float decay, uint32_t n_uniform, uint32_t n_nonuniform) {
+	if (t->training_step == 0) {
+		t->ema_step = 0;
+		const Dataset& ds = t->data->ds;
+		const uint32_t n_el = GRID_N_CELLS * (t->cfg.max_cascade + 1);
+		k_mark_untrained<<<div_round_up(n_el, 128), 128, 0, s>>>(n_el, (float*)t->grid.p, ds.n_images, ds.d_cams, raw_xforms(ds), true);
+		NGP_HIP(hipGetLastError());
+	}
+	grid_update_samples(t, s, n_uniform, n_nonuniform);
+	grid_update_finish(t, s, decay, n_uniform, n_nonuniform);
+}
+// the update's sample counts at a step (training_prep_nerf, testbed_nerf.cu:3622-3630)
+static void grid_update_counts(const ngp_nerf_trainer* t, uint32_t step, uint32_t* nu, uint32_t* nn) {
+	const uint32_t nc = t->cfg.max_cascade + 1;
+	*nu = step < 256 ? GRID_N_CELLS * nc : GRID_N_CELLS / 4 * nc;
+	*nn = step < 256 ? 0u : GRID_N_CELLS / 4 * nc;
 }
 
 // Data parallel: this shard's counters and loss as five floats for one all-reduce (sum). The u32
@@ -907,9 +937,16 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		// training_prep_nerf (a prelaunched sampler implies no update was due at this step)
 		if (!pre && density_grid_update_due(t->training_step)) {
 			ProfScope ps("nerf_density_grid", s);
-			const uint32_t nc = cfg.max_cascade + 1;
-			if (t->training_step < 256) update_density_grid(t, s, 0.95f, GRID_N_CELLS * nc, 0);
-			else update_density_grid(t, s, 0.95f, GRID_N_CELLS / 4 * nc, GRID_N_CELLS / 4 * nc);
+			uint32_t nu, nn;
+			grid_update_counts(t, t->training_step, &nu, &nn);
+			if (t->grid_pregen) {  // the samples were generated (and sorted) under the last step's training pass
+				NGP_CHECK(nu == t->pregen_nu && nn == t->pregen_nn, "nerf: pregenerated density-grid samples are stale");
+				t->grid_pregen = false;
+				NGP_HIP(hipStreamWaitEvent(s, t->ev_gen, 0));
+				grid_update_finish(t, s, 0.95f, nu, nn);
+			} else {
+				update_density_grid(t, s, 0.95f, nu, nn);
+			}
 		}
 		// train_nerf_step (testbed_nerf.cu:3867-4132)
 		const SamplePlan sp = sample_plan(t);
@@ -1078,6 +1115,16 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			t->pre_R = np.R;
 			t->pre_max_inference = np.max_inference;
 			t->prelaunched = true;
+		}
+		// next step's density-grid update: its samples now, under this step's training pass (one GPU)
+		static const bool pregen_on = !getenv("NGP_GRID_PREGEN") || atoi(getenv("NGP_GRID_PREGEN")) != 0;  // A/B knob
+		if (pregen_on && can_pipeline && !dp && t->training_step > 0 && density_grid_update_due(t->training_step)) {
+			if (!t->ev_gen) NGP_HIP(hipEventCreateWithFlags(&t->ev_gen, hipEventDisableTiming));
+			grid_update_counts(t, t->training_step, &t->pregen_nu, &t->pregen_nn);
+			t->pregen_rng = t->grid_rng;
+			grid_update_samples(t, t->sample_stream, t->pregen_nu, t->pregen_nn);
+			NGP_HIP(hipEventRecord(t->ev_gen, t->sample_stream));
+			t->grid_pregen = true;
 		}
 		if (st) {
 			st->step = t->training_step;

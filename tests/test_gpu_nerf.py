@@ -488,9 +488,11 @@ def test_fused_encoding_inference_bitwise(pkg, log2_T, max_level):
 
 @pytest.mark.gpu
 def test_sampler_pipelining_is_exact(pkg):
-    """Launching the next step's sampler under the training pass (default) trains exactly like the
-    serial step: same per-step counts, same parameters, density grid and bitfield, bit for bit, across
-    density-grid updates, growing ray counts and steps that read the loss back."""
+    """Launching the next step's sampler under the training pass (default), and the next density-grid update's
+    sample generation and sort, trains exactly like the serial step: same per-step counts, same parameters,
+    density grid and bitfield, bit for bit, across density-grid updates, growing ray counts, steps that read the
+    loss back and steps where the caller takes writable buffers (discarding pregenerated update samples: the
+    grid rng is restored)."""
     ds = pkg.synthetic.lego_like_dataset(n_images=12, width=128, height=128, seed=5)
     cfg = pkg.nerf.default_config(1.0)
     runs = []
@@ -499,7 +501,11 @@ def test_sampler_pipelining_is_exact(pkg):
         tr = pkg.Trainer(net, pkg.nerf_config("C2")["optimizer"], seed=7)
         run = pkg.nerf.NerfTraining(net, tr, ds, cfg, seed=1337)
         run.set_pipeline(pipeline)
-        stats = [run.train_step(get_loss=(i % 37 == 0)) for i in range(300)]
+        stats = []
+        for i in range(300):
+            stats.append(run.train_step(get_loss=(i % 37 == 0)))
+            if i in (47, 271):  # updates due at steps 48 and 272 were pregenerated: discarded here
+                run.writable_buffers()
         torch.cuda.synchronize()
         runs.append((stats, tr.serialize(), run.density_grid.cpu().numpy(), run.bitfield.cpu().numpy(), (net, tr, run)))
     (s1, p1, g1, b1, _), (s0, p0, g0, b0, _) = runs

@@ -99,7 +99,14 @@ def main():
     print(json.dumps({
         "warm_steps": args.steps, "warm_seconds": round(t_warm, 2), "measured_steps": args.measure,
         "ms_per_step_wall": round(1e3 * dt / args.measure, 4),
-        "rays_per_batch": float(np.mean(rays)), "samples_before_compaction": float(np.mean(pre)),
+        "rays_per_batch": float(np.mean(rays)),
+        "rays_per_batch_changed": float(np.mean(np.diff(np.asarray(rays)) != 0)) if len(rays) > 1 else 0.0,
+        # how predictable the next step's ray count is (a speculative sampler must guess it): the step-to-step
+        # differences in units of 256 rays, and the hit rate of R_{k+1} = R_{k-1} and of R_{k+1} in {R_k, R_{k-1}}
+        "rays_delta_hist": {str(int(k)): int(v) for k, v in zip(*np.unique(np.diff(np.asarray(rays)) // 256, return_counts=True))},
+        "rays_hit_prev2": float(np.mean(np.asarray(rays)[2:] == np.asarray(rays)[:-2])) if len(rays) > 2 else 0.0,
+        "rays_hit_last_two": float(np.mean((np.asarray(rays)[2:] == np.asarray(rays)[1:-1]) |
+                                           (np.asarray(rays)[2:] == np.asarray(rays)[:-2]))) if len(rays) > 2 else 0.0, "samples_before_compaction": float(np.mean(pre)),
         "compacted_samples": float(np.mean(comp)),
         "samples_per_s": float(np.sum(comp) / dt), "phases": phases, "sampler_stats": stats}, indent=1), flush=True)
 
