@@ -995,6 +995,9 @@ int ngp_model_set_option(ngp_model* m, const char* key, double value) {
 		} else {
 			throw Error("unknown model option: " + k);
 		}
+		// a graph captured before the change launches the old kernels: mark it stale (the NeRF trainer re-captures,
+		// ngp_graph_launch of a caller's graph fails loudly)
+		++m->ws_epoch;
 	});
 }
 
@@ -1513,7 +1516,7 @@ void ngp::trainer_ctl_values(const ngp_trainer* t, uint32_t** ctl, uint32_t* ste
 }
 void ngp::graph_launch_ctl_written(ngp_graph* g, void* stream) {
 	NGP_CHECK(g && g->exec, "graph launch: no graph");
-	NGP_CHECK(g->ws_epoch == g->trainer->model->ws_epoch, "graph launch: the model's workspaces were reallocated since capture");
+	NGP_CHECK(g->ws_epoch == g->trainer->model->ws_epoch, "graph launch: the model's workspaces were reallocated (or its options changed) since capture");
 	NGP_HIP(hipGraphLaunch(g->exec, S(stream)));
 	g->launched();
 }

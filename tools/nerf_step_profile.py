@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--res", type=int, default=800)
     ap.add_argument("--pipeline", type=int, default=1, help="1: next step's sampler under the training pass (default), 0: serial step")
     ap.add_argument("--option", action="append", default=[], help="model option key=value (ngp_model_set_option)")
+    ap.add_argument("--option-after-warmup", action="append", default=[],
+                    help="model option key=value set after the warm-up steps (timing experiments: win_debug)")
     ap.add_argument("--fox", action="store_true", help="the fox capture (data/fox, tools/stage_fox.sh) instead of the stand-in")
     ap.add_argument("--profiler", type=int, default=1, help="0: no engine HIP-event profiler in the measured steps (wall time only)")
     ap.add_argument("--env-after-warmup", action="append", default=[],
@@ -59,6 +61,9 @@ def main():
             print(f"step {i} {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t_warm = time.time() - t0
+    for kv in args.option_after_warmup:
+        key, value = kv.split("=")
+        net.set_option(key, float(value))
     for kv in args.env_after_warmup:
         key, value = kv.split("=", 1)
         os.environ[key] = value
