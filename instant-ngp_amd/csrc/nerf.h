@@ -94,6 +94,11 @@ struct LossArgs {
 	// them instead of compositing each ray again. Same float operations, so the same bits either way.
 	float* state;
 	uint64_t state_cap;
+	// optional (null: off): the loss's compaction scan also publishes the step's counters to host-mapped memory
+	// ({ray_counter[0], ray_counter[1], compacted total, 0}, then pub_seq at [4] after a system-scope fence), as soon
+	// as they are final: the host sizes the next step while pass 2, the rollover and the training pass run
+	volatile uint32_t* pub_host;
+	uint32_t pub_seq;
 };
 
 // The kernels (each cites its reference kernel in nerf.hip).
@@ -105,8 +110,9 @@ void fill_rollover_f32(uint32_t n_elements, uint32_t stride, const uint32_t* n_i
 void fill_rollover_pair(uint32_t n_elements, const uint32_t* n_input, f16* dloss, uint32_t stride16, float* coords,
                         uint32_t stride32, hipStream_t s);
 // What the single-GPU NeRF step does right after the rollover, in the same launch (block 0, thread 0): publish the
-// step's counters ctr[0..3] to host-mapped memory (then seq, after a system-scope fence), and write the optimizer
-// control block the training graph reads ({ctl[0] = step, ctl[CTL_CFG..] = cfg}, set_device_ctl). bytes: cfg.
+// step's counters ctr[0..3] to host-mapped memory (then seq, after a system-scope fence; host null: published
+// earlier, by the loss's scan), and write the optimizer control block the training graph reads ({ctl[0] = step,
+// ctl[CTL_CFG..] = cfg}, set_device_ctl). bytes: cfg.
 struct StepPublish {
 	const uint32_t* ctr; volatile uint32_t* host; uint32_t seq;
 	uint32_t* ctl; uint32_t step; uint32_t cfg_off, cfg_words; uint32_t cfg[32];  // cfg at ctl + cfg_off (words)

@@ -1009,7 +1009,8 @@ __device__ __forceinline__ void scan1_store(uint32_t* out, uint32_t n, uint32_t 
 // total, one block: a quarter of the block scans of a per-element scan (the loss's compaction: ~32 K rays, two
 // tiles instead of eight); a consumer adds the at most 3 values of its group before it.
 __global__ void __launch_bounds__(SCAN1_THREADS) k_scan4(uint32_t n, const uint32_t* __restrict__ in, uint32_t* __restrict__ gpre,
-                                                         uint32_t* __restrict__ total) {
+                                                         uint32_t* __restrict__ total, const uint32_t* __restrict__ ray_counter,
+                                                         volatile uint32_t* pub_host, uint32_t pub_seq) {
 	__shared__ uint32_t lds[32];
 	const uint32_t ng = (n + 3) / 4;
 	uint32_t run = 0;
@@ -1032,7 +1033,14 @@ __global__ void __launch_bounds__(SCAN1_THREADS) k_scan4(uint32_t n, const uint3
 		scan1_store(gpre, ng, g0 + 4 * threadIdx.x, o);
 		run += tot;
 	}
-	if (threadIdx.x == 0) *total = run;
+	if (threadIdx.x == 0) {
+		*total = run;
+		if (pub_host) {  // LossArgs::pub_host: the step's counters are final here
+			pub_host[0] = ray_counter[0]; pub_host[1] = ray_counter[1]; pub_host[2] = run; pub_host[3] = 0u;
+			__threadfence_system();
+			pub_host[4] = pub_seq;
+		}
+	}
 }
 // The count waves' exclusive prefixes (bpre[2 w]: samples before wave w, bpre[2 w + 1]: rays with samples
 // before it) from their sums, one block; and the counters: rays kept, and the total count of every ray (the
@@ -1507,7 +1515,7 @@ void compute_loss(const Dataset& ds, const ngp_nerf_config& cfg, const LossArgs&
 	}
 	{
 		ProfScope ps("loss_scan", s);
-		k_scan4<<<1, SCAN1_THREADS, 0, s>>>(a.n_rays, craw, gpre, a.compacted_counter);
+		k_scan4<<<1, SCAN1_THREADS, 0, s>>>(a.n_rays, craw, gpre, a.compacted_counter, a.ray_counter, a.pub_host, a.pub_seq);
 		NGP_HIP(hipGetLastError());
 	}
 	ProfScope ps("loss_pass2", s);
@@ -1604,9 +1612,11 @@ __global__ void k_rollover_pair_publish(uint32_t n_elements, uint32_t stride16, 
                                         float* d32, const StepPublish pub) {
 	if (blockIdx.x == 0 && threadIdx.x == 0) {
 		volatile uint32_t* host = pub.host;
-		host[0] = pub.ctr[0]; host[1] = pub.ctr[1]; host[2] = pub.ctr[2]; host[3] = pub.ctr[3];
-		__threadfence_system();
-		host[4] = pub.seq;
+		if (host) {
+			host[0] = pub.ctr[0]; host[1] = pub.ctr[1]; host[2] = pub.ctr[2]; host[3] = pub.ctr[3];
+			__threadfence_system();
+			host[4] = pub.seq;
+		}
 		pub.ctl[0] = pub.step;
 		for (uint32_t k = 0; k < pub.cfg_words; ++k) pub.ctl[pub.cfg_off + k] = pub.cfg[k];
 	}
@@ -1625,7 +1635,7 @@ __global__ void k_rollover_pair_publish(uint32_t n_elements, uint32_t stride16, 
 }
 void fill_rollover_pair_publish(uint32_t n_elements, const uint32_t* n_input, f16* dloss, uint32_t stride16, float* coords,
                                 uint32_t stride32, const StepPublish& pub, hipStream_t s) {
-	NGP_CHECK(pub.host && pub.ctl && pub.cfg_words <= 32, "rollover publish: host counters, control block and config required");
+	NGP_CHECK(pub.ctl && pub.cfg_words <= 32, "rollover publish: control block and config required");
 	const uint64_t n = (uint64_t)n_elements * (stride16 > stride32 ? stride16 : stride32);
 	const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(div_round_up(n, 256), 1024));
 	k_rollover_pair_publish<<<blocks, 256, 0, s>>>(n_elements, stride16, stride32, n_input, dloss, coords, pub);

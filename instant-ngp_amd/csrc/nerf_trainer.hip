@@ -182,6 +182,20 @@ struct ngp_nerf_trainer {
 	Buf grid, grid_tmp, bitfield, mean, gpos, gidx, gdens, grid_mask, splat_scratch, gpos_sorted;
 	// training workspaces
 	Buf ray_indices, rays, numsteps, coords, mlp_out, dloss, coords_c, loss, counters, scan_tmp, tmp_u32, tmp_f32;
+	// Early publish (one GPU): the counters are published by the loss's scan, so the host launches the next step's
+	// sampler while this step's loss pass 2, rollover and training pass still run; the sampler's outputs then
+	// alternate between two sets by step parity (the set it writes was last read two steps before), so it waits on
+	// nothing. Default under cone stepping only (aabb_scale > 1: the count pass, ~1.5x the training pass, is the
+	// step's critical path; fox 0.517 -> 0.499 ms); at cone 0 the two are balanced and a count pass already resident
+	// when the training pass starts keeps its one-wave-per-SIMD MLP kernel off the SIMDs (Lego 0.421 -> 0.440 ms,
+	// gpurun_out/r06bd). NGP_NERF_EARLY=1: always, 0: never (publish in the rollover, one set, the sampler waits
+	// for this step's release).
+	Buf ray_indices_b, rays_b, numsteps_b, coords_b, counters_b;
+	bool early() const {
+		static const int knob = getenv("NGP_NERF_EARLY") ? atoi(getenv("NGP_NERF_EARLY")) : -1;
+		const bool on = knob < 0 ? cfg.cone_angle_constant > 1e-5f : knob != 0;
+		return on && !dp();
+	}
 	Buf loss_state;  // compute_loss: pass 1's per-sample compositing state for pass 2 (LossArgs::state)
 	// training error map (Testbed::Nerf::Training::ErrorMap and its update window, testbed.h:668-677, 736-738)
 	Buf em_data, em_cdf_x, em_cdf_y, em_cdf_img;
@@ -349,7 +363,7 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
                              uint32_t* numsteps, const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
                              uint32_t* compacted_counter, const float* mean_density, float loss_scale, bool zero_loss = false,
                              float* error_map = nullptr, uint32_t em_w = 0, uint32_t em_h = 0, float* state = nullptr,
-                             uint64_t state_cap = 0);
+                             uint64_t state_cap = 0, volatile uint32_t* pub_host = nullptr, uint32_t pub_seq = 0);
 
 int ngp_nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* cfg, void* stream, uint32_t n_rays,
                           uint32_t n_rays_total, ngp_rng rng, uint32_t max_samples_compacted, const uint32_t* ray_counter,
@@ -390,7 +404,8 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
                              const void* network_output, uint32_t out_stride, const uint32_t* ray_indices, const float* rays,
                              uint32_t* numsteps, const float* coords_in, float* coords_out, void* dloss_doutput, float* loss,
                              uint32_t* compacted_counter, const float* mean_density, float loss_scale, bool zero_loss,
-                             float* error_map, uint32_t em_w, uint32_t em_h, float* state, uint64_t state_cap) {
+                             float* error_map, uint32_t em_w, uint32_t em_h, float* state, uint64_t state_cap,
+                             volatile uint32_t* pub_host, uint32_t pub_seq) {
 	if (!ds || !cfg || !ray_counter || !network_output || !numsteps || !coords_in || !coords_out || !dloss_doutput ||
 	    !compacted_counter || !mean_density)
 		return NGP_INVALID;
@@ -404,6 +419,8 @@ static int nerf_compute_loss(const ngp_nerf_dataset* ds, const ngp_nerf_config* 
 		a.mean_density = mean_density; a.loss_scale = loss_scale; a.zero_loss = zero_loss;
 		a.error_map = error_map; a.em_w = em_w; a.em_h = em_h;
 		a.state = state; a.state_cap = state ? state_cap : 0;
+		a.pub_host = pub_host; a.pub_seq = pub_seq;
+		NGP_CHECK(n_rays > 0 || !pub_host, "compute_loss: the counters are published by the scan, which needs rays");
 		if (n_rays == 0) { NGP_HIP(hipMemsetAsync(compacted_counter, 0, 4, S(stream))); return NGP_OK; }
 		static thread_local Buf tmp, tmpf;
 		compute_loss(ds->ds, *cfg, a, tmp.get<uint32_t>(2 * (size_t)n_rays), tmpf.get<float>(loss_tmp_f32(n_rays)), S(stream));
@@ -484,7 +501,11 @@ int ngp_nerf_trainer_set_config(ngp_nerf_trainer* t, const ngp_nerf_config* cfg)
 			          "set_config: the aabb is fixed for the trainer's lifetime (reset the trainer)");
 		NGP_CHECK(cfg->target_batch_size > 0 && cfg->target_batch_size % 256 == 0, "set_config: target_batch_size");
 		t->drain();  // a prelaunched sampler ran with the old knobs
+		const bool early_was = t->early();
 		t->cfg = *cfg;
+		// the sample-set choice changes with the cone (ngp_nerf_trainer::early): let the last step's passes finish
+		// reading their set first
+		if (t->early() != early_was) NGP_HIP(hipDeviceSynchronize());
 	});
 }
 
@@ -574,6 +595,8 @@ int ngp_nerf_render(ngp_nerf_renderer* r, ngp_model* model, const ngp_nerf_confi
 int ngp_nerf_trainer_set_data_parallel(ngp_nerf_trainer* t, uint32_t rank, uint32_t world, ngp_allreduce_fn allreduce, void* user) {
 	if (!t || world == 0 || rank >= world || (world > 1 && !allreduce)) return NGP_INVALID;
 	t->drain();
+	// the sample-set choice (ngp_nerf_trainer::early) depends on the exchange: the last step's passes finish first
+	if (hipDeviceSynchronize() != hipSuccess) return NGP_ERROR;
 	t->rank = rank;
 	t->world = world;
 	t->allreduce = allreduce;
@@ -770,11 +793,12 @@ static SamplePlan sample_plan(ngp_nerf_trainer* t) {
 	if (t->measured_before_compaction_local == 0) p.max_inference = p.max_samples;
 	else p.max_inference = next_multiple(std::min(t->measured_before_compaction_local, p.max_samples), 256);
 	p.Ra = std::max(p.Rl, 1u);
-	p.ray_indices = t->ray_indices.get<uint32_t>(p.Ra);
-	p.rays = t->rays.get<float>((size_t)p.Ra * 6);
-	p.numsteps = t->numsteps.get<uint32_t>((size_t)p.Ra * 2);
-	p.coords = t->coords.get<float>((size_t)p.max_samples * 7);
-	p.ctr = t->counters.get<uint32_t>(4);  // rays kept, steps, compacted steps
+	const bool b = t->early() && (t->training_step & 1u);  // the step's sample set (ngp_nerf_trainer::early)
+	p.ray_indices = (b ? t->ray_indices_b : t->ray_indices).get<uint32_t>(p.Ra);
+	p.rays = (b ? t->rays_b : t->rays).get<float>((size_t)p.Ra * 6);
+	p.numsteps = (b ? t->numsteps_b : t->numsteps).get<uint32_t>((size_t)p.Ra * 2);
+	p.coords = (b ? t->coords_b : t->coords).get<float>((size_t)p.max_samples * 7);
+	p.ctr = (b ? t->counters_b : t->counters).get<uint32_t>(4);  // rays kept, steps, compacted steps
 	return p;
 }
 static void launch_sampler(ngp_nerf_trainer* t, const SamplePlan& p, hipStream_t s) {
@@ -980,6 +1004,14 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		const bool dp = t->dp();
 		const float loss_scale_local = 128.0f * (float)Rl / (float)R;
 		float* error_map = error_map_window(t, s);
+		if (!t->host_ctr) {
+			void* p = nullptr;
+			NGP_HIP(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+			t->host_ctr = (volatile uint32_t*)p;
+			memset(p, 0, 64);
+		}
+		const bool early_pub = t->early() && Rl > 0;
+		const uint32_t pub_seq = dp ? 0u : ++t->publish_seq;
 		{
 		ProfScope ps("nerf_loss", s);
 		// pass 1 keeps each composited sample's state for pass 2 (indexed like the sampler's samples, at most max_samples)
@@ -987,24 +1019,19 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		float* lstate = keep_state ? t->loss_state.get<float>((size_t)5 * sp.max_samples) : nullptr;
 		check_rc(nerf_compute_loss(t->data, &cfg, s, Rl, R, rng, Bl, ctr, mlp_out, 4, ray_indices, rays, numsteps, coords, coords_c,
 		                               dloss, loss, ctr + 2, (const float*)t->mean.p, dp ? loss_scale_local : 128.0f, true,
-		                               error_map, t->em_w, t->em_h, lstate, sp.max_samples));
+		                               error_map, t->em_w, t->em_h, lstate, sp.max_samples, early_pub ? t->host_ctr : nullptr,
+		                               pub_seq));
 		}
 		// the step's counters are final here (the training pass does not touch them): publish them before
-		// the training pass so the host can size the next step while it runs
-		if (!t->host_ctr) {
-			void* p = nullptr;
-			NGP_HIP(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
-			t->host_ctr = (volatile uint32_t*)p;
-			memset(p, 0, 64);
-		}
+		// the training pass so the host can size the next step while it runs (early_pub: already published)
 		if (!dp) {
 			// single GPU: the rollover launch (fill_rollover_and_rescale + fill_rollover) also publishes the counters
 			// and writes the optimizer control block the training graph reads (a separate publish kernel and
 			// ngp_graph_launch's k_set_ctl before: two launches less per step)
 			StepPublish pub{};
 			pub.ctr = ctr;
-			pub.host = t->host_ctr;
-			pub.seq = ++t->publish_seq;
+			pub.host = early_pub ? nullptr : t->host_ctr;
+			pub.seq = pub_seq;
 			trainer_ctl_values(t->trainer, &pub.ctl, &pub.step, &pub.cfg_off, &pub.cfg_words, pub.cfg);
 			fill_rollover_pair_publish(Bl, ctr + 2, dloss, 16, coords_c, 7, pub, s);
 		} else {
@@ -1033,7 +1060,9 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 			}
 			// sample buffers and counters released: an event (by the time the host launches the next sampler this
 			// is long done, and a completed event's wait costs ~1.3 us against ~3.6 for a value wait)
-			if (nerf_waitval() == 2) {
+			if (t->early()) {
+				// nothing to release: the next sampler writes the other sample set
+			} else if (nerf_waitval() == 2) {
 				t->ensure_signals();
 				NGP_HIP(hipStreamWriteValue32(s, t->sig_free, ++t->seq_free, 0));
 			} else {
@@ -1103,8 +1132,12 @@ int ngp_nerf_train_step(ngp_nerf_trainer* t, void* stream, int get_loss, ngp_ner
 		// next step's sampler, concurrent with this step's training pass (no density-grid update due first)
 		if (can_pipeline && t->measured_batch_size > 0 && !density_grid_update_due(t->training_step)) {
 			const SamplePlan np = sample_plan(t);
-			if (nerf_waitval() == 2) NGP_HIP(hipStreamWaitValue32(t->sample_stream, t->sig_free, t->seq_free, hipStreamWaitValueGte, 0xFFFFFFFFu));
-			else NGP_HIP(hipStreamWaitEvent(t->sample_stream, t->ev_free, 0));
+			// early(): the sampler writes the other sample set, which the step before last read (complete: this step's
+			// counters are published), so it waits on nothing
+			if (!t->early()) {
+				if (nerf_waitval() == 2) NGP_HIP(hipStreamWaitValue32(t->sample_stream, t->sig_free, t->seq_free, hipStreamWaitValueGte, 0xFFFFFFFFu));
+				else NGP_HIP(hipStreamWaitEvent(t->sample_stream, t->ev_free, 0));
+			}
 			launch_sampler(t, np, t->sample_stream);
 			if (nerf_waitval()) {
 				t->ensure_signals();

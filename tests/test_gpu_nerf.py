@@ -487,14 +487,16 @@ def test_fused_encoding_inference_bitwise(pkg, log2_T, max_level):
 
 
 @pytest.mark.gpu
-def test_sampler_pipelining_is_exact(pkg):
+@pytest.mark.parametrize("aabb_scale", [1.0, 4.0])
+def test_sampler_pipelining_is_exact(pkg, aabb_scale):
     """Launching the next step's sampler under the training pass (default), and the next density-grid update's
     sample generation and sort, trains exactly like the serial step: same per-step counts, same parameters,
     density grid and bitfield, bit for bit, across density-grid updates, growing ray counts, steps that read the
     loss back and steps where the caller takes writable buffers (discarding pregenerated update samples: the
-    grid rng is restored)."""
+    grid rng is restored). aabb_scale 4 (cone stepping) also runs the early counter publish: the next sampler under
+    this step's loss pass 2 and training pass, writing the other of two sample sets."""
     ds = pkg.synthetic.lego_like_dataset(n_images=12, width=128, height=128, seed=5)
-    cfg = pkg.nerf.default_config(1.0)
+    cfg = pkg.nerf.default_config(aabb_scale)
     runs = []
     for pipeline in (True, False):
         net = pkg.create_nerf_network(pkg.nerf_config("C2"))
