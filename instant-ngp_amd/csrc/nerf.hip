@@ -398,7 +398,9 @@ constexpr uint32_t RG = NGP_SAMPLER_RG;  // lanes per ray (16 = one DPP row)
 #define NGP_SAMPLER_ROUND_CAP 1  // verify rounds per march iteration (0: until every lane is verified)
 #endif
 #ifndef NGP_SAMPLER_PRIO
-#define NGP_SAMPLER_PRIO 0  // s_setprio of the cone-stepping count pass (it shares the SIMDs with the training pass)
+#define NGP_SAMPLER_PRIO 3  // s_setprio of the cone-stepping count pass (it shares the SIMDs with the training pass and
+                            // is the fox step's critical path): neutral in round 4, fox -1 % since the early counter
+                            // publish starts it under the training pass (gpurun_out/r06bl, r06bm)
 #endif
 #ifndef NGP_SAMPLER_END_CONE
 #define NGP_SAMPLER_END_CONE 0  // sampling_end under cone stepping (off: measured slower with the speculative march)
