@@ -1808,7 +1808,7 @@ void grid_generate_samples(uint32_t n, Rng rng, uint32_t step, const ngp_nerf_co
 }
 // The splat as a counting sort by cell bin (fox: 5.2 M samples into 10.5 M cells). The direct splat's atomics are
 // scattered over the whole grid and run at ~32 G/s whatever their locality (an XCD-sliced variant that kept each
-// XCD's cells L2-resident measured no faster, DESIGN §10): here each sample costs two LDS atomics and 8 B of
+// XCD's cells L2-resident measured no faster, DESIGN §9): here each sample costs two LDS atomics and 8 B of
 // coalesced-ish traffic instead. Bins of 8192 cells (32 KB of LDS):
 //   k_splat_hist: per-block LDS histogram of the samples' bins, added to the global counts (one atomic per bin and
 //     block);
